@@ -1,0 +1,144 @@
+// pybind11 entry points of the native extension `fraud_detection_amd._fdx_native`.
+//
+// Device pointers and hipStream_t handles cross the boundary as Python integers (taken from
+// torch tensors' data_ptr() and torch.cuda.current_stream().cuda_stream).  All operand shape and
+// dtype validation happens in fraud_detection_amd/ops/*.py BEFORE a launch (the kernels assume
+// padded 32-column rows, 16 B alignment and in-bounds index arrays).
+#include <hip/hip_runtime.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <string>
+
+#include "kernels/launchers.h"
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+template <typename T>
+static T* P(u p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(u s) { return reinterpret_cast<hipStream_t>(s); }
+
+static py::dict device_info(int dev) {
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) throw std::runtime_error("hipGetDeviceProperties failed");
+  py::dict d;
+  d["name"] = std::string(prop.name);
+  d["gcn_arch"] = std::string(prop.gcnArchName);
+  d["cu_count"] = prop.multiProcessorCount;
+  d["total_mem"] = (unsigned long long)prop.totalGlobalMem;
+  d["lds_per_block"] = (unsigned long long)prop.sharedMemPerBlock;
+  d["clock_khz"] = prop.clockRate;
+  d["l2_bytes"] = prop.l2CacheSize;
+  int rt = 0;
+  hipRuntimeGetVersion(&rt);
+  d["hip_runtime_version"] = rt;
+  return d;
+}
+
+static void stream_sync(u stream) {
+  hipError_t e = hipStreamSynchronize(S(stream));
+  if (e != hipSuccess) throw std::runtime_error(std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+}
+
+PYBIND11_MODULE(_fdx_native, m) {
+  m.doc() = "MI355X (gfx950) HIP kernels for fraud_detection_amd";
+  m.attr("ARCH") = "gfx950";
+  m.attr("LR_PART_STRIDE") = fdx::kLRPartStride;
+  m.def("device_info", &device_info, py::arg("device") = 0);
+  m.def("stream_sync", &stream_sync);
+
+  // scaler
+  m.def("scaler_partial", [](u X, int64_t n, int ld, int d, u pivot, u partial, int nblocks, u s) {
+    fdx::launch_scaler_partial(P<const float>(X), n, ld, d, P<const float>(pivot), P<double>(partial), nblocks, S(s));
+  });
+  m.def("scaler_reduce", [](u partial, int nblocks, u sums, u s) {
+    fdx::launch_scaler_reduce(P<const double>(partial), nblocks, P<double>(sums), S(s));
+  });
+  m.def("scaler_finalize", [](u sums, double n, u pivot, int d, u mean64, u var64, u scale64, u mean32, u inv32, u s) {
+    fdx::launch_scaler_finalize(P<const double>(sums), n, P<const float>(pivot), d, P<double>(mean64), P<double>(var64),
+                                P<double>(scale64), P<float>(mean32), P<float>(inv32), S(s));
+  });
+  m.def("scale_cast", [](u X, int64_t n, int ld, int d, u idx, u mean32, u inv32, u labels, float bias_value,
+                         float out_scale, int out_kind, u out, u s) {
+    fdx::launch_scale_cast(P<const float>(X), n, ld, d, P<const int64_t>(idx), P<const float>(mean32),
+                           P<const float>(inv32), P<const uint8_t>(labels), bias_value, out_scale, out_kind,
+                           P<void>(out), S(s));
+  });
+  m.def("compact_count", [](u labels, int64_t n, int target, u counts, int nblocks, u s) {
+    fdx::launch_compact_count(P<const uint8_t>(labels), n, target, P<int64_t>(counts), nblocks, S(s));
+  });
+  m.def("exclusive_scan_small", [](u a, int n, u total, u s) {
+    fdx::launch_exclusive_scan_small(P<int64_t>(a), n, P<int64_t>(total), S(s));
+  });
+  m.def("compact_write", [](u labels, int64_t n, int target, u offsets, u out_idx, int nblocks, u s) {
+    fdx::launch_compact_write(P<const uint8_t>(labels), n, target, P<const int64_t>(offsets), P<int64_t>(out_idx),
+                              nblocks, S(s));
+  });
+
+  // predict / linear shap
+  m.def("predict_bf16", [](u X, int64_t n, u w, u prob, u logit, u s) {
+    fdx::launch_predict_bf16(P<const uint16_t>(X), n, P<const float>(w), P<float>(prob), P<float>(logit), S(s));
+  });
+  m.def("predict_fp8", [](u X, int64_t n, u w, u prob, u logit, u s) {
+    fdx::launch_predict_fp8(P<const uint8_t>(X), n, P<const float>(w), P<float>(prob), P<float>(logit), S(s));
+  });
+  m.def("predict_shap", [](u X, int in_kind, int64_t n, int ld, int dz, int dphi, u a, u c, float bias, u prob,
+                           u logit, u phi, int ld_phi, u s) {
+    fdx::launch_predict_shap(P<const void>(X), in_kind, n, ld, dz, dphi, P<const float>(a), P<const float>(c), bias,
+                             P<float>(prob), P<float>(logit), P<float>(phi), ld_phi, S(s));
+  });
+
+  // logistic regression
+  m.def("logreg_pass_blocks", &fdx::logreg_pass_blocks);
+  m.def("logreg_pass", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, u partial, int nblocks, u s) {
+    fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
+                            hess, P<float>(partial), nblocks, S(s));
+  });
+  m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, float xs, u partial,
+                              int nblocks, u s) {
+    fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
+                                P<const int>(done), hess, xs, P<float>(partial), nblocks, S(s));
+  });
+  m.def("logreg_reduce", [](u partial, int nblocks, int ncols, u out, u done, u s) {
+    fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
+  });
+  m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi, u s) {
+    fdx::launch_newton_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), d, C, tol,
+                              max_iter, fi, S(s));
+  });
+  m.def("sgd_update", [](u red, u state, u w32, int d, double C, double lr, double mom, int fi, u s) {
+    fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), d, C, lr, mom, fi, S(s));
+  });
+
+  // knn / smote
+  m.def("row_half_norms", [](u X, int m, u out, int m_pad, u s) {
+    fdx::launch_row_half_norms(P<const float>(X), m, P<float>(out), m_pad, S(s));
+  });
+  m.def("knn_topk", [](u Q, int mq_pad, int mq, u C, u chalf, int mc_pad, int mc, int64_t self_off, int k, u oidx,
+                       u oscore, u s) {
+    fdx::launch_knn_topk(P<const float>(Q), mq_pad, mq, P<const float>(C), P<const float>(chalf), mc_pad, mc,
+                         self_off, k, P<int>(oidx), P<float>(oscore), S(s));
+  });
+  m.def("smote_generate", [](u C, u nbr, int mq, int k, int64_t q_off, int64_t n_new, uint64_t seed,
+                             uint64_t counter_base, float label, int out_kind, float out_scale, u out, u s) {
+    fdx::launch_smote_generate(P<const float>(C), P<const int>(nbr), mq, k, q_off, n_new, seed, counter_base, label,
+                               out_kind, out_scale, P<void>(out), S(s));
+  });
+
+  // auc / confusion
+  m.def("auc_compact", [](u scores, u labels, int64_t n, u pos, u counter, u s) {
+    fdx::launch_auc_compact(P<const float>(scores), P<const uint8_t>(labels), n, P<float>(pos),
+                            P<unsigned long long>(counter), S(s));
+  });
+  m.def("sort_chunks", [](u pos, int64_t cap, u counter, int chunk, int nchunks, u s) {
+    fdx::launch_sort_chunks(P<float>(pos), cap, P<const unsigned long long>(counter), chunk, nchunks, S(s));
+  });
+  m.def("auc_count", [](u scores, u labels, int64_t n, u pos, u counter, int chunk, int nchunks, u out, u s) {
+    fdx::launch_auc_count(P<const float>(scores), P<const uint8_t>(labels), n, P<const float>(pos),
+                          P<const unsigned long long>(counter), chunk, nchunks, P<unsigned long long>(out), S(s));
+  });
+  m.def("confusion", [](u scores, u labels, int64_t n, float thr, u out4, u s) {
+    fdx::launch_confusion(P<const float>(scores), P<const uint8_t>(labels), n, thr, P<unsigned long long>(out4), S(s));
+  });
+}

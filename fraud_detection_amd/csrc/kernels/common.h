@@ -1,0 +1,153 @@
+// Shared device helpers for the gfx950 (MI355X / CDNA4) kernels of fraud_detection_amd.
+//
+// Design centre: the reference's feature matrix is [N][30] (Kaggle creditcard
+// schema: Time, V1..V28, Amount).  Every device-resident training/serving row is padded to 32
+// columns so a row is exactly 64 B in bf16 (4 x 16 B vector loads, one cache line pair):
+//
+//     col 0..29 : standardized features
+//     col 30    : 1.0  (intercept column; the logistic weight w[30] is the intercept)
+//     col 31    : label (0/1) for training buffers, 0 for inference buffers (w[31] is always 0)
+//
+// Wave size is 64 on CDNA (never 32): all cross-lane reductions below use width-64 shuffles.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fdx {
+
+constexpr int kWave = 64;
+constexpr int kCols = 32;        // padded row width
+constexpr int kBiasCol = 30;     // constant 1.0 column
+constexpr int kLabelCol = 31;    // label column in training buffers
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// ---- bf16 <-> f32 -------------------------------------------------------------------------
+__device__ __forceinline__ float bf16lo(uint32_t packed) { return __uint_as_float(packed << 16); }
+__device__ __forceinline__ float bf16hi(uint32_t packed) { return __uint_as_float(packed & 0xffff0000u); }
+__device__ __forceinline__ float bf16_to_f32(uint16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Round-to-nearest-even f32 -> bf16 through the compiler's native conversion (gfx950 emits
+// v_cvt_pk_bf16_f32, which keeps NaNs NaN; MI355X_MICROARCH.md "Correctness boundaries").
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
+}
+
+// ---- OCP fp8 e4m3fn (gfx950 is OCP, not fnuz) ---------------------------------------------
+// Software RNE encode/decode so the storage format is bit-exact and testable on the host.
+__host__ __device__ __forceinline__ float fp8e4m3_to_f32(uint8_t v) {
+  uint32_t s = (v >> 7) & 1u, e = (v >> 3) & 0xfu, m = v & 7u;
+  float out;
+  if (e == 0) {
+    out = (float)m * 0.001953125f;  // m * 2^-9 (subnormal: 2^-6 * m/8)
+  } else if (e == 15 && m == 7) {
+    out = __builtin_nanf("");
+  } else {
+    out = __builtin_ldexpf(1.0f + (float)m * 0.125f, (int)e - 7);
+  }
+  return s ? -out : out;
+}
+__host__ __device__ __forceinline__ uint8_t f32_to_fp8e4m3(float f) {
+  uint32_t bits = __builtin_bit_cast(uint32_t, f);
+  uint8_t sign = (uint8_t)((bits >> 31) << 7);
+  float a = __builtin_fabsf(f);
+  if (!(a == a)) return 0x7f;                 // NaN
+  if (a >= 464.0f) return sign | 0x7e;        // saturate to 448 (finite, OCP satfinite)
+  if (a < 0.0009765625f) return sign;         // below half of min subnormal 2^-9
+  int e;
+  float fr = __builtin_frexpf(a, &e);         // a = fr * 2^e, fr in [0.5, 1)
+  int be = e - 1 + 7;                         // biased exponent of 1.xxx form
+  if (be <= 0) {                              // subnormal: value = m * 2^-9
+    float q = a * 512.0f;
+    float r = __builtin_rintf(q);             // RNE
+    return sign | (uint8_t)r;
+  }
+  float mant = (fr * 2.0f - 1.0f) * 8.0f;     // 3-bit mantissa in [0,8)
+  float r = __builtin_rintf(mant);
+  if (r >= 8.0f) { r = 0.0f; be += 1; }
+  if (be > 15 || (be == 15 && r >= 7.0f)) return sign | 0x7e;
+  return sign | (uint8_t)(be << 3) | (uint8_t)r;
+}
+
+// ---- cross-lane reductions (wave64) ---------------------------------------------------------
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+// Sum over lanes that share (lane & (group-1)); i.e. reduce across the lane bits >= log2(group).
+template <int GROUP, typename T>
+__device__ __forceinline__ T strided_sum(T v) {
+#pragma unroll
+  for (int o = GROUP; o < kWave; o <<= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+// Sum within aligned groups of G lanes (G = 2,4,8,...).
+template <int G, typename T>
+__device__ __forceinline__ T group_sum(T v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ float fast_sigmoid(float z) {
+  // 1/(1+exp(-z)) with exp via v_exp_f32 (exp2); saturates cleanly at +-inf.
+  return __frcp_rn(1.0f + __expf(-z));
+}
+// log(1 + exp(z)) computed stably.
+__device__ __forceinline__ float softplus(float z) {
+  return z > 0.0f ? z + log1pf(__expf(-z)) : log1pf(__expf(z));
+}
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+// ---- Philox4x32-10 counter-based RNG (deterministic, order-independent) -------------------
+struct Philox4 { uint32_t x, y, z, w; };
+__host__ __device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+  uint64_t p = (uint64_t)a * (uint64_t)b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+__host__ __device__ __forceinline__ Philox4 philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2,
+                                                          uint32_t c3, uint32_t k0, uint32_t k1) {
+  const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t hi0, hi1;
+    uint32_t lo0 = mulhilo(M0, c0, &hi0);
+    uint32_t lo1 = mulhilo(M1, c2, &hi1);
+    uint32_t n0 = hi1 ^ c1 ^ k0, n1 = lo1, n2 = hi0 ^ c3 ^ k1, n3 = lo0;
+    c0 = n0; c1 = n1; c2 = n2; c3 = n3;
+    k0 += W0; k1 += W1;
+  }
+  return Philox4{c0, c1, c2, c3};
+}
+__host__ __device__ __forceinline__ float u32_to_unit(uint32_t v) {  // [0, 1)
+  return (float)(v >> 8) * (1.0f / 16777216.0f);
+}
+// Unbiased-enough range reduction: floor(v * n / 2^32) (Lemire multiply-shift).
+__host__ __device__ __forceinline__ uint32_t u32_range(uint32_t v, uint32_t n) {
+  return (uint32_t)(((uint64_t)v * (uint64_t)n) >> 32);
+}
+
+// Grid sizing for streaming kernels: enough blocks to fill 256 CUs several times over
+// (cdna_hip_programming.md Guideline 11), grid-stride beyond that.
+__host__ inline int stream_grid(int64_t work_items, int items_per_block, int max_blocks = 2048) {
+  int64_t b = (work_items + items_per_block - 1) / items_per_block;
+  if (b < 1) b = 1;
+  if (b > max_blocks) b = max_blocks;
+  return (int)b;
+}
+
+}  // namespace fdx

@@ -1,0 +1,95 @@
+// Host-side launch entry points for every HIP kernel in fraud_detection_amd.
+// Each launcher enqueues on the caller's hipStream_t (torch's current stream when called from
+// Python) and throws std::runtime_error on a launch error.  No allocation, no synchronisation:
+// every launcher is safe to capture into a hipGraph (cdna_hip_programming.md Guideline 9).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdexcept>
+#include <string>
+
+namespace fdx {
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    throw std::runtime_error(std::string("fdx kernel launch failed [") + what +
+                             "]: " + hipGetErrorString(e));
+  }
+}
+
+// ---- scaler.hip ----
+void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float* pivot,
+                           double* partial, int nblocks, hipStream_t stream);
+void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream);
+void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
+                            double* mean64, double* var64, double* scale64, float* mean32,
+                            float* inv32, hipStream_t stream);
+void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* idx,
+                       const float* mean32, const float* inv32, const uint8_t* labels,
+                       float bias_value, float out_scale, int out_kind, void* out,
+                       hipStream_t stream);
+void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t* counts,
+                          int nblocks, hipStream_t stream);
+void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream);
+void launch_compact_write(const uint8_t* labels, int64_t n, int target, const int64_t* offsets,
+                          int64_t* out_idx, int nblocks, hipStream_t stream);
+
+// ---- predict.hip ----
+void launch_predict_bf16(const uint16_t* X, int64_t n, const float* w, float* prob, float* logit,
+                         hipStream_t stream);
+void launch_predict_fp8(const uint8_t* X, int64_t n, const float* w, float* prob, float* logit,
+                        hipStream_t stream);
+// Fused predict + linear SHAP.  in_kind: 0 = bf16 [n][32], 1 = raw fp32 [n][ld].
+// z = sum_{j<dz} a_j x_j + bias;  phi_j = a_j (x_j - c_j), j < dphi.
+void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, int dphi,
+                         const float* a, const float* c, float bias, float* prob, float* logit,
+                         float* phi, int ld_phi, hipStream_t stream);
+
+// ---- logreg.hip ----
+constexpr int kLRPartStride = 1088;  // [0,32) grad, 32 loss, 33 wsum, [64,1088) Hessian 32x32
+int logreg_pass_blocks();
+void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
+                        const float* class_w, const int* done, int hessian, float* partial,
+                        int nblocks, hipStream_t stream);
+void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
+                            const float* class_w, const int* done, int hessian, float x_scale,
+                            float* partial, int nblocks, hipStream_t stream);
+void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
+                          const int* done, hipStream_t stream);
+// state layout: see logreg.hip NewtonState.
+void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
+                          double C, double tol, int max_iter, int fit_intercept,
+                          hipStream_t stream);
+void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
+                       double momentum, int fit_intercept, hipStream_t stream);
+
+// ---- knn.hip ----
+void launch_row_half_norms(const float* X, int m, float* out, int m_pad, hipStream_t stream);
+void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const float* chalf,
+                     int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
+                     float* out_score, hipStream_t stream);
+
+// ---- smote.hip ----
+void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
+                           int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
+                           int out_kind, float out_scale, void* out, hipStream_t stream);
+
+// ---- auc.hip ----
+void launch_auc_compact(const float* scores, const uint8_t* labels, int64_t n, float* pos,
+                        unsigned long long* counter, hipStream_t stream);
+void launch_sort_chunks(float* pos, int64_t npos_cap, const unsigned long long* counter,
+                        int chunk, int nchunks, hipStream_t stream);
+void launch_auc_count(const float* scores, const uint8_t* labels, int64_t n, const float* pos,
+                      const unsigned long long* counter, int chunk, int nchunks,
+                      unsigned long long* out_pairs, hipStream_t stream);
+void launch_confusion(const float* scores, const uint8_t* labels, int64_t n, float threshold,
+                      unsigned long long* out4, hipStream_t stream);
+
+// ---- kernelshap.hip ----
+void launch_kernelshap(const float* X, int n_expl, int d, const float* w, float b,
+                       const float* bg, int n_bg, const uint16_t* Z, int S, const float* Amat,
+                       const float* zlast, int link, float* phi, float* fx_out, float* f0_out,
+                       hipStream_t stream);
+
+}  // namespace fdx

@@ -1,0 +1,415 @@
+// K4 logreg_fused_step: logistic-regression training on MI355X.
+//
+// Reference behaviour being replaced: sklearn LogisticRegression(C=1, l2, lbfgs, max_iter=1000)
+// that produced models/logistic_model.joblib and the XGB fit loop of
+// train_model.py:58-106.  Objective (sklearn/linear_model/_logistic.py:453-470):
+//     obj(w) = (1/S) sum_i s_i * logloss_i + 1/(2 C S) * ||w_{0..d-1}||^2,  S = sum_i s_i,
+// intercept (w[30], the constant-1 column) unpenalised.
+//
+// One streaming pass per iteration over the padded bf16 (or fp8) training rows (col 31 = label):
+//   z = x.w -> p = sigmoid(z) -> r = s (p - y):   g += r x,  loss += s (softplus(z) - y z)
+//   H += (sqrt(s p (1-p)) x)(sqrt(s p (1-p)) x)^T          (only for the Newton solver)
+// The gradient/loss part runs on the VALU in fp32 (exact enough that the optimum is not biased by
+// bf16 rounding of the update terms); the 32x32 Hessian is an MFMA GEMM over the row axis:
+// each wave stages its 64 scaled rows (4 KiB) in a private LDS tile and reads them back with the
+// gfx950 transpose read ds_read_b64_tr_b16, which delivers exactly the A (= S^T) and B (= S)
+// fragments of v_mfma_f32_32x32x16_bf16 (cdna_hip_programming.md §3, T10) -- one register
+// fragment serves both operands.  4 MFMAs per 64 rows keep the Hessian far under the HBM time.
+//
+// Per-block partials are reduced in a fixed order (fp64) by a second kernel, so a fit is bitwise
+// reproducible run to run (no float atomics).  The Newton system (<= 32 unknowns) is solved on
+// device by a one-block fp64 Cholesky with backtracking, so a whole fit is a sequence of launches
+// with no host synchronisation (hipGraph-capturable); a device-side `done` flag turns the
+// remaining iterations into no-ops once converged.  With data parallelism the reduced 1088-double
+// vector is all-reduced over RCCL between the reduce and the update kernels (parallel/dp.py).
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = kThreads / kWave;
+constexpr int kPassBlocks = 1024;  // 4 per CU x 4 waves: 16 waves/CU of streaming loads
+
+typedef short lds_s4 __attribute__((ext_vector_type(4)));
+
+template <int FMT>
+__device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
+  x[0] = bf16lo(v.x); x[1] = bf16hi(v.x); x[2] = bf16lo(v.y); x[3] = bf16hi(v.y);
+  x[4] = bf16lo(v.z); x[5] = bf16hi(v.z); x[6] = bf16lo(v.w); x[7] = bf16hi(v.w);
+}
+__device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8], int q, int d, float inv_s) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t word = j < 4 ? v.x : v.y;
+    const float f = fp8e4m3_to_f32((uint8_t)(word >> (8 * (j & 3))));
+    x[j] = (q * 8 + j < d) ? f * inv_s : f;
+  }
+}
+
+template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
+__global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
+    const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
+    const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
+    float* __restrict__ partial) {
+  if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
+  __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
+  __shared__ float red[kWaves][34];
+  const int lane = lane_id(), wv = wave_id();
+  const int q = lane & 3, rr = lane >> 2;
+  float wl[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j];
+  const float cw0 = class_w[0], cw1 = class_w[1];
+  const float inv_s = 1.0f / x_scale;
+  float g[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) g[j] = 0.0f;
+  float lacc = 0.0f, wacc = 0.0f;
+  f32x16_t acc = {};
+  // transpose-read lane geometry (constant per lane): 16-lane group grp reads 4 rows x 16 cols
+  const int grp = lane >> 4, gi = lane & 15;
+  const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
+  uint16_t* my_tile = tile[wv];
+
+  const int64_t n = row_end - row_begin;
+  const int64_t step = (int64_t)gridDim.x * kWaves * 64;
+  for (int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64; base < n; base += step) {
+    float xs[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = base + 16 * u + rr;
+      if constexpr (FMT == 0) {
+        const uint4* X = reinterpret_cast<const uint4*>(Xv);
+        const uint4 v = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
+        unpack8<0>(v, xs[u]);
+      } else {
+        const uint2* X = reinterpret_cast<const uint2*>(Xv);
+        const uint2 v = row < n ? X[(row_begin + row) * 4 + q] : make_uint2(0, 0);
+        unpack8_fp8(v, xs[u], q, d_feat, inv_s);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float* x = xs[u];
+      float y = (q == 3) ? x[7] : 0.0f;
+      if (q == 3) x[7] = 0.0f;
+      float zp = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) zp = fmaf(wl[j], x[j], zp);
+      zp = group_sum<4>(zp);
+      y = group_sum<4>(y);
+      const bool ok = base + 16 * u + rr < n;
+      const float sw = ok ? (y > 0.5f ? cw1 : cw0) : 0.0f;
+      const float zc = fminf(fmaxf(zp, -80.0f), 80.0f);
+      const float e = __expf(-zc);
+      const float p = __frcp_rn(1.0f + e);
+      const float r = sw * (p - y);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = fmaf(r, x[j], g[j]);
+      if (q == 0) {
+        lacc = fmaf(sw, softplus(zp) - y * zp, lacc);
+        wacc += sw;
+      }
+      if constexpr (HESS) {
+        const float dd = sqrtf(sw * p * (e * p));  // sqrt(s p (1-p)), 1-p = e p (no cancellation)
+        uint4 pk;
+        pk.x = pack_bf16x2(x[0] * dd, x[1] * dd);
+        pk.y = pack_bf16x2(x[2] * dd, x[3] * dd);
+        pk.z = pack_bf16x2(x[4] * dd, x[5] * dd);
+        pk.w = pack_bf16x2(x[6] * dd, x[7] * dd);
+        *reinterpret_cast<uint4*>(my_tile + (16 * u + rr) * kCols + 8 * q) = pk;
+      }
+    }
+    if constexpr (HESS) {
+      // Wave-private tile: LDS instructions of one wave execute in order, so the transpose
+      // reads below observe this wave's writes; the wave_barrier only pins compiler order.
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const lds_s4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off));
+        const lds_s4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off +
+                                                        4 * kCols));
+        bf16x8_t f;
+        f[0] = a0[0]; f[1] = a0[1]; f[2] = a0[2]; f[3] = a0[3];
+        f[4] = a1[0]; f[5] = a1[1]; f[6] = a1[2]; f[7] = a1[3];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, f, acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+
+  // ---- block reduction (fixed order) ----
+#pragma unroll
+  for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
+  lacc = wave_sum(lacc);
+  wacc = wave_sum(wacc);
+  if (lane < 4) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[wv][8 * lane + j] = g[j];
+  }
+  if (lane == 0) {
+    red[wv][32] = lacc;
+    red[wv][33] = wacc;
+  }
+  float* hb = reinterpret_cast<float*>(&tile[0][0]);  // 4 x 1024 floats = the 16 KiB tile
+  if constexpr (HESS) {
+    // each wave overwrites only its own tile region (same bytes it read from)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int row = (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+      hb[wv * 1024 + row * kCols + (lane & 31)] = acc[k];
+    }
+  }
+  __syncthreads();
+  float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
+  if (threadIdx.x < 34) {
+    const int t = threadIdx.x;
+    out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+  }
+  if constexpr (HESS) {
+    for (int e = threadIdx.x; e < 1024; e += kThreads)
+      out[64 + e] = ((hb[e] + hb[1024 + e]) + hb[2048 + e]) + hb[3072 + e];
+  }
+}
+
+// Stage 2: fixed-order fp64 reduction of [nblocks][1088] partials.  Block = 64 columns x 16
+// row-groups (1024 threads).
+__global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __restrict__ partial,
+                                                             int nblocks, int ncols,
+                                                             double* __restrict__ out,
+                                                             const int* __restrict__ done) {
+  if (done != nullptr && *done) return;
+  __shared__ double red[16][64];
+  const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  double a0 = 0.0, a1 = 0.0;
+  if (col < ncols) {
+    int b = grp;
+    for (; b + 16 < nblocks; b += 32) {
+      a0 += (double)partial[(int64_t)b * kLRPartStride + col];
+      a1 += (double)partial[(int64_t)(b + 16) * kLRPartStride + col];
+    }
+    if (b < nblocks) a0 += (double)partial[(int64_t)b * kLRPartStride + col];
+  }
+  red[grp][c] = a0 + a1;
+  __syncthreads();
+  if (grp == 0 && col < ncols) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += red[k][c];
+    out[col] = s;
+  }
+}
+
+// ---- Newton / SGD state (fp64, on device) -------------------------------------------------
+enum : int {
+  kW = 0, kWPrev = 32, kStep = 64, kVel = 96,
+  kObjPrev = 128, kIter = 129, kBacktracks = 130, kGmax = 131, kObj = 132, kNAccepted = 133,
+  kConverged = 134, kStateSize = 256
+};
+
+__device__ void build_grad(const double* red, const double* st, int d, int fit_intercept,
+                           double reg, double S, double* grad, int t) {
+  if (t < kCols) {
+    double gv = 0.0;
+    if (t < d) gv = red[t] / S + reg * st[kW + t];
+    else if (t == kBiasCol && fit_intercept) gv = red[t] / S;
+    grad[t] = gv;
+  }
+}
+
+__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
+                                                           double* __restrict__ st,
+                                                           float* __restrict__ w32,
+                                                           int* __restrict__ done, int d, double C,
+                                                           double tol, int max_iter,
+                                                           int fit_intercept) {
+  if (*done) return;
+  __shared__ double A[32][33];
+  __shared__ double b[32];
+  __shared__ double grad[32];
+  __shared__ int idx[32];
+  __shared__ int decision;  // 0 accept+step, 1 backtrack, 2 converged
+  __shared__ double obj_s;
+  const int t = threadIdx.x;
+  const double S = red[33] > 0.0 ? red[33] : 1.0;
+  const double reg = 1.0 / (C * S);
+  const int m = d + (fit_intercept ? 1 : 0);
+  if (t < 32) idx[t] = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
+  build_grad(red, st, d, fit_intercept, reg, S, grad, t);
+  __syncthreads();
+  if (t == 0) {
+    double wn2 = 0.0;
+    for (int j = 0; j < d; ++j) wn2 += st[kW + j] * st[kW + j];
+    const double obj = red[32] / S + 0.5 * reg * wn2;
+    double gmax = 0.0;
+    for (int k = 0; k < m; ++k) gmax = fmax(gmax, fabs(grad[idx[k]]));
+    const int it = (int)st[kIter];
+    const double prev = st[kObjPrev];
+    int dec;
+    if (it > 0 && obj > prev + 1e-12 * fabs(prev) && st[kBacktracks] < 40.0) dec = 1;
+    else if (gmax <= tol) dec = 2;
+    else dec = 0;
+    decision = dec;
+    obj_s = obj;
+    st[kObj] = obj;
+    if (dec != 1) st[kGmax] = gmax;
+  }
+  __syncthreads();
+  const int dec = decision;
+  if (dec == 1) {  // objective went up: halve the last step from the last accepted point
+    if (t < kCols) {
+      st[kStep + t] *= 0.5;
+      st[kW + t] = st[kWPrev + t] + st[kStep + t];
+    }
+    if (t == 0) st[kBacktracks] += 1.0;
+  } else if (dec == 2) {
+    if (t == 0) {
+      st[kConverged] = 1.0;
+      *done = 1;
+    }
+  } else {
+    // H_active = H/S + reg I (penalised coords); solve H s = -grad by Cholesky (fp64).
+    if (t < m) {
+      for (int k = 0; k < m; ++k) {
+        const int r = idx[t], c = idx[k];
+        double h = red[64 + r * kCols + c] / S;
+        if (r == c && r < d) h += reg;
+        A[t][k] = h;
+      }
+      b[t] = -grad[idx[t]];
+    }
+    __syncthreads();
+    for (int k = 0; k < m; ++k) {
+      if (t == 0) {
+        double piv = A[k][k];
+        A[k][k] = sqrt(piv > 1e-300 ? piv : 1e-300);
+      }
+      __syncthreads();
+      if (t > k && t < m) A[t][k] /= A[k][k];
+      __syncthreads();
+      if (t > k && t < m) {
+        for (int j = k + 1; j <= t; ++j) A[t][j] -= A[t][k] * A[j][k];
+      }
+      __syncthreads();
+    }
+    for (int k = 0; k < m; ++k) {  // L y = b
+      if (t == 0) b[k] /= A[k][k];
+      __syncthreads();
+      if (t > k && t < m) b[t] -= A[t][k] * b[k];
+      __syncthreads();
+    }
+    for (int k = m - 1; k >= 0; --k) {  // L^T x = y
+      if (t == 0) b[k] /= A[k][k];
+      __syncthreads();
+      if (t < k) b[t] -= A[k][t] * b[k];
+      __syncthreads();
+    }
+    if (t < kCols) {
+      st[kWPrev + t] = st[kW + t];
+      st[kStep + t] = 0.0;
+    }
+    __syncthreads();
+    if (t < m) {
+      const int j = idx[t];
+      st[kStep + j] = b[t];
+      st[kW + j] = st[kWPrev + j] + b[t];
+    }
+    if (t == 0) {
+      st[kObjPrev] = obj_s;
+      st[kBacktracks] = 0.0;
+      st[kNAccepted] += 1.0;
+    }
+  }
+  __syncthreads();
+  if (t < kCols) w32[t] = (t == kLabelCol) ? 0.0f : (float)st[kW + t];
+  if (t == 0) {
+    st[kIter] += 1.0;
+    if (dec != 2 && (int)st[kIter] >= max_iter) *done = 1;
+  }
+}
+
+// Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.
+__global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict__ red,
+                                                        double* __restrict__ st,
+                                                        float* __restrict__ w32, int d, double C,
+                                                        double lr, double momentum,
+                                                        int fit_intercept) {
+  __shared__ double grad[32];
+  const int t = threadIdx.x;
+  const double S = red[33] > 0.0 ? red[33] : 1.0;
+  const double reg = 1.0 / (C * S);
+  build_grad(red, st, d, fit_intercept, reg, S, grad, t);
+  __syncthreads();
+  if (t < kCols) {
+    const double v = momentum * st[kVel + t] - lr * grad[t];
+    st[kVel + t] = v;
+    st[kW + t] += v;
+    w32[t] = (t == kLabelCol) ? 0.0f : (float)st[kW + t];
+  }
+  if (t == 0) {
+    double wn2 = 0.0;
+    for (int j = 0; j < d; ++j) wn2 += st[kW + j] * st[kW + j];
+    st[kObj] = red[32] / S + 0.5 * reg * wn2;
+    st[kIter] += 1.0;
+  }
+}
+
+}  // namespace
+
+int logreg_pass_blocks() { return kPassBlocks; }
+
+void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
+                        const float* class_w, const int* done, int hessian, float* partial,
+                        int nblocks, hipStream_t stream) {
+  if (hessian)
+    logreg_pass_kernel<true, 0><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
+                                                                 class_w, done, 1.0f, 32, partial);
+  else
+    logreg_pass_kernel<false, 0><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
+                                                                  class_w, done, 1.0f, 32, partial);
+  check_launch("logreg_pass");
+}
+
+void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
+                            const float* class_w, const int* done, int hessian, float x_scale,
+                            float* partial, int nblocks, hipStream_t stream) {
+  // fp8 rows store features * x_scale for columns < 30; the bias (col 30) and label (col 31)
+  // are stored unscaled.
+  if (hessian)
+    logreg_pass_kernel<true, 1><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
+                                                                 class_w, done, x_scale, 30,
+                                                                 partial);
+  else
+    logreg_pass_kernel<false, 1><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
+                                                                  class_w, done, x_scale, 30,
+                                                                  partial);
+  check_launch("logreg_pass_fp8");
+}
+
+void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
+                          const int* done, hipStream_t stream) {
+  // ncols = 64 for gradient-only passes (SGD), kLRPartStride when the Hessian was accumulated.
+  logreg_reduce_kernel<<<(ncols + 63) / 64, 1024, 0, stream>>>(partial, nblocks, ncols, out, done);
+  check_launch("logreg_reduce");
+}
+
+void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
+                          double C, double tol, int max_iter, int fit_intercept,
+                          hipStream_t stream) {
+  newton_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter,
+                                             fit_intercept);
+  check_launch("newton_update");
+}
+
+void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
+                       double momentum, int fit_intercept, hipStream_t stream) {
+  sgd_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, d, C, lr, momentum, fit_intercept);
+  check_launch("sgd_update");
+}
+
+}  // namespace fdx

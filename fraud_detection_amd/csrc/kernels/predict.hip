@@ -1,0 +1,229 @@
+// K5 predict_fused and K6 shap_linear.
+//
+// Reference behaviour being replaced: LogisticRegression.predict / predict_proba after
+// StandardScaler.transform (api/app.py:194-240, predict_single.py:28-32, deploy.py:33-37,
+// evaluate_model.py:26-27, xai_tasks.py:95-100) and the linear attribution
+// phi_i = w_i (x_i - E[x_i]) of shap.LinearExplainer (explain_model.py:24-27, api/worker.py:75)
+// / coef_ * x (xai_tasks.py:103-110).  SURVEY.md §2.3 rows K5, K6.
+//
+// MI355X mapping: pure HBM streaming.
+//   * predict (bf16 rows, 64 B): 4 lanes per row x 16 B, so one wave-instruction reads 16 whole
+//     rows = 1 KiB contiguous; 4 row-groups are issued before any is consumed (ILP).  Each lane
+//     reduces 8 products, a 4-lane butterfly (DPP-able xor 1/2) finishes the dot, and the 4
+//     results land one per quad lane so the 64 output floats of a wave-iteration are written by
+//     one store instruction (a 256 B permutation, fully coalesced).
+//   * predict (fp8 e4m3 rows, 32 B): 2 lanes per row x 16 B.
+//   * predict+SHAP: 8 lanes per row x 4 columns; the SHAP output (30 floats/row) dominates the
+//     traffic, so lanes store their 4 attributions directly (16 B stores for padded layouts).
+//     Input is either the standardized bf16 training layout or raw fp32 features with the scaler
+//     folded into the weights (a_j = w_j / sigma_j, c_j = mu_j + sigma_j * bg_j) so online
+//     serving reads each raw byte exactly once.
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ float dot8_bf16(const uint4& v, const float* w) {
+  float z = bf16lo(v.x) * w[0];
+  z = fmaf(bf16hi(v.x), w[1], z);
+  z = fmaf(bf16lo(v.y), w[2], z);
+  z = fmaf(bf16hi(v.y), w[3], z);
+  z = fmaf(bf16lo(v.z), w[4], z);
+  z = fmaf(bf16hi(v.z), w[5], z);
+  z = fmaf(bf16lo(v.w), w[6], z);
+  z = fmaf(bf16hi(v.w), w[7], z);
+  return z;
+}
+
+__device__ __forceinline__ float dot16_fp8(const uint4& v, const float* w) {
+  const uint32_t words[4] = {v.x, v.y, v.z, v.w};
+  float z = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+#pragma unroll
+    for (int b = 0; b < 4; ++b) z = fmaf(fp8e4m3_to_f32((uint8_t)(words[k] >> (8 * b))), w[4 * k + b], z);
+  }
+  return z;
+}
+
+// bf16: LPR = 4 lanes per row (8 elems each); fp8: LPR = 2 (16 elems each).
+template <int LPR>
+__global__ __launch_bounds__(kThreads) void predict_kernel(const uint4* __restrict__ X, int64_t n,
+                                                           const float* __restrict__ w,
+                                                           float* __restrict__ prob,
+                                                           float* __restrict__ logit) {
+  constexpr int EPL = 32 / LPR;            // elements per lane
+  constexpr int RPI = kWave / LPR;         // rows per wave-instruction
+  constexpr int U = LPR;                   // row groups per iteration (so LPR lanes write U rows)
+  const int lane = lane_id();
+  const int q = lane & (LPR - 1);
+  const int rr = lane / LPR;
+  float wl[EPL];
+#pragma unroll
+  for (int j = 0; j < EPL; ++j) {
+    const int c = q * EPL + j;
+    wl[j] = (c == kLabelCol) ? 0.0f : w[c];
+  }
+  const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * RPI * U;
+  for (int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * RPI * U; base < n;
+       base += step) {
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t row = base + u * RPI + rr;
+      v[u] = row < n ? X[row * LPR + q] : make_uint4(0, 0, 0, 0);
+    }
+    float z[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float t;
+      if constexpr (LPR == 4) t = dot8_bf16(v[u], wl);
+      else t = dot16_fp8(v[u], wl);
+      z[u] = group_sum<LPR>(t);
+    }
+    float mine = z[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) mine = (q == u) ? z[u] : mine;
+    const int64_t row = base + q * RPI + rr;
+    if (row < n) {
+      if (logit) logit[row] = mine;
+      if (prob) prob[row] = fast_sigmoid(mine);
+    }
+  }
+}
+
+// Fused predict + linear SHAP.  8 lanes per row, 4 columns per lane.
+template <int IN, int VEC>  // IN: 0 = bf16 [n][32], 1 = fp32 [n][ld]
+__global__ __launch_bounds__(kThreads) void predict_shap_kernel(
+    const void* __restrict__ Xv, int64_t n, int ld, int dz, int dphi, const float* __restrict__ a,
+    const float* __restrict__ c, float bias, float* __restrict__ prob, float* __restrict__ logit,
+    float* __restrict__ phi, int ld_phi) {
+  const int lane = lane_id();
+  const int c0 = (lane & 7) * 4;
+  const int rsub = lane >> 3;
+  float al[4], cl[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    al[j] = (c0 + j < dz) ? a[c0 + j] : 0.0f;
+    cl[j] = c[c0 + j];
+  }
+  constexpr int U = 4;
+  const int64_t ngroups = (n + 7) >> 3;
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
+  for (int64_t g = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); g < ngroups;
+       g += nwaves * U) {
+    float x[U][4];
+    int64_t rows[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      rows[u] = (g + u * nwaves) * 8 + rsub;
+      const bool ok = (g + u * nwaves) < ngroups && rows[u] < n;
+      if constexpr (IN == 0) {
+        const uint16_t* X = reinterpret_cast<const uint16_t*>(Xv);
+        uint2 t = ok ? *reinterpret_cast<const uint2*>(X + rows[u] * kCols + c0) : make_uint2(0, 0);
+        x[u][0] = bf16lo(t.x); x[u][1] = bf16hi(t.x); x[u][2] = bf16lo(t.y); x[u][3] = bf16hi(t.y);
+      } else {
+        const float* X = reinterpret_cast<const float*>(Xv);
+        const int dd = dz > dphi ? dz : dphi;
+        const float* p = X + rows[u] * (int64_t)ld + c0;
+        if (ok) {
+          if (VEC == 4 && c0 + 4 <= dd) {
+            float4 t = *reinterpret_cast<const float4*>(p);
+            x[u][0] = t.x; x[u][1] = t.y; x[u][2] = t.z; x[u][3] = t.w;
+          } else if (VEC >= 2 && c0 + 2 <= dd) {
+            float2 t = *reinterpret_cast<const float2*>(p);
+            x[u][0] = t.x; x[u][1] = t.y;
+            if (c0 + 4 <= dd) {
+              float2 t2 = *reinterpret_cast<const float2*>(p + 2);
+              x[u][2] = t2.x; x[u][3] = t2.y;
+            } else {
+              x[u][2] = (c0 + 2 < dd) ? p[2] : 0.0f;
+              x[u][3] = 0.0f;
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[u][j] = (c0 + j < dd) ? p[j] : 0.0f;
+          }
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) x[u][j] = 0.0f;
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float z = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z = fmaf(al[j], x[u][j], z);
+      z = group_sum<8>(z) + bias;
+      const bool ok = (g + u * nwaves) < ngroups && rows[u] < n;
+      if (!ok) continue;
+      if (phi) {
+        float o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = al[j] * (x[u][j] - cl[j]);
+        float* dst = phi + rows[u] * (int64_t)ld_phi + c0;
+        if ((ld_phi & 3) == 0 && c0 + 4 <= dphi) {
+          *reinterpret_cast<float4*>(dst) = make_float4(o[0], o[1], o[2], o[3]);
+        } else if ((ld_phi & 1) == 0 && c0 + 2 <= dphi) {
+          *reinterpret_cast<float2*>(dst) = make_float2(o[0], o[1]);
+          if (c0 + 4 <= dphi) *reinterpret_cast<float2*>(dst + 2) = make_float2(o[2], o[3]);
+          else if (c0 + 2 < dphi) dst[2] = o[2];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c0 + j < dphi) dst[j] = o[j];
+        }
+      }
+      if ((lane & 7) == 0) {
+        if (logit) logit[rows[u]] = z;
+        if (prob) prob[rows[u]] = fast_sigmoid(z);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+void launch_predict_bf16(const uint16_t* X, int64_t n, const float* w, float* prob, float* logit,
+                         hipStream_t stream) {
+  const int grid = stream_grid(n, (kThreads / kWave) * 64, 2048);
+  predict_kernel<4><<<grid, kThreads, 0, stream>>>(reinterpret_cast<const uint4*>(X), n, w, prob,
+                                                   logit);
+  check_launch("predict_bf16");
+}
+
+void launch_predict_fp8(const uint8_t* X, int64_t n, const float* w, float* prob, float* logit,
+                        hipStream_t stream) {
+  const int grid = stream_grid(n, (kThreads / kWave) * 64, 2048);
+  predict_kernel<2><<<grid, kThreads, 0, stream>>>(reinterpret_cast<const uint4*>(X), n, w, prob,
+                                                   logit);
+  check_launch("predict_fp8");
+}
+
+void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, int dphi,
+                         const float* a, const float* c, float bias, float* prob, float* logit,
+                         float* phi, int ld_phi, hipStream_t stream) {
+  const int grid = stream_grid((n + 7) / 8, (kThreads / kWave) * 4, 2048);
+  if (in_kind == 0) {
+    predict_shap_kernel<0, 1><<<grid, kThreads, 0, stream>>>(X, n, kCols, dz, dphi, a, c, bias,
+                                                             prob, logit, phi, ld_phi);
+  } else {
+    const uintptr_t al = reinterpret_cast<uintptr_t>(X);
+    if ((ld % 4) == 0 && (al % 16) == 0)
+      predict_shap_kernel<1, 4><<<grid, kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
+                                                               prob, logit, phi, ld_phi);
+    else if ((ld % 2) == 0 && (al % 8) == 0)
+      predict_shap_kernel<1, 2><<<grid, kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
+                                                               prob, logit, phi, ld_phi);
+    else
+      predict_shap_kernel<1, 1><<<grid, kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
+                                                               prob, logit, phi, ld_phi);
+  }
+  check_launch("predict_shap");
+}
+
+}  // namespace fdx

@@ -1,0 +1,375 @@
+// K1 scaler_stats / K2 scale_cast / stable label compaction.
+//
+// Reference behaviour being replaced: sklearn StandardScaler.fit / transform called from
+// train_model.py:36-40, preprocess.py:32-33, api/app.py:194, predict_single.py:25
+// (SURVEY.md §2.3 rows K1, K2).  Semantics: population variance (ddof=0), float64 accumulation,
+// near-constant columns get scale 1 (sklearn/preprocessing/_data.py:76-89,1046-1051).
+//
+// MI355X mapping: the raw matrix is row-major fp32 [n][ld] (ld >= d, d <= 30).  A wave reads
+// 8 rows per instruction with 8 lanes per row, each lane owning 4 fixed columns, so 64 lanes
+// touch 8 consecutive rows (960 B contiguous for ld = 30): coalesced without LDS staging, and
+// each lane's per-column accumulators live in registers with static indices.  Sums are taken
+// relative to a pivot row in fp64 (exact zero variance for constant columns, no cancellation
+// for the Time column whose mean is ~1e5), block partials are reduced in a fixed order by a
+// second kernel, so results are bitwise deterministic.
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+
+namespace {
+
+constexpr int kThreads = 256;  // 4 waves
+constexpr int kUnroll = 4;     // row groups in flight per lane
+
+// Load the (up to) 4 columns [c0, c0+4) of row r, masking columns >= d.
+template <int VEC>
+__device__ __forceinline__ void load_row4(const float* __restrict__ X, int64_t r, int ld, int c0,
+                                          int d, float v[4]) {
+  const float* p = X + r * (int64_t)ld + c0;
+  if constexpr (VEC == 4) {
+    if (c0 + 4 <= d) {
+      float4 t = *reinterpret_cast<const float4*>(p);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      return;
+    }
+  }
+  if constexpr (VEC >= 2) {
+    if (c0 + 2 <= d) {
+      float2 t = *reinterpret_cast<const float2*>(p);
+      v[0] = t.x; v[1] = t.y;
+      if (c0 + 4 <= d) {
+        float2 u = *reinterpret_cast<const float2*>(p + 2);
+        v[2] = u.x; v[3] = u.y;
+      } else {
+        v[2] = (c0 + 2 < d) ? p[2] : 0.0f;
+        v[3] = 0.0f;
+      }
+      return;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (c0 + j < d) ? p[j] : 0.0f;
+}
+
+template <int VEC>
+__global__ __launch_bounds__(kThreads) void scaler_partial_kernel(const float* __restrict__ X,
+                                                                  int64_t n, int ld, int d,
+                                                                  const float* __restrict__ pivot,
+                                                                  double* __restrict__ partial) {
+  const int lane = lane_id();
+  const int c0 = (lane & 7) * 4;
+  const int rsub = lane >> 3;
+  double piv[4], s[4], q[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    piv[j] = (c0 + j < d) ? (double)pivot[c0 + j] : 0.0;
+    s[j] = 0.0;
+    q[j] = 0.0;
+  }
+  const int64_t ngroups = (n + 7) >> 3;  // groups of 8 rows
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
+  for (int64_t g = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); g < ngroups;
+       g += nwaves * kUnroll) {
+    float v[kUnroll][4];
+    bool ok[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      const int64_t r = (g + u * nwaves) * 8 + rsub;
+      ok[u] = (g + u * nwaves) < ngroups && r < n;
+      if (ok[u]) {
+        load_row4<VEC>(X, r, ld, c0, d, v[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = 0.0f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (!ok[u]) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const double dd = (double)v[u][j] - piv[j];
+        s[j] += dd;
+        q[j] = fma(dd, dd, q[j]);
+      }
+    }
+  }
+  // reduce over the 8 row-lanes that share a column set (lane bits 3..5)
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s[j] = strided_sum<8>(s[j]);
+    q[j] = strided_sum<8>(q[j]);
+  }
+  __shared__ double red[kThreads / kWave][8][8];
+  if (lane < 8) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      red[wave_id()][lane][j] = s[j];
+      red[wave_id()][lane][4 + j] = q[j];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    const int c = threadIdx.x, l8 = c >> 2, j = c & 3;
+    double ss = 0.0, qq = 0.0;
+#pragma unroll
+    for (int w = 0; w < kThreads / kWave; ++w) {  // fixed order
+      ss += red[w][l8][j];
+      qq += red[w][l8][4 + j];
+    }
+    partial[(int64_t)blockIdx.x * 64 + c] = ss;
+    partial[(int64_t)blockIdx.x * 64 + 32 + c] = qq;
+  }
+}
+
+// Fixed-order reduction of [nblocks][64] fp64 partials into sums[64].
+__global__ __launch_bounds__(256) void scaler_reduce_kernel(const double* __restrict__ partial,
+                                                            int nblocks, double* __restrict__ sums) {
+  __shared__ double red[4][64];
+  const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  double acc = 0.0;
+  for (int b = grp; b < nblocks; b += 4) acc += partial[(int64_t)b * 64 + e];
+  red[grp][e] = acc;
+  __syncthreads();
+  if (threadIdx.x < 64) sums[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+}
+
+// mean / var / scale from (possibly all-reduced) shifted sums.  One wave.
+__global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n,
+                                       const float* __restrict__ pivot, int d,
+                                       double* __restrict__ mean64, double* __restrict__ var64,
+                                       double* __restrict__ scale64, float* __restrict__ mean32,
+                                       float* __restrict__ inv32) {
+  const int c = threadIdx.x;
+  if (c >= kCols) return;
+  if (c < d) {
+    const double m = sums[c] / n;
+    const double mean = (double)pivot[c] + m;
+    double var = sums[32 + c] / n - m * m;
+    if (var < 0.0) var = 0.0;
+    const double eps = 2.220446049250313e-16;
+    const double ub = n * eps * var + (n * mean * eps) * (n * mean * eps);
+    const double scale = (var <= ub) ? 1.0 : sqrt(var);
+    mean64[c] = mean;
+    var64[c] = var;
+    scale64[c] = scale;
+    mean32[c] = (float)mean;
+    inv32[c] = (float)(1.0 / scale);
+  } else {
+    mean64[c] = 0.0; var64[c] = 0.0; scale64[c] = 1.0;
+    mean32[c] = 0.0f; inv32[c] = 0.0f;
+  }
+}
+
+// K2: standardize + pad to 32 columns + cast.  OUT: 0 = bf16, 1 = fp32, 2 = fp8 e4m3fn.
+// Optional row gather (idx != nullptr): output row i reads input row idx[i].
+template <int VEC, int OUT>
+__global__ __launch_bounds__(kThreads) void scale_cast_kernel(
+    const float* __restrict__ X, int64_t n, int ld, int d, const int64_t* __restrict__ idx,
+    const float* __restrict__ mean32, const float* __restrict__ inv32,
+    const uint8_t* __restrict__ labels, float bias_value, float out_scale, void* __restrict__ out) {
+  const int lane = lane_id();
+  const int c0 = (lane & 7) * 4;
+  const int rsub = lane >> 3;
+  float mu[4], inv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    mu[j] = mean32[c0 + j];
+    inv[j] = inv32[c0 + j];
+  }
+  const int64_t ngroups = (n + 7) >> 3;
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
+  for (int64_t g = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); g < ngroups;
+       g += nwaves * kUnroll) {
+    float v[kUnroll][4];
+    int64_t rows[kUnroll];
+    bool ok[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      rows[u] = (g + u * nwaves) * 8 + rsub;
+      ok[u] = (g + u * nwaves) < ngroups && rows[u] < n;
+      if (ok[u]) {
+        const int64_t src = idx ? idx[rows[u]] : rows[u];
+        load_row4<VEC>(X, src, ld, c0, d, v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) {
+      if (!ok[u]) continue;
+      float o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        if (c < d) o[j] = (v[u][j] - mu[j]) * inv[j];
+        else if (c == kBiasCol) o[j] = bias_value;
+        else if (c == kLabelCol) {
+          const int64_t src = idx ? idx[rows[u]] : rows[u];
+          o[j] = labels ? (float)labels[src] : 0.0f;
+        } else o[j] = 0.0f;
+      }
+      const int64_t base = rows[u] * kCols + c0;
+      if constexpr (OUT == 0) {
+        uint2 pk;
+        pk.x = pack_bf16x2(o[0], o[1]);
+        pk.y = pack_bf16x2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + base) = pk;
+      } else if constexpr (OUT == 1) {
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(out) + base) =
+            make_float4(o[0], o[1], o[2], o[3]);
+      } else {
+        // fp8 storage: features are multiplied by out_scale (per-tensor) before encoding;
+        // bias / label columns are stored unscaled (1.0 and 0/1 are exact in e4m3).
+        uint32_t pk = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float val = (c0 + j < d) ? o[j] * out_scale : o[j];
+          pk |= (uint32_t)f32_to_fp8e4m3(val) << (8 * j);
+        }
+        *reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(out) + base) = pk;
+      }
+    }
+  }
+}
+
+// ---- stable compaction of row indices whose label == target -------------------------------
+// Blocks own contiguous row ranges so the output order equals the input order.
+constexpr int kCompactThreads = 256;
+
+__device__ __forceinline__ void block_range(int64_t n, int64_t* lo, int64_t* hi) {
+  const int64_t per = ((n + gridDim.x - 1) / gridDim.x + kCompactThreads - 1) / kCompactThreads *
+                      kCompactThreads;
+  *lo = (int64_t)blockIdx.x * per;
+  *hi = *lo + per < n ? *lo + per : n;
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(
+    const uint8_t* __restrict__ labels, int64_t n, int target, int64_t* __restrict__ counts) {
+  int64_t lo, hi;
+  block_range(n, &lo, &hi);
+  int64_t c = 0;
+  for (int64_t r = lo + threadIdx.x; r < hi; r += kCompactThreads) c += (labels[r] == target);
+  c = wave_sum(c);
+  __shared__ int64_t red[kCompactThreads / kWave];
+  if (lane_id() == 0) red[wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < kCompactThreads / kWave; ++w) t += red[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+// In-place exclusive scan of a small int64 array (n <= 4096), one block; writes total to tot.
+__global__ __launch_bounds__(1024) void exclusive_scan_small_kernel(int64_t* __restrict__ a, int n,
+                                                                    int64_t* __restrict__ tot) {
+  __shared__ int64_t s[4096];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = a[i];
+  __syncthreads();
+  if (threadIdx.x == 0) {  // n is tiny (<= 4096): a serial scan is ~microseconds and exact
+    int64_t run = 0;
+    for (int i = 0; i < n; ++i) {
+      const int64_t v = s[i];
+      s[i] = run;
+      run += v;
+    }
+    *tot = run;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = s[i];
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(
+    const uint8_t* __restrict__ labels, int64_t n, int target,
+    const int64_t* __restrict__ offsets, int64_t* __restrict__ out_idx) {
+  int64_t lo, hi;
+  block_range(n, &lo, &hi);
+  __shared__ int64_t wave_cnt[kCompactThreads / kWave];
+  int64_t base = offsets[blockIdx.x];
+  const int lane = lane_id(), w = wave_id();
+  for (int64_t r0 = lo; r0 < hi; r0 += kCompactThreads) {
+    const int64_t r = r0 + threadIdx.x;
+    const bool hit = (r < hi) && labels[r] == target;
+    const unsigned long long m = __ballot(hit);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[w] = __popcll(m);
+    __syncthreads();
+    int64_t off = base;
+    for (int i = 0; i < w; ++i) off += wave_cnt[i];
+    if (hit) out_idx[off + before] = r;
+    int64_t total = 0;
+    for (int i = 0; i < kCompactThreads / kWave; ++i) total += wave_cnt[i];
+    base += total;
+    __syncthreads();
+  }
+}
+
+inline int vec_for(const void* p, int ld) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  if ((ld % 4) == 0 && (a % 16) == 0) return 4;
+  if ((ld % 2) == 0 && (a % 8) == 0) return 2;
+  return 1;
+}
+
+}  // namespace
+
+void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float* pivot,
+                           double* partial, int nblocks, hipStream_t stream) {
+  switch (vec_for(X, ld)) {
+    case 4: scaler_partial_kernel<4><<<nblocks, kThreads, 0, stream>>>(X, n, ld, d, pivot, partial); break;
+    case 2: scaler_partial_kernel<2><<<nblocks, kThreads, 0, stream>>>(X, n, ld, d, pivot, partial); break;
+    default: scaler_partial_kernel<1><<<nblocks, kThreads, 0, stream>>>(X, n, ld, d, pivot, partial); break;
+  }
+  check_launch("scaler_partial");
+}
+
+void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream) {
+  scaler_reduce_kernel<<<1, 256, 0, stream>>>(partial, nblocks, sums);
+  check_launch("scaler_reduce");
+}
+
+void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
+                            double* mean64, double* var64, double* scale64, float* mean32,
+                            float* inv32, hipStream_t stream) {
+  scaler_finalize_kernel<<<1, 64, 0, stream>>>(sums, n, pivot, d, mean64, var64, scale64, mean32,
+                                               inv32);
+  check_launch("scaler_finalize");
+}
+
+void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* idx,
+                       const float* mean32, const float* inv32, const uint8_t* labels,
+                       float bias_value, float out_scale, int out_kind, void* out,
+                       hipStream_t stream) {
+  const int grid = stream_grid((n + 7) / 8, (kThreads / kWave) * kUnroll, 2048);
+  const int vec = vec_for(X, ld);
+#define FDX_SC(V, O)                                                                              \
+  scale_cast_kernel<V, O><<<grid, kThreads, 0, stream>>>(X, n, ld, d, idx, mean32, inv32, labels, \
+                                                         bias_value, out_scale, out)
+  if (out_kind == 0) {
+    if (vec == 4) FDX_SC(4, 0); else if (vec == 2) FDX_SC(2, 0); else FDX_SC(1, 0);
+  } else if (out_kind == 1) {
+    if (vec == 4) FDX_SC(4, 1); else if (vec == 2) FDX_SC(2, 1); else FDX_SC(1, 1);
+  } else {
+    if (vec == 4) FDX_SC(4, 2); else if (vec == 2) FDX_SC(2, 2); else FDX_SC(1, 2);
+  }
+#undef FDX_SC
+  check_launch("scale_cast");
+}
+
+void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t* counts,
+                          int nblocks, hipStream_t stream) {
+  compact_count_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, counts);
+  check_launch("compact_count");
+}
+void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream) {
+  exclusive_scan_small_kernel<<<1, 1024, 0, stream>>>(a, n, total);
+  check_launch("exclusive_scan_small");
+}
+void launch_compact_write(const uint8_t* labels, int64_t n, int target, const int64_t* offsets,
+                          int64_t* out_idx, int nblocks, hipStream_t stream) {
+  compact_write_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, offsets,
+                                                                out_idx);
+  check_launch("compact_write");
+}
+
+}  // namespace fdx

@@ -1,0 +1,89 @@
+// K9 smote_generate: synthetic minority rows x_new = x_i + lambda (x_nn - x_i).
+//
+// Reference behaviour being replaced: imblearn SMOTE._generate_samples (random row i among the
+// minority rows, random neighbour among its k nearest, lambda ~ U[0,1)) used at
+// train_model.py:65-66,91-92 and preprocess.py:43-44.  imblearn draws
+// from numpy MT19937; here every sample s owns Philox4x32-10 counter (s, counter_base), so the
+// output is independent of launch geometry and the CPU oracle (ops/reference.py) reproduces it
+// bit for bit before the bf16 rounding.
+//
+// MI355X mapping: write-bound stream.  4 lanes per synthetic row, 8 columns (two 16 B gathers of
+// each parent row, L2-resident) per lane, one 16 B store per lane: 16 rows = 1 KiB per
+// wave-instruction, written straight into the training buffer after the real rows (bf16 with
+// col 30 = 1 and col 31 = label, or fp8).
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kThreads = 256;
+
+template <int OUT>  // 0 = bf16 rows (64 B), 2 = fp8 e4m3 rows (32 B)
+__global__ __launch_bounds__(kThreads) void smote_generate_kernel(
+    const float* __restrict__ C, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
+    int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
+    float out_scale, void* __restrict__ out) {
+  const int lane = lane_id();
+  const int q = lane & 3, rr = lane >> 2;
+  const uint32_t range = (uint32_t)mq * (uint32_t)k;
+  const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 16;
+  for (int64_t s = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 16 + rr; s < n_new;
+       s += step) {
+    const Philox4 r = philox4x32_10((uint32_t)s, (uint32_t)(s >> 32), cb0, cb1, key0, key1);
+    const uint32_t pick = u32_range(r.x, range);
+    const int i = (int)(pick / (uint32_t)k);
+    const int kk = (int)(pick % (uint32_t)k);
+    const float lam = u32_to_unit(r.y);
+    const int jn = nbr[(int64_t)i * k + kk];
+    const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
+    const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
+    const float4 a0 = xi[0], a1 = xi[1], b0 = xj[0], b1 = xj[1];
+    float o[8] = {fmaf(lam, b0.x - a0.x, a0.x), fmaf(lam, b0.y - a0.y, a0.y),
+                  fmaf(lam, b0.z - a0.z, a0.z), fmaf(lam, b0.w - a0.w, a0.w),
+                  fmaf(lam, b1.x - a1.x, a1.x), fmaf(lam, b1.y - a1.y, a1.y),
+                  fmaf(lam, b1.z - a1.z, a1.z), fmaf(lam, b1.w - a1.w, a1.w)};
+    if (q == 3) {
+      o[6] = 1.0f;   // col 30: intercept column
+      o[7] = label;  // col 31: label
+    }
+    if constexpr (OUT == 0) {
+      uint4 pk;
+      pk.x = pack_bf16x2(o[0], o[1]);
+      pk.y = pack_bf16x2(o[2], o[3]);
+      pk.z = pack_bf16x2(o[4], o[5]);
+      pk.w = pack_bf16x2(o[6], o[7]);
+      reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
+    } else {
+      uint2 pk = make_uint2(0, 0);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const bool feat = (8 * q + jj) < kBiasCol;
+        const uint32_t b = f32_to_fp8e4m3(feat ? o[jj] * out_scale : o[jj]);
+        if (jj < 4) pk.x |= b << (8 * jj);
+        else pk.y |= b << (8 * (jj - 4));
+      }
+      reinterpret_cast<uint2*>(out)[s * 4 + q] = pk;
+    }
+  }
+}
+
+}  // namespace
+
+void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
+                           int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
+                           int out_kind, float out_scale, void* out, hipStream_t stream) {
+  if (n_new <= 0) return;
+  const int grid = stream_grid(n_new, (kThreads / kWave) * 16, 4096);
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
+  if (out_kind == 0)
+    smote_generate_kernel<0><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
+                                                           c0, c1, label, out_scale, out);
+  else
+    smote_generate_kernel<2><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
+                                                           c0, c1, label, out_scale, out);
+  check_launch("smote_generate");
+}
+
+}  // namespace fdx

@@ -1,0 +1,198 @@
+"""End-to-end device training pipeline: the MI355X replacement for train_model.py's hot path.
+
+Reference call stack (train_model.py:20-114):
+    split -> StandardScaler.fit(train) -> SMOTE(k=5).fit_resample -> classifier.fit -> AUC
+Here every numeric step is a HIP kernel on the rank's row shard:
+    K1 scaler stats (+ all-reduce C1) -> K2 standardize/pad/cast into the training buffer
+    -> stable minority compaction -> K2 gather (fp32 minority rows) -> all-gather C3
+    -> K8 MFMA k-NN (local queries vs global minority) -> K9 Philox SMOTE rows written in place
+    -> K4 Newton (all-reduce C5 per iteration) or momentum SGD (all-reduce C4 per minibatch).
+Evaluation: folded-scaler predict on raw fp32 test rows (K5) -> exact AUC (K10) + confusion.
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import asdict, dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import knn as knn_ops
+from ..ops import logreg as lr_ops
+from ..ops import metrics as metric_ops
+from ..ops import predict as pred_ops
+from ..ops import scaler as scaler_ops
+from ..ops.layout import BIAS_COL, DEFAULT_FP8_SCALE, NCOLS, TORCH_STORAGE
+
+
+@dataclass
+class TrainConfig:
+    solver: str = "newton"          # newton | sgd
+    C: float = 1.0
+    tol: float = 1e-8
+    max_iter: int = 25
+    fit_intercept: bool = True
+    class_weight: str | None = None  # None | "balanced"
+    smote: bool = True
+    k_neighbors: int = 5
+    sampling_ratio: float = 1.0     # minority : majority after SMOTE (1.0 = imblearn 'auto')
+    seed: int = 42
+    storage: str = "bf16"           # bf16 | fp8
+    fp8_scale: float = DEFAULT_FP8_SCALE
+    sgd_lr: float = 0.5
+    sgd_momentum: float = 0.9
+    sgd_epochs: int = 5
+    sgd_batch_rows: int = 1 << 22
+    check_every: int = 4
+    init_std: float = 0.01          # random-init weights ~ N(0, init_std^2) (seeded by `seed`)
+
+
+@dataclass
+class PipelineResult:
+    w: np.ndarray                  # [32] float64 standardized-space weights, w[30] = intercept
+    scaler: scaler_ops.ScalerStats
+    fit: lr_ops.FitInfo
+    n_rows: int                    # local raw training rows
+    n_train_rows: int              # local post-SMOTE rows
+    n_minority: int
+    n_synthetic: int
+    timings: dict = field(default_factory=dict)
+
+    @property
+    def coef(self) -> np.ndarray:
+        return self.w[: self.scaler.d].copy()
+
+    @property
+    def intercept(self) -> float:
+        return float(self.w[BIAS_COL])
+
+    def folded(self, bg_std=None):
+        mean, _, scale = self.scaler.numpy()
+        return pred_ops.fold_scaler(self.w, mean, scale, bg_std)
+
+
+class _Timer:
+    def __init__(self, device, enabled: bool):
+        self.enabled = enabled and device.type == "cuda"
+        self.device = device
+        self.t = {}
+        self._last = time.perf_counter()
+
+    def mark(self, name: str):
+        if not self.enabled:
+            return
+        torch.cuda.synchronize(self.device)
+        now = time.perf_counter()
+        self.t[name] = self.t.get(name, 0.0) + (now - self._last)
+        self._last = now
+
+
+class DevicePipeline:
+    def __init__(self, cfg: TrainConfig | None = None, comm=None):
+        self.cfg = cfg or TrainConfig()
+        self.comm = comm
+        self._ws = None
+        self._buf = None
+
+    def _world(self):
+        c = self.comm
+        return (c.rank, c.world_size) if c is not None else (0, 1)
+
+    def _train_buffer(self, n_rows: int, device) -> torch.Tensor:
+        dt = TORCH_STORAGE[self.cfg.storage]
+        if self._buf is None or self._buf.shape[0] < n_rows or self._buf.device != device or self._buf.dtype != dt:
+            self._buf = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
+        return self._buf[:n_rows]
+
+    def fit(self, X: torch.Tensor, y: torch.Tensor, profile: bool = False) -> PipelineResult:
+        cfg = self.cfg
+        dev = X.device
+        rank, world = self._world()
+        comm = self.comm if world > 1 else None
+        tm = _Timer(dev, profile)
+        n, d = X.shape
+        # ---- K1: scaler statistics (C1 all-reduce inside) --------------------------------
+        stats = scaler_ops.scaler_fit(X, comm=comm)
+        tm.mark("scaler_fit")
+        # ---- class counts (C2) and SMOTE quota ---------------------------------------------
+        idx_min = scaler_ops.compact_indices(y, 1)
+        n_min = int(idx_min.shape[0])
+        n_maj = n - n_min
+        n_new = 0
+        if cfg.smote and n_min > 0:
+            n_new = max(0, int(round(n_maj * cfg.sampling_ratio)) - n_min)
+        rows = self._train_buffer(n + n_new, dev)
+        # ---- K2: standardize + pad + cast the real rows (label in col 31) ---------------
+        scaler_ops.scale_cast(X, stats, labels=y, out_dtype=cfg.storage, out=rows[:n], fp8_scale=cfg.fp8_scale)
+        tm.mark("scale_cast")
+        if n_new > 0:
+            # ---- minority rows in fp32, gathered across ranks (C3) -----------------------
+            xmin = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min)
+            if comm is not None:
+                xall, counts = comm.all_gather_rows(xmin)
+                q_off = int(sum(counts[:rank]))
+            else:
+                xall, q_off = xmin, 0
+            tm.mark("minority_gather")
+            k = min(cfg.k_neighbors, xall.shape[0] - 1)
+            if k < 1:
+                raise ValueError("SMOTE needs at least 2 minority samples")
+            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off)
+            tm.mark("knn")
+            knn_ops.smote_generate(xall, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
+                                   fp8_scale=cfg.fp8_scale)
+            tm.mark("smote_generate")
+        # ---- class weights ---------------------------------------------------------------
+        class_w = (1.0, 1.0)
+        if cfg.class_weight == "balanced":
+            tot = float(n + n_new)
+            pos = float(n_min + n_new)
+            if comm is not None:
+                tot = comm.all_reduce_scalar(tot)
+                pos = comm.all_reduce_scalar(pos)
+            class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
+        # ---- K4: fit ---------------------------------------------------------------------
+        if dev.type == "cuda" and (self._ws is None or self._ws.device != dev):
+            self._ws = lr_ops.LRWorkspace(dev)
+        w0 = np.zeros(NCOLS)
+        if cfg.init_std > 0:
+            w0[:d] = np.random.default_rng(cfg.seed).normal(0.0, cfg.init_std, d)
+        if cfg.solver == "newton":
+            fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
+                                    fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
+                                    check_every=cfg.check_every, workspace=self._ws)
+        elif cfg.solver == "sgd":
+            fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
+                                 batch_rows=cfg.sgd_batch_rows, class_w=class_w, d=d, w0=w0,
+                                 fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
+                                 workspace=self._ws)
+        else:
+            raise ValueError(f"unknown solver {cfg.solver!r}")
+        tm.mark("fit")
+        return PipelineResult(w=fit.w, scaler=stats, fit=fit, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
+                              n_synthetic=n_new, timings=dict(tm.t))
+
+
+def evaluate(result: PipelineResult, X_test: torch.Tensor, y_test: torch.Tensor, comm=None) -> dict:
+    """Exact test ROC-AUC + confusion matrix at p > 0.5 (evaluate_model.py:26-53)."""
+    a, c, bias = result.folded()
+    dev = X_test.device
+    at = torch.from_numpy(a).to(dev)
+    ct = torch.from_numpy(c).to(dev)
+    _, _, logit = pred_ops.predict_shap_raw(X_test, at, ct, bias, dphi=0, want_logit=True)
+    if comm is not None and comm.world_size > 1:
+        logit_all, _ = comm.all_gather_rows(logit.reshape(-1, 1))
+        y_all, _ = comm.all_gather_rows(y_test.reshape(-1, 1))
+        logit, y_test = logit_all.reshape(-1).contiguous(), y_all.reshape(-1).contiguous()
+    auc = metric_ops.roc_auc(logit, y_test)
+    cm = metric_ops.confusion_counts(logit, y_test, 0.0)
+    tn, fp, fn, tp = (int(v) for v in cm)
+    return {"auc": auc, "tn": tn, "fp": fp, "fn": fn, "tp": tp,
+            "recall": tp / max(tp + fn, 1), "precision": tp / max(tp + fp, 1),
+            "accuracy": (tp + tn) / max(tn + fp + fn + tp, 1)}
+
+
+def result_summary(r: PipelineResult) -> dict:
+    d = {k: v for k, v in asdict(r.fit).items() if k != "w" and k != "history"}
+    d.update(n_rows=r.n_rows, n_train_rows=r.n_train_rows, n_minority=r.n_minority, n_synthetic=r.n_synthetic)
+    return d

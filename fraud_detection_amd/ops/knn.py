@@ -1,0 +1,98 @@
+"""K8 k-nearest neighbours (SMOTE) and K9 SMOTE sample generation."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import reference as ref
+from .layout import DEFAULT_FP8_SCALE, DTYPE_KIND, NCOLS, check_rows, storage_kind
+from .native import native, ptr, stream_of
+
+
+def _pad32(n: int) -> int:
+    return max(32, (n + 31) // 32 * 32)
+
+
+def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
+    if X.shape[0] == n_pad and X.is_contiguous():
+        return X
+    out = torch.zeros((n_pad, NCOLS), device=X.device, dtype=torch.float32)
+    out[: X.shape[0]] = X
+    return out
+
+
+def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False):
+    """k nearest candidates (squared L2) of each query row.
+
+    Q [mq, 32] / C [mc, 32] fp32 padded rows.  If ``self_offset >= 0``, query row q is candidate
+    row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
+    (ascending distance, ties -> smaller index) and optionally squared distances.
+    """
+    for t, nm in ((Q, "Q"), (C, "C")):
+        if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
+            raise ValueError(f"{nm} must be fp32 [m, 32]")
+    mq, mc = Q.shape[0], C.shape[0]
+    if not 1 <= k <= 8:
+        raise ValueError("k must be in [1, 8]")
+    n_valid = mc - (1 if self_offset >= 0 else 0)
+    if n_valid < k:
+        raise ValueError(f"need at least k={k} candidates besides self, have {n_valid}")
+    if self_offset >= 0 and self_offset + mq > mc:
+        raise ValueError("self_offset + mq exceeds the candidate set")
+    if not Q.is_cuda:
+        idx, d2 = ref.knn_topk(Q.numpy(), C.numpy(), k, self_offset)
+        idx_t = torch.from_numpy(idx)
+        return (idx_t, torch.from_numpy(d2.astype(np.float32))) if want_dist else idx_t
+    m = native()
+    s = stream_of(Q)
+    mq_pad, mc_pad = _pad32(mq), _pad32(mc)
+    Qp = _padded(Q.contiguous(), mq_pad)
+    Cp = _padded(C.contiguous(), mc_pad)
+    chalf = torch.empty(mc_pad, device=C.device, dtype=torch.float32)
+    m.row_half_norms(ptr(Cp), mc, ptr(chalf), mc_pad, s)
+    idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
+    score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
+    m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), ptr(chalf), mc_pad, mc, int(self_offset), int(k), ptr(idx),
+               ptr(score), s)
+    if want_dist:
+        qn = (Q.double() ** 2).sum(1, keepdim=True)
+        return idx, (qn - 2.0 * score.double()).float()
+    return idx
+
+
+def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int, out: torch.Tensor,
+                   seed: int = 42, counter_base: int = 0, label: float = 1.0,
+                   fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:
+    """Write ``n_new`` synthetic rows into ``out`` (a [n_new, 32] bf16/fp8 view, e.g. the tail of
+    the training buffer).  Sample s interpolates minority row (q_offset + i) toward neighbour
+    nbr[i, kk] with Philox draws keyed by (seed, s, counter_base)."""
+    if C.dtype != torch.float32 or C.dim() != 2 or C.shape[1] != NCOLS:
+        raise ValueError("C must be fp32 [m, 32]")
+    if nbr.dtype != torch.int32 or nbr.dim() != 2:
+        raise ValueError("nbr must be int32 [mq, k]")
+    mq, k = nbr.shape
+    if q_offset < 0 or q_offset + mq > C.shape[0]:
+        raise ValueError("query rows out of range of C")
+    check_rows(out, "out")
+    if out.shape[0] != n_new:
+        raise ValueError("out must have n_new rows")
+    kind = storage_kind(out)
+    if n_new == 0:
+        return out
+    if not C.is_cuda:
+        nb = nbr.numpy()
+        if nb.min() < 0 or nb.max() >= C.shape[0]:
+            raise ValueError("neighbour index out of range")
+        rows = ref.smote_generate(C.numpy(), nb, q_offset, n_new, seed, counter_base, label)
+        if kind == "bf16":
+            out.copy_(torch.from_numpy(rows).to(torch.bfloat16))
+        else:
+            r2 = rows.copy()
+            r2[:, :30] *= fp8_scale
+            out.copy_(torch.from_numpy(ref.fp8_encode(r2)))
+        return out
+    m = native()
+    m.smote_generate(ptr(C), ptr(nbr), mq, k, int(q_offset), int(n_new), int(seed) & (2**64 - 1),
+                     int(counter_base) & (2**64 - 1), float(label), DTYPE_KIND[kind], float(fp8_scale), ptr(out),
+                     stream_of(C))
+    return out

@@ -1,0 +1,164 @@
+"""K1 scaler statistics / K2 standardize+pad+cast / stable label compaction."""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import reference as ref
+from .layout import DEFAULT_FP8_SCALE, DTYPE_KIND, NCOLS, NFEAT_MAX, TORCH_STORAGE
+from .native import native, ptr, stream_of
+
+_SCALER_BLOCKS = 1024
+
+
+@dataclass
+class ScalerStats:
+    """StandardScaler parameters; fp64 for sklearn export, fp32 copies feed the kernels."""
+
+    n: float
+    d: int
+    mean64: torch.Tensor   # [32] float64
+    var64: torch.Tensor    # [32] float64
+    scale64: torch.Tensor  # [32] float64
+    mean32: torch.Tensor   # [32] float32
+    inv32: torch.Tensor    # [32] float32 (0 beyond d)
+
+    def to(self, device) -> "ScalerStats":
+        return ScalerStats(self.n, self.d, *(t.to(device) for t in
+                                             (self.mean64, self.var64, self.scale64, self.mean32, self.inv32)))
+
+    def numpy(self):
+        d = self.d
+        return (self.mean64[:d].cpu().numpy(), self.var64[:d].cpu().numpy(), self.scale64[:d].cpu().numpy())
+
+
+def _check_X(X: torch.Tensor) -> None:
+    if X.dim() != 2 or X.dtype != torch.float32:
+        raise ValueError(f"X must be 2-D float32, got {X.dtype} {tuple(X.shape)}")
+    if X.shape[1] > NFEAT_MAX:
+        raise ValueError(f"at most {NFEAT_MAX} features supported, got {X.shape[1]}")
+    if X.stride(1) != 1:
+        raise ValueError("X must be row-major with unit column stride")
+
+
+def scaler_partial_sums(X: torch.Tensor, pivot: torch.Tensor) -> torch.Tensor:
+    """Shifted fp64 sums [64] = (sum(x - pivot) | sum((x - pivot)^2)) over the rows of X."""
+    _check_X(X)
+    n, d = X.shape
+    if not X.is_cuda:
+        return torch.from_numpy(ref.scaler_sums(X.numpy(), pivot.cpu().numpy()))
+    m = native()
+    piv = torch.zeros(NCOLS, device=X.device, dtype=torch.float32)
+    piv[:d] = pivot[:d]
+    nb = min(_SCALER_BLOCKS, max(1, (n + 255) // 256))
+    partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
+    sums = torch.empty(64, device=X.device, dtype=torch.float64)
+    s = stream_of(X)
+    m.scaler_partial(ptr(X), n, X.stride(0), d, ptr(piv), ptr(partial), nb, s)
+    m.scaler_reduce(ptr(partial), nb, ptr(sums), s)
+    return sums
+
+
+def scaler_finalize(sums: torch.Tensor, n_total: float, pivot: torch.Tensor, d: int) -> ScalerStats:
+    dev = sums.device
+    if not sums.is_cuda:
+        mean, var, scale, m32, i32 = ref.scaler_finalize(sums.numpy(), float(n_total), pivot.cpu().numpy(), d)
+        return ScalerStats(float(n_total), d, torch.from_numpy(mean), torch.from_numpy(var),
+                           torch.from_numpy(scale), torch.from_numpy(m32), torch.from_numpy(i32))
+    m = native()
+    piv = torch.zeros(NCOLS, device=dev, dtype=torch.float32)
+    piv[:d] = pivot[:d]
+    mean64 = torch.empty(32, device=dev, dtype=torch.float64)
+    var64 = torch.empty_like(mean64)
+    scale64 = torch.empty_like(mean64)
+    mean32 = torch.empty(32, device=dev, dtype=torch.float32)
+    inv32 = torch.empty_like(mean32)
+    m.scaler_finalize(ptr(sums), float(n_total), ptr(piv), d, ptr(mean64), ptr(var64), ptr(scale64),
+                      ptr(mean32), ptr(inv32), stream_of(sums))
+    return ScalerStats(float(n_total), d, mean64, var64, scale64, mean32, inv32)
+
+
+def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) -> ScalerStats:
+    """StandardScaler.fit on device.  With ``comm`` (parallel.comm.Communicator) the shifted sums
+    and row counts are all-reduced so every rank gets the global statistics (collective C1)."""
+    _check_X(X)
+    n, d = X.shape
+    if pivot is None:
+        pivot = X[0].clone() if n > 0 else torch.zeros(d, device=X.device)
+        if comm is not None and comm.world_size > 1:
+            pivot = comm.broadcast(pivot.contiguous(), src=0)
+    sums = scaler_partial_sums(X, pivot)
+    n_total = float(n)
+    if comm is not None and comm.world_size > 1:
+        sums = comm.all_reduce(sums)
+        n_total = float(comm.all_reduce_scalar(float(n)))
+    return scaler_finalize(sums, n_total, pivot, d)
+
+
+def scale_cast(X: torch.Tensor, stats: ScalerStats, labels: torch.Tensor | None = None,
+               out_dtype: str = "bf16", out: torch.Tensor | None = None, idx: torch.Tensor | None = None,
+               bias_value: float = 1.0, fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:
+    """Standardize raw fp32 rows into the padded 32-column device layout (K2)."""
+    _check_X(X)
+    n_out = X.shape[0] if idx is None else idx.shape[0]
+    d = X.shape[1]
+    if labels is not None and (labels.dtype != torch.uint8 or labels.shape[0] != X.shape[0]):
+        raise ValueError("labels must be uint8 [n] aligned with X")
+    if out is None:
+        out = torch.empty((n_out, NCOLS), device=X.device, dtype=TORCH_STORAGE[out_dtype])
+    if out.shape != (n_out, NCOLS) or out.dtype != TORCH_STORAGE[out_dtype] or not out.is_contiguous():
+        raise ValueError(f"bad output buffer {tuple(out.shape)} {out.dtype}")
+    if not X.is_cuda:
+        r = ref.scale_cast(X.numpy(), stats.mean32.cpu().numpy(), stats.inv32.cpu().numpy(),
+                           None if labels is None else labels.numpy(), bias_value, out_dtype, fp8_scale,
+                           None if idx is None else idx.numpy())
+        out.copy_(r)
+        return out
+    if idx is not None:
+        if idx.dtype != torch.int64 or not idx.is_cuda:
+            raise ValueError("idx must be a device int64 tensor")
+    if out.data_ptr() % 16:
+        raise ValueError("output rows must be 16-byte aligned")
+    m = native()
+    m.scale_cast(ptr(X), X.shape[0] if idx is None else n_out, X.stride(0), d, ptr(idx),
+                 ptr(stats.mean32), ptr(stats.inv32), ptr(labels), float(bias_value), float(fp8_scale),
+                 DTYPE_KIND[out_dtype], ptr(out), stream_of(X))
+    return out
+
+
+def compact_indices(labels: torch.Tensor, target: int = 1, nblocks: int = 512) -> torch.Tensor:
+    """Stable indices of rows whose label == target (device: 3 deterministic kernels)."""
+    if labels.dtype != torch.uint8 or labels.dim() != 1:
+        raise ValueError("labels must be 1-D uint8")
+    n = labels.shape[0]
+    if not labels.is_cuda:
+        return torch.nonzero(labels == target, as_tuple=False).reshape(-1).to(torch.int64)
+    m = native()
+    s = stream_of(labels)
+    nb = int(max(1, min(nblocks, (n + 255) // 256)))
+    counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
+    total = torch.empty(1, device=labels.device, dtype=torch.int64)
+    m.compact_count(ptr(labels), n, target, ptr(counts), nb, s)
+    m.exclusive_scan_small(ptr(counts), nb, ptr(total), s)
+    cnt = int(total.item())  # host sync: output size is data dependent
+    out = torch.empty(cnt, device=labels.device, dtype=torch.int64)
+    if cnt:
+        m.compact_write(ptr(labels), n, target, ptr(counts), ptr(out), nb, s)
+    return out
+
+
+def stats_from_numpy(mean: np.ndarray, scale: np.ndarray, n: float = 0.0, var=None, device="cpu") -> ScalerStats:
+    """Build kernel-ready stats from an existing (e.g. sklearn) scaler's mean_/scale_."""
+    d = len(mean)
+    mean64 = np.zeros(32)
+    scale64 = np.ones(32)
+    var64 = np.zeros(32)
+    mean64[:d] = mean
+    scale64[:d] = scale
+    var64[:d] = scale ** 2 if var is None else var
+    inv32 = np.zeros(32, dtype=np.float32)
+    inv32[:d] = (1.0 / np.asarray(scale, dtype=np.float64)).astype(np.float32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(device)  # noqa: E731
+    return ScalerStats(float(n), d, t(mean64), t(var64), t(scale64), t(mean64.astype(np.float32)), t(inv32))

@@ -1,0 +1,220 @@
+"""Numerics of every HIP kernel against its CPU oracle (ops/reference.py / sklearn), on MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_amd.data.synthetic import separable
+from fraud_detection_amd.ops import knn as K
+from fraud_detection_amd.ops import logreg as L
+from fraud_detection_amd.ops import metrics as M
+from fraud_detection_amd.ops import predict as P
+from fraud_detection_amd.ops import reference as ref
+from fraud_detection_amd.ops import scaler as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _data(n, seed=0, rate=0.01):
+    X, y = separable(n, fraud_rate=rate, seed=seed)
+    return X, y
+
+
+@pytest.mark.parametrize("n,d", [(1, 30), (37, 30), (100_003, 30), (4096, 7), (2048, 29)])
+def test_scaler_stats_match_sklearn(dev, n, d):
+    from sklearn.preprocessing import StandardScaler
+
+    X, _ = _data(max(n, 2), seed=n)
+    X = X[:n, :d].contiguous()
+    X[:, min(2, d - 1)] = 3.25  # constant column -> scale 1
+    st = S.scaler_fit(X.to(dev))
+    sk = StandardScaler().fit(X.numpy().astype(np.float64))
+    mean, var, scale = st.numpy()
+    np.testing.assert_allclose(mean, sk.mean_, rtol=1e-12, atol=1e-9)
+    np.testing.assert_allclose(var, sk.var_, rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(scale, sk.scale_, rtol=1e-9, atol=1e-9)
+
+
+def test_scaler_odd_row_stride(dev):
+    X, _ = _data(5000, seed=9)
+    big = torch.zeros((5000, 33))
+    big[:, :30] = X
+    Xs = big[:, :30]  # ld = 33, odd: scalar-load kernel variant
+    st = S.scaler_fit(Xs.to(dev))
+    st_ref = S.scaler_fit(Xs.contiguous())
+    np.testing.assert_allclose(st.numpy()[0], st_ref.numpy()[0], rtol=1e-12)
+
+
+@pytest.mark.parametrize("kind", ["bf16", "f32", "fp8"])
+def test_scale_cast_matches_oracle(dev, kind):
+    X, y = _data(10_007, seed=3)
+    st = S.scaler_fit(X)
+    out_cpu = S.scale_cast(X, st, labels=y, out_dtype=kind) if kind != "fp8" else None
+    out_gpu = S.scale_cast(X.to(dev), st.to(dev), labels=y.to(dev), out_dtype=kind).cpu()
+    if kind == "fp8":
+        exp = S.scale_cast(X[:512], st, labels=y[:512], out_dtype="fp8")
+        assert torch.equal(out_gpu[:512], exp)
+    else:
+        assert torch.equal(out_gpu, out_cpu)
+    r = ref.rows_to_f32(out_gpu).numpy()
+    assert np.all(r[:, 30] == 1.0)
+    assert np.array_equal(r[:, 31], y.numpy().astype(np.float32))
+
+
+def test_scale_cast_gather(dev):
+    X, y = _data(20_000, seed=4)
+    st = S.scaler_fit(X)
+    idx = S.compact_indices(y.to(dev), 1)
+    assert torch.equal(idx.cpu(), torch.nonzero(y == 1).reshape(-1))
+    g = S.scale_cast(X.to(dev), st.to(dev), labels=y.to(dev), out_dtype="f32", idx=idx).cpu()
+    e = S.scale_cast(X, st, labels=y, out_dtype="f32", idx=idx.cpu())
+    assert torch.equal(g, e)
+
+
+def test_predict_bf16_and_fp8(dev):
+    X, y = _data(50_001, seed=5)
+    st = S.scaler_fit(X)
+    w = torch.from_numpy(np.r_[np.random.default_rng(0).normal(0, 0.5, 30), -3.0, 7.0])  # w[31] ignored
+    rows = S.scale_cast(X, st, labels=y, out_dtype="bf16")
+    p_ref, z_ref = P.predict_rows(rows, w, want_logit=True)
+    p, z = P.predict_rows(rows.to(dev), w, want_logit=True)
+    np.testing.assert_allclose(z.cpu().numpy(), z_ref.numpy(), rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(p.cpu().numpy(), p_ref.numpy(), rtol=1e-5, atol=1e-6)
+    rows8 = S.scale_cast(X.to(dev), st.to(dev), labels=y.to(dev), out_dtype="fp8")
+    p8, z8 = P.predict_rows(rows8, w, want_logit=True)
+    z8_ref = ref.predict_rows(ref.rows_to_f32(rows8.cpu()).numpy(), w.numpy())[1]
+    np.testing.assert_allclose(z8.cpu().numpy(), z8_ref, rtol=1e-5, atol=1e-4)
+
+
+def test_predict_shap_raw(dev):
+    X, _ = _data(30_011, seed=6)
+    st = S.scaler_fit(X)
+    w = np.r_[np.random.default_rng(1).normal(0, 1, 30), -4.2, 0.0]
+    mean, _, scale = st.numpy()
+    bg = np.random.default_rng(2).normal(0, 0.1, 30)
+    a, c, b = P.fold_scaler(w, mean, scale, bg)
+    at, ct = torch.from_numpy(a), torch.from_numpy(c)
+    p, phi, z = P.predict_shap_raw(X.to(dev), at.to(dev), ct.to(dev), b, want_logit=True)
+    Xs = (X.double().numpy() - mean) / scale
+    z_ref = Xs @ w[:30] + w[30]
+    phi_ref = w[:30] * (Xs - bg)
+    np.testing.assert_allclose(z.cpu().numpy(), z_ref, rtol=2e-5, atol=2e-4)
+    np.testing.assert_allclose(phi.cpu().numpy(), phi_ref, rtol=2e-4, atol=2e-4)
+    # additivity: sum(phi) = z - z(background)
+    z_bg = bg @ w[:30] + w[30]
+    np.testing.assert_allclose(phi.cpu().double().numpy().sum(1), z.cpu().numpy() - z_bg, atol=5e-3)
+
+
+def test_predict_shap_rows_bf16(dev):
+    X, y = _data(9_999, seed=8)
+    st = S.scaler_fit(X)
+    rows = S.scale_cast(X, st, labels=y, out_dtype="bf16")
+    w = torch.from_numpy(np.r_[np.random.default_rng(3).normal(0, 1, 30), -2.0, 0.0])
+    bg = torch.zeros(32)
+    p_ref, phi_ref = P.predict_shap_rows(rows, w, bg)
+    p, phi = P.predict_shap_rows(rows.to(dev), w, bg)
+    np.testing.assert_allclose(p.cpu().numpy(), p_ref.numpy(), rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(phi.cpu().numpy(), phi_ref.numpy(), rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("kind", ["bf16", "fp8"])
+def test_logreg_pass(dev, kind):
+    X, y = _data(70_000, seed=10, rate=0.05)
+    st = S.scaler_fit(X)
+    rows = S.scale_cast(X.to(dev), st.to(dev), labels=y.to(dev), out_dtype=kind)
+    w = torch.from_numpy(np.r_[np.random.default_rng(4).normal(0, 0.3, 30), -2.5, 0.0])
+    g, loss, ws, H = L.logreg_pass(rows, w, class_w=(1.0, 3.0))
+    g_r, loss_r, ws_r, H_r = ref.logreg_pass(ref.rows_to_f32(rows.cpu()).numpy(), w.numpy(), (1.0, 3.0))
+    np.testing.assert_allclose(g, g_r, rtol=1e-4, atol=1e-2)
+    assert abs(loss - loss_r) / loss_r < 1e-5
+    assert ws == pytest.approx(ws_r)
+    rel = np.linalg.norm(H - H_r) / np.linalg.norm(H_r)
+    assert rel < 5e-3, rel  # bf16-rounded sqrt(D) X operands, fp32 MFMA accumulation
+    np.testing.assert_allclose(H, H.T, atol=1e-6 * np.abs(H).max())
+
+
+def test_newton_gpu_matches_cpu_and_sklearn(dev):
+    from sklearn.linear_model import LogisticRegression
+
+    X, y = _data(60_000, seed=11, rate=0.03)
+    st = S.scaler_fit(X)
+    rows = S.scale_cast(X, st, labels=y, out_dtype="bf16")
+    fit_g = L.newton_fit(rows.to(dev), C=1.0, tol=1e-9, max_iter=30)
+    fit_c = L.newton_fit(rows, C=1.0, tol=1e-9, max_iter=30)
+    assert fit_g.converged and fit_c.converged
+    np.testing.assert_allclose(fit_g.w[:31], fit_c.w[:31], rtol=1e-5, atol=1e-5)
+    R = ref.rows_to_f32(rows).double().numpy()
+    sk = LogisticRegression(C=1.0, tol=1e-10, max_iter=2000).fit(R[:, :30], R[:, 31])
+    np.testing.assert_allclose(fit_g.w[:30], sk.coef_[0], atol=1e-4)
+    assert fit_g.w[30] == pytest.approx(sk.intercept_[0], abs=1e-4)
+
+
+def test_newton_deterministic(dev):
+    X, y = _data(40_000, seed=12, rate=0.05)
+    st = S.scaler_fit(X.to(dev))
+    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
+    a = L.newton_fit(rows, max_iter=15).w
+    b = L.newton_fit(rows, max_iter=15).w
+    assert np.array_equal(a, b)
+
+
+def test_sgd_reduces_objective(dev):
+    X, y = _data(40_000, seed=13, rate=0.1)
+    st = S.scaler_fit(X)
+    rows = S.scale_cast(X, st, labels=y).to(dev)
+    f0 = L.newton_fit(rows, max_iter=1).objective  # objective at w = 0
+    fs = L.sgd_fit(rows, lr=0.5, epochs=30, batch_rows=8192)
+    assert fs.objective < 0.7 * f0
+
+
+@pytest.mark.parametrize("mq,k", [(33, 5), (400, 5), (1000, 3), (2500, 8)])
+def test_knn_topk_exact(dev, mq, k):
+    rng = np.random.default_rng(mq)
+    C = np.zeros((mq + 17, 32), np.float32)
+    C[:, :30] = rng.normal(size=(mq + 17, 30))
+    C[:, 30] = 1.0
+    Ct = torch.from_numpy(C)
+    off = 5
+    Q = Ct[off: off + mq].contiguous()
+    idx, d2 = K.knn_topk(Q.to(dev), Ct.to(dev), k=k, self_offset=off, want_dist=True)
+    idx_r, d2_r = ref.knn_topk(Q.numpy(), C, k, off)
+    idx = idx.cpu().numpy()
+    match = (idx == idx_r).all(1)
+    # allow disagreement only where the reference distances are within fp32 rounding
+    for r in np.flatnonzero(~match):
+        gap = np.abs(np.sort(d2_r[r]) - np.sort(d2.cpu().numpy()[r].astype(np.float64)))
+        assert gap.max() < 1e-3, (r, idx[r], idx_r[r])
+    assert match.mean() > 0.99
+    assert not np.any(idx == (np.arange(mq)[:, None] + off))  # self excluded
+
+
+def test_smote_generate_matches_oracle(dev):
+    rng = np.random.default_rng(0)
+    m = 300
+    C = np.zeros((m, 32), np.float32)
+    C[:, :30] = rng.normal(size=(m, 30))
+    C[:, 30] = 1.0
+    C[:, 31] = 1.0
+    Ct = torch.from_numpy(C)
+    nbr = K.knn_topk(Ct, Ct, k=5, self_offset=0)
+    n_new = 50_000
+    out = torch.empty((n_new, 32), dtype=torch.bfloat16, device=dev)
+    K.smote_generate(Ct.to(dev), nbr.to(dev), 0, n_new, out, seed=42, counter_base=3)
+    exp = ref.smote_generate(C, nbr.numpy(), 0, n_new, 42, 3)
+    np.testing.assert_allclose(out.float().cpu().numpy(), exp, rtol=1e-2, atol=1e-2)
+    assert np.all(out[:, 31].float().cpu().numpy() == 1.0)
+
+
+@pytest.mark.parametrize("n,rate,quant", [(1000, 0.1, None), (300_000, 0.002, None), (200_000, 0.3, 0.05),
+                                          (50_000, 0.5, 1.0)])
+def test_auc_exact(dev, n, rate, quant):
+    from sklearn.metrics import roc_auc_score
+
+    rng = np.random.default_rng(n)
+    y = (rng.random(n) < rate).astype(np.uint8)
+    s = rng.normal(size=n).astype(np.float32) + y * 1.5
+    if quant:
+        s = (np.round(s / quant) * quant).astype(np.float32)  # heavy ties
+    auc = M.roc_auc(torch.from_numpy(s).to(dev), torch.from_numpy(y).to(dev))
+    assert auc == pytest.approx(roc_auc_score(y, s), abs=1e-12)
+    cm = M.confusion_counts(torch.from_numpy(s).to(dev), torch.from_numpy(y).to(dev), 0.3)
+    assert np.array_equal(cm, ref.confusion(s, y, 0.3))
