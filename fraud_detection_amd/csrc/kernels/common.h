@@ -100,13 +100,23 @@ __device__ __forceinline__ T group_sum(T v) {
   return v;
 }
 
+// v_rcp_f32 (1 ulp), no IEEE division expansion.
+__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
+
 __device__ __forceinline__ float fast_sigmoid(float z) {
   // 1/(1+exp(-z)) with exp via v_exp_f32 (exp2); saturates cleanly at +-inf.
-  return __frcp_rn(1.0f + __expf(-z));
+  return fast_rcp(1.0f + __expf(-z));
+}
+// log1p(t) for t >= 0 with the hardware log (v_log_f32): Kahan's correction u = 1 + t,
+// log1p(t) = log(u) * t / (u - 1), accurate to a few ulp without the libm log1pf expansion.
+__device__ __forceinline__ float log1p_fast(float t) {
+  const float u = 1.0f + t;
+  const float d = u - 1.0f;
+  return d == 0.0f ? t : __logf(u) * (t * fast_rcp(d));
 }
 // log(1 + exp(z)) computed stably.
 __device__ __forceinline__ float softplus(float z) {
-  return z > 0.0f ? z + log1pf(__expf(-z)) : log1pf(__expf(z));
+  return fmaxf(z, 0.0f) + log1p_fast(__expf(-fabsf(z)));
 }
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }

@@ -90,31 +90,59 @@ __global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restr
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
 
+  // per-lane parking row for one tile's 16 scores (stride 17 floats: conflict-free column reads)
+  __shared__ float park_all[kWaves][kWave * 17];
+  float* park = park_all[wv];
   const int ntiles = mc_pad / 32;
+  // Register double buffer: the next candidate tile (16 floats of one row + 16 norms per lane,
+  // L2-resident) is fetched while the current tile's MFMA chain and top-k run.
+  float4 cv[4], nv[4];
+  auto fetch = [&](int t, float4 (&a)[4], float4 (&b)[4]) {
+    const int cb = t * 32;
+    const float4* p = reinterpret_cast<const float4*>(C + (int64_t)(cb + j) * kCols + 16 * h);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[k] = p[k];
+      // accumulator rows (k&3)+8(k>>2)+4h -> 4 contiguous candidates per register group
+      b[k] = *reinterpret_cast<const float4*>(chalf + cb + 8 * k + 4 * h);
+    }
+  };
+  if (wv < ntiles) fetch(wv, cv, nv);
   for (int t = wv; t < ntiles; t += kWaves) {
     const int c0 = t * 32;
     float ac[16];
-    {
-      const float4* p = reinterpret_cast<const float4*>(C + (int64_t)(c0 + j) * kCols + 16 * h);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 v = p[k];
-        ac[4 * k] = v.x; ac[4 * k + 1] = v.y; ac[4 * k + 2] = v.z; ac[4 * k + 3] = v.w;
-      }
-    }
     f32x16_t acc;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // rows (k&3)+8(k>>2)+4h -> 4 contiguous candidates per group
-      const float4 nv = *reinterpret_cast<const float4*>(chalf + c0 + 8 * k + 4 * h);
-      acc[4 * k] = -nv.x; acc[4 * k + 1] = -nv.y; acc[4 * k + 2] = -nv.z; acc[4 * k + 3] = -nv.w;
+    for (int k = 0; k < 4; ++k) {
+      ac[4 * k] = cv[k].x; ac[4 * k + 1] = cv[k].y; ac[4 * k + 2] = cv[k].z; ac[4 * k + 3] = cv[k].w;
+      acc[4 * k] = -nv[k].x; acc[4 * k + 1] = -nv[k].y; acc[4 * k + 2] = -nv[k].z; acc[4 * k + 3] = -nv[k].w;
     }
+    if (t + kWaves < ntiles) fetch(t + kWaves, cv, nv);
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[s], bq[s], acc, 0, 0, 0);
+    // Filter: a candidate can only enter the list if it beats the CURRENT k-th best (which only
+    // improves), so 16 compares build a bitmask; the tile's scores are parked in this lane's LDS
+    // row and only set bits are inserted (dynamic index via LDS, not register arrays).
+    unsigned mask = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ci = c0 + (r & 3) + 8 * (r >> 2) + 4 * h;
       const float sc = (ci == self_c || ci >= mc) ? kNegBig : acc[r];
-      topk_insert<K>(bs, bi, sc, ci);
+      acc[r] = sc;
+      mask |= better(sc, ci, bs[K - 1], bi[K - 1]) ? (1u << r) : 0u;
+    }
+    if (__any(mask != 0)) {
+      float* my = park + lane * 17;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) my[r] = acc[r];
+      while (__any(mask != 0)) {
+        if (mask) {
+          const int r = __builtin_ctz(mask);
+          mask &= mask - 1;
+          const int ci = c0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          topk_insert<K>(bs, bi, my[r], ci);
+        }
+      }
     }
   }
   // merge with the other half-wave (same query, other candidate rows)

@@ -22,6 +22,8 @@
 // with no host synchronisation (hipGraph-capturable); a device-side `done` flag turns the
 // remaining iterations into no-ops once converged.  With data parallelism the reduced 1088-double
 // vector is all-reduced over RCCL between the reduce and the update kernels (parallel/dp.py).
+#include <type_traits>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -49,10 +51,10 @@ __device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8], int q, i
 }
 
 template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
-__global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
+__global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    float* __restrict__ partial) {
+    int hess_stride, float* __restrict__ partial) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][34];
@@ -75,21 +77,38 @@ __global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
 
   const int64_t n = row_end - row_begin;
   const int64_t step = (int64_t)gridDim.x * kWaves * 64;
-  for (int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64; base < n; base += step) {
+  const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
+  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
+  typedef typename std::conditional<FMT == 0, uint4, uint2>::type vec_t;
+  auto load_tile = [&](int64_t b, vec_t (&v)[4]) {
+    const vec_t* X = reinterpret_cast<const vec_t*>(Xv);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = b + 16 * u + rr;
+      if (row < n) v[u] = X[(row_begin + row) * 4 + q];
+      else if constexpr (FMT == 0) v[u] = make_uint4(0, 0, 0, 0);
+      else v[u] = make_uint2(0, 0);
+    }
+  };
+  int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
+  vec_t cur[4];
+  if (base < n) load_tile(base, cur);
+  // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
+  // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
+  // is unchanged; H only shapes the step (sub-sampled Newton).
+  int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
+  for (; base < n; base += step) {
+    vec_t nxt[4];
+    if (base + step < n) load_tile(base + step, nxt);
+    const bool do_h = HESS && hphase == 0;
+    hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int64_t row = base + 16 * u + rr;
-      if constexpr (FMT == 0) {
-        const uint4* X = reinterpret_cast<const uint4*>(Xv);
-        const uint4 v = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
-        unpack8<0>(v, xs[u]);
-      } else {
-        const uint2* X = reinterpret_cast<const uint2*>(Xv);
-        const uint2 v = row < n ? X[(row_begin + row) * 4 + q] : make_uint2(0, 0);
-        unpack8_fp8(v, xs[u], q, d_feat, inv_s);
-      }
+      if constexpr (FMT == 0) unpack8<0>(cur[u], xs[u]);
+      else unpack8_fp8(cur[u], xs[u], q, d_feat, inv_s);
     }
+    float zq = 0.0f, yq = 0.0f, swq = 0.0f;  // the row (u == q) whose loss this lane accounts for
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float* x = xs[u];
@@ -101,19 +120,18 @@ __global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
       zp = group_sum<4>(zp);
       y = group_sum<4>(y);
       const bool ok = base + 16 * u + rr < n;
-      const float sw = ok ? (y > 0.5f ? cw1 : cw0) : 0.0f;
+      const bool pos = y > 0.5f;
+      const float sw = ok ? (pos ? cw1 : cw0) : 0.0f;
       const float zc = fminf(fmaxf(zp, -80.0f), 80.0f);
-      const float e = __expf(-zc);
-      const float p = __frcp_rn(1.0f + e);
+      const float eh = __expf(-0.5f * zc);   // exp(-z/2)
+      const float p = fast_rcp(fmaf(eh, eh, 1.0f));
       const float r = sw * (p - y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(r, x[j], g[j]);
-      if (q == 0) {
-        lacc = fmaf(sw, softplus(zp) - y * zp, lacc);
-        wacc += sw;
-      }
-      if constexpr (HESS) {
-        const float dd = sqrtf(sw * p * (e * p));  // sqrt(s p (1-p)), 1-p = e p (no cancellation)
+      if (q == u) { zq = zp; yq = y; swq = sw; }
+      if (do_h) {
+        // sqrt(s p (1-p)) = sqrt(s) * p * exp(-z/2)   (1-p = p e^{-z}): no sqrt, no cancellation
+        const float dd = ok ? (pos ? scw1 : scw0) * p * eh : 0.0f;
         uint4 pk;
         pk.x = pack_bf16x2(x[0] * dd, x[1] * dd);
         pk.y = pack_bf16x2(x[2] * dd, x[3] * dd);
@@ -122,7 +140,7 @@ __global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
         *reinterpret_cast<uint4*>(my_tile + (16 * u + rr) * kCols + 8 * q) = pk;
       }
     }
-    if constexpr (HESS) {
+    if (do_h) {
       // Wave-private tile: LDS instructions of one wave execute in order, so the transpose
       // reads below observe this wave's writes; the wave_barrier only pins compiler order.
       __builtin_amdgcn_wave_barrier();
@@ -140,6 +158,11 @@ __global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
       }
       __builtin_amdgcn_wave_barrier();
     }
+    // weighted log-loss of this lane's row: max(z,0) - y z + log1p(exp(-|z|))
+    lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
+    wacc += swq;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
   }
 
   // ---- block reduction (fixed order) ----
@@ -158,10 +181,11 @@ __global__ __launch_bounds__(kThreads) void logreg_pass_kernel(
   float* hb = reinterpret_cast<float*>(&tile[0][0]);  // 4 x 1024 floats = the 16 KiB tile
   if constexpr (HESS) {
     // each wave overwrites only its own tile region (same bytes it read from)
+    const float hscale = (float)hess_stride;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int row = (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-      hb[wv * 1024 + row * kCols + (lane & 31)] = acc[k];
+      hb[wv * 1024 + row * kCols + (lane & 31)] = acc[k] * hscale;
     }
   }
   __syncthreads();
@@ -361,17 +385,39 @@ __global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict
 
 }  // namespace
 
-int logreg_pass_blocks() { return kPassBlocks; }
+// Grid = resident capacity of the Hessian pass (blocks/CU from the occupancy query x CUs): a
+// grid-stride stream must not launch a partial second round of blocks, which would double the
+// tail (every block owns an equal share of rows).
+int logreg_pass_blocks() {
+  static int cached = 0;
+  if (cached) return cached;
+  int dev = 0, cus = 256, per_cu = 3;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+    int occ = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true, 0>, kThreads, 0) ==
+            hipSuccess && occ > 0)
+      per_cu = occ;
+  }
+  cached = cus * per_cu;
+  if (cached < 64) cached = 64;
+  if (cached > kPassBlocks * 2) cached = kPassBlocks * 2;
+  return cached;
+}
 
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, float* partial,
                         int nblocks, hipStream_t stream) {
-  if (hessian)
+  // hessian: 0 = gradient/loss only; h >= 1 = also the Hessian, from every h-th row tile.
+  if (hessian > 0)
     logreg_pass_kernel<true, 0><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                 class_w, done, 1.0f, 32, partial);
+                                                                 class_w, done, 1.0f, 32, hessian,
+                                                                 partial);
   else
     logreg_pass_kernel<false, 0><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                  class_w, done, 1.0f, 32, partial);
+                                                                  class_w, done, 1.0f, 32, 1,
+                                                                  partial);
   check_launch("logreg_pass");
 }
 
@@ -380,13 +426,13 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
                             float* partial, int nblocks, hipStream_t stream) {
   // fp8 rows store features * x_scale for columns < 30; the bias (col 30) and label (col 31)
   // are stored unscaled.
-  if (hessian)
+  if (hessian > 0)
     logreg_pass_kernel<true, 1><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
                                                                  class_w, done, x_scale, 30,
-                                                                 partial);
+                                                                 hessian, partial);
   else
     logreg_pass_kernel<false, 1><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                  class_w, done, x_scale, 30,
+                                                                  class_w, done, x_scale, 30, 1,
                                                                   partial);
   check_launch("logreg_pass_fp8");
 }

@@ -232,6 +232,75 @@ __global__ __launch_bounds__(kThreads) void scale_cast_kernel(
   }
 }
 
+// K2 fast path for contiguous rows (ld == d, 16 B aligned base): a 128-row tile is one
+// contiguous block of 128*d floats, loaded with fully coalesced 16 B loads into LDS (the 120 B
+// rows of the creditcard layout are not 16 B aligned individually), then re-read row-wise so
+// every lane emits 8 output columns: one 16 B bf16 store (64 lanes = 16 rows = 1 KiB contiguous).
+constexpr int kTileRows = 128;
+
+template <int OUT>
+__global__ __launch_bounds__(kThreads) void scale_cast_tiled_kernel(
+    const float* __restrict__ X, int64_t n, int d, const float* __restrict__ mean32,
+    const float* __restrict__ inv32, const uint8_t* __restrict__ labels, float bias_value,
+    float out_scale, void* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) float tile[kTileRows * 30];
+  const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+  const int64_t total = n * (int64_t)d;
+  const int q = threadIdx.x & 3;  // column group of both of this lane's slots
+  float mu[8], inv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    mu[j] = mean32[8 * q + j];
+    inv[j] = inv32[8 * q + j];
+  }
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t f0 = t * kTileRows * (int64_t)d;  // first float of the tile
+    const int nf = (int)((total - f0) < (int64_t)kTileRows * d ? (total - f0) : (int64_t)kTileRows * d);
+    const int nf4 = nf >> 2;
+    const float4* src = reinterpret_cast<const float4*>(X + f0);
+    for (int i = threadIdx.x; i < nf4; i += kThreads) reinterpret_cast<float4*>(tile)[i] = src[i];
+    for (int i = (nf4 << 2) + threadIdx.x; i < nf; i += kThreads) tile[i] = X[f0 + i];
+    __syncthreads();
+    const int rows = (int)((n - t * kTileRows) < kTileRows ? (n - t * kTileRows) : kTileRows);
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int slot = threadIdx.x + k * kThreads;  // 512 slots = 128 rows x 4 column groups
+      const int r = slot >> 2;
+      if (r >= rows) continue;
+      const int64_t grow = t * kTileRows + r;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * q + j;
+        if (c < d) o[j] = (tile[r * d + c] - mu[j]) * inv[j];
+        else if (c == kBiasCol) o[j] = bias_value;
+        else if (c == kLabelCol) o[j] = labels ? (float)labels[grow] : 0.0f;
+        else o[j] = 0.0f;
+      }
+      if constexpr (OUT == 0) {
+        uint4 pk;
+        pk.x = pack_bf16x2(o[0], o[1]); pk.y = pack_bf16x2(o[2], o[3]);
+        pk.z = pack_bf16x2(o[4], o[5]); pk.w = pack_bf16x2(o[6], o[7]);
+        reinterpret_cast<uint4*>(out)[grow * 4 + q] = pk;
+      } else if constexpr (OUT == 1) {
+        float4* dst = reinterpret_cast<float4*>(out) + grow * 8 + 2 * q;
+        dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+        dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+        uint2 pk = make_uint2(0, 0);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float v = (8 * q + j < d) ? o[j] * out_scale : o[j];
+          const uint32_t b = f32_to_fp8e4m3(v);
+          if (j < 4) pk.x |= b << (8 * j); else pk.y |= b << (8 * (j - 4));
+        }
+        reinterpret_cast<uint2*>(out)[grow * 4 + q] = pk;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---- stable compaction of row indices whose label == target -------------------------------
 // Blocks own contiguous row ranges so the output order equals the input order.
 constexpr int kCompactThreads = 256;
@@ -340,6 +409,18 @@ void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* 
                        const float* mean32, const float* inv32, const uint8_t* labels,
                        float bias_value, float out_scale, int out_kind, void* out,
                        hipStream_t stream) {
+  if (idx == nullptr && ld == d && d <= 30 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 &&
+      (reinterpret_cast<uintptr_t>(out) % 16) == 0) {
+    const int grid = stream_grid((n + kTileRows - 1) / kTileRows, 1, 2048);
+    if (out_kind == 0)
+      scale_cast_tiled_kernel<0><<<grid, kThreads, 0, stream>>>(X, n, d, mean32, inv32, labels, bias_value, out_scale, out);
+    else if (out_kind == 1)
+      scale_cast_tiled_kernel<1><<<grid, kThreads, 0, stream>>>(X, n, d, mean32, inv32, labels, bias_value, out_scale, out);
+    else
+      scale_cast_tiled_kernel<2><<<grid, kThreads, 0, stream>>>(X, n, d, mean32, inv32, labels, bias_value, out_scale, out);
+    check_launch("scale_cast_tiled");
+    return;
+  }
   const int grid = stream_grid((n + 7) / 8, (kThreads / kWave) * kUnroll, 2048);
   const int vec = vec_for(X, ld);
 #define FDX_SC(V, O)                                                                              \

@@ -29,7 +29,7 @@ from ..ops.layout import BIAS_COL, DEFAULT_FP8_SCALE, NCOLS, TORCH_STORAGE
 class TrainConfig:
     solver: str = "newton"          # newton | sgd
     C: float = 1.0
-    tol: float = 1e-8
+    tol: float = 1e-6               # max |grad| of the mean objective (sklearn lbfgs uses 1e-4)
     max_iter: int = 25
     fit_intercept: bool = True
     class_weight: str | None = None  # None | "balanced"
@@ -45,6 +45,7 @@ class TrainConfig:
     sgd_batch_rows: int = 1 << 22
     check_every: int = 4
     init_std: float = 0.01          # random-init weights ~ N(0, init_std^2) (seeded by `seed`)
+    hess_stride: int | str = "auto"  # Newton: Hessian from every k-th row tile (gradient always exact)
 
 
 @dataclass
@@ -160,7 +161,7 @@ class DevicePipeline:
         if cfg.solver == "newton":
             fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
-                                    check_every=cfg.check_every, workspace=self._ws)
+                                    check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride)
         elif cfg.solver == "sgd":
             fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                  batch_rows=cfg.sgd_batch_rows, class_w=class_w, d=d, w0=w0,

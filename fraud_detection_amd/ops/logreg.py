@@ -66,15 +66,23 @@ class LRWorkspace:
         self.class_w.copy_(torch.tensor(class_w, dtype=torch.float32))
 
 
-def _pass(m, rows, ws: LRWorkspace, hessian: bool, begin: int, end: int, fp8_scale: float, s: int, done=True):
+HESS_SAMPLE_ROWS = 1 << 22  # auto Hessian sub-sampling keeps >= ~4M rows in the H estimate
+
+
+def auto_hess_stride(n_rows: int) -> int:
+    return int(max(1, min(8, n_rows // HESS_SAMPLE_ROWS)))
+
+
+def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True):
+    """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact)."""
     dptr = ptr(ws.done) if done else 0
+    h = int(hessian)
     if storage_kind(rows) == "bf16":
-        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, int(hessian), ptr(ws.partial),
-                      ws.nblocks, s)
+        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, ptr(ws.partial), ws.nblocks, s)
     else:
-        m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, int(hessian), float(fp8_scale),
+        m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, float(fp8_scale),
                           ptr(ws.partial), ws.nblocks, s)
-    m.logreg_reduce(ptr(ws.partial), ws.nblocks, PART_STRIDE if hessian else 64, ptr(ws.red), dptr, s)
+    m.logreg_reduce(ptr(ws.partial), ws.nblocks, PART_STRIDE if h else 64, ptr(ws.red), dptr, s)
 
 
 def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian: bool = True,
@@ -106,9 +114,11 @@ def _default_w0(w0):
 def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: int = 25,
                class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
-               sync: bool = True) -> FitInfo:
+               sync: bool = True, hess_stride: int | str = "auto") -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
-    this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration)."""
+    this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
+    ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
+    gradient and objective always use all rows, so the converged solution is unchanged."""
     check_rows(rows)
     w0 = _default_w0(w0)
     if not rows.is_cuda:
@@ -118,10 +128,13 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     ws.reset(w0, class_w)
     s = stream_of(rows)
     n = rows.shape[0]
+    hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
+    if comm is not None and comm.world_size > 1:
+        hs = int(comm.all_reduce_scalar(hs, op="min"))  # identical H sampling rule on every rank
     it = 0
     while it < max_iter:
         for _ in range(min(check_every, max_iter - it)):
-            _pass(m, rows, ws, True, 0, n, fp8_scale, s)
+            _pass(m, rows, ws, hs, 0, n, fp8_scale, s)
             if comm is not None and comm.world_size > 1:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),

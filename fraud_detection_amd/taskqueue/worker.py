@@ -1,0 +1,150 @@
+"""Queue worker: leases batches, runs handlers (batched on the GPU when the task has one), acks late.
+
+    python -m fraud_detection_amd.taskqueue.worker --app xai_tasks:celery_app [--batch 256]
+
+Equivalent of ``celery -A xai_tasks.celery_app worker --concurrency=1`` (docker-compose.yml:98).
+A crash between compute and ack (e.g. the pod is killed) leaves the lease to expire and the
+task is redelivered (acks_late; docs/WorkerRecoveryTestPlan.md:52-56).  Fault injection for
+tests: FDX_FAULT=worker_crash_after_compute makes the process exit hard before acking.
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import logging
+import os
+import signal
+import socket
+import threading
+import time
+import traceback
+
+from .app import MaxRetriesExceededError, Request, Retry, TaskApp, TaskCall
+from .queue import DurableQueue
+
+logger = logging.getLogger("fdx.worker")
+
+
+class Worker:
+    def __init__(self, app: TaskApp, batch: int = 256, visibility_timeout: float = 60.0, poll_interval: float = 0.05,
+                 name: str | None = None, metrics=None):
+        self.app = app
+        self.queue: DurableQueue = app.queue
+        self.batch = batch
+        self.visibility_timeout = visibility_timeout
+        self.poll_interval = poll_interval
+        self.name = name or f"{socket.gethostname()}:{os.getpid()}:{id(self) & 0xffff:x}"
+        self.metrics = metrics
+        self._stop = threading.Event()
+
+    def stop(self, *_):
+        self._stop.set()
+
+    def run_once(self) -> int:
+        """Lease and process one batch.  Returns the number of tasks handled."""
+        leased = self.queue.lease(self.name, self.batch, self.visibility_timeout, names=list(self.app.tasks) or None)
+        if not leased:
+            return 0
+        by_name: dict[str, list] = {}
+        for lt in leased:
+            by_name.setdefault(lt.name, []).append(lt)
+        for name, items in by_name.items():
+            task = self.app.tasks.get(name)
+            if task is None:
+                for lt in items:
+                    self.queue.fail(lt.id, f"unregistered task {name}")
+                continue
+            calls = [TaskCall(lt.id, lt.args, lt.kwargs,
+                              Request(id=lt.id, retries=lt.attempts, headers=lt.headers,
+                                      correlation_id=lt.headers.get("correlation_id"))) for lt in items]
+            t0 = time.perf_counter()
+            if task.batch_fn is not None:
+                try:
+                    results = task.batch_fn(calls)
+                except Exception as e:  # whole-batch failure: fall back to per-call so one bad row can't poison it
+                    logger.warning("batch handler for %s failed (%s); retrying calls individually", name, e)
+                    results = [self._run_single(task, c) for c in calls]
+            else:
+                results = [self._run_single(task, c) for c in calls]
+            dt = time.perf_counter() - t0
+            if os.getenv("FDX_FAULT") == "worker_crash_after_compute":
+                os._exit(17)  # simulate SIGKILL between compute and ack
+            for call, res in zip(calls, results):
+                self._settle(task, call, res, dt / max(len(calls), 1))
+        if self.metrics is not None:
+            self.metrics.queue_depth.set(self.queue.depth())
+        return len(leased)
+
+    def _run_single(self, task, call):
+        try:
+            return task.run_call(call)
+        except Exception as e:  # noqa: BLE001 - settled below
+            return e
+
+    def _settle(self, task, call: TaskCall, res, dt: float):
+        m = self.metrics
+        if isinstance(res, Retry):
+            st = self.queue.retry(call.id, res.countdown, repr(res.exc), worker=self.name)
+            if m is not None:
+                m.task_failure.inc()
+            logger.info("task %s retry in %.1fs -> %s", call.id, res.countdown, st)
+        elif isinstance(res, MaxRetriesExceededError):
+            self.queue.fail(call.id, str(res), result={"status": "FAILED"})
+            if m is not None:
+                m.task_failure.inc()
+        elif isinstance(res, BaseException):
+            self.queue.fail(call.id, "".join(traceback.format_exception_only(type(res), res)))
+            if m is not None:
+                m.task_failure.inc()
+        else:
+            failed = isinstance(res, dict) and res.get("status") == "FAILED"
+            self.queue.ack(call.id, res, worker=self.name)
+            if m is not None:
+                (m.task_failure if failed else m.task_success).inc()
+                m.task_duration.observe(dt)
+
+    def run(self, max_idle: float | None = None):
+        idle_since = time.time()
+        while not self._stop.is_set():
+            n = self.run_once()
+            if n:
+                idle_since = time.time()
+            else:
+                if max_idle is not None and time.time() - idle_since > max_idle:
+                    break
+                time.sleep(self.poll_interval)
+
+
+def load_app(spec: str) -> TaskApp:
+    """``module:attr`` or ``module.attr`` (celery -A style)."""
+    if ":" in spec:
+        mod, attr = spec.split(":", 1)
+    else:
+        mod, _, attr = spec.rpartition(".")
+    return getattr(importlib.import_module(mod), attr or "celery_app")
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--app", default="xai_tasks:celery_app")
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--visibility-timeout", type=float, default=60.0)
+    ap.add_argument("--metrics-port", type=int, default=int(os.getenv("FDX_WORKER_METRICS_PORT", "8001")))
+    ap.add_argument("--max-idle", type=float, default=None)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
+    app = load_app(a.app)
+    from ..obs.metrics import worker_metrics, start_metrics_server
+
+    metrics = worker_metrics()
+    if a.metrics_port:
+        start_metrics_server(a.metrics_port)
+    w = Worker(app, a.batch, a.visibility_timeout, metrics=metrics)
+    signal.signal(signal.SIGTERM, w.stop)
+    signal.signal(signal.SIGINT, w.stop)
+    logger.info("worker %s started (tasks: %s)", w.name, ", ".join(app.tasks))
+    w.run(max_idle=a.max_idle)
+
+
+if __name__ == "__main__":
+    main()

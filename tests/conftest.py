@@ -1,11 +1,21 @@
 import os
 import sys
+import tempfile
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+
+# Hermetic service state for the whole test session (set before any api/db module import).
+_TMP = tempfile.mkdtemp(prefix="fdx_tests_")
+os.environ.setdefault("DATABASE_URL", f"sqlite:///{_TMP}/fraud.db")
+os.environ.setdefault("MLFLOW_TRACKING_URI", f"file:{_TMP}/mlruns")
+os.environ.setdefault("MODEL_PATH", os.path.join(ROOT, "models", "logistic_model.joblib"))
+os.environ.setdefault("FEATURE_NAMES_PATH", os.path.join(ROOT, "models", "feature_names.json"))
+os.environ.setdefault("FDX_DEVICE", "cpu")
+os.chdir(ROOT)
 
 import torch  # noqa: E402  (before any extension import)
 
