@@ -1,0 +1,44 @@
+"""Exploratory data analysis (reference path eda.py:1-48): class-count and amount plots, then a
+processed_data.csv with standardized Amount/Time (columns V1..V28, Class, scaled_amount,
+scaled_time).  Standardization uses the device scaler kernel when a GPU is present."""
+import os
+
+import matplotlib
+
+matplotlib.use("Agg")
+import matplotlib.pyplot as plt  # noqa: E402
+import numpy as np  # noqa: E402
+import pandas as pd  # noqa: E402
+import torch  # noqa: E402
+
+from fraud_detection_amd.ops import scaler as S  # noqa: E402
+
+
+def main(path: str = os.getenv("DATA_CSV", "data/creditcard.csv")):
+    df = pd.read_csv(path)
+    os.makedirs("plots", exist_ok=True)
+    counts = df["Class"].value_counts().sort_index()
+    print(counts)
+    fig, ax = plt.subplots(figsize=(6, 4))
+    ax.bar(["Non-Fraud", "Fraud"][: len(counts)], counts.values)
+    ax.set_title("Class Distribution")
+    fig.savefig("plots/class_distribution.png")
+    plt.close(fig)
+    fig, ax = plt.subplots(figsize=(8, 4))
+    ax.hist(df["Amount"].values, bins=50)
+    ax.set_title("Transaction Amount Distribution")
+    fig.savefig("plots/amount_distribution.png")
+    plt.close(fig)
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    at = torch.from_numpy(df[["Amount", "Time"]].to_numpy(np.float32)).to(dev)
+    st = S.scaler_fit(at)
+    mean, _, scale = st.numpy()
+    df["scaled_amount"] = (df["Amount"] - mean[0]) / scale[0]
+    df["scaled_time"] = (df["Time"] - mean[1]) / scale[1]
+    df = df.drop(["Time", "Amount"], axis=1)
+    df.to_csv("processed_data.csv", index=False)
+    print("Saved processed_data.csv", df.shape)
+
+
+if __name__ == "__main__":
+    main()

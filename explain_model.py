@@ -1,0 +1,80 @@
+"""Batch explainability (reference path explain_model.py:1-49): LinearSHAP of the served model on
+the (already scaled) test split, summary plot and dependence plots of the top-3 features by mean
+|phi|, saved under plots/.  Fixes the reference's double scaling (explain_model.py:19; SURVEY.md
+App. D item 3): the npz features are already standardized, so the explainer runs on them
+directly, with the test set as background (LinearExplainer(model, X_test_scaled)).
+``--kernel`` additionally runs KernelSHAP (MFMA coalition GEMM) on a sample for comparison."""
+import argparse
+import os
+
+import matplotlib
+
+matplotlib.use("Agg")
+import matplotlib.pyplot as plt  # noqa: E402
+import numpy as np  # noqa: E402
+
+from fraud_detection_amd.compat.sklearn_export import load_artifacts  # noqa: E402
+from fraud_detection_amd.models.explainers import KernelExplainer, LinearExplainer  # noqa: E402
+
+
+def summary_plot(phi, X, names, path):
+    order = np.argsort(np.abs(phi).mean(0))[::-1][:20]
+    fig, ax = plt.subplots(figsize=(12, 8))
+    for row, j in enumerate(order[::-1]):
+        v = X[:, j]
+        lo, hi = np.percentile(v, [5, 95])
+        col = np.clip((v - lo) / (hi - lo + 1e-12), 0, 1)
+        jitter = (np.random.default_rng(j).random(len(v)) - 0.5) * 0.6
+        ax.scatter(phi[:, j], row + jitter, c=col, cmap="coolwarm", s=4, alpha=0.6)
+    ax.set_yticks(range(len(order)), [names[j] for j in order[::-1]])
+    ax.set_xlabel("SHAP value (impact on log-odds)")
+    fig.tight_layout()
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def dependence_plot(j, phi, X, names, path):
+    fig, ax = plt.subplots(figsize=(8, 6))
+    ax.scatter(X[:, j], phi[:, j], s=4, alpha=0.5)
+    ax.set_xlabel(names[j])
+    ax.set_ylabel(f"SHAP value for {names[j]}")
+    fig.tight_layout()
+    fig.savefig(path)
+    plt.close(fig)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", action="store_true", help="also run KernelSHAP on --n rows")
+    ap.add_argument("--n", type=int, default=1000)
+    a = ap.parse_args(argv)
+    os.makedirs("plots", exist_ok=True)
+    print("Loading model, scaler, and data...")
+    art = load_artifacts("models/logistic_model.joblib", "models/scaler.joblib", "models/feature_names.json")
+    data = np.load("data/preprocessed_data.npz")
+    X_test = data["X_test"].astype(np.float32)
+    d = X_test.shape[1]
+    names = [f"Feature_{i}" for i in range(d)]
+    # features are already standardized: identity scaler, background = test set
+    expl = LinearExplainer(art.coef, art.intercept, np.zeros(d), np.ones(d), background=X_test)
+    print("Computing SHAP values for the test set...")
+    phi = expl.shap_values(X_test)
+    summary_plot(phi, X_test, names, "plots/shap_summary.png")
+    top = np.argsort(np.abs(phi).mean(0))[-3:][::-1]
+    for j in top:
+        dependence_plot(j, phi, X_test, names, f"plots/shap_dependence_feature_{j}.png")
+    out = {"top_features": [int(j) for j in top], "expected_value": expl.expected_value}
+    if a.kernel:
+        w = np.zeros(32)
+        w[:d] = art.coef
+        bg = X_test[np.random.default_rng(0).choice(len(X_test), min(100, len(X_test)), replace=False)]
+        ke = KernelExplainer(w, art.intercept, bg, link="identity")
+        phik, fx, f0 = ke.explain(X_test[: a.n])
+        out["kernelshap_rows"] = int(min(a.n, len(X_test)))
+        out["kernelshap_efficiency_max_err"] = float(np.abs(phik.sum(1) - (fx - f0)).max())
+    print("SHAP explainability completed. Plots saved in 'plots/'.", out)
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -91,14 +91,15 @@ PYBIND11_MODULE(_fdx_native, m) {
 
   // logistic regression
   m.def("logreg_pass_blocks", &fdx::logreg_pass_blocks);
-  m.def("logreg_pass", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, u partial, int nblocks, u s) {
+  m.def("logreg_pass", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
+                          int nblocks, u s) {
     fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
-                            hess, P<float>(partial), nblocks, S(s));
+                            hess, sub, P<float>(partial), nblocks, S(s));
   });
-  m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, float xs, u partial,
-                              int nblocks, u s) {
+  m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
+                              u partial, int nblocks, u s) {
     fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
-                                P<const int>(done), hess, xs, P<float>(partial), nblocks, S(s));
+                                P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s));
   });
   m.def("logreg_reduce", [](u partial, int nblocks, int ncols, u out, u done, u s) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
@@ -124,6 +125,14 @@ PYBIND11_MODULE(_fdx_native, m) {
                              uint64_t counter_base, float label, int out_kind, float out_scale, u out, u s) {
     fdx::launch_smote_generate(P<const float>(C), P<const int>(nbr), mq, k, q_off, n_new, seed, counter_base, label,
                                out_kind, out_scale, P<void>(out), S(s));
+  });
+
+  // kernelshap
+  m.def("kernelshap", [](u X, int E, int d, u a, float bias, u bg, u cb, int nbg, u Z, int nS, int S_pad, u A, u Az,
+                         int link, u phi, u fx, u f0, u s) {
+    fdx::launch_kernelshap(P<const float>(X), E, d, P<const float>(a), bias, P<const float>(bg), P<const float>(cb),
+                           nbg, P<const uint16_t>(Z), nS, S_pad, P<const float>(A), P<const float>(Az), link,
+                           P<float>(phi), P<float>(fx), P<float>(f0), S(s));
   });
 
   // auc / confusion

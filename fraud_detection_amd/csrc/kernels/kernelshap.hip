@@ -1,0 +1,168 @@
+// K7 kernelshap_coalition_gemm: batched KernelSHAP for the (scaler-folded) logistic model.
+//
+// Reference: shap.KernelExplainer semantics (BASELINE.json config 4),
+// the north-star "coalition-masked batched GEMM" XAI path.  Host side (models/explainers.py):
+// coalition design Z [S][M] and the efficiency-constrained WLS operator A [M-1][S] (solved once).
+//
+// Per explanation e (one workgroup):
+//   logit(z_s, b) = sum_k z_sk u_bk + c_b,   u_b = a * (x_e - B_b),   c_b = a . B_b + bias
+// is a (n_bg x 32) x (32 x S) product.  The background intercepts are folded in as K column 31
+// (Z[:,31] = 1, U[:,31] = c_b), so the accumulator IS the logit.  v_mfma_f32_32x32x16_bf16 with
+// the background row on the M axis and the coalition on the N axis: Z is exactly representable
+// in bf16 and u is split into hi + lo bf16 halves (two MFMAs, ~16 mantissa bits per product,
+// fp32 accumulation).  The epilogue applies the link (sigmoid for probability space), sums the
+// 16 accumulator rows of each lane plus the partner half-wave, i.e. the mean over background
+// rows, into LDS f[s].  Then y = link(f) - link(f0) and phi_{<M} = A y - (A z_M) delta,
+// phi_M = delta - sum(phi_{<M}), delta = link(f(x)) - link(f0).
+//
+// MFMA operand maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) supplies
+// A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7 -> both are 16 contiguous bytes of a
+// row (U row b for A, Z row s for B); accumulator row = (i & 3) + 8 (i >> 2) + 4 h, col = r.
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kWaves = 4;
+constexpr int kMaxBg = 128;     // 4 background tiles of 32
+constexpr int kMaxS = 4096;     // coalitions per design (LDS f[] capacity)
+
+__device__ __forceinline__ short bf16_bits(float f) { return (short)f32_to_bf16(f); }
+
+// link: 0 = identity on probabilities (shap default), 1 = logit of the mean probability,
+//       2 = model log-odds (mean of logits; KernelSHAP == LinearSHAP exactly)
+__global__ __launch_bounds__(kThreads) void kernelshap_kernel(
+    const float* __restrict__ X, int n_expl, int d, const float* __restrict__ a, float bias,
+    const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
+    const uint16_t* __restrict__ Z, int S, int S_pad, const float* __restrict__ Amat,
+    const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
+    float* __restrict__ f0_out) {
+  __shared__ float f[kMaxS];
+  __shared__ float xs[32];
+  __shared__ float red[8];
+  const int e = blockIdx.x;
+  const int lane = lane_id(), wv = wave_id();
+  const int r = lane & 31, h = lane >> 5;
+  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? X[(int64_t)e * d + threadIdx.x] : 0.0f;
+  __syncthreads();
+  const int ntb = (n_bg + 31) >> 5;  // background tiles in use (uniform)
+  // U fragments (hi / lo) for every background tile and both k-steps: 16 regs x 4 tiles
+  bf16x8_t uhi[4][2], ulo[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int b = 32 * t + r;
+    const bool okb = b < n_bg && t < ntb;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = 16 * ks + 8 * h + j;
+        float u = 0.0f;
+        if (okb) {
+          if (k < d) u = a[k] * (xs[k] - Bg[(int64_t)b * d + k]);
+          else if (k == 31) u = cb[b];
+        }
+        const short hi = bf16_bits(u);
+        const float hif = __uint_as_float(((uint32_t)(uint16_t)hi) << 16);
+        uhi[t][ks][j] = hi;
+        ulo[t][ks][j] = bf16_bits(u - hif);
+      }
+    }
+  }
+  const float inv_nb = 1.0f / (float)n_bg;
+  const int nst = S_pad / 32;
+  for (int st = wv; st < nst; st += kWaves) {
+    const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
+    const uint4 z0 = zr[h], z1 = zr[2 + h];  // k-step 0: cols 8h..8h+7; k-step 1: 16+8h..
+    bf16x8_t zb[2];
+    zb[0] = __builtin_bit_cast(bf16x8_t, z0);
+    zb[1] = __builtin_bit_cast(bf16x8_t, z1);
+    float fs = 0.0f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (t >= ntb) break;  // uniform
+      f32x16_t acc = {};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uhi[t][0], zb[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ulo[t][0], zb[0], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uhi[t][1], zb[1], acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ulo[t][1], zb[1], acc, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int b = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float v = link == 2 ? acc[i] : fast_sigmoid(acc[i]);
+        fs += b < n_bg ? v : 0.0f;
+      }
+    }
+    fs += __shfl_xor(fs, 32, kWave);
+    if (h == 0) f[32 * st + r] = fs * inv_nb;
+  }
+  // f0 (background mean output) and f(x)
+  float z0s = 0.0f;
+  for (int b = threadIdx.x; b < n_bg; b += kThreads) z0s += link == 2 ? cb[b] : fast_sigmoid(cb[b]);
+  z0s = wave_sum(z0s);
+  if (lane == 0) red[wv] = z0s;
+  float zx = 0.0f;
+  if (threadIdx.x < 32) zx = threadIdx.x < d ? a[threadIdx.x] * xs[threadIdx.x] : 0.0f;
+  zx = wave_sum(zx);
+  if (threadIdx.x == 0) red[4] = zx;
+  __syncthreads();
+  const float f0m = (red[0] + red[1] + red[2] + red[3]) * inv_nb;
+  const float logit_x = red[4] + bias;
+  float f0l, fxl;
+  if (link == 2) { f0l = f0m; fxl = logit_x; }
+  else if (link == 1) {
+    const float p0 = fminf(fmaxf(f0m, 1e-12f), 1.0f - 1e-7f);
+    f0l = __logf(p0 / (1.0f - p0));
+    fxl = logit_x;
+  } else { f0l = f0m; fxl = fast_sigmoid(logit_x); }
+  const float delta = fxl - f0l;
+  for (int s = threadIdx.x; s < S; s += kThreads) {
+    float v = f[s];
+    if (link == 1) {
+      v = fminf(fmaxf(v, 1e-12f), 1.0f - 1e-7f);
+      v = __logf(v / (1.0f - v));
+    }
+    f[s] = v - f0l;
+  }
+  __syncthreads();
+  // phi_i = sum_s A[i][s] y_s - Az[i] delta, i < d-1: 8 threads per output
+  const int i = threadIdx.x >> 3, part = threadIdx.x & 7;
+  float acc = 0.0f;
+  if (i < d - 1) {
+    const float* Ai = Amat + (int64_t)i * S;
+    for (int s = part; s < S; s += 8) acc = fmaf(Ai[s], f[s], acc);
+  }
+  acc = group_sum<8>(acc);
+  __shared__ float ph[32];
+  if (part == 0 && i < d - 1) ph[i] = acc - Az[i] * delta;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float sum = 0.0f;
+    for (int k = 0; k < d - 1; ++k) sum += ph[k];
+    ph[d - 1] = delta - sum;
+    fx_out[e] = fxl;
+    f0_out[e] = f0l;
+  }
+  __syncthreads();
+  if (threadIdx.x < d) phi[(int64_t)e * d + threadIdx.x] = ph[threadIdx.x];
+}
+
+}  // namespace
+
+void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
+                       const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
+                       const float* Az, int link, float* phi, float* fx_out, float* f0_out,
+                       hipStream_t stream) {
+  if (d < 2 || d > 30) throw std::runtime_error("kernelshap: 2 <= d <= 30");
+  if (n_bg < 1 || n_bg > kMaxBg) throw std::runtime_error("kernelshap: 1 <= n_bg <= 128");
+  if (S < 1 || S_pad % 32 != 0 || S_pad < S || S_pad > kMaxS)
+    throw std::runtime_error("kernelshap: S_pad must be a multiple of 32 in [S, 4096]");
+  if (n_expl <= 0) return;
+  kernelshap_kernel<<<n_expl, kThreads, 0, stream>>>(X, n_expl, d, a, bias, bg, cb, n_bg, Z, S, S_pad, Amat, Az,
+                                                      link, phi, fx_out, f0_out);
+  check_launch("kernelshap");
+}
+
+}  // namespace fdx

@@ -50,11 +50,11 @@ void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, 
 constexpr int kLRPartStride = 1088;  // [0,32) grad, 32 loss, 33 wsum, [64,1088) Hessian 32x32
 int logreg_pass_blocks();
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
-                        const float* class_w, const int* done, int hessian, float* partial,
-                        int nblocks, hipStream_t stream);
+                        const float* class_w, const int* done, int hessian, int row_sub,
+                        float* partial, int nblocks, hipStream_t stream);
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
-                            const float* class_w, const int* done, int hessian, float x_scale,
-                            float* partial, int nblocks, hipStream_t stream);
+                            const float* class_w, const int* done, int hessian, int row_sub,
+                            float x_scale, float* partial, int nblocks, hipStream_t stream);
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.
@@ -87,9 +87,11 @@ void launch_confusion(const float* scores, const uint8_t* labels, int64_t n, flo
                       unsigned long long* out4, hipStream_t stream);
 
 // ---- kernelshap.hip ----
-void launch_kernelshap(const float* X, int n_expl, int d, const float* w, float b,
-                       const float* bg, int n_bg, const uint16_t* Z, int S, const float* Amat,
-                       const float* zlast, int link, float* phi, float* fx_out, float* f0_out,
+// X [E][d] raw explanations; a [32] folded weights; bg [n_bg][d] raw background; cb [n_bg]
+// background logits; Z [S_pad][32] bf16 coalitions (col 31 = 1); Amat [d-1][S]; Az [d-1].
+void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
+                       const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
+                       const float* Az, int link, float* phi, float* fx_out, float* f0_out,
                        hipStream_t stream);
 
 }  // namespace fdx

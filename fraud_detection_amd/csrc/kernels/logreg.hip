@@ -54,7 +54,7 @@ template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, float* __restrict__ partial) {
+    int hess_stride, int row_sub, float* __restrict__ partial) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][34];
@@ -76,7 +76,9 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   uint16_t* my_tile = tile[wv];
 
   const int64_t n = row_end - row_begin;
-  const int64_t step = (int64_t)gridDim.x * kWaves * 64;
+  // row_sub > 1: only 64-row tiles t with (t mod G*row_sub) < G are visited (G = waves in the
+  // grid): a uniform 1/row_sub subsample used by the early progressive-Newton iterations.
+  const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
   // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
   typedef typename std::conditional<FMT == 0, uint4, uint2>::type vec_t;
@@ -246,6 +248,10 @@ __device__ void build_grad(const double* red, const double* st, int d, int fit_i
   }
 }
 
+// One wave (64 threads): every operand is staged in LDS with parallel loads first (the
+// reduced 1088-double vector and the 256-double state), so no thread walks global memory
+// serially; reductions are wave-parallel, the Cholesky trailing update is spread over (i, j)
+// pairs, and the barriers of a single-wave workgroup are nearly free.
 __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
                                                            double* __restrict__ st,
                                                            float* __restrict__ w32,
@@ -253,108 +259,115 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
                                                            double tol, int max_iter,
                                                            int fit_intercept) {
   if (*done) return;
+  __shared__ double sr[kLRPartStride];
+  __shared__ double ss[kStateSize];
   __shared__ double A[32][33];
   __shared__ double b[32];
   __shared__ double grad[32];
   __shared__ int idx[32];
-  __shared__ int decision;  // 0 accept+step, 1 backtrack, 2 converged
-  __shared__ double obj_s;
   const int t = threadIdx.x;
-  const double S = red[33] > 0.0 ? red[33] : 1.0;
+  for (int i = t; i < kLRPartStride; i += 64) sr[i] = red[i];
+  for (int i = t; i < kStateSize; i += 64) ss[i] = st[i];
+  __syncthreads();
+  const double S = sr[33] > 0.0 ? sr[33] : 1.0;
   const double reg = 1.0 / (C * S);
   const int m = d + (fit_intercept ? 1 : 0);
   if (t < 32) idx[t] = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
-  build_grad(red, st, d, fit_intercept, reg, S, grad, t);
+  build_grad(sr, ss, d, fit_intercept, reg, S, grad, t);
+  __syncthreads();
+  double w2 = (t < d) ? ss[kW + t] * ss[kW + t] : 0.0;
+  double ga = (t < m) ? fabs(grad[idx[t]]) : 0.0;
+  w2 = wave_sum(w2);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ga = fmax(ga, __shfl_xor(ga, o, kWave));
+  const double obj = sr[32] / S + 0.5 * reg * w2;
+  const double gmax = ga;
+  const int it = (int)ss[kIter];
+  const double prev = ss[kObjPrev];
+  // Backtrack only on a real increase: the loss is accumulated in fp32 per block (relative
+  // noise ~1e-7), so near the optimum a true decrease can hide below that noise floor.
+  int dec;
+  if (it > 0 && obj > prev + 1e-6 * fabs(prev) && ss[kBacktracks] < 40.0) dec = 1;
+  else if (gmax <= tol) dec = 2;
+  else dec = 0;
   __syncthreads();
   if (t == 0) {
-    double wn2 = 0.0;
-    for (int j = 0; j < d; ++j) wn2 += st[kW + j] * st[kW + j];
-    const double obj = red[32] / S + 0.5 * reg * wn2;
-    double gmax = 0.0;
-    for (int k = 0; k < m; ++k) gmax = fmax(gmax, fabs(grad[idx[k]]));
-    const int it = (int)st[kIter];
-    const double prev = st[kObjPrev];
-    int dec;
-    if (it > 0 && obj > prev + 1e-12 * fabs(prev) && st[kBacktracks] < 40.0) dec = 1;
-    else if (gmax <= tol) dec = 2;
-    else dec = 0;
-    decision = dec;
-    obj_s = obj;
-    st[kObj] = obj;
-    if (dec != 1) st[kGmax] = gmax;
+    ss[kObj] = obj;
+    if (dec != 1) ss[kGmax] = gmax;
   }
-  __syncthreads();
-  const int dec = decision;
   if (dec == 1) {  // objective went up: halve the last step from the last accepted point
     if (t < kCols) {
-      st[kStep + t] *= 0.5;
-      st[kW + t] = st[kWPrev + t] + st[kStep + t];
+      ss[kStep + t] *= 0.5;
+      ss[kW + t] = ss[kWPrev + t] + ss[kStep + t];
     }
-    if (t == 0) st[kBacktracks] += 1.0;
+    if (t == 0) ss[kBacktracks] += 1.0;
   } else if (dec == 2) {
     if (t == 0) {
-      st[kConverged] = 1.0;
+      ss[kConverged] = 1.0;
       *done = 1;
     }
   } else {
     // H_active = H/S + reg I (penalised coords); solve H s = -grad by Cholesky (fp64).
-    if (t < m) {
-      for (int k = 0; k < m; ++k) {
-        const int r = idx[t], c = idx[k];
-        double h = red[64 + r * kCols + c] / S;
-        if (r == c && r < d) h += reg;
-        A[t][k] = h;
-      }
-      b[t] = -grad[idx[t]];
+    for (int p = t; p < m * m; p += 64) {
+      const int i = p / m, k = p % m;
+      const int r = idx[i], c = idx[k];
+      double h = sr[64 + r * kCols + c] / S;
+      if (r == c && r < d) h += reg;
+      A[i][k] = h;
     }
+    if (t < m) b[t] = -grad[idx[t]];
     __syncthreads();
     for (int k = 0; k < m; ++k) {
-      if (t == 0) {
-        double piv = A[k][k];
-        A[k][k] = sqrt(piv > 1e-300 ? piv : 1e-300);
-      }
+      const double lkk = sqrt(fmax(A[k][k], 1e-300));
       __syncthreads();
-      if (t > k && t < m) A[t][k] /= A[k][k];
+      if (t == 0) A[k][k] = lkk;
+      if (t > k && t < m) A[t][k] /= lkk;
       __syncthreads();
-      if (t > k && t < m) {
-        for (int j = k + 1; j <= t; ++j) A[t][j] -= A[t][k] * A[j][k];
+      const int nt = m - k - 1;
+      for (int p = t; p < nt * nt; p += 64) {
+        const int i = k + 1 + p / nt, j = k + 1 + p % nt;
+        if (j <= i) A[i][j] -= A[i][k] * A[j][k];
       }
       __syncthreads();
     }
     for (int k = 0; k < m; ++k) {  // L y = b
-      if (t == 0) b[k] /= A[k][k];
+      const double yk = b[k] / A[k][k];
       __syncthreads();
-      if (t > k && t < m) b[t] -= A[t][k] * b[k];
+      if (t == 0) b[k] = yk;
+      if (t > k && t < m) b[t] -= A[t][k] * yk;
       __syncthreads();
     }
     for (int k = m - 1; k >= 0; --k) {  // L^T x = y
-      if (t == 0) b[k] /= A[k][k];
+      const double xk = b[k] / A[k][k];
       __syncthreads();
-      if (t < k) b[t] -= A[k][t] * b[k];
+      if (t == 0) b[k] = xk;
+      if (t < k) b[t] -= A[k][t] * xk;
       __syncthreads();
     }
     if (t < kCols) {
-      st[kWPrev + t] = st[kW + t];
-      st[kStep + t] = 0.0;
+      ss[kWPrev + t] = ss[kW + t];
+      ss[kStep + t] = 0.0;
     }
     __syncthreads();
     if (t < m) {
       const int j = idx[t];
-      st[kStep + j] = b[t];
-      st[kW + j] = st[kWPrev + j] + b[t];
+      ss[kStep + j] = b[t];
+      ss[kW + j] = ss[kWPrev + j] + b[t];
     }
     if (t == 0) {
-      st[kObjPrev] = obj_s;
-      st[kBacktracks] = 0.0;
-      st[kNAccepted] += 1.0;
+      ss[kObjPrev] = obj;
+      ss[kBacktracks] = 0.0;
+      ss[kNAccepted] += 1.0;
     }
   }
   __syncthreads();
-  if (t < kCols) w32[t] = (t == kLabelCol) ? 0.0f : (float)st[kW + t];
   if (t == 0) {
-    st[kIter] += 1.0;
-    if (dec != 2 && (int)st[kIter] >= max_iter) *done = 1;
+    ss[kIter] += 1.0;
+    if (dec != 2 && (int)ss[kIter] >= max_iter) *done = 1;
   }
+  __syncthreads();
+  if (t < kCols) w32[t] = (t == kLabelCol) ? 0.0f : (float)ss[kW + t];
+  for (int i = t; i < kStateSize; i += 64) st[i] = ss[i];
 }
 
 // Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.
@@ -407,33 +420,32 @@ int logreg_pass_blocks() {
 }
 
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
-                        const float* class_w, const int* done, int hessian, float* partial,
-                        int nblocks, hipStream_t stream) {
+                        const float* class_w, const int* done, int hessian, int row_sub,
+                        float* partial, int nblocks, hipStream_t stream) {
   // hessian: 0 = gradient/loss only; h >= 1 = also the Hessian, from every h-th row tile.
+  // row_sub >= 1: visit a uniform 1/row_sub of the 64-row tiles (progressive Newton).
+  if (row_sub < 1) row_sub = 1;
   if (hessian > 0)
-    logreg_pass_kernel<true, 0><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                 class_w, done, 1.0f, 32, hessian,
-                                                                 partial);
+    logreg_pass_kernel<true, 0><<<nblocks, kThreads, 0, stream>>>(
+        X, row_begin, row_end, w, class_w, done, 1.0f, 32, hessian, row_sub, partial);
   else
-    logreg_pass_kernel<false, 0><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                  class_w, done, 1.0f, 32, 1,
-                                                                  partial);
+    logreg_pass_kernel<false, 0><<<nblocks, kThreads, 0, stream>>>(
+        X, row_begin, row_end, w, class_w, done, 1.0f, 32, 1, row_sub, partial);
   check_launch("logreg_pass");
 }
 
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
-                            const float* class_w, const int* done, int hessian, float x_scale,
-                            float* partial, int nblocks, hipStream_t stream) {
+                            const float* class_w, const int* done, int hessian, int row_sub,
+                            float x_scale, float* partial, int nblocks, hipStream_t stream) {
   // fp8 rows store features * x_scale for columns < 30; the bias (col 30) and label (col 31)
   // are stored unscaled.
+  if (row_sub < 1) row_sub = 1;
   if (hessian > 0)
-    logreg_pass_kernel<true, 1><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                 class_w, done, x_scale, 30,
-                                                                 hessian, partial);
+    logreg_pass_kernel<true, 1><<<nblocks, kThreads, 0, stream>>>(
+        X, row_begin, row_end, w, class_w, done, x_scale, 30, hessian, row_sub, partial);
   else
-    logreg_pass_kernel<false, 1><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w,
-                                                                  class_w, done, x_scale, 30, 1,
-                                                                  partial);
+    logreg_pass_kernel<false, 1><<<nblocks, kThreads, 0, stream>>>(
+        X, row_begin, row_end, w, class_w, done, x_scale, 30, 1, row_sub, partial);
   check_launch("logreg_pass_fp8");
 }
 

@@ -123,6 +123,52 @@ __global__ __launch_bounds__(kThreads) void scaler_partial_kernel(const float* _
   }
 }
 
+// Fast path for contiguous rows (ld == d, 16 B aligned): 128-row tiles arrive through fully
+// coalesced 16 B loads into LDS; thread (column c = tid & 31, row group tid >> 5) then walks
+// its column of the tile (consecutive lanes read consecutive floats: conflict-free).
+constexpr int kStatTileRows = 128;
+
+__global__ __launch_bounds__(kThreads) void scaler_partial_tiled_kernel(const float* __restrict__ X,
+                                                                        int64_t n, int d,
+                                                                        const float* __restrict__ pivot,
+                                                                        double* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) float tile[kStatTileRows * 30];
+  __shared__ double red[2][8][32];
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const double piv = (c < d) ? (double)pivot[c] : 0.0;
+  double s = 0.0, q = 0.0;
+  const int64_t ntiles = (n + kStatTileRows - 1) / kStatTileRows;
+  const int64_t total = n * (int64_t)d;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t f0 = t * kStatTileRows * (int64_t)d;
+    const int nf = (int)((total - f0) < (int64_t)kStatTileRows * d ? (total - f0) : (int64_t)kStatTileRows * d);
+    const int nf4 = nf >> 2;
+    const float4* src = reinterpret_cast<const float4*>(X + f0);
+    for (int i = threadIdx.x; i < nf4; i += kThreads) reinterpret_cast<float4*>(tile)[i] = src[i];
+    for (int i = (nf4 << 2) + threadIdx.x; i < nf; i += kThreads) tile[i] = X[f0 + i];
+    __syncthreads();
+    const int rows = nf / d;
+    if (c < d) {
+      for (int r = rg; r < rows; r += 8) {
+        const double dd = (double)tile[r * d + c] - piv;
+        s += dd;
+        q = fma(dd, dd, q);
+      }
+    }
+    __syncthreads();
+  }
+  red[0][rg][c] = s;
+  red[1][rg][c] = q;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    double ss = 0.0, qq = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) { ss += red[0][g][c]; qq += red[1][g][c]; }  // fixed order
+    partial[(int64_t)blockIdx.x * 64 + c] = ss;
+    partial[(int64_t)blockIdx.x * 64 + 32 + c] = qq;
+  }
+}
+
 // Fixed-order reduction of [nblocks][64] fp64 partials into sums[64].
 __global__ __launch_bounds__(256) void scaler_reduce_kernel(const double* __restrict__ partial,
                                                             int nblocks, double* __restrict__ sums) {
@@ -384,6 +430,11 @@ inline int vec_for(const void* p, int ld) {
 
 void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float* pivot,
                            double* partial, int nblocks, hipStream_t stream) {
+  if (ld == d && d <= 30 && (reinterpret_cast<uintptr_t>(X) % 16) == 0) {
+    scaler_partial_tiled_kernel<<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, partial);
+    check_launch("scaler_partial_tiled");
+    return;
+  }
   switch (vec_for(X, ld)) {
     case 4: scaler_partial_kernel<4><<<nblocks, kThreads, 0, stream>>>(X, n, ld, d, pivot, partial); break;
     case 2: scaler_partial_kernel<2><<<nblocks, kThreads, 0, stream>>>(X, n, ld, d, pivot, partial); break;

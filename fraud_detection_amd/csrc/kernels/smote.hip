@@ -27,43 +27,60 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   const int lane = lane_id();
   const int q = lane & 3, rr = lane >> 2;
   const uint32_t range = (uint32_t)mq * (uint32_t)k;
-  const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 16;
-  for (int64_t s = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 16 + rr; s < n_new;
-       s += step) {
-    const Philox4 r = philox4x32_10((uint32_t)s, (uint32_t)(s >> 32), cb0, cb1, key0, key1);
+  const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 64;
+  for (int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 64; base < n_new;
+       base += step) {
+    // one Philox draw per lane = one sample per lane (64 samples per wave-iteration)
+    const int64_t sl = base + lane;
+    const Philox4 r = philox4x32_10((uint32_t)sl, (uint32_t)(sl >> 32), cb0, cb1, key0, key1);
     const uint32_t pick = u32_range(r.x, range);
-    const int i = (int)(pick / (uint32_t)k);
-    const int kk = (int)(pick % (uint32_t)k);
-    const float lam = u32_to_unit(r.y);
-    const int jn = nbr[(int64_t)i * k + kk];
-    const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
-    const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
-    const float4 a0 = xi[0], a1 = xi[1], b0 = xj[0], b1 = xj[1];
-    float o[8] = {fmaf(lam, b0.x - a0.x, a0.x), fmaf(lam, b0.y - a0.y, a0.y),
-                  fmaf(lam, b0.z - a0.z, a0.z), fmaf(lam, b0.w - a0.w, a0.w),
-                  fmaf(lam, b1.x - a1.x, a1.x), fmaf(lam, b1.y - a1.y, a1.y),
-                  fmaf(lam, b1.z - a1.z, a1.z), fmaf(lam, b1.w - a1.w, a1.w)};
-    if (q == 3) {
-      o[6] = 1.0f;   // col 30: intercept column
-      o[7] = label;  // col 31: label
-    }
-    if constexpr (OUT == 0) {
-      uint4 pk;
-      pk.x = pack_bf16x2(o[0], o[1]);
-      pk.y = pack_bf16x2(o[2], o[3]);
-      pk.z = pack_bf16x2(o[4], o[5]);
-      pk.w = pack_bf16x2(o[6], o[7]);
-      reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
-    } else {
-      uint2 pk = make_uint2(0, 0);
+    const int my_i = (int)(pick / (uint32_t)k);
+    const int my_j = sl < n_new ? nbr[(int64_t)my_i * k + (int)(pick % (uint32_t)k)] : 0;
+    const float my_lam = u32_to_unit(r.y);
+    // 4 row groups of 16 samples: 4 lanes per sample, 8 columns per lane; gathers issued first
+    float4 a0[4], a1[4], b0[4], b1[4];
+    float lam[4];
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const bool feat = (8 * q + jj) < kBiasCol;
-        const uint32_t b = f32_to_fp8e4m3(feat ? o[jj] * out_scale : o[jj]);
-        if (jj < 4) pk.x |= b << (8 * jj);
-        else pk.y |= b << (8 * (jj - 4));
+    for (int u = 0; u < 4; ++u) {
+      const int src = 16 * u + rr;
+      const int i = __shfl(my_i, src, kWave);
+      const int jn = __shfl(my_j, src, kWave);
+      lam[u] = __shfl(my_lam, src, kWave);
+      const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
+      const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
+      a0[u] = xi[0]; a1[u] = xi[1]; b0[u] = xj[0]; b1[u] = xj[1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t s = base + 16 * u + rr;
+      if (s >= n_new) continue;
+      const float l = lam[u];
+      float o[8] = {fmaf(l, b0[u].x - a0[u].x, a0[u].x), fmaf(l, b0[u].y - a0[u].y, a0[u].y),
+                    fmaf(l, b0[u].z - a0[u].z, a0[u].z), fmaf(l, b0[u].w - a0[u].w, a0[u].w),
+                    fmaf(l, b1[u].x - a1[u].x, a1[u].x), fmaf(l, b1[u].y - a1[u].y, a1[u].y),
+                    fmaf(l, b1[u].z - a1[u].z, a1[u].z), fmaf(l, b1[u].w - a1[u].w, a1[u].w)};
+      if (q == 3) {
+        o[6] = 1.0f;   // col 30: intercept column
+        o[7] = label;  // col 31: label
       }
-      reinterpret_cast<uint2*>(out)[s * 4 + q] = pk;
+      if constexpr (OUT == 0) {
+        uint4 pk;
+        pk.x = pack_bf16x2(o[0], o[1]);
+        pk.y = pack_bf16x2(o[2], o[3]);
+        pk.z = pack_bf16x2(o[4], o[5]);
+        pk.w = pack_bf16x2(o[6], o[7]);
+        reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
+      } else {
+        uint2 pk = make_uint2(0, 0);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const bool feat = (8 * q + jj) < kBiasCol;
+          const uint32_t b = f32_to_fp8e4m3(feat ? o[jj] * out_scale : o[jj]);
+          if (jj < 4) pk.x |= b << (8 * jj);
+          else pk.y |= b << (8 * (jj - 4));
+        }
+        reinterpret_cast<uint2*>(out)[s * 4 + q] = pk;
+      }
     }
   }
 }
@@ -74,7 +91,7 @@ void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, void* out, hipStream_t stream) {
   if (n_new <= 0) return;
-  const int grid = stream_grid(n_new, (kThreads / kWave) * 16, 4096);
+  const int grid = stream_grid(n_new, (kThreads / kWave) * 64, 2048);
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
   if (out_kind == 0)

@@ -29,7 +29,8 @@ from ..ops.layout import BIAS_COL, DEFAULT_FP8_SCALE, NCOLS, TORCH_STORAGE
 class TrainConfig:
     solver: str = "newton"          # newton | sgd
     C: float = 1.0
-    tol: float = 1e-6               # max |grad| of the mean objective (sklearn lbfgs uses 1e-4)
+    tol: float = 1e-4               # max |grad| of the mean objective: the reference model's
+                                    # LogisticRegression(tol=1e-4) lbfgs stopping rule (App. C)
     max_iter: int = 25
     fit_intercept: bool = True
     class_weight: str | None = None  # None | "balanced"

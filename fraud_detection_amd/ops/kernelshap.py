@@ -1,0 +1,58 @@
+"""K7 KernelSHAP coalition GEMM (csrc/kernels/kernelshap.hip) -- device wrapper."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .native import native, ptr, stream_of
+
+_LINKS = {"identity": 0, "logit": 1, "logit_model": 2}
+
+
+def _device_design(expl, dev):
+    """Upload the explainer's design once: Z as bf16 [S_pad, 32] (col 31 = 1 folds the
+    background intercepts into the GEMM), A [d-1, S], A z_M, background rows and logits."""
+    key = (str(dev),)
+    if expl._dev_cache is not None and expl._dev_cache[0] == key:
+        return expl._dev_cache[1]
+    d = expl.d
+    S = expl.Z.shape[0]
+    S_pad = (S + 31) // 32 * 32
+    if S_pad > 4096:
+        raise ValueError("at most 4096 coalitions per design on device")
+    Zp = np.zeros((S_pad, 32), np.float32)
+    Zp[:S, :d] = expl.Z
+    Zp[:, 31] = 1.0
+    a32 = np.zeros(32, np.float32)
+    a32[:d] = expl.a[:d]
+    cb = (expl.B.astype(np.float64) @ expl.a[:d] + expl.bias).astype(np.float32)
+    t = {
+        "Z": torch.from_numpy(Zp).to(dev).to(torch.bfloat16).contiguous(),
+        "A": torch.from_numpy(expl.A.astype(np.float32)).to(dev).contiguous(),
+        "Az": torch.from_numpy((expl.A @ expl.zM).astype(np.float32)).to(dev),
+        "a": torch.from_numpy(a32).to(dev),
+        "bg": torch.from_numpy(np.ascontiguousarray(expl.B, np.float32)).to(dev),
+        "cb": torch.from_numpy(cb).to(dev),
+        "S": S, "S_pad": S_pad,
+    }
+    expl._dev_cache = (key, t)
+    return t
+
+
+def kernelshap(X: torch.Tensor, expl, sync: bool = True):
+    """X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else tensors)."""
+    if X.dim() != 2 or X.dtype != torch.float32 or X.shape[1] != expl.d or not X.is_contiguous():
+        raise ValueError(f"X must be contiguous float32 [E, {expl.d}]")
+    m = native()
+    dev = X.device
+    t = _device_design(expl, dev)
+    E = X.shape[0]
+    phi = torch.empty((E, expl.d), device=dev, dtype=torch.float32)
+    fx = torch.empty(E, device=dev, dtype=torch.float32)
+    f0 = torch.empty(E, device=dev, dtype=torch.float32)
+    m.kernelshap(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]), expl.B.shape[0],
+                 ptr(t["Z"]), t["S"], t["S_pad"], ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi), ptr(fx),
+                 ptr(f0), stream_of(X))
+    if not sync:
+        return phi, fx, f0
+    return phi.cpu().numpy().astype(np.float64), fx.cpu().numpy().astype(np.float64), float(f0[0].item()) if E else 0.0

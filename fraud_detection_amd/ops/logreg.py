@@ -54,16 +54,25 @@ class LRWorkspace:
         self.class_w = torch.ones(2, device=device, dtype=torch.float32)
 
     def reset(self, w0: np.ndarray, class_w=(1.0, 1.0)):
-        st = np.zeros(STATE_SIZE)
+        """Initial state via pinned staging + async H2D copies (no stream drain).  The staging
+        buffers are only rewritten after the previous fit's final state read-back synchronised."""
+        if not hasattr(self, "_st_h"):
+            self._st_h = torch.zeros(STATE_SIZE, dtype=torch.float64, pin_memory=True)
+            self._w_h = torch.zeros(NCOLS, dtype=torch.float32, pin_memory=True)
+            self._cw_h = torch.zeros(2, dtype=torch.float32, pin_memory=True)
+        st = self._st_h.numpy()
+        st[:] = 0.0
         st[S_W:S_W + 32] = w0
         st[S_WPREV:S_WPREV + 32] = w0
         st[S_OBJPREV] = np.inf
-        self.state.copy_(torch.from_numpy(st))
-        w32 = np.asarray(w0, dtype=np.float32).copy()
+        w32 = self._w_h.numpy()
+        w32[:] = np.asarray(w0, dtype=np.float32)
         w32[LABEL_COL] = 0
-        self.w32.copy_(torch.from_numpy(w32))
+        self._cw_h.numpy()[:] = class_w
+        self.state.copy_(self._st_h, non_blocking=True)
+        self.w32.copy_(self._w_h, non_blocking=True)
+        self.class_w.copy_(self._cw_h, non_blocking=True)
         self.done.zero_()
-        self.class_w.copy_(torch.tensor(class_w, dtype=torch.float32))
 
 
 HESS_SAMPLE_ROWS = 1 << 22  # auto Hessian sub-sampling keeps >= ~4M rows in the H estimate
@@ -73,14 +82,28 @@ def auto_hess_stride(n_rows: int) -> int:
     return int(max(1, min(8, n_rows // HESS_SAMPLE_ROWS)))
 
 
-def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True):
-    """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact)."""
+def progressive_schedule(n_rows: int) -> list:
+    """Warm-up phases [(tile_subsample, newton_iters), ...] before the full-data phase.  Each
+    phase keeps >= ~1M rows, so its optimum is within sampling noise of the full one and the
+    full-data phase then needs ~2-3 quadratic-convergence steps."""
+    if n_rows >= (16 << 20):
+        return [(16, 2), (4, 2)]
+    if n_rows >= (4 << 20):
+        return [(4, 3)]
+    return []
+
+
+def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True,
+          sub: int = 1):
+    """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact).
+    sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up)."""
     dptr = ptr(ws.done) if done else 0
     h = int(hessian)
     if storage_kind(rows) == "bf16":
-        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, ptr(ws.partial), ws.nblocks, s)
+        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
+                      ws.nblocks, s)
     else:
-        m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, float(fp8_scale),
+        m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
                           ptr(ws.partial), ws.nblocks, s)
     m.logreg_reduce(ptr(ws.partial), ws.nblocks, PART_STRIDE if h else 64, ptr(ws.red), dptr, s)
 
@@ -114,7 +137,7 @@ def _default_w0(w0):
 def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: int = 25,
                class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
-               sync: bool = True, hess_stride: int | str = "auto") -> FitInfo:
+               sync: bool = True, hess_stride: int | str = "auto", progressive="auto") -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
@@ -129,21 +152,57 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     s = stream_of(rows)
     n = rows.shape[0]
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
+    n_sched = n
     if comm is not None and comm.world_size > 1:
         hs = int(comm.all_reduce_scalar(hs, op="min"))  # identical H sampling rule on every rank
-    it = 0
-    while it < max_iter:
-        for _ in range(min(check_every, max_iter - it)):
+        n_sched = int(comm.all_reduce_scalar(n, op="min"))  # identical warm-up schedule on every rank
+    sched = progressive_schedule(n_sched) if progressive == "auto" else list(progressive or [])
+
+    # Progressive warm-up: Newton steps on uniform 1/sub tile subsets (never "converge": tol=0),
+    # then full-data Newton until the exact gradient meets `tol`.  Between phases the objective
+    # history is reset so backtracking only compares objectives of the same sample.
+    for sub, iters in sched:
+        hs_w = auto_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
+        for _ in range(iters):
+            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub)
+            if comm is not None and comm.world_size > 1:
+                comm.all_reduce_(ws.red)
+            m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
+                            int(fit_intercept), s)
+        ws.state[S_OBJPREV].fill_(float("inf"))
+        ws.state[S_BACKTRACKS].zero_()
+    warm = sum(it for _, it in sched)
+
+    def enqueue_chunk(k: int) -> int:
+        for _ in range(k):
             _pass(m, rows, ws, hs, 0, n, fp8_scale, s)
             if comm is not None and comm.world_size > 1:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
-                            int(max_iter), int(fit_intercept), s)
-            it += 1
+                            int(max_iter + warm), int(fit_intercept), s)
+        return k
+
+    # Convergence is checked one chunk behind: chunk i+1 is already queued when the host reads
+    # chunk i's `done` flag (async copy into pinned memory), so the GPU never waits on the host.
+    # Iterations after convergence are device-side no-ops.  Every rank reads identical flags.
+    flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+    events = [torch.cuda.Event(), torch.cuda.Event()]
+    it = enqueue_chunk(min(check_every, max_iter))
+    flags[0].copy_(ws.done, non_blocking=True)
+    events[0].record()
+    cur = 0
+    while it < max_iter:
+        it += enqueue_chunk(min(check_every, max_iter - it))
+        nxt = cur ^ 1
+        flags[nxt].copy_(ws.done, non_blocking=True)
+        events[nxt].record()
         if not sync:
+            cur = nxt
             continue
-        if int(ws.done.item()):
+        events[cur].synchronize()
+        if int(flags[cur][0]):
             break
+        cur = nxt
     return _info_from_state(ws.state.cpu().numpy())
 
 

@@ -256,7 +256,7 @@ class NewtonStateRef:
         obj = red[32] / S + 0.5 * reg * float(np.dot(self.w[:d], self.w[:d]))
         gmax = float(np.max(np.abs(grad[idx])))
         self.obj = obj
-        if self.iter > 0 and obj > self.obj_prev + 1e-12 * abs(self.obj_prev) and self.backtracks < 40:
+        if self.iter > 0 and obj > self.obj_prev + 1e-6 * abs(self.obj_prev) and self.backtracks < 40:
             self.step *= 0.5
             self.w = self.w_prev + self.step
             self.backtracks += 1

@@ -10,7 +10,7 @@ from . import reference as ref
 from .layout import DEFAULT_FP8_SCALE, DTYPE_KIND, NCOLS, NFEAT_MAX, TORCH_STORAGE
 from .native import native, ptr, stream_of
 
-_SCALER_BLOCKS = 1024
+_SCALER_BLOCKS = 2048  # 8 resident blocks per CU x 256 CUs
 
 
 @dataclass

@@ -1,0 +1,180 @@
+"""Training entry point behind train_model.py (reference call stack: SURVEY.md §3.1).
+
+    read CSV (native reader) -> stratified 80/20 split (rs=42)
+    -> StratifiedKFold(5, shuffle, rs=42): per fold the device pipeline (scaler on the fold's
+       train rows -> SMOTE k-NN + generation -> fit) and the fold's validation AUC
+    -> final pipeline on the whole train split -> exact test AUC
+    -> artifacts in the reference layout (models/logistic_model.joblib, scaler.joblib,
+       columns.joblib, feature_names.json; models/xgb_model.joblib for the GBDT family)
+    -> MLflow run (params model_type / scale_pos_weight / cv_folds, metrics test_auc /
+       cv_auc_mean / cv_auc_std, sklearn model with signature + input example, scaler artifact),
+       registration when test_auc >= MLFLOW_AUC_THRESHOLD and the serving alias set to
+       MLFLOW_MODEL_STAGE.  Tracking failures never fail training (train_model.py:165-166).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import tempfile
+import time
+
+import numpy as np
+import torch
+
+from .compat import mlflow_compat as mlf
+from .compat.sklearn_export import LinearArtifacts, make_logistic, save_artifacts
+from .config import Settings
+from .data.io import missing_report, read_table, stratified_folds, stratified_split
+from .models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+logger = logging.getLogger("train")
+
+
+def _device(name: str) -> torch.device:
+    if name == "auto":
+        return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    return torch.device(name)
+
+
+def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds: int = 5, model_dir: str = "models",
+        verbose: bool = True, cfg: TrainConfig | None = None) -> dict:
+    s = settings or Settings.load()
+    say = print if verbose else (lambda *a, **k: None)
+    dev = _device(s.device)
+    t0 = time.time()
+    say("Loading dataset...")
+    X, y, names = read_table(s.data_csv)
+    if y is None:
+        raise ValueError(f"{s.data_csv} has no 'Class' column")
+    say("Checking missing values...")
+    miss = missing_report(X, names)
+    say({k: v for k, v in miss.items() if v} or "no missing values")
+    if any(miss.values()):
+        raise ValueError("missing feature values; impute before training")
+    say("Splitting dataset (Train 80% / Test 20%)...")
+    tr, te = stratified_split(y, 0.2, 42)
+    Xtr, ytr = torch.from_numpy(X[tr]).to(dev), torch.from_numpy(y[tr]).to(dev)
+    Xte, yte = torch.from_numpy(X[te]).to(dev), torch.from_numpy(y[te]).to(dev)
+    neg, pos = int((y[tr] == 0).sum()), int((y[tr] == 1).sum())
+    scale_pos_weight = neg / pos if pos > 0 else 1.0
+    say(f" Class balance before SMOTE -> [{neg} {pos}]")
+    cfg = cfg or TrainConfig(solver=s.solver, storage=s.dtype, seed=s.seed, k_neighbors=s.smote_k)
+    if model_type not in ("logistic", "gbdt"):
+        raise ValueError("model_type must be 'logistic' or 'gbdt'")
+    cv_scores = []
+    if cv_folds and cv_folds > 1 and pos >= cv_folds:
+        say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
+        for k, (ftr, fva) in enumerate(stratified_folds(y[tr], cv_folds, 42)):
+            fi = torch.from_numpy(ftr).to(dev)
+            vi = torch.from_numpy(fva).to(dev)
+            res = _fit(model_type, cfg, Xtr.index_select(0, fi).contiguous(), ytr.index_select(0, fi).contiguous())
+            auc = _score(model_type, res, Xtr.index_select(0, vi).contiguous(), ytr.index_select(0, vi).contiguous())
+            cv_scores.append(auc)
+            say(f"  Fold {k + 1} AUC: {auc:.4f}")
+        say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
+    say(f" Training final {model_type} model with SMOTE on the full training set...")
+    res = _fit(model_type, cfg, Xtr, ytr)
+    if model_type == "logistic":
+        ev = evaluate(res, Xte, yte)
+        auc = ev["auc"]
+        say(f" Class balance after SMOTE -> [{res.n_rows - res.n_minority} {res.n_minority + res.n_synthetic}]")
+    else:
+        auc = _score(model_type, res, Xte, yte)
+        ev = {"auc": auc}
+    say(f"Test AUC: {auc:.4f}")
+    paths = _save(model_type, res, names, model_dir, cfg)
+    say(f" Model and scaler saved to /{model_dir}")
+    summary = {"test_auc": float(auc), "cv_auc_mean": float(np.mean(cv_scores)) if cv_scores else None,
+               "cv_auc_std": float(np.std(cv_scores)) if cv_scores else None, "cv_scores": cv_scores,
+               "scale_pos_weight": scale_pos_weight, "paths": paths, "device": str(dev), "eval": ev,
+               "seconds": round(time.time() - t0, 3), "registered_version": None}
+    try:
+        summary["registered_version"] = _track(s, model_type, res, summary, paths, Xte, names, say)
+    except Exception as e:  # noqa: BLE001 - tracking is best effort (reference train_model.py:165-166)
+        say(f" MLflow Tracking Failed (likely connection error): {e}")
+    return summary
+
+
+def _fit(model_type, cfg, X, y):
+    if model_type == "logistic":
+        return DevicePipeline(cfg).fit(X, y)
+    from .models.gbdt import GBDTPipeline
+
+    return GBDTPipeline(cfg).fit(X, y)
+
+
+def _score(model_type, res, X, y) -> float:
+    if model_type == "logistic":
+        return float(evaluate(res, X, y)["auc"])
+    return float(res.evaluate(X, y)["auc"])
+
+
+def _save(model_type, res, names, model_dir, cfg) -> dict:
+    mean, var, scale = res.scaler.numpy()
+    if model_type == "logistic":
+        art = LinearArtifacts(coef=res.coef, intercept=res.intercept, mean=mean, var=var, scale=scale,
+                              n_samples_seen=int(res.scaler.n), feature_names=names, n_iter=res.fit.n_iter, C=cfg.C)
+        return save_artifacts(art, model_dir)
+    return res.save(model_dir, names)
+
+
+def _track(s: Settings, model_type, res, summary, paths, Xte, names, say):
+    mlf.set_tracking_uri(s.mlflow_tracking_uri)
+    mlf.set_experiment(s.mlflow_experiment)
+    version = None
+    with mlf.start_run() as run:
+        mlf.log_param("model_type", "LogisticRegression" if model_type == "logistic" else "GBDT")
+        mlf.log_param("scale_pos_weight", summary["scale_pos_weight"])
+        mlf.log_param("cv_folds", len(summary["cv_scores"]) or 0)
+        mlf.log_param("device", summary["device"])
+        mlf.log_metric("test_auc", summary["test_auc"])
+        if summary["cv_auc_mean"] is not None:
+            mlf.log_metric("cv_auc_mean", summary["cv_auc_mean"])
+            mlf.log_metric("cv_auc_std", summary["cv_auc_std"])
+        sample = Xte[:5].cpu().numpy().astype(np.float64)
+        if model_type == "logistic":
+            model = make_logistic(res.coef, res.intercept, res.fit.n_iter)
+            sc = (sample - res.scaler.numpy()[0]) / res.scaler.numpy()[2]
+            sig = mlf.infer_signature(sc, model.predict_proba(sc)[:, 1])
+            uri = mlf.log_sklearn_model(model, "model", signature=sig, input_example=sc[:1],
+                                        extra_files={"scaler.joblib": paths["scaler"],
+                                                     "feature_names.json": paths["feature_names"]})
+        else:
+            uri = res.log_model(mlf, paths)
+        mlf.log_artifact(paths["scaler"])
+        say(f" Logged run to MLflow experiment '{s.mlflow_experiment}' with input signature and examples")
+        if summary["test_auc"] >= s.mlflow_auc_threshold:
+            version = mlf.register_model(uri, s.mlflow_model_name)
+            mlf.set_registered_model_alias(s.mlflow_model_name, s.mlflow_model_stage, version)
+            say(f" Registered model version {version} (AUC {summary['test_auc']:.4f} >= {s.mlflow_auc_threshold}) "
+                f"as models:/{s.mlflow_model_name}@{s.mlflow_model_stage}")
+        else:
+            say(f"i Model not registered (AUC {summary['test_auc']:.4f} < {s.mlflow_auc_threshold})")
+        summary["run_id"] = run.info.run_id
+    return version
+
+
+def main(argv=None):
+    import argparse
+
+    ap = argparse.ArgumentParser(description="Train the fraud model on MI355X (train_model.py)")
+    ap.add_argument("--model", default=os.getenv("FDX_MODEL_TYPE", "logistic"), choices=["logistic", "gbdt"])
+    ap.add_argument("--cv-folds", type=int, default=5)
+    ap.add_argument("--model-dir", default="models")
+    ap.add_argument("--json", default=None, help="write the run summary here")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    out = run(model_type=a.model, cv_folds=a.cv_folds, model_dir=a.model_dir)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump({k: v for k, v in out.items() if k != "eval"} | {"eval": out["eval"]}, f, indent=1, default=str)
+    return 0
+
+
+if __name__ == "__main__":  # pragma: no cover
+    raise SystemExit(main())
+
+
+def tempdir() -> str:  # helper for scripts/tests
+    return tempfile.mkdtemp(prefix="fdx_train_")

@@ -1,0 +1,108 @@
+"""Data-parallel correctness on CPU ranks (gloo), SURVEY.md §7.5 "Distributed".
+
+The DP pipeline (sharded rows; all-reduced scaler sums C1, all-gathered minority rows C3,
+all-reduced Newton gradient/Hessian C5, gathered test scores for the exact AUC) must match the
+single-process computation on the concatenated data."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, out_dir, smote):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    comm = Communicator(backend="gloo")
+    X, y = separable(24_000, fraud_rate=0.02, seed=100)
+    Xt, yt = separable(8_000, fraud_rate=0.02, seed=200)
+    sh = slice(rank * len(X) // world, (rank + 1) * len(X) // world)
+    sht = slice(rank * len(Xt) // world, (rank + 1) * len(Xt) // world)
+    cfg = TrainConfig(smote=smote, tol=1e-8, init_std=0.0)
+    res = DevicePipeline(cfg, comm).fit(X[sh].contiguous(), y[sh].contiguous())
+    ev = evaluate(res, Xt[sht].contiguous(), yt[sht].contiguous(), comm)
+    mean, var, scale = res.scaler.numpy()
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), w=res.w, mean=mean, var=var, auc=ev["auc"],
+             n_train=res.n_train_rows)
+    comm.barrier()
+    comm.close()
+
+
+def _run(world, smote, tmp_path):
+    port = _free_port()
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), smote), nprocs=world, start_method="spawn")
+    return [dict(np.load(os.path.join(tmp_path, f"r{r}.npz"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_matches_single_process_without_smote(tmp_path, world):
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    outs = _run(world, False, tmp_path)
+    X, y = separable(24_000, fraud_rate=0.02, seed=100)
+    Xt, yt = separable(8_000, fraud_rate=0.02, seed=200)
+    ref = DevicePipeline(TrainConfig(smote=False, tol=1e-8, init_std=0.0)).fit(X, y)
+    ev = evaluate(ref, Xt, yt)
+    for o in outs:  # every rank holds the same global model
+        np.testing.assert_allclose(o["mean"], ref.scaler.numpy()[0], rtol=1e-10, atol=1e-9)
+        np.testing.assert_allclose(o["var"], ref.scaler.numpy()[1], rtol=1e-8)
+        np.testing.assert_allclose(o["w"], ref.w, atol=1e-7)
+        assert float(o["auc"]) == pytest.approx(ev["auc"], abs=1e-6)
+    assert np.array_equal(outs[0]["w"], outs[-1]["w"])
+
+
+def test_dp_with_smote_balances_globally(tmp_path):
+    outs = _run(2, True, tmp_path)
+    assert np.array_equal(outs[0]["w"], outs[1]["w"])
+    assert float(outs[0]["auc"]) > 0.9
+    # each rank oversamples its shard to balance; globally 2 * n_majority rows
+    from fraud_detection_amd.data.synthetic import separable
+
+    _, y = separable(24_000, fraud_rate=0.02, seed=100)
+    n_maj = [int((y[r * 12000:(r + 1) * 12000] == 0).sum()) for r in range(2)]
+    assert [int(o["n_train"]) for o in outs] == [2 * m for m in n_maj]
+
+
+def _knn_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from fraud_detection_amd.ops import knn as K
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    comm = Communicator(backend="gloo")
+    rng = np.random.default_rng(0)
+    C = np.zeros((90, 32), np.float32)
+    C[:, :30] = rng.normal(size=(90, 30))
+    mine = torch.from_numpy(C[rank * 30:(rank + 1) * 30])
+    allc, counts = comm.all_gather_rows(mine)
+    off = int(sum(counts[:rank]))
+    nbr = K.knn_topk(mine, allc, k=5, self_offset=off)
+    np.save(os.path.join(out_dir, f"knn{rank}.npy"), nbr.numpy())
+    comm.close()
+
+
+def test_dp_knn_equals_global(tmp_path):
+    port = _free_port()
+    mp.start_processes(_knn_worker, args=(3, port, str(tmp_path)), nprocs=3, start_method="spawn")
+    from fraud_detection_amd.ops import reference as ref
+
+    rng = np.random.default_rng(0)
+    C = np.zeros((90, 32), np.float32)
+    C[:, :30] = rng.normal(size=(90, 30))
+    full, _ = ref.knn_topk(C, C, 5, 0)
+    got = np.concatenate([np.load(os.path.join(tmp_path, f"knn{r}.npy")) for r in range(3)])
+    assert np.array_equal(got, full)

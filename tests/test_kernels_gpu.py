@@ -159,6 +159,16 @@ def test_newton_subsampled_hessian_same_solution(dev):
     np.testing.assert_allclose(sub.w[:31], full.w[:31], atol=2e-5)
 
 
+def test_newton_progressive_same_solution(dev):
+    X, y = _data(300_000, seed=22, rate=0.02)
+    st = S.scaler_fit(X.to(dev))
+    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
+    base = L.newton_fit(rows, tol=1e-6, max_iter=30, progressive=[])
+    prog = L.newton_fit(rows, tol=1e-6, max_iter=30, progressive=[(8, 2), (2, 2)])
+    assert base.converged and prog.converged
+    np.testing.assert_allclose(prog.w[:31], base.w[:31], atol=1e-4)
+
+
 def test_newton_deterministic(dev):
     X, y = _data(40_000, seed=12, rate=0.05)
     st = S.scaler_fit(X.to(dev))
@@ -213,6 +223,23 @@ def test_smote_generate_matches_oracle(dev):
     exp = ref.smote_generate(C, nbr.numpy(), 0, n_new, 42, 3)
     np.testing.assert_allclose(out.float().cpu().numpy(), exp, rtol=1e-2, atol=1e-2)
     assert np.all(out[:, 31].float().cpu().numpy() == 1.0)
+
+
+@pytest.mark.parametrize("link,tol", [("logit_model", 2e-4), ("identity", 2e-5), ("logit", 2e-4)])
+def test_kernelshap_matches_oracle(dev, link, tol):
+    from fraud_detection_amd.models.explainers import KernelExplainer, kernelshap_reference
+
+    rng = np.random.default_rng(5)
+    a = np.r_[rng.normal(0, 0.5, 30), 0, 0]
+    B = rng.normal(size=(100, 30)).astype(np.float32)
+    X = rng.normal(size=(64, 30)).astype(np.float32)
+    ke = KernelExplainer(a, -3.0, B, link=link, device=str(dev))
+    phi, fx, f0 = ke.explain(X)
+    phi_r, fx_r, f0_r = kernelshap_reference(X, a, -3.0, B, ke.Z, ke.A, ke.zM, link)
+    np.testing.assert_allclose(phi, phi_r, atol=tol, rtol=1e-3)
+    np.testing.assert_allclose(phi.sum(1), fx - f0, atol=1e-4)          # efficiency
+    if link == "logit_model":                                          # == LinearSHAP exactly
+        np.testing.assert_allclose(phi, a[None, :30] * (X - B.mean(0)), atol=tol)
 
 
 @pytest.mark.parametrize("n,rate,quant", [(1000, 0.1, None), (300_000, 0.002, None), (200_000, 0.3, 0.05),

@@ -90,17 +90,25 @@ def main():
 
     def lr_pass(h):
         def f():
-            nat.logreg_pass(ptr(rows2), 0, N2, ptr(ws.w32), ptr(ws.class_w), 0, h, ptr(ws.partial), ws.nblocks, s)
+            nat.logreg_pass(ptr(rows2), 0, N2, ptr(ws.w32), ptr(ws.class_w), 0, h, 1, ptr(ws.partial), ws.nblocks, s)
         return f
     case("logreg_pass_hess_2n", lr_pass(1), N2 * 64)
     case("logreg_pass_hess_s3_2n", lr_pass(3), N2 * 64)
     case("logreg_pass_grad_2n", lr_pass(0), N2 * 64)
-    case("logreg_pass_fp8_hess", lambda: nat.logreg_pass_fp8(ptr(out8), 0, n, ptr(ws.w32), ptr(ws.class_w), 0, 1, 4.0,
+    case("logreg_pass_fp8_hess", lambda: nat.logreg_pass_fp8(ptr(out8), 0, n, ptr(ws.w32), ptr(ws.class_w), 0, 1, 1, 4.0,
                                                              ptr(ws.partial), ws.nblocks, s), n * 32)
     case("logreg_reduce", lambda: nat.logreg_reduce(ptr(ws.partial), ws.nblocks, 1088, ptr(ws.red), 0, s),
          ws.nblocks * 1088 * 4)
     case("newton_update", lambda: nat.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0,
                                                     0.0, 1 << 30, 1, s), 0)
+    case("newton_fit_2n_tol1e-4", lambda: L.newton_fit(rows2, tol=1e-4, workspace=ws), N2 * 64)
+    case("newton_fit_2n_noprog", lambda: L.newton_fit(rows2, tol=1e-4, workspace=ws, progressive=[]), N2 * 64)
+    from fraud_detection_amd.models.explainers import KernelExplainer
+    from fraud_detection_amd.ops.kernelshap import kernelshap
+
+    ke = KernelExplainer(a_, b_, X[:100].cpu().numpy(), device="cuda")
+    Xe = X[:1000].contiguous()
+    case("kernelshap_1k_expl", lambda: kernelshap(Xe, ke, sync=False), 1000 * 30 * 4)
     idx = S.compact_indices(y, 1)
     case("compact_indices", lambda: S.compact_indices(y, 1), n)
     xmin = S.scale_cast(X, st, labels=y, out_dtype="f32", idx=idx)
