@@ -79,6 +79,14 @@ __host__ __device__ __forceinline__ uint8_t f32_to_fp8e4m3(float f) {
 }
 
 // ---- cross-lane reductions (wave64) ---------------------------------------------------------
+// Broadcast lane `src` (wave-uniform, usually a compile-time constant) of a 64-bit value.
+__device__ __forceinline__ double rdlane(double v, int src) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(u & 0xffffffffu), src);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(u >> 32), src);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

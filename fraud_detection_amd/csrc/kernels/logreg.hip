@@ -212,16 +212,20 @@ __global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __rest
   __shared__ double red[16][64];
   const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + c;
-  double a0 = 0.0, a1 = 0.0;
+  // 8 independent accumulators keep 8 loads in flight per lane (the partials were just written
+  // by the pass and sit in L2/MALL: this kernel is load-latency bound, not bandwidth bound).
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
   if (col < ncols) {
     int b = grp;
-    for (; b + 16 < nblocks; b += 32) {
-      a0 += (double)partial[(int64_t)b * kLRPartStride + col];
-      a1 += (double)partial[(int64_t)(b + 16) * kLRPartStride + col];
+    for (; b + 7 * 16 < nblocks; b += 8 * 16) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc[u] += (double)partial[(int64_t)(b + u * 16) * kLRPartStride + col];
     }
-    if (b < nblocks) a0 += (double)partial[(int64_t)b * kLRPartStride + col];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (b + u * 16 < nblocks) acc[u] += (double)partial[(int64_t)(b + u * 16) * kLRPartStride + col];
   }
-  red[grp][c] = a0 + a1;
+  red[grp][c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (grp == 0 && col < ncols) {
     double s = 0.0;
@@ -248,39 +252,53 @@ __device__ void build_grad(const double* red, const double* st, int d, int fit_i
   }
 }
 
-// One wave (64 threads): every operand is staged in LDS with parallel loads first (the
-// reduced 1088-double vector and the 256-double state), so no thread walks global memory
-// serially; reductions are wave-parallel, the Cholesky trailing update is spread over (i, j)
-// pairs, and the barriers of a single-wave workgroup are nearly free.
+// One wave (64 threads).  The kernel is latency-bound, so: all global loads (the reduced
+// 1088-double vector, the 256-double state, the done flag) are in flight together before the
+// first wait; reductions are wave-parallel; the Cholesky gives lane i row i (no integer
+// division, one fp64 reciprocal per column); the triangular solves keep b in lane registers
+// and broadcast with shuffles; barriers of a single-wave workgroup are nearly free.
 __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
                                                            double* __restrict__ st,
                                                            float* __restrict__ w32,
                                                            int* __restrict__ done, int d, double C,
                                                            double tol, int max_iter,
                                                            int fit_intercept) {
-  if (*done) return;
   __shared__ double sr[kLRPartStride];
   __shared__ double ss[kStateSize];
-  __shared__ double A[32][33];
-  __shared__ double b[32];
   __shared__ double grad[32];
   __shared__ int idx[32];
   const int t = threadIdx.x;
-  for (int i = t; i < kLRPartStride; i += 64) sr[i] = red[i];
-  for (int i = t; i < kStateSize; i += 64) ss[i] = st[i];
+  {
+    // Issue every global load before the first wait: 17 + 4 independent loads per lane plus
+    // the done flag, instead of a load -> wait -> ds_write chain per element.
+    constexpr int NR = kLRPartStride / 64, NS = kStateSize / 64;
+    const int dn = *done;
+    double v[NR], u[NS];
+#pragma unroll
+    for (int i = 0; i < NR; ++i) v[i] = red[t + 64 * i];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) u[i] = st[t + 64 * i];
+    if (dn) return;
+#pragma unroll
+    for (int i = 0; i < NR; ++i) sr[t + 64 * i] = v[i];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) ss[t + 64 * i] = u[i];
+  }
   __syncthreads();
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
   const double reg = 1.0 / (C * S);
+  const double invS = 1.0 / S;
   const int m = d + (fit_intercept ? 1 : 0);
-  if (t < 32) idx[t] = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
+  const int my = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
+  if (t < 32) idx[t] = my;
   build_grad(sr, ss, d, fit_intercept, reg, S, grad, t);
   __syncthreads();
   double w2 = (t < d) ? ss[kW + t] * ss[kW + t] : 0.0;
-  double ga = (t < m) ? fabs(grad[idx[t]]) : 0.0;
+  double ga = (t < m) ? fabs(grad[my]) : 0.0;
   w2 = wave_sum(w2);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) ga = fmax(ga, __shfl_xor(ga, o, kWave));
-  const double obj = sr[32] / S + 0.5 * reg * w2;
+  const double obj = sr[32] * invS + 0.5 * reg * w2;
   const double gmax = ga;
   const int it = (int)ss[kIter];
   const double prev = ss[kObjPrev];
@@ -308,41 +326,52 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     }
   } else {
     // H_active = H/S + reg I (penalised coords); solve H s = -grad by Cholesky (fp64).
-    for (int p = t; p < m * m; p += 64) {
-      const int i = p / m, k = p % m;
-      const int r = idx[i], c = idx[k];
-      double h = sr[64 + r * kCols + c] / S;
-      if (r == c && r < d) h += reg;
-      A[i][k] = h;
-    }
-    if (t < m) b[t] = -grad[idx[t]];
-    __syncthreads();
-    for (int k = 0; k < m; ++k) {
-      const double lkk = sqrt(fmax(A[k][k], 1e-300));
-      __syncthreads();
-      if (t == 0) A[k][k] = lkk;
-      if (t > k && t < m) A[t][k] /= lkk;
-      __syncthreads();
-      const int nt = m - k - 1;
-      for (int p = t; p < nt * nt; p += 64) {
-        const int i = k + 1 + p / nt, j = k + 1 + p % nt;
-        if (j <= i) A[i][j] -= A[i][k] * A[j][k];
+    // Lane i owns row i of A in registers (a[32], fully unrolled so every index is static);
+    // column k of L is broadcast with readlane, so the factorisation has no LDS traffic and
+    // no barriers.  Rows/columns >= m are identity-padded and never read back.
+    double a[32];
+    {
+      const double* hr = sr + 64 + (my >= 0 ? my : 0) * kCols;
+#pragma unroll
+      for (int k = 0; k < 32; ++k) {
+        double h = 0.0;
+        if (t < m && k < m) {
+          h = hr[idx[k]] * invS;
+          if (k == t && my < d) h += reg;
+        } else if (k == t) {
+          h = 1.0;
+        }
+        a[k] = h;
       }
-      __syncthreads();
     }
-    for (int k = 0; k < m; ++k) {  // L y = b
-      const double yk = b[k] / A[k][k];
-      __syncthreads();
-      if (t == 0) b[k] = yk;
-      if (t > k && t < m) b[t] -= A[t][k] * yk;
-      __syncthreads();
+    double bi = (t < m) ? -grad[my] : 0.0;
+    double dv[32];
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      if (k < m) {
+        const double lkk = sqrt(fmax(rdlane(a[k], k), 1e-300));
+        const double inv = 1.0 / lkk;
+        dv[k] = inv;
+        a[k] = (t == k) ? lkk : a[k] * inv;  // column k of L (rows t > k)
+#pragma unroll
+        for (int j = k + 1; j < 32; ++j) a[j] = fma(-a[k], rdlane(a[k], j), a[j]);
+      } else {
+        dv[k] = 0.0;
+      }
     }
-    for (int k = m - 1; k >= 0; --k) {  // L^T x = y
-      const double xk = b[k] / A[k][k];
-      __syncthreads();
-      if (t == 0) b[k] = xk;
-      if (t < k) b[t] -= A[k][t] * xk;
-      __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {  // L y = b (column sweep; b lives in lane registers)
+      if (k < m) {
+        const double yk = rdlane(bi, k) * dv[k];
+        bi = (t == k) ? yk : (t > k ? fma(-a[k], yk, bi) : bi);
+      }
+    }
+#pragma unroll
+    for (int k = 31; k >= 0; --k) {  // L^T x = y: x_k = (y_k - sum_{i>k} L[i][k] x_i) / L[k][k]
+      if (k < m) {
+        const double s = wave_sum((t > k && t < m) ? a[k] * bi : 0.0);
+        if (t == k) bi = (bi - s) * dv[k];
+      }
     }
     if (t < kCols) {
       ss[kWPrev + t] = ss[kW + t];
@@ -350,9 +379,8 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     }
     __syncthreads();
     if (t < m) {
-      const int j = idx[t];
-      ss[kStep + j] = b[t];
-      ss[kW + j] = ss[kWPrev + j] + b[t];
+      ss[kStep + my] = bi;
+      ss[kW + my] = ss[kWPrev + my] + bi;
     }
     if (t == 0) {
       ss[kObjPrev] = obj;
@@ -367,7 +395,8 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   }
   __syncthreads();
   if (t < kCols) w32[t] = (t == kLabelCol) ? 0.0f : (float)ss[kW + t];
-  for (int i = t; i < kStateSize; i += 64) st[i] = ss[i];
+#pragma unroll
+  for (int i = 0; i < kStateSize / 64; ++i) st[t + 64 * i] = ss[t + 64 * i];
 }
 
 // Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.

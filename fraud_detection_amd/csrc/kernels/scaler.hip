@@ -170,15 +170,30 @@ __global__ __launch_bounds__(kThreads) void scaler_partial_tiled_kernel(const fl
 }
 
 // Fixed-order reduction of [nblocks][64] fp64 partials into sums[64].
-__global__ __launch_bounds__(256) void scaler_reduce_kernel(const double* __restrict__ partial,
-                                                            int nblocks, double* __restrict__ sums) {
-  __shared__ double red[4][64];
+// 16 waves, each summing a strided subset of block partials with 8 independent accumulators
+// (eight loads in flight per lane instead of one dependent chain of nblocks/4 loads); the
+// summation tree is fixed by (nblocks, thread) only, so results are run-to-run deterministic.
+__global__ __launch_bounds__(1024) void scaler_reduce_kernel(const double* __restrict__ partial,
+                                                             int nblocks, double* __restrict__ sums) {
+  __shared__ double red[16][64];
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  double acc = 0.0;
-  for (int b = grp; b < nblocks; b += 4) acc += partial[(int64_t)b * 64 + e];
-  red[grp][e] = acc;
+  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int b = grp;
+  for (; b + 7 * 16 < nblocks; b += 8 * 16) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += partial[(int64_t)(b + u * 16) * 64 + e];
+  }
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (b + u * 16 < nblocks) acc[u] += partial[(int64_t)(b + u * 16) * 64 + e];
+  red[grp][e] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
-  if (threadIdx.x < 64) sums[e] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  if (threadIdx.x < 64) {
+    double s = 0.0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) s += red[g][e];
+    sums[e] = s;
+  }
 }
 
 // mean / var / scale from (possibly all-reduced) shifted sums.  One wave.
@@ -444,7 +459,7 @@ void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float
 }
 
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream) {
-  scaler_reduce_kernel<<<1, 256, 0, stream>>>(partial, nblocks, sums);
+  scaler_reduce_kernel<<<1, 1024, 0, stream>>>(partial, nblocks, sums);
   check_launch("scaler_reduce");
 }
 

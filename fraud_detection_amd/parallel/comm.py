@@ -45,10 +45,36 @@ class Communicator:
             self.backend = "single"
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self._native = None
-        if self.world_size > 1 and os.environ.get("FDX_COMM", "") == "rccl" and torch.cuda.is_available():
+        mode = os.environ.get("FDX_COMM", "auto")  # auto | rccl | torch
+        if self.world_size > 1 and self.backend == "nccl" and mode in ("auto", "rccl") and torch.cuda.is_available():
+            self._native = self._try_native(strict=(mode == "rccl"))
+
+    def _try_native(self, strict: bool):
+        """Bring up the native RCCL communicator and verify it with a known all-reduce; every
+        rank must pass, otherwise all ranks keep using the ProcessGroup (collective decision)."""
+        nat, ok = None, 1
+        try:
             from .rccl import NativeRCCL
 
-            self._native = NativeRCCL(self.rank, self.world_size, self.local_rank)
+            nat = NativeRCCL(self.rank, self.world_size, self.local_rank)
+            ok = int(nat.verify())
+        except Exception:  # noqa: BLE001
+            if strict:
+                raise
+            ok = 0
+        flag = torch.tensor([ok], dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 1:
+            return nat
+        if nat is not None:
+            nat.close()
+        if strict:
+            raise RuntimeError("native RCCL verification failed on some rank")
+        return None
+
+    @property
+    def native_rccl(self) -> bool:
+        return self._native is not None
 
     # ---- basic collectives -------------------------------------------------------------
     def barrier(self):

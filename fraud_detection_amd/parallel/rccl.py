@@ -1,0 +1,64 @@
+"""Python side of the native RCCL communicator (csrc/comm/rccl_comm.cpp).
+
+The unique id is created by rank 0 and shared through the default torch.distributed store, so
+the native communicator lives beside (not instead of) the ProcessGroup used for barriers and
+host-side collectives.  ``verify()`` runs a known all-reduce through the native path; callers
+(parallel/comm.py) fall back to the ProcessGroup if any rank fails it.
+"""
+from __future__ import annotations
+
+import importlib
+
+import torch
+import torch.distributed as dist
+
+_DT = {torch.float32: 0, torch.float64: 1, torch.int64: 2, torch.uint8: 3, torch.int32: 4, torch.bfloat16: 5}
+_OP = {"sum": 0, "max": 1, "min": 2}
+
+
+class NativeRCCL:
+    def __init__(self, rank: int, world_size: int, local_rank: int, key: str = "fdx_rccl_uid"):
+        self.lib = importlib.import_module("fraud_detection_amd._fdx_comm")
+        self.rank, self.world_size = rank, world_size
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            uid = self.lib.unique_id()
+            store.set(key, uid)
+        else:
+            store.wait([key])
+            uid = store.get(key)
+        torch.cuda.set_device(local_rank)
+        self.handle = self.lib.init_rank(bytes(uid), world_size, rank)
+
+    def _stream(self, t: torch.Tensor) -> int:
+        return torch.cuda.current_stream(t.device).cuda_stream
+
+    def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if not t.is_contiguous():
+            raise ValueError("native all_reduce needs a contiguous tensor")
+        self.lib.all_reduce(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), _DT[t.dtype], _OP[op], self._stream(t))
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        out = torch.empty((self.world_size,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.lib.all_gather(self.handle, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], self._stream(t))
+        return out
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        self.lib.broadcast(self.handle, t.data_ptr(), t.numel(), _DT[t.dtype], root, self._stream(t))
+        return t
+
+    def verify(self) -> bool:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        x = torch.full((1088,), float(self.rank + 1), dtype=torch.float64, device=dev)
+        self.all_reduce_(x)
+        torch.cuda.synchronize(dev)
+        expect = self.world_size * (self.world_size + 1) / 2.0
+        return bool(torch.all(x == expect).item())
+
+    def close(self):
+        if self.handle:
+            try:
+                self.lib.destroy(self.handle)
+            finally:
+                self.handle = 0
