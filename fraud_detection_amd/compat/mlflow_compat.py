@@ -130,6 +130,22 @@ class Run:
             shutil.copy2(src, os.path.join(d, name))
         return f"runs:/{self.run_id}/{artifact_path}"
 
+    def log_files_model(self, files: dict, artifact_path: str = "model", flavor: str = "fdx_gbdt",
+                        flavor_conf: dict | None = None, signature=None) -> str:
+        """A model stored as plain files (no pickle), e.g. the JSON tree ensemble."""
+        d = os.path.join(self.artifact_dir, artifact_path)
+        os.makedirs(d, exist_ok=True)
+        for name, src in files.items():
+            shutil.copy2(src, os.path.join(d, name))
+        mlmodel = {"artifact_path": artifact_path, "flavors": {flavor: dict(flavor_conf or {})},
+                   "model_uuid": uuid.uuid4().hex, "run_id": self.run_id,
+                   "utc_time_created": time.strftime("%Y-%m-%d %H:%M:%S", time.gmtime()),
+                   "written_by": "fraud_detection_amd"}
+        if signature is not None:
+            mlmodel["signature"] = signature
+        _write_yaml(os.path.join(d, "MLmodel"), mlmodel)
+        return f"runs:/{self.run_id}/{artifact_path}"
+
     def end(self, status: str = "FINISHED"):
         meta = os.path.join(self.dir, "meta.yaml")
         m = _read_yaml(meta)
@@ -311,6 +327,15 @@ def log_sklearn_model(model, artifact_path="model", signature=None, input_exampl
 
         return mlflow.sklearn.log_model(model, artifact_path, signature=signature, input_example=input_example)
     return _active().log_sklearn_model(model, artifact_path, signature, input_example, extra_files)
+
+
+def log_files_model(files: dict, artifact_path: str = "model", flavor: str = "fdx_gbdt", flavor_conf: dict | None = None,
+                    signature=None) -> str:
+    if _real_mlflow is not None:  # pragma: no cover
+        for src in files.values():
+            _real_mlflow.log_artifact(src, artifact_path)
+        return f"runs:/{_real_mlflow.active_run().info.run_id}/{artifact_path}"
+    return _active().log_files_model(files, artifact_path, flavor, flavor_conf, signature)
 
 
 def last_run_id() -> str | None:

@@ -135,6 +135,45 @@ PYBIND11_MODULE(_fdx_native, m) {
                            P<float>(phi), P<float>(fx), P<float>(f0), S(s));
   });
 
+  // gbdt (K11)
+  m.def("gbdt_bin", [](u X, int64_t n, int ld, int d, u cuts, u nbins, u bins, u s) {
+    fdx::launch_gbdt_bin(P<const float>(X), n, ld, d, P<const float>(cuts), P<const int>(nbins), P<uint8_t>(bins), S(s));
+  });
+  m.def("gbdt_grad", [](u margin, u label, int64_t n, float spw, float gscale, float hscale, u gh, u s) {
+    fdx::launch_gbdt_grad(P<const float>(margin), P<const uint8_t>(label), n, spw, gscale, hscale, P<int2>(gh), S(s));
+  });
+  m.def("gbdt_hist_blocks", [] { return fdx::gbdt_hist_blocks(); });
+  m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u s) {
+    fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const int2>(gh), P<const int>(ridx), P<const int64_t>(seg),
+                          P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), S(s));
+  });
+  m.def("gbdt_split", [](u hist, u gcnt, int level, int d, u nbins, u cuts, double ginv, double hinv, double lam,
+                         double mcw, double gamma, u feat, u bin, u thr, u gain, u ng, u nh, u s) {
+    fdx::launch_gbdt_split(P<unsigned long long>(hist), P<const int64_t>(gcnt), level, d, P<const int>(nbins),
+                           P<const float>(cuts), ginv, hinv, lam, mcw, gamma, P<int>(feat), P<int>(bin), P<float>(thr),
+                           P<double>(gain), P<long long>(ng), P<long long>(nh), S(s));
+  });
+  m.def("gbdt_partition", [](u bins, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u boff, int nblocks,
+                             u seg, u segR, u ridx_out, u nid_out, u s) {
+    fdx::launch_gbdt_partition(P<const uint8_t>(bins), P<const int>(ridx), P<const uint8_t>(nid), n, P<const int>(feat),
+                               P<const int>(bin), level, P<uint8_t>(flag), P<int64_t>(boff), nblocks, P<int64_t>(seg),
+                               P<int64_t>(segR), P<int>(ridx_out), P<uint8_t>(nid_out), S(s));
+  });
+  m.def("gbdt_leaf", [](u ng, u nh, int depth, double ginv, double hinv, double lam, double mcw, double eta, u leaf,
+                        u s) {
+    fdx::launch_gbdt_leaf(P<const long long>(ng), P<const long long>(nh), depth, ginv, hinv, lam, mcw, eta,
+                          P<float>(leaf), S(s));
+  });
+  m.def("gbdt_margin", [](u ridx, u nid, int64_t n, u leaf, int depth, u margin, u s) {
+    fdx::launch_gbdt_margin(P<const int>(ridx), P<const uint8_t>(nid), n, P<const float>(leaf), depth,
+                            P<float>(margin), S(s));
+  });
+  m.def("gbdt_predict", [](u X, int64_t n, int ld, int d, u feat, u thr, u leaf, int ntrees, int depth, float base,
+                           u out, u s) {
+    fdx::launch_gbdt_predict(P<const float>(X), n, ld, d, P<const int>(feat), P<const float>(thr), P<const float>(leaf),
+                             ntrees, depth, base, P<float>(out), S(s));
+  });
+
   // auc / confusion
   m.def("auc_compact", [](u scores, u labels, int64_t n, u pos, u counter, u s) {
     fdx::launch_auc_compact(P<const float>(scores), P<const uint8_t>(labels), n, P<float>(pos),

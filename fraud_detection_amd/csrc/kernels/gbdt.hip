@@ -1,0 +1,541 @@
+// K11 gbdt_*: histogram gradient-boosted trees (XGBoost "hist" semantics) on MI355X.
+//
+// Reference behaviour being replaced: XGBClassifier(objective='binary:logistic',
+// n_estimators=100, learning_rate=0.1, max_depth=5, scale_pos_weight=neg/pos) fitted in
+// train_model.py:69-80 (per CV fold) and :95-106 (final), SURVEY.md §2.3 row K11.
+//
+// Design (MI355X-first, not a port of xgboost's CPU/CUDA updaters):
+//  * Features are quantised once to u8 bins (<= 256 quantile cuts per feature; row = 32 bytes),
+//    so the per-level data stream is 32 B/row instead of 120 B of fp32.
+//  * Gradients/Hessians are quantised per boosting round to int32 fixed point (power-of-two
+//    scale) and histograms accumulate in int64: LDS atomics (ds_add_u64) then one global
+//    atomic flush per (block, node).  Integer addition is associative, so histograms -- and
+//    therefore every split decision -- are bitwise deterministic regardless of scheduling, the
+//    sibling histogram is an exact parent - child subtraction, and the data-parallel
+//    all-reduce of histograms over RCCL is exact too.
+//  * Rows stay node-partitioned (a permutation `ridx` with contiguous per-node segments, stable
+//    partition per level), so a histogram block touches only the rows of the nodes it builds.
+//    Only the smaller child of every split is histogrammed; the larger one is parent - sibling.
+//  * Trees are complete heaps of depth D: a node that does not split becomes a pass-through
+//    ("everything goes left", threshold +inf), so training and inference walk exactly D levels
+//    with no divergence on tree shape, and leaves sit at heap ids [2^D - 1, 2^(D+1) - 1).
+//  * Split search: one wave per feature, 4 bins per lane, int64 prefix scan, gain in fp64 with
+//    contraction disabled (the numpy oracle in ops/reference.py reproduces it bit-for-bit).
+//  * No host synchronisation inside a fit: segment sizes, build flags and leaf values stay on
+//    device, so a boosting round is a fixed launch sequence (hipGraph-capturable).
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kGBBins = 256;
+constexpr int kGBRowBytes = 32;
+constexpr int kGBMaxFeat = 30;
+constexpr int kHistEntries = kGBMaxFeat * kGBBins * 2;  // per node: [feature][bin][g, h]
+constexpr int kHistThreads = 1024;
+constexpr int kPartThreads = 256;
+
+__device__ __forceinline__ int heap_first(int level) { return (1 << level) - 1; }
+
+// Build flag of a node at level >= 1: the smaller child of each split (ties: the left one) is
+// histogrammed; its sibling is derived.  `gcnt` holds global (all-rank) row counts.
+__device__ __forceinline__ bool is_built(int node, const int64_t* gcnt) {
+  if (node == 0) return true;
+  const bool left = (node & 1) != 0;
+  const int sib = left ? node + 1 : node - 1;
+  const int64_t c = gcnt[node], s = gcnt[sib];
+  return left ? (c <= s) : (c < s);
+}
+
+// ---- quantisation ----------------------------------------------------------------------------
+// 8 lanes per row, 4 features per lane: the 8 lanes write one 32-byte binned row.
+__global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__ X, int64_t n, int ld,
+                                                       int d, const float* __restrict__ cuts,
+                                                       const int* __restrict__ nbins,
+                                                       uint8_t* __restrict__ bins) {
+  __shared__ float sc[kGBMaxFeat][kGBBins];
+  __shared__ int snb[32];
+  for (int i = threadIdx.x; i < d * kGBBins; i += blockDim.x) sc[i / kGBBins][i % kGBBins] = cuts[i];
+  if (threadIdx.x < 32) snb[threadIdx.x] = threadIdx.x < d ? nbins[threadIdx.x] : 1;
+  __syncthreads();
+  const int sub = threadIdx.x & 7;
+  const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 8);
+  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 8) + (threadIdx.x >> 3); r < n; r += stride) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = sub * 4 + j;
+      int b = 0;
+      if (f < d) {
+        const float x = X[r * ld + f];
+        int lo = 0, hi = snb[f] - 1;  // cuts[f][nb-1] = +inf: result in [0, nb-1]
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (sc[f][mid] > x) hi = mid;
+          else lo = mid + 1;
+        }
+        b = lo;
+      }
+      packed |= (uint32_t)b << (8 * j);
+    }
+    reinterpret_cast<uint32_t*>(bins + r * kGBRowBytes)[sub] = packed;
+  }
+}
+
+// ---- per-round gradients ---------------------------------------------------------------------
+// logistic: g = (p - y) w, h = max(p (1 - p), 1e-16) w, w = scale_pos_weight for positives.
+__global__ __launch_bounds__(256) void gbdt_grad_kernel(const float* __restrict__ margin,
+                                                        const uint8_t* __restrict__ label, int64_t n,
+                                                        float spw, float gscale, float hscale,
+                                                        int2* __restrict__ gh) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+    // fp64 so the quantised values match the numpy oracle except at measure-zero ties
+    const double m = (double)margin[i];
+    const double p = 1.0 / (1.0 + exp(-m));
+    const bool pos = label[i] != 0;
+    const double w = pos ? (double)spw : 1.0;
+    const double g = (p - (pos ? 1.0 : 0.0)) * w;
+    const double h = fmax(p * (1.0 - p), 1e-16) * w;
+    gh[i] = make_int2((int)rint(g * (double)gscale), (int)rint(h * (double)hscale));
+  }
+}
+
+// ---- histograms ------------------------------------------------------------------------------
+// Grid: resident blocks (1 per CU: 120 KiB of LDS).  The rows of this level's *built* nodes
+// are concatenated in node order into a virtual range that the grid splits evenly, so the work
+// per block is balanced whatever the segment sizes are.
+__global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
+    const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
+    const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
+    unsigned long long* __restrict__ hist) {
+  __shared__ unsigned long long sh[kHistEntries];  // 120 KiB
+  const int h0 = heap_first(level), nn = 1 << level;
+  int64_t total = 0;
+  for (int k = 0; k < nn; ++k)
+    if (is_built(h0 + k, gcnt)) total += seg[2 * (h0 + k) + 1];
+  const int64_t chunk = (total + gridDim.x - 1) / gridDim.x;
+  const int64_t vb = (int64_t)blockIdx.x * chunk;
+  const int64_t ve = min(vb + chunk, total);
+  if (vb >= ve) return;
+  const int nent = d * kGBBins * 2;
+  int64_t off = 0;
+  for (int k = 0; k < nn; ++k) {
+    const int node = h0 + k;
+    if (!is_built(node, gcnt)) continue;
+    const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
+    const int64_t lo = max(off, vb), hi = min(off + sc, ve);
+    off += sc;
+    if (lo >= hi) continue;
+    for (int i = threadIdx.x; i < nent; i += kHistThreads) sh[i] = 0ull;
+    __syncthreads();
+    for (int64_t v = lo + threadIdx.x; v < hi; v += kHistThreads) {
+      const int64_t p = sb + (v - (off - sc));
+      const int64_t row = ridx[p];
+      const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
+      const uint4 b0 = br[0], b1 = br[1];
+      const int2 q = gh[row];
+      const unsigned long long qg = (unsigned long long)(long long)q.x;
+      const unsigned long long qh = (unsigned long long)(long long)q.y;
+      const uint32_t words[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int f = 0; f < kGBMaxFeat; ++f) {
+        if (f < d) {
+          const int b = (words[f >> 2] >> (8 * (f & 3))) & 0xff;
+          unsigned long long* e = sh + (f * kGBBins + b) * 2;
+          atomicAdd(e, qg);
+          atomicAdd(e + 1, qh);
+        }
+      }
+    }
+    __syncthreads();
+    unsigned long long* dst = hist + (int64_t)node * kHistEntries;
+    for (int i = threadIdx.x; i < nent; i += kHistThreads) {
+      const unsigned long long x = sh[i];
+      if (x) atomicAdd(dst + i, x);
+    }
+    __syncthreads();
+  }
+}
+
+// ---- split search ----------------------------------------------------------------------------
+struct SplitOut {
+  int* feat;       // [heap]  -1: no split (pass-through)
+  int* bin;        // [heap]
+  float* thr;      // [heap]  cut value; rows with x < thr go left; +inf when not split
+  double* gain;    // [heap]
+  long long* cg;   // [heap]  node sums (int64 fixed point), written for the children
+  long long* ch;
+};
+
+__global__ __launch_bounds__(kHistThreads) void gbdt_split_kernel(
+    unsigned long long* __restrict__ hist, const int64_t* __restrict__ gcnt, int level, int d,
+    const int* __restrict__ nbins, const float* __restrict__ cuts, double ginv, double hinv,
+    double lambda, double min_child_weight, double gamma, int* __restrict__ tfeat,
+    int* __restrict__ tbin, float* __restrict__ tthr, double* __restrict__ tgain,
+    long long* __restrict__ ng, long long* __restrict__ nh) {
+#pragma clang fp contract(off)
+  const int node = heap_first(level) + blockIdx.x;
+  const int lane = lane_id(), wv = wave_id();
+  constexpr int kW = kHistThreads / kWave;
+  long long* H = reinterpret_cast<long long*>(hist) + (int64_t)node * kHistEntries;
+  const int nent = d * kGBBins * 2;
+  if (!is_built(node, gcnt)) {  // exact sibling subtraction: H = parent - built sibling
+    const int parent = (node - 1) >> 1;
+    const int sib = (node & 1) ? node + 1 : node - 1;
+    const long long* P = reinterpret_cast<long long*>(hist) + (int64_t)parent * kHistEntries;
+    const long long* S = reinterpret_cast<long long*>(hist) + (int64_t)sib * kHistEntries;
+    for (int i = threadIdx.x; i < nent; i += kHistThreads) H[i] = P[i] - S[i];
+    __syncthreads();
+  }
+  __shared__ double fgain[32];
+  __shared__ int fbin[32];
+  __shared__ long long fgl[32], fhl[32];
+  __shared__ long long tot[2];
+  for (int f = wv; f < d; f += kW) {
+    const long long* hf = H + f * kGBBins * 2;
+    long long g[4], h[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      g[j] = hf[(lane * 4 + j) * 2];
+      h[j] = hf[(lane * 4 + j) * 2 + 1];
+    }
+#pragma unroll
+    for (int j = 1; j < 4; ++j) { g[j] += g[j - 1]; h[j] += h[j - 1]; }
+    long long eg = g[3], eh = h[3];  // inclusive scan of lane totals
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const long long ug = __shfl_up(eg, o, kWave), uh = __shfl_up(eh, o, kWave);
+      if (lane >= o) { eg += ug; eh += uh; }
+    }
+    const long long Gq = __shfl(eg, 63, kWave), Hq = __shfl(eh, 63, kWave);
+    const long long pg = eg - g[3], ph = eh - h[3];  // exclusive prefix of this lane
+    const double G = (double)Gq * ginv, Hs = (double)Hq * hinv;
+    const double root = G * G / (Hs + lambda);
+    const int nb = nbins[f];
+    double best = -1.0e300;
+    int bb = 0x7fffffff;
+    long long bgl = 0, bhl = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int b = lane * 4 + j;
+      const long long GLq = pg + g[j], HLq = ph + h[j];
+      const double GL = (double)GLq * ginv, HL = (double)HLq * hinv;
+      const double GR = (double)(Gq - GLq) * ginv, HR = (double)(Hq - HLq) * hinv;
+      if (b < nb - 1 && HL >= min_child_weight && HR >= min_child_weight) {
+        const double gain = (GL * GL / (HL + lambda) + GR * GR / (HR + lambda)) - root;
+        if (gain > best) { best = gain; bb = b; bgl = GLq; bhl = HLq; }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {  // argmax, ties -> lowest bin
+      const double og = __shfl_xor(best, o, kWave);
+      const int ob = __shfl_xor(bb, o, kWave);
+      const long long ogl = __shfl_xor(bgl, o, kWave), ohl = __shfl_xor(bhl, o, kWave);
+      if (og > best || (og == best && ob < bb)) { best = og; bb = ob; bgl = ogl; bhl = ohl; }
+    }
+    if (lane == 0) {
+      fgain[f] = best;
+      fbin[f] = bb;
+      fgl[f] = bgl;
+      fhl[f] = bhl;
+      if (f == 0) { tot[0] = Gq; tot[1] = Hq; }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double best = -1.0e300;
+    int bf = -1;
+    for (int f = 0; f < d; ++f)  // ties -> lowest feature
+      if (fgain[f] > best) { best = fgain[f]; bf = f; }
+    const long long Gq = tot[0], Hq = tot[1];
+    // xgboost: a split needs loss_chg > kRtEps (1e-6) and is pruned when loss_chg < gamma
+    const bool split = bf >= 0 && best > 1e-6 && !(best < gamma);
+    const int l = 2 * node + 1, r = 2 * node + 2;
+    if (split) {
+      tfeat[node] = bf;
+      tbin[node] = fbin[bf];
+      tthr[node] = cuts[bf * kGBBins + fbin[bf]];
+      tgain[node] = best;
+      ng[l] = fgl[bf]; nh[l] = fhl[bf];
+      ng[r] = Gq - fgl[bf]; nh[r] = Hq - fhl[bf];
+    } else {
+      tfeat[node] = -1;
+      tbin[node] = 255;
+      tthr[node] = __builtin_inff();
+      tgain[node] = 0.0;
+      ng[l] = Gq; nh[l] = Hq;
+      ng[r] = 0; nh[r] = 0;
+    }
+    if (node == 0) { ng[0] = Gq; nh[0] = Hq; }
+  }
+}
+
+// ---- stable partition of every node segment --------------------------------------------------
+__device__ __forceinline__ void part_range(int64_t n, int64_t* lo, int64_t* hi) {
+  const int64_t per = (n + gridDim.x - 1) / gridDim.x;
+  *lo = min((int64_t)blockIdx.x * per, n);
+  *hi = min(*lo + per, n);
+}
+
+__device__ __forceinline__ bool goes_right(const uint8_t* bins, int64_t row, int node,
+                                           const int* feat, const int* bin) {
+  const int f = feat[node];
+  return f >= 0 && bins[row * kGBRowBytes + f] > bin[node];
+}
+
+__global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
+    const uint8_t* __restrict__ bins, const int* __restrict__ ridx, const uint8_t* __restrict__ nid,
+    int64_t n, const int* __restrict__ feat, const int* __restrict__ bin,
+    uint8_t* __restrict__ flag, int64_t* __restrict__ counts) {
+  int64_t lo, hi;
+  part_range(n, &lo, &hi);
+  int64_t c = 0;
+  for (int64_t p = lo + threadIdx.x; p < hi; p += kPartThreads) {
+    const bool r = goes_right(bins, ridx[p], nid[p], feat, bin);
+    flag[p] = r;
+    c += r;
+  }
+  c = wave_sum(c);
+  __shared__ int64_t red[kPartThreads / kWave];
+  if (lane_id() == 0) red[wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < kPartThreads / kWave; ++w) t += red[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+// Rights before position p (global exclusive prefix of flags), from the scanned block offsets.
+__device__ int64_t rights_before(const uint8_t* flag, const int64_t* boff, int64_t n, int nblocks,
+                                 int64_t p) {
+  const int64_t per = (n + nblocks - 1) / nblocks;
+  if (p >= n) return boff[nblocks];  // boff[nblocks] holds the total
+  const int blk = (int)(p / per);
+  int64_t c = 0;
+  for (int64_t q = (int64_t)blk * per + lane_id(); q < p; q += kWave) c += flag[q];
+  return boff[blk] + wave_sum(c);
+}
+
+// One wave per node of the level: child segments of the next level.
+__global__ __launch_bounds__(kWave) void gbdt_seg_kernel(const uint8_t* __restrict__ flag,
+                                                         const int64_t* __restrict__ boff, int64_t n,
+                                                         int nblocks, int level,
+                                                         int64_t* __restrict__ seg,
+                                                         int64_t* __restrict__ segR) {
+  const int node = heap_first(level) + blockIdx.x;
+  const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
+  const int64_t r0 = rights_before(flag, boff, n, nblocks, sb);
+  const int64_t r1 = rights_before(flag, boff, n, nblocks, sb + sc);
+  if (lane_id() == 0) {
+    const int64_t nr = r1 - r0;
+    segR[node] = r0;
+    seg[2 * (2 * node + 1)] = sb;
+    seg[2 * (2 * node + 1) + 1] = sc - nr;
+    seg[2 * (2 * node + 2)] = sb + sc - nr;
+    seg[2 * (2 * node + 2) + 1] = nr;
+  }
+}
+
+__global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
+    const uint8_t* __restrict__ flag, const int64_t* __restrict__ boff, const int* __restrict__ ridx,
+    const uint8_t* __restrict__ nid, int64_t n, const int64_t* __restrict__ seg,
+    const int64_t* __restrict__ segR, int* __restrict__ ridx_out, uint8_t* __restrict__ nid_out) {
+  int64_t lo, hi;
+  part_range(n, &lo, &hi);
+  __shared__ int64_t wave_cnt[kPartThreads / kWave];
+  int64_t base = boff[blockIdx.x];
+  const int lane = lane_id(), w = wave_id();
+  for (int64_t p0 = lo; p0 < hi; p0 += kPartThreads) {
+    const int64_t p = p0 + threadIdx.x;
+    const bool ok = p < hi;
+    const bool r = ok && flag[p];
+    const unsigned long long m = __ballot(r);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) wave_cnt[w] = __popcll(m);
+    __syncthreads();
+    int64_t R = base;  // global rights before p
+    for (int i = 0; i < w; ++i) R += wave_cnt[i];
+    R += before;
+    if (ok) {
+      const int node = nid[p];
+      const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
+      const int64_t rin = R - segR[node];  // rights before p inside the segment
+      const int64_t nr = seg[2 * (2 * node + 2) + 1];
+      int64_t dst;
+      uint8_t child;
+      if (r) { dst = sb + (sc - nr) + rin; child = (uint8_t)(2 * node + 2); }
+      else { dst = sb + (p - sb) - rin; child = (uint8_t)(2 * node + 1); }
+      ridx_out[dst] = ridx[p];
+      nid_out[dst] = child;
+    }
+    int64_t total = 0;
+    for (int i = 0; i < kPartThreads / kWave; ++i) total += wave_cnt[i];
+    base += total;
+    __syncthreads();
+  }
+}
+
+// ---- leaves ----------------------------------------------------------------------------------
+// xgboost CalcWeight: 0 if H < min_child_weight or H <= 0, else -G / (H + lambda); the stored
+// leaf value is eta * weight.
+__global__ void gbdt_leaf_kernel(const long long* __restrict__ ng, const long long* __restrict__ nh,
+                                 int depth, double ginv, double hinv, double lambda,
+                                 double min_child_weight, double eta, float* __restrict__ leaf) {
+#pragma clang fp contract(off)
+  const int nl = 1 << depth;
+  for (int i = threadIdx.x; i < nl; i += blockDim.x) {
+    const int node = heap_first(depth) + i;
+    const double G = (double)ng[node] * ginv, H = (double)nh[node] * hinv;
+    double w = 0.0;
+    if (!(H < min_child_weight || H <= 0.0)) w = -G / (H + lambda);
+    leaf[i] = (float)(eta * w);
+  }
+}
+
+__global__ __launch_bounds__(256) void gbdt_margin_kernel(const int* __restrict__ ridx,
+                                                          const uint8_t* __restrict__ nid, int64_t n,
+                                                          const float* __restrict__ leaf, int depth,
+                                                          float* __restrict__ margin) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int base = heap_first(depth);
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += stride)
+    margin[ridx[p]] += leaf[nid[p] - base];
+}
+
+// ---- inference on fp32 rows ------------------------------------------------------------------
+// One thread per row; the row sits in LDS (dynamic feature index without scratch), the trees of
+// the current chunk in LDS; every row walks exactly `depth` levels per tree.
+constexpr int kPredThreads = 256;
+constexpr int kPredLdsFloats = 12288;  // 48 KiB of trees per chunk
+
+__global__ __launch_bounds__(kPredThreads) void gbdt_predict_kernel(
+    const float* __restrict__ X, int64_t n, int ld, int d, const int* __restrict__ feat,
+    const float* __restrict__ thr, const float* __restrict__ leaf, int ntrees, int depth,
+    float base_margin, float* __restrict__ out) {
+  __shared__ float xr[kPredThreads][kGBMaxFeat + 1];
+  __shared__ float tl[kPredLdsFloats];
+  const int ni = (1 << depth) - 1, nl = 1 << depth;
+  const int per_tree = 2 * ni + nl;
+  const int chunk = kPredLdsFloats / per_tree;
+  const int64_t r = (int64_t)blockIdx.x * kPredThreads + threadIdx.x;
+  const bool ok = r < n;
+  for (int j = 0; j < d; ++j) xr[threadIdx.x][j] = ok ? X[r * ld + j] : 0.0f;
+  float acc = base_margin;
+  for (int t0 = 0; t0 < ntrees; t0 += chunk) {
+    const int nt = min(chunk, ntrees - t0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nt * ni; i += kPredThreads) {
+      const int t = i / ni, k = i % ni;
+      tl[t * per_tree + k] = __int_as_float(feat[(int64_t)(t0 + t) * ni + k]);
+      tl[t * per_tree + ni + k] = thr[(int64_t)(t0 + t) * ni + k];
+    }
+    for (int i = threadIdx.x; i < nt * nl; i += kPredThreads) {
+      const int t = i / nl, k = i % nl;
+      tl[t * per_tree + 2 * ni + k] = leaf[(int64_t)(t0 + t) * nl + k];
+    }
+    __syncthreads();
+    for (int t = 0; t < nt; ++t) {
+      const float* T = tl + t * per_tree;
+      int node = 0;
+      for (int l = 0; l < depth; ++l) {
+        const int f = __float_as_int(T[node]);
+        const bool right = f >= 0 && !(xr[threadIdx.x][f] < T[ni + node]);
+        node = 2 * node + 1 + (right ? 1 : 0);
+      }
+      acc += T[2 * ni + node - ni];
+    }
+  }
+  if (ok) out[r] = acc;
+}
+
+}  // namespace
+
+void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,
+                     uint8_t* bins, hipStream_t stream) {
+  if (d > kGBMaxFeat) throw std::runtime_error("gbdt: at most 30 features");
+  const int grid = stream_grid(n, 256 / 8, 4096);
+  gbdt_bin_kernel<<<grid, 256, 0, stream>>>(X, n, ld, d, cuts, nbins, bins);
+  check_launch("gbdt_bin");
+}
+
+void launch_gbdt_grad(const float* margin, const uint8_t* label, int64_t n, float spw, float gscale,
+                      float hscale, int2* gh, hipStream_t stream) {
+  const int grid = stream_grid(n, 256, 4096);
+  gbdt_grad_kernel<<<grid, 256, 0, stream>>>(margin, label, n, spw, gscale, hscale, gh);
+  check_launch("gbdt_grad");
+}
+
+int gbdt_hist_blocks() {
+  static int cached = 0;
+  if (cached) return cached;
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+  }
+  cached = cus;  // 120 KiB of LDS per block: one resident block per CU
+  return cached;
+}
+
+void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
+                      const int64_t* gcnt, int level, int d, unsigned long long* hist,
+                      hipStream_t stream) {
+  gbdt_hist_kernel<<<gbdt_hist_blocks(), kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d,
+                                                                     hist);
+  check_launch("gbdt_hist");
+}
+
+void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
+                       const float* cuts, double ginv, double hinv, double lambda,
+                       double min_child_weight, double gamma, int* feat, int* bin, float* thr,
+                       double* gain, long long* ng, long long* nh, hipStream_t stream) {
+  gbdt_split_kernel<<<1 << level, kHistThreads, 0, stream>>>(hist, gcnt, level, d, nbins, cuts, ginv, hinv,
+                                                             lambda, min_child_weight, gamma, feat, bin,
+                                                             thr, gain, ng, nh);
+  check_launch("gbdt_split");
+}
+
+void launch_gbdt_partition(const uint8_t* bins, const int* ridx, const uint8_t* nid, int64_t n,
+                           const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
+                           int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
+                           hipStream_t stream) {
+  if (nblocks > 4096) throw std::runtime_error("gbdt: at most 4096 partition blocks");
+  gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(bins, ridx, nid, n, feat, bin, flag, boff);
+  check_launch("gbdt_part_count");
+  launch_exclusive_scan_small(boff, nblocks, boff + nblocks, stream);
+  gbdt_seg_kernel<<<1 << level, kWave, 0, stream>>>(flag, boff, n, nblocks, level, seg, segR);
+  check_launch("gbdt_seg");
+  gbdt_part_scatter_kernel<<<nblocks, kPartThreads, 0, stream>>>(flag, boff, ridx, nid, n, seg, segR,
+                                                                 ridx_out, nid_out);
+  check_launch("gbdt_part_scatter");
+}
+
+void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,
+                      double lambda, double min_child_weight, double eta, float* leaf, hipStream_t stream) {
+  gbdt_leaf_kernel<<<1, 256, 0, stream>>>(ng, nh, depth, ginv, hinv, lambda, min_child_weight, eta, leaf);
+  check_launch("gbdt_leaf");
+}
+
+void launch_gbdt_margin(const int* ridx, const uint8_t* nid, int64_t n, const float* leaf, int depth,
+                        float* margin, hipStream_t stream) {
+  const int grid = stream_grid(n, 256, 4096);
+  gbdt_margin_kernel<<<grid, 256, 0, stream>>>(ridx, nid, n, leaf, depth, margin);
+  check_launch("gbdt_margin");
+}
+
+void launch_gbdt_predict(const float* X, int64_t n, int ld, int d, const int* feat, const float* thr,
+                         const float* leaf, int ntrees, int depth, float base_margin, float* out,
+                         hipStream_t stream) {
+  if (depth < 1 || depth > 8) throw std::runtime_error("gbdt: depth must be in [1, 8]");
+  if (d > kGBMaxFeat) throw std::runtime_error("gbdt: at most 30 features");
+  const int64_t grid = (n + kPredThreads - 1) / kPredThreads;
+  if (grid == 0) return;
+  gbdt_predict_kernel<<<(unsigned)grid, kPredThreads, 0, stream>>>(X, n, ld, d, feat, thr, leaf, ntrees, depth,
+                                                                   base_margin, out);
+  check_launch("gbdt_predict");
+}
+
+}  // namespace fdx

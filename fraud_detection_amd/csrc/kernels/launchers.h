@@ -94,4 +94,28 @@ void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float 
                        const float* Az, int link, float* phi, float* fx_out, float* f0_out,
                        hipStream_t stream);
 
+// ---- K11 gbdt (gbdt.hip) ----
+void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,
+                     uint8_t* bins, hipStream_t stream);
+void launch_gbdt_grad(const float* margin, const uint8_t* label, int64_t n, float spw, float gscale,
+                      float hscale, int2* gh, hipStream_t stream);
+int gbdt_hist_blocks();
+void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
+                      const int64_t* gcnt, int level, int d, unsigned long long* hist, hipStream_t stream);
+void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
+                       const float* cuts, double ginv, double hinv, double lambda,
+                       double min_child_weight, double gamma, int* feat, int* bin, float* thr,
+                       double* gain, long long* ng, long long* nh, hipStream_t stream);
+void launch_gbdt_partition(const uint8_t* bins, const int* ridx, const uint8_t* nid, int64_t n,
+                           const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
+                           int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
+                           hipStream_t stream);
+void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,
+                      double lambda, double min_child_weight, double eta, float* leaf, hipStream_t stream);
+void launch_gbdt_margin(const int* ridx, const uint8_t* nid, int64_t n, const float* leaf, int depth,
+                        float* margin, hipStream_t stream);
+void launch_gbdt_predict(const float* X, int64_t n, int ld, int d, const int* feat, const float* thr,
+                         const float* leaf, int ntrees, int depth, float base_margin, float* out,
+                         hipStream_t stream);
+
 }  // namespace fdx

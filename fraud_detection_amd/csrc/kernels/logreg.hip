@@ -266,6 +266,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   __shared__ double sr[kLRPartStride];
   __shared__ double ss[kStateSize];
   __shared__ double grad[32];
+  __shared__ double Lc[32][33];
   __shared__ int idx[32];
   const int t = threadIdx.x;
   {
@@ -345,16 +346,24 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       }
     }
     double bi = (t < m) ? -grad[my] : 0.0;
+    // Column k of L, once computed, goes to LDS (Lc[k][j] = L[j][k]); the trailing update then
+    // reads it with uniform-address (broadcast) LDS loads instead of one readlane pair + hazard
+    // nops per element.  1/sqrt via v_rsq_f64 + two Newton refinements (no div/sqrt sequences).
     double dv[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
       if (k < m) {
-        const double lkk = sqrt(fmax(rdlane(a[k], k), 1e-300));
-        const double inv = 1.0 / lkk;
+        const double akk = fmax(rdlane(a[k], k), 1e-300);
+        double inv = __builtin_amdgcn_rsq(akk);
+        inv = inv * fma(-0.5 * akk * inv, inv, 1.5);
+        inv = inv * fma(-0.5 * akk * inv, inv, 1.5);
         dv[k] = inv;
-        a[k] = (t == k) ? lkk : a[k] * inv;  // column k of L (rows t > k)
+        const double ak = (t == k) ? akk * inv : a[k] * inv;  // column k of L (rows t > k)
+        a[k] = ak;
+        if (t < 32) Lc[k][t] = ak;
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = k + 1; j < 32; ++j) a[j] = fma(-a[k], rdlane(a[k], j), a[j]);
+        for (int j = k + 1; j < 32; ++j) a[j] = fma(-ak, Lc[k][j], a[j]);
       } else {
         dv[k] = 0.0;
       }
@@ -367,10 +376,11 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       }
     }
 #pragma unroll
-    for (int k = 31; k >= 0; --k) {  // L^T x = y: x_k = (y_k - sum_{i>k} L[i][k] x_i) / L[k][k]
+    for (int k = 31; k >= 0; --k) {  // L^T x = y (column sweep): lane t < k needs L[k][t] = Lc[t][k]
       if (k < m) {
-        const double s = wave_sum((t > k && t < m) ? a[k] * bi : 0.0);
-        if (t == k) bi = (bi - s) * dv[k];
+        const double xk = rdlane(bi, k) * dv[k];
+        const double lkt = (t < k) ? Lc[t][k] : 0.0;
+        bi = (t == k) ? xk : (t < k ? fma(-lkt, xk, bi) : bi);
       }
     }
     if (t < kCols) {

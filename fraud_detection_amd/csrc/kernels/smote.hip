@@ -19,7 +19,7 @@ namespace {
 
 constexpr int kThreads = 256;
 
-template <int OUT>  // 0 = bf16 rows (64 B), 2 = fp8 e4m3 rows (32 B)
+template <int OUT>  // 0 = bf16 rows (64 B), 1 = fp32 rows (128 B, GBDT input), 2 = fp8 e4m3 rows (32 B)
 __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     const float* __restrict__ C, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
     int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
@@ -70,6 +70,10 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
         pk.z = pack_bf16x2(o[4], o[5]);
         pk.w = pack_bf16x2(o[6], o[7]);
         reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
+      } else if constexpr (OUT == 1) {
+        float4* dst = reinterpret_cast<float4*>(out) + s * 8 + 2 * q;
+        dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+        dst[1] = make_float4(o[4], o[5], o[6], o[7]);
       } else {
         uint2 pk = make_uint2(0, 0);
 #pragma unroll
@@ -96,6 +100,9 @@ void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
   if (out_kind == 0)
     smote_generate_kernel<0><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
+                                                           c0, c1, label, out_scale, out);
+  else if (out_kind == 1)
+    smote_generate_kernel<1><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
                                                            c0, c1, label, out_scale, out);
   else
     smote_generate_kernel<2><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,

@@ -1,0 +1,282 @@
+"""K11 GBDT ops: quantile binning, boosting rounds and inference (csrc/kernels/gbdt.hip).
+
+Device path: one boosting round = gradient kernel -> per level (histogram, [RCCL all-reduce of the
+int64 histograms and child counts under DP], split, stable partition) -> leaf values -> margin
+update.  Nothing in a round synchronises with the host.  CPU tensors run the numpy oracle
+(ops/reference_gbdt.py), which builds the same trees from the same quantised gradients.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from . import reference_gbdt as R
+from .native import native, ptr, stream_of
+
+MAX_BIN = R.MAX_BIN
+MAX_FEAT = 30
+HIST_ENTRIES = MAX_FEAT * MAX_BIN * 2
+PART_BLOCKS = 1024
+
+
+@dataclass
+class GBDTParams:
+    """xgboost.XGBClassifier parameter names and defaults used by train_model.py:69-80."""
+    n_estimators: int = 100
+    learning_rate: float = 0.1
+    max_depth: int = 5
+    reg_lambda: float = 1.0
+    min_child_weight: float = 1.0
+    gamma: float = 0.0
+    max_bin: int = 256
+    scale_pos_weight: float = 1.0
+    base_score: float = 0.5
+    cut_sample_rows: int = 1 << 20
+
+    def validate(self):
+        if not 1 <= self.max_depth <= 7:
+            raise ValueError("max_depth must be in [1, 7] (node ids are stored in one byte)")
+        if not 2 <= self.max_bin <= MAX_BIN:
+            raise ValueError("max_bin must be in [2, 256]")
+        if not 0.0 < self.base_score < 1.0:
+            raise ValueError("base_score must be in (0, 1)")
+        if self.n_estimators < 0 or self.learning_rate <= 0:
+            raise ValueError("bad n_estimators / learning_rate")
+        return self
+
+
+@dataclass
+class TreeEnsemble:
+    depth: int
+    feat: np.ndarray   # [T, 2^D - 1] int32 (-1 = pass-through)
+    bin: np.ndarray    # [T, 2^D - 1] int32
+    thr: np.ndarray    # [T, 2^D - 1] float32
+    gain: np.ndarray   # [T, 2^D - 1] float64
+    leaf: np.ndarray   # [T, 2^D] float32
+    cuts: np.ndarray   # [d, 256] float32
+    nbins: np.ndarray  # [d] int32
+    base_score: float = 0.5
+    params: dict = field(default_factory=dict)
+
+    @property
+    def n_trees(self) -> int:
+        return int(self.feat.shape[0])
+
+    @property
+    def n_features(self) -> int:
+        return int(self.nbins.shape[0])
+
+    @property
+    def base_margin(self) -> float:
+        return float(np.log(self.base_score / (1.0 - self.base_score)))
+
+    def feature_importance(self, kind: str = "gain") -> np.ndarray:
+        """xgboost-style importances: "gain" (mean gain per split) or "weight" (split count)."""
+        d = self.n_features
+        cnt = np.zeros(d)
+        tot = np.zeros(d)
+        m = self.feat >= 0
+        np.add.at(cnt, self.feat[m], 1.0)
+        np.add.at(tot, self.feat[m], self.gain[m])
+        if kind == "weight":
+            return cnt
+        return np.where(cnt > 0, tot / np.maximum(cnt, 1), 0.0)
+
+    def to_dict(self) -> dict:
+        return {"format": "fdx-gbdt/1", "depth": self.depth, "base_score": self.base_score,
+                "params": self.params, "feat": self.feat.tolist(), "bin": self.bin.tolist(),
+                "thr": [[float(v) if np.isfinite(v) else "inf" for v in row] for row in self.thr],
+                "gain": self.gain.tolist(), "leaf": self.leaf.tolist(),
+                "cuts": [[float(v) if np.isfinite(v) else "inf" for v in row[:nb]] for row, nb in zip(self.cuts, self.nbins)],
+                "nbins": self.nbins.tolist()}
+
+    @classmethod
+    def from_dict(cls, o: dict) -> "TreeEnsemble":
+        if o.get("format") != "fdx-gbdt/1":
+            raise ValueError("not an fdx-gbdt/1 model")
+        f = lambda v: np.inf if v == "inf" else float(v)  # noqa: E731
+        depth = int(o["depth"])
+        ni = (1 << depth) - 1
+        nbins = np.asarray(o["nbins"], np.int32)
+        cuts = np.full((len(nbins), MAX_BIN), np.inf, np.float32)
+        for i, row in enumerate(o["cuts"]):
+            cuts[i, : len(row)] = [f(v) for v in row]
+        feat = np.asarray(o["feat"], np.int32).reshape(-1, ni)
+        return cls(depth=depth, feat=feat, bin=np.asarray(o["bin"], np.int32).reshape(-1, ni),
+                   thr=np.asarray([[f(v) for v in row] for row in o["thr"]], np.float32).reshape(-1, ni),
+                   gain=np.asarray(o["gain"], np.float64).reshape(-1, ni),
+                   leaf=np.asarray(o["leaf"], np.float32).reshape(-1, 1 << depth), cuts=cuts, nbins=nbins,
+                   base_score=float(o["base_score"]), params=dict(o.get("params", {})))
+
+
+# ---- binning ---------------------------------------------------------------------------------
+def quantile_cuts(X: torch.Tensor, max_bin: int = MAX_BIN, sample_rows: int = 1 << 20, comm=None):
+    """Per-feature quantile cuts from a deterministic strided row sample.  Under DP every rank
+    contributes a sample and the cuts come from the gathered sample, so all ranks agree."""
+    n, d = X.shape
+    if d > MAX_FEAT:
+        raise ValueError(f"at most {MAX_FEAT} features")
+    world = comm.world_size if comm is not None else 1
+    per = max(1, sample_rows // world)
+    stride = max(1, n // per)
+    samp = X[::stride][:per].contiguous()
+    if comm is not None and world > 1:
+        samp, _ = comm.all_gather_rows(samp)
+    return R.quantile_cuts(samp.float().cpu().numpy(), max_bin)
+
+
+def bin_rows(X: torch.Tensor, cuts: np.ndarray, nbins: np.ndarray) -> torch.Tensor:
+    """u8 [n, 32] bins (features in bytes 0..d-1)."""
+    n, d = X.shape
+    if not X.is_cuda:
+        return torch.from_numpy(R.bin_rows(X.numpy(), cuts, nbins))
+    if X.dtype != torch.float32 or X.stride(1) != 1:
+        raise ValueError("X must be float32 with unit column stride")
+    m = native()
+    out = torch.empty((n, R.ROW_BYTES), dtype=torch.uint8, device=X.device)
+    ct = torch.from_numpy(np.ascontiguousarray(cuts[:d])).to(X.device)
+    nt = torch.from_numpy(np.ascontiguousarray(nbins[:d])).to(X.device)
+    if n:
+        m.gbdt_bin(ptr(X), n, X.stride(0), d, ptr(ct), ptr(nt), ptr(out), stream_of(X))
+    return out
+
+
+# ---- training --------------------------------------------------------------------------------
+class _Workspace:
+    def __init__(self, n: int, depth: int, dev: torch.device):
+        nheap = (2 << depth) - 1
+        self.gh = torch.empty((n, 2), dtype=torch.int32, device=dev)
+        self.ridx = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.nid = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        self.flag = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+        self.boff = torch.empty(PART_BLOCKS + 1, dtype=torch.int64, device=dev)
+        self.seg = torch.zeros((nheap, 2), dtype=torch.int64, device=dev)
+        self.segR = torch.zeros(nheap, dtype=torch.int64, device=dev)
+        self.gcnt = torch.zeros(nheap, dtype=torch.int64, device=dev)
+        self.hist = torch.zeros(((1 << depth) - 1) * HIST_ENTRIES, dtype=torch.int64, device=dev)
+        self.ng = torch.zeros(nheap, dtype=torch.int64, device=dev)
+        self.nh = torch.zeros(nheap, dtype=torch.int64, device=dev)
+        self.iota = torch.arange(n, dtype=torch.int32, device=dev)
+
+
+def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm=None,
+        cuts=None, sample_weight_pos: float | None = None, return_margin: bool = False):
+    """Boost `n_estimators` depth-D trees on standardized float32 rows X [n, d] with labels y."""
+    p = (params or GBDTParams()).validate()
+    n, d = X.shape
+    if d > MAX_FEAT:
+        raise ValueError(f"at most {MAX_FEAT} features")
+    if y.dtype != torch.uint8 or y.shape[0] != n:
+        raise ValueError("y must be uint8 [n]")
+    if cuts is None:
+        cuts = quantile_cuts(X, p.max_bin, p.cut_sample_rows, comm)
+    cuts_np, nbins = cuts
+    spw = float(p.scale_pos_weight if sample_weight_pos is None else sample_weight_pos)
+    gscale, hscale = R.grad_scales(spw)
+    D = p.max_depth
+    ni, nl = (1 << D) - 1, 1 << D
+    T = p.n_estimators
+    base_margin = float(np.log(p.base_score / (1.0 - p.base_score)))
+    bins = bin_rows(X, cuts_np, nbins)
+    ens_kw = dict(depth=D, cuts=cuts_np, nbins=nbins, base_score=p.base_score, params=dict(p.__dict__))
+    if not X.is_cuda:
+        feat = np.zeros((T, ni), np.int32); binv = np.zeros((T, ni), np.int32)
+        thr = np.zeros((T, ni), np.float32); gain = np.zeros((T, ni)); leaf = np.zeros((T, nl), np.float32)
+        b = bins.numpy()
+        yy = y.numpy()
+        margin = np.full(n, np.float32(base_margin), np.float32)
+        for t in range(T):
+            q = R.gradients(margin, yy, spw, gscale, hscale)
+            tr, node = R.build_tree(b, q, cuts_np, nbins, D, p.reg_lambda, p.min_child_weight, p.gamma,
+                                    p.learning_rate, gscale, hscale, comm)
+            feat[t], binv[t], thr[t], gain[t], leaf[t] = tr.feat, tr.bin, tr.thr, tr.gain, tr.leaf
+            margin = (margin + tr.leaf[node]).astype(np.float32)
+        ens = TreeEnsemble(feat=feat, bin=binv, thr=thr, gain=gain, leaf=leaf, **ens_kw)
+        return (ens, torch.from_numpy(margin)) if return_margin else ens
+
+    m = native()
+    dev = X.device
+    s = stream_of(X)
+    ws = _Workspace(n, D, dev)
+    dist = comm is not None and comm.world_size > 1
+    n_global = int(comm.all_reduce_scalar(float(n))) if dist else n
+    ct = torch.from_numpy(np.ascontiguousarray(cuts_np[:d])).to(dev)
+    nt = torch.from_numpy(np.ascontiguousarray(nbins[:d])).to(dev)
+    feat = torch.empty((T, ni), dtype=torch.int32, device=dev)
+    binv = torch.empty((T, ni), dtype=torch.int32, device=dev)
+    thr = torch.empty((T, ni), dtype=torch.float32, device=dev)
+    gain = torch.empty((T, ni), dtype=torch.float64, device=dev)
+    leaf = torch.empty((T, nl), dtype=torch.float32, device=dev)
+    margin = torch.full((n,), base_margin, dtype=torch.float32, device=dev)
+    root = torch.tensor([[0, n]], dtype=torch.int64, device=dev)
+    groot = torch.tensor([n_global], dtype=torch.int64, device=dev)
+    lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
+    ginv, hinv = 1.0 / gscale, 1.0 / hscale
+    for t in range(T):
+        m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), s)
+        ws.hist.zero_()
+        ws.seg[0:1].copy_(root)
+        ws.gcnt[0:1].copy_(groot)
+        cur = 0
+        ws.ridx[0].copy_(ws.iota)
+        ws.nid[0].zero_()
+        for level in range(D):
+            h0, nn = (1 << level) - 1, 1 << level
+            m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
+                        ptr(ws.hist), s)
+            if dist:
+                comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
+            m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,
+                         ptr(feat[t]), ptr(binv[t]), ptr(thr[t]), ptr(gain[t]), ptr(ws.ng), ptr(ws.nh), s)
+            if n:
+                m.gbdt_partition(ptr(bins), ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(feat[t]), ptr(binv[t]),
+                                 level, ptr(ws.flag), ptr(ws.boff), PART_BLOCKS, ptr(ws.seg), ptr(ws.segR),
+                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), s)
+            else:
+                ws.seg[2 * h0 + 1:2 * (h0 + nn) + 1].zero_()
+            cur ^= 1
+            c0 = 2 * h0 + 1
+            ws.gcnt[c0:c0 + 2 * nn].copy_(ws.seg[c0:c0 + 2 * nn, 1])
+            if dist:
+                comm.all_reduce_(ws.gcnt[c0:c0 + 2 * nn])
+        m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(leaf[t]), s)
+        if n:
+            m.gbdt_margin(ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(leaf[t]), D, ptr(margin), s)
+    ens = TreeEnsemble(feat=feat.cpu().numpy(), bin=binv.cpu().numpy(), thr=thr.cpu().numpy(),
+                       gain=gain.cpu().numpy(), leaf=leaf.cpu().numpy(), **ens_kw)
+    return (ens, margin) if return_margin else ens
+
+
+# ---- inference -------------------------------------------------------------------------------
+class DeviceEnsemble:
+    """Tree arrays resident on a device for repeated inference."""
+
+    def __init__(self, ens: TreeEnsemble, device: torch.device):
+        self.ens = ens
+        self.device = device
+        self.feat = torch.from_numpy(np.ascontiguousarray(ens.feat)).to(device)
+        self.thr = torch.from_numpy(np.ascontiguousarray(ens.thr)).to(device)
+        self.leaf = torch.from_numpy(np.ascontiguousarray(ens.leaf)).to(device)
+
+
+def predict_margin(X: torch.Tensor, ens: TreeEnsemble, dens: DeviceEnsemble | None = None) -> torch.Tensor:
+    """float32 margins of standardized rows X [n, d] (d <= 30, any row stride)."""
+    n, d = X.shape
+    if d != ens.n_features:
+        raise ValueError(f"model has {ens.n_features} features, X has {d}")
+    if not X.is_cuda:
+        return torch.from_numpy(R.predict_margin(X.numpy(), ens.feat, ens.thr, ens.leaf, ens.depth, ens.base_margin))
+    if X.dtype != torch.float32 or X.stride(1) != 1:
+        raise ValueError("X must be float32 with unit column stride")
+    dens = dens if dens is not None and dens.device == X.device else DeviceEnsemble(ens, X.device)
+    out = torch.empty(n, dtype=torch.float32, device=X.device)
+    if n:
+        native().gbdt_predict(ptr(X), n, X.stride(0), d, ptr(dens.feat), ptr(dens.thr), ptr(dens.leaf), ens.n_trees,
+                              ens.depth, ens.base_margin, ptr(out), stream_of(X))
+    return out
+
+
+def predict_proba(X: torch.Tensor, ens: TreeEnsemble, dens: DeviceEnsemble | None = None) -> torch.Tensor:
+    return torch.sigmoid(predict_margin(X, ens, dens))

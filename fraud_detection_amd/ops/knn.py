@@ -63,7 +63,7 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
 def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int, out: torch.Tensor,
                    seed: int = 42, counter_base: int = 0, label: float = 1.0,
                    fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:
-    """Write ``n_new`` synthetic rows into ``out`` (a [n_new, 32] bf16/fp8 view, e.g. the tail of
+    """Write ``n_new`` synthetic rows into ``out`` (a [n_new, 32] bf16/fp32/fp8 view, e.g. the tail of
     the training buffer).  Sample s interpolates minority row (q_offset + i) toward neighbour
     nbr[i, kk] with Philox draws keyed by (seed, s, counter_base)."""
     if C.dtype != torch.float32 or C.dim() != 2 or C.shape[1] != NCOLS:
@@ -86,6 +86,8 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
         rows = ref.smote_generate(C.numpy(), nb, q_offset, n_new, seed, counter_base, label)
         if kind == "bf16":
             out.copy_(torch.from_numpy(rows).to(torch.bfloat16))
+        elif kind == "f32":
+            out.copy_(torch.from_numpy(rows))
         else:
             r2 = rows.copy()
             r2[:, :30] *= fp8_scale

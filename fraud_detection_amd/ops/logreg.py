@@ -82,13 +82,18 @@ def auto_hess_stride(n_rows: int) -> int:
     return int(max(1, min(8, n_rows // HESS_SAMPLE_ROWS)))
 
 
+def auto_hess_refresh(n_rows: int) -> int:
+    """Full-data Newton iterations per fresh Hessian (lazy Hessian) -- see tools/newton_trace.py."""
+    return 0 if n_rows < (1 << 20) else 4
+
+
 def progressive_schedule(n_rows: int) -> list:
     """Warm-up phases [(tile_subsample, newton_iters), ...] before the full-data phase.  Each
     phase keeps >= ~1M rows, so its optimum is within sampling noise of the full one and the
     full-data phase then needs ~2-3 quadratic-convergence steps."""
-    if n_rows >= (16 << 20):
+    if n_rows >= (8 << 20):
         return [(16, 2), (4, 2)]
-    if n_rows >= (4 << 20):
+    if n_rows >= (2 << 20):
         return [(4, 3)]
     return []
 
@@ -137,11 +142,16 @@ def _default_w0(w0):
 def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: int = 25,
                class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
-               sync: bool = True, hess_stride: int | str = "auto", progressive="auto") -> FitInfo:
+               sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
+               hess_refresh: int | str = "auto") -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
-    gradient and objective always use all rows, so the converged solution is unchanged."""
+    gradient and objective always use all rows, so the converged solution is unchanged.
+    ``hess_refresh``: in the full-data phase a fresh Hessian only every k-th iteration; the
+    iterations in between stream the gradient alone (-36% bytes of MFMA-free work per pass) and
+    reuse the last reduced Hessian still held in the workspace (lazy-Hessian Newton).  0 = every
+    iteration.  The fixed point is unchanged: only the step's curvature model is older."""
     check_rows(rows)
     w0 = _default_w0(w0)
     if not rows.is_cuda:
@@ -173,11 +183,17 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         ws.state[S_BACKTRACKS].zero_()
     warm = sum(it for _, it in sched)
 
+    refresh = auto_hess_refresh(n_sched) if hess_refresh == "auto" else int(hess_refresh)
+    full_it = [0]
+
     def enqueue_chunk(k: int) -> int:
         for _ in range(k):
-            _pass(m, rows, ws, hs, 0, n, fp8_scale, s)
+            fresh = refresh <= 0 or full_it[0] % refresh == 0
+            full_it[0] += 1
+            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s)
             if comm is not None and comm.world_size > 1:
-                comm.all_reduce_(ws.red)
+                # a gradient-only pass leaves the (already all-reduced) Hessian in red[64:]
+                comm.all_reduce_(ws.red if fresh else ws.red[:64])
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
                             int(max_iter + warm), int(fit_intercept), s)
         return k

@@ -106,3 +106,40 @@ def test_dp_knn_equals_global(tmp_path):
     full, _ = ref.knn_topk(C, C, 5, 0)
     got = np.concatenate([np.load(os.path.join(tmp_path, f"knn{r}.npy")) for r in range(3)])
     assert np.array_equal(got, full)
+
+
+def _gbdt_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    from fraud_detection_amd.ops import gbdt as gb
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    comm = Communicator(backend="gloo")
+    X, y, cuts = _gbdt_data()
+    sh = slice(rank * len(X) // world, (rank + 1) * len(X) // world)
+    ens = gb.fit(torch.from_numpy(X[sh].copy()), torch.from_numpy(y[sh].copy()),
+                 gb.GBDTParams(n_estimators=4, max_depth=3), comm=comm, cuts=cuts)
+    np.savez(os.path.join(out_dir, f"g{rank}.npz"), feat=ens.feat, bin=ens.bin, leaf=ens.leaf)
+    comm.close()
+
+
+def _gbdt_data():
+    from fraud_detection_amd.ops import reference_gbdt as R
+
+    rng = np.random.default_rng(11)
+    X = rng.normal(size=(3000, 5)).astype(np.float32)
+    y = (X[:, 0] + 0.5 * X[:, 1] ** 2 + rng.normal(size=3000) > 1.2).astype(np.uint8)
+    return X, y, R.quantile_cuts(X, 64)
+
+
+def test_dp_gbdt_equals_single_process(tmp_path):
+    """Histogram all-reduce (int64, exact) makes the DP trees bit-identical to one process."""
+    port = _free_port()
+    mp.start_processes(_gbdt_worker, args=(2, port, str(tmp_path)), nprocs=2, start_method="spawn")
+    from fraud_detection_amd.ops import gbdt as gb
+
+    X, y, cuts = _gbdt_data()
+    ref = gb.fit(torch.from_numpy(X), torch.from_numpy(y), gb.GBDTParams(n_estimators=4, max_depth=3), cuts=cuts)
+    for r in range(2):
+        o = np.load(os.path.join(tmp_path, f"g{r}.npz"))
+        assert np.array_equal(o["feat"], ref.feat) and np.array_equal(o["bin"], ref.bin)
+        assert np.array_equal(o["leaf"], ref.leaf)

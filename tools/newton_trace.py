@@ -43,21 +43,33 @@ def main():
     w0[:30] = np.random.default_rng(42).normal(0.0, 0.01, 30)
     print(f"rows {n}  auto_hess_stride {L.auto_hess_stride(n)}  auto schedule {L.progressive_schedule(n)}")
 
+    # name: (warm-up schedule, full-data Hessian stride, Hessian refresh period (0 = every iter))
     variants = {
-        "auto": (L.progressive_schedule(n), L.auto_hess_stride(n)),
-        "none_h3": ([], 3), "none_h1": ([], 1),
-        "s4x3_h1": ([(4, 3)], 1), "s4x3_h2": ([(4, 3)], 2), "s4x3_h3": ([(4, 3)], 3),
-        "s4x2_h1": ([(4, 2)], 1), "s8x2s2x1_h2": ([(8, 2), (2, 1)], 2),
-        "s16x2s4x2_h2": ([(16, 2), (4, 2)], 2), "s4x4_h2": ([(4, 4)], 2),
+        "auto": (L.progressive_schedule(n), L.auto_hess_stride(n), L.auto_hess_refresh(n)),
+        "s4x3_h3_r0": ([(4, 3)], 3, 0),
+        "s16x2s4x2_h2_r0": ([(16, 2), (4, 2)], 2, 0),
+        "s16x3s4x2_h2_r0": ([(16, 3), (4, 2)], 2, 0),
+        "s16x2s4x2_h2_r2": ([(16, 2), (4, 2)], 2, 2),
+        "s16x2s4x2_h2_r9": ([(16, 2), (4, 2)], 2, 99),
+        "s16x3s4x2_h2_r9": ([(16, 3), (4, 2)], 2, 99),
+        "s16x2s4x2_h1_r9": ([(16, 2), (4, 2)], 1, 99),
+        "s16x2s4x2_h3_r9": ([(16, 2), (4, 2)], 3, 99),
+        "s32x2s8x2s2x1_h2_r9": ([(32, 2), (8, 2), (2, 1)], 2, 99),
+        "s16x2s4x3_h2_r9": ([(16, 2), (4, 3)], 2, 99),
     }
     out = {}
-    for name, (sched, hs) in variants.items():
+    for name, (sched, hs, refresh) in variants.items():
         ws.reset(w0, (1.0, 1.0))
         trace = []
+        j_full = 0
         for phase, (sub, iters) in enumerate(sched + [(1, 25)]):
             full = sub == 1
             hs_w = hs if full else L.auto_hess_stride(n // sub)
             for _ in range(iters):
+                if full:
+                    fresh = refresh <= 0 or j_full % refresh == 0
+                    j_full += 1
+                    hs_w = hs if fresh else 0
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 L._pass(m, rows, ws, hs_w, 0, n, 4.0, s, sub=sub)
