@@ -83,8 +83,10 @@ def auto_hess_stride(n_rows: int) -> int:
 
 
 def auto_hess_refresh(n_rows: int) -> int:
-    """Full-data Newton iterations per fresh Hessian (lazy Hessian) -- see tools/newton_trace.py."""
-    return 0 if n_rows < (1 << 20) else 4
+    """Full-data Newton iterations per fresh Hessian (lazy Hessian).  Only after a progressive
+    warm-up: started near the optimum, a stale Hessian costs no iterations (profiles/r1_s12:
+    2 full passes either way) but saves the MFMA work; started cold it slows convergence."""
+    return 4 if progressive_schedule(n_rows) else 0
 
 
 def progressive_schedule(n_rows: int) -> list:
@@ -92,7 +94,7 @@ def progressive_schedule(n_rows: int) -> list:
     phase keeps >= ~1M rows, so its optimum is within sampling noise of the full one and the
     full-data phase then needs ~2-3 quadratic-convergence steps."""
     if n_rows >= (8 << 20):
-        return [(16, 2), (4, 2)]
+        return [(16, 3), (4, 2)]
     if n_rows >= (2 << 20):
         return [(4, 3)]
     return []

@@ -37,11 +37,25 @@ def _device(name: str) -> torch.device:
     return torch.device(name)
 
 
+def _shard(idx: np.ndarray, comm) -> np.ndarray:
+    """This rank's rows of an index set (strided, so every shard keeps the class mix)."""
+    if comm is None:
+        return idx
+    return idx[comm.rank::comm.world_size]
+
+
 def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds: int = 5, model_dir: str = "models",
-        verbose: bool = True, cfg: TrainConfig | None = None) -> dict:
+        verbose: bool = True, cfg: TrainConfig | None = None, comm=None) -> dict:
+    """Single process, or data parallel when ``comm`` spans several ranks (torchrun: one rank per
+    GPU).  Every rank reads the table and derives the same split; each fits on its strided shard
+    with RCCL all-reduced statistics, so all ranks hold the same model; rank 0 writes artifacts."""
     s = settings or Settings.load()
-    say = print if verbose else (lambda *a, **k: None)
+    comm = comm if (comm is not None and comm.world_size > 1) else None
+    lead = comm is None or comm.rank == 0
+    say = print if (verbose and lead) else (lambda *a, **k: None)
     dev = _device(s.device)
+    if comm is not None and dev.type == "cuda":
+        dev = torch.device("cuda", torch.cuda.current_device())
     t0 = time.time()
     say("Loading dataset...")
     X, y, names = read_table(s.data_csv)
@@ -54,9 +68,11 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         raise ValueError("missing feature values; impute before training")
     say("Splitting dataset (Train 80% / Test 20%)...")
     tr, te = stratified_split(y, 0.2, 42)
-    Xtr, ytr = torch.from_numpy(X[tr]).to(dev), torch.from_numpy(y[tr]).to(dev)
-    Xte, yte = torch.from_numpy(X[te]).to(dev), torch.from_numpy(y[te]).to(dev)
     neg, pos = int((y[tr] == 0).sum()), int((y[tr] == 1).sum())
+    y_tr_all = y[tr]
+    tr_m, te_m = _shard(tr, comm), _shard(te, comm)
+    Xtr, ytr = torch.from_numpy(X[tr_m]).to(dev), torch.from_numpy(y[tr_m]).to(dev)
+    Xte, yte = torch.from_numpy(X[te_m]).to(dev), torch.from_numpy(y[te_m]).to(dev)
     scale_pos_weight = neg / pos if pos > 0 else 1.0
     say(f" Class balance before SMOTE -> [{neg} {pos}]")
     cfg = cfg or TrainConfig(solver=s.solver, storage=s.dtype, seed=s.seed, k_neighbors=s.smote_k)
@@ -65,24 +81,27 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     cv_scores = []
     if cv_folds and cv_folds > 1 and pos >= cv_folds:
         say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
-        for k, (ftr, fva) in enumerate(stratified_folds(y[tr], cv_folds, 42)):
-            fi = torch.from_numpy(ftr).to(dev)
-            vi = torch.from_numpy(fva).to(dev)
-            res = _fit(model_type, cfg, Xtr.index_select(0, fi).contiguous(), ytr.index_select(0, fi).contiguous())
-            auc = _score(model_type, res, Xtr.index_select(0, vi).contiguous(), ytr.index_select(0, vi).contiguous())
+        for k, (ftr, fva) in enumerate(stratified_folds(y_tr_all, cv_folds, 42)):
+            fi, vi = _shard(tr[ftr], comm), _shard(tr[fva], comm)
+            res = _fit(model_type, cfg, torch.from_numpy(X[fi]).to(dev), torch.from_numpy(y[fi]).to(dev), comm)
+            auc = _score(model_type, res, torch.from_numpy(X[vi]).to(dev), torch.from_numpy(y[vi]).to(dev), comm)
             cv_scores.append(auc)
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
     say(f" Training final {model_type} model with SMOTE on the full training set...")
-    res = _fit(model_type, cfg, Xtr, ytr)
+    res = _fit(model_type, cfg, Xtr, ytr, comm)
     if model_type == "logistic":
-        ev = evaluate(res, Xte, yte)
+        ev = evaluate(res, Xte, yte, comm)
         auc = ev["auc"]
-        say(f" Class balance after SMOTE -> [{res.n_rows - res.n_minority} {res.n_minority + res.n_synthetic}]")
+        say(f" Class balance after SMOTE -> [{res.n_rows - res.n_minority} {res.n_minority + res.n_synthetic}]"
+            + (f" (rank 0 of {comm.world_size})" if comm else ""))
     else:
-        auc = _score(model_type, res, Xte, yte)
-        ev = {"auc": auc}
+        ev = res.evaluate(Xte, yte, comm)
+        auc = ev["auc"]
     say(f"Test AUC: {auc:.4f}")
+    if not lead:
+        comm.barrier()
+        return {"test_auc": float(auc), "cv_scores": cv_scores, "rank": comm.rank}
     paths = _save(model_type, res, names, model_dir, cfg)
     say(f" Model and scaler saved to /{model_dir}")
     summary = {"test_auc": float(auc), "cv_auc_mean": float(np.mean(cv_scores)) if cv_scores else None,
@@ -93,21 +112,24 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         summary["registered_version"] = _track(s, model_type, res, summary, paths, Xte, names, say)
     except Exception as e:  # noqa: BLE001 - tracking is best effort (reference train_model.py:165-166)
         say(f" MLflow Tracking Failed (likely connection error): {e}")
+    if comm is not None:
+        summary["world_size"] = comm.world_size
+        comm.barrier()
     return summary
 
 
-def _fit(model_type, cfg, X, y):
+def _fit(model_type, cfg, X, y, comm=None):
     if model_type == "logistic":
-        return DevicePipeline(cfg).fit(X, y)
+        return DevicePipeline(cfg, comm).fit(X, y)
     from .models.gbdt import GBDTPipeline
 
-    return GBDTPipeline(cfg).fit(X, y)
+    return GBDTPipeline(cfg, comm=comm).fit(X, y)
 
 
-def _score(model_type, res, X, y) -> float:
+def _score(model_type, res, X, y, comm=None) -> float:
     if model_type == "logistic":
-        return float(evaluate(res, X, y)["auc"])
-    return float(res.evaluate(X, y)["auc"])
+        return float(evaluate(res, X, y, comm)["auc"])
+    return float(res.evaluate(X, y, comm)["auc"])
 
 
 def _save(model_type, res, names, model_dir, cfg) -> dict:
@@ -165,7 +187,22 @@ def main(argv=None):
     ap.add_argument("--json", default=None, help="write the run summary here")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
-    out = run(model_type=a.model, cv_folds=a.cv_folds, model_dir=a.model_dir)
+    comm = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:  # torchrun: one rank per GPU, RCCL (gloo on CPU)
+        from .parallel.comm import Communicator
+
+        dev = None
+        if torch.cuda.is_available():
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            dev = torch.device("cuda", torch.cuda.current_device())
+        comm = Communicator(device=dev)
+    try:
+        out = run(model_type=a.model, cv_folds=a.cv_folds, model_dir=a.model_dir, comm=comm)
+    finally:
+        if comm is not None:
+            comm.close()
+    if comm is not None and comm.rank != 0:
+        return 0
     if a.json:
         with open(a.json, "w") as f:
             json.dump({k: v for k, v in out.items() if k != "eval"} | {"eval": out["eval"]}, f, indent=1, default=str)

@@ -143,3 +143,36 @@ def test_dp_gbdt_equals_single_process(tmp_path):
         o = np.load(os.path.join(tmp_path, f"g{r}.npz"))
         assert np.array_equal(o["feat"], ref.feat) and np.array_equal(o["bin"], ref.bin)
         assert np.array_equal(o["leaf"], ref.leaf)
+
+
+def _train_worker(rank, world, port, out_dir, csv):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), DATA_CSV=csv, MLFLOW_TRACKING_URI=os.path.join(out_dir, "mlruns"),
+                      MLFLOW_AUC_THRESHOLD="0.5", FDX_DEVICE="cpu")
+    from fraud_detection_amd import train
+    from fraud_detection_amd.config import Settings
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    comm = Communicator(backend="gloo")
+    out = train.run(Settings.load(), cv_folds=2, model_dir=os.path.join(out_dir, "models"), verbose=False, comm=comm)
+    np.save(os.path.join(out_dir, f"auc{rank}.npy"), np.array([out["test_auc"]] + list(out["cv_scores"])))
+    comm.close()
+
+
+def test_dp_train_entry_point(tmp_path, monkeypatch):
+    """torchrun-style DP training: both ranks report the same (global) AUCs, rank 0 alone writes
+    artifacts, and the result matches single-process training to SMOTE sampling noise."""
+    from fraud_detection_amd import train
+    from fraud_detection_amd.config import Settings
+    from fraud_detection_amd.data.synthetic import separable_frame
+
+    csv = str(tmp_path / "cc.csv")
+    separable_frame(30_000, fraud_rate=0.02, seed=8).to_csv(csv, index=False)
+    port = _free_port()
+    mp.start_processes(_train_worker, args=(2, port, str(tmp_path), csv), nprocs=2, start_method="spawn")
+    a0, a1 = np.load(tmp_path / "auc0.npy"), np.load(tmp_path / "auc1.npy")
+    assert np.array_equal(a0, a1)
+    assert os.path.exists(tmp_path / "models" / "logistic_model.joblib")
+    monkeypatch.setenv("DATA_CSV", csv)
+    single = train.run(Settings.load(), cv_folds=2, model_dir=str(tmp_path / "single"), verbose=False)
+    assert abs(single["test_auc"] - a0[0]) < 0.01
