@@ -168,4 +168,33 @@ __host__ inline int stream_grid(int64_t work_items, int items_per_block, int max
   return (int)b;
 }
 
+__host__ inline int device_cu_count() {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+              ? prop.multiProcessorCount
+              : 256;
+  }
+  return cus;
+}
+
+// Blocks of `kernel` resident on the whole device at once (occupancy x CUs).  A grid-stride
+// stream gives every block an equal share of the work, so launching more blocks than fit in one
+// round adds a partial second round (a tail at ~1/occupancy efficiency); launch exactly this
+// many.  Call sites cache it in a function-local static per template instantiation.
+template <typename K>
+__host__ inline int resident_cap(K kernel, int threads, size_t dyn_lds = 0) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, dyn_lds) != hipSuccess || occ < 1) occ = 1;
+  return occ * device_cu_count();
+}
+__host__ inline int capped_grid(int64_t work_items, int items_per_block, int cap) {
+  int64_t b = (work_items + items_per_block - 1) / items_per_block;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
 }  // namespace fdx

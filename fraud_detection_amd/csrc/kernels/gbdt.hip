@@ -456,7 +456,8 @@ __global__ __launch_bounds__(kPredThreads) void gbdt_predict_kernel(
 void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,
                      uint8_t* bins, hipStream_t stream) {
   if (d > kGBMaxFeat) throw std::runtime_error("gbdt: at most 30 features");
-  const int grid = stream_grid(n, 256 / 8, 4096);
+  static const int cap = resident_cap(gbdt_bin_kernel, 256);
+  const int grid = capped_grid(n, 256 / 8, cap);
   gbdt_bin_kernel<<<grid, 256, 0, stream>>>(X, n, ld, d, cuts, nbins, bins);
   check_launch("gbdt_bin");
 }

@@ -93,7 +93,13 @@ __global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restr
   // per-lane parking row for one tile's 16 scores (stride 17 floats: conflict-free column reads)
   __shared__ float park_all[kWaves][kWave * 17];
   float* park = park_all[wv];
-  const int ntiles = mc_pad / 32;
+  // blockIdx.y selects a contiguous slice of candidate tiles (split-K over candidates: enough
+  // workgroups to fill 256 CUs and several waves per SIMD to hide the top-k VALU work behind
+  // other waves' MFMA); slices write partial lists merged by knn_merge_kernel.
+  const int all_tiles = mc_pad / 32;
+  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
+  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  const int ntiles = t_hi;
   // Register double buffer: the next candidate tile (16 floats of one row + 16 norms per lane,
   // L2-resident) is fetched while the current tile's MFMA chain and top-k run.
   float4 cv[4], nv[4];
@@ -107,8 +113,8 @@ __global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restr
       b[k] = *reinterpret_cast<const float4*>(chalf + cb + 8 * k + 4 * h);
     }
   };
-  if (wv < ntiles) fetch(wv, cv, nv);
-  for (int t = wv; t < ntiles; t += kWaves) {
+  if (t_lo + wv < ntiles) fetch(t_lo + wv, cv, nv);
+  for (int t = t_lo + wv; t < ntiles; t += kWaves) {
     const int c0 = t * 32;
     float ac[16];
     f32x16_t acc;
@@ -166,12 +172,37 @@ __global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restr
       for (int k = 0; k < K; ++k) topk_insert<K>(bs, bi, ls[w2][j][k], li[w2][j][k]);
     }
     if (qg < mq) {
+      // gridDim.y > 1: partial list of this slice at [blockIdx.y][q][k] of the workspace
+      const int64_t o = ((int64_t)blockIdx.y * mq + qg) * K;
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        out_idx[(int64_t)qg * K + k] = bi[k];
-        if (out_score) out_score[(int64_t)qg * K + k] = bs[k];
+        out_idx[o + k] = bi[k];
+        if (out_score) out_score[o + k] = bs[k];
       }
     }
+  }
+}
+
+// Merge the per-slice top-k lists of every query (same ordering: score desc, index asc).
+template <int K>
+__global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ ps, const int* __restrict__ pi,
+                                                        int nsplit, int mq, int* __restrict__ out_idx,
+                                                        float* __restrict__ out_score) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= mq) return;
+  float bs[K];
+  int bi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  for (int s = 0; s < nsplit; ++s) {
+    const int64_t o = ((int64_t)s * mq + q) * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) topk_insert<K>(bs, bi, ps[o + k], pi[o + k]);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    out_idx[(int64_t)q * K + k] = bi[k];
+    if (out_score) out_score[(int64_t)q * K + k] = bs[k];
   }
 }
 
@@ -182,14 +213,31 @@ void launch_row_half_norms(const float* X, int m, float* out, int m_pad, hipStre
   check_launch("row_half_norms");
 }
 
+int knn_splits(int mq_pad, int mc_pad) {
+  // ~2048 workgroups (8 per CU), each slice keeping >= 8 candidate tiles per wave
+  const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
+  int s = (2048 + qblocks - 1) / qblocks;
+  const int max_s = tiles / (kWaves * 8);
+  if (s > max_s) s = max_s;
+  if (s > 64) s = 64;
+  return s < 1 ? 1 : s;
+}
+
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const float* chalf,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, hipStream_t stream) {
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk: pads must be x32");
-  const int grid = mq_pad / 32;
-#define FDX_KNN(KK)                                                                           \
-  knn_topk_kernel<KK><<<grid, kThreads, 0, stream>>>(Q, mq, C, chalf, mc_pad, mc, self_offset, \
-                                                     out_idx, out_score)
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > 1 && (ws_score == nullptr || ws_idx == nullptr))
+    throw std::runtime_error("knn_topk: split search needs the [nsplit][mq][k] workspaces");
+  const dim3 grid(mq_pad / 32, nsplit);
+  int* oi = nsplit > 1 ? ws_idx : out_idx;
+  float* os = nsplit > 1 ? ws_score : out_score;
+#define FDX_KNN(KK)                                                                             \
+  knn_topk_kernel<KK><<<grid, kThreads, 0, stream>>>(Q, mq, C, chalf, mc_pad, mc, self_offset, oi, \
+                                                     os);                                        \
+  if (nsplit > 1)                                                                               \
+    knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
   switch (k) {
     case 1: FDX_KNN(1); break;
     case 2: FDX_KNN(2); break;

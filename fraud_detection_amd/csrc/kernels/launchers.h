@@ -66,9 +66,10 @@ void launch_sgd_update(const double* red, double* state, float* w32, int d, doub
 
 // ---- knn.hip ----
 void launch_row_half_norms(const float* X, int m, float* out, int m_pad, hipStream_t stream);
+int knn_splits(int mq_pad, int mc_pad);
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const float* chalf,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, hipStream_t stream);
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
 
 // ---- smote.hip ----
 void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,

@@ -207,20 +207,25 @@ void launch_predict_fp8(const uint8_t* X, int64_t n, const float* w, float* prob
 void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, int dphi,
                          const float* a, const float* c, float bias, float* prob, float* logit,
                          float* phi, int ld_phi, hipStream_t stream) {
-  const int grid = stream_grid((n + 7) / 8, (kThreads / kWave) * 4, 2048);
+  static const int cap01 = resident_cap(predict_shap_kernel<0, 1>, kThreads);
+  static const int cap14 = resident_cap(predict_shap_kernel<1, 4>, kThreads);
+  static const int cap12 = resident_cap(predict_shap_kernel<1, 2>, kThreads);
+  static const int cap11 = resident_cap(predict_shap_kernel<1, 1>, kThreads);
+  const int64_t units = (n + 7) / 8, per_block = (kThreads / kWave) * 4;
+  int grid = capped_grid(units, per_block, cap01);
   if (in_kind == 0) {
     predict_shap_kernel<0, 1><<<grid, kThreads, 0, stream>>>(X, n, kCols, dz, dphi, a, c, bias,
                                                              prob, logit, phi, ld_phi);
   } else {
     const uintptr_t al = reinterpret_cast<uintptr_t>(X);
     if ((ld % 4) == 0 && (al % 16) == 0)
-      predict_shap_kernel<1, 4><<<grid, kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
+      predict_shap_kernel<1, 4><<<capped_grid(units, per_block, cap14), kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
                                                                prob, logit, phi, ld_phi);
     else if ((ld % 2) == 0 && (al % 8) == 0)
-      predict_shap_kernel<1, 2><<<grid, kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
+      predict_shap_kernel<1, 2><<<capped_grid(units, per_block, cap12), kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
                                                                prob, logit, phi, ld_phi);
     else
-      predict_shap_kernel<1, 1><<<grid, kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
+      predict_shap_kernel<1, 1><<<capped_grid(units, per_block, cap11), kThreads, 0, stream>>>(X, n, ld, dz, dphi, a, c, bias,
                                                                prob, logit, phi, ld_phi);
   }
   check_launch("predict_shap");

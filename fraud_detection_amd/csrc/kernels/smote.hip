@@ -95,17 +95,20 @@ void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, void* out, hipStream_t stream) {
   if (n_new <= 0) return;
-  const int grid = stream_grid(n_new, (kThreads / kWave) * 64, 2048);
+  const int64_t per_block = (kThreads / kWave) * 64;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
+  static const int cap0 = resident_cap(smote_generate_kernel<0>, kThreads);
+  static const int cap1 = resident_cap(smote_generate_kernel<1>, kThreads);
+  static const int cap2 = resident_cap(smote_generate_kernel<2>, kThreads);
   if (out_kind == 0)
-    smote_generate_kernel<0><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
-                                                           c0, c1, label, out_scale, out);
+    smote_generate_kernel<0><<<capped_grid(n_new, per_block, cap0), kThreads, 0, stream>>>(
+        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, out);
   else if (out_kind == 1)
-    smote_generate_kernel<1><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
-                                                           c0, c1, label, out_scale, out);
+    smote_generate_kernel<1><<<capped_grid(n_new, per_block, cap1), kThreads, 0, stream>>>(
+        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, out);
   else
-    smote_generate_kernel<2><<<grid, kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
+    smote_generate_kernel<2><<<capped_grid(n_new, per_block, cap2), kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
                                                            c0, c1, label, out_scale, out);
   check_launch("smote_generate");
 }

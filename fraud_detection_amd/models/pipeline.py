@@ -116,16 +116,20 @@ class DevicePipeline:
         # ---- K1: scaler statistics (C1 all-reduce inside) --------------------------------
         stats = scaler_ops.scaler_fit(X, comm=comm)
         tm.mark("scaler_fit")
-        # ---- class counts (C2) and SMOTE quota ---------------------------------------------
-        idx_min = scaler_ops.compact_indices(y, 1)
+        # ---- class counts (C2): count kernels now, host reads the total while K2 runs -------
+        pending = scaler_ops.compact_indices_async(y, 1)
+        # ---- K2: standardize + pad + cast the real rows (label in col 31) into a buffer sized
+        # for the largest possible SMOTE output, so it does not wait for the minority count
+        cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) if cfg.smote else 0)
+        rows_cap = self._train_buffer(cap, dev)
+        scaler_ops.scale_cast(X, stats, labels=y, out_dtype=cfg.storage, out=rows_cap[:n], fp8_scale=cfg.fp8_scale)
+        idx_min = pending.result()
         n_min = int(idx_min.shape[0])
         n_maj = n - n_min
         n_new = 0
         if cfg.smote and n_min > 0:
             n_new = max(0, int(round(n_maj * cfg.sampling_ratio)) - n_min)
-        rows = self._train_buffer(n + n_new, dev)
-        # ---- K2: standardize + pad + cast the real rows (label in col 31) ---------------
-        scaler_ops.scale_cast(X, stats, labels=y, out_dtype=cfg.storage, out=rows[:n], fp8_scale=cfg.fp8_scale)
+        rows = rows_cap[: n + n_new]
         tm.mark("scale_cast")
         if n_new > 0:
             # ---- minority rows in fp32, gathered across ranks (C3) -----------------------

@@ -21,12 +21,14 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
     return out
 
 
-def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False):
+def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
+             nsplit: int | None = None):
     """k nearest candidates (squared L2) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows.  If ``self_offset >= 0``, query row q is candidate
     row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
     (ascending distance, ties -> smaller index) and optionally squared distances.
+    ``nsplit``: candidate slices searched by separate workgroups and merged (None = auto).
     """
     for t, nm in ((Q, "Q"), (C, "C")):
         if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
@@ -52,8 +54,13 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     m.row_half_norms(ptr(Cp), mc, ptr(chalf), mc_pad, s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
+    ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
+    ws_s = ws_i = None
+    if ns > 1:
+        ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
+        ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
     m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), ptr(chalf), mc_pad, mc, int(self_offset), int(k), ptr(idx),
-               ptr(score), s)
+               ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     if want_dist:
         qn = (Q.double() ** 2).sum(1, keepdim=True)
         return idx, (qn - 2.0 * score.double()).float()

@@ -128,13 +128,52 @@ def scale_cast(X: torch.Tensor, stats: ScalerStats, labels: torch.Tensor | None 
     return out
 
 
-def compact_indices(labels: torch.Tensor, target: int = 1, nblocks: int = 512) -> torch.Tensor:
-    """Stable indices of rows whose label == target (device: 3 deterministic kernels)."""
+class PendingCompaction:
+    """Count/scan kernels enqueued, the total on its way to pinned host memory.  ``result()``
+    waits only for those kernels (work enqueued after them keeps the GPU busy meanwhile), then
+    enqueues the write of the stable index list."""
+
+    _pool: list = []  # rotating pinned slots (pinned allocation costs tens of microseconds)
+    _next = 0
+
+    def __init__(self, labels, target, nb, counts, total):
+        self.labels, self.target, self.nb, self.counts = labels, target, nb, counts
+        if not PendingCompaction._pool:
+            PendingCompaction._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(8)]
+        self.host = PendingCompaction._pool[PendingCompaction._next % 8]
+        PendingCompaction._next += 1
+        self.host.copy_(total, non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+        self._out = None
+
+    def result(self) -> torch.Tensor:
+        if self._out is None:
+            self.event.synchronize()
+            cnt = int(self.host[0])
+            out = torch.empty(cnt, device=self.labels.device, dtype=torch.int64)
+            if cnt:
+                native().compact_write(ptr(self.labels), self.labels.shape[0], self.target, ptr(self.counts), ptr(out),
+                                       self.nb, stream_of(self.labels))
+            self._out = out
+        return self._out
+
+
+class _Ready:
+    def __init__(self, out):
+        self._out = out
+
+    def result(self):
+        return self._out
+
+
+def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 512):
+    """Stable indices of rows whose label == target, as a pending result (see PendingCompaction)."""
     if labels.dtype != torch.uint8 or labels.dim() != 1:
         raise ValueError("labels must be 1-D uint8")
     n = labels.shape[0]
     if not labels.is_cuda:
-        return torch.nonzero(labels == target, as_tuple=False).reshape(-1).to(torch.int64)
+        return _Ready(torch.nonzero(labels == target, as_tuple=False).reshape(-1).to(torch.int64))
     m = native()
     s = stream_of(labels)
     nb = int(max(1, min(nblocks, (n + 255) // 256)))
@@ -142,11 +181,12 @@ def compact_indices(labels: torch.Tensor, target: int = 1, nblocks: int = 512) -
     total = torch.empty(1, device=labels.device, dtype=torch.int64)
     m.compact_count(ptr(labels), n, target, ptr(counts), nb, s)
     m.exclusive_scan_small(ptr(counts), nb, ptr(total), s)
-    cnt = int(total.item())  # host sync: output size is data dependent
-    out = torch.empty(cnt, device=labels.device, dtype=torch.int64)
-    if cnt:
-        m.compact_write(ptr(labels), n, target, ptr(counts), ptr(out), nb, s)
-    return out
+    return PendingCompaction(labels, target, nb, counts, total)
+
+
+def compact_indices(labels: torch.Tensor, target: int = 1, nblocks: int = 512) -> torch.Tensor:
+    """Stable indices of rows whose label == target (device: 3 deterministic kernels)."""
+    return compact_indices_async(labels, target, nblocks).result()
 
 
 def stats_from_numpy(mean: np.ndarray, scale: np.ndarray, n: float = 0.0, var=None, device="cpu") -> ScalerStats:

@@ -208,6 +208,20 @@ def test_knn_topk_exact(dev, mq, k):
     assert not np.any(idx == (np.arange(mq)[:, None] + off))  # self excluded
 
 
+@pytest.mark.parametrize("nsplit", [2, 3, 7, 40])
+def test_knn_split_search_identical(dev, nsplit):
+    """Candidate slices + merge must reproduce the single-slice lists exactly (incl. tie order)."""
+    rng = np.random.default_rng(7)
+    C = np.zeros((3001, 32), np.float32)
+    C[:, :30] = np.round(rng.normal(size=(3001, 30)) * 4) / 4  # coarse grid -> many exact ties
+    C[1500:1600] = C[100:200]                                  # duplicate rows across slices
+    Ct = torch.from_numpy(C).to(dev)
+    Q = Ct[:1000].contiguous()
+    a, sa = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, nsplit=1)
+    b, sb = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, nsplit=nsplit)
+    assert torch.equal(a, b) and torch.equal(sa, sb)
+
+
 def test_smote_generate_matches_oracle(dev):
     rng = np.random.default_rng(0)
     m = 300
