@@ -5,13 +5,25 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
 namespace fdx {
 
+// FDX_SYNC_LAUNCH=1: synchronise after every launch so an asynchronous fault is reported with
+// the name of the kernel that caused it (debug mode, like AMD_SERIALIZE_KERNEL=3 but attributed).
+inline bool sync_launch_mode() {
+  static const int mode = [] {
+    const char* v = std::getenv("FDX_SYNC_LAUNCH");
+    return (v != nullptr && v[0] != '\0' && v[0] != '0') ? 1 : 0;
+  }();
+  return mode != 0;
+}
+
 inline void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
+  if (e == hipSuccess && sync_launch_mode()) e = hipDeviceSynchronize();
   if (e != hipSuccess) {
     throw std::runtime_error(std::string("fdx kernel launch failed [") + what +
                              "]: " + hipGetErrorString(e));

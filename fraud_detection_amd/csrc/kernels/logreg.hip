@@ -257,6 +257,7 @@ __device__ void build_grad(const double* red, const double* st, int d, int fit_i
 // first wait; reductions are wave-parallel; the Cholesky gives lane i row i (no integer
 // division, one fp64 reciprocal per column); the triangular solves keep b in lane registers
 // and broadcast with shuffles; barriers of a single-wave workgroup are nearly free.
+template <int MT>  // MT > 0: compile-time number of active coordinates (identity index map)
 __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
                                                            double* __restrict__ st,
                                                            float* __restrict__ w32,
@@ -266,7 +267,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   __shared__ double sr[kLRPartStride];
   __shared__ double ss[kStateSize];
   __shared__ double grad[32];
-  __shared__ double Lc[32][33];
+  __shared__ double Lc[64][65];  // [column][row], padded: every lane writes/reads in bounds
   __shared__ int idx[32];
   const int t = threadIdx.x;
   {
@@ -289,7 +290,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
   const double reg = 1.0 / (C * S);
   const double invS = 1.0 / S;
-  const int m = d + (fit_intercept ? 1 : 0);
+  const int m = MT > 0 ? MT : d + (fit_intercept ? 1 : 0);
   const int my = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
   if (t < 32) idx[t] = my;
   build_grad(sr, ss, d, fit_intercept, reg, S, grad, t);
@@ -326,29 +327,30 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       *done = 1;
     }
   } else {
-    // H_active = H/S + reg I (penalised coords); solve H s = -grad by Cholesky (fp64).
-    // Lane i owns row i of A in registers (a[32], fully unrolled so every index is static);
-    // column k of L is broadcast with readlane, so the factorisation has no LDS traffic and
-    // no barriers.  Rows/columns >= m are identity-padded and never read back.
+    // Solve (H + reg*S*I_pen) s = -S*grad, i.e. (H/S + reg I_pen) s = -grad, by Cholesky in fp64.
+    // Lane t owns row t of A in registers (a[32], fully unrolled: static indices).  With MT > 0
+    // (compile-time m; the index map is then the identity) every guard below is static, so the
+    // single wave -- whose cost is its instruction count -- runs a branch-free stream.  Column k
+    // of L goes to LDS once (Lc[k][t]); the trailing update reads it back as uniform-address
+    // broadcasts and the back substitution reads column t (Lc[t][k]).  1/sqrt: v_rsq_f64 + one
+    // Newton refinement (~46 bits; the Newton step only needs to be a good descent direction).
+    // Rows/columns >= m are identity-padded and never read back.
+    const double regS = reg * S;
     double a[32];
     {
-      const double* hr = sr + 64 + (my >= 0 ? my : 0) * kCols;
+      const int row = (MT > 0) ? (t < 32 ? t : 0) : (my >= 0 ? my : 0);
+      const double* hr = sr + 64 + row * kCols;
 #pragma unroll
       for (int k = 0; k < 32; ++k) {
-        double h = 0.0;
-        if (t < m && k < m) {
-          h = hr[idx[k]] * invS;
-          if (k == t && my < d) h += reg;
-        } else if (k == t) {
-          h = 1.0;
-        }
-        a[k] = h;
+        const int col = (MT > 0) ? k : idx[k];
+        const double hv = hr[col < 0 ? 0 : col];
+        const bool act = (t < m) && (k < m);
+        const double dg = (k == t && my < d) ? regS : 0.0;
+        a[k] = act ? hv + dg : (k == t ? 1.0 : 0.0);
       }
     }
-    double bi = (t < m) ? -grad[my] : 0.0;
-    // Column k of L, once computed, goes to LDS (Lc[k][j] = L[j][k]); the trailing update then
-    // reads it with uniform-address (broadcast) LDS loads instead of one readlane pair + hazard
-    // nops per element.  1/sqrt via v_rsq_f64 + two Newton refinements (no div/sqrt sequences).
+    double bi = (t < m) ? -grad[my < 0 ? 0 : my] * S : 0.0;
+    constexpr int JE = MT > 0 ? MT : 32;
     double dv[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
@@ -356,14 +358,13 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         const double akk = fmax(rdlane(a[k], k), 1e-300);
         double inv = __builtin_amdgcn_rsq(akk);
         inv = inv * fma(-0.5 * akk * inv, inv, 1.5);
-        inv = inv * fma(-0.5 * akk * inv, inv, 1.5);
         dv[k] = inv;
         const double ak = (t == k) ? akk * inv : a[k] * inv;  // column k of L (rows t > k)
         a[k] = ak;
-        if (t < 32) Lc[k][t] = ak;
+        Lc[k][t] = ak;
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = k + 1; j < 32; ++j) a[j] = fma(-ak, Lc[k][j], a[j]);
+        for (int j = k + 1; j < JE; ++j) a[j] = fma(-ak, Lc[k][j], a[j]);
       } else {
         dv[k] = 0.0;
       }
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     for (int k = 31; k >= 0; --k) {  // L^T x = y (column sweep): lane t < k needs L[k][t] = Lc[t][k]
       if (k < m) {
         const double xk = rdlane(bi, k) * dv[k];
-        const double lkt = (t < k) ? Lc[t][k] : 0.0;
+        const double lkt = Lc[t][k];
         bi = (t == k) ? xk : (t < k ? fma(-lkt, xk, bi) : bi);
       }
     }
@@ -498,8 +499,10 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept,
                           hipStream_t stream) {
-  newton_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter,
-                                             fit_intercept);
+  if (d + (fit_intercept ? 1 : 0) == 31)  // 30 features + intercept: the specialised stream
+    newton_update_kernel<31><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept);
+  else
+    newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept);
   check_launch("newton_update");
 }
 

@@ -390,23 +390,42 @@ __global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(
   }
 }
 
-// In-place exclusive scan of a small int64 array (n <= 4096), one block; writes total to tot.
+// In-place exclusive scan of a small int64 array (n <= 4096), one block of 1024 threads; writes
+// the total to tot.  Each thread owns 4 consecutive elements; lane totals are scanned with wave
+// shuffles, wave totals by wave 0 -- integer adds, so the result is exact and order-free.
 __global__ __launch_bounds__(1024) void exclusive_scan_small_kernel(int64_t* __restrict__ a, int n,
                                                                     int64_t* __restrict__ tot) {
-  __shared__ int64_t s[4096];
-  for (int i = threadIdx.x; i < n; i += blockDim.x) s[i] = a[i];
+  __shared__ int64_t wsum[16];
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  int64_t v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = (4 * t + j < n) ? a[4 * t + j] : 0;
+  const int64_t mine = (v[0] + v[1]) + (v[2] + v[3]);
+  int64_t inc = mine;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int64_t u = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += u;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
   __syncthreads();
-  if (threadIdx.x == 0) {  // n is tiny (<= 4096): a serial scan is ~microseconds and exact
-    int64_t run = 0;
-    for (int i = 0; i < n; ++i) {
-      const int64_t v = s[i];
-      s[i] = run;
-      run += v;
+  if (w == 0) {
+    int64_t x = lane < 16 ? wsum[lane] : 0;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const int64_t u = __shfl_up(x, o, kWave);
+      if (lane >= o) x += u;
     }
-    *tot = run;
+    if (lane < 16) wsum[lane] = x;  // inclusive scan of wave totals
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) a[i] = s[i];
+  int64_t run = (w > 0 ? wsum[w - 1] : 0) + inc - mine;  // exclusive prefix of this thread
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (4 * t + j < n) a[4 * t + j] = run;
+    run += v[j];
+  }
+  if (t == 0) *tot = wsum[15];
 }
 
 __global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(

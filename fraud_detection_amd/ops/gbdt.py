@@ -124,7 +124,16 @@ def quantile_cuts(X: torch.Tensor, max_bin: int = MAX_BIN, sample_rows: int = 1 
     samp = X[::stride][:per].contiguous()
     if comm is not None and world > 1:
         samp, _ = comm.all_gather_rows(samp)
-    return R.quantile_cuts(samp.float().cpu().numpy(), max_bin)
+    if not samp.is_cuda:
+        return R.quantile_cuts(samp.float().numpy(), max_bin)
+    # Device sort of the sample (rocPRIM radix sort through torch); only the max_bin - 1 quantile
+    # rows and the minimum row come back to the host, where deduplication is trivial.  Sorting is
+    # exact, so the cuts equal the CPU oracle's on the same sample.
+    m = samp.shape[0]
+    srt = torch.sort(samp.float(), dim=0).values
+    idx = torch.as_tensor((np.arange(1, max_bin, dtype=np.int64) * m) // max_bin, device=samp.device)
+    picks = torch.cat([srt[:1], srt.index_select(0, idx)]).cpu().numpy()
+    return R.cuts_from_sorted_picks(picks[1:], picks[0], max_bin)
 
 
 def bin_rows(X: torch.Tensor, cuts: np.ndarray, nbins: np.ndarray) -> torch.Tensor:
@@ -161,9 +170,27 @@ class _Workspace:
         self.iota = torch.arange(n, dtype=torch.int32, device=dev)
 
 
+def _resume(checkpoint, sig, T):
+    """Trees of a matching checkpoint (numpy arrays) and how many rounds they cover."""
+    if checkpoint is None:
+        return None, 0
+    got = checkpoint.latest(sig)
+    if got is None:
+        return None, 0
+    tensors, meta = got
+    t0 = min(int(meta["trees_done"]), T)
+    return {k: v.numpy()[:t0] for k, v in tensors.items()}, t0
+
+
 def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm=None,
-        cuts=None, sample_weight_pos: float | None = None, return_margin: bool = False):
-    """Boost `n_estimators` depth-D trees on standardized float32 rows X [n, d] with labels y."""
+        cuts=None, sample_weight_pos: float | None = None, return_margin: bool = False,
+        checkpoint=None, checkpoint_every: int = 10):
+    """Boost `n_estimators` depth-D trees on standardized float32 rows X [n, d] with labels y.
+
+    ``checkpoint``: a utils.checkpoint.CheckpointManager.  Every ``checkpoint_every`` rounds the
+    trees so far are saved; a later call with the same data/config resumes after the last saved
+    round.  Training margins are recomputed from the saved trees (bins and float thresholds agree
+    exactly), so a resumed fit is bit-identical to an uninterrupted one."""
     p = (params or GBDTParams()).validate()
     n, d = X.shape
     if d > MAX_FEAT:
@@ -181,18 +208,42 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     base_margin = float(np.log(p.base_score / (1.0 - p.base_score)))
     bins = bin_rows(X, cuts_np, nbins)
     ens_kw = dict(depth=D, cuts=cuts_np, nbins=nbins, base_score=p.base_score, params=dict(p.__dict__))
+    sig = None
+    if checkpoint is not None:
+        from ..utils.checkpoint import config_signature
+
+        n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
+        sig = config_signature(params={k: v for k, v in p.__dict__.items() if k != "n_estimators"}, spw=spw,
+                               cuts=cuts_np, nbins=nbins, n=n_all, d=d)
+    prev, t0 = _resume(checkpoint, sig, T)
+
+    def _partial(t_done, feat, binv, thr, gain, leaf):
+        return TreeEnsemble(feat=feat[:t_done], bin=binv[:t_done], thr=thr[:t_done], gain=gain[:t_done],
+                            leaf=leaf[:t_done], **ens_kw)
+
+    def _save(t_done, feat, binv, thr, gain, leaf):
+        if checkpoint is not None and t_done > 0:
+            checkpoint.save(t_done, {"feat": feat[:t_done], "bin": binv[:t_done], "thr": thr[:t_done],
+                                     "gain": gain[:t_done], "leaf": leaf[:t_done]},
+                            {"signature": sig, "trees_done": t_done, "kind": "gbdt"})
+
     if not X.is_cuda:
         feat = np.zeros((T, ni), np.int32); binv = np.zeros((T, ni), np.int32)
         thr = np.zeros((T, ni), np.float32); gain = np.zeros((T, ni)); leaf = np.zeros((T, nl), np.float32)
         b = bins.numpy()
         yy = y.numpy()
         margin = np.full(n, np.float32(base_margin), np.float32)
-        for t in range(T):
+        if t0:
+            feat[:t0], binv[:t0], thr[:t0], gain[:t0], leaf[:t0] = (prev[k] for k in ("feat", "bin", "thr", "gain", "leaf"))
+            margin = R.predict_margin(X.numpy(), feat[:t0], thr[:t0], leaf[:t0], D, base_margin)
+        for t in range(t0, T):
             q = R.gradients(margin, yy, spw, gscale, hscale)
             tr, node = R.build_tree(b, q, cuts_np, nbins, D, p.reg_lambda, p.min_child_weight, p.gamma,
                                     p.learning_rate, gscale, hscale, comm)
             feat[t], binv[t], thr[t], gain[t], leaf[t] = tr.feat, tr.bin, tr.thr, tr.gain, tr.leaf
             margin = (margin + tr.leaf[node]).astype(np.float32)
+            if (t + 1) % max(1, checkpoint_every) == 0 or t + 1 == T:
+                _save(t + 1, feat, binv, thr, gain, leaf)
         ens = TreeEnsemble(feat=feat, bin=binv, thr=thr, gain=gain, leaf=leaf, **ens_kw)
         return (ens, torch.from_numpy(margin)) if return_margin else ens
 
@@ -210,11 +261,15 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     gain = torch.empty((T, ni), dtype=torch.float64, device=dev)
     leaf = torch.empty((T, nl), dtype=torch.float32, device=dev)
     margin = torch.full((n,), base_margin, dtype=torch.float32, device=dev)
+    if t0:
+        for name, dst in (("feat", feat), ("bin", binv), ("thr", thr), ("gain", gain), ("leaf", leaf)):
+            dst[:t0].copy_(torch.from_numpy(np.ascontiguousarray(prev[name])))
+        margin = predict_margin(X, _partial(t0, prev["feat"], prev["bin"], prev["thr"], prev["gain"], prev["leaf"]))
     root = torch.tensor([[0, n]], dtype=torch.int64, device=dev)
     groot = torch.tensor([n_global], dtype=torch.int64, device=dev)
     lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
     ginv, hinv = 1.0 / gscale, 1.0 / hscale
-    for t in range(T):
+    for t in range(t0, T):
         m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), s)
         ws.hist.zero_()
         ws.seg[0:1].copy_(root)
@@ -244,6 +299,8 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(leaf[t]), s)
         if n:
             m.gbdt_margin(ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(leaf[t]), D, ptr(margin), s)
+        if checkpoint is not None and ((t + 1) % max(1, checkpoint_every) == 0 or t + 1 == T):
+            _save(t + 1, feat, binv, thr, gain, leaf)  # device -> host copy: syncs every k rounds only
     ens = TreeEnsemble(feat=feat.cpu().numpy(), bin=binv.cpu().numpy(), thr=thr.cpu().numpy(),
                        gain=gain.cpu().numpy(), leaf=leaf.cpu().numpy(), **ens_kw)
     return (ens, margin) if return_margin else ens

@@ -224,25 +224,50 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     return _info_from_state(ws.state.cpu().numpy())
 
 
+def _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm):
+    from ..utils.checkpoint import config_signature
+
+    n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
+    return config_signature(kind="sgd", n=n_all, d=d, C=C, lr=lr, momentum=momentum, batch_rows=batch_rows,
+                            class_w=list(class_w), fit_intercept=fit_intercept)
+
+
 def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float = 0.9, epochs: int = 5,
             batch_rows: int = 1 << 20, class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True,
-            comm=None, fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None) -> FitInfo:
+            comm=None, fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None,
+            checkpoint=None, checkpoint_every: int = 0) -> FitInfo:
     """Momentum minibatch SGD.  Each minibatch is a contiguous window of ``batch_rows`` rows of
-    this rank's shard (rows are stored pre-shuffled); DP all-reduces the minibatch gradient."""
+    this rank's shard (rows are stored pre-shuffled); DP all-reduces the minibatch gradient.
+
+    ``checkpoint`` (utils.checkpoint.CheckpointManager): every ``checkpoint_every`` minibatches
+    (and at each epoch end) the solver state -- weights, velocity, objective, step counter -- and
+    the data cursor (epoch, minibatch) are saved; a matching checkpoint is resumed from, giving
+    the same result as an uninterrupted fit."""
     check_rows(rows)
     w0 = _default_w0(w0)
     n = rows.shape[0]
+    sig = _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm) if checkpoint else None
+    got = checkpoint.latest(sig) if checkpoint is not None else None
+    start = (0, 0)
     if not rows.is_cuda:
-        return _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_intercept, comm, fp8_scale)
+        return _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_intercept, comm, fp8_scale,
+                            checkpoint, checkpoint_every, sig, got)
     m = native()
     ws = workspace or LRWorkspace(rows.device)
     ws.reset(w0, class_w)
+    if got is not None:
+        st = got[0]["state"].to(torch.float64)
+        ws.state.copy_(st.to(rows.device))
+        w32 = st[S_W:S_W + 32].to(torch.float32)
+        w32[LABEL_COL] = 0.0
+        ws.w32.copy_(w32.to(rows.device))
+        start = (int(got[1]["epoch"]), int(got[1]["batch"]))
     s = stream_of(rows)
     nb = max(1, (n + batch_rows - 1) // batch_rows)
     if comm is not None and comm.world_size > 1:
         nb = int(comm.all_reduce_scalar(nb, op="max"))
-    for _ in range(epochs):
-        for b in range(nb):
+    for ep in range(start[0], epochs):
+        for b in range(start[1] if ep == start[0] else 0, nb):
             lo = min(b * batch_rows, n)
             hi = min(lo + batch_rows, n)
             _pass(m, rows, ws, False, lo, hi, fp8_scale, s, done=False)
@@ -250,6 +275,12 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
                 comm.all_reduce_(ws.red[:64])
             m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), d, float(C), float(lr), float(momentum),
                          int(fit_intercept), s)
+            gstep = ep * nb + b + 1
+            last = b + 1 == nb
+            if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
+                nxt = (ep + 1, 0) if last else (ep, b + 1)
+                checkpoint.save(ep * nb + b + 1, {"state": ws.state},
+                                {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
     return _info_from_state(ws.state.cpu().numpy(), sgd=True)
 
 
@@ -282,7 +313,8 @@ def _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm,
                    objective=st.obj, grad_max=st.gmax, history=hist)
 
 
-def _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_intercept, comm, fp8_scale):
+def _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_intercept, comm, fp8_scale,
+                 checkpoint=None, checkpoint_every=0, sig=None, got=None):
     R = ref.rows_to_f32(rows, fp8_scale, d).double().numpy()
     n = R.shape[0]
     w = w0.copy()
@@ -292,8 +324,13 @@ def _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_
         nb = int(comm.all_reduce_scalar(nb, op="max"))
     obj = np.inf
     it = 0
-    for _ in range(epochs):
-        for b in range(nb):
+    start = (0, 0)
+    if got is not None:
+        st = got[0]["state"].numpy()
+        w, v, obj, it = st[S_W:S_W + 32].copy(), st[S_VEL:S_VEL + 32].copy(), float(st[S_OBJ]), int(st[S_ITER])
+        start = (int(got[1]["epoch"]), int(got[1]["batch"]))
+    for ep in range(start[0], epochs):
+        for b in range(start[1] if ep == start[0] else 0, nb):
             lo = min(b * batch_rows, n)
             hi = min(lo + batch_rows, n)
             red = _reduced_cpu(R[lo:hi], w, class_w, False, comm)
@@ -307,5 +344,12 @@ def _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_
             w = w + v
             obj = red[32] / S + 0.5 * reg * float(w[:d] @ w[:d])
             it += 1
+            last = b + 1 == nb
+            if checkpoint is not None and (last or (checkpoint_every and it % checkpoint_every == 0)):
+                st = np.zeros(STATE_SIZE)
+                st[S_W:S_W + 32], st[S_VEL:S_VEL + 32], st[S_OBJ], st[S_ITER] = w, v, obj, it
+                nxt = (ep + 1, 0) if last else (ep, b + 1)
+                checkpoint.save(ep * nb + b + 1, {"state": st},
+                                {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
     w[LABEL_COL] = 0.0
     return FitInfo(w=w, n_iter=it, n_newton_steps=0, converged=True, objective=obj, grad_max=float("nan"))

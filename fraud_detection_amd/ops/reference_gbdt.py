@@ -32,13 +32,23 @@ def quantile_cuts(sample: np.ndarray, max_bin: int = MAX_BIN):
         raise ValueError("max_bin must be in [2, 256]")
     cuts = np.full((d, MAX_BIN), np.inf, dtype=np.float32)
     nbins = np.zeros(d, dtype=np.int32)
+    if m == 0:
+        nbins[:] = 1
+        return cuts, nbins
     idx = (np.arange(1, max_bin, dtype=np.int64) * m) // max_bin
+    srt = np.sort(sample, axis=0)
+    return cuts_from_sorted_picks(srt[idx], srt[0], max_bin)
+
+
+def cuts_from_sorted_picks(picks: np.ndarray, vmin: np.ndarray, max_bin: int = MAX_BIN):
+    """picks [max_bin-1, d]: sample values at the quantile positions; vmin [d]: sample minimum."""
+    picks = np.asarray(picks, dtype=np.float32)
+    d = picks.shape[1]
+    cuts = np.full((d, MAX_BIN), np.inf, dtype=np.float32)
+    nbins = np.zeros(d, dtype=np.int32)
     for f in range(d):
-        v = np.sort(sample[:, f])
-        c = np.unique(v[idx]) if m > 0 else np.zeros(0, np.float32)
-        if m > 0:
-            c = c[c > v[0]]
-        c = c[: max_bin - 1]
+        c = np.unique(picks[:, f])
+        c = c[c > vmin[f]][: max_bin - 1]
         cuts[f, : len(c)] = c
         nbins[f] = len(c) + 1  # + the +inf cut
     return cuts, nbins

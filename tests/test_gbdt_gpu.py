@@ -108,3 +108,25 @@ def test_gbdt_pipeline_gpu_quality(dev):
     ev = res.evaluate(Xt, yt)
     assert ev["auc"] > 0.93, ev
     assert res.n_train_rows == 2 * (400_000 - int(y.sum()))
+
+
+def test_gbdt_device_resume_bit_identical(dev, tmp_path):
+    from fraud_detection_amd.utils.checkpoint import CheckpointManager
+
+    Xd, yd, X, y = _data(30_000, 10, seed=13)
+    p10 = gb.GBDTParams(n_estimators=10, max_depth=4)
+    cuts = R.quantile_cuts(X, 256)
+    full = gb.fit(Xd, yd, p10, cuts=cuts)
+    mgr = CheckpointManager(str(tmp_path), prefix="g")
+    gb.fit(Xd, yd, gb.GBDTParams(n_estimators=4, max_depth=4), cuts=cuts, checkpoint=mgr, checkpoint_every=2)
+    res = gb.fit(Xd, yd, p10, cuts=cuts, checkpoint=mgr, checkpoint_every=2)
+    for k in ("feat", "bin", "thr", "leaf"):
+        assert np.array_equal(getattr(res, k), getattr(full, k)), k
+
+
+def test_gbdt_deterministic_runs(dev):
+    Xd, yd, X, y = _data(50_000, 30, seed=14)
+    p = gb.GBDTParams(n_estimators=8, max_depth=5)
+    a, ma = gb.fit(Xd, yd, p, return_margin=True)
+    b, mb = gb.fit(Xd, yd, p, return_margin=True)
+    assert np.array_equal(a.leaf, b.leaf) and torch.equal(ma, mb)

@@ -169,6 +169,45 @@ def test_newton_progressive_same_solution(dev):
     np.testing.assert_allclose(prog.w[:31], base.w[:31], atol=1e-4)
 
 
+@pytest.mark.parametrize("d,fi", [(20, True), (30, False), (12, False)])
+def test_newton_generic_shapes(dev, d, fi):
+    """The generic (runtime-m) Newton update kernel, beside the m = 31 specialisation."""
+    X, y = _data(50_000, seed=30 + d, rate=0.05)
+    X = X[:, :d].contiguous()
+    st = S.scaler_fit(X)
+    rows = S.scale_cast(X, st, labels=y)
+    fit_g = L.newton_fit(rows.to(dev), d=d, fit_intercept=fi, tol=1e-7, max_iter=30)
+    fit_c = L.newton_fit(rows, d=d, fit_intercept=fi, tol=1e-7, max_iter=30)
+    assert fit_g.converged and fit_c.converged
+    np.testing.assert_allclose(fit_g.w[:31], fit_c.w[:31], rtol=1e-5, atol=1e-5)
+    if not fi:
+        assert fit_g.w[30] == 0.0
+
+
+def test_newton_lazy_hessian_same_solution(dev):
+    X, y = _data(200_000, seed=23, rate=0.02)
+    st = S.scaler_fit(X.to(dev))
+    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
+    base = L.newton_fit(rows, tol=1e-7, max_iter=40, hess_refresh=0, progressive=[])
+    lazy = L.newton_fit(rows, tol=1e-7, max_iter=40, hess_refresh=3, progressive=[(4, 2)])
+    assert base.converged and lazy.converged
+    np.testing.assert_allclose(lazy.w[:31], base.w[:31], atol=2e-5)
+
+
+def test_sgd_device_resume_bit_identical(dev, tmp_path):
+    from fraud_detection_amd.utils.checkpoint import CheckpointManager
+
+    X, y = _data(30_000, seed=24, rate=0.05)
+    st = S.scaler_fit(X.to(dev))
+    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
+    kw = dict(lr=0.3, epochs=3, batch_rows=4096)
+    full = L.sgd_fit(rows, **kw)
+    mgr = CheckpointManager(str(tmp_path), prefix="sgd")
+    L.sgd_fit(rows, **{**kw, "epochs": 1}, checkpoint=mgr, checkpoint_every=3)
+    res = L.sgd_fit(rows, **kw, checkpoint=mgr, checkpoint_every=3)
+    assert np.array_equal(res.w, full.w)
+
+
 def test_newton_deterministic(dev):
     X, y = _data(40_000, seed=12, rate=0.05)
     st = S.scaler_fit(X.to(dev))
