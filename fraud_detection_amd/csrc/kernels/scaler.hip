@@ -204,6 +204,9 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
                                        float* __restrict__ inv32) {
   const int c = threadIdx.x;
   if (c >= kCols) return;
+  // n < 0: the (all-reduced) row count rides in the unused slot sums[31] (one collective for the
+  // sums and the count, and no host round trip for n)
+  if (n < 0.0) n = sums[kCols - 1];
   if (c < d) {
     const double m = sums[c] / n;
     const double mean = (double)pivot[c] + m;

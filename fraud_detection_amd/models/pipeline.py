@@ -125,17 +125,24 @@ class DevicePipeline:
         scaler_ops.scale_cast(X, stats, labels=y, out_dtype=cfg.storage, out=rows_cap[:n], fp8_scale=cfg.fp8_scale)
         idx_min = pending.result()
         n_min = int(idx_min.shape[0])
+
+        def quota(n_r, nmin_r):
+            return max(0, int(round((n_r - nmin_r) * cfg.sampling_ratio)) - nmin_r) if (cfg.smote and nmin_r > 0) else 0
+
         n_maj = n - n_min
-        n_new = 0
-        if cfg.smote and n_min > 0:
-            n_new = max(0, int(round(n_maj * cfg.sampling_ratio)) - n_min)
+        n_new = quota(n, n_min)
         rows = rows_cap[: n + n_new]
+        # DP: one small all-gather of (minority, rows) per rank gives every rank the minority
+        # counts (for the row all-gather) and every rank's post-SMOTE size (for the identical
+        # Newton schedule) -- no further host-synchronising collectives in the fit.
+        ranks = comm.all_gather_ints([n_min, n]) if comm is not None else [[n_min, n]]
+        n_sched = min(r[1] + quota(r[1], r[0]) for r in ranks)
         tm.mark("scale_cast")
         if n_new > 0:
             # ---- minority rows in fp32, gathered across ranks (C3) -----------------------
             xmin = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min)
             if comm is not None:
-                xall, counts = comm.all_gather_rows(xmin)
+                xall, counts = comm.all_gather_rows(xmin, counts=[r[0] for r in ranks])
                 q_off = int(sum(counts[:rank]))
             else:
                 xall, q_off = xmin, 0
@@ -150,12 +157,9 @@ class DevicePipeline:
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
         class_w = (1.0, 1.0)
-        if cfg.class_weight == "balanced":
-            tot = float(n + n_new)
-            pos = float(n_min + n_new)
-            if comm is not None:
-                tot = comm.all_reduce_scalar(tot)
-                pos = comm.all_reduce_scalar(pos)
+        if cfg.class_weight == "balanced":  # global counts from the exchanged (minority, rows) pairs
+            tot = float(sum(r[1] + quota(r[1], r[0]) for r in ranks))
+            pos = float(sum(r[0] + quota(r[1], r[0]) for r in ranks))
             class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         # ---- K4: fit ---------------------------------------------------------------------
         if dev.type == "cuda" and (self._ws is None or self._ws.device != dev):
@@ -166,7 +170,8 @@ class DevicePipeline:
         if cfg.solver == "newton":
             fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
-                                    check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride)
+                                    check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride,
+                                    n_sched=n_sched)
         elif cfg.solver == "sgd":
             fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                  batch_rows=cfg.sgd_batch_rows, class_w=class_w, d=d, w0=w0,

@@ -145,7 +145,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
-               hess_refresh: int | str = "auto") -> FitInfo:
+               hess_refresh: int | str = "auto", n_sched: int | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
@@ -164,10 +164,15 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     s = stream_of(rows)
     n = rows.shape[0]
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
-    n_sched = n
+    # The warm-up schedule sets the number of collectives, so every rank must derive the same one:
+    # from ``n_sched`` (the smallest rank's row count, known to all ranks without a collective when
+    # the caller exchanged sizes already) or else from one min-all-reduce.  The Hessian stride is a
+    # rank-local choice (each rank rescales its own sub-sampled Hessian).
     if comm is not None and comm.world_size > 1:
-        hs = int(comm.all_reduce_scalar(hs, op="min"))  # identical H sampling rule on every rank
-        n_sched = int(comm.all_reduce_scalar(n, op="min"))  # identical warm-up schedule on every rank
+        if n_sched is None:
+            n_sched = int(comm.all_reduce_scalar(n, op="min"))
+    else:
+        n_sched = n
     sched = progressive_schedule(n_sched) if progressive == "auto" else list(progressive or [])
 
     # Progressive warm-up: Newton steps on uniform 1/sub tile subsets (never "converge": tol=0),

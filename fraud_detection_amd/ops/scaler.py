@@ -15,9 +15,10 @@ _SCALER_BLOCKS = 2048  # 8 resident blocks per CU x 256 CUs
 
 @dataclass
 class ScalerStats:
-    """StandardScaler parameters; fp64 for sklearn export, fp32 copies feed the kernels."""
+    """StandardScaler parameters; fp64 for sklearn export, fp32 copies feed the kernels.
+    ``n`` may be given as a device tensor (the all-reduced count): it is read on first use."""
 
-    n: float
+    n_src: object          # float, or a 1-element device tensor holding the row count
     d: int
     mean64: torch.Tensor   # [32] float64
     var64: torch.Tensor    # [32] float64
@@ -25,8 +26,14 @@ class ScalerStats:
     mean32: torch.Tensor   # [32] float32
     inv32: torch.Tensor    # [32] float32 (0 beyond d)
 
+    @property
+    def n(self) -> float:
+        if isinstance(self.n_src, torch.Tensor):
+            self.n_src = float(self.n_src.item())
+        return float(self.n_src)
+
     def to(self, device) -> "ScalerStats":
-        return ScalerStats(self.n, self.d, *(t.to(device) for t in
+        return ScalerStats(self.n_src, self.d, *(t.to(device) for t in
                                              (self.mean64, self.var64, self.scale64, self.mean32, self.inv32)))
 
     def numpy(self):
@@ -61,8 +68,11 @@ def scaler_partial_sums(X: torch.Tensor, pivot: torch.Tensor) -> torch.Tensor:
     return sums
 
 
-def scaler_finalize(sums: torch.Tensor, n_total: float, pivot: torch.Tensor, d: int) -> ScalerStats:
+def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int) -> ScalerStats:
+    """``n_total`` None: the count is in sums[31] (device) -- see scaler_fit."""
     dev = sums.device
+    if n_total is None and not sums.is_cuda:
+        n_total = float(sums[31])
     if not sums.is_cuda:
         mean, var, scale, m32, i32 = ref.scaler_finalize(sums.numpy(), float(n_total), pivot.cpu().numpy(), d)
         return ScalerStats(float(n_total), d, torch.from_numpy(mean), torch.from_numpy(var),
@@ -75,9 +85,10 @@ def scaler_finalize(sums: torch.Tensor, n_total: float, pivot: torch.Tensor, d: 
     scale64 = torch.empty_like(mean64)
     mean32 = torch.empty(32, device=dev, dtype=torch.float32)
     inv32 = torch.empty_like(mean32)
-    m.scaler_finalize(ptr(sums), float(n_total), ptr(piv), d, ptr(mean64), ptr(var64), ptr(scale64),
-                      ptr(mean32), ptr(inv32), stream_of(sums))
-    return ScalerStats(float(n_total), d, mean64, var64, scale64, mean32, inv32)
+    m.scaler_finalize(ptr(sums), -1.0 if n_total is None else float(n_total), ptr(piv), d, ptr(mean64), ptr(var64),
+                      ptr(scale64), ptr(mean32), ptr(inv32), stream_of(sums))
+    n_src = sums[31:32] if n_total is None else float(n_total)
+    return ScalerStats(n_src, d, mean64, var64, scale64, mean32, inv32)
 
 
 def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) -> ScalerStats:
@@ -90,11 +101,12 @@ def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) ->
         if comm is not None and comm.world_size > 1:
             pivot = comm.broadcast(pivot.contiguous(), src=0)
     sums = scaler_partial_sums(X, pivot)
-    n_total = float(n)
     if comm is not None and comm.world_size > 1:
+        # count rides in the unused slot 31 (d <= 30): one all-reduce, no host sync
+        sums[31:32].fill_(float(n))
         sums = comm.all_reduce(sums)
-        n_total = float(comm.all_reduce_scalar(float(n)))
-    return scaler_finalize(sums, n_total, pivot, d)
+        return scaler_finalize(sums, None, pivot, d)
+    return scaler_finalize(sums, float(n), pivot, d)
 
 
 def scale_cast(X: torch.Tensor, stats: ScalerStats, labels: torch.Tensor | None = None,

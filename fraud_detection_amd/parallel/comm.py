@@ -110,16 +110,29 @@ class Communicator:
             dist.broadcast(t, src=src)
         return t
 
-    def all_gather_rows(self, x: torch.Tensor):
+    def all_gather_ints(self, vals) -> list:
+        """All-gather a short list of ints from every rank (one small collective + one sync)."""
+        if self.world_size == 1:
+            return [list(vals)]
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        t = torch.tensor(list(vals), dtype=torch.int64, device=dev)
+        out = [torch.zeros_like(t) for _ in range(self.world_size)]
+        dist.all_gather(out, t)
+        return torch.stack(out).cpu().tolist()
+
+    def all_gather_rows(self, x: torch.Tensor, counts: list | None = None):
         """Variable-length all-gather along dim 0 (collective C3, SMOTE minority rows).
-        Returns (concatenated tensor, list of per-rank row counts)."""
+        Returns (concatenated tensor, list of per-rank row counts).  ``counts``: the per-rank row
+        counts when the caller already exchanged them (saves a collective and a host sync)."""
         if self.world_size == 1:
             return x, [x.shape[0]]
         dev = x.device
-        n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
-        counts = [torch.zeros_like(n) for _ in range(self.world_size)]
-        dist.all_gather(counts, n)
-        counts = [int(c.item()) for c in counts]
+        if counts is None:
+            n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
+            cl = [torch.zeros_like(n) for _ in range(self.world_size)]
+            dist.all_gather(cl, n)
+            counts = [int(c.item()) for c in cl]
+        counts = [int(c) for c in counts]
         mx = max(counts)
         pad = torch.zeros((mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=dev)
         pad[: x.shape[0]] = x
