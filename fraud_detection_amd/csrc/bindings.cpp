@@ -104,9 +104,10 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("logreg_reduce", [](u partial, int nblocks, int ncols, u out, u done, u s) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });
-  m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi, u s) {
+  m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi,
+                            int phase_start, u s) {
     fdx::launch_newton_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), d, C, tol,
-                              max_iter, fi, S(s));
+                              max_iter, fi, phase_start, S(s));
   });
   m.def("sgd_update", [](u red, u state, u w32, int d, double C, double lr, double mom, int fi, u s) {
     fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), d, C, lr, mom, fi, S(s));

@@ -71,7 +71,7 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
-                          double C, double tol, int max_iter, int fit_intercept,
+                          double C, double tol, int max_iter, int fit_intercept, int phase_start,
                           hipStream_t stream);
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
                        double momentum, int fit_intercept, hipStream_t stream);

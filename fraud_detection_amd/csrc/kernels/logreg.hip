@@ -263,7 +263,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
                                                            float* __restrict__ w32,
                                                            int* __restrict__ done, int d, double C,
                                                            double tol, int max_iter,
-                                                           int fit_intercept) {
+                                                           int fit_intercept, int phase_start) {
   __shared__ double sr[kLRPartStride];
   __shared__ double ss[kStateSize];
   __shared__ double grad[32];
@@ -303,11 +303,14 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   const double obj = sr[32] * invS + 0.5 * reg * w2;
   const double gmax = ga;
   const int it = (int)ss[kIter];
-  const double prev = ss[kObjPrev];
+  // phase_start: first iteration of a progressive-Newton phase -- objectives of different row
+  // samples are not comparable, so no backtracking against the previous phase.
+  const double prev = phase_start ? __builtin_inf() : ss[kObjPrev];
+  const double nbt = phase_start ? 0.0 : ss[kBacktracks];
   // Backtrack only on a real increase: the loss is accumulated in fp32 per block (relative
   // noise ~1e-7), so near the optimum a true decrease can hide below that noise floor.
   int dec;
-  if (it > 0 && obj > prev + 1e-6 * fabs(prev) && ss[kBacktracks] < 40.0) dec = 1;
+  if (it > 0 && obj > prev + 1e-6 * fabs(prev) && nbt < 40.0) dec = 1;
   else if (gmax <= tol) dec = 2;
   else dec = 0;
   __syncthreads();
@@ -320,7 +323,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       ss[kStep + t] *= 0.5;
       ss[kW + t] = ss[kWPrev + t] + ss[kStep + t];
     }
-    if (t == 0) ss[kBacktracks] += 1.0;
+    if (t == 0) ss[kBacktracks] = nbt + 1.0;
   } else if (dec == 2) {
     if (t == 0) {
       ss[kConverged] = 1.0;
@@ -497,12 +500,14 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 }
 
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
-                          double C, double tol, int max_iter, int fit_intercept,
+                          double C, double tol, int max_iter, int fit_intercept, int phase_start,
                           hipStream_t stream) {
   if (d + (fit_intercept ? 1 : 0) == 31)  // 30 features + intercept: the specialised stream
-    newton_update_kernel<31><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept);
+    newton_update_kernel<31><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
+                                                   phase_start);
   else
-    newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept);
+    newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
+                                                  phase_start);
   check_launch("newton_update");
 }
 

@@ -393,6 +393,90 @@ __global__ __launch_bounds__(kCompactThreads) void compact_count_kernel(
   }
 }
 
+// ---- vectorised compaction: 16 labels per thread (one 16-byte load) --------------------------
+// Bit 7 of each byte of the result is set iff that byte of x equals the pattern byte (exact: the
+// masked add cannot borrow across bytes).
+__device__ __forceinline__ uint32_t match_bytes(uint32_t x, uint32_t pat) {
+  const uint32_t v = x ^ pat;
+  const uint32_t y = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(y | v | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t nibble_of(uint32_t m) {  // bits 7,15,23,31 -> bits 0..3
+  return ((m >> 7) & 1u) | ((m >> 14) & 2u) | ((m >> 21) & 4u) | ((m >> 28) & 8u);
+}
+// 16-bit match mask of label group g (labels [16g, 16g+16) clipped to n)
+__device__ __forceinline__ uint32_t group_mask(const uint8_t* __restrict__ labels, int64_t n, int64_t g,
+                                               int target, uint32_t pat) {
+  if (16 * g + 16 <= n) {
+    const uint4 v = reinterpret_cast<const uint4*>(labels)[g];
+    return nibble_of(match_bytes(v.x, pat)) | (nibble_of(match_bytes(v.y, pat)) << 4) |
+           (nibble_of(match_bytes(v.z, pat)) << 8) | (nibble_of(match_bytes(v.w, pat)) << 12);
+  }
+  uint32_t m = 0;
+  for (int j = 0; j < 16 && 16 * g + j < n; ++j) m |= (labels[16 * g + j] == target ? 1u : 0u) << j;
+  return m;
+}
+__device__ __forceinline__ void group_range(int64_t ngroups, int64_t* lo, int64_t* hi) {
+  const int64_t per = (ngroups + gridDim.x - 1) / gridDim.x;
+  *lo = min((int64_t)blockIdx.x * per, ngroups);
+  *hi = min(*lo + per, ngroups);
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_count16_kernel(
+    const uint8_t* __restrict__ labels, int64_t n, int target, int64_t* __restrict__ counts) {
+  int64_t lo, hi;
+  group_range((n + 15) / 16, &lo, &hi);
+  const uint32_t pat = 0x01010101u * (uint32_t)(target & 0xff);
+  int64_t c = 0;
+  for (int64_t g = lo + threadIdx.x; g < hi; g += kCompactThreads) c += __popc(group_mask(labels, n, g, target, pat));
+  c = wave_sum(c);
+  __shared__ int64_t red[kCompactThreads / kWave];
+  if (lane_id() == 0) red[wave_id()] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int64_t t = 0;
+    for (int w = 0; w < kCompactThreads / kWave; ++w) t += red[w];
+    counts[blockIdx.x] = t;
+  }
+}
+
+__global__ __launch_bounds__(kCompactThreads) void compact_write16_kernel(
+    const uint8_t* __restrict__ labels, int64_t n, int target, const int64_t* __restrict__ offsets,
+    int64_t* __restrict__ out_idx) {
+  int64_t lo, hi;
+  group_range((n + 15) / 16, &lo, &hi);
+  const uint32_t pat = 0x01010101u * (uint32_t)(target & 0xff);
+  __shared__ int wave_tot[kCompactThreads / kWave];
+  const int lane = lane_id(), w = wave_id();
+  int64_t base = offsets[blockIdx.x];
+  for (int64_t g0 = lo; g0 < hi; g0 += kCompactThreads) {  // block-uniform trip count
+    const int64_t g = g0 + threadIdx.x;
+    uint32_t m = g < hi ? group_mask(labels, n, g, target, pat) : 0u;
+    const int c = __popc(m);
+    int inc = c;  // inclusive scan within the wave
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int u = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += u;
+    }
+    if (lane == kWave - 1) wave_tot[w] = inc;
+    __syncthreads();
+    int64_t off = base + inc - c;
+    int total = 0;
+    for (int i = 0; i < kCompactThreads / kWave; ++i) {
+      if (i < w) off += wave_tot[i];
+      total += wave_tot[i];
+    }
+    while (m) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1;
+      out_idx[off++] = 16 * g + j;
+    }
+    base += total;
+    __syncthreads();
+  }
+}
+
 // In-place exclusive scan of a small int64 array (n <= 4096), one block of 1024 threads; writes
 // the total to tot.  Each thread owns 4 consecutive elements; lane totals are scanned with wave
 // shuffles, wave totals by wave 0 -- integer adds, so the result is exact and order-free.
@@ -525,9 +609,16 @@ void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* 
   check_launch("scale_cast");
 }
 
+// Vector path when the label array is 16-byte aligned (torch allocations are); count and write
+// make the same choice from the same pointer, so their per-block ranges agree.
+static inline bool compact_vec(const uint8_t* labels) { return (reinterpret_cast<uintptr_t>(labels) & 15) == 0; }
+
 void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t* counts,
                           int nblocks, hipStream_t stream) {
-  compact_count_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, counts);
+  if (compact_vec(labels))
+    compact_count16_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, counts);
+  else
+    compact_count_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, counts);
   check_launch("compact_count");
 }
 void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream) {
@@ -536,8 +627,10 @@ void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t 
 }
 void launch_compact_write(const uint8_t* labels, int64_t n, int target, const int64_t* offsets,
                           int64_t* out_idx, int nblocks, hipStream_t stream) {
-  compact_write_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, offsets,
-                                                                out_idx);
+  if (compact_vec(labels))
+    compact_write16_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, offsets, out_idx);
+  else
+    compact_write_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, offsets, out_idx);
   check_launch("compact_write");
 }
 

@@ -44,7 +44,7 @@ class TrainConfig:
     sgd_momentum: float = 0.9
     sgd_epochs: int = 5
     sgd_batch_rows: int = 1 << 22
-    check_every: int = 4
+    check_every: int = 1            # Newton: iterations per convergence-flag read (host reads one chunk behind)
     init_std: float = 0.01          # random-init weights ~ N(0, init_std^2) (seeded by `seed`)
     hess_stride: int | str = "auto"  # Newton: Hessian from every k-th row tile (gradient always exact)
 

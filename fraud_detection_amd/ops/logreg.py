@@ -48,31 +48,35 @@ class LRWorkspace:
         self.nblocks = nblocks or m.logreg_pass_blocks()
         self.partial = torch.empty(self.nblocks * PART_STRIDE, device=device, dtype=torch.float32)
         self.red = torch.zeros(PART_STRIDE, device=device, dtype=torch.float64)
-        self.state = torch.zeros(STATE_SIZE, device=device, dtype=torch.float64)
-        self.w32 = torch.zeros(NCOLS, device=device, dtype=torch.float32)
-        self.done = torch.zeros(1, device=device, dtype=torch.int32)
-        self.class_w = torch.ones(2, device=device, dtype=torch.float32)
+        # state (f64[256]) | w32 (f32[32]) | class_w (f32[2]) | done (i32): one device blob, so a
+        # reset is ONE async copy from a pinned mirror of the same layout
+        self._blob = torch.zeros(_BLOB_BYTES, device=device, dtype=torch.uint8)
+        self.state, self.w32, self.class_w, self.done = _blob_views(self._blob)
 
     def reset(self, w0: np.ndarray, class_w=(1.0, 1.0)):
-        """Initial state via pinned staging + async H2D copies (no stream drain).  The staging
-        buffers are only rewritten after the previous fit's final state read-back synchronised."""
-        if not hasattr(self, "_st_h"):
-            self._st_h = torch.zeros(STATE_SIZE, dtype=torch.float64, pin_memory=True)
-            self._w_h = torch.zeros(NCOLS, dtype=torch.float32, pin_memory=True)
-            self._cw_h = torch.zeros(2, dtype=torch.float32, pin_memory=True)
-        st = self._st_h.numpy()
+        """Initial state via pinned staging + one async H2D copy (no stream drain).  The staging
+        buffer is only rewritten after the previous fit's final state read-back synchronised."""
+        if not hasattr(self, "_blob_h"):
+            self._blob_h = torch.zeros(_BLOB_BYTES, dtype=torch.uint8, pin_memory=True)
+            self._views_h = [v.numpy() for v in _blob_views(self._blob_h)]
+        st, w32, cw, done = self._views_h
         st[:] = 0.0
         st[S_W:S_W + 32] = w0
         st[S_WPREV:S_WPREV + 32] = w0
         st[S_OBJPREV] = np.inf
-        w32 = self._w_h.numpy()
         w32[:] = np.asarray(w0, dtype=np.float32)
         w32[LABEL_COL] = 0
-        self._cw_h.numpy()[:] = class_w
-        self.state.copy_(self._st_h, non_blocking=True)
-        self.w32.copy_(self._w_h, non_blocking=True)
-        self.class_w.copy_(self._cw_h, non_blocking=True)
-        self.done.zero_()
+        cw[:] = class_w
+        done[:] = 0
+        self._blob.copy_(self._blob_h, non_blocking=True)
+
+
+_BLOB_BYTES = 2304
+
+
+def _blob_views(blob: torch.Tensor):
+    return (blob[0:2048].view(torch.float64), blob[2048:2176].view(torch.float32),
+            blob[2176:2184].view(torch.float32), blob[2184:2188].view(torch.int32))
 
 
 HESS_SAMPLE_ROWS = 1 << 22  # auto Hessian sub-sampling keeps >= ~4M rows in the H estimate
@@ -178,16 +182,18 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     # Progressive warm-up: Newton steps on uniform 1/sub tile subsets (never "converge": tol=0),
     # then full-data Newton until the exact gradient meets `tol`.  Between phases the objective
     # history is reset so backtracking only compares objectives of the same sample.
+    # phase_start=1 on a phase's first iteration: the kernel forgets the previous phase's objective
+    # and backtrack count (no extra fill kernels between phases).
+    first = [0]
     for sub, iters in sched:
         hs_w = auto_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
-        for _ in range(iters):
+        for j in range(iters):
             _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub)
             if comm is not None and comm.world_size > 1:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
-                            int(fit_intercept), s)
-        ws.state[S_OBJPREV].fill_(float("inf"))
-        ws.state[S_BACKTRACKS].zero_()
+                            int(fit_intercept), int(j == 0), s)
+        first[0] = 1
     warm = sum(it for _, it in sched)
 
     refresh = auto_hess_refresh(n_sched) if hess_refresh == "auto" else int(hess_refresh)
@@ -202,7 +208,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                 # a gradient-only pass leaves the (already all-reduced) Hessian in red[64:]
                 comm.all_reduce_(ws.red if fresh else ws.red[:64])
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
-                            int(max_iter + warm), int(fit_intercept), s)
+                            int(max_iter + warm), int(fit_intercept), first[0], s)
+            first[0] = 0
         return k
 
     # Convergence is checked one chunk behind: chunk i+1 is already queued when the host reads

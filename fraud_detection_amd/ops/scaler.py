@@ -50,6 +50,16 @@ def _check_X(X: torch.Tensor) -> None:
         raise ValueError("X must be row-major with unit column stride")
 
 
+def _pivot_dev(pivot: torch.Tensor, d: int, dev) -> torch.Tensor:
+    """The kernels read pivot[c] for c < d only: a contiguous fp32 device row is used in place."""
+    if pivot.is_cuda and pivot.device == dev and pivot.dtype == torch.float32 and pivot.is_contiguous() \
+            and pivot.numel() >= d:
+        return pivot
+    piv = torch.zeros(NCOLS, device=dev, dtype=torch.float32)
+    piv[:d] = pivot[:d].to(dev, torch.float32)
+    return piv
+
+
 def scaler_partial_sums(X: torch.Tensor, pivot: torch.Tensor) -> torch.Tensor:
     """Shifted fp64 sums [64] = (sum(x - pivot) | sum((x - pivot)^2)) over the rows of X."""
     _check_X(X)
@@ -57,8 +67,7 @@ def scaler_partial_sums(X: torch.Tensor, pivot: torch.Tensor) -> torch.Tensor:
     if not X.is_cuda:
         return torch.from_numpy(ref.scaler_sums(X.numpy(), pivot.cpu().numpy()))
     m = native()
-    piv = torch.zeros(NCOLS, device=X.device, dtype=torch.float32)
-    piv[:d] = pivot[:d]
+    piv = _pivot_dev(pivot, d, X.device)
     nb = min(_SCALER_BLOCKS, max(1, (n + 255) // 256))
     partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
     sums = torch.empty(64, device=X.device, dtype=torch.float64)
@@ -78,8 +87,7 @@ def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int) ->
         return ScalerStats(float(n_total), d, torch.from_numpy(mean), torch.from_numpy(var),
                            torch.from_numpy(scale), torch.from_numpy(m32), torch.from_numpy(i32))
     m = native()
-    piv = torch.zeros(NCOLS, device=dev, dtype=torch.float32)
-    piv[:d] = pivot[:d]
+    piv = _pivot_dev(pivot, d, dev)
     mean64 = torch.empty(32, device=dev, dtype=torch.float64)
     var64 = torch.empty_like(mean64)
     scale64 = torch.empty_like(mean64)
@@ -97,9 +105,11 @@ def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) ->
     _check_X(X)
     n, d = X.shape
     if pivot is None:
-        pivot = X[0].clone() if n > 0 else torch.zeros(d, device=X.device)
         if comm is not None and comm.world_size > 1:
+            pivot = X[0].clone() if n > 0 else torch.zeros(d, device=X.device)
             pivot = comm.broadcast(pivot.contiguous(), src=0)
+        else:
+            pivot = X[0] if n > 0 else torch.zeros(d, device=X.device)  # a view: no copy kernel
     sums = scaler_partial_sums(X, pivot)
     if comm is not None and comm.world_size > 1:
         # count rides in the unused slot 31 (d <= 30): one all-reduce, no host sync

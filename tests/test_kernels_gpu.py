@@ -309,3 +309,16 @@ def test_auc_exact(dev, n, rate, quant):
     assert auc == pytest.approx(roc_auc_score(y, s), abs=1e-12)
     cm = M.confusion_counts(torch.from_numpy(s).to(dev), torch.from_numpy(y).to(dev), 0.3)
     assert np.array_equal(cm, ref.confusion(s, y, 0.3))
+
+
+@pytest.mark.parametrize("n", [1, 15, 16, 17, 4095, 100_003, 2_000_001])
+@pytest.mark.parametrize("offset", [0, 3])
+def test_compact_indices_exact(dev, n, offset):
+    """Vectorised (16-byte aligned) and scalar (offset view) compaction == torch.nonzero."""
+    g = torch.Generator().manual_seed(n)
+    lab = (torch.rand(n + offset, generator=g) < 0.3).to(torch.uint8).to(dev)
+    view = lab[offset:]
+    for target in (0, 1):
+        got = S.compact_indices(view, target)
+        ref_idx = torch.nonzero(view == target).reshape(-1)
+        assert torch.equal(got, ref_idx)

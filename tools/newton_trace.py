@@ -65,7 +65,7 @@ def main():
         for phase, (sub, iters) in enumerate(sched + [(1, 25)]):
             full = sub == 1
             hs_w = hs if full else L.auto_hess_stride(n // sub)
-            for _ in range(iters):
+            for jj in range(iters):
                 if full:
                     fresh = refresh <= 0 or j_full % refresh == 0
                     j_full += 1
@@ -74,7 +74,7 @@ def main():
                 t0 = time.perf_counter()
                 L._pass(m, rows, ws, hs_w, 0, n, 4.0, s, sub=sub)
                 m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0,
-                                a.tol if full else 0.0, 1 << 30, 1, s)
+                                a.tol if full else 0.0, 1 << 30, 1, int(jj == 0 and phase > 0), s)
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) * 1e6
                 st = ws.state.cpu().numpy()
@@ -82,9 +82,6 @@ def main():
                                   bt=int(st[L.S_BACKTRACKS]), us=round(dt, 1)))
                 if int(ws.done.item()):
                     break
-            if not full:
-                ws.state[L.S_OBJPREV].fill_(float("inf"))
-                ws.state[L.S_BACKTRACKS].zero_()
         full_passes = sum(1 for t in trace if t["sub"] == 1)
         tot = sum(t["us"] for t in trace)
         print(f"== {name:14s} passes {len(trace):2d} (full {full_passes})  sum {tot:8.1f} us  final gmax {trace[-1]['gmax']:.2e} obj {trace[-1]['obj']:.9f}")
