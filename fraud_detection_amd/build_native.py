@@ -60,6 +60,10 @@ def _run(cmd: list[str]) -> None:
 
 
 COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
+# Per-file code generation options.  knn.hip: MFMA accumulators in arch VGPRs (gfx950's unified
+# register file) -- its 16-float score tile is consumed by VALU right after every MFMA chain, and
+# the AGPR form costs 32 v_accvgpr moves per 32x32 tile.
+PER_FILE_FLAGS = {"knn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
 
 
 def _compile(src: str, obj: str, headers: list[str], force: bool, extra: list[str]) -> str:
@@ -78,7 +82,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     tasks = []
     for src in kern_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        tasks.append((src, obj, inc))
+        tasks.append((src, obj, inc + PER_FILE_FLAGS.get(os.path.basename(src), [])))
     bind_src = os.path.join(CSRC, "bindings.cpp")
     tasks.append((bind_src, os.path.join(BUILD, "bindings.o"), inc + _py_includes()))
     comm_src = os.path.join(CSRC, "comm", "rccl_comm.cpp")

@@ -178,6 +178,12 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
 
   // auc / confusion
+  m.def("auc_hist", [](u scores, u labels, int64_t n, int bits, u hist, u s) {
+    fdx::launch_auc_hist(P<const float>(scores), P<const uint8_t>(labels), n, bits, P<unsigned>(hist), S(s));
+  });
+  m.def("auc_hist_reduce", [](u hist, int bits, u out, u s) {
+    fdx::launch_auc_hist_reduce(P<const unsigned>(hist), bits, P<unsigned long long>(out), S(s));
+  });
   m.def("auc_compact", [](u scores, u labels, int64_t n, u pos, u counter, u s) {
     fdx::launch_auc_compact(P<const float>(scores), P<const uint8_t>(labels), n, P<float>(pos),
                             P<unsigned long long>(counter), S(s));

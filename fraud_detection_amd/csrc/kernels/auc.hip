@@ -123,6 +123,77 @@ __global__ __launch_bounds__(kThreads) void confusion_kernel(const float* __rest
   }
 }
 
+// ---- histogram AUC (mergeable across ranks) ---------------------------------------------------
+// Order-preserving u32 key of a float: larger float -> larger key (incl. negatives, -0 < +0).
+__device__ __forceinline__ uint32_t order_key(float f) {
+  uint32_t b = __float_as_uint(f);
+  if (b == 0x80000000u) b = 0u;  // -0 == +0 (ties, as in the exact AUC)
+  return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+
+// hist[label][key >> (32 - bits)] += 1 for every score; u32 global atomics on 2 x 2^bits
+// counters (2^20 by default: spread enough that contention is negligible).
+__global__ __launch_bounds__(kThreads) void auc_hist_kernel(const float* __restrict__ scores,
+                                                            const uint8_t* __restrict__ labels, int64_t n,
+                                                            int bits, unsigned* __restrict__ hist) {
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  const int sh = 32 - bits;
+  const int64_t nb = (int64_t)1 << bits;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += stride) {
+    const uint32_t b = order_key(scores[i]) >> sh;
+    atomicAdd(&hist[(labels[i] != 0 ? nb : 0) + b], 1u);
+  }
+}
+
+// out[0] = sum_b P_b (2 N_<b + N_b)  (twice the tie-averaged pair count, exact u64),
+// out[1] = P, out[2] = N.  One block of 1024 threads, each scanning a contiguous range of bins.
+__global__ __launch_bounds__(1024) void auc_hist_reduce_kernel(const unsigned* __restrict__ hist, int bits,
+                                                               unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long wsum[16];
+  __shared__ unsigned long long red[3][16];
+  const int64_t nb = (int64_t)1 << bits;
+  const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+  const int64_t per = (nb + 1023) / 1024;
+  const int64_t lo = min((int64_t)t * per, nb), hi = min(lo + per, nb);
+  const unsigned* neg = hist;
+  const unsigned* pos = hist + nb;
+  unsigned long long nsum = 0, psum = 0;
+  for (int64_t b = lo; b < hi; ++b) { nsum += neg[b]; psum += pos[b]; }
+  unsigned long long inc = nsum;  // block exclusive scan of the per-thread negative counts
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const unsigned long long u = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += u;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  if (w == 0) {
+    unsigned long long x = lane < 16 ? wsum[lane] : 0ull;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const unsigned long long u = __shfl_up(x, o, kWave);
+      if (lane >= o) x += u;
+    }
+    if (lane < 16) wsum[lane] = x;
+  }
+  __syncthreads();
+  unsigned long long nbefore = (w > 0 ? wsum[w - 1] : 0ull) + inc - nsum;
+  unsigned long long num = 0;
+  for (int64_t b = lo; b < hi; ++b) {
+    const unsigned long long nb_ = neg[b], pb = pos[b];
+    num += pb * (2ull * nbefore + nb_);
+    nbefore += nb_;
+  }
+  num = wave_sum(num); psum = wave_sum(psum); nsum = wave_sum(nsum);
+  if (lane == 0) { red[0][w] = num; red[1][w] = psum; red[2][w] = nsum; }
+  __syncthreads();
+  if (t < 3) {
+    unsigned long long a = 0;
+    for (int i = 0; i < 16; ++i) a += red[t][i];
+    out[t] = a;
+  }
+}
+
 }  // namespace
 
 void launch_auc_compact(const float* scores, const uint8_t* labels, int64_t n, float* pos,
@@ -156,6 +227,20 @@ void launch_confusion(const float* scores, const uint8_t* labels, int64_t n, flo
   const int grid = stream_grid(n, kThreads * 8, 1024);
   confusion_kernel<<<grid, kThreads, 0, stream>>>(scores, labels, n, threshold, out4);
   check_launch("confusion");
+}
+
+void launch_auc_hist(const float* scores, const uint8_t* labels, int64_t n, int bits, unsigned* hist,
+                     hipStream_t stream) {
+  if (bits < 8 || bits > 24) throw std::runtime_error("auc_hist: bits must be in [8, 24]");
+  if (n <= 0) return;
+  const int grid = stream_grid(n, kThreads, 4096);
+  auc_hist_kernel<<<grid, kThreads, 0, stream>>>(scores, labels, n, bits, hist);
+  check_launch("auc_hist");
+}
+
+void launch_auc_hist_reduce(const unsigned* hist, int bits, unsigned long long* out, hipStream_t stream) {
+  auc_hist_reduce_kernel<<<1, 1024, 0, stream>>>(hist, bits, out);
+  check_launch("auc_hist_reduce");
 }
 
 }  // namespace fdx

@@ -14,6 +14,8 @@
 // the 4 waves merge their lists through LDS.  Ties break on the smaller candidate index.
 // K-index layout: MFMA step s, slot h <-> feature 16h + s, so each lane's operand for all 16
 // steps is 16 CONTIGUOUS floats of one row (four 16 B loads).
+#include <cmath>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -48,7 +50,7 @@ __global__ void row_half_norms_kernel(const float* __restrict__ X, int m, float*
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= m_pad) return;
   if (r >= m) {
-    out[r] = 3.0e38f;  // padding candidates can never be selected
+    out[r] = -3.0e38f;  // padding candidates can never be selected
     return;
   }
   const float4* p = reinterpret_cast<const float4*>(X + (int64_t)r * kCols);
@@ -58,7 +60,7 @@ __global__ void row_half_norms_kernel(const float* __restrict__ X, int m, float*
     const float4 v = p[k];
     s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
   }
-  out[r] = 0.5f * s;
+  out[r] = -0.5f * s;  // stored negated: it initialises the MFMA accumulator directly
 }
 
 // Q: [mq_pad][32] fp32 queries, C: [mc_pad][32] fp32 candidates, chalf: [mc_pad] 0.5||c||^2.
@@ -121,14 +123,22 @@ __global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restr
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       ac[4 * k] = cv[k].x; ac[4 * k + 1] = cv[k].y; ac[4 * k + 2] = cv[k].z; ac[4 * k + 3] = cv[k].w;
-      acc[4 * k] = -nv[k].x; acc[4 * k + 1] = -nv[k].y; acc[4 * k + 2] = -nv[k].z; acc[4 * k + 3] = -nv[k].w;
+      acc[4 * k] = nv[k].x; acc[4 * k + 1] = nv[k].y; acc[4 * k + 2] = nv[k].z; acc[4 * k + 3] = nv[k].w;
     }
     if (t + kWaves < ntiles) fetch(t + kWaves, cv, nv);
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[s], bq[s], acc, 0, 0, 0);
-    // Filter: a candidate can only enter the list if it beats the CURRENT k-th best (which only
-    // improves), so 16 compares build a bitmask; the tile's scores are parked in this lane's LDS
-    // row and only set bits are inserted (dynamic index via LDS, not register arrays).
+    // Fast path: the tile's best score (v_max3 tree) against this lane's current k-th best.  Once
+    // the lists are warm almost every tile fails for every lane, costing ~10 VALU instead of the
+    // exact masked filter below (the max includes self/padding, which can only cause a harmless
+    // trip into the exact path).
+    float mx = acc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    if (!__any(mx >= bs[K - 1])) continue;
+    // Exact filter: a candidate can only enter the list if it beats the CURRENT k-th best (which
+    // only improves), so 16 compares build a bitmask; the tile's scores are parked in this lane's
+    // LDS row and only set bits are inserted (dynamic index via LDS, not register arrays).
     unsigned mask = 0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -214,13 +224,24 @@ void launch_row_half_norms(const float* X, int m, float* out, int m_pad, hipStre
 }
 
 int knn_splits(int mq_pad, int mc_pad) {
-  // ~2048 workgroups (8 per CU), each slice keeping >= 8 candidate tiles per wave
+  // Candidate slices restart their top-k lists (fill cost), so use the fewest slices that give
+  // >= 2 workgroups per CU with the best whole-round balance over the CUs.
   const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
-  int s = (2048 + qblocks - 1) / qblocks;
-  const int max_s = tiles / (kWaves * 8);
-  if (s > max_s) s = max_s;
-  if (s > 64) s = 64;
-  return s < 1 ? 1 : s;
+  const int cus = device_cu_count();
+  int max_s = tiles / (kWaves * 8);
+  if (max_s > 16) max_s = 16;
+  if (max_s < 1) max_s = 1;
+  int best = 1;
+  double best_eff = -1.0;
+  for (int s = 1; s <= max_s; ++s) {
+    const double blocks = (double)qblocks * s;
+    const double rounds = std::ceil(blocks / cus);
+    double eff = blocks / (rounds * cus);     // load balance of the last round
+    if (blocks < 2.0 * cus) eff *= 0.5;       // too few waves per SIMD to overlap VALU with MFMA
+    eff -= 0.01 * (s - 1);                    // fill cost of every extra slice
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+  }
+  return best;
 }
 
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const float* chalf,

@@ -98,6 +98,11 @@ void launch_auc_count(const float* scores, const uint8_t* labels, int64_t n, con
                       unsigned long long* out_pairs, hipStream_t stream);
 void launch_confusion(const float* scores, const uint8_t* labels, int64_t n, float threshold,
                       unsigned long long* out4, hipStream_t stream);
+// histogram AUC: hist = [2][2^bits] u32 (negatives, positives) keyed on the order-preserving
+// score key's top bits; reduce -> {twice pair count, P, N}.  Mergeable by summing histograms.
+void launch_auc_hist(const float* scores, const uint8_t* labels, int64_t n, int bits, unsigned* hist,
+                     hipStream_t stream);
+void launch_auc_hist_reduce(const unsigned* hist, int bits, unsigned long long* out, hipStream_t stream);
 
 // ---- kernelshap.hip ----
 // X [E][d] raw explanations; a [32] folded weights; bg [n_bg][d] raw background; cb [n_bg]

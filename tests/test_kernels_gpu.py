@@ -322,3 +322,17 @@ def test_compact_indices_exact(dev, n, offset):
         got = S.compact_indices(view, target)
         ref_idx = torch.nonzero(view == target).reshape(-1)
         assert torch.equal(got, ref_idx)
+
+
+@pytest.mark.parametrize("n,rate", [(2_000_000, 0.002), (300_001, 0.3)])
+def test_auc_hist_matches_oracle_and_exact(dev, n, rate):
+    g = torch.Generator().manual_seed(n)
+    y = (torch.rand(n, generator=g) < rate).to(torch.uint8)
+    s = (torch.randn(n, generator=g) + 1.7 * y.float()).contiguous()
+    s[:1000] = torch.round(s[:1000] * 4) / 4  # some exact ties
+    hg = M.score_histogram(s.to(dev), y.to(dev))
+    hc = M.score_histogram(s, y)
+    assert torch.equal(hg.cpu(), hc)
+    assert M.auc_from_histogram(hg) == M.auc_from_histogram(hc)
+    exact = M.roc_auc(s.to(dev), y.to(dev))
+    assert abs(M.roc_auc_hist(s.to(dev), y.to(dev)) - exact) < 2e-4

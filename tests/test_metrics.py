@@ -1,0 +1,57 @@
+"""K10 metrics on CPU: exact AUC == sklearn, histogram AUC close to it and mergeable by summation
+(the data-parallel collective C6), ROC points, confusion counts."""
+import numpy as np
+import pytest
+import torch
+from sklearn.metrics import confusion_matrix, roc_auc_score
+
+from fraud_detection_amd.ops import metrics as M
+
+
+def _scores(n=50_000, rate=0.02, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    y = (torch.rand(n, generator=g) < rate).to(torch.uint8)
+    s = torch.randn(n, generator=g) + 2.0 * y.float()
+    s[:500] = torch.round(s[:500])  # ties
+    return s.contiguous(), y
+
+
+def test_exact_auc_equals_sklearn():
+    s, y = _scores()
+    assert M.roc_auc(s, y) == pytest.approx(roc_auc_score(y.numpy(), s.numpy()), abs=1e-12)
+
+
+def test_hist_auc_close_and_exact_when_bins_resolve_ties():
+    s, y = _scores()
+    assert abs(M.roc_auc_hist(s, y, bits=20) - M.roc_auc(s, y)) < 2e-4
+    # scores on a coarse grid: every distinct value has its own bin -> hist AUC is exact
+    q = torch.round(s * 8) / 8
+    assert M.roc_auc_hist(q, y, bits=20) == pytest.approx(M.roc_auc(q, y), abs=1e-12)
+
+
+def test_hist_merges_across_shards():
+    s, y = _scores(40_001)
+    full = M.score_histogram(s, y)
+    parts = sum(M.score_histogram(s[i::3].contiguous(), y[i::3].contiguous()) for i in range(3))
+    assert torch.equal(full, parts)
+
+
+def test_order_key_is_monotone():
+    v = np.array([-np.inf, -3.5, -1e-30, -0.0, 0.0, 1e-30, 2.0, np.inf], np.float32)
+    k = M._order_key_np(v)
+    assert np.all(np.diff(k.astype(np.int64)) >= 0)
+
+
+def test_roc_curve_hist_endpoints():
+    s, y = _scores()
+    fpr, tpr = M.roc_curve_hist(s, y)
+    assert fpr[0] == 0 and tpr[0] == 0 and fpr[-1] == pytest.approx(1) and tpr[-1] == pytest.approx(1)
+    assert np.all(np.diff(fpr) >= 0) and np.all(np.diff(tpr) >= 0)
+    assert np.trapz(tpr, fpr) == pytest.approx(M.roc_auc(s, y), abs=5e-3)
+
+
+def test_confusion_counts_match_sklearn():
+    s, y = _scores()
+    tn, fp, fn, tp = M.confusion_counts(s, y, 0.5)
+    ref = confusion_matrix(y.numpy(), (s.numpy() > 0.5).astype(int)).ravel()
+    assert [tn, fp, fn, tp] == list(ref)
