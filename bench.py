@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--rows-per-gpu", type=int, default=10_000_000)
     ap.add_argument("--solver", default="newton", choices=["newton", "sgd"])
     ap.add_argument("--storage", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--smote-scope", default="auto", choices=["auto", "global", "shard"],
+                    help="SMOTE neighbour set under DP; auto = shard for N > 1 (identical at N = 1)")
     ap.add_argument("--no-extras", action="store_true", help="skip the post-timing AUC/SHAP measurements")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -71,7 +73,8 @@ def main():
     X, y = separable(n_train, seed=1000 + rank, device=dev)
     Xt, yt = separable(n_test, seed=5000 + rank, device=dev)
 
-    cfg = TrainConfig(solver=args.solver, storage=args.storage, seed=42)
+    scope = args.smote_scope if args.smote_scope != "auto" else ("shard" if world > 1 else "global")
+    cfg = TrainConfig(solver=args.solver, storage=args.storage, seed=42, smote_scope=scope)
     pipe = DevicePipeline(cfg, comm)
     rng = np.random.default_rng(7)
 
@@ -130,6 +133,7 @@ def main():
             "parallelism": f"dp{world}",
             "rows_per_gpu": args.rows_per_gpu,
             "post_smote_rows_global": int(rows_global),
+            "smote_scope": scope,
         },
     }
     out.update(extras)

@@ -114,13 +114,13 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
 
   // knn / smote
-  m.def("row_half_norms", [](u X, int m, u out, int m_pad, u s) {
-    fdx::launch_row_half_norms(P<const float>(X), m, P<float>(out), m_pad, S(s));
+  m.def("knn_prep", [](u X, int m_, int m_pad, int role, u out, u s) {
+    fdx::launch_knn_prep(P<const float>(X), m_, m_pad, role, P<float>(out), S(s));
   });
   m.def("knn_splits", [](int mq_pad, int mc_pad) { return fdx::knn_splits(mq_pad, mc_pad); });
-  m.def("knn_topk", [](u Q, int mq_pad, int mq, u C, u chalf, int mc_pad, int mc, int64_t self_off, int k, u oidx,
+  m.def("knn_topk", [](u Q, int mq_pad, int mq, u C, int mc_pad, int mc, int64_t self_off, int k, u oidx,
                        u oscore, u ws_score, u ws_idx, int nsplit, u s) {
-    fdx::launch_knn_topk(P<const float>(Q), mq_pad, mq, P<const float>(C), P<const float>(chalf), mc_pad, mc,
+    fdx::launch_knn_topk(P<const float>(Q), mq_pad, mq, P<const float>(C), mc_pad, mc,
                          self_off, k, P<int>(oidx), P<float>(oscore), P<float>(ws_score), P<int>(ws_idx), nsplit,
                          S(s));
   });

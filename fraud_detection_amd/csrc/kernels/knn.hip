@@ -26,6 +26,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 constexpr int kMaxK = 8;
 constexpr float kNegBig = -3.0e38f;
+constexpr int kQFlush = 4;               // flush a wave's queues once any lane holds this many
+constexpr int kQCap = kQFlush - 1 + 16 + 1;  // + one tile's worth of appends + the dump slot
 
 __device__ __forceinline__ bool better(float s, int i, float s2, int i2) {
   return s > s2 || (s == s2 && i < i2);
@@ -45,35 +47,59 @@ __device__ __forceinline__ void topk_insert(float (&bs)[K], int (&bi)[K], float 
   }
 }
 
-__global__ void row_half_norms_kernel(const float* __restrict__ X, int m, float* __restrict__ out,
-                                      int m_pad) {
+// Rows for the score GEMM, padded to 32 floats.  Feature columns 0..29 are copied; the
+// squared-norm term rides in column 30 so that one MFMA chain yields the whole score:
+//   candidate: [c_0..c_29, -0.5 ||c||^2, 0]      (padding rows: [0.., -3e38, 0] -> never chosen)
+//   query:     [q_0..q_29, 1, 0]                  (padding rows: zeros)
+// so  score(c, q) = q.c - 0.5 ||c||^2  with no norm loads and a zero-initialised accumulator.
+__global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, int role,
+                                float* __restrict__ out) {
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= m_pad) return;
+  float4* o = reinterpret_cast<float4*>(out + (int64_t)r * kCols);
   if (r >= m) {
-    out[r] = -3.0e38f;  // padding candidates can never be selected
+#pragma unroll
+    for (int k = 0; k < kCols / 4; ++k) o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (role == 0) out[(int64_t)r * kCols + 30] = -3.0e38f;
     return;
   }
   const float4* p = reinterpret_cast<const float4*>(X + (int64_t)r * kCols);
   float s = 0.0f;
 #pragma unroll
   for (int k = 0; k < kCols / 4; ++k) {
-    const float4 v = p[k];
-    s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+    float4 v = p[k];
+    if (k == kCols / 4 - 1) {  // columns 28..31: keep 28, 29; 30 = norm term / 1, 31 = 0
+      s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s);
+      v.z = 0.0f; v.w = 0.0f;
+    } else {
+      s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+    }
+    o[k] = v;
   }
-  out[r] = -0.5f * s;  // stored negated: it initialises the MFMA accumulator directly
+  out[(int64_t)r * kCols + 30] = role == 0 ? -0.5f * s : 1.0f;
 }
 
-// Q: [mq_pad][32] fp32 queries, C: [mc_pad][32] fp32 candidates, chalf: [mc_pad] 0.5||c||^2.
+// Q: [mq_pad][32] query rows and C: [mc_pad][32] candidate rows, both from knn_prep_kernel.
 // Query row q is candidate row (self_offset + q) when self_offset >= 0 (self excluded).
+//
+// One wave per workgroup: blockIdx.x owns 32 queries, blockIdx.y a contiguous slice of the
+// candidate tiles (the per-slice lists are merged by knn_merge_kernel).  Per 32-candidate tile:
+//   * 16 v_mfma_f32_32x32x2_f32 give lane (j, h) the scores of query j against the 16 candidate
+//     rows of half h (exact fp32: score = q.c - 0.5||c||^2, the norm term is column 30);
+//   * a branch-free filter appends every score >= the lane's threshold to a per-lane LDS queue
+//     (non-passing lanes store into a private dump slot instead: no exec-mask juggling);
+//   * once any lane holds kQFlush entries the queues are inserted into the per-lane top-k
+//     (exact score-then-index order, self/padding excluded) and the threshold becomes the k-th
+//     best of the UNION of the two half-lists of the query (lanes j and j+32), which is a valid
+//     filter for both halves and about twice as tight.
 template <int K>
-__global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restrict__ Q, int mq,
-                                                            const float* __restrict__ C,
-                                                            const float* __restrict__ chalf,
-                                                            int mc_pad, int mc,
-                                                            int64_t self_offset,
-                                                            int* __restrict__ out_idx,
-                                                            float* __restrict__ out_score) {
-  const int lane = lane_id(), wv = wave_id();
+__global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict__ Q, int mq,
+                                                         const float* __restrict__ C,
+                                                         int mc_pad, int mc,
+                                                         int64_t self_offset,
+                                                         int* __restrict__ out_idx,
+                                                         float* __restrict__ out_score) {
+  const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
   const int q0 = blockIdx.x * 32;
   const int qg = q0 + j;  // this lane's query (column of the score tile)
@@ -91,104 +117,93 @@ __global__ __launch_bounds__(kThreads) void knn_topk_kernel(const float* __restr
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  float thr = kNegBig;
 
-  // per-lane parking row for one tile's 16 scores (stride 17 floats: conflict-free column reads)
-  __shared__ float park_all[kWaves][kWave * 17];
-  float* park = park_all[wv];
-  // blockIdx.y selects a contiguous slice of candidate tiles (split-K over candidates: enough
-  // workgroups to fill 256 CUs and several waves per SIMD to hide the top-k VALU work behind
-  // other waves' MFMA); slices write partial lists merged by knn_merge_kernel.
+  // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks.  Slot
+  // kQCap - 1 is the lane's dump slot.
+  __shared__ int2 qent[kQCap * kWave];  // (score bits, candidate index) at [slot * 64 + lane]
+  int qn = 0;
+  auto flush = [&]() {
+    for (int e = 0; __any(e < qn); ++e) {
+      if (e < qn) {
+        const int2 v = qent[e * kWave + lane];
+        const int ci = v.y;
+        if (ci != self_c && ci < mc) topk_insert<K>(bs, bi, __int_as_float(v.x), ci);
+      }
+    }
+    qn = 0;
+    // k-th best of the union of this lane's and its partner's (other half) sorted lists
+    float ps[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
+    int ia = 0, ib = 0;
+    float kth = kNegBig;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float a = kNegBig, b = kNegBig;
+#pragma unroll
+      for (int u = 0; u < K; ++u) { if (u == ia) a = bs[u]; if (u == ib) b = ps[u]; }
+      const bool ta = a >= b;
+      kth = ta ? a : b;
+      ia += ta ? 1 : 0;
+      ib += ta ? 0 : 1;
+    }
+    thr = kth;
+  };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
   const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
-  const int ntiles = t_hi;
-  // Register double buffer: the next candidate tile (16 floats of one row + 16 norms per lane,
-  // L2-resident) is fetched while the current tile's MFMA chain and top-k run.
-  float4 cv[4], nv[4];
-  auto fetch = [&](int t, float4 (&a)[4], float4 (&b)[4]) {
-    const int cb = t * 32;
-    const float4* p = reinterpret_cast<const float4*>(C + (int64_t)(cb + j) * kCols + 16 * h);
+  // register double buffer: the next tile's 16 floats per lane (L2-resident) are in flight
+  // while the current tile's MFMA chain and filter run
+  float4 cv[4];
+  auto fetch = [&](int t, float4 (&a)[4]) {
+    const float4* p = reinterpret_cast<const float4*>(C + (int64_t)(t * 32 + j) * kCols + 16 * h);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      a[k] = p[k];
-      // accumulator rows (k&3)+8(k>>2)+4h -> 4 contiguous candidates per register group
-      b[k] = *reinterpret_cast<const float4*>(chalf + cb + 8 * k + 4 * h);
-    }
+    for (int k = 0; k < 4; ++k) a[k] = p[k];
   };
-  if (t_lo + wv < ntiles) fetch(t_lo + wv, cv, nv);
-  for (int t = t_lo + wv; t < ntiles; t += kWaves) {
+  if (t_lo < t_hi) fetch(t_lo, cv);
+  for (int t = t_lo; t < t_hi; ++t) {
     const int c0 = t * 32;
     float ac[16];
-    f32x16_t acc;
+    f32x16_t acc = {};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       ac[4 * k] = cv[k].x; ac[4 * k + 1] = cv[k].y; ac[4 * k + 2] = cv[k].z; ac[4 * k + 3] = cv[k].w;
-      acc[4 * k] = nv[k].x; acc[4 * k + 1] = nv[k].y; acc[4 * k + 2] = nv[k].z; acc[4 * k + 3] = nv[k].w;
     }
-    if (t + kWaves < ntiles) fetch(t + kWaves, cv, nv);
+    if (t + 1 < t_hi) fetch(t + 1, cv);
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[s], bq[s], acc, 0, 0, 0);
-    // Fast path: the tile's best score (v_max3 tree) against this lane's current k-th best.  Once
-    // the lists are warm almost every tile fails for every lane, costing ~10 VALU instead of the
-    // exact masked filter below (the max includes self/padding, which can only cause a harmless
-    // trip into the exact path).
     float mx = acc[0];
 #pragma unroll
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
-    if (!__any(mx >= bs[K - 1])) continue;
-    // Exact filter: a candidate can only enter the list if it beats the CURRENT k-th best (which
-    // only improves), so 16 compares build a bitmask; the tile's scores are parked in this lane's
-    // LDS row and only set bits are inserted (dynamic index via LDS, not register arrays).
-    unsigned mask = 0;
+    if (!__any(mx >= thr)) continue;
+    const int cbase = c0 + 4 * h;
+    int qe = qn * kWave + lane;                     // element of this lane's next free slot
+    const int de = (kQCap - 1) * kWave + lane;      // this lane's dump slot
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int ci = c0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      const float sc = (ci == self_c || ci >= mc) ? kNegBig : acc[r];
-      acc[r] = sc;
-      mask |= better(sc, ci, bs[K - 1], bi[K - 1]) ? (1u << r) : 0u;
+      const bool pass = acc[r] >= thr;
+      qent[pass ? qe : de] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
+      qe += pass ? kWave : 0;
     }
-    if (__any(mask != 0)) {
-      float* my = park + lane * 17;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) my[r] = acc[r];
-      while (__any(mask != 0)) {
-        if (mask) {
-          const int r = __builtin_ctz(mask);
-          mask &= mask - 1;
-          const int ci = c0 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          topk_insert<K>(bs, bi, my[r], ci);
-        }
-      }
-    }
+    qn = (qe - lane) / kWave;
+    if (__any(qn >= kQFlush)) flush();
   }
-  // merge with the other half-wave (same query, other candidate rows)
+  flush();
+  // merge with the other half (same query, other candidate rows); lanes h == 0 write
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const float s2 = __shfl_xor(bs[k], 32, kWave);
     const int i2 = __shfl_xor(bi[k], 32, kWave);
     if (h == 0) topk_insert<K>(bs, bi, s2, i2);
   }
-  __shared__ float ls[kWaves][32][K];
-  __shared__ int li[kWaves][32][K];
-  if (h == 0) {
+  if (h == 0 && qg < mq) {
+    // gridDim.y > 1: partial list of this slice at [blockIdx.y][q][k] of the workspace
+    const int64_t o = ((int64_t)blockIdx.y * mq + qg) * K;
 #pragma unroll
-    for (int k = 0; k < K; ++k) { ls[wv][j][k] = bs[k]; li[wv][j][k] = bi[k]; }
-  }
-  __syncthreads();
-  if (wv == 0 && h == 0) {
-#pragma unroll
-    for (int w2 = 1; w2 < kWaves; ++w2) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) topk_insert<K>(bs, bi, ls[w2][j][k], li[w2][j][k]);
-    }
-    if (qg < mq) {
-      // gridDim.y > 1: partial list of this slice at [blockIdx.y][q][k] of the workspace
-      const int64_t o = ((int64_t)blockIdx.y * mq + qg) * K;
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        out_idx[o + k] = bi[k];
-        if (out_score) out_score[o + k] = bs[k];
-      }
+    for (int k = 0; k < K; ++k) {
+      out_idx[o + k] = bi[k];
+      if (out_score) out_score[o + k] = bs[k];
     }
   }
 }
@@ -218,33 +233,32 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict_
 
 }  // namespace
 
-void launch_row_half_norms(const float* X, int m, float* out, int m_pad, hipStream_t stream) {
-  row_half_norms_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, out, m_pad);
-  check_launch("row_half_norms");
+void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, hipStream_t stream) {
+  knn_prep_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, m_pad, role, out);
+  check_launch("knn_prep");
 }
 
 int knn_splits(int mq_pad, int mc_pad) {
-  // Candidate slices restart their top-k lists (fill cost), so use the fewest slices that give
-  // >= 2 workgroups per CU with the best whole-round balance over the CUs.
+  // Candidate slices restart their top-k lists (fill cost), so use the fewest slices that fill
+  // the resident capacity (one-wave workgroups) with the best whole-round balance.
+  static const int cap = resident_cap(knn_topk_kernel<5>, kWave);
   const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
-  const int cus = device_cu_count();
-  int max_s = tiles / (kWaves * 8);
-  if (max_s > 16) max_s = 16;
+  int max_s = tiles / 8;
+  if (max_s > 32) max_s = 32;
   if (max_s < 1) max_s = 1;
   int best = 1;
   double best_eff = -1.0;
   for (int s = 1; s <= max_s; ++s) {
     const double blocks = (double)qblocks * s;
-    const double rounds = std::ceil(blocks / cus);
-    double eff = blocks / (rounds * cus);     // load balance of the last round
-    if (blocks < 2.0 * cus) eff *= 0.5;       // too few waves per SIMD to overlap VALU with MFMA
-    eff -= 0.01 * (s - 1);                    // fill cost of every extra slice
+    const double rounds = std::ceil(blocks / cap);
+    double eff = blocks / (rounds * cap);            // occupancy of the resident slots over all rounds
+    eff -= 0.004 * (s - 1);                          // fill cost of every extra slice
     if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
   }
   return best;
 }
 
-void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const float* chalf,
+void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk: pads must be x32");
@@ -255,7 +269,7 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const f
   int* oi = nsplit > 1 ? ws_idx : out_idx;
   float* os = nsplit > 1 ? ws_score : out_score;
 #define FDX_KNN(KK)                                                                             \
-  knn_topk_kernel<KK><<<grid, kThreads, 0, stream>>>(Q, mq, C, chalf, mc_pad, mc, self_offset, oi, \
+  knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi,           \
                                                      os);                                        \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)

@@ -77,9 +77,10 @@ void launch_sgd_update(const double* red, double* state, float* w32, int d, doub
                        double momentum, int fit_intercept, hipStream_t stream);
 
 // ---- knn.hip ----
-void launch_row_half_norms(const float* X, int m, float* out, int m_pad, hipStream_t stream);
+// role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29)
+void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, hipStream_t stream);
 int knn_splits(int mq_pad, int mc_pad);
-void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C, const float* chalf,
+void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
 

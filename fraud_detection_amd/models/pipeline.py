@@ -47,6 +47,10 @@ class TrainConfig:
     check_every: int = 1            # Newton: iterations per convergence-flag read (host reads one chunk behind)
     init_std: float = 0.01          # random-init weights ~ N(0, init_std^2) (seeded by `seed`)
     hess_stride: int | str = "auto"  # Newton: Hessian from every k-th row tile (gradient always exact)
+    # SMOTE neighbour set under data parallelism: "global" = all ranks' minority rows (all-gather;
+    # identical to single-process imblearn on the whole table, k-NN work grows with the world
+    # size), "shard" = each rank's own minority rows (per-partition SMOTE: constant work per rank)
+    smote_scope: str = "global"
 
 
 @dataclass
@@ -108,6 +112,8 @@ class DevicePipeline:
 
     def fit(self, X: torch.Tensor, y: torch.Tensor, profile: bool = False) -> PipelineResult:
         cfg = self.cfg
+        if cfg.smote_scope not in ("global", "shard"):
+            raise ValueError("smote_scope must be 'global' or 'shard'")
         dev = X.device
         rank, world = self._world()
         comm = self.comm if world > 1 else None
@@ -141,7 +147,7 @@ class DevicePipeline:
         if n_new > 0:
             # ---- minority rows in fp32, gathered across ranks (C3) -----------------------
             xmin = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min)
-            if comm is not None:
+            if comm is not None and cfg.smote_scope == "global":
                 xall, counts = comm.all_gather_rows(xmin, counts=[r[0] for r in ranks])
                 q_off = int(sum(counts[:rank]))
             else:

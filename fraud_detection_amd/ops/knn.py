@@ -23,9 +23,9 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
              nsplit: int | None = None):
-    """k nearest candidates (squared L2) of each query row.
+    """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
-    Q [mq, 32] / C [mc, 32] fp32 padded rows.  If ``self_offset >= 0``, query row q is candidate
+    Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
     row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
     (ascending distance, ties -> smaller index) and optionally squared distances.
     ``nsplit``: candidate slices searched by separate workgroups and merged (None = auto).
@@ -48,10 +48,12 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     m = native()
     s = stream_of(Q)
     mq_pad, mc_pad = _pad32(mq), _pad32(mc)
-    Qp = _padded(Q.contiguous(), mq_pad)
-    Cp = _padded(C.contiguous(), mc_pad)
-    chalf = torch.empty(mc_pad, device=C.device, dtype=torch.float32)
-    m.row_half_norms(ptr(Cp), mc, ptr(chalf), mc_pad, s)
+    Qc, Cc = Q.contiguous(), C.contiguous()
+    # GEMM-ready rows: the -0.5||c||^2 term rides in column 30 (see knn.hip knn_prep_kernel)
+    Qp = torch.empty((mq_pad, NCOLS), device=Q.device, dtype=torch.float32)
+    Cp = torch.empty((mc_pad, NCOLS), device=C.device, dtype=torch.float32)
+    m.knn_prep(ptr(Cc), mc, mc_pad, 0, ptr(Cp), s)
+    m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
     ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
@@ -59,10 +61,10 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     if ns > 1:
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
-    m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), ptr(chalf), mc_pad, mc, int(self_offset), int(k), ptr(idx),
+    m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
                ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     if want_dist:
-        qn = (Q.double() ** 2).sum(1, keepdim=True)
+        qn = (Q[:, :30].double() ** 2).sum(1, keepdim=True)
         return idx, (qn - 2.0 * score.double()).float()
     return idx
 

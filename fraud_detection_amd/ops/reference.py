@@ -292,9 +292,10 @@ class NewtonStateRef:
 # K8 / K9 SMOTE
 # ------------------------------------------------------------------------------------------
 def knn_topk(Q: np.ndarray, C: np.ndarray, k: int, self_offset: int = -1):
-    """Exact k nearest neighbours (squared L2) with the kernel's tie rule (smaller index)."""
-    Q = np.asarray(Q, dtype=np.float64)
-    C = np.asarray(C, dtype=np.float64)
+    """Exact k nearest neighbours (squared L2 over the 30 feature columns; columns 30/31 of the
+    padded layout -- intercept and label -- are not features) with the kernel's tie rule."""
+    Q = np.asarray(Q, dtype=np.float64)[:, :30]
+    C = np.asarray(C, dtype=np.float64)[:, :30]
     score = Q @ C.T - 0.5 * np.sum(C * C, axis=1)[None, :]
     if self_offset >= 0:
         rows = np.arange(Q.shape[0])

@@ -52,19 +52,37 @@ class Communicator:
     def _try_native(self, strict: bool):
         """Bring up the native RCCL communicator and verify it with a known all-reduce; every
         rank must pass, otherwise all ranks keep using the ProcessGroup (collective decision)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+
+        def agree(ok: int) -> bool:
+            flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            return int(flag.item()) == 1
+
+        # 1) every rank can load the module -- agreed BEFORE the collective init, so a rank that
+        #    fails early can never leave the others blocked inside ncclCommInitRank
+        try:
+            from .rccl import NativeRCCL, available
+
+            ok = int(available())
+        except Exception:  # noqa: BLE001
+            if strict:
+                raise
+            ok = 0
+        if not agree(ok):
+            if strict:
+                raise RuntimeError("native RCCL unavailable on some rank")
+            return None
+        # 2) init on all ranks, 3) known all-reduce, agreed again
         nat, ok = None, 1
         try:
-            from .rccl import NativeRCCL
-
             nat = NativeRCCL(self.rank, self.world_size, self.local_rank)
             ok = int(nat.verify())
         except Exception:  # noqa: BLE001
             if strict:
                 raise
             ok = 0
-        flag = torch.tensor([ok], dtype=torch.int32, device=torch.device("cuda", torch.cuda.current_device()))
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-        if int(flag.item()) == 1:
+        if agree(ok):
             return nat
         if nat is not None:
             nat.close()

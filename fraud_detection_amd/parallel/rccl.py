@@ -16,6 +16,12 @@ _DT = {torch.float32: 0, torch.float64: 1, torch.int64: 2, torch.uint8: 3, torch
 _OP = {"sum": 0, "max": 1, "min": 2}
 
 
+def available() -> bool:
+    """The extension loads and links the same RCCL as torch (version query, no communicator)."""
+    lib = importlib.import_module("fraud_detection_amd._fdx_comm")
+    return int(lib.version()) > 0
+
+
 class NativeRCCL:
     def __init__(self, rank: int, world_size: int, local_rank: int, key: str = "fdx_rccl_uid"):
         self.lib = importlib.import_module("fraud_detection_amd._fdx_comm")

@@ -20,7 +20,7 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world, port, out_dir, smote):
+def _worker(rank, world, port, out_dir, smote, scope="global"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from fraud_detection_amd.data.synthetic import separable
@@ -32,7 +32,7 @@ def _worker(rank, world, port, out_dir, smote):
     Xt, yt = separable(8_000, fraud_rate=0.02, seed=200)
     sh = slice(rank * len(X) // world, (rank + 1) * len(X) // world)
     sht = slice(rank * len(Xt) // world, (rank + 1) * len(Xt) // world)
-    cfg = TrainConfig(smote=smote, tol=1e-8, init_std=0.0)
+    cfg = TrainConfig(smote=smote, tol=1e-8, init_std=0.0, smote_scope=scope)
     res = DevicePipeline(cfg, comm).fit(X[sh].contiguous(), y[sh].contiguous())
     ev = evaluate(res, Xt[sht].contiguous(), yt[sht].contiguous(), comm)
     mean, var, scale = res.scaler.numpy()
@@ -42,9 +42,9 @@ def _worker(rank, world, port, out_dir, smote):
     comm.close()
 
 
-def _run(world, smote, tmp_path):
+def _run(world, smote, tmp_path, scope="global"):
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path), smote), nprocs=world, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), smote, scope), nprocs=world, start_method="spawn")
     return [dict(np.load(os.path.join(tmp_path, f"r{r}.npz"))) for r in range(world)]
 
 
@@ -176,3 +176,16 @@ def test_dp_train_entry_point(tmp_path, monkeypatch):
     monkeypatch.setenv("DATA_CSV", csv)
     single = train.run(Settings.load(), cv_folds=2, model_dir=str(tmp_path / "single"), verbose=False)
     assert abs(single["test_auc"] - a0[0]) < 0.01
+
+
+def test_dp_shard_scope_smote(tmp_path):
+    """Per-partition SMOTE (neighbours within each rank's minority rows): same balance and row
+    counts as the global scope, one model on all ranks, comparable AUC."""
+    outs = _run(2, True, tmp_path, scope="shard")
+    assert np.array_equal(outs[0]["w"], outs[1]["w"])
+    assert float(outs[0]["auc"]) > 0.9
+    from fraud_detection_amd.data.synthetic import separable
+
+    _, y = separable(24_000, fraud_rate=0.02, seed=100)
+    n_maj = [int((y[r * 12000:(r + 1) * 12000] == 0).sum()) for r in range(2)]
+    assert [int(o["n_train"]) for o in outs] == [2 * m for m in n_maj]
