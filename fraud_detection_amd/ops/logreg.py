@@ -149,7 +149,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
-               hess_refresh: int | str = "auto", n_sched: int | None = None) -> FitInfo:
+               hess_refresh: int | str = "auto", n_sched: int | None = None,
+               local_warmup: bool = True) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
@@ -184,16 +185,28 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     # history is reset so backtracking only compares objectives of the same sample.
     # phase_start=1 on a phase's first iteration: the kernel forgets the previous phase's objective
     # and backtrack count (no extra fill kernels between phases).
+    # Data parallel: with ``local_warmup`` every rank runs the warm-up on its own shard (no
+    # collective per iteration) and the ranks then average their weights with ONE all-reduce --
+    # a warm start for the global full-data phase, whose fixed point does not depend on it.
+    dp = comm is not None and comm.world_size > 1
+    sync_warm = dp and not local_warmup
     first = [0]
     for sub, iters in sched:
         hs_w = auto_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
             _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub)
-            if comm is not None and comm.world_size > 1:
+            if sync_warm:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
                             int(fit_intercept), int(j == 0), s)
         first[0] = 1
+    if dp and local_warmup and sched:
+        wv = ws.state[S_W:S_W + 32]
+        comm.all_reduce_(wv)
+        wv.div_(comm.world_size)
+        ws.state[S_WPREV:S_WPREV + 32].copy_(wv)
+        ws.w32.copy_(wv)
+        ws.w32[LABEL_COL] = 0.0
     warm = sum(it for _, it in sched)
 
     refresh = auto_hess_refresh(n_sched) if hess_refresh == "auto" else int(hess_refresh)

@@ -4,8 +4,11 @@ One process per GPU.  Backends:
   * ``nccl``  torch.distributed over RCCL (on ROCm the "nccl" backend IS RCCL) across xGMI;
   * ``rccl``  the native communicator in csrc/comm/rccl_comm.cpp (ncclCommInitRank on our own
               unique id, collectives enqueued on the compute stream: no ProcessGroup work
-              objects, capturable in hipGraphs) -- selected with FDX_COMM=rccl;
-  * ``gloo``  CPU tensors (tests, world_size > 1 without GPUs).
+              objects, capturable in hipGraphs) -- used for the hot all-reduces whenever every
+              rank loads it and passes a known all-reduce (FDX_COMM=auto, the default;
+              FDX_COMM=torch forces the ProcessGroup, FDX_COMM=rccl makes failure fatal);
+  * ``gloo``  CPU tensors (tests, world_size > 1 without GPUs; CUDA tensors are host-staged,
+              so several ranks can share one GPU in tests).
 
 All payloads in this framework are tiny (<= 8.5 KB per Newton iteration) except the SMOTE
 minority all-gather, so the API is shaped for latency: one fused buffer per step, in-place
@@ -102,11 +105,20 @@ class Communicator:
             else:
                 dist.barrier()
 
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        # gloo moves CUDA tensors through host memory (tests run several ranks on one GPU)
+        return self.backend == "gloo" and t.is_cuda
+
     def all_reduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         if self.world_size == 1:
             return t
         if self._native is not None and t.is_cuda and op == "sum":
             self._native.all_reduce_(t)
+            return t
+        if self._host_staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=_op(op))
+            t.copy_(h)
             return t
         dist.all_reduce(t, op=_op(op))
         return t
@@ -125,7 +137,12 @@ class Communicator:
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:
             t = t.contiguous()
-            dist.broadcast(t, src=src)
+            if self._host_staged(t):
+                h = t.cpu()
+                dist.broadcast(h, src=src)
+                t.copy_(h)
+            else:
+                dist.broadcast(t, src=src)
         return t
 
     def all_gather_ints(self, vals) -> list:
@@ -144,6 +161,9 @@ class Communicator:
         counts when the caller already exchanged them (saves a collective and a host sync)."""
         if self.world_size == 1:
             return x, [x.shape[0]]
+        if self._host_staged(x):
+            out, c = self.all_gather_rows(x.cpu(), counts)
+            return out.to(x.device), c
         dev = x.device
         if counts is None:
             n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
