@@ -28,15 +28,23 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   const int q = lane & 3, rr = lane >> 2;
   const uint32_t range = (uint32_t)mq * (uint32_t)k;
   const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 64;
-  for (int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 64; base < n_new;
-       base += step) {
-    // one Philox draw per lane = one sample per lane (64 samples per wave-iteration)
-    const int64_t sl = base + lane;
+  // One Philox draw per lane = one sample per lane (64 samples per wave-iteration).  Software
+  // pipeline: the NEXT iteration's draw and its neighbour-index load are issued before this
+  // iteration's row gathers and stores, so the dependent nbr -> row chain costs one memory
+  // latency per iteration instead of two.
+  auto draw = [&](int64_t b, int& di, int& dj, float& dl) {
+    const int64_t sl = b + lane;
     const Philox4 r = philox4x32_10((uint32_t)sl, (uint32_t)(sl >> 32), cb0, cb1, key0, key1);
     const uint32_t pick = u32_range(r.x, range);
-    const int my_i = (int)(pick / (uint32_t)k);
-    const int my_j = sl < n_new ? nbr[(int64_t)my_i * k + (int)(pick % (uint32_t)k)] : 0;
-    const float my_lam = u32_to_unit(r.y);
+    di = (int)(pick / (uint32_t)k);
+    dj = sl < n_new ? nbr[(int64_t)di * k + (int)(pick % (uint32_t)k)] : 0;
+    dl = u32_to_unit(r.y);
+  };
+  int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 64;
+  int my_i = 0, my_j = 0;
+  float my_lam = 0.0f;
+  if (base < n_new) draw(base, my_i, my_j, my_lam);
+  for (; base < n_new; base += step) {
     // 4 row groups of 16 samples: 4 lanes per sample, 8 columns per lane; gathers issued first
     float4 a0[4], a1[4], b0[4], b1[4];
     float lam[4];
@@ -50,6 +58,11 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
       const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
       a0[u] = xi[0]; a1[u] = xi[1]; b0[u] = xj[0]; b1[u] = xj[1];
     }
+    // next iteration's draw + neighbour-index load, issued AFTER this iteration's gathers:
+    // vector loads return in issue order, so waiting for the gathers does not wait for it
+    int nx_i = 0, nx_j = 0;
+    float nx_lam = 0.0f;
+    if (base + step < n_new) draw(base + step, nx_i, nx_j, nx_lam);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t s = base + 16 * u + rr;
@@ -86,6 +99,9 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
         reinterpret_cast<uint2*>(out)[s * 4 + q] = pk;
       }
     }
+    my_i = nx_i;
+    my_j = nx_j;
+    my_lam = nx_lam;
   }
 }
 
