@@ -7,6 +7,7 @@ update.  Nothing in a round synchronises with the host.  CPU tensors run the num
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -184,7 +185,7 @@ def _resume(checkpoint, sig, T):
 
 def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm=None,
         cuts=None, sample_weight_pos: float | None = None, return_margin: bool = False,
-        checkpoint=None, checkpoint_every: int = 10):
+        checkpoint=None, checkpoint_every: int = 10, use_graph: bool | None = None):
     """Boost `n_estimators` depth-D trees on standardized float32 rows X [n, d] with labels y.
 
     ``checkpoint``: a utils.checkpoint.CheckpointManager.  Every ``checkpoint_every`` rounds the
@@ -249,7 +250,6 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
 
     m = native()
     dev = X.device
-    s = stream_of(X)
     ws = _Workspace(n, D, dev)
     dist = comm is not None and comm.world_size > 1
     n_global = int(comm.all_reduce_scalar(float(n))) if dist else n
@@ -269,8 +269,11 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     groot = torch.tensor([n_global], dtype=torch.int64, device=dev)
     lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
     ginv, hinv = 1.0 / gscale, 1.0 / hscale
-    for t in range(t0, T):
-        m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), s)
+
+    def round_body(o_feat, o_bin, o_thr, o_gain, o_leaf):
+        """One boosting round: a fixed launch sequence with static pointers (graph-capturable)."""
+        st = stream_of(X)  # the capture stream while a hipGraph is being recorded
+        m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
         ws.hist.zero_()
         ws.seg[0:1].copy_(root)
         ws.gcnt[0:1].copy_(groot)
@@ -280,15 +283,15 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
             m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
-                        ptr(ws.hist), s)
+                        ptr(ws.hist), st)
             if dist:
                 comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,
-                         ptr(feat[t]), ptr(binv[t]), ptr(thr[t]), ptr(gain[t]), ptr(ws.ng), ptr(ws.nh), s)
+                         ptr(o_feat), ptr(o_bin), ptr(o_thr), ptr(o_gain), ptr(ws.ng), ptr(ws.nh), st)
             if n:
-                m.gbdt_partition(ptr(bins), ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(feat[t]), ptr(binv[t]),
+                m.gbdt_partition(ptr(bins), ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
                                  level, ptr(ws.flag), ptr(ws.boff), PART_BLOCKS, ptr(ws.seg), ptr(ws.segR),
-                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), s)
+                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st)
             else:
                 ws.seg[2 * h0 + 1:2 * (h0 + nn) + 1].zero_()
             cur ^= 1
@@ -296,11 +299,37 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             ws.gcnt[c0:c0 + 2 * nn].copy_(ws.seg[c0:c0 + 2 * nn, 1])
             if dist:
                 comm.all_reduce_(ws.gcnt[c0:c0 + 2 * nn])
-        m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(leaf[t]), s)
+        m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(o_leaf), st)
         if n:
-            m.gbdt_margin(ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(leaf[t]), D, ptr(margin), s)
+            m.gbdt_margin(ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_leaf), D, ptr(margin), st)
+
+    def after_round(t):
         if checkpoint is not None and ((t + 1) % max(1, checkpoint_every) == 0 or t + 1 == T):
             _save(t + 1, feat, binv, thr, gain, leaf)  # device -> host copy: syncs every k rounds only
+
+    # hipGraph: a round is ~5 + 6*D launches with static shapes, so after one eager round it is
+    # recorded once and replayed (one graph launch per round instead of ~45 Python->HIP launches;
+    # the per-round tree lands in a fixed record and is copied into its slot).  Not under DP,
+    # where the round contains host-side collectives.
+    if use_graph is None:
+        use_graph = os.environ.get("FDX_GBDT_GRAPH", "1") != "0"
+    graphable = use_graph and not dist and n > 0 and T - t0 >= 3
+    graph = None
+    for t in range(t0, T):
+        if graphable and t == t0 + 1:  # round t0 ran eagerly: its kernels had to execute
+            from ..runtime.graphs import capture
+
+            rec = [torch.empty(ni, dtype=torch.int32, device=dev), torch.empty(ni, dtype=torch.int32, device=dev),
+                   torch.empty(ni, dtype=torch.float32, device=dev), torch.empty(ni, dtype=torch.float64, device=dev),
+                   torch.empty(nl, dtype=torch.float32, device=dev)]
+            graph = capture(lambda: round_body(*rec))
+        if graph is not None:
+            graph.replay()
+            for dst, src in zip((feat[t], binv[t], thr[t], gain[t], leaf[t]), rec):
+                dst.copy_(src)
+        else:
+            round_body(feat[t], binv[t], thr[t], gain[t], leaf[t])
+        after_round(t)
     ens = TreeEnsemble(feat=feat.cpu().numpy(), bin=binv.cpu().numpy(), thr=thr.cpu().numpy(),
                        gain=gain.cpu().numpy(), leaf=leaf.cpu().numpy(), **ens_kw)
     return (ens, margin) if return_margin else ens

@@ -130,3 +130,14 @@ def test_gbdt_deterministic_runs(dev):
     a, ma = gb.fit(Xd, yd, p, return_margin=True)
     b, mb = gb.fit(Xd, yd, p, return_margin=True)
     assert np.array_equal(a.leaf, b.leaf) and torch.equal(ma, mb)
+
+
+def test_gbdt_hipgraph_replay_bit_identical(dev):
+    Xd, yd, X, y = _data(200_000, 30, seed=15)
+    cuts = R.quantile_cuts(X, 256)
+    p = gb.GBDTParams(n_estimators=12, max_depth=5)
+    g_ens, g_m = gb.fit(Xd, yd, p, cuts=cuts, return_margin=True, use_graph=True)
+    e_ens, e_m = gb.fit(Xd, yd, p, cuts=cuts, return_margin=True, use_graph=False)
+    for k in ("feat", "bin", "thr", "gain", "leaf"):
+        assert np.array_equal(getattr(g_ens, k), getattr(e_ens, k)), k
+    assert torch.equal(g_m, e_m)
