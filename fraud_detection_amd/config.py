@@ -34,6 +34,7 @@ ENV_MAP = {
     "FDX_KERNELSHAP_BACKGROUND": "kernelshap_background",
     "FDX_SMOTE_K": "smote_k",
     "FDX_SEED": "seed",
+    "FDX_SPLIT": "split",
 }
 
 
@@ -63,6 +64,7 @@ class Settings:
     kernelshap_background: int = 100
     smote_k: int = 5
     seed: int = 42
+    split: str = "auto"            # sklearn (reference-exact) | device (K3 kernel) | auto
     extra: dict = field(default_factory=dict)
 
     @classmethod

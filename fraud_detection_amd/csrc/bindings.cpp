@@ -75,6 +75,11 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_compact_write(P<const uint8_t>(labels), n, target, P<const int64_t>(offsets), P<int64_t>(out_idx),
                               nblocks, S(s));
   });
+  m.def("strat_assign", [](u labels, int64_t n, u offsets, u total, uint32_t seed, double test_frac, int k, u out,
+                           int nblocks, u s) {
+    fdx::launch_strat_assign(P<const uint8_t>(labels), n, P<const int64_t>(offsets), P<const int64_t>(total), seed,
+                             test_frac, k, P<uint8_t>(out), nblocks, S(s));
+  });
 
   // predict / linear shap
   m.def("predict_bf16", [](u X, int64_t n, u w, u prob, u logit, u s) {

@@ -46,6 +46,10 @@ void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t*
 void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream);
 void launch_compact_write(const uint8_t* labels, int64_t n, int target, const int64_t* offsets,
                           int64_t* out_idx, int nblocks, hipStream_t stream);
+// K3 stratified split/fold codes (split.hip): 255 = test, 0..k-1 = fold; offsets/total from
+// compact_count(target=1) + exclusive_scan_small over the same nblocks.
+void launch_strat_assign(const uint8_t* labels, int64_t n, const int64_t* offsets, const int64_t* total,
+                         uint32_t seed, double test_frac, int k, uint8_t* out, int nblocks, hipStream_t stream);
 
 // ---- predict.hip ----
 void launch_predict_bf16(const uint16_t* X, int64_t n, const float* w, float* prob, float* logit,

@@ -30,6 +30,8 @@ from .models.pipeline import DevicePipeline, TrainConfig, evaluate
 
 logger = logging.getLogger("train")
 
+DEVICE_SPLIT_ROWS = 2_000_000
+
 
 def _device(name: str) -> torch.device:
     if name == "auto":
@@ -67,12 +69,26 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     if any(miss.values()):
         raise ValueError("missing feature values; impute before training")
     say("Splitting dataset (Train 80% / Test 20%)...")
-    tr, te = stratified_split(y, 0.2, 42)
-    neg, pos = int((y[tr] == 0).sum()), int((y[tr] == 1).sum())
-    y_tr_all = y[tr]
-    tr_m, te_m = _shard(tr, comm), _shard(te, comm)
-    Xtr, ytr = torch.from_numpy(X[tr_m]).to(dev), torch.from_numpy(y[tr_m]).to(dev)
-    Xte, yte = torch.from_numpy(X[te_m]).to(dev), torch.from_numpy(y[te_m]).to(dev)
+    mode = s.split
+    if mode == "auto":  # the sklearn split is a host argsort: past a few million rows use K3
+        mode = "device" if dev.type == "cuda" and X.shape[0] >= DEVICE_SPLIT_ROWS else "sklearn"
+    if mode == "device":
+        from .ops import split as SP
+
+        Xd, yd = torch.from_numpy(X).to(dev), torch.from_numpy(y).to(dev)  # one upload, then on-device gathers
+        codes = SP.assign(yd, 0.2, cv_folds if cv_folds and cv_folds > 1 else 0, 42)
+        tr, te, dev_folds = SP.split_indices(codes, cv_folds if cv_folds and cv_folds > 1 else 0)
+        take = lambda idx: (Xd.index_select(0, idx), yd.index_select(0, idx))  # noqa: E731
+        pos = int(yd.index_select(0, tr).sum())
+        neg = int(tr.shape[0]) - pos
+    elif mode == "sklearn":
+        tr, te = stratified_split(y, 0.2, 42)
+        take = lambda idx: (torch.from_numpy(X[idx]).to(dev), torch.from_numpy(y[idx]).to(dev))  # noqa: E731
+        neg, pos = int((y[tr] == 0).sum()), int((y[tr] == 1).sum())
+    else:
+        raise ValueError("split must be sklearn | device | auto")
+    Xtr, ytr = take(_shard(tr, comm))
+    Xte, yte = take(_shard(te, comm))
     scale_pos_weight = neg / pos if pos > 0 else 1.0
     say(f" Class balance before SMOTE -> [{neg} {pos}]")
     cfg = cfg or TrainConfig(solver=s.solver, storage=s.dtype, seed=s.seed, k_neighbors=s.smote_k)
@@ -81,10 +97,13 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     cv_scores = []
     if cv_folds and cv_folds > 1 and pos >= cv_folds:
         say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
-        for k, (ftr, fva) in enumerate(stratified_folds(y_tr_all, cv_folds, 42)):
-            fi, vi = _shard(tr[ftr], comm), _shard(tr[fva], comm)
-            res = _fit(model_type, cfg, torch.from_numpy(X[fi]).to(dev), torch.from_numpy(y[fi]).to(dev), comm)
-            auc = _score(model_type, res, torch.from_numpy(X[vi]).to(dev), torch.from_numpy(y[vi]).to(dev), comm)
+        if mode == "device":
+            folds = dev_folds
+        else:
+            folds = [(tr[a], tr[b]) for a, b in stratified_folds(y[tr], cv_folds, 42)]
+        for k, (ftr, fva) in enumerate(folds):
+            res = _fit(model_type, cfg, *take(_shard(ftr, comm)), comm)
+            auc = _score(model_type, res, *take(_shard(fva, comm)), comm)
             cv_scores.append(auc)
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
@@ -112,6 +131,7 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         summary["registered_version"] = _track(s, model_type, res, summary, paths, Xte, names, say)
     except Exception as e:  # noqa: BLE001 - tracking is best effort (reference train_model.py:165-166)
         say(f" MLflow Tracking Failed (likely connection error): {e}")
+    summary["split"] = mode
     if comm is not None:
         summary["world_size"] = comm.world_size
         comm.barrier()
@@ -185,6 +205,8 @@ def main(argv=None):
     ap.add_argument("--cv-folds", type=int, default=5)
     ap.add_argument("--model-dir", default="models")
     ap.add_argument("--json", default=None, help="write the run summary here")
+    ap.add_argument("--split", default=None, choices=["auto", "sklearn", "device"],
+                    help="sklearn: reference-identical split; device: K3 kernel (default auto: device >= 2M rows on GPU)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     comm = None
@@ -197,7 +219,8 @@ def main(argv=None):
             dev = torch.device("cuda", torch.cuda.current_device())
         comm = Communicator(device=dev)
     try:
-        out = run(model_type=a.model, cv_folds=a.cv_folds, model_dir=a.model_dir, comm=comm)
+        st = Settings.load(**({"split": a.split} if a.split else {}))
+        out = run(st, model_type=a.model, cv_folds=a.cv_folds, model_dir=a.model_dir, comm=comm)
     finally:
         if comm is not None:
             comm.close()

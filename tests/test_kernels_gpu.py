@@ -336,3 +336,13 @@ def test_auc_hist_matches_oracle_and_exact(dev, n, rate):
     assert M.auc_from_histogram(hg) == M.auc_from_histogram(hc)
     exact = M.roc_auc(s.to(dev), y.to(dev))
     assert abs(M.roc_auc_hist(s.to(dev), y.to(dev)) - exact) < 2e-4
+
+
+@pytest.mark.parametrize("n,rate,k,seed", [(1, 0.5, 5, 42), (1037, 0.02, 5, 42), (2_000_003, 0.0017, 5, 42),
+                                           (300_000, 0.3, 10, 9), (65_536, 0.01, 0, 42)])
+def test_strat_assign_matches_oracle(n, rate, k, seed):
+    from fraud_detection_amd.ops import split as SP
+
+    y = (np.random.default_rng(n).random(n) < rate).astype(np.uint8)
+    got = SP.assign(torch.from_numpy(y).cuda(), 0.2, k, seed).cpu().numpy()
+    assert np.array_equal(got, SP.assign_numpy(y, 0.2, k, seed))
