@@ -35,6 +35,7 @@ ENV_MAP = {
     "FDX_SMOTE_K": "smote_k",
     "FDX_SEED": "seed",
     "FDX_SPLIT": "split",
+    "FDX_CV_PARALLEL": "cv_parallel",
 }
 
 
@@ -65,6 +66,7 @@ class Settings:
     smote_k: int = 5
     seed: int = 42
     split: str = "auto"            # sklearn (reference-exact) | device (K3 kernel) | auto
+    cv_parallel: str = "auto"      # dp (each fold over all ranks) | fold (whole folds per rank) | auto
     extra: dict = field(default_factory=dict)
 
     @classmethod

@@ -31,6 +31,7 @@ from .models.pipeline import DevicePipeline, TrainConfig, evaluate
 logger = logging.getLogger("train")
 
 DEVICE_SPLIT_ROWS = 2_000_000
+FOLD_PARALLEL_ROWS = 8_000_000
 
 
 def _device(name: str) -> torch.device:
@@ -101,10 +102,11 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
             folds = dev_folds
         else:
             folds = [(tr[a], tr[b]) for a, b in stratified_folds(y[tr], cv_folds, 42)]
-        for k, (ftr, fva) in enumerate(folds):
-            res = _fit(model_type, cfg, *take(_shard(ftr, comm)), comm)
-            auc = _score(model_type, res, *take(_shard(fva, comm)), comm)
-            cv_scores.append(auc)
+        cv_mode = s.cv_parallel
+        if cv_mode == "auto":  # small folds are latency-bound under DP: give each rank whole folds
+            cv_mode = "fold" if comm is not None and len(tr) < FOLD_PARALLEL_ROWS else "dp"
+        cv_scores = _cross_validate(model_type, cfg, folds, take, comm, cv_mode)
+        for k, auc in enumerate(cv_scores):
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
     say(f" Training final {model_type} model with SMOTE on the full training set...")
@@ -136,6 +138,31 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         summary["world_size"] = comm.world_size
         comm.barrier()
     return summary
+
+
+def _cross_validate(model_type, cfg, folds, take, comm, mode: str) -> list:
+    """K12 per-fold orchestration (train_model.py:58-85).  The table is resident (device split:
+    on the GPU), so each fold is an on-device gather, never a host copy.
+      dp   -- every fold is fitted data-parallel over all ranks (large folds);
+      fold -- fold k runs whole on rank k % world (no collectives inside a fit), and the fold AUCs
+              are exchanged once at the end: the fold-parallel mode of SURVEY.md §2.4."""
+    if comm is None or mode == "dp":
+        out = []
+        for ftr, fva in folds:
+            res = _fit(model_type, cfg, *take(_shard(ftr, comm)), comm)
+            out.append(_score(model_type, res, *take(_shard(fva, comm)), comm))
+        return out
+    if mode != "fold":
+        raise ValueError("cv_parallel must be dp | fold | auto")
+    mine = {}
+    for k in range(comm.rank, len(folds), comm.world_size):
+        ftr, fva = folds[k]
+        res = _fit(model_type, cfg, *take(ftr), None)
+        mine[k] = _score(model_type, res, *take(fva), None)
+    merged = {}
+    for part in comm.all_gather_object(mine):
+        merged.update(part)
+    return [merged[k] for k in range(len(folds))]
 
 
 def _fit(model_type, cfg, X, y, comm=None):

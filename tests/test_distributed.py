@@ -176,6 +176,8 @@ def test_dp_train_entry_point(tmp_path, monkeypatch):
     monkeypatch.setenv("DATA_CSV", csv)
     single = train.run(Settings.load(), cv_folds=2, model_dir=str(tmp_path / "single"), verbose=False)
     assert abs(single["test_auc"] - a0[0]) < 0.01
+    # small folds run fold-parallel (whole folds per rank): CV scores equal the single-process ones
+    assert np.allclose(a0[1:], single["cv_scores"], rtol=0, atol=1e-12)
 
 
 def test_dp_shard_scope_smote(tmp_path):
