@@ -28,7 +28,7 @@ from contextlib import asynccontextmanager
 
 import numpy as np
 from fastapi import FastAPI, HTTPException, Request, Response, status
-from fastapi.responses import JSONResponse
+from fastapi.responses import HTMLResponse, JSONResponse
 from sqlalchemy import select, text
 from sqlalchemy.exc import SQLAlchemyError
 
@@ -281,6 +281,16 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
             raise HTTPException(status_code=404, detail="SHAP explanation not found. Calculation may still be pending.")
         return {"transaction_id": transaction_id, "created_at": r.created_at, "shap_values": r.shap_values,
                 "feature_names": r.feature_names}
+
+    @app.get("/ui", include_in_schema=False)
+    def console():
+        """Minimal browser console (fraud-frontend/index.html): /predict then /explain polling."""
+        path = os.environ.get("FDX_UI_HTML") or os.path.join(os.path.dirname(__file__), "..", "..", "fraud-frontend",
+                                                             "index.html")
+        if not os.path.exists(path):
+            raise HTTPException(status_code=404, detail="console not installed")
+        with open(path, encoding="utf-8") as f:
+            return HTMLResponse(f.read())
 
     @app.get("/metrics", include_in_schema=False)
     def prometheus_metrics():

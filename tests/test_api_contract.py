@@ -146,3 +146,10 @@ def test_health_degraded_when_db_down(tmp_path):
     assert r.status_code == 503
     assert r.json()["detail"]["status"] == "DEGRADED"
     assert os.path.exists("models/logistic_model.joblib")
+
+
+def test_console_page(svc):
+    c, _, _ = svc
+    r = c.get("/ui")
+    assert r.status_code == 200 and "text/html" in r.headers["content-type"]
+    assert "/predict" in r.text and "/explain/" in r.text
