@@ -55,9 +55,15 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("scaler_reduce", [](u partial, int nblocks, u sums, u s) {
     fdx::launch_scaler_reduce(P<const double>(partial), nblocks, P<double>(sums), S(s));
   });
-  m.def("scaler_finalize", [](u sums, double n, u pivot, int d, u mean64, u var64, u scale64, u mean32, u inv32, u s) {
+  m.def("scaler_finalize", [](u sums, double n, u pivot, int d, u mean64, u var64, u scale64, u mean32, u inv32,
+                              u aff, u s) {
     fdx::launch_scaler_finalize(P<const double>(sums), n, P<const float>(pivot), d, P<double>(mean64), P<double>(var64),
-                                P<double>(scale64), P<float>(mean32), P<float>(inv32), S(s));
+                                P<double>(scale64), P<float>(mean32), P<float>(inv32), P<double>(aff), S(s));
+  });
+  m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,
+                                int nblocks, u s) {
+    fdx::launch_scaler_stats_cast(P<const float>(X), n, d, P<const float>(pivot), P<const uint8_t>(labels), bias_value,
+                                  P<void>(out), P<double>(partial), nblocks, S(s));
   });
   m.def("scale_cast", [](u X, int64_t n, int ld, int d, u idx, u mean32, u inv32, u labels, float bias_value,
                          float out_scale, int out_kind, u out, u s) {
@@ -110,9 +116,12 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });
   m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi,
-                            int phase_start, u s) {
+                            int phase_start, u aff, u s) {
     fdx::launch_newton_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), d, C, tol,
-                              max_iter, fi, phase_start, S(s));
+                              max_iter, fi, phase_start, P<const double>(aff), S(s));
+  });
+  m.def("logreg_fold", [](u state, u aff, u w32, u s) {
+    fdx::launch_logreg_fold(P<const double>(state), P<const double>(aff), P<float>(w32), S(s));
   });
   m.def("sgd_update", [](u red, u state, u w32, int d, double C, double lr, double mom, int fi, u s) {
     fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), d, C, lr, mom, fi, S(s));

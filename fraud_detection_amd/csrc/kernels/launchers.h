@@ -36,7 +36,10 @@ void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream);
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
-                            float* inv32, hipStream_t stream);
+                            float* inv32, double* aff, hipStream_t stream);
+// fused K1+K2 for bf16 training rows: shifted sums -> partial[nblocks][64], rows s = x - pivot
+void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
+                              float bias_value, void* out, double* partial, int nblocks, hipStream_t stream);
 void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* idx,
                        const float* mean32, const float* inv32, const uint8_t* labels,
                        float bias_value, float out_scale, int out_kind, void* out,
@@ -74,9 +77,12 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.
+// aff (nullable, [64] = c | 1/sigma): the rows are pivot-shifted, not standardized -- the kernel
+// maps the reduced sums into standardized space and writes folded weights to w32.
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
-                          hipStream_t stream);
+                          const double* aff, hipStream_t stream);
+void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream);
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
                        double momentum, int fit_intercept, hipStream_t stream);
 

@@ -257,14 +257,26 @@ __device__ void build_grad(const double* red, const double* st, int d, int fit_i
 // first wait; reductions are wave-parallel; the Cholesky gives lane i row i (no integer
 // division, one fp64 reciprocal per column); the triangular solves keep b in lane registers
 // and broadcast with shuffles; barriers of a single-wave workgroup are nearly free.
+// Weights for pivot-shifted rows s = x - pivot from the standardized-space state:
+// v_j = w_j inv_j, v_30 = w_30 - sum_j w_j inv_j c_j (c = 0 off the feature columns).
+__device__ __forceinline__ void store_folded(const double* ss, const double* cA, const double* iA,
+                                             float* __restrict__ w32, int t) {
+  double p = (t < 32) ? ss[kW + t] * iA[t] * cA[t] : 0.0;
+  p = wave_sum(p);
+  if (t < kCols)
+    w32[t] = (t == kLabelCol) ? 0.0f : (t == kBiasCol) ? (float)(ss[kW + t] - p) : (float)(ss[kW + t] * iA[t]);
+}
+
 template <int MT>  // MT > 0: compile-time number of active coordinates (identity index map)
 __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
                                                            double* __restrict__ st,
                                                            float* __restrict__ w32,
                                                            int* __restrict__ done, int d, double C,
                                                            double tol, int max_iter,
-                                                           int fit_intercept, int phase_start) {
+                                                           int fit_intercept, int phase_start,
+                                                           const double* __restrict__ aff) {
   __shared__ double sr[kLRPartStride];
+  __shared__ double cA[32], iA[32], h30[32];
   __shared__ double ss[kStateSize];
   __shared__ double grad[32];
   __shared__ double Lc[64][65];  // [column][row], padded: every lane writes/reads in bounds
@@ -275,6 +287,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     // the done flag, instead of a load -> wait -> ds_write chain per element.
     constexpr int NR = kLRPartStride / 64, NS = kStateSize / 64;
     const int dn = *done;
+    const double av = aff ? aff[t] : 0.0;
     double v[NR], u[NS];
 #pragma unroll
     for (int i = 0; i < NR; ++i) v[i] = red[t + 64 * i];
@@ -285,8 +298,25 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     for (int i = 0; i < NR; ++i) sr[t + 64 * i] = v[i];
 #pragma unroll
     for (int i = 0; i < NS; ++i) ss[t + 64 * i] = u[i];
+    if (t < 32) cA[t] = av; else iA[t - 32] = av;
   }
   __syncthreads();
+  if (aff) {
+    // Rows hold s = x - pivot; standardized z = (s - c) * inv with c = inv = identity on the
+    // intercept/label/padding columns.  The sums map exactly: g_z[j] = inv_j (g_j - c_j g_30),
+    // H_z[j][k] = inv_j inv_k (H_jk - c_j H_30k - c_k H_j30 + c_j c_k H_30,30) (H symmetric).
+    const double g30 = sr[kBiasCol];
+    if (t < 32) h30[t] = sr[64 + kBiasCol * kCols + t];
+    __syncthreads();
+    if (t < 32) sr[t] = iA[t] * (sr[t] - cA[t] * g30);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int e = t + 64 * i, j = e >> 5, k = e & 31;
+      const double hv = sr[64 + e] - cA[j] * h30[k] - cA[k] * h30[j] + cA[j] * cA[k] * h30[kBiasCol];
+      sr[64 + e] = iA[j] * iA[k] * hv;
+    }
+    __syncthreads();
+  }
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
   const double reg = 1.0 / (C * S);
   const double invS = 1.0 / S;
@@ -408,9 +438,25 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     if (dec != 2 && (int)ss[kIter] >= max_iter) *done = 1;
   }
   __syncthreads();
-  if (t < kCols) w32[t] = (t == kLabelCol) ? 0.0f : (float)ss[kW + t];
+  if (aff) {
+    store_folded(ss, cA, iA, w32, t);
+  } else if (t < kCols) {
+    w32[t] = (t == kLabelCol) ? 0.0f : (float)ss[kW + t];
+  }
 #pragma unroll
   for (int i = 0; i < kStateSize / 64; ++i) st[t + 64 * i] = ss[t + 64 * i];
+}
+
+// Standardized-space weights (state) -> weights for pivot-shifted rows.  One wave.
+__global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restrict__ st,
+                                                         const double* __restrict__ aff,
+                                                         float* __restrict__ w32) {
+  __shared__ double ss[kW + 32], cA[32], iA[32];
+  const int t = threadIdx.x;
+  const double av = aff[t];
+  if (t < 32) { cA[t] = av; ss[kW + t] = st[kW + t]; } else { iA[t - 32] = av; }
+  __syncthreads();
+  store_folded(ss, cA, iA, w32, t);
 }
 
 // Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.
@@ -501,14 +547,19 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
-                          hipStream_t stream) {
+                          const double* aff, hipStream_t stream) {
   if (d + (fit_intercept ? 1 : 0) == 31)  // 30 features + intercept: the specialised stream
     newton_update_kernel<31><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
-                                                   phase_start);
+                                                   phase_start, aff);
   else
     newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
-                                                  phase_start);
+                                                  phase_start, aff);
   check_launch("newton_update");
+}
+
+void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream) {
+  logreg_fold_kernel<<<1, 64, 0, stream>>>(state, aff, w32);
+  check_launch("logreg_fold");
 }
 
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,

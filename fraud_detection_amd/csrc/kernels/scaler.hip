@@ -170,6 +170,76 @@ __global__ __launch_bounds__(kThreads) void scaler_partial_tiled_kernel(const fl
   }
 }
 
+// K1+K2 fused (bf16 training rows, standardization folded into the solver): one read of the raw
+// tile feeds both the shifted fp64 column sums (as scaler_partial_tiled) and the padded bf16 row
+// s = x - pivot (col 30 = bias_value, col 31 = label).  The standardization z = (s - c) / sigma
+// is applied later as an exact affine map on the solver's 32x32 sums (newton_update with aff),
+// so the raw matrix is read once instead of twice (stats, then cast) per fit.
+__global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
+    const float* __restrict__ X, int64_t n, int d, const float* __restrict__ pivot,
+    const uint8_t* __restrict__ labels, float bias_value, uint16_t* __restrict__ out,
+    double* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) float tile[kStatTileRows * 30];
+  __shared__ double red[2][8][32];
+  const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
+  const double piv = (c < d) ? (double)pivot[c] : 0.0;
+  const int q = threadIdx.x & 3;  // cast: column group of both of this lane's row slots
+  float pv[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) pv[j] = (8 * q + j < d) ? pivot[8 * q + j] : 0.0f;
+  double s = 0.0, sq = 0.0;
+  const int64_t ntiles = (n + kStatTileRows - 1) / kStatTileRows;
+  const int64_t total = n * (int64_t)d;
+  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+    const int64_t f0 = t * kStatTileRows * (int64_t)d;
+    const int nf = (int)((total - f0) < (int64_t)kStatTileRows * d ? (total - f0) : (int64_t)kStatTileRows * d);
+    const int nf4 = nf >> 2;
+    const float4* src = reinterpret_cast<const float4*>(X + f0);
+    for (int i = threadIdx.x; i < nf4; i += kThreads) reinterpret_cast<float4*>(tile)[i] = src[i];
+    for (int i = (nf4 << 2) + threadIdx.x; i < nf; i += kThreads) tile[i] = X[f0 + i];
+    __syncthreads();
+    const int rows = nf / d;
+    if (c < d) {
+      for (int r = rg; r < rows; r += 8) {
+        const double dd = (double)tile[r * d + c] - piv;
+        s += dd;
+        sq = fma(dd, dd, sq);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int slot = threadIdx.x + k * kThreads;  // 512 slots = 128 rows x 4 column groups
+      const int r = slot >> 2;
+      if (r >= rows) continue;
+      const int64_t grow = t * kStatTileRows + r;
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int cc = 8 * q + j;
+        if (cc < d) o[j] = tile[r * d + cc] - pv[j];
+        else if (cc == kBiasCol) o[j] = bias_value;
+        else if (cc == kLabelCol) o[j] = labels ? (float)labels[grow] : 0.0f;
+        else o[j] = 0.0f;
+      }
+      uint4 pk;
+      pk.x = pack_bf16x2(o[0], o[1]); pk.y = pack_bf16x2(o[2], o[3]);
+      pk.z = pack_bf16x2(o[4], o[5]); pk.w = pack_bf16x2(o[6], o[7]);
+      reinterpret_cast<uint4*>(out)[grow * 4 + q] = pk;
+    }
+    __syncthreads();
+  }
+  red[0][rg][c] = s;
+  red[1][rg][c] = sq;
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    double ss = 0.0, qq = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) { ss += red[0][g][c]; qq += red[1][g][c]; }  // fixed order
+    partial[(int64_t)blockIdx.x * 64 + c] = ss;
+    partial[(int64_t)blockIdx.x * 64 + 32 + c] = qq;
+  }
+}
+
 // Fixed-order reduction of [nblocks][64] fp64 partials into sums[64].
 // 16 waves, each summing a strided subset of block partials with 8 independent accumulators
 // (eight loads in flight per lane instead of one dependent chain of nblocks/4 loads); the
@@ -198,11 +268,13 @@ __global__ __launch_bounds__(1024) void scaler_reduce_kernel(const double* __res
 }
 
 // mean / var / scale from (possibly all-reduced) shifted sums.  One wave.
+// aff (optional, [64]): the map from pivot-shifted rows s = x - pivot to standardized ones,
+// z = (s - aff[c]) * aff[32 + c]; identity (0, 1) beyond d, so the intercept/label columns pass.
 __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n,
                                        const float* __restrict__ pivot, int d,
                                        double* __restrict__ mean64, double* __restrict__ var64,
                                        double* __restrict__ scale64, float* __restrict__ mean32,
-                                       float* __restrict__ inv32) {
+                                       float* __restrict__ inv32, double* __restrict__ aff) {
   const int c = threadIdx.x;
   if (c >= kCols) return;
   // n < 0: the (all-reduced) row count rides in the unused slot sums[31] (one collective for the
@@ -221,9 +293,17 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
     scale64[c] = scale;
     mean32[c] = (float)mean;
     inv32[c] = (float)(1.0 / scale);
+    if (aff) {
+      aff[c] = m;  // mean - pivot, without the cancellation of (pivot + m) - pivot
+      aff[32 + c] = 1.0 / scale;
+    }
   } else {
     mean64[c] = 0.0; var64[c] = 0.0; scale64[c] = 1.0;
     mean32[c] = 0.0f; inv32[c] = 0.0f;
+    if (aff) {
+      aff[c] = 0.0;
+      aff[32 + c] = 1.0;
+    }
   }
 }
 
@@ -541,10 +621,19 @@ void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipS
 
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
-                            float* inv32, hipStream_t stream) {
+                            float* inv32, double* aff, hipStream_t stream) {
   scaler_finalize_kernel<<<1, 64, 0, stream>>>(sums, n, pivot, d, mean64, var64, scale64, mean32,
-                                               inv32);
+                                               inv32, aff);
   check_launch("scaler_finalize");
+}
+
+void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
+                              float bias_value, void* out, double* partial, int nblocks, hipStream_t stream) {
+  if (d > 30 || (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(out) % 16) != 0)
+    throw std::invalid_argument("scaler_stats_cast: contiguous 16-byte aligned rows, d <= 30");
+  scaler_stats_cast_kernel<<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
+                                                             reinterpret_cast<uint16_t*>(out), partial);
+  check_launch("scaler_stats_cast");
 }
 
 void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* idx,

@@ -39,6 +39,9 @@ class TrainConfig:
     sampling_ratio: float = 1.0     # minority : majority after SMOTE (1.0 = imblearn 'auto')
     seed: int = 42
     storage: str = "bf16"           # bf16 | fp8
+    # bf16 + Newton on GPU: scaler statistics and the row cast share one read of X (rows stay
+    # pivot-shifted; the solver applies the standardization as an exact affine map of its sums)
+    fold_scaler: bool = True
     fp8_scale: float = DEFAULT_FP8_SCALE
     sgd_lr: float = 0.5
     sgd_momentum: float = 0.9
@@ -119,16 +122,26 @@ class DevicePipeline:
         comm = self.comm if world > 1 else None
         tm = _Timer(dev, profile)
         n, d = X.shape
-        # ---- K1: scaler statistics (C1 all-reduce inside) --------------------------------
-        stats = scaler_ops.scaler_fit(X, comm=comm)
-        tm.mark("scaler_fit")
-        # ---- class counts (C2): count kernels now, host reads the total while K2 runs -------
-        pending = scaler_ops.compact_indices_async(y, 1)
-        # ---- K2: standardize + pad + cast the real rows (label in col 31) into a buffer sized
-        # for the largest possible SMOTE output, so it does not wait for the minority count
+        fused = (cfg.fold_scaler and cfg.storage == "bf16" and cfg.solver == "newton" and dev.type == "cuda"
+                 and scaler_ops.fused_cast_ok(X))
+        # training buffer sized for the largest possible SMOTE output, so the cast does not wait
+        # for the minority count
         cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) if cfg.smote else 0)
         rows_cap = self._train_buffer(cap, dev)
-        scaler_ops.scale_cast(X, stats, labels=y, out_dtype=cfg.storage, out=rows_cap[:n], fp8_scale=cfg.fp8_scale)
+        if fused:
+            # ---- class counts (C2): count kernels first, host reads the total during K1+K2 ----
+            pending = scaler_ops.compact_indices_async(y, 1)
+            # ---- K1+K2 fused: statistics (C1 all-reduce inside) + pivot-shifted bf16 rows ----
+            stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm)
+            tm.mark("scaler_fit")
+        else:
+            # ---- K1: scaler statistics (C1 all-reduce inside) ----------------------------
+            stats = scaler_ops.scaler_fit(X, comm=comm)
+            tm.mark("scaler_fit")
+            pending = scaler_ops.compact_indices_async(y, 1)
+            # ---- K2: standardize + pad + cast the real rows (label in col 31) --------------
+            scaler_ops.scale_cast(X, stats, labels=y, out_dtype=cfg.storage, out=rows_cap[:n],
+                                  fp8_scale=cfg.fp8_scale)
         idx_min = pending.result()
         n_min = int(idx_min.shape[0])
 
@@ -158,7 +171,10 @@ class DevicePipeline:
                 raise ValueError("SMOTE needs at least 2 minority samples")
             nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off)
             tm.mark("knn")
-            knn_ops.smote_generate(xall, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
+            # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
+            # neighbours found in standardized space are interpolated in shifted coordinates
+            src = stats.standard_to_shifted(xall) if fused else xall
+            knn_ops.smote_generate(src, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
                                    fp8_scale=cfg.fp8_scale)
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
@@ -177,7 +193,7 @@ class DevicePipeline:
             fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
                                     check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride,
-                                    n_sched=n_sched)
+                                    n_sched=n_sched, affine=stats.aff if fused else None)
         elif cfg.solver == "sgd":
             fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                  batch_rows=cfg.sgd_batch_rows, class_w=class_w, d=d, w0=w0,

@@ -150,7 +150,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
                hess_refresh: int | str = "auto", n_sched: int | None = None,
-               local_warmup: bool = True) -> FitInfo:
+               local_warmup: bool = True, affine: torch.Tensor | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
@@ -158,15 +158,26 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     ``hess_refresh``: in the full-data phase a fresh Hessian only every k-th iteration; the
     iterations in between stream the gradient alone (-36% bytes of MFMA-free work per pass) and
     reuse the last reduced Hessian still held in the workspace (lazy-Hessian Newton).  0 = every
-    iteration.  The fixed point is unchanged: only the step's curvature model is older."""
+    iteration.  The fixed point is unchanged: only the step's curvature model is older.
+    ``affine``: [64] float64 (c | 1/sigma) when the rows are pivot-shifted instead of standardized
+    (ops/scaler.scaler_fit_cast): the fit still runs in standardized space (same w, same C)."""
     check_rows(rows)
     w0 = _default_w0(w0)
     if not rows.is_cuda:
+        if affine is not None:
+            a = affine.cpu().double()
+            rows = ((ref.rows_to_f32(rows, fp8_scale, d).double() - a[:32]) * a[32:]).float()
         return _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm, fp8_scale)
     m = native()
     ws = workspace or LRWorkspace(rows.device)
     ws.reset(w0, class_w)
     s = stream_of(rows)
+    aff = 0
+    if affine is not None:
+        if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
+            raise ValueError("affine must be a [64] float64 tensor on the rows' device")
+        aff = ptr(affine)
+        m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)  # w0 is standardized-space
     n = rows.shape[0]
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
     # The warm-up schedule sets the number of collectives, so every rank must derive the same one:
@@ -198,15 +209,18 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             if sync_warm:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
-                            int(fit_intercept), int(j == 0), s)
+                            int(fit_intercept), int(j == 0), aff, s)
         first[0] = 1
     if dp and local_warmup and sched:
         wv = ws.state[S_W:S_W + 32]
         comm.all_reduce_(wv)
         wv.div_(comm.world_size)
         ws.state[S_WPREV:S_WPREV + 32].copy_(wv)
-        ws.w32.copy_(wv)
-        ws.w32[LABEL_COL] = 0.0
+        if aff:
+            m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)
+        else:
+            ws.w32.copy_(wv)
+            ws.w32[LABEL_COL] = 0.0
     warm = sum(it for _, it in sched)
 
     refresh = auto_hess_refresh(n_sched) if hess_refresh == "auto" else int(hess_refresh)
@@ -221,7 +235,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                 # a gradient-only pass leaves the (already all-reduced) Hessian in red[64:]
                 comm.all_reduce_(ws.red if fresh else ws.red[:64])
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
-                            int(max_iter + warm), int(fit_intercept), first[0], s)
+                            int(max_iter + warm), int(fit_intercept), first[0], aff, s)
             first[0] = 0
         return k
 

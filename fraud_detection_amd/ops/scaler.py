@@ -25,6 +25,9 @@ class ScalerStats:
     scale64: torch.Tensor  # [32] float64
     mean32: torch.Tensor   # [32] float32
     inv32: torch.Tensor    # [32] float32 (0 beyond d)
+    # set by scaler_fit_cast: [64] float64 (c | 1/sigma) mapping pivot-shifted rows s = x - pivot
+    # to standardized ones, z = (s - c) / sigma (identity beyond d)
+    aff: torch.Tensor | None = None
 
     @property
     def n(self) -> float:
@@ -34,7 +37,18 @@ class ScalerStats:
 
     def to(self, device) -> "ScalerStats":
         return ScalerStats(self.n_src, self.d, *(t.to(device) for t in
-                                             (self.mean64, self.var64, self.scale64, self.mean32, self.inv32)))
+                                             (self.mean64, self.var64, self.scale64, self.mean32, self.inv32)),
+                           aff=None if self.aff is None else self.aff.to(device))
+
+    def shifted_to_standard(self, rows_f32: torch.Tensor) -> torch.Tensor:
+        """z rows from pivot-shifted fp32 rows [m, 32] (affine map on the feature columns)."""
+        a = self.aff.to(rows_f32.device, torch.float32)
+        return (rows_f32 - a[:32]) * a[32:]
+
+    def standard_to_shifted(self, rows_f32: torch.Tensor) -> torch.Tensor:
+        """Pivot-shifted fp32 rows from standardized ones (inverse of shifted_to_standard)."""
+        a = self.aff.to(rows_f32.device, torch.float64)
+        return torch.addcmul(a[:32].float(), rows_f32, (1.0 / a[32:]).float())
 
     def numpy(self):
         d = self.d
@@ -77,15 +91,24 @@ def scaler_partial_sums(X: torch.Tensor, pivot: torch.Tensor) -> torch.Tensor:
     return sums
 
 
-def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int) -> ScalerStats:
+def _aff_cpu(sums: np.ndarray, n: float, scale: np.ndarray, d: int) -> torch.Tensor:
+    aff = np.zeros(64)
+    aff[32:] = 1.0
+    aff[:d] = sums[:d] / n
+    aff[32:32 + d] = 1.0 / scale[:d]
+    return torch.from_numpy(aff)
+
+
+def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int, want_aff: bool = False) -> ScalerStats:
     """``n_total`` None: the count is in sums[31] (device) -- see scaler_fit."""
     dev = sums.device
     if n_total is None and not sums.is_cuda:
         n_total = float(sums[31])
     if not sums.is_cuda:
         mean, var, scale, m32, i32 = ref.scaler_finalize(sums.numpy(), float(n_total), pivot.cpu().numpy(), d)
+        aff = _aff_cpu(sums.numpy(), float(n_total), scale, d) if want_aff else None
         return ScalerStats(float(n_total), d, torch.from_numpy(mean), torch.from_numpy(var),
-                           torch.from_numpy(scale), torch.from_numpy(m32), torch.from_numpy(i32))
+                           torch.from_numpy(scale), torch.from_numpy(m32), torch.from_numpy(i32), aff=aff)
     m = native()
     piv = _pivot_dev(pivot, d, dev)
     mean64 = torch.empty(32, device=dev, dtype=torch.float64)
@@ -93,10 +116,11 @@ def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int) ->
     scale64 = torch.empty_like(mean64)
     mean32 = torch.empty(32, device=dev, dtype=torch.float32)
     inv32 = torch.empty_like(mean32)
+    aff = torch.empty(64, device=dev, dtype=torch.float64) if want_aff else None
     m.scaler_finalize(ptr(sums), -1.0 if n_total is None else float(n_total), ptr(piv), d, ptr(mean64), ptr(var64),
-                      ptr(scale64), ptr(mean32), ptr(inv32), stream_of(sums))
+                      ptr(scale64), ptr(mean32), ptr(inv32), ptr(aff), stream_of(sums))
     n_src = sums[31:32] if n_total is None else float(n_total)
-    return ScalerStats(n_src, d, mean64, var64, scale64, mean32, inv32)
+    return ScalerStats(n_src, d, mean64, var64, scale64, mean32, inv32, aff=aff)
 
 
 def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) -> ScalerStats:
@@ -117,6 +141,60 @@ def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) ->
         sums = comm.all_reduce(sums)
         return scaler_finalize(sums, None, pivot, d)
     return scaler_finalize(sums, float(n), pivot, d)
+
+
+def fused_cast_ok(X: torch.Tensor) -> bool:
+    """The fused K1+K2 kernel reads contiguous 16-byte aligned [n, d <= 30] fp32 rows."""
+    return (not X.is_cuda) or (X.is_contiguous() and X.data_ptr() % 16 == 0 and X.shape[1] <= 30)
+
+
+def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Tensor, comm=None,
+                    pivot: torch.Tensor | None = None, bias_value: float = 1.0) -> ScalerStats:
+    """StandardScaler.fit fused with the bf16 row cast: ONE read of X yields the (all-reduced)
+    statistics and pivot-shifted training rows s = x - pivot in ``out`` (bf16 [n, 32], col 30 =
+    bias_value, col 31 = label).  The returned stats carry ``aff``, which the Newton solver uses
+    to work in standardized space on these rows (ops/logreg.newton_fit(affine=...)): same model,
+    half the raw-matrix traffic of scaler_fit + scale_cast."""
+    _check_X(X)
+    n, d = X.shape
+    if out.shape != (n, NCOLS) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+        raise ValueError(f"bad output buffer {tuple(out.shape)} {out.dtype}")
+    if labels is not None and (labels.dtype != torch.uint8 or labels.shape[0] != n):
+        raise ValueError("labels must be uint8 [n] aligned with X")
+    dist = comm is not None and comm.world_size > 1
+    if pivot is None:
+        if dist:
+            pivot = X[0].clone() if n > 0 else torch.zeros(d, device=X.device)
+            pivot = comm.broadcast(pivot.contiguous(), src=0)
+        else:
+            pivot = X[0] if n > 0 else torch.zeros(d, device=X.device)
+    if not X.is_cuda:
+        sums = torch.from_numpy(ref.scaler_sums(X.numpy(), pivot.cpu().numpy()))
+        o = torch.zeros((n, NCOLS), dtype=torch.float32)
+        o[:, :d] = X - pivot[:d].to(torch.float32)
+        o[:, 30] = bias_value
+        if labels is not None:
+            o[:, 31] = labels.to(torch.float32)
+        out.copy_(o.to(torch.bfloat16))
+    else:
+        if not fused_cast_ok(X) or out.data_ptr() % 16:
+            raise ValueError("scaler_fit_cast: X must be contiguous and 16-byte aligned with d <= 30")
+        m = native()
+        piv = _pivot_dev(pivot, d, X.device)
+        nb = min(_SCALER_BLOCKS, max(1, (n + 255) // 256))  # = scaler_partial_sums: same summation order
+        partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
+        sums = torch.empty(64, device=X.device, dtype=torch.float64)
+        s = stream_of(X)
+        if n > 0:
+            m.scaler_stats_cast(ptr(X), n, d, ptr(piv), ptr(labels), float(bias_value), ptr(out), ptr(partial), nb, s)
+            m.scaler_reduce(ptr(partial), nb, ptr(sums), s)
+        else:
+            sums.zero_()
+    if dist:
+        sums[31:32].fill_(float(n))
+        sums = comm.all_reduce(sums)
+        return scaler_finalize(sums, None, pivot, d, want_aff=True)
+    return scaler_finalize(sums, float(n), pivot, d, want_aff=True)
 
 
 def scale_cast(X: torch.Tensor, stats: ScalerStats, labels: torch.Tensor | None = None,

@@ -346,3 +346,48 @@ def test_strat_assign_matches_oracle(n, rate, k, seed):
     y = (np.random.default_rng(n).random(n) < rate).astype(np.uint8)
     got = SP.assign(torch.from_numpy(y).cuda(), 0.2, k, seed).cpu().numpy()
     assert np.array_equal(got, SP.assign_numpy(y, 0.2, k, seed))
+
+
+@pytest.mark.parametrize("n,d", [(1, 30), (1037, 30), (600_011, 30), (4096, 7)])
+def test_scaler_fit_cast_fused(dev, n, d):
+    """Fused K1+K2: same statistics as scaler_fit (bit-identical sums), rows = bf16(x - pivot)."""
+    X, y = _data(max(n, 2), seed=n)
+    X = X[:n, :d].contiguous()
+    y = y[:n].contiguous()
+    Xd, yd = X.to(dev), y.to(dev)
+    out = torch.empty((n, 32), dtype=torch.bfloat16, device=dev)
+    st = S.scaler_fit_cast(Xd, yd, out)
+    ref_st = S.scaler_fit(Xd)
+    for a, b in zip(st.numpy(), ref_st.numpy()):
+        assert np.array_equal(a, b)
+    exp = torch.empty((n, 32), dtype=torch.bfloat16)
+    st_cpu = S.scaler_fit_cast(X, y, exp)
+    assert torch.equal(out.cpu(), exp)
+    np.testing.assert_allclose(st.aff.cpu().numpy(), st_cpu.aff.numpy(), rtol=1e-12, atol=1e-12)
+
+
+def test_newton_affine_matches_cpu(dev):
+    X, y = _data(300_000, seed=21)
+    sh = torch.empty((X.shape[0], 32), dtype=torch.bfloat16)
+    st = S.scaler_fit_cast(X, y, sh)
+    f_cpu = L.newton_fit(sh, tol=1e-8, affine=st.aff, w0=np.r_[np.full(30, 0.1), 0.0, 0.0])
+    f_gpu = L.newton_fit(sh.to(dev), tol=1e-8, affine=st.aff.to(dev), w0=np.r_[np.full(30, 0.1), 0.0, 0.0],
+                         progressive=[])
+    assert f_gpu.converged
+    np.testing.assert_allclose(f_gpu.w, f_cpu.w, rtol=0, atol=2e-4)
+
+
+def test_pipeline_fold_scaler_same_model(dev):
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    X, y = separable(3_000_000, seed=41, device=dev)
+    Xt, yt = separable(500_000, seed=42, device=dev)
+    res = {}
+    for fold in (True, False):
+        r = DevicePipeline(TrainConfig(fold_scaler=fold, tol=1e-6)).fit(X, y)
+        res[fold] = (r, evaluate(r, Xt, yt))
+    (ra, ea), (rb, eb) = res[True], res[False]
+    assert ra.fit.converged and rb.fit.converged
+    assert ra.n_train_rows == rb.n_train_rows
+    assert np.allclose(ra.w, rb.w, rtol=0, atol=5e-3)
+    assert abs(ea["auc"] - eb["auc"]) < 2e-4 and ea["auc"] > 0.95

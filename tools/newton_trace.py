@@ -74,7 +74,7 @@ def main():
                 t0 = time.perf_counter()
                 L._pass(m, rows, ws, hs_w, 0, n, 4.0, s, sub=sub)
                 m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0,
-                                a.tol if full else 0.0, 1 << 30, 1, int(jj == 0 and phase > 0), s)
+                                a.tol if full else 0.0, 1 << 30, 1, int(jj == 0 and phase > 0), 0, s)
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) * 1e6
                 st = ws.state.cpu().numpy()

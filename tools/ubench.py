@@ -100,7 +100,7 @@ def main():
     case("logreg_reduce", lambda: nat.logreg_reduce(ptr(ws.partial), ws.nblocks, 1088, ptr(ws.red), 0, s),
          ws.nblocks * 1088 * 4)
     case("newton_update", lambda: nat.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0,
-                                                    0.0, 1 << 30, 1, 0, s), 0)
+                                                    0.0, 1 << 30, 1, 0, 0, s), 0)
     case("newton_fit_2n_tol1e-4", lambda: L.newton_fit(rows2, tol=1e-4, workspace=ws), N2 * 64)
     case("newton_fit_2n_noprog", lambda: L.newton_fit(rows2, tol=1e-4, workspace=ws, progressive=[]), N2 * 64)
     from fraud_detection_amd.models.explainers import KernelExplainer
