@@ -60,6 +60,7 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_scaler_finalize(P<const double>(sums), n, P<const float>(pivot), d, P<double>(mean64), P<double>(var64),
                                 P<double>(scale64), P<float>(mean32), P<float>(inv32), P<double>(aff), S(s));
   });
+  m.def("scaler_stats_cast_blocks", []() { return fdx::scaler_stats_cast_blocks(); });
   m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,
                                 int nblocks, u s) {
     fdx::launch_scaler_stats_cast(P<const float>(X), n, d, P<const float>(pivot), P<const uint8_t>(labels), bias_value,
@@ -139,9 +140,9 @@ PYBIND11_MODULE(_fdx_native, m) {
                          S(s));
   });
   m.def("smote_generate", [](u C, u nbr, int mq, int k, int64_t q_off, int64_t n_new, uint64_t seed,
-                             uint64_t counter_base, float label, int out_kind, float out_scale, u out, u s) {
+                             uint64_t counter_base, float label, int out_kind, float out_scale, u aff, u out, u s) {
     fdx::launch_smote_generate(P<const float>(C), P<const int>(nbr), mq, k, q_off, n_new, seed, counter_base, label,
-                               out_kind, out_scale, P<void>(out), S(s));
+                               out_kind, out_scale, P<const double>(aff), P<void>(out), S(s));
   });
 
   // kernelshap

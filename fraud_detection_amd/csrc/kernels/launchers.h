@@ -37,6 +37,7 @@ void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipS
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
                             float* inv32, double* aff, hipStream_t stream);
+int scaler_stats_cast_blocks();  // resident blocks of the fused kernel on this device
 // fused K1+K2 for bf16 training rows: shifted sums -> partial[nblocks][64], rows s = x - pivot
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
                               float bias_value, void* out, double* partial, int nblocks, hipStream_t stream);
@@ -97,7 +98,7 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
 // ---- smote.hip ----
 void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
-                           int out_kind, float out_scale, void* out, hipStream_t stream);
+                           int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream);
 
 // ---- auc.hip ----
 void launch_auc_compact(const float* scores, const uint8_t* labels, int64_t n, float* pos,

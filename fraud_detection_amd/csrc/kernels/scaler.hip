@@ -190,15 +190,41 @@ __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
   double s = 0.0, sq = 0.0;
   const int64_t ntiles = (n + kStatTileRows - 1) / kStatTileRows;
   const int64_t total = n * (int64_t)d;
-  for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+  // Register double buffer: tile t+G's global loads (<= 4 float4 + 1 tail float per thread) are
+  // in flight while tile t is reduced and cast out of LDS.
+  constexpr int kV4 = (kStatTileRows * 30 / 4 + kThreads - 1) / kThreads;  // 4
+  float4 buf[kV4];
+  float tail = 0.0f;
+  auto fetch = [&](int64_t t) {
     const int64_t f0 = t * kStatTileRows * (int64_t)d;
     const int nf = (int)((total - f0) < (int64_t)kStatTileRows * d ? (total - f0) : (int64_t)kStatTileRows * d);
     const int nf4 = nf >> 2;
     const float4* src = reinterpret_cast<const float4*>(X + f0);
-    for (int i = threadIdx.x; i < nf4; i += kThreads) reinterpret_cast<float4*>(tile)[i] = src[i];
-    for (int i = (nf4 << 2) + threadIdx.x; i < nf; i += kThreads) tile[i] = X[f0 + i];
+#pragma unroll
+    for (int u = 0; u < kV4; ++u) {
+      const int i = threadIdx.x + u * kThreads;
+      if (i < nf4) buf[u] = src[i];
+    }
+    const int ti = (nf4 << 2) + threadIdx.x;
+    if (ti < nf) tail = X[f0 + ti];
+    return nf;
+  };
+  int64_t t = blockIdx.x;
+  int nf = t < ntiles ? fetch(t) : 0;
+  for (; t < ntiles; t += gridDim.x) {
+    {
+      const int nf4 = nf >> 2;
+#pragma unroll
+      for (int u = 0; u < kV4; ++u) {
+        const int i = threadIdx.x + u * kThreads;
+        if (i < nf4) reinterpret_cast<float4*>(tile)[i] = buf[u];
+      }
+      const int ti = (nf4 << 2) + threadIdx.x;
+      if (ti < nf) tile[ti] = tail;
+    }
     __syncthreads();
     const int rows = nf / d;
+    if (t + gridDim.x < ntiles) nf = fetch(t + gridDim.x);
     if (c < d) {
       for (int r = rg; r < rows; r += 8) {
         const double dd = (double)tile[r * d + c] - piv;
@@ -627,10 +653,17 @@ void launch_scaler_finalize(const double* sums, double n, const float* pivot, in
   check_launch("scaler_finalize");
 }
 
+int scaler_stats_cast_blocks() {
+  static const int cap = resident_cap(scaler_stats_cast_kernel, kThreads);
+  return cap;
+}
+
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
                               float bias_value, void* out, double* partial, int nblocks, hipStream_t stream) {
   if (d > 30 || (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(out) % 16) != 0)
     throw std::invalid_argument("scaler_stats_cast: contiguous 16-byte aligned rows, d <= 30");
+  // every block must be resident at once (a second round of blocks would double the span);
+  // nblocks is fixed by the caller (partial buffer), the grid-stride loop covers the rest
   scaler_stats_cast_kernel<<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
                                                              reinterpret_cast<uint16_t*>(out), partial);
   check_launch("scaler_stats_cast");

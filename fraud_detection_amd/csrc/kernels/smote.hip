@@ -23,9 +23,19 @@ template <int OUT>  // 0 = bf16 rows (64 B), 1 = fp32 rows (128 B, GBDT input), 
 __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     const float* __restrict__ C, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
     int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
-    float out_scale, void* __restrict__ out) {
+    float out_scale, const double* __restrict__ aff, void* __restrict__ out) {
   const int lane = lane_id();
   const int q = lane & 3, rr = lane >> 2;
+  // aff (optional): the parents are standardized rows z but the training buffer holds
+  // pivot-shifted rows s = z * sigma + c (scaler folded into the solver); interpolation commutes
+  // with the affine map, so it is applied to the output (mul then add, as the numpy oracle).
+  float sig[8], cc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool feat = aff != nullptr && 8 * q + j < kBiasCol;
+    sig[j] = feat ? (float)(1.0 / aff[32 + 8 * q + j]) : 1.0f;
+    cc[j] = feat ? (float)aff[8 * q + j] : 0.0f;
+  }
   const uint32_t range = (uint32_t)mq * (uint32_t)k;
   const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 64;
   // One Philox draw per lane = one sample per lane (64 samples per wave-iteration).  Software
@@ -72,6 +82,10 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
                     fmaf(l, b0[u].z - a0[u].z, a0[u].z), fmaf(l, b0[u].w - a0[u].w, a0[u].w),
                     fmaf(l, b1[u].x - a1[u].x, a1[u].x), fmaf(l, b1[u].y - a1[u].y, a1[u].y),
                     fmaf(l, b1[u].z - a1[u].z, a1[u].z), fmaf(l, b1[u].w - a1[u].w, a1[u].w)};
+      if (aff) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = __fadd_rn(__fmul_rn(o[j], sig[j]), cc[j]);
+      }
       if (q == 3) {
         o[6] = 1.0f;   // col 30: intercept column
         o[7] = label;  // col 31: label
@@ -109,7 +123,7 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
 
 void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
-                           int out_kind, float out_scale, void* out, hipStream_t stream) {
+                           int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream) {
   if (n_new <= 0) return;
   const int64_t per_block = (kThreads / kWave) * 64;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
@@ -119,13 +133,13 @@ void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_
   static const int cap2 = resident_cap(smote_generate_kernel<2>, kThreads);
   if (out_kind == 0)
     smote_generate_kernel<0><<<capped_grid(n_new, per_block, cap0), kThreads, 0, stream>>>(
-        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, out);
+        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
   else if (out_kind == 1)
     smote_generate_kernel<1><<<capped_grid(n_new, per_block, cap1), kThreads, 0, stream>>>(
-        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, out);
+        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
   else
     smote_generate_kernel<2><<<capped_grid(n_new, per_block, cap2), kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
-                                                           c0, c1, label, out_scale, out);
+                                                           c0, c1, label, out_scale, aff, out);
   check_launch("smote_generate");
 }
 

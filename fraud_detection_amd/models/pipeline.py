@@ -173,9 +173,8 @@ class DevicePipeline:
             tm.mark("knn")
             # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
             # neighbours found in standardized space are interpolated in shifted coordinates
-            src = stats.standard_to_shifted(xall) if fused else xall
-            knn_ops.smote_generate(src, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
-                                   fp8_scale=cfg.fp8_scale)
+            knn_ops.smote_generate(xall, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
+                                   fp8_scale=cfg.fp8_scale, affine=stats.aff if fused else None)
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
         class_w = (1.0, 1.0)

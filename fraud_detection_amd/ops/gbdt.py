@@ -17,7 +17,6 @@ from . import reference_gbdt as R
 from .native import native, ptr, stream_of
 
 MAX_BIN = R.MAX_BIN
-GRAPH_MAX_ROWS = 2_000_000  # profiles/r1_s21: at 6.4M rows eager is faster (1.54 vs 1.62 ms/tree)
 MAX_FEAT = 30
 HIST_ENTRIES = MAX_FEAT * MAX_BIN * 2
 PART_BLOCKS = 1024
@@ -311,10 +310,11 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     # hipGraph: a round is ~5 + 6*D launches with static shapes, so after one eager round it is
     # recorded once and replayed (one graph launch per round instead of ~45 Python->HIP launches;
     # the per-round tree lands in a fixed record and is copied into its slot).  Not under DP,
-    # where the round contains host-side collectives.
-    if use_graph is None:  # auto: replay pays off while launches, not kernels, bound a round
-        env = os.environ.get("FDX_GBDT_GRAPH", "auto")
-        use_graph = (n <= GRAPH_MAX_ROWS) if env == "auto" else env != "0"
+    # where the round contains host-side collectives.  Opt-in (FDX_GBDT_GRAPH=1): eager launches
+    # already run ahead of the GPU, and replay + record copies measured 0.61 vs 0.50 ms/tree at
+    # 0.96M rows and 1.62 vs 1.54 at 6.4M (profiles/r1_s22).
+    if use_graph is None:  # opt-in: measured slower than eager launches (profiles/r1_s22)
+        use_graph = os.environ.get("FDX_GBDT_GRAPH", "0") == "1"
     graphable = use_graph and not dist and n > 0 and T - t0 >= 3
     graph = None
     for t in range(t0, T):

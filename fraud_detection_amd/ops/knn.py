@@ -71,10 +71,12 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
 
 def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int, out: torch.Tensor,
                    seed: int = 42, counter_base: int = 0, label: float = 1.0,
-                   fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:
+                   fp8_scale: float = DEFAULT_FP8_SCALE, affine: torch.Tensor | None = None) -> torch.Tensor:
     """Write ``n_new`` synthetic rows into ``out`` (a [n_new, 32] bf16/fp32/fp8 view, e.g. the tail of
     the training buffer).  Sample s interpolates minority row (q_offset + i) toward neighbour
-    nbr[i, kk] with Philox draws keyed by (seed, s, counter_base)."""
+    nbr[i, kk] with Philox draws keyed by (seed, s, counter_base).  ``affine`` ([64] float64,
+    ScalerStats.aff): C holds standardized rows but ``out`` pivot-shifted ones -- each feature is
+    written as z * sigma + c."""
     if C.dtype != torch.float32 or C.dim() != 2 or C.shape[1] != NCOLS:
         raise ValueError("C must be fp32 [m, 32]")
     if nbr.dtype != torch.int32 or nbr.dim() != 2:
@@ -93,6 +95,10 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
         if nb.min() < 0 or nb.max() >= C.shape[0]:
             raise ValueError("neighbour index out of range")
         rows = ref.smote_generate(C.numpy(), nb, q_offset, n_new, seed, counter_base, label)
+        if affine is not None:
+            a = affine.cpu().numpy()
+            sig = (1.0 / a[32:62]).astype(np.float32)
+            rows[:, :30] = rows[:, :30] * sig + a[:30].astype(np.float32)
         if kind == "bf16":
             out.copy_(torch.from_numpy(rows).to(torch.bfloat16))
         elif kind == "f32":
@@ -104,6 +110,6 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
         return out
     m = native()
     m.smote_generate(ptr(C), ptr(nbr), mq, k, int(q_offset), int(n_new), int(seed) & (2**64 - 1),
-                     int(counter_base) & (2**64 - 1), float(label), DTYPE_KIND[kind], float(fp8_scale), ptr(out),
-                     stream_of(C))
+                     int(counter_base) & (2**64 - 1), float(label), DTYPE_KIND[kind], float(fp8_scale),
+                     ptr(affine), ptr(out), stream_of(C))
     return out

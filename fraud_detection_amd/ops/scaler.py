@@ -181,7 +181,8 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
             raise ValueError("scaler_fit_cast: X must be contiguous and 16-byte aligned with d <= 30")
         m = native()
         piv = _pivot_dev(pivot, d, X.device)
-        nb = min(_SCALER_BLOCKS, max(1, (n + 255) // 256))  # = scaler_partial_sums: same summation order
+        # all blocks resident at once (occupancy-derived), never more than the tiles
+        nb = max(1, min(m.scaler_stats_cast_blocks(), (n + 127) // 128))
         partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
         sums = torch.empty(64, device=X.device, dtype=torch.float64)
         s = stream_of(X)

@@ -350,7 +350,7 @@ def test_strat_assign_matches_oracle(n, rate, k, seed):
 
 @pytest.mark.parametrize("n,d", [(1, 30), (1037, 30), (600_011, 30), (4096, 7)])
 def test_scaler_fit_cast_fused(dev, n, d):
-    """Fused K1+K2: same statistics as scaler_fit (bit-identical sums), rows = bf16(x - pivot)."""
+    """Fused K1+K2: same statistics as scaler_fit (to fp64 summation order), rows = bf16(x - pivot)."""
     X, y = _data(max(n, 2), seed=n)
     X = X[:n, :d].contiguous()
     y = y[:n].contiguous()
@@ -359,11 +359,25 @@ def test_scaler_fit_cast_fused(dev, n, d):
     st = S.scaler_fit_cast(Xd, yd, out)
     ref_st = S.scaler_fit(Xd)
     for a, b in zip(st.numpy(), ref_st.numpy()):
-        assert np.array_equal(a, b)
+        np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12)
     exp = torch.empty((n, 32), dtype=torch.bfloat16)
     st_cpu = S.scaler_fit_cast(X, y, exp)
     assert torch.equal(out.cpu(), exp)
     np.testing.assert_allclose(st.aff.cpu().numpy(), st_cpu.aff.numpy(), rtol=1e-12, atol=1e-12)
+
+
+def test_smote_affine_output_matches_oracle(dev):
+    X, y = _data(200_000, seed=23, rate=0.02)
+    sh = torch.empty((X.shape[0], 32), dtype=torch.bfloat16)
+    st = S.scaler_fit_cast(X, y, sh)
+    idx = torch.nonzero(y == 1).reshape(-1)
+    xmin = S.scale_cast(X[idx].contiguous(), st, labels=y[idx].contiguous(), out_dtype="f32")
+    nbr = K.knn_topk(xmin, xmin, 5, 0)
+    out_cpu = torch.empty((50_000, 32), dtype=torch.bfloat16)
+    K.smote_generate(xmin, nbr, 0, 50_000, out_cpu, seed=7, affine=st.aff)
+    out_gpu = torch.empty((50_000, 32), dtype=torch.bfloat16, device=dev)
+    K.smote_generate(xmin.to(dev), nbr.to(dev), 0, 50_000, out_gpu, seed=7, affine=st.aff.to(dev))
+    assert torch.equal(out_gpu.cpu(), out_cpu)
 
 
 def test_newton_affine_matches_cpu(dev):

@@ -71,6 +71,7 @@ def main():
     pivot = X[0].clone()
     case("scaler_stats", lambda: S.scaler_partial_sums(X, pivot), n * 120)
     outb = torch.empty((n, 32), device=dev, dtype=torch.bfloat16)
+    case("scaler_stats_cast_bf16", lambda: S.scaler_fit_cast(X, y, outb), n * (120 + 1 + 64))
     outf = torch.empty((n, 32), device=dev, dtype=torch.float32)
     out8 = torch.empty((n, 32), device=dev, dtype=torch.uint8)
     case("scale_cast_bf16", lambda: S.scale_cast(X, st, labels=y, out=outb), n * (120 + 1 + 64))
