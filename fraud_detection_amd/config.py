@@ -36,6 +36,7 @@ ENV_MAP = {
     "FDX_SEED": "seed",
     "FDX_SPLIT": "split",
     "FDX_CV_PARALLEL": "cv_parallel",
+    "FDX_CHECKPOINT_DIR": "checkpoint_dir",
 }
 
 
@@ -67,6 +68,7 @@ class Settings:
     seed: int = 42
     split: str = "auto"            # sklearn (reference-exact) | device (K3 kernel) | auto
     cv_parallel: str = "auto"      # dp (each fold over all ranks) | fold (whole folds per rank) | auto
+    checkpoint_dir: str = ""       # job resume: completed CV folds + GBDT tree checkpoints
     extra: dict = field(default_factory=dict)
 
     @classmethod

@@ -26,7 +26,7 @@ constexpr int kUnroll = 4;     // row groups in flight per lane
 // Load the (up to) 4 columns [c0, c0+4) of row r, masking columns >= d.
 template <int VEC>
 __device__ __forceinline__ void load_row4(const float* __restrict__ X, int64_t r, int ld, int c0,
-                                          int d, float v[4]) {
+                                          int d, float (&v)[4]) {
   const float* p = X + r * (int64_t)ld + c0;
   if constexpr (VEC == 4) {
     if (c0 + 4 <= d) {
@@ -170,6 +170,23 @@ __global__ __launch_bounds__(kThreads) void scaler_partial_tiled_kernel(const fl
   }
 }
 
+// One 128-row tile of the raw matrix into registers: 4 float4 slots + 1 tail float per thread
+// (960 float4 per tile with d = 30 over 256 threads).  Returns the tile's float count.
+__device__ __forceinline__ int stats_fetch(const float* __restrict__ X, int64_t t, int d, int64_t total,
+                                           float4& b0, float4& b1, float4& b2, float4& b3, float& tail) {
+  const int64_t f0 = t * kStatTileRows * (int64_t)d;
+  const int nf = (int)((total - f0) < (int64_t)kStatTileRows * d ? (total - f0) : (int64_t)kStatTileRows * d);
+  const int nf4 = nf >> 2, i = threadIdx.x;
+  const float4* src = reinterpret_cast<const float4*>(X + f0);
+  if (i < nf4) b0 = src[i];
+  if (i + kThreads < nf4) b1 = src[i + kThreads];
+  if (i + 2 * kThreads < nf4) b2 = src[i + 2 * kThreads];
+  if (i + 3 * kThreads < nf4) b3 = src[i + 3 * kThreads];
+  const int ti = (nf4 << 2) + i;
+  if (ti < nf) tail = X[f0 + ti];
+  return nf;
+}
+
 // K1+K2 fused (bf16 training rows, standardization folded into the solver): one read of the raw
 // tile feeds both the shifted fp64 column sums (as scaler_partial_tiled) and the padded bf16 row
 // s = x - pivot (col 30 = bias_value, col 31 = label).  The standardization z = (s - c) / sigma
@@ -192,39 +209,24 @@ __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
   const int64_t total = n * (int64_t)d;
   // Register double buffer: tile t+G's global loads (<= 4 float4 + 1 tail float per thread) are
   // in flight while tile t is reduced and cast out of LDS.
-  constexpr int kV4 = (kStatTileRows * 30 / 4 + kThreads - 1) / kThreads;  // 4
-  float4 buf[kV4];
+  float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, b2 = b0, b3 = b0;
   float tail = 0.0f;
-  auto fetch = [&](int64_t t) {
-    const int64_t f0 = t * kStatTileRows * (int64_t)d;
-    const int nf = (int)((total - f0) < (int64_t)kStatTileRows * d ? (total - f0) : (int64_t)kStatTileRows * d);
-    const int nf4 = nf >> 2;
-    const float4* src = reinterpret_cast<const float4*>(X + f0);
-#pragma unroll
-    for (int u = 0; u < kV4; ++u) {
-      const int i = threadIdx.x + u * kThreads;
-      if (i < nf4) buf[u] = src[i];
-    }
-    const int ti = (nf4 << 2) + threadIdx.x;
-    if (ti < nf) tail = X[f0 + ti];
-    return nf;
-  };
   int64_t t = blockIdx.x;
-  int nf = t < ntiles ? fetch(t) : 0;
+  int nf = t < ntiles ? stats_fetch(X, t, d, total, b0, b1, b2, b3, tail) : 0;
   for (; t < ntiles; t += gridDim.x) {
     {
-      const int nf4 = nf >> 2;
-#pragma unroll
-      for (int u = 0; u < kV4; ++u) {
-        const int i = threadIdx.x + u * kThreads;
-        if (i < nf4) reinterpret_cast<float4*>(tile)[i] = buf[u];
-      }
+      const int nf4 = nf >> 2, i = threadIdx.x;
+      float4* t4 = reinterpret_cast<float4*>(tile);
+      if (i < nf4) t4[i] = b0;
+      if (i + kThreads < nf4) t4[i + kThreads] = b1;
+      if (i + 2 * kThreads < nf4) t4[i + 2 * kThreads] = b2;
+      if (i + 3 * kThreads < nf4) t4[i + 3 * kThreads] = b3;
       const int ti = (nf4 << 2) + threadIdx.x;
       if (ti < nf) tile[ti] = tail;
     }
     __syncthreads();
     const int rows = nf / d;
-    if (t + gridDim.x < ntiles) nf = fetch(t + gridDim.x);
+    if (t + gridDim.x < ntiles) nf = stats_fetch(X, t + gridDim.x, d, total, b0, b1, b2, b3, tail);
     if (c < d) {
       for (int r = rg; r < rows; r += 8) {
         const double dd = (double)tile[r * d + c] - piv;
@@ -354,20 +356,23 @@ __global__ __launch_bounds__(kThreads) void scale_cast_kernel(
   for (int64_t g = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); g < ngroups;
        g += nwaves * kUnroll) {
     float v[kUnroll][4];
-    int64_t rows[kUnroll];
     bool ok[kUnroll];
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
-      rows[u] = (g + u * nwaves) * 8 + rsub;
-      ok[u] = (g + u * nwaves) < ngroups && rows[u] < n;
+      const int64_t row = (g + u * nwaves) * 8 + rsub;
+      ok[u] = (g + u * nwaves) < ngroups && row < n;
       if (ok[u]) {
-        const int64_t src = idx ? idx[rows[u]] : rows[u];
+        const int64_t src = idx ? idx[row] : row;
         load_row4<VEC>(X, src, ld, c0, d, v[u]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[u][j] = 0.0f;  // defined on every path: v stays in VGPRs
       }
     }
 #pragma unroll
     for (int u = 0; u < kUnroll; ++u) {
       if (!ok[u]) continue;
+      const int64_t row = (g + u * nwaves) * 8 + rsub;  // recomputed: no int64 array to spill
       float o[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -375,11 +380,11 @@ __global__ __launch_bounds__(kThreads) void scale_cast_kernel(
         if (c < d) o[j] = (v[u][j] - mu[j]) * inv[j];
         else if (c == kBiasCol) o[j] = bias_value;
         else if (c == kLabelCol) {
-          const int64_t src = idx ? idx[rows[u]] : rows[u];
+          const int64_t src = idx ? idx[row] : row;
           o[j] = labels ? (float)labels[src] : 0.0f;
         } else o[j] = 0.0f;
       }
-      const int64_t base = rows[u] * kCols + c0;
+      const int64_t base = row * kCols + c0;
       if constexpr (OUT == 0) {
         uint2 pk;
         pk.x = pack_bf16x2(o[0], o[1]);

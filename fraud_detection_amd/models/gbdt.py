@@ -182,11 +182,13 @@ class GBDTResult:
 
 class GBDTPipeline:
     def __init__(self, cfg: TrainConfig | None = None, params: gb.GBDTParams | None = None, comm=None,
-                 scale_pos_weight: float | str = "auto"):
+                 scale_pos_weight: float | str = "auto", checkpoint_dir: str | None = None,
+                 checkpoint_every: int = 10):
         self.cfg = cfg or TrainConfig()
         self.params = params or gb.GBDTParams()
         self.comm = comm
         self.spw = scale_pos_weight
+        self.checkpoint_dir, self.checkpoint_every = checkpoint_dir, checkpoint_every
 
     def fit(self, X: torch.Tensor, y: torch.Tensor) -> GBDTResult:
         cfg = self.cfg
@@ -226,7 +228,12 @@ class GBDTPipeline:
         labels[n:] = 1
         t["prep"] = time.perf_counter() - t0
         params = gb.GBDTParams(**{**self.params.__dict__, "scale_pos_weight": spw})
-        ens = gb.fit(rows[:, :d], labels, params, comm=comm)
+        ck = None
+        if self.checkpoint_dir:
+            from ..utils.checkpoint import CheckpointManager
+
+            ck = CheckpointManager(self.checkpoint_dir, prefix="gbdt", keep=2, rank=rank)
+        ens = gb.fit(rows[:, :d], labels, params, comm=comm, checkpoint=ck, checkpoint_every=self.checkpoint_every)
         t["boost"] = time.perf_counter() - t0 - t["prep"]
         return GBDTResult(scaler=stats, ensemble=ens, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
                           n_synthetic=n_new, scale_pos_weight=spw, timings=t)

@@ -227,6 +227,9 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             checkpoint.save(t_done, {"feat": feat[:t_done], "bin": binv[:t_done], "thr": thr[:t_done],
                                      "gain": gain[:t_done], "leaf": leaf[:t_done]},
                             {"signature": sig, "trees_done": t_done, "kind": "gbdt"})
+            fault = os.environ.get("FDX_FAULT", "")
+            if fault.startswith("gbdt_crash_after_trees=") and t_done >= int(fault.split("=", 1)[1]):
+                os._exit(17)  # simulated lost rank right after a checkpoint (resume tests)
 
     if not X.is_cuda:
         feat = np.zeros((T, ni), np.int32); binv = np.zeros((T, ni), np.int32)

@@ -96,6 +96,13 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     if model_type not in ("logistic", "gbdt"):
         raise ValueError("model_type must be 'logistic' or 'gbdt'")
     cv_scores = []
+    from dataclasses import asdict
+
+    ck_dir = s.checkpoint_dir or None
+    progress = _Progress(ck_dir, lead, signature=None if ck_dir is None else _job_signature(
+        s, model_type, cv_folds, mode, asdict(cfg), X.shape, comm))
+    if progress.folds:
+        say(f" Resuming: {len(progress.folds)} completed fold(s) from {progress.path}")
     if cv_folds and cv_folds > 1 and pos >= cv_folds:
         say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
         if mode == "device":
@@ -105,12 +112,13 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         cv_mode = s.cv_parallel
         if cv_mode == "auto":  # small folds are latency-bound under DP: give each rank whole folds
             cv_mode = "fold" if comm is not None and len(tr) < FOLD_PARALLEL_ROWS else "dp"
-        cv_scores = _cross_validate(model_type, cfg, folds, take, comm, cv_mode)
+        cv_scores = _cross_validate(model_type, cfg, folds, take, comm, cv_mode, progress)
         for k, auc in enumerate(cv_scores):
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
     say(f" Training final {model_type} model with SMOTE on the full training set...")
-    res = _fit(model_type, cfg, Xtr, ytr, comm)
+    res = _fit(model_type, cfg, Xtr, ytr, comm,
+               checkpoint=None if ck_dir is None else os.path.join(ck_dir, f"final_{model_type}"))
     if model_type == "logistic":
         ev = evaluate(res, Xte, yte, comm)
         auc = ev["auc"]
@@ -134,43 +142,90 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     except Exception as e:  # noqa: BLE001 - tracking is best effort (reference train_model.py:165-166)
         say(f" MLflow Tracking Failed (likely connection error): {e}")
     summary["split"] = mode
+    summary["resumed_folds"] = sorted(progress.resumed)
     if comm is not None:
         summary["world_size"] = comm.world_size
         comm.barrier()
     return summary
 
 
-def _cross_validate(model_type, cfg, folds, take, comm, mode: str) -> list:
+class _Progress:
+    """Job-level resume: completed CV folds are recorded in
+    ``<checkpoint_dir>/train_progress.json`` (atomic rename, rank 0 writes), so a job restarted
+    after a crash or a lost rank (``torchrun --max-restarts``) skips them; the final GBDT fit
+    resumes from its tree checkpoints.  A record is used only if the job signature (data file,
+    model, folds, split, training config, world size) matches."""
+
+    def __init__(self, directory, lead: bool, signature):
+        self.path = os.path.join(directory, "train_progress.json") if directory else None
+        self.lead, self.sig = lead, signature
+        self.folds: dict = {}
+        if self.path and os.path.exists(self.path):
+            with open(self.path) as f:
+                d = json.load(f)
+            if d.get("signature") == signature:
+                self.folds = {int(k): float(v) for k, v in d.get("folds", {}).items()}
+        self.resumed = set(self.folds)
+
+    def record(self, k: int, auc: float):
+        self.folds[k] = float(auc)
+        if self.path and self.lead:
+            os.makedirs(os.path.dirname(self.path), exist_ok=True)
+            tmp = self.path + ".tmp"
+            with open(tmp, "w") as f:
+                json.dump({"signature": self.sig, "folds": self.folds}, f)
+            os.replace(tmp, self.path)
+        fault = os.getenv("FDX_FAULT", "")
+        if fault.startswith("train_crash_after_fold=") and len(self.folds) == int(fault.split("=", 1)[1]):
+            logger.error("FDX_FAULT: simulated crash after %d fold(s)", len(self.folds))
+            os._exit(17)  # hard exit, like a killed rank: no cleanup, no flush
+
+
+def _job_signature(s, model_type, cv_folds, split_mode, cfg: dict, shape, comm) -> str:
+    from .utils.checkpoint import config_signature
+
+    st = os.stat(s.data_csv)
+    return config_signature(data=os.path.abspath(s.data_csv), size=st.st_size, mtime=int(st.st_mtime),
+                            shape=list(shape), model=model_type, folds=cv_folds, split=split_mode, cfg=cfg,
+                            world=1 if comm is None else comm.world_size)
+
+
+def _cross_validate(model_type, cfg, folds, take, comm, mode: str, progress: _Progress | None = None) -> list:
     """K12 per-fold orchestration (train_model.py:58-85).  The table is resident (device split:
     on the GPU), so each fold is an on-device gather, never a host copy.
       dp   -- every fold is fitted data-parallel over all ranks (large folds);
       fold -- fold k runs whole on rank k % world (no collectives inside a fit), and the fold AUCs
-              are exchanged once at the end: the fold-parallel mode of SURVEY.md §2.4."""
+              are exchanged once at the end: the fold-parallel mode of SURVEY.md §2.4.
+    Folds already in ``progress`` (a resumed job) are not recomputed."""
+    progress = progress or _Progress(None, True, None)
     if comm is None or mode == "dp":
-        out = []
-        for ftr, fva in folds:
+        for k, (ftr, fva) in enumerate(folds):
+            if k in progress.folds:
+                continue
             res = _fit(model_type, cfg, *take(_shard(ftr, comm)), comm)
-            out.append(_score(model_type, res, *take(_shard(fva, comm)), comm))
-        return out
+            progress.record(k, _score(model_type, res, *take(_shard(fva, comm)), comm))
+        return [progress.folds[k] for k in range(len(folds))]
     if mode != "fold":
         raise ValueError("cv_parallel must be dp | fold | auto")
     mine = {}
     for k in range(comm.rank, len(folds), comm.world_size):
+        if k in progress.folds:
+            continue
         ftr, fva = folds[k]
         res = _fit(model_type, cfg, *take(ftr), None)
         mine[k] = _score(model_type, res, *take(fva), None)
-    merged = {}
     for part in comm.all_gather_object(mine):
-        merged.update(part)
-    return [merged[k] for k in range(len(folds))]
+        for k, auc in sorted(part.items()):
+            progress.record(k, auc)
+    return [progress.folds[k] for k in range(len(folds))]
 
 
-def _fit(model_type, cfg, X, y, comm=None):
+def _fit(model_type, cfg, X, y, comm=None, checkpoint: str | None = None):
     if model_type == "logistic":
         return DevicePipeline(cfg, comm).fit(X, y)
     from .models.gbdt import GBDTPipeline
 
-    return GBDTPipeline(cfg, comm=comm).fit(X, y)
+    return GBDTPipeline(cfg, comm=comm, checkpoint_dir=checkpoint).fit(X, y)
 
 
 def _score(model_type, res, X, y, comm=None) -> float:
@@ -232,6 +287,8 @@ def main(argv=None):
     ap.add_argument("--cv-folds", type=int, default=5)
     ap.add_argument("--model-dir", default="models")
     ap.add_argument("--json", default=None, help="write the run summary here")
+    ap.add_argument("--checkpoint-dir", default=None,
+                    help="resume directory: completed CV folds + GBDT tree checkpoints (FDX_CHECKPOINT_DIR)")
     ap.add_argument("--split", default=None, choices=["auto", "sklearn", "device"],
                     help="sklearn: reference-identical split; device: K3 kernel (default auto: device >= 2M rows on GPU)")
     a = ap.parse_args(argv)
@@ -246,7 +303,8 @@ def main(argv=None):
             dev = torch.device("cuda", torch.cuda.current_device())
         comm = Communicator(device=dev)
     try:
-        st = Settings.load(**({"split": a.split} if a.split else {}))
+        over = {k: v for k, v in (("split", a.split), ("checkpoint_dir", a.checkpoint_dir)) if v}
+        st = Settings.load(**over)
         out = run(st, model_type=a.model, cv_folds=a.cv_folds, model_dir=a.model_dir, comm=comm)
     finally:
         if comm is not None:
