@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     int hess_stride, int row_sub, float* __restrict__ partial) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
-  __shared__ float red[kWaves][34];
+  __shared__ float red[kWaves][35];
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 3, rr = lane >> 2;
   float wl[8];
@@ -68,7 +68,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   float g[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) g[j] = 0.0f;
-  float lacc = 0.0f, wacc = 0.0f;
+  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f;  // whacc: weight of the rows feeding H
   f32x16_t acc = {};
   // transpose-read lane geometry (constant per lane): 16-lane group grp reads 4 rows x 16 cols
   const int grp = lane >> 4, gi = lane & 15;
@@ -163,6 +163,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     // weighted log-loss of this lane's row: max(z,0) - y z + log1p(exp(-|z|))
     lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
     wacc += swq;
+    if (do_h) whacc += swq;
 #pragma unroll
     for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
   }
@@ -172,6 +173,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
   lacc = wave_sum(lacc);
   wacc = wave_sum(wacc);
+  whacc = wave_sum(whacc);
   if (lane < 4) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[wv][8 * lane + j] = g[j];
@@ -179,6 +181,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   if (lane == 0) {
     red[wv][32] = lacc;
     red[wv][33] = wacc;
+    red[wv][34] = HESS ? whacc * (float)hess_stride : 0.0f;
   }
   float* hb = reinterpret_cast<float*>(&tile[0][0]);  // 4 x 1024 floats = the 16 KiB tile
   if constexpr (HESS) {
@@ -192,7 +195,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   }
   __syncthreads();
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
-  if (threadIdx.x < 34) {
+  if (threadIdx.x < (HESS ? 35 : 34)) {  // slot 34 (Hessian weight) only from Hessian passes
     const int t = threadIdx.x;
     out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
   }
@@ -369,6 +372,10 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     // Newton refinement (~46 bits; the Newton step only needs to be a good descent direction).
     // Rows/columns >= m are identity-padded and never read back.
     const double regS = reg * S;
+    // H may come from another row sample than g (sub-sampled warm-up, or a lazy-Hessian pass
+    // reusing an older H): red[34] is the weight of the rows behind H, so H * S / S_H is the
+    // sample-mean Hessian at the gradient's scale.
+    const double hw = sr[34] > 0.0 ? S / sr[34] : 1.0;
     double a[32];
     {
       const int row = (MT > 0) ? (t < 32 ? t : 0) : (my >= 0 ? my : 0);
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         const double hv = hr[col < 0 ? 0 : col];
         const bool act = (t < m) && (k < m);
         const double dg = (k == t && my < d) ? regS : 0.0;
-        a[k] = act ? hv + dg : (k == t ? 1.0 : 0.0);
+        a[k] = act ? fma(hv, hw, dg) : (k == t ? 1.0 : 0.0);
       }
     }
     double bi = (t < m) ? -grad[my < 0 ? 0 : my] * S : 0.0;

@@ -82,6 +82,9 @@ def _blob_views(blob: torch.Tensor):
 HESS_SAMPLE_ROWS = 1 << 22  # auto Hessian sub-sampling keeps >= ~4M rows in the H estimate
 
 
+GRAD_SLOTS = 34  # red[0:32] gradient, red[32] loss, red[33] weight; red[34] = Hessian-sample weight
+
+
 def auto_hess_stride(n_rows: int) -> int:
     return int(max(1, min(8, n_rows // HESS_SAMPLE_ROWS)))
 
@@ -116,7 +119,8 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
     else:
         m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
                           ptr(ws.partial), ws.nblocks, s)
-    m.logreg_reduce(ptr(ws.partial), ws.nblocks, PART_STRIDE if h else 64, ptr(ws.red), dptr, s)
+    # gradient-only: reduce slots 0..33 and keep red[34] (weight of the rows behind the held H)
+    m.logreg_reduce(ptr(ws.partial), ws.nblocks, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
 
 
 def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian: bool = True,
@@ -212,6 +216,9 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                             int(fit_intercept), int(j == 0), aff, s)
         first[0] = 1
     if dp and local_warmup and sched:
+        # the full-data phase starts from the warm-up Hessian: sum the ranks' sample Hessians and
+        # their weights so every rank takes the same first step
+        comm.all_reduce_(ws.red[GRAD_SLOTS:])
         wv = ws.state[S_W:S_W + 32]
         comm.all_reduce_(wv)
         wv.div_(comm.world_size)
@@ -228,12 +235,14 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
 
     def enqueue_chunk(k: int) -> int:
         for _ in range(k):
-            fresh = refresh <= 0 or full_it[0] % refresh == 0
+            # after a warm-up the first full-data iterations reuse its last Hessian (a >= 1M-row
+            # sample mean, rescaled to the full gradient through red[34]); then every refresh-th
+            fresh = refresh <= 0 or (full_it[0] + (1 if warm else 0)) % refresh == 0
             full_it[0] += 1
             _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s)
             if comm is not None and comm.world_size > 1:
-                # a gradient-only pass leaves the (already all-reduced) Hessian in red[64:]
-                comm.all_reduce_(ws.red if fresh else ws.red[:64])
+                # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
+                comm.all_reduce_(ws.red if fresh else ws.red[:GRAD_SLOTS])
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
                             int(max_iter + warm), int(fit_intercept), first[0], aff, s)
             first[0] = 0
@@ -311,7 +320,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
             hi = min(lo + batch_rows, n)
             _pass(m, rows, ws, False, lo, hi, fp8_scale, s, done=False)
             if comm is not None and comm.world_size > 1:
-                comm.all_reduce_(ws.red[:64])
+                comm.all_reduce_(ws.red[:GRAD_SLOTS])
             m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), d, float(C), float(lr), float(momentum),
                          int(fit_intercept), s)
             gstep = ep * nb + b + 1

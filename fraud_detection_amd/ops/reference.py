@@ -269,7 +269,8 @@ class NewtonStateRef:
         else:
             self.gmax = gmax
             Hf = np.asarray(red[64:]).reshape(32, 32)
-            A = Hf[np.ix_(idx, idx)] / S
+            SH = red[34] if red[34] > 0 else S  # weight of the rows behind H (device: slot 34)
+            A = Hf[np.ix_(idx, idx)] / SH
             for k, j in enumerate(idx):
                 if j < d:
                     A[k, k] += reg

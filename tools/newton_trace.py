@@ -46,6 +46,9 @@ def main():
     # name: (warm-up schedule, full-data Hessian stride, Hessian refresh period (0 = every iter))
     variants = {
         "auto": (L.progressive_schedule(n), L.auto_hess_stride(n), L.auto_hess_refresh(n)),
+        "s16x3s4x1_h4_r4": ([(16, 3), (4, 1)], 4, 4),
+        "s16x2s4x2_h4_r4": ([(16, 2), (4, 2)], 4, 4),
+        "s8x2s2x1_h4_r4": ([(8, 2), (2, 1)], 4, 4),
         "s4x3_h3_r0": ([(4, 3)], 3, 0),
         "s16x2s4x2_h2_r0": ([(16, 2), (4, 2)], 2, 0),
         "s16x3s4x2_h2_r0": ([(16, 3), (4, 2)], 2, 0),
@@ -67,7 +70,8 @@ def main():
             hs_w = hs if full else L.auto_hess_stride(n // sub)
             for jj in range(iters):
                 if full:
-                    fresh = refresh <= 0 or j_full % refresh == 0
+                    # as ops/logreg.newton_fit: after a warm-up the first full iterations reuse its H
+                    fresh = refresh <= 0 or (j_full + (1 if sched else 0)) % refresh == 0
                     j_full += 1
                     hs_w = hs if fresh else 0
                 torch.cuda.synchronize()
