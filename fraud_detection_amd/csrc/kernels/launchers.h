@@ -13,6 +13,16 @@ namespace fdx {
 
 // FDX_SYNC_LAUNCH=1: synchronise after every launch so an asynchronous fault is reported with
 // the name of the kernel that caused it (debug mode, like AMD_SERIALIZE_KERNEL=3 but attributed).
+// FDX_NT_STORES=1: streaming (nontemporal) stores for the big write-once outputs (fused scaler
+// rows, SMOTE rows) -- an A/B switch for profiling.
+inline bool nt_stores() {
+  static const bool on = [] {
+    const char* e = std::getenv("FDX_NT_STORES");
+    return e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 inline bool sync_launch_mode() {
   static const int mode = [] {
     const char* v = std::getenv("FDX_SYNC_LAUNCH");

@@ -192,6 +192,7 @@ __device__ __forceinline__ int stats_fetch(const float* __restrict__ X, int64_t 
 // s = x - pivot (col 30 = bias_value, col 31 = label).  The standardization z = (s - c) / sigma
 // is applied later as an exact affine map on the solver's 32x32 sums (newton_update with aff),
 // so the raw matrix is read once instead of twice (stats, then cast) per fit.
+template <bool NT>
 __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
     const float* __restrict__ X, int64_t n, int d, const float* __restrict__ pivot,
     const uint8_t* __restrict__ labels, float bias_value, uint16_t* __restrict__ out,
@@ -252,7 +253,8 @@ __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
       uint4 pk;
       pk.x = pack_bf16x2(o[0], o[1]); pk.y = pack_bf16x2(o[2], o[3]);
       pk.z = pack_bf16x2(o[4], o[5]); pk.w = pack_bf16x2(o[6], o[7]);
-      reinterpret_cast<uint4*>(out)[grow * 4 + q] = pk;
+      if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(out) + grow * 4 + q);
+      else reinterpret_cast<uint4*>(out)[grow * 4 + q] = pk;
     }
     __syncthreads();
   }
@@ -659,8 +661,9 @@ void launch_scaler_finalize(const double* sums, double n, const float* pivot, in
 }
 
 int scaler_stats_cast_blocks() {
-  static const int cap = resident_cap(scaler_stats_cast_kernel, kThreads);
-  return cap;
+  static const int cap = resident_cap(scaler_stats_cast_kernel<false>, kThreads);
+  static const int cap_nt = resident_cap(scaler_stats_cast_kernel<true>, kThreads);
+  return nt_stores() ? cap_nt : cap;
 }
 
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
@@ -669,8 +672,12 @@ void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* piv
     throw std::invalid_argument("scaler_stats_cast: contiguous 16-byte aligned rows, d <= 30");
   // every block must be resident at once (a second round of blocks would double the span);
   // nblocks is fixed by the caller (partial buffer), the grid-stride loop covers the rest
-  scaler_stats_cast_kernel<<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
-                                                             reinterpret_cast<uint16_t*>(out), partial);
+  if (nt_stores())
+    scaler_stats_cast_kernel<true><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
+                                                                     reinterpret_cast<uint16_t*>(out), partial);
+  else
+    scaler_stats_cast_kernel<false><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
+                                                                      reinterpret_cast<uint16_t*>(out), partial);
   check_launch("scaler_stats_cast");
 }
 

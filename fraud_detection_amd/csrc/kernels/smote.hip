@@ -19,7 +19,7 @@ namespace {
 
 constexpr int kThreads = 256;
 
-template <int OUT>  // 0 = bf16 rows (64 B), 1 = fp32 rows (128 B, GBDT input), 2 = fp8 e4m3 rows (32 B)
+template <int OUT, bool NT = false>  // OUT: 0 = bf16 rows (64 B), 1 = fp32 (GBDT input), 2 = fp8 e4m3 (32 B)
 __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     const float* __restrict__ C, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
     int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
@@ -96,7 +96,10 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
         pk.y = pack_bf16x2(o[2], o[3]);
         pk.z = pack_bf16x2(o[4], o[5]);
         pk.w = pack_bf16x2(o[6], o[7]);
-        reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
+        // NT: streaming store (nt policy) so the output stream does not evict the L2-resident
+        // parent rows every gather reads
+        if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(out) + s * 4 + q);
+        else reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
       } else if constexpr (OUT == 1) {
         float4* dst = reinterpret_cast<float4*>(out) + s * 8 + 2 * q;
         dst[0] = make_float4(o[0], o[1], o[2], o[3]);
@@ -131,7 +134,11 @@ void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_
   static const int cap0 = resident_cap(smote_generate_kernel<0>, kThreads);
   static const int cap1 = resident_cap(smote_generate_kernel<1>, kThreads);
   static const int cap2 = resident_cap(smote_generate_kernel<2>, kThreads);
-  if (out_kind == 0)
+  static const int capn = resident_cap(smote_generate_kernel<0, true>, kThreads);
+  if (out_kind == 0 && nt_stores())
+    smote_generate_kernel<0, true><<<capped_grid(n_new, per_block, capn), kThreads, 0, stream>>>(
+        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
+  else if (out_kind == 0)
     smote_generate_kernel<0><<<capped_grid(n_new, per_block, cap0), kThreads, 0, stream>>>(
         C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
   else if (out_kind == 1)

@@ -216,9 +216,6 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                             int(fit_intercept), int(j == 0), aff, s)
         first[0] = 1
     if dp and local_warmup and sched:
-        # the full-data phase starts from the warm-up Hessian: sum the ranks' sample Hessians and
-        # their weights so every rank takes the same first step
-        comm.all_reduce_(ws.red[GRAD_SLOTS:])
         wv = ws.state[S_W:S_W + 32]
         comm.all_reduce_(wv)
         wv.div_(comm.world_size)
@@ -235,9 +232,10 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
 
     def enqueue_chunk(k: int) -> int:
         for _ in range(k):
-            # after a warm-up the first full-data iterations reuse its last Hessian (a >= 1M-row
-            # sample mean, rescaled to the full gradient through red[34]); then every refresh-th
-            fresh = refresh <= 0 or (full_it[0] + (1 if warm else 0)) % refresh == 0
+            # a fresh Hessian on the first full-data iteration, then every refresh-th (starting
+            # the full phase from the warm-up's 4M-row Hessian instead cost one more full pass:
+            # 8 vs 7 iterations, profiles/r1_s25)
+            fresh = refresh <= 0 or full_it[0] % refresh == 0
             full_it[0] += 1
             _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s)
             if comm is not None and comm.world_size > 1:

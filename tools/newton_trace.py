@@ -44,25 +44,26 @@ def main():
     print(f"rows {n}  auto_hess_stride {L.auto_hess_stride(n)}  auto schedule {L.progressive_schedule(n)}")
 
     # name: (warm-up schedule, full-data Hessian stride, Hessian refresh period (0 = every iter))
+    # name: (warm-up schedule, full-data Hessian stride, Hessian refresh period (0 = every iter),
+    #        1 = the full phase starts from the warm-up's last Hessian)
     variants = {
-        "auto": (L.progressive_schedule(n), L.auto_hess_stride(n), L.auto_hess_refresh(n)),
-        "s16x3s4x1_h4_r4": ([(16, 3), (4, 1)], 4, 4),
-        "s16x2s4x2_h4_r4": ([(16, 2), (4, 2)], 4, 4),
-        "s8x2s2x1_h4_r4": ([(8, 2), (2, 1)], 4, 4),
-        "s4x3_h3_r0": ([(4, 3)], 3, 0),
-        "s16x2s4x2_h2_r0": ([(16, 2), (4, 2)], 2, 0),
-        "s16x3s4x2_h2_r0": ([(16, 3), (4, 2)], 2, 0),
-        "s16x2s4x2_h2_r2": ([(16, 2), (4, 2)], 2, 2),
-        "s16x2s4x2_h2_r9": ([(16, 2), (4, 2)], 2, 99),
-        "s16x3s4x2_h2_r9": ([(16, 3), (4, 2)], 2, 99),
-        "s16x2s4x2_h1_r9": ([(16, 2), (4, 2)], 1, 99),
-        "s16x2s4x2_h3_r9": ([(16, 2), (4, 2)], 3, 99),
-        "s32x2s8x2s2x1_h2_r9": ([(32, 2), (8, 2), (2, 1)], 2, 99),
-        "s16x2s4x3_h2_r9": ([(16, 2), (4, 3)], 2, 99),
+        "auto": (L.progressive_schedule(n), L.auto_hess_stride(n), L.auto_hess_refresh(n), 0),
+        "auto_lazy0": (L.progressive_schedule(n), L.auto_hess_stride(n), L.auto_hess_refresh(n), 1),
+        "s16x3s4x2_h4_r4": ([(16, 3), (4, 2)], 4, 4, 0),
+        "s16x3s4x1_h4_r4": ([(16, 3), (4, 1)], 4, 4, 0),
+        "s16x2s4x2_h4_r4": ([(16, 2), (4, 2)], 4, 4, 0),
+        "s16x3s4x2_h8_r4": ([(16, 3), (4, 2)], 8, 4, 0),
+        "s32x3s8x2_h4_r4": ([(32, 3), (8, 2)], 4, 4, 0),
+        "s32x3s8x1s2x1_h4_r4": ([(32, 3), (8, 1), (2, 1)], 4, 4, 0),
+        "s16x3s4x2_h4_r0": ([(16, 3), (4, 2)], 4, 0, 0),
     }
     out = {}
-    for name, (sched, hs, refresh) in variants.items():
+    aff = res.scaler.aff  # the pipeline's rows are pivot-shifted (scaler folded into the solver)
+    aptr = ptr(aff) if aff is not None else 0
+    for name, (sched, hs, refresh, lazy0) in variants.items():
         ws.reset(w0, (1.0, 1.0))
+        if aptr:
+            m.logreg_fold(ptr(ws.state), aptr, ptr(ws.w32), s)
         trace = []
         j_full = 0
         for phase, (sub, iters) in enumerate(sched + [(1, 25)]):
@@ -70,15 +71,14 @@ def main():
             hs_w = hs if full else L.auto_hess_stride(n // sub)
             for jj in range(iters):
                 if full:
-                    # as ops/logreg.newton_fit: after a warm-up the first full iterations reuse its H
-                    fresh = refresh <= 0 or (j_full + (1 if sched else 0)) % refresh == 0
+                    fresh = refresh <= 0 or (j_full + lazy0) % refresh == 0
                     j_full += 1
                     hs_w = hs if fresh else 0
                 torch.cuda.synchronize()
                 t0 = time.perf_counter()
                 L._pass(m, rows, ws, hs_w, 0, n, 4.0, s, sub=sub)
                 m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0,
-                                a.tol if full else 0.0, 1 << 30, 1, int(jj == 0 and phase > 0), 0, s)
+                                a.tol if full else 0.0, 1 << 30, 1, int(jj == 0 and phase > 0), aptr, s)
                 torch.cuda.synchronize()
                 dt = (time.perf_counter() - t0) * 1e6
                 st = ws.state.cpu().numpy()
