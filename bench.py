@@ -59,9 +59,13 @@ def main():
     if not torch.cuda.is_available():
         print("bench.py requires a ROCm GPU", file=sys.stderr)
         return 2
+    # Rehearsal knobs for a one-GPU box (never used by the driver's runs): FDX_BENCH_ONE_GPU=1 puts
+    # every rank on cuda:0, FDX_BENCH_BACKEND=gloo swaps RCCL for host-staged gloo collectives.
+    if os.environ.get("FDX_BENCH_ONE_GPU") == "1":
+        local_rank = 0
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    comm = Communicator(device=dev) if world_env > 1 else None
+    comm = Communicator(backend=os.environ.get("FDX_BENCH_BACKEND") or None, device=dev) if world_env > 1 else None
     rank = comm.rank if comm else 0
     world = comm.world_size if comm else 1
     if args.gpus != world and rank == 0:

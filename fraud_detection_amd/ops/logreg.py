@@ -79,7 +79,9 @@ def _blob_views(blob: torch.Tensor):
             blob[2176:2184].view(torch.float32), blob[2184:2188].view(torch.int32))
 
 
-HESS_SAMPLE_ROWS = 1 << 22  # auto Hessian sub-sampling keeps >= ~4M rows in the H estimate
+# auto Hessian sub-sampling keeps >= ~2M rows in the H estimate: at 16M rows stride 8 converges in
+# the same 2 full passes as stride 3 and saves ~19 us of MFMA staging (profiles/r1_s26 trace)
+HESS_SAMPLE_ROWS = 1 << 21
 
 
 GRAD_SLOTS = 34  # red[0:32] gradient, red[32] loss, red[33] weight; red[34] = Hessian-sample weight
@@ -157,7 +159,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                local_warmup: bool = True, affine: torch.Tensor | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
-    ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~4M rows per rank);
+    ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
     gradient and objective always use all rows, so the converged solution is unchanged.
     ``hess_refresh``: in the full-data phase a fresh Hessian only every k-th iteration; the
     iterations in between stream the gradient alone (-36% bytes of MFMA-free work per pass) and
