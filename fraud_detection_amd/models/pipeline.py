@@ -12,7 +12,7 @@ Evaluation: folded-scaler predict on raw fp32 test rows (K5) -> exact AUC (K10) 
 from __future__ import annotations
 
 import time
-from dataclasses import asdict, dataclass, field
+from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -58,14 +58,18 @@ class TrainConfig:
 
 @dataclass
 class PipelineResult:
-    w: np.ndarray                  # [32] float64 standardized-space weights, w[30] = intercept
     scaler: scaler_ops.ScalerStats
-    fit: lr_ops.FitInfo
+    fit: lr_ops.FitInfo            # or lr_ops.PendingFit (device fits: read lazily)
     n_rows: int                    # local raw training rows
     n_train_rows: int              # local post-SMOTE rows
     n_minority: int
     n_synthetic: int
     timings: dict = field(default_factory=dict)
+
+    @property
+    def w(self) -> np.ndarray:
+        """[32] float64 standardized-space weights, w[30] = intercept."""
+        return self.fit.w
 
     @property
     def coef(self) -> np.ndarray:
@@ -201,7 +205,7 @@ class DevicePipeline:
         else:
             raise ValueError(f"unknown solver {cfg.solver!r}")
         tm.mark("fit")
-        return PipelineResult(w=fit.w, scaler=stats, fit=fit, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
+        return PipelineResult(scaler=stats, fit=fit, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
                               n_synthetic=n_new, timings=dict(tm.t))
 
 
@@ -225,6 +229,6 @@ def evaluate(result: PipelineResult, X_test: torch.Tensor, y_test: torch.Tensor,
 
 
 def result_summary(r: PipelineResult) -> dict:
-    d = {k: v for k, v in asdict(r.fit).items() if k != "w" and k != "history"}
+    d = {k: v for k, v in lr_ops.fit_asdict(r.fit).items() if k != "w" and k != "history"}
     d.update(n_rows=r.n_rows, n_train_rows=r.n_train_rows, n_minority=r.n_minority, n_synthetic=r.n_synthetic)
     return d

@@ -39,6 +39,61 @@ class FitInfo:
     history: list = field(default_factory=list)
 
 
+_FIT_FIELDS = ("w", "n_iter", "n_newton_steps", "converged", "objective", "grad_max", "history")
+
+
+class PendingFit:
+    """A device fit whose solver state is on its way to pinned host memory.  Reading any FitInfo
+    field waits for that copy only, so a caller that does not look at the result right away (a
+    training loop, the benchmark) queues the next fit behind this one with no host round trip at
+    the fit boundary.  Pinned slots rotate through a small pool; a slot's previous owner is
+    materialised before the slot is reused."""
+
+    _pool: list = []
+    _owners: list = []
+    _next = 0
+    _POOL = 8
+
+    def __init__(self, state_dev: torch.Tensor, sgd: bool = False):
+        cls = PendingFit
+        if not cls._pool:
+            cls._pool = [torch.empty(state_dev.numel(), dtype=torch.float64, pin_memory=True)
+                         for _ in range(cls._POOL)]
+            cls._owners = [None] * cls._POOL
+        slot = cls._next % cls._POOL
+        cls._next += 1
+        prev = cls._owners[slot]
+        if prev is not None:
+            prev._materialize()
+        cls._owners[slot] = self
+        self._slot, self._sgd, self._info = slot, sgd, None
+        cls._pool[slot].copy_(state_dev, non_blocking=True)
+        self._event = torch.cuda.Event()
+        self._event.record()
+
+    def _materialize(self) -> FitInfo:
+        if self._info is None:
+            self._event.synchronize()
+            self._info = _info_from_state(PendingFit._pool[self._slot].numpy().copy(), self._sgd)
+            if PendingFit._owners[self._slot] is self:
+                PendingFit._owners[self._slot] = None
+        return self._info
+
+    def __getattr__(self, name):
+        if name in _FIT_FIELDS:
+            return getattr(self._materialize(), name)
+        raise AttributeError(name)
+
+    def as_fit_info(self) -> FitInfo:
+        return self._materialize()
+
+
+def fit_asdict(fit) -> dict:
+    """dataclasses.asdict for FitInfo or PendingFit."""
+    f = fit.as_fit_info() if isinstance(fit, PendingFit) else fit
+    return {k: getattr(f, k) for k in _FIT_FIELDS}
+
+
 class LRWorkspace:
     """Device buffers reused across iterations / fits (no allocation inside the loop)."""
 
@@ -251,8 +306,10 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     # Convergence is checked one chunk behind: chunk i+1 is already queued when the host reads
     # chunk i's `done` flag (async copy into pinned memory), so the GPU never waits on the host.
     # Iterations after convergence are device-side no-ops.  Every rank reads identical flags.
-    flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
-    events = [torch.cuda.Event(), torch.cuda.Event()]
+    if getattr(ws, "_flags", None) is None:  # pinned allocations cost tens of us: once per workspace
+        ws._flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        ws._events = [torch.cuda.Event(), torch.cuda.Event()]
+    flags, events = ws._flags, ws._events
     it = enqueue_chunk(min(check_every, max_iter))
     flags[0].copy_(ws.done, non_blocking=True)
     events[0].record()
@@ -269,7 +326,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         if int(flags[cur][0]):
             break
         cur = nxt
-    return _info_from_state(ws.state.cpu().numpy())
+    return PendingFit(ws.state)
 
 
 def _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm):
