@@ -1,0 +1,132 @@
+#!/usr/bin/env python3
+"""The BASELINE.json target configurations on one MI355X (bench.py measures config 3's Newton
+variant; this tool covers the others).  One JSON object per config on stdout.
+
+    python tools/baseline_configs.py [--only c2,c3,c4,c5] [--json out.json]
+
+c2  batch /predict: raw fp32 rows -> folded scaler + GEMV + sigmoid (one kernel), 1M x 30; and the
+    bf16-row variant (scale_cast to the padded bf16 layout, then the predict kernel)
+c3  SMOTE k-NN + logistic SGD train, 10M x 30 (8M train / 2M test), bf16 rows, AUC >= 0.95
+c4  async XAI worker path: KernelSHAP coalition GEMM (MFMA), 1k explanations per batch
+c5  fp8 rows: the DP=8 per-GPU shard of 100M rows (12.5M rows) as one fit, and the whole 100M
+    rows on ONE GPU (HBM sizing: raw + padded rows + SMOTE output resident together)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+CPU_PREDICT_ROWS_PER_S = 25.7e6   # BASELINE.md §2, predict_proba @ 1M rows
+CPU_TRAIN_ROWS_PER_S = 3.50e6     # BASELINE.md §2, LR lbfgs fit @ 10M rows (15.97M post-SMOTE)
+CPU_LINEAR_SHAP_PER_S = 316e6     # BASELINE.md §2, LinearSHAP values/s @ 10M rows
+
+
+def _timed(fn, reps, warmup=2):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        out = fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / reps, out
+
+
+def c2(dev):
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+    from fraud_detection_amd.ops import predict as P
+    from fraud_detection_amd.ops import scaler as S
+
+    X, y = separable(2_000_000, seed=3, device=dev)
+    res = DevicePipeline(TrainConfig()).fit(X, y)
+    Xq, _ = separable(1_000_000, seed=4, device=dev)
+    a, c, b = res.folded()
+    at, ct = torch.from_numpy(a).to(dev), torch.from_numpy(c).to(dev)
+    t_raw, _ = _timed(lambda: P.predict_shap_raw(Xq, at, ct, b, dphi=0), 20)
+    rows = torch.empty((Xq.shape[0], 32), dtype=torch.bfloat16, device=dev)
+    w = torch.from_numpy(res.w)
+
+    def bf16_path():
+        S.scale_cast(Xq, res.scaler, out=rows)
+        return P.predict_rows(rows, w)
+    t_bf16, _ = _timed(bf16_path, 20)
+    n = Xq.shape[0]
+    return {"config": "c2 batch predict 1M x 30", "rows": n,
+            "raw_fused_rows_per_s": round(n / t_raw, 1), "raw_fused_us": round(t_raw * 1e6, 1),
+            "bf16_rows_per_s": round(n / t_bf16, 1), "bf16_us": round(t_bf16 * 1e6, 1),
+            "vs_cpu_predict_proba": round(n / t_raw / CPU_PREDICT_ROWS_PER_S, 1)}
+
+
+def _train_cfg(dev, n_total, storage, solver, reps=5, label=""):
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    n_test = n_total // 5
+    X, y = separable(n_total - n_test, seed=1000, device=dev)
+    Xt, yt = separable(n_test, seed=5000, device=dev)
+    pipe = DevicePipeline(TrainConfig(storage=storage, solver=solver, seed=42))
+    torch.cuda.reset_peak_memory_stats(dev)
+    dt, res = _timed(lambda: pipe.fit(X, y), reps, warmup=1)
+    ev = evaluate(res, Xt, yt)
+    return {"config": label, "rows_raw": n_total, "rows_post_smote": res.n_train_rows, "storage": storage,
+            "solver": solver, "ms_per_fit": round(dt * 1e3, 3),
+            "post_smote_rows_per_s": round(res.n_train_rows / dt, 1),
+            "vs_cpu_lbfgs_fit": round(res.n_train_rows / dt / CPU_TRAIN_ROWS_PER_S, 1),
+            "auc": round(ev["auc"], 6), "converged": bool(res.fit.converged), "iters": int(res.fit.n_iter),
+            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2)}
+
+
+def c3(dev):
+    return _train_cfg(dev, 10_000_000, "bf16", "sgd", label="c3 SMOTE + logistic SGD, 10M x 30 bf16")
+
+
+def c4(dev):
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.explainers import kernelshap_throughput
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+    X, y = separable(2_000_000, seed=3, device=dev)
+    res = DevicePipeline(TrainConfig()).fit(X, y)
+    out = kernelshap_throughput(res, dev, None, n_expl=1000)
+    out["config"] = "c4 KernelSHAP coalition GEMM, 1k explanations/batch (1 GPU; DP=8 multiplies by ranks)"
+    out["vs_cpu_linear_shap"] = round(out["kernelshap_values_per_sec"] / CPU_LINEAR_SHAP_PER_S, 2)
+    return out
+
+
+def c5(dev):
+    shard = _train_cfg(dev, 12_500_000, "fp8", "newton", reps=5,
+                       label="c5 fp8 rows: the 12.5M-row per-GPU shard of 100M at DP=8")
+    whole = _train_cfg(dev, 100_000_000, "fp8", "newton", reps=2,
+                       label="c5 fp8 rows: all 100M rows on one GPU (HBM sizing)")
+    return [shard, whole]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="c2,c3,c4,c5")
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    out = []
+    for name in a.only.split(","):
+        r = globals()[name](dev)
+        for item in (r if isinstance(r, list) else [r]):
+            print(json.dumps(item), flush=True)
+            out.append(item)
+        torch.cuda.empty_cache()
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
