@@ -60,6 +60,9 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_scaler_finalize(P<const double>(sums), n, P<const float>(pivot), d, P<double>(mean64), P<double>(var64),
                                 P<double>(scale64), P<float>(mean32), P<float>(inv32), P<double>(aff), S(s));
   });
+  m.def("fp8_hw_check", [](u dec, u vals, int n, u enc, u s) {
+    fdx::launch_fp8_hw_check(P<float>(dec), P<const float>(vals), n, P<uint8_t>(enc), S(s));
+  });
   m.def("scaler_stats_cast_blocks", []() { return fdx::scaler_stats_cast_blocks(); });
   m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,
                                 int nblocks, u s) {

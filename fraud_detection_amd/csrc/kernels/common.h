@@ -42,6 +42,26 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f32_to_bf16(lo) | ((uint32_t)f32_to_bf16(hi) << 16);
 }
 
+// Hardware conversions (gfx950 v_cvt_pk_f32_fp8 / v_cvt_pk_fp8_f32 read and write OCP e4m3):
+// one instruction per 2 values instead of the ~20-op software decode below, which made the fp8
+// training pass VALU-bound.  tests/test_kernels_gpu.py::test_fp8_hardware_conversions pins them
+// against the software codec (all 256 codes; an encode sweep).
+__device__ __forceinline__ void fp8x4_to_f32(uint32_t w, float* out) {
+  const auto lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, false);
+  const auto hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, true);
+  out[0] = lo[0]; out[1] = lo[1]; out[2] = hi[0]; out[3] = hi[1];
+}
+// 4 floats -> 4 e4m3 bytes (RNE).  Inputs are clamped to +-448 first (OCP satfinite, as the
+// software encoder); NaN is not expected on these paths (standardized features).
+__device__ __forceinline__ uint32_t f32x4_to_fp8(float a, float b, float c, float d) {
+  const float m = 448.0f;
+  a = fminf(fmaxf(a, -m), m); b = fminf(fmaxf(b, -m), m);
+  c = fminf(fmaxf(c, -m), m); d = fminf(fmaxf(d, -m), m);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
 // ---- OCP fp8 e4m3fn (gfx950 is OCP, not fnuz) ---------------------------------------------
 // Software RNE encode/decode so the storage format is bit-exact and testable on the host.
 __host__ __device__ __forceinline__ float fp8e4m3_to_f32(uint8_t v) {

@@ -48,6 +48,7 @@ void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipS
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
                             float* inv32, double* aff, hipStream_t stream);
+void launch_fp8_hw_check(float* dec, const float* vals, int n, uint8_t* enc, hipStream_t stream);
 int scaler_stats_cast_blocks();  // resident blocks of the fused kernel on this device
 // fused K1+K2 for bf16 training rows: shifted sums -> partial[nblocks][64], rows s = x - pivot
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,

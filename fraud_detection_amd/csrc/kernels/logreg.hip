@@ -42,12 +42,10 @@ __device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
   x[4] = bf16lo(v.z); x[5] = bf16hi(v.z); x[6] = bf16lo(v.w); x[7] = bf16hi(v.w);
 }
 __device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8], int q, int d, float inv_s) {
+  fp8x4_to_f32(v.x, x);  // hardware OCP e4m3 decode, 2 values per instruction
+  fp8x4_to_f32(v.y, x + 4);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t word = j < 4 ? v.x : v.y;
-    const float f = fp8e4m3_to_f32((uint8_t)(word >> (8 * (j & 3))));
-    x[j] = (q * 8 + j < d) ? f * inv_s : f;
-  }
+  for (int j = 0; j < 8; ++j) x[j] = (q * 8 + j < d) ? x[j] * inv_s : x[j];
 }
 
 template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)

@@ -43,8 +43,10 @@ __device__ __forceinline__ float dot16_fp8(const uint4& v, const float* w) {
   float z = 0.0f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
+    float f[4];
+    fp8x4_to_f32(words[k], f);  // hardware OCP e4m3 decode
 #pragma unroll
-    for (int b = 0; b < 4; ++b) z = fmaf(fp8e4m3_to_f32((uint8_t)(words[k] >> (8 * b))), w[4 * k + b], z);
+    for (int b = 0; b < 4; ++b) z = fmaf(f[b], w[4 * k + b], z);
   }
   return z;
 }

@@ -623,6 +623,21 @@ __global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(
   }
 }
 
+// Hardware fp8 codec self-check: decode all 256 codes, encode n floats (4 per thread).
+__global__ void fp8_hw_check_kernel(float* __restrict__ dec, const float* __restrict__ vals, int n,
+                                    uint8_t* __restrict__ enc) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < 64) {
+    const uint32_t w = (uint32_t)(4 * t) | ((uint32_t)(4 * t + 1) << 8) | ((uint32_t)(4 * t + 2) << 16) |
+                       ((uint32_t)(4 * t + 3) << 24);
+    fp8x4_to_f32(w, dec + 4 * t);
+  }
+  if (4 * t + 3 < n) {
+    const uint32_t e = f32x4_to_fp8(vals[4 * t], vals[4 * t + 1], vals[4 * t + 2], vals[4 * t + 3]);
+    *reinterpret_cast<uint32_t*>(enc + 4 * t) = e;
+  }
+}
+
 inline int vec_for(const void* p, int ld) {
   const uintptr_t a = reinterpret_cast<uintptr_t>(p);
   if ((ld % 4) == 0 && (a % 16) == 0) return 4;
@@ -716,6 +731,12 @@ void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* 
 // Vector path when the label array is 16-byte aligned (torch allocations are); count and write
 // make the same choice from the same pointer, so their per-block ranges agree.
 static inline bool compact_vec(const uint8_t* labels) { return (reinterpret_cast<uintptr_t>(labels) & 15) == 0; }
+
+void launch_fp8_hw_check(float* dec, const float* vals, int n, uint8_t* enc, hipStream_t stream) {
+  const int threads = 256, blocks = (n / 4 + threads - 1) / threads + 1;
+  fp8_hw_check_kernel<<<blocks, threads, 0, stream>>>(dec, vals, n, enc);
+  check_launch("fp8_hw_check");
+}
 
 void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t* counts,
                           int nblocks, hipStream_t stream) {

@@ -408,3 +408,28 @@ def test_pipeline_fold_scaler_same_model(dev):
     assert ra.n_train_rows == rb.n_train_rows
     assert np.allclose(ra.w, rb.w, rtol=0, atol=5e-3)
     assert abs(ea["auc"] - eb["auc"]) < 2e-4 and ea["auc"] > 0.95
+
+
+def test_fp8_hardware_conversions(dev):
+    """gfx950 v_cvt_pk_f32_fp8 / v_cvt_pk_fp8_f32 against the software OCP e4m3 codec."""
+    from fraud_detection_amd.ops.native import native, ptr, stream_of
+
+    dec = torch.empty(256, dtype=torch.float32, device=dev)
+    rng = np.random.default_rng(0)
+    vals = np.concatenate([rng.normal(0, 3, 40_000), rng.uniform(-500, 500, 20_000),
+                           rng.normal(0, 0.01, 20_000), [0.0, -0.0, 448.0, -448.0, 464.0, 1e6, 2.0 ** -10]])
+    vals = vals[: len(vals) // 4 * 4].astype(np.float32)
+    vt = torch.from_numpy(vals).to(dev)
+    enc = torch.empty(len(vals), dtype=torch.uint8, device=dev)
+    native().fp8_hw_check(ptr(dec), ptr(vt), len(vals), ptr(enc), stream_of(vt))
+    codes = np.arange(256, dtype=np.uint8)
+    sw = ref.fp8_decode(codes)
+    hw = dec.cpu().numpy()
+    finite = np.isfinite(sw)
+    assert np.array_equal(hw[finite], sw[finite])
+    assert np.all(np.isnan(hw[~finite]))
+    e_sw = ref.fp8_encode(vals)
+    e_hw = enc.cpu().numpy()
+    # identical codes, except that -0.0 / tiny negatives may encode as +0 vs -0
+    diff = e_hw != e_sw
+    assert np.all(ref.fp8_decode(e_hw[diff]) == ref.fp8_decode(e_sw[diff])), vals[diff][:10]
