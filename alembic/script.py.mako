@@ -1,22 +1,23 @@
+## Template for `alembic revision`: every revision in this repo carries the same four
+## identifiers the built-in runner (fraud_detection_amd/store/migrations.py) reads.
+<%text># -*- revision -*-</%text>
 """${message}
 
-Revision ID: ${up_revision}
-Revises: ${down_revision | comma,n}
-Create Date: ${create_date}
+revision ${up_revision} (parent: ${down_revision | comma,n}), generated ${create_date}
 """
-from alembic import op
 import sqlalchemy as sa
+from alembic import op
 ${imports if imports else ""}
 
-revision = ${repr(up_revision)}
-down_revision = ${repr(down_revision)}
-branch_labels = ${repr(branch_labels)}
-depends_on = ${repr(depends_on)}
+revision, down_revision = ${repr(up_revision)}, ${repr(down_revision)}
+branch_labels, depends_on = ${repr(branch_labels)}, ${repr(depends_on)}
 
 
 def upgrade() -> None:
-    ${upgrades if upgrades else "pass"}
+    """Forward DDL for this revision."""
+    ${upgrades if upgrades else "return None"}
 
 
 def downgrade() -> None:
-    ${downgrades if downgrades else "pass"}
+    """Inverse of upgrade()."""
+    ${downgrades if downgrades else "return None"}

@@ -1,26 +1,34 @@
-"""Model loader utility (reference: api/utils.py:10-25)."""
+"""Model loader (reference contract: api/utils.py:10-25).
+
+``load_model_and_features(model_path=None, features_path=None) -> (LogisticRegression, [names])``
+with the reference's env defaults (MODEL_PATH, FEATURE_NAMES_PATH) and FileNotFoundError when the
+model is absent.  The model object is rebuilt from the decoded artifact
+(fraud_detection_amd.compat.sklearn_export): pickles this framework did not write are decoded
+without executing them.
+"""
 import json
 import logging
 import os
 
 from fraud_detection_amd.compat.sklearn_export import load_artifacts, make_logistic
 
-logger = logging.getLogger(__name__)
+log = logging.getLogger(__name__)
+_DEFAULTS = {"MODEL_PATH": "./models/logistic_model.joblib",
+             "FEATURE_NAMES_PATH": "./models/feature_names.json"}
 
 
-def load_model_and_features(model_path: str | None = None, features_path: str | None = None):
-    """Return (sklearn LogisticRegression, feature_names).  Files written by this framework are
-    loaded with joblib; foreign pickles only through the non-executing decoder."""
-    model_path = model_path or os.getenv("MODEL_PATH", "./models/logistic_model.joblib")
-    features_path = features_path or os.getenv("FEATURE_NAMES_PATH", "./models/feature_names.json")
-    if not os.path.exists(model_path):
-        logger.error("Model file not found: %s", model_path)
-        raise FileNotFoundError(f"Model not found at {model_path}")
-    scaler_path = os.path.join(os.path.dirname(model_path), "scaler.joblib")
-    art = load_artifacts(model_path, scaler_path, features_path if os.path.exists(features_path) else None)
-    model = make_logistic(art.coef, art.intercept, art.n_iter, art.C)
-    feature_names = []
-    if os.path.exists(features_path):
-        with open(features_path, "r", encoding="utf-8") as f:
-            feature_names = json.load(f)
-    return model, feature_names
+def _resolve(explicit, env):
+    return explicit or os.getenv(env, _DEFAULTS[env])
+
+
+def load_model_and_features(model_path=None, features_path=None):
+    mpath = _resolve(model_path, "MODEL_PATH")
+    fpath = _resolve(features_path, "FEATURE_NAMES_PATH")
+    if not os.path.isfile(mpath):
+        log.error("Model file not found: %s", mpath)
+        raise FileNotFoundError(f"Model not found at {mpath}")
+    have_names = os.path.isfile(fpath)
+    art = load_artifacts(mpath, os.path.join(os.path.dirname(mpath), "scaler.joblib"),
+                         fpath if have_names else None)
+    names = json.load(open(fpath, encoding="utf-8")) if have_names else []
+    return make_logistic(art.coef, art.intercept, art.n_iter, art.C), names
