@@ -179,6 +179,23 @@ __host__ __device__ __forceinline__ uint32_t u32_range(uint32_t v, uint32_t n) {
   return (uint32_t)(((uint64_t)v * (uint64_t)n) >> 32);
 }
 
+// SMOTE draw of sample s (Philox counter (s, counter_base), key seed): query row i uniform over
+// the mq rows, neighbour slot uniform over k (one Lemire pick over mq*k), interpolation weight on
+// a 2^-16 grid.  Packed as {i | lam_hi << 24, j | lam_lo << 24} so a draw is 8 bytes (smote.hip plan,
+// virtual SMOTE in logreg.hip); ops/reference.py smote_generate is the numpy oracle.
+__device__ __forceinline__ uint2 smote_draw(int64_t s, uint32_t cb0, uint32_t cb1, uint32_t key0, uint32_t key1,
+                                            uint32_t range, uint32_t k, const int* __restrict__ nbr) {
+  const Philox4 r = philox4x32_10((uint32_t)s, (uint32_t)(s >> 32), cb0, cb1, key0, key1);
+  const uint32_t pick = u32_range(r.x, range);
+  const uint32_t i = pick / k;
+  const uint32_t j = (uint32_t)nbr[(int64_t)i * k + (pick - i * k)];
+  const uint32_t lam = r.y >> 16;
+  return make_uint2(i | ((lam >> 8) << 24), j | ((lam & 0xffu) << 24));
+}
+__host__ __device__ __forceinline__ float smote_lambda(uint32_t dx, uint32_t dy) {
+  return (float)(((dx >> 24) << 8) | (dy >> 24)) * (1.0f / 65536.0f);
+}
+
 // Grid sizing for streaming kernels: enough blocks to fill 256 CUs several times over
 // (cdna_hip_programming.md Guideline 11), grid-stride beyond that.
 __host__ inline int stream_grid(int64_t work_items, int items_per_block, int max_blocks = 2048) {

@@ -1,7 +1,8 @@
 // K9 smote_generate: synthetic minority rows x_new = x_i + lambda (x_nn - x_i).
 //
 // Reference behaviour being replaced: imblearn SMOTE._generate_samples (random row i among the
-// minority rows, random neighbour among its k nearest, lambda ~ U[0,1)) used at
+// minority rows, random neighbour among its k nearest, lambda ~ U[0,1) -- here on a 2^-16 grid, so
+// a draw packs into 8 bytes: common.h smote_draw) used at
 // train_model.py:65-66,91-92 and preprocess.py:43-44.  imblearn draws
 // from numpy MT19937; here every sample s owns Philox4x32-10 counter (s, counter_base), so the
 // output is independent of launch geometry and the CPU oracle (ops/reference.py) reproduces it
@@ -44,11 +45,10 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   // latency per iteration instead of two.
   auto draw = [&](int64_t b, int& di, int& dj, float& dl) {
     const int64_t sl = b + lane;
-    const Philox4 r = philox4x32_10((uint32_t)sl, (uint32_t)(sl >> 32), cb0, cb1, key0, key1);
-    const uint32_t pick = u32_range(r.x, range);
-    di = (int)(pick / (uint32_t)k);
-    dj = sl < n_new ? nbr[(int64_t)di * k + (int)(pick % (uint32_t)k)] : 0;
-    dl = u32_to_unit(r.y);
+    const uint2 d = sl < n_new ? smote_draw(sl, cb0, cb1, key0, key1, range, (uint32_t)k, nbr) : make_uint2(0, 0);
+    di = (int)(d.x & 0xffffffu);
+    dj = (int)(d.y & 0xffffffu);
+    dl = smote_lambda(d.x, d.y);
   };
   int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 64;
   int my_i = 0, my_j = 0;
@@ -122,7 +122,28 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   }
 }
 
+// The draws alone (8 B per sample): virtual SMOTE rebuilds the rows from them inside every solver
+// pass (logreg.hip), 64 MB per pass for 8M samples instead of 512 MB of stored bf16 rows.
+__global__ __launch_bounds__(kThreads) void smote_plan_kernel(const int* __restrict__ nbr, uint32_t range,
+                                                              uint32_t k, int64_t n_new, uint32_t key0,
+                                                              uint32_t key1, uint32_t cb0, uint32_t cb1,
+                                                              uint2* __restrict__ plan) {
+  const int64_t step = (int64_t)gridDim.x * kThreads;
+  for (int64_t s = (int64_t)blockIdx.x * kThreads + threadIdx.x; s < n_new; s += step)
+    plan[s] = smote_draw(s, cb0, cb1, key0, key1, range, k, nbr);
+}
+
 }  // namespace
+
+void launch_smote_plan(const int* nbr, int mq, int k, int64_t n_new, uint64_t seed, uint64_t counter_base,
+                       void* plan, hipStream_t stream) {
+  if (n_new <= 0) return;
+  static const int cap = resident_cap(smote_plan_kernel, kThreads);
+  smote_plan_kernel<<<capped_grid(n_new, kThreads, cap), kThreads, 0, stream>>>(
+      nbr, (uint32_t)mq * (uint32_t)k, (uint32_t)k, n_new, (uint32_t)seed, (uint32_t)(seed >> 32),
+      (uint32_t)counter_base, (uint32_t)(counter_base >> 32), reinterpret_cast<uint2*>(plan));
+  check_launch("smote_plan");
+}
 
 void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,

@@ -307,6 +307,32 @@ def knn_topk(Q: np.ndarray, C: np.ndarray, k: int, self_offset: int = -1):
     return idx, d2
 
 
+def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int) -> np.ndarray:
+    """uint32 [n_new, 2] SMOTE draws {i | lam_hi << 24, j | lam_lo << 24} (common.h smote_draw):
+    query row i and neighbour slot from one Lemire pick over mq*k, lam = (r.y >> 16) / 2^16."""
+    nbr = np.asarray(nbr)
+    mq, k = nbr.shape
+    s = np.arange(n_new, dtype=np.uint64)
+    r = philox4x32_10((s & _MASK32).astype(np.uint32), (s >> np.uint64(32)).astype(np.uint32),
+                      np.full(n_new, counter_base & 0xFFFFFFFF, np.uint32),
+                      np.full(n_new, (counter_base >> 32) & 0xFFFFFFFF, np.uint32),
+                      seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+    pick = u32_range(r[0], mq * k)
+    i = (pick // k).astype(np.uint32)
+    j = nbr[i, pick % k].astype(np.uint32)
+    lam = r[1].astype(np.uint32) >> np.uint32(16)
+    return np.stack([i | ((lam >> np.uint32(8)) << np.uint32(24)), j | ((lam & np.uint32(0xFF)) << np.uint32(24))], 1)
+
+
+def smote_draws_decode(plan: np.ndarray):
+    """(i, j, lam float32) from smote_plan words."""
+    p = np.asarray(plan, dtype=np.uint32)
+    lam16 = ((p[:, 0] >> np.uint32(24)) << np.uint32(8)) | (p[:, 1] >> np.uint32(24))
+    mask = np.uint32(0xFFFFFF)
+    return ((p[:, 0] & mask).astype(np.int64), (p[:, 1] & mask).astype(np.int64),
+            lam16.astype(np.float32) * np.float32(1.0 / 65536.0))
+
+
 def smote_generate(C: np.ndarray, nbr: np.ndarray, q_offset: int, n_new: int, seed: int,
                    counter_base: int, label: float = 1.0) -> np.ndarray:
     """fp32 synthetic rows (before bf16/fp8 rounding), bit-exact Philox draws."""
@@ -318,11 +344,8 @@ def smote_generate(C: np.ndarray, nbr: np.ndarray, q_offset: int, n_new: int, se
                       np.full(n_new, counter_base & 0xFFFFFFFF, np.uint32),
                       np.full(n_new, (counter_base >> 32) & 0xFFFFFFFF, np.uint32),
                       seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    pick = u32_range(r[0], mq * k)
-    i = pick // k
-    kk = pick % k
-    lam = u32_to_unit(r[1])[:, None]
-    j = nbr[i, kk]
+    i, j, lam = smote_draws_decode(smote_plan(nbr, n_new, seed, counter_base))
+    lam = lam[:, None]
     xi = C[q_offset + i]
     xj = C[j]
     out = (xi + lam * (xj - xi)).astype(np.float32)

@@ -117,6 +117,16 @@ def main():
     case(f"knn_topk_{m}", lambda: K.knn_topk(xmin, xmin, 5, 0), m * m * 64)
     nbr = K.knn_topk(xmin, xmin, 5, 0)
     case("smote_generate_n", lambda: K.smote_generate(xmin, nbr, 0, n, outb), n * 64)
+    # virtual SMOTE: n real rows + n synthesized in the pass (vs logreg_pass_*_2n over 2n stored rows)
+    vr = L.VirtualRows(xmin, nbr, 0, n, seed=42)
+
+    def lr_pass_virtual(h):
+        def f():
+            L._pass(nat, rows2[:n], ws, h, 0, N2, 4.0, s, done=False, vrows=vr)
+        return f
+    case("logreg_pass_virtual_hess_s3_2n", lr_pass_virtual(3), n * 64)
+    case("logreg_pass_virtual_grad_2n", lr_pass_virtual(0), n * 64)
+    case("newton_fit_virtual_2n_tol1e-4", lambda: L.newton_fit(rows2[:n], tol=1e-4, workspace=ws, vrows=vr), n * 64)
     sc = torch.randn(2_000_000, device=dev)
     yl = (torch.rand(2_000_000, device=dev) < 0.002).to(torch.uint8)
     case("roc_auc_2M", lambda: M.roc_auc(sc, yl), 2_000_000 * 5)
