@@ -117,11 +117,11 @@ PYBIND11_MODULE(_fdx_native, m) {
                                 P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s));
   });
   m.def("logreg_pass_smote", [](u X, int fmt, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub,
-                                float xs, u C, u plan, int64_t q_off, int64_t n_real, float label, float out_scale,
-                                u aff, u partial, int nblocks, u s) {
+                                float xs, u parents, u plan, int64_t q_off, int64_t n_real, float label,
+                                float out_scale, u partial, int nblocks, u s) {
     fdx::VSmote v;
-    v.C = P<const float>(C); v.plan = P<const void>(plan); v.q_offset = q_off; v.n_real = n_real;
-    v.label = label; v.out_scale = out_scale; v.aff = P<const double>(aff);
+    v.P = P<const void>(parents); v.plan = P<const void>(plan); v.q_offset = q_off; v.n_real = n_real;
+    v.label = label; v.out_scale = out_scale;
     fdx::launch_logreg_pass_smote(P<const void>(X), fmt, rb, re, P<const float>(w), P<const float>(cw),
                                   P<const int>(done), hess, sub, xs, v, P<float>(partial), nblocks, S(s));
   });
@@ -154,10 +154,13 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("smote_plan", [](u nbr, int mq, int k, int64_t n_new, uint64_t seed, uint64_t counter_base, u plan, u s) {
     fdx::launch_smote_plan(P<const int>(nbr), mq, k, n_new, seed, counter_base, P<void>(plan), S(s));
   });
-  m.def("smote_generate", [](u C, u nbr, int mq, int k, int64_t q_off, int64_t n_new, uint64_t seed,
+  m.def("smote_parents", [](u C, int64_t m_rows, u aff, u out, u s) {
+    fdx::launch_smote_parents(P<const float>(C), m_rows, P<const double>(aff), P<uint16_t>(out), S(s));
+  });
+  m.def("smote_generate", [](u C, int parents_bf16, u nbr, int mq, int k, int64_t q_off, int64_t n_new, uint64_t seed,
                              uint64_t counter_base, float label, int out_kind, float out_scale, u aff, u out, u s) {
-    fdx::launch_smote_generate(P<const float>(C), P<const int>(nbr), mq, k, q_off, n_new, seed, counter_base, label,
-                               out_kind, out_scale, P<const double>(aff), P<void>(out), S(s));
+    fdx::launch_smote_generate(P<const void>(C), parents_bf16, P<const int>(nbr), mq, k, q_off, n_new, seed,
+                               counter_base, label, out_kind, out_scale, P<const double>(aff), P<void>(out), S(s));
   });
 
   // kernelshap

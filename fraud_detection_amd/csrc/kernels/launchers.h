@@ -92,12 +92,11 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
 // (launch_smote_plan) -- bit-identical to the stored rows launch_smote_generate writes from the
 // same draws, without storing them or re-reading them every Newton pass ("virtual SMOTE").
 struct VSmote {
-  const float* C = nullptr;      // fp32 standardized parent rows [.., 32] (all ranks' minority rows)
+  const void* P = nullptr;       // bf16 output-space parents (launch_smote_parents), all ranks' minority rows
   const void* plan = nullptr;    // [n_new] uint2 draws (launch_smote_plan), or nullptr
   int64_t q_offset = 0;          // this rank's query rows start at C[q_offset]
   int64_t n_real = 0;            // global index of the first SMOTE row
   float label = 1.0f, out_scale = 1.0f;
-  const double* aff = nullptr;   // [64] pivot-shift map (c | 1/sigma), nullable
 };
 void launch_logreg_pass_smote(const void* X, int fmt, int64_t row_begin, int64_t row_end, const float* w,
                               const float* class_w, const int* done, int hessian, int row_sub, float x_scale,
@@ -127,7 +126,10 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
 // j: neighbour row index into C, lam: 16-bit interpolation weight); requires mq, mc < 2^24.
 void launch_smote_plan(const int* nbr, int mq, int k, int64_t n_new, uint64_t seed, uint64_t counter_base,
                        void* plan, hipStream_t stream);
-void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
+// P [m, 32] bf16 = output-space parents: bf16(C * sigma + c) on the feature columns (aff nullable)
+void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t* P, hipStream_t stream);
+// C: fp32 standardized parents (+ aff applied per sample) or, parents_bf16, smote_parents output
+void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int mq, int k, int64_t q_offset,
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream);
 

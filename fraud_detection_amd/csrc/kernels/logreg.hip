@@ -50,16 +50,16 @@ __device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8], int q, i
 
 // Row sources of a pass.  Rows [0, n_split) of the window are "real", rows [n_split, n) are SMOTE
 // rows: stored after the real rows (VIRT = false) or rebuilt from their 8-byte draw (VIRT = true:
-// parents i, j and the 16-bit lambda of smote.hip's plan) -- the same interpolation, affine map
-// and rounding as smote_generate_kernel, so both sources give bit-identical rows.  The 64-row
+// parents i, j and the 16-bit lambda of smote.hip's plan) and the bf16 output-space parents -- the
+// same interpolation and rounding as smote_generate_kernel<.., PB = true>, so both sources give
+// bit-identical rows.  The 64-row
 // tiles of the two ranges are visited zipped (real, SMOTE, real, ...): HBM-bound real tiles and
 // ALU/L2-bound rebuilt tiles overlap on every CU instead of running as two phases.  Without SMOTE
 // rows (n_split >= n) the zip is the identity, tile t = rows [64t, 64t + 64).
 struct VSmoteK {
-  const float* C;        // fp32 standardized parent rows
+  const uint4* P;        // bf16 output-space parent rows (smote.hip smote_parents_kernel)
   const uint2* plan;     // per SMOTE row: {i | lam_hi << 24, j | lam_lo << 24}
-  const double* aff;     // nullable pivot-shift map (c | 1/sigma)
-  int64_t q_offset;      // parent i is C[q_offset + i]
+  int64_t q_offset;      // parent i is P[q_offset + i]
   int64_t n_split;       // global index of the first SMOTE row (INT64_MAX: none)
   float label, out_scale;
 };
@@ -107,16 +107,6 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   // uniform 1/row_sub subsample used by the early progressive-Newton iterations.
   const int64_t vstep = (int64_t)gridDim.x * kWaves * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
-  // rebuilt-row constants (VIRT): per-lane affine map of its 8 columns (pivot-shifted rows)
-  float sig[8], cc[8];
-  if constexpr (VIRT) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const bool feat = vs.aff != nullptr && 8 * q + j < kBiasCol;
-      sig[j] = feat ? (float)(1.0 / vs.aff[32 + 8 * q + j]) : 1.0f;
-      cc[j] = feat ? (float)vs.aff[8 * q + j] : 0.0f;
-    }
-  }
   // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
   typedef typename std::conditional<FMT == 0, uint4, uint2>::type vec_t;
   auto load_tile = [&](int64_t r0, int64_t lim, bool syn, vec_t (&v)[4]) {
@@ -140,16 +130,14 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
         const uint32_t dx = (uint32_t)__shfl((int)dr.x, src, kWave);
         const uint32_t dy = (uint32_t)__shfl((int)dr.y, src, kWave);
         const float l = smote_lambda(dx, dy);
-        const float4* xi = reinterpret_cast<const float4*>(vs.C + (vs.q_offset + (int64_t)(dx & 0xffffffu)) * kCols + 8 * q);
-        const float4* xj = reinterpret_cast<const float4*>(vs.C + (int64_t)(dy & 0xffffffu) * kCols + 8 * q);
-        const float4 a0 = xi[0], a1 = xi[1], b0 = xj[0], b1 = xj[1];
-        float o[8] = {fmaf(l, b0.x - a0.x, a0.x), fmaf(l, b0.y - a0.y, a0.y), fmaf(l, b0.z - a0.z, a0.z),
-                      fmaf(l, b0.w - a0.w, a0.w), fmaf(l, b1.x - a1.x, a1.x), fmaf(l, b1.y - a1.y, a1.y),
-                      fmaf(l, b1.z - a1.z, a1.z), fmaf(l, b1.w - a1.w, a1.w)};
-        if (vs.aff != nullptr) {
+        // one 16 B gather per parent: this lane's 8 bf16 columns (64 B parent rows, L2-resident)
+        const uint4 pi = vs.P[(vs.q_offset + (int64_t)(dx & 0xffffffu)) * 4 + q];
+        const uint4 pj = vs.P[(int64_t)(dy & 0xffffffu) * 4 + q];
+        float a[8], bq[8], o[8];
+        unpack8<0>(pi, a);
+        unpack8<0>(pj, bq);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] = __fadd_rn(__fmul_rn(o[j], sig[j]), cc[j]);
-        }
+        for (int j = 0; j < 8; ++j) o[j] = fmaf(l, bq[j] - a[j], a[j]);
         if (q == 3) {
           o[6] = 1.0f;
           o[7] = vs.label;
@@ -651,7 +639,7 @@ void launch_logreg_pass_smote(const void* X, int fmt, int64_t row_begin, int64_t
   // v.plan == nullptr: SMOTE rows stored in X after the real rows; else rebuilt from the plan
   if (row_sub < 1) row_sub = 1;
   VSmoteK k{};
-  k.C = v.C; k.plan = reinterpret_cast<const uint2*>(v.plan); k.aff = v.aff; k.q_offset = v.q_offset;
+  k.P = reinterpret_cast<const uint4*>(v.P); k.plan = reinterpret_cast<const uint2*>(v.plan); k.q_offset = v.q_offset;
   k.n_split = v.n_real; k.label = v.label; k.out_scale = v.out_scale;
   const int d = fmt == 0 ? 32 : 30;
   const int h = hessian > 0 ? hessian : 1;

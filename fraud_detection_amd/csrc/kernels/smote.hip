@@ -20,9 +20,12 @@ namespace {
 
 constexpr int kThreads = 256;
 
-template <int OUT, bool NT = false>  // OUT: 0 = bf16 rows (64 B), 1 = fp32 (GBDT input), 2 = fp8 e4m3 (32 B)
+// OUT: 0 = bf16 rows (64 B), 1 = fp32 (GBDT input), 2 = fp8 e4m3 (32 B).
+// PB: parents are bf16 rows already in output space (smote_parents_kernel: the affine map applied
+// once per parent instead of once per sample; half the gather bytes); else fp32 rows (+ aff).
+template <int OUT, bool NT = false, bool PB = false>
 __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
-    const float* __restrict__ C, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
+    const void* __restrict__ Cv, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
     int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
     float out_scale, const double* __restrict__ aff, void* __restrict__ out) {
   const int lane = lane_id();
@@ -30,10 +33,12 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   // aff (optional): the parents are standardized rows z but the training buffer holds
   // pivot-shifted rows s = z * sigma + c (scaler folded into the solver); interpolation commutes
   // with the affine map, so it is applied to the output (mul then add, as the numpy oracle).
+  const float* C = reinterpret_cast<const float*>(Cv);
+  const uint4* Cb = reinterpret_cast<const uint4*>(Cv);
   float sig[8], cc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const bool feat = aff != nullptr && 8 * q + j < kBiasCol;
+    const bool feat = !PB && aff != nullptr && 8 * q + j < kBiasCol;
     sig[j] = feat ? (float)(1.0 / aff[32 + 8 * q + j]) : 1.0f;
     cc[j] = feat ? (float)aff[8 * q + j] : 0.0f;
   }
@@ -64,9 +69,17 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
       const int i = __shfl(my_i, src, kWave);
       const int jn = __shfl(my_j, src, kWave);
       lam[u] = __shfl(my_lam, src, kWave);
-      const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
-      const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
-      a0[u] = xi[0]; a1[u] = xi[1]; b0[u] = xj[0]; b1[u] = xj[1];
+      if constexpr (PB) {
+        const uint4 pi = Cb[(q_offset + i) * 4 + q], pj = Cb[(int64_t)jn * 4 + q];
+        a0[u] = make_float4(bf16lo(pi.x), bf16hi(pi.x), bf16lo(pi.y), bf16hi(pi.y));
+        a1[u] = make_float4(bf16lo(pi.z), bf16hi(pi.z), bf16lo(pi.w), bf16hi(pi.w));
+        b0[u] = make_float4(bf16lo(pj.x), bf16hi(pj.x), bf16lo(pj.y), bf16hi(pj.y));
+        b1[u] = make_float4(bf16lo(pj.z), bf16hi(pj.z), bf16lo(pj.w), bf16hi(pj.w));
+      } else {
+        const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
+        const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
+        a0[u] = xi[0]; a1[u] = xi[1]; b0[u] = xj[0]; b1[u] = xj[1];
+      }
     }
     // next iteration's draw + neighbour-index load, issued AFTER this iteration's gathers:
     // vector loads return in issue order, so waiting for the gathers does not wait for it
@@ -82,7 +95,7 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
                     fmaf(l, b0[u].z - a0[u].z, a0[u].z), fmaf(l, b0[u].w - a0[u].w, a0[u].w),
                     fmaf(l, b1[u].x - a1[u].x, a1[u].x), fmaf(l, b1[u].y - a1[u].y, a1[u].y),
                     fmaf(l, b1[u].z - a1[u].z, a1[u].z), fmaf(l, b1[u].w - a1[u].w, a1[u].w)};
-      if (aff) {
+      if (!PB && aff) {
 #pragma unroll
         for (int j = 0; j < 8; ++j) o[j] = __fadd_rn(__fmul_rn(o[j], sig[j]), cc[j]);
       }
@@ -122,6 +135,19 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   }
 }
 
+// Output-space parents: P = bf16(z * sigma + c) on the feature columns (the pivot-shifted layout of
+// the training rows; identity without aff), columns 30/31 copied.  One thread per element.
+__global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __restrict__ C, int64_t m,
+                                                                 const double* __restrict__ aff,
+                                                                 uint16_t* __restrict__ P) {
+  const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= m * kCols) return;
+  const int c = (int)(e & (kCols - 1));
+  float v = C[e];
+  if (aff != nullptr && c < kBiasCol) v = __fadd_rn(__fmul_rn(v, (float)(1.0 / aff[32 + c])), (float)aff[c]);
+  P[e] = f32_to_bf16(v);
+}
+
 // The draws alone (8 B per sample): virtual SMOTE rebuilds the rows from them inside every solver
 // pass (logreg.hip), 64 MB per pass for 8M samples instead of 512 MB of stored bf16 rows.
 __global__ __launch_bounds__(kThreads) void smote_plan_kernel(const int* __restrict__ nbr, uint32_t range,
@@ -145,29 +171,31 @@ void launch_smote_plan(const int* nbr, int mq, int k, int64_t n_new, uint64_t se
   check_launch("smote_plan");
 }
 
-void launch_smote_generate(const float* C, const int* nbr, int mq, int k, int64_t q_offset,
+void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t* P, hipStream_t stream) {
+  if (m <= 0) return;
+  smote_parents_kernel<<<(int)((m * kCols + kThreads - 1) / kThreads), kThreads, 0, stream>>>(C, m, aff, P);
+  check_launch("smote_parents");
+}
+
+void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int mq, int k, int64_t q_offset,
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream) {
   if (n_new <= 0) return;
   const int64_t per_block = (kThreads / kWave) * 64;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
-  static const int cap0 = resident_cap(smote_generate_kernel<0>, kThreads);
-  static const int cap1 = resident_cap(smote_generate_kernel<1>, kThreads);
-  static const int cap2 = resident_cap(smote_generate_kernel<2>, kThreads);
-  static const int capn = resident_cap(smote_generate_kernel<0, true>, kThreads);
-  if (out_kind == 0 && nt_stores())
-    smote_generate_kernel<0, true><<<capped_grid(n_new, per_block, capn), kThreads, 0, stream>>>(
-        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
-  else if (out_kind == 0)
-    smote_generate_kernel<0><<<capped_grid(n_new, per_block, cap0), kThreads, 0, stream>>>(
-        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
-  else if (out_kind == 1)
-    smote_generate_kernel<1><<<capped_grid(n_new, per_block, cap1), kThreads, 0, stream>>>(
-        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);
-  else
-    smote_generate_kernel<2><<<capped_grid(n_new, per_block, cap2), kThreads, 0, stream>>>(C, nbr, mq, k, q_offset, n_new, k0, k1,
-                                                           c0, c1, label, out_scale, aff, out);
+#define FDX_SG(O, NT, PB)                                                                             \
+  do {                                                                                                \
+    static const int cap = resident_cap(smote_generate_kernel<O, NT, PB>, kThreads);                  \
+    smote_generate_kernel<O, NT, PB><<<capped_grid(n_new, per_block, cap), kThreads, 0, stream>>>(    \
+        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);                  \
+  } while (0)
+  const bool pb = parents_bf16 != 0;
+  if (out_kind == 0 && nt_stores()) { if (pb) FDX_SG(0, true, true); else FDX_SG(0, true, false); }
+  else if (out_kind == 0) { if (pb) FDX_SG(0, false, true); else FDX_SG(0, false, false); }
+  else if (out_kind == 1) { if (pb) FDX_SG(1, false, true); else FDX_SG(1, false, false); }
+  else { if (pb) FDX_SG(2, false, true); else FDX_SG(2, false, false); }
+#undef FDX_SG
   check_launch("smote_generate");
 }
 

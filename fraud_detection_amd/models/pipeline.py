@@ -185,13 +185,14 @@ class DevicePipeline:
             tm.mark("knn")
             # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
             # neighbours found in standardized space are interpolated in shifted coordinates
+            # parents in the training rows' space (bf16, pivot-shifted when the scaler is folded)
+            parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
             if virtual:
-                vrows = lr_ops.VirtualRows(xall, nbr, q_off, n_new, seed=cfg.seed, counter_base=rank,
-                                           affine=stats.aff if fused else None)
+                vrows = lr_ops.VirtualRows(parents, nbr, q_off, n_new, seed=cfg.seed, counter_base=rank)
                 vrows.ensure_plan()
             else:
-                knn_ops.smote_generate(xall, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
-                                       fp8_scale=cfg.fp8_scale, affine=stats.aff if fused else None)
+                knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
+                                       fp8_scale=cfg.fp8_scale)
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
         class_w = (1.0, 1.0)

@@ -69,6 +69,24 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     return idx
 
 
+def smote_parents(C: torch.Tensor, affine: torch.Tensor | None = None) -> torch.Tensor:
+    """bf16 [m, 32] SMOTE parents in the training rows' space: bf16(z * sigma + c) on the feature
+    columns with ``affine`` (ScalerStats.aff, pivot-shifted rows), bf16(z) without; columns 30/31
+    copied.  Sampling from them halves the gather bytes and drops the per-sample affine map."""
+    if C.dtype != torch.float32 or C.dim() != 2 or C.shape[1] != NCOLS:
+        raise ValueError("C must be fp32 [m, 32]")
+    C = C.contiguous()
+    if not C.is_cuda:
+        v = C.numpy().copy()
+        if affine is not None:
+            a = affine.cpu().numpy()
+            v[:, :30] = (v[:, :30] * (1.0 / a[32:62]).astype(np.float32)) + a[:30].astype(np.float32)
+        return torch.from_numpy(v).to(torch.bfloat16)
+    P = torch.empty((C.shape[0], NCOLS), dtype=torch.bfloat16, device=C.device)
+    native().smote_parents(ptr(C), C.shape[0], ptr(affine), ptr(P), stream_of(C))
+    return P
+
+
 def smote_plan(nbr: torch.Tensor, n_new: int, seed: int = 42, counter_base: int = 0) -> torch.Tensor:
     """int32 [n_new, 2] SMOTE draws (the same ones smote_generate interpolates): word 0 = query row i
     | lam_hi << 24, word 1 = neighbour row j | lam_lo << 24 (16-bit lambda).  Virtual SMOTE
@@ -92,11 +110,15 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
                    fp8_scale: float = DEFAULT_FP8_SCALE, affine: torch.Tensor | None = None) -> torch.Tensor:
     """Write ``n_new`` synthetic rows into ``out`` (a [n_new, 32] bf16/fp32/fp8 view, e.g. the tail of
     the training buffer).  Sample s interpolates minority row (q_offset + i) toward neighbour
-    nbr[i, kk] with Philox draws keyed by (seed, s, counter_base).  ``affine`` ([64] float64,
-    ScalerStats.aff): C holds standardized rows but ``out`` pivot-shifted ones -- each feature is
-    written as z * sigma + c."""
-    if C.dtype != torch.float32 or C.dim() != 2 or C.shape[1] != NCOLS:
-        raise ValueError("C must be fp32 [m, 32]")
+    nbr[i, kk] with Philox draws keyed by (seed, s, counter_base).  C: fp32 standardized parents,
+    or bf16 parents from smote_parents (already in the output space; ``affine`` must be None).
+    ``affine`` ([64] float64, ScalerStats.aff) with fp32 parents: ``out`` holds pivot-shifted rows
+    -- each feature is written as z * sigma + c."""
+    if C.dtype not in (torch.float32, torch.bfloat16) or C.dim() != 2 or C.shape[1] != NCOLS:
+        raise ValueError("C must be fp32 or bf16 [m, 32]")
+    pb = C.dtype == torch.bfloat16
+    if pb and affine is not None:
+        raise ValueError("bf16 parents are already in the output space (smote_parents): no affine")
     if nbr.dtype != torch.int32 or nbr.dim() != 2:
         raise ValueError("nbr must be int32 [mq, k]")
     mq, k = nbr.shape
@@ -112,7 +134,7 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
         nb = nbr.numpy()
         if nb.min() < 0 or nb.max() >= C.shape[0]:
             raise ValueError("neighbour index out of range")
-        rows = ref.smote_generate(C.numpy(), nb, q_offset, n_new, seed, counter_base, label)
+        rows = ref.smote_generate(C.float().numpy(), nb, q_offset, n_new, seed, counter_base, label)
         if affine is not None:
             a = affine.cpu().numpy()
             sig = (1.0 / a[32:62]).astype(np.float32)
@@ -127,7 +149,7 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
             out.copy_(torch.from_numpy(ref.fp8_encode(r2)))
         return out
     m = native()
-    m.smote_generate(ptr(C), ptr(nbr), mq, k, int(q_offset), int(n_new), int(seed) & (2**64 - 1),
+    m.smote_generate(ptr(C), int(pb), ptr(nbr), mq, k, int(q_offset), int(n_new), int(seed) & (2**64 - 1),
                      int(counter_base) & (2**64 - 1), float(label), DTYPE_KIND[kind], float(fp8_scale),
                      ptr(affine), ptr(out), stream_of(C))
     return out

@@ -168,17 +168,16 @@ def progressive_schedule(n_rows: int) -> list:
 class VirtualRows:
     """Virtual SMOTE: ``n_new`` synthetic minority rows that follow the stored rows of a fit.  The
     pass kernels rebuild each one from its 8-byte draw (``plan``, ops/knn.smote_plan: parents i, j
-    and lambda), with the parents ``C``/``q_offset``, ``label``, ``affine`` and storage rounding of
-    ops/knn.smote_generate -- so the fit is bit-identical to the materialized one while the
-    synthetic rows are never written to HBM nor read back in every Newton pass."""
-    C: torch.Tensor                  # fp32 [mc, 32] standardized parent rows
-    nbr: torch.Tensor                # int32 [mq, k] neighbour indices into C
+    and lambda) and the bf16 parents ``P`` (ops/knn.smote_parents) with the interpolation and
+    rounding of ops/knn.smote_generate -- so the fit is bit-identical to the materialized one
+    while the synthetic rows are never written to HBM nor read back in every Newton pass."""
+    P: torch.Tensor                  # bf16 [mc, 32] parents in the training rows' space
+    nbr: torch.Tensor                # int32 [mq, k] neighbour indices into P
     q_offset: int
     n_new: int
     seed: int = 42
     counter_base: int = 0
     label: float = 1.0
-    affine: torch.Tensor | None = None
     plan: torch.Tensor | None = None  # int32 [n_new, 2] draws (built on first use)
 
     def ensure_plan(self) -> torch.Tensor:
@@ -194,9 +193,8 @@ class VirtualRows:
 
         out = torch.empty((rows.shape[0] + self.n_new, NCOLS), dtype=rows.dtype, device=rows.device)
         out[: rows.shape[0]] = rows
-        knn_ops.smote_generate(self.C, self.nbr, self.q_offset, self.n_new, out[rows.shape[0]:], seed=self.seed,
-                               counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale,
-                               affine=self.affine)
+        knn_ops.smote_generate(self.P, self.nbr, self.q_offset, self.n_new, out[rows.shape[0]:], seed=self.seed,
+                               counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale)
         return out
 
 
@@ -214,12 +212,11 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
     if vrows is not None and vrows.n_new > 0:
         v = vrows
         m.logreg_pass_smote(ptr(rows), fmt, begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
-                            float(fp8_scale), ptr(v.C), ptr(v.ensure_plan()), int(v.q_offset), rows.shape[0],
-                            float(v.label), float(fp8_scale), ptr(v.affine) if v.affine is not None else 0,
-                            ptr(ws.partial), ws.nblocks, s)
+                            float(fp8_scale), ptr(v.P), ptr(v.ensure_plan()), int(v.q_offset), rows.shape[0],
+                            float(v.label), float(fp8_scale), ptr(ws.partial), ws.nblocks, s)
     elif n_split is not None and n_split < end:
         m.logreg_pass_smote(ptr(rows), fmt, begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
-                            float(fp8_scale), 0, 0, 0, int(n_split), 1.0, float(fp8_scale), 0, ptr(ws.partial),
+                            float(fp8_scale), 0, 0, 0, int(n_split), 1.0, float(fp8_scale), ptr(ws.partial),
                             ws.nblocks, s)
     elif fmt == 0:        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
                       ws.nblocks, s)

@@ -26,7 +26,7 @@ def _setup(dev, n, kind, affine, seed=5):
     xmin = S.scale_cast(X, st, labels=y, out_dtype="f32", idx=idx)
     nbr = K.knn_topk(xmin, xmin, k=5, self_offset=0)
     n_new = n - 2 * int(idx.numel())
-    v = L.VirtualRows(xmin, nbr, 0, n_new, seed=11, counter_base=2, affine=st.aff if affine else None)
+    v = L.VirtualRows(K.smote_parents(xmin, st.aff if affine else None), nbr, 0, n_new, seed=11, counter_base=2)
     return rows, v
 
 
@@ -96,6 +96,19 @@ def test_zipped_stored_pass_matches_oracle(dev):
     np.testing.assert_allclose(red[64:].reshape(32, 32), H0, rtol=1e-4, atol=1e-2)
 
 
+@pytest.mark.gpu
+def test_smote_parents_match_cpu(dev):
+    X, y = separable(50_000, fraud_rate=0.05, seed=8)
+    rows = torch.empty((X.shape[0], 32), dtype=torch.bfloat16)
+    st = S.scaler_fit_cast(X, y, rows)
+    idx = torch.nonzero(y == 1).reshape(-1)
+    xmin = S.scale_cast(X[idx].contiguous(), st, labels=y[idx].contiguous(), out_dtype="f32")
+    for aff in (None, st.aff):
+        cpu = K.smote_parents(xmin, aff)
+        gpu = K.smote_parents(xmin.to(dev), aff.to(dev) if aff is not None else None).cpu()
+        assert torch.equal(cpu, gpu)
+
+
 def test_virtual_rows_materialize_cpu():
     """CPU path: a fit given VirtualRows materializes them and equals the explicit concatenation."""
     X, y = separable(20_000, fraud_rate=0.05, seed=3)
@@ -104,7 +117,7 @@ def test_virtual_rows_materialize_cpu():
     idx = torch.nonzero(y == 1).reshape(-1)
     xmin = S.scale_cast(X[idx].contiguous(), st, labels=y[idx].contiguous(), out_dtype="f32")
     nbr = K.knn_topk(xmin, xmin, k=5, self_offset=0)
-    v = L.VirtualRows(xmin, nbr, 0, 5_000, seed=9)
+    v = L.VirtualRows(K.smote_parents(xmin), nbr, 0, 5_000, seed=9)
     full = v.materialize(rows)
     a = L.newton_fit(rows, tol=1e-6, vrows=v)
     b = L.newton_fit(full, tol=1e-6)

@@ -118,7 +118,7 @@ def main():
     nbr = K.knn_topk(xmin, xmin, 5, 0)
     case("smote_generate_n", lambda: K.smote_generate(xmin, nbr, 0, n, outb), n * 64)
     # virtual SMOTE: n real rows + n synthesized in the pass (vs logreg_pass_*_2n over 2n stored rows)
-    vr = L.VirtualRows(xmin, nbr, 0, n, seed=42)
+    vr = L.VirtualRows(K.smote_parents(xmin), nbr, 0, n, seed=42)
 
     def lr_pass_virtual(h):
         def f():
