@@ -28,6 +28,7 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     const void* __restrict__ Cv, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
     int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
     float out_scale, const double* __restrict__ aff, void* __restrict__ out) {
+#pragma clang fp contract(off)  // affine map = mul then add (the oracle); the interpolation is an explicit fmaf
   const int lane = lane_id();
   const int q = lane & 3, rr = lane >> 2;
   // aff (optional): the parents are standardized rows z but the training buffer holds
@@ -97,7 +98,7 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
                     fmaf(l, b1[u].z - a1[u].z, a1[u].z), fmaf(l, b1[u].w - a1[u].w, a1[u].w)};
       if (!PB && aff) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = __fadd_rn(__fmul_rn(o[j], sig[j]), cc[j]);
+        for (int j = 0; j < 8; ++j) o[j] = o[j] * sig[j] + cc[j];
       }
       if (q == 3) {
         o[6] = 1.0f;   // col 30: intercept column
@@ -140,11 +141,12 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
 __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __restrict__ C, int64_t m,
                                                                  const double* __restrict__ aff,
                                                                  uint16_t* __restrict__ P) {
+#pragma clang fp contract(off)  // mul then add, two roundings (= the numpy oracle), never an fma
   const int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (e >= m * kCols) return;
   const int c = (int)(e & (kCols - 1));
   float v = C[e];
-  if (aff != nullptr && c < kBiasCol) v = __fadd_rn(__fmul_rn(v, (float)(1.0 / aff[32 + c])), (float)aff[c]);
+  if (aff != nullptr && c < kBiasCol) v = v * (float)(1.0 / aff[32 + c]) + (float)aff[c];
   P[e] = f32_to_bf16(v);
 }
 
