@@ -109,7 +109,20 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
   // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
   typedef typename std::conditional<FMT == 0, uint4, uint2>::type vec_t;
-  auto load_tile = [&](int64_t r0, int64_t lim, bool syn, vec_t (&v)[4]) {
+  // plan entry of tile row `lane` (SMOTE tiles): loaded one iteration ahead of its gathers, so the
+  // HBM latency of the draws is off the per-tile dependency chain (draw -> parent gathers)
+  auto load_plan = [&](int64_t vtt) -> uint2 {
+    if constexpr (VIRT) {
+      if (vtt < T) {
+        int64_t a = 0, l = 0;
+        bool sy = false;
+        tile_of(vtt, a, l, sy);
+        if (sy && a + lane < l) return vs.plan[row_begin + a + lane - vs.n_split];
+      }
+    }
+    return make_uint2(0, 0);
+  };
+  auto load_tile = [&](int64_t r0, int64_t lim, bool syn, vec_t (&v)[4], uint2 dr) {
     const vec_t* X = reinterpret_cast<const vec_t*>(Xv);
     if (!VIRT || !syn) {
 #pragma unroll
@@ -123,7 +136,6 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     }
     if constexpr (VIRT) {
       // lane L fetches the draw of tile row L (one coalesced 512 B load), shuffled to the row's lanes
-      const uint2 dr = (r0 + lane < lim) ? vs.plan[row_begin + r0 + lane - vs.n_split] : make_uint2(0, 0);
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int src = 16 * u + rr;
@@ -166,9 +178,10 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   int64_t r0 = 0, lim = 0;
   bool syn = false;
   vec_t cur[4];
+  uint2 pl_n = load_plan(vt + vstep);
   if (vt < T) {
     tile_of(vt, r0, lim, syn);
-    load_tile(r0, lim, syn, cur);
+    load_tile(r0, lim, syn, cur, load_plan(vt));
   }
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
@@ -178,10 +191,12 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     vec_t nxt[4];
     int64_t r0n = 0, limn = 0;
     bool synn = false;
+    const uint2 pl_nn = load_plan(vt + 2 * vstep);
     if (vt + vstep < T) {
       tile_of(vt + vstep, r0n, limn, synn);
-      load_tile(r0n, limn, synn, nxt);
+      load_tile(r0n, limn, synn, nxt, pl_n);
     }
+    pl_n = pl_nn;
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
