@@ -116,15 +116,6 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
                                 P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s));
   });
-  m.def("logreg_pass_smote", [](u X, int fmt, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub,
-                                float xs, u parents, u plan, int64_t q_off, int64_t n_real, float label,
-                                float out_scale, u partial, int nblocks, u s) {
-    fdx::VSmote v;
-    v.P = P<const void>(parents); v.plan = P<const void>(plan); v.q_offset = q_off; v.n_real = n_real;
-    v.label = label; v.out_scale = out_scale;
-    fdx::launch_logreg_pass_smote(P<const void>(X), fmt, rb, re, P<const float>(w), P<const float>(cw),
-                                  P<const int>(done), hess, sub, xs, v, P<float>(partial), nblocks, S(s));
-  });
   m.def("logreg_reduce", [](u partial, int nblocks, int ncols, u out, u done, u s) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });
@@ -150,9 +141,6 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_knn_topk(P<const float>(Q), mq_pad, mq, P<const float>(C), mc_pad, mc,
                          self_off, k, P<int>(oidx), P<float>(oscore), P<float>(ws_score), P<int>(ws_idx), nsplit,
                          S(s));
-  });
-  m.def("smote_plan", [](u nbr, int mq, int k, int64_t n_new, uint64_t seed, uint64_t counter_base, u plan, u s) {
-    fdx::launch_smote_plan(P<const int>(nbr), mq, k, n_new, seed, counter_base, P<void>(plan), S(s));
   });
   m.def("smote_parents", [](u C, int64_t m_rows, u aff, u out, u s) {
     fdx::launch_smote_parents(P<const float>(C), m_rows, P<const double>(aff), P<uint16_t>(out), S(s));

@@ -181,8 +181,8 @@ __host__ __device__ __forceinline__ uint32_t u32_range(uint32_t v, uint32_t n) {
 
 // SMOTE draw of sample s (Philox counter (s, counter_base), key seed): query row i uniform over
 // the mq rows, neighbour slot uniform over k (one Lemire pick over mq*k), interpolation weight on
-// a 2^-16 grid.  Packed as {i | lam_hi << 24, j | lam_lo << 24} so a draw is 8 bytes (smote.hip plan,
-// virtual SMOTE in logreg.hip); ops/reference.py smote_generate is the numpy oracle.
+// a 2^-16 grid.  Packed as {i | lam_hi << 24, j | lam_lo << 24} (8 bytes per draw);
+// ops/reference.py smote_plan / smote_generate is the numpy oracle.
 __device__ __forceinline__ uint2 smote_draw(int64_t s, uint32_t cb0, uint32_t cb1, uint32_t key0, uint32_t key1,
                                             uint32_t range, uint32_t k, const int* __restrict__ nbr) {
   const Philox4 r = philox4x32_10((uint32_t)s, (uint32_t)(s >> 32), cb0, cb1, key0, key1);

@@ -87,20 +87,6 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
                             float x_scale, float* partial, int nblocks, hipStream_t stream);
-// SMOTE-aware pass: rows [n_real, row_end) of the window are SMOTE rows.  plan == nullptr: they
-// are stored in X after the real rows; else they are rebuilt in the kernel from their 8-byte draws
-// (launch_smote_plan) -- bit-identical to the stored rows launch_smote_generate writes from the
-// same draws, without storing them or re-reading them every Newton pass ("virtual SMOTE").
-struct VSmote {
-  const void* P = nullptr;       // bf16 output-space parents (launch_smote_parents), all ranks' minority rows
-  const void* plan = nullptr;    // [n_new] uint2 draws (launch_smote_plan), or nullptr
-  int64_t q_offset = 0;          // this rank's query rows start at C[q_offset]
-  int64_t n_real = 0;            // global index of the first SMOTE row
-  float label = 1.0f, out_scale = 1.0f;
-};
-void launch_logreg_pass_smote(const void* X, int fmt, int64_t row_begin, int64_t row_end, const float* w,
-                              const float* class_w, const int* done, int hessian, int row_sub, float x_scale,
-                              const VSmote& v, float* partial, int nblocks, hipStream_t stream);
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.
@@ -122,10 +108,6 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
 
 // ---- smote.hip ----
-// Draws of SMOTE samples [0, n_new): plan[s] = {i | lam_hi << 24, j | lam_lo << 24} (i: query row,
-// j: neighbour row index into C, lam: 16-bit interpolation weight); requires mq, mc < 2^24.
-void launch_smote_plan(const int* nbr, int mq, int k, int64_t n_new, uint64_t seed, uint64_t counter_base,
-                       void* plan, hipStream_t stream);
 // P [m, 32] bf16 = output-space parents: bf16(C * sigma + c) on the feature columns (aff nullable)
 void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t* P, hipStream_t stream);
 // C: fp32 standardized parents (+ aff applied per sample) or, parents_bf16, smote_parents output

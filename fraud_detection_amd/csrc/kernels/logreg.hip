@@ -48,27 +48,11 @@ __device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8], int q, i
   for (int j = 0; j < 8; ++j) x[j] = (q * 8 + j < d) ? x[j] * inv_s : x[j];
 }
 
-// Row sources of a pass.  Rows [0, n_split) of the window are "real", rows [n_split, n) are SMOTE
-// rows: stored after the real rows (VIRT = false) or rebuilt from their 8-byte draw (VIRT = true:
-// parents i, j and the 16-bit lambda of smote.hip's plan) and the bf16 output-space parents -- the
-// same interpolation and rounding as smote_generate_kernel<.., PB = true>, so both sources give
-// bit-identical rows.  The 64-row
-// tiles of the two ranges are visited zipped (real, SMOTE, real, ...): HBM-bound real tiles and
-// ALU/L2-bound rebuilt tiles overlap on every CU instead of running as two phases.  Without SMOTE
-// rows (n_split >= n) the zip is the identity, tile t = rows [64t, 64t + 64).
-struct VSmoteK {
-  const uint4* P;        // bf16 output-space parent rows (smote.hip smote_parents_kernel)
-  const uint2* plan;     // per SMOTE row: {i | lam_hi << 24, j | lam_lo << 24}
-  int64_t q_offset;      // parent i is P[q_offset + i]
-  int64_t n_split;       // global index of the first SMOTE row (INT64_MAX: none)
-  float label, out_scale;
-};
-
-template <bool HESS, int FMT, bool VIRT = false>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
+template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, int row_sub, float* __restrict__ partial, VSmoteK vs) {
+    int hess_stride, int row_sub, float* __restrict__ partial) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][35];
@@ -90,113 +74,32 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   uint16_t* my_tile = tile[wv];
 
   const int64_t n = row_end - row_begin;
-  // zipped tile space: Tr real tiles, Ts SMOTE tiles, interleaved while both last
-  const int64_t nr = vs.n_split - row_begin < 0 ? 0 : (vs.n_split - row_begin > n ? n : vs.n_split - row_begin);
-  const int64_t Tr = (nr + 63) >> 6, Ts = (n - nr + 63) >> 6, Tm = Tr < Ts ? Tr : Ts, T = Tr + Ts;
-  auto tile_of = [&](int64_t vt, int64_t& r0, int64_t& lim, bool& syn) {
-    if (vt < 2 * Tm) {
-      syn = (vt & 1) != 0;
-      r0 = (vt >> 1) << 6;
-    } else {
-      syn = Ts > Tr;
-      r0 = (vt - Tm) << 6;
-    }
-    if (syn) { r0 += nr; lim = n; } else { lim = nr; }
-  };
-  // row_sub > 1: only tiles vt with (vt mod G*row_sub) < G are visited (G = waves in the grid): a
-  // uniform 1/row_sub subsample used by the early progressive-Newton iterations.
-  const int64_t vstep = (int64_t)gridDim.x * kWaves * row_sub;
+  // row_sub > 1: only 64-row tiles t with (t mod G*row_sub) < G are visited (G = waves in the
+  // grid): a uniform 1/row_sub subsample used by the early progressive-Newton iterations.
+  const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
   // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
   typedef typename std::conditional<FMT == 0, uint4, uint2>::type vec_t;
-  // plan entry of tile row `lane` (SMOTE tiles): loaded one iteration ahead of its gathers, so the
-  // HBM latency of the draws is off the per-tile dependency chain (draw -> parent gathers)
-  auto load_plan = [&](int64_t vtt) -> uint2 {
-    if constexpr (VIRT) {
-      if (vtt < T) {
-        int64_t a = 0, l = 0;
-        bool sy = false;
-        tile_of(vtt, a, l, sy);
-        if (sy && a + lane < l) return vs.plan[row_begin + a + lane - vs.n_split];
-      }
-    }
-    return make_uint2(0, 0);
-  };
-  auto load_tile = [&](int64_t r0, int64_t lim, bool syn, vec_t (&v)[4], uint2 dr) {
+  auto load_tile = [&](int64_t b, vec_t (&v)[4]) {
     const vec_t* X = reinterpret_cast<const vec_t*>(Xv);
-    if (!VIRT || !syn) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t row = r0 + 16 * u + rr;
-        if (row < lim) v[u] = X[(row_begin + row) * 4 + q];
-        else if constexpr (FMT == 0) v[u] = make_uint4(0, 0, 0, 0);
-        else v[u] = make_uint2(0, 0);
-      }
-      return;
-    }
-    if constexpr (VIRT) {
-      // lane L fetches the draw of tile row L (one coalesced 512 B load), shuffled to the row's lanes
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int src = 16 * u + rr;
-        const uint32_t dx = (uint32_t)__shfl((int)dr.x, src, kWave);
-        const uint32_t dy = (uint32_t)__shfl((int)dr.y, src, kWave);
-        const float l = smote_lambda(dx, dy);
-        // one 16 B gather per parent: this lane's 8 bf16 columns (64 B parent rows, L2-resident)
-        const uint4 pi = vs.P[(vs.q_offset + (int64_t)(dx & 0xffffffu)) * 4 + q];
-        const uint4 pj = vs.P[(int64_t)(dy & 0xffffffu) * 4 + q];
-        float a[8], bq[8], o[8];
-        unpack8<0>(pi, a);
-        unpack8<0>(pj, bq);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaf(l, bq[j] - a[j], a[j]);
-        if (q == 3) {
-          o[6] = 1.0f;
-          o[7] = vs.label;
-        }
-        if (r0 + 16 * u + rr >= lim) {
-          if constexpr (FMT == 0) v[u] = make_uint4(0, 0, 0, 0);
-          else v[u] = make_uint2(0, 0);
-        } else if constexpr (FMT == 0) {
-          v[u] = make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]), pack_bf16x2(o[4], o[5]),
-                            pack_bf16x2(o[6], o[7]));
-        } else {
-          uint2 pk = make_uint2(0, 0);
-#pragma unroll
-          for (int jj = 0; jj < 8; ++jj) {
-            const bool feat = (8 * q + jj) < kBiasCol;
-            const uint32_t bt = f32_to_fp8e4m3(feat ? o[jj] * vs.out_scale : o[jj]);
-            if (jj < 4) pk.x |= bt << (8 * jj);
-            else pk.y |= bt << (8 * (jj - 4));
-          }
-          v[u] = pk;
-        }
-      }
+    for (int u = 0; u < 4; ++u) {
+      const int64_t row = b + 16 * u + rr;
+      if (row < n) v[u] = X[(row_begin + row) * 4 + q];
+      else if constexpr (FMT == 0) v[u] = make_uint4(0, 0, 0, 0);
+      else v[u] = make_uint2(0, 0);
     }
   };
-  int64_t vt = (int64_t)blockIdx.x * kWaves + wv;
-  int64_t r0 = 0, lim = 0;
-  bool syn = false;
+  int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
   vec_t cur[4];
-  uint2 pl_n = load_plan(vt + vstep);
-  if (vt < T) {
-    tile_of(vt, r0, lim, syn);
-    load_tile(r0, lim, syn, cur, load_plan(vt));
-  }
+  if (base < n) load_tile(base, cur);
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
   // is unchanged; H only shapes the step (sub-sampled Newton).
   int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
-  for (; vt < T; vt += vstep) {
+  for (; base < n; base += step) {
     vec_t nxt[4];
-    int64_t r0n = 0, limn = 0;
-    bool synn = false;
-    const uint2 pl_nn = load_plan(vt + 2 * vstep);
-    if (vt + vstep < T) {
-      tile_of(vt + vstep, r0n, limn, synn);
-      load_tile(r0n, limn, synn, nxt, pl_n);
-    }
-    pl_n = pl_nn;
+    if (base + step < n) load_tile(base + step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
@@ -216,7 +119,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
       for (int j = 0; j < 8; ++j) zp = fmaf(wl[j], x[j], zp);
       zp = group_sum<4>(zp);
       y = group_sum<4>(y);
-      const bool ok = r0 + 16 * u + rr < lim;
+      const bool ok = base + 16 * u + rr < n;
       const bool pos = y > 0.5f;
       const float sw = ok ? (pos ? cw1 : cw0) : 0.0f;
       const float zc = fminf(fmaxf(zp, -80.0f), 80.0f);
@@ -261,8 +164,6 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     if (do_h) whacc += swq;
 #pragma unroll
     for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-    r0 = r0n;
-    lim = limn;
   }
 
   // ---- block reduction (fixed order) ----
@@ -594,12 +495,6 @@ __global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict
 // Grid = resident capacity of the Hessian pass (blocks/CU from the occupancy query x CUs): a
 // grid-stride stream must not launch a partial second round of blocks, which would double the
 // tail (every block owns an equal share of rows).
-VSmoteK no_smote() {
-  VSmoteK k{};
-  k.n_split = INT64_MAX;
-  return k;
-}
-
 int logreg_pass_blocks() {
   static int cached = 0;
   if (cached) return cached;
@@ -626,10 +521,10 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
   if (row_sub < 1) row_sub = 1;
   if (hessian > 0)
     logreg_pass_kernel<true, 0><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, 1.0f, 32, hessian, row_sub, partial, no_smote());
+        X, row_begin, row_end, w, class_w, done, 1.0f, 32, hessian, row_sub, partial);
   else
     logreg_pass_kernel<false, 0><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, 1.0f, 32, 1, row_sub, partial, no_smote());
+        X, row_begin, row_end, w, class_w, done, 1.0f, 32, 1, row_sub, partial);
   check_launch("logreg_pass");
 }
 
@@ -641,36 +536,11 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
   if (row_sub < 1) row_sub = 1;
   if (hessian > 0)
     logreg_pass_kernel<true, 1><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, x_scale, 30, hessian, row_sub, partial, no_smote());
+        X, row_begin, row_end, w, class_w, done, x_scale, 30, hessian, row_sub, partial);
   else
     logreg_pass_kernel<false, 1><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, x_scale, 30, 1, row_sub, partial, no_smote());
+        X, row_begin, row_end, w, class_w, done, x_scale, 30, 1, row_sub, partial);
   check_launch("logreg_pass_fp8");
-}
-
-void launch_logreg_pass_smote(const void* X, int fmt, int64_t row_begin, int64_t row_end, const float* w,
-                              const float* class_w, const int* done, int hessian, int row_sub, float x_scale,
-                              const VSmote& v, float* partial, int nblocks, hipStream_t stream) {
-  // v.plan == nullptr: SMOTE rows stored in X after the real rows; else rebuilt from the plan
-  if (row_sub < 1) row_sub = 1;
-  VSmoteK k{};
-  k.P = reinterpret_cast<const uint4*>(v.P); k.plan = reinterpret_cast<const uint2*>(v.plan); k.q_offset = v.q_offset;
-  k.n_split = v.n_real; k.label = v.label; k.out_scale = v.out_scale;
-  const int d = fmt == 0 ? 32 : 30;
-  const int h = hessian > 0 ? hessian : 1;
-  const float xs = fmt == 0 ? 1.0f : x_scale;
-#define FDX_LR(HS, F, V) logreg_pass_kernel<HS, F, V><<<nblocks, kThreads, 0, stream>>>( \
-    X, row_begin, row_end, w, class_w, done, xs, d, h, row_sub, partial, k)
-  const bool virt = v.plan != nullptr;
-  if (fmt == 0) {
-    if (hessian > 0) { if (virt) FDX_LR(true, 0, true); else FDX_LR(true, 0, false); }
-    else { if (virt) FDX_LR(false, 0, true); else FDX_LR(false, 0, false); }
-  } else {
-    if (hessian > 0) { if (virt) FDX_LR(true, 1, true); else FDX_LR(true, 1, false); }
-    else { if (virt) FDX_LR(false, 1, true); else FDX_LR(false, 1, false); }
-  }
-#undef FDX_LR
-  check_launch("logreg_pass_smote");
 }
 
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,

@@ -150,28 +150,7 @@ __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __
   P[e] = f32_to_bf16(v);
 }
 
-// The draws alone (8 B per sample): virtual SMOTE rebuilds the rows from them inside every solver
-// pass (logreg.hip), 64 MB per pass for 8M samples instead of 512 MB of stored bf16 rows.
-__global__ __launch_bounds__(kThreads) void smote_plan_kernel(const int* __restrict__ nbr, uint32_t range,
-                                                              uint32_t k, int64_t n_new, uint32_t key0,
-                                                              uint32_t key1, uint32_t cb0, uint32_t cb1,
-                                                              uint2* __restrict__ plan) {
-  const int64_t step = (int64_t)gridDim.x * kThreads;
-  for (int64_t s = (int64_t)blockIdx.x * kThreads + threadIdx.x; s < n_new; s += step)
-    plan[s] = smote_draw(s, cb0, cb1, key0, key1, range, k, nbr);
-}
-
 }  // namespace
-
-void launch_smote_plan(const int* nbr, int mq, int k, int64_t n_new, uint64_t seed, uint64_t counter_base,
-                       void* plan, hipStream_t stream) {
-  if (n_new <= 0) return;
-  static const int cap = resident_cap(smote_plan_kernel, kThreads);
-  smote_plan_kernel<<<capped_grid(n_new, kThreads, cap), kThreads, 0, stream>>>(
-      nbr, (uint32_t)mq * (uint32_t)k, (uint32_t)k, n_new, (uint32_t)seed, (uint32_t)(seed >> 32),
-      (uint32_t)counter_base, (uint32_t)(counter_base >> 32), reinterpret_cast<uint2*>(plan));
-  check_launch("smote_plan");
-}
 
 void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t* P, hipStream_t stream) {
   if (m <= 0) return;

@@ -5,8 +5,8 @@ Reference call stack (train_model.py:20-114):
 Here every numeric step is a HIP kernel on the rank's row shard:
     K1 scaler stats (+ all-reduce C1) -> K2 standardize/pad/cast into the training buffer
     -> stable minority compaction -> K2 gather (fp32 minority rows) -> all-gather C3
-    -> K8 MFMA k-NN (local queries vs global minority) -> K9 Philox SMOTE rows (virtual: rebuilt
-       inside every K4 pass from their draws; materialize: written after the real rows)
+    -> K8 MFMA k-NN (local queries vs global minority) -> K9 Philox SMOTE rows written in place
+       from bf16 parents in the training rows' space
     -> K4 Newton (all-reduce C5 per iteration) or momentum SGD (all-reduce C4 per minibatch).
 Evaluation: folded-scaler predict on raw fp32 test rows (K5) -> exact AUC (K10) + confusion.
 """
@@ -55,9 +55,6 @@ class TrainConfig:
     # identical to single-process imblearn on the whole table, k-NN work grows with the world
     # size), "shard" = each rank's own minority rows (per-partition SMOTE: constant work per rank)
     smote_scope: str = "global"
-    # "virtual": synthetic rows are rebuilt inside every solver pass from their Philox draws (bit-
-    # identical fit, no SMOTE write, half the bytes per pass); "materialize": written to HBM once
-    smote_mode: str = "virtual"
 
 
 @dataclass
@@ -134,10 +131,7 @@ class DevicePipeline:
                  and scaler_ops.fused_cast_ok(X))
         # training buffer sized for the largest possible SMOTE output, so the cast does not wait
         # for the minority count
-        if cfg.smote_mode not in ("virtual", "materialize"):
-            raise ValueError("smote_mode must be 'virtual' or 'materialize'")
-        virtual = cfg.smote_mode == "virtual" and dev.type == "cuda"
-        cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) if cfg.smote and not virtual else 0)
+        cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) if cfg.smote else 0)
         rows_cap = self._train_buffer(cap, dev)
         if fused:
             # ---- class counts (C2): count kernels first, host reads the total during K1+K2 ----
@@ -161,8 +155,7 @@ class DevicePipeline:
 
         n_maj = n - n_min
         n_new = quota(n, n_min)
-        rows = rows_cap[: n + (0 if virtual else n_new)]
-        vrows = None
+        rows = rows_cap[: n + n_new]
         # DP: one small all-gather of (minority, rows) per rank gives every rank the minority
         # counts (for the row all-gather) and every rank's post-SMOTE size (for the identical
         # Newton schedule) -- no further host-synchronising collectives in the fit.
@@ -185,14 +178,11 @@ class DevicePipeline:
             tm.mark("knn")
             # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
             # neighbours found in standardized space are interpolated in shifted coordinates
-            # parents in the training rows' space (bf16, pivot-shifted when the scaler is folded)
+            # parents in the training rows' space (bf16, pivot-shifted when the scaler is folded):
+            # half the gather bytes of fp32 parents and no per-sample affine map
             parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
-            if virtual:
-                vrows = lr_ops.VirtualRows(parents, nbr, q_off, n_new, seed=cfg.seed, counter_base=rank)
-                vrows.ensure_plan()
-            else:
-                knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
-                                       fp8_scale=cfg.fp8_scale)
+            knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
+                                   fp8_scale=cfg.fp8_scale)
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
         class_w = (1.0, 1.0)
@@ -210,13 +200,12 @@ class DevicePipeline:
             fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
                                     check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride,
-                                    n_sched=n_sched, affine=stats.aff if fused else None, vrows=vrows,
-                                    n_split=n if n_new and not virtual else None)
+                                    n_sched=n_sched, affine=stats.aff if fused else None)
         elif cfg.solver == "sgd":
             fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                  batch_rows=cfg.sgd_batch_rows, class_w=class_w, d=d, w0=w0,
                                  fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
-                                 workspace=self._ws, vrows=vrows, n_split=n if n_new and not virtual else None)
+                                 workspace=self._ws)
         else:
             raise ValueError(f"unknown solver {cfg.solver!r}")
         tm.mark("fit")

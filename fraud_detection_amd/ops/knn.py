@@ -87,24 +87,6 @@ def smote_parents(C: torch.Tensor, affine: torch.Tensor | None = None) -> torch.
     return P
 
 
-def smote_plan(nbr: torch.Tensor, n_new: int, seed: int = 42, counter_base: int = 0) -> torch.Tensor:
-    """int32 [n_new, 2] SMOTE draws (the same ones smote_generate interpolates): word 0 = query row i
-    | lam_hi << 24, word 1 = neighbour row j | lam_lo << 24 (16-bit lambda).  Virtual SMOTE
-    (ops/logreg.VirtualRows) rebuilds the rows from them inside every solver pass."""
-    if nbr.dtype != torch.int32 or nbr.dim() != 2:
-        raise ValueError("nbr must be int32 [mq, k]")
-    mq, k = nbr.shape
-    if mq >= 1 << 24 or (mq and int(nbr.max()) >= 1 << 24):
-        raise ValueError("SMOTE draws pack row indices in 24 bits")
-    if not nbr.is_cuda:
-        return torch.from_numpy(ref.smote_plan(nbr.numpy(), n_new, seed, counter_base).view(np.int32))
-    plan = torch.empty((n_new, 2), dtype=torch.int32, device=nbr.device)
-    if n_new > 0:
-        native().smote_plan(ptr(nbr), mq, k, int(n_new), int(seed) & (2**64 - 1), int(counter_base) & (2**64 - 1),
-                            ptr(plan), stream_of(nbr))
-    return plan
-
-
 def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int, out: torch.Tensor,
                    seed: int = 42, counter_base: int = 0, label: float = 1.0,
                    fp8_scale: float = DEFAULT_FP8_SCALE, affine: torch.Tensor | None = None) -> torch.Tensor:

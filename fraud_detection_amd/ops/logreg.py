@@ -164,61 +164,14 @@ def progressive_schedule(n_rows: int) -> list:
     return []
 
 
-@dataclass
-class VirtualRows:
-    """Virtual SMOTE: ``n_new`` synthetic minority rows that follow the stored rows of a fit.  The
-    pass kernels rebuild each one from its 8-byte draw (``plan``, ops/knn.smote_plan: parents i, j
-    and lambda) and the bf16 parents ``P`` (ops/knn.smote_parents) with the interpolation and
-    rounding of ops/knn.smote_generate -- so the fit is bit-identical to the materialized one
-    while the synthetic rows are never written to HBM nor read back in every Newton pass."""
-    P: torch.Tensor                  # bf16 [mc, 32] parents in the training rows' space
-    nbr: torch.Tensor                # int32 [mq, k] neighbour indices into P
-    q_offset: int
-    n_new: int
-    seed: int = 42
-    counter_base: int = 0
-    label: float = 1.0
-    plan: torch.Tensor | None = None  # int32 [n_new, 2] draws (built on first use)
-
-    def ensure_plan(self) -> torch.Tensor:
-        if self.plan is None:
-            from . import knn as knn_ops
-
-            self.plan = knn_ops.smote_plan(self.nbr, self.n_new, self.seed, self.counter_base)
-        return self.plan
-
-    def materialize(self, rows: torch.Tensor, fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:
-        """[rows; synthetic rows] as one stored tensor (CPU path, tests)."""
-        from . import knn as knn_ops
-
-        out = torch.empty((rows.shape[0] + self.n_new, NCOLS), dtype=rows.dtype, device=rows.device)
-        out[: rows.shape[0]] = rows
-        knn_ops.smote_generate(self.P, self.nbr, self.q_offset, self.n_new, out[rows.shape[0]:], seed=self.seed,
-                               counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale)
-        return out
-
-
 def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True,
-          sub: int = 1, vrows: VirtualRows | None = None, n_split: int | None = None):
+          sub: int = 1):
     """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact).
-    sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up).
-    vrows: rows [rows.shape[0], end) are virtual SMOTE rows rebuilt inside the pass.
-    n_split: rows [n_split, end) of ``rows`` are stored SMOTE rows; their tiles are visited zipped
-    with the real ones exactly as the virtual rows are (a materialized fit then equals the virtual
-    one bit for bit)."""
+    sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up)."""
     dptr = ptr(ws.done) if done else 0
     h = int(hessian)
-    fmt = 0 if storage_kind(rows) == "bf16" else 1
-    if vrows is not None and vrows.n_new > 0:
-        v = vrows
-        m.logreg_pass_smote(ptr(rows), fmt, begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
-                            float(fp8_scale), ptr(v.P), ptr(v.ensure_plan()), int(v.q_offset), rows.shape[0],
-                            float(v.label), float(fp8_scale), ptr(ws.partial), ws.nblocks, s)
-    elif n_split is not None and n_split < end:
-        m.logreg_pass_smote(ptr(rows), fmt, begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
-                            float(fp8_scale), 0, 0, 0, int(n_split), 1.0, float(fp8_scale), ptr(ws.partial),
-                            ws.nblocks, s)
-    elif fmt == 0:        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
+    if storage_kind(rows) == "bf16":
+        m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
                       ws.nblocks, s)
     else:
         m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
@@ -258,8 +211,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
                hess_refresh: int | str = "auto", n_sched: int | None = None,
-               local_warmup: bool = True, affine: torch.Tensor | None = None,
-               vrows: VirtualRows | None = None, n_split: int | None = None) -> FitInfo:
+               local_warmup: bool = True, affine: torch.Tensor | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -269,13 +221,9 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     reuse the last reduced Hessian still held in the workspace (lazy-Hessian Newton).  0 = every
     iteration.  The fixed point is unchanged: only the step's curvature model is older.
     ``affine``: [64] float64 (c | 1/sigma) when the rows are pivot-shifted instead of standardized
-    (ops/scaler.scaler_fit_cast): the fit still runs in standardized space (same w, same C).
-    ``vrows``: virtual SMOTE rows appended to ``rows`` (synthesized in every pass, never stored).
-    ``n_split``: rows[n_split:] are stored SMOTE rows (visited zipped with the real ones, as vrows)."""
+    (ops/scaler.scaler_fit_cast): the fit still runs in standardized space (same w, same C)."""
     check_rows(rows)
     w0 = _default_w0(w0)
-    if vrows is not None and (not rows.is_cuda or vrows.n_new == 0):
-        rows, vrows = (vrows.materialize(rows, fp8_scale) if vrows.n_new else rows), None
     if not rows.is_cuda:
         if affine is not None:
             a = affine.cpu().double()
@@ -291,7 +239,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
         m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)  # w0 is standardized-space
-    n = rows.shape[0] + (vrows.n_new if vrows is not None else 0)
+    n = rows.shape[0]
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
     # The warm-up schedule sets the number of collectives, so every rank must derive the same one:
     # from ``n_sched`` (the smallest rank's row count, known to all ranks without a collective when
@@ -318,7 +266,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     for sub, iters in sched:
         hs_w = auto_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
-            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, vrows=vrows, n_split=n_split)
+            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub)
             if sync_warm:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
@@ -346,7 +294,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             # 8 vs 7 iterations, profiles/r1_s25)
             fresh = refresh <= 0 or full_it[0] % refresh == 0
             full_it[0] += 1
-            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, vrows=vrows, n_split=n_split)
+            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s)
             if comm is not None and comm.world_size > 1:
                 # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
                 comm.all_reduce_(ws.red if fresh else ws.red[:GRAD_SLOTS])
@@ -392,8 +340,7 @@ def _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, co
 def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float = 0.9, epochs: int = 5,
             batch_rows: int = 1 << 20, class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True,
             comm=None, fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None,
-            checkpoint=None, checkpoint_every: int = 0, vrows: VirtualRows | None = None,
-            n_split: int | None = None) -> FitInfo:
+            checkpoint=None, checkpoint_every: int = 0) -> FitInfo:
     """Momentum minibatch SGD.  Each minibatch is a contiguous window of ``batch_rows`` rows of
     this rank's shard (rows are stored pre-shuffled); DP all-reduces the minibatch gradient.
 
@@ -403,9 +350,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
     the same result as an uninterrupted fit."""
     check_rows(rows)
     w0 = _default_w0(w0)
-    if vrows is not None and (not rows.is_cuda or vrows.n_new == 0):
-        rows, vrows = (vrows.materialize(rows, fp8_scale) if vrows.n_new else rows), None
-    n = rows.shape[0] + (vrows.n_new if vrows is not None else 0)
+    n = rows.shape[0]
     sig = _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm) if checkpoint else None
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
@@ -430,7 +375,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
         for b in range(start[1] if ep == start[0] else 0, nb):
             lo = min(b * batch_rows, n)
             hi = min(lo + batch_rows, n)
-            _pass(m, rows, ws, False, lo, hi, fp8_scale, s, done=False, vrows=vrows, n_split=n_split)
+            _pass(m, rows, ws, False, lo, hi, fp8_scale, s, done=False)
             if comm is not None and comm.world_size > 1:
                 comm.all_reduce_(ws.red[:GRAD_SLOTS])
             m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), d, float(C), float(lr), float(momentum),

@@ -117,28 +117,8 @@ def main():
     case(f"knn_topk_{m}", lambda: K.knn_topk(xmin, xmin, 5, 0), m * m * 64)
     nbr = K.knn_topk(xmin, xmin, 5, 0)
     case("smote_generate_n", lambda: K.smote_generate(xmin, nbr, 0, n, outb), n * 64)
-    # virtual SMOTE: n real rows + n synthesized in the pass (vs logreg_pass_*_2n over 2n stored rows)
-    vr = L.VirtualRows(K.smote_parents(xmin), nbr, 0, n, seed=42)
-
-    def lr_pass_virtual(h):
-        def f():
-            L._pass(nat, rows2[:n], ws, h, 0, N2, 4.0, s, done=False, vrows=vr)
-        return f
-    case("logreg_pass_virtual_hess_s3_2n", lr_pass_virtual(3), n * 64)
-    case("logreg_pass_virtual_grad_2n", lr_pass_virtual(0), n * 64)
-    # same draws grouped by parent row (sorted plan): isolates the parent-gather locality cost
-    plan = vr.ensure_plan()
-    order = torch.argsort(plan[:, 0] & 0xFFFFFF, stable=True)
-    vr_sorted = L.VirtualRows(vr.P, nbr, 0, n, seed=42, plan=plan[order].contiguous())
-
-    def lr_pass_virtual_sorted(h):
-        def f():
-            L._pass(nat, rows2[:n], ws, h, 0, N2, 4.0, s, done=False, vrows=vr_sorted)
-        return f
-    case("logreg_pass_virtual_grad_2n_sorted", lr_pass_virtual_sorted(0), n * 64)
-    case("logreg_pass_virtual_hess_s3_2n_sorted", lr_pass_virtual_sorted(3), n * 64)
-    case("smote_plan_n", lambda: K.smote_plan(nbr, n, 42, 0), n * 8)
-    case("newton_fit_virtual_2n_tol1e-4", lambda: L.newton_fit(rows2[:n], tol=1e-4, workspace=ws, vrows=vr), n * 64)
+    par = K.smote_parents(xmin)
+    case("smote_generate_n_bf16_parents", lambda: K.smote_generate(par, nbr, 0, n, outb), n * 64)
     sc = torch.randn(2_000_000, device=dev)
     yl = (torch.rand(2_000_000, device=dev) < 0.002).to(torch.uint8)
     case("roc_auc_2M", lambda: M.roc_auc(sc, yl), 2_000_000 * 5)
