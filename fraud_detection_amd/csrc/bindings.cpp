@@ -116,6 +116,10 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
                                 P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s));
   });
+  m.def("newton_update_stamped", [](u red, u state, u w32, u done, double C, u aff, u stamps, u s) {
+    fdx::launch_newton_update_stamped(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), C,
+                                      P<const double>(aff), P<unsigned long long>(stamps), S(s));
+  });
   m.def("logreg_reduce", [](u partial, int nblocks, int ncols, u out, u done, u s) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });

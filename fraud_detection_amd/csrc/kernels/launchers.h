@@ -95,6 +95,9 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
                           const double* aff, hipStream_t stream);
+// tools/newton_stamps.py: the d = 30 update with s_memtime stamps at its 7 phase boundaries
+void launch_newton_update_stamped(const double* red, double* state, float* w32, int* done, double C,
+                                  const double* aff, unsigned long long* stamps, hipStream_t stream);
 void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream);
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
                        double momentum, int fit_intercept, hipStream_t stream);

@@ -268,14 +268,30 @@ __device__ __forceinline__ void store_folded(const double* ss, const double* cA,
     w32[t] = (t == kLabelCol) ? 0.0f : (t == kBiasCol) ? (float)(ss[kW + t] - p) : (float)(ss[kW + t] * iA[t]);
 }
 
-template <int MT>  // MT > 0: compile-time number of active coordinates (identity index map)
+// In-kernel phase stamps (STAMP = true, tools/newton_stamps.py only): s_memtime at the phase
+// boundaries, one asm statement with its own lgkmcnt(0) (cdna_hip_programming.md §7).
+#define FDX_STAMP(i)                                                                              \
+  do {                                                                                            \
+    if constexpr (STAMP) {                                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                          \
+      unsigned long long t_;                                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
+      __builtin_amdgcn_sched_barrier(0);                                                          \
+      tsv[i] = t_;                                                                                \
+    }                                                                                             \
+  } while (0)
+
+template <int MT, bool STAMP = false>  // MT > 0: compile-time number of active coordinates (identity index map)
 __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
                                                            double* __restrict__ st,
                                                            float* __restrict__ w32,
                                                            int* __restrict__ done, int d, double C,
                                                            double tol, int max_iter,
                                                            int fit_intercept, int phase_start,
-                                                           const double* __restrict__ aff) {
+                                                           const double* __restrict__ aff,
+                                                           unsigned long long* __restrict__ stamps = nullptr) {
+  unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  FDX_STAMP(0);
   __shared__ double sr[kLRPartStride];
   __shared__ double cA[32], iA[32], h30[32];
   __shared__ double ss[kStateSize];
@@ -302,6 +318,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     if (t < 32) cA[t] = av; else iA[t - 32] = av;
   }
   __syncthreads();
+  FDX_STAMP(1);
   if (aff) {
     // Rows hold s = x - pivot; standardized z = (s - c) * inv with c = inv = identity on the
     // intercept/label/padding columns.  The sums map exactly: g_z[j] = inv_j (g_j - c_j g_30),
@@ -318,6 +335,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     }
     __syncthreads();
   }
+  FDX_STAMP(2);
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
   const double reg = 1.0 / (C * S);
   const double invS = 1.0 / S;
@@ -388,6 +406,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       }
     }
     double bi = (t < m) ? -grad[my < 0 ? 0 : my] * S : 0.0;
+    FDX_STAMP(3);
     constexpr int JE = MT > 0 ? MT : 32;
     double dv[32];
 #pragma unroll
@@ -407,6 +426,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         dv[k] = 0.0;
       }
     }
+    FDX_STAMP(4);
 #pragma unroll
     for (int k = 0; k < 32; ++k) {  // L y = b (column sweep; b lives in lane registers)
       if (k < m) {
@@ -422,6 +442,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         bi = (t == k) ? xk : (t < k ? fma(-lkt, xk, bi) : bi);
       }
     }
+    FDX_STAMP(5);
     if (t < kCols) {
       ss[kWPrev + t] = ss[kW + t];
       ss[kStep + t] = 0.0;
@@ -450,7 +471,12 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   }
 #pragma unroll
   for (int i = 0; i < kStateSize / 64; ++i) st[t + 64 * i] = ss[t + 64 * i];
+  FDX_STAMP(6);
+  if constexpr (STAMP) {
+    if (t < 8) stamps[t] = tsv[t];
+  }
 }
+#undef FDX_STAMP
 
 // Standardized-space weights (state) -> weights for pivot-shifted rows.  One wave.
 __global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restrict__ st,
@@ -560,6 +586,13 @@ void launch_newton_update(const double* red, double* state, float* w32, int* don
     newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
                                                   phase_start, aff);
   check_launch("newton_update");
+}
+
+void launch_newton_update_stamped(const double* red, double* state, float* w32, int* done, double C,
+                                  const double* aff, unsigned long long* stamps, hipStream_t stream) {
+  newton_update_kernel<31, true><<<1, 64, 0, stream>>>(red, state, w32, done, 30, C, 0.0, 1 << 30, 1, 0, aff,
+                                                       stamps);
+  check_launch("newton_update_stamped");
 }
 
 void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream) {

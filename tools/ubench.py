@@ -117,6 +117,7 @@ def main():
     case(f"knn_topk_{m}", lambda: K.knn_topk(xmin, xmin, 5, 0), m * m * 64)
     nbr = K.knn_topk(xmin, xmin, 5, 0)
     case("smote_generate_n", lambda: K.smote_generate(xmin, nbr, 0, n, outb), n * 64)
+    case("write_only_fill_n_rows", lambda: outb.zero_(), n * 64)   # store-bandwidth ceiling for SMOTE
     par = K.smote_parents(xmin)
     case("smote_generate_n_bf16_parents", lambda: K.smote_generate(par, nbr, 0, n, outb), n * 64)
     sc = torch.randn(2_000_000, device=dev)
