@@ -120,12 +120,21 @@ __device__ __forceinline__ T strided_sum(T v) {
   for (int o = GROUP; o < kWave; o <<= 1) v += __shfl_xor(v, o, kWave);
   return v;
 }
-// Sum within aligned groups of G lanes (G = 2,4,8,...).
+// Sum within aligned groups of G lanes (G = 2,4,8,...).  Float groups of 2/4 use DPP quad
+// permutes (a VALU operand modifier, no LDS round trip like ds_bpermute); same association
+// order as the xor butterfly, so results are bit-identical to it.
 template <int G, typename T>
 __device__ __forceinline__ T group_sum(T v) {
+  if constexpr (sizeof(T) == 4 && (G == 2 || G == 4) && !__is_integral(T)) {
+    v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));  // xor 1
+    if constexpr (G == 4)
+      v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));  // xor 2
+    return v;
+  } else {
 #pragma unroll
-  for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, kWave);
-  return v;
+    for (int o = 1; o < G; o <<= 1) v += __shfl_xor(v, o, kWave);
+    return v;
+  }
 }
 
 // v_rcp_f32 (1 ulp), no IEEE division expansion.

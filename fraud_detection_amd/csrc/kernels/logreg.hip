@@ -383,8 +383,8 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     // Lane t owns row t of A in registers (a[32], fully unrolled: static indices).  With MT > 0
     // (compile-time m; the index map is then the identity) every guard below is static, so the
     // single wave -- whose cost is its instruction count -- runs a branch-free stream.  Column k
-    // of L goes to LDS once (Lc[k][t]); the trailing update reads it back as uniform-address
-    // broadcasts and the back substitution reads column t (Lc[t][k]).  1/sqrt: v_rsq_f64 + one
+    // of L goes to LDS once (Lc[k][t]) for the back substitution, which reads column t
+    // (Lc[t][k]).  1/sqrt: v_rsq_f64 + one
     // Newton refinement (~46 bits; the Newton step only needs to be a good descent direction).
     // Rows/columns >= m are identity-padded and never read back.
     const double regS = reg * S;
@@ -409,6 +409,10 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     FDX_STAMP(3);
     constexpr int JE = MT > 0 ? MT : 32;
     double dv[32];
+    // Column k of L is broadcast to the trailing update with v_readlane (L[j][k] lives in lane j:
+    // an SGPR operand of the fma) instead of an LDS write + wait + read-back per column, which
+    // was ~680 cycles of a 31-step dependent chain (tools/newton_stamps.py).  The forward solve
+    // L y = b rides in the same sweep (b is one more column of the right-hand side).
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
       if (k < m) {
@@ -418,22 +422,17 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         dv[k] = inv;
         const double ak = (t == k) ? akk * inv : a[k] * inv;  // column k of L (rows t > k)
         a[k] = ak;
-        Lc[k][t] = ak;
-        __builtin_amdgcn_wave_barrier();
+        Lc[k][t] = ak;  // only the back substitution reads it (column t of lane t's row)
+        const double yk = rdlane(bi, k) * inv;
+        bi = (t == k) ? yk : (t > k ? fma(-ak, yk, bi) : bi);
 #pragma unroll
-        for (int j = k + 1; j < JE; ++j) a[j] = fma(-ak, Lc[k][j], a[j]);
+        for (int j = k + 1; j < JE; ++j) a[j] = fma(-ak, rdlane(ak, j), a[j]);
       } else {
         dv[k] = 0.0;
       }
     }
     FDX_STAMP(4);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {  // L y = b (column sweep; b lives in lane registers)
-      if (k < m) {
-        const double yk = rdlane(bi, k) * dv[k];
-        bi = (t == k) ? yk : (t > k ? fma(-a[k], yk, bi) : bi);
-      }
-    }
+    __builtin_amdgcn_wave_barrier();  // Lc complete (one wave: LDS ops retire in order)
 #pragma unroll
     for (int k = 31; k >= 0; --k) {  // L^T x = y (column sweep): lane t < k needs L[k][t] = Lc[t][k]
       if (k < m) {
