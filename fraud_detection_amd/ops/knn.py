@@ -1,6 +1,8 @@
 """K8 k-nearest neighbours (SMOTE) and K9 SMOTE sample generation."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -22,13 +24,16 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 
 
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
-             nsplit: int | None = None):
+             nsplit: int | None = None, engine: str | None = None):
     """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
     row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
     (ascending distance, ties -> smaller index) and optionally squared distances.
     ``nsplit``: candidate slices searched by separate workgroups and merged (None = auto).
+    ``engine``: "bf16x3" (default; FDX_KNN env) = bf16x3 MFMA filter with exact fp32 re-scoring of
+    the survivors, "fp32" = the fp32-MFMA chain over every candidate.  Both return exact fp32
+    rankings.
     """
     for t, nm in ((Q, "Q"), (C, "C")):
         if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
@@ -56,13 +61,27 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
-    ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
+    fp32_mfma = (engine or os.environ.get("FDX_KNN", "bf16x3")) == "fp32"
+    if fp32_mfma:
+        ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
+    else:
+        ns = m.knn3_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
     ws_s = ws_i = None
     if ns > 1:
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
-    m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
-               ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
+    if fp32_mfma:
+        m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
+                   ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
+    else:
+        # hi/lo bf16 split of both operands (+ per-tile candidate norm bound) for the bf16x3 filter
+        Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
+        Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
+        tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
+        m.knn_split(ptr(Cp), mc_pad, 0, ptr(Chl), ptr(tmax), s)
+        m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
+        m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset), int(k),
+                    ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     if want_dist:
         qn = (Q[:, :30].double() ** 2).sum(1, keepdim=True)
         return idx, (qn - 2.0 * score.double()).float()
