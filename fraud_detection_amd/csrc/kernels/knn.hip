@@ -214,10 +214,11 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
 // is split x = hi + lo (two bf16 rows) and the tile score is hi.hi + hi.lo + lo.hi on
 // v_mfma_f32_32x32x16_bf16 (6 MFMAs = 192 cycles), |approx - exact| <= 2^-16 sum|q_f c_f| (the
 // omitted lo.lo term, the split residuals and fp32 accumulation).  That approximate score only
-// FILTERS: a candidate enters the queue when approx >= thr - margin, margin = 2^-13 (||q|| tmax
-// + 0.5 tmax^2) >= 8x the error bound (tmax = largest ||c|| of the tile), and the queue is
-// re-scored exactly in fp32 before the top-k insertion -- no true neighbour can be filtered
-// out, and lists, threshold and returned scores are exact fp32 (ties -> smaller index).
+// FILTERS: a candidate passes when approx >= thr - margin, margin = 2^-13 (||q|| tmax +
+// 0.5 tmax^2) >= 8x the error bound (tmax = largest ||c|| of the tile); a tile with any pass is
+// staged to LDS in fp32 and its passing rows are re-scored exactly before the top-k insertion
+// -- no true neighbour can be filtered out, and lists, threshold and returned scores are exact
+// fp32 (ties -> smaller index).
 
 // hi/lo bf16 split of prepped rows: hl[r] = 8 x uint4 (hi cols 0..31, then lo cols 0..31);
 // role 0 (candidates) also writes tmax[r / 32] = max feature norm over the 32-row tile.
@@ -268,21 +269,24 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
   const int q0 = blockIdx.x * 32;
   const int qg = q0 + j;
   const int64_t self_c = self_offset >= 0 ? self_offset + qg : -1;
-  // the block's 32 query rows (fp32, prepped: col 30 = 1) for the exact re-score
-  __shared__ float qs[32][kCols + 1];
-  __shared__ int qidx[kQCap * kWave];  // per-lane queue of candidate indices, [slot][lane]
+  // the block's 32 query rows and the current candidate tile, fp32 (prepped), for the exact
+  // re-score from LDS (row stride 36 floats: 16 B aligned, b128 reads of 8 consecutive rows
+  // spread over the banks)
+  constexpr int kLd = kCols + 4;
+  __shared__ __attribute__((aligned(16))) float qs[32 * kLd];
+  __shared__ __attribute__((aligned(16))) float cs[32 * kLd];
   {
-    const float* src = Q + (int64_t)q0 * kCols;
+    const float4* src = reinterpret_cast<const float4*>(Q + (int64_t)q0 * kCols);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int e = lane + 64 * i;
-      qs[e >> 5][e & 31] = src[e];
+    for (int i = 0; i < 4; ++i) {
+      const int e = lane + 64 * i;  // float4 index: row e >> 3, cols 4 (e & 7) ..
+      *reinterpret_cast<float4*>(&qs[(e >> 3) * kLd + 4 * (e & 7)]) = src[e];
     }
   }
   __syncthreads();
   float qn2 = 0.0f;
 #pragma unroll
-  for (int f = 0; f < 30; ++f) qn2 = fmaf(qs[j][f], qs[j][f], qn2);
+  for (int f = 0; f < 30; ++f) qn2 = fmaf(qs[j * kLd + f], qs[j * kLd + f], qn2);
   const float qn = sqrtf(qn2);
   // B operand (query j): MFMA 0 covers columns 8h..8h+7, MFMA 1 columns 16+8h..16+8h+7
   const uint4* qr = Qhl + (int64_t)qg * 8;
@@ -294,28 +298,68 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
   float thr = kNegBig;
-  int qn_cnt = 0;
-  auto rescore = [&](int ci) -> float {
-    const float4* cr = reinterpret_cast<const float4*>(C + (int64_t)ci * kCols);
+  // exact fp32 score of tile row rl against this lane's query (a k-ordered fmaf chain)
+  auto rescore = [&](int rl) -> float {
     float acc = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      const float4 v = cr[k];
-      acc = fmaf(qs[j][4 * k], v.x, acc);
-      acc = fmaf(qs[j][4 * k + 1], v.y, acc);
-      acc = fmaf(qs[j][4 * k + 2], v.z, acc);
-      acc = fmaf(qs[j][4 * k + 3], v.w, acc);
+      const float4 c = *reinterpret_cast<const float4*>(&cs[rl * kLd + 4 * k]);
+      const float4 q = *reinterpret_cast<const float4*>(&qs[j * kLd + 4 * k]);
+      acc = fmaf(q.x, c.x, acc);
+      acc = fmaf(q.y, c.y, acc);
+      acc = fmaf(q.z, c.z, acc);
+      acc = fmaf(q.w, c.w, acc);
     }
     return acc;
   };
-  auto flush = [&]() {
-    for (int e = 0; __any(e < qn_cnt); ++e) {
-      if (e < qn_cnt) {
-        const int ci = qidx[e * kWave + lane];
-        if (ci != self_c && ci < mc) topk_insert<K>(bs, bi, rescore(ci), ci);
-      }
+  const int all_tiles = mc_pad / 32;
+  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
+  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  // register double buffer of the next tile: hi/lo bf16 operands of candidate row j (this lane's
+  // K half) and its fp32 columns 16h..16h+15 (staged to LDS only when a score passes)
+  uint4 cv[4];
+  float4 cf[4];
+  auto fetch = [&](int t, uint4 (&a)[4], float4 (&f)[4]) {
+    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
+    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
+    const float4* pf = reinterpret_cast<const float4*>(C + (int64_t)(t * 32 + j) * kCols + 16 * h);
+    f[0] = pf[0]; f[1] = pf[1]; f[2] = pf[2]; f[3] = pf[3];
+  };
+  if (t_lo < t_hi) fetch(t_lo, cv, cf);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int c0 = t * 32;
+    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, cv[0]), ch1 = __builtin_bit_cast(bf16x8_t, cv[1]);
+    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, cv[2]), cl1 = __builtin_bit_cast(bf16x8_t, cv[3]);
+    const float4 f0 = cf[0], f1 = cf[1], f2 = cf[2], f3 = cf[3];
+    const float tm = tmax[t];
+    if (t + 1 < t_hi) fetch(t + 1, cv, cf);
+    f32x16_t acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, ql0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
+    const float cut = thr - 0x1p-13f * fmaf(qn, tm, 0.5f * tm * tm);
+    float mx = acc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    if (!__any(mx >= cut)) continue;
+    // stage the tile's fp32 rows (lane j, h: row j, columns 16h..16h+15) and re-score exactly
+    float* crow = &cs[j * kLd + 16 * h];
+    *reinterpret_cast<float4*>(crow) = f0;
+    *reinterpret_cast<float4*>(crow + 4) = f1;
+    *reinterpret_cast<float4*>(crow + 8) = f2;
+    *reinterpret_cast<float4*>(crow + 12) = f3;
+    __builtin_amdgcn_wave_barrier();  // one wave: LDS ops retire in order
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int rl = 4 * h + (r & 3) + 8 * (r >> 2);
+      const int ci = c0 + rl;
+      if (acc[r] >= cut && ci != self_c && ci < mc) topk_insert<K>(bs, bi, rescore(rl), ci);
     }
-    qn_cnt = 0;
+    __builtin_amdgcn_wave_barrier();  // cs is rewritten by the next staging tile
+    // threshold = k-th best of the union of this lane's and its partner's (other half) lists
     float ps[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
@@ -332,47 +376,7 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
       ib += ta ? 0 : 1;
     }
     thr = kth;
-  };
-  const int all_tiles = mc_pad / 32;
-  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
-  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
-  uint4 cv[4];
-  auto fetch = [&](int t, uint4 (&a)[4]) {
-    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
-    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
-  };
-  if (t_lo < t_hi) fetch(t_lo, cv);
-  for (int t = t_lo; t < t_hi; ++t) {
-    const int c0 = t * 32;
-    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, cv[0]), ch1 = __builtin_bit_cast(bf16x8_t, cv[1]);
-    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, cv[2]), cl1 = __builtin_bit_cast(bf16x8_t, cv[3]);
-    const float tm = tmax[t];
-    if (t + 1 < t_hi) fetch(t + 1, cv);
-    f32x16_t acc = {};
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, ql0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
-    const float cut = thr - 0x1p-13f * fmaf(qn, tm, 0.5f * tm * tm);
-    float mx = acc[0];
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
-    if (!__any(mx >= cut)) continue;
-    const int cbase = c0 + 4 * h;
-    int qe = qn_cnt * kWave + lane;
-    const int de = (kQCap - 1) * kWave + lane;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const bool pass = acc[r] >= cut;
-      qidx[pass ? qe : de] = cbase + (r & 3) + 8 * (r >> 2);
-      qe += pass ? kWave : 0;
-    }
-    qn_cnt = (qe - lane) / kWave;
-    if (__any(qn_cnt >= kQFlush)) flush();
   }
-  flush();
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const float s2 = __shfl_xor(bs[k], 32, kWave);
