@@ -352,11 +352,15 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
     *reinterpret_cast<float4*>(crow + 8) = f2;
     *reinterpret_cast<float4*>(crow + 12) = f3;
     __builtin_amdgcn_wave_barrier();  // one wave: LDS ops retire in order
+    uint32_t pm = 0;  // passing accumulator rows of this lane (static indices -> no acc spill)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < 16; ++r) pm |= (acc[r] >= cut ? 1u : 0u) << r;
+    while (pm) {
+      const int r = __builtin_ctz(pm);
+      pm &= pm - 1;
       const int rl = 4 * h + (r & 3) + 8 * (r >> 2);
       const int ci = c0 + rl;
-      if (acc[r] >= cut && ci != self_c && ci < mc) topk_insert<K>(bs, bi, rescore(rl), ci);
+      if (ci != self_c && ci < mc) topk_insert<K>(bs, bi, rescore(rl), ci);
     }
     __builtin_amdgcn_wave_barrier();  // cs is rewritten by the next staging tile
     // threshold = k-th best of the union of this lane's and its partner's (other half) lists

@@ -31,9 +31,9 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
     (ascending distance, ties -> smaller index) and optionally squared distances.
     ``nsplit``: candidate slices searched by separate workgroups and merged (None = auto).
-    ``engine``: "bf16x3" (default; FDX_KNN env) = bf16x3 MFMA filter with exact fp32 re-scoring of
-    the survivors, "fp32" = the fp32-MFMA chain over every candidate.  Both return exact fp32
-    rankings.
+    ``engine``: "fp32" (default; FDX_KNN env) = the fp32-MFMA chain over every candidate,
+    "bf16x3" = bf16x3 MFMA filter with exact fp32 re-scoring of the survivors (experimental:
+    slower at the bench size, profiles/r1_s32).  Both return exact fp32 rankings.
     """
     for t, nm in ((Q, "Q"), (C, "C")):
         if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
@@ -61,7 +61,7 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
-    fp32_mfma = (engine or os.environ.get("FDX_KNN", "bf16x3")) == "fp32"
+    fp32_mfma = (engine or os.environ.get("FDX_KNN", "fp32")) == "fp32"
     if fp32_mfma:
         ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
     else:
