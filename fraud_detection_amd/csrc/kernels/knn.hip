@@ -98,7 +98,8 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
                                                          int mc_pad, int mc,
                                                          int64_t self_offset,
                                                          int* __restrict__ out_idx,
-                                                         float* __restrict__ out_score) {
+                                                         float* __restrict__ out_score,
+                                                         const float* __restrict__ thr0) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
   const int q0 = blockIdx.x * 32;
@@ -117,7 +118,10 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = kNegBig;
+  // thr0 (optional): a lower bound of each query's k-th best score (the k-th best over a candidate
+  // sample, ops/knn.py): filters from the first tile instead of after the lists fill
+  const float thr_lo = (thr0 != nullptr && qg < mq) ? thr0[qg] : kNegBig;
+  float thr = thr_lo;
 
   // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks.  Slot
   // kQCap - 1 is the lane's dump slot.
@@ -148,7 +152,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = kth;
+    thr = fmaxf(kth, thr_lo);
   };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
@@ -263,7 +267,8 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
                                                           const uint4* __restrict__ Chl,
                                                           const float* __restrict__ tmax, int mc_pad, int mc,
                                                           int64_t self_offset, int* __restrict__ out_idx,
-                                                          float* __restrict__ out_score) {
+                                                          float* __restrict__ out_score,
+                                                          const float* __restrict__ thr0) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
   const int q0 = blockIdx.x * 32;
@@ -297,7 +302,8 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = kNegBig;
+  const float thr_lo = (thr0 != nullptr && qg < mq) ? thr0[qg] : kNegBig;
+  float thr = thr_lo;
   // exact fp32 score of tile row rl against this lane's query (a k-ordered fmaf chain)
   auto rescore = [&](int rl) -> float {
     float acc = 0.0f;
@@ -379,7 +385,7 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = kth;
+    thr = fmaxf(kth, thr_lo);
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -472,7 +478,8 @@ int knn3_splits(int mq_pad, int mc_pad) {
 
 void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream) {
+                      float* out_score, float* ws_score, int* ws_idx, int nsplit, const float* thr0,
+                      hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk3: pads must be x32");
   if (nsplit < 1) nsplit = 1;
   if (nsplit > 1 && (ws_score == nullptr || ws_idx == nullptr))
@@ -483,7 +490,7 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
   const uint4* qh = reinterpret_cast<const uint4*>(Qhl);
   const uint4* chl = reinterpret_cast<const uint4*>(Chl);
 #define FDX_KNN3(KK)                                                                            \
-  knn_topk3_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, mq, C, chl, tmax, mc_pad, mc, self_offset, oi, os); \
+  knn_topk3_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, mq, C, chl, tmax, mc_pad, mc, self_offset, oi, os, thr0); \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
   switch (k) {
@@ -503,7 +510,8 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
 
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream) {
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, const float* thr0,
+                     hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk: pads must be x32");
   if (nsplit < 1) nsplit = 1;
   if (nsplit > 1 && (ws_score == nullptr || ws_idx == nullptr))
@@ -513,7 +521,7 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
   float* os = nsplit > 1 ? ws_score : out_score;
 #define FDX_KNN(KK)                                                                             \
   knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi,           \
-                                                     os);                                        \
+                                                     os, thr0);                                  \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
   switch (k) {

@@ -112,10 +112,14 @@ void launch_knn_split(const float* Xp, int m_pad, int role, uint4* hl, float* tm
 int knn3_splits(int mq_pad, int mc_pad);
 void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
+                      float* out_score, float* ws_score, int* ws_idx, int nsplit, const float* thr0,
+                      hipStream_t stream);
+// thr0 (nullable, [mq]): per-query lower bound of the k-th best score (a sample search), used as
+// the initial filter threshold
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, const float* thr0,
+                     hipStream_t stream);
 
 // ---- smote.hip ----
 // P [m, 32] bf16 = output-space parents: bf16(C * sigma + c) on the feature columns (aff nullable)

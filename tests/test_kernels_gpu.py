@@ -260,8 +260,10 @@ def test_knn_bf16x3_filter_equals_fp32_engine(dev, scale):
     C[:, :30] *= np.float32(scale / 300.0 if scale != 1.0 else 1.0)
     Ct = torch.from_numpy(C).to(dev)
     Q = Ct[:2000].contiguous()
-    a, sa = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32")
+    a, sa = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32", seed_tiles=0)
     b, sb = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="bf16x3")
+    c, sc = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32", seed_tiles=8)
+    assert torch.equal(a, c) and torch.equal(sa, sc)   # threshold seeding never changes a list
     if scale == 1.0:
         assert torch.equal(a, b) and torch.equal(sa, sb)
     else:
