@@ -1,8 +1,6 @@
 """K8 k-nearest neighbours (SMOTE) and K9 SMOTE sample generation."""
 from __future__ import annotations
 
-import os
-
 import numpy as np
 import torch
 
@@ -24,17 +22,13 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 
 
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
-             nsplit: int | None = None, engine: str | None = None, seed_tiles: int = 8):
+             nsplit: int | None = None):
     """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
     row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
     (ascending distance, ties -> smaller index) and optionally squared distances.
     ``nsplit``: candidate slices searched by separate workgroups and merged (None = auto).
-    ``engine``: "fp32" (default; FDX_KNN env) = the fp32-MFMA chain over every candidate,
-    "bf16x3" = bf16x3 MFMA filter with exact fp32 re-scoring of the survivors.  Both return
-    exact fp32 rankings.  ``seed_tiles``: candidate tiles of the threshold-seeding sample search
-    (0 = off).
     """
     for t, nm in ((Q, "Q"), (C, "C")):
         if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
@@ -62,41 +56,13 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
-    fp32_mfma = (engine or os.environ.get("FDX_KNN", "fp32")) == "fp32"
-    if fp32_mfma:
-        ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
-    else:
-        ns = m.knn3_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
-    # Threshold seed: the exact (k+1)-th best score over a strided sample of candidate tiles is a
-    # lower bound of every query's k-th best (self may sit in the sample: hence k+1), so the full
-    # search filters from its first tile instead of inserting whole tiles until its lists fill.
-    thr0 = None
-    n_tiles = mc_pad // 32
-    if seed_tiles and n_tiles >= 4 * seed_tiles and k + 1 <= 8:
-        step = n_tiles // seed_tiles
-        rows = (torch.arange(seed_tiles, device=C.device) * step * 32)[:, None] + torch.arange(32, device=C.device)
-        Cs = Cp.index_select(0, rows.reshape(-1))
-        s_idx = torch.empty((mq, k + 1), device=Q.device, dtype=torch.int32)
-        s_sc = torch.empty((mq, k + 1), device=Q.device, dtype=torch.float32)
-        m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cs), Cs.shape[0], Cs.shape[0], -1, k + 1, ptr(s_idx), ptr(s_sc),
-                   0, 0, 1, 0, s)
-        thr0 = s_sc[:, k].contiguous()
+    ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
     ws_s = ws_i = None
     if ns > 1:
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
-    if fp32_mfma:
-        m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
-                   ptr(score), ptr(ws_s), ptr(ws_i), ns, ptr(thr0), s)
-    else:
-        # hi/lo bf16 split of both operands (+ per-tile candidate norm bound) for the bf16x3 filter
-        Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
-        Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
-        tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
-        m.knn_split(ptr(Cp), mc_pad, 0, ptr(Chl), ptr(tmax), s)
-        m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
-        m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset), int(k),
-                    ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, ptr(thr0), s)
+    m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
+               ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     if want_dist:
         qn = (Q[:, :30].double() ** 2).sum(1, keepdim=True)
         return idx, (qn - 2.0 * score.double()).float()

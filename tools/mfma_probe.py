@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Minimal driver for PMC runs of the MFMA kernels: the bench's minority k-NN self-search
-(13.6k x 13.6k, k = 5) with both engines, and one 1k-explanation KernelSHAP batch."""
+(13.6k x 13.6k, k = 5), and one 1k-explanation KernelSHAP batch."""
 import os
 import sys
 
@@ -27,8 +27,7 @@ def main():
     ke = KernelExplainer(a, -3.0, X[:100].cpu().numpy(), device="cuda")
     Xe = X[:1000].contiguous()
     for _ in range(reps):
-        for eng in ("fp32", "bf16x3"):
-            K.knn_topk(xmin, xmin, 5, 0, engine=eng)
+        K.knn_topk(xmin, xmin, 5, 0)
         kernelshap(Xe, ke, sync=False)
     torch.cuda.synchronize()
     print("mfma_probe done", tuple(xmin.shape))

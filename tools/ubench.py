@@ -115,10 +115,6 @@ def main():
     xmin = S.scale_cast(X, st, labels=y, out_dtype="f32", idx=idx)
     m = xmin.shape[0]
     case(f"knn_topk_{m}", lambda: K.knn_topk(xmin, xmin, 5, 0), m * m * 64)
-    case(f"knn_topk_{m}_unseeded", lambda: K.knn_topk(xmin, xmin, 5, 0, seed_tiles=0), m * m * 64)
-    case(f"knn_topk_{m}_bf16x3", lambda: K.knn_topk(xmin, xmin, 5, 0, engine="bf16x3"), m * m * 64)
-    case(f"knn_topk_{m}_bf16x3_unseeded", lambda: K.knn_topk(xmin, xmin, 5, 0, engine="bf16x3", seed_tiles=0),
-         m * m * 64)
     nbr = K.knn_topk(xmin, xmin, 5, 0)
     case("smote_generate_n", lambda: K.smote_generate(xmin, nbr, 0, n, outb), n * 64)
     case("write_only_fill_n_rows", lambda: outb.zero_(), n * 64)   # store-bandwidth ceiling for SMOTE
