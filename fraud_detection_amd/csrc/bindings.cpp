@@ -157,10 +157,10 @@ PYBIND11_MODULE(_fdx_native, m) {
 
   // kernelshap
   m.def("kernelshap", [](u X, int E, int d, u a, float bias, u bg, u cb, int nbg, u Z, int nS, int S_pad, u A, u Az,
-                         int link, u phi, u fx, u f0, u s) {
+                         int link, u phi, u fx, u f0, u s, u stamps) {
     fdx::launch_kernelshap(P<const float>(X), E, d, P<const float>(a), bias, P<const float>(bg), P<const float>(cb),
                            nbg, P<const uint16_t>(Z), nS, S_pad, P<const float>(A), P<const float>(Az), link,
-                           P<float>(phi), P<float>(fx), P<float>(f0), S(s));
+                           P<float>(phi), P<float>(fx), P<float>(f0), S(s), P<unsigned long long>(stamps));
   });
 
   // gbdt (K11)

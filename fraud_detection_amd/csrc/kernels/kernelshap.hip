@@ -33,12 +33,27 @@ __device__ __forceinline__ short bf16_bits(float f) { return (short)f32_to_bf16(
 
 // link: 0 = identity on probabilities (shap default), 1 = logit of the mean probability,
 //       2 = model log-odds (mean of logits; KernelSHAP == LinearSHAP exactly)
+// STAMP (tools/kernelshap_stamps.py): s_memtime of thread 0 at the phase boundaries -> stamps[e][8]
+#define FDX_STAMP(i)                                                                              \
+  do {                                                                                            \
+    if constexpr (STAMP) {                                                                        \
+      __builtin_amdgcn_sched_barrier(0);                                                          \
+      unsigned long long t_;                                                                      \
+      asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");                 \
+      __builtin_amdgcn_sched_barrier(0);                                                          \
+      tsv[i] = t_;                                                                                \
+    }                                                                                             \
+  } while (0)
+
+template <bool STAMP = false>
 __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     const float* __restrict__ X, int n_expl, int d, const float* __restrict__ a, float bias,
     const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
     const uint16_t* __restrict__ Z, int S, int S_pad, const float* __restrict__ Amat,
     const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
-    float* __restrict__ f0_out) {
+    float* __restrict__ f0_out, unsigned long long* __restrict__ stamps = nullptr) {
+  unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  FDX_STAMP(0);
   __shared__ float f[kMaxS];
   __shared__ float xs[32];
   __shared__ float red[8];
@@ -71,6 +86,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
       }
     }
   }
+  FDX_STAMP(1);
   const float inv_nb = 1.0f / (float)n_bg;
   const int nst = S_pad / 32;
   for (int st = wv; st < nst; st += kWaves) {
@@ -98,6 +114,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     fs += __shfl_xor(fs, 32, kWave);
     if (h == 0) f[32 * st + r] = fs * inv_nb;
   }
+  FDX_STAMP(2);
   // f0 (background mean output) and f(x)
   float z0s = 0.0f;
   for (int b = threadIdx.x; b < n_bg; b += kThreads) z0s += link == 2 ? cb[b] : fast_sigmoid(cb[b]);
@@ -108,6 +125,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
   zx = wave_sum(zx);
   if (threadIdx.x == 0) red[4] = zx;
   __syncthreads();
+  FDX_STAMP(3);
   const float f0m = (red[0] + red[1] + red[2] + red[3]) * inv_nb;
   const float logit_x = red[4] + bias;
   float f0l, fxl;
@@ -127,6 +145,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     f[s] = v - f0l;
   }
   __syncthreads();
+  FDX_STAMP(4);
   // phi_i = sum_s A[i][s] y_s - Az[i] delta, i < d-1: 8 threads per output
   const int i = threadIdx.x >> 3, part = threadIdx.x & 7;
   float acc = 0.0f;
@@ -138,6 +157,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
   __shared__ float ph[32];
   if (part == 0 && i < d - 1) ph[i] = acc - Az[i] * delta;
   __syncthreads();
+  FDX_STAMP(5);
   if (threadIdx.x == 0) {
     float sum = 0.0f;
     for (int k = 0; k < d - 1; ++k) sum += ph[k];
@@ -147,21 +167,33 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
   }
   __syncthreads();
   if (threadIdx.x < d) phi[(int64_t)e * d + threadIdx.x] = ph[threadIdx.x];
+  FDX_STAMP(6);
+  if constexpr (STAMP) {
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) stamps[(int64_t)e * 8 + k] = tsv[k];
+    }
+  }
 }
+#undef FDX_STAMP
 
 }  // namespace
 
 void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
                        const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
                        const float* Az, int link, float* phi, float* fx_out, float* f0_out,
-                       hipStream_t stream) {
+                       hipStream_t stream, unsigned long long* stamps) {
   if (d < 2 || d > 30) throw std::runtime_error("kernelshap: 2 <= d <= 30");
   if (n_bg < 1 || n_bg > kMaxBg) throw std::runtime_error("kernelshap: 1 <= n_bg <= 128");
   if (S < 1 || S_pad % 32 != 0 || S_pad < S || S_pad > kMaxS)
     throw std::runtime_error("kernelshap: S_pad must be a multiple of 32 in [S, 4096]");
   if (n_expl <= 0) return;
-  kernelshap_kernel<<<n_expl, kThreads, 0, stream>>>(X, n_expl, d, a, bias, bg, cb, n_bg, Z, S, S_pad, Amat, Az,
-                                                      link, phi, fx_out, f0_out);
+  if (stamps != nullptr)
+    kernelshap_kernel<true><<<n_expl, kThreads, 0, stream>>>(X, n_expl, d, a, bias, bg, cb, n_bg, Z, S, S_pad, Amat,
+                                                             Az, link, phi, fx_out, f0_out, stamps);
+  else
+    kernelshap_kernel<false><<<n_expl, kThreads, 0, stream>>>(X, n_expl, d, a, bias, bg, cb, n_bg, Z, S, S_pad, Amat,
+                                                              Az, link, phi, fx_out, f0_out);
   check_launch("kernelshap");
 }
 

@@ -140,7 +140,7 @@ void launch_auc_hist_reduce(const unsigned* hist, int bits, unsigned long long* 
 void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
                        const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
                        const float* Az, int link, float* phi, float* fx_out, float* f0_out,
-                       hipStream_t stream);
+                       hipStream_t stream, unsigned long long* stamps = nullptr);
 
 // ---- K11 gbdt (gbdt.hip) ----
 void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,

@@ -39,8 +39,9 @@ def _device_design(expl, dev):
     return t
 
 
-def kernelshap(X: torch.Tensor, expl, sync: bool = True):
-    """X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else tensors)."""
+def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | None = None):
+    """X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else tensors).
+    ``stamps`` (int64 [E, 8], tools/kernelshap_stamps.py): per-explanation phase timestamps."""
     if X.dim() != 2 or X.dtype != torch.float32 or X.shape[1] != expl.d or not X.is_contiguous():
         raise ValueError(f"X must be contiguous float32 [E, {expl.d}]")
     m = native()
@@ -52,7 +53,7 @@ def kernelshap(X: torch.Tensor, expl, sync: bool = True):
     f0 = torch.empty(E, device=dev, dtype=torch.float32)
     m.kernelshap(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]), expl.B.shape[0],
                  ptr(t["Z"]), t["S"], t["S_pad"], ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi), ptr(fx),
-                 ptr(f0), stream_of(X))
+                 ptr(f0), stream_of(X), ptr(stamps))
     if not sync:
         return phi, fx, f0
     return phi.cpu().numpy().astype(np.float64), fx.cpu().numpy().astype(np.float64), float(f0[0].item()) if E else 0.0
