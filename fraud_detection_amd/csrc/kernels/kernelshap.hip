@@ -5,7 +5,7 @@
 // coalition design Z [S][M] and the efficiency-constrained WLS operator A [M-1][S] (solved once).
 //
 // Per explanation e (one workgroup):
-//   logit(z_s, b) = sum_k z_sk u_bk + c_b,   u_b = a * (x_e - B_b),   c_b = a . B_b + bias
+//   logit(z_s, b) = sum_k z_sk u_bk + c_b,   u_b = a * x_e - W_b,   W_b = a * B_b,   c_b = a . B_b + bias
 // is a (n_bg x 32) x (32 x S) product.  The background intercepts are folded in as K column 31
 // (Z[:,31] = 1, U[:,31] = c_b), so the accumulator IS the logit.  v_mfma_f32_32x32x16_bf16 with
 // the background row on the M axis and the coalition on the N axis: Z is exactly representable
@@ -54,16 +54,18 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     float* __restrict__ f0_out, unsigned long long* __restrict__ stamps = nullptr) {
   unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   FDX_STAMP(0);
-  __shared__ float f[kMaxS];
+  __shared__ __attribute__((aligned(16))) float f[kMaxS];
   __shared__ float xs[32];
   __shared__ float red[8];
   const int e = blockIdx.x;
   const int lane = lane_id(), wv = wave_id();
   const int r = lane & 31, h = lane >> 5;
-  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? X[(int64_t)e * d + threadIdx.x] : 0.0f;
+  // v = a o x (col 31: 0); u_b = v - W_b with W = [a o B_b, 0.., -c_b] precomputed per design
+  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? a[threadIdx.x] * X[(int64_t)e * d + threadIdx.x] : 0.0f;
   __syncthreads();
   const int ntb = (n_bg + 31) >> 5;  // background tiles in use (uniform)
-  // U fragments (hi / lo) for every background tile and both k-steps: 16 regs x 4 tiles
+  // U fragments (hi / lo) for every background tile and both k-steps: 16 regs x 4 tiles; each
+  // lane's 8 W values of a (tile, k-step) are two contiguous float4 loads
   bf16x8_t uhi[4][2], ulo[4][2];
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
@@ -71,14 +73,17 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     const bool okb = b < n_bg && t < ntb;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
+      const int k0 = 16 * ks + 8 * h;
+      float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
+      if (okb) {
+        const float4* wr = reinterpret_cast<const float4*>(Bg + (int64_t)b * kCols + k0);
+        w0 = wr[0];
+        w1 = wr[1];
+      }
+      const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const int k = 16 * ks + 8 * h + j;
-        float u = 0.0f;
-        if (okb) {
-          if (k < d) u = a[k] * (xs[k] - Bg[(int64_t)b * d + k]);
-          else if (k == 31) u = cb[b];
-        }
+        const float u = okb ? xs[k0 + j] - wv8[j] : 0.0f;
         const short hi = bf16_bits(u);
         const float hif = __uint_as_float(((uint32_t)(uint16_t)hi) << 16);
         uhi[t][ks][j] = hi;
@@ -121,7 +126,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
   z0s = wave_sum(z0s);
   if (lane == 0) red[wv] = z0s;
   float zx = 0.0f;
-  if (threadIdx.x < 32) zx = threadIdx.x < d ? a[threadIdx.x] * xs[threadIdx.x] : 0.0f;
+  if (threadIdx.x < 32) zx = xs[threadIdx.x];  // a o x
   zx = wave_sum(zx);
   if (threadIdx.x == 0) red[4] = zx;
   __syncthreads();
@@ -136,22 +141,38 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     fxl = logit_x;
   } else { f0l = f0m; fxl = fast_sigmoid(logit_x); }
   const float delta = fxl - f0l;
-  for (int s = threadIdx.x; s < S; s += kThreads) {
+  for (int s = threadIdx.x; s < S_pad; s += kThreads) {
     float v = f[s];
     if (link == 1) {
       v = fminf(fmaxf(v, 1e-12f), 1.0f - 1e-7f);
       v = __logf(v / (1.0f - v));
     }
-    f[s] = v - f0l;
+    f[s] = s < S ? v - f0l : 0.0f;  // padded coalitions contribute nothing (A is zero there too)
   }
   __syncthreads();
   FDX_STAMP(4);
-  // phi_i = sum_s A[i][s] y_s - Az[i] delta, i < d-1: 8 threads per output
+  // phi_i = sum_s A[i][s] y_s - Az[i] delta, i < d-1: 8 threads per output, float4 steps of the
+  // (S_pad-strided, zero-padded) A row, 4 independent accumulators (4 loads in flight)
   const int i = threadIdx.x >> 3, part = threadIdx.x & 7;
   float acc = 0.0f;
   if (i < d - 1) {
-    const float* Ai = Amat + (int64_t)i * S;
-    for (int s = part; s < S; s += 8) acc = fmaf(Ai[s], f[s], acc);
+    const float4* Ai = reinterpret_cast<const float4*>(Amat + (int64_t)i * S_pad);
+    const float4* fv = reinterpret_cast<const float4*>(f);
+    float a4[4] = {0.f, 0.f, 0.f, 0.f};
+    const int nq = S_pad >> 2;  // float4 columns; S_pad % 32 == 0 -> nq % 8 == 0
+    int q = part;
+    for (; q + 24 < nq; q += 32) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const float4 av = Ai[q + 8 * u], yv = fv[q + 8 * u];
+        a4[u] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[u]))));
+      }
+    }
+    for (; q < nq; q += 8) {
+      const float4 av = Ai[q], yv = fv[q];
+      a4[0] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[0]))));
+    }
+    acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
   }
   acc = group_sum<8>(acc);
   __shared__ float ph[32];

@@ -135,8 +135,10 @@ void launch_auc_hist(const float* scores, const uint8_t* labels, int64_t n, int 
 void launch_auc_hist_reduce(const unsigned* hist, int bits, unsigned long long* out, hipStream_t stream);
 
 // ---- kernelshap.hip ----
-// X [E][d] raw explanations; a [32] folded weights; bg [n_bg][d] raw background; cb [n_bg]
-// background logits; Z [S_pad][32] bf16 coalitions (col 31 = 1); Amat [d-1][S]; Az [d-1].
+// X [E][d] raw explanations; a [32] folded weights; bg = W [n_bg][32] = [a o B_b, 0.., -c_b] (the
+// background rows pre-multiplied by the weights, col 31 = minus the background logit); cb [n_bg]
+// background logits; Z [S_pad][32] bf16 coalitions (col 31 = 1); Amat [d-1][S_pad] (zero-padded);
+// Az [d-1].
 void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
                        const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
                        const float* Az, int link, float* phi, float* fx_out, float* f0_out,

@@ -11,7 +11,8 @@ _LINKS = {"identity": 0, "logit": 1, "logit_model": 2}
 
 def _device_design(expl, dev):
     """Upload the explainer's design once: Z as bf16 [S_pad, 32] (col 31 = 1 folds the
-    background intercepts into the GEMM), A [d-1, S], A z_M, background rows and logits."""
+    background intercepts into the GEMM), A [d-1, S_pad] (zero-padded), A z_M, the weighted
+    background rows W and the background logits."""
     key = (str(dev),)
     if expl._dev_cache is not None and expl._dev_cache[0] == key:
         return expl._dev_cache[1]
@@ -26,12 +27,18 @@ def _device_design(expl, dev):
     a32 = np.zeros(32, np.float32)
     a32[:d] = expl.a[:d]
     cb = (expl.B.astype(np.float64) @ expl.a[:d] + expl.bias).astype(np.float32)
+    # W = [a o B_b, 0.., -c_b]: u_b = a o x - W_b, with u_b[31] = c_b folding the intercepts
+    W = np.zeros((expl.B.shape[0], 32), np.float32)
+    W[:, :d] = (expl.B.astype(np.float32) * a32[:d][None, :]).astype(np.float32)
+    W[:, 31] = -cb
+    Ap = np.zeros((d - 1, S_pad), np.float32)
+    Ap[:, :S] = expl.A
     t = {
         "Z": torch.from_numpy(Zp).to(dev).to(torch.bfloat16).contiguous(),
-        "A": torch.from_numpy(expl.A.astype(np.float32)).to(dev).contiguous(),
+        "A": torch.from_numpy(Ap).to(dev).contiguous(),
         "Az": torch.from_numpy((expl.A @ expl.zM).astype(np.float32)).to(dev),
         "a": torch.from_numpy(a32).to(dev),
-        "bg": torch.from_numpy(np.ascontiguousarray(expl.B, np.float32)).to(dev),
+        "bg": torch.from_numpy(W).to(dev),
         "cb": torch.from_numpy(cb).to(dev),
         "S": S, "S_pad": S_pad,
     }
