@@ -64,6 +64,9 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
   if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? a[threadIdx.x] * X[(int64_t)e * d + threadIdx.x] : 0.0f;
   __syncthreads();
   const int ntb = (n_bg + 31) >> 5;  // background tiles in use (uniform)
+  // sigmoid links: u is pre-scaled by -log2(e), so the accumulator is -z log2(e) and
+  // sigma(z) = 1 / (1 + exp2(acc)) needs no multiply per element
+  const float us = link == 2 ? 1.0f : -1.4426950408889634f;
   // U fragments (hi / lo) for every background tile and both k-steps: 16 regs x 4 tiles; each
   // lane's 8 W values of a (tile, k-step) are two contiguous float4 loads
   bf16x8_t uhi[4][2], ulo[4][2];
@@ -83,7 +86,7 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
       const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float u = okb ? xs[k0 + j] - wv8[j] : 0.0f;
+        const float u = okb ? (xs[k0 + j] - wv8[j]) * us : 0.0f;
         const short hi = bf16_bits(u);
         const float hif = __uint_as_float(((uint32_t)(uint16_t)hi) << 16);
         uhi[t][ks][j] = hi;
@@ -109,11 +112,16 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ulo[t][0], zb[0], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uhi[t][1], zb[1], acc, 0, 0, 0);
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ulo[t][1], zb[1], acc, 0, 0, 0);
+      if (t < ntb - 1 || (n_bg & 31) == 0) {  // full tile (uniform)
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int b = 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-        const float v = link == 2 ? acc[i] : fast_sigmoid(acc[i]);
-        fs += b < n_bg ? v : 0.0f;
+        for (int i = 0; i < 16; ++i)
+          fs += link == 2 ? acc[i] : fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
+      } else {  // partial last tile: rows past n_bg are skipped (whole-wave skips for i >= 4 at n_bg = 100)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h < n_bg)
+            fs += link == 2 ? acc[i] : fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
+        }
       }
     }
     fs += __shfl_xor(fs, 32, kWave);
