@@ -188,17 +188,20 @@ __host__ __device__ __forceinline__ uint32_t u32_range(uint32_t v, uint32_t n) {
   return (uint32_t)(((uint64_t)v * (uint64_t)n) >> 32);
 }
 
-// SMOTE draw of sample s (Philox counter (s, counter_base), key seed): query row i uniform over
-// the mq rows, neighbour slot uniform over k (one Lemire pick over mq*k), interpolation weight on
-// a 2^-16 grid.  Packed as {i | lam_hi << 24, j | lam_lo << 24} (8 bytes per draw);
-// ops/reference.py smote_plan / smote_generate is the numpy oracle.
-__device__ __forceinline__ uint2 smote_draw(int64_t s, uint32_t cb0, uint32_t cb1, uint32_t key0, uint32_t key1,
-                                            uint32_t range, uint32_t k, const int* __restrict__ nbr) {
-  const Philox4 r = philox4x32_10((uint32_t)s, (uint32_t)(s >> 32), cb0, cb1, key0, key1);
-  const uint32_t pick = u32_range(r.x, range);
-  const uint32_t i = pick / k;
-  const uint32_t j = (uint32_t)nbr[(int64_t)i * k + (pick - i * k)];
-  const uint32_t lam = r.y >> 16;
+// SMOTE draws: one Philox4x32-10 call per PAIR of samples.  In each 128-sample block
+// [128 m, 128 m + 128), counter 64 m + L (L < 64) gives sample 128 m + L its (query/neighbour pick,
+// lambda) from words (x, y) and sample 128 m + 64 + L from (z, w).  Query row i and neighbour
+// slot come from one Lemire pick over mq*k; lambda is on a 2^-16 grid.  A draw packs into 8
+// bytes {i | lam_hi << 24, j | lam_lo << 24}.  ops/reference.py smote_plan is the numpy oracle.
+// pick / k: for pick < 2^22, floor((pick + 0.5) * (1/k)) in fp32 is exact (the rounding error
+// stays under 0.5/k of the nearest integer), 3 VALU ops instead of the integer-division
+// expansion; larger ranges fall back to it.
+__device__ __forceinline__ uint2 smote_pack_draw(uint32_t word_pick, uint32_t word_lam, uint32_t range, uint32_t k,
+                                                 float inv_k, bool small, const int* __restrict__ nbr) {
+  const uint32_t pick = u32_range(word_pick, range);
+  const uint32_t i = small ? (uint32_t)(((float)pick + 0.5f) * inv_k) : pick / k;
+  const uint32_t j = (uint32_t)nbr[__umul24(i, k) + (pick - __umul24(i, k))];
+  const uint32_t lam = word_lam >> 16;
   return make_uint2(i | ((lam >> 8) << 24), j | ((lam & 0xffu) << 24));
 }
 __host__ __device__ __forceinline__ float smote_lambda(uint32_t dx, uint32_t dy) {

@@ -44,95 +44,110 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     cc[j] = feat ? (float)aff[8 * q + j] : 0.0f;
   }
   const uint32_t range = (uint32_t)mq * (uint32_t)k;
-  const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 64;
-  // One Philox draw per lane = one sample per lane (64 samples per wave-iteration).  Software
-  // pipeline: the NEXT iteration's draw and its neighbour-index load are issued before this
-  // iteration's row gathers and stores, so the dependent nbr -> row chain costs one memory
-  // latency per iteration instead of two.
-  auto draw = [&](int64_t b, int& di, int& dj, float& dl) {
-    const int64_t sl = b + lane;
-    const uint2 d = sl < n_new ? smote_draw(sl, cb0, cb1, key0, key1, range, (uint32_t)k, nbr) : make_uint2(0, 0);
-    di = (int)(d.x & 0xffffffu);
-    dj = (int)(d.y & 0xffffffu);
-    dl = smote_lambda(d.x, d.y);
+  const float inv_k = 1.0f / (float)k;
+  const bool small = range < (1u << 22);
+  const int64_t step = (int64_t)gridDim.x * (kThreads / kWave) * 128;
+  // One Philox call per lane = two samples per lane (128 samples per wave-iteration, two halves
+  // of 64 rows).  Software pipeline: the NEXT iteration's draws and neighbour-index loads are
+  // issued behind this iteration's first row gathers, so the dependent nbr -> row chain costs one
+  // memory latency per iteration instead of two.
+  auto draw2 = [&](int64_t b, int (&di)[2], int (&dj)[2], float (&dl)[2]) {
+    const int64_t c = (b >> 1) + lane;  // b is a multiple of 128
+    const Philox4 r = philox4x32_10((uint32_t)c, (uint32_t)(c >> 32), cb0, cb1, key0, key1);
+    const uint32_t wp[2] = {r.x, r.z}, wl[2] = {r.y, r.w};
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const uint2 d = (b + 64 * hh + lane < n_new) ? smote_pack_draw(wp[hh], wl[hh], range, (uint32_t)k, inv_k, small, nbr)
+                                                   : make_uint2(0, 0);
+      di[hh] = (int)(d.x & 0xffffffu);
+      dj[hh] = (int)(d.y & 0xffffffu);
+      dl[hh] = smote_lambda(d.x, d.y);
+    }
   };
-  int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 64;
-  int my_i = 0, my_j = 0;
-  float my_lam = 0.0f;
-  if (base < n_new) draw(base, my_i, my_j, my_lam);
+  int64_t base = ((int64_t)blockIdx.x * (kThreads / kWave) + wave_id()) * 128;
+  int my_i[2] = {0, 0}, my_j[2] = {0, 0};
+  float my_lam[2] = {0.0f, 0.0f};
+  if (base < n_new) draw2(base, my_i, my_j, my_lam);
   for (; base < n_new; base += step) {
-    // 4 row groups of 16 samples: 4 lanes per sample, 8 columns per lane; gathers issued first
-    float4 a0[4], a1[4], b0[4], b1[4];
-    float lam[4];
+    int nx_i[2] = {0, 0}, nx_j[2] = {0, 0};
+    float nx_lam[2] = {0.0f, 0.0f};
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int src = 16 * u + rr;
-      const int i = __shfl(my_i, src, kWave);
-      const int jn = __shfl(my_j, src, kWave);
-      lam[u] = __shfl(my_lam, src, kWave);
-      if constexpr (PB) {
-        const uint4 pi = Cb[(q_offset + i) * 4 + q], pj = Cb[(int64_t)jn * 4 + q];
-        a0[u] = make_float4(bf16lo(pi.x), bf16hi(pi.x), bf16lo(pi.y), bf16hi(pi.y));
-        a1[u] = make_float4(bf16lo(pi.z), bf16hi(pi.z), bf16lo(pi.w), bf16hi(pi.w));
-        b0[u] = make_float4(bf16lo(pj.x), bf16hi(pj.x), bf16lo(pj.y), bf16hi(pj.y));
-        b1[u] = make_float4(bf16lo(pj.z), bf16hi(pj.z), bf16lo(pj.w), bf16hi(pj.w));
-      } else {
-        const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
-        const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
-        a0[u] = xi[0]; a1[u] = xi[1]; b0[u] = xj[0]; b1[u] = xj[1];
-      }
-    }
-    // next iteration's draw + neighbour-index load, issued AFTER this iteration's gathers:
-    // vector loads return in issue order, so waiting for the gathers does not wait for it
-    int nx_i = 0, nx_j = 0;
-    float nx_lam = 0.0f;
-    if (base + step < n_new) draw(base + step, nx_i, nx_j, nx_lam);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t s = base + 16 * u + rr;
-      if (s >= n_new) continue;
-      const float l = lam[u];
-      float o[8] = {fmaf(l, b0[u].x - a0[u].x, a0[u].x), fmaf(l, b0[u].y - a0[u].y, a0[u].y),
-                    fmaf(l, b0[u].z - a0[u].z, a0[u].z), fmaf(l, b0[u].w - a0[u].w, a0[u].w),
-                    fmaf(l, b1[u].x - a1[u].x, a1[u].x), fmaf(l, b1[u].y - a1[u].y, a1[u].y),
-                    fmaf(l, b1[u].z - a1[u].z, a1[u].z), fmaf(l, b1[u].w - a1[u].w, a1[u].w)};
-      if (!PB && aff) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = o[j] * sig[j] + cc[j];
-      }
-      if (q == 3) {
-        o[6] = 1.0f;   // col 30: intercept column
-        o[7] = label;  // col 31: label
-      }
-      if constexpr (OUT == 0) {
-        uint4 pk;
-        pk.x = pack_bf16x2(o[0], o[1]);
-        pk.y = pack_bf16x2(o[2], o[3]);
-        pk.z = pack_bf16x2(o[4], o[5]);
-        pk.w = pack_bf16x2(o[6], o[7]);
-        // NT: streaming store (nt policy) so the output stream does not evict the L2-resident
-        // parent rows every gather reads
-        if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(out) + s * 4 + q);
-        else reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
-      } else if constexpr (OUT == 1) {
-        float4* dst = reinterpret_cast<float4*>(out) + s * 8 + 2 * q;
-        dst[0] = make_float4(o[0], o[1], o[2], o[3]);
-        dst[1] = make_float4(o[4], o[5], o[6], o[7]);
-      } else {
-        uint2 pk = make_uint2(0, 0);
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) {
-          const bool feat = (8 * q + jj) < kBiasCol;
-          const uint32_t b = f32_to_fp8e4m3(feat ? o[jj] * out_scale : o[jj]);
-          if (jj < 4) pk.x |= b << (8 * jj);
-          else pk.y |= b << (8 * (jj - 4));
+    for (int hh = 0; hh < 2; ++hh) {
+      const int64_t hbase = base + 64 * hh;
+      // 4 row groups of 16 samples: 4 lanes per sample, 8 columns per lane; gathers issued first
+      float4 a0[4], a1[4], b0[4], b1[4];
+      float lam[4];
+  #pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int src = 16 * u + rr;
+        const int i = __shfl(my_i[hh], src, kWave);
+        const int jn = __shfl(my_j[hh], src, kWave);
+        lam[u] = __shfl(my_lam[hh], src, kWave);
+        if constexpr (PB) {
+          const uint4 pi = Cb[(q_offset + i) * 4 + q], pj = Cb[(int64_t)jn * 4 + q];
+          a0[u] = make_float4(bf16lo(pi.x), bf16hi(pi.x), bf16lo(pi.y), bf16hi(pi.y));
+          a1[u] = make_float4(bf16lo(pi.z), bf16hi(pi.z), bf16lo(pi.w), bf16hi(pi.w));
+          b0[u] = make_float4(bf16lo(pj.x), bf16hi(pj.x), bf16lo(pj.y), bf16hi(pj.y));
+          b1[u] = make_float4(bf16lo(pj.z), bf16hi(pj.z), bf16lo(pj.w), bf16hi(pj.w));
+        } else {
+          const float4* xi = reinterpret_cast<const float4*>(C + (q_offset + i) * kCols + 8 * q);
+          const float4* xj = reinterpret_cast<const float4*>(C + (int64_t)jn * kCols + 8 * q);
+          a0[u] = xi[0]; a1[u] = xi[1]; b0[u] = xj[0]; b1[u] = xj[1];
         }
-        reinterpret_cast<uint2*>(out)[s * 4 + q] = pk;
+      }
+      // next iteration's draws + neighbour-index loads, issued AFTER the first half's gathers:
+      // vector loads return in issue order, so waiting for the gathers does not wait for them
+      if (hh == 0 && base + step < n_new) draw2(base + step, nx_i, nx_j, nx_lam);
+  #pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t s = hbase + 16 * u + rr;
+        if (s >= n_new) continue;
+        const float l = lam[u];
+        float o[8] = {fmaf(l, b0[u].x - a0[u].x, a0[u].x), fmaf(l, b0[u].y - a0[u].y, a0[u].y),
+                      fmaf(l, b0[u].z - a0[u].z, a0[u].z), fmaf(l, b0[u].w - a0[u].w, a0[u].w),
+                      fmaf(l, b1[u].x - a1[u].x, a1[u].x), fmaf(l, b1[u].y - a1[u].y, a1[u].y),
+                      fmaf(l, b1[u].z - a1[u].z, a1[u].z), fmaf(l, b1[u].w - a1[u].w, a1[u].w)};
+        if (!PB && aff) {
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = o[j] * sig[j] + cc[j];
+        }
+        if (q == 3) {
+          o[6] = 1.0f;   // col 30: intercept column
+          o[7] = label;  // col 31: label
+        }
+        if constexpr (OUT == 0) {
+          uint4 pk;
+          pk.x = pack_bf16x2(o[0], o[1]);
+          pk.y = pack_bf16x2(o[2], o[3]);
+          pk.z = pack_bf16x2(o[4], o[5]);
+          pk.w = pack_bf16x2(o[6], o[7]);
+          // NT: streaming store (nt policy) so the output stream does not evict the L2-resident
+          // parent rows every gather reads
+          if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(out) + s * 4 + q);
+          else reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
+        } else if constexpr (OUT == 1) {
+          float4* dst = reinterpret_cast<float4*>(out) + s * 8 + 2 * q;
+          dst[0] = make_float4(o[0], o[1], o[2], o[3]);
+          dst[1] = make_float4(o[4], o[5], o[6], o[7]);
+        } else {
+          uint2 pk = make_uint2(0, 0);
+  #pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const bool feat = (8 * q + jj) < kBiasCol;
+            const uint32_t b = f32_to_fp8e4m3(feat ? o[jj] * out_scale : o[jj]);
+            if (jj < 4) pk.x |= b << (8 * jj);
+            else pk.y |= b << (8 * (jj - 4));
+          }
+          reinterpret_cast<uint2*>(out)[s * 4 + q] = pk;
+        }
       }
     }
-    my_i = nx_i;
-    my_j = nx_j;
-    my_lam = nx_lam;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      my_i[hh] = nx_i[hh];
+      my_j[hh] = nx_j[hh];
+      my_lam[hh] = nx_lam[hh];
+    }
   }
 }
 
@@ -162,7 +177,7 @@ void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int 
                            int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream) {
   if (n_new <= 0) return;
-  const int64_t per_block = (kThreads / kWave) * 64;
+  const int64_t per_block = (kThreads / kWave) * 128;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
 #define FDX_SG(O, NT, PB)                                                                             \

@@ -308,19 +308,25 @@ def knn_topk(Q: np.ndarray, C: np.ndarray, k: int, self_offset: int = -1):
 
 
 def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int) -> np.ndarray:
-    """uint32 [n_new, 2] SMOTE draws {i | lam_hi << 24, j | lam_lo << 24} (common.h smote_draw):
-    query row i and neighbour slot from one Lemire pick over mq*k, lam = (r.y >> 16) / 2^16."""
+    """uint32 [n_new, 2] SMOTE draws {i | lam_hi << 24, j | lam_lo << 24} (common.h
+    smote_pack_draw): one Philox call per pair of samples -- in 128-sample block m, counter
+    64 m + L serves sample 128 m + L with words (x, y) and sample 128 m + 64 + L with (z, w); query
+    row i and neighbour slot from one Lemire pick over mq*k, lam = (word >> 16) / 2^16."""
     nbr = np.asarray(nbr)
     mq, k = nbr.shape
     s = np.arange(n_new, dtype=np.uint64)
-    r = philox4x32_10((s & _MASK32).astype(np.uint32), (s >> np.uint64(32)).astype(np.uint32),
+    c = (s // np.uint64(128)) * np.uint64(64) + (s % np.uint64(64))
+    half = ((s % np.uint64(128)) // np.uint64(64)).astype(bool)
+    r = philox4x32_10((c & _MASK32).astype(np.uint32), (c >> np.uint64(32)).astype(np.uint32),
                       np.full(n_new, counter_base & 0xFFFFFFFF, np.uint32),
                       np.full(n_new, (counter_base >> 32) & 0xFFFFFFFF, np.uint32),
                       seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    pick = u32_range(r[0], mq * k)
+    wp = np.where(half, r[2], r[0])
+    wl = np.where(half, r[3], r[1])
+    pick = u32_range(wp, mq * k)
     i = (pick // k).astype(np.uint32)
     j = nbr[i, pick % k].astype(np.uint32)
-    lam = r[1].astype(np.uint32) >> np.uint32(16)
+    lam = wl.astype(np.uint32) >> np.uint32(16)
     return np.stack([i | ((lam >> np.uint32(8)) << np.uint32(24)), j | ((lam & np.uint32(0xFF)) << np.uint32(24))], 1)
 
 
