@@ -4,9 +4,12 @@
 // minority rows, random neighbour among its k nearest, lambda ~ U[0,1) -- here on a 2^-16 grid, so
 // a draw packs into 8 bytes: common.h smote_draw) used at
 // train_model.py:65-66,91-92 and preprocess.py:43-44.  imblearn draws
-// from numpy MT19937; here every sample s owns Philox4x32-10 counter (s, counter_base), so the
-// output is independent of launch geometry and the CPU oracle (ops/reference.py) reproduces it
-// bit for bit before the bf16 rounding.
+// from numpy MT19937; here draws are counter-based Philox4x32-10 with one call per PAIR of
+// samples (in 128-sample block m, counter (64 m + L, counter_base) serves samples 128 m + L and
+// 128 m + 64 + L; common.h smote_pack_draw), so the output is independent of launch geometry and
+// the CPU oracle (ops/reference.py smote_plan) reproduces it bit for bit before the bf16
+// rounding.  Row indices are packed in 24 bits: the host refuses parent sets >= 2^24 rows
+// (ops/reference.py smote_check_ranges).
 //
 // MI355X mapping: write-bound stream.  4 lanes per synthetic row, 8 columns (two 16 B gathers of
 // each parent row, L2-resident) per lane, one 16 B store per lane: 16 rows = 1 KiB per

@@ -106,6 +106,7 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
     mq, k = nbr.shape
     if q_offset < 0 or q_offset + mq > C.shape[0]:
         raise ValueError("query rows out of range of C")
+    ref.smote_check_ranges(C.shape[0], mq, k)
     check_rows(out, "out")
     if out.shape[0] != n_new:
         raise ValueError("out must have n_new rows")

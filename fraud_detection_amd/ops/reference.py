@@ -307,6 +307,19 @@ def knn_topk(Q: np.ndarray, C: np.ndarray, k: int, self_offset: int = -1):
     return idx, d2
 
 
+SMOTE_MAX_ROWS = 1 << 24  # i / j are packed into 24 bits of a draw (common.h smote_pack_draw)
+
+
+def smote_check_ranges(n_parents: int, mq: int, k: int) -> None:
+    """The packed draw holds i and j in 24 bits and the Lemire pick ranges over mq*k in 32 bits:
+    refuse sizes that would silently wrap.  Shard the SMOTE query set above this."""
+    if n_parents >= SMOTE_MAX_ROWS:
+        raise ValueError(f"SMOTE parent set has {n_parents} rows; the packed draw indexes < 2^24 "
+                         f"({SMOTE_MAX_ROWS}) rows -- use smote_scope='shard' or subsample the minority class")
+    if mq * k >= 1 << 32:
+        raise ValueError(f"SMOTE pick range mq*k = {mq}*{k} does not fit 32 bits")
+
+
 def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int) -> np.ndarray:
     """uint32 [n_new, 2] SMOTE draws {i | lam_hi << 24, j | lam_lo << 24} (common.h
     smote_pack_draw): one Philox call per pair of samples -- in 128-sample block m, counter
@@ -314,6 +327,7 @@ def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int) -> np.
     row i and neighbour slot from one Lemire pick over mq*k, lam = (word >> 16) / 2^16."""
     nbr = np.asarray(nbr)
     mq, k = nbr.shape
+    smote_check_ranges(mq, mq, k)
     s = np.arange(n_new, dtype=np.uint64)
     c = (s // np.uint64(128)) * np.uint64(64) + (s % np.uint64(64))
     half = ((s % np.uint64(128)) // np.uint64(64)).astype(bool)
@@ -344,12 +358,6 @@ def smote_generate(C: np.ndarray, nbr: np.ndarray, q_offset: int, n_new: int, se
     """fp32 synthetic rows (before bf16/fp8 rounding), bit-exact Philox draws."""
     C = np.asarray(C, dtype=np.float32)
     nbr = np.asarray(nbr)
-    mq, k = nbr.shape
-    s = np.arange(n_new, dtype=np.uint64)
-    r = philox4x32_10((s & _MASK32).astype(np.uint32), (s >> np.uint64(32)).astype(np.uint32),
-                      np.full(n_new, counter_base & 0xFFFFFFFF, np.uint32),
-                      np.full(n_new, (counter_base >> 32) & 0xFFFFFFFF, np.uint32),
-                      seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
     i, j, lam = smote_draws_decode(smote_plan(nbr, n_new, seed, counter_base))
     lam = lam[:, None]
     xi = C[q_offset + i]

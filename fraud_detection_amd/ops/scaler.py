@@ -235,14 +235,24 @@ class PendingCompaction:
     enqueues the write of the stable index list."""
 
     _pool: list = []  # rotating pinned slots (pinned allocation costs tens of microseconds)
+    _owners: list = []  # the pending compaction whose count each slot still holds
     _next = 0
+    _POOL = 8
 
     def __init__(self, labels, target, nb, counts, total):
+        cls = PendingCompaction
         self.labels, self.target, self.nb, self.counts = labels, target, nb, counts
-        if not PendingCompaction._pool:
-            PendingCompaction._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(8)]
-        self.host = PendingCompaction._pool[PendingCompaction._next % 8]
-        PendingCompaction._next += 1
+        if not cls._pool:
+            cls._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(cls._POOL)]
+            cls._owners = [None] * cls._POOL
+        slot = cls._next % cls._POOL
+        cls._next += 1
+        prev = cls._owners[slot]
+        if prev is not None:  # a ninth compaction in flight: settle the slot's previous owner first
+            prev.result()
+        cls._owners[slot] = self
+        self._slot = slot
+        self.host = cls._pool[slot]
         self.host.copy_(total, non_blocking=True)
         self.event = torch.cuda.Event()
         self.event.record()
@@ -252,6 +262,8 @@ class PendingCompaction:
         if self._out is None:
             self.event.synchronize()
             cnt = int(self.host[0])
+            if PendingCompaction._owners[self._slot] is self:
+                PendingCompaction._owners[self._slot] = None
             out = torch.empty(cnt, device=self.labels.device, dtype=torch.int64)
             if cnt:
                 native().compact_write(ptr(self.labels), self.labels.shape[0], self.target, ptr(self.counts), ptr(out),

@@ -5,7 +5,12 @@ Semantics kept from the reference's Celery configuration (xai_tasks.py:63; docs/
     (DONE) after the handler returns; a worker that dies mid-task lets the lease expire and the
     task is redelivered to another worker;
   * retry with countdown: ``retry(countdown=s)`` re-queues with eta = now + s, attempts += 1;
-  * max_retries: once attempts exceed it the task is FAILED (terminal);
+  * max_retries: once attempts exceed it the task is FAILED (terminal).  A lease that expires
+    (the worker died or hung mid-task) counts as an attempt too, so a task that kills its worker
+    every time is not redelivered forever;
+  * ownership: ack / retry / fail / extend only act on a row that is still LEASED by the calling
+    worker, so a slow worker whose lease expired cannot settle the task a second worker now owns
+    (or overwrite a DONE row).
   * queue depth is observable (the KEDA trigger of k8s/keda-scaledobject.yaml used the Redis list
     length; here ``depth()`` / the ``fdx_queue_depth`` gauge).
 Claiming is a conditional UPDATE per row (status/lease predicate in the WHERE clause), which is
@@ -17,7 +22,7 @@ import time
 import uuid
 from dataclasses import dataclass
 
-from sqlalchemy import and_, func, or_, select, update
+from sqlalchemy import and_, case, func, or_, select, update
 from sqlalchemy.engine import Engine
 
 from ..store.db import make_engine
@@ -67,52 +72,74 @@ class DurableQueue:
             q = q.where(t.c.name.in_(names))
         q = q.order_by(t.c.eta).limit(batch * 2)
         out = []
+        expired = and_(t.c.status == LEASED, t.c.lease_until < now)
         with self.engine.begin() as c:
             cand = [r[0] for r in c.execute(q)]
             for tid in cand:
                 if len(out) >= batch:
                     break
                 res = c.execute(update(t).where(and_(t.c.id == tid, ready)).values(
-                    status=LEASED, worker=worker, lease_until=now + visibility_timeout, updated_at=now))
-                if res.rowcount == 1:
-                    row = c.execute(select(t).where(t.c.id == tid)).mappings().one()
-                    out.append(LeasedTask(row["id"], row["name"], list(row["args"]), dict(row["kwargs"]),
-                                          dict(row["headers"]), row["attempts"], row["max_retries"]))
+                    status=LEASED, worker=worker, lease_until=now + visibility_timeout, updated_at=now,
+                    attempts=case((expired, t.c.attempts + 1), else_=t.c.attempts)))
+                if res.rowcount != 1:
+                    continue
+                row = c.execute(select(t).where(t.c.id == tid)).mappings().one()
+                if row["attempts"] > row["max_retries"]:
+                    c.execute(update(t).where(t.c.id == tid).values(
+                        status=FAILED, worker=None, lease_until=0.0, updated_at=now,
+                        error=f"lease expired after {row['attempts']} attempts (max_retries={row['max_retries']})"))
+                    continue
+                out.append(LeasedTask(row["id"], row["name"], list(row["args"]), dict(row["kwargs"]),
+                                      dict(row["headers"]), row["attempts"], row["max_retries"]))
         return out
 
-    def ack(self, task_id: str, result=None, worker: str | None = None) -> bool:
-        t = TaskRecord.__table__
+    @staticmethod
+    def _owned(t, task_id: str, worker: str | None):
         cond = [t.c.id == task_id, t.c.status == LEASED]
         if worker is not None:
             cond.append(t.c.worker == worker)
+        return and_(*cond)
+
+    def ack(self, task_id: str, result=None, worker: str | None = None) -> bool:
+        t = TaskRecord.__table__
         with self.engine.begin() as c:
-            r = c.execute(update(t).where(and_(*cond)).values(status=DONE, result=result, updated_at=time.time()))
+            r = c.execute(update(t).where(self._owned(t, task_id, worker)).values(
+                status=DONE, result=result, updated_at=time.time()))
         return r.rowcount == 1
 
-    def retry(self, task_id: str, countdown: float, error: str = "", worker: str | None = None) -> str:
-        """Re-queue after a failure; returns the new status (QUEUED or FAILED)."""
+    def retry(self, task_id: str, countdown: float, error: str = "", worker: str | None = None) -> str | None:
+        """Re-queue after a failure; returns the new status (QUEUED or FAILED), or None when the
+        task is no longer leased by ``worker`` (nothing changed)."""
         t = TaskRecord.__table__
         now = time.time()
         with self.engine.begin() as c:
-            row = c.execute(select(t.c.attempts, t.c.max_retries).where(t.c.id == task_id)).one()
+            row = c.execute(select(t.c.attempts, t.c.max_retries).where(self._owned(t, task_id, worker))).first()
+            if row is None:
+                return None
             attempts = row[0] + 1
             status = FAILED if attempts > row[1] else QUEUED
-            c.execute(update(t).where(t.c.id == task_id).values(
+            r = c.execute(update(t).where(self._owned(t, task_id, worker)).values(
                 status=status, attempts=attempts, eta=now + float(countdown), lease_until=0.0, error=error[:4000],
-                updated_at=now))
-        return status
+                worker=None, updated_at=now))
+        return status if r.rowcount == 1 else None
 
-    def fail(self, task_id: str, error: str = "", result=None):
+    def fail(self, task_id: str, error: str = "", result=None, worker: str | None = None) -> bool:
+        """Terminal failure of a task still leased by ``worker``; returns whether a row changed."""
         t = TaskRecord.__table__
         with self.engine.begin() as c:
-            c.execute(update(t).where(t.c.id == task_id).values(status=FAILED, error=error[:4000], result=result,
-                                                                 updated_at=time.time()))
+            r = c.execute(update(t).where(self._owned(t, task_id, worker)).values(
+                status=FAILED, error=error[:4000], result=result, updated_at=time.time()))
+        return r.rowcount == 1
 
-    def extend(self, task_ids: list[str], visibility_timeout: float, worker: str):
+    def extend(self, task_ids: list[str], visibility_timeout: float, worker: str) -> int:
+        """Heartbeat: push the lease of every task still held by ``worker``; returns rows extended."""
+        if not task_ids:
+            return 0
         t = TaskRecord.__table__
         with self.engine.begin() as c:
-            c.execute(update(t).where(and_(t.c.id.in_(task_ids), t.c.worker == worker, t.c.status == LEASED)).values(
+            r = c.execute(update(t).where(and_(t.c.id.in_(task_ids), t.c.worker == worker, t.c.status == LEASED)).values(
                 lease_until=time.time() + visibility_timeout))
+        return r.rowcount
 
     # ---- introspection -------------------------------------------------------------------
     def status(self, task_id: str) -> dict | None:

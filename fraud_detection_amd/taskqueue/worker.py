@@ -25,6 +25,32 @@ from .queue import DurableQueue
 logger = logging.getLogger("fdx.worker")
 
 
+class _LeaseHeartbeat:
+    """Extends the leases of an in-flight batch every visibility_timeout/3 seconds, so a batch
+    that runs longer than the visibility timeout is not redelivered while it is still running."""
+
+    def __init__(self, queue: DurableQueue, ids: list[str], visibility_timeout: float, worker: str):
+        self.queue, self.ids, self.vt, self.worker = queue, ids, visibility_timeout, worker
+        self._done = threading.Event()
+        self._th = threading.Thread(target=self._beat, name="fdx-lease-heartbeat", daemon=True)
+
+    def _beat(self):
+        while not self._done.wait(max(self.vt / 3.0, 0.01)):
+            try:
+                self.queue.extend(self.ids, self.vt, self.worker)
+            except Exception as e:  # noqa: BLE001 - a missed beat only risks a redelivery
+                logger.warning("lease heartbeat failed: %s", e)
+
+    def __enter__(self):
+        self._th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._done.set()
+        self._th.join()
+        return False
+
+
 class Worker:
     def __init__(self, app: TaskApp, batch: int = 256, visibility_timeout: float = 60.0, poll_interval: float = 0.05,
                  name: str | None = None, metrics=None):
@@ -45,6 +71,13 @@ class Worker:
         leased = self.queue.lease(self.name, self.batch, self.visibility_timeout, names=list(self.app.tasks) or None)
         if not leased:
             return 0
+        with _LeaseHeartbeat(self.queue, [lt.id for lt in leased], self.visibility_timeout, self.name):
+            self._process(leased)
+        if self.metrics is not None:
+            self.metrics.queue_depth.set(self.queue.depth())
+        return len(leased)
+
+    def _process(self, leased):
         by_name: dict[str, list] = {}
         for lt in leased:
             by_name.setdefault(lt.name, []).append(lt)
@@ -52,7 +85,7 @@ class Worker:
             task = self.app.tasks.get(name)
             if task is None:
                 for lt in items:
-                    self.queue.fail(lt.id, f"unregistered task {name}")
+                    self.queue.fail(lt.id, f"unregistered task {name}", worker=self.name)
                 continue
             calls = [TaskCall(lt.id, lt.args, lt.kwargs,
                               Request(id=lt.id, retries=lt.attempts, headers=lt.headers,
@@ -71,9 +104,6 @@ class Worker:
                 os._exit(17)  # simulate SIGKILL between compute and ack
             for call, res in zip(calls, results):
                 self._settle(task, call, res, dt / max(len(calls), 1))
-        if self.metrics is not None:
-            self.metrics.queue_depth.set(self.queue.depth())
-        return len(leased)
 
     def _run_single(self, task, call):
         try:
@@ -89,11 +119,11 @@ class Worker:
                 m.task_failure.inc()
             logger.info("task %s retry in %.1fs -> %s", call.id, res.countdown, st)
         elif isinstance(res, MaxRetriesExceededError):
-            self.queue.fail(call.id, str(res), result={"status": "FAILED"})
+            self.queue.fail(call.id, str(res), result={"status": "FAILED"}, worker=self.name)
             if m is not None:
                 m.task_failure.inc()
         elif isinstance(res, BaseException):
-            self.queue.fail(call.id, "".join(traceback.format_exception_only(type(res), res)))
+            self.queue.fail(call.id, "".join(traceback.format_exception_only(type(res), res)), worker=self.name)
             if m is not None:
                 m.task_failure.inc()
         else:

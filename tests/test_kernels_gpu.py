@@ -433,3 +433,14 @@ def test_fp8_hardware_conversions(dev):
     # identical codes, except that -0.0 / tiny negatives may encode as +0 vs -0
     diff = e_hw != e_sw
     assert np.all(ref.fp8_decode(e_hw[diff]) == ref.fp8_decode(e_sw[diff])), vals[diff][:10]
+
+
+@pytest.mark.gpu
+def test_compaction_slots_survive_many_in_flight(dev):
+    """more pending compactions than pinned slots; each keeps its own count."""
+    g = torch.Generator().manual_seed(3)
+    labs = [(torch.rand(50_000 + 977 * i, generator=g) < 0.01 * (i + 1)).to(torch.uint8) for i in range(12)]
+    pend = [S.compact_indices_async(l.to(dev), 1) for l in labs]
+    for l, p in zip(labs, pend):
+        exp = torch.nonzero(l == 1).reshape(-1)
+        assert torch.equal(p.result().cpu(), exp)

@@ -77,3 +77,54 @@ def test_smote_bf16_parents_need_no_affine():
         K.smote_generate(P, nbr, 0, 10, out, affine=st.aff)
     K.smote_generate(P, nbr, 0, 10, out)
     assert torch.all(out[:, 31] == 1)
+
+
+def test_fp32_reciprocal_pick_division_is_exact():
+    """common.h smote_pack_draw: for pick < 2^22, floor((pick + 0.5f) * RN(1/k)) == pick / k for
+    every k the kernel accepts (1..8) and beyond (to 64) -- exhaustive over the pick range."""
+    p = np.arange(1 << 22, dtype=np.uint32)
+    pf = p.astype(np.float32) + np.float32(0.5)
+    for k in range(1, 65):
+        inv = np.float32(1.0) / np.float32(k)
+        got = np.floor(pf * inv).astype(np.uint32)   # fp32 multiply, round-to-nearest
+        assert np.array_equal(got, p // np.uint32(k)), k
+
+
+def test_smote_range_guard():
+    """i/j are packed in 24 bits -- parent sets of 2^24 rows or more must be refused,
+    never silently wrapped."""
+    with pytest.raises(ValueError, match="2\\^24"):
+        ref.smote_check_ranges(1 << 24, 1000, 5)
+    with pytest.raises(ValueError, match="32 bits"):
+        ref.smote_check_ranges(1000, 1 << 30, 5)
+    ref.smote_check_ranges((1 << 24) - 1, (1 << 24) - 1, 5)
+    # the op checks before touching data: a huge virtual parent set via an expanded view
+    C = torch.zeros((1, 32), dtype=torch.float32).expand(1 << 24, 32)
+    nbr = torch.zeros((4, 5), dtype=torch.int32)
+    with pytest.raises(ValueError, match="2\\^24"):
+        K.smote_generate(C, nbr, 0, 4, torch.empty((4, 32), dtype=torch.float32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mq", [100_000, 1_000_000])   # mq*k below / above 2^22 (fp32-reciprocal vs div path)
+def test_smote_device_draws_exact(dev, mq):
+    """Device (i, j, lambda) == smote_plan bit for bit: integer-valued fp32 parents make the fused
+    interpolation exact, so any wrong draw shows up as a differing output value."""
+    k, n_new, M = 5, 300_000, mq + 4096
+    rng = np.random.default_rng(mq)
+    C = np.zeros((M, 32), np.float32)
+    r = np.arange(M, dtype=np.float32)
+    C[:, 0] = r                                # row id (exact in fp32 below 2^24)
+    C[:, 1] = (r * 7) % 1021
+    C[:, 2] = M - r
+    nbr = rng.integers(0, M, size=(mq, k)).astype(np.int32)
+    q_off = M - mq
+    out = torch.empty((n_new, 32), dtype=torch.float32, device=dev)
+    K.smote_generate(torch.from_numpy(C).to(dev), torch.from_numpy(nbr).to(dev), q_off, n_new, out,
+                     seed=11, counter_base=7)
+    i, j, lam = ref.smote_draws_decode(ref.smote_plan(nbr, n_new, 11, 7))
+    assert (mq * k < (1 << 22)) == (mq == 100_000)
+    xi, xj = C[q_off + i, :3].astype(np.float64), C[j, :3].astype(np.float64)
+    exp = (xi + lam.astype(np.float64)[:, None] * (xj - xi)).astype(np.float32)  # exact, then one rounding
+    got = out[:, :3].cpu().numpy()
+    assert np.array_equal(got, exp)

@@ -40,6 +40,53 @@ def test_lease_expiry_redelivers(q):
     assert q.ack(tid, worker="w2")
 
 
+def test_stale_worker_cannot_retry_or_fail(q):
+    """after A's lease expires and B re-leases, A's retry()/fail() must be no-ops."""
+    tid = q.send("t.x")
+    assert q.lease("A", 10, visibility_timeout=0.05)
+    time.sleep(0.1)
+    assert [t.id for t in q.lease("B", 10, 30)] == [tid]
+    assert q.retry(tid, 0, "late A", worker="A") is None
+    assert not q.fail(tid, "late A", worker="A")
+    st = q.status(tid)
+    assert st["status"] == "LEASED" and st["worker"] == "B"
+    assert q.ack(tid, {"ok": 1}, worker="B")
+    assert not q.fail(tid, "after done", worker="B")       # a DONE row is never overwritten
+    assert q.retry(tid, 0, worker="B") is None
+    assert q.status(tid)["status"] == "DONE"
+
+
+def test_lease_expiry_counts_as_attempt(q):
+    """A task that kills its worker every time ends FAILED after max_retries redeliveries."""
+    tid = q.send("t.x", max_retries=2)
+    seen = []
+    for _ in range(5):
+        got = q.lease("w", 10, visibility_timeout=0.02)
+        seen.append(len(got))
+        time.sleep(0.04)
+    assert seen[:3] == [1, 1, 1] and seen[3:] == [0, 0]
+    st = q.status(tid)
+    assert st["status"] == "FAILED" and "lease expired" in st["error"]
+
+
+def test_heartbeat_extends_long_batch(tmp_path):
+    """A batch running past the visibility timeout keeps its lease (worker heartbeat)."""
+    app = TaskApp("t", queue=DurableQueue(url=f"sqlite:///{tmp_path}/hb.db"))
+    steals = []
+
+    @app.task()
+    def slow(x):
+        time.sleep(0.5)
+        steals.extend(app.queue.lease("thief", 10, 30))
+        return x
+
+    tid = slow.delay(3).id
+    w = Worker(app, batch=4, visibility_timeout=0.15, poll_interval=0.01, name="w1")
+    assert w.run_once() == 1
+    assert steals == []
+    assert app.queue.status(tid)["status"] == "DONE"
+
+
 def test_retry_countdown_and_max_retries(q):
     tid = q.send("t.x", max_retries=2)
     q.lease("w", 1, 30)

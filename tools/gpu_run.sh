@@ -1,0 +1,62 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-session scratch scripts).
+#
+#   gpurun --timeout 1200 -- bash tools/gpu_run.sh <tag> <stage> [<stage> ...]
+#
+# Stages (run in order, each under its own time limit; the first failure ends the call):
+#   tests        pytest -m gpu (one process, per-test timeout)
+#   tests:<expr> pytest -m gpu -k <expr>
+#   smoke        __graft_entry__.smoke()
+#   bench        bench.py defaults (N=1)
+#   bench50      bench.py --steps 50
+#   configs      tools/baseline_configs.py (every BASELINE config)
+#   latency      tools/serve_latency.py
+#   prof         rocprofv3 --kernel-trace --stats of a short bench
+#   pmc          two PMC passes over a short bench
+#   py:<script>  python <script> (extra args via FDX_PY_ARGS)
+# Output lands in gpurun_out/<tag>/.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+TAG=$1; shift
+OUT=$GRAFT_REPO_ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+R=$GRAFT_REPO_ROOT
+
+step() {  # name, seconds, command...
+  local name=$1 secs=$2; shift 2
+  echo "[gpu_run] $name: $*"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[gpu_run] $name rc=$rc"
+  if [ $rc -ne 0 ]; then
+    tail -40 "$OUT/$name.log"
+    exit $rc
+  fi
+  grep -h '^{' "$OUT/$name.log" | cut -c 1-600 || true
+}
+
+for st in "$@"; do
+  case "$st" in
+    tests) step tests 1000 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread ;;
+    tests:*) step tests_k 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -k "${st#tests:}" ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) step bench 600 python bench.py ;;
+    bench50) step bench50 600 python bench.py --steps 50 --warmup 5 ;;
+    configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;
+    latency) step latency 600 python tools/serve_latency.py --json "$OUT/latency.json" ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp
+      step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-extras
+      cd "$R" ;;
+    pmc)
+      cd /tmp && export TMPDIR=/tmp
+      step pmc_a 120 rocprofv3 --pmc FETCH_SIZE SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/pmc_a" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-extras
+      step pmc_b 120 rocprofv3 --pmc WRITE_SIZE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_b" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-extras
+      cd "$R" ;;
+    py:*) # shellcheck disable=SC2086
+      s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
+    *) echo "unknown stage $st"; exit 2 ;;
+  esac
+done
+echo "[gpu_run] all stages ok"
