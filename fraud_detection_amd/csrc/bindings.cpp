@@ -156,11 +156,21 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
 
   // kernelshap
-  m.def("kernelshap", [](u X, int E, int d, u a, float bias, u bg, u cb, int nbg, u Z, int nS, int S_pad, u A, u Az,
-                         int link, u phi, u fx, u f0, u s, u stamps) {
+  m.def("kernelshap", [](u X, int E, int d, u a, float bias, u bg, u cb, int nbg, u Z, int nS, int S_pad, int parts,
+                         u A, u Az, int link, u phi, u fx, u f0, u ws, u cnt, u s, u stamps) {
     fdx::launch_kernelshap(P<const float>(X), E, d, P<const float>(a), bias, P<const float>(bg), P<const float>(cb),
-                           nbg, P<const uint16_t>(Z), nS, S_pad, P<const float>(A), P<const float>(Az), link,
-                           P<float>(phi), P<float>(fx), P<float>(f0), S(s), P<unsigned long long>(stamps));
+                           nbg, P<const uint16_t>(Z), nS, S_pad, parts, P<const float>(A), P<const float>(Az), link,
+                           P<float>(phi), P<float>(fx), P<float>(f0), P<float>(ws), P<unsigned>(cnt), S(s),
+                           P<unsigned long long>(stamps));
+  });
+  m.def("kernelshap_linear_resident", [](int S_pad, int parts) { return fdx::kernelshap_linear_resident(S_pad, parts); });
+  m.def("kernelshap_tree", [](u Xs, int ldx, int E, int d, u feat, u thr, u leaf, int T, int depth, float base, u bw,
+                              int bw_ld, int nbg, u Zm, int nS, int S_pad, int parts, u A, u Az, int link, u phi,
+                              u fx, u f0, u ws, u cnt, u s) {
+    fdx::launch_kernelshap_tree(P<const float>(Xs), ldx, E, d, P<const int>(feat), P<const float>(thr),
+                                P<const float>(leaf), T, depth, base, P<const uint32_t>(bw), bw_ld, nbg,
+                                P<const uint32_t>(Zm), nS, S_pad, parts, P<const float>(A), P<const float>(Az), link,
+                                P<float>(phi), P<float>(fx), P<float>(f0), P<float>(ws), P<unsigned>(cnt), S(s));
   });
 
   // gbdt (K11)

@@ -22,6 +22,7 @@ constexpr int kLabelCol = 31;    // label column in training buffers
 
 typedef short bf16x8_t __attribute__((ext_vector_type(8)));
 typedef short bf16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));

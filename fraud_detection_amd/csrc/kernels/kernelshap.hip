@@ -1,19 +1,38 @@
-// K7 kernelshap_coalition_gemm: batched KernelSHAP for the (scaler-folded) logistic model.
+// K7 KernelSHAP on MI355X: batched coalition evaluation + efficiency-constrained WLS projection.
 //
-// Reference: shap.KernelExplainer semantics (BASELINE.json config 4),
-// the north-star "coalition-masked batched GEMM" XAI path.  Host side (models/explainers.py):
-// coalition design Z [S][M] and the efficiency-constrained WLS operator A [M-1][S] (solved once).
+// Reference: shap.KernelExplainer semantics (BASELINE.json config 4), the
+// north-star "coalition-masked batched GEMM" XAI path the async worker runs
+// (reference xai_tasks.py:103-115, api/worker.py:53-75).  Host side (models/explainers.py): the
+// coalition design Z [S][M] and the WLS operator A [M-1][S] are built once per design.
 //
-// Per explanation e (one workgroup):
-//   logit(z_s, b) = sum_k z_sk u_bk + c_b,   u_b = a * x_e - W_b,   W_b = a * B_b,   c_b = a . B_b + bias
-// is a (n_bg x 32) x (32 x S) product.  The background intercepts are folded in as K column 31
-// (Z[:,31] = 1, U[:,31] = c_b), so the accumulator IS the logit.  v_mfma_f32_32x32x16_bf16 with
-// the background row on the M axis and the coalition on the N axis: Z is exactly representable
-// in bf16 and u is split into hi + lo bf16 halves (two MFMAs, ~16 mantissa bits per product,
-// fp32 accumulation).  The epilogue applies the link (sigmoid for probability space), sums the
-// 16 accumulator rows of each lane plus the partner half-wave, i.e. the mean over background
-// rows, into LDS f[s].  Then y = link(f) - link(f0) and phi_{<M} = A y - (A z_M) delta,
-// phi_M = delta - sum(phi_{<M}), delta = link(f(x)) - link(f0).
+// Work decomposition (both model families): workgroup (e, p) = explanation e, coalition part p of
+// P.  A part evaluates f(z_s) for its coalition tiles, forms y_s = link(f_s) - link(f0) in LDS and
+// projects it, acc_i = sum_{s in part} A[i][s] y_s.  P = 1 finishes in place; P > 1 writes the
+// partial to a workspace and the LAST part to arrive (device-scope counter) sums the partials in
+// part order -- deterministic -- and finishes: phi_{<M} = acc - (A z_M) delta,
+// phi_M = delta - sum(phi_{<M}), delta = link(f(x)) - link(f0).  P is chosen on the host so that
+// E x P workgroups fill the 256 CUs in whole dispatch rounds (ops/kernelshap.py).
+//
+// Linear model (kernelshap_linear_kernel): the coalition logits are linear in z,
+//   logit(z_s, b) = sum_k z_sk u_bk + c_b,   u_b = a * x_e - W_b,   W_b = a * B_b,
+// a (n_bg x 32) x (32 x S) product per explanation.  v_mfma_f32_32x32x16_bf16 with the background
+// row on M and the coalition on N; Z is exact in bf16, u is split into hi + lo bf16 halves (two
+// MFMAs, ~16 mantissa bits per product, fp32 accumulation) and the background intercepts ride in
+// K column 31 (Z[:,31] = 1, U[:,31] = c_b).  The U fragments of an explanation are built ONCE per
+// workgroup into LDS (conflict-free 16 B per lane) instead of per wave in registers: 4x less build
+// work and ~60 fewer VGPRs, so all 1000 workgroups of a 1k-explanation batch are resident in one
+// dispatch round.  Sigmoid epilogue: u is pre-scaled by -log2(e) so sigma = 1 / (1 + exp2(acc)),
+// and two background rows share one reciprocal, 1/d0 + 1/d1 = (d0 + d1) / (d0 d1): per pair one
+// v_exp_f32 + 1/2 v_rcp_f32 instead of one of each (the phase is VALU-issue bound).  exp2 overflow
+// (logit < -88) turns a pair into NaN; that tile is re-summed per element (rcp(inf) = 0).
+//
+// Tree ensemble (kernelshap_tree_kernel, model-agnostic path for the GBDT family): the model is
+// evaluated on the masked rows z * x + (1 - z) * B_b without materialising them.  Per tree t the
+// host precomputes bw[t][b] = nodes where background row b goes right; the kernel computes
+// xw[t] for x and, per (coalition, tree), Zt = the z-bit of each node's feature.  The effective
+// direction bits are then ONE bitfield insert, R = (Zt & xw) | (~Zt & bw), and the walk is 2 VALU
+// ops per level on a 1-based heap.  xw / bw are wave-uniform (a wave holds 64 coalitions x one
+// background row), leaves sit in LDS.
 //
 // MFMA operand maps (cdna_hip_programming.md §3): lane l (r = l & 31, h = l >> 5) supplies
 // A[row r][k = 8h + j] and B[k = 8h + j][col r], j = 0..7 -> both are 16 contiguous bytes of a
@@ -26,13 +45,15 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kWaves = 4;
-constexpr int kMaxBg = 128;     // 4 background tiles of 32
-constexpr int kMaxS = 4096;     // coalitions per design (LDS f[] capacity)
+constexpr int kMaxBg = 128;      // 4 background tiles of 32
+constexpr int kMaxS = 4096;      // coalitions per design
+constexpr int kMaxParts = 8;
+constexpr float kNullAcc = 70.0f;     // exact in bf16; sigma = 1 / (1 + 2^70)
+constexpr int kTreeLdsLeaves = 8192;  // leaves (floats) staged in LDS by the tree kernel
+constexpr int kMaxTrees = 2048;
 
 __device__ __forceinline__ short bf16_bits(float f) { return (short)f32_to_bf16(f); }
 
-// link: 0 = identity on probabilities (shap default), 1 = logit of the mean probability,
-//       2 = model log-odds (mean of logits; KernelSHAP == LinearSHAP exactly)
 // STAMP (tools/kernelshap_stamps.py): s_memtime of thread 0 at the phase boundaries -> stamps[e][8]
 #define FDX_STAMP(i)                                                                              \
   do {                                                                                            \
@@ -45,129 +66,45 @@ __device__ __forceinline__ short bf16_bits(float f) { return (short)f32_to_bf16(
     }                                                                                             \
   } while (0)
 
-template <bool STAMP = false>
-__global__ __launch_bounds__(kThreads) void kernelshap_kernel(
-    const float* __restrict__ X, int n_expl, int d, const float* __restrict__ a, float bias,
-    const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
-    const uint16_t* __restrict__ Z, int S, int S_pad, const float* __restrict__ Amat,
-    const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
-    float* __restrict__ f0_out, unsigned long long* __restrict__ stamps = nullptr) {
-  unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  FDX_STAMP(0);
-  __shared__ __attribute__((aligned(16))) float f[kMaxS];
-  __shared__ float xs[32];
-  __shared__ float red[8];
-  const int e = blockIdx.x;
-  const int lane = lane_id(), wv = wave_id();
-  const int r = lane & 31, h = lane >> 5;
-  // v = a o x (col 31: 0); u_b = v - W_b with W = [a o B_b, 0.., -c_b] precomputed per design
-  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? a[threadIdx.x] * X[(int64_t)e * d + threadIdx.x] : 0.0f;
-  __syncthreads();
-  const int ntb = (n_bg + 31) >> 5;  // background tiles in use (uniform)
-  // sigmoid links: u is pre-scaled by -log2(e), so the accumulator is -z log2(e) and
-  // sigma(z) = 1 / (1 + exp2(acc)) needs no multiply per element
-  const float us = link == 2 ? 1.0f : -1.4426950408889634f;
-  // U fragments (hi / lo) for every background tile and both k-steps: 16 regs x 4 tiles; each
-  // lane's 8 W values of a (tile, k-step) are two contiguous float4 loads
-  bf16x8_t uhi[4][2], ulo[4][2];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int b = 32 * t + r;
-    const bool okb = b < n_bg && t < ntb;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int k0 = 16 * ks + 8 * h;
-      float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
-      if (okb) {
-        const float4* wr = reinterpret_cast<const float4*>(Bg + (int64_t)b * kCols + k0);
-        w0 = wr[0];
-        w1 = wr[1];
-      }
-      const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float u = okb ? (xs[k0 + j] - wv8[j]) * us : 0.0f;
-        const short hi = bf16_bits(u);
-        const float hif = __uint_as_float(((uint32_t)(uint16_t)hi) << 16);
-        uhi[t][ks][j] = hi;
-        ulo[t][ks][j] = bf16_bits(u - hif);
-      }
-    }
-  }
-  FDX_STAMP(1);
-  const float inv_nb = 1.0f / (float)n_bg;
-  const int nst = S_pad / 32;
-  for (int st = wv; st < nst; st += kWaves) {
-    const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
-    const uint4 z0 = zr[h], z1 = zr[2 + h];  // k-step 0: cols 8h..8h+7; k-step 1: 16+8h..
-    bf16x8_t zb[2];
-    zb[0] = __builtin_bit_cast(bf16x8_t, z0);
-    zb[1] = __builtin_bit_cast(bf16x8_t, z1);
-    float fs = 0.0f;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t >= ntb) break;  // uniform
-      f32x16_t acc = {};
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uhi[t][0], zb[0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ulo[t][0], zb[0], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uhi[t][1], zb[1], acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ulo[t][1], zb[1], acc, 0, 0, 0);
-      if (t < ntb - 1 || (n_bg & 31) == 0) {  // full tile (uniform)
-#pragma unroll
-        for (int i = 0; i < 16; ++i)
-          fs += link == 2 ? acc[i] : fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
-      } else {  // partial last tile: rows past n_bg are skipped (whole-wave skips for i >= 4 at n_bg = 100)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          if (32 * t + (i & 3) + 8 * (i >> 2) + 4 * h < n_bg)
-            fs += link == 2 ? acc[i] : fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
-        }
-      }
-    }
-    fs += __shfl_xor(fs, 32, kWave);
-    if (h == 0) f[32 * st + r] = fs * inv_nb;
-  }
-  FDX_STAMP(2);
-  // f0 (background mean output) and f(x)
-  float z0s = 0.0f;
-  for (int b = threadIdx.x; b < n_bg; b += kThreads) z0s += link == 2 ? cb[b] : fast_sigmoid(cb[b]);
-  z0s = wave_sum(z0s);
-  if (lane == 0) red[wv] = z0s;
-  float zx = 0.0f;
-  if (threadIdx.x < 32) zx = xs[threadIdx.x];  // a o x
-  zx = wave_sum(zx);
-  if (threadIdx.x == 0) red[4] = zx;
-  __syncthreads();
-  FDX_STAMP(3);
-  const float f0m = (red[0] + red[1] + red[2] + red[3]) * inv_nb;
-  const float logit_x = red[4] + bias;
-  float f0l, fxl;
-  if (link == 2) { f0l = f0m; fxl = logit_x; }
-  else if (link == 1) {
+// link: 0 = identity on probabilities (shap default), 1 = logit of the mean probability,
+//       2 = model log-odds (mean of logits; for the linear model KernelSHAP == LinearSHAP exactly)
+__device__ __forceinline__ void link_pair(int link, float f0m, float logit_x, float& f0l, float& fxl) {
+  if (link == 2) {
+    f0l = f0m;
+    fxl = logit_x;
+  } else if (link == 1) {
     const float p0 = fminf(fmaxf(f0m, 1e-12f), 1.0f - 1e-7f);
     f0l = __logf(p0 / (1.0f - p0));
     fxl = logit_x;
-  } else { f0l = f0m; fxl = fast_sigmoid(logit_x); }
-  const float delta = fxl - f0l;
-  for (int s = threadIdx.x; s < S_pad; s += kThreads) {
-    float v = f[s];
+  } else {
+    f0l = f0m;
+    fxl = fast_sigmoid(logit_x);
+  }
+}
+
+// y_s = link(f_s) - f0l over the part's coalitions (in place in LDS), padded coalitions -> 0.
+__device__ __forceinline__ void form_y(float* ys, int s0, int ns, int S, int link, float f0l) {
+  for (int s = threadIdx.x; s < ns; s += kThreads) {
+    float v = ys[s];
     if (link == 1) {
       v = fminf(fmaxf(v, 1e-12f), 1.0f - 1e-7f);
       v = __logf(v / (1.0f - v));
     }
-    f[s] = s < S ? v - f0l : 0.0f;  // padded coalitions contribute nothing (A is zero there too)
+    ys[s] = s0 + s < S ? v - f0l : 0.0f;  // A is zero-padded there too
   }
-  __syncthreads();
-  FDX_STAMP(4);
-  // phi_i = sum_s A[i][s] y_s - Az[i] delta, i < d-1: 8 threads per output, float4 steps of the
-  // (S_pad-strided, zero-padded) A row, 4 independent accumulators (4 loads in flight)
+}
+
+// Partial projection acc_i = sum_{s < ns} A[i][s0 + s] y_s for i < d-1 into ph[i]: 8 threads per
+// output, float4 steps of the (S_pad-strided, zero-padded) A row, 4 independent accumulators.
+__device__ __forceinline__ void project_part(const float* ys, int s0, int ns, const float* __restrict__ Amat,
+                                             int S_pad, int d, float* ph) {
   const int i = threadIdx.x >> 3, part = threadIdx.x & 7;
   float acc = 0.0f;
   if (i < d - 1) {
-    const float4* Ai = reinterpret_cast<const float4*>(Amat + (int64_t)i * S_pad);
-    const float4* fv = reinterpret_cast<const float4*>(f);
+    const float4* Ai = reinterpret_cast<const float4*>(Amat + (int64_t)i * S_pad + s0);
+    const float4* fv = reinterpret_cast<const float4*>(ys);
     float a4[4] = {0.f, 0.f, 0.f, 0.f};
-    const int nq = S_pad >> 2;  // float4 columns; S_pad % 32 == 0 -> nq % 8 == 0
+    const int nq = ns >> 2;  // ns % 32 == 0 -> nq % 8 == 0
     int q = part;
     for (; q + 24 < nq; q += 32) {
 #pragma unroll
@@ -183,10 +120,43 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
     acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
   }
   acc = group_sum<8>(acc);
-  __shared__ float ph[32];
-  if (part == 0 && i < d - 1) ph[i] = acc - Az[i] * delta;
+  if (part == 0 && i < d - 1) ph[i] = acc;
+}
+
+// Finish explanation e from its part's projection ph (LDS).  P > 1: publish the partial, the last
+// part to arrive sums all partials in part order.  Returns after the phi row is written (or not,
+// for a part that is not last).
+__device__ __forceinline__ void finish(int e, int p, int P, int d, float* ph, const float* __restrict__ Az,
+                                       float delta, float fxl, float f0l, float* __restrict__ phi,
+                                       float* __restrict__ fx_out, float* __restrict__ f0_out,
+                                       float* __restrict__ ws, unsigned* __restrict__ cnt, int* flag) {
   __syncthreads();
-  FDX_STAMP(5);
+  if (P > 1) {
+    if (threadIdx.x < d - 1) {
+      ws[((int64_t)e * kMaxParts + p) * 32 + threadIdx.x] = ph[threadIdx.x];
+      __threadfence();  // each writer publishes its partial device-wide before the arrival counts
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = atomicAdd(cnt + e, 1u);
+      const bool last = old == (unsigned)(P - 1);
+      if (last) cnt[e] = 0u;  // self-cleaning for the next launch (no other part touches it now)
+      *flag = last ? 1 : 0;
+      __threadfence();
+    }
+    __syncthreads();
+    if (*flag == 0) return;
+    if (threadIdx.x < d - 1) {
+      float s = 0.0f;
+      for (int q = 0; q < P; ++q)  // fixed part order: deterministic
+        s += __hip_atomic_load(ws + ((int64_t)e * kMaxParts + q) * 32 + threadIdx.x, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      ph[threadIdx.x] = s;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < d - 1) ph[threadIdx.x] -= Az[threadIdx.x] * delta;
+  __syncthreads();
   if (threadIdx.x == 0) {
     float sum = 0.0f;
     for (int k = 0; k < d - 1; ++k) sum += ph[k];
@@ -196,34 +166,358 @@ __global__ __launch_bounds__(kThreads) void kernelshap_kernel(
   }
   __syncthreads();
   if (threadIdx.x < d) phi[(int64_t)e * d + threadIdx.x] = ph[threadIdx.x];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Linear model
+// ------------------------------------------------------------------------------------------------
+template <int NTB, bool LOGITS, bool STAMP>
+__global__ __launch_bounds__(kThreads) void kernelshap_linear_kernel(
+    const float* __restrict__ X, int d, const float* __restrict__ a, float bias,
+    const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
+    const uint16_t* __restrict__ Z, int S, int S_pad, int P, const float* __restrict__ Amat,
+    const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
+    float* __restrict__ f0_out, float* __restrict__ ws, unsigned* __restrict__ cnt,
+    unsigned long long* __restrict__ stamps) {
+  unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  FDX_STAMP(0);
+  extern __shared__ __attribute__((aligned(16))) float ys[];  // this part's coalitions
+  __shared__ uint4 Uhi[4 * 2 * 2 * 32], Ulo[4 * 2 * 2 * 32];  // [tile][kstep][half][row]
+  __shared__ float xs[32];
+  __shared__ float red[8];
+  __shared__ float ph[32];
+  __shared__ int flag;
+  const int e = blockIdx.x / P, p = blockIdx.x - e * P;
+  const int lane = lane_id(), wv = wave_id();
+  const int r = lane & 31, h = lane >> 5;
+  const int nst = S_pad >> 5;
+  const int st0 = (p * nst) / P, st1 = ((p + 1) * nst) / P;
+  // v = a o x (col 31: 0); u_b = v - W_b with W = [a o B_b, 0.., -c_b] precomputed per design
+  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? a[threadIdx.x] * X[(int64_t)e * d + threadIdx.x] : 0.0f;
+  __syncthreads();
+  // sigmoid links: u is pre-scaled by -log2(e), so the accumulator is -z log2(e)
+  const float us = LOGITS ? 1.0f : -1.4426950408889634f;
+  // cooperative U build: entry q = ((t * 2 + ks) * 2 + hh) * 32 + rr holds the 8 bf16 values lane
+  // (rr, hh) feeds for background tile t, k-step ks (two entries per thread)
+  for (int q = threadIdx.x; q < 512; q += kThreads) {
+    const int rr = q & 31, hh = (q >> 5) & 1, ks = (q >> 6) & 1, t = q >> 7;
+    const int b = 32 * t + rr, k0 = 16 * ks + 8 * hh;
+    float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
+    const bool okb = b < n_bg;
+    if (okb) {
+      const float4* wr = reinterpret_cast<const float4*>(Bg + (int64_t)b * kCols + k0);
+      w0 = wr[0];
+      w1 = wr[1];
+    }
+    const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      float uu[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj) {
+        // rows past n_bg are NULL rows: u = 0 except the intercept column, where the sigmoid
+        // links get acc = kNullAcc (2^-70 ~ 0 after the sigmoid, finite in the paired
+        // reciprocal) and the logit link gets 0 -- every background tile is then a full tile
+        const bool icpt = k0 + j + jj == kCols - 1;
+        uu[jj] = okb ? (xs[k0 + j + jj] - wv8[j + jj]) * us : (!LOGITS && icpt ? kNullAcc : 0.0f);
+      }
+      const uint16_t h0 = f32_to_bf16(uu[0]), h1 = f32_to_bf16(uu[1]);
+      const float r0 = uu[0] - __uint_as_float(((uint32_t)h0) << 16);
+      const float r1 = uu[1] - __uint_as_float(((uint32_t)h1) << 16);
+      hw[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      lw[j >> 1] = pack_bf16x2(r0, r1);
+    }
+    Uhi[q] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    Ulo[q] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  }
+  __syncthreads();
+  FDX_STAMP(1);
+  const float inv_nb = 1.0f / (float)n_bg;
+  for (int st = st0 + wv; st < st1; st += kWaves) {
+    const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
+    const bf16x8_t zb0 = __builtin_bit_cast(bf16x8_t, zr[h]), zb1 = __builtin_bit_cast(bf16x8_t, zr[2 + h]);
+    auto mfma_tile = [&](int t) {
+      const int q0 = (t * 2 + 0) * 64 + h * 32 + r, q1 = (t * 2 + 1) * 64 + h * 32 + r;
+      const bf16x8_t uh0 = __builtin_bit_cast(bf16x8_t, Uhi[q0]), ul0 = __builtin_bit_cast(bf16x8_t, Ulo[q0]);
+      const bf16x8_t uh1 = __builtin_bit_cast(bf16x8_t, Uhi[q1]), ul1 = __builtin_bit_cast(bf16x8_t, Ulo[q1]);
+      f32x16_t acc = {};
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh0, zb0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul0, zb0, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh1, zb1, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul1, zb1, acc, 0, 0, 0);
+      return acc;
+    };
+    auto epilogue = [&](const f32x16_t& acc) {
+      if constexpr (LOGITS) {
+        float ts = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) ts += acc[i];
+        return ts;
+      } else {
+        // 4 background rows per step in packed f32: rows (i, i+2) and (i+1, i+3) pair up so
+        // that the sums d0 + d1 and products d0 d1 of both pairs are one v_pk_add / v_pk_mul
+        f32x2_t ts2 = {0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+          const f32x2_t e02 = {__builtin_amdgcn_exp2f(acc[i]), __builtin_amdgcn_exp2f(acc[i + 2])};
+          const f32x2_t e13 = {__builtin_amdgcn_exp2f(acc[i + 1]), __builtin_amdgcn_exp2f(acc[i + 3])};
+          const f32x2_t d02 = e02 + 1.0f, d13 = e13 + 1.0f;
+          const f32x2_t pr = d02 * d13;
+          const f32x2_t rc = {fast_rcp(pr.x), fast_rcp(pr.y)};
+          ts2 = __builtin_elementwise_fma(d02 + d13, rc, ts2);
+        }
+        float ts = ts2.x + ts2.y;
+        if (__builtin_isnan(ts)) {  // exp2 overflow (logit < -88) in this lane: per-element form
+          ts = 0.0f;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) ts += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
+        }
+        return ts;
+      }
+    };
+    // double-buffered: the MFMA chain of tile t+1 is issued before the epilogue of tile t, so
+    // the matrix core works under the (VALU-bound) epilogue
+    float fs = 0.0f;
+    f32x16_t cur = mfma_tile(0);
+#pragma unroll
+    for (int t = 0; t < NTB; ++t) {
+      f32x16_t nxt = {};
+      if (t + 1 < NTB) nxt = mfma_tile(t + 1);
+      fs += epilogue(cur);
+      cur = nxt;
+    }
+    fs += __shfl_xor(fs, 32, kWave);
+    if (h == 0) ys[32 * (st - st0) + r] = fs * inv_nb;
+  }
+  FDX_STAMP(2);
+  // f0 (background mean output) and f(x)
+  float z0s = 0.0f;
+  for (int b = threadIdx.x; b < n_bg; b += kThreads) z0s += LOGITS ? cb[b] : fast_sigmoid(cb[b]);
+  z0s = wave_sum(z0s);
+  if (lane == 0) red[wv] = z0s;
+  float zx = 0.0f;
+  if (threadIdx.x < 32) zx = xs[threadIdx.x];  // a o x
+  zx = wave_sum(zx);
+  if (threadIdx.x == 0) red[4] = zx;
+  __syncthreads();
+  FDX_STAMP(3);
+  float f0l, fxl;
+  link_pair(link, (red[0] + red[1] + red[2] + red[3]) * inv_nb, red[4] + bias, f0l, fxl);
+  const int s0 = 32 * st0, ns = 32 * (st1 - st0);
+  form_y(ys, s0, ns, S, link, f0l);
+  __syncthreads();
+  FDX_STAMP(4);
+  project_part(ys, s0, ns, Amat, S_pad, d, ph);
+  FDX_STAMP(5);
+  finish(e, p, P, d, ph, Az, fxl - f0l, fxl, f0l, phi, fx_out, f0_out, ws, cnt, &flag);
   FDX_STAMP(6);
   if constexpr (STAMP) {
-    if (threadIdx.x == 0) {
+    if (threadIdx.x == 0 && p == 0) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) stamps[(int64_t)e * 8 + k] = tsv[k];
     }
   }
 }
+
+// ------------------------------------------------------------------------------------------------
+// Tree ensemble (depth D <= 5: the 31 internal nodes of a tree fit one 32-bit mask)
+// ------------------------------------------------------------------------------------------------
+// Walk one tree from the effective direction bits R1 (bit n + 1 = node n goes right; heap 1-based)
+template <int D>
+__device__ __forceinline__ int walk(uint32_t R1) {
+  int node = 1;
+#pragma unroll
+  for (int l = 0; l < D; ++l) node = (node << 1) | (int)((R1 >> node) & 1u);
+  return node - (1 << D);  // leaf index
+}
+
+template <int D, bool LOGITS, bool LEAF_LDS>
+__global__ __launch_bounds__(kThreads) void kernelshap_tree_kernel(
+    const float* __restrict__ Xs, int ldx, int d, const int* __restrict__ feat, const float* __restrict__ thr,
+    const float* __restrict__ leaf, int T, float base_margin, const uint32_t* __restrict__ bw, int bw_ld,
+    int n_bg, const uint32_t* __restrict__ Zm, int S, int S_pad, int P, const float* __restrict__ Amat,
+    const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
+    float* __restrict__ f0_out, float* __restrict__ ws, unsigned* __restrict__ cnt) {
+  constexpr int NI = (1 << D) - 1, NL = 1 << D;
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
+  float* ys = dyn;                          // this part's coalitions
+  float* lf = dyn + ((S_pad + 3) & ~3);     // leaves [T][NL] (LEAF_LDS)
+  __shared__ float xs[32];
+  __shared__ uint32_t xw[kMaxTrees];        // x's direction bits per tree, pre-shifted (bit n + 1)
+  __shared__ float red[8];
+  __shared__ float ph[32];
+  __shared__ int flag;
+  const int e = blockIdx.x / P, p = blockIdx.x - e * P;
+  const int lane = lane_id(), wv = wave_id();
+  const int nst = S_pad >> 5;
+  const int st0 = (p * nst) / P, st1 = ((p + 1) * nst) / P;
+  const int s0 = 32 * st0, ns = 32 * (st1 - st0);
+  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? Xs[(int64_t)e * ldx + threadIdx.x] : 0.0f;
+  if constexpr (LEAF_LDS) {
+    for (int i = threadIdx.x; i < T * NL; i += kThreads) lf[i] = leaf[i];
+  }
+  __syncthreads();
+  for (int t = threadIdx.x; t < T; t += kThreads) {
+    uint32_t m = 0;
+    for (int n = 0; n < NI; ++n) {
+      const int f = feat[t * NI + n];
+      if (f >= 0 && !(xs[f] < thr[t * NI + n])) m |= 2u << n;
+    }
+    xw[t] = m;
+  }
+  __syncthreads();
+  const float* LF = LEAF_LDS ? lf : leaf;
+  const float inv_nb = 1.0f / (float)n_bg;
+  // one coalition per lane, 32 background rows per pass (wave-uniform b -> uniform bw / xw loads)
+  for (int s = s0 + threadIdx.x; s < s0 + ns; s += kThreads) {
+    const uint32_t zmask = Zm[s];
+    float fs = 0.0f;
+    for (int b0 = 0; b0 < n_bg; b0 += 32) {
+      const int nb = min(32, n_bg - b0);  // uniform
+      float mg[32];
+#pragma unroll
+      for (int j = 0; j < 32; ++j) mg[j] = base_margin;
+      for (int t = 0; t < T; ++t) {
+        const int* ft = feat + t * NI;
+        uint32_t Zt = 0;
+#pragma unroll
+        for (int n = 0; n < NI; ++n) {
+          const int f = max(ft[n], 0);  // uniform address: scalar load
+          Zt |= ((zmask >> f) & 1u) << (n + 1);
+        }
+        const uint32_t xt = __builtin_amdgcn_readfirstlane(xw[t]);
+        const uint32_t* bt = bw + (int64_t)t * bw_ld + b0;
+        const float* lt = LF + t * NL;
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+          if (j < nb) {
+            const uint32_t R1 = (Zt & xt) | (~Zt & bt[j]);
+            mg[j] += lt[walk<D>(R1)];
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 32; ++j)
+        if (j < nb) fs += LOGITS ? mg[j] : fast_sigmoid(mg[j]);
+    }
+    ys[s - s0] = fs * inv_nb;
+  }
+  // f0 = mean_b link(model(B_b)) and f(x): the same walks with Zt = 0 / all ones
+  float z0s = 0.0f;
+  for (int b = threadIdx.x; b < n_bg; b += kThreads) {
+    float m = base_margin;
+    for (int t = 0; t < T; ++t) m += LF[t * NL + walk<D>(bw[(int64_t)t * bw_ld + b])];
+    z0s += LOGITS ? m : fast_sigmoid(m);
+  }
+  z0s = wave_sum(z0s);
+  if (lane == 0) red[wv] = z0s;
+  if (threadIdx.x == 0) {
+    float m = base_margin;
+    for (int t = 0; t < T; ++t) m += LF[t * NL + walk<D>(xw[t])];
+    red[4] = m;
+  }
+  __syncthreads();
+  float f0l, fxl;
+  link_pair(link, (red[0] + red[1] + red[2] + red[3]) * inv_nb, red[4], f0l, fxl);
+  form_y(ys, s0, ns, S, link, f0l);
+  __syncthreads();
+  project_part(ys, s0, ns, Amat, S_pad, d, ph);
+  finish(e, p, P, d, ph, Az, fxl - f0l, fxl, f0l, phi, fx_out, f0_out, ws, cnt, &flag);
+}
+
 #undef FDX_STAMP
+
+void check_design(int d, int S, int S_pad, int P) {
+  if (d < 2 || d > 30) throw std::runtime_error("kernelshap: 2 <= d <= 30");
+  if (S < 1 || S_pad % 32 != 0 || S_pad < S || S_pad > kMaxS)
+    throw std::runtime_error("kernelshap: S_pad must be a multiple of 32 in [S, 4096]");
+  if (P < 1 || P > kMaxParts || P > S_pad / 32) throw std::runtime_error("kernelshap: 1 <= parts <= 8 and <= S_pad/32");
+}
+
+size_t part_lds(int S_pad, int P) { return (size_t)(((S_pad / 32 + P - 1) / P) * 32) * sizeof(float); }
 
 }  // namespace
 
+int kernelshap_linear_resident(int S_pad, int P) {
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernelshap_linear_kernel<4, false, false>, kThreads,
+                                                   part_lds(S_pad, P)) != hipSuccess || occ < 1)
+    occ = 1;
+  return occ * device_cu_count();
+}
+
 void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
-                       const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
-                       const float* Az, int link, float* phi, float* fx_out, float* f0_out,
-                       hipStream_t stream, unsigned long long* stamps) {
-  if (d < 2 || d > 30) throw std::runtime_error("kernelshap: 2 <= d <= 30");
+                       const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, int parts,
+                       const float* Amat, const float* Az, int link, float* phi, float* fx_out, float* f0_out,
+                       float* ws, unsigned* cnt, hipStream_t stream, unsigned long long* stamps) {
+  check_design(d, S, S_pad, parts);
   if (n_bg < 1 || n_bg > kMaxBg) throw std::runtime_error("kernelshap: 1 <= n_bg <= 128");
-  if (S < 1 || S_pad % 32 != 0 || S_pad < S || S_pad > kMaxS)
-    throw std::runtime_error("kernelshap: S_pad must be a multiple of 32 in [S, 4096]");
+  if (parts > 1 && (ws == nullptr || cnt == nullptr)) throw std::runtime_error("kernelshap: parts > 1 needs ws/cnt");
   if (n_expl <= 0) return;
-  if (stamps != nullptr)
-    kernelshap_kernel<true><<<n_expl, kThreads, 0, stream>>>(X, n_expl, d, a, bias, bg, cb, n_bg, Z, S, S_pad, Amat,
-                                                             Az, link, phi, fx_out, f0_out, stamps);
-  else
-    kernelshap_kernel<false><<<n_expl, kThreads, 0, stream>>>(X, n_expl, d, a, bias, bg, cb, n_bg, Z, S, S_pad, Amat,
-                                                              Az, link, phi, fx_out, f0_out);
+  const dim3 grid((unsigned)((int64_t)n_expl * parts));
+  const size_t lds = part_lds(S_pad, parts);
+#define FDX_KS(NT, LG, ST)                                                                             \
+  kernelshap_linear_kernel<NT, LG, ST><<<grid, kThreads, lds, stream>>>(X, d, a, bias, bg, cb, n_bg, Z, S, \
+                                                                        S_pad, parts, Amat, Az, link, phi,  \
+                                                                        fx_out, f0_out, ws, cnt, stamps)
+#define FDX_KS_NT(LG, ST)                     \
+  do {                                        \
+    switch ((n_bg + 31) >> 5) {               \
+      case 1: FDX_KS(1, LG, ST); break;       \
+      case 2: FDX_KS(2, LG, ST); break;       \
+      case 3: FDX_KS(3, LG, ST); break;       \
+      default: FDX_KS(4, LG, ST); break;      \
+    }                                         \
+  } while (0)
+  const bool logits = link == 2;
+  if (stamps != nullptr) {
+    if (logits) FDX_KS_NT(true, true); else FDX_KS_NT(false, true);
+  } else {
+    if (logits) FDX_KS_NT(true, false); else FDX_KS_NT(false, false);
+  }
+#undef FDX_KS_NT
+#undef FDX_KS
   check_launch("kernelshap");
+}
+
+void launch_kernelshap_tree(const float* Xs, int ldx, int n_expl, int d, const int* feat, const float* thr,
+                            const float* leaf, int ntrees, int depth, float base_margin, const uint32_t* bw,
+                            int bw_ld, int n_bg, const uint32_t* Zm, int S, int S_pad, int parts,
+                            const float* Amat, const float* Az, int link, float* phi, float* fx_out,
+                            float* f0_out, float* ws, unsigned* cnt, hipStream_t stream) {
+  check_design(d, S, S_pad, parts);
+  if (depth < 1 || depth > 5) throw std::runtime_error("kernelshap_tree: depth must be in [1, 5]");
+  if (ntrees < 1 || ntrees > kMaxTrees) throw std::runtime_error("kernelshap_tree: 1 <= trees <= 2048");
+  if (n_bg < 1 || bw_ld < n_bg) throw std::runtime_error("kernelshap_tree: bad background");
+  if (parts > 1 && (ws == nullptr || cnt == nullptr)) throw std::runtime_error("kernelshap: parts > 1 needs ws/cnt");
+  if (n_expl <= 0) return;
+  const dim3 grid((unsigned)((int64_t)n_expl * parts));
+  const bool lds_leaves = ntrees * (1 << depth) <= kTreeLdsLeaves;
+  const size_t lds = ((size_t)((S_pad + 3) & ~3) + (lds_leaves ? (size_t)ntrees << depth : 0)) * sizeof(float);
+  const bool logits = link == 2;
+#define FDX_KT(D_, LG, LL)                                                                                 \
+  kernelshap_tree_kernel<D_, LG, LL><<<grid, kThreads, lds, stream>>>(                                     \
+      Xs, ldx, d, feat, thr, leaf, ntrees, base_margin, bw, bw_ld, n_bg, Zm, S, S_pad, parts, Amat, Az, link, \
+      phi, fx_out, f0_out, ws, cnt)
+#define FDX_KT_D(D_)                                              \
+  do {                                                            \
+    if (logits) {                                                 \
+      if (lds_leaves) FDX_KT(D_, true, true); else FDX_KT(D_, true, false);   \
+    } else {                                                      \
+      if (lds_leaves) FDX_KT(D_, false, true); else FDX_KT(D_, false, false); \
+    }                                                             \
+  } while (0)
+  switch (depth) {
+    case 1: FDX_KT_D(1); break;
+    case 2: FDX_KT_D(2); break;
+    case 3: FDX_KT_D(3); break;
+    case 4: FDX_KT_D(4); break;
+    default: FDX_KT_D(5); break;
+  }
+#undef FDX_KT_D
+#undef FDX_KT
+  check_launch("kernelshap_tree");
 }
 
 }  // namespace fdx

@@ -138,11 +138,22 @@ void launch_auc_hist_reduce(const unsigned* hist, int bits, unsigned long long* 
 // X [E][d] raw explanations; a [32] folded weights; bg = W [n_bg][32] = [a o B_b, 0.., -c_b] (the
 // background rows pre-multiplied by the weights, col 31 = minus the background logit); cb [n_bg]
 // background logits; Z [S_pad][32] bf16 coalitions (col 31 = 1); Amat [d-1][S_pad] (zero-padded);
-// Az [d-1].
+// Az [d-1].  parts: coalition parts per explanation (grid = E x parts); parts > 1 needs ws
+// [E][8][32] f32 and cnt [E] u32 (zeroed once; the kernel leaves it zeroed).
 void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
-                       const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, const float* Amat,
-                       const float* Az, int link, float* phi, float* fx_out, float* f0_out,
-                       hipStream_t stream, unsigned long long* stamps = nullptr);
+                       const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, int parts,
+                       const float* Amat, const float* Az, int link, float* phi, float* fx_out, float* f0_out,
+                       float* ws, unsigned* cnt, hipStream_t stream, unsigned long long* stamps = nullptr);
+// workgroups of the linear kernel resident on the device at once (parts -> LDS per workgroup)
+int kernelshap_linear_resident(int S_pad, int parts);
+// Tree-ensemble model (depth <= 5): Xs [E][ldx] standardized rows; feat/thr [T][2^D-1], leaf
+// [T][2^D]; bw [T][bw_ld] direction bits of the background rows (bit n+1 = node n goes right);
+// Zm [S_pad] coalition bitmasks (bit k = feature k taken from x).
+void launch_kernelshap_tree(const float* Xs, int ldx, int n_expl, int d, const int* feat, const float* thr,
+                            const float* leaf, int ntrees, int depth, float base_margin, const uint32_t* bw,
+                            int bw_ld, int n_bg, const uint32_t* Zm, int S, int S_pad, int parts,
+                            const float* Amat, const float* Az, int link, float* phi, float* fx_out,
+                            float* f0_out, float* ws, unsigned* cnt, hipStream_t stream);
 
 // ---- K11 gbdt (gbdt.hip) ----
 void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,

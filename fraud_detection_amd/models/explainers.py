@@ -22,9 +22,19 @@ i.e. one (n_bg x M) x (M x S) GEMM per explanation: on MI355X bf16 MFMA with Z e
 and u split into hi + lo bf16 (fp32-grade products), sigmoid/mean epilogue fused, then A y.
 Identity link on logits (``link="logit_model"``) makes KernelSHAP exactly equal LinearSHAP, which
 is the exact oracle the tests use.
+
+Model-agnostic paths (shap.KernelExplainer takes any model; reference train_model.py:95-113 ships an
+XGBoost model):
+  * ``TreeKernelExplainer`` -- the GBDT family: every masked row z * x + (1 - z) * B_b is walked
+    through the ensemble inside the kernel (kernelshap_tree_kernel), never materialised;
+  * ``FunctionKernelExplainer`` -- any callable on device tensors (e.g. a torch model): masked rows
+    are built in chunks on the device, the model is called on them, and the shared WLS operator
+    projects the coalition values.
+All three share one cached coalition design per (M, nsamples, seed).
 """
 from __future__ import annotations
 
+import functools
 import itertools
 import math
 import time
@@ -109,6 +119,16 @@ def coalition_design(M: int, nsamples: int | None = None, seed: int = 0):
             for i in range(nfixed, len(weights)):
                 weights[i] *= scale
     return np.asarray(rows, np.uint8), np.asarray(weights, np.float64)
+
+
+@functools.lru_cache(maxsize=16)
+def cached_design(M: int, nsamples: int | None = None, seed: int = 0):
+    """(Z, w, A, zM) for a design, solved once per process (read-only arrays)."""
+    Z, w = coalition_design(M, nsamples, seed)
+    A, zM = wls_operator(Z, w)
+    for v in (Z, w, A, zM):
+        v.setflags(write=False)
+    return Z, w, A, zM
 
 
 def wls_operator(Z: np.ndarray, w: np.ndarray):
@@ -199,8 +219,7 @@ class KernelExplainer:
         self.bias = float(bias)
         self.B = B
         self.link = link
-        self.Z, self.w = coalition_design(self.d, nsamples, seed)
-        self.A, self.zM = wls_operator(self.Z, self.w)
+        self.Z, self.w, self.A, self.zM = cached_design(self.d, nsamples or None, seed)
         self.device = torch.device("cuda", 0) if (device == "auto" and torch.cuda.is_available()) else torch.device(
             "cpu" if device == "auto" else device)
         self._dev_cache = None
@@ -220,6 +239,170 @@ class KernelExplainer:
 
             return kernelshap(torch.from_numpy(X).to(self.device), self)
         return kernelshap_reference(X, self.a, self.bias, self.B, self.Z, self.A, self.zM, self.link)
+
+
+def _project(f, f0, fx, A, zM):
+    """Efficiency-constrained WLS projection of coalition values f [E, S] (fp64 numpy)."""
+    y = f - f0
+    delta = fx - f0
+    phi = np.empty((f.shape[0], A.shape[0] + 1))
+    phi[:, :-1] = y @ A.T - np.outer(delta, A @ zM)
+    phi[:, -1] = delta - phi[:, :-1].sum(1)
+    return phi
+
+
+def _standardize(X, mean, scale) -> np.ndarray:
+    """The device scaler's arithmetic ((x - mean32) * inv32 in fp32, ops/reference.scale_cast)."""
+    d = len(mean)
+    m32 = np.asarray(mean, np.float64).astype(np.float32)
+    i32 = (1.0 / np.asarray(scale, np.float64)).astype(np.float32)
+    return ((np.asarray(X, np.float32)[:, :d] - m32[None, :]) * i32[None, :]).astype(np.float32)
+
+
+def tree_direction_bits(Xs: np.ndarray, ens) -> np.ndarray:
+    """uint32 [T, n]: bit n+1 set where row goes right at internal node n (1-based heap; the
+    kernel's convention).  Pass-through nodes (feat -1) go left."""
+    Xs = np.asarray(Xs, np.float32)
+    T, ni = ens.feat.shape
+    if ni > 31:
+        raise ValueError("tree KernelSHAP supports depth <= 5")
+    out = np.zeros((T, Xs.shape[0]), np.uint32)
+    for n in range(ni):
+        f = ens.feat[:, n]
+        v = Xs[:, np.maximum(f, 0)].T                       # [T, n]
+        right = (f[:, None] >= 0) & ~(v < ens.thr[:, n][:, None])
+        out |= right.astype(np.uint32) << np.uint32(n + 1)
+    return out
+
+
+def _margins_from_bits(R1: np.ndarray, ens) -> np.ndarray:
+    """float32 margins (tree order, as the kernel) from direction bits R1 [T, ...]."""
+    D = ens.depth
+    node = np.ones(R1.shape[1:], np.int64)
+    m = np.full(R1.shape[1:], np.float32(ens.base_margin), np.float32)
+    for t in range(R1.shape[0]):
+        node[...] = 1
+        for _ in range(D):
+            node = (node << 1) | ((R1[t] >> node.astype(np.uint32)) & 1).astype(np.int64)
+        m = (m + ens.leaf[t][node - (1 << D)]).astype(np.float32)
+    return m
+
+
+def kernelshap_tree_reference(Xs: np.ndarray, Bs: np.ndarray, ens, Z: np.ndarray, A: np.ndarray, zM: np.ndarray,
+                              link: str = "identity") -> tuple:
+    """fp64 oracle of the tree path on STANDARDIZED rows: f(z) = mean_b link(model(z x + (1-z) B_b))
+    with float32 margins summed in tree order (the kernel's and the predict kernel's order)."""
+    Xs = np.asarray(Xs, np.float32)
+    Bs = np.asarray(Bs, np.float32)
+    bw = tree_direction_bits(Bs, ens)                      # [T, nb]
+    xw = tree_direction_bits(Xs, ens)                      # [T, E]
+    T, ni = ens.feat.shape
+    fidx = np.maximum(ens.feat, 0)
+    zb = Z.astype(bool)
+    # node z-bits per (tree, coalition): Zt[t, s] bit n+1 = z_s[feat[t, n]]
+    Zt = np.zeros((T, Z.shape[0]), np.uint32)
+    for n in range(ni):
+        Zt |= zb[:, fidx[:, n]].T.astype(np.uint32) << np.uint32(n + 1)
+    sig = (lambda v: v.astype(np.float64)) if link == "logit_model" else (lambda v: 1.0 / (1.0 + np.exp(-v.astype(np.float64))))
+    f0 = float(np.mean(sig(_margins_from_bits(bw, ens))))
+    mx = _margins_from_bits(xw, ens).astype(np.float64)
+    fx = mx if link == "logit_model" else 1.0 / (1.0 + np.exp(-mx))
+    f = np.empty((Xs.shape[0], Z.shape[0]))
+    for e in range(Xs.shape[0]):
+        R1 = (Zt[:, :, None] & xw[:, e][:, None, None]) | (~Zt[:, :, None] & bw[:, None, :])  # [T, S, nb]
+        f[e] = sig(_margins_from_bits(R1, ens)).mean(1)
+    if link == "logit":
+        f, f0, fx = _link(f, link), float(_link(np.asarray(f0), link)), _link(fx, link)
+    return _project(f, f0, fx, A, zM), fx, f0
+
+
+class TreeKernelExplainer:
+    """KernelSHAP of a tree ensemble (ops/gbdt.TreeEnsemble trained on standardized rows) over RAW
+    inputs: the model is standardize -> ensemble, as served.  Background: <= 128 raw rows."""
+
+    def __init__(self, ens, mean, scale, background: np.ndarray, nsamples: int | None = None,
+                 link: str = "identity", seed: int = 0, device="auto"):
+        B = np.asarray(background, np.float32)
+        if B.shape[0] > 128:
+            raise ValueError("at most 128 background rows (summarize larger sets)")
+        if ens.depth > 5:
+            raise ValueError("tree KernelSHAP supports depth <= 5 (the reference trains max_depth=5)")
+        self.ens = ens
+        self.d = B.shape[1]
+        self.mean = np.asarray(mean, np.float64)
+        self.scale = np.asarray(scale, np.float64)
+        self.B = B
+        self.Bs = _standardize(B, self.mean, self.scale)
+        self.bw = tree_direction_bits(self.Bs, ens)         # [T, n_bg]
+        self.link = link
+        self.Z, self.w, self.A, self.zM = cached_design(self.d, nsamples or None, seed)
+        self.zmasks = (self.Z.astype(np.uint64) << np.arange(self.d, dtype=np.uint64)[None, :]).sum(1).astype(np.uint32)
+        self.device = torch.device("cuda", 0) if (device == "auto" and torch.cuda.is_available()) else torch.device(
+            "cpu" if device == "auto" else device)
+        self._dev_cache = None
+
+    @property
+    def nsamples(self) -> int:
+        return self.Z.shape[0]
+
+    def shap_values(self, X) -> np.ndarray:
+        return self.explain(X)[0]
+
+    def explain(self, X):
+        """-> (phi [E, d], fx [E], f0) in the link's space (identity: probabilities)."""
+        X = np.ascontiguousarray(X, np.float32)
+        if self.device.type == "cuda":
+            from ..ops.kernelshap import kernelshap_tree
+
+            return kernelshap_tree(torch.from_numpy(X).to(self.device), self)
+        return kernelshap_tree_reference(_standardize(X, self.mean, self.scale), self.Bs, self.ens, self.Z, self.A,
+                                         self.zM, self.link)
+
+
+class FunctionKernelExplainer:
+    """KernelSHAP of any model given as ``fn(rows: Tensor[N, d]) -> Tensor[N]`` (the model output
+    in the link's input space: probabilities for identity / logit, log-odds for logit_model).
+    Masked rows are formed on ``device`` in chunks of explanations and the coalition values are
+    projected with the shared WLS operator (a plain GEMM: hipBLASLt through torch)."""
+
+    def __init__(self, fn, background: np.ndarray, nsamples: int | None = None, link: str = "identity",
+                 seed: int = 0, device="auto", max_rows_per_call: int = 1 << 24):
+        self.fn = fn
+        self.B = np.asarray(background, np.float32)
+        self.d = self.B.shape[1]
+        self.link = link
+        self.Z, self.w, self.A, self.zM = cached_design(self.d, nsamples or None, seed)
+        self.device = torch.device("cuda", 0) if (device == "auto" and torch.cuda.is_available()) else torch.device(
+            "cpu" if device == "auto" else device)
+        self.max_rows = max_rows_per_call
+
+    @property
+    def nsamples(self) -> int:
+        return self.Z.shape[0]
+
+    def shap_values(self, X) -> np.ndarray:
+        return self.explain(X)[0]
+
+    @torch.no_grad()
+    def explain(self, X):
+        dev = self.device
+        X = torch.as_tensor(np.ascontiguousarray(X, np.float32), device=dev)
+        B = torch.from_numpy(self.B).to(dev)
+        Z = torch.from_numpy(self.Z.astype(np.float32)).to(dev)            # [S, d]
+        E, S, nb = X.shape[0], Z.shape[0], B.shape[0]
+        f0 = float(self.fn(B).double().mean())
+        fx = self.fn(X).double()
+        per = max(1, self.max_rows // (S * nb))
+        f = torch.empty((E, S), dtype=torch.float64, device=dev)
+        for e0 in range(0, E, per):
+            xe = X[e0:e0 + per]                                             # [c, d]
+            rows = Z[None, :, None, :] * xe[:, None, None, :] + (1 - Z)[None, :, None, :] * B[None, None, :, :]
+            out = self.fn(rows.reshape(-1, self.d)).double().reshape(xe.shape[0], S, nb)
+            f[e0:e0 + per] = out.mean(2)
+        f, fx = f.cpu().numpy(), fx.cpu().numpy()
+        if self.link == "logit":
+            f, f0, fx = _link(f, "logit"), float(_link(np.asarray(f0), "logit")), _link(fx, "logit")
+        return _project(f, f0, fx, self.A, self.zM), fx, f0
 
 
 def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 100, reps: int = 5) -> dict:

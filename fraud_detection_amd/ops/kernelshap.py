@@ -1,4 +1,13 @@
-"""K7 KernelSHAP coalition GEMM (csrc/kernels/kernelshap.hip) -- device wrapper."""
+"""K7 KernelSHAP device wrappers (csrc/kernels/kernelshap.hip): the linear-model MFMA coalition
+GEMM and the tree-ensemble masked-evaluation kernel, sharing the WLS projection.
+
+Work is split into ``parts`` coalition ranges per explanation so that E x parts workgroups fill
+the 256 CUs in whole dispatch rounds (a 512-explanation worker lease would otherwise leave half
+the device idle, and 1100 explanations would run a second, mostly empty round).  Partials of an
+explanation are summed in part order by the last part to arrive, so results do not depend on
+scheduling (tests/test_kernelshap.py checks run-to-run bit identity per part count; different
+part counts differ only in the fp32 summation order of the projection).
+"""
 from __future__ import annotations
 
 import numpy as np
@@ -7,10 +16,47 @@ import torch
 from .native import native, ptr, stream_of
 
 _LINKS = {"identity": 0, "logit": 1, "logit_model": 2}
+MAX_PARTS = 8
+
+
+def choose_parts(n_expl: int, n_tiles: int, target_wgs: int) -> int:
+    """Coalition parts per explanation: split only while E x P is below ``target_wgs`` (enough
+    workgroups to keep every SIMD issuing).  Measured on MI355X (profiles/r2_b): a split costs
+    each extra part its own U build / f0 and a device-scope release fence at the hand-off (the
+    L2s of the 8 XCDs are not coherent, so the fence writes back L2), so above the target P = 1
+    wins -- 1000 explanations run 78 us at P = 1 vs 114 us at P = 2."""
+    if n_expl <= 0:
+        return 1
+    return int(max(1, min(MAX_PARTS, max(1, n_tiles // 4), -(-target_wgs // n_expl))))
+
+
+def _cu_count(dev) -> int:
+    return int(native().device_info(dev.index or 0)["cu_count"])
+
+
+class _Workspace:
+    """Partial-projection workspace [E, 8, 32] f32 + arrival counters [E] u32 (kept zeroed by the
+    kernel itself), grown on demand, one per device."""
+
+    def __init__(self):
+        self.ws = None
+        self.cnt = None
+
+    def get(self, E: int, dev):
+        if self.ws is None or self.ws.shape[0] < E or self.ws.device != dev:
+            cap = max(E, 1024)
+            self.ws = torch.empty((cap, MAX_PARTS, 32), device=dev, dtype=torch.float32)
+            self.cnt = torch.zeros(cap, device=dev, dtype=torch.int32)
+        return self.ws, self.cnt
+
+
+def _check_x(X, d):
+    if X.dim() != 2 or X.dtype != torch.float32 or X.shape[1] != d or not X.is_contiguous():
+        raise ValueError(f"X must be contiguous float32 [E, {d}]")
 
 
 def _device_design(expl, dev):
-    """Upload the explainer's design once: Z as bf16 [S_pad, 32] (col 31 = 1 folds the
+    """Upload the linear explainer's design once: Z as bf16 [S_pad, 32] (col 31 = 1 folds the
     background intercepts into the GEMM), A [d-1, S_pad] (zero-padded), A z_M, the weighted
     background rows W and the background logits."""
     key = (str(dev),)
@@ -40,27 +86,98 @@ def _device_design(expl, dev):
         "a": torch.from_numpy(a32).to(dev),
         "bg": torch.from_numpy(W).to(dev),
         "cb": torch.from_numpy(cb).to(dev),
-        "S": S, "S_pad": S_pad,
+        "S": S, "S_pad": S_pad, "ws": _Workspace(),
     }
     expl._dev_cache = (key, t)
     return t
 
 
-def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | None = None):
-    """X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else tensors).
-    ``stamps`` (int64 [E, 8], tools/kernelshap_stamps.py): per-explanation phase timestamps."""
-    if X.dim() != 2 or X.dtype != torch.float32 or X.shape[1] != expl.d or not X.is_contiguous():
-        raise ValueError(f"X must be contiguous float32 [E, {expl.d}]")
+def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | None = None,
+               parts: int | None = None):
+    """Linear model.  X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else
+    device tensors).  ``stamps`` (int64 [E, 8], tools/kernelshap_stamps.py): per-explanation phase
+    timestamps (forces parts = 1).  ``parts``: coalition parts per explanation (None = auto)."""
+    _check_x(X, expl.d)
     m = native()
     dev = X.device
     t = _device_design(expl, dev)
     E = X.shape[0]
+    n_tiles = t["S_pad"] // 32
+    if stamps is not None:
+        parts = 1
+    elif parts is None:
+        # measured (profiles/r2_e): the split's hand-off costs more than the idle CUs it fills
+        # until the batch is tiny (64 explanations: 25.8 us at P = 1 vs 31.9 at P = 8)
+        parts = choose_parts(E, n_tiles, 16)
+    parts = max(1, min(int(parts), MAX_PARTS, n_tiles))
     phi = torch.empty((E, expl.d), device=dev, dtype=torch.float32)
     fx = torch.empty(E, device=dev, dtype=torch.float32)
     f0 = torch.empty(E, device=dev, dtype=torch.float32)
+    ws, cnt = t["ws"].get(E, dev) if parts > 1 else (None, None)
     m.kernelshap(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]), expl.B.shape[0],
-                 ptr(t["Z"]), t["S"], t["S_pad"], ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi), ptr(fx),
-                 ptr(f0), stream_of(X), ptr(stamps))
+                 ptr(t["Z"]), t["S"], t["S_pad"], parts, ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi),
+                 ptr(fx), ptr(f0), ptr(ws), ptr(cnt), stream_of(X), ptr(stamps))
+    if not sync:
+        return phi, fx, f0
+    return phi.cpu().numpy().astype(np.float64), fx.cpu().numpy().astype(np.float64), float(f0[0].item()) if E else 0.0
+
+
+def _tree_device_design(expl, dev):
+    key = (str(dev),)
+    if expl._dev_cache is not None and expl._dev_cache[0] == key:
+        return expl._dev_cache[1]
+    ens = expl.ens
+    S = expl.Z.shape[0]
+    S_pad = (S + 31) // 32 * 32
+    if S_pad > 4096:
+        raise ValueError("at most 4096 coalitions per design on device")
+    Zm = np.zeros(S_pad, np.uint32)
+    Zm[:S] = expl.zmasks
+    Ap = np.zeros((expl.d - 1, S_pad), np.float32)
+    Ap[:, :S] = expl.A
+    from ..ops.scaler import stats_from_numpy
+
+    t = {
+        "feat": torch.from_numpy(np.ascontiguousarray(ens.feat, np.int32)).to(dev),
+        "thr": torch.from_numpy(np.ascontiguousarray(ens.thr, np.float32)).to(dev),
+        "leaf": torch.from_numpy(np.ascontiguousarray(ens.leaf, np.float32)).to(dev),
+        "bw": torch.from_numpy(np.ascontiguousarray(expl.bw.view(np.int32))).to(dev),
+        "Zm": torch.from_numpy(Zm.view(np.int32)).to(dev),
+        "A": torch.from_numpy(Ap).to(dev).contiguous(),
+        "Az": torch.from_numpy((expl.A @ expl.zM).astype(np.float32)).to(dev),
+        "stats": stats_from_numpy(expl.mean, expl.scale, device=dev),
+        "S": S, "S_pad": S_pad, "ws": _Workspace(),
+    }
+    expl._dev_cache = (key, t)
+    return t
+
+
+def kernelshap_tree(X: torch.Tensor, expl, sync: bool = True, parts: int | None = None):
+    """Tree ensemble (models/explainers.TreeKernelExplainer).  X [E, d] RAW fp32 on device; the
+    rows are standardized on device with the model's scaler (the same kernel as predict), then
+    every (coalition, background row) masked row is walked through the ensemble in the kernel."""
+    _check_x(X, expl.d)
+    m = native()
+    dev = X.device
+    t = _tree_device_design(expl, dev)
+    from ..ops.scaler import scale_cast
+
+    E = X.shape[0]
+    Xs = scale_cast(X, t["stats"], out_dtype="f32")  # [E, 32]
+    n_tiles = t["S_pad"] // 32
+    if parts is None:
+        # a workgroup carries ms of work here: split until every CU holds 4 workgroups
+        parts = choose_parts(E, n_tiles, 4 * _cu_count(dev))
+    parts = max(1, min(int(parts), MAX_PARTS, n_tiles))
+    ens = expl.ens
+    phi = torch.empty((E, expl.d), device=dev, dtype=torch.float32)
+    fx = torch.empty(E, device=dev, dtype=torch.float32)
+    f0 = torch.empty(E, device=dev, dtype=torch.float32)
+    ws, cnt = t["ws"].get(E, dev) if parts > 1 else (None, None)
+    m.kernelshap_tree(ptr(Xs), Xs.stride(0), E, expl.d, ptr(t["feat"]), ptr(t["thr"]), ptr(t["leaf"]), ens.n_trees,
+                      ens.depth, float(ens.base_margin), ptr(t["bw"]), expl.bw.shape[1], expl.B.shape[0], ptr(t["Zm"]),
+                      t["S"], t["S_pad"], parts, ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi), ptr(fx),
+                      ptr(f0), ptr(ws), ptr(cnt), stream_of(X))
     if not sync:
         return phi, fx, f0
     return phi.cpu().numpy().astype(np.float64), fx.cpu().numpy().astype(np.float64), float(f0[0].item()) if E else 0.0

@@ -29,8 +29,9 @@ def main():
 
     dev = torch.device("cuda", 0)
     X, _ = separable(max(a.expl, 100), seed=1)
-    w = np.r_[np.random.default_rng(0).normal(0, 0.2, 30), 0.0, 0.0]
-    ke = KernelExplainer(w, -3.0, X[:100].numpy(), link=a.link, device="cuda")
+    Xr = X.numpy().astype(np.float64)  # standardized-space weights folded onto raw features
+    w = np.r_[np.random.default_rng(0).normal(0, 0.4, 30) / Xr.std(0), 0.0, 0.0]
+    ke = KernelExplainer(w, float(-3.0 - w[:30] @ Xr.mean(0)), X[:100].numpy(), link=a.link, device="cuda")
     Xe = X[: a.expl].contiguous().to(dev)
     st = torch.zeros((a.expl, 8), dtype=torch.int64, device=dev)
     for _ in range(3):
