@@ -32,6 +32,8 @@ ENV_MAP = {
     "FDX_XAI_BATCH": "xai_batch",
     "FDX_KERNELSHAP_NSAMPLES": "kernelshap_nsamples",
     "FDX_KERNELSHAP_BACKGROUND": "kernelshap_background",
+    "FDX_KERNELSHAP_LINK": "kernelshap_link",
+    "FDX_XAI_METHOD": "xai_method",
     "FDX_SMOTE_K": "smote_k",
     "FDX_SEED": "seed",
     "FDX_SPLIT": "split",
@@ -63,7 +65,9 @@ class Settings:
     microbatch_max: int = 4096
     xai_batch: int = 512
     kernelshap_nsamples: int = 0   # 0 -> shap default 2*M + 2048
-    kernelshap_background: int = 100
+    kernelshap_background: int = 100   # rows saved with the model (shap_background.npy)
+    kernelshap_link: str = "identity"  # identity (probabilities) | logit | logit_model
+    xai_method: str = "auto"           # auto (kernel when a background exists) | linear | kernel
     smote_k: int = 5
     seed: int = 42
     split: str = "auto"            # sklearn (reference-exact) | device (K3 kernel) | auto

@@ -174,8 +174,11 @@ class GBDTResult:
         return paths
 
     def log_model(self, mlf, paths: dict) -> str:
-        return mlf.log_files_model({MODEL_FILE: paths["model"], "scaler.joblib": paths["scaler"],
-                                    "feature_names.json": paths["feature_names"]}, "model", "fdx_gbdt",
+        files = {MODEL_FILE: paths["model"], "scaler.joblib": paths["scaler"],
+                 "feature_names.json": paths["feature_names"]}
+        if paths.get("background"):
+            files["shap_background.npy"] = paths["background"]
+        return mlf.log_files_model(files, "model", "fdx_gbdt",
                                    {"model_file": MODEL_FILE, "format": "fdx-gbdt/1", "depth": self.ensemble.depth,
                                     "n_trees": self.ensemble.n_trees})
 

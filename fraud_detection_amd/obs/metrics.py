@@ -33,10 +33,14 @@ class ApiMetrics:
     http_req_size: Histogram
     http_resp_size: Histogram
     microbatch_size: Histogram
-    gpu_kernel_seconds: Histogram
 
     def render(self) -> bytes:
-        return generate_latest(self.registry)
+        """This app's metrics plus the process-global ones (worker / training / span / GPU
+        metrics observed in the same process, e.g. an in-process worker or a fit)."""
+        from prometheus_client import REGISTRY
+
+        out = generate_latest(self.registry)
+        return out if self.registry is REGISTRY else out + generate_latest(REGISTRY)
 
 
 def api_metrics(registry: CollectorRegistry | None = None) -> ApiMetrics:
@@ -60,8 +64,6 @@ def api_metrics(registry: CollectorRegistry | None = None) -> ApiMetrics:
                                  ["handler"], buckets=size_buckets, registry=r),
         microbatch_size=Histogram("fdx_microbatch_size", "Rows per fused GPU predict launch",
                                   buckets=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 4096), registry=r),
-        gpu_kernel_seconds=Histogram("fdx_gpu_kernel_seconds", "Device time of serving launches",
-                                     ["kernel"], buckets=_LAT_BUCKETS, registry=r),
     )
 
 
@@ -111,15 +113,60 @@ class TrainMetrics:
     hbm_used_bytes: Gauge
 
 
+_train_lock = threading.Lock()
+
+
 def train_metrics(registry: CollectorRegistry | None = None) -> TrainMetrics:
-    r = registry or CollectorRegistry()
-    return TrainMetrics(
-        registry=r,
-        rows_per_second=Gauge("fdx_train_rows_per_second", "Post-SMOTE rows fitted per second", registry=r),
-        allreduce_seconds=Histogram("fdx_allreduce_seconds", "All-reduce latency", ["op"], buckets=_LAT_BUCKETS,
-                                    registry=r),
-        hbm_used_bytes=Gauge("fdx_hbm_used_bytes", "Device memory in use", registry=r),
-    )
+    """Training metrics, one set per registry (default: the process-global one that /metrics and
+    the worker's :8001 server expose)."""
+    from prometheus_client import REGISTRY
+
+    r = registry or REGISTRY
+    with _train_lock:
+        existing = getattr(r, "_fdx_train_metrics", None)
+        if existing is not None:
+            return existing
+        m = TrainMetrics(
+            registry=r,
+            rows_per_second=Gauge("fdx_train_rows_per_second", "Post-SMOTE rows fitted per second", registry=r),
+            allreduce_seconds=Histogram("fdx_allreduce_seconds", "Collective latency (host-observed, synchronised)",
+                                        ["op"], buckets=_LAT_BUCKETS, registry=r),
+            hbm_used_bytes=Gauge("fdx_hbm_used_bytes", "Device memory in use (torch allocator + native)", registry=r),
+        )
+        r._fdx_train_metrics = m
+        return m
+
+
+_span_lock = threading.Lock()
+
+
+def span_histogram(registry: CollectorRegistry | None = None) -> Histogram:
+    from prometheus_client import REGISTRY
+
+    r = registry or REGISTRY
+    with _span_lock:
+        h = getattr(r, "_fdx_span_hist", None)
+        if h is None:
+            h = Histogram("fdx_span_seconds", "Duration of traced spans", ["name"], buckets=_LAT_BUCKETS, registry=r)
+            r._fdx_span_hist = h
+        return h
+
+
+_gpu_lock = threading.Lock()
+
+
+def gpu_kernel_histogram(registry: CollectorRegistry | None = None) -> Histogram:
+    """fdx_gpu_kernel_seconds{kernel}: device time of serving / XAI launches (HIP events)."""
+    from prometheus_client import REGISTRY
+
+    r = registry or REGISTRY
+    with _gpu_lock:
+        h = getattr(r, "_fdx_gpu_hist", None)
+        if h is None:
+            h = Histogram("fdx_gpu_kernel_seconds", "Device time of serving / XAI launches (HIP events)", ["kernel"],
+                          buckets=_LAT_BUCKETS, registry=r)
+            r._fdx_gpu_hist = h
+        return h
 
 
 _servers: dict[int, object] = {}

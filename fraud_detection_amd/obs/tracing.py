@@ -6,16 +6,25 @@ API -> worker propagation was only a correlation-id argument.  Here a W3C ``trac
 generated per request and carried in the task headers, so worker spans can join the request
 trace whenever a real OTel SDK is present.
 
-Device ranges: ``roctx_range("name")`` pushes/pops a ROCTx range (libroctx64) so rocprofv3
---marker-trace shows pipeline phases; it is a no-op when the library is unavailable.
+Without the OTel SDK, ``span`` still records each finished span (trace id, span id, parent span
+id, name, duration, attributes) in a bounded in-process ring (``recent_spans``) and the
+``fdx_span_seconds`` histogram, so the API -> worker trace continuation is observable and tested
+(tests/test_observability.py).
+
+Device ranges: ``roctx_range("name")`` pushes/pops a ROCTx range so rocprofv3 --marker-trace shows
+pipeline phases (rocprofiler-sdk's librocprofiler-sdk-roctx first, the legacy libroctx64 after);
+it is a no-op when neither library is available.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
 import ctypes
 import logging
 import os
 import secrets
+import threading
+import time
 
 logger = logging.getLogger(__name__)
 
@@ -60,15 +69,68 @@ def configure(service_name: str | None = None) -> bool:
         return False
 
 
+_RECENT: collections.deque = collections.deque(maxlen=4096)
+_RECENT_LOCK = threading.Lock()
+_SPAN_HIST = None
+
+
+def parse_traceparent(tp: str | None):
+    """(trace_id, parent_span_id) of a W3C traceparent, or (None, None)."""
+    if not tp:
+        return None, None
+    parts = tp.split("-")
+    if len(parts) != 4 or len(parts[1]) != 32 or len(parts[2]) != 16:
+        return None, None
+    return parts[1], parts[2]
+
+
+def traceparent_of(record: dict) -> str:
+    return f"00-{record['trace_id']}-{record['span_id']}-01"
+
+
+def recent_spans(name: str | None = None) -> list[dict]:
+    with _RECENT_LOCK:
+        return [dict(r) for r in _RECENT if name is None or r["name"] == name]
+
+
+def _observe(name: str, dt: float):
+    global _SPAN_HIST
+    try:
+        if _SPAN_HIST is None:
+            from .metrics import span_histogram
+
+            _SPAN_HIST = span_histogram()
+        _SPAN_HIST.labels(name).observe(dt)
+    except Exception:  # noqa: BLE001 - metrics are best effort
+        pass
+
+
 @contextlib.contextmanager
-def span(name: str, **attrs):
-    if HAVE_OTEL:  # pragma: no cover
-        with _ot.get_tracer("fraud_detection_amd").start_as_current_span(name) as s:
-            for k, v in attrs.items():
-                s.set_attribute(k, v)
-            yield s
-    else:
-        yield None
+def span(name: str, parent: str | None = None, **attrs):
+    """A span named ``name``; ``parent`` is a W3C traceparent to continue (e.g. the header the API
+    put on a queued task).  Yields a dict record (``traceparent_of(rec)`` propagates it)."""
+    trace_id, parent_id = parse_traceparent(parent)
+    rec = {"name": name, "trace_id": trace_id or secrets.token_hex(16), "span_id": secrets.token_hex(8),
+           "parent_span_id": parent_id, "attrs": dict(attrs), "start": time.time()}
+    t0 = time.perf_counter()
+    try:
+        if HAVE_OTEL:  # pragma: no cover
+            ctx = None
+            if parent:
+                from opentelemetry.propagate import extract
+
+                ctx = extract({"traceparent": parent})
+            with _ot.get_tracer("fraud_detection_amd").start_as_current_span(name, context=ctx) as s:
+                for k, v in attrs.items():
+                    s.set_attribute(k, v)
+                yield rec
+        else:
+            yield rec
+    finally:
+        rec["seconds"] = time.perf_counter() - t0
+        with _RECENT_LOCK:
+            _RECENT.append(rec)
+        _observe(name, rec["seconds"])
 
 
 _roctx = None
@@ -80,17 +142,23 @@ def _load_roctx():
     if _roctx_tried:
         return _roctx
     _roctx_tried = True
-    for name in ("libroctx64.so.4", "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+    for name in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so",
+                 "librocprofiler-sdk-roctx.so.1", "libroctx64.so.4", "libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
         try:
             lib = ctypes.CDLL(name)
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
             lib.roctxRangePushA.restype = ctypes.c_int
             lib.roctxRangePop.restype = ctypes.c_int
             _roctx = lib
+            logger.debug("roctx ranges via %s", name)
             break
-        except OSError:
+        except (OSError, AttributeError):
             continue
     return _roctx
+
+
+def roctx_available() -> bool:
+    return _load_roctx() is not None
 
 
 @contextlib.contextmanager

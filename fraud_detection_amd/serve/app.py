@@ -40,7 +40,7 @@ from ..store import db as store_db
 from ..store.migrations import upgrade
 from ..store.models import ShapExplanation, StatusEnum, TransactionResult
 from .batcher import MicroBatcher
-from .engine import InferenceEngine
+from .engine import InferenceEngine, load_engine_dir
 from .schemas import BatchIn, BatchOut, PredictAccepted, PredictionOut, PredictResponse, TransactionIn
 
 logger = logging.getLogger("api.app")
@@ -49,23 +49,23 @@ TASK_NAME = "xai_tasks.compute_shap"
 
 
 def load_production_engine(settings: Settings, device: str) -> tuple[InferenceEngine, str]:
-    """models:/<name>@<alias> from the registry, falling back to the local joblib artifacts
-    (api/app.py:34-44)."""
+    """models:/<name>@<alias> from the registry (either model family: the sklearn-flavour linear
+    model or the fdx-gbdt tree ensemble), falling back to the local artifacts (api/app.py:34-44)."""
     from ..compat import mlflow_compat
-    from ..compat.sklearn_export import load_artifacts
 
     uri = f"models:/{settings.mlflow_model_name}@{settings.mlflow_model_stage}"
+    kw = {"kernel_nsamples": settings.kernelshap_nsamples, "kernel_link": settings.kernelshap_link}
     try:
         mdir = mlflow_compat.resolve_model_dir(uri, settings.mlflow_tracking_uri)
-        art = load_artifacts(os.path.join(mdir, "model.pkl"), os.path.join(mdir, "scaler.joblib"),
-                             os.path.join(mdir, "feature_names.json"), trusted=True)
-        logger.info("Loaded model %s using alias '%s'", settings.mlflow_model_name, settings.mlflow_model_stage)
-        return InferenceEngine(art, device=device, source="mlflow"), "mlflow"
+        eng = load_engine_dir(mdir, device=device, source="mlflow", **kw)
+        logger.info("Loaded %s model %s using alias '%s'", eng.kind, settings.mlflow_model_name,
+                    settings.mlflow_model_stage)
+        return eng, "mlflow"
     except Exception as e:  # noqa: BLE001
         logger.warning("Failed to load model from registry alias '%s' (%s); falling back to local model file",
                        settings.mlflow_model_stage, e)
     eng = InferenceEngine.from_paths(settings.model_path, settings.scaler_path, settings.feature_names_path,
-                                     device=device)
+                                     device=device, **kw)
     return eng, "local"
 
 
@@ -227,7 +227,7 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
         metrics.predictions_submitted.inc()
         x = _validate(transaction.features)
         with metrics.inference_time.time():
-            prob, _, _ = await batcher_().submit(x)
+            prob, _ = await batcher_().submit(x)
         prediction = int(prob > 0.5)
         features_dict = {f"feature_{i}": float(v) for i, v in enumerate(x.tolist())}
         _persist_pending(transaction.transaction_id, features_dict, prob)
@@ -255,9 +255,14 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
             raise HTTPException(status_code=422, detail=f"rows must be [n, {eng.d}]")
         metrics.predictions_submitted.inc(X.shape[0])
         with metrics.inference_time.time():
-            p, _, phi = eng.predict_explain(X)
+            if batch.explain:
+                ex = eng.explain(X, settings.xai_method)
+                p, phi = ex.prob, ex.phi
+            else:
+                p, _ = eng.predict_proba(X)
+                phi = None
         return BatchOut(predictions=(p > 0.5).astype(int).tolist(), scores=p.tolist(),
-                        shap_values=phi.tolist() if batch.explain else None)
+                        shap_values=phi.tolist() if phi is not None else None)
 
     @app.get("/result/{transaction_id}", response_model=PredictResponse, tags=["Prediction"])
     def get_result(transaction_id: str):
@@ -280,7 +285,7 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
         if r is None:
             raise HTTPException(status_code=404, detail="SHAP explanation not found. Calculation may still be pending.")
         return {"transaction_id": transaction_id, "created_at": r.created_at, "shap_values": r.shap_values,
-                "feature_names": r.feature_names}
+                "feature_names": r.feature_names, "explainer": r.explainer, "base_value": r.base_value}
 
     @app.get("/ui", include_in_schema=False)
     def console():

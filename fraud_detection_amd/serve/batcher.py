@@ -42,11 +42,11 @@ class MicroBatcher:
             self._task = None
 
     async def submit(self, row: np.ndarray):
-        """-> (prob, logit, phi[d]) for one row."""
+        """-> (prob, logit) for one row."""
         if not self.enabled or self._task is None:
-            p, z, phi = self.engine.predict_explain(row[None, :])
+            p, z = self.engine.predict_proba(row[None, :])
             self._observe(1)
-            return float(p[0]), float(z[0]), phi[0]
+            return float(p[0]), float(z[0])
         fut = asyncio.get_running_loop().create_future()
         await self._q.put((row, fut))
         return await fut
@@ -73,11 +73,11 @@ class MicroBatcher:
                 futs.append(f)
             X = np.stack(rows)
             try:
-                p, z, phi = await loop.run_in_executor(None, self.engine.predict_explain, X)
+                p, z = await loop.run_in_executor(None, self.engine.predict_proba, X)
                 self._observe(len(rows))
                 for i, f in enumerate(futs):
                     if not f.done():
-                        f.set_result((float(p[i]), float(z[i]), phi[i]))
+                        f.set_result((float(p[i]), float(z[i])))
             except Exception as e:  # noqa: BLE001
                 for f in futs:
                     if not f.done():

@@ -1,19 +1,33 @@
-"""Inference engine shared by the API, the XAI worker and the library predictors.
+"""Inference engines shared by the API, the XAI worker and the library predictors.
 
-Holds one linear model + StandardScaler with the scaler folded into the weights
-(ops/predict.py fold_scaler), so a request's raw features are read exactly once by the fused
-predict + LinearSHAP kernel (K5/K6).  Device policy: ``device="auto"`` uses the GPU when one is
-present; CPU execution is exact fp64 numpy (what the reference's sklearn path computes).
+Two model families, one interface (``predict_proba`` / ``predict_explain`` / ``explain``):
 
-Background for LinearSHAP: the standardized training mean (0 by construction), i.e. the
-``shap.LinearExplainer(model, X_train_scaled)`` semantics of explain_model.py:24, with the
-attributions defined on the model's standardized inputs.
+* ``InferenceEngine`` -- the linear model (reference: models/logistic_model.joblib + scaler.joblib,
+  api/app.py:34-48) with the StandardScaler folded into the weights (ops/predict.py fold_scaler),
+  so a request's raw features are read exactly once by the fused predict + LinearSHAP kernel
+  (K5/K6).
+* ``TreeInferenceEngine`` -- the GBDT family (reference train_model.py:95-113 trains and dumps an
+  XGBClassifier): scaler -> tree-ensemble predict kernel (K11), explained with the masked-row
+  KernelSHAP tree kernel (K7 tree path).
+
+Explanations (``explain``): ``method="linear"`` is LinearSHAP (shap.LinearExplainer semantics of
+explain_model.py:24 / api/worker.py:53, log-odds space, background = the standardized training
+mean); ``method="kernel"`` is KernelSHAP (shap.KernelExplainer semantics, probability space,
+background = the <= 128 training rows stored next to the model as ``shap_background.npy``);
+``"auto"`` picks kernel when a background is available.
+
+Device policy: ``device="auto"`` uses the GPU when one is present; CPU execution is exact fp64
+numpy (what the reference's sklearn path computes).  Host <-> device traffic goes through
+persistent pinned staging buffers (one upload and one download per call, no per-request pinned
+allocation).
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import threading
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -23,53 +37,255 @@ from ..ops import predict as P
 
 logger = logging.getLogger(__name__)
 
+BACKGROUND_FILE = "shap_background.npy"
+MAX_BACKGROUND = 128
 
-def _pick_device(device: str) -> torch.device:
+
+def _pick_device(device) -> torch.device:
+    if isinstance(device, torch.device):
+        return device
     if device == "auto":
         return torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
     return torch.device(device)
 
 
-class InferenceEngine:
-    def __init__(self, artifacts: LinearArtifacts, device: str = "auto", bg_std: np.ndarray | None = None,
-                 source: str = "local"):
-        self.art = artifacts
-        self.source = source
-        self.d = len(artifacts.mean)
-        self.feature_names = list(artifacts.feature_names)
-        self.a, self.c, self.bias = P.fold_scaler(artifacts.padded_weights(), artifacts.mean, artifacts.scale, bg_std)
+def load_background(model_dir: str | None) -> np.ndarray | None:
+    """The KernelSHAP background saved by training (float32 [<=128, d]; no pickle)."""
+    if not model_dir:
+        return None
+    p = os.path.join(model_dir, BACKGROUND_FILE)
+    if not os.path.exists(p):
+        return None
+    B = np.load(p, allow_pickle=False)
+    if B.ndim != 2 or B.shape[0] < 1 or B.shape[0] > MAX_BACKGROUND or not np.all(np.isfinite(B)):
+        raise ValueError(f"{p}: expected a finite [1..{MAX_BACKGROUND}, d] float array, got {B.shape}")
+    return np.ascontiguousarray(B, dtype=np.float32)
+
+
+def sample_background(X: np.ndarray, n: int = 100, seed: int = 42) -> np.ndarray:
+    """shap.sample-style background: ``n`` training rows drawn without replacement."""
+    X = np.asarray(X, dtype=np.float32)
+    n = max(1, min(int(n), MAX_BACKGROUND, X.shape[0]))
+    idx = np.sort(np.random.default_rng(seed).choice(X.shape[0], n, replace=False))
+    return np.ascontiguousarray(X[idx])
+
+
+def save_background(B: np.ndarray, model_dir: str) -> str:
+    os.makedirs(model_dir, exist_ok=True)
+    p = os.path.join(model_dir, BACKGROUND_FILE)
+    np.save(p, np.ascontiguousarray(B, dtype=np.float32), allow_pickle=False)
+    return p
+
+
+@dataclass
+class Explanation:
+    prob: np.ndarray        # [B] P(fraud)
+    logit: np.ndarray       # [B] model log-odds / margin
+    phi: np.ndarray         # [B, d] attributions
+    base_value: float       # E[f] over the background, in phi's space
+    method: str             # "linear" | "kernel"
+    space: str              # "log-odds" | "probability"
+
+
+class _KernelTimer:
+    """HIP-event device time of a launch sequence on the current stream -> fdx_gpu_kernel_seconds
+    {kernel}.  Read after the caller's synchronisation (no extra sync)."""
+
+    def __init__(self, name: str):
+        self.name = name
+        self.t0 = torch.cuda.Event(enable_timing=True)
+        self.t1 = torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        self.t0.record()
+        return self
+
+    def __exit__(self, *exc):
+        self.t1.record()
+        return False
+
+    def observe(self):
+        try:
+            from ..obs.metrics import gpu_kernel_histogram
+
+            gpu_kernel_histogram().labels(self.name).observe(self.t0.elapsed_time(self.t1) / 1e3)
+        except Exception:  # noqa: BLE001 - metrics are best effort
+            pass
+
+
+class _Staging:
+    """Persistent pinned host buffers + device buffers for one engine (grown on demand).  Calls
+    are serialised by the engine lock, so one set suffices."""
+
+    def __init__(self, device: torch.device, d: int, n_out: int):
+        self.device, self.d, self.n_out = device, d, n_out
+        self.cap = 0
+
+    def ensure(self, n: int):
+        if n > self.cap:
+            cap = max(n, 2 * self.cap, 256)
+            self.hin = torch.empty((cap, self.d), dtype=torch.float32, pin_memory=True)
+            self.din = torch.empty((cap, self.d), dtype=torch.float32, device=self.device)
+            self.hout = torch.empty(cap * self.n_out, dtype=torch.float32, pin_memory=True)
+            self.dout = torch.empty(cap * self.n_out, dtype=torch.float32, device=self.device)
+            self.cap = cap
+
+    def upload(self, X: np.ndarray) -> torch.Tensor:
+        n = X.shape[0]
+        self.ensure(n)
+        self.hin[:n].numpy()[...] = X
+        xd = self.din[:n]
+        xd.copy_(self.hin[:n], non_blocking=True)
+        return xd
+
+    def download(self, n_vals: int) -> np.ndarray:
+        """Copy dout[:n_vals] to host (on the current stream) and wait for it."""
+        self.hout[:n_vals].copy_(self.dout[:n_vals], non_blocking=True)
+        torch.cuda.current_stream(self.device).synchronize()
+        return self.hout[:n_vals].numpy()
+
+
+class _EngineBase:
+    kind = "?"
+
+    def __init__(self, device, source: str, background: np.ndarray | None, kernel_nsamples: int = 0,
+                 kernel_link: str = "identity"):
         self.device = _pick_device(device)
+        self.source = source
+        self.background = background
+        self.kernel_nsamples = int(kernel_nsamples or 0)
+        self.kernel_link = kernel_link
         self._lock = threading.Lock()
+        self._kexpl = None
         if self.device.type == "cuda":
             from ..ops.native import native
 
             native()  # fail loudly rather than serve through an eager fallback
-            self._a = torch.from_numpy(self.a).to(self.device)
-            self._c = torch.from_numpy(self.c).to(self.device)
             self._stream = torch.cuda.Stream(self.device)
 
-    @classmethod
-    def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto") -> "InferenceEngine":
-        model_path = model_path or os.getenv("MODEL_PATH", "./models/logistic_model.joblib")
-        scaler_path = scaler_path or os.getenv("SCALER_PATH") or os.path.join(os.path.dirname(model_path),
-                                                                               "scaler.joblib")
-        features_path = features_path or os.getenv("FEATURE_NAMES_PATH", "./models/feature_names.json")
-        return cls(load_artifacts(model_path, scaler_path, features_path), device=device, source="local")
+    # ---- shared API ------------------------------------------------------------------------
+    @property
+    def has_background(self) -> bool:
+        return self.background is not None
 
-    # ---- core ----------------------------------------------------------------------------
-    def predict_explain(self, X: np.ndarray):
-        """X raw features [B, d] -> (prob [B], logit [B], phi [B, d]) as numpy."""
+    def predict(self, X: np.ndarray):
+        p, _ = self.predict_proba(X)
+        return (p > 0.5).astype(np.int64), p
+
+    def _check(self, X) -> np.ndarray:
         X = np.ascontiguousarray(X, dtype=np.float32)
         if X.ndim != 2 or X.shape[1] != self.d:
             raise ValueError(f"expected [B, {self.d}] features, got {X.shape}")
+        return X
+
+    def resolve_method(self, method: str = "auto") -> str:
+        method = (method or "auto").lower()
+        if method == "auto":
+            return "kernel" if self.has_background else self.default_method
+        if method == "kernel" and not self.has_background:
+            raise ValueError("KernelSHAP needs a background (shap_background.npy next to the model)")
+        if method not in self.methods:
+            raise ValueError(f"{self.kind} model supports {self.methods}, not {method!r}")
+        return method
+
+    def kernel_explainer(self):
+        if self._kexpl is None:
+            if not self.has_background:
+                raise ValueError("no background for KernelSHAP")
+            self._kexpl = self._make_kernel_explainer()
+        return self._kexpl
+
+    def explain(self, X: np.ndarray, method: str = "auto") -> Explanation:
+        X = self._check(X)
+        m = self.resolve_method(method)
+        if m == "linear":
+            p, z, phi = self.predict_explain(X)
+            return Explanation(p, z, phi, self.expected_value(), "linear", "log-odds")
+        p, z = self.predict_proba(X)
+        if X.shape[0] == 0:
+            return Explanation(p, z, np.zeros((0, self.d)), 0.0, "kernel", "probability")
+        ke = self.kernel_explainer()
+        if self.device.type == "cuda":
+            with self._lock, torch.cuda.stream(self._stream):
+                xd = torch.from_numpy(X).to(self.device, non_blocking=False)
+                with _KernelTimer(f"kernelshap_{self.kind}") as kt:
+                    phi, fx, f0 = self._kernel_device(xd, ke)
+                kt.observe()
+        else:
+            phi, fx, f0 = ke.explain(X)
+        space = "log-odds" if ke.link == "logit_model" else "probability"
+        return Explanation(p, z, np.asarray(phi, np.float64), float(f0), "kernel", space)
+
+
+class InferenceEngine(_EngineBase):
+    """Linear model + folded scaler (see module docstring)."""
+
+    kind = "linear"
+    methods = ("linear", "kernel")
+    default_method = "linear"
+
+    def __init__(self, artifacts: LinearArtifacts, device: str = "auto", bg_std: np.ndarray | None = None,
+                 source: str = "local", background: np.ndarray | None = None, kernel_nsamples: int = 0,
+                 kernel_link: str = "identity"):
+        self.art = artifacts
+        self.d = len(artifacts.mean)
+        self.feature_names = list(artifacts.feature_names)
+        self.a, self.c, self.bias = P.fold_scaler(artifacts.padded_weights(), artifacts.mean, artifacts.scale, bg_std)
+        super().__init__(device, source, background, kernel_nsamples, kernel_link)
+        if self.device.type == "cuda":
+            self._a = torch.from_numpy(self.a).to(self.device)
+            self._c = torch.from_numpy(self.c).to(self.device)
+            self._stage = _Staging(self.device, self.d, self.d + 2)
+
+    @classmethod
+    def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto",
+                   source: str = "local", **kw) -> "_EngineBase":
+        model_path = model_path or os.getenv("MODEL_PATH", "./models/logistic_model.joblib")
+        if model_path.endswith(".json"):
+            return TreeInferenceEngine.from_paths(model_path, scaler_path, features_path, device, source, **kw)
+        scaler_path = scaler_path or os.getenv("SCALER_PATH") or os.path.join(os.path.dirname(model_path),
+                                                                               "scaler.joblib")
+        features_path = features_path or os.getenv("FEATURE_NAMES_PATH", "./models/feature_names.json")
+        bg = load_background(os.path.dirname(os.path.abspath(model_path)))
+        return cls(load_artifacts(model_path, scaler_path, features_path), device=device, source=source,
+                   background=bg, **kw)
+
+    # ---- core ------------------------------------------------------------------------------
+    def _device_run(self, X: np.ndarray, want_phi: bool):
+        n, d = X.shape
+        with self._lock, torch.cuda.stream(self._stream):
+            st = self._stage
+            xd = st.upload(X)
+            dphi = d if want_phi else 0
+            out = st.dout
+            prob, logit = out[:n], out[n:2 * n]
+            phi = out[2 * n:2 * n + n * dphi].view(n, dphi) if want_phi else None
+            m = P.native()
+            with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
+                m.predict_shap(P.ptr(xd), 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                               P.ptr(prob), P.ptr(logit), P.ptr(phi) if want_phi else 0, dphi, P.stream_of(xd))
+            o = st.download(n * (2 + dphi))
+            kt.observe()
+        p = o[:n].astype(np.float64)
+        z = o[n:2 * n].astype(np.float64)
+        ph = o[2 * n:].reshape(n, dphi).astype(np.float64) if want_phi else None
+        return p, z, ph
+
+    def predict_explain(self, X: np.ndarray):
+        """X raw features [B, d] -> (prob [B], logit [B], phi [B, d]) as numpy (LinearSHAP)."""
+        X = self._check(X)
         if self.device.type != "cuda" or X.shape[0] == 0:
             return self._cpu(X)
-        with self._lock, torch.cuda.stream(self._stream):
-            xt = torch.from_numpy(X).pin_memory().to(self.device, non_blocking=True)
-            prob, phi, logit = P.predict_shap_raw(xt, self._a, self._c, self.bias, want_logit=True)
-            out = torch.cat([prob[:, None], logit[:, None], phi], 1).cpu()
-        o = out.numpy()
-        return o[:, 0].astype(np.float64), o[:, 1].astype(np.float64), o[:, 2:].astype(np.float64)
+        return self._device_run(X, True)
+
+    def predict_proba(self, X: np.ndarray):
+        """-> (prob [B], logit [B])."""
+        X = self._check(X)
+        if self.device.type != "cuda" or X.shape[0] == 0:
+            p, z, _ = self._cpu(X)
+            return p, z
+        p, z, _ = self._device_run(X, False)
+        return p, z
 
     def _cpu(self, X: np.ndarray):
         Xd = X.astype(np.float64)
@@ -78,13 +294,147 @@ class InferenceEngine:
         phi = self.a[None, : self.d] * (Xd - self.c[None, : self.d])
         return p, z, phi
 
-    def predict(self, X: np.ndarray):
-        p, _, _ = self.predict_explain(X)
-        return (p > 0.5).astype(np.int64), p
+    def _make_kernel_explainer(self):
+        from ..models.explainers import KernelExplainer
+
+        return KernelExplainer(self.a, self.bias, self.background, nsamples=self.kernel_nsamples or None,
+                               link=self.kernel_link, device=str(self.device))
+
+    def _kernel_device(self, xd, ke):
+        from ..ops.kernelshap import kernelshap
+
+        return kernelshap(xd, ke)
 
     def expected_value(self) -> float:
         """Model output (log-odds) at the background point: logit(x = c) = sum a*c + bias."""
         return float(self.a[: self.d] @ self.c[: self.d] + self.bias)
 
     def health(self) -> bool:
-        return np.all(np.isfinite(self.a)) and np.isfinite(self.bias)
+        return bool(np.all(np.isfinite(self.a)) and np.isfinite(self.bias))
+
+
+class TreeInferenceEngine(_EngineBase):
+    """GBDT family: standardize -> tree ensemble (fdx-gbdt/1 JSON, no pickle)."""
+
+    kind = "gbdt"
+    methods = ("kernel",)
+    default_method = "kernel"
+
+    def __init__(self, ensemble, mean, var, scale, feature_names, device: str = "auto", source: str = "local",
+                 background: np.ndarray | None = None, kernel_nsamples: int = 0, kernel_link: str = "identity",
+                 n_samples_seen: int = 0):
+        from ..ops.scaler import stats_from_numpy
+
+        self.ens = ensemble
+        self.mean = np.asarray(mean, np.float64)
+        self.var = np.asarray(var, np.float64)
+        self.scale = np.asarray(scale, np.float64)
+        self.d = len(self.mean)
+        if ensemble.n_features != self.d:
+            raise ValueError(f"ensemble has {ensemble.n_features} features, scaler {self.d}")
+        self.feature_names = list(feature_names)
+        self.n_samples_seen = n_samples_seen
+        super().__init__(device, source, background, kernel_nsamples, kernel_link)
+        self._stats = stats_from_numpy(self.mean, self.scale, device=self.device)
+        if self.device.type == "cuda":
+            from ..ops.gbdt import DeviceEnsemble
+
+            self._dens = DeviceEnsemble(ensemble, self.device)
+            self._stage = _Staging(self.device, self.d, 1)
+
+    @classmethod
+    def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto", source="local",
+                   **kw) -> "TreeInferenceEngine":
+        import joblib
+
+        from ..compat.sklearn_export import FEATURE_NAMES, _is_ours
+        from ..compat import safe_joblib
+        from ..ops.gbdt import TreeEnsemble
+
+        model_path = model_path or os.getenv("MODEL_PATH", "./models/xgb_model.json")
+        mdir = os.path.dirname(os.path.abspath(model_path))
+        scaler_path = scaler_path or os.path.join(mdir, "scaler.joblib")
+        features_path = features_path or os.path.join(mdir, "feature_names.json")
+        with open(model_path) as f:
+            o = json.load(f)
+        ens = TreeEnsemble.from_dict(o)
+        if _is_ours(mdir) or source == "mlflow":
+            sc = joblib.load(scaler_path)
+            mean, var, scale, nss = sc.mean_, sc.var_, sc.scale_, int(np.ravel(sc.n_samples_seen_)[0])
+        else:
+            s = safe_joblib.decode_scaler(scaler_path)
+            mean, var, scale, nss = s["mean_"], s["var_"], s["scale_"], s["n_samples_seen"]
+        names = o.get("feature_names")
+        if not names and features_path and os.path.exists(features_path):
+            with open(features_path) as f:
+                names = json.load(f)
+        return cls(ens, mean, var, scale, names or FEATURE_NAMES[: len(mean)], device=device, source=source,
+                   background=load_background(mdir), n_samples_seen=nss, **kw)
+
+    def predict_proba(self, X: np.ndarray):
+        """-> (prob [B], margin [B])."""
+        X = self._check(X)
+        if self.device.type != "cuda" or X.shape[0] == 0:
+            from ..models.explainers import _standardize
+            from ..ops import reference_gbdt as RG
+
+            e = self.ens
+            m = RG.predict_margin(_standardize(X, self.mean, self.scale), e.feat, e.thr, e.leaf, e.depth,
+                                  e.base_margin).astype(np.float64)
+            return 1.0 / (1.0 + np.exp(-m)), m
+        from ..ops import gbdt as gb
+        from ..ops.scaler import scale_cast
+
+        n = X.shape[0]
+        with self._lock, torch.cuda.stream(self._stream):
+            st = self._stage
+            xd = st.upload(X)
+            with _KernelTimer("gbdt_predict") as kt:
+                rows = scale_cast(xd, self._stats, out_dtype="f32")
+                margin = gb.predict_margin(rows[:, : self.d], self.ens, self._dens)
+            st.dout[:n].copy_(margin)
+            m = st.download(n).astype(np.float64)
+            kt.observe()
+        return 1.0 / (1.0 + np.exp(-m)), m
+
+    def predict_explain(self, X: np.ndarray):
+        """(prob, margin, phi) with KernelSHAP phi (the only explainer of a tree model here)."""
+        e = self.explain(X, "kernel")
+        return e.prob, e.logit, e.phi
+
+    def _make_kernel_explainer(self):
+        from ..models.explainers import TreeKernelExplainer
+
+        return TreeKernelExplainer(self.ens, self.mean, self.scale, self.background,
+                                   nsamples=self.kernel_nsamples or None, link=self.kernel_link,
+                                   device=str(self.device))
+
+    def _kernel_device(self, xd, ke):
+        from ..ops.kernelshap import kernelshap_tree
+
+        return kernelshap_tree(xd, ke)
+
+    def expected_value(self) -> float:
+        return float(self.ens.base_margin)
+
+    def health(self) -> bool:
+        return bool(np.all(np.isfinite(self.ens.leaf)))
+
+
+def load_engine_dir(model_dir: str, device="auto", source: str = "local", **kw) -> _EngineBase:
+    """Engine for a model directory (local artifacts or a resolved MLflow model dir): GBDT when an
+    fdx-gbdt JSON is present (xgb_model.json), else the linear joblib layout (model.pkl for
+    MLflow's sklearn flavour, logistic_model.joblib locally)."""
+    for name in ("xgb_model.json",):
+        p = os.path.join(model_dir, name)
+        if os.path.exists(p):
+            return TreeInferenceEngine.from_paths(p, os.path.join(model_dir, "scaler.joblib"),
+                                                  os.path.join(model_dir, "feature_names.json"), device, source, **kw)
+    for name in ("model.pkl", "logistic_model.joblib"):
+        p = os.path.join(model_dir, name)
+        if os.path.exists(p):
+            art = load_artifacts(p, os.path.join(model_dir, "scaler.joblib"),
+                                 os.path.join(model_dir, "feature_names.json"),
+                                 trusted=True if source == "mlflow" else None)
+            return InferenceEngine(art, device=device, source=source, background=load_background(model_dir), **kw)
+    raise FileNotFoundError(f"no model artifacts in {model_dir}")

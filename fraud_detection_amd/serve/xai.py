@@ -1,10 +1,15 @@
 """Async explainability service behind task ``xai_tasks.compute_shap`` (reference: xai_tasks.py:63-167,
 dead duplicate api/worker.py:65-102).
 
-One worker lease = one fused device launch: every leased task's features are stacked into one
-[B, 30] matrix and scored + explained by the predict/LinearSHAP kernel (K5/K6), then all rows
-are upserted in one DB transaction into BOTH ``transaction_results`` (status COMPLETED,
-prediction_score, shap_values) and ``shap_explanations`` (what /explain reads).
+One worker lease = one batched device explanation: every leased task's features are stacked into
+one [B, 30] matrix, scored, and explained -- by KernelSHAP (BASELINE config 4: the MFMA coalition
+GEMM for the linear model, the masked-row tree kernel for GBDT; background = the training rows
+saved with the model) or LinearSHAP (fused predict + phi kernel) when ``FDX_XAI_METHOD=linear`` or
+no background exists -- then all rows are upserted in one DB transaction into BOTH
+``transaction_results`` (status COMPLETED, prediction_score, shap_values) and
+``shap_explanations`` (what /explain reads, with the explainer and its base value).  The model is
+the one the API serves: the registry alias, else the local artifacts (either family).  Scaling
+out: one worker process per GPU (``worker --gpus N``) leasing disjoint batches.
 
 Fixes relative to the reference: the feature keys the API sends
 (``feature_i``) are mapped positionally; features are standardized (the scaler is folded into
@@ -33,6 +38,8 @@ from ..store import db as store_db
 from ..store.migrations import upgrade
 from ..store.models import ShapExplanation, StatusEnum, TransactionResult
 from ..taskqueue.app import BoundTask, MaxRetriesExceededError
+from ..config import Settings
+from ..obs import tracing
 from .engine import InferenceEngine
 
 logger = logging.getLogger("xai")
@@ -42,14 +49,21 @@ _FEATURE_KEY = re.compile(r"^feature_(\d+)$")
 
 class XaiService:
     def __init__(self, engine: InferenceEngine | None = None, db_url: str | None = None, device: str = "auto",
-                 metrics=None):
+                 metrics=None, method: str | None = None, settings: Settings | None = None):
         self._engine = engine
         self._engine_mtime = None
+        self._injected = engine is not None
         self.device = device
         self.db_url = db_url
         self.metrics = metrics
+        self.settings = settings
+        self._method = method
         self._lock = threading.Lock()
         self._db = None
+
+    @property
+    def method(self) -> str:
+        return self._method or os.getenv("FDX_XAI_METHOD", "auto")
 
     # ---- resources ---------------------------------------------------------------------
     def db(self):
@@ -59,11 +73,18 @@ class XaiService:
         return self._db
 
     def engine(self) -> InferenceEngine:
+        """The API's model (registry alias -> local artifacts), reloaded when a local model file
+        changes on disk."""
         with self._lock:
-            path = os.getenv("MODEL_PATH", "./models/logistic_model.joblib")
+            if self._injected:
+                return self._engine
+            st = self.settings or Settings.load()
+            path = st.model_path
             mtime = os.path.getmtime(path) if os.path.exists(path) else None
             if self._engine is None or (self._engine.source == "local" and mtime != self._engine_mtime):
-                self._engine = InferenceEngine.from_paths(path, None, os.getenv("FEATURE_NAMES_PATH"), device=self.device)
+                from .app import load_production_engine
+
+                self._engine, _ = load_production_engine(st, self.device)
                 self._engine_mtime = mtime
             return self._engine
 
@@ -107,15 +128,22 @@ class XaiService:
                 good.append(i)
             except Exception as e:  # noqa: BLE001 - bad payload: this call fails, others proceed
                 results[i] = self._fail_or_retry(task, c, e, countdown=10.0, mark_failed=True)
+        method = ""
         if good:
             X = np.stack(rows)
-            p, _, phi = eng.predict_explain(X)
+            parent = next((calls[i].request.headers.get("traceparent") for i in good
+                           if getattr(calls[i], "request", None) is not None and calls[i].request.headers), None)
+            with tracing.span("xai.compute_shap", parent=parent, batch=len(good)) as sp, \
+                    tracing.roctx_range("xai.explain_batch"):
+                ex = eng.explain(X, self.method)
+                method = ex.method
+                sp["attrs"]["method"] = method
             try:
                 self._maybe_inject_db_fault()
-                self._store(calls, good, p, phi, names)
+                self._store(calls, good, ex, names)
                 for j, i in enumerate(good):
                     results[i] = {"transaction_id": str(calls[i].args[0]), "status": "COMPLETED",
-                                  "prediction_score": float(p[j])}
+                                  "prediction_score": float(ex.prob[j]), "explainer": method}
             except SQLAlchemyError as e:
                 logger.error("Database error for %d explanations: %s", len(good), e)
                 for i in good:
@@ -144,7 +172,8 @@ class XaiService:
             if random.random() < float(f.split("=", 1)[1]):
                 raise OperationalError("injected fault", None, Exception("FDX_FAULT"))
 
-    def _store(self, calls, good, p, phi, names):
+    def _store(self, calls, good, ex, names):
+        p, phi = ex.prob, ex.phi
         Session = store_db.session_factory(self.db())
         with Session() as s:
             for j, i in enumerate(good):
@@ -164,11 +193,13 @@ class XaiService:
                     rec.shap_values = sv
                     rec.prediction_score = float(p[j])
                     rec.status = StatusEnum.COMPLETED.value
-                ex = s.get(ShapExplanation, tx)
-                if ex is None:
-                    s.add(ShapExplanation(transaction_id=tx, correlation_id=cid, shap_values=sv, feature_names=names))
+                row = s.get(ShapExplanation, tx)
+                if row is None:
+                    s.add(ShapExplanation(transaction_id=tx, correlation_id=cid, shap_values=sv, feature_names=names,
+                                          explainer=ex.method, base_value=float(ex.base_value)))
                 else:
-                    ex.shap_values, ex.correlation_id, ex.feature_names = sv, cid, names
+                    row.shap_values, row.correlation_id, row.feature_names = sv, cid, names
+                    row.explainer, row.base_value = ex.method, float(ex.base_value)
             s.commit()
 
     def _mark_failed(self, tx):

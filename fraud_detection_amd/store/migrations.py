@@ -11,7 +11,7 @@ from __future__ import annotations
 import argparse
 import logging
 
-from sqlalchemy import inspect, select
+from sqlalchemy import inspect, select, text
 from sqlalchemy.engine import Engine
 
 from .db import make_engine
@@ -30,11 +30,26 @@ def _noop(engine: Engine):
     return None
 
 
+def _add_columns(table, cols):
+    """ALTER TABLE ADD COLUMN for the ones a database created before this revision lacks (a table
+    created fresh from the current models already has them)."""
+    def op(engine: Engine):
+        have = {c["name"] for c in inspect(engine).get_columns(table.__tablename__)}
+        with engine.begin() as c:
+            for name in cols:
+                if name not in have:
+                    col = table.__table__.c[name]
+                    c.execute(text(f"ALTER TABLE {table.__tablename__} ADD COLUMN {name} "
+                                   f"{col.type.compile(dialect=engine.dialect)}"))
+    return op
+
+
 REVISIONS = [
     ("0001", "initial transaction_results", _create(TransactionResult)),
     ("291cc0eb137d", "unique constraint on transaction id (primary key already unique)", _noop),
     ("fbae492048d4", "shap_explanations table", _create(ShapExplanation)),
     ("fdx_0004", "durable task queue", _create(TaskRecord)),
+    ("fdx_0005", "shap_explanations.explainer / base_value", _add_columns(ShapExplanation, ["explainer", "base_value"])),
 ]
 
 

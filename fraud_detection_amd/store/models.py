@@ -46,6 +46,8 @@ class ShapExplanation(Base):
     correlation_id: Mapped[str | None] = mapped_column(String(255), nullable=True)
     shap_values: Mapped[dict] = mapped_column(JSONType, nullable=False)
     feature_names: Mapped[list | None] = mapped_column(JSONType, nullable=True)
+    explainer: Mapped[str | None] = mapped_column(String(32), nullable=True)   # linear | kernel (fdx_0005)
+    base_value: Mapped[float | None] = mapped_column(Float, nullable=True)     # E[f] over the background
     created_at = mapped_column(DateTime(timezone=True), server_default=func.current_timestamp())
 
 

@@ -154,14 +154,63 @@ def load_app(spec: str) -> TaskApp:
     return getattr(importlib.import_module(mod), attr or "celery_app")
 
 
+def _spawn_per_gpu(n: int, argv: list[str]) -> int:
+    """One worker process per GPU (the service-level data parallelism of the XAI path, BASELINE
+    config 4): child i sees only GPU i (HIP_VISIBLE_DEVICES, set before it touches HIP) and leases
+    its own disjoint batches from the shared queue.  The parent never initialises the GPU; it
+    forwards SIGTERM/SIGINT and exits with the first non-zero child status."""
+    import subprocess
+    import sys
+
+    rest = []
+    skip = False
+    for i, a in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        if a == "--gpus":
+            skip = True
+            continue
+        if a.startswith("--gpus="):
+            continue
+        rest.append(a)
+    procs = []
+    for g in range(n):
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(g), FDX_DEVICE="cuda:0", FDX_WORKER_RANK=str(g))
+        if "FDX_WORKER_METRICS_PORT" in os.environ or "--metrics-port" not in rest:
+            base = int(os.environ.get("FDX_WORKER_METRICS_PORT", "8001"))
+            env["FDX_WORKER_METRICS_PORT"] = str(base + g)
+        procs.append(subprocess.Popen([sys.executable, "-m", "fraud_detection_amd.taskqueue.worker", *rest], env=env))
+
+    def _fwd(signum, _frame):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+
+    signal.signal(signal.SIGTERM, _fwd)
+    signal.signal(signal.SIGINT, _fwd)
+    rc = 0
+    for p in procs:
+        r = p.wait()
+        rc = rc or r
+    return rc
+
+
 def main(argv=None):
+    import sys
+
+    argv = list(sys.argv[1:] if argv is None else argv)
     ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=int(os.getenv("FDX_WORKER_GPUS", "0")),
+                    help="spawn one worker process per GPU (0 = this process only)")
     ap.add_argument("--app", default="xai_tasks:celery_app")
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--visibility-timeout", type=float, default=60.0)
     ap.add_argument("--metrics-port", type=int, default=int(os.getenv("FDX_WORKER_METRICS_PORT", "8001")))
     ap.add_argument("--max-idle", type=float, default=None)
     a = ap.parse_args(argv)
+    if a.gpus and a.gpus > 1:
+        return _spawn_per_gpu(a.gpus, argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
     app = load_app(a.app)
     from ..obs.metrics import worker_metrics, start_metrics_server
@@ -177,4 +226,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main() or 0)

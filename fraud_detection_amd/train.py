@@ -132,6 +132,11 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         comm.barrier()
         return {"test_auc": float(auc), "cv_scores": cv_scores, "rank": comm.rank}
     paths = _save(model_type, res, names, model_dir, cfg)
+    # KernelSHAP background (shap.sample of the training rows) for the async XAI worker
+    from .serve.engine import sample_background, save_background
+
+    paths["background"] = save_background(sample_background(Xtr[: 1 << 20].cpu().numpy(), s.kernelshap_background,
+                                                            s.seed), model_dir)
     say(f" Model and scaler saved to /{model_dir}")
     summary = {"test_auc": float(auc), "cv_auc_mean": float(np.mean(cv_scores)) if cv_scores else None,
                "cv_auc_std": float(np.std(cv_scores)) if cv_scores else None, "cv_scores": cv_scores,
@@ -261,9 +266,10 @@ def _track(s: Settings, model_type, res, summary, paths, Xte, names, say):
             model = make_logistic(res.coef, res.intercept, res.fit.n_iter)
             sc = (sample - res.scaler.numpy()[0]) / res.scaler.numpy()[2]
             sig = mlf.infer_signature(sc, model.predict_proba(sc)[:, 1])
-            uri = mlf.log_sklearn_model(model, "model", signature=sig, input_example=sc[:1],
-                                        extra_files={"scaler.joblib": paths["scaler"],
-                                                     "feature_names.json": paths["feature_names"]})
+            extra = {"scaler.joblib": paths["scaler"], "feature_names.json": paths["feature_names"]}
+            if paths.get("background"):
+                extra["shap_background.npy"] = paths["background"]
+            uri = mlf.log_sklearn_model(model, "model", signature=sig, input_example=sc[:1], extra_files=extra)
         else:
             uri = res.log_model(mlf, paths)
         mlf.log_artifact(paths["scaler"])

@@ -90,9 +90,9 @@ def test_heartbeat_extends_long_batch(tmp_path):
 def test_retry_countdown_and_max_retries(q):
     tid = q.send("t.x", max_retries=2)
     q.lease("w", 1, 30)
-    assert q.retry(tid, countdown=0.2) == "QUEUED"
+    assert q.retry(tid, countdown=1.5) == "QUEUED"
     assert q.lease("w", 1, 30) == []              # not before eta
-    time.sleep(0.25)
+    time.sleep(1.6)
     assert len(q.lease("w", 1, 30)) == 1
     assert q.retry(tid, 0) == "QUEUED"
     q.lease("w", 1, 30)
