@@ -41,8 +41,9 @@ def parse():
     ap.add_argument("--rows-per-gpu", type=int, default=10_000_000)
     ap.add_argument("--solver", default="newton", choices=["newton", "sgd"])
     ap.add_argument("--storage", default="bf16", choices=["bf16", "fp8"])
-    ap.add_argument("--smote-scope", default="auto", choices=["auto", "global", "shard"],
-                    help="SMOTE neighbour set under DP; auto = shard for N > 1 (identical at N = 1)")
+    ap.add_argument("--smote-scope", default="global", choices=["global", "shard"],
+                    help="SMOTE under DP: global = exactly the single-process SMOTE (default), "
+                         "shard = per-partition oversampling")
     ap.add_argument("--no-extras", action="store_true", help="skip the post-timing AUC/SHAP measurements")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
@@ -77,7 +78,7 @@ def main():
     X, y = separable(n_train, seed=1000 + rank, device=dev)
     Xt, yt = separable(n_test, seed=5000 + rank, device=dev)
 
-    scope = args.smote_scope if args.smote_scope != "auto" else ("shard" if world > 1 else "global")
+    scope = args.smote_scope
     cfg = TrainConfig(solver=args.solver, storage=args.storage, seed=42, smote_scope=scope)
     pipe = DevicePipeline(cfg, comm)
     rng = np.random.default_rng(7)
@@ -102,6 +103,7 @@ def main():
     if comm:
         elapsed = comm.max_over_ranks(elapsed)
     ms_per_step = 1000.0 * elapsed / max(args.steps, 1)
+    coll = comm.collective_summary() if comm else {}
     rows_local = res.n_train_rows
     rows_global = comm.all_reduce_scalar(float(rows_local)) if comm else float(rows_local)
     raw_global = comm.all_reduce_scalar(float(n_train)) if comm else float(n_train)
@@ -117,6 +119,9 @@ def main():
         prof = pipe.fit(X, y, profile=True)
         extras["phase_ms"] = {k: round(v * 1000, 3) for k, v in prof.timings.items()}
         extras.update(_shap_throughput(res, dev, comm))
+        extras.update(_variants(args, X, y, Xt, yt, dev, comm, scope))
+        extras.update(_end_to_end(X, y, Xt, yt, cfg, dev, comm))
+        extras.update(_worker_kernelshap(res, X, dev, comm))
     out = {
         "metric": "train_rows_per_sec (SMOTE k-NN + logistic fit, post-SMOTE rows/s, whole job); AUC; SHAP values/s",
         "value": round(value, 1),
@@ -140,6 +145,8 @@ def main():
             "smote_scope": scope,
         },
     }
+    if coll:
+        out["collectives_timed_region"] = {k: v for k, v in coll.items()}
     out.update(extras)
     if rank == 0:
         line = json.dumps(out)
@@ -150,6 +157,101 @@ def main():
     if comm:
         comm.close()
     return 0
+
+
+def _timed_fits(pipe, X, y, dev, comm, reps=3):
+    for _ in range(1):
+        pipe.fit(X, y)
+    if comm:
+        comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    r = None
+    for _ in range(reps):
+        r = pipe.fit(X, y)
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    return r, (comm.max_over_ranks(dt) if comm else dt)
+
+
+def _variants(args, X, y, Xt, yt, dev, comm, scope) -> dict:
+    """Config 3 names the SGD solver and config 5 fp8 rows: ms/fit + AUC of those variants in the
+    same run (the headline step above is the bf16 Newton fit)."""
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    out = {}
+    for name, kw in (("sgd_bf16", dict(solver="sgd", storage="bf16")), ("newton_fp8", dict(solver="newton", storage="fp8"))):
+        if kw["solver"] == args.solver and kw["storage"] == args.storage:
+            continue
+        pipe = DevicePipeline(TrainConfig(seed=42, smote_scope=scope, **kw), comm)
+        r, dt = _timed_fits(pipe, X, y, dev, comm)
+        rows = comm.all_reduce_scalar(float(r.n_train_rows)) if comm else float(r.n_train_rows)
+        out[name] = {"ms_per_fit": round(dt * 1e3, 4), "rows_per_sec": round(rows / dt, 1),
+                     "auc": round(evaluate(r, Xt, yt, comm)["auc"], 6)}
+    return out
+
+
+def _end_to_end(X, y, Xt, yt, cfg, dev, comm) -> dict:
+    """BASELINE.md §3 end-to-end pipeline: raw rows in host memory (the parsed CSV, pinned) ->
+    upload -> scaler + SMOTE + fit -> exact test AUC, wall clock of the whole chain."""
+    from fraud_detection_amd.models.pipeline import DevicePipeline, evaluate
+
+    Xh, yh = X.cpu().pin_memory(), y.cpu().pin_memory()
+    Xth, yth = Xt.cpu().pin_memory(), yt.cpu().pin_memory()
+    pipe = DevicePipeline(cfg, comm)
+
+    def chain():
+        Xd, yd = Xh.to(dev, non_blocking=True), yh.to(dev, non_blocking=True)
+        Xtd, ytd = Xth.to(dev, non_blocking=True), yth.to(dev, non_blocking=True)
+        r = pipe.fit(Xd, yd)
+        return evaluate(r, Xtd, ytd, comm)["auc"]
+
+    chain()
+    if comm:
+        comm.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        auc = chain()
+    torch.cuda.synchronize(dev)
+    dt = (time.perf_counter() - t0) / reps
+    if comm:
+        dt = comm.max_over_ranks(dt)
+    raw = float(X.shape[0] + Xt.shape[0])
+    raw = comm.all_reduce_scalar(raw) if comm else raw
+    return {"end_to_end": {"ms": round(dt * 1e3, 3), "raw_rows_per_sec": round(raw / dt, 1), "auc": round(auc, 6),
+                           "includes": "host->device upload of raw train+test rows, scaler, SMOTE, fit, exact AUC"}}
+
+
+def _worker_kernelshap(res, X, dev, comm) -> dict:
+    """BASELINE config 4 as the async worker runs it: InferenceEngine.explain on a 1k-explanation
+    lease from host memory (upload, predict, KernelSHAP MFMA coalition GEMM, download)."""
+    from fraud_detection_amd.compat.sklearn_export import LinearArtifacts
+    from fraud_detection_amd.serve.engine import InferenceEngine, sample_background
+
+    mean, var, scale = res.scaler.numpy()
+    art = LinearArtifacts(coef=res.coef, intercept=res.intercept, mean=mean, var=var, scale=scale,
+                          n_samples_seen=int(res.scaler.n), feature_names=[f"f{i}" for i in range(len(mean))])
+    Xh = X[:200_000].cpu().numpy()
+    eng = InferenceEngine(art, device=dev, background=sample_background(Xh, 100))
+    lease = Xh[1000:2000]
+    for _ in range(3):
+        eng.explain(lease, "kernel")
+    if comm:
+        comm.barrier()
+    t0 = time.perf_counter()
+    reps = 10
+    for _ in range(reps):
+        ex = eng.explain(lease, "kernel")
+    dt = (time.perf_counter() - t0) / reps
+    if comm:
+        dt = comm.max_over_ranks(dt)
+    world = comm.world_size if comm else 1
+    err = float(abs(ex.phi.sum(1) - (ex.prob - ex.base_value)).max())
+    return {"kernelshap_worker_values_per_sec": round(1000 * 30 * world / dt, 1),
+            "kernelshap_worker": {"explanations_per_lease": 1000, "ms_per_lease": round(dt * 1e3, 3),
+                                  "efficiency_max_err": err, "per_gpu_worker_processes": world}}
 
 
 def _shap_throughput(res, dev, comm) -> dict:

@@ -149,10 +149,11 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("smote_parents", [](u C, int64_t m_rows, u aff, u out, u s) {
     fdx::launch_smote_parents(P<const float>(C), m_rows, P<const double>(aff), P<uint16_t>(out), S(s));
   });
-  m.def("smote_generate", [](u C, int parents_bf16, u nbr, int mq, int k, int64_t q_off, int64_t n_new, uint64_t seed,
-                             uint64_t counter_base, float label, int out_kind, float out_scale, u aff, u out, u s) {
-    fdx::launch_smote_generate(P<const void>(C), parents_bf16, P<const int>(nbr), mq, k, q_off, n_new, seed,
-                               counter_base, label, out_kind, out_scale, P<const double>(aff), P<void>(out), S(s));
+  m.def("smote_generate", [](u C, int parents_bf16, u nbr, int mq, int k, int64_t q_off, int64_t n_new,
+                             int64_t sample_offset, uint64_t seed, uint64_t counter_base, float label, int out_kind,
+                             float out_scale, u aff, u out, u s) {
+    fdx::launch_smote_generate(P<const void>(C), parents_bf16, P<const int>(nbr), mq, k, q_off, n_new, sample_offset,
+                               seed, counter_base, label, out_kind, out_scale, P<const double>(aff), P<void>(out), S(s));
   });
 
   // kernelshap

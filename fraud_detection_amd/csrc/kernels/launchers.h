@@ -115,7 +115,7 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
 void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t* P, hipStream_t stream);
 // C: fp32 standardized parents (+ aff applied per sample) or, parents_bf16, smote_parents output
 void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int mq, int k, int64_t q_offset,
-                           int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
+                           int64_t n_new, int64_t sample_offset, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream);
 
 // ---- auc.hip ----

@@ -8,7 +8,10 @@
 // samples (in 128-sample block m, counter (64 m + L, counter_base) serves samples 128 m + L and
 // 128 m + 64 + L; common.h smote_pack_draw), so the output is independent of launch geometry and
 // the CPU oracle (ops/reference.py smote_plan) reproduces it bit for bit before the bf16
-// rounding.  Row indices are packed in 24 bits: the host refuses parent sets >= 2^24 rows
+// rounding.  ``sample_offset`` (a multiple of 128) places this launch's samples at global sample
+// indices [sample_offset, sample_offset + n_new): data-parallel ranks each generate a 128-aligned
+// slice of ONE global draw sequence, so the union equals the single-process output exactly.
+// Row indices are packed in 24 bits: the host refuses parent sets >= 2^24 rows
 // (ops/reference.py smote_check_ranges).
 //
 // MI355X mapping: write-bound stream.  4 lanes per synthetic row, 8 columns (two 16 B gathers of
@@ -29,7 +32,7 @@ constexpr int kThreads = 256;
 template <int OUT, bool NT = false, bool PB = false>
 __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     const void* __restrict__ Cv, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
-    int64_t n_new, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
+    int64_t n_new, int64_t s_off, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
     float out_scale, const double* __restrict__ aff, void* __restrict__ out) {
 #pragma clang fp contract(off)  // affine map = mul then add (the oracle); the interpolation is an explicit fmaf
   const int lane = lane_id();
@@ -55,7 +58,7 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   // issued behind this iteration's first row gathers, so the dependent nbr -> row chain costs one
   // memory latency per iteration instead of two.
   auto draw2 = [&](int64_t b, int (&di)[2], int (&dj)[2], float (&dl)[2]) {
-    const int64_t c = (b >> 1) + lane;  // b is a multiple of 128
+    const int64_t c = ((s_off + b) >> 1) + lane;  // s_off and b are multiples of 128
     const Philox4 r = philox4x32_10((uint32_t)c, (uint32_t)(c >> 32), cb0, cb1, key0, key1);
     const uint32_t wp[2] = {r.x, r.z}, wl[2] = {r.y, r.w};
 #pragma unroll
@@ -177,9 +180,11 @@ void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t
 }
 
 void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int mq, int k, int64_t q_offset,
-                           int64_t n_new, uint64_t seed, uint64_t counter_base, float label,
+                           int64_t n_new, int64_t sample_offset, uint64_t seed, uint64_t counter_base, float label,
                            int out_kind, float out_scale, const double* aff, void* out, hipStream_t stream) {
   if (n_new <= 0) return;
+  if (sample_offset < 0 || (sample_offset & 127) != 0)
+    throw std::runtime_error("smote_generate: sample_offset must be a non-negative multiple of 128");
   const int64_t per_block = (kThreads / kWave) * 128;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
@@ -187,7 +192,7 @@ void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int 
   do {                                                                                                \
     static const int cap = resident_cap(smote_generate_kernel<O, NT, PB>, kThreads);                  \
     smote_generate_kernel<O, NT, PB><<<capped_grid(n_new, per_block, cap), kThreads, 0, stream>>>(    \
-        C, nbr, mq, k, q_offset, n_new, k0, k1, c0, c1, label, out_scale, aff, out);                  \
+        C, nbr, mq, k, q_offset, n_new, sample_offset, k0, k1, c0, c1, label, out_scale, aff, out);   \
   } while (0)
   const bool pb = parents_bf16 != 0;
   if (out_kind == 0 && nt_stores()) { if (pb) FDX_SG(0, true, true); else FDX_SG(0, true, false); }

@@ -23,7 +23,7 @@ from ..ops import knn as knn_ops
 from ..ops import metrics as metric_ops
 from ..ops import scaler as scaler_ops
 from ..ops.layout import NCOLS
-from .pipeline import TrainConfig
+from .pipeline import TrainConfig, global_smote_slices
 
 MODEL_FILE = "xgb_model.json"
 
@@ -211,21 +211,34 @@ class GBDTPipeline:
             spw = neg / pos if pos > 0 else 1.0
         else:
             spw = float(self.spw)
-        n_new = max(0, int(round(n_maj * cfg.sampling_ratio)) - n_min) if (cfg.smote and n_min > 0) else 0
+        def quota(n_r, nmin_r):
+            return max(0, int(round((n_r - nmin_r) * cfg.sampling_ratio)) - nmin_r) if (cfg.smote and nmin_r > 0) else 0
+
+        # SMOTE: single process, or under DP the exact global scheme of models/pipeline.py (every
+        # rank a 128-aligned slice of one global draw sequence over all minority rows)
+        ranks = comm.all_gather_ints([n_min, n]) if comm else [[n_min, n]]
+        if comm:
+            per, s_off = global_smote_slices(ranks, quota, rank)
+        else:
+            per, s_off = [quota(n, n_min)], 0
+        n_new = per[rank]
         rows = torch.empty((n + n_new, NCOLS), dtype=torch.float32, device=X.device)
         scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", out=rows[:n])
-        if n_new > 0:
+        if sum(per) > 0:
             xmin = rows[:n].index_select(0, idx_min).contiguous()
-            if comm:
-                xall, counts = comm.all_gather_rows(xmin)
-                q_off = int(sum(counts[:rank]))
-            else:
-                xall, q_off = xmin, 0
+            counts = [r[0] for r in ranks]
+            xall = comm.all_gather_rows(xmin, counts=counts)[0] if comm else xmin
+            q_off = int(sum(counts[:rank]))
             k = min(cfg.k_neighbors, xall.shape[0] - 1)
             if k < 1:
                 raise ValueError("SMOTE needs at least 2 minority samples")
-            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off)
-            knn_ops.smote_generate(xall, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank)
+            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off) if n_min > 0 else \
+                torch.empty((0, k), dtype=torch.int32, device=X.device)
+            if comm:
+                nbr = comm.all_gather_rows(nbr, counts=counts)[0]
+            if n_new > 0:
+                knn_ops.smote_generate(xall, nbr, 0, n_new, rows[n:], seed=cfg.seed, counter_base=0,
+                                       sample_offset=s_off)
         labels = torch.empty(n + n_new, dtype=torch.uint8, device=X.device)
         labels[:n] = y
         labels[n:] = 1

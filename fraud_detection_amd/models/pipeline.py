@@ -51,9 +51,11 @@ class TrainConfig:
     check_every: int = 1            # Newton: iterations per convergence-flag read (host reads one chunk behind)
     init_std: float = 0.01          # random-init weights ~ N(0, init_std^2) (seeded by `seed`)
     hess_stride: int | str = "auto"  # Newton: Hessian from every k-th row tile (gradient always exact)
-    # SMOTE neighbour set under data parallelism: "global" = all ranks' minority rows (all-gather;
-    # identical to single-process imblearn on the whole table, k-NN work grows with the world
-    # size), "shard" = each rank's own minority rows (per-partition SMOTE: constant work per rank)
+    # SMOTE under data parallelism: "global" = the single-process result exactly -- every rank
+    # draws a 128-aligned slice of ONE global sample sequence over ALL minority rows and their
+    # global neighbours (all-gather of minority rows C3 and of the k-NN index rows), so the union
+    # of the ranks' synthetic rows equals the one-process SMOTE output bit for bit; "shard" = each
+    # rank oversamples its own minority rows (per-partition SMOTE: constant work per rank)
     smote_scope: str = "global"
 
 
@@ -130,8 +132,8 @@ class DevicePipeline:
         fused = (cfg.fold_scaler and cfg.storage == "bf16" and cfg.solver == "newton" and dev.type == "cuda"
                  and scaler_ops.fused_cast_ok(X))
         # training buffer sized for the largest possible SMOTE output, so the cast does not wait
-        # for the minority count
-        cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) if cfg.smote else 0)
+        # for the minority count (+128: a global-scope slice boundary moves by < 128 rows)
+        cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) + 128 if cfg.smote else 0)
         rows_cap = self._train_buffer(cap, dev)
         if fused:
             # ---- class counts (C2): count kernels first, host reads the total during K1+K2 ----
@@ -149,23 +151,28 @@ class DevicePipeline:
                                   fp8_scale=cfg.fp8_scale)
         idx_min = pending.result()
         n_min = int(idx_min.shape[0])
+        _maybe_fault(rank)
 
         def quota(n_r, nmin_r):
             return max(0, int(round((n_r - nmin_r) * cfg.sampling_ratio)) - nmin_r) if (cfg.smote and nmin_r > 0) else 0
 
-        n_maj = n - n_min
-        n_new = quota(n, n_min)
-        rows = rows_cap[: n + n_new]
         # DP: one small all-gather of (minority, rows) per rank gives every rank the minority
         # counts (for the row all-gather) and every rank's post-SMOTE size (for the identical
         # Newton schedule) -- no further host-synchronising collectives in the fit.
         ranks = comm.all_gather_ints([n_min, n]) if comm is not None else [[n_min, n]]
-        n_sched = min(r[1] + quota(r[1], r[0]) for r in ranks)
+        glob = comm is not None and cfg.smote_scope == "global"
+        if glob:
+            new_per_rank, s_off = global_smote_slices(ranks, quota, rank)
+        else:
+            new_per_rank, s_off = [quota(r[1], r[0]) for r in ranks], 0
+        n_new = new_per_rank[rank]
+        n_sched = min(r[1] + q for r, q in zip(ranks, new_per_rank))
+        rows = rows_cap[: n + n_new]
         tm.mark("scale_cast")
-        if n_new > 0:
+        if sum(new_per_rank) > 0:
             # ---- minority rows in fp32, gathered across ranks (C3) -----------------------
             xmin = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min)
-            if comm is not None and cfg.smote_scope == "global":
+            if glob:
                 xall, counts = comm.all_gather_rows(xmin, counts=[r[0] for r in ranks])
                 q_off = int(sum(counts[:rank]))
             else:
@@ -174,21 +181,27 @@ class DevicePipeline:
             k = min(cfg.k_neighbors, xall.shape[0] - 1)
             if k < 1:
                 raise ValueError("SMOTE needs at least 2 minority samples")
-            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off)
+            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off) if n_min > 0 else \
+                torch.empty((0, k), dtype=torch.int32, device=dev)
+            if glob:  # every rank needs every minority row's neighbour list (int32, k per row)
+                nbr, _ = comm.all_gather_rows(nbr, counts=[r[0] for r in ranks])
+                q_off = 0
             tm.mark("knn")
             # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
             # neighbours found in standardized space are interpolated in shifted coordinates
             # parents in the training rows' space (bf16, pivot-shifted when the scaler is folded):
             # half the gather bytes of fp32 parents and no per-sample affine map
-            parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
-            knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed, counter_base=rank,
-                                   fp8_scale=cfg.fp8_scale)
+            if n_new > 0:
+                parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
+                knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
+                                       counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,
+                                       sample_offset=s_off)
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
         class_w = (1.0, 1.0)
         if cfg.class_weight == "balanced":  # global counts from the exchanged (minority, rows) pairs
-            tot = float(sum(r[1] + quota(r[1], r[0]) for r in ranks))
-            pos = float(sum(r[0] + quota(r[1], r[0]) for r in ranks))
+            tot = float(sum(r[1] + q for r, q in zip(ranks, new_per_rank)))
+            pos = float(sum(r[0] + q for r, q in zip(ranks, new_per_rank)))
             class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         # ---- K4: fit ---------------------------------------------------------------------
         if dev.type == "cuda" and (self._ws is None or self._ws.device != dev):
@@ -211,6 +224,34 @@ class DevicePipeline:
         tm.mark("fit")
         return PipelineResult(scaler=stats, fit=fit, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
                               n_synthetic=n_new, timings=dict(tm.t))
+
+
+def _maybe_fault(rank: int):
+    """FDX_FAULT=dp_rank_crash:<r> makes rank r raise mid-fit (between two collectives) -- the
+    lost-rank drill of tests/test_distributed.py: every rank must exit non-zero, none may hang."""
+    import os
+
+    f = os.environ.get("FDX_FAULT", "")
+    if f.startswith("dp_rank_crash:") and int(f.split(":", 1)[1]) == rank:
+        raise RuntimeError(f"FDX_FAULT: simulated crash of rank {rank} mid-fit")
+
+
+def global_smote_slices(ranks, quota, rank: int):
+    """(rows per rank, this rank's 128-aligned sample offset) for global-scope DP SMOTE: the
+    global quota (one-process formula on the summed counts) is cut at 128-aligned boundaries
+    near each rank's proportional share, so every rank's slice starts on a Philox pair block."""
+    n_g = sum(r[1] for r in ranks)
+    nmin_g = sum(r[0] for r in ranks)
+    total = quota(n_g, nmin_g)
+    shares = [quota(r[1], r[0]) for r in ranks]
+    bounds = [0]
+    acc = 0
+    for s in shares[:-1]:
+        acc += s
+        bounds.append(min(total, max(bounds[-1], 128 * int(round(acc / 128.0)))))
+    bounds.append(total)
+    per = [bounds[i + 1] - bounds[i] for i in range(len(ranks))]
+    return per, bounds[rank]
 
 
 def evaluate(result: PipelineResult, X_test: torch.Tensor, y_test: torch.Tensor, comm=None) -> dict:

@@ -89,13 +89,15 @@ def smote_parents(C: torch.Tensor, affine: torch.Tensor | None = None) -> torch.
 
 def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int, out: torch.Tensor,
                    seed: int = 42, counter_base: int = 0, label: float = 1.0,
-                   fp8_scale: float = DEFAULT_FP8_SCALE, affine: torch.Tensor | None = None) -> torch.Tensor:
+                   fp8_scale: float = DEFAULT_FP8_SCALE, affine: torch.Tensor | None = None,
+                   sample_offset: int = 0) -> torch.Tensor:
     """Write ``n_new`` synthetic rows into ``out`` (a [n_new, 32] bf16/fp32/fp8 view, e.g. the tail of
     the training buffer).  Sample s interpolates minority row (q_offset + i) toward neighbour
     nbr[i, kk] with Philox draws keyed by (seed, s, counter_base).  C: fp32 standardized parents,
     or bf16 parents from smote_parents (already in the output space; ``affine`` must be None).
     ``affine`` ([64] float64, ScalerStats.aff) with fp32 parents: ``out`` holds pivot-shifted rows
-    -- each feature is written as z * sigma + c."""
+    -- each feature is written as z * sigma + c.  ``sample_offset`` (multiple of 128): these are
+    samples [sample_offset, sample_offset + n_new) of one global draw sequence (DP ranks)."""
     if C.dtype not in (torch.float32, torch.bfloat16) or C.dim() != 2 or C.shape[1] != NCOLS:
         raise ValueError("C must be fp32 or bf16 [m, 32]")
     pb = C.dtype == torch.bfloat16
@@ -107,6 +109,8 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
     if q_offset < 0 or q_offset + mq > C.shape[0]:
         raise ValueError("query rows out of range of C")
     ref.smote_check_ranges(C.shape[0], mq, k)
+    if sample_offset < 0 or sample_offset % 128:
+        raise ValueError("sample_offset must be a non-negative multiple of 128")
     check_rows(out, "out")
     if out.shape[0] != n_new:
         raise ValueError("out must have n_new rows")
@@ -117,7 +121,8 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
         nb = nbr.numpy()
         if nb.min() < 0 or nb.max() >= C.shape[0]:
             raise ValueError("neighbour index out of range")
-        rows = ref.smote_generate(C.float().numpy(), nb, q_offset, n_new, seed, counter_base, label)
+        rows = ref.smote_generate(C.float().numpy(), nb, q_offset, n_new, seed, counter_base, label,
+                                  sample_offset=sample_offset)
         if affine is not None:
             a = affine.cpu().numpy()
             sig = (1.0 / a[32:62]).astype(np.float32)
@@ -132,7 +137,8 @@ def smote_generate(C: torch.Tensor, nbr: torch.Tensor, q_offset: int, n_new: int
             out.copy_(torch.from_numpy(ref.fp8_encode(r2)))
         return out
     m = native()
-    m.smote_generate(ptr(C), int(pb), ptr(nbr), mq, k, int(q_offset), int(n_new), int(seed) & (2**64 - 1),
+    m.smote_generate(ptr(C), int(pb), ptr(nbr), mq, k, int(q_offset), int(n_new), int(sample_offset),
+                     int(seed) & (2**64 - 1),
                      int(counter_base) & (2**64 - 1), float(label), DTYPE_KIND[kind], float(fp8_scale),
                      ptr(affine), ptr(out), stream_of(C))
     return out

@@ -320,7 +320,7 @@ def smote_check_ranges(n_parents: int, mq: int, k: int) -> None:
         raise ValueError(f"SMOTE pick range mq*k = {mq}*{k} does not fit 32 bits")
 
 
-def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int) -> np.ndarray:
+def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int, sample_offset: int = 0) -> np.ndarray:
     """uint32 [n_new, 2] SMOTE draws {i | lam_hi << 24, j | lam_lo << 24} (common.h
     smote_pack_draw): one Philox call per pair of samples -- in 128-sample block m, counter
     64 m + L serves sample 128 m + L with words (x, y) and sample 128 m + 64 + L with (z, w); query
@@ -328,7 +328,7 @@ def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int) -> np.
     nbr = np.asarray(nbr)
     mq, k = nbr.shape
     smote_check_ranges(mq, mq, k)
-    s = np.arange(n_new, dtype=np.uint64)
+    s = np.arange(n_new, dtype=np.uint64) + np.uint64(sample_offset)
     c = (s // np.uint64(128)) * np.uint64(64) + (s % np.uint64(64))
     half = ((s % np.uint64(128)) // np.uint64(64)).astype(bool)
     r = philox4x32_10((c & _MASK32).astype(np.uint32), (c >> np.uint64(32)).astype(np.uint32),
@@ -354,11 +354,11 @@ def smote_draws_decode(plan: np.ndarray):
 
 
 def smote_generate(C: np.ndarray, nbr: np.ndarray, q_offset: int, n_new: int, seed: int,
-                   counter_base: int, label: float = 1.0) -> np.ndarray:
+                   counter_base: int, label: float = 1.0, sample_offset: int = 0) -> np.ndarray:
     """fp32 synthetic rows (before bf16/fp8 rounding), bit-exact Philox draws."""
     C = np.asarray(C, dtype=np.float32)
     nbr = np.asarray(nbr)
-    i, j, lam = smote_draws_decode(smote_plan(nbr, n_new, seed, counter_base))
+    i, j, lam = smote_draws_decode(smote_plan(nbr, n_new, seed, counter_base, sample_offset))
     lam = lam[:, None]
     xi = C[q_offset + i]
     xj = C[j]

@@ -13,14 +13,72 @@ One process per GPU.  Backends:
 All payloads in this framework are tiny (<= 8.5 KB per Newton iteration) except the SMOTE
 minority all-gather, so the API is shaped for latency: one fused buffer per step, in-place
 all-reduce on the current stream.
+
+Ordering contract between the two communicators on one GPU (torch ProcessGroup for barriers,
+scalars and gathers; the native RCCL communicator for the hot device all-reduces): both are only
+ever driven from this class, in program order, from one host thread per rank.  The native
+collectives run on the current compute stream; a ProcessGroup collective waits for the current
+stream before it starts and (synchronous ops) makes the current stream wait for its completion.
+So on every rank the device executes ONE total order of collectives -- the program order -- and
+since every rank runs the same control flow, all ranks issue the same sequence: no cross-
+communicator deadlock is possible.  ``FDX_COMM_TRACE=1`` records that sequence per rank
+(``trace``), and tests/test_distributed.py asserts it is identical on every rank.
+
+Every collective is timed (HIP events on the stream it runs on, host clock for gloo) and
+observed in ``fdx_allreduce_seconds{op}``; ``collective_summary()`` gives the per-op breakdown
+bench.py reports under DP.
 """
 from __future__ import annotations
 
+import contextlib
 import os
+import time
 from datetime import timedelta
 
 import torch
 import torch.distributed as dist
+
+
+class CollectiveStats:
+    """Per-op count / bytes / total and max seconds.  Device-timed entries are resolved lazily
+    (their events complete asynchronously); ``summary()`` synchronises and resolves them."""
+
+    def __init__(self):
+        self.pending = []
+        self.acc: dict = {}
+
+    def _add(self, op: str, nbytes: int, sec: float):
+        a = self.acc.setdefault(op, [0, 0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += nbytes
+        a[2] += sec
+        a[3] = max(a[3], sec)
+        try:
+            from ..obs.metrics import train_metrics
+
+            train_metrics().allreduce_seconds.labels(op).observe(sec)
+        except Exception:  # noqa: BLE001 - metrics are best effort
+            pass
+
+    def resolve(self, block: bool = False):
+        keep = []
+        for op, nbytes, e0, e1 in self.pending:
+            if block or e1.query():
+                self._add(op, nbytes, e0.elapsed_time(e1) / 1e3)
+            else:
+                keep.append((op, nbytes, e0, e1))
+        self.pending = keep
+
+    def summary(self) -> dict:
+        if self.pending:
+            torch.cuda.synchronize()
+            self.resolve(block=True)
+        return {op: {"count": a[0], "bytes": a[1], "total_ms": round(a[2] * 1e3, 4),
+                     "mean_us": round(a[2] / max(a[0], 1) * 1e6, 2), "max_us": round(a[3] * 1e6, 2)}
+                for op, a in sorted(self.acc.items())}
+
+    def reset(self):
+        self.pending, self.acc = [], {}
 
 
 class Communicator:
@@ -47,6 +105,9 @@ class Communicator:
             self.rank = 0
             self.backend = "single"
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.stats = CollectiveStats()
+        self._timing = os.environ.get("FDX_COMM_TIMING", "1") == "1"
+        self.trace = [] if os.environ.get("FDX_COMM_TRACE", "0") == "1" else None
         self._native = None
         mode = os.environ.get("FDX_COMM", "auto")  # auto | rccl | torch
         if self.world_size > 1 and self.backend == "nccl" and mode in ("auto", "rccl") and torch.cuda.is_available():
@@ -97,13 +158,40 @@ class Communicator:
     def native_rccl(self) -> bool:
         return self._native is not None
 
+    # ---- instrumentation ---------------------------------------------------------------
+    @contextlib.contextmanager
+    def _timed(self, op: str, t: torch.Tensor | None = None, path: str = ""):
+        nbytes = 0 if t is None else t.numel() * t.element_size()
+        if self.trace is not None:
+            self.trace.append((op, path, nbytes))
+        if not self._timing or self.world_size == 1:
+            yield
+            return
+        if t is not None and t.is_cuda and path in ("rccl", "nccl"):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            yield
+            e1.record()
+            self.stats.pending.append((op, nbytes, e0, e1))
+            if len(self.stats.pending) > 1024:
+                self.stats.resolve()
+        else:
+            t0 = time.perf_counter()
+            yield
+            self.stats._add(op, nbytes, time.perf_counter() - t0)
+
+    def collective_summary(self) -> dict:
+        return self.stats.summary()
+
     # ---- basic collectives -------------------------------------------------------------
     def barrier(self):
         if self.world_size > 1:
-            if self.backend == "nccl" and torch.cuda.is_available():
-                dist.barrier(device_ids=[torch.cuda.current_device()])
-            else:
-                dist.barrier()
+            with self._timed("barrier", None, self.backend):
+                if self.backend == "nccl" and torch.cuda.is_available():
+                    dist.barrier(device_ids=[torch.cuda.current_device()])
+                else:
+                    dist.barrier()
 
     def _host_staged(self, t: torch.Tensor) -> bool:
         # gloo moves CUDA tensors through host memory (tests run several ranks on one GPU)
@@ -113,15 +201,22 @@ class Communicator:
         if self.world_size == 1:
             return t
         if self._native is not None and t.is_cuda and op == "sum":
-            self._native.all_reduce_(t)
+            path = "rccl"
+        elif self._host_staged(t):
+            path = "gloo-staged"
+        else:
+            path = self.backend
+        with self._timed(f"all_reduce_{op}", t, path):
+            if self._native is not None and t.is_cuda and op == "sum":
+                self._native.all_reduce_(t)
+                return t
+            if self._host_staged(t):
+                h = t.cpu()
+                dist.all_reduce(h, op=_op(op))
+                t.copy_(h)
+                return t
+            dist.all_reduce(t, op=_op(op))
             return t
-        if self._host_staged(t):
-            h = t.cpu()
-            dist.all_reduce(h, op=_op(op))
-            t.copy_(h)
-            return t
-        dist.all_reduce(t, op=_op(op))
-        return t
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         return self.all_reduce_(t.clone(), op)
@@ -131,18 +226,20 @@ class Communicator:
             return x
         dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=_op(op))
-        return float(t.item())
+        with self._timed(f"all_reduce_scalar_{op}", None, self.backend):
+            dist.all_reduce(t, op=_op(op))
+            return float(t.item())
 
     def broadcast(self, t: torch.Tensor, src: int = 0) -> torch.Tensor:
         if self.world_size > 1:
             t = t.contiguous()
-            if self._host_staged(t):
-                h = t.cpu()
-                dist.broadcast(h, src=src)
-                t.copy_(h)
-            else:
-                dist.broadcast(t, src=src)
+            with self._timed("broadcast", t, "gloo-staged" if self._host_staged(t) else self.backend):
+                if self._host_staged(t):
+                    h = t.cpu()
+                    dist.broadcast(h, src=src)
+                    t.copy_(h)
+                else:
+                    dist.broadcast(t, src=src)
         return t
 
     def all_gather_ints(self, vals) -> list:
@@ -152,8 +249,9 @@ class Communicator:
         dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         t = torch.tensor(list(vals), dtype=torch.int64, device=dev)
         out = [torch.zeros_like(t) for _ in range(self.world_size)]
-        dist.all_gather(out, t)
-        return torch.stack(out).cpu().tolist()
+        with self._timed("all_gather_ints", None, self.backend):
+            dist.all_gather(out, t)
+            return torch.stack(out).cpu().tolist()
 
     def all_gather_rows(self, x: torch.Tensor, counts: list | None = None):
         """Variable-length all-gather along dim 0 (collective C3, SMOTE minority rows).
@@ -162,8 +260,13 @@ class Communicator:
         if self.world_size == 1:
             return x, [x.shape[0]]
         if self._host_staged(x):
-            out, c = self.all_gather_rows(x.cpu(), counts)
-            return out.to(x.device), c
+            with self._timed("all_gather_rows_staged", x, "gloo-staged"):
+                out, c = self._all_gather_rows(x.cpu(), counts)
+                return out.to(x.device), c
+        with self._timed("all_gather_rows", x, self.backend):
+            return self._all_gather_rows(x, counts)
+
+    def _all_gather_rows(self, x: torch.Tensor, counts: list | None):
         dev = x.device
         if counts is None:
             n = torch.tensor([x.shape[0]], dtype=torch.int64, device=dev)
@@ -209,5 +312,6 @@ def single() -> Communicator:
     if _SINGLE is None:
         c = Communicator.__new__(Communicator)
         c.world_size, c.rank, c.local_rank, c.backend, c._native, c.initialized_here = 1, 0, 0, "single", None, False
+        c.stats, c._timing, c.trace = CollectiveStats(), False, None
         _SINGLE = c
     return _SINGLE

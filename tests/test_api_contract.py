@@ -34,9 +34,11 @@ def svc(tmp_path, monkeypatch):
     from fraud_detection_amd.config import Settings
 
     s = Settings.load(database_url=url, mlflow_tracking_uri=f"file:{tmp_path}/mlruns", device="cpu")
+    xai_tasks.service.settings, xai_tasks.service._engine, xai_tasks.service._injected = s, None, False
     app = create_app(s, task_app=xai_tasks.celery_app, db_engine=make_engine(url))
     with TestClient(app) as c:
         yield c, xai_tasks, q
+    xai_tasks.service.settings, xai_tasks.service._engine = None, None
 
 
 def test_predict_contract_and_golden(svc):

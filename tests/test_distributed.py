@@ -3,8 +3,12 @@
 The DP pipeline (sharded rows; all-reduced scaler sums C1, all-gathered minority rows C3,
 all-reduced Newton gradient/Hessian C5, gathered test scores for the exact AUC) must match the
 single-process computation on the concatenated data."""
+import json
 import os
 import socket
+import subprocess
+import sys
+import time
 
 import numpy as np
 import pytest
@@ -22,7 +26,7 @@ def _free_port() -> int:
 
 def _worker(rank, world, port, out_dir, smote, scope="global"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK=str(rank))
+                      LOCAL_RANK=str(rank), FDX_COMM_TRACE="1")
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
     from fraud_detection_amd.parallel.comm import Communicator
@@ -37,7 +41,8 @@ def _worker(rank, world, port, out_dir, smote, scope="global"):
     ev = evaluate(res, Xt[sht].contiguous(), yt[sht].contiguous(), comm)
     mean, var, scale = res.scaler.numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), w=res.w, mean=mean, var=var, auc=ev["auc"],
-             n_train=res.n_train_rows)
+             n_train=res.n_train_rows, trace=np.array([f"{op}|{path}" for op, path, _ in comm.trace]),
+             stats=np.array(json.dumps(comm.collective_summary())))
     comm.barrier()
     comm.close()
 
@@ -70,12 +75,45 @@ def test_dp_with_smote_balances_globally(tmp_path):
     outs = _run(2, True, tmp_path)
     assert np.array_equal(outs[0]["w"], outs[1]["w"])
     assert float(outs[0]["auc"]) > 0.9
-    # each rank oversamples its shard to balance; globally 2 * n_majority rows
+    # the ranks together hold exactly the one-process post-SMOTE table: 2 * n_majority rows
     from fraud_detection_amd.data.synthetic import separable
 
     _, y = separable(24_000, fraud_rate=0.02, seed=100)
-    n_maj = [int((y[r * 12000:(r + 1) * 12000] == 0).sum()) for r in range(2)]
-    assert [int(o["n_train"]) for o in outs] == [2 * m for m in n_maj]
+    assert sum(int(o["n_train"]) for o in outs) == 2 * int((y == 0).sum())
+
+
+@pytest.mark.parametrize("world", [3, 8])
+def test_dp_global_smote_equals_single_process(tmp_path, world):
+    """8-rank readiness: the full pipeline with smote_scope="global" under DP equals
+    the single-process fit -- identical synthetic rows (one global Philox draw sequence, sliced at
+    128-aligned boundaries), so the weights agree up to the all-reduce summation order."""
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    outs = _run(world, True, tmp_path)
+    X, y = separable(24_000, fraud_rate=0.02, seed=100)
+    Xt, yt = separable(8_000, fraud_rate=0.02, seed=200)
+    ref = DevicePipeline(TrainConfig(smote=True, tol=1e-8, init_std=0.0)).fit(X, y)
+    ev = evaluate(ref, Xt, yt)
+    assert sum(int(o["n_train"]) for o in outs) == ref.n_train_rows
+    for o in outs:
+        np.testing.assert_allclose(o["w"], ref.w, atol=1e-7)
+        assert float(o["auc"]) == pytest.approx(ev["auc"], abs=1e-6)
+
+
+def test_global_smote_slices_cover_the_quota():
+    from fraud_detection_amd.models.pipeline import global_smote_slices
+
+    quota = lambda n, m: max(0, (n - m) - m) if m > 0 else 0  # noqa: E731
+    ranks = [[37, 5000], [0, 4000], [90, 6100], [12, 333], [5, 9000], [64, 4096], [1, 10], [40, 7777]]
+    per, offs = zip(*[global_smote_slices(ranks, quota, r) for r in range(len(ranks))])
+    per = per[0]
+    total = quota(sum(r[1] for r in ranks), sum(r[0] for r in ranks))
+    assert sum(per) == total and all(p >= 0 for p in per)
+    assert all(o % 128 == 0 for o in offs) and list(offs) == [sum(per[:r]) for r in range(len(ranks))]
+    # boundaries sit within 64 rows of the cumulative per-rank shares (capped at the global quota)
+    cum = np.cumsum([quota(r[1], r[0]) for r in ranks])[:-1]
+    assert all(abs(o - min(c, total)) <= 64 for o, c in zip(offs[1:], cum))
 
 
 def _knn_worker(rank, world, port, out_dir):
@@ -190,4 +228,36 @@ def test_dp_shard_scope_smote(tmp_path):
 
     _, y = separable(24_000, fraud_rate=0.02, seed=100)
     n_maj = [int((y[r * 12000:(r + 1) * 12000] == 0).sum()) for r in range(2)]
-    assert [int(o["n_train"]) for o in outs] == [2 * m for m in n_maj]
+    assert [int(o["n_train"]) for o in outs] == [2 * m for m in n_maj]   # per-partition quotas
+
+
+def test_collective_order_is_identical_on_every_rank(tmp_path):
+    """The ordering contract of parallel/comm.py: every rank issues the same collective sequence
+    (op, communicator path) -- the property that rules out cross-communicator deadlock -- and
+    every collective is timed (fdx_allreduce_seconds / collective_summary)."""
+    outs = _run(4, True, tmp_path)
+    seqs = [list(o["trace"]) for o in outs]
+    assert len(seqs[0]) > 5 and all(sq == seqs[0] for sq in seqs)
+    st = json.loads(str(outs[0]["stats"]))
+    assert st["all_reduce_sum"]["count"] >= 2 and st["all_gather_rows"]["count"] >= 2
+    assert all(v["total_ms"] >= 0 for v in st.values())
+
+
+def test_lost_rank_fails_the_whole_job(tmp_path):
+    """A rank raising mid-fit (between collectives) makes torchrun tear the job down: the launcher
+    exits non-zero well within the store timeout instead of leaving the survivors blocked."""
+    from fraud_detection_amd.data.synthetic import separable_frame
+
+    csv = str(tmp_path / "cc.csv")
+    separable_frame(8_000, fraud_rate=0.02, seed=3).to_csv(csv, index=False)
+    env = dict(os.environ, DATA_CSV=csv, FDX_DEVICE="cpu", FDX_FAULT="dp_rank_crash:1", FDX_DIST_TIMEOUT="300",
+               MLFLOW_TRACKING_URI=str(tmp_path / "mlruns"), PYTHONPATH=os.path.dirname(os.path.dirname(__file__)))
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={_free_port()}", "train_model.py"],
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))), env=env,
+                       capture_output=True, text=True, timeout=240)
+    dt = time.time() - t0
+    assert r.returncode != 0
+    assert "simulated crash of rank 1" in (r.stdout + r.stderr)
+    assert dt < 200, f"job took {dt:.0f}s to fail"

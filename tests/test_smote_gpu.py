@@ -128,3 +128,23 @@ def test_smote_device_draws_exact(dev, mq):
     exp = (xi + lam.astype(np.float64)[:, None] * (xj - xi)).astype(np.float32)  # exact, then one rounding
     got = out[:, :3].cpu().numpy()
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.gpu
+def test_smote_sample_offset_slices_equal_one_launch(dev):
+    """DP global scope: 128-aligned slices of one draw sequence == one launch (device and oracle)."""
+    st, xmin = _minority(seed=10)
+    P = K.smote_parents(xmin, st.aff).to(dev)
+    nbr = K.knn_topk(xmin, xmin, k=5, self_offset=0).to(dev)
+    n = 10_000
+    whole = torch.empty((n, 32), dtype=torch.bfloat16, device=dev)
+    K.smote_generate(P, nbr, 0, n, whole, seed=3)
+    parts = torch.empty_like(whole)
+    for a, b in ((0, 1280), (1280, 1280), (1280, 7296), (7296, n)):
+        K.smote_generate(P, nbr, 0, b - a, parts[a:b], seed=3, sample_offset=a)
+    assert torch.equal(whole, parts)
+    cpu = torch.empty((n - 1280, 32), dtype=torch.bfloat16)
+    K.smote_generate(P.cpu(), nbr.cpu(), 0, n - 1280, cpu, seed=3, sample_offset=1280)
+    e = cpu.float()
+    g = whole[1280:].float().cpu()
+    assert torch.mean((g != e).float()) < 1e-3 and torch.allclose(g, e, rtol=2 ** -7, atol=1e-6)

@@ -1,0 +1,165 @@
+"""The async XAI worker explains with KernelSHAP (BASELINE config 4) through the model the API
+serves -- the linear model with a stored background, and a GBDT registered under the MLflow
+alias -- plus the schema migration, trace continuation and metrics
+that come with it.  CPU here (exact fp64 oracles); tests/test_serving_gpu.py repeats the round
+trips on the device kernels."""
+import os
+import uuid
+
+import numpy as np
+import pytest
+from fastapi.testclient import TestClient
+
+from _models import gbdt_registered, kaggle_like_rows, linear_dir_with_background
+from fraud_detection_amd.config import Settings
+from fraud_detection_amd.serve.app import create_app
+from fraud_detection_amd.store.db import make_engine
+from fraud_detection_amd.taskqueue.queue import DurableQueue
+from fraud_detection_amd.taskqueue.worker import Worker
+
+
+def _service(tmp_path, **settings_kw):
+    import xai_tasks
+
+    url = f"sqlite:///{tmp_path}/k.db"
+    q = DurableQueue(url=url)
+    xai_tasks.celery_app.use_queue(q)
+    s = Settings.load(database_url=url, device="cpu", **settings_kw)
+    xai_tasks.service.db_url = url
+    xai_tasks.service._db = None
+    xai_tasks.service._engine = None
+    xai_tasks.service._injected = False
+    xai_tasks.service.settings = s
+    app = create_app(s, task_app=xai_tasks.celery_app, db_engine=make_engine(url))
+    return app, xai_tasks
+
+
+@pytest.fixture()
+def restore_service():
+    import xai_tasks
+
+    yield
+    xai_tasks.service.settings = None
+    xai_tasks.service._engine = None
+    xai_tasks.service._injected = False
+
+
+def test_linear_model_with_background_is_explained_by_kernelshap(tmp_path, restore_service):
+    from fraud_detection_amd.models.explainers import kernelshap_reference
+    from fraud_detection_amd.obs import tracing
+
+    mdir = linear_dir_with_background(tmp_path)
+    app, xt = _service(tmp_path, model_path=os.path.join(mdir, "logistic_model.joblib"),
+                       scaler_path=os.path.join(mdir, "scaler.joblib"),
+                       feature_names_path=os.path.join(mdir, "feature_names.json"),
+                       mlflow_tracking_uri=f"file:{tmp_path}/none")
+    rows = kaggle_like_rows(5, seed=9)
+    with TestClient(app) as c:
+        txs = []
+        for r in rows:
+            tx = str(uuid.uuid4())
+            assert c.post("/predict", json={"features": r.tolist(), "transaction_id": tx}).status_code == 200
+            txs.append(tx)
+        assert Worker(xt.celery_app, batch=64).run_once() == 5
+        eng = app.state.fdx["engine"]
+        ke = eng.kernel_explainer()
+        phi_ref, fx_ref, f0_ref = kernelshap_reference(rows, ke.a, ke.bias, ke.B, ke.Z, ke.A, ke.zM, "identity")
+        for j, tx in enumerate(txs):
+            e = c.get(f"/explain/{tx}").json()
+            assert e["explainer"] == "kernel"
+            phi = np.array([e["shap_values"][n] for n in e["feature_names"]])
+            np.testing.assert_allclose(phi, phi_ref[j], atol=1e-9)
+            assert phi.sum() == pytest.approx(fx_ref[j] - e["base_value"], abs=1e-9)   # efficiency
+            assert e["base_value"] == pytest.approx(f0_ref, abs=1e-12)
+    # the worker continued the request's trace (traceparent header -> span parent)
+    sp = tracing.recent_spans("xai.compute_shap")[-1]
+    assert sp["parent_span_id"] is not None and sp["attrs"]["method"] == "kernel"
+
+
+def test_method_switch_to_linear(tmp_path, restore_service, monkeypatch):
+    mdir = linear_dir_with_background(tmp_path)
+    app, xt = _service(tmp_path, model_path=os.path.join(mdir, "logistic_model.joblib"),
+                       mlflow_tracking_uri=f"file:{tmp_path}/none")
+    monkeypatch.setenv("FDX_XAI_METHOD", "linear")
+    with TestClient(app) as c:
+        tx = str(uuid.uuid4())
+        c.post("/predict", json={"features": [0.1] * 30, "transaction_id": tx})
+        Worker(xt.celery_app).run_once()
+        assert c.get(f"/explain/{tx}").json()["explainer"] == "linear"
+
+
+def test_gbdt_alias_is_served_and_explained(tmp_path, restore_service):
+    """a GBDT registered under the production alias is what /predict serves (no
+    silent fallback to the old LR joblib), and the worker explains it with KernelSHAP."""
+    from fraud_detection_amd.models.explainers import TreeKernelExplainer
+
+    kw, res, X = gbdt_registered(tmp_path)
+    app, xt = _service(tmp_path, **kw)
+    rows = X[:4].numpy()
+    with TestClient(app) as c:
+        h = c.get("/health").json()
+        assert h["dependencies"]["model"] == "UP"
+        eng = app.state.fdx["engine"]
+        assert eng.kind == "gbdt" and eng.source == "mlflow"
+        txs = []
+        for r in rows:
+            tx = str(uuid.uuid4())
+            b = c.post("/predict", json={"features": r.tolist(), "transaction_id": tx}).json()
+            txs.append((tx, b["score"]))
+        margin = res.predict_margin(X[:4]).numpy().astype(np.float64)
+        np.testing.assert_allclose([s for _, s in txs], 1 / (1 + np.exp(-margin)), atol=1e-6)
+        assert Worker(xt.celery_app, batch=16).run_once() == 4
+        te = TreeKernelExplainer(res.ensemble, *res.scaler.numpy()[::2], eng.background, device="cpu")
+        phi_ref, fx_ref, f0_ref = te.explain(rows)
+        for j, (tx, score) in enumerate(txs):
+            e = c.get(f"/explain/{tx}").json()
+            assert e["explainer"] == "kernel"
+            phi = np.array([e["shap_values"][n] for n in e["feature_names"]])
+            np.testing.assert_allclose(phi, phi_ref[j], atol=1e-9)
+            assert phi.sum() == pytest.approx(score - e["base_value"], abs=1e-4)     # efficiency
+        bo = c.post("/predict/batch", json={"rows": rows.tolist(), "explain": True}).json()
+        np.testing.assert_allclose(bo["shap_values"], phi_ref, atol=1e-9)
+
+
+def test_migration_adds_explainer_columns_to_an_old_database(tmp_path):
+    from sqlalchemy import inspect, text
+
+    from fraud_detection_amd.store.migrations import upgrade
+
+    eng = make_engine(f"sqlite:///{tmp_path}/old.db")
+    upgrade(eng, target="fdx_0004")          # a database as round 1 left it
+    with eng.begin() as c:
+        c.execute(text("ALTER TABLE shap_explanations DROP COLUMN explainer"))
+        c.execute(text("ALTER TABLE shap_explanations DROP COLUMN base_value"))
+        c.execute(text("INSERT INTO shap_explanations (transaction_id, shap_values) VALUES ('t1', '{}')"))
+    assert "explainer" not in {c["name"] for c in inspect(eng).get_columns("shap_explanations")}
+    assert upgrade(eng) == ["fdx_0005"]
+    cols = {c["name"] for c in inspect(eng).get_columns("shap_explanations")}
+    assert {"explainer", "base_value"} <= cols
+    with eng.connect() as c:
+        assert c.execute(text("SELECT transaction_id FROM shap_explanations")).scalar() == "t1"
+
+
+def test_worker_spawns_one_process_per_gpu(monkeypatch):
+    """--gpus N: N children, child i pinned to GPU i (HIP_VISIBLE_DEVICES), parent exits with the
+    first failing child's status (here each child fails fast on a bogus app spec)."""
+    import subprocess
+
+    from fraud_detection_amd.taskqueue import worker as W
+
+    seen = []
+
+    class P:
+        def __init__(self, cmd, env):
+            seen.append(env["HIP_VISIBLE_DEVICES"])
+            self.rc = 3 if env["HIP_VISIBLE_DEVICES"] == "1" else 0
+
+        def wait(self):
+            return self.rc
+
+        def poll(self):
+            return self.rc
+
+    monkeypatch.setattr(subprocess, "Popen", P)
+    assert W.main(["--gpus", "4", "--app", "nope:app"]) == 3
+    assert seen == ["0", "1", "2", "3"]
