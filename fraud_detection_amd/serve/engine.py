@@ -233,8 +233,9 @@ class InferenceEngine(_EngineBase):
         self.a, self.c, self.bias = P.fold_scaler(artifacts.padded_weights(), artifacts.mean, artifacts.scale, bg_std)
         super().__init__(device, source, background, kernel_nsamples, kernel_link)
         if self.device.type == "cuda":
-            self._a = torch.from_numpy(self.a).to(self.device)
-            self._c = torch.from_numpy(self.c).to(self.device)
+            # the fused kernel reads fp32 weights (the fold is computed in fp64, then rounded once)
+            self._a = torch.from_numpy(self.a.astype(np.float32)).to(self.device)
+            self._c = torch.from_numpy(self.c.astype(np.float32)).to(self.device)
             self._stage = _Staging(self.device, self.d, self.d + 2)
 
     @classmethod
