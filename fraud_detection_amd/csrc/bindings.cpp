@@ -65,10 +65,12 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
   m.def("scaler_stats_cast_blocks", []() { return fdx::scaler_stats_cast_blocks(); });
   m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,
-                                int nblocks, u s) {
+                                int nblocks, u s, u colscale, float out_scale) {
     fdx::launch_scaler_stats_cast(P<const float>(X), n, d, P<const float>(pivot), P<const uint8_t>(labels), bias_value,
-                                  P<void>(out), P<double>(partial), nblocks, S(s));
-  });
+                                  P<void>(out), P<double>(partial), nblocks, S(s), P<const float>(colscale), out_scale);
+  }, py::arg("X"), py::arg("n"), py::arg("d"), py::arg("pivot"), py::arg("labels"), py::arg("bias_value"),
+     py::arg("out"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("colscale") = 0,
+     py::arg("out_scale") = 1.0f);
   m.def("scale_cast", [](u X, int64_t n, int ld, int d, u idx, u mean32, u inv32, u labels, float bias_value,
                          float out_scale, int out_kind, u out, u s) {
     fdx::launch_scale_cast(P<const float>(X), n, ld, d, P<const int64_t>(idx), P<const float>(mean32),

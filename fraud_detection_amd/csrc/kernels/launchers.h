@@ -50,9 +50,11 @@ void launch_scaler_finalize(const double* sums, double n, const float* pivot, in
                             float* inv32, double* aff, hipStream_t stream);
 void launch_fp8_hw_check(float* dec, const float* vals, int n, uint8_t* enc, hipStream_t stream);
 int scaler_stats_cast_blocks();  // resident blocks of the fused kernel on this device
-// fused K1+K2 for bf16 training rows: shifted sums -> partial[nblocks][64], rows s = x - pivot
+// fused K1+K2: shifted sums -> partial[nblocks][64], rows s = x - pivot in bf16, or (colscale set)
+// fp8 e4m3 of (x - pivot) * colscale * out_scale
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
-                              float bias_value, void* out, double* partial, int nblocks, hipStream_t stream);
+                              float bias_value, void* out, double* partial, int nblocks, hipStream_t stream,
+                              const float* colscale = nullptr, float out_scale = 1.0f);
 void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* idx,
                        const float* mean32, const float* inv32, const uint8_t* labels,
                        float bias_value, float out_scale, int out_kind, void* out,

@@ -192,19 +192,27 @@ __device__ __forceinline__ int stats_fetch(const float* __restrict__ X, int64_t 
 // s = x - pivot (col 30 = bias_value, col 31 = label).  The standardization z = (s - c) / sigma
 // is applied later as an exact affine map on the solver's 32x32 sums (newton_update with aff),
 // so the raw matrix is read once instead of twice (stats, then cast) per fit.
-template <bool NT>
+// FP8: the row is written as OCP e4m3 of (x - pivot) * colscale * out_scale (32 B/row, half the
+// bf16 bytes).  e4m3 needs values near unit scale, so the host passes a sample estimate of the
+// mean as the pivot and of 1/sigma as colscale (ops/scaler.py fp8_fused_prescale); the exact
+// statistics from this same pass turn that into the solver's affine map, so the prescale only
+// has to be roughly right.
+template <bool NT, bool FP8>
 __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
     const float* __restrict__ X, int64_t n, int d, const float* __restrict__ pivot,
-    const uint8_t* __restrict__ labels, float bias_value, uint16_t* __restrict__ out,
-    double* __restrict__ partial) {
+    const uint8_t* __restrict__ labels, float bias_value, void* __restrict__ outv,
+    double* __restrict__ partial, const float* __restrict__ colscale, float out_scale) {
   __shared__ __attribute__((aligned(16))) float tile[kStatTileRows * 30];
   __shared__ double red[2][8][32];
   const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
   const double piv = (c < d) ? (double)pivot[c] : 0.0;
   const int q = threadIdx.x & 3;  // cast: column group of both of this lane's row slots
-  float pv[8];
+  float pv[8], ks[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) pv[j] = (8 * q + j < d) ? pivot[8 * q + j] : 0.0f;
+  for (int j = 0; j < 8; ++j) {
+    pv[j] = (8 * q + j < d) ? pivot[8 * q + j] : 0.0f;
+    ks[j] = (FP8 && 8 * q + j < d) ? colscale[8 * q + j] * out_scale : 1.0f;
+  }
   double s = 0.0, sq = 0.0;
   const int64_t ntiles = (n + kStatTileRows - 1) / kStatTileRows;
   const int64_t total = n * (int64_t)d;
@@ -245,16 +253,22 @@ __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int cc = 8 * q + j;
-        if (cc < d) o[j] = tile[r * d + cc] - pv[j];
+        if (cc < d) o[j] = FP8 ? (tile[r * d + cc] - pv[j]) * ks[j] : tile[r * d + cc] - pv[j];
         else if (cc == kBiasCol) o[j] = bias_value;
         else if (cc == kLabelCol) o[j] = labels ? (float)labels[grow] : 0.0f;
         else o[j] = 0.0f;
       }
-      uint4 pk;
-      pk.x = pack_bf16x2(o[0], o[1]); pk.y = pack_bf16x2(o[2], o[3]);
-      pk.z = pack_bf16x2(o[4], o[5]); pk.w = pack_bf16x2(o[6], o[7]);
-      if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(out) + grow * 4 + q);
-      else reinterpret_cast<uint4*>(out)[grow * 4 + q] = pk;
+      if constexpr (FP8) {
+        const uint2 pk = make_uint2(f32x4_to_fp8(o[0], o[1], o[2], o[3]), f32x4_to_fp8(o[4], o[5], o[6], o[7]));
+        if constexpr (NT) __builtin_nontemporal_store(u32x2_t{pk.x, pk.y}, reinterpret_cast<u32x2_t*>(outv) + grow * 4 + q);
+        else reinterpret_cast<uint2*>(outv)[grow * 4 + q] = pk;
+      } else {
+        uint4 pk;
+        pk.x = pack_bf16x2(o[0], o[1]); pk.y = pack_bf16x2(o[2], o[3]);
+        pk.z = pack_bf16x2(o[4], o[5]); pk.w = pack_bf16x2(o[6], o[7]);
+        if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(outv) + grow * 4 + q);
+        else reinterpret_cast<uint4*>(outv)[grow * 4 + q] = pk;
+      }
     }
     __syncthreads();
   }
@@ -676,23 +690,28 @@ void launch_scaler_finalize(const double* sums, double n, const float* pivot, in
 }
 
 int scaler_stats_cast_blocks() {
-  static const int cap = resident_cap(scaler_stats_cast_kernel<false>, kThreads);
-  static const int cap_nt = resident_cap(scaler_stats_cast_kernel<true>, kThreads);
+  static const int cap = resident_cap(scaler_stats_cast_kernel<false, false>, kThreads);
+  static const int cap_nt = resident_cap(scaler_stats_cast_kernel<true, false>, kThreads);
   return nt_stores() ? cap_nt : cap;
 }
 
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
-                              float bias_value, void* out, double* partial, int nblocks, hipStream_t stream) {
+                              float bias_value, void* out, double* partial, int nblocks, hipStream_t stream,
+                              const float* colscale, float out_scale) {
   if (d > 30 || (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(out) % 16) != 0)
     throw std::invalid_argument("scaler_stats_cast: contiguous 16-byte aligned rows, d <= 30");
   // every block must be resident at once (a second round of blocks would double the span);
   // nblocks is fixed by the caller (partial buffer), the grid-stride loop covers the rest
-  if (nt_stores())
-    scaler_stats_cast_kernel<true><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
-                                                                     reinterpret_cast<uint16_t*>(out), partial);
-  else
-    scaler_stats_cast_kernel<false><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value,
-                                                                      reinterpret_cast<uint16_t*>(out), partial);
+#define FDX_SSC(NT, F8)                                                                                 \
+  scaler_stats_cast_kernel<NT, F8><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value, \
+                                                                     out, partial, colscale, out_scale)
+  const bool fp8 = colscale != nullptr;
+  if (nt_stores()) {
+    if (fp8) FDX_SSC(true, true); else FDX_SSC(true, false);
+  } else {
+    if (fp8) FDX_SSC(false, true); else FDX_SSC(false, false);
+  }
+#undef FDX_SSC
   check_launch("scaler_stats_cast");
 }
 

@@ -40,8 +40,9 @@ class TrainConfig:
     sampling_ratio: float = 1.0     # minority : majority after SMOTE (1.0 = imblearn 'auto')
     seed: int = 42
     storage: str = "bf16"           # bf16 | fp8
-    # bf16 + Newton on GPU: scaler statistics and the row cast share one read of X (rows stay
-    # pivot-shifted; the solver applies the standardization as an exact affine map of its sums)
+    # Newton on GPU (bf16 or fp8 rows): scaler statistics and the row cast share one read of X
+    # (rows stay shifted / prescaled; the solver applies the standardization as an exact affine
+    # map of its sums)
     fold_scaler: bool = True
     fp8_scale: float = DEFAULT_FP8_SCALE
     sgd_lr: float = 0.5
@@ -120,6 +121,67 @@ class DevicePipeline:
             self._buf = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
         return self._buf[:n_rows]
 
+    def fit_host(self, X: torch.Tensor, y: torch.Tensor, device=None, budget: int | None = None,
+                 profile: bool = False) -> PipelineResult:
+        """Fit from host-resident raw rows (the parsed table), planned against free HBM
+        (runtime/hbm.py): ``resident`` uploads once and runs the fused fast path; ``stream_raw``
+        keeps the raw shard on the host and streams it twice (exact statistics, then
+        standardize+cast into the device-resident training rows) -- a shard larger than HBM
+        trains as long as its training rows fit."""
+        from ..runtime import hbm
+
+        cfg = self.cfg
+        dev = torch.device(device) if device is not None else (
+            torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
+        n, d = X.shape
+        frac = float(y[: 1 << 20].float().mean()) if n else 0.0
+        plan = hbm.plan_fit(n, d, cfg.storage, cfg.smote, cfg.sampling_ratio, minority_frac=max(frac, 1e-3),
+                            dev=dev, budget=budget)
+        self.last_plan = plan
+        if plan.mode == "resident":
+            res = self.fit(X.to(dev, non_blocking=True), y.to(dev, non_blocking=True), profile)
+        else:
+            res = self._fit_streaming(X, y, dev, plan, profile)
+        res.timings["hbm_plan"] = plan.as_dict()
+        hbm.observe_hbm(dev)
+        return res
+
+    def _fit_streaming(self, X, y, dev, plan, profile) -> PipelineResult:
+        cfg = self.cfg
+        rank, world = self._world()
+        comm = self.comm if world > 1 else None
+        tm = _Timer(dev, profile)
+        n, d = X.shape
+        cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) + 128 if cfg.smote else 0)
+        rows_cap = self._train_buffer(cap, dev)
+        chunks = _HostChunks(X, y, dev, plan.chunk_rows)
+        pivot = X[0].to(dev, torch.float32) if n else torch.zeros(d, device=dev)
+        if comm is not None:
+            pivot = comm.broadcast(pivot.contiguous(), src=0)
+        # pass 1: exact shifted fp64 sums over the streamed chunks (C1 all-reduce after)
+        sums = torch.zeros(64, dtype=torch.float64, device=dev)
+        for _, xd, _ in chunks:
+            sums += scaler_ops.scaler_partial_sums(xd, pivot)
+        if comm is not None:
+            sums[31:32].fill_(float(n))
+            sums = comm.all_reduce(sums)
+            stats = scaler_ops.scaler_finalize(sums, None, pivot, d)
+        else:
+            stats = scaler_ops.scaler_finalize(sums, float(n), pivot, d)
+        tm.mark("scaler_fit")
+        # pass 2: standardize + cast into the resident training rows; minority rows in fp32
+        xmins = []
+        for c0, xd, yd in chunks:
+            m = xd.shape[0]
+            scaler_ops.scale_cast(xd, stats, labels=yd, out_dtype=cfg.storage, out=rows_cap[c0:c0 + m],
+                                  fp8_scale=cfg.fp8_scale)
+            idx = scaler_ops.compact_indices(yd, 1)
+            if idx.numel():
+                xmins.append(scaler_ops.scale_cast(xd, stats, labels=yd, out_dtype="f32", idx=idx))
+        xmin = torch.cat(xmins) if xmins else torch.empty((0, NCOLS), dtype=torch.float32, device=dev)
+        _maybe_fault(rank)
+        return self._finish(stats, rows_cap, n, d, int(xmin.shape[0]), False, tm, comm, rank, dev, lambda: xmin)
+
     def fit(self, X: torch.Tensor, y: torch.Tensor, profile: bool = False) -> PipelineResult:
         cfg = self.cfg
         if cfg.smote_scope not in ("global", "shard"):
@@ -129,8 +191,8 @@ class DevicePipeline:
         comm = self.comm if world > 1 else None
         tm = _Timer(dev, profile)
         n, d = X.shape
-        fused = (cfg.fold_scaler and cfg.storage == "bf16" and cfg.solver == "newton" and dev.type == "cuda"
-                 and scaler_ops.fused_cast_ok(X))
+        fused = (cfg.fold_scaler and cfg.storage in ("bf16", "fp8") and cfg.solver == "newton"
+                 and dev.type == "cuda" and scaler_ops.fused_cast_ok(X))
         # training buffer sized for the largest possible SMOTE output, so the cast does not wait
         # for the minority count (+128: a global-scope slice boundary moves by < 128 rows)
         cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) + 128 if cfg.smote else 0)
@@ -138,8 +200,8 @@ class DevicePipeline:
         if fused:
             # ---- class counts (C2): count kernels first, host reads the total during K1+K2 ----
             pending = scaler_ops.compact_indices_async(y, 1)
-            # ---- K1+K2 fused: statistics (C1 all-reduce inside) + pivot-shifted bf16 rows ----
-            stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm)
+            # ---- K1+K2 fused: statistics (C1 all-reduce inside) + shifted bf16 / fp8 rows ----
+            stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
             tm.mark("scaler_fit")
         else:
             # ---- K1: scaler statistics (C1 all-reduce inside) ----------------------------
@@ -152,6 +214,13 @@ class DevicePipeline:
         idx_min = pending.result()
         n_min = int(idx_min.shape[0])
         _maybe_fault(rank)
+        return self._finish(stats, rows_cap, n, d, n_min, fused, tm, comm, rank, dev,
+                            lambda: scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min))
+
+    def _finish(self, stats, rows_cap, n, d, n_min, fused, tm, comm, rank, dev, get_xmin) -> PipelineResult:
+        """SMOTE (+ DP exchange) and the solver on the device-resident training rows
+        rows_cap[:n] (shared by the resident and the host-streaming preparation)."""
+        cfg = self.cfg
 
         def quota(n_r, nmin_r):
             return max(0, int(round((n_r - nmin_r) * cfg.sampling_ratio)) - nmin_r) if (cfg.smote and nmin_r > 0) else 0
@@ -171,7 +240,7 @@ class DevicePipeline:
         tm.mark("scale_cast")
         if sum(new_per_rank) > 0:
             # ---- minority rows in fp32, gathered across ranks (C3) -----------------------
-            xmin = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min)
+            xmin = get_xmin()
             if glob:
                 xall, counts = comm.all_gather_rows(xmin, counts=[r[0] for r in ranks])
                 q_off = int(sum(counts[:rank]))
@@ -216,7 +285,9 @@ class DevicePipeline:
                                     n_sched=n_sched, affine=stats.aff if fused else None)
         elif cfg.solver == "sgd":
             fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
-                                 batch_rows=cfg.sgd_batch_rows, class_w=class_w, d=d, w0=w0,
+                                 batch_rows=min(cfg.sgd_batch_rows, getattr(getattr(self, "last_plan", None),
+                                                                            "sgd_batch_rows", cfg.sgd_batch_rows)),
+                                 class_w=class_w, d=d, w0=w0,
                                  fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
                                  workspace=self._ws)
         else:
@@ -224,6 +295,63 @@ class DevicePipeline:
         tm.mark("fit")
         return PipelineResult(scaler=stats, fit=fit, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
                               n_synthetic=n_new, timings=dict(tm.t))
+
+
+class _HostChunks:
+    """Double-buffered host -> device streaming of raw row chunks: the H2D copy of chunk i+1 runs
+    on a side stream while the compute stream works on chunk i (events order the buffer reuse)."""
+
+    def __init__(self, X: torch.Tensor, y: torch.Tensor, dev: torch.device, chunk: int):
+        self.X, self.y, self.dev, self.chunk = X, y, dev, int(chunk)
+        self.n, self.d = X.shape
+        self.cuda = dev.type == "cuda"
+        if self.cuda:
+            self.pinned = X.is_pinned() and y.is_pinned()
+            if not self.pinned:
+                self.px = [torch.empty((self.chunk, self.d), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+                self.py = [torch.empty(self.chunk, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+            self.dx = [torch.empty((self.chunk, self.d), dtype=torch.float32, device=dev) for _ in range(2)]
+            self.dy = [torch.empty(self.chunk, dtype=torch.uint8, device=dev) for _ in range(2)]
+            self.copy_stream = torch.cuda.Stream(dev)
+            self.copied = [torch.cuda.Event() for _ in range(2)]
+            self.consumed = [torch.cuda.Event() for _ in range(2)]
+            self.staged = [torch.cuda.Event() for _ in range(2)]
+
+    def _issue(self, c0: int, slot: int):
+        c1 = min(self.n, c0 + self.chunk)
+        m = c1 - c0
+        if self.pinned:
+            sx, sy = self.X[c0:c1], self.y[c0:c1]
+        else:
+            self.staged[slot].synchronize()  # the previous H2D out of this pinned slot is done
+            self.px[slot][:m].copy_(self.X[c0:c1])
+            self.py[slot][:m].copy_(self.y[c0:c1])
+            sx, sy = self.px[slot][:m], self.py[slot][:m]
+        with torch.cuda.stream(self.copy_stream):
+            self.copy_stream.wait_event(self.consumed[slot])  # compute is done with this device slot
+            self.dx[slot][:m].copy_(sx, non_blocking=True)
+            self.dy[slot][:m].copy_(sy, non_blocking=True)
+            self.staged[slot].record(self.copy_stream)
+            self.copied[slot].record(self.copy_stream)
+
+    def __iter__(self):
+        starts = list(range(0, self.n, self.chunk))
+        if not self.cuda:
+            for c0 in starts:
+                c1 = min(self.n, c0 + self.chunk)
+                yield c0, self.X[c0:c1].to(self.dev), self.y[c0:c1].to(self.dev)
+            return
+        cur = torch.cuda.current_stream(self.dev)
+        if starts:
+            self._issue(starts[0], 0)
+        for i, c0 in enumerate(starts):
+            slot = i & 1
+            if i + 1 < len(starts):
+                self._issue(starts[i + 1], slot ^ 1)
+            m = min(self.n, c0 + self.chunk) - c0
+            cur.wait_event(self.copied[slot])
+            yield c0, self.dx[slot][:m], self.dy[slot][:m]
+            self.consumed[slot].record(cur)
 
 
 def _maybe_fault(rank: int):

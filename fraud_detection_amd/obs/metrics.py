@@ -44,6 +44,8 @@ class ApiMetrics:
 
 
 def api_metrics(registry: CollectorRegistry | None = None) -> ApiMetrics:
+    gpu_kernel_histogram()  # declared with the app (observed by the device engines)
+    span_histogram()
     r = registry or CollectorRegistry()
     size_buckets = (100, 1_000, 10_000, 100_000, 1_000_000)
     return ApiMetrics(

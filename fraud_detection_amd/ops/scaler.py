@@ -148,20 +148,52 @@ def fused_cast_ok(X: torch.Tensor) -> bool:
     return (not X.is_cuda) or (X.is_contiguous() and X.data_ptr() % 16 == 0 and X.shape[1] <= 30)
 
 
+def fp8_fused_prescale(X: torch.Tensor, comm=None, sample_rows: int = 65536):
+    """(pivot [d], colscale [d]) float32 for the fp8 fused cast: mean and 1/std of the first
+    ``sample_rows`` rows (rank 0's under DP, broadcast), so the stored e4m3 values are ~z * scale.
+    Only a prescale: the exact statistics of the same pass define the solver's affine map."""
+    n, d = X.shape
+    if comm is not None and comm.world_size > 1:
+        buf = torch.zeros(2 * d, device=X.device, dtype=torch.float32)
+        if comm.rank == 0:
+            buf.copy_(torch.cat(_sample_moments(X, sample_rows)))
+        buf = comm.broadcast(buf, src=0)
+        return buf[:d].contiguous(), buf[d:].contiguous()
+    return _sample_moments(X, sample_rows)
+
+
+def _sample_moments(X: torch.Tensor, sample_rows: int):
+    smp = X[: max(1, min(X.shape[0], sample_rows))].double()
+    mu = smp.mean(0)
+    sd = smp.std(0, unbiased=False)
+    k = torch.where(sd > 0, 1.0 / sd, torch.ones_like(sd))
+    return mu.float().contiguous(), k.float().contiguous()
+
+
 def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Tensor, comm=None,
-                    pivot: torch.Tensor | None = None, bias_value: float = 1.0) -> ScalerStats:
-    """StandardScaler.fit fused with the bf16 row cast: ONE read of X yields the (all-reduced)
-    statistics and pivot-shifted training rows s = x - pivot in ``out`` (bf16 [n, 32], col 30 =
-    bias_value, col 31 = label).  The returned stats carry ``aff``, which the Newton solver uses
-    to work in standardized space on these rows (ops/logreg.newton_fit(affine=...)): same model,
-    half the raw-matrix traffic of scaler_fit + scale_cast."""
+                    pivot: torch.Tensor | None = None, bias_value: float = 1.0,
+                    fp8_scale: float = DEFAULT_FP8_SCALE) -> ScalerStats:
+    """StandardScaler.fit fused with the row cast: ONE read of X yields the (all-reduced)
+    statistics and the training rows in ``out`` [n, 32] (col 30 = bias_value, col 31 = label):
+      * bf16: pivot-shifted rows s = x - pivot;
+      * fp8 (uint8 out): e4m3 of s' = (x - p) * k * fp8_scale with a sample prescale (p ~ mean,
+        k ~ 1/sigma: fp8_fused_prescale) -- 32 B rows, half the bf16 bytes.
+    The returned stats carry ``aff`` mapping the stored feature values (fp8: after dividing by
+    fp8_scale) to standardized ones, z = (v - c) * inv, which the Newton solver applies as an exact
+    affine map of its sums (ops/logreg.newton_fit(affine=...)): same model, half the raw-matrix
+    traffic of scaler_fit + scale_cast."""
     _check_X(X)
     n, d = X.shape
-    if out.shape != (n, NCOLS) or out.dtype != torch.bfloat16 or not out.is_contiguous():
+    fp8 = out.dtype == torch.uint8
+    if out.shape != (n, NCOLS) or out.dtype not in (torch.bfloat16, torch.uint8) or not out.is_contiguous():
         raise ValueError(f"bad output buffer {tuple(out.shape)} {out.dtype}")
     if labels is not None and (labels.dtype != torch.uint8 or labels.shape[0] != n):
         raise ValueError("labels must be uint8 [n] aligned with X")
     dist = comm is not None and comm.world_size > 1
+    colscale = None
+    if fp8:
+        pivot_fp8, colscale = fp8_fused_prescale(X, comm)
+        pivot = pivot_fp8 if pivot is None else pivot
     if pivot is None:
         if dist:
             pivot = X[0].clone() if n > 0 else torch.zeros(d, device=X.device)
@@ -172,10 +204,12 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         sums = torch.from_numpy(ref.scaler_sums(X.numpy(), pivot.cpu().numpy()))
         o = torch.zeros((n, NCOLS), dtype=torch.float32)
         o[:, :d] = X - pivot[:d].to(torch.float32)
+        if fp8:
+            o[:, :d] *= colscale[:d] * fp8_scale
         o[:, 30] = bias_value
         if labels is not None:
             o[:, 31] = labels.to(torch.float32)
-        out.copy_(o.to(torch.bfloat16))
+        out.copy_(torch.from_numpy(ref.fp8_encode(o.numpy())) if fp8 else o.to(torch.bfloat16))
     else:
         if not fused_cast_ok(X) or out.data_ptr() % 16:
             raise ValueError("scaler_fit_cast: X must be contiguous and 16-byte aligned with d <= 30")
@@ -187,15 +221,22 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         sums = torch.empty(64, device=X.device, dtype=torch.float64)
         s = stream_of(X)
         if n > 0:
-            m.scaler_stats_cast(ptr(X), n, d, ptr(piv), ptr(labels), float(bias_value), ptr(out), ptr(partial), nb, s)
+            m.scaler_stats_cast(ptr(X), n, d, ptr(piv), ptr(labels), float(bias_value), ptr(out), ptr(partial), nb, s,
+                                ptr(colscale), float(fp8_scale) if fp8 else 1.0)
             m.scaler_reduce(ptr(partial), nb, ptr(sums), s)
         else:
             sums.zero_()
     if dist:
         sums[31:32].fill_(float(n))
         sums = comm.all_reduce(sums)
-        return scaler_finalize(sums, None, pivot, d, want_aff=True)
-    return scaler_finalize(sums, float(n), pivot, d, want_aff=True)
+        st = scaler_finalize(sums, None, pivot, d, want_aff=True)
+    else:
+        st = scaler_finalize(sums, float(n), pivot, d, want_aff=True)
+    if fp8:  # stored v = s * k  ->  z = (s - c) * inv = (v - k c) * (inv / k)
+        k = torch.ones(32, device=st.aff.device, dtype=torch.float64)
+        k[:d] = colscale[:d].to(st.aff.device, torch.float64)
+        st.aff = torch.cat([st.aff[:32] * k, st.aff[32:] / k])
+    return st
 
 
 def scale_cast(X: torch.Tensor, stats: ScalerStats, labels: torch.Tensor | None = None,

@@ -60,6 +60,10 @@ class Worker:
         self.visibility_timeout = visibility_timeout
         self.poll_interval = poll_interval
         self.name = name or f"{socket.gethostname()}:{os.getpid()}:{id(self) & 0xffff:x}"
+        if metrics is None:  # the process-global worker metrics (what :8001 and /metrics expose)
+            from ..obs.metrics import worker_metrics
+
+            metrics = worker_metrics()
         self.metrics = metrics
         self._stop = threading.Event()
 

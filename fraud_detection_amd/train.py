@@ -27,6 +27,9 @@ from .compat.sklearn_export import LinearArtifacts, make_logistic, save_artifact
 from .config import Settings
 from .data.io import missing_report, read_table, stratified_folds, stratified_split
 from .models.pipeline import DevicePipeline, TrainConfig, evaluate
+from .obs import tracing
+from .obs.metrics import train_metrics
+from .runtime.hbm import observe_hbm
 
 logger = logging.getLogger("train")
 
@@ -117,8 +120,16 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
     say(f" Training final {model_type} model with SMOTE on the full training set...")
-    res = _fit(model_type, cfg, Xtr, ytr, comm,
-               checkpoint=None if ck_dir is None else os.path.join(ck_dir, f"final_{model_type}"))
+    t_fit = time.perf_counter()
+    with tracing.span("train.final_fit", model=model_type), tracing.roctx_range("train.final_fit"):
+        res = _fit(model_type, cfg, Xtr, ytr, comm,
+                   checkpoint=None if ck_dir is None else os.path.join(ck_dir, f"final_{model_type}"))
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+    t_fit = time.perf_counter() - t_fit
+    tm = train_metrics()
+    tm.rows_per_second.set(float(res.n_train_rows) * (comm.world_size if comm else 1) / max(t_fit, 1e-9))
+    observe_hbm(dev)
     if model_type == "logistic":
         ev = evaluate(res, Xte, yte, comm)
         auc = ev["auc"]

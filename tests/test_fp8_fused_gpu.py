@@ -1,0 +1,61 @@
+"""fp8 training rows written by the fused scaler pass (BASELINE config 5): one read
+of the raw matrix gives the exact statistics and 32-byte e4m3 rows of the prescaled values; the
+solver applies the exact affine map.  Checked against the CPU oracle of the same pass and against
+the bf16 fit (AUC), plus the unfused two-pass fp8 path."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_amd.data.synthetic import separable
+from fraud_detection_amd.ops import reference as ref
+from fraud_detection_amd.ops import scaler as S
+
+
+def test_fp8_fused_cpu_oracle_roundtrip():
+    """The CPU oracle of the fp8 fused cast: decoded rows / fp8_scale through aff == z to e4m3
+    precision, and the stats are the exact ones."""
+    X, y = separable(20_000, fraud_rate=0.02, seed=4)
+    out = torch.empty((X.shape[0], 32), dtype=torch.uint8)
+    st = S.scaler_fit_cast(X, y, out, fp8_scale=4.0)
+    ex = S.scaler_fit(X)
+    np.testing.assert_allclose(st.mean64.numpy(), ex.mean64.numpy(), rtol=1e-12, atol=1e-9)
+    v = ref.rows_to_f32(out, 4.0).double()
+    a = st.aff.double()
+    z = (v[:, :30] - a[:30]) * a[32:62]
+    z_ex = (X.double() - ex.mean64[:30]) / ex.scale64[:30]
+    err = (z - z_ex).abs() / (z_ex.abs() + 0.25)
+    assert float(err.max()) < 0.07                    # one e4m3 rounding (2^-4 relative)
+    assert torch.all(ref.rows_to_f32(out, 4.0)[:, 31] == y.float())
+
+
+@pytest.mark.gpu
+def test_fp8_fused_device_matches_oracle(dev):
+    X, y = separable(300_003, fraud_rate=0.02, seed=5)
+    out_c = torch.empty((X.shape[0], 32), dtype=torch.uint8)
+    st_c = S.scaler_fit_cast(X, y, out_c, fp8_scale=4.0)
+    out_g = torch.empty((X.shape[0], 32), dtype=torch.uint8, device=dev)
+    st_g = S.scaler_fit_cast(X.to(dev), y.to(dev), out_g, fp8_scale=4.0)
+    np.testing.assert_allclose(st_g.aff.cpu().numpy(), st_c.aff.numpy(), rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(st_g.mean64.cpu().numpy(), st_c.mean64.numpy(), rtol=1e-12, atol=1e-9)
+    dg, dc = ref.rows_to_f32(out_g.cpu(), 4.0), ref.rows_to_f32(out_c, 4.0)
+    # hardware vs software e4m3 rounding may differ on exact ties only
+    assert float((dg != dc).float().mean()) < 1e-4
+    assert torch.allclose(dg, dc, rtol=0.07, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_fp8_fused_fit_matches_bf16(dev):
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    X, y = separable(2_000_000, seed=6, device=dev)
+    Xt, yt = separable(500_000, seed=7, device=dev)
+    out = {}
+    for name, kw in (("bf16", dict(storage="bf16")), ("fp8", dict(storage="fp8")),
+                     ("fp8_unfused", dict(storage="fp8", fold_scaler=False))):
+        r = DevicePipeline(TrainConfig(seed=42, **kw)).fit(X, y)
+        out[name] = (r, evaluate(r, Xt, yt)["auc"])
+    assert out["fp8"][0].fit.converged
+    assert abs(out["fp8"][1] - out["bf16"][1]) < 1e-3
+    assert abs(out["fp8"][1] - out["fp8_unfused"][1]) < 1e-3
+    w8, wb = out["fp8"][0].w[:31], out["bf16"][0].w[:31]
+    assert np.linalg.norm(w8 - wb) / np.linalg.norm(wb) < 0.05
