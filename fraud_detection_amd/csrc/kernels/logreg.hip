@@ -41,11 +41,12 @@ __device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
   x[0] = bf16lo(v.x); x[1] = bf16hi(v.x); x[2] = bf16lo(v.y); x[3] = bf16hi(v.y);
   x[4] = bf16lo(v.z); x[5] = bf16hi(v.z); x[6] = bf16lo(v.w); x[7] = bf16hi(v.w);
 }
-__device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8], int q, int d, float inv_s) {
+// fp8 rows hold features * x_scale: decoded values stay in that scale -- 1/x_scale is folded into
+// the weights (z), the gradient (once, at the end) and the Hessian (once, at the end) instead of
+// one multiply per decoded value.
+__device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8]) {
   fp8x4_to_f32(v.x, x);  // hardware OCP e4m3 decode, 2 values per instruction
   fp8x4_to_f32(v.y, x + 4);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) x[j] = (q * 8 + j < d) ? x[j] * inv_s : x[j];
 }
 
 template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
@@ -58,11 +59,14 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   __shared__ float red[kWaves][35];
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 3, rr = lane >> 2;
-  float wl[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j];
-  const float cw0 = class_w[0], cw1 = class_w[1];
   const float inv_s = 1.0f / x_scale;
+  float wl[8], cs[8];  // cs: per-column decode scale (fp8 feature columns: 1/x_scale)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    cs[j] = (FMT == 1 && q * 8 + j < d_feat) ? inv_s : 1.0f;
+    wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j] * cs[j];
+  }
+  const float cw0 = class_w[0], cw1 = class_w[1];
   float g[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) g[j] = 0.0f;
@@ -106,7 +110,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       if constexpr (FMT == 0) unpack8<0>(cur[u], xs[u]);
-      else unpack8_fp8(cur[u], xs[u], q, d_feat, inv_s);
+      else unpack8_fp8(cur[u], xs[u]);
     }
     float zq = 0.0f, yq = 0.0f, swq = 0.0f;  // the row (u == q) whose loss this lane accounts for
 #pragma unroll
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 
   // ---- block reduction (fixed order) ----
 #pragma unroll
-  for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
+  for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]) * cs[j];
   lacc = wave_sum(lacc);
   wacc = wave_sum(wacc);
   whacc = wave_sum(whacc);
@@ -185,10 +189,13 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   if constexpr (HESS) {
     // each wave overwrites only its own tile region (same bytes it read from)
     const float hscale = (float)hess_stride;
+    const int hcol = lane & 31;
+    const float ccol = (FMT == 1 && hcol < d_feat) ? hscale * inv_s : hscale;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int row = (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-      hb[wv * 1024 + row * kCols + (lane & 31)] = acc[k] * hscale;
+      const float crow = (FMT == 1 && row < d_feat) ? inv_s : 1.0f;
+      hb[wv * 1024 + row * kCols + hcol] = acc[k] * (ccol * crow);
     }
   }
   __syncthreads();

@@ -149,8 +149,9 @@ def fused_cast_ok(X: torch.Tensor) -> bool:
 
 
 def fp8_fused_prescale(X: torch.Tensor, comm=None, sample_rows: int = 65536):
-    """(pivot [d], colscale [d]) float32 for the fp8 fused cast: mean and 1/std of the first
-    ``sample_rows`` rows (rank 0's under DP, broadcast), so the stored e4m3 values are ~z * scale.
+    """(pivot [d], colscale [d]) float32 for the fp8 fused cast: mean and 1/std of ``sample_rows``
+    rows strided over the shard (rank 0's under DP, broadcast), so the stored e4m3 values are
+    ~z * scale.
     Only a prescale: the exact statistics of the same pass define the solver's affine map."""
     n, d = X.shape
     if comm is not None and comm.world_size > 1:
@@ -163,7 +164,10 @@ def fp8_fused_prescale(X: torch.Tensor, comm=None, sample_rows: int = 65536):
 
 
 def _sample_moments(X: torch.Tensor, sample_rows: int):
-    smp = X[: max(1, min(X.shape[0], sample_rows))].double()
+    # strided over the whole shard: tables are often ordered (the creditcard Time column is
+    # sorted), so the first rows are not a sample
+    stride = max(1, X.shape[0] // max(1, sample_rows))
+    smp = X[::stride][:sample_rows].double()
     mu = smp.mean(0)
     sd = smp.std(0, unbiased=False)
     k = torch.where(sd > 0, 1.0 / sd, torch.ones_like(sd))

@@ -14,7 +14,7 @@ from fraud_detection_amd.ops import scaler as S
 def test_fp8_fused_cpu_oracle_roundtrip():
     """The CPU oracle of the fp8 fused cast: decoded rows / fp8_scale through aff == z to e4m3
     precision, and the stats are the exact ones."""
-    X, y = separable(20_000, fraud_rate=0.02, seed=4)
+    X, y = separable(140_000, fraud_rate=0.02, seed=4)   # > the 65536-row prescale sample; Time is sorted
     out = torch.empty((X.shape[0], 32), dtype=torch.uint8)
     st = S.scaler_fit_cast(X, y, out, fp8_scale=4.0)
     ex = S.scaler_fit(X)

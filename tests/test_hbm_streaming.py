@@ -39,21 +39,22 @@ def test_streaming_fit_equals_resident_cpu():
 @pytest.mark.gpu
 @pytest.mark.parametrize("storage", ["bf16", "fp8"])
 def test_streaming_fit_larger_than_budget_gpu(dev, storage):
-    """4M raw rows (480 MB fp32) against a 400 MB budget: the raw shard cannot be resident, the
-    streamed fit equals the resident unfused fit (same kernels, chunked statistics)."""
+    """4M raw rows (480 MB fp32) against a budget below raw + training rows: the raw shard cannot
+    be resident, the streamed fit equals the resident unfused fit (same kernels, chunked sums)."""
     X, y = separable(4_000_000, seed=11)
     Xt, yt = separable(500_000, seed=12, device=dev)
     Xp, yp = X.pin_memory(), y.pin_memory()
     cfg = TrainConfig(storage=storage, fold_scaler=False, seed=42)
     pipe = DevicePipeline(cfg)
-    st = pipe.fit_host(Xp, yp, device=dev, budget=400 << 20)
+    budget = (800 if storage == "bf16" else 600) << 20
+    st = pipe.fit_host(Xp, yp, device=dev, budget=budget)
     assert pipe.last_plan.mode == "stream_raw"
-    assert pipe.last_plan.raw_bytes > 400 << 20
+    assert pipe.last_plan.raw_bytes + pipe.last_plan.rows_bytes > budget
     ref = DevicePipeline(cfg).fit(X.to(dev), y.to(dev))
     np.testing.assert_allclose(st.scaler.mean64.cpu().numpy(), ref.scaler.mean64.cpu().numpy(), rtol=1e-10)
     np.testing.assert_allclose(st.w[:31], ref.w[:31], atol=1e-5)
     a1, a2 = evaluate(st, Xt, yt)["auc"], evaluate(ref, Xt, yt)["auc"]
     assert a1 > 0.95 and abs(a1 - a2) < 1e-5
     # unpinned host rows go through the staging buffers
-    st2 = DevicePipeline(cfg).fit_host(X, y, device=dev, budget=400 << 20)
+    st2 = DevicePipeline(cfg).fit_host(X, y, device=dev, budget=budget)
     np.testing.assert_allclose(st2.w[:31], st.w[:31], atol=1e-7)
