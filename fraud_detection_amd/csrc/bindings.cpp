@@ -46,6 +46,16 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.attr("ARCH") = "gfx950";
   m.attr("LR_PART_STRIDE") = fdx::kLRPartStride;
   m.def("device_info", &device_info, py::arg("device") = 0);
+  // device-side address of a pinned (hipHostMalloc'd) host buffer, 0 if it is not mapped: the
+  // small-batch serving path reads requests from / writes results to pinned memory directly
+  m.def("host_device_pointer", [](u host_ptr) -> u {
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, reinterpret_cast<void*>(host_ptr), 0) != hipSuccess) {
+      (void)hipGetLastError();
+      return 0;
+    }
+    return reinterpret_cast<u>(d);
+  });
   m.def("stream_sync", &stream_sync);
 
   // scaler

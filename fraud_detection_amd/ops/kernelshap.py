@@ -92,11 +92,22 @@ def _device_design(expl, dev):
     return t
 
 
+def _outputs(E, d, dev, out):
+    if out is not None:
+        phi, fx, f0 = out
+        if phi.shape != (E, d) or fx.shape[0] != E or f0.shape[0] < E or not phi.is_contiguous():
+            raise ValueError("out = (phi [E, d] contiguous, fx [E], f0 [E]) float32 device tensors")
+        return phi, fx, f0
+    return (torch.empty((E, d), device=dev, dtype=torch.float32), torch.empty(E, device=dev, dtype=torch.float32),
+            torch.empty(E, device=dev, dtype=torch.float32))
+
+
 def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | None = None,
-               parts: int | None = None):
+               parts: int | None = None, out=None):
     """Linear model.  X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else
     device tensors).  ``stamps`` (int64 [E, 8], tools/kernelshap_stamps.py): per-explanation phase
-    timestamps (forces parts = 1).  ``parts``: coalition parts per explanation (None = auto)."""
+    timestamps (forces parts = 1).  ``parts``: coalition parts per explanation (None = auto).
+    ``out``: preallocated (phi, fx, f0) device tensors (e.g. views of one staging buffer)."""
     _check_x(X, expl.d)
     m = native()
     dev = X.device
@@ -110,9 +121,7 @@ def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | 
         # until the batch is tiny (64 explanations: 25.8 us at P = 1 vs 31.9 at P = 8)
         parts = choose_parts(E, n_tiles, 16)
     parts = max(1, min(int(parts), MAX_PARTS, n_tiles))
-    phi = torch.empty((E, expl.d), device=dev, dtype=torch.float32)
-    fx = torch.empty(E, device=dev, dtype=torch.float32)
-    f0 = torch.empty(E, device=dev, dtype=torch.float32)
+    phi, fx, f0 = _outputs(E, expl.d, dev, out)
     ws, cnt = t["ws"].get(E, dev) if parts > 1 else (None, None)
     m.kernelshap(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]), expl.B.shape[0],
                  ptr(t["Z"]), t["S"], t["S_pad"], parts, ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi),
@@ -152,7 +161,7 @@ def _tree_device_design(expl, dev):
     return t
 
 
-def kernelshap_tree(X: torch.Tensor, expl, sync: bool = True, parts: int | None = None):
+def kernelshap_tree(X: torch.Tensor, expl, sync: bool = True, parts: int | None = None, out=None):
     """Tree ensemble (models/explainers.TreeKernelExplainer).  X [E, d] RAW fp32 on device; the
     rows are standardized on device with the model's scaler (the same kernel as predict), then
     every (coalition, background row) masked row is walked through the ensemble in the kernel."""
@@ -170,9 +179,7 @@ def kernelshap_tree(X: torch.Tensor, expl, sync: bool = True, parts: int | None 
         parts = choose_parts(E, n_tiles, 4 * _cu_count(dev))
     parts = max(1, min(int(parts), MAX_PARTS, n_tiles))
     ens = expl.ens
-    phi = torch.empty((E, expl.d), device=dev, dtype=torch.float32)
-    fx = torch.empty(E, device=dev, dtype=torch.float32)
-    f0 = torch.empty(E, device=dev, dtype=torch.float32)
+    phi, fx, f0 = _outputs(E, expl.d, dev, out)
     ws, cnt = t["ws"].get(E, dev) if parts > 1 else (None, None)
     m.kernelshap_tree(ptr(Xs), Xs.stride(0), E, expl.d, ptr(t["feat"]), ptr(t["thr"]), ptr(t["leaf"]), ens.n_trees,
                       ens.depth, float(ens.base_margin), ptr(t["bw"]), expl.bw.shape[1], expl.B.shape[0], ptr(t["Zm"]),

@@ -113,13 +113,19 @@ class _KernelTimer:
             pass
 
 
+ZERO_COPY_ROWS = int(os.environ.get("FDX_ZERO_COPY_ROWS", "256"))
+
+
 class _Staging:
     """Persistent pinned host buffers + device buffers for one engine (grown on demand).  Calls
-    are serialised by the engine lock, so one set suffices."""
+    are serialised by the engine lock, so one set suffices.  Small batches (<= ZERO_COPY_ROWS)
+    skip both memcpys: the kernel reads the request from, and writes the result to, the pinned
+    buffers through their device mapping (hipHostGetDevicePointer) -- one launch + one sync."""
 
     def __init__(self, device: torch.device, d: int, n_out: int):
         self.device, self.d, self.n_out = device, d, n_out
         self.cap = 0
+        self.in_map = self.out_map = 0
 
     def ensure(self, n: int):
         if n > self.cap:
@@ -129,6 +135,15 @@ class _Staging:
             self.hout = torch.empty(cap * self.n_out, dtype=torch.float32, pin_memory=True)
             self.dout = torch.empty(cap * self.n_out, dtype=torch.float32, device=self.device)
             self.cap = cap
+            from ..ops.native import native
+
+            m = native()
+            self.in_map = m.host_device_pointer(self.hin.data_ptr())
+            self.out_map = m.host_device_pointer(self.hout.data_ptr())
+
+    def zero_copy(self, n: int) -> bool:
+        self.ensure(n)
+        return n <= ZERO_COPY_ROWS and self.in_map != 0 and self.out_map != 0
 
     def upload(self, X: np.ndarray) -> torch.Tensor:
         n = X.shape[0]
@@ -201,20 +216,32 @@ class _EngineBase:
         if m == "linear":
             p, z, phi = self.predict_explain(X)
             return Explanation(p, z, phi, self.expected_value(), "linear", "log-odds")
-        p, z = self.predict_proba(X)
-        if X.shape[0] == 0:
-            return Explanation(p, z, np.zeros((0, self.d)), 0.0, "kernel", "probability")
+        n, d = X.shape
+        if n == 0:
+            p, z = self.predict_proba(X)
+            return Explanation(p, z, np.zeros((0, d)), 0.0, "kernel", "probability")
         ke = self.kernel_explainer()
-        if self.device.type == "cuda":
-            with self._lock, torch.cuda.stream(self._stream):
-                xd = torch.from_numpy(X).to(self.device, non_blocking=False)
-                with _KernelTimer(f"kernelshap_{self.kind}") as kt:
-                    phi, fx, f0 = self._kernel_device(xd, ke)
-                kt.observe()
-        else:
-            phi, fx, f0 = ke.explain(X)
         space = "log-odds" if ke.link == "logit_model" else "probability"
-        return Explanation(p, z, np.asarray(phi, np.float64), float(f0), "kernel", space)
+        if self.device.type != "cuda":
+            p, z = self.predict_proba(X)
+            phi, fx, f0 = ke.explain(X)
+            return Explanation(p, z, np.asarray(phi, np.float64), float(f0), "kernel", space)
+        # one upload, one launch sequence, one download: phi / f(x) / f0 land in a single staging
+        # buffer; the score comes from the kernel's f(x) (identity link: the probability)
+        with self._lock, torch.cuda.stream(self._stream):
+            st = self._xstage
+            xd = st.upload(X)
+            o = st.dout
+            outs = (o[: n * d].view(n, d), o[n * d: n * d + n], o[n * d + n: n * d + 2 * n])
+            with _KernelTimer(f"kernelshap_{self.kind}") as kt:
+                self._kernel_device(xd, ke, outs)
+            h = st.download(n * d + 2 * n)
+            kt.observe()
+        phi = h[: n * d].reshape(n, d).astype(np.float64)
+        fx = h[n * d: n * d + n].astype(np.float64)
+        z = self._logit_host(X)
+        p = fx if ke.link == "identity" else 1.0 / (1.0 + np.exp(-z))
+        return Explanation(p, z, phi, float(h[n * d + n]), "kernel", space)
 
 
 class InferenceEngine(_EngineBase):
@@ -237,6 +264,7 @@ class InferenceEngine(_EngineBase):
             self._a = torch.from_numpy(self.a.astype(np.float32)).to(self.device)
             self._c = torch.from_numpy(self.c.astype(np.float32)).to(self.device)
             self._stage = _Staging(self.device, self.d, self.d + 2)
+            self._xstage = _Staging(self.device, self.d, self.d + 2)
 
     @classmethod
     def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto",
@@ -254,18 +282,29 @@ class InferenceEngine(_EngineBase):
     # ---- core ------------------------------------------------------------------------------
     def _device_run(self, X: np.ndarray, want_phi: bool):
         n, d = X.shape
+        dphi = d if want_phi else 0
         with self._lock, torch.cuda.stream(self._stream):
             st = self._stage
-            xd = st.upload(X)
-            dphi = d if want_phi else 0
-            out = st.dout
-            prob, logit = out[:n], out[n:2 * n]
-            phi = out[2 * n:2 * n + n * dphi].view(n, dphi) if want_phi else None
             m = P.native()
-            with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
-                m.predict_shap(P.ptr(xd), 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
-                               P.ptr(prob), P.ptr(logit), P.ptr(phi) if want_phi else 0, dphi, P.stream_of(xd))
-            o = st.download(n * (2 + dphi))
+            s = torch.cuda.current_stream(self.device).cuda_stream
+            if st.zero_copy(n):
+                # request and result stay in pinned memory: no memcpy, one launch, one sync
+                st.hin[:n].numpy()[...] = X
+                xo, oo = st.in_map, st.out_map
+                with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
+                    m.predict_shap(xo, 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                                   oo, oo + 4 * n, oo + 8 * n if want_phi else 0, dphi, s)
+                torch.cuda.current_stream(self.device).synchronize()
+                o = st.hout[: n * (2 + dphi)].numpy()
+            else:
+                xd = st.upload(X)
+                out = st.dout
+                prob, logit = out[:n], out[n:2 * n]
+                phi = out[2 * n:2 * n + n * dphi].view(n, dphi) if want_phi else None
+                with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
+                    m.predict_shap(P.ptr(xd), 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                                   P.ptr(prob), P.ptr(logit), P.ptr(phi) if want_phi else 0, dphi, s)
+                o = st.download(n * (2 + dphi))
             kt.observe()
         p = o[:n].astype(np.float64)
         z = o[n:2 * n].astype(np.float64)
@@ -301,10 +340,13 @@ class InferenceEngine(_EngineBase):
         return KernelExplainer(self.a, self.bias, self.background, nsamples=self.kernel_nsamples or None,
                                link=self.kernel_link, device=str(self.device))
 
-    def _kernel_device(self, xd, ke):
+    def _kernel_device(self, xd, ke, out):
         from ..ops.kernelshap import kernelshap
 
-        return kernelshap(xd, ke)
+        return kernelshap(xd, ke, sync=False, out=out)
+
+    def _logit_host(self, X: np.ndarray) -> np.ndarray:
+        return X.astype(np.float64) @ self.a[: self.d] + self.bias
 
     def expected_value(self) -> float:
         """Model output (log-odds) at the background point: logit(x = c) = sum a*c + bias."""
@@ -342,6 +384,7 @@ class TreeInferenceEngine(_EngineBase):
 
             self._dens = DeviceEnsemble(ensemble, self.device)
             self._stage = _Staging(self.device, self.d, 1)
+            self._xstage = _Staging(self.device, self.d, self.d + 2)
 
     @classmethod
     def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto", source="local",
@@ -410,10 +453,18 @@ class TreeInferenceEngine(_EngineBase):
                                    nsamples=self.kernel_nsamples or None, link=self.kernel_link,
                                    device=str(self.device))
 
-    def _kernel_device(self, xd, ke):
+    def _kernel_device(self, xd, ke, out):
         from ..ops.kernelshap import kernelshap_tree
 
-        return kernelshap_tree(xd, ke)
+        return kernelshap_tree(xd, ke, sync=False, out=out)
+
+    def _logit_host(self, X: np.ndarray) -> np.ndarray:
+        from ..models.explainers import _standardize
+        from ..ops import reference_gbdt as RG
+
+        e = self.ens
+        return RG.predict_margin(_standardize(X, self.mean, self.scale), e.feat, e.thr, e.leaf, e.depth,
+                                 e.base_margin).astype(np.float64)
 
     def expected_value(self) -> float:
         return float(self.ens.base_margin)

@@ -116,15 +116,27 @@ def test_gpu_gbdt_alias_served_and_explained(dev, tmp_path, restore_service):
 
 
 def test_engine_staging_reuses_pinned_buffers(dev):
+    """Pinned staging is allocated once; small batches run zero-copy (kernel on the pinned
+    buffers' device mapping), large ones through the memcpy path -- same results."""
+    from fraud_detection_amd.serve import engine as E
     from fraud_detection_amd.serve.engine import InferenceEngine
 
     eng = InferenceEngine.from_paths(device="cuda")
     p1, _ = eng.predict_proba(np.asarray([GOLDEN_SAMPLE], np.float32))
+    assert eng._stage.zero_copy(1), "pinned host buffers must be device-mapped on MI355X"
     buf = eng._stage.hin.data_ptr()
-    for n in (1, 7, 200):
+    for n in (1, 7, 200, E.ZERO_COPY_ROWS + 1):
         p, z, phi = eng.predict_explain(np.asarray([GOLDEN_SAMPLE] * n, np.float32))
         assert p.shape == (n,) and phi.shape == (n, 30)
         assert p[0] == pytest.approx(0.011905, abs=5e-7)
+    assert eng._stage.hin.data_ptr() != 0
+    X2 = kaggle_like_rows(E.ZERO_COPY_ROWS + 40, seed=3)
+    a = eng.predict_explain(X2[:E.ZERO_COPY_ROWS])          # zero-copy
+    b = eng.predict_explain(X2)                              # memcpy path (grows the buffers once)
+    np.testing.assert_allclose(a[0], b[0][:E.ZERO_COPY_ROWS], rtol=0, atol=0)
+    np.testing.assert_allclose(a[2], b[2][:E.ZERO_COPY_ROWS], rtol=0, atol=0)
+    buf = eng._stage.hin.data_ptr()
+    eng.predict_proba(X2[:5])
     assert eng._stage.hin.data_ptr() == buf            # no per-request pinned allocation
     assert p1[0] == pytest.approx(0.011905, abs=5e-7)
     cpu = InferenceEngine.from_paths(device="cpu")
