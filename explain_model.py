@@ -3,7 +3,10 @@ the (already scaled) test split, summary plot and dependence plots of the top-3 
 |phi|, saved under plots/.  Fixes the reference's double scaling (explain_model.py:19; SURVEY.md
 App. D item 3): the npz features are already standardized, so the explainer runs on them
 directly, with the test set as background (LinearExplainer(model, X_test_scaled)).
-``--kernel`` additionally runs KernelSHAP (MFMA coalition GEMM) on a sample for comparison."""
+``--kernel`` additionally runs KernelSHAP (MFMA coalition GEMM) on ``--n`` rows; under torchrun
+(one rank per GPU) the rows are sharded across ranks (contiguous slices, collective C7 broadcast of
+the design is implicit: every rank builds the same cached design) and the phi rows are gathered to
+rank 0 (collective C8), which writes ``plots/kernelshap_values.npy``."""
 import argparse
 import os
 
@@ -43,11 +46,47 @@ def dependence_plot(j, phi, X, names, path):
     plt.close(fig)
 
 
+def kernel_sharded(ke, X: np.ndarray, comm):
+    """KernelSHAP of X split over the ranks of ``comm`` (None = this process): each rank explains
+    its contiguous shard on its own device, rank 0 receives every row in order."""
+    import torch
+
+    rank, world = (comm.rank, comm.world_size) if comm is not None else (0, 1)
+    lo, hi = rank * len(X) // world, (rank + 1) * len(X) // world
+    phi, fx, f0 = ke.explain(X[lo:hi])
+    if comm is None or world == 1:
+        return phi, fx, f0
+    part = torch.from_numpy(np.concatenate([phi, fx[:, None]], 1).astype(np.float64))
+    if comm.backend == "nccl":
+        part = part.to(torch.device("cuda", torch.cuda.current_device()))
+    allp, _ = comm.all_gather_rows(part)
+    allp = allp.cpu().numpy()
+    return allp[:, :-1], allp[:, -1], f0
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", action="store_true", help="also run KernelSHAP on --n rows")
-    ap.add_argument("--n", type=int, default=1000)
+    ap.add_argument("--rows", "--n", dest="n", type=int, default=1000, help="KernelSHAP rows (alias --n)")
     a = ap.parse_args(argv)
+    comm = None
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        import torch
+
+        from fraud_detection_amd.parallel.comm import Communicator
+
+        if torch.cuda.is_available():
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        comm = Communicator()
+    try:
+        return _main(a, comm)
+    finally:
+        if comm is not None:
+            comm.close()
+
+
+def _main(a, comm):
+    lead = comm is None or comm.rank == 0
     os.makedirs("plots", exist_ok=True)
     print("Loading model, scaler, and data...")
     art = load_artifacts("models/logistic_model.joblib", "models/scaler.joblib", "models/feature_names.json")
@@ -59,19 +98,28 @@ def main(argv=None):
     expl = LinearExplainer(art.coef, art.intercept, np.zeros(d), np.ones(d), background=X_test)
     print("Computing SHAP values for the test set...")
     phi = expl.shap_values(X_test)
-    summary_plot(phi, X_test, names, "plots/shap_summary.png")
     top = np.argsort(np.abs(phi).mean(0))[-3:][::-1]
-    for j in top:
-        dependence_plot(j, phi, X_test, names, f"plots/shap_dependence_feature_{j}.png")
+    if lead:
+        summary_plot(phi, X_test, names, "plots/shap_summary.png")
+        for j in top:
+            dependence_plot(j, phi, X_test, names, f"plots/shap_dependence_feature_{j}.png")
     out = {"top_features": [int(j) for j in top], "expected_value": expl.expected_value}
     if a.kernel:
         w = np.zeros(32)
         w[:d] = art.coef
         bg = X_test[np.random.default_rng(0).choice(len(X_test), min(100, len(X_test)), replace=False)]
-        ke = KernelExplainer(w, art.intercept, bg, link="identity")
-        phik, fx, f0 = ke.explain(X_test[: a.n])
-        out["kernelshap_rows"] = int(min(a.n, len(X_test)))
+        dev = "auto"
+        if comm is not None and comm.backend == "nccl":
+            import torch
+
+            dev = f"cuda:{torch.cuda.current_device()}"
+        ke = KernelExplainer(w, art.intercept, bg, link="identity", device=dev)
+        phik, fx, f0 = kernel_sharded(ke, X_test[: a.n], comm)
+        out["kernelshap_rows"] = int(phik.shape[0])
+        out["kernelshap_ranks"] = comm.world_size if comm is not None else 1
         out["kernelshap_efficiency_max_err"] = float(np.abs(phik.sum(1) - (fx - f0)).max())
+        if lead:
+            np.save("plots/kernelshap_values.npy", phik)
     print("SHAP explainability completed. Plots saved in 'plots/'.", out)
     return out
 
