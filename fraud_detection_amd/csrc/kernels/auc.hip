@@ -194,7 +194,43 @@ __global__ __launch_bounds__(1024) void auc_hist_reduce_kernel(const unsigned* _
   }
 }
 
+// Exact AUC for any class balance (the chunked path above costs ~N log(chunk) per 16384
+// positives, quadratic in spirit once positives are common).  Input: the scores sorted ascending
+// (rocPRIM radix sort through torch.sort), the inclusive prefix count of positives in that order
+// and, per element, the index where its tie segment starts (inclusive max-scan of the segment-
+// start positions).  The thread at each segment end adds
+//     pos_in_seg * (2 * neg_before_seg + neg_in_seg)
+// -- twice the pairs the segment's positives win plus the ties -- as an exact 64-bit integer:
+// the sum is order independent, so the result is bitwise deterministic and equal to sklearn's
+// tie-averaged AUC.  O(N) after the sort.
+__global__ __launch_bounds__(kThreads) void auc_segments_kernel(const float* __restrict__ s,
+                                                                const int64_t* __restrict__ pos_incl,
+                                                                const int64_t* __restrict__ seg_start,
+                                                                int64_t n, unsigned long long* __restrict__ out) {
+  unsigned long long acc = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const bool end = (i == n - 1) || !(s[i] == s[i + 1]);
+    if (!end) continue;
+    const int64_t st = seg_start[i];
+    const int64_t pos_before = st > 0 ? pos_incl[st - 1] : 0;
+    const int64_t pos_in = pos_incl[i] - pos_before;
+    const int64_t neg_in = (i + 1 - st) - pos_in;
+    const int64_t neg_before = st - pos_before;
+    acc += (unsigned long long)pos_in * (unsigned long long)(2 * neg_before + neg_in);
+  }
+  acc = wave_sum(acc);
+  if (lane_id() == 0 && acc != 0ull) atomicAdd(out, acc);
+}
+
 }  // namespace
+
+void launch_auc_segments(const float* sorted_scores, const int64_t* pos_incl, const int64_t* seg_start, int64_t n,
+                         unsigned long long* out_twice_pairs, hipStream_t stream) {
+  if (n <= 0) return;
+  const int grid = stream_grid(n, kThreads * 4, 4096);
+  auc_segments_kernel<<<grid, kThreads, 0, stream>>>(sorted_scores, pos_incl, seg_start, n, out_twice_pairs);
+  check_launch("auc_segments");
+}
 
 void launch_auc_compact(const float* scores, const uint8_t* labels, int64_t n, float* pos,
                         unsigned long long* counter, hipStream_t stream) {

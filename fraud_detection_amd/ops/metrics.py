@@ -8,6 +8,9 @@ from . import reference as ref
 from .native import native, ptr, stream_of
 
 _CHUNK = 16384
+# above this many positives the sorted-positive-chunk count (~N log(chunk) per 16384 positives)
+# loses to one full sort + an O(N) tie-segment pass
+SORT_PATH_POSITIVES = 100_000
 
 
 def _check(scores: torch.Tensor, labels: torch.Tensor):
@@ -36,11 +39,29 @@ def auc_pair_counts(scores: torch.Tensor, labels: torch.Tensor):
     N = n - P
     if P == 0 or N == 0:
         return 0, P, N
+    if min(P, N) > SORT_PATH_POSITIVES:
+        return auc_pair_counts_sorted(scores, labels), P, N
     nchunks = (P + _CHUNK - 1) // _CHUNK
     m.sort_chunks(ptr(pos), n, ptr(counter), _CHUNK, nchunks, s)
     out = torch.zeros(1, device=scores.device, dtype=torch.int64)
     m.auc_count(ptr(scores), ptr(labels), n, ptr(pos), ptr(counter), _CHUNK, nchunks, ptr(out), s)
     return int(out.item()), P, N
+
+
+def auc_pair_counts_sorted(scores: torch.Tensor, labels: torch.Tensor) -> int:
+    """twice_pairs via a device sort of all scores (rocPRIM radix sort) and one tie-segment pass
+    (auc_segments kernel): exact for any class balance, O(N log N)."""
+    n = scores.shape[0]
+    s_sorted, order = torch.sort(scores)
+    lab = labels.index_select(0, order).to(torch.int64)
+    pos_incl = torch.cumsum(lab, 0)
+    idx = torch.arange(n, device=scores.device, dtype=torch.int64)
+    is_start = torch.ones(n, dtype=torch.bool, device=scores.device)
+    is_start[1:] = s_sorted[1:] != s_sorted[:-1]
+    seg_start = torch.cummax(torch.where(is_start, idx, torch.zeros_like(idx)), 0).values
+    out = torch.zeros(1, device=scores.device, dtype=torch.int64)
+    native().auc_segments(ptr(s_sorted), ptr(pos_incl), ptr(seg_start), n, ptr(out), stream_of(scores))
+    return int(out.item())
 
 
 def roc_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:

@@ -55,3 +55,33 @@ def test_confusion_counts_match_sklearn():
     tn, fp, fn, tp = M.confusion_counts(s, y, 0.5)
     ref = confusion_matrix(y.numpy(), (s.numpy() > 0.5).astype(int)).ravel()
     assert [tn, fp, fn, tp] == list(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rate,ties", [(20_000_000, 0.5, False), (3_000_001, 0.3, True)])
+def test_exact_auc_sort_path_large_p(dev, n, rate, ties):
+    """a 20M-row 50%-positive AUC through the sort + tie-segment path is exact
+    (== sklearn), and the auto-selection takes that path above SORT_PATH_POSITIVES."""
+    import time
+
+    from sklearn.metrics import roc_auc_score
+
+    from fraud_detection_amd.ops import metrics as M
+
+    g = torch.Generator().manual_seed(n)
+    y = (torch.rand(n, generator=g) < rate).to(torch.uint8)
+    s = torch.randn(n, generator=g) + 0.8 * y.float()
+    if ties:
+        s = torch.round(s * 64) / 64          # heavy ties
+    sd, yd = s.to(dev), y.to(dev)
+    M.roc_auc(sd, yd)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    got = M.roc_auc(sd, yd)
+    dt = time.perf_counter() - t0
+    exp = roc_auc_score(y.numpy(), s.numpy())
+    assert got == pytest.approx(exp, abs=1e-12)
+    twice = M.auc_pair_counts_sorted(sd, yd)
+    P = int(y.sum())
+    assert twice == round(exp * 2 * P * (n - P))
+    assert dt < 1.0, f"{dt:.3f}s"           # measured budget (sort + scans + segment pass)
