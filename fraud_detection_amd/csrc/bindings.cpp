@@ -66,12 +66,18 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_scaler_reduce(P<const double>(partial), nblocks, P<double>(sums), S(s));
   });
   m.def("scaler_finalize", [](u sums, double n, u pivot, int d, u mean64, u var64, u scale64, u mean32, u inv32,
-                              u aff, u s) {
+                              u aff, u s, u colscale) {
     fdx::launch_scaler_finalize(P<const double>(sums), n, P<const float>(pivot), d, P<double>(mean64), P<double>(var64),
-                                P<double>(scale64), P<float>(mean32), P<float>(inv32), P<double>(aff), S(s));
+                                P<double>(scale64), P<float>(mean32), P<float>(inv32), P<double>(aff), S(s),
+                                P<const float>(colscale));
   });
   m.def("fp8_hw_check", [](u dec, u vals, int n, u enc, u s) {
     fdx::launch_fp8_hw_check(P<float>(dec), P<const float>(vals), n, P<uint8_t>(enc), S(s));
+  });
+  m.def("fp8_prescale_blocks", []() { return fdx::fp8_prescale_blocks(); });
+  m.def("fp8_prescale", [](u X, int64_t n, int d, int64_t ns, int64_t stride, u partial, u sums, u mu, u k, u s) {
+    fdx::launch_fp8_prescale(P<const float>(X), n, d, ns, stride, P<double>(partial), P<double>(sums), P<float>(mu),
+                             P<float>(k), S(s));
   });
   m.def("scaler_stats_cast_blocks", []() { return fdx::scaler_stats_cast_blocks(); });
   m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,

@@ -47,8 +47,12 @@ void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream);
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
-                            float* inv32, double* aff, hipStream_t stream);
+                            float* inv32, double* aff, hipStream_t stream,
+                            const float* colscale = nullptr);
 void launch_fp8_hw_check(float* dec, const float* vals, int n, uint8_t* enc, hipStream_t stream);
+int fp8_prescale_blocks();  // partial rows ([n][64] fp64) launch_fp8_prescale needs
+void launch_fp8_prescale(const float* X, int64_t n, int d, int64_t ns, int64_t stride, double* partial,
+                         double* sums, float* mu, float* k, hipStream_t stream);
 int scaler_stats_cast_blocks();  // resident blocks of the fused kernel on this device
 // fused K1+K2: shifted sums -> partial[nblocks][64], rows s = x - pivot in bf16, or (colscale set)
 // fp8 e4m3 of (x - pivot) * colscale * out_scale

@@ -318,7 +318,8 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
                                        const float* __restrict__ pivot, int d,
                                        double* __restrict__ mean64, double* __restrict__ var64,
                                        double* __restrict__ scale64, float* __restrict__ mean32,
-                                       float* __restrict__ inv32, double* __restrict__ aff) {
+                                       float* __restrict__ inv32, double* __restrict__ aff,
+                                       const float* __restrict__ colscale) {
   const int c = threadIdx.x;
   if (c >= kCols) return;
   // n < 0: the (all-reduced) row count rides in the unused slot sums[31] (one collective for the
@@ -338,8 +339,11 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
     mean32[c] = (float)mean;
     inv32[c] = (float)(1.0 / scale);
     if (aff) {
-      aff[c] = m;  // mean - pivot, without the cancellation of (pivot + m) - pivot
-      aff[32 + c] = 1.0 / scale;
+      // mean - pivot, without the cancellation of (pivot + m) - pivot; fp8 rows store v = s * k
+      // (colscale), so z = (s - m) / scale = (v - k m) * (1 / (scale k))
+      const double k = colscale ? (double)colscale[c] : 1.0;
+      aff[c] = m * k;
+      aff[32 + c] = 1.0 / scale / k;
     }
   } else {
     mean64[c] = 0.0; var64[c] = 0.0; scale64[c] = 1.0;
@@ -349,6 +353,48 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
       aff[32 + c] = 1.0;
     }
   }
+}
+
+// fp8 prescale sample (ops/scaler.fp8_fused_prescale): fp64 sums of ns rows strided by `stride`
+// (rows 0, stride, 2 stride, ...), shifted by row 0, in the [nblocks][64] partial layout that
+// scaler_reduce_kernel folds.  Thread (column c = tid & 31, row lane tid >> 5): the 32 lanes of a
+// half-wave read one row's d floats contiguously.
+constexpr int kSampleBlocks = 128;
+
+__global__ __launch_bounds__(kThreads) void sample_partial_kernel(const float* __restrict__ X, int d, int64_t ns,
+                                                                  int64_t stride, double* __restrict__ partial) {
+  const int c = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  double s = 0.0, q = 0.0;
+  if (c < d) {
+    const double piv = (double)X[c];
+    for (int64_t i = (int64_t)blockIdx.x * 8 + rl; i < ns; i += (int64_t)gridDim.x * 8) {
+      const double v = (double)X[i * stride * d + c] - piv;
+      s += v;
+      q = fma(v, v, q);
+    }
+  }
+  __shared__ double red[8][64];
+  red[rl][c] = s;
+  red[rl][32 + c] = q;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) a += red[r][threadIdx.x];  // fixed order
+    partial[(int64_t)blockIdx.x * 64 + threadIdx.x] = a;
+  }
+}
+
+// mean and 1 / std (population; constant columns -> 1) of the sample, as float32 prescale vectors
+__global__ void sample_finalize_kernel(const double* __restrict__ sums, const float* __restrict__ X, int d,
+                                       double ns, float* __restrict__ mu, float* __restrict__ k) {
+  const int c = threadIdx.x;
+  if (c >= d) return;
+  const double m = sums[c] / ns;
+  double var = sums[32 + c] / ns - m * m;
+  if (var < 0.0) var = 0.0;
+  mu[c] = (float)((double)X[c] + m);
+  k[c] = var > 0.0 ? (float)(1.0 / sqrt(var)) : 1.0f;
 }
 
 // K2: standardize + pad to 32 columns + cast.  OUT: 0 = bf16, 1 = fp32, 2 = fp8 e4m3fn.
@@ -683,10 +729,22 @@ void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipS
 
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
-                            float* inv32, double* aff, hipStream_t stream) {
+                            float* inv32, double* aff, hipStream_t stream, const float* colscale) {
   scaler_finalize_kernel<<<1, 64, 0, stream>>>(sums, n, pivot, d, mean64, var64, scale64, mean32,
-                                               inv32, aff);
+                                               inv32, aff, colscale);
   check_launch("scaler_finalize");
+}
+
+int fp8_prescale_blocks() { return kSampleBlocks; }
+
+void launch_fp8_prescale(const float* X, int64_t n, int d, int64_t ns, int64_t stride, double* partial,
+                         double* sums, float* mu, float* k, hipStream_t stream) {
+  if (d < 1 || d > kCols - 2) throw std::runtime_error("fp8_prescale: 1 <= d <= 30");
+  if (ns < 1 || stride < 1 || (ns - 1) * stride >= n) throw std::runtime_error("fp8_prescale: sample out of range");
+  sample_partial_kernel<<<kSampleBlocks, kThreads, 0, stream>>>(X, d, ns, stride, partial);
+  scaler_reduce_kernel<<<1, 1024, 0, stream>>>(partial, kSampleBlocks, sums);
+  sample_finalize_kernel<<<1, 64, 0, stream>>>(sums, X, d, (double)ns, mu, k);
+  check_launch("fp8_prescale");
 }
 
 int scaler_stats_cast_blocks() {

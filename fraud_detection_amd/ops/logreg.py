@@ -211,7 +211,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
                hess_refresh: int | str = "auto", n_sched: int | None = None,
-               local_warmup: bool = True, affine: torch.Tensor | None = None) -> FitInfo:
+               local_warmup: bool = True, affine: torch.Tensor | None = None, lookahead: int = 2) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -303,29 +303,32 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             first[0] = 0
         return k
 
-    # Convergence is checked one chunk behind: chunk i+1 is already queued when the host reads
-    # chunk i's `done` flag (async copy into pinned memory), so the GPU never waits on the host.
-    # Iterations after convergence are device-side no-ops.  Every rank reads identical flags.
-    if getattr(ws, "_flags", None) is None:  # pinned allocations cost tens of us: once per workspace
-        ws._flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
-        ws._events = [torch.cuda.Event(), torch.cuda.Event()]
+    # Convergence is checked ``lookahead`` chunks behind: chunks i+1..i+lookahead are already
+    # queued when the host reads chunk i's `done` flag (async copy into pinned memory), so the GPU
+    # keeps ``lookahead`` iterations of work while the host wakes up and enqueues the next one
+    # (a fp8 full-data pass is ~50 us: one chunk of slack left the GPU waiting on the host).
+    # Iterations after convergence are device-side no-ops (uniform early exit on `done`, a few us
+    # each).  Every rank reads identical flags.
+    depth = max(1, int(lookahead))
+    if getattr(ws, "_flags", None) is None or len(ws._flags) < depth + 1:
+        # pinned allocations cost tens of us: once per workspace
+        ws._flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(depth + 1)]
+        ws._events = [torch.cuda.Event() for _ in range(depth + 1)]
     flags, events = ws._flags, ws._events
-    it = enqueue_chunk(min(check_every, max_iter))
-    flags[0].copy_(ws.done, non_blocking=True)
-    events[0].record()
-    cur = 0
+    pending = []
+    it, slot = 0, 0
     while it < max_iter:
         it += enqueue_chunk(min(check_every, max_iter - it))
-        nxt = cur ^ 1
-        flags[nxt].copy_(ws.done, non_blocking=True)
-        events[nxt].record()
-        if not sync:
-            cur = nxt
+        flags[slot].copy_(ws.done, non_blocking=True)
+        events[slot].record()
+        pending.append(slot)
+        slot = (slot + 1) % (depth + 1)
+        if not sync or len(pending) <= depth:
             continue
-        events[cur].synchronize()
-        if int(flags[cur][0]):
+        c = pending.pop(0)
+        events[c].synchronize()
+        if int(flags[c][0]):
             break
-        cur = nxt
     return PendingFit(ws.state)
 
 

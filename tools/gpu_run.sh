@@ -12,6 +12,9 @@
 #   configs      tools/baseline_configs.py (every BASELINE config)
 #   latency      tools/serve_latency.py
 #   prof         rocprofv3 --kernel-trace --stats of a short bench
+#   proffp8      the same with fp8 training rows
+#   benchfp8     bench.py --storage fp8
+#   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   pmc          two PMC passes over a short bench
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
@@ -43,11 +46,18 @@ for st in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     bench50) step bench50 600 python bench.py --steps 50 --warmup 5 ;;
+    benchfp8) step benchfp8 600 python bench.py --storage fp8 ;;
+    quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
+           step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;
     latency) step latency 600 python tools/serve_latency.py --json "$OUT/latency.json" ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
       step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-extras
+      cd "$R" ;;
+    proffp8)
+      cd /tmp && export TMPDIR=/tmp
+      step proffp8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proffp8" -o run -- python3 "$R/bench.py" --storage fp8 --steps 5 --warmup 1 --no-extras
       cd "$R" ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
