@@ -171,8 +171,11 @@ __device__ __forceinline__ void finish(int e, int p, int P, int d, float* ph, co
 // ------------------------------------------------------------------------------------------------
 // Linear model
 // ------------------------------------------------------------------------------------------------
-template <int NTB, bool LOGITS, bool STAMP>
-__global__ __launch_bounds__(kThreads) void kernelshap_linear_kernel(
+// amdgpu_waves_per_eu(4): <= 128 VGPRs (126, no scratch) so 4 workgroups share a CU and a
+// 1000-explanation batch is ONE dispatch round of 1024 slots; left to itself the compiler took
+// 152 VGPRs (3 workgroups per CU: 768 + a 232-workgroup second round, 57 us vs ~35 us).
+template <int NTB, int NGL, bool LOGITS, bool STAMP>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void kernelshap_linear_kernel(
     const float* __restrict__ X, int d, const float* __restrict__ a, float bias,
     const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
     const uint16_t* __restrict__ Z, int S, int S_pad, int P, const float* __restrict__ Amat,
@@ -248,18 +251,24 @@ __global__ __launch_bounds__(kThreads) void kernelshap_linear_kernel(
       acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul1, zb1, acc, 0, 0, 0);
       return acc;
     };
-    auto epilogue = [&](const f32x16_t& acc) {
+    // NG: 8-row accumulator groups holding a real background row (group j = acc[4j..4j+3],
+    // rows 8j + {0..3} + 4h).  The partial last background tile evaluates only its leading NGL
+    // groups (compile-time, so the MFMA chain of the next tile still interleaves): 100 rows run
+    // 13 of 16 groups instead of 4 full tiles (the padded rows were 22% of the epilogue work).
+    auto epilogue = [&](const f32x16_t& acc, auto ngc) {
+      constexpr int ng = decltype(ngc)::value;
       if constexpr (LOGITS) {
         float ts = 0.0f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) ts += acc[i];
+        for (int i = 0; i < 16; ++i)
+          if ((i >> 2) < ng) ts += acc[i];
         return ts;
       } else {
         // 4 background rows per step in packed f32: rows (i, i+2) and (i+1, i+3) pair up so
         // that the sums d0 + d1 and products d0 d1 of both pairs are one v_pk_add / v_pk_mul
         f32x2_t ts2 = {0.0f, 0.0f};
 #pragma unroll
-        for (int i = 0; i < 16; i += 4) {
+        for (int i = 0; i < 4 * ng; i += 4) {
           const f32x2_t e02 = {__builtin_amdgcn_exp2f(acc[i]), __builtin_amdgcn_exp2f(acc[i + 2])};
           const f32x2_t e13 = {__builtin_amdgcn_exp2f(acc[i + 1]), __builtin_amdgcn_exp2f(acc[i + 3])};
           const f32x2_t d02 = e02 + 1.0f, d13 = e13 + 1.0f;
@@ -271,7 +280,8 @@ __global__ __launch_bounds__(kThreads) void kernelshap_linear_kernel(
         if (__builtin_isnan(ts)) {  // exp2 overflow (logit < -88) in this lane: per-element form
           ts = 0.0f;
 #pragma unroll
-          for (int i = 0; i < 16; ++i) ts += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
+          for (int i = 0; i < 16; ++i)
+            if ((i >> 2) < ng) ts += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
         }
         return ts;
       }
@@ -281,12 +291,12 @@ __global__ __launch_bounds__(kThreads) void kernelshap_linear_kernel(
     float fs = 0.0f;
     f32x16_t cur = mfma_tile(0);
 #pragma unroll
-    for (int t = 0; t < NTB; ++t) {
-      f32x16_t nxt = {};
-      if (t + 1 < NTB) nxt = mfma_tile(t + 1);
-      fs += epilogue(cur);
+    for (int t = 0; t < NTB - 1; ++t) {
+      const f32x16_t nxt = mfma_tile(t + 1);
+      fs += epilogue(cur, std::integral_constant<int, 4>{});
       cur = nxt;
     }
+    fs += epilogue(cur, std::integral_constant<int, NGL>{});
     fs += __shfl_xor(fs, 32, kWave);
     if (h == 0) ys[32 * (st - st0) + r] = fs * inv_nb;
   }
@@ -441,7 +451,7 @@ size_t part_lds(int S_pad, int P) { return (size_t)(((S_pad / 32 + P - 1) / P) *
 
 int kernelshap_linear_resident(int S_pad, int P) {
   int occ = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernelshap_linear_kernel<4, false, false>, kThreads,
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernelshap_linear_kernel<4, 4, false, false>, kThreads,
                                                    part_lds(S_pad, P)) != hipSuccess || occ < 1)
     occ = 1;
   return occ * device_cu_count();
@@ -457,26 +467,37 @@ void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float 
   if (n_expl <= 0) return;
   const dim3 grid((unsigned)((int64_t)n_expl * parts));
   const size_t lds = part_lds(S_pad, parts);
-#define FDX_KS(NT, LG, ST)                                                                             \
-  kernelshap_linear_kernel<NT, LG, ST><<<grid, kThreads, lds, stream>>>(X, d, a, bias, bg, cb, n_bg, Z, S, \
-                                                                        S_pad, parts, Amat, Az, link, phi,  \
-                                                                        fx_out, f0_out, ws, cnt, stamps)
-#define FDX_KS_NT(LG, ST)                     \
-  do {                                        \
-    switch ((n_bg + 31) >> 5) {               \
-      case 1: FDX_KS(1, LG, ST); break;       \
-      case 2: FDX_KS(2, LG, ST); break;       \
-      case 3: FDX_KS(3, LG, ST); break;       \
-      default: FDX_KS(4, LG, ST); break;      \
-    }                                         \
+#define FDX_KS(NT, NG, LG, ST)                                                                     \
+  kernelshap_linear_kernel<NT, NG, LG, ST><<<grid, kThreads, lds, stream>>>(                           \
+      X, d, a, bias, bg, cb, n_bg, Z, S, S_pad, parts, Amat, Az, link, phi, fx_out, f0_out, ws, cnt, stamps)
+#define FDX_KS_NG(NT, LG)                         \
+  do {                                            \
+    switch (ngl) {                                \
+      case 1: FDX_KS(NT, 1, LG, false); break;    \
+      case 2: FDX_KS(NT, 2, LG, false); break;    \
+      case 3: FDX_KS(NT, 3, LG, false); break;    \
+      default: FDX_KS(NT, 4, LG, false); break;   \
+    }                                             \
+  } while (0)
+#define FDX_KS_NT(LG)                           \
+  do {                                          \
+    switch (ntb) {                              \
+      case 1: FDX_KS_NG(1, LG); break;          \
+      case 2: FDX_KS_NG(2, LG); break;          \
+      case 3: FDX_KS_NG(3, LG); break;          \
+      default: FDX_KS_NG(4, LG); break;         \
+    }                                           \
   } while (0)
   const bool logits = link == 2;
-  if (stamps != nullptr) {
-    if (logits) FDX_KS_NT(true, true); else FDX_KS_NT(false, true);
+  const int ntb = (n_bg + 31) >> 5;
+  const int ngl = (n_bg - 32 * (ntb - 1) + 7) >> 3;  // groups of 8 rows holding a real row in the last tile
+  if (stamps != nullptr) {  // phase stamps: 4 full tiles (padded rows are NULL rows: same result)
+    if (logits) FDX_KS(4, 4, true, true); else FDX_KS(4, 4, false, true);
   } else {
-    if (logits) FDX_KS_NT(true, false); else FDX_KS_NT(false, false);
+    if (logits) FDX_KS_NT(true); else FDX_KS_NT(false);
   }
 #undef FDX_KS_NT
+#undef FDX_KS_NG
 #undef FDX_KS
   check_launch("kernelshap");
 }

@@ -405,8 +405,9 @@ class FunctionKernelExplainer:
         return _project(f, f0, fx, self.A, self.zM), fx, f0
 
 
-def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 100, reps: int = 5) -> dict:
-    """bench.py extra: KernelSHAP values/s for 1k explanations/batch (DP: per-rank shards)."""
+def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 100, reps: int = 20) -> dict:
+    """bench.py extra: KernelSHAP values/s for 1k explanations/batch (DP: per-rank shards).  Enough
+    warm-up and repetitions that the clock ramp and the first launch do not dominate a ~60 us batch."""
     from ..data.synthetic import separable
 
     a, c, b = res.folded()
@@ -416,8 +417,9 @@ def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 1
     Xd = Xe.to(dev)
     from ..ops.kernelshap import kernelshap
 
-    for _ in range(2):
-        kernelshap(Xd, ke)
+    kernelshap(Xd, ke)
+    for _ in range(10):
+        kernelshap(Xd, ke, sync=False)
     if comm:
         comm.barrier()
     torch.cuda.synchronize(dev)
