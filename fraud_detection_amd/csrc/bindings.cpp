@@ -158,6 +158,22 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_knn_prep(P<const float>(X), m_, m_pad, role, P<float>(out), S(s));
   });
   m.def("knn_splits", [](int mq_pad, int mc_pad) { return fdx::knn_splits(mq_pad, mc_pad); });
+  m.def("knn_lds_splits", [](int mq_pad, int mc_pad) { return fdx::knn_lds_splits(mq_pad, mc_pad); });
+  m.def("knn_topk_lds", [](u Q, int mq_pad, int mq, u C, int mc_pad, int mc, int64_t self_off, int k, u oidx,
+                           u oscore, u ws_score, u ws_idx, int nsplit, u s) {
+    fdx::launch_knn_topk_lds(P<const float>(Q), mq_pad, mq, P<const float>(C), mc_pad, mc, self_off, k, P<int>(oidx),
+                             P<float>(oscore), P<float>(ws_score), P<int>(ws_idx), nsplit, S(s));
+  });
+  m.def("knn3_splits", [](int mq_pad, int mc_pad) { return fdx::knn3_splits(mq_pad, mc_pad); });
+  m.def("knn_split", [](u Xp, int m_pad, int role, u hl, u tmax, u s) {
+    fdx::launch_knn_split(P<const float>(Xp), m_pad, role, P<uint4>(hl), P<float>(tmax), S(s));
+  });
+  m.def("knn_topk3", [](u Q, u Qhl, int mq_pad, int mq, u C, u Chl, u tmax, int mc_pad, int mc, int64_t self_off,
+                        int k, u oidx, u oscore, u wss, u wsi, int nsplit, u s) {
+    fdx::launch_knn_topk3(P<const float>(Q), P<const void>(Qhl), mq_pad, mq, P<const float>(C), P<const void>(Chl),
+                          P<const float>(tmax), mc_pad, mc, self_off, k, P<int>(oidx), P<float>(oscore),
+                          P<float>(wss), P<int>(wsi), nsplit, S(s));
+  });
   m.def("knn_topk", [](u Q, int mq_pad, int mq, u C, int mc_pad, int mc, int64_t self_off, int k, u oidx,
                        u oscore, u ws_score, u ws_idx, int nsplit, u s) {
     fdx::launch_knn_topk(P<const float>(Q), mq_pad, mq, P<const float>(C), mc_pad, mc,

@@ -208,6 +208,345 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
   }
 }
 
+// ---- LDS-tiled fp32 engine --------------------------------------------------------------------
+// At config-5 scale (170k minority rows of a 100M-row table) the candidate set (21.8 MB of prepped
+// rows) lives in the Infinity Cache, not L2, and the one-wave kernel above re-streams it for every
+// 32-query block: 116 GB at ~5.3 TB/s, 21.7 ms, MFMA ~54% busy (profiles/r2_s3h).  Here a
+// workgroup of kLW waves owns 32 kLW queries and stages each chunk of kCh candidate tiles ONCE
+// into LDS for all of its waves (double-buffered: the next chunk's global loads are in flight
+// while the waves run the MFMA chains of this one), cutting the streamed bytes kLW-fold.  Rows sit
+// at a 36-float stride: the ds_read_b128 operand reads (row j, 16 floats of half h) hit 16
+// distinct 16-B slots in every lane group, and the cooperative 8-lane row stores are contiguous.
+// Per wave the score/filter/top-k logic is the one-wave kernel's.
+constexpr int kLW = 4;         // waves (query blocks) per workgroup
+constexpr int kCh = 2;         // candidate tiles per staged chunk
+constexpr int kLdC = kCols + 4;
+
+template <int K>
+__global__ __launch_bounds__(kLW * kWave) void knn_topk_lds_kernel(const float* __restrict__ Q, int mq,
+                                                                   const float* __restrict__ C, int mc_pad, int mc,
+                                                                   int64_t self_offset, int* __restrict__ out_idx,
+                                                                   float* __restrict__ out_score) {
+  const int lane = lane_id(), wv = wave_id();
+  const int h = lane >> 5, j = lane & 31;
+  const int qg = (blockIdx.x * kLW + wv) * 32 + j;
+  const int64_t self_c = self_offset >= 0 ? self_offset + qg : -1;
+  __shared__ __attribute__((aligned(16))) float cbuf[2][kCh * 32 * kLdC];
+  __shared__ int2 qall[kLW][kQCap * kWave];
+  int2* qent = qall[wv];
+  float bq[16];
+  {
+    const float4* p = reinterpret_cast<const float4*>(Q + (int64_t)qg * kCols + 16 * h);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = p[k];
+      bq[4 * k] = v.x; bq[4 * k + 1] = v.y; bq[4 * k + 2] = v.z; bq[4 * k + 3] = v.w;
+    }
+  }
+  float bs[K];
+  int bi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  float thr = kNegBig;
+  int qn = 0;
+  auto flush = [&]() {
+    for (int e = 0; __any(e < qn); ++e) {
+      if (e < qn) {
+        const int2 v = qent[e * kWave + lane];
+        const int ci = v.y;
+        if (ci != self_c && ci < mc) topk_insert<K>(bs, bi, __int_as_float(v.x), ci);
+      }
+    }
+    qn = 0;
+    float ps[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
+    int ia = 0, ib = 0;
+    float kth = kNegBig;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float a = kNegBig, b = kNegBig;
+#pragma unroll
+      for (int u = 0; u < K; ++u) { if (u == ia) a = bs[u]; if (u == ib) b = ps[u]; }
+      const bool ta = a >= b;
+      kth = ta ? a : b;
+      ia += ta ? 1 : 0;
+      ib += ta ? 0 : 1;
+    }
+    thr = kth;
+  };
+  const int all_tiles = mc_pad / 32;
+  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
+  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  // chunk c covers tiles [t_lo + kCh c, min(t_hi, t_lo + kCh (c + 1))): kCh * 32 rows * 8 float4
+  // = 2 kCh float4 per thread (rows past the slice are not read: their tiles are not processed)
+  constexpr int kVec = kCh * 32 * 8 / (kLW * kWave);
+  float4 st[kVec];
+  auto load = [&](int c) {
+    const int64_t r0 = (int64_t)(t_lo + kCh * c) * 32;
+    const int64_t rmax = (int64_t)t_hi * 32;
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      const int e = threadIdx.x + i * kLW * kWave;  // float4 index in the chunk: row e >> 3
+      const int64_t r = r0 + (e >> 3);
+      st[i] = r < rmax ? reinterpret_cast<const float4*>(C + r * kCols)[e & 7] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      const int e = threadIdx.x + i * kLW * kWave;
+      *reinterpret_cast<float4*>(&cbuf[b][(e >> 3) * kLdC + 4 * (e & 7)]) = st[i];
+    }
+  };
+  const int nch = (t_hi - t_lo + kCh - 1) / kCh;
+  if (nch > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load(c + 1);
+    const float* cb = cbuf[c & 1];
+    const int ntile = min(kCh, t_hi - (t_lo + kCh * c));
+    for (int tt = 0; tt < ntile; ++tt) {
+      const int c0 = (t_lo + kCh * c + tt) * 32;
+      const float* crow = cb + (tt * 32 + j) * kLdC + 16 * h;
+      float ac[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 v = *reinterpret_cast<const float4*>(crow + 4 * k);
+        ac[4 * k] = v.x; ac[4 * k + 1] = v.y; ac[4 * k + 2] = v.z; ac[4 * k + 3] = v.w;
+      }
+      f32x16_t acc = {};
+#pragma unroll
+      for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[s], bq[s], acc, 0, 0, 0);
+      float mx = acc[0];
+#pragma unroll
+      for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+      if (!__any(mx >= thr)) continue;
+      const int cbase = c0 + 4 * h;
+      int qe = qn * kWave + lane;
+      const int de = (kQCap - 1) * kWave + lane;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool pass = acc[r] >= thr;
+        qent[pass ? qe : de] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
+        qe += pass ? kWave : 0;
+      }
+      qn = (qe - lane) / kWave;
+      if (__any(qn >= kQFlush)) flush();
+    }
+    if (c + 1 < nch) store((c + 1) & 1);  // that buffer was last read in chunk c - 1 (barrier since)
+    __syncthreads();
+  }
+  flush();
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float s2 = __shfl_xor(bs[k], 32, kWave);
+    const int i2 = __shfl_xor(bi[k], 32, kWave);
+    if (h == 0) topk_insert<K>(bs, bi, s2, i2);
+  }
+  if (h == 0 && qg < mq) {
+    const int64_t o = ((int64_t)blockIdx.y * mq + qg) * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      out_idx[o + k] = bi[k];
+      if (out_score) out_score[o + k] = bs[k];
+    }
+  }
+}
+
+// ---- bf16x3 MFMA filter + exact fp32 re-score ---------------------------------------------
+// The fp32 MFMA chain above is 16 x v_mfma_f32_32x32x2_f32 = 1024 SIMD cycles per 32x32 tile
+// (profiles/r1_s31: 206 us of the bench step at 13.6k minority rows).  Here every prepped row x
+// is split x = hi + lo (two bf16 rows) and the tile score is hi.hi + hi.lo + lo.hi on
+// v_mfma_f32_32x32x16_bf16 (6 MFMAs = 192 cycles), |approx - exact| <= 2^-16 sum|q_f c_f| (the
+// omitted lo.lo term, the split residuals and fp32 accumulation).  That approximate score only
+// FILTERS: a candidate passes when approx >= thr - margin, margin = 2^-13 (||q|| tmax +
+// 0.5 tmax^2) >= 8x the error bound (tmax = largest ||c|| of the tile); a tile with any pass is
+// staged to LDS in fp32 and its passing rows are re-scored exactly before the top-k insertion
+// -- no true neighbour can be filtered out, and lists, threshold and returned scores are exact
+// fp32 (ties -> smaller index).
+
+// hi/lo bf16 split of prepped rows: hl[r] = 8 x uint4 (hi cols 0..31, then lo cols 0..31);
+// role 0 (candidates) also writes tmax[r / 32] = max feature norm over the 32-row tile.
+__global__ __launch_bounds__(256) void knn_split_kernel(const float* __restrict__ Xp, int m_pad, int role,
+                                                        uint4* __restrict__ hl, float* __restrict__ tmax) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  const bool ok = r < m_pad;
+  float x[32];
+  const float4* p = reinterpret_cast<const float4*>(Xp + (int64_t)(ok ? r : 0) * kCols);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float4 v = p[k];
+    x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+  }
+  uint32_t h[16], l[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float a = x[2 * k], b = x[2 * k + 1];
+    const uint32_t ph = pack_bf16x2(a, b);
+    h[k] = ph;
+    l[k] = pack_bf16x2(a - bf16lo(ph), b - bf16hi(ph));
+  }
+  if (ok) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      hl[(int64_t)r * 8 + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
+      hl[(int64_t)r * 8 + 4 + k] = make_uint4(l[4 * k], l[4 * k + 1], l[4 * k + 2], l[4 * k + 3]);
+    }
+  }
+  if (role == 0) {
+    // candidate rows carry -0.5 ||c||^2 in column 30 (padding rows: -3e38 -> norm 0)
+    float n2 = (ok && x[30] > -1.0e37f) ? -2.0f * x[30] : 0.0f;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) n2 = fmaxf(n2, __shfl_xor(n2, o, kWave));
+    if (ok && (r & 31) == 0) tmax[r >> 5] = sqrtf(n2) * 1.0001f;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
+                                                          int mq, const float* __restrict__ C,
+                                                          const uint4* __restrict__ Chl,
+                                                          const float* __restrict__ tmax, int mc_pad, int mc,
+                                                          int64_t self_offset, int* __restrict__ out_idx,
+                                                          float* __restrict__ out_score) {
+  const int lane = threadIdx.x;
+  const int h = lane >> 5, j = lane & 31;
+  const int q0 = blockIdx.x * 32;
+  const int qg = q0 + j;
+  const int64_t self_c = self_offset >= 0 ? self_offset + qg : -1;
+  // the block's 32 query rows and the current candidate tile, fp32 (prepped), for the exact
+  // re-score from LDS (row stride 36 floats: 16 B aligned, b128 reads of 8 consecutive rows
+  // spread over the banks)
+  constexpr int kLd = kCols + 4;
+  __shared__ __attribute__((aligned(16))) float qs[32 * kLd];
+  __shared__ __attribute__((aligned(16))) float cs[32 * kLd];
+  {
+    const float4* src = reinterpret_cast<const float4*>(Q + (int64_t)q0 * kCols);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = lane + 64 * i;  // float4 index: row e >> 3, cols 4 (e & 7) ..
+      *reinterpret_cast<float4*>(&qs[(e >> 3) * kLd + 4 * (e & 7)]) = src[e];
+    }
+  }
+  __syncthreads();
+  float qn2 = 0.0f;
+#pragma unroll
+  for (int f = 0; f < 30; ++f) qn2 = fmaf(qs[j * kLd + f], qs[j * kLd + f], qn2);
+  const float qn = sqrtf(qn2);
+  // B operand (query j): MFMA 0 covers columns 8h..8h+7, MFMA 1 columns 16+8h..16+8h+7
+  const uint4* qr = Qhl + (int64_t)qg * 8;
+  const bf16x8_t qh0 = __builtin_bit_cast(bf16x8_t, qr[h]), qh1 = __builtin_bit_cast(bf16x8_t, qr[2 + h]);
+  const bf16x8_t ql0 = __builtin_bit_cast(bf16x8_t, qr[4 + h]), ql1 = __builtin_bit_cast(bf16x8_t, qr[6 + h]);
+
+  float bs[K];
+  int bi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  float thr = kNegBig;
+  // exact fp32 score of tile row rl against this lane's query (a k-ordered fmaf chain)
+  auto rescore = [&](int rl) -> float {
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float4 c = *reinterpret_cast<const float4*>(&cs[rl * kLd + 4 * k]);
+      const float4 q = *reinterpret_cast<const float4*>(&qs[j * kLd + 4 * k]);
+      acc = fmaf(q.x, c.x, acc);
+      acc = fmaf(q.y, c.y, acc);
+      acc = fmaf(q.z, c.z, acc);
+      acc = fmaf(q.w, c.w, acc);
+    }
+    return acc;
+  };
+  const int all_tiles = mc_pad / 32;
+  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
+  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  // register double buffer of the next tile: hi/lo bf16 operands of candidate row j (this lane's
+  // K half), 64 B per lane.  The fp32 rows are fetched only for a tile with a passing score (once
+  // the lists are full that is rare: half the streamed bytes of fetching them with every tile)
+  uint4 cv[4];
+  auto fetch = [&](int t, uint4 (&a)[4]) {
+    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
+    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
+  };
+  if (t_lo < t_hi) fetch(t_lo, cv);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int c0 = t * 32;
+    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, cv[0]), ch1 = __builtin_bit_cast(bf16x8_t, cv[1]);
+    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, cv[2]), cl1 = __builtin_bit_cast(bf16x8_t, cv[3]);
+    const float tm = tmax[t];
+    if (t + 1 < t_hi) fetch(t + 1, cv);
+    f32x16_t acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, ql0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
+    const float cut = thr - 0x1p-13f * fmaf(qn, tm, 0.5f * tm * tm);
+    float mx = acc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    if (!__any(mx >= cut)) continue;
+    // stage the tile's fp32 rows (lane j, h: row j, columns 16h..16h+15) and re-score exactly
+    {
+      const float4* pf = reinterpret_cast<const float4*>(C + (int64_t)(c0 + j) * kCols + 16 * h);
+      const float4 f0 = pf[0], f1 = pf[1], f2 = pf[2], f3 = pf[3];
+      float* crow = &cs[j * kLd + 16 * h];
+      *reinterpret_cast<float4*>(crow) = f0;
+      *reinterpret_cast<float4*>(crow + 4) = f1;
+      *reinterpret_cast<float4*>(crow + 8) = f2;
+      *reinterpret_cast<float4*>(crow + 12) = f3;
+    }
+    __builtin_amdgcn_wave_barrier();  // one wave: LDS ops retire in order
+    uint32_t pm = 0;  // passing accumulator rows of this lane (static indices -> no acc spill)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) pm |= (acc[r] >= cut ? 1u : 0u) << r;
+    while (pm) {
+      const int r = __builtin_ctz(pm);
+      pm &= pm - 1;
+      const int rl = 4 * h + (r & 3) + 8 * (r >> 2);
+      const int ci = c0 + rl;
+      if (ci != self_c && ci < mc) topk_insert<K>(bs, bi, rescore(rl), ci);
+    }
+    __builtin_amdgcn_wave_barrier();  // cs is rewritten by the next staging tile
+    // threshold = k-th best of the union of this lane's and its partner's (other half) lists
+    float ps[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
+    int ia = 0, ib = 0;
+    float kth = kNegBig;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float a = kNegBig, b = kNegBig;
+#pragma unroll
+      for (int u = 0; u < K; ++u) { if (u == ia) a = bs[u]; if (u == ib) b = ps[u]; }
+      const bool ta = a >= b;
+      kth = ta ? a : b;
+      ia += ta ? 1 : 0;
+      ib += ta ? 0 : 1;
+    }
+    thr = kth;
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float s2 = __shfl_xor(bs[k], 32, kWave);
+    const int i2 = __shfl_xor(bi[k], 32, kWave);
+    if (h == 0) topk_insert<K>(bs, bi, s2, i2);
+  }
+  if (h == 0 && qg < mq) {
+    const int64_t o = ((int64_t)blockIdx.y * mq + qg) * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      out_idx[o + k] = bi[k];
+      if (out_score) out_score[o + k] = bs[k];
+    }
+  }
+}
+
 // Merge the per-slice top-k lists of every query (same ordering: score desc, index asc).
 template <int K>
 __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ ps, const int* __restrict__ pi,
@@ -256,6 +595,108 @@ int knn_splits(int mq_pad, int mc_pad) {
     if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
   }
   return best;
+}
+
+int knn_lds_splits(int mq_pad, int mc_pad) {
+  static const int cap = resident_cap(knn_topk_lds_kernel<5>, kLW * kWave);
+  const int qblocks = mq_pad / (32 * kLW), tiles = mc_pad / 32;
+  int max_s = tiles / (8 * kCh);
+  if (max_s > 64) max_s = 64;
+  if (max_s < 1) max_s = 1;
+  int best = 1;
+  double best_eff = -1.0;
+  for (int s = 1; s <= max_s; ++s) {
+    const double blocks = (double)qblocks * s;
+    const double rounds = std::ceil(blocks / cap);
+    double eff = blocks / (rounds * cap);
+    eff -= 0.004 * (s - 1);
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+  }
+  return best;
+}
+
+void launch_knn_topk_lds(const float* Q, int mq_pad, int mq, const float* C, int mc_pad, int mc,
+                         int64_t self_offset, int k, int* out_idx, float* out_score, float* ws_score, int* ws_idx,
+                         int nsplit, hipStream_t stream) {
+  if (mq_pad % (32 * kLW) != 0 || mc_pad % 32 != 0)
+    throw std::runtime_error("knn_topk_lds: query pad must be x128, candidate pad x32");
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > 1 && (ws_score == nullptr || ws_idx == nullptr))
+    throw std::runtime_error("knn_topk_lds: split search needs the [nsplit][mq][k] workspaces");
+  const dim3 grid(mq_pad / (32 * kLW), nsplit);
+  int* oi = nsplit > 1 ? ws_idx : out_idx;
+  float* os = nsplit > 1 ? ws_score : out_score;
+#define FDX_KNNL(KK)                                                                                          \
+  knn_topk_lds_kernel<KK><<<grid, kLW * kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os);       \
+  if (nsplit > 1)                                                                                             \
+    knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
+  switch (k) {
+    case 1: FDX_KNNL(1); break;
+    case 2: FDX_KNNL(2); break;
+    case 3: FDX_KNNL(3); break;
+    case 4: FDX_KNNL(4); break;
+    case 5: FDX_KNNL(5); break;
+    case 6: FDX_KNNL(6); break;
+    case 7: FDX_KNNL(7); break;
+    case 8: FDX_KNNL(8); break;
+    default: throw std::runtime_error("knn_topk_lds: k must be in [1, 8]");
+  }
+#undef FDX_KNNL
+  check_launch("knn_topk_lds");
+}
+
+void launch_knn_split(const float* Xp, int m_pad, int role, uint4* hl, float* tmax, hipStream_t stream) {
+  knn_split_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(Xp, m_pad, role, hl, tmax);
+  check_launch("knn_split");
+}
+
+int knn3_splits(int mq_pad, int mc_pad) {
+  static const int cap = resident_cap(knn_topk3_kernel<5>, kWave);
+  const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
+  int max_s = tiles / 8;
+  if (max_s > 32) max_s = 32;
+  if (max_s < 1) max_s = 1;
+  int best = 1;
+  double best_eff = -1.0;
+  for (int s = 1; s <= max_s; ++s) {
+    const double blocks = (double)qblocks * s;
+    const double rounds = std::ceil(blocks / cap);
+    double eff = blocks / (rounds * cap);
+    eff -= 0.004 * (s - 1);
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+  }
+  return best;
+}
+
+void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
+                      const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
+                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream) {
+  if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk3: pads must be x32");
+  if (nsplit < 1) nsplit = 1;
+  if (nsplit > 1 && (ws_score == nullptr || ws_idx == nullptr))
+    throw std::runtime_error("knn_topk3: split search needs the [nsplit][mq][k] workspaces");
+  const dim3 grid(mq_pad / 32, nsplit);
+  int* oi = nsplit > 1 ? ws_idx : out_idx;
+  float* os = nsplit > 1 ? ws_score : out_score;
+  const uint4* qh = reinterpret_cast<const uint4*>(Qhl);
+  const uint4* chl = reinterpret_cast<const uint4*>(Chl);
+#define FDX_KNN3(KK)                                                                            \
+  knn_topk3_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, mq, C, chl, tmax, mc_pad, mc, self_offset, oi, os); \
+  if (nsplit > 1)                                                                               \
+    knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
+  switch (k) {
+    case 1: FDX_KNN3(1); break;
+    case 2: FDX_KNN3(2); break;
+    case 3: FDX_KNN3(3); break;
+    case 4: FDX_KNN3(4); break;
+    case 5: FDX_KNN3(5); break;
+    case 6: FDX_KNN3(6); break;
+    case 7: FDX_KNN3(7); break;
+    case 8: FDX_KNN3(8); break;
+    default: throw std::runtime_error("knn_topk3: k must be in [1, 8]");
+  }
+#undef FDX_KNN3
+  check_launch("knn_topk3");
 }
 
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,

@@ -112,6 +112,19 @@ void launch_sgd_update(const double* red, double* state, float* w32, int d, doub
 // role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29)
 void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, hipStream_t stream);
 int knn_splits(int mq_pad, int mc_pad);
+// bf16x3 MFMA filter + exact fp32 re-score (knn.hip): hl [m_pad][8] uint4 = hi | lo bf16 rows of
+// the prepped rows; tmax [mc_pad / 32] max candidate norm per tile (role 0 only)
+void launch_knn_split(const float* Xp, int m_pad, int role, uint4* hl, float* tmax, hipStream_t stream);
+int knn3_splits(int mq_pad, int mc_pad);
+// LDS-tiled fp32 engine: workgroups of 4 waves x 32 queries share staged candidate chunks
+// (mq_pad multiple of 128)
+int knn_lds_splits(int mq_pad, int mc_pad);
+void launch_knn_topk_lds(const float* Q, int mq_pad, int mq, const float* C, int mc_pad, int mc,
+                         int64_t self_offset, int k, int* out_idx, float* out_score, float* ws_score, int* ws_idx,
+                         int nsplit, hipStream_t stream);
+void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
+                      const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
+                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
                      float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);

@@ -23,6 +23,7 @@ from ..ops import logreg as lr_ops
 from ..ops import metrics as metric_ops
 from ..ops import predict as pred_ops
 from ..ops import scaler as scaler_ops
+from ..obs import tracing
 from ..ops.layout import BIAS_COL, DEFAULT_FP8_SCALE, NCOLS, TORCH_STORAGE
 
 
@@ -89,13 +90,24 @@ class PipelineResult:
 
 
 class _Timer:
+    """Phase timer (profile=True: device-synchronised wall time per phase) and, with
+    FDX_ROCTX_PHASES=1, a roctx marker at every phase end so ``rocprofv3 --marker-trace`` lines the
+    kernels up with the pipeline phases (the fit itself is one roctx range, see DevicePipeline)."""
+
     def __init__(self, device, enabled: bool):
         self.enabled = enabled and device.type == "cuda"
         self.device = device
         self.t = {}
         self._last = time.perf_counter()
+        self.rx = tracing.roctx_phases() if device.type == "cuda" else None
+        if self.rx is not None:
+            self.rx.roctxRangePushA(b"fdx.pipeline.fit")
 
     def mark(self, name: str):
+        if self.rx is not None:
+            tracing.roctx_mark(self.rx, "fdx.phase_end:" + name)
+            if name == "fit":  # the solver is the last phase of every fit path
+                self.rx.roctxRangePop()
         if not self.enabled:
             return
         torch.cuda.synchronize(self.device)

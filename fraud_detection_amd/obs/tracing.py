@@ -149,6 +149,7 @@ def _load_roctx():
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
             lib.roctxRangePushA.restype = ctypes.c_int
             lib.roctxRangePop.restype = ctypes.c_int
+            lib.roctxMarkA.argtypes = [ctypes.c_char_p]
             _roctx = lib
             logger.debug("roctx ranges via %s", name)
             break
@@ -171,3 +172,16 @@ def roctx_range(name: str):
     finally:
         if lib is not None:
             lib.roctxRangePop()
+
+
+def roctx_phases():
+    """The roctx library when FDX_ROCTX_PHASES=1 (pipeline phase markers: off by default, the
+    ctypes calls are host time on the fit's critical path), else None."""
+    if os.getenv("FDX_ROCTX_PHASES", "0") != "1":
+        return None
+    return _load_roctx()
+
+
+def roctx_mark(lib, name: str) -> None:
+    if lib is not None:
+        lib.roctxMarkA(name.encode())

@@ -1,6 +1,8 @@
 """K8 k-nearest neighbours (SMOTE) and K9 SMOTE sample generation."""
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -21,14 +23,40 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
     return out
 
 
+# Engines (all exact fp32 rankings, tests/test_kernels_gpu.py):
+#   fp32    one-wave workgroups (32 queries) streaming candidate tiles from L2 / Infinity Cache
+#           through a 16 x v_mfma_f32_32x32x2_f32 chain per 32x32 tile;
+#   fp32lds 4-wave workgroups (128 queries) sharing double-buffered LDS-staged candidate chunks
+#           (4x fewer streamed bytes, half the occupancy);
+#   bf16x3  hi.hi + hi.lo + lo.hi bf16 MFMA filter (5.3x fewer MFMA cycles) + exact re-score.
+# Measured on MI355X from 13.6k to 170k minority rows (profiles/r2_s3i/knn_engines.jsonl): fp32
+# is fastest at every size (46 -> 104 TFLOP/s-equivalent; fp32lds 0.66-0.99x, bf16x3 0.86-0.96x):
+# the search is bound by the per-tile filter/top-k bookkeeping beside the MFMA chain, neither by
+# the streamed bytes nor by the matrix pipe alone.  auto = fp32; FDX_KNN selects another engine.
+KNN_BF16X3_MIN_CANDIDATES = 1 << 62
+
+
+def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:
+    e = engine or os.environ.get("FDX_KNN", "auto")
+    if e == "auto":
+        return "bf16x3" if mc >= KNN_BF16X3_MIN_CANDIDATES else "fp32"
+    if e not in ("fp32", "fp32lds", "bf16x3"):
+        raise ValueError(f"unknown k-NN engine {e!r}")
+    return e
+
+
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
-             nsplit: int | None = None):
+             nsplit: int | None = None, engine: str | None = None):
     """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
     row ``self_offset + q`` and is excluded (SMOTE's self-match removal).  Returns int32 [mq, k]
     (ascending distance, ties -> smaller index) and optionally squared distances.
     ``nsplit``: candidate slices searched by separate workgroups and merged (None = auto).
+    ``engine``: "fp32" = exact fp32 MFMA chain over every candidate (16 x 32x32x2 f32 per tile);
+    "bf16x3" = hi.hi + hi.lo + lo.hi bf16 MFMA filter (6 x 32x32x16 bf16 per tile) with a provable
+    margin and exact fp32 re-scoring of the survivors; None/"auto" (FDX_KNN env) picks by size.
+    Both return the exact fp32 ranking.
     """
     for t, nm in ((Q, "Q"), (C, "C")):
         if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
@@ -47,7 +75,10 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         return (idx_t, torch.from_numpy(d2.astype(np.float32))) if want_dist else idx_t
     m = native()
     s = stream_of(Q)
+    eng = knn_engine(mq, mc, engine)
     mq_pad, mc_pad = _pad32(mq), _pad32(mc)
+    if eng == "fp32lds":
+        mq_pad = (mq_pad + 127) // 128 * 128  # 4 query blocks of 32 per workgroup
     Qc, Cc = Q.contiguous(), C.contiguous()
     # GEMM-ready rows: the -0.5||c||^2 term rides in column 30 (see knn.hip knn_prep_kernel)
     Qp = torch.empty((mq_pad, NCOLS), device=Q.device, dtype=torch.float32)
@@ -56,13 +87,29 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
-    ns = m.knn_splits(mq_pad, mc_pad) if nsplit is None else max(1, int(nsplit))
+    if nsplit is not None:
+        ns = max(1, int(nsplit))
+    else:
+        ns = {"fp32": m.knn_splits, "fp32lds": m.knn_lds_splits, "bf16x3": m.knn3_splits}[eng](mq_pad, mc_pad)
     ws_s = ws_i = None
     if ns > 1:
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
-    m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
-               ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
+    if eng == "fp32":
+        m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
+                   ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
+    elif eng == "fp32lds":
+        m.knn_topk_lds(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
+                       ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
+    else:
+        # hi/lo bf16 split of both operands (+ per-tile candidate norm bound) for the filter
+        Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
+        Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
+        tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
+        m.knn_split(ptr(Cp), mc_pad, 0, ptr(Chl), ptr(tmax), s)
+        m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
+        m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
+                    int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     if want_dist:
         qn = (Q[:, :30].double() ** 2).sum(1, keepdim=True)
         return idx, (qn - 2.0 * score.double()).float()

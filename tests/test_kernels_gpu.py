@@ -247,6 +247,54 @@ def test_knn_topk_exact(dev, mq, k):
     assert not np.any(idx == (np.arange(mq)[:, None] + off))  # self excluded
 
 
+@pytest.mark.parametrize("engine", ["bf16x3", "fp32lds"])
+@pytest.mark.parametrize("mq,k,scale", [(400, 5, 1.0), (2500, 8, 1.0), (3000, 5, 40.0)])
+def test_knn_engine_exact(dev, mq, k, scale, engine):
+    """The bf16x3 filter engine returns the exact fp32 ranking: same lists as the oracle (up to
+    fp32 rounding of near-equal distances), self excluded, including large-magnitude features."""
+    rng = np.random.default_rng(mq + 1)
+    C = np.zeros((mq + 17, 32), np.float32)
+    C[:, :30] = rng.normal(size=(mq + 17, 30)) * scale
+    Ct = torch.from_numpy(C)
+    off = 5
+    Q = Ct[off: off + mq].contiguous()
+    idx, d2 = K.knn_topk(Q.to(dev), Ct.to(dev), k=k, self_offset=off, want_dist=True, engine=engine)
+    idx_r, d2_r = ref.knn_topk(Q.numpy(), C, k, off)
+    idx = idx.cpu().numpy()
+    match = (idx == idx_r).all(1)
+    for r in np.flatnonzero(~match):
+        gap = np.abs(np.sort(d2_r[r]) - np.sort(d2.cpu().numpy()[r].astype(np.float64)))
+        assert gap.max() < 1e-3 * scale * scale, (r, idx[r], idx_r[r])
+    assert match.mean() > 0.99
+    assert not np.any(idx == (np.arange(mq)[:, None] + off))
+
+
+def test_knn_engines_agree_with_ties_and_auto_selection(dev):
+    """The engines give identical lists and scores on a coarse grid with exact ties and duplicate
+    rows, and agree on a 70k-row candidate set."""
+    rng = np.random.default_rng(11)
+    C = np.zeros((3001, 32), np.float32)
+    C[:, :30] = np.round(rng.normal(size=(3001, 30)) * 4) / 4
+    C[1500:1600] = C[100:200]
+    Ct = torch.from_numpy(C).to(dev)
+    Q = Ct[:1000].contiguous()
+    a, sa = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32")
+    b, sb = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="bf16x3")
+    assert torch.equal(a, b)
+    assert torch.allclose(sa, sb, rtol=0, atol=1e-4)
+    for ns in (1, 3, 40):  # the LDS engine runs the same MFMA chain: bit-identical lists + scores
+        c, sc = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32lds", nsplit=ns)
+        assert torch.equal(a, c) and torch.equal(sa, sc)
+    assert K.knn_engine(10, 170_000) == "fp32"  # measured fastest at every size (ops/knn.py)
+    # a larger candidate set: 256 queries, all three engines
+    Cb = torch.from_numpy(rng.normal(size=(70_000, 32)).astype(np.float32)).to(dev)
+    Qb = Cb[:256].contiguous()
+    ia = K.knn_topk(Qb, Cb, k=5, self_offset=0, engine="fp32")
+    for eng in ("fp32lds", "bf16x3"):
+        ib = K.knn_topk(Qb, Cb, k=5, self_offset=0, engine=eng)
+        assert (ia == ib).all(1).float().mean().item() > 0.99
+
+
 @pytest.mark.parametrize("nsplit", [2, 3, 7, 40])
 def test_knn_split_search_identical(dev, nsplit):
     """Candidate slices + merge must reproduce the single-slice lists exactly (incl. tie order)."""

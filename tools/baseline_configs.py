@@ -77,12 +77,14 @@ def _train_cfg(dev, n_total, storage, solver, reps=5, label=""):
     torch.cuda.reset_peak_memory_stats(dev)
     dt, res = _timed(lambda: pipe.fit(X, y), reps, warmup=1)
     ev = evaluate(res, Xt, yt)
+    phases = pipe.fit(X, y, profile=True).timings  # device-synchronised per-phase wall time
     return {"config": label, "rows_raw": n_total, "rows_post_smote": res.n_train_rows, "storage": storage,
             "solver": solver, "ms_per_fit": round(dt * 1e3, 3),
             "post_smote_rows_per_s": round(res.n_train_rows / dt, 1),
             "vs_cpu_lbfgs_fit": round(res.n_train_rows / dt / CPU_TRAIN_ROWS_PER_S, 1),
             "auc": round(ev["auc"], 6), "converged": bool(res.fit.converged), "iters": int(res.fit.n_iter),
-            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2)}
+            "peak_hbm_gib": round(torch.cuda.max_memory_allocated(dev) / 2**30, 2),
+            "phase_ms": {k: round(v * 1e3, 3) for k, v in phases.items() if isinstance(v, float)}}
 
 
 def c3(dev):
@@ -105,9 +107,13 @@ def c4(dev):
 def c5(dev):
     shard = _train_cfg(dev, 12_500_000, "fp8", "newton", reps=5,
                        label="c5 fp8 rows: the 12.5M-row per-GPU shard of 100M at DP=8")
+    shard_bf16 = _train_cfg(dev, 12_500_000, "bf16", "newton", reps=5,
+                            label="c5 reference point: the same shard with bf16 rows")
+    shard["fp8_vs_bf16_rows_per_s"] = round(shard["post_smote_rows_per_s"] / shard_bf16["post_smote_rows_per_s"], 3)
+    shard["fp8_vs_bf16_fit_phase"] = round(shard_bf16["phase_ms"]["fit"] / shard["phase_ms"]["fit"], 3)
     whole = _train_cfg(dev, 100_000_000, "fp8", "newton", reps=2,
                        label="c5 fp8 rows: all 100M rows on one GPU (HBM sizing)")
-    return [shard, whole]
+    return [shard, shard_bf16, whole]
 
 
 def main():

@@ -13,6 +13,7 @@
 #   latency      tools/serve_latency.py
 #   prof         rocprofv3 --kernel-trace --stats of a short bench
 #   proffp8      the same with fp8 training rows
+#   marker       rocprofv3 --marker-trace --kernel-trace with the pipeline's roctx phase markers
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   pmc          two PMC passes over a short bench
@@ -58,6 +59,12 @@ for st in "$@"; do
     proffp8)
       cd /tmp && export TMPDIR=/tmp
       step proffp8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proffp8" -o run -- python3 "$R/bench.py" --storage fp8 --steps 5 --warmup 1 --no-extras
+      cd "$R" ;;
+    marker)  # roctx phase markers + kernels of a short bench (FDX_ROCTX_PHASES=1)
+      cd /tmp && export TMPDIR=/tmp
+      export FDX_ROCTX_PHASES=1
+      step marker 300 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$OUT/marker" -o run -- python3 "$R/bench.py" --steps 3 --warmup 1 --no-extras
+      unset FDX_ROCTX_PHASES
       cd "$R" ;;
     pmc)
       cd /tmp && export TMPDIR=/tmp
