@@ -30,7 +30,8 @@ def main(path: str = os.getenv("DATA_CSV", "data/creditcard.csv")):
     fig.savefig("plots/amount_distribution.png")
     plt.close(fig)
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    at = torch.from_numpy(df[["Amount", "Time"]].to_numpy(np.float32)).to(dev)
+    # a 2-column frame converts column-major: the scaler kernel reads row-major rows
+    at = torch.from_numpy(np.ascontiguousarray(df[["Amount", "Time"]].to_numpy(np.float32))).to(dev)
     st = S.scaler_fit(at)
     mean, _, scale = st.numpy()
     df["scaled_amount"] = (df["Amount"] - mean[0]) / scale[0]

@@ -46,3 +46,17 @@ def test_explain_model_kernel_sharded_over_two_ranks(workdir):
     dp = np.load(workdir / "plots" / "kernelshap_values.npy")
     assert dp.shape == single.shape == (64, 30)
     np.testing.assert_allclose(dp, single, atol=1e-12)
+
+
+def test_eda_script_on_generated_csv(tmp_path):
+    """scripts/generate_synthetic_data.py -> eda.py: both plots and processed_data.csv (the
+    2-column Amount/Time frame converts column-major; the scaler needs row-major rows)."""
+    _run([os.path.join(ROOT, "scripts", "generate_synthetic_data.py"), "--separable", "--rows", "5000"], tmp_path)
+    _run([os.path.join(ROOT, "eda.py")], tmp_path)
+    assert (tmp_path / "plots" / "class_distribution.png").exists()
+    assert (tmp_path / "plots" / "amount_distribution.png").exists()
+    import pandas as pd
+
+    df = pd.read_csv(tmp_path / "processed_data.csv")
+    assert {"scaled_amount", "scaled_time", "Class"} <= set(df.columns)
+    assert abs(df["scaled_amount"].mean()) < 1e-3 and abs(df["scaled_amount"].std(ddof=0) - 1) < 1e-3

@@ -11,6 +11,7 @@
 #   bench50      bench.py --steps 50
 #   configs      tools/baseline_configs.py (every BASELINE config)
 #   latency      tools/serve_latency.py
+#   plots        the reference script chain (generate -> eda -> preprocess -> train -> evaluate -> explain) with its plots
 #   prof         rocprofv3 --kernel-trace --stats of a short bench
 #   proffp8      the same with fp8 training rows
 #   marker       rocprofv3 --marker-trace --kernel-trace with the pipeline's roctx phase markers
@@ -51,6 +52,7 @@ for st in "$@"; do
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;
+    plots) step plots 900 python scripts/run_reference_pipeline.py --out "$OUT/plots" --kernel ;;
     latency) step latency 600 python tools/serve_latency.py --json "$OUT/latency.json" ;;
     prof)
       cd /tmp && export TMPDIR=/tmp

@@ -11,8 +11,8 @@ import re
 
 
 def short(name: str) -> str:
-    n = re.sub(r"\(.*", "", name)
-    n = n.replace("void ", "").replace("fdx::(anonymous namespace)::", "")
+    n = name.replace("void ", "").replace("fdx::(anonymous namespace)::", "").replace("(anonymous namespace)::", "")
+    n = re.sub(r"\(.*", "", n)
     return n[-60:]
 
 
