@@ -31,6 +31,10 @@ import torch
 
 BASELINE_TRAIN_ROWS_PER_S = 3.50e6      # 15.97M post-SMOTE rows in 4.56 s
 BASELINE_LINEAR_SHAP_PER_S = 316e6      # BASELINE.md §2, LinearSHAP values/s at 10M
+# CPU KernelSHAP (config 4's missing CPU baseline): shap's algorithm as vectorised fp64 numpy on this
+# image's 8-core EPYC, 2042 coalitions x 100 background rows (tools/cpu_kernelshap_baseline.py,
+# profiles/r2_s3k/cpu_kernelshap_baseline.json)
+BASELINE_CPU_KERNELSHAP_PER_S = 4671.3
 
 
 def parse():
@@ -297,6 +301,7 @@ def _shap_throughput(res, dev, comm) -> dict:
         from fraud_detection_amd.models.explainers import kernelshap_throughput
 
         out.update(kernelshap_throughput(res, dev, comm))
+        out["kernelshap_vs_cpu_kernelshap"] = round(out["kernelshap_values_per_sec"] / BASELINE_CPU_KERNELSHAP_PER_S, 1)
     except (ImportError, AttributeError):
         pass
     return out
