@@ -548,29 +548,76 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
 }
 
 // Merge the per-slice top-k lists of every query (same ordering: score desc, index asc).
+// lps (a power of two >= nsplit, <= 64) lanes per query: lane s loads slice s's sorted list, then
+// log2(lps) butterfly rounds merge lists pairwise through shuffles (a static-index merge of two
+// sorted K-lists).  The order is total (candidate indices are unique across slices), so the
+// result equals sequential insertion -- but 13.6k queries x 9 slices take ~4 us instead of the
+// ~30 us of one thread walking all slices of a query.
 template <int K>
 __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict__ ps, const int* __restrict__ pi,
-                                                        int nsplit, int mq, int* __restrict__ out_idx,
+                                                        int nsplit, int lps_log2, int mq, int* __restrict__ out_idx,
                                                         float* __restrict__ out_score) {
-  const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= mq) return;
+  const int gl = blockIdx.x * 256 + threadIdx.x;
+  const int q = gl >> lps_log2, sl = gl & ((1 << lps_log2) - 1);
   float bs[K];
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  for (int s = 0; s < nsplit; ++s) {
-    const int64_t o = ((int64_t)s * mq + q) * K;
+  if (q < mq && sl < nsplit) {
+    const int64_t o = ((int64_t)sl * mq + q) * K;
 #pragma unroll
-    for (int k = 0; k < K; ++k) topk_insert<K>(bs, bi, ps[o + k], pi[o + k]);
+    for (int k = 0; k < K; ++k) { bs[k] = ps[o + k]; bi[k] = pi[o + k]; }
   }
+  for (int off = 1; off < (1 << lps_log2); off <<= 1) {
+    float os[K];
+    int oi[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    out_idx[(int64_t)q * K + k] = bi[k];
-    if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+    for (int k = 0; k < K; ++k) {
+      os[k] = __shfl_xor(bs[k], off, kWave);
+      oi[k] = __shfl_xor(bi[k], off, kWave);
+    }
+    float ns[K];
+    int ni[K];
+    int ia = 0, ib = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float a = kNegBig, b = kNegBig;
+      int ai = 0x7fffffff, bj = 0x7fffffff;
+#pragma unroll
+      for (int u = 0; u < K; ++u) {
+        if (u == ia) { a = bs[u]; ai = bi[u]; }
+        if (u == ib) { b = os[u]; bj = oi[u]; }
+      }
+      const bool ta = !better(b, bj, a, ai);
+      ns[k] = ta ? a : b;
+      ni[k] = ta ? ai : bj;
+      ia += ta ? 1 : 0;
+      ib += ta ? 0 : 1;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) { bs[k] = ns[k]; bi[k] = ni[k]; }
+  }
+  if (sl == 0 && q < mq) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      out_idx[(int64_t)q * K + k] = bi[k];
+      if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+    }
   }
 }
 
 }  // namespace
+
+int merge_log2(int nsplit) {
+  if (nsplit > kWave) throw std::runtime_error("knn merge: at most 64 candidate slices");
+  int l = 0;
+  while ((1 << l) < nsplit) ++l;
+  return l;
+}
+
+unsigned merge_blocks(int mq, int nsplit) {
+  return (unsigned)(((int64_t)mq << merge_log2(nsplit)) + 255) / 256;
+}
 
 void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, hipStream_t stream) {
   knn_prep_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, m_pad, role, out);
@@ -629,7 +676,7 @@ void launch_knn_topk_lds(const float* Q, int mq_pad, int mq, const float* C, int
 #define FDX_KNNL(KK)                                                                                          \
   knn_topk_lds_kernel<KK><<<grid, kLW * kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os);       \
   if (nsplit > 1)                                                                                             \
-    knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
+    knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {
     case 1: FDX_KNNL(1); break;
     case 2: FDX_KNNL(2); break;
@@ -683,7 +730,7 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
 #define FDX_KNN3(KK)                                                                            \
   knn_topk3_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, mq, C, chl, tmax, mc_pad, mc, self_offset, oi, os); \
   if (nsplit > 1)                                                                               \
-    knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
+    knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {
     case 1: FDX_KNN3(1); break;
     case 2: FDX_KNN3(2); break;
@@ -713,7 +760,7 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
   knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi,           \
                                                      os);                                        \
   if (nsplit > 1)                                                                               \
-    knn_merge_kernel<KK><<<(mq + 255) / 256, 256, 0, stream>>>(ws_score, ws_idx, nsplit, mq, out_idx, out_score)
+    knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {
     case 1: FDX_KNN(1); break;
     case 2: FDX_KNN(2); break;

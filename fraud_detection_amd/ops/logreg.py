@@ -211,7 +211,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
                hess_refresh: int | str = "auto", n_sched: int | None = None,
-               local_warmup: bool = True, affine: torch.Tensor | None = None, lookahead: int = 2) -> FitInfo:
+               local_warmup: bool = True, affine: torch.Tensor | None = None,
+               lookahead: int | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -309,6 +310,11 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     # (a fp8 full-data pass is ~50 us: one chunk of slack left the GPU waiting on the host).
     # Iterations after convergence are device-side no-ops (uniform early exit on `done`, a few us
     # each).  Every rank reads identical flags.
+    # Under DP every queued iteration also queues its gradient all-reduce, which runs in full even
+    # when the iteration is a no-op (~15 us per collective at 8 ranks, profiles/r2_s3l): one chunk
+    # of slack there (a full-data pass is >= ~60 us, enough to hide the host's wake-up), two alone.
+    if lookahead is None:
+        lookahead = 1 if (comm is not None and comm.world_size > 1) else 2
     depth = max(1, int(lookahead))
     if getattr(ws, "_flags", None) is None or len(ws._flags) < depth + 1:
         # pinned allocations cost tens of us: once per workspace

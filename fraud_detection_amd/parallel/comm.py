@@ -21,7 +21,12 @@ collectives run on the current compute stream; a ProcessGroup collective waits f
 stream before it starts and (synchronous ops) makes the current stream wait for its completion.
 So on every rank the device executes ONE total order of collectives -- the program order -- and
 since every rank runs the same control flow, all ranks issue the same sequence: no cross-
-communicator deadlock is possible.  ``FDX_COMM_TRACE=1`` records that sequence per rank
+communicator deadlock is possible.  Host-value exchanges (``all_gather_ints``,
+``all_reduce_scalar``) go over a third, CPU-only gloo group: they never wait for the device
+stream (a DP fit's row/minority-count exchange used to block the host behind the ~280 us fused
+scaler pass, leaving the GPU idle while the host then enqueued the k-NN), and they only ever wait
+on other ranks' HOSTS, which have already enqueued every earlier device collective -- so they
+cannot close a cycle with the device order either.  ``FDX_COMM_TRACE=1`` records that sequence per rank
 (``trace``), and tests/test_distributed.py asserts it is identical on every rank.
 
 Every collective is timed (HIP events on the stream it runs on, host clock for gloo) and
@@ -112,6 +117,18 @@ class Communicator:
         mode = os.environ.get("FDX_COMM", "auto")  # auto | rccl | torch
         if self.world_size > 1 and self.backend == "nccl" and mode in ("auto", "rccl") and torch.cuda.is_available():
             self._native = self._try_native(strict=(mode == "rccl"))
+        # CPU gloo group for host-int exchanges (created collectively: every rank, same point)
+        self._host_pg = None
+        hp = os.environ.get("FDX_HOST_PG", "1")  # 1 (nccl only) | 0 | force (also under gloo: tests)
+        if self.world_size > 1 and ((self.backend != "gloo" and hp == "1") or hp == "force"):
+            try:
+                self._host_pg = dist.new_group(backend="gloo")
+            except Exception as e:  # noqa: BLE001 - no gloo transport: host values ride the device PG
+                import logging
+
+                logging.getLogger(__name__).warning("CPU gloo group unavailable (%s): host exchanges use %s",
+                                                    e, self.backend)
+                self._host_pg = None
 
     def _try_native(self, strict: bool):
         """Bring up the native RCCL communicator and verify it with a known all-reduce; every
@@ -224,6 +241,11 @@ class Communicator:
     def all_reduce_scalar(self, x: float, op: str = "sum") -> float:
         if self.world_size == 1:
             return x
+        if self._host_pg is not None:
+            t = torch.tensor([float(x)], dtype=torch.float64)
+            with self._timed(f"all_reduce_scalar_{op}", None, "gloo-host"):
+                dist.all_reduce(t, op=_op(op), group=self._host_pg)
+                return float(t.item())
         dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
         t = torch.tensor([float(x)], dtype=torch.float64, device=dev)
         with self._timed(f"all_reduce_scalar_{op}", None, self.backend):
@@ -246,9 +268,15 @@ class Communicator:
         """All-gather a short list of ints from every rank (one small collective + one sync)."""
         if self.world_size == 1:
             return [list(vals)]
-        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else torch.device("cpu")
+        host = self._host_pg is not None
+        dev = torch.device("cuda", torch.cuda.current_device()) if (self.backend == "nccl" and not host) \
+            else torch.device("cpu")
         t = torch.tensor(list(vals), dtype=torch.int64, device=dev)
         out = [torch.zeros_like(t) for _ in range(self.world_size)]
+        if host:
+            with self._timed("all_gather_ints", None, "gloo-host"):
+                dist.all_gather(out, t, group=self._host_pg)
+                return torch.stack(out).tolist()
         with self._timed("all_gather_ints", None, self.backend):
             dist.all_gather(out, t)
             return torch.stack(out).cpu().tolist()
@@ -295,6 +323,7 @@ class Communicator:
         if self._native is not None:
             self._native.close()
             self._native = None
+        self._host_pg = None
         if self.initialized_here and dist.is_initialized():
             dist.destroy_process_group()
             self.initialized_here = False

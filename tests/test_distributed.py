@@ -261,3 +261,33 @@ def test_lost_rank_fails_the_whole_job(tmp_path):
     assert r.returncode != 0
     assert "simulated crash of rank 1" in (r.stdout + r.stderr)
     assert dt < 200, f"job took {dt:.0f}s to fail"
+
+
+def _host_pg_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank), FDX_HOST_PG="force")
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    comm = Communicator(backend="gloo")
+    assert comm._host_pg is not None
+    got = comm.all_gather_ints([rank, 10 * rank + 1])
+    s = comm.all_reduce_scalar(float(rank + 1))
+    mx = comm.max_over_ranks(float(rank))
+    mn = comm.all_reduce_scalar(float(rank + 5), op="min")
+    np.savez(os.path.join(out_dir, f"h{rank}.npz"), got=np.array(got), s=s, mx=mx, mn=mn,
+             stats=np.array(json.dumps(comm.collective_summary())))
+    comm.barrier()
+    comm.close()
+
+
+def test_host_value_exchanges_use_the_cpu_group(tmp_path):
+    """all_gather_ints / all_reduce_scalar over the CPU-only gloo group (the path DP fits take
+    under RCCL, so the row/minority-count exchange never waits for the device stream)."""
+    world = 3
+    port = _free_port()
+    mp.start_processes(_host_pg_worker, args=(world, port, str(tmp_path)), nprocs=world, start_method="spawn")
+    for r in range(world):
+        d = dict(np.load(os.path.join(tmp_path, f"h{r}.npz")))
+        assert d["got"].tolist() == [[q, 10 * q + 1] for q in range(world)]
+        assert float(d["s"]) == 6.0 and float(d["mx"]) == 2.0 and float(d["mn"]) == 5.0
+        assert "all_gather_ints" in json.loads(str(d["stats"]))
