@@ -67,7 +67,7 @@ class Settings:
     kernelshap_nsamples: int = 0   # 0 -> shap default 2*M + 2048
     kernelshap_background: int = 100   # rows saved with the model (shap_background.npy)
     kernelshap_link: str = "identity"  # identity (probabilities) | logit | logit_model
-    xai_method: str = "auto"           # auto (kernel when a background exists) | linear | kernel
+    xai_method: str = "auto"           # auto (kernel when a background exists) | linear | kernel | tree (GBDT)
     smote_k: int = 5
     seed: int = 42
     split: str = "auto"            # sklearn (reference-exact) | device (K3 kernel) | auto

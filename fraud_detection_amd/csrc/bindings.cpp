@@ -199,6 +199,12 @@ PYBIND11_MODULE(_fdx_native, m) {
                            P<unsigned long long>(stamps));
   });
   m.def("kernelshap_linear_resident", [](int S_pad, int parts) { return fdx::kernelshap_linear_resident(S_pad, parts); });
+  m.def("treeshap", [](u Xs, int ldx, int E, int d, u feat, u thr, u leaf, int T, int depth, float base, u bw,
+                       int bw_ld, int n_bg, float f0, u phi, u fx, u f0o, u s) {
+    fdx::launch_treeshap(P<const float>(Xs), ldx, E, d, P<const int>(feat), P<const float>(thr), P<const float>(leaf),
+                         T, depth, base, P<const uint32_t>(bw), bw_ld, n_bg, f0, P<float>(phi), P<float>(fx),
+                         P<float>(f0o), S(s));
+  });
   m.def("kernelshap_tree", [](u Xs, int ldx, int E, int d, u feat, u thr, u leaf, int T, int depth, float base, u bw,
                               int bw_ld, int nbg, u Zm, int nS, int S_pad, int parts, u A, u Az, int link, u phi,
                               u fx, u f0, u ws, u cnt, u s) {

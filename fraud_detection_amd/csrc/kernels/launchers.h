@@ -171,6 +171,11 @@ int kernelshap_linear_resident(int S_pad, int parts);
 // Tree-ensemble model (depth <= 5): Xs [E][ldx] standardized rows; feat/thr [T][2^D-1], leaf
 // [T][2^D]; bw [T][bw_ld] direction bits of the background rows (bit n+1 = node n goes right);
 // Zm [S_pad] coalition bitmasks (bit k = feature k taken from x).
+// interventional TreeSHAP (treeshap.hip): exact SHAP of the ensemble margin vs a background set;
+// Xs standardized [n_expl][ldx], bw [T][bw_ld] background direction bits, f0 = mean background margin
+void launch_treeshap(const float* Xs, int ldx, int n_expl, int d, const int* feat, const float* thr,
+                     const float* leaf, int ntrees, int depth, float base_margin, const uint32_t* bw, int bw_ld,
+                     int n_bg, float f0, float* phi, float* fx_out, float* f0_out, hipStream_t stream);
 void launch_kernelshap_tree(const float* Xs, int ldx, int n_expl, int d, const int* feat, const float* thr,
                             const float* leaf, int ntrees, int depth, float base_margin, const uint32_t* bw,
                             int bw_ld, int n_bg, const uint32_t* Zm, int S, int S_pad, int parts,

@@ -1,0 +1,195 @@
+// K7b interventional TreeSHAP for the GBDT family: exact SHAP values of the ensemble's margin
+// (log-odds) against a background set, per explanation.
+//
+// Reference behaviour: shap.TreeExplainer(model, data=background, feature_perturbation=
+// "interventional", model_output="raw") on the XGBClassifier the reference trains
+// (train_model.py:95-113; the explainer family of explain_model.py:24-27 for trees).  The
+// model-agnostic KernelSHAP path (kernelshap.hip, tree kernel) samples 2042 coalitions and walks
+// every tree once per (coalition, background row); this computes the same attributions exactly,
+// with no coalition sampling, in O(reachable leaves) per (background row, tree).
+//
+// For one explained row x and one background row z the hybrid game v(S) = f(x_S, z_~S) of a tree
+// is a sum over leaves of v_L 1[A_L in S, B_L disjoint from S], where A_L (B_L) are the features
+// whose split sends the path the way x (z) goes while z (x) goes the other way.  The Shapley
+// value of such a term is v_L (a-1)! b! / (a+b)! for i in A_L and -v_L a! (b-1)! / (a+b)! for i
+// in B_L (a = |A_L|, b = |B_L|).  A depth-first walk follows the x- and z-branches at nodes where
+// they differ (a feature already in A or B is forced to its side), so it visits only the leaves
+// some hybrid reaches -- 1 to a few per (z, tree) in practice, at most 2^depth.
+// phi(x) = mean over z of the per-z values; sum(phi) = margin(x) - mean_z margin(z) exactly.
+//
+// MI355X mapping: one workgroup per explanation; x's direction bits per tree go to LDS once,
+// the background rows' bits (per tree, precomputed per design) stream from L2; each thread owns
+// (tree, background row) pairs in tree-major order (neighbouring threads share a tree: uniform
+// feat / leaf reads) and accumulates into ITS OWN column of an LDS phi table, so there are no
+// atomics and the final per-feature sums run in a fixed order: bitwise deterministic.  The
+// walk is a compile-time recursion over the depth with two call sites per level (2^D inlined
+// leaf handlers).
+#include "common.h"
+#include "launchers.h"
+
+namespace fdx {
+namespace {
+
+constexpr int kTSThreads = 256;
+constexpr int kTSMaxTrees = 2048;
+constexpr int kTSLdsLeaves = 4096;  // with the 32 KB phi table: <= 64 KB of LDS per workgroup
+constexpr int kTSMaxDepth = 5;
+
+// Shapley weights of a leaf term with a = |A|, b = |B| (a + b <= depth): positive (features in
+// A) (a-1)! b! / (a+b)!, negative (features in B) a! (b-1)! / (a+b)!.
+__device__ __forceinline__ float fact(int n) {
+  float r = 1.0f;
+  for (int i = 2; i <= n; ++i) r *= (float)i;
+  return r;
+}
+
+struct LeafCtx {
+  const float* lf;    // this tree's leaves
+  float* ph;          // LDS phi table [feature][kTSThreads] (this thread's column at + tid)
+  const float* wp;    // [6][6] weights
+  const float* wn;
+};
+
+template <int D, int L>
+__device__ __forceinline__ void walk_pairs(int k, uint32_t A, uint32_t B, uint32_t xb, uint32_t zb,
+                                           const int* __restrict__ ft, const LeafCtx& c) {
+  if constexpr (L == D) {
+    if ((A | B) == 0u) return;  // x and z reach this leaf together: no attribution
+    const float v = c.lf[k - (1 << D)];
+    const int a = __popc(A), b = __popc(B);
+    const float pw = v * c.wp[a * 6 + b], nw = v * c.wn[a * 6 + b];
+    for (uint32_t m = A; m; m &= m - 1u) c.ph[(__ffs(m) - 1) * kTSThreads] += pw;
+    for (uint32_t m = B; m; m &= m - 1u) c.ph[(__ffs(m) - 1) * kTSThreads] -= nw;
+  } else {
+    const int f = ft[k - 1];
+    int c1 = 2 * k, c2 = 0;
+    uint32_t A1 = A, B2 = B;
+    if (f >= 0) {
+      const int dx = (int)((xb >> k) & 1u), dz = (int)((zb >> k) & 1u);
+      const uint32_t bit = 1u << f;
+      if (dx == dz || (A & bit)) {
+        c1 = 2 * k + dx;
+      } else if (B & bit) {
+        c1 = 2 * k + dz;
+      } else {  // the hybrids split here: x's side puts f in A, z's side puts f in B
+        c1 = 2 * k + dx;
+        A1 = A | bit;
+        c2 = 2 * k + dz;
+        B2 = B | bit;
+      }
+    }
+    walk_pairs<D, L + 1>(c1, A1, B, xb, zb, ft, c);
+    if (c2) walk_pairs<D, L + 1>(c2, A, B2, xb, zb, ft, c);
+  }
+}
+
+template <int D>
+__device__ __forceinline__ float tree_margin(uint32_t bits, const float* __restrict__ lf) {
+  int node = 1;
+#pragma unroll
+  for (int l = 0; l < D; ++l) node = (node << 1) | (int)((bits >> node) & 1u);
+  return lf[node - (1 << D)];
+}
+
+template <int D, bool LEAF_LDS>
+__global__ __launch_bounds__(kTSThreads) void treeshap_kernel(
+    const float* __restrict__ Xs, int ldx, int d, const int* __restrict__ feat, const float* __restrict__ thr,
+    const float* __restrict__ leaf, int T, float base_margin, const uint32_t* __restrict__ bw, int bw_ld,
+    int n_bg, float f0, float* __restrict__ phi, float* __restrict__ fx_out, float* __restrict__ f0_out) {
+  constexpr int NI = (1 << D) - 1, NL = 1 << D;
+  extern __shared__ __attribute__((aligned(16))) float dyn[];
+  float* ph = dyn;                          // [32][kTSThreads]
+  float* lfs = dyn + 32 * kTSThreads;       // [T][NL] when LEAF_LDS
+  __shared__ float xs[32];
+  __shared__ uint32_t xw[kTSMaxTrees];
+  __shared__ float wtab[2][36];
+  __shared__ float red[kTSThreads / kWave];
+  const int e = blockIdx.x, tid = threadIdx.x;
+  if (tid < 32) xs[tid] = tid < d ? Xs[(int64_t)e * ldx + tid] : 0.0f;
+  if (tid < 36) {
+    const int a = tid / 6, b = tid % 6;
+    const float den = fact(a + b);
+    wtab[0][tid] = (a >= 1) ? fact(a - 1) * fact(b) / den : 0.0f;
+    wtab[1][tid] = (b >= 1) ? fact(a) * fact(b - 1) / den : 0.0f;
+  }
+  for (int i = tid; i < 32 * kTSThreads; i += kTSThreads) ph[i] = 0.0f;
+  if constexpr (LEAF_LDS) {
+    for (int i = tid; i < T * NL; i += kTSThreads) lfs[i] = leaf[i];
+  }
+  __syncthreads();
+  // x's direction bits per tree (bit n + 1: internal node n sends x right; pass-through: left)
+  for (int t = tid; t < T; t += kTSThreads) {
+    uint32_t m = 0;
+    for (int n = 0; n < NI; ++n) {
+      const int f = feat[t * NI + n];
+      if (f >= 0 && !(xs[f] < thr[t * NI + n])) m |= 2u << n;
+    }
+    xw[t] = m;
+  }
+  __syncthreads();
+  const float* LF = LEAF_LDS ? lfs : leaf;
+  LeafCtx c{nullptr, ph + tid, wtab[0], wtab[1]};
+  const int npairs = T * n_bg;
+  for (int p = tid; p < npairs; p += kTSThreads) {
+    const int t = p / n_bg, b = p - t * n_bg;
+    c.lf = LF + t * NL;
+    walk_pairs<D, 0>(1, 0u, 0u, xw[t], bw[(int64_t)t * bw_ld + b], feat + t * NI, c);
+  }
+  // f(x): this thread's trees, then a fixed-order block sum (tree order within a thread)
+  float mx = 0.0f;
+  for (int t = tid; t < T; t += kTSThreads) mx += tree_margin<D>(xw[t], LF + t * NL);
+  mx = wave_sum(mx);
+  if (lane_id() == 0) red[wave_id()] = mx;
+  __syncthreads();
+  // phi[f] = (sum over this table's 256 columns) / n_bg: 8 threads per feature, 32 columns each
+  const int f = tid >> 3, part = tid & 7;
+  float s = 0.0f;
+  if (f < d) {
+    const float* row = ph + f * kTSThreads + part * 32;
+#pragma unroll 8
+    for (int i = 0; i < 32; ++i) s += row[i];
+  }
+  s = group_sum<8>(s);
+  if (part == 0 && f < d) phi[(int64_t)e * d + f] = s / (float)n_bg;
+  if (tid == 0) {
+    float m = base_margin;
+    for (int w = 0; w < kTSThreads / kWave; ++w) m += red[w];
+    fx_out[e] = m;
+    f0_out[e] = f0;
+  }
+}
+
+}  // namespace
+
+void launch_treeshap(const float* Xs, int ldx, int n_expl, int d, const int* feat, const float* thr,
+                     const float* leaf, int ntrees, int depth, float base_margin, const uint32_t* bw, int bw_ld,
+                     int n_bg, float f0, float* phi, float* fx_out, float* f0_out, hipStream_t stream) {
+  if (d < 1 || d > 30) throw std::runtime_error("treeshap: 1 <= d <= 30");
+  if (depth < 1 || depth > kTSMaxDepth) throw std::runtime_error("treeshap: depth must be in [1, 5]");
+  if (ntrees < 1 || ntrees > kTSMaxTrees) throw std::runtime_error("treeshap: 1 <= trees <= 2048");
+  if (n_bg < 1 || bw_ld < n_bg) throw std::runtime_error("treeshap: bad background");
+  if (n_expl <= 0) return;
+  const bool lds_leaves = ntrees * (1 << depth) <= kTSLdsLeaves;
+  const size_t lds = (size_t)(32 * kTSThreads + (lds_leaves ? ntrees << depth : 0)) * sizeof(float);
+#define FDX_TS(D_, LL)                                                                                  \
+  treeshap_kernel<D_, LL><<<n_expl, kTSThreads, lds, stream>>>(Xs, ldx, d, feat, thr, leaf, ntrees,     \
+                                                               base_margin, bw, bw_ld, n_bg, f0, phi,    \
+                                                               fx_out, f0_out)
+#define FDX_TS_D(D_)                              \
+  do {                                            \
+    if (lds_leaves) FDX_TS(D_, true);             \
+    else FDX_TS(D_, false);                       \
+  } while (0)
+  switch (depth) {
+    case 1: FDX_TS_D(1); break;
+    case 2: FDX_TS_D(2); break;
+    case 3: FDX_TS_D(3); break;
+    case 4: FDX_TS_D(4); break;
+    default: FDX_TS_D(5); break;
+  }
+#undef FDX_TS_D
+#undef FDX_TS
+  check_launch("treeshap");
+}
+
+}  // namespace fdx

@@ -27,6 +27,8 @@ Model-agnostic paths (shap.KernelExplainer takes any model; reference train_mode
 XGBoost model):
   * ``TreeKernelExplainer`` -- the GBDT family: every masked row z * x + (1 - z) * B_b is walked
     through the ensemble inside the kernel (kernelshap_tree_kernel), never materialised;
+  * ``TreeExplainer`` -- interventional TreeSHAP of the GBDT margin: exact, no coalition sampling
+    (treeshap.hip), orders of magnitude less work than KernelSHAP on trees;
   * ``FunctionKernelExplainer`` -- any callable on device tensors (e.g. a torch model): masked rows
     are built in chunks on the device, the model is called on them, and the shared WLS operator
     projects the coalition values.
@@ -357,6 +359,114 @@ class TreeKernelExplainer:
             return kernelshap_tree(torch.from_numpy(X).to(self.device), self)
         return kernelshap_tree_reference(_standardize(X, self.mean, self.scale), self.Bs, self.ens, self.Z, self.A,
                                          self.zM, self.link)
+
+
+def _treeshap_weights(depth: int):
+    """(Wpos, Wneg) [depth+1, depth+1]: (a-1)! b! / (a+b)! and a! (b-1)! / (a+b)!."""
+    f = [math.factorial(i) for i in range(2 * depth + 2)]
+    wp = np.zeros((depth + 1, depth + 1))
+    wn = np.zeros((depth + 1, depth + 1))
+    for a in range(depth + 1):
+        for b in range(depth + 1 - a):
+            if a:
+                wp[a, b] = f[a - 1] * f[b] / f[a + b]
+            if b:
+                wn[a, b] = f[a] * f[b - 1] / f[a + b]
+    return wp, wn
+
+
+def treeshap_reference(Xs: np.ndarray, Bs: np.ndarray, ens) -> tuple:
+    """fp64 oracle of interventional TreeSHAP on STANDARDIZED rows (treeshap.hip's algorithm):
+    per (x, background z, tree) a depth-first walk over the leaves some hybrid x_S z_~S reaches,
+    leaf value v with A (features taken from x where z goes the other way) and B (vice versa)
+    contributes v (a-1)! b! / (a+b)! to every i in A and -v a! (b-1)! / (a+b)! to every i in B.
+    Returns (phi [E, d] of the margin, margin(x) [E], f0 = mean background margin)."""
+    Xs = np.asarray(Xs, np.float32)
+    Bs = np.asarray(Bs, np.float32)
+    xw = tree_direction_bits(Xs, ens)
+    bw = tree_direction_bits(Bs, ens)
+    D = ens.depth
+    wp, wn = _treeshap_weights(D)
+    E, d = Xs.shape
+    nb = Bs.shape[0]
+    phi = np.zeros((E, d))
+
+    def walk(t, k, level, A, B, xb, zb, acc):
+        if level == D:
+            if A or B:
+                v = float(ens.leaf[t, k - (1 << D)])
+                a, b = bin(A).count("1"), bin(B).count("1")
+                for i in range(d):
+                    if A >> i & 1:
+                        acc[i] += v * wp[a, b]
+                    if B >> i & 1:
+                        acc[i] -= v * wn[a, b]
+            return
+        f = int(ens.feat[t, k - 1])
+        if f < 0:
+            return walk(t, 2 * k, level + 1, A, B, xb, zb, acc)
+        dx, dz = (xb >> k) & 1, (zb >> k) & 1
+        bit = 1 << f
+        if dx == dz or A & bit:
+            return walk(t, 2 * k + dx, level + 1, A, B, xb, zb, acc)
+        if B & bit:
+            return walk(t, 2 * k + dz, level + 1, A, B, xb, zb, acc)
+        walk(t, 2 * k + dx, level + 1, A | bit, B, xb, zb, acc)
+        walk(t, 2 * k + dz, level + 1, A, B | bit, xb, zb, acc)
+
+    for e in range(E):
+        acc = np.zeros(d)
+        for b in range(nb):
+            for t in range(ens.n_trees):
+                walk(t, 1, 0, 0, 0, int(xw[t, e]), int(bw[t, b]), acc)
+        phi[e] = acc / nb
+    fx = _margins_from_bits(xw, ens).astype(np.float64)
+    f0 = float(np.mean(_margins_from_bits(bw, ens).astype(np.float64)))
+    return phi, fx, f0
+
+
+class TreeExplainer:
+    """Interventional TreeSHAP of a tree ensemble (ops/gbdt.TreeEnsemble on standardized rows)
+    over RAW inputs, in margin (log-odds) space -- shap.TreeExplainer(model, data=background,
+    feature_perturbation="interventional") semantics, exact (no coalition sampling): the fast
+    explainer of the GBDT family (csrc/kernels/treeshap.hip).  Background: <= 1024 raw rows."""
+
+    link = "logit_model"
+
+    def __init__(self, ens, mean, scale, background: np.ndarray, device="auto"):
+        B = np.asarray(background, np.float32)
+        if B.shape[0] < 1 or B.shape[0] > 1024:
+            raise ValueError("1..1024 background rows")
+        if ens.depth > 5:
+            raise ValueError("TreeSHAP kernel supports depth <= 5 (the reference trains max_depth=5)")
+        self.ens = ens
+        self.d = B.shape[1]
+        self.mean = np.asarray(mean, np.float64)
+        self.scale = np.asarray(scale, np.float64)
+        self.B = B
+        self.Bs = _standardize(B, self.mean, self.scale)
+        self.bw = tree_direction_bits(self.Bs, ens)
+        # expected value: mean background margin (float32 tree-order sums, as the predict kernel)
+        self.f0 = float(np.mean(_margins_from_bits(self.bw, ens).astype(np.float64)))
+        self.device = torch.device("cuda", 0) if (device == "auto" and torch.cuda.is_available()) else torch.device(
+            "cpu" if device == "auto" else device)
+        self._dev_cache = None
+
+    @property
+    def expected_value(self) -> float:
+        return self.f0
+
+    def shap_values(self, X) -> np.ndarray:
+        return self.explain(X)[0]
+
+    def explain(self, X):
+        """-> (phi [E, d], margin(x) [E], f0) in log-odds space; sum(phi) = margin(x) - f0."""
+        X = np.ascontiguousarray(X, np.float32)
+        if self.device.type == "cuda":
+            from ..ops.treeshap import treeshap
+
+            return treeshap(torch.from_numpy(X).to(self.device), self)
+        return treeshap_reference(_standardize(X, self.mean, self.scale), self.Bs, self.ens)
 
 
 class FunctionKernelExplainer:

@@ -83,7 +83,7 @@ class Explanation:
     logit: np.ndarray       # [B] model log-odds / margin
     phi: np.ndarray         # [B, d] attributions
     base_value: float       # E[f] over the background, in phi's space
-    method: str             # "linear" | "kernel"
+    method: str             # "linear" | "kernel" | "tree"
     space: str              # "log-odds" | "probability"
 
 
@@ -197,8 +197,8 @@ class _EngineBase:
         method = (method or "auto").lower()
         if method == "auto":
             return "kernel" if self.has_background else self.default_method
-        if method == "kernel" and not self.has_background:
-            raise ValueError("KernelSHAP needs a background (shap_background.npy next to the model)")
+        if method in ("kernel", "tree") and not self.has_background:
+            raise ValueError(f"{method} SHAP needs a background (shap_background.npy next to the model)")
         if method not in self.methods:
             raise ValueError(f"{self.kind} model supports {self.methods}, not {method!r}")
         return method
@@ -213,6 +213,8 @@ class _EngineBase:
     def explain(self, X: np.ndarray, method: str = "auto") -> Explanation:
         X = self._check(X)
         m = self.resolve_method(method)
+        if m == "tree":
+            return self._explain_tree(X)
         if m == "linear":
             p, z, phi = self.predict_explain(X)
             return Explanation(p, z, phi, self.expected_value(), "linear", "log-odds")
@@ -360,7 +362,7 @@ class TreeInferenceEngine(_EngineBase):
     """GBDT family: standardize -> tree ensemble (fdx-gbdt/1 JSON, no pickle)."""
 
     kind = "gbdt"
-    methods = ("kernel",)
+    methods = ("kernel", "tree")  # tree: interventional TreeSHAP of the margin (exact, log-odds)
     default_method = "kernel"
 
     def __init__(self, ensemble, mean, var, scale, feature_names, device: str = "auto", source: str = "local",
@@ -445,6 +447,38 @@ class TreeInferenceEngine(_EngineBase):
         """(prob, margin, phi) with KernelSHAP phi (the only explainer of a tree model here)."""
         e = self.explain(X, "kernel")
         return e.prob, e.logit, e.phi
+
+    def tree_explainer(self):
+        if getattr(self, "_texpl", None) is None:
+            if not self.has_background:
+                raise ValueError("TreeSHAP needs a background (shap_background.npy next to the model)")
+            from ..models.explainers import TreeExplainer
+
+            self._texpl = TreeExplainer(self.ens, self.mean, self.scale, self.background, device=str(self.device))
+        return self._texpl
+
+    def _explain_tree(self, X: np.ndarray) -> "Explanation":
+        """Interventional TreeSHAP (log-odds): one staging upload, one launch sequence, one download."""
+        te = self.tree_explainer()
+        n, d = X.shape
+        if self.device.type != "cuda" or n == 0:
+            phi, fx, f0 = te.explain(X) if n else (np.zeros((0, d)), np.zeros(0), te.expected_value)
+            return Explanation(1.0 / (1.0 + np.exp(-fx)), fx, np.asarray(phi, np.float64), float(f0), "tree",
+                               "log-odds")
+        from ..ops.treeshap import treeshap
+
+        with self._lock, torch.cuda.stream(self._stream):
+            st = self._xstage
+            xd = st.upload(X)
+            o = st.dout
+            outs = (o[: n * d].view(n, d), o[n * d: n * d + n], o[n * d + n: n * d + 2 * n])
+            with _KernelTimer("treeshap_gbdt") as kt:
+                treeshap(xd, te, sync=False, out=outs)
+            h = st.download(n * d + 2 * n)
+            kt.observe()
+        phi = h[: n * d].reshape(n, d).astype(np.float64)
+        fx = h[n * d: n * d + n].astype(np.float64)
+        return Explanation(1.0 / (1.0 + np.exp(-fx)), fx, phi, float(h[n * d + n]), "tree", "log-odds")
 
     def _make_kernel_explainer(self):
         from ..models.explainers import TreeKernelExplainer

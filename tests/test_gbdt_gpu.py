@@ -141,3 +141,27 @@ def test_gbdt_hipgraph_replay_bit_identical(dev):
     for k in ("feat", "bin", "thr", "gain", "leaf"):
         assert np.array_equal(getattr(g_ens, k), getattr(e_ens, k)), k
     assert torch.equal(g_m, e_m)
+
+
+@pytest.mark.parametrize("depth,n_bg", [(5, 32), (3, 7)])
+def test_treeshap_kernel_matches_oracle(dev, depth, n_bg):
+    """Interventional TreeSHAP on the device (treeshap.hip) vs the fp64 oracle of the same
+    algorithm (exact vs brute-force Shapley in tests/test_treeshap.py): same attributions to fp32
+    accumulation order, efficiency, bitwise run-to-run determinism."""
+    from fraud_detection_amd.models.explainers import TreeExplainer
+
+    Xd, yd, X, _ = _data(60_000, 30, seed=31)
+    ens = gb.fit(Xd, yd, gb.GBDTParams(n_estimators=40, max_depth=depth))
+    mean, scale = X.mean(0).astype(np.float64), X.std(0).astype(np.float64)
+    raw = (X * scale + mean).astype(np.float32)  # the explainer standardizes raw rows
+    te_g = TreeExplainer(ens, mean, scale, raw[:n_bg], device=str(dev))
+    te_c = TreeExplainer(ens, mean, scale, raw[:n_bg], device="cpu")
+    rows = raw[1000:1012]
+    pg, fg, f0g = te_g.explain(rows)
+    pc, fc, f0c = te_c.explain(rows)
+    np.testing.assert_allclose(pg, pc, atol=2e-5)
+    np.testing.assert_allclose(fg, fc, atol=1e-5)
+    assert f0g == pytest.approx(f0c)
+    np.testing.assert_allclose(pg.sum(1), fg - f0g, atol=1e-4)
+    pg2, _, _ = te_g.explain(rows)
+    assert np.array_equal(pg, pg2)

@@ -163,3 +163,31 @@ def test_worker_spawns_one_process_per_gpu(monkeypatch):
     monkeypatch.setattr(subprocess, "Popen", P)
     assert W.main(["--gpus", "4", "--app", "nope:app"]) == 3
     assert seen == ["0", "1", "2", "3"]
+
+
+def test_gbdt_worker_explains_with_treeshap(tmp_path, restore_service, monkeypatch):
+    """FDX_XAI_METHOD=tree: the worker explains the served GBDT with interventional TreeSHAP
+    (exact, margin space): stored phi equal the TreeExplainer oracle and sum to margin - E[margin]."""
+    from fraud_detection_amd.models.explainers import TreeExplainer
+
+    monkeypatch.setenv("FDX_XAI_METHOD", "tree")
+    kw, res, X = gbdt_registered(tmp_path)
+    app, xt = _service(tmp_path, **kw)
+    rows = X[:3].numpy()
+    with TestClient(app) as c:
+        eng = app.state.fdx["engine"]
+        txs = []
+        for r in rows:
+            tx = str(uuid.uuid4())
+            c.post("/predict", json={"features": r.tolist(), "transaction_id": tx})
+            txs.append(tx)
+        assert Worker(xt.celery_app, batch=16).run_once() == 3
+        mean, _, scale = res.scaler.numpy()
+        phi_ref, fx_ref, f0_ref = TreeExplainer(res.ensemble, mean, scale, eng.background, device="cpu").explain(rows)
+        for j, tx in enumerate(txs):
+            e = c.get(f"/explain/{tx}").json()
+            assert e["explainer"] == "tree"
+            phi = np.array([e["shap_values"][n] for n in e["feature_names"]])
+            np.testing.assert_allclose(phi, phi_ref[j], atol=1e-9)
+            assert e["base_value"] == pytest.approx(f0_ref)
+            assert phi.sum() == pytest.approx(fx_ref[j] - f0_ref, abs=1e-5)
