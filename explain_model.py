@@ -6,7 +6,10 @@ directly, with the test set as background (LinearExplainer(model, X_test_scaled)
 ``--kernel`` additionally runs KernelSHAP (MFMA coalition GEMM) on ``--n`` rows; under torchrun
 (one rank per GPU) the rows are sharded across ranks (contiguous slices, collective C7 broadcast of
 the design is implicit: every rank builds the same cached design) and the phi rows are gathered to
-rank 0 (collective C8), which writes ``plots/kernelshap_values.npy``."""
+rank 0 (collective C8), which writes ``plots/kernelshap_values.npy``.  ``--tree``: when a GBDT was
+trained (``train_model.py --model gbdt`` -> models/xgb_model.json), explain it with interventional
+TreeSHAP (exact, margin space; shap.TreeExplainer(model, data=background) semantics) on --n rows:
+plots/treeshap_summary.png and plots/treeshap_values.npy."""
 import argparse
 import os
 
@@ -68,6 +71,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--kernel", action="store_true", help="also run KernelSHAP on --n rows")
     ap.add_argument("--rows", "--n", dest="n", type=int, default=1000, help="KernelSHAP rows (alias --n)")
+    ap.add_argument("--tree", action="store_true", help="TreeSHAP of the GBDT model (models/xgb_model.json)")
     a = ap.parse_args(argv)
     comm = None
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
@@ -120,8 +124,35 @@ def _main(a, comm):
         out["kernelshap_efficiency_max_err"] = float(np.abs(phik.sum(1) - (fx - f0)).max())
         if lead:
             np.save("plots/kernelshap_values.npy", phik)
+    if a.tree and lead:
+        out.update(tree_explain(X_test, names, a.n))
     print("SHAP explainability completed. Plots saved in 'plots/'.", out)
     return out
+
+
+def tree_explain(X_test, names, n) -> dict:
+    """Interventional TreeSHAP of the GBDT on the (standardized) test rows, background = 100 test
+    rows: the ensemble was trained on standardized rows, so the explainer's scaler is identity."""
+    import json
+
+    from fraud_detection_amd.models.explainers import TreeExplainer
+    from fraud_detection_amd.models.gbdt import MODEL_FILE
+    from fraud_detection_amd.ops.gbdt import TreeEnsemble
+
+    path = os.path.join("models", MODEL_FILE)
+    if not os.path.exists(path):
+        raise SystemExit(f"--tree needs a GBDT model at {path} (train_model.py --model gbdt)")
+    with open(path) as f:
+        ens = TreeEnsemble.from_dict(json.load(f))
+    d = X_test.shape[1]
+    bg = X_test[np.random.default_rng(1).choice(len(X_test), min(100, len(X_test)), replace=False)]
+    te = TreeExplainer(ens, np.zeros(d), np.ones(d), bg)
+    rows = X_test[:n]
+    phi, fx, f0 = te.explain(rows)
+    summary_plot(phi, rows, names, "plots/treeshap_summary.png")
+    np.save("plots/treeshap_values.npy", phi)
+    return {"treeshap_rows": int(phi.shape[0]), "treeshap_expected_value": float(f0),
+            "treeshap_efficiency_max_err": float(np.abs(phi.sum(1) - (fx - f0)).max())}
 
 
 if __name__ == "__main__":

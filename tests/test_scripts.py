@@ -60,3 +60,18 @@ def test_eda_script_on_generated_csv(tmp_path):
     df = pd.read_csv(tmp_path / "processed_data.csv")
     assert {"scaled_amount", "scaled_time", "Class"} <= set(df.columns)
     assert abs(df["scaled_amount"].mean()) < 1e-3 and abs(df["scaled_amount"].std(ddof=0) - 1) < 1e-3
+
+
+def test_explain_model_tree_shap_of_a_gbdt(workdir):
+    """explain_model.py --tree: interventional TreeSHAP of models/xgb_model.json on the test rows."""
+    import json
+
+    from test_treeshap import random_ensemble
+
+    ens = random_ensemble(30, 4, 12, 5)
+    with open(workdir / "models" / "xgb_model.json", "w") as f:
+        json.dump(ens.to_dict(), f)
+    out = _run([os.path.join(ROOT, "explain_model.py"), "--tree", "--rows", "50"], workdir)
+    assert "treeshap_rows" in out
+    phi = np.load(workdir / "plots" / "treeshap_values.npy")
+    assert phi.shape == (50, 30) and (workdir / "plots" / "treeshap_summary.png").exists()
