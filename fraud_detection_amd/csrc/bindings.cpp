@@ -232,11 +232,19 @@ PYBIND11_MODULE(_fdx_native, m) {
                            P<const float>(cuts), ginv, hinv, lam, mcw, gamma, P<int>(feat), P<int>(bin), P<float>(thr),
                            P<double>(gain), P<long long>(ng), P<long long>(nh), S(s));
   });
-  m.def("gbdt_partition", [](u bins, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u boff, int nblocks,
-                             u seg, u segR, u ridx_out, u nid_out, u s) {
-    fdx::launch_gbdt_partition(P<const uint8_t>(bins), P<const int>(ridx), P<const uint8_t>(nid), n, P<const int>(feat),
+  m.def("gbdt_transpose", [](u bins, int64_t n, int d, u binsT, int64_t ldt, u s) {
+    fdx::launch_gbdt_transpose(P<const uint8_t>(bins), n, d, P<uint8_t>(binsT), ldt, S(s));
+  });
+  m.def("gbdt_partition", [](u binsT, int64_t ldt, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u boff,
+                             int nblocks, u seg, u segR, u ridx_out, u nid_out, u s) {
+    fdx::launch_gbdt_partition(P<const uint8_t>(binsT), ldt, P<const int>(ridx), P<const uint8_t>(nid), n, P<const int>(feat),
                                P<const int>(bin), level, P<uint8_t>(flag), P<int64_t>(boff), nblocks, P<int64_t>(seg),
                                P<int64_t>(segR), P<int>(ridx_out), P<uint8_t>(nid_out), S(s));
+  });
+  m.def("gbdt_round_init", [](u hist, int64_t hist_words, u seg, u gcnt, int64_t n, int64_t n_global, u ridx, u nid,
+                              u s) {
+    fdx::launch_gbdt_round_init(P<unsigned long long>(hist), hist_words, P<int64_t>(seg), P<int64_t>(gcnt), n,
+                                n_global, P<int>(ridx), P<uint8_t>(nid), S(s));
   });
   m.def("gbdt_leaf", [](u ng, u nh, int depth, double ginv, double hinv, double lam, double mcw, double eta, u leaf,
                         u s) {

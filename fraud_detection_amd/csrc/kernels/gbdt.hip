@@ -279,23 +279,80 @@ __device__ __forceinline__ void part_range(int64_t n, int64_t* lo, int64_t* hi) 
   *hi = min(*lo + per, n);
 }
 
-__device__ __forceinline__ bool goes_right(const uint8_t* bins, int64_t row, int node,
+// binsT: FEATURE-major u8 bins [d][ldt].  The partition reads one feature byte per row: from the
+// row-major [n][32] layout every such byte costs a whole sector (~205 MB of traffic per level at
+// 6.4M rows); a feature column is 1 B/row and stays L2 / Infinity Cache resident.
+__device__ __forceinline__ bool goes_right(const uint8_t* binsT, int64_t ldt, int64_t row, int node,
                                            const int* feat, const int* bin) {
   const int f = feat[node];
-  return f >= 0 && bins[row * kGBRowBytes + f] > bin[node];
+  return f >= 0 && binsT[(int64_t)f * ldt + row] > bin[node];
 }
 
+// Row-major [n][32] -> feature-major [d][ldt] (ldt % 4 == 0): a 256-row tile through LDS, each
+// thread writes 4 consecutive rows of one feature as one 32-bit word.  Once per fit.
+__global__ __launch_bounds__(256) void gbdt_transpose_kernel(const uint8_t* __restrict__ bins, int64_t n, int d,
+                                                             uint8_t* __restrict__ binsT, int64_t ldt) {
+  __shared__ uint32_t tile[256][kGBRowBytes / 4 + 1];
+  const int64_t r0 = (int64_t)blockIdx.x * 256;
+  const int t = threadIdx.x;
+  {
+    const int64_t r = r0 + t;
+    const uint4* src = reinterpret_cast<const uint4*>(bins + r * kGBRowBytes);
+    uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+    if (r < n) {
+      a = src[0];
+      b = src[1];
+    }
+    tile[t][0] = a.x; tile[t][1] = a.y; tile[t][2] = a.z; tile[t][3] = a.w;
+    tile[t][4] = b.x; tile[t][5] = b.y; tile[t][6] = b.z; tile[t][7] = b.w;
+  }
+  __syncthreads();
+  const int q = t & 63;  // rows 4q .. 4q+3 of the tile
+  for (int f = t >> 6; f < d; f += 4) {
+    uint32_t w = 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w |= ((tile[4 * q + i][f >> 2] >> (8 * (f & 3))) & 0xffu) << (8 * i);
+    const int64_t r = r0 + 4 * q;
+    if (r < ldt) *reinterpret_cast<uint32_t*>(binsT + (int64_t)f * ldt + r) = w;
+  }
+}
+
+// 4 consecutive rows per thread per step with every load of the step issued before the first
+// use (the one-row loop was a chain of dependent load latencies: ~45 us per level at 6.4M rows)
+constexpr int kPartRows = 4;
+
 __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
-    const uint8_t* __restrict__ bins, const int* __restrict__ ridx, const uint8_t* __restrict__ nid,
+    const uint8_t* __restrict__ binsT, int64_t ldt, const int* __restrict__ ridx, const uint8_t* __restrict__ nid,
     int64_t n, const int* __restrict__ feat, const int* __restrict__ bin,
     uint8_t* __restrict__ flag, int64_t* __restrict__ counts) {
   int64_t lo, hi;
   part_range(n, &lo, &hi);
   int64_t c = 0;
-  for (int64_t p = lo + threadIdx.x; p < hi; p += kPartThreads) {
-    const bool r = goes_right(bins, ridx[p], nid[p], feat, bin);
-    flag[p] = r;
-    c += r;
+  for (int64_t p0 = lo + (int64_t)kPartRows * threadIdx.x; p0 < hi; p0 += (int64_t)kPartRows * kPartThreads) {
+    int row[kPartRows], nd[kPartRows];
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const bool ok = p0 + u < hi;
+      row[u] = ok ? ridx[p0 + u] : 0;
+      nd[u] = ok ? (int)nid[p0 + u] : 0;
+    }
+    int f[kPartRows], bv[kPartRows];
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      f[u] = feat[nd[u]];
+      bv[u] = bin[nd[u]];
+    }
+    uint8_t v[kPartRows];
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) v[u] = f[u] >= 0 ? binsT[(int64_t)f[u] * ldt + row[u]] : 0;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      if (p0 + u < hi) {
+        const bool r = f[u] >= 0 && (int)v[u] > bv[u];
+        flag[p0 + u] = r;
+        c += r;
+      }
+    }
   }
   c = wave_sum(c);
   __shared__ int64_t red[kPartThreads / kWave];
@@ -339,42 +396,84 @@ __global__ __launch_bounds__(kWave) void gbdt_seg_kernel(const uint8_t* __restri
   }
 }
 
+// Stable scatter of this block's range into the children's segments, kPartRows consecutive rows
+// per thread per step (one block-wide exclusive prefix of the right-going counts per 1024 rows).
 __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
     const uint8_t* __restrict__ flag, const int64_t* __restrict__ boff, const int* __restrict__ ridx,
     const uint8_t* __restrict__ nid, int64_t n, const int64_t* __restrict__ seg,
     const int64_t* __restrict__ segR, int* __restrict__ ridx_out, uint8_t* __restrict__ nid_out) {
   int64_t lo, hi;
   part_range(n, &lo, &hi);
-  __shared__ int64_t wave_cnt[kPartThreads / kWave];
+  __shared__ int wave_cnt[kPartThreads / kWave];
   int64_t base = boff[blockIdx.x];
   const int lane = lane_id(), w = wave_id();
-  for (int64_t p0 = lo; p0 < hi; p0 += kPartThreads) {
-    const int64_t p = p0 + threadIdx.x;
-    const bool ok = p < hi;
-    const bool r = ok && flag[p];
-    const unsigned long long m = __ballot(r);
-    const int before = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wave_cnt[w] = __popcll(m);
-    __syncthreads();
-    int64_t R = base;  // global rights before p
-    for (int i = 0; i < w; ++i) R += wave_cnt[i];
-    R += before;
-    if (ok) {
-      const int node = nid[p];
-      const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
-      const int64_t rin = R - segR[node];  // rights before p inside the segment
-      const int64_t nr = seg[2 * (2 * node + 2) + 1];
-      int64_t dst;
-      uint8_t child;
-      if (r) { dst = sb + (sc - nr) + rin; child = (uint8_t)(2 * node + 2); }
-      else { dst = sb + (p - sb) - rin; child = (uint8_t)(2 * node + 1); }
-      ridx_out[dst] = ridx[p];
-      nid_out[dst] = child;
+  for (int64_t s0 = lo; s0 < hi; s0 += (int64_t)kPartRows * kPartThreads) {
+    const int64_t p0 = s0 + (int64_t)kPartRows * threadIdx.x;
+    int rf[kPartRows], ri[kPartRows], nd[kPartRows];
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const bool ok = p0 + u < hi;
+      rf[u] = ok ? (int)flag[p0 + u] : 0;
+      ri[u] = ok ? ridx[p0 + u] : 0;
+      nd[u] = ok ? (int)nid[p0 + u] : 0;
     }
+    const int cnt = rf[0] + rf[1] + rf[2] + rf[3];
+    int incl = cnt;  // inclusive wave scan of the per-thread counts (thread order = row order)
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int t = __shfl_up(incl, o, kWave);
+      if (lane >= o) incl += t;
+    }
+    if (lane == kWave - 1) wave_cnt[w] = incl;
+    __syncthreads();
+    int64_t R = base + (incl - cnt);  // global rights before row p0
     int64_t total = 0;
-    for (int i = 0; i < kPartThreads / kWave; ++i) total += wave_cnt[i];
+#pragma unroll
+    for (int i = 0; i < kPartThreads / kWave; ++i) {
+      if (i < w) R += wave_cnt[i];
+      total += wave_cnt[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) {
+      const int64_t p = p0 + u;
+      if (p < hi) {
+        const int node = nd[u];
+        const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
+        const int64_t rin = R - segR[node];  // rights before p inside the segment
+        const int64_t nr = seg[2 * (2 * node + 2) + 1];
+        int64_t dst;
+        uint8_t child;
+        if (rf[u]) { dst = sb + (sc - nr) + rin; child = (uint8_t)(2 * node + 2); }
+        else { dst = sb + (p - sb) - rin; child = (uint8_t)(2 * node + 1); }
+        ridx_out[dst] = ri[u];
+        nid_out[dst] = child;
+      }
+      R += rf[u];
+    }
     base += total;
     __syncthreads();
+  }
+}
+
+// ---- per-round state -------------------------------------------------------------------------
+// One launch instead of five torch fills/copies at the start of every boosting round: zero the
+// level histograms, root segment [0, n) and its global count, ridx = 0..n-1, nid = 0 (root).
+__global__ __launch_bounds__(256) void gbdt_round_init_kernel(unsigned long long* __restrict__ hist,
+                                                              int64_t hist_words, int64_t* __restrict__ seg,
+                                                              int64_t* __restrict__ gcnt, int64_t n,
+                                                              int64_t n_global, int* __restrict__ ridx,
+                                                              uint8_t* __restrict__ nid) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = i0; i < hist_words; i += stride) hist[i] = 0ull;
+  for (int64_t i = i0; i < n; i += stride) {
+    ridx[i] = (int)i;
+    nid[i] = 0;
+  }
+  if (i0 == 0) {
+    seg[0] = 0;
+    seg[1] = n;
+    gcnt[0] = n_global;
   }
 }
 
@@ -499,12 +598,19 @@ void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level,
   check_launch("gbdt_split");
 }
 
-void launch_gbdt_partition(const uint8_t* bins, const int* ridx, const uint8_t* nid, int64_t n,
+void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT, int64_t ldt, hipStream_t stream) {
+  if (ldt < n || ldt % 4 != 0) throw std::runtime_error("gbdt_transpose: ldt must be >= n and a multiple of 4");
+  if (n <= 0) return;
+  gbdt_transpose_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(bins, n, d, binsT, ldt);
+  check_launch("gbdt_transpose");
+}
+
+void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
                            const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
                            int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
                            hipStream_t stream) {
   if (nblocks > 4096) throw std::runtime_error("gbdt: at most 4096 partition blocks");
-  gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(bins, ridx, nid, n, feat, bin, flag, boff);
+  gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(binsT, ldt, ridx, nid, n, feat, bin, flag, boff);
   check_launch("gbdt_part_count");
   launch_exclusive_scan_small(boff, nblocks, boff + nblocks, stream);
   gbdt_seg_kernel<<<1 << level, kWave, 0, stream>>>(flag, boff, n, nblocks, level, seg, segR);
@@ -512,6 +618,13 @@ void launch_gbdt_partition(const uint8_t* bins, const int* ridx, const uint8_t* 
   gbdt_part_scatter_kernel<<<nblocks, kPartThreads, 0, stream>>>(flag, boff, ridx, nid, n, seg, segR,
                                                                  ridx_out, nid_out);
   check_launch("gbdt_part_scatter");
+}
+
+void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
+                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream) {
+  gbdt_round_init_kernel<<<device_cu_count() * 4, 256, 0, stream>>>(hist, hist_words, seg, gcnt, n, n_global, ridx,
+                                                                    nid);
+  check_launch("gbdt_round_init");
 }
 
 void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,

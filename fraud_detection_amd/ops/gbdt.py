@@ -168,7 +168,6 @@ class _Workspace:
         self.hist = torch.zeros(((1 << depth) - 1) * HIST_ENTRIES, dtype=torch.int64, device=dev)
         self.ng = torch.zeros(nheap, dtype=torch.int64, device=dev)
         self.nh = torch.zeros(nheap, dtype=torch.int64, device=dev)
-        self.iota = torch.arange(n, dtype=torch.int32, device=dev)
 
 
 def _resume(checkpoint, sig, T):
@@ -254,6 +253,11 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     m = native()
     dev = X.device
     ws = _Workspace(n, D, dev)
+    # feature-major copy of the bins for the partition's one-byte-per-row reads (gbdt.hip)
+    ldt = max(4, (n + 255) // 256 * 256)
+    binsT = torch.empty(d * ldt, dtype=torch.uint8, device=dev)
+    if n:
+        m.gbdt_transpose(ptr(bins), n, d, ptr(binsT), ldt, stream_of(X))
     dist = comm is not None and comm.world_size > 1
     n_global = int(comm.all_reduce_scalar(float(n))) if dist else n
     ct = torch.from_numpy(np.ascontiguousarray(cuts_np[:d])).to(dev)
@@ -268,8 +272,6 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         for name, dst in (("feat", feat), ("bin", binv), ("thr", thr), ("gain", gain), ("leaf", leaf)):
             dst[:t0].copy_(torch.from_numpy(np.ascontiguousarray(prev[name])))
         margin = predict_margin(X, _partial(t0, prev["feat"], prev["bin"], prev["thr"], prev["gain"], prev["leaf"]))
-    root = torch.tensor([[0, n]], dtype=torch.int64, device=dev)
-    groot = torch.tensor([n_global], dtype=torch.int64, device=dev)
     lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
     ginv, hinv = 1.0 / gscale, 1.0 / hscale
 
@@ -277,12 +279,10 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         """One boosting round: a fixed launch sequence with static pointers (graph-capturable)."""
         st = stream_of(X)  # the capture stream while a hipGraph is being recorded
         m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
-        ws.hist.zero_()
-        ws.seg[0:1].copy_(root)
-        ws.gcnt[0:1].copy_(groot)
+        # zero histograms, root segment + global count, ridx = iota, nid = root: one launch
+        m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n, n_global,
+                          ptr(ws.ridx[0]), ptr(ws.nid[0]), st)
         cur = 0
-        ws.ridx[0].copy_(ws.iota)
-        ws.nid[0].zero_()
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
             m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
@@ -292,7 +292,7 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,
                          ptr(o_feat), ptr(o_bin), ptr(o_thr), ptr(o_gain), ptr(ws.ng), ptr(ws.nh), st)
             if n:
-                m.gbdt_partition(ptr(bins), ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
+                m.gbdt_partition(ptr(binsT), ldt, ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
                                  level, ptr(ws.flag), ptr(ws.boff), PART_BLOCKS, ptr(ws.seg), ptr(ws.segR),
                                  ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st)
             else:
