@@ -251,9 +251,11 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_gbdt_leaf(P<const long long>(ng), P<const long long>(nh), depth, ginv, hinv, lam, mcw, eta,
                           P<float>(leaf), S(s));
   });
-  m.def("gbdt_margin", [](u ridx, u nid, int64_t n, u leaf, int depth, u margin, u s) {
-    fdx::launch_gbdt_margin(P<const int>(ridx), P<const uint8_t>(nid), n, P<const float>(leaf), depth,
-                            P<float>(margin), S(s));
+  m.def("gbdt_margin", [](u binsT, int64_t ldt, int64_t n, u feat, u bin, u leaf, int depth, u margin, u label,
+                          float spw, float gscale, float hscale, u gh, u s) {
+    fdx::launch_gbdt_margin(P<const uint8_t>(binsT), ldt, n, P<const int>(feat), P<const int>(bin),
+                            P<const float>(leaf), depth, P<float>(margin), P<const uint8_t>(label), spw, gscale,
+                            hscale, P<int2>(gh), S(s));
   });
   m.def("gbdt_predict", [](u X, int64_t n, int ld, int d, u feat, u thr, u leaf, int ntrees, int depth, float base,
                            u out, u s) {

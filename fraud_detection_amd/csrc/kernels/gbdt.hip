@@ -32,6 +32,7 @@ namespace {
 constexpr int kGBBins = 256;
 constexpr int kGBRowBytes = 32;
 constexpr int kGBMaxFeat = 30;
+constexpr int kGBMaxNodes = 127;  // internal nodes of a depth-7 tree (node ids fit a byte)
 constexpr int kHistEntries = kGBMaxFeat * kGBBins * 2;  // per node: [feature][bin][g, h]
 constexpr int kHistThreads = 1024;
 constexpr int kPartThreads = 256;
@@ -85,21 +86,24 @@ __global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__
 
 // ---- per-round gradients ---------------------------------------------------------------------
 // logistic: g = (p - y) w, h = max(p (1 - p), 1e-16) w, w = scale_pos_weight for positives.
+// fp64 so the quantised values match the numpy oracle except at measure-zero ties.
+__device__ __forceinline__ int2 quantised_grad(float margin, bool pos, float spw, float gscale, float hscale) {
+  const double m = (double)margin;
+  const double p = 1.0 / (1.0 + exp(-m));
+  const double w = pos ? (double)spw : 1.0;
+  const double g = (p - (pos ? 1.0 : 0.0)) * w;
+  const double h = fmax(p * (1.0 - p), 1e-16) * w;
+  return make_int2((int)rint(g * (double)gscale), (int)rint(h * (double)hscale));
+}
+
+// First round of a fit only: later rounds get their gradients from gbdt_margin_kernel<true>.
 __global__ __launch_bounds__(256) void gbdt_grad_kernel(const float* __restrict__ margin,
                                                         const uint8_t* __restrict__ label, int64_t n,
                                                         float spw, float gscale, float hscale,
                                                         int2* __restrict__ gh) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    // fp64 so the quantised values match the numpy oracle except at measure-zero ties
-    const double m = (double)margin[i];
-    const double p = 1.0 / (1.0 + exp(-m));
-    const bool pos = label[i] != 0;
-    const double w = pos ? (double)spw : 1.0;
-    const double g = (p - (pos ? 1.0 : 0.0)) * w;
-    const double h = fmax(p * (1.0 - p), 1e-16) * w;
-    gh[i] = make_int2((int)rint(g * (double)gscale), (int)rint(h * (double)hscale));
-  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    gh[i] = quantised_grad(margin[i], label[i] != 0, spw, gscale, hscale);
 }
 
 // ---- histograms ------------------------------------------------------------------------------
@@ -507,14 +511,40 @@ __global__ void gbdt_leaf_kernel(const long long* __restrict__ ng, const long lo
   }
 }
 
-__global__ __launch_bounds__(256) void gbdt_margin_kernel(const int* __restrict__ ridx,
-                                                          const uint8_t* __restrict__ nid, int64_t n,
+// margin += leaf of the new tree, in row order, plus (GRAD) the next round's quantised gradients
+// from the updated margin.  Each row re-walks the tree through the feature-major bins with the
+// partition's own goes_right, so it reaches the leaf the partition would have put it in, and
+// the last level needs no partition at all (ops/gbdt.py).  The earlier update went through the
+// partition order (margin[ridx[p]] += leaf[nid[p]]: a random 4-B read-modify-write per row) after
+// a last-level partition, and a separate gradient pass re-read every margin: 50-78 + ~65 + 20 us
+// per round at 6.4M rows against 61 us for this walk (profiles/r2_s4b).  The walk is bound by
+// the bins' line traffic -- the rows of a wave read up to 2^l feature columns at level l, ~200 MB
+// over a depth-5 walk -- so walking 4 rows per thread in lockstep measured slower (68-71 us).
+template <bool GRAD>
+__global__ __launch_bounds__(256) void gbdt_margin_kernel(const uint8_t* __restrict__ binsT, int64_t ldt,
+                                                          int64_t n, const int* __restrict__ feat,
+                                                          const int* __restrict__ bin,
                                                           const float* __restrict__ leaf, int depth,
-                                                          float* __restrict__ margin) {
+                                                          float* __restrict__ margin,
+                                                          const uint8_t* __restrict__ label, float spw,
+                                                          float gscale, float hscale, int2* __restrict__ gh) {
+  __shared__ int sf[kGBMaxNodes], sb[kGBMaxNodes];
+  __shared__ float sl[kGBMaxNodes + 1];
+  const int ni = heap_first(depth);
+  for (int i = threadIdx.x; i < ni; i += blockDim.x) {
+    sf[i] = feat[i];
+    sb[i] = bin[i];
+  }
+  for (int i = threadIdx.x; i <= ni; i += blockDim.x) sl[i] = leaf[i];
+  __syncthreads();
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int base = heap_first(depth);
-  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += stride)
-    margin[ridx[p]] += leaf[nid[p] - base];
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
+    int node = 0;
+    for (int l = 0; l < depth; ++l) node = 2 * node + 1 + (int)goes_right(binsT, ldt, r, node, sf, sb);
+    const float m = margin[r] + sl[node - ni];
+    margin[r] = m;
+    if constexpr (GRAD) gh[r] = quantised_grad(m, label[r] != 0, spw, gscale, hscale);
+  }
 }
 
 // ---- inference on fp32 rows ------------------------------------------------------------------
@@ -646,10 +676,17 @@ void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, doubl
   check_launch("gbdt_leaf");
 }
 
-void launch_gbdt_margin(const int* ridx, const uint8_t* nid, int64_t n, const float* leaf, int depth,
-                        float* margin, hipStream_t stream) {
+void launch_gbdt_margin(const uint8_t* binsT, int64_t ldt, int64_t n, const int* feat, const int* bin,
+                        const float* leaf, int depth, float* margin, const uint8_t* label, float spw, float gscale,
+                        float hscale, int2* gh, hipStream_t stream) {
+  if (depth < 1 || depth > 7) throw std::runtime_error("gbdt_margin: depth must be in [1, 7]");
   const int grid = stream_grid(n, 256, 4096);
-  gbdt_margin_kernel<<<grid, 256, 0, stream>>>(ridx, nid, n, leaf, depth, margin);
+  if (gh)
+    gbdt_margin_kernel<true><<<grid, 256, 0, stream>>>(binsT, ldt, n, feat, bin, leaf, depth, margin, label, spw,
+                                                       gscale, hscale, gh);
+  else
+    gbdt_margin_kernel<false><<<grid, 256, 0, stream>>>(binsT, ldt, n, feat, bin, leaf, depth, margin, label,
+                                                        spw, gscale, hscale, gh);
   check_launch("gbdt_margin");
 }
 

@@ -204,8 +204,9 @@ void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_
                             int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream);
 void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,
                       double lambda, double min_child_weight, double eta, float* leaf, hipStream_t stream);
-void launch_gbdt_margin(const int* ridx, const uint8_t* nid, int64_t n, const float* leaf, int depth,
-                        float* margin, hipStream_t stream);
+void launch_gbdt_margin(const uint8_t* binsT, int64_t ldt, int64_t n, const int* feat, const int* bin,
+                        const float* leaf, int depth, float* margin, const uint8_t* label, float spw, float gscale,
+                        float hscale, int2* gh, hipStream_t stream);
 void launch_gbdt_predict(const float* X, int64_t n, int ld, int d, const int* feat, const float* thr,
                          const float* leaf, int ntrees, int depth, float base_margin, float* out,
                          hipStream_t stream);

@@ -275,10 +275,13 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
     ginv, hinv = 1.0 / gscale, 1.0 / hscale
 
-    def round_body(o_feat, o_bin, o_thr, o_gain, o_leaf):
-        """One boosting round: a fixed launch sequence with static pointers (graph-capturable)."""
+    def round_body(o_feat, o_bin, o_thr, o_gain, o_leaf, grad_first=False, grad_next=True):
+        """One boosting round: a fixed launch sequence with static pointers (graph-capturable).
+        The gradients of a round come from the previous round's margin update (gbdt_margin with
+        gh), so only the first round of a fit launches gbdt_grad."""
         st = stream_of(X)  # the capture stream while a hipGraph is being recorded
-        m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
+        if grad_first:
+            m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
         # zero histograms, root segment + global count, ridx = iota, nid = root: one launch
         m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n, n_global,
                           ptr(ws.ridx[0]), ptr(ws.nid[0]), st)
@@ -291,6 +294,8 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
                 comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,
                          ptr(o_feat), ptr(o_bin), ptr(o_thr), ptr(o_gain), ptr(ws.ng), ptr(ws.nh), st)
+            if level == D - 1:
+                break  # leaves: the margin walk and gbdt_leaf (split-kernel child sums) need no partition
             if n:
                 m.gbdt_partition(ptr(binsT), ldt, ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
                                  level, ptr(ws.flag), ptr(ws.boff), PART_BLOCKS, ptr(ws.seg), ptr(ws.segR),
@@ -304,7 +309,8 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
                 comm.all_reduce_(ws.gcnt[c0:c0 + 2 * nn])
         m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(o_leaf), st)
         if n:
-            m.gbdt_margin(ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_leaf), D, ptr(margin), st)
+            m.gbdt_margin(ptr(binsT), ldt, n, ptr(o_feat), ptr(o_bin), ptr(o_leaf), D, ptr(margin), ptr(y), spw,
+                          gscale, hscale, ptr(ws.gh) if grad_next else 0, st)
 
     def after_round(t):
         if checkpoint is not None and ((t + 1) % max(1, checkpoint_every) == 0 or t + 1 == T):
@@ -333,7 +339,7 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             for dst, src in zip((feat[t], binv[t], thr[t], gain[t], leaf[t]), rec):
                 dst.copy_(src)
         else:
-            round_body(feat[t], binv[t], thr[t], gain[t], leaf[t])
+            round_body(feat[t], binv[t], thr[t], gain[t], leaf[t], grad_first=(t == t0), grad_next=(t + 1 < T))
         after_round(t)
     ens = TreeEnsemble(feat=feat.cpu().numpy(), bin=binv.cpu().numpy(), thr=thr.cpu().numpy(),
                        gain=gain.cpu().numpy(), leaf=leaf.cpu().numpy(), **ens_kw)
