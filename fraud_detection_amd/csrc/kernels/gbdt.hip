@@ -110,6 +110,13 @@ __global__ __launch_bounds__(256) void gbdt_grad_kernel(const float* __restrict_
 // Grid: resident blocks (1 per CU: 120 KiB of LDS).  The rows of this level's *built* nodes
 // are concatenated in node order into a virtual range that the grid splits evenly, so the work
 // per block is balanced whatever the segment sizes are.
+//
+// LDS layout: a g plane [feature][bin] then an h plane, not the global [feature][bin][g, h]
+// interleave.  An int64 LDS atomic's bank pair is (u64 index mod 32); interleaved, every g
+// (h) atomic of a wave lands on the 16 even (odd) pairs, so the 64 random bins of a wave
+// collide twice as often.  Split planes give each atomic all 32 pairs.
+constexpr int kHistPlane = kGBMaxFeat * kGBBins;
+__device__ __forceinline__ int lds_hist_slot(int i) { return (i & 1) * kHistPlane + (i >> 1); }
 __global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
     const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
@@ -132,7 +139,7 @@ __global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
     const int64_t lo = max(off, vb), hi = min(off + sc, ve);
     off += sc;
     if (lo >= hi) continue;
-    for (int i = threadIdx.x; i < nent; i += kHistThreads) sh[i] = 0ull;
+    for (int i = threadIdx.x; i < nent; i += kHistThreads) sh[lds_hist_slot(i)] = 0ull;
     __syncthreads();
     for (int64_t v = lo + threadIdx.x; v < hi; v += kHistThreads) {
       const int64_t p = sb + (v - (off - sc));
@@ -147,16 +154,16 @@ __global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
       for (int f = 0; f < kGBMaxFeat; ++f) {
         if (f < d) {
           const int b = (words[f >> 2] >> (8 * (f & 3))) & 0xff;
-          unsigned long long* e = sh + (f * kGBBins + b) * 2;
+          unsigned long long* e = sh + f * kGBBins + b;
           atomicAdd(e, qg);
-          atomicAdd(e + 1, qh);
+          atomicAdd(e + kHistPlane, qh);
         }
       }
     }
     __syncthreads();
     unsigned long long* dst = hist + (int64_t)node * kHistEntries;
     for (int i = threadIdx.x; i < nent; i += kHistThreads) {
-      const unsigned long long x = sh[i];
+      const unsigned long long x = sh[lds_hist_slot(i)];
       if (x) atomicAdd(dst + i, x);
     }
     __syncthreads();
