@@ -63,9 +63,10 @@ COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", "
 # Per-file code generation options.  knn.hip: MFMA accumulators in arch VGPRs (gfx950's unified
 # register file) -- its 16-float score tile is consumed by VALU right after every MFMA chain, and
 # the AGPR form costs 32 v_accvgpr moves per 32x32 tile.
-# kernelshap.hip: same reasoning -- every MFMA tile feeds the sigmoid epilogue directly.
+# kernelshap.hip: same reasoning -- every MFMA tile feeds the sigmoid epilogue directly; and no SLP
+# packing of its scalar f32 epilogue into v_pk_*_f32 (no faster than two plain ops, dearer beside MFMAs).
 PER_FILE_FLAGS = {"knn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"],
-                  "kernelshap.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+                  "kernelshap.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1", "-fno-slp-vectorize"]}
 
 
 def _compile(src: str, obj: str, headers: list[str], force: bool, extra: list[str]) -> str:

@@ -198,6 +198,13 @@ PYBIND11_MODULE(_fdx_native, m) {
                            P<float>(phi), P<float>(fx), P<float>(f0), P<float>(ws), P<unsigned>(cnt), S(s),
                            P<unsigned long long>(stamps));
   });
+  m.def("kernelshap_paired", [](u X, int E, int d, u a, float bias, u bg, u cb, int nbg, u Z, int Ppad, int parts,
+                                u A, u Az, int link, u phi, u fx, u f0, u ws, u cnt, u s) {
+    fdx::launch_kernelshap_paired(P<const float>(X), E, d, P<const float>(a), bias, P<const float>(bg),
+                                  P<const float>(cb), nbg, P<const uint16_t>(Z), Ppad, parts, P<const float>(A),
+                                  P<const float>(Az), link, P<float>(phi), P<float>(fx), P<float>(f0), P<float>(ws),
+                                  P<unsigned>(cnt), S(s));
+  });
   m.def("kernelshap_linear_resident", [](int S_pad, int parts) { return fdx::kernelshap_linear_resident(S_pad, parts); });
   m.def("treeshap", [](u Xs, int ldx, int E, int d, u feat, u thr, u leaf, int T, int depth, float base, u bw,
                        int bw_ld, int n_bg, float f0, u phi, u fx, u f0o, u s) {

@@ -94,30 +94,39 @@ __device__ __forceinline__ void form_y(float* ys, int s0, int ns, int S, int lin
   }
 }
 
+// One thread's share (lanes part, part + 8, ...) of sum_{s < ns} Ai[s] y_s: float4 steps, 4
+// independent accumulators.  ns % 32 == 0, Ai and ys 16-B aligned.
+__device__ __forceinline__ float seg_dot(const float* __restrict__ Ai_, const float* ys, int ns, int part) {
+  const float4* Ai = reinterpret_cast<const float4*>(Ai_);
+  const float4* fv = reinterpret_cast<const float4*>(ys);
+  float a4[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nq = ns >> 2;  // ns % 32 == 0 -> nq % 8 == 0
+  int q = part;
+  for (; q + 24 < nq; q += 32) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float4 av = Ai[q + 8 * u], yv = fv[q + 8 * u];
+      a4[u] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[u]))));
+    }
+  }
+  for (; q < nq; q += 8) {
+    const float4 av = Ai[q], yv = fv[q];
+    a4[0] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[0]))));
+  }
+  return (a4[0] + a4[1]) + (a4[2] + a4[3]);
+}
+
 // Partial projection acc_i = sum_{s < ns} A[i][s0 + s] y_s for i < d-1 into ph[i]: 8 threads per
-// output, float4 steps of the (S_pad-strided, zero-padded) A row, 4 independent accumulators.
+// output over the (S_pad-strided, zero-padded) A row.  off2 >= 0: a second segment of ns
+// coalitions at A column off2 + s0 with values ys[ns..2 ns) (the complement half of a paired design).
 __device__ __forceinline__ void project_part(const float* ys, int s0, int ns, const float* __restrict__ Amat,
-                                             int S_pad, int d, float* ph) {
+                                             int S_pad, int d, float* ph, int off2 = -1) {
   const int i = threadIdx.x >> 3, part = threadIdx.x & 7;
   float acc = 0.0f;
   if (i < d - 1) {
-    const float4* Ai = reinterpret_cast<const float4*>(Amat + (int64_t)i * S_pad + s0);
-    const float4* fv = reinterpret_cast<const float4*>(ys);
-    float a4[4] = {0.f, 0.f, 0.f, 0.f};
-    const int nq = ns >> 2;  // ns % 32 == 0 -> nq % 8 == 0
-    int q = part;
-    for (; q + 24 < nq; q += 32) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const float4 av = Ai[q + 8 * u], yv = fv[q + 8 * u];
-        a4[u] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[u]))));
-      }
-    }
-    for (; q < nq; q += 8) {
-      const float4 av = Ai[q], yv = fv[q];
-      a4[0] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[0]))));
-    }
-    acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    const float* Ai = Amat + (int64_t)i * S_pad;
+    acc = seg_dot(Ai + s0, ys, ns, part);
+    if (off2 >= 0) acc += seg_dot(Ai + off2 + s0, ys + ns, ns, part);
   }
   acc = group_sum<8>(acc);
   if (part == 0 && i < d - 1) ph[i] = acc;
@@ -331,6 +340,212 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 }
 
 // ------------------------------------------------------------------------------------------------
+// Linear model, complement-paired design
+// ------------------------------------------------------------------------------------------------
+// shap's sampler draws coalitions in complement pairs (z, 1 - z), and for the linear model
+//   L_b(1 - z) = T_b - L_b(z),   T_b = logit(x) + c_b,
+// so one MFMA tile yields the logits of 32 coalitions AND of their 32 complements.  The host
+// (ops/kernelshap.py) stores Ppad base coalitions; slot Ppad + p is the complement of base p (a
+// base whose complement is not in the design gets a zero A column there).  With
+// E = exp2(-log2(e) L_b(z)) and K_b = e^{-T_b}:
+//   sigma(L_b(z)) = 1 / (1 + E),   sigma(L_b(1 - z)) = E / (E + K_b),
+// and background rows pair up under one reciprocal for both: e0/g0 + e1/g1 = (e0 g1 + e1 g0) /
+// (g0 g1).  Per 4 evaluations: 2 v_exp + 2 v_rcp (the unpaired kernel: 4 + 2) and half the MFMA
+// work.  Null background rows (past n_bg) have u = 0 and K = 1, i.e. both sigmas are exactly 1/2;
+// that constant is subtracted once per coalition instead of pushing them to 0 (which needs exp2
+// ranges that overflow the paired products).  Non-finite tiles (|logits| > ~40 in a pair) are
+// re-summed per element from tau_b = log2(K_b).
+template <int NTB, int NGL, bool LOGITS>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void kernelshap_paired_kernel(
+    const float* __restrict__ X, int d, const float* __restrict__ a, float bias,
+    const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
+    const uint16_t* __restrict__ Z, int Ppad, int P, const float* __restrict__ Amat,
+    const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
+    float* __restrict__ f0_out, float* __restrict__ ws, unsigned* __restrict__ cnt) {
+  extern __shared__ __attribute__((aligned(16))) float ys[];  // [2][ns]: base, then complements
+  __shared__ uint4 Uhi[4 * 2 * 2 * 32], Ulo[4 * 2 * 2 * 32];  // [tile][kstep][half][row]
+  // K_b and tau_b = log2 K_b in MFMA row order: within 4 rows, (0, 2) then (1, 3) -- the two
+  // packed pairs the epilogue consumes are one 16-B LDS read
+  __shared__ float4 Kq[kMaxBg / 4], Tq[kMaxBg / 4];
+  __shared__ f32x2_t rem[kWaves - 1][kWaves][32];  // remainder tiles: per-wave partial sums
+  __shared__ float xs[32];
+  __shared__ float red[8];
+  __shared__ float ph[32];
+  __shared__ int flag;
+  const int e = blockIdx.x / P, p = blockIdx.x - e * P;
+  const int lane = lane_id(), wv = wave_id();
+  const int r = lane & 31, h = lane >> 5;
+  const int nst = Ppad >> 5;
+  const int st0 = (p * nst) / P, st1 = ((p + 1) * nst) / P;
+  const int ns = 32 * (st1 - st0);
+  constexpr float kNegLog2e = -1.4426950408889634f;
+  if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? a[threadIdx.x] * X[(int64_t)e * d + threadIdx.x] : 0.0f;
+  __syncthreads();
+  const float lx = wave_sum(lane < 32 ? xs[lane] : 0.0f) + bias;  // logit(x), in every wave
+  const float us = LOGITS ? 1.0f : kNegLog2e;
+  for (int q = threadIdx.x; q < 512; q += kThreads) {
+    const int rr = q & 31, hh = (q >> 5) & 1, ks = (q >> 6) & 1, t = q >> 7;
+    const int b = 32 * t + rr, k0 = 16 * ks + 8 * hh;
+    float4 w0 = make_float4(0.f, 0.f, 0.f, 0.f), w1 = w0;
+    const bool okb = b < n_bg;
+    if (okb) {
+      const float4* wr = reinterpret_cast<const float4*>(Bg + (int64_t)b * kCols + k0);
+      w0 = wr[0];
+      w1 = wr[1];
+    }
+    const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+    uint32_t hw[4], lw[4];
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      const float u0 = okb ? (xs[k0 + j] - wv8[j]) * us : 0.0f;
+      const float u1 = okb ? (xs[k0 + j + 1] - wv8[j + 1]) * us : 0.0f;
+      const uint16_t h0 = f32_to_bf16(u0), h1 = f32_to_bf16(u1);
+      hw[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+      lw[j >> 1] = pack_bf16x2(u0 - __uint_as_float(((uint32_t)h0) << 16), u1 - __uint_as_float(((uint32_t)h1) << 16));
+    }
+    Uhi[q] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    Ulo[q] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  }
+  if (threadIdx.x < kMaxBg) {
+    const int b = threadIdx.x;
+    const float tau = (!LOGITS && b < n_bg) ? kNegLog2e * (lx + cb[b]) : 0.0f;
+    const int q = (b & ~3) | ((b & 1) << 1) | ((b >> 1) & 1);
+    reinterpret_cast<float*>(Tq)[q] = tau;
+    reinterpret_cast<float*>(Kq)[q] = __builtin_amdgcn_exp2f(tau);
+  }
+  __syncthreads();
+  const float inv_nb = 1.0f / (float)n_bg;
+  // null rows evaluated per coalition: each adds exactly 1/2 to both sigma sums
+  const float null_half = 0.5f * (float)(32 * (NTB - 1) + 8 * NGL - n_bg);
+  float sumT = 0.0f;  // LOGITS: sum_b T_b (complement logit sum = sumT - base logit sum)
+  if constexpr (LOGITS) {
+    for (int b = lane; b < n_bg; b += kWave) sumT += lx + cb[b];
+    sumT = wave_sum(sumT);
+  }
+  // (coalition tile, background tile) -> 32 x 32 logits; zb0/zb1 = the tile's Z fragments
+  auto mfma_tile = [&](const bf16x8_t& zb0, const bf16x8_t& zb1, int t, int oz) {
+    const int q0 = (t * 2 + 0) * 64 + h * 32 + r + oz, q1 = (t * 2 + 1) * 64 + h * 32 + r + oz;
+    const bf16x8_t uh0 = __builtin_bit_cast(bf16x8_t, Uhi[q0]), ul0 = __builtin_bit_cast(bf16x8_t, Ulo[q0]);
+    const bf16x8_t uh1 = __builtin_bit_cast(bf16x8_t, Uhi[q1]), ul1 = __builtin_bit_cast(bf16x8_t, Ulo[q1]);
+    f32x16_t acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh0, zb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul0, zb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh1, zb1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul1, zb1, acc, 0, 0, 0);
+    return acc;
+  };
+  // -> (sum of sigma over the lane's rows for z, the same for 1 - z); rows of group j of tile t
+  // are 32 t + 8 j + 4 h + {0..3}
+  auto epilogue = [&](const f32x16_t& acc, int t, auto ngc) {
+    constexpr int ng = decltype(ngc)::value;
+    if constexpr (LOGITS) {
+      float ts = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4 * ng; ++i) ts += acc[i];
+      return f32x2_t{ts, 0.0f};
+    } else {
+      // scalar f32 on purpose (and -fno-slp-vectorize for this file): v_pk_*_f32 issue no faster
+      // than two plain ops here and cost more beside the MFMAs (MI355X_MICROARCH constants table)
+      float tb0 = 0.0f, tb1 = 0.0f, tc0 = 0.0f, tc1 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4 * ng; i += 4) {
+        const float4 kk = Kq[8 * t + 2 * (i >> 2) + h];  // rows +0, +2, +1, +3
+        const float e0 = __builtin_amdgcn_exp2f(acc[i]), e1 = __builtin_amdgcn_exp2f(acc[i + 1]);
+        const float e2 = __builtin_amdgcn_exp2f(acc[i + 2]), e3 = __builtin_amdgcn_exp2f(acc[i + 3]);
+        const float d0 = e0 + 1.0f, d1 = e1 + 1.0f, d2 = e2 + 1.0f, d3 = e3 + 1.0f;
+        tb0 = fmaf(d0 + d1, fast_rcp(d0 * d1), tb0);
+        tb1 = fmaf(d2 + d3, fast_rcp(d2 * d3), tb1);
+        const float g0 = e0 + kk.x, g1 = e1 + kk.z, g2 = e2 + kk.y, g3 = e3 + kk.w;
+        tc0 = fmaf(fmaf(e0, g1, e1 * g0), fast_rcp(g0 * g1), tc0);
+        tc1 = fmaf(fmaf(e2, g3, e3 * g2), fast_rcp(g2 * g3), tc1);
+      }
+      f32x2_t tb = {tb0, tb1}, tcm = {tc0, tc1};
+      f32x2_t out = {tb.x + tb.y, tcm.x + tcm.y};
+      // overflow (NaN) or an underflowed pair product (rcp -> inf) somewhere in this lane's tile
+      if (!__builtin_isfinite(out.x + out.y)) {
+        out = f32x2_t{0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 4 * ng; i += 4) {
+          const float4 tt = Tq[8 * t + 2 * (i >> 2) + h];
+          const float tv[4] = {tt.x, tt.z, tt.y, tt.w};  // rows +0, +1, +2, +3
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            out.x += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i + k]));
+            out.y += fast_rcp(1.0f + __builtin_amdgcn_exp2f(tv[k] - acc[i + k]));
+          }
+        }
+      }
+      return out;
+    }
+  };
+  auto store_y = [&](int st, float sb, float sc) {  // per-coalition totals over all background rows
+    const float fb = LOGITS ? sb : sb - null_half;
+    const float fc = LOGITS ? sumT - sb : sc - null_half;
+    ys[32 * (st - st0) + r] = fb * inv_nb;
+    ys[ns + 32 * (st - st0) + r] = fc * inv_nb;
+  };
+  // Whole coalition tiles round-robin over the waves; the remainder (< 4 tiles) is split by
+  // background tile so that no SIMD carries an extra tile (wave w of every workgroup sits on SIMD
+  // w: 33 tiles as 9 + 8 + 8 + 8 made SIMD 0 the critical path), partials summed in a fixed order.
+  const int nfull = (st1 - st0) / kWaves * kWaves;
+  for (int st = st0 + wv; st < st0 + nfull; st += kWaves) {
+    const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
+    const bf16x8_t zb0 = __builtin_bit_cast(bf16x8_t, zr[h]), zb1 = __builtin_bit_cast(bf16x8_t, zr[2 + h]);
+    // an opaque zero per iteration keeps the U fragment reads inside the loop: hoisted, the 64
+    // VGPRs of U plus the two-sum epilogue spill (the LDS re-read is 4 KB per tile per wave)
+    int oz;
+    asm volatile("s_mov_b32 %0, 0" : "=s"(oz));
+    f32x2_t fs = {0.0f, 0.0f};
+    f32x16_t cur = mfma_tile(zb0, zb1, 0, oz);
+#pragma unroll
+    for (int t = 0; t < NTB - 1; ++t) {
+      const f32x16_t nxt = mfma_tile(zb0, zb1, t + 1, oz);
+      fs += epilogue(cur, t, std::integral_constant<int, 4>{});
+      cur = nxt;
+    }
+    fs += epilogue(cur, NTB - 1, std::integral_constant<int, NGL>{});
+    fs.x += __shfl_xor(fs.x, 32, kWave);
+    fs.y += __shfl_xor(fs.y, 32, kWave);
+    if (h == 0) store_y(st, fs.x, fs.y);
+  }
+  if (nfull < st1 - st0) {
+    for (int st = st0 + nfull; st < st1; ++st) {
+      f32x2_t fs = {0.0f, 0.0f};
+      if (wv < NTB) {  // wave-uniform
+        const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
+        const bf16x8_t zb0 = __builtin_bit_cast(bf16x8_t, zr[h]), zb1 = __builtin_bit_cast(bf16x8_t, zr[2 + h]);
+        const f32x16_t acc = mfma_tile(zb0, zb1, wv, 0);
+        fs = wv == NTB - 1 ? epilogue(acc, wv, std::integral_constant<int, NGL>{})
+                           : epilogue(acc, wv, std::integral_constant<int, 4>{});
+        fs.x += __shfl_xor(fs.x, 32, kWave);
+        fs.y += __shfl_xor(fs.y, 32, kWave);
+      }
+      if (h == 0) rem[st - st0 - nfull][wv][r] = fs;
+    }
+    __syncthreads();
+    if (wv == 0 && h == 0) {
+      for (int st = st0 + nfull; st < st1; ++st) {
+        f32x2_t tot = rem[st - st0 - nfull][0][r];
+        for (int w = 1; w < NTB; ++w) tot += rem[st - st0 - nfull][w][r];  // fixed order
+        store_y(st, tot.x, tot.y);
+      }
+    }
+  }
+  // f0 (background mean output) and f(x)
+  float z0s = 0.0f;
+  for (int b = threadIdx.x; b < n_bg; b += kThreads) z0s += LOGITS ? cb[b] : fast_sigmoid(cb[b]);
+  z0s = wave_sum(z0s);
+  if (lane == 0) red[wv] = z0s;
+  __syncthreads();
+  float f0l, fxl;
+  link_pair(link, (red[0] + red[1] + red[2] + red[3]) * inv_nb, lx, f0l, fxl);
+  form_y(ys, 0, 2 * ns, 2 * ns, link, f0l);  // padded slots have zero A columns: no masking
+  __syncthreads();
+  project_part(ys, 32 * st0, ns, Amat, 2 * Ppad, d, ph, Ppad);
+  finish(e, p, P, d, ph, Az, fxl - f0l, fxl, f0l, phi, fx_out, f0_out, ws, cnt, &flag);
+}
+
+// ------------------------------------------------------------------------------------------------
 // Tree ensemble (depth D <= 5: the 31 internal nodes of a tree fit one 32-bit mask)
 // ------------------------------------------------------------------------------------------------
 // Walk one tree from the effective direction bits R1 (bit n + 1 = node n goes right; heap 1-based)
@@ -500,6 +715,48 @@ void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float 
 #undef FDX_KS_NG
 #undef FDX_KS
   check_launch("kernelshap");
+}
+
+void launch_kernelshap_paired(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
+                              const float* cb, int n_bg, const uint16_t* Z, int Ppad, int parts, const float* Amat,
+                              const float* Az, int link, float* phi, float* fx_out, float* f0_out, float* ws,
+                              unsigned* cnt, hipStream_t stream) {
+  check_design(d, 2 * Ppad, 2 * Ppad, 1);
+  if (parts < 1 || parts > kMaxParts || parts > Ppad / 32)
+    throw std::runtime_error("kernelshap_paired: 1 <= parts <= 8 and <= Ppad/32");
+  if (n_bg < 1 || n_bg > kMaxBg) throw std::runtime_error("kernelshap: 1 <= n_bg <= 128");
+  if (parts > 1 && (ws == nullptr || cnt == nullptr)) throw std::runtime_error("kernelshap: parts > 1 needs ws/cnt");
+  if (n_expl <= 0) return;
+  const dim3 grid((unsigned)((int64_t)n_expl * parts));
+  const size_t lds = 2 * part_lds(Ppad, parts);
+#define FDX_KP(NT, NG, LG)                                                                          \
+  kernelshap_paired_kernel<NT, NG, LG><<<grid, kThreads, lds, stream>>>(                             \
+      X, d, a, bias, bg, cb, n_bg, Z, Ppad, parts, Amat, Az, link, phi, fx_out, f0_out, ws, cnt)
+#define FDX_KP_NG(NT, LG)                       \
+  do {                                          \
+    switch (ngl) {                              \
+      case 1: FDX_KP(NT, 1, LG); break;         \
+      case 2: FDX_KP(NT, 2, LG); break;         \
+      case 3: FDX_KP(NT, 3, LG); break;         \
+      default: FDX_KP(NT, 4, LG); break;        \
+    }                                           \
+  } while (0)
+#define FDX_KP_NT(LG)                           \
+  do {                                          \
+    switch (ntb) {                              \
+      case 1: FDX_KP_NG(1, LG); break;          \
+      case 2: FDX_KP_NG(2, LG); break;          \
+      case 3: FDX_KP_NG(3, LG); break;          \
+      default: FDX_KP_NG(4, LG); break;         \
+    }                                           \
+  } while (0)
+  const int ntb = (n_bg + 31) >> 5;
+  const int ngl = (n_bg - 32 * (ntb - 1) + 7) >> 3;
+  if (link == 2) FDX_KP_NT(true); else FDX_KP_NT(false);
+#undef FDX_KP_NT
+#undef FDX_KP_NG
+#undef FDX_KP
+  check_launch("kernelshap_paired");
 }
 
 void launch_kernelshap_tree(const float* Xs, int ldx, int n_expl, int d, const int* feat, const float* thr,

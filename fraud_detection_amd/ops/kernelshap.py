@@ -10,6 +10,8 @@ part counts differ only in the fp32 summation order of the projection).
 """
 from __future__ import annotations
 
+import os
+
 import numpy as np
 import torch
 
@@ -55,20 +57,66 @@ def _check_x(X, d):
         raise ValueError(f"X must be contiguous float32 [E, {d}]")
 
 
+def complement_pairs(Z: np.ndarray):
+    """Split a coalition design into (base [P], comp [P]) row indices with Z[comp[p]] = 1 - Z[base[p]]
+    (comp = -1 where the complement is not in the design).  shap's sampler draws coalitions in
+    complement pairs, so P is ~S/2 (2042 rows at M = 30 -> 1032 pairs)."""
+    keys = {z.tobytes(): i for i, z in enumerate(Z)}
+    used = np.zeros(len(Z), bool)
+    base, comp = [], []
+    for i, z in enumerate(Z):
+        if used[i]:
+            continue
+        used[i] = True
+        j = keys.get((1 - z).tobytes(), -1)
+        if j >= 0 and not used[j]:
+            used[j] = True
+        else:
+            j = -1
+        base.append(i)
+        comp.append(j)
+    return np.asarray(base, np.int64), np.asarray(comp, np.int64)
+
+
+def _paired_enabled() -> bool:
+    return os.environ.get("FDX_KS_PAIRED", "1") != "0"
+
+
 def _device_design(expl, dev):
     """Upload the linear explainer's design once: Z as bf16 [S_pad, 32] (col 31 = 1 folds the
     background intercepts into the GEMM), A [d-1, S_pad] (zero-padded), A z_M, the weighted
-    background rows W and the background logits."""
-    key = (str(dev),)
+    background rows W and the background logits.
+
+    Paired layout (default, kernelshap_paired_kernel): Z holds the Ppad base coalitions of the
+    complement pairs and A [d-1, 2 Ppad] has the base columns first, then each base's complement
+    (zero columns for padding and for complements the design does not contain: they carry no
+    weight, so the WLS solution is unchanged)."""
+    key = (str(dev), _paired_enabled())
     if expl._dev_cache is not None and expl._dev_cache[0] == key:
         return expl._dev_cache[1]
     d = expl.d
     S = expl.Z.shape[0]
-    S_pad = (S + 31) // 32 * 32
-    if S_pad > 4096:
-        raise ValueError("at most 4096 coalitions per design on device")
-    Zp = np.zeros((S_pad, 32), np.float32)
-    Zp[:S, :d] = expl.Z
+    paired = key[1]
+    if paired:
+        base, comp = complement_pairs(expl.Z)
+        Ppad = (len(base) + 31) // 32 * 32
+        if 2 * Ppad > 4096:
+            raise ValueError("at most 2048 coalition pairs per design on device")
+        Zp = np.zeros((Ppad, 32), np.float32)
+        Zp[: len(base), :d] = expl.Z[base]
+        Ap = np.zeros((d - 1, 2 * Ppad), np.float32)
+        Ap[:, : len(base)] = expl.A[:, base]
+        has = comp >= 0
+        Ap[:, Ppad + np.nonzero(has)[0]] = expl.A[:, comp[has]]
+        S_pad = 2 * Ppad
+    else:
+        S_pad = (S + 31) // 32 * 32
+        if S_pad > 4096:
+            raise ValueError("at most 4096 coalitions per design on device")
+        Zp = np.zeros((S_pad, 32), np.float32)
+        Zp[:S, :d] = expl.Z
+        Ap = np.zeros((d - 1, S_pad), np.float32)
+        Ap[:, :S] = expl.A
     Zp[:, 31] = 1.0
     a32 = np.zeros(32, np.float32)
     a32[:d] = expl.a[:d]
@@ -77,8 +125,6 @@ def _device_design(expl, dev):
     W = np.zeros((expl.B.shape[0], 32), np.float32)
     W[:, :d] = (expl.B.astype(np.float32) * a32[:d][None, :]).astype(np.float32)
     W[:, 31] = -cb
-    Ap = np.zeros((d - 1, S_pad), np.float32)
-    Ap[:, :S] = expl.A
     t = {
         "Z": torch.from_numpy(Zp).to(dev).to(torch.bfloat16).contiguous(),
         "A": torch.from_numpy(Ap).to(dev).contiguous(),
@@ -86,7 +132,7 @@ def _device_design(expl, dev):
         "a": torch.from_numpy(a32).to(dev),
         "bg": torch.from_numpy(W).to(dev),
         "cb": torch.from_numpy(cb).to(dev),
-        "S": S, "S_pad": S_pad, "ws": _Workspace(),
+        "S": S, "S_pad": S_pad, "paired": paired, "ws": _Workspace(),
     }
     expl._dev_cache = (key, t)
     return t
@@ -113,8 +159,11 @@ def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | 
     dev = X.device
     t = _device_design(expl, dev)
     E = X.shape[0]
-    n_tiles = t["S_pad"] // 32
+    # MFMA tiles of 32 coalitions (paired: 32 base coalitions, i.e. 64 with the complements)
+    n_tiles = t["S_pad"] // (64 if t["paired"] else 32)
     if stamps is not None:
+        if t["paired"]:
+            raise ValueError("phase stamps exist only in the unpaired kernel (FDX_KS_PAIRED=0)")
         parts = 1
     elif parts is None:
         # measured (profiles/r2_e): the split's hand-off costs more than the idle CUs it fills
@@ -123,9 +172,14 @@ def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | 
     parts = max(1, min(int(parts), MAX_PARTS, n_tiles))
     phi, fx, f0 = _outputs(E, expl.d, dev, out)
     ws, cnt = t["ws"].get(E, dev) if parts > 1 else (None, None)
-    m.kernelshap(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]), expl.B.shape[0],
-                 ptr(t["Z"]), t["S"], t["S_pad"], parts, ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi),
-                 ptr(fx), ptr(f0), ptr(ws), ptr(cnt), stream_of(X), ptr(stamps))
+    if t["paired"]:
+        m.kernelshap_paired(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]),
+                            expl.B.shape[0], ptr(t["Z"]), t["S_pad"] // 2, parts, ptr(t["A"]), ptr(t["Az"]),
+                            _LINKS[expl.link], ptr(phi), ptr(fx), ptr(f0), ptr(ws), ptr(cnt), stream_of(X))
+    else:
+        m.kernelshap(ptr(X), E, expl.d, ptr(t["a"]), float(expl.bias), ptr(t["bg"]), ptr(t["cb"]), expl.B.shape[0],
+                     ptr(t["Z"]), t["S"], t["S_pad"], parts, ptr(t["A"]), ptr(t["Az"]), _LINKS[expl.link], ptr(phi),
+                     ptr(fx), ptr(f0), ptr(ws), ptr(cnt), stream_of(X), ptr(stamps))
     if not sync:
         return phi, fx, f0
     return phi.cpu().numpy().astype(np.float64), fx.cpu().numpy().astype(np.float64), float(f0[0].item()) if E else 0.0

@@ -150,3 +150,96 @@ def test_tree_kernel_matches_oracle(dev, depth, trees, nbg):
     assert abs(f0 - ref[2]) < 1e-6
     np.testing.assert_allclose(phi, ref[0], atol=2e-5)
     np.testing.assert_allclose(phi.sum(1), fx - f0, atol=1e-5)
+
+
+# ---------------------------------------------------------------------------------------------
+def _paired_emulation(X, ke, link):
+    """numpy emulation of kernelshap_paired_kernel's arithmetic: base logits from one GEMM,
+    complement logits T_b - L_b(z), sigma(1 - z) = E / (E + K_b), null background rows padded to
+    a multiple of 8 and removed again as the exact 1/2 per row, paired A layout."""
+    from fraud_detection_amd.ops.kernelshap import complement_pairs
+
+    d = ke.d
+    base, comp = complement_pairs(ke.Z)
+    Ppad = (len(base) + 31) // 32 * 32
+    Zb = np.zeros((Ppad, d))
+    Zb[: len(base)] = ke.Z[base]
+    Ap = np.zeros((d - 1, 2 * Ppad))
+    Ap[:, : len(base)] = ke.A[:, base]
+    has = comp >= 0
+    Ap[:, Ppad + np.nonzero(has)[0]] = ke.A[:, comp[has]]
+    a = ke.a[:d]
+    B = ke.B.astype(np.float64)
+    nb = B.shape[0]
+    nb_pad = (nb + 7) // 8 * 8
+    c = np.zeros(nb_pad)
+    c[:nb] = B @ a + ke.bias
+    phis = []
+    for x in np.asarray(X, np.float64):
+        lx = x @ a + ke.bias
+        U = np.zeros((nb_pad, d))
+        U[:nb] = a * (x - B)
+        L = Zb @ U.T + np.where(np.arange(nb_pad) < nb, c, 0.0)[None, :]        # [Ppad, nb_pad]
+        T = np.where(np.arange(nb_pad) < nb, lx + c, 0.0)
+        if link == "logit_model":
+            fb = L[:, :nb].sum(1)
+            fc = T[:nb].sum() - fb
+            f0, fx = c[:nb].mean(), lx
+        else:
+            E = np.exp(-L)
+            K = np.exp(-T)
+            nulls = 0.5 * (nb_pad - nb)
+            fb = (1.0 / (1.0 + E)).sum(1) - nulls
+            fc = (E / (E + K[None, :])).sum(1) - nulls
+            f0, fx = (1.0 / (1.0 + np.exp(-c[:nb]))).mean(), 1.0 / (1.0 + np.exp(-lx))
+        y = np.r_[fb, fc] / nb - f0
+        delta = fx - f0
+        ph = np.empty(d)
+        ph[:-1] = Ap @ y - (ke.A @ ke.zM) * delta
+        ph[-1] = delta - ph[:-1].sum()
+        phis.append(ph)
+    return np.asarray(phis)
+
+
+def test_complement_pairs_cover_design():
+    from fraud_detection_amd.ops.kernelshap import complement_pairs
+
+    Z, _, _, _ = EX.cached_design(30)
+    base, comp = complement_pairs(Z)
+    idx = np.r_[base, comp[comp >= 0]]
+    assert np.array_equal(np.sort(idx), np.arange(len(Z)))             # every row exactly once
+    assert np.array_equal(Z[comp[comp >= 0]], 1 - Z[base[comp >= 0]])
+    assert len(base) <= len(Z) // 2 + 32                                # shap samples in pairs
+
+
+@pytest.mark.parametrize("link", ["identity", "logit_model"])
+def test_paired_arithmetic_matches_oracle(link):
+    a, bias = _linear_model()
+    X, _ = separable(6, seed=5)
+    B, _ = separable(37, seed=6)                                        # 37 rows: 3 null rows padded
+    ke = EX.KernelExplainer(a, bias, B.numpy(), link=link, device="cpu")
+    ref = EX.kernelshap_reference(X.numpy(), ke.a, ke.bias, ke.B, ke.Z, ke.A, ke.zM, link)
+    np.testing.assert_allclose(_paired_emulation(X.numpy(), ke, link), ref[0], atol=1e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("link", ["identity", "logit", "logit_model"])
+def test_paired_kernel_matches_unpaired(dev, link, monkeypatch):
+    """The complement-paired kernel (default) and the one-coalition-per-column kernel explain
+    the same design: equal to fp32 rounding, both within the oracle tolerance."""
+    a, bias = _linear_model()
+    X, _ = separable(200, seed=11)
+    B, _ = separable(100, seed=12)
+    ke = EX.KernelExplainer(a, bias, B.numpy(), link=link, device=str(dev))
+    from fraud_detection_amd.ops.kernelshap import kernelshap
+
+    Xd = X.to(dev)
+    monkeypatch.setenv("FDX_KS_PAIRED", "1")
+    pp = kernelshap(Xd, ke)
+    monkeypatch.setenv("FDX_KS_PAIRED", "0")
+    pu = kernelshap(Xd, ke)
+    ref = EX.kernelshap_reference(X.numpy(), ke.a, ke.bias, ke.B, ke.Z, ke.A, ke.zM, link)
+    tol = 2e-4 if link == "logit" else 2e-5
+    np.testing.assert_allclose(pp[0], ref[0], atol=tol)
+    np.testing.assert_allclose(pp[0], pu[0], atol=tol)
+    np.testing.assert_allclose(pp[1], pu[1], rtol=1e-6, atol=1e-7)
