@@ -201,7 +201,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("kernelshap_paired", [](u X, int E, int d, u a, float bias, u bg, u cb, int nbg, u Z, int Ppad, int parts,
                                 u A, u Az, int link, u phi, u fx, u f0, u ws, u cnt, u s) {
     fdx::launch_kernelshap_paired(P<const float>(X), E, d, P<const float>(a), bias, P<const float>(bg),
-                                  P<const float>(cb), nbg, P<const uint16_t>(Z), Ppad, parts, P<const float>(A),
+                                  P<const float>(cb), nbg, P<const uint32_t>(Z), Ppad, parts, P<const float>(A),
                                   P<const float>(Az), link, P<float>(phi), P<float>(fx), P<float>(f0), P<float>(ws),
                                   P<unsigned>(cnt), S(s));
   });

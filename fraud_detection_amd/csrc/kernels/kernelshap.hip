@@ -102,11 +102,16 @@ __device__ __forceinline__ float seg_dot(const float* __restrict__ Ai_, const fl
   float a4[4] = {0.f, 0.f, 0.f, 0.f};
   const int nq = ns >> 2;  // ns % 32 == 0 -> nq % 8 == 0
   int q = part;
-  for (; q + 24 < nq; q += 32) {
+  // 8 A loads in flight per round: the phase is L2-latency bound (every workgroup of the single
+  // dispatch round reaches it at about the same time, so nothing else hides the latency)
+  for (; q + 56 < nq; q += 64) {
+    float4 av[8];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const float4 av = Ai[q + 8 * u], yv = fv[q + 8 * u];
-      a4[u] = fmaf(av.x, yv.x, fmaf(av.y, yv.y, fmaf(av.z, yv.z, fmaf(av.w, yv.w, a4[u]))));
+    for (int u = 0; u < 8; ++u) av[u] = Ai[q + 8 * u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const float4 yv = fv[q + 8 * u];
+      a4[u & 3] = fmaf(av[u].x, yv.x, fmaf(av[u].y, yv.y, fmaf(av[u].z, yv.z, fmaf(av[u].w, yv.w, a4[u & 3]))));
     }
   }
   for (; q < nq; q += 8) {
@@ -276,6 +281,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         // 4 background rows per step in packed f32: rows (i, i+2) and (i+1, i+3) pair up so
         // that the sums d0 + d1 and products d0 d1 of both pairs are one v_pk_add / v_pk_mul
         f32x2_t ts2 = {0.0f, 0.0f};
+        float mx = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4 * ng; i += 4) {
           const f32x2_t e02 = {__builtin_amdgcn_exp2f(acc[i]), __builtin_amdgcn_exp2f(acc[i + 2])};
@@ -284,9 +290,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
           const f32x2_t pr = d02 * d13;
           const f32x2_t rc = {fast_rcp(pr.x), fast_rcp(pr.y)};
           ts2 = __builtin_elementwise_fma(d02 + d13, rc, ts2);
+          mx = fmaxf(fmaxf(mx, pr.x), pr.y);
         }
         float ts = ts2.x + ts2.y;
-        if (__builtin_isnan(ts)) {  // exp2 overflow (logit < -88) in this lane: per-element form
+        // an overflowed pair product (a logit below ~-44 zeroes its partner's sigma too) or
+        // exp2 overflow (logit < -88): per-element form
+        if (!(mx < __builtin_inff()) || __builtin_isnan(ts)) {
           ts = 0.0f;
 #pragma unroll
           for (int i = 0; i < 16; ++i)
@@ -347,27 +356,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // so one MFMA tile yields the logits of 32 coalitions AND of their 32 complements.  The host
 // (ops/kernelshap.py) stores Ppad base coalitions; slot Ppad + p is the complement of base p (a
 // base whose complement is not in the design gets a zero A column there).  With
-// E = exp2(-log2(e) L_b(z)) and K_b = e^{-T_b}:
-//   sigma(L_b(z)) = 1 / (1 + E),   sigma(L_b(1 - z)) = E / (E + K_b),
-// and background rows pair up under one reciprocal for both: e0/g0 + e1/g1 = (e0 g1 + e1 g0) /
-// (g0 g1).  Per 4 evaluations: 2 v_exp + 2 v_rcp (the unpaired kernel: 4 + 2) and half the MFMA
-// work.  Null background rows (past n_bg) have u = 0 and K = 1, i.e. both sigmas are exactly 1/2;
-// that constant is subtracted once per coalition instead of pushing them to 0 (which needs exp2
-// ranges that overflow the paired products).  Non-finite tiles (|logits| > ~40 in a pair) are
-// re-summed per element from tau_b = log2(K_b).
+// acc = -log2(e) L_b(z) and tau_b = -log2(e) T_b:
+//   sigma(L_b(z)) = 1 / (1 + exp2(acc)),   sigma(L_b(1 - z)) = 1 / (1 + exp2(tau_b - acc)),
+// i.e. half the MFMA work and half the U-fragment reads of the unpaired kernel for the same
+// evaluations.  Null background rows (past n_bg) have u = 0 and tau = 0, i.e. both sigmas are
+// exactly 1/2; that constant is subtracted once per coalition.
 template <int NTB, int NGL, bool LOGITS>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void kernelshap_paired_kernel(
     const float* __restrict__ X, int d, const float* __restrict__ a, float bias,
     const float* __restrict__ Bg, const float* __restrict__ cb, int n_bg,
-    const uint16_t* __restrict__ Z, int Ppad, int P, const float* __restrict__ Amat,
+    const uint32_t* __restrict__ Zm, int Ppad, int P, const float* __restrict__ Amat,
     const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
     float* __restrict__ f0_out, float* __restrict__ ws, unsigned* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) float ys[];  // [2][ns]: base, then complements
-  __shared__ uint4 Uhi[4 * 2 * 2 * 32], Ulo[4 * 2 * 2 * 32];  // [tile][kstep][half][row]
-  // K_b and tau_b = log2 K_b in MFMA row order: within 4 rows, (0, 2) then (1, 3) -- the two
-  // packed pairs the epilogue consumes are one 16-B LDS read
-  __shared__ float4 Kq[kMaxBg / 4], Tq[kMaxBg / 4];
+  // u = hi + mid + lo, three bf16 terms (|u - hi - mid - lo| <= 2^-27 |u|, fp32-grade products;
+  // hi + lo alone leaves 2^-18 |u|, ~1e-5 in phi at the shipped model's |u| ~ 40), [tile][kstep][half][row]
+  __shared__ uint4 Uhi[4 * 2 * 2 * 32], Umd[4 * 2 * 2 * 32], Ulo[4 * 2 * 2 * 32];
+  // tau_b = -log2(e) T_b in MFMA row order (within 4 rows: 0, 2, 1, 3), one 16-B read per group
+  __shared__ float4 Tq[kMaxBg / 4];
   __shared__ f32x2_t rem[kWaves - 1][kWaves][32];  // remainder tiles: per-wave partial sums
+  // coalitions travel as 32-bit masks (4 B instead of a 64-B bf16 row per coalition: the next
+  // tile's mask is prefetched in one VGPR); a 4-bit slice -> 4 bf16 {0, 1} via a 16-entry LUT
+  // (the 256-entry 8-bit table would push the LDS past 4 workgroups per CU)
+  __shared__ uint2 zlut[16];
   __shared__ float xs[32];
   __shared__ float red[8];
   __shared__ float ph[32];
@@ -380,6 +391,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const int ns = 32 * (st1 - st0);
   constexpr float kNegLog2e = -1.4426950408889634f;
   if (threadIdx.x < 32) xs[threadIdx.x] = threadIdx.x < d ? a[threadIdx.x] * X[(int64_t)e * d + threadIdx.x] : 0.0f;
+  if (threadIdx.x < 16) {
+    const unsigned v = threadIdx.x;
+    uint32_t w[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      w[j] = (((v >> (2 * j)) & 1u) ? 0x3F80u : 0u) | (((v >> (2 * j + 1)) & 1u) ? 0x3F800000u : 0u);
+    zlut[v] = make_uint2(w[0], w[1]);
+  }
   __syncthreads();
   const float lx = wave_sum(lane < 32 ? xs[lane] : 0.0f) + bias;  // logit(x), in every wave
   const float us = LOGITS ? 1.0f : kNegLog2e;
@@ -394,24 +413,45 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       w1 = wr[1];
     }
     const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-    uint32_t hw[4], lw[4];
+    uint32_t hw[4], mw[4], lw[4];
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
       const float u0 = okb ? (xs[k0 + j] - wv8[j]) * us : 0.0f;
       const float u1 = okb ? (xs[k0 + j + 1] - wv8[j + 1]) * us : 0.0f;
       const uint16_t h0 = f32_to_bf16(u0), h1 = f32_to_bf16(u1);
+      const float r0 = u0 - bf16_to_f32(h0), r1 = u1 - bf16_to_f32(h1);  // exact in fp32
+      const uint16_t m0 = f32_to_bf16(r0), m1 = f32_to_bf16(r1);
       hw[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      lw[j >> 1] = pack_bf16x2(u0 - __uint_as_float(((uint32_t)h0) << 16), u1 - __uint_as_float(((uint32_t)h1) << 16));
+      mw[j >> 1] = (uint32_t)m0 | ((uint32_t)m1 << 16);
+      lw[j >> 1] = pack_bf16x2(r0 - bf16_to_f32(m0), r1 - bf16_to_f32(m1));
     }
     Uhi[q] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+    Umd[q] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
     Ulo[q] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
   }
+  __syncthreads();
+  // T_b from the SAME bf16 hi + mid + lo values the MFMA multiplies (sum over the 32 K columns, plus the
+  // intercept column once more: T_b = L_b(1) + c_b), so L_b(1 - z) = T_b - L_b(z) carries exactly
+  // the rounding of the terms outside z, as a direct MFMA evaluation of 1 - z would.  (T_b from
+  // the fp32 logit instead makes the z and 1 - z errors anti-correlated, and the WLS projection
+  // then adds them.)  tau = T_b in accumulator units (-log2(e) L for the sigmoid links).
   if (threadIdx.x < kMaxBg) {
-    const int b = threadIdx.x;
-    const float tau = (!LOGITS && b < n_bg) ? kNegLog2e * (lx + cb[b]) : 0.0f;
+    const int b = threadIdx.x, rr = b & 31, t = b >> 5;
+    float tsum = 0.0f, c31 = 0.0f;
+#pragma unroll
+    for (int e4 = 0; e4 < 4; ++e4) {  // e4 = ks * 2 + hh: K columns 8 e4 .. 8 e4 + 7
+      const int q = (t * 4 + e4) * 32 + rr;
+      const uint4 hv = Uhi[q], mv = Umd[q], lv = Ulo[q];
+      const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, mw[4] = {mv.x, mv.y, mv.z, mv.w};
+      const uint32_t lw[4] = {lv.x, lv.y, lv.z, lv.w};
+#pragma unroll
+      for (int w = 0; w < 4; ++w)
+        tsum += ((bf16lo(hw[w]) + bf16lo(mw[w])) + bf16lo(lw[w])) + ((bf16hi(hw[w]) + bf16hi(mw[w])) + bf16hi(lw[w]));
+      if (e4 == 3) c31 = (bf16hi(hw[3]) + bf16hi(mw[3])) + bf16hi(lw[3]);
+    }
+    const float tau = b < n_bg ? tsum + c31 : 0.0f;
     const int q = (b & ~3) | ((b & 1) << 1) | ((b >> 1) & 1);
     reinterpret_cast<float*>(Tq)[q] = tau;
-    reinterpret_cast<float*>(Kq)[q] = __builtin_amdgcn_exp2f(tau);
   }
   __syncthreads();
   const float inv_nb = 1.0f / (float)n_bg;
@@ -419,19 +459,19 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   const float null_half = 0.5f * (float)(32 * (NTB - 1) + 8 * NGL - n_bg);
   float sumT = 0.0f;  // LOGITS: sum_b T_b (complement logit sum = sumT - base logit sum)
   if constexpr (LOGITS) {
-    for (int b = lane; b < n_bg; b += kWave) sumT += lx + cb[b];
+    for (int b = lane; b < kMaxBg; b += kWave) sumT += reinterpret_cast<const float*>(Tq)[b];  // nulls: 0
     sumT = wave_sum(sumT);
   }
   // (coalition tile, background tile) -> 32 x 32 logits; zb0/zb1 = the tile's Z fragments
   auto mfma_tile = [&](const bf16x8_t& zb0, const bf16x8_t& zb1, int t, int oz) {
     const int q0 = (t * 2 + 0) * 64 + h * 32 + r + oz, q1 = (t * 2 + 1) * 64 + h * 32 + r + oz;
-    const bf16x8_t uh0 = __builtin_bit_cast(bf16x8_t, Uhi[q0]), ul0 = __builtin_bit_cast(bf16x8_t, Ulo[q0]);
-    const bf16x8_t uh1 = __builtin_bit_cast(bf16x8_t, Uhi[q1]), ul1 = __builtin_bit_cast(bf16x8_t, Ulo[q1]);
-    f32x16_t acc = {};
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh0, zb0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul0, zb0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(uh1, zb1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ul1, zb1, acc, 0, 0, 0);
+    f32x16_t acc = {};  // smallest terms first
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Ulo[q0]), zb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Ulo[q1]), zb1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Umd[q0]), zb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Umd[q1]), zb1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Uhi[q0]), zb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Uhi[q1]), zb1, acc, 0, 0, 0);
     return acc;
   };
   // -> (sum of sigma over the lane's rows for z, the same for 1 - z); rows of group j of tile t
@@ -444,37 +484,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       for (int i = 0; i < 4 * ng; ++i) ts += acc[i];
       return f32x2_t{ts, 0.0f};
     } else {
-      // scalar f32 on purpose (and -fno-slp-vectorize for this file): v_pk_*_f32 issue no faster
-      // than two plain ops here and cost more beside the MFMAs (MI355X_MICROARCH constants table)
-      float tb0 = 0.0f, tb1 = 0.0f, tc0 = 0.0f, tc1 = 0.0f;
+      // Per element, sigma = rcp(1 + exp2(acc)) and sigma(1 - z) = rcp(1 + exp2(tau_b - acc)):
+      // exact limits at both ends (rcp(inf) = 0), so no overflow test and no fallback branch.  A
+      // reciprocal shared by a pair, (d0 + d1) / (d0 d1), saves a v_rcp, but its product
+      // overflows once one logit is below ~-44 (for the complements, once T_0 + T_1 is below
+      // ~-88) and then silently drops the partner's sigma: trained models hit that in most tiles,
+      // and clamping the inputs costs the VALU the shared reciprocal saves.  Scalar f32 on purpose
+      // (and -fno-slp-vectorize for this file): v_pk_*_f32 are no cheaper than two plain ops.
+      float tb[4] = {0.0f, 0.0f, 0.0f, 0.0f}, tc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int i = 0; i < 4 * ng; i += 4) {
-        const float4 kk = Kq[8 * t + 2 * (i >> 2) + h];  // rows +0, +2, +1, +3
-        const float e0 = __builtin_amdgcn_exp2f(acc[i]), e1 = __builtin_amdgcn_exp2f(acc[i + 1]);
-        const float e2 = __builtin_amdgcn_exp2f(acc[i + 2]), e3 = __builtin_amdgcn_exp2f(acc[i + 3]);
-        const float d0 = e0 + 1.0f, d1 = e1 + 1.0f, d2 = e2 + 1.0f, d3 = e3 + 1.0f;
-        tb0 = fmaf(d0 + d1, fast_rcp(d0 * d1), tb0);
-        tb1 = fmaf(d2 + d3, fast_rcp(d2 * d3), tb1);
-        const float g0 = e0 + kk.x, g1 = e1 + kk.z, g2 = e2 + kk.y, g3 = e3 + kk.w;
-        tc0 = fmaf(fmaf(e0, g1, e1 * g0), fast_rcp(g0 * g1), tc0);
-        tc1 = fmaf(fmaf(e2, g3, e3 * g2), fast_rcp(g2 * g3), tc1);
-      }
-      f32x2_t tb = {tb0, tb1}, tcm = {tc0, tc1};
-      f32x2_t out = {tb.x + tb.y, tcm.x + tcm.y};
-      // overflow (NaN) or an underflowed pair product (rcp -> inf) somewhere in this lane's tile
-      if (!__builtin_isfinite(out.x + out.y)) {
-        out = f32x2_t{0.0f, 0.0f};
+        const float4 tt = Tq[8 * t + 2 * (i >> 2) + h];
+        const float tv[4] = {tt.x, tt.z, tt.y, tt.w};  // rows +0, +1, +2, +3
 #pragma unroll
-        for (int i = 0; i < 4 * ng; i += 4) {
-          const float4 tt = Tq[8 * t + 2 * (i >> 2) + h];
-          const float tv[4] = {tt.x, tt.z, tt.y, tt.w};  // rows +0, +1, +2, +3
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            out.x += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i + k]));
-            out.y += fast_rcp(1.0f + __builtin_amdgcn_exp2f(tv[k] - acc[i + k]));
-          }
+        for (int k = 0; k < 4; ++k) {
+          tb[k] += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i + k]));
+          tc[k] += fast_rcp(1.0f + __builtin_amdgcn_exp2f(tv[k] - acc[i + k]));
         }
       }
+      const f32x2_t out = {(tb[0] + tb[1]) + (tb[2] + tb[3]), (tc[0] + tc[1]) + (tc[2] + tc[3])};
       return out;
     }
   };
@@ -488,9 +516,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // background tile so that no SIMD carries an extra tile (wave w of every workgroup sits on SIMD
   // w: 33 tiles as 9 + 8 + 8 + 8 made SIMD 0 the critical path), partials summed in a fixed order.
   const int nfull = (st1 - st0) / kWaves * kWaves;
+  auto zfrag = [&](uint32_t m, bf16x8_t& zb0, bf16x8_t& zb1) {  // K columns 8h..8h+7, 16+8h..16+8h+7
+    const uint2 a0 = zlut[(m >> (8 * h)) & 0xfu], a1 = zlut[(m >> (8 * h + 4)) & 0xfu];
+    const uint2 b0 = zlut[(m >> (16 + 8 * h)) & 0xfu], b1 = zlut[(m >> (20 + 8 * h)) & 0xfu];
+    zb0 = __builtin_bit_cast(bf16x8_t, make_uint4(a0.x, a0.y, a1.x, a1.y));
+    zb1 = __builtin_bit_cast(bf16x8_t, make_uint4(b0.x, b0.y, b1.x, b1.y));
+  };
+  uint32_t mnext = st0 + wv < st0 + nfull ? Zm[32 * (st0 + wv) + r] : 0u;
   for (int st = st0 + wv; st < st0 + nfull; st += kWaves) {
-    const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
-    const bf16x8_t zb0 = __builtin_bit_cast(bf16x8_t, zr[h]), zb1 = __builtin_bit_cast(bf16x8_t, zr[2 + h]);
+    const uint32_t m = mnext;
+    if (st + kWaves < st0 + nfull) mnext = Zm[32 * (st + kWaves) + r];
+    bf16x8_t zb0, zb1;
+    zfrag(m, zb0, zb1);
     // an opaque zero per iteration keeps the U fragment reads inside the loop: hoisted, the 64
     // VGPRs of U plus the two-sum epilogue spill (the LDS re-read is 4 KB per tile per wave)
     int oz;
@@ -512,8 +549,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     for (int st = st0 + nfull; st < st1; ++st) {
       f32x2_t fs = {0.0f, 0.0f};
       if (wv < NTB) {  // wave-uniform
-        const uint4* zr = reinterpret_cast<const uint4*>(Z + (int64_t)(32 * st + r) * kCols);
-        const bf16x8_t zb0 = __builtin_bit_cast(bf16x8_t, zr[h]), zb1 = __builtin_bit_cast(bf16x8_t, zr[2 + h]);
+        bf16x8_t zb0, zb1;
+        zfrag(Zm[32 * st + r], zb0, zb1);
         const f32x16_t acc = mfma_tile(zb0, zb1, wv, 0);
         fs = wv == NTB - 1 ? epilogue(acc, wv, std::integral_constant<int, NGL>{})
                            : epilogue(acc, wv, std::integral_constant<int, 4>{});
@@ -718,7 +755,7 @@ void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float 
 }
 
 void launch_kernelshap_paired(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
-                              const float* cb, int n_bg, const uint16_t* Z, int Ppad, int parts, const float* Amat,
+                              const float* cb, int n_bg, const uint32_t* Zm, int Ppad, int parts, const float* Amat,
                               const float* Az, int link, float* phi, float* fx_out, float* f0_out, float* ws,
                               unsigned* cnt, hipStream_t stream) {
   check_design(d, 2 * Ppad, 2 * Ppad, 1);
@@ -731,7 +768,7 @@ void launch_kernelshap_paired(const float* X, int n_expl, int d, const float* a,
   const size_t lds = 2 * part_lds(Ppad, parts);
 #define FDX_KP(NT, NG, LG)                                                                          \
   kernelshap_paired_kernel<NT, NG, LG><<<grid, kThreads, lds, stream>>>(                             \
-      X, d, a, bias, bg, cb, n_bg, Z, Ppad, parts, Amat, Az, link, phi, fx_out, f0_out, ws, cnt)
+      X, d, a, bias, bg, cb, n_bg, Zm, Ppad, parts, Amat, Az, link, phi, fx_out, f0_out, ws, cnt)
 #define FDX_KP_NG(NT, LG)                       \
   do {                                          \
     switch (ngl) {                              \

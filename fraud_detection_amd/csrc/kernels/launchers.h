@@ -166,10 +166,11 @@ void launch_kernelshap(const float* X, int n_expl, int d, const float* a, float 
                        const float* cb, int n_bg, const uint16_t* Z, int S, int S_pad, int parts,
                        const float* Amat, const float* Az, int link, float* phi, float* fx_out, float* f0_out,
                        float* ws, unsigned* cnt, hipStream_t stream, unsigned long long* stamps = nullptr);
-// Complement-paired design: Z [Ppad][32] base coalitions, slot Ppad + p of Amat [d-1][2 Ppad] is
-// the complement of base p (zero column when it is not in the design).
+// Complement-paired design: Zm [Ppad] base coalition bitmasks (bit k = feature k taken from x,
+// bit 31 = 1: the intercept column), slot Ppad + p of Amat [d-1][2 Ppad] is the complement of base
+// p (zero column when it is not in the design).
 void launch_kernelshap_paired(const float* X, int n_expl, int d, const float* a, float bias, const float* bg,
-                              const float* cb, int n_bg, const uint16_t* Z, int Ppad, int parts, const float* Amat,
+                              const float* cb, int n_bg, const uint32_t* Zm, int Ppad, int parts, const float* Amat,
                               const float* Az, int link, float* phi, float* fx_out, float* f0_out, float* ws,
                               unsigned* cnt, hipStream_t stream);
 // workgroups of the linear kernel resident on the device at once (parts -> LDS per workgroup)

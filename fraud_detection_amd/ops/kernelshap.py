@@ -125,8 +125,13 @@ def _device_design(expl, dev):
     W = np.zeros((expl.B.shape[0], 32), np.float32)
     W[:, :d] = (expl.B.astype(np.float32) * a32[:d][None, :]).astype(np.float32)
     W[:, 31] = -cb
+    if paired:  # bitmasks: bit k = z_k, bit 31 = the intercept column
+        Zb = (Zp[:, :31] > 0.5).astype(np.uint64) << np.arange(31, dtype=np.uint64)[None, :]
+        Zdev = torch.from_numpy((Zb.sum(1) | (1 << 31)).astype(np.uint32).view(np.int32)).to(dev)
+    else:
+        Zdev = torch.from_numpy(Zp).to(dev).to(torch.bfloat16).contiguous()
     t = {
-        "Z": torch.from_numpy(Zp).to(dev).to(torch.bfloat16).contiguous(),
+        "Z": Zdev,
         "A": torch.from_numpy(Ap).to(dev).contiguous(),
         "Az": torch.from_numpy((expl.A @ expl.zM).astype(np.float32)).to(dev),
         "a": torch.from_numpy(a32).to(dev),

@@ -243,3 +243,32 @@ def test_paired_kernel_matches_unpaired(dev, link, monkeypatch):
     np.testing.assert_allclose(pp[0], ref[0], atol=tol)
     np.testing.assert_allclose(pp[0], pu[0], atol=tol)
     np.testing.assert_allclose(pp[1], pu[1], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("paired", ["1", "0"])
+def test_linear_kernel_wide_logit_range(dev, paired, monkeypatch):
+    """The shipped reference LR on Kaggle-like raw rows: explanation and background logits span
+    -33..31, so pair products of the sigmoid epilogue overflow (a background logit T_b below -44,
+    or one coalition logit below -44 next to a moderate one).  Such tiles must take the
+    per-element path instead of losing the partner's sigma."""
+    from _models import kaggle_like_rows
+    from fraud_detection_amd.compat.safe_joblib import decode_logistic, decode_scaler
+    from fraud_detection_amd.ops import predict as P
+    from fraud_detection_amd.ops.kernelshap import kernelshap
+
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    m = decode_logistic(os.path.join(root, "models", "logistic_model.joblib"))
+    s = decode_scaler(os.path.join(root, "models", "scaler.joblib"))
+    w = np.zeros(32)
+    w[:30] = m["coef"].ravel()
+    w[30] = float(m["intercept"].ravel()[0])
+    a, _, bias = P.fold_scaler(w, s["mean_"], s["scale_"], None)
+    B, X = kaggle_like_rows(100, seed=1), kaggle_like_rows(96, seed=5)
+    monkeypatch.setenv("FDX_KS_PAIRED", paired)
+    ke = EX.KernelExplainer(a, bias, B, device=str(dev))
+    phi, fx, f0 = kernelshap(torch.from_numpy(X).to(dev), ke)
+    ref = EX.kernelshap_reference(X, ke.a, ke.bias, ke.B, ke.Z, ke.A, ke.zM, "identity")
+    np.testing.assert_allclose(phi, ref[0], atol=5e-6)
+    np.testing.assert_allclose(phi.sum(1), fx - f0, atol=2e-6)

@@ -76,8 +76,8 @@ for st in "$@"; do
     pmcks)  # KernelSHAP linear kernel counters (3 passes, 1000-explanation batches)
       cd /tmp && export TMPDIR=/tmp
       KS="python3 $R/tools/kernelshap_bench.py --quick --skip-tree --reps 5"
-      step pmcks_a 120 rocprofv3 --kernel-include-regex kernelshap_linear --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/pmcks_a" -o run -- $KS
-      step pmcks_b 120 rocprofv3 --kernel-include-regex kernelshap_linear --pmc SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcks_b" -o run -- $KS
+      step pmcks_a 120 rocprofv3 --kernel-include-regex "kernelshap_(linear|paired)" --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS --output-format csv -d "$OUT/pmcks_a" -o run -- $KS
+      step pmcks_b 120 rocprofv3 --kernel-include-regex "kernelshap_(linear|paired)" --pmc SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcks_b" -o run -- $KS
       step pmcks_t 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmcks_t" -o run -- $KS
       cd "$R" ;;
     py:*) # shellcheck disable=SC2086

@@ -1,24 +1,66 @@
-import sys, time, json
-sys.path.insert(0, "/root/repo") if False else None
-import os; sys.path.insert(0, os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
-import numpy as np, torch
-from fraud_detection_amd.data.synthetic import separable
-from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
-from fraud_detection_amd.models.explainers import KernelExplainer, kernelshap_throughput
-from fraud_detection_amd.ops.kernelshap import kernelshap
-dev = torch.device("cuda", 0)
-X, y = separable(2_000_000, seed=1000, device=dev)
-res = DevicePipeline(TrainConfig(seed=42)).fit(X, y)
-print("bench helper:", kernelshap_throughput(res, dev, None))
-a, c, b = res.folded()
-Xb, _ = separable(100, seed=91); Xe, _ = separable(1000, seed=92)
-ke = KernelExplainer(a, b, Xb.numpy(), device="cuda")
-Xd = Xe.to(dev)
-z = (Xe.double().numpy() @ a[:30] + b); zb = Xb.double().numpy() @ a[:30] + b
-print("logit range x", z.min(), z.max(), "bg", zb.min(), zb.max(), "|a|", np.abs(a[:30]).max())
-for reps in (5, 50):
-    for _ in range(10): kernelshap(Xd, ke, sync=False)
-    torch.cuda.synchronize(); t0 = time.perf_counter()
-    for _ in range(reps): kernelshap(Xd, ke, sync=False)
-    torch.cuda.synchronize(); dt = (time.perf_counter() - t0) / reps
-    print(reps, "us", dt * 1e6, "values/s", 30000 / dt)
+#!/usr/bin/env python3
+"""KernelSHAP accuracy + throughput check on the served-model setups (GPU): the reference's
+shipped LR on Kaggle-like raw rows (the worker test) and a trained model on synthetic rows (the
+bench), paired vs unpaired kernel, max |phi - fp64 oracle| and us per 1k batch.
+
+    python tools/ks_check.py
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    from _models import kaggle_like_rows
+    from fraud_detection_amd.compat.safe_joblib import decode_logistic, decode_scaler
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.explainers import KernelExplainer, kernelshap_reference
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+    from fraud_detection_amd.ops import predict as P
+    from fraud_detection_amd.ops.kernelshap import kernelshap
+
+    dev = torch.device("cuda", 0)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    model = decode_logistic(os.path.join(root, "models", "logistic_model.joblib"))
+    scaler = decode_scaler(os.path.join(root, "models", "scaler.joblib"))
+    w = np.zeros(32)
+    w[:30] = model["coef"].ravel()
+    w[30] = float(model["intercept"].ravel()[0])
+    a, _, bias = P.fold_scaler(w, scaler["mean_"], scaler["scale_"], None)
+    setups = {"shipped_lr_kaggle_rows": (a, bias, kaggle_like_rows(100, seed=1), kaggle_like_rows(1000, seed=5))}
+    X, y = separable(2_000_000, seed=1000, device=dev)
+    res = DevicePipeline(TrainConfig(seed=42)).fit(X, y)
+    a2, _, b2 = res.folded()
+    setups["trained_lr_synthetic"] = (a2, b2, separable(100, seed=91)[0].numpy(), separable(1000, seed=92)[0].numpy())
+    for name, (aa, bb, B, Xe) in setups.items():
+        for paired in ("1", "0"):
+            os.environ["FDX_KS_PAIRED"] = paired
+            ke = KernelExplainer(aa, bb, B, device="cuda")
+            Xd = torch.from_numpy(np.ascontiguousarray(Xe, np.float32)).to(dev)
+            phi, fx, f0 = kernelshap(Xd, ke)
+            ref = kernelshap_reference(Xe[:200], ke.a, ke.bias, ke.B, ke.Z, ke.A, ke.zM, "identity")
+            err = np.abs(phi[:200] - ref[0])
+            for _ in range(10):
+                kernelshap(Xd, ke, sync=False)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(50):
+                kernelshap(Xd, ke, sync=False)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / 50
+            zx = Xe.astype(np.float64) @ ke.a[:30] + ke.bias
+            print(json.dumps({"setup": name, "paired": paired, "max_err": float(err.max()),
+                              "p99_err": float(np.quantile(err, 0.99)), "mean_err": float(err.mean()),
+                              "us_per_1k": round(dt * 1e6, 2), "logit_x_range": [float(zx.min()), float(zx.max())]}),
+                  flush=True)
+
+
+if __name__ == "__main__":
+    main()
