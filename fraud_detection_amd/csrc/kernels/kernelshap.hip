@@ -23,8 +23,9 @@
 // work and ~60 fewer VGPRs, so all 1000 workgroups of a 1k-explanation batch are resident in one
 // dispatch round.  Sigmoid epilogue: u is pre-scaled by -log2(e) so sigma = 1 / (1 + exp2(acc)),
 // and two background rows share one reciprocal, 1/d0 + 1/d1 = (d0 + d1) / (d0 d1): per pair one
-// v_exp_f32 + 1/2 v_rcp_f32 instead of one of each (the phase is VALU-issue bound).  exp2 overflow
-// (logit < -88) turns a pair into NaN; that tile is re-summed per element (rcp(inf) = 0).
+// v_exp_f32 + 1/2 v_rcp_f32 instead of one of each (the phase is VALU-issue bound); the exp2
+// argument is shifted by -40 so the pair product cannot overflow while either sigma matters.
+// exp2 overflow (logit < ~-116) turns a pair into NaN; that tile is re-summed per element.
 //
 // Tree ensemble (kernelshap_tree_kernel, model-agnostic path for the GBDT family): the model is
 // evaluated on the masked rows z * x + (1 - z) * B_b without materialising them.  Per tree t the
@@ -49,6 +50,7 @@ constexpr int kMaxBg = 128;      // 4 background tiles of 32
 constexpr int kMaxS = 4096;      // coalitions per design
 constexpr int kMaxParts = 8;
 constexpr float kNullAcc = 70.0f;     // exact in bf16; sigma = 1 / (1 + 2^70)
+constexpr float kPairShift = 40.0f;   // exp2 argument shift of the paired-reciprocal epilogue
 constexpr int kTreeLdsLeaves = 8192;  // leaves (floats) staged in LDS by the tree kernel
 constexpr int kMaxTrees = 2048;
 
@@ -237,7 +239,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         // links get acc = kNullAcc (2^-70 ~ 0 after the sigmoid, finite in the paired
         // reciprocal) and the logit link gets 0 -- every background tile is then a full tile
         const bool icpt = k0 + j + jj == kCols - 1;
-        uu[jj] = okb ? (xs[k0 + j + jj] - wv8[j + jj]) * us : (!LOGITS && icpt ? kNullAcc : 0.0f);
+        // column 30 (never a feature: d <= 30) carries the epilogue's -kPairShift, exact in bf16,
+        // against Z[:, 30] = 1: acc = -log2(e) L - 40 without touching the intercept's precision
+        const bool shift = !LOGITS && k0 + j + jj == kBiasCol;
+        uu[jj] = shift ? -kPairShift
+                       : okb ? (xs[k0 + j + jj] - wv8[j + jj]) * us : (!LOGITS && icpt ? kNullAcc : 0.0f);
       }
       const uint16_t h0 = f32_to_bf16(uu[0]), h1 = f32_to_bf16(uu[1]);
       const float r0 = uu[0] - __uint_as_float(((uint32_t)h0) << 16);
@@ -279,27 +285,29 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
         return ts;
       } else {
         // 4 background rows per step in packed f32: rows (i, i+2) and (i+1, i+3) pair up so
-        // that the sums d0 + d1 and products d0 d1 of both pairs are one v_pk_add / v_pk_mul
+        // that the sums d0 + d1 and products d0 d1 of both pairs are one v_pk_add / v_pk_mul.
+        // Scaled by 2^-S (S = kPairShift, folded into the GEMM): E' = 2^-S E, d' = 2^-S + E',
+        // sigma = 2^-S / d', so d' is in [2^-40, 2^128] and a pair product d0' d1' can overflow
+        // only if d1' > 1, i.e. when the partner's sigma is below 2^-40 anyway (unscaled, a logit
+        // below -44 next to any moderate one overflowed and silently dropped the partner's sigma;
+        // trained models hit that in most tiles).  It never underflows (>= 2^-80).
+        constexpr float kOne = 1.0f / 1099511627776.0f;  // 2^-40
         f32x2_t ts2 = {0.0f, 0.0f};
-        float mx = 0.0f;
 #pragma unroll
         for (int i = 0; i < 4 * ng; i += 4) {
           const f32x2_t e02 = {__builtin_amdgcn_exp2f(acc[i]), __builtin_amdgcn_exp2f(acc[i + 2])};
           const f32x2_t e13 = {__builtin_amdgcn_exp2f(acc[i + 1]), __builtin_amdgcn_exp2f(acc[i + 3])};
-          const f32x2_t d02 = e02 + 1.0f, d13 = e13 + 1.0f;
+          const f32x2_t d02 = e02 + kOne, d13 = e13 + kOne;
           const f32x2_t pr = d02 * d13;
           const f32x2_t rc = {fast_rcp(pr.x), fast_rcp(pr.y)};
           ts2 = __builtin_elementwise_fma(d02 + d13, rc, ts2);
-          mx = fmaxf(fmaxf(mx, pr.x), pr.y);
         }
-        float ts = ts2.x + ts2.y;
-        // an overflowed pair product (a logit below ~-44 zeroes its partner's sigma too) or
-        // exp2 overflow (logit < -88): per-element form
-        if (!(mx < __builtin_inff()) || __builtin_isnan(ts)) {
+        float ts = (ts2.x + ts2.y) * kOne;
+        if (__builtin_isnan(ts)) {  // exp2 overflow (logit below ~-116) in this lane: per-element form
           ts = 0.0f;
 #pragma unroll
           for (int i = 0; i < 16; ++i)
-            if ((i >> 2) < ng) ts += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i]));
+            if ((i >> 2) < ng) ts += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i] + kPairShift));
         }
         return ts;
       }

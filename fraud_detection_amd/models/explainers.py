@@ -515,9 +515,11 @@ class FunctionKernelExplainer:
         return _project(f, f0, fx, self.A, self.zM), fx, f0
 
 
-def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 100, reps: int = 20) -> dict:
-    """bench.py extra: KernelSHAP values/s for 1k explanations/batch (DP: per-rank shards).  Enough
-    warm-up and repetitions that the clock ramp and the first launch do not dominate a ~60 us batch."""
+def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 100, reps: int = 100) -> dict:
+    """bench.py extra: KernelSHAP values/s for 1k explanations/batch (DP: per-rank shards), the
+    steady state of a loaded XAI worker.  ~20 ms of back-to-back batches first: the GPU clock
+    ramps over milliseconds, and after only 10 warm-up batches (0.6 ms) a 55 us batch measured
+    61-63 us (profiles/r2_s5h)."""
     from ..data.synthetic import separable
 
     a, c, b = res.folded()
@@ -528,7 +530,7 @@ def kernelshap_throughput(res, dev, comm=None, n_expl: int = 1000, n_bg: int = 1
     from ..ops.kernelshap import kernelshap
 
     kernelshap(Xd, ke)
-    for _ in range(10):
+    for _ in range(300):
         kernelshap(Xd, ke, sync=False)
     if comm:
         comm.barrier()

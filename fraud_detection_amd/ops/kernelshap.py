@@ -79,7 +79,11 @@ def complement_pairs(Z: np.ndarray):
 
 
 def _paired_enabled() -> bool:
-    return os.environ.get("FDX_KS_PAIRED", "1") != "0"
+    """FDX_KS_PAIRED=1 selects the complement-paired kernel.  Default off: measured on MI355X
+    (profiles/r2_s5f, r2_s5h) the one-coalition-per-column kernel with the shifted pair reciprocal
+    runs 55 us per 1k batch against 62 us for the paired one -- the paired layout halves the MFMA
+    work, but its safe (per-element) sigma costs more VALU than the pair reciprocal it gives up."""
+    return os.environ.get("FDX_KS_PAIRED", "0") == "1"
 
 
 def _device_design(expl, dev):
@@ -87,7 +91,7 @@ def _device_design(expl, dev):
     background intercepts into the GEMM), A [d-1, S_pad] (zero-padded), A z_M, the weighted
     background rows W and the background logits.
 
-    Paired layout (default, kernelshap_paired_kernel): Z holds the Ppad base coalitions of the
+    Paired layout (FDX_KS_PAIRED=1, kernelshap_paired_kernel): Z holds the Ppad base coalitions of the
     complement pairs and A [d-1, 2 Ppad] has the base columns first, then each base's complement
     (zero columns for padding and for complements the design does not contain: they carry no
     weight, so the WLS solution is unchanged)."""
@@ -117,6 +121,7 @@ def _device_design(expl, dev):
         Zp[:S, :d] = expl.Z
         Ap = np.zeros((d - 1, S_pad), np.float32)
         Ap[:, :S] = expl.A
+        Zp[:, 30] = 1.0  # the epilogue's exp2 shift rides in U column 30 (kernelshap.hip kPairShift)
     Zp[:, 31] = 1.0
     a32 = np.zeros(32, np.float32)
     a32[:d] = expl.a[:d]
