@@ -364,11 +364,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
 // so one MFMA tile yields the logits of 32 coalitions AND of their 32 complements.  The host
 // (ops/kernelshap.py) stores Ppad base coalitions; slot Ppad + p is the complement of base p (a
 // base whose complement is not in the design gets a zero A column there).  With
-// acc = -log2(e) L_b(z) and tau_b = -log2(e) T_b:
-//   sigma(L_b(z)) = 1 / (1 + exp2(acc)),   sigma(L_b(1 - z)) = 1 / (1 + exp2(tau_b - acc)),
-// i.e. half the MFMA work and half the U-fragment reads of the unpaired kernel for the same
-// evaluations.  Null background rows (past n_bg) have u = 0 and tau = 0, i.e. both sigmas are
-// exactly 1/2; that constant is subtracted once per coalition.
+// acc = -log2(e) L_b(z) (shifted by -40 like the unpaired kernel) and tau_b from T_b:
+//   sigma(L_b(z)) = 1 / (1 + exp2(acc + 40)),   sigma(L_b(1 - z)) = 1 / (1 + exp2(tau_b - acc + 40)),
+// both summed with the unpaired kernel's shifted pair reciprocal: half the MFMA work, U-fragment
+// reads and Z traffic of the unpaired kernel for the same evaluations, one extra v_sub per pair.
+// Null background rows (past n_bg) have u = 0 and T = 0, i.e. both sigmas are exactly 1/2; that
+// constant is subtracted once per coalition.
 template <int NTB, int NGL, bool LOGITS>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) void kernelshap_paired_kernel(
     const float* __restrict__ X, int d, const float* __restrict__ a, float bias,
@@ -377,9 +378,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
     const float* __restrict__ Az, int link, float* __restrict__ phi, float* __restrict__ fx_out,
     float* __restrict__ f0_out, float* __restrict__ ws, unsigned* __restrict__ cnt) {
   extern __shared__ __attribute__((aligned(16))) float ys[];  // [2][ns]: base, then complements
-  // u = hi + mid + lo, three bf16 terms (|u - hi - mid - lo| <= 2^-27 |u|, fp32-grade products;
-  // hi + lo alone leaves 2^-18 |u|, ~1e-5 in phi at the shipped model's |u| ~ 40), [tile][kstep][half][row]
-  __shared__ uint4 Uhi[4 * 2 * 2 * 32], Umd[4 * 2 * 2 * 32], Ulo[4 * 2 * 2 * 32];
+  __shared__ uint4 Uhi[4 * 2 * 2 * 32], Ulo[4 * 2 * 2 * 32];  // [tile][kstep][half][row]
   // tau_b = -log2(e) T_b in MFMA row order (within 4 rows: 0, 2, 1, 3), one 16-B read per group
   __shared__ float4 Tq[kMaxBg / 4];
   __shared__ f32x2_t rem[kWaves - 1][kWaves][32];  // remainder tiles: per-wave partial sums
@@ -421,43 +420,43 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       w1 = wr[1];
     }
     const float wv8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
-    uint32_t hw[4], mw[4], lw[4];
+    uint32_t hw[4], lw[4];
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const float u0 = okb ? (xs[k0 + j] - wv8[j]) * us : 0.0f;
-      const float u1 = okb ? (xs[k0 + j + 1] - wv8[j + 1]) * us : 0.0f;
-      const uint16_t h0 = f32_to_bf16(u0), h1 = f32_to_bf16(u1);
-      const float r0 = u0 - bf16_to_f32(h0), r1 = u1 - bf16_to_f32(h1);  // exact in fp32
-      const uint16_t m0 = f32_to_bf16(r0), m1 = f32_to_bf16(r1);
+      float uu[2];
+#pragma unroll
+      for (int jj = 0; jj < 2; ++jj)  // column 30: the exp2 shift (-kPairShift, every row, exact in bf16)
+        uu[jj] = !LOGITS && k0 + j + jj == kBiasCol ? -kPairShift : okb ? (xs[k0 + j + jj] - wv8[j + jj]) * us : 0.0f;
+      const uint16_t h0 = f32_to_bf16(uu[0]), h1 = f32_to_bf16(uu[1]);
       hw[j >> 1] = (uint32_t)h0 | ((uint32_t)h1 << 16);
-      mw[j >> 1] = (uint32_t)m0 | ((uint32_t)m1 << 16);
-      lw[j >> 1] = pack_bf16x2(r0 - bf16_to_f32(m0), r1 - bf16_to_f32(m1));
+      lw[j >> 1] = pack_bf16x2(uu[0] - bf16_to_f32(h0), uu[1] - bf16_to_f32(h1));
     }
     Uhi[q] = make_uint4(hw[0], hw[1], hw[2], hw[3]);
-    Umd[q] = make_uint4(mw[0], mw[1], mw[2], mw[3]);
     Ulo[q] = make_uint4(lw[0], lw[1], lw[2], lw[3]);
   }
   __syncthreads();
-  // T_b from the SAME bf16 hi + mid + lo values the MFMA multiplies (sum over the 32 K columns, plus the
-  // intercept column once more: T_b = L_b(1) + c_b), so L_b(1 - z) = T_b - L_b(z) carries exactly
-  // the rounding of the terms outside z, as a direct MFMA evaluation of 1 - z would.  (T_b from
-  // the fp32 logit instead makes the z and 1 - z errors anti-correlated, and the WLS projection
-  // then adds them.)  tau = T_b in accumulator units (-log2(e) L for the sigmoid links).
+  // T_b from the SAME bf16 hi + lo values the MFMA multiplies (the 30 feature columns plus the
+  // intercept column twice: T_b = L_b(1) + c_b; not the shift column), so L_b(1 - z) = T_b - L_b(z)
+  // carries exactly the rounding of the terms outside z, as a direct MFMA evaluation of 1 - z
+  // would.  (T_b from the fp32 logit instead makes the z and 1 - z errors anti-correlated, and the
+  // WLS projection then adds them.)  Stored as tau = T_b - 2 S in accumulator units: with acc =
+  // -log2(e) L_b(z) - S, the complement's shifted exponent is tau - acc.
   if (threadIdx.x < kMaxBg) {
     const int b = threadIdx.x, rr = b & 31, t = b >> 5;
     float tsum = 0.0f, c31 = 0.0f;
 #pragma unroll
     for (int e4 = 0; e4 < 4; ++e4) {  // e4 = ks * 2 + hh: K columns 8 e4 .. 8 e4 + 7
       const int q = (t * 4 + e4) * 32 + rr;
-      const uint4 hv = Uhi[q], mv = Umd[q], lv = Ulo[q];
-      const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, mw[4] = {mv.x, mv.y, mv.z, mv.w};
-      const uint32_t lw[4] = {lv.x, lv.y, lv.z, lv.w};
+      const uint4 hv = Uhi[q], lv = Ulo[q];
+      const uint32_t hw[4] = {hv.x, hv.y, hv.z, hv.w}, lw[4] = {lv.x, lv.y, lv.z, lv.w};
 #pragma unroll
-      for (int w = 0; w < 4; ++w)
-        tsum += ((bf16lo(hw[w]) + bf16lo(mw[w])) + bf16lo(lw[w])) + ((bf16hi(hw[w]) + bf16hi(mw[w])) + bf16hi(lw[w]));
-      if (e4 == 3) c31 = (bf16hi(hw[3]) + bf16hi(mw[3])) + bf16hi(lw[3]);
+      for (int w = 0; w < 4; ++w) {
+        if (e4 != 3 || w != 3) tsum += bf16lo(hw[w]) + bf16lo(lw[w]);  // column 30 = the shift
+        tsum += bf16hi(hw[w]) + bf16hi(lw[w]);
+      }
+      if (e4 == 3) c31 = bf16hi(hw[3]) + bf16hi(lw[3]);
     }
-    const float tau = b < n_bg ? tsum + c31 : 0.0f;
+    const float tau = (b < n_bg ? tsum + c31 : 0.0f) - (LOGITS ? 0.0f : 2.0f * kPairShift);
     const int q = (b & ~3) | ((b & 1) << 1) | ((b >> 1) & 1);
     reinterpret_cast<float*>(Tq)[q] = tau;
   }
@@ -473,13 +472,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
   // (coalition tile, background tile) -> 32 x 32 logits; zb0/zb1 = the tile's Z fragments
   auto mfma_tile = [&](const bf16x8_t& zb0, const bf16x8_t& zb1, int t, int oz) {
     const int q0 = (t * 2 + 0) * 64 + h * 32 + r + oz, q1 = (t * 2 + 1) * 64 + h * 32 + r + oz;
-    f32x16_t acc = {};  // smallest terms first
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Ulo[q0]), zb0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Ulo[q1]), zb1, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Umd[q0]), zb0, acc, 0, 0, 0);
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Umd[q1]), zb1, acc, 0, 0, 0);
+    f32x16_t acc = {};
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Uhi[q0]), zb0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Ulo[q0]), zb0, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Uhi[q1]), zb1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, Ulo[q1]), zb1, acc, 0, 0, 0);
     return acc;
   };
   // -> (sum of sigma over the lane's rows for z, the same for 1 - z); rows of group j of tile t
@@ -492,25 +489,43 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4))) v
       for (int i = 0; i < 4 * ng; ++i) ts += acc[i];
       return f32x2_t{ts, 0.0f};
     } else {
-      // Per element, sigma = rcp(1 + exp2(acc)) and sigma(1 - z) = rcp(1 + exp2(tau_b - acc)):
-      // exact limits at both ends (rcp(inf) = 0), so no overflow test and no fallback branch.  A
-      // reciprocal shared by a pair, (d0 + d1) / (d0 d1), saves a v_rcp, but its product
-      // overflows once one logit is below ~-44 (for the complements, once T_0 + T_1 is below
-      // ~-88) and then silently drops the partner's sigma: trained models hit that in most tiles,
-      // and clamping the inputs costs the VALU the shared reciprocal saves.  Scalar f32 on purpose
-      // (and -fno-slp-vectorize for this file): v_pk_*_f32 are no cheaper than two plain ops.
-      float tb[4] = {0.0f, 0.0f, 0.0f, 0.0f}, tc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      // The unpaired kernel's shifted pair reciprocal, for z and for 1 - z: with shifted
+      // exponents E' = exp2(acc) and E'' = exp2(tau - acc) (both 2^-40 times the unshifted ones),
+      // d = 2^-40 + E, sigma = 2^-40 / d, rows (0, 1) and (2, 3) share one reciprocal.  A pair
+      // product overflows only when the partner's sigma is below 2^-40 and never underflows.
+      // (The cheaper complement form E / (E + K_b) has products no shift keeps in range: it
+      // dropped sigmas at T_0 + T_1 < -88.)
+      constexpr float kOne = 1.0f / 1099511627776.0f;  // 2^-40
+      float tb0 = 0.0f, tb1 = 0.0f, tc0 = 0.0f, tc1 = 0.0f;
 #pragma unroll
       for (int i = 0; i < 4 * ng; i += 4) {
         const float4 tt = Tq[8 * t + 2 * (i >> 2) + h];
         const float tv[4] = {tt.x, tt.z, tt.y, tt.w};  // rows +0, +1, +2, +3
+        float db[4], dc[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-          tb[k] += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i + k]));
-          tc[k] += fast_rcp(1.0f + __builtin_amdgcn_exp2f(tv[k] - acc[i + k]));
+          db[k] = __builtin_amdgcn_exp2f(acc[i + k]) + kOne;
+          dc[k] = __builtin_amdgcn_exp2f(tv[k] - acc[i + k]) + kOne;
+        }
+        tb0 = fmaf(db[0] + db[1], fast_rcp(db[0] * db[1]), tb0);
+        tb1 = fmaf(db[2] + db[3], fast_rcp(db[2] * db[3]), tb1);
+        tc0 = fmaf(dc[0] + dc[1], fast_rcp(dc[0] * dc[1]), tc0);
+        tc1 = fmaf(dc[2] + dc[3], fast_rcp(dc[2] * dc[3]), tc1);
+      }
+      f32x2_t out = {(tb0 + tb1) * kOne, (tc0 + tc1) * kOne};
+      if (__builtin_isnan(out.x + out.y)) {  // exp2 overflow (a logit below ~-116): per element
+        out = f32x2_t{0.0f, 0.0f};
+#pragma unroll
+        for (int i = 0; i < 4 * ng; i += 4) {
+          const float4 tt = Tq[8 * t + 2 * (i >> 2) + h];
+          const float tv[4] = {tt.x, tt.z, tt.y, tt.w};
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            out.x += fast_rcp(1.0f + __builtin_amdgcn_exp2f(acc[i + k] + kPairShift));
+            out.y += fast_rcp(1.0f + __builtin_amdgcn_exp2f(tv[k] - acc[i + k] + kPairShift));
+          }
         }
       }
-      const f32x2_t out = {(tb[0] + tb[1]) + (tb[2] + tb[3]), (tc[0] + tc[1]) + (tc[2] + tc[3])};
       return out;
     }
   };

@@ -132,7 +132,8 @@ def _device_design(expl, dev):
     W[:, 31] = -cb
     if paired:  # bitmasks: bit k = z_k, bit 31 = the intercept column
         Zb = (Zp[:, :31] > 0.5).astype(np.uint64) << np.arange(31, dtype=np.uint64)[None, :]
-        Zdev = torch.from_numpy((Zb.sum(1) | (1 << 31)).astype(np.uint32).view(np.int32)).to(dev)
+        # bit 30 = the epilogue's exp2 shift column (kernelshap.hip kPairShift)
+        Zdev = torch.from_numpy((Zb.sum(1) | (1 << 30) | (1 << 31)).astype(np.uint32).view(np.int32)).to(dev)
     else:
         Zdev = torch.from_numpy(Zp).to(dev).to(torch.bfloat16).contiguous()
     t = {
