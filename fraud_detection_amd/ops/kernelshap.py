@@ -78,12 +78,15 @@ def complement_pairs(Z: np.ndarray):
     return np.asarray(base, np.int64), np.asarray(comp, np.int64)
 
 
-def _paired_enabled() -> bool:
-    """FDX_KS_PAIRED=1 selects the complement-paired kernel.  Default off: measured on MI355X
-    (profiles/r2_s5f, r2_s5h) the one-coalition-per-column kernel with the shifted pair reciprocal
-    runs 55 us per 1k batch against 62 us for the paired one -- the paired layout halves the MFMA
-    work, but its safe (per-element) sigma costs more VALU than the pair reciprocal it gives up."""
-    return os.environ.get("FDX_KS_PAIRED", "0") == "1"
+def _paired_enabled(link: str) -> bool:
+    """FDX_KS_PAIRED=1/0 forces the complement-paired / unpaired kernel; by default (auto) the
+    paired one runs for the log-odds link only.  Measured on MI355X (profiles/r2_s5): with the
+    sigmoid links both run ~55 us per 1k batch (bound by the sigmoid epilogue's issue rate); the
+    log-odds link has no epilogue and the paired kernel's half MFMA work shows, 25.2 vs 34.4 us."""
+    env = os.environ.get("FDX_KS_PAIRED", "auto")
+    if env in ("0", "1"):
+        return env == "1"
+    return link == "logit_model"
 
 
 def _device_design(expl, dev):
@@ -95,7 +98,7 @@ def _device_design(expl, dev):
     complement pairs and A [d-1, 2 Ppad] has the base columns first, then each base's complement
     (zero columns for padding and for complements the design does not contain: they carry no
     weight, so the WLS solution is unchanged)."""
-    key = (str(dev), _paired_enabled())
+    key = (str(dev), _paired_enabled(expl.link))
     if expl._dev_cache is not None and expl._dev_cache[0] == key:
         return expl._dev_cache[1]
     d = expl.d
