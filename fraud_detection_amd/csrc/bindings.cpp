@@ -142,10 +142,12 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });
   m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi,
-                            int phase_start, u aff, u s) {
+                            int phase_start, u aff, u s, u done_host, int seq) {
     fdx::launch_newton_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), d, C, tol,
-                              max_iter, fi, phase_start, P<const double>(aff), S(s));
-  });
+                              max_iter, fi, phase_start, P<const double>(aff), S(s), P<int>(done_host), seq);
+  }, py::arg("red"), py::arg("state"), py::arg("w32"), py::arg("done"), py::arg("d"), py::arg("C"), py::arg("tol"),
+     py::arg("max_iter"), py::arg("fi"), py::arg("phase_start"), py::arg("aff"), py::arg("s"), py::arg("done_host") = 0,
+     py::arg("seq") = 0);
   m.def("logreg_fold", [](u state, u aff, u w32, u s) {
     fdx::launch_logreg_fold(P<const double>(state), P<const double>(aff), P<float>(w32), S(s));
   });

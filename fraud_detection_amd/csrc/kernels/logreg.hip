@@ -296,7 +296,8 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
                                                            double tol, int max_iter,
                                                            int fit_intercept, int phase_start,
                                                            const double* __restrict__ aff,
-                                                           unsigned long long* __restrict__ stamps = nullptr) {
+                                                           unsigned long long* __restrict__ stamps = nullptr,
+                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
   unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   FDX_STAMP(0);
   __shared__ double sr[kLRPartStride];
@@ -317,7 +318,11 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     for (int i = 0; i < NR; ++i) v[i] = red[t + 64 * i];
 #pragma unroll
     for (int i = 0; i < NS; ++i) u[i] = st[t + 64 * i];
-    if (dn) return;
+    if (dn) {
+      if (done_host != nullptr && t == 0)
+        __hip_atomic_store(done_host, (seq << 1) | 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NR; ++i) sr[t + 64 * i] = v[i];
 #pragma unroll
@@ -468,6 +473,11 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   if (t == 0) {
     ss[kIter] += 1.0;
     if (dec != 2 && (int)ss[kIter] >= max_iter) *done = 1;
+    // done_host: a mapped pinned word (seq << 1 | done) the host polls -- no D2H copy kernel
+    // and no event per convergence check; seq tells it that this launch has run.  A system-scope
+    // store (written through to host memory, not left in L2 until the end of the stream)
+    if (done_host != nullptr)
+      __hip_atomic_store(done_host, (seq << 1) | *done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   __syncthreads();
   if (aff) {
@@ -584,13 +594,13 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
-                          const double* aff, hipStream_t stream) {
+                          const double* aff, hipStream_t stream, int* done_host, int seq) {
   if (d + (fit_intercept ? 1 : 0) == 31)  // 30 features + intercept: the specialised stream
     newton_update_kernel<31><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
-                                                   phase_start, aff);
+                                                   phase_start, aff, nullptr, done_host, seq);
   else
     newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
-                                                  phase_start, aff);
+                                                  phase_start, aff, nullptr, done_host, seq);
   check_launch("newton_update");
 }
 

@@ -12,6 +12,9 @@ The device loop never synchronises with the host inside a chunk of iterations: a
 """
 from __future__ import annotations
 
+import os
+import time
+
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -206,6 +209,19 @@ def _default_w0(w0):
     return w
 
 
+def _await_flag(flag: torch.Tensor, seq: int, stream: int, spin_s: float = 0.05):
+    """Poll a mapped pinned flag word until the Newton update tagged ``seq`` has written it.
+    After ``spin_s`` the host stops spinning and synchronises the stream instead (a stalled or
+    faulted device then surfaces as the stream's error rather than a hang)."""
+    t0 = time.perf_counter()
+    while (int(flag[0]) >> 1) != seq:
+        if time.perf_counter() - t0 > spin_s:
+            native().stream_sync(stream)
+            if (int(flag[0]) >> 1) != seq:
+                raise RuntimeError("newton_fit: convergence flag not written after the stream drained")
+            return
+
+
 def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: int = 25,
                class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
                fp8_scale: float = DEFAULT_FP8_SCALE, check_every: int = 4, workspace: LRWorkspace | None = None,
@@ -288,8 +304,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     refresh = auto_hess_refresh(n_sched) if hess_refresh == "auto" else int(hess_refresh)
     full_it = [0]
 
-    def enqueue_chunk(k: int) -> int:
-        for _ in range(k):
+    def enqueue_chunk(k: int, done_host: int = 0, seq: int = 0) -> int:
+        for i in range(k):
             # a fresh Hessian on the first full-data iteration, then every refresh-th (starting
             # the full phase from the warm-up's 4M-row Hessian instead cost one more full pass:
             # 8 vs 7 iterations, profiles/r1_s25)
@@ -300,7 +316,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                 # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
                 comm.all_reduce_(ws.red if fresh else ws.red[:GRAD_SLOTS])
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
-                            int(max_iter + warm), int(fit_intercept), first[0], aff, s)
+                            int(max_iter + warm), int(fit_intercept), first[0], aff, s,
+                            done_host if i == k - 1 else 0, seq)
             first[0] = 0
         return k
 
@@ -317,23 +334,35 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         lookahead = 1 if (comm is not None and comm.world_size > 1) else 2
     depth = max(1, int(lookahead))
     if getattr(ws, "_flags", None) is None or len(ws._flags) < depth + 1:
-        # pinned allocations cost tens of us: once per workspace
+        # pinned allocations cost tens of us: once per workspace.  The chunk's last Newton update
+        # writes (seq << 1) | done straight into a mapped pinned word (device address below) and
+        # the host polls it: no D2H copy kernel and no event per check, whose dependency gaps cost
+        # ~10 us each in the timeline (profiles/r2_s5).
         ws._flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(depth + 1)]
+        ws._flag_dev = [int(m.host_device_pointer(f.data_ptr())) for f in ws._flags]
         ws._events = [torch.cuda.Event() for _ in range(depth + 1)]
-    flags, events = ws._flags, ws._events
+        ws._seq = 0
+    flags, events, fdev = ws._flags, ws._events, ws._flag_dev
+    if os.environ.get("FDX_NEWTON_FLAG", "map") == "copy":  # A/B: D2H copy + event per check
+        fdev = [0] * len(fdev)
     pending = []
     it, slot = 0, 0
     while it < max_iter:
-        it += enqueue_chunk(min(check_every, max_iter - it))
-        flags[slot].copy_(ws.done, non_blocking=True)
-        events[slot].record()
-        pending.append(slot)
+        ws._seq = (ws._seq + 1) & 0x3FFFFFFF
+        it += enqueue_chunk(min(check_every, max_iter - it), fdev[slot], ws._seq)
+        if not fdev[slot]:  # not a mapped allocation: copy the flag behind an event instead
+            flags[slot].copy_(ws.done, non_blocking=True)
+            events[slot].record()
+        pending.append((slot, ws._seq))
         slot = (slot + 1) % (depth + 1)
         if not sync or len(pending) <= depth:
             continue
-        c = pending.pop(0)
-        events[c].synchronize()
-        if int(flags[c][0]):
+        c, seq = pending.pop(0)
+        if fdev[c]:
+            _await_flag(flags[c], seq, s)
+        else:
+            events[c].synchronize()
+        if int(flags[c][0]) & 1:
             break
     return PendingFit(ws.state)
 
