@@ -331,7 +331,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     # when the iteration is a no-op (~15 us per collective at 8 ranks, profiles/r2_s3l): one chunk
     # of slack there (a full-data pass is >= ~60 us, enough to hide the host's wake-up), two alone.
     if lookahead is None:
-        lookahead = 1 if (comm is not None and comm.world_size > 1) else 2
+        lookahead = int(os.environ.get("FDX_NEWTON_LOOKAHEAD", "0")) or (
+            1 if (comm is not None and comm.world_size > 1) else 2)
     depth = max(1, int(lookahead))
     if getattr(ws, "_flags", None) is None or len(ws._flags) < depth + 1:
         # pinned allocations cost tens of us: once per workspace.  The chunk's last Newton update
