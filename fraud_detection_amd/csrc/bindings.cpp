@@ -151,9 +151,11 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("logreg_fold", [](u state, u aff, u w32, u s) {
     fdx::launch_logreg_fold(P<const double>(state), P<const double>(aff), P<float>(w32), S(s));
   });
-  m.def("sgd_update", [](u red, u state, u w32, int d, double C, double lr, double mom, int fi, u s) {
-    fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), d, C, lr, mom, fi, S(s));
-  });
+  m.def("sgd_update", [](u red, u state, u w32, int d, double C, double lr, double mom, int fi, u s, u aff) {
+    fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), d, C, lr, mom, fi, S(s),
+                           P<const double>(aff));
+  }, py::arg("red"), py::arg("state"), py::arg("w32"), py::arg("d"), py::arg("C"), py::arg("lr"), py::arg("mom"),
+     py::arg("fi"), py::arg("s"), py::arg("aff") = 0);
 
   // knn / smote
   m.def("knn_prep", [](u X, int m_, int m_pad, int role, u out, u s) {

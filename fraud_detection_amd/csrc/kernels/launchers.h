@@ -107,7 +107,7 @@ void launch_newton_update_stamped(const double* red, double* state, float* w32, 
                                   const double* aff, unsigned long long* stamps, hipStream_t stream);
 void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream);
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
-                       double momentum, int fit_intercept, hipStream_t stream);
+                       double momentum, int fit_intercept, hipStream_t stream, const double* aff = nullptr);
 
 // ---- knn.hip ----
 // role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29)

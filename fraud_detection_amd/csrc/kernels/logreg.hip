@@ -506,23 +506,41 @@ __global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restric
   store_folded(ss, cA, iA, w32, t);
 }
 
-// Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.
+// Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.  aff (nullable): the rows are
+// pivot-shifted (fused scaler pass); the gradient maps into standardized space exactly as in the
+// Newton update (g_z[j] = inv_j (g_j - c_j g_30)) and w32 gets the folded weights.
 __global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict__ red,
                                                         double* __restrict__ st,
                                                         float* __restrict__ w32, int d, double C,
                                                         double lr, double momentum,
-                                                        int fit_intercept) {
-  __shared__ double grad[32];
+                                                        int fit_intercept, const double* __restrict__ aff) {
+  __shared__ double grad[32], rz[34], ss[kW + 32], cA[32], iA[32];
   const int t = threadIdx.x;
   const double S = red[33] > 0.0 ? red[33] : 1.0;
   const double reg = 1.0 / (C * S);
-  build_grad(red, st, d, fit_intercept, reg, S, grad, t);
+  const double* rr = red;
+  if (aff) {
+    const double av = aff[t];
+    if (t < 32) cA[t] = av; else iA[t - 32] = av;
+    __syncthreads();
+    if (t < 32) rz[t] = iA[t] * (red[t] - cA[t] * red[kBiasCol]);
+    if (t == 32 || t == 33) rz[t] = red[t];
+    __syncthreads();
+    rr = rz;
+  }
+  build_grad(rr, st, d, fit_intercept, reg, S, grad, t);
   __syncthreads();
   if (t < kCols) {
     const double v = momentum * st[kVel + t] - lr * grad[t];
     st[kVel + t] = v;
-    st[kW + t] += v;
-    w32[t] = (t == kLabelCol) ? 0.0f : (float)st[kW + t];
+    ss[kW + t] = st[kW + t] + v;
+    st[kW + t] = ss[kW + t];
+  }
+  __syncthreads();
+  if (aff) {
+    store_folded(ss, cA, iA, w32, t);
+  } else if (t < kCols) {
+    w32[t] = (t == kLabelCol) ? 0.0f : (float)ss[kW + t];
   }
   if (t == 0) {
     double wn2 = 0.0;
@@ -617,8 +635,8 @@ void launch_logreg_fold(const double* state, const double* aff, float* w32, hipS
 }
 
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
-                       double momentum, int fit_intercept, hipStream_t stream) {
-  sgd_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, d, C, lr, momentum, fit_intercept);
+                       double momentum, int fit_intercept, hipStream_t stream, const double* aff) {
+  sgd_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, d, C, lr, momentum, fit_intercept, aff);
   check_launch("sgd_update");
 }
 

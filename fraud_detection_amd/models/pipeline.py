@@ -203,7 +203,7 @@ class DevicePipeline:
         comm = self.comm if world > 1 else None
         tm = _Timer(dev, profile)
         n, d = X.shape
-        fused = (cfg.fold_scaler and cfg.storage in ("bf16", "fp8") and cfg.solver == "newton"
+        fused = (cfg.fold_scaler and cfg.storage in ("bf16", "fp8") and cfg.solver in ("newton", "sgd")
                  and dev.type == "cuda" and scaler_ops.fused_cast_ok(X))
         # training buffer sized for the largest possible SMOTE output, so the cast does not wait
         # for the minority count (+128: a global-scope slice boundary moves by < 128 rows)
@@ -301,7 +301,7 @@ class DevicePipeline:
                                                                             "sgd_batch_rows", cfg.sgd_batch_rows)),
                                  class_w=class_w, d=d, w0=w0,
                                  fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
-                                 workspace=self._ws)
+                                 workspace=self._ws, affine=stats.aff if fused else None)
         else:
             raise ValueError(f"unknown solver {cfg.solver!r}")
         tm.mark("fit")

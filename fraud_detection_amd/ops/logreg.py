@@ -379,17 +379,30 @@ def _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, co
 def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float = 0.9, epochs: int = 5,
             batch_rows: int = 1 << 20, class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True,
             comm=None, fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None,
-            checkpoint=None, checkpoint_every: int = 0) -> FitInfo:
+            checkpoint=None, checkpoint_every: int = 0, affine: torch.Tensor | None = None) -> FitInfo:
     """Momentum minibatch SGD.  Each minibatch is a contiguous window of ``batch_rows`` rows of
     this rank's shard (rows are stored pre-shuffled); DP all-reduces the minibatch gradient.
 
     ``checkpoint`` (utils.checkpoint.CheckpointManager): every ``checkpoint_every`` minibatches
     (and at each epoch end) the solver state -- weights, velocity, objective, step counter -- and
     the data cursor (epoch, minibatch) are saved; a matching checkpoint is resumed from, giving
-    the same result as an uninterrupted fit."""
+    the same result as an uninterrupted fit.
+
+    ``affine``: [64] float64 (c | 1/sigma) for pivot-shifted rows (the fused scaler pass, as in
+    newton_fit): the fit runs in standardized space, the update kernel maps each minibatch
+    gradient and streams folded weights."""
     check_rows(rows)
     w0 = _default_w0(w0)
     n = rows.shape[0]
+    if affine is not None and not rows.is_cuda:
+        a = affine.cpu().double()
+        rows = ((ref.rows_to_f32(rows, fp8_scale, d).double() - a[:32]) * a[32:]).float()
+        affine = None
+    aff = 0
+    if affine is not None:
+        if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
+            raise ValueError("affine must be a [64] float64 tensor on the rows' device")
+        aff = ptr(affine)
     sig = _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm) if checkpoint else None
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
@@ -399,6 +412,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
     m = native()
     ws = workspace or LRWorkspace(rows.device)
     ws.reset(w0, class_w)
+    s = stream_of(rows)
     if got is not None:
         st = got[0]["state"].to(torch.float64)
         ws.state.copy_(st.to(rows.device))
@@ -406,7 +420,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
         w32[LABEL_COL] = 0.0
         ws.w32.copy_(w32.to(rows.device))
         start = (int(got[1]["epoch"]), int(got[1]["batch"]))
-    s = stream_of(rows)
+    if aff:
+        m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)  # the state is standardized-space
     nb = max(1, (n + batch_rows - 1) // batch_rows)
     if comm is not None and comm.world_size > 1:
         nb = int(comm.all_reduce_scalar(nb, op="max"))
@@ -418,7 +433,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float
             if comm is not None and comm.world_size > 1:
                 comm.all_reduce_(ws.red[:GRAD_SLOTS])
             m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), d, float(C), float(lr), float(momentum),
-                         int(fit_intercept), s)
+                         int(fit_intercept), s, aff)
             gstep = ep * nb + b + 1
             last = b + 1 == nb
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):

@@ -49,3 +49,16 @@ def test_shift_roundtrip():
     assert torch.allclose(s[:, :30], (X - X[0]), rtol=1e-5, atol=5e-2)
     assert torch.equal(s[:, 30:], z[:, 30:])
     assert torch.allclose(st.shifted_to_standard(s), z, rtol=1e-4, atol=1e-4)
+
+
+def test_affine_sgd_equals_standardized_sgd():
+    """SGD on pivot-shifted rows with the affine map (the fused scaler path) follows the same
+    standardized-space trajectory as SGD on standardized rows."""
+    X, y = _data()
+    shifted = torch.empty((X.shape[0], 32), dtype=torch.bfloat16)
+    st = S.scaler_fit_cast(X, y, shifted)
+    z = S.scale_cast(X, st, labels=y, out_dtype="f32")
+    kw = dict(C=1.0, lr=0.5, momentum=0.9, epochs=3, batch_rows=8192)
+    f_ref = L.sgd_fit(z, **kw)
+    f_aff = L.sgd_fit(shifted, affine=st.aff, **kw)
+    assert np.allclose(f_aff.w, f_ref.w, rtol=0, atol=3e-3)

@@ -492,3 +492,18 @@ def test_compaction_slots_survive_many_in_flight(dev):
     for l, p in zip(labs, pend):
         exp = torch.nonzero(l == 1).reshape(-1)
         assert torch.equal(p.result().cpu(), exp)
+
+
+@pytest.mark.gpu
+def test_sgd_fused_scaler_matches_unfused(dev):
+    """The SGD solver on the fused scaler pass (pivot-shifted rows + affine-mapped updates) gives
+    the unfused pipeline's model (standardized rows)."""
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
+
+    X, y = separable(400_000, fraud_rate=0.01, seed=13, device=dev)
+    Xt, yt = separable(100_000, fraud_rate=0.01, seed=14, device=dev)
+    r_f = DevicePipeline(TrainConfig(solver="sgd", seed=42)).fit(X, y)
+    r_u = DevicePipeline(TrainConfig(solver="sgd", seed=42, fold_scaler=False)).fit(X, y)
+    assert np.allclose(r_f.fit.w[:31], r_u.fit.w[:31], rtol=0, atol=5e-3)
+    assert abs(evaluate(r_f, Xt, yt)["auc"] - evaluate(r_u, Xt, yt)["auc"]) < 1e-3
