@@ -18,6 +18,9 @@
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   pmc          two PMC passes over a short bench
+#   ksab         KernelSHAP: accuracy vs fp64 + us per batch on three models (tools/ks_check.py), and
+#                tools/kernelshap_bench.py with the paired and the unpaired kernel
+#   newtonab     bench 50 steps x 3 with the Newton flag copied (event) vs polled (mapped pinned word)
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -80,6 +83,15 @@ for st in "$@"; do
       step pmcks_b 120 rocprofv3 --kernel-include-regex "kernelshap_(linear|paired)" --pmc SQ_INSTS_MFMA SQ_INST_CYCLES_VMEM SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT --output-format csv -d "$OUT/pmcks_b" -o run -- $KS
       step pmcks_t 120 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmcks_t" -o run -- $KS
       cd "$R" ;;
+    ksab)
+      step ks_check 300 python tools/ks_check.py
+      for P in 1 0; do
+        FDX_KS_PAIRED=$P step ks_bench_paired$P 200 python tools/kernelshap_bench.py --quick --skip-tree --reps 20
+      done ;;
+    newtonab)
+      for r in 1 2 3; do for F in copy map; do
+        FDX_NEWTON_FLAG=$F step newton_${F}_$r 300 python bench.py --steps 50 --warmup 5 --no-extras
+      done; done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
     *) echo "unknown stage $st"; exit 2 ;;
