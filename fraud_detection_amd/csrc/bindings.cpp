@@ -247,11 +247,13 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_gbdt_transpose(P<const uint8_t>(bins), n, d, P<uint8_t>(binsT), ldt, S(s));
   });
   m.def("gbdt_partition", [](u binsT, int64_t ldt, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u boff,
-                             int nblocks, u seg, u segR, u ridx_out, u nid_out, u s) {
+                             int nblocks, u seg, u segR, u ridx_out, u nid_out, u s, u gcnt) {
     fdx::launch_gbdt_partition(P<const uint8_t>(binsT), ldt, P<const int>(ridx), P<const uint8_t>(nid), n, P<const int>(feat),
                                P<const int>(bin), level, P<uint8_t>(flag), P<int64_t>(boff), nblocks, P<int64_t>(seg),
-                               P<int64_t>(segR), P<int>(ridx_out), P<uint8_t>(nid_out), S(s));
-  });
+                               P<int64_t>(segR), P<int>(ridx_out), P<uint8_t>(nid_out), S(s), P<int64_t>(gcnt));
+  }, py::arg("binsT"), py::arg("ldt"), py::arg("ridx"), py::arg("nid"), py::arg("n"), py::arg("feat"), py::arg("bin"),
+     py::arg("level"), py::arg("flag"), py::arg("boff"), py::arg("nblocks"), py::arg("seg"), py::arg("segR"),
+     py::arg("ridx_out"), py::arg("nid_out"), py::arg("s"), py::arg("gcnt") = 0);
   m.def("gbdt_round_init", [](u hist, int64_t hist_words, u seg, u gcnt, int64_t n, int64_t n_global, u ridx, u nid,
                               u s) {
     fdx::launch_gbdt_round_init(P<unsigned long long>(hist), hist_words, P<int64_t>(seg), P<int64_t>(gcnt), n,

@@ -405,7 +405,8 @@ __global__ __launch_bounds__(kWave) void gbdt_seg_kernel(const uint8_t* __restri
                                                          const int64_t* __restrict__ boff, int64_t n,
                                                          int nblocks, int level,
                                                          int64_t* __restrict__ seg,
-                                                         int64_t* __restrict__ segR) {
+                                                         int64_t* __restrict__ segR,
+                                                         int64_t* __restrict__ gcnt) {
   const int node = heap_first(level) + blockIdx.x;
   const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
   const int64_t r0 = rights_before(flag, boff, n, nblocks, sb);
@@ -417,6 +418,10 @@ __global__ __launch_bounds__(kWave) void gbdt_seg_kernel(const uint8_t* __restri
     seg[2 * (2 * node + 1) + 1] = sc - nr;
     seg[2 * (2 * node + 2)] = sb + sc - nr;
     seg[2 * (2 * node + 2) + 1] = nr;
+    if (gcnt != nullptr) {  // the children's (global, once all-reduced) row counts: no copy kernel
+      gcnt[2 * node + 1] = sc - nr;
+      gcnt[2 * node + 2] = nr;
+    }
   }
 }
 
@@ -658,12 +663,12 @@ void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT
 void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
                            const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
                            int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
-                           hipStream_t stream) {
+                           hipStream_t stream, int64_t* gcnt) {
   if (nblocks > 4096) throw std::runtime_error("gbdt: at most 4096 partition blocks");
   gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(binsT, ldt, ridx, nid, n, feat, bin, flag, boff);
   check_launch("gbdt_part_count");
   launch_exclusive_scan_small(boff, nblocks, boff + nblocks, stream);
-  gbdt_seg_kernel<<<1 << level, kWave, 0, stream>>>(flag, boff, n, nblocks, level, seg, segR);
+  gbdt_seg_kernel<<<1 << level, kWave, 0, stream>>>(flag, boff, n, nblocks, level, seg, segR, gcnt);
   check_launch("gbdt_seg");
   gbdt_part_scatter_kernel<<<nblocks, kPartThreads, 0, stream>>>(flag, boff, ridx, nid, n, seg, segR,
                                                                  ridx_out, nid_out);

@@ -207,7 +207,7 @@ void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT
 void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
                            const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
                            int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
-                           hipStream_t stream);
+                           hipStream_t stream, int64_t* gcnt = nullptr);
 void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
                             int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream);
 void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,

@@ -297,14 +297,15 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             if level == D - 1:
                 break  # leaves: the margin walk and gbdt_leaf (split-kernel child sums) need no partition
             if n:
+                # the seg kernel also writes the children's counts into gcnt (no copy launch)
                 m.gbdt_partition(ptr(binsT), ldt, ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
                                  level, ptr(ws.flag), ptr(ws.boff), PART_BLOCKS, ptr(ws.seg), ptr(ws.segR),
-                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st)
-            else:
-                ws.seg[2 * h0 + 1:2 * (h0 + nn) + 1].zero_()
+                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st, ptr(ws.gcnt))
             cur ^= 1
             c0 = 2 * h0 + 1
-            ws.gcnt[c0:c0 + 2 * nn].copy_(ws.seg[c0:c0 + 2 * nn, 1])
+            if not n:
+                ws.seg[2 * h0 + 1:2 * (h0 + nn) + 1].zero_()
+                ws.gcnt[c0:c0 + 2 * nn].zero_()
             if dist:
                 comm.all_reduce_(ws.gcnt[c0:c0 + 2 * nn])
         m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(o_leaf), st)
