@@ -154,9 +154,10 @@ def test_tree_kernel_matches_oracle(dev, depth, trees, nbg):
 
 # ---------------------------------------------------------------------------------------------
 def _paired_emulation(X, ke, link):
-    """numpy emulation of kernelshap_paired_kernel's arithmetic: base logits from one GEMM,
-    complement logits T_b - L_b(z), sigma(1 - z) = E / (E + K_b), null background rows padded to
-    a multiple of 8 and removed again as the exact 1/2 per row, paired A layout."""
+    """numpy (fp64) emulation of the complement-paired layout: base logits from one GEMM,
+    complement logits T_b - L_b(z) (here through sigma(1 - z) = E / (E + K_b), the same identity the
+    kernel evaluates with a shifted exponent), null background rows padded to a multiple of 8 and
+    removed again as the exact 1/2 per row, paired A layout."""
     from fraud_detection_amd.ops.kernelshap import complement_pairs
 
     d = ke.d
