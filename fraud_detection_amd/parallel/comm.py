@@ -86,9 +86,18 @@ class CollectiveStats:
         self.pending, self.acc = [], {}
 
 
+def _single_node_gloo_iface():
+    """Every rank of a single-node job whose rendezvous is on the loopback address reaches the
+    others over loopback: pin gloo's TCP device to `lo` instead of resolving the host name (which
+    may not resolve in a container) unless the user chose an interface."""
+    if os.environ.get("MASTER_ADDR", "127.0.0.1") in ("127.0.0.1", "localhost") and os.path.exists("/sys/class/net/lo"):
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+
+
 class Communicator:
     def __init__(self, backend: str | None = None, device: torch.device | None = None):
         self.initialized_here = False
+        _single_node_gloo_iface()
         if dist.is_available() and dist.is_initialized():
             self.world_size = dist.get_world_size()
             self.rank = dist.get_rank()
