@@ -285,23 +285,36 @@ __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
 }
 
 // Fixed-order reduction of [nblocks][64] fp64 partials into sums[64].
-// 16 waves, each summing a strided subset of block partials with 8 independent accumulators
-// (eight loads in flight per lane instead of one dependent chain of nblocks/4 loads); the
-// summation tree is fixed by (nblocks, thread) only, so results are run-to-run deterministic.
+// 16 waves, each summing a strided subset of block partials with 32 independent accumulators:
+// the partials come from a whole-device pass (dirty in other XCDs' L2s), so every load round is
+// a long latency -- 32 loads in flight per lane make ~4 rounds for 2048 blocks instead of 16
+// with 8 (15.7 us).  The summation tree is fixed by (nblocks, thread) only, so results are
+// run-to-run deterministic.
 __global__ __launch_bounds__(1024) void scaler_reduce_kernel(const double* __restrict__ partial,
                                                              int nblocks, double* __restrict__ sums) {
+  constexpr int U = 32;
   __shared__ double red[16][64];
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  int b = grp;
-  for (; b + 7 * 16 < nblocks; b += 8 * 16) {
+  double acc[U];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += partial[(int64_t)(b + u * 16) * 64 + e];
+  for (int u = 0; u < U; ++u) acc[u] = 0.0;
+  int b = grp;
+  for (; b + (U - 1) * 16 < nblocks; b += U * 16) {
+    double v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = partial[(int64_t)(b + u * 16) * 64 + e];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] += v[u];
   }
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
+  for (int u = 0; u < U; ++u)
     if (b + u * 16 < nblocks) acc[u] += partial[(int64_t)(b + u * 16) * 64 + e];
-  red[grp][e] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+#pragma unroll
+  for (int w = U / 2; w >= 1; w >>= 1) {
+#pragma unroll
+    for (int u = 0; u < w; ++u) acc[u] += acc[u + w];
+  }
+  red[grp][e] = acc[0];
   __syncthreads();
   if (threadIdx.x < 64) {
     double s = 0.0;
