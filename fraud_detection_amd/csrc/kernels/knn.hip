@@ -52,22 +52,45 @@ __device__ __forceinline__ void topk_insert(float (&bs)[K], int (&bi)[K], float 
 //   candidate: [c_0..c_29, -0.5 ||c||^2, 0]      (padding rows: [0.., -3e38, 0] -> never chosen)
 //   query:     [q_0..q_29, 1, 0]                  (padding rows: zeros)
 // so  score(c, q) = q.c - 0.5 ||c||^2  with no norm loads and a zero-initialised accumulator.
+// role 2 (queries == candidates, the SMOTE self-search): one read of X writes both operands,
+// candidates to `out` and queries to `outq`.  P != nullptr (candidate roles): the same launch also
+// writes the bf16 SMOTE parents of smote_parents_kernel (smote.hip), bit for bit.
 __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, int role,
-                                float* __restrict__ out) {
+                                float* __restrict__ out, float* __restrict__ outq,
+                                const double* __restrict__ aff, uint16_t* __restrict__ P) {
+#pragma clang fp contract(off)  // the parents' mul-then-add must match smote_parents_kernel
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= m_pad) return;
   float4* o = reinterpret_cast<float4*>(out + (int64_t)r * kCols);
+  float4* oq = role == 2 ? reinterpret_cast<float4*>(outq + (int64_t)r * kCols) : nullptr;
   if (r >= m) {
 #pragma unroll
-    for (int k = 0; k < kCols / 4; ++k) o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (role == 0) out[(int64_t)r * kCols + 30] = -3.0e38f;
+    for (int k = 0; k < kCols / 4; ++k) {
+      o[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (oq) oq[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if (role != 1) out[(int64_t)r * kCols + 30] = -3.0e38f;
     return;
   }
   const float4* p = reinterpret_cast<const float4*>(X + (int64_t)r * kCols);
+  uint2* pp = P ? reinterpret_cast<uint2*>(P + (int64_t)r * kCols) : nullptr;
   float s = 0.0f;
 #pragma unroll
   for (int k = 0; k < kCols / 4; ++k) {
     float4 v = p[k];
+    if (pp) {
+      float4 u = v;
+      if (aff != nullptr) {
+        const int c = 4 * k;
+        u.x = u.x * (float)(1.0 / aff[32 + c]) + (float)aff[c];
+        u.y = u.y * (float)(1.0 / aff[32 + c + 1]) + (float)aff[c + 1];
+        if (c + 2 < kBiasCol) {
+          u.z = u.z * (float)(1.0 / aff[32 + c + 2]) + (float)aff[c + 2];
+          u.w = u.w * (float)(1.0 / aff[32 + c + 3]) + (float)aff[c + 3];
+        }
+      }
+      pp[k] = make_uint2(pack_bf16x2(u.x, u.y), pack_bf16x2(u.z, u.w));
+    }
     if (k == kCols / 4 - 1) {  // columns 28..31: keep 28, 29; 30 = norm term / 1, 31 = 0
       s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s);
       v.z = 0.0f; v.w = 0.0f;
@@ -75,8 +98,10 @@ __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, i
       s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
     }
     o[k] = v;
+    if (oq) oq[k] = v;
   }
-  out[(int64_t)r * kCols + 30] = role == 0 ? -0.5f * s : 1.0f;
+  out[(int64_t)r * kCols + 30] = role == 1 ? 1.0f : -0.5f * s;
+  if (oq) outq[(int64_t)r * kCols + 30] = 1.0f;
 }
 
 // Q: [mq_pad][32] query rows and C: [mc_pad][32] candidate rows, both from knn_prep_kernel.
@@ -619,8 +644,11 @@ unsigned merge_blocks(int mq, int nsplit) {
   return (unsigned)(((int64_t)mq << merge_log2(nsplit)) + 255) / 256;
 }
 
-void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, hipStream_t stream) {
-  knn_prep_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, m_pad, role, out);
+void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, float* outq,
+                     const double* aff, uint16_t* P, hipStream_t stream) {
+  if (role < 0 || role > 2 || (role == 2) != (outq != nullptr) || (role == 1 && P != nullptr))
+    throw std::invalid_argument("knn_prep: role 2 needs outq (and only it); parents need a candidate role");
+  knn_prep_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, m_pad, role, out, outq, aff, P);
   check_launch("knn_prep");
 }
 

@@ -110,8 +110,11 @@ void launch_sgd_update(const double* red, double* state, float* w32, int d, doub
                        double momentum, int fit_intercept, hipStream_t stream, const double* aff = nullptr);
 
 // ---- knn.hip ----
-// role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29)
-void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, hipStream_t stream);
+// role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29);
+// role 2: both from one read (candidates -> out, queries -> outq).  P (roles 0/2, optional): the
+// bf16 SMOTE parents of launch_smote_parents (with aff) written by the same launch.
+void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, float* outq,
+                     const double* aff, uint16_t* P, hipStream_t stream);
 int knn_splits(int mq_pad, int mc_pad);
 // bf16x3 MFMA filter + exact fp32 re-score (knn.hip): hl [m_pad][8] uint4 = hi | lo bf16 rows of
 // the prepped rows; tmax [mc_pad / 32] max candidate norm per tile (role 0 only)

@@ -262,18 +262,24 @@ class DevicePipeline:
             k = min(cfg.k_neighbors, xall.shape[0] - 1)
             if k < 1:
                 raise ValueError("SMOTE needs at least 2 minority samples")
-            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off) if n_min > 0 else \
-                torch.empty((0, k), dtype=torch.int32, device=dev)
+            # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
+            # neighbours found in standardized space are interpolated in shifted coordinates.
+            # Parents live in the training rows' space (bf16, pivot-shifted when the scaler is
+            # folded): half the gather bytes of fp32 parents and no per-sample affine map.  The
+            # k-NN operand prep writes them from the same read of the minority rows.
+            parents = None
+            if n_new > 0 and n_min > 0:
+                parents = torch.empty((xall.shape[0], NCOLS), dtype=torch.bfloat16, device=dev)
+            nbr = knn_ops.knn_topk(xmin, xall, k=k, self_offset=q_off, parents=parents,
+                                   parents_affine=stats.aff if (fused and parents is not None) else None) \
+                if n_min > 0 else torch.empty((0, k), dtype=torch.int32, device=dev)
             if glob:  # every rank needs every minority row's neighbour list (int32, k per row)
                 nbr, _ = comm.all_gather_rows(nbr, counts=[r[0] for r in ranks])
                 q_off = 0
             tm.mark("knn")
-            # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
-            # neighbours found in standardized space are interpolated in shifted coordinates
-            # parents in the training rows' space (bf16, pivot-shifted when the scaler is folded):
-            # half the gather bytes of fp32 parents and no per-sample affine map
             if n_new > 0:
-                parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
+                if parents is None:
+                    parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
                 knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
                                        counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,
                                        sample_offset=s_off)

@@ -45,8 +45,22 @@ def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:
     return e
 
 
+def _check_parents(parents: torch.Tensor | None, C: torch.Tensor, affine: torch.Tensor | None) -> int:
+    if parents is None:
+        if affine is not None:
+            raise ValueError("parents_affine without parents")
+        return 0
+    if parents.dtype != torch.bfloat16 or tuple(parents.shape) != (C.shape[0], NCOLS) or \
+            not parents.is_contiguous() or parents.device != C.device:
+        raise ValueError("parents must be a contiguous bf16 [mc, 32] tensor on C's device")
+    if affine is not None and (affine.dtype != torch.float64 or affine.numel() < 64 or affine.device != C.device):
+        raise ValueError("parents_affine must be ScalerStats.aff (float64 [64]) on C's device")
+    return ptr(parents)
+
+
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
-             nsplit: int | None = None, engine: str | None = None):
+             nsplit: int | None = None, engine: str | None = None, parents: torch.Tensor | None = None,
+             parents_affine: torch.Tensor | None = None):
     """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
@@ -57,6 +71,8 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     "bf16x3" = hi.hi + hi.lo + lo.hi bf16 MFMA filter (6 x 32x32x16 bf16 per tile) with a provable
     margin and exact fp32 re-scoring of the survivors; None/"auto" (FDX_KNN env) picks by size.
     Both return the exact fp32 ranking.
+    ``parents`` (bf16 [mc, 32], optional): also filled with ``smote_parents(C, parents_affine)``
+    by the operand-prep launch that already reads C (one launch fewer on the SMOTE path).
     """
     for t, nm in ((Q, "Q"), (C, "C")):
         if t.dim() != 2 or t.shape[1] != NCOLS or t.dtype != torch.float32:
@@ -70,6 +86,8 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     if self_offset >= 0 and self_offset + mq > mc:
         raise ValueError("self_offset + mq exceeds the candidate set")
     if not Q.is_cuda:
+        if _check_parents(parents, C, parents_affine):
+            parents.copy_(smote_parents(C, parents_affine))
         idx, d2 = ref.knn_topk(Q.numpy(), C.numpy(), k, self_offset)
         idx_t = torch.from_numpy(idx)
         return (idx_t, torch.from_numpy(d2.astype(np.float32))) if want_dist else idx_t
@@ -83,8 +101,13 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     # GEMM-ready rows: the -0.5||c||^2 term rides in column 30 (see knn.hip knn_prep_kernel)
     Qp = torch.empty((mq_pad, NCOLS), device=Q.device, dtype=torch.float32)
     Cp = torch.empty((mc_pad, NCOLS), device=C.device, dtype=torch.float32)
-    m.knn_prep(ptr(Cc), mc, mc_pad, 0, ptr(Cp), s)
-    m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
+    pp = _check_parents(parents, Cc, parents_affine)
+    if Qc.data_ptr() == Cc.data_ptr() and mq == mc and mq_pad == mc_pad:
+        # SMOTE self-search: one launch reads the rows once and writes both operands (+ parents)
+        m.knn_prep(ptr(Cc), mc, mc_pad, 2, ptr(Cp), s, ptr(Qp), ptr(parents_affine), pp)
+    else:
+        m.knn_prep(ptr(Cc), mc, mc_pad, 0, ptr(Cp), s, 0, ptr(parents_affine), pp)
+        m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
     idx = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
     score = torch.empty((mq, k), device=Q.device, dtype=torch.float32) if want_dist else None
     if nsplit is not None:

@@ -43,6 +43,35 @@ def test_smote_parents_match_cpu(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("self_search", [True, False])
+def test_knn_prep_writes_parents(dev, self_search):
+    """knn_topk(parents=...) fills the parents from the operand-prep launch (role 2 when queries
+    are the candidates, role 0 otherwise): == smote_parents bit for bit, same neighbour lists."""
+    st, xmin = _minority(n=80_000, seed=12)
+    C = xmin.to(dev)
+    Q = C if self_search else C[: C.shape[0] // 2].clone()
+    aff = st.aff.to(dev)
+    base = K.knn_topk(Q, C, k=5, self_offset=0)
+    for a in (None, aff):
+        P = torch.empty((C.shape[0], 32), dtype=torch.bfloat16, device=dev)
+        nbr = K.knn_topk(Q, C, k=5, self_offset=0, parents=P, parents_affine=a)
+        assert torch.equal(nbr, base)
+        assert torch.equal(P, K.smote_parents(C, a))
+    with pytest.raises(ValueError):
+        K.knn_topk(Q, C, k=5, self_offset=0, parents=torch.empty((3, 32), dtype=torch.bfloat16, device=dev))
+
+
+def test_knn_topk_parents_cpu():
+    st, xmin = _minority(n=20_000, seed=13)
+    P = torch.empty((xmin.shape[0], 32), dtype=torch.bfloat16)
+    nbr = K.knn_topk(xmin, xmin, k=5, self_offset=0, parents=P, parents_affine=st.aff)
+    assert torch.equal(nbr, K.knn_topk(xmin, xmin, k=5, self_offset=0))
+    assert torch.equal(P, K.smote_parents(xmin, st.aff))
+    with pytest.raises(ValueError):
+        K.knn_topk(xmin, xmin, k=5, self_offset=0, parents_affine=st.aff)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["bf16", "fp8", "f32"])
 def test_smote_generate_bf16_parents(dev, kind):
     st, xmin = _minority(seed=9)
