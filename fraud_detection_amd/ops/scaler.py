@@ -298,9 +298,10 @@ class PendingCompaction:
     _next = 0
     _POOL = 8
 
-    def __init__(self, labels, target, nb, counts, total):
+    def __init__(self, labels, target, nb, counts, total, side: bool = False):
         cls = PendingCompaction
         self.labels, self.target, self.nb, self.counts = labels, target, nb, counts
+        self.side = side
         if not cls._pool:
             cls._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(cls._POOL)]
             cls._owners = [None] * cls._POOL
@@ -320,6 +321,8 @@ class PendingCompaction:
     def result(self) -> torch.Tensor:
         if self._out is None:
             self.event.synchronize()
+            if self.side:  # counts were written on the side stream
+                torch.cuda.current_stream(self.labels.device).wait_event(self.event)
             cnt = int(self.host[0])
             if PendingCompaction._owners[self._slot] is self:
                 PendingCompaction._owners[self._slot] = None
@@ -339,21 +342,36 @@ class _Ready:
         return self._out
 
 
-def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 512):
-    """Stable indices of rows whose label == target, as a pending result (see PendingCompaction)."""
+def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 512,
+                          side=None, ready=None):
+    """Stable indices of rows whose label == target, as a pending result (see PendingCompaction).
+
+    ``side`` (torch.cuda.Stream) runs the count/scan kernels and the count's copy to the host on
+    that stream, after ``ready`` (a torch.cuda.Event recorded on the current stream once the labels
+    are written): the caller can enqueue its big kernel on the current stream first and the count
+    runs beside it instead of in front of it (pipeline.fit: the fused scaler pass starts ~30 us
+    sooner at the fit boundary, profiles/r2_s6).  ``result()`` orders the current stream after the
+    side stream's kernels before it writes the index list."""
     if labels.dtype != torch.uint8 or labels.dim() != 1:
         raise ValueError("labels must be 1-D uint8")
     n = labels.shape[0]
     if not labels.is_cuda:
         return _Ready(torch.nonzero(labels == target, as_tuple=False).reshape(-1).to(torch.int64))
     m = native()
-    s = stream_of(labels)
     nb = int(max(1, min(nblocks, (n + 255) // 256)))
     counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
     total = torch.empty(1, device=labels.device, dtype=torch.int64)
-    m.compact_count(ptr(labels), n, target, ptr(counts), nb, s)
-    m.exclusive_scan_small(ptr(counts), nb, ptr(total), s)
-    return PendingCompaction(labels, target, nb, counts, total)
+    if side is None:
+        s = stream_of(labels)
+        m.compact_count(ptr(labels), n, target, ptr(counts), nb, s)
+        m.exclusive_scan_small(ptr(counts), nb, ptr(total), s)
+        return PendingCompaction(labels, target, nb, counts, total)
+    if ready is not None:
+        side.wait_event(ready)
+    with torch.cuda.stream(side):
+        m.compact_count(ptr(labels), n, target, ptr(counts), nb, side.cuda_stream)
+        m.exclusive_scan_small(ptr(counts), nb, ptr(total), side.cuda_stream)
+        return PendingCompaction(labels, target, nb, counts, total, side=True)
 
 
 def compact_indices(labels: torch.Tensor, target: int = 1, nblocks: int = 512) -> torch.Tensor:

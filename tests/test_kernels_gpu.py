@@ -372,6 +372,25 @@ def test_compact_indices_exact(dev, n, offset):
         assert torch.equal(got, ref_idx)
 
 
+@pytest.mark.parametrize("n", [17, 2_000_001])
+def test_compact_indices_side_stream(dev, n):
+    """Count/scan on a side stream behind a ready event, index write on the compute stream (the
+    pipeline's placement beside the fused scaler pass) == torch.nonzero, while the compute stream
+    is busy with a large kernel and the labels are written on the compute stream just before."""
+    g = torch.Generator().manual_seed(n)
+    src = (torch.rand(n, generator=g) < 0.3).to(torch.uint8).to(dev)
+    lab = torch.empty_like(src)
+    big = torch.randn(4096, 4096, device=dev)
+    side = torch.cuda.Stream(dev)
+    lab.copy_(src)  # labels produced on the compute stream
+    ready = torch.cuda.Event()
+    ready.record()
+    _ = big @ big  # compute stream keeps working
+    pend = S.compact_indices_async(lab, 1, side=side, ready=ready)
+    got = pend.result()
+    assert torch.equal(got, torch.nonzero(src == 1).reshape(-1))
+
+
 @pytest.mark.parametrize("n,rate", [(2_000_000, 0.002), (300_001, 0.3)])
 def test_auc_hist_matches_oracle_and_exact(dev, n, rate):
     g = torch.Generator().manual_seed(n)

@@ -21,6 +21,7 @@
 #   ksab         KernelSHAP: accuracy vs fp64 + us per batch on three models (tools/ks_check.py), and
 #                tools/kernelshap_bench.py with the paired and the unpaired kernel
 #   newtonab     bench 50 steps x 3 with the Newton flag copied (event) vs polled (mapped pinned word)
+#   sideab       bench 50 steps x 2: class counts on a side stream vs in front of the scaler pass
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -92,6 +93,11 @@ for st in "$@"; do
       for r in 1 2 3; do for F in copy map; do
         FDX_NEWTON_FLAG=$F step newton_${F}_$r 300 python bench.py --steps 50 --warmup 5 --no-extras
       done; done ;;
+    sideab)  # class-count kernels on a side stream beside the fused scaler pass vs in front of it
+      for i in 1 2; do
+        FDX_COUNT_SIDE=0 step "sideab_front_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras &&
+        FDX_COUNT_SIDE=1 step "sideab_side_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
+      done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
     *) echo "unknown stage $st"; exit 2 ;;
