@@ -301,7 +301,10 @@ class PendingCompaction:
     def __init__(self, labels, target, nb, counts, total, side: bool = False):
         cls = PendingCompaction
         self.labels, self.target, self.nb, self.counts = labels, target, nb, counts
-        self.side = side
+        # a side-stream count writes `total` concurrently with the compute stream: hold it until
+        # result() has waited for that stream, or the caching allocator hands its block to a
+        # compute-stream tensor while the scan may still write it
+        self.side, self.total = side, total
         if not cls._pool:
             cls._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(cls._POOL)]
             cls._owners = [None] * cls._POOL
@@ -326,6 +329,7 @@ class PendingCompaction:
             cnt = int(self.host[0])
             if PendingCompaction._owners[self._slot] is self:
                 PendingCompaction._owners[self._slot] = None
+            self.total = None
             out = torch.empty(cnt, device=self.labels.device, dtype=torch.int64)
             if cnt:
                 native().compact_write(ptr(self.labels), self.labels.shape[0], self.target, ptr(self.counts), ptr(out),

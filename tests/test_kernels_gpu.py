@@ -383,12 +383,16 @@ def test_compact_indices_side_stream(dev, n):
     big = torch.randn(4096, 4096, device=dev)
     side = torch.cuda.Stream(dev)
     lab.copy_(src)  # labels produced on the compute stream
+    _ = big @ big
     ready = torch.cuda.Event()
-    ready.record()
-    _ = big @ big  # compute stream keeps working
+    ready.record()  # the side stream's count waits behind the matmul ...
     pend = S.compact_indices_async(lab, 1, side=side, ready=ready)
+    # ... while the compute stream allocates and writes small int64 tensors that run concurrently
+    # with it: the side stream's scratch must stay owned by the pending result until result()
+    junk = [torch.full((1,), -7, dtype=torch.int64, device=dev) for _ in range(64)]
     got = pend.result()
     assert torch.equal(got, torch.nonzero(src == 1).reshape(-1))
+    del junk
 
 
 @pytest.mark.parametrize("n,rate", [(2_000_000, 0.002), (300_001, 0.3)])
