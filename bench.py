@@ -165,6 +165,13 @@ def main():
         out["collectives_timed_region"] = {k: v for k, v in coll.items()}
     out.update(extras)
     if rank == 0:
+        # every measured variant must reach BASELINE's AUC target: a number from a wrong model is
+        # not a measurement (stderr, so the one-line JSON contract is unchanged)
+        aucs = {"headline": out.get("auc")}
+        aucs.update({k: v.get("auc") for k, v in out.items() if isinstance(v, dict) and "auc" in v})
+        low = {k: v for k, v in aucs.items() if v is not None and v < 0.95}
+        if low:
+            print(f"[bench] WARNING: AUC below the 0.95 target: {low}", file=sys.stderr, flush=True)
         line = json.dumps(out)
         print(line, flush=True)
         if args.json_out:

@@ -219,7 +219,8 @@ class DevicePipeline:
             if os.environ.get("FDX_COUNT_SIDE", "1") == "1":
                 if self._side is None or self._side.device != dev:
                     self._side = torch.cuda.Stream(dev)
-                ready = torch.cuda.Event()
+                    self._ready = torch.cuda.Event()  # re-recorded every fit (a wait binds the latest record)
+                ready = self._ready
                 ready.record()
                 stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
                 pending = scaler_ops.compact_indices_async(y, 1, side=self._side, ready=ready)

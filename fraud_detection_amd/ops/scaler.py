@@ -363,19 +363,27 @@ def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 
         return _Ready(torch.nonzero(labels == target, as_tuple=False).reshape(-1).to(torch.int64))
     m = native()
     nb = int(max(1, min(nblocks, (n + 255) // 256)))
-    counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
-    total = torch.empty(1, device=labels.device, dtype=torch.int64)
     if side is None:
+        counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
+        total = torch.empty(1, device=labels.device, dtype=torch.int64)
         s = stream_of(labels)
         m.compact_count(ptr(labels), n, target, ptr(counts), nb, s)
         m.exclusive_scan_small(ptr(counts), nb, ptr(total), s)
         return PendingCompaction(labels, target, nb, counts, total)
+    compute = torch.cuda.current_stream(labels.device)
     if ready is not None:
         side.wait_event(ready)
     with torch.cuda.stream(side):
+        # scratch from the SIDE stream's pool: a block from the compute stream's pool may have
+        # been freed by a tensor whose compute-stream kernels are still queued (e.g. the scaler
+        # pass's partial sums), which is safe only for compute-stream reuse
+        counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
+        total = torch.empty(1, device=labels.device, dtype=torch.int64)
         m.compact_count(ptr(labels), n, target, ptr(counts), nb, side.cuda_stream)
         m.exclusive_scan_small(ptr(counts), nb, ptr(total), side.cuda_stream)
-        return PendingCompaction(labels, target, nb, counts, total, side=True)
+        pend = PendingCompaction(labels, target, nb, counts, total, side=True)
+    counts.record_stream(compute)  # result() launches the index write on the compute stream
+    return pend
 
 
 def compact_indices(labels: torch.Tensor, target: int = 1, nblocks: int = 512) -> torch.Tensor:

@@ -59,3 +59,27 @@ def test_fp8_fused_fit_matches_bf16(dev):
     assert abs(out["fp8"][1] - out["fp8_unfused"][1]) < 1e-3
     w8, wb = out["fp8"][0].w[:31], out["bf16"][0].w[:31]
     assert np.linalg.norm(w8 - wb) / np.linalg.norm(wb) < 0.05
+
+
+@pytest.mark.gpu
+def test_back_to_back_fits_are_identical(dev):
+    """The bench pattern: one pipeline fitting again and again with nothing synchronising the
+    host between fits, bf16 and fp8 interleaved on the same data.  Every repeat must give the
+    bit-identical model and the same minority / SMOTE counts: a cross-stream reuse of scratch
+    (the class counts run on a side stream beside the fused scaler pass) shows up here as a
+    changed count or weight vector."""
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+    X, y = separable(3_000_000, seed=8, device=dev)
+    pipes = {s: DevicePipeline(TrainConfig(seed=42, storage=s)) for s in ("bf16", "fp8")}
+    runs = [(s, p.fit(X, y)) for _ in range(4) for s, p in pipes.items()]  # results read afterwards
+    torch.cuda.synchronize()
+    first = {}
+    for s, r in runs:
+        key = (r.n_minority, r.n_synthetic, r.n_train_rows, tuple(np.asarray(r.w[:31]).tolist()))
+        if s not in first:
+            first[s] = key
+            assert r.fit.converged
+        else:
+            assert key == first[s], s
+    assert first["bf16"][0] == first["fp8"][0] == int((y == 1).sum())

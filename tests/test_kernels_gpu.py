@@ -375,20 +375,25 @@ def test_compact_indices_exact(dev, n, offset):
 @pytest.mark.parametrize("n", [17, 2_000_001])
 def test_compact_indices_side_stream(dev, n):
     """Count/scan on a side stream behind a ready event, index write on the compute stream (the
-    pipeline's placement beside the fused scaler pass) == torch.nonzero, while the compute stream
-    is busy with a large kernel and the labels are written on the compute stream just before."""
+    pipeline's placement beside the fused scaler pass) == torch.nonzero.  The compute stream frees
+    scratch of the count's size classes while kernels that still write it are queued (as the
+    scaler pass's partial sums are): the side stream must not be handed those blocks."""
     g = torch.Generator().manual_seed(n)
     src = (torch.rand(n, generator=g) < 0.3).to(torch.uint8).to(dev)
     lab = torch.empty_like(src)
     big = torch.randn(4096, 4096, device=dev)
     side = torch.cuda.Stream(dev)
     lab.copy_(src)  # labels produced on the compute stream
-    _ = big @ big
     ready = torch.cuda.Event()
-    ready.record()  # the side stream's count waits behind the matmul ...
+    ready.record()  # the side stream need not wait for what follows
+    nb = max(1, min(512, (n + 255) // 256))
+    tmp_counts = torch.empty(nb, dtype=torch.int64, device=dev)
+    tmp_total = torch.empty(1, dtype=torch.int64, device=dev)
+    _ = big @ big
+    tmp_counts.fill_(-7)  # queued behind the matmul
+    tmp_total.fill_(-7)
+    del tmp_counts, tmp_total  # freed to the compute stream's pool with writes still queued
     pend = S.compact_indices_async(lab, 1, side=side, ready=ready)
-    # ... while the compute stream allocates and writes small int64 tensors that run concurrently
-    # with it: the side stream's scratch must stay owned by the pending result until result()
     junk = [torch.full((1,), -7, dtype=torch.int64, device=dev) for _ in range(64)]
     got = pend.result()
     assert torch.equal(got, torch.nonzero(src == 1).reshape(-1))
