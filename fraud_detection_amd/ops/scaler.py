@@ -1,6 +1,7 @@
 """K1 scaler statistics / K2 standardize+pad+cast / stable label compaction."""
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -150,6 +151,21 @@ def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) ->
     return scaler_finalize(sums, float(n), pivot, d)
 
 
+_GRID_CACHE: dict = {}
+
+
+def _stats_cast_grid(m, dev) -> int:
+    r = int(os.environ.get("FDX_SCALER_RESERVE", "0"))
+    key = (dev.index, r)
+    if key not in _GRID_CACHE:
+        cap = int(m.scaler_stats_cast_blocks())
+        if r > 0:
+            cus = torch.cuda.get_device_properties(dev).multi_processor_count
+            cap = max(cus, cap - r * cus)
+        _GRID_CACHE[key] = cap
+    return _GRID_CACHE[key]
+
+
 def fused_cast_ok(X: torch.Tensor) -> bool:
     """The fused K1+K2 kernel reads contiguous 16-byte aligned [n, d <= 30] fp32 rows."""
     return (not X.is_cuda) or (X.is_contiguous() and X.data_ptr() % 16 == 0 and X.shape[1] <= 30)
@@ -236,8 +252,9 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
             raise ValueError("scaler_fit_cast: X must be contiguous and 16-byte aligned with d <= 30")
         m = native()
         piv = _pivot_dev(pivot, d, X.device)
-        # all blocks resident at once (occupancy-derived), never more than the tiles
-        nb = max(1, min(m.scaler_stats_cast_blocks(), (n + 127) // 128))
+        # all blocks resident at once (occupancy-derived), never more than the tiles;
+        # FDX_SCALER_RESERVE=r leaves r block slots per CU free for kernels running beside the pass
+        nb = max(1, min(_stats_cast_grid(m, X.device), (n + 127) // 128))
         partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
         sums = torch.empty(64, device=X.device, dtype=torch.float64)
         s = stream_of(X)

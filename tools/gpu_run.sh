@@ -22,6 +22,7 @@
 #                tools/kernelshap_bench.py with the paired and the unpaired kernel
 #   newtonab     bench 50 steps x 3 with the Newton flag copied (event) vs polled (mapped pinned word)
 #   sideab       bench 50 steps x 2: class counts on a side stream vs in front of the scaler pass
+#   reserveab    bench 50 steps x 2 with 0/1/2 scaler block slots per CU reserved
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -97,6 +98,12 @@ for st in "$@"; do
       for i in 1 2; do
         FDX_COUNT_SIDE=0 step "sideab_front_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras &&
         FDX_COUNT_SIDE=1 step "sideab_side_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
+      done ;;
+    reserveab)  # fused scaler pass grid: 0 / 1 / 2 block slots per CU left free for the side-stream count
+      for i in 1 2; do
+        for r in 0 1 2; do
+          FDX_SCALER_RESERVE=$r step "reserve${r}_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
+        done
       done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
