@@ -52,8 +52,16 @@ def available() -> bool:
     return _mod is not None
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_of(t: torch.Tensor) -> int:
-    """hipStream_t (as int) of torch's current stream on t's device."""
+    """hipStream_t (as int) of torch's current stream on t's device.  The raw-handle query skips
+    building a torch Stream object (a few us of host time per launch on the fit's critical path,
+    profiles/r2_s6/host_profile_*.txt)."""
+    idx = t.device.index
+    if _raw_stream is not None and idx is not None:
+        return int(_raw_stream(idx))
     return torch.cuda.current_stream(t.device).cuda_stream
 
 

@@ -535,3 +535,16 @@ def test_sgd_fused_scaler_matches_unfused(dev):
     r_u = DevicePipeline(TrainConfig(solver="sgd", seed=42, fold_scaler=False)).fit(X, y)
     assert np.allclose(r_f.fit.w[:31], r_u.fit.w[:31], rtol=0, atol=5e-3)
     assert abs(evaluate(r_f, Xt, yt)["auc"] - evaluate(r_u, Xt, yt)["auc"]) < 1e-3
+
+
+def test_stream_of_follows_current_stream(dev):
+    """ops.native.stream_of (raw handle query) == torch's current stream, inside and outside a
+    stream context: every launcher enqueues where torch would."""
+    from fraud_detection_amd.ops.native import stream_of
+
+    t = torch.empty(1, device=dev)
+    assert stream_of(t) == torch.cuda.current_stream(dev).cuda_stream
+    side = torch.cuda.Stream(dev)
+    with torch.cuda.stream(side):
+        assert stream_of(t) == side.cuda_stream
+    assert stream_of(t) == torch.cuda.current_stream(dev).cuda_stream
