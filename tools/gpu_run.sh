@@ -23,6 +23,7 @@
 #   newtonab     bench 50 steps x 3 with the Newton flag copied (event) vs polled (mapped pinned word)
 #   sideab       bench 50 steps x 2: class counts on a side stream vs in front of the scaler pass
 #   reserveab    bench 50 steps x 2 with 0/1/2 scaler block slots per CU reserved
+#   lookab       bench 50 steps x 4: Newton flag lookahead 1 vs 2
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -103,6 +104,12 @@ for st in "$@"; do
       for i in 1 2; do
         for r in 0 1 2; do
           FDX_SCALER_RESERVE=$r step "reserve${r}_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
+        done
+      done ;;
+    lookab)  # Newton convergence-flag lookahead 1 vs 2 (single GPU), 50-step benches interleaved x4
+      for i in 1 2 3 4; do
+        for la in 1 2; do
+          FDX_NEWTON_LOOKAHEAD=$la step "look${la}_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
         done
       done ;;
     py:*) # shellcheck disable=SC2086
