@@ -24,6 +24,18 @@ inline bool nt_stores() {
   return on;
 }
 
+// The fused scaler pass's row stream: plain stores by default.  Measured on the current kernel
+// (profiles/r2_s6/nt_stores_ab.txt): 269 us plain vs 280 us nontemporal, while the SMOTE output
+// keeps the nontemporal policy (122 vs 127 us).  FDX_NT_SCALER=1 restores nontemporal stores here;
+// FDX_NT_STORES=0 turns them off everywhere.
+inline bool nt_stores_scaler() {
+  static const bool on = [] {
+    const char* e = std::getenv("FDX_NT_SCALER");
+    return nt_stores() && e != nullptr && e[0] == '1';
+  }();
+  return on;
+}
+
 inline bool sync_launch_mode() {
   static const int mode = [] {
     const char* v = std::getenv("FDX_SYNC_LAUNCH");

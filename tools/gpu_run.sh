@@ -24,6 +24,8 @@
 #   sideab       bench 50 steps x 2: class counts on a side stream vs in front of the scaler pass
 #   reserveab    bench 50 steps x 2 with 0/1/2 scaler block slots per CU reserved
 #   lookab       bench 50 steps x 4: Newton flag lookahead 1 vs 2
+#   ntab         kernel stats with nontemporal row stores on vs off
+#   ntscab       bench 50 steps x 3: scaler row stores plain vs nontemporal
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -111,6 +113,16 @@ for st in "$@"; do
         for la in 1 2; do
           FDX_NEWTON_LOOKAHEAD=$la step "look${la}_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
         done
+      done ;;
+    ntab)  # kernel stats with nontemporal row-stream stores on vs off (scaler pass + SMOTE output)
+      cd /tmp && export TMPDIR=/tmp
+      FDX_NT_STORES=1 step ntab_on 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nt_on" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-extras &&
+      FDX_NT_STORES=0 step ntab_off 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/nt_off" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-extras || exit 1
+      cd "$R" ;;
+    ntscab)  # fused scaler pass row stores: plain (default) vs nontemporal, 50-step benches interleaved x3
+      for i in 1 2 3; do
+        FDX_NT_SCALER=0 step "ntsc0_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras &&
+        FDX_NT_SCALER=1 step "ntsc1_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
       done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
