@@ -40,8 +40,8 @@ BASELINE_CPU_KERNELSHAP_PER_S = 4671.3
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rows-per-gpu", type=int, default=10_000_000)
     ap.add_argument("--solver", default="newton", choices=["newton", "sgd"])
     ap.add_argument("--storage", default="bf16", choices=["bf16", "fp8"])
