@@ -29,7 +29,7 @@ constexpr int kThreads = 256;
 // OUT: 0 = bf16 rows (64 B), 1 = fp32 (GBDT input), 2 = fp8 e4m3 (32 B).
 // PB: parents are bf16 rows already in output space (smote_parents_kernel: the affine map applied
 // once per parent instead of once per sample; half the gather bytes); else fp32 rows (+ aff).
-template <int OUT, bool NT = false, bool PB = false>
+template <int OUT, bool NT = false, bool PB = false, bool G2 = false>
 __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
     const void* __restrict__ Cv, const int* __restrict__ nbr, int mq, int k, int64_t q_offset,
     int64_t n_new, int64_t s_off, uint32_t key0, uint32_t key1, uint32_t cb0, uint32_t cb1, float label,
@@ -77,6 +77,54 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
   for (; base < n_new; base += step) {
     int nx_i[2] = {0, 0}, nx_j[2] = {0, 0};
     float nx_lam[2] = {0.0f, 0.0f};
+    if constexpr (G2 && PB && OUT == 0) {
+      // both halves' parent gathers issued up front (16 loads in flight per lane, kept packed:
+      // 64 VGPRs), then the next draws, then interpolate + store: one exposed gather latency per
+      // iteration instead of two.  Same arithmetic as below: bit-identical rows.
+      uint4 pi[2][4], pj[2][4];
+      float lam[2][4];
+  #pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+  #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int src = 16 * u + rr;
+          const int i = __shfl(my_i[hh], src, kWave);
+          const int jn = __shfl(my_j[hh], src, kWave);
+          lam[hh][u] = __shfl(my_lam[hh], src, kWave);
+          pi[hh][u] = Cb[(q_offset + i) * 4 + q];
+          pj[hh][u] = Cb[(int64_t)jn * 4 + q];
+        }
+      }
+      if (base + step < n_new) draw2(base + step, nx_i, nx_j, nx_lam);
+  #pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+  #pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int64_t s = base + 64 * hh + 16 * u + rr;
+          if (s >= n_new) continue;
+          const float l = lam[hh][u];
+          const uint4 a = pi[hh][u], b = pj[hh][u];
+          const float av[8] = {bf16lo(a.x), bf16hi(a.x), bf16lo(a.y), bf16hi(a.y),
+                               bf16lo(a.z), bf16hi(a.z), bf16lo(a.w), bf16hi(a.w)};
+          const float bv[8] = {bf16lo(b.x), bf16hi(b.x), bf16lo(b.y), bf16hi(b.y),
+                               bf16lo(b.z), bf16hi(b.z), bf16lo(b.w), bf16hi(b.w)};
+          float o[8];
+  #pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = fmaf(l, bv[j] - av[j], av[j]);
+          if (q == 3) {
+            o[6] = 1.0f;   // col 30: intercept column
+            o[7] = label;  // col 31: label
+          }
+          uint4 pk;
+          pk.x = pack_bf16x2(o[0], o[1]);
+          pk.y = pack_bf16x2(o[2], o[3]);
+          pk.z = pack_bf16x2(o[4], o[5]);
+          pk.w = pack_bf16x2(o[6], o[7]);
+          if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(out) + s * 4 + q);
+          else reinterpret_cast<uint4*>(out)[s * 4 + q] = pk;
+        }
+      }
+    } else {
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int64_t hbase = base + 64 * hh;
@@ -147,6 +195,7 @@ __global__ __launch_bounds__(kThreads) void smote_generate_kernel(
         }
       }
     }
+    }  // G2 else
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       my_i[hh] = nx_i[hh];
@@ -187,14 +236,20 @@ void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int 
   const int64_t per_block = (kThreads / kWave) * 128;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
-#define FDX_SG(O, NT, PB)                                                                             \
+#define FDX_SG(O, NT, PB, ...)                                                                        \
   do {                                                                                                \
-    static const int cap = resident_cap(smote_generate_kernel<O, NT, PB>, kThreads);                  \
-    smote_generate_kernel<O, NT, PB><<<capped_grid(n_new, per_block, cap), kThreads, 0, stream>>>(    \
+    static const int cap = resident_cap(smote_generate_kernel<O, NT, PB, ##__VA_ARGS__>, kThreads);   \
+    smote_generate_kernel<O, NT, PB, ##__VA_ARGS__><<<capped_grid(n_new, per_block, cap), kThreads, 0, \
+                                                      stream>>>(                                      \
         C, nbr, mq, k, q_offset, n_new, sample_offset, k0, k1, c0, c1, label, out_scale, aff, out);   \
   } while (0)
   const bool pb = parents_bf16 != 0;
-  if (out_kind == 0 && nt_stores()) { if (pb) FDX_SG(0, true, true); else FDX_SG(0, true, false); }
+  static const bool g2 = [] {  // A/B: FDX_SMOTE_G2=1 issues both halves' gathers up front
+    const char* e = std::getenv("FDX_SMOTE_G2");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (out_kind == 0 && nt_stores() && pb && g2) FDX_SG(0, true, true, true);
+  else if (out_kind == 0 && nt_stores()) { if (pb) FDX_SG(0, true, true); else FDX_SG(0, true, false); }
   else if (out_kind == 0) { if (pb) FDX_SG(0, false, true); else FDX_SG(0, false, false); }
   else if (out_kind == 1) { if (pb) FDX_SG(1, false, true); else FDX_SG(1, false, false); }
   else { if (pb) FDX_SG(2, false, true); else FDX_SG(2, false, false); }

@@ -26,6 +26,7 @@
 #   lookab       bench 50 steps x 4: Newton flag lookahead 1 vs 2
 #   ntab         kernel stats with nontemporal row stores on vs off
 #   ntscab       bench 50 steps x 3: scaler row stores plain vs nontemporal
+#   smoteab      SMOTE up-front gathers (FDX_SMOTE_G2) A/B: exactness tests, kernel stats, bench
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -123,6 +124,16 @@ for st in "$@"; do
       for i in 1 2 3; do
         FDX_NT_SCALER=0 step "ntsc0_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras &&
         FDX_NT_SCALER=1 step "ntsc1_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
+      done ;;
+    smoteab)  # SMOTE: both halves' gathers up front (FDX_SMOTE_G2=1) vs per half; exactness tests under G2, kernel stats, bench x2
+      FDX_SMOTE_G2=1 step smoteab_tests 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "smote or pipeline or back_to_back" &&
+      cd /tmp && export TMPDIR=/tmp &&
+      FDX_SMOTE_G2=0 step smoteab_prof0 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/g2_0" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-extras &&
+      FDX_SMOTE_G2=1 step smoteab_prof1 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/g2_1" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-extras &&
+      cd "$R" || exit 1
+      for i in 1 2; do
+        FDX_SMOTE_G2=0 step "g2off_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras &&
+        FDX_SMOTE_G2=1 step "g2on_$i" 300 python bench.py --steps 50 --warmup 5 --no-extras || exit 1
       done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
