@@ -56,28 +56,83 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _self_launch(args) -> int:
+    """``python bench.py --gpus N`` with no torchrun around it: start N ranks (one process per
+    GPU, RCCL over xGMI) as CHILD processes via torch.distributed.run and exit with their status.
+    Nothing in this parent touches the GPU (no torch.cuda call before the children exist), and the
+    parent is never replaced by exec -- it waits for the launcher and forwards its exit code (the
+    launcher tears every rank down when one fails)."""
+    import subprocess
+
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC: RCCL peer buffers on this driver
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] self-launch: {args.gpus} ranks via torch.distributed.run", file=sys.stderr, flush=True)
+    rc = subprocess.call(cmd, env=env)
+    return 0 if rc == 0 else (rc if rc > 0 else 1)
+
+
+def _cpu_mode() -> bool:
+    """FDX_BENCH_DEVICE=cpu: the same code path on CPU tensors over gloo -- the CPU test of the
+    launch / rank / JSON contract (never a performance number)."""
+    return os.environ.get("FDX_BENCH_DEVICE", "cuda") == "cpu"
+
+
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        return _self_launch(args)
+    world_env = int(world_env or "1")
+    if world_env != args.gpus:
+        print(f"[bench] FATAL: --gpus {args.gpus} but WORLD_SIZE={world_env}: the launcher and the "
+              "requested GPU count disagree", file=sys.stderr, flush=True)
+        return 2
+
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
     from fraud_detection_amd.parallel.comm import Communicator
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if not torch.cuda.is_available():
-        print("bench.py requires a ROCm GPU", file=sys.stderr)
-        return 2
-    # Rehearsal knobs for a one-GPU box (never used by the driver's runs): FDX_BENCH_ONE_GPU=1 puts
-    # every rank on cuda:0, FDX_BENCH_BACKEND=gloo swaps RCCL for host-staged gloo collectives.
-    if os.environ.get("FDX_BENCH_ONE_GPU") == "1":
-        local_rank = 0
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
-    comm = Communicator(backend=os.environ.get("FDX_BENCH_BACKEND") or None, device=dev) if world_env > 1 else None
+    if _cpu_mode():
+        dev = torch.device("cpu")
+        comm = Communicator(backend="gloo") if world_env > 1 else None
+        args.no_extras = True
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py requires a ROCm GPU (FDX_BENCH_DEVICE=cpu for the CPU contract test)", file=sys.stderr)
+            return 2
+        # Rehearsal knobs for a one-GPU box (never used by the driver's runs): FDX_BENCH_ONE_GPU=1
+        # puts every rank on cuda:0, FDX_BENCH_BACKEND=gloo swaps RCCL for host-staged gloo.
+        if os.environ.get("FDX_BENCH_ONE_GPU") == "1":
+            local_rank = 0
+        elif local_rank >= torch.cuda.device_count():
+            print(f"[bench] FATAL: LOCAL_RANK {local_rank} but only {torch.cuda.device_count()} GPUs visible",
+                  file=sys.stderr, flush=True)
+            return 2
+        torch.cuda.set_device(local_rank)
+        dev = torch.device("cuda", local_rank)
+        comm = Communicator(backend=os.environ.get("FDX_BENCH_BACKEND") or None, device=dev) if world_env > 1 else None
     rank = comm.rank if comm else 0
     world = comm.world_size if comm else 1
-    if args.gpus != world and rank == 0:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        raise SystemExit(f"[bench] FATAL: communicator world {world} != --gpus {args.gpus}")
 
     n_total = args.rows_per_gpu
     n_test = n_total // 5
@@ -99,11 +154,13 @@ def main():
         res = step()
     if comm:
         comm.barrier()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
+    if comm:
+        comm.stats.reset()  # the per-collective breakdown covers the timed steps only
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
-    torch.cuda.synchronize(dev)
+    _sync(dev)
     if comm:
         comm.barrier()
     elapsed = time.perf_counter() - t0

@@ -4,7 +4,11 @@
     models/scaler.joblib           sklearn.preprocessing.StandardScaler   (real object)
     models/columns.joblib          list[str] feature order
     models/feature_names.json      same list as JSON
-    models/xgb_model.joblib        (GBDT family, when trained)
+    models/xgb_model.joblib        GBDT family (when trained): a models.gbdt.GBDTClassifier --
+                                   predict / predict_proba on SCALED rows, like the reference's
+                                   XGBClassifier dump (train_model.py:113); loading it needs this
+                                   package importable, as the reference's needs xgboost
+    models/xgb_model.json          the same trees as fdx-gbdt/1 JSON: what serving loads (no pickle)
 
 The GPU-fitted parameters are written into genuine sklearn 1.7 estimator objects, so any tool
 that loads the reference's artifacts (api/app.py, predict_single.py, evaluate_model.py, MLflow's

@@ -5,8 +5,13 @@
   scale_pos_weight, base_score) over numpy arrays or torch tensors; device kernels on a GPU
   tensor, the numpy oracle on CPU.  Models serialise to JSON (no pickle).
 * ``GBDTPipeline`` -- the reference's per-fold recipe on device: StandardScaler fit on the
-  fold's rows -> SMOTE (MFMA k-NN + Philox interpolation, fp32 rows) -> boosting with
-  scale_pos_weight = neg/pos measured before SMOTE (train_model.py:52-54) -> exact AUC.
+  fold's rows -> SMOTE (MFMA k-NN + Philox interpolation, fp32 rows) -> boosting -> exact AUC.
+  ``scale_pos_weight="auto"`` (default) is neg/pos of the rows the trees are fit on, i.e. AFTER
+  SMOTE (= 1 at sampling_ratio 1): the reference computes neg/pos BEFORE SMOTE
+  (train_model.py:52-54) and applies it to the SMOTE-balanced rows (:77), compensating the class
+  imbalance twice (AUC 0.9467 < 0.95 on the bench data, profiles/r2_s4b).
+  ``scale_pos_weight="reference"`` reproduces that pre-SMOTE value on purpose; a number is used
+  as given.
 """
 from __future__ import annotations
 
@@ -26,6 +31,8 @@ from ..ops.layout import NCOLS
 from .pipeline import TrainConfig, global_smote_slices
 
 MODEL_FILE = "xgb_model.json"
+JOBLIB_FILE = "xgb_model.joblib"  # the reference's artifact name (train_model.py:113)
+_PARAM_FIELDS = frozenset(gb.GBDTParams.__dataclass_fields__)
 
 
 def _as_tensor(X, device=None, dtype=torch.float32) -> torch.Tensor:
@@ -58,6 +65,17 @@ class GBDTClassifier:
 
     def get_params(self, deep: bool = True) -> dict:
         return dict(self.params.__dict__)
+
+    def __getstate__(self):  # joblib/pickle: plain values and host arrays only (no device tensors)
+        st = dict(self.__dict__)
+        st["_dens"] = None
+        st["params"] = dict(self.params.__dict__)
+        return st
+
+    def __setstate__(self, st):
+        st = dict(st)
+        st["params"] = gb.GBDTParams(**{k: v for k, v in st["params"].items() if k in _PARAM_FIELDS})
+        self.__dict__.update(st)
 
     def fit(self, X, y, comm=None):
         dev = self._dev(X)
@@ -105,7 +123,7 @@ class GBDTClassifier:
         with open(path) as f:
             o = json.load(f)
         ens = gb.TreeEnsemble.from_dict(o)
-        m = cls(device=device, **{k: v for k, v in ens.params.items() if k in gb.GBDTParams.__dataclass_fields__})
+        m = cls(device=device, **{k: v for k, v in ens.params.items() if k in _PARAM_FIELDS})
         m.ensemble = ens
         m.feature_names_in_ = o.get("feature_names")
         return m
@@ -150,7 +168,8 @@ class GBDTResult:
 
         os.makedirs(model_dir, exist_ok=True)
         mean, var, scale = self.scaler.numpy()
-        paths = {"model": os.path.join(model_dir, MODEL_FILE), "scaler": os.path.join(model_dir, "scaler.joblib"),
+        paths = {"model": os.path.join(model_dir, MODEL_FILE), "joblib": os.path.join(model_dir, JOBLIB_FILE),
+                 "scaler": os.path.join(model_dir, "scaler.joblib"),
                  "columns": os.path.join(model_dir, "columns.joblib"),
                  "feature_names": os.path.join(model_dir, "feature_names.json")}
         o = self.ensemble.to_dict()
@@ -158,6 +177,10 @@ class GBDTResult:
         o["scale_pos_weight"] = self.scale_pos_weight
         with open(paths["model"], "w") as f:
             json.dump(o, f)
+        clf = GBDTClassifier(**{k: v for k, v in self.ensemble.params.items() if k in _PARAM_FIELDS})
+        clf.params.scale_pos_weight = float(self.scale_pos_weight)
+        clf.ensemble, clf.feature_names_in_ = self.ensemble, list(feature_names)
+        joblib.dump(clf, paths["joblib"])
         joblib.dump(make_scaler(mean, var, scale, int(self.scaler.n), feature_names), paths["scaler"])
         joblib.dump(list(feature_names), paths["columns"])
         with open(paths["feature_names"], "w") as f:
@@ -167,7 +190,7 @@ class GBDTResult:
         if os.path.exists(prov):
             with open(prov) as f:
                 meta = json.load(f)
-        meta.update(writer=MARKER, gbdt_model=MODEL_FILE)
+        meta.update(writer=MARKER, gbdt_model=MODEL_FILE, gbdt_joblib=JOBLIB_FILE)
         meta.setdefault("model", meta.get("model", "logistic_model.joblib"))
         with open(prov, "w") as f:
             json.dump(meta, f)
@@ -203,14 +226,6 @@ class GBDTPipeline:
         stats = scaler_ops.scaler_fit(X, comm=comm)
         idx_min = scaler_ops.compact_indices(y, 1)
         n_min = int(idx_min.shape[0])
-        n_maj = n - n_min
-        if self.spw == "auto":
-            neg, pos = float(n_maj), float(n_min)
-            if comm:
-                neg, pos = comm.all_reduce_scalar(neg), comm.all_reduce_scalar(pos)
-            spw = neg / pos if pos > 0 else 1.0
-        else:
-            spw = float(self.spw)
         def quota(n_r, nmin_r):
             return max(0, int(round((n_r - nmin_r) * cfg.sampling_ratio)) - nmin_r) if (cfg.smote and nmin_r > 0) else 0
 
@@ -222,6 +237,14 @@ class GBDTPipeline:
         else:
             per, s_off = [quota(n, n_min)], 0
         n_new = per[rank]
+        neg = float(sum(r[1] - r[0] for r in ranks))
+        pos = float(sum(r[0] for r in ranks))
+        if self.spw == "auto":  # the fitted rows' balance (post-SMOTE)
+            spw = neg / (pos + sum(per)) if pos + sum(per) > 0 else 1.0
+        elif self.spw == "reference":  # train_model.py:52-54 (pre-SMOTE, App. D #11)
+            spw = neg / pos if pos > 0 else 1.0
+        else:
+            spw = float(self.spw)
         rows = torch.empty((n + n_new, NCOLS), dtype=torch.float32, device=X.device)
         scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", out=rows[:n])
         if sum(per) > 0:

@@ -261,9 +261,13 @@ class DevicePipeline:
             new_per_rank, s_off = [quota(r[1], r[0]) for r in ranks], 0
         n_new = new_per_rank[rank]
         n_sched = min(r[1] + q for r, q in zip(ranks, new_per_rank))
+        if n + n_new > rows_cap.shape[0]:  # global_smote_slices guarantees this never fires
+            raise RuntimeError(f"SMOTE slice of {n_new} rows exceeds the training buffer ({rows_cap.shape[0]} rows)")
         rows = rows_cap[: n + n_new]
         tm.mark("scale_cast")
-        if sum(new_per_rank) > 0:
+        # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a
+        # quota; shard scope has no collective in this block, so only a rank with its own quota enters
+        if (sum(new_per_rank) > 0) if glob else (n_new > 0):
             # ---- minority rows in fp32, gathered across ranks (C3) -----------------------
             xmin = get_xmin()
             if glob:
@@ -398,16 +402,19 @@ def _maybe_fault(rank: int):
 def global_smote_slices(ranks, quota, rank: int):
     """(rows per rank, this rank's 128-aligned sample offset) for global-scope DP SMOTE: the
     global quota (one-process formula on the summed counts) is cut at 128-aligned boundaries
-    near each rank's proportional share, so every rank's slice starts on a Philox pair block."""
+    near each rank's share IN PROPORTION TO ITS RAW ROWS, so every rank's slice starts on a Philox
+    pair block and fits the training buffer the rank sized before the exchange
+    (n_r + ceil(n_r * ratio) + 128: the share is <= n_r * ratio and rounding moves a slice by < 128
+    rows) -- also on a rank that holds no minority rows -- and post-SMOTE rows stay balanced."""
     n_g = sum(r[1] for r in ranks)
     nmin_g = sum(r[0] for r in ranks)
     total = quota(n_g, nmin_g)
-    shares = [quota(r[1], r[0]) for r in ranks]
     bounds = [0]
     acc = 0
-    for s in shares[:-1]:
-        acc += s
-        bounds.append(min(total, max(bounds[-1], 128 * int(round(acc / 128.0)))))
+    for r in ranks[:-1]:
+        acc += r[1]
+        cum = total * acc // max(n_g, 1)
+        bounds.append(min(total, max(bounds[-1], 128 * ((cum + 64) // 128))))
     bounds.append(total)
     per = [bounds[i + 1] - bounds[i] for i in range(len(ranks))]
     return per, bounds[rank]

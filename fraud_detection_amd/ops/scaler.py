@@ -315,9 +315,13 @@ class PendingCompaction:
     _next = 0
     _POOL = 8
 
-    def __init__(self, labels, target, nb, counts, total, side: bool = False):
+    def __init__(self, labels, target, nb, counts, total, side: bool = False, home=None):
         cls = PendingCompaction
         self.labels, self.target, self.nb, self.counts = labels, target, nb, counts
+        # the stream the index list belongs to (its consumers run there): result() enqueues the
+        # write there whichever stream is current when it is called -- e.g. when a later
+        # compaction settles this one from inside its side-stream context
+        self.home = home if home is not None else torch.cuda.current_stream(labels.device)
         # a side-stream count writes `total` concurrently with the compute stream: hold it until
         # result() has waited for that stream, or the caching allocator hands its block to a
         # compute-stream tensor while the scan may still write it
@@ -341,17 +345,18 @@ class PendingCompaction:
     def result(self) -> torch.Tensor:
         if self._out is None:
             self.event.synchronize()
-            if self.side:  # counts were written on the side stream
-                torch.cuda.current_stream(self.labels.device).wait_event(self.event)
-            cnt = int(self.host[0])
-            if PendingCompaction._owners[self._slot] is self:
-                PendingCompaction._owners[self._slot] = None
-            self.total = None
-            out = torch.empty(cnt, device=self.labels.device, dtype=torch.int64)
-            if cnt:
-                native().compact_write(ptr(self.labels), self.labels.shape[0], self.target, ptr(self.counts), ptr(out),
-                                       self.nb, stream_of(self.labels))
-            self._out = out
+            with torch.cuda.stream(self.home):
+                if self.side:  # counts were written on the side stream
+                    self.home.wait_event(self.event)
+                cnt = int(self.host[0])
+                if PendingCompaction._owners[self._slot] is self:
+                    PendingCompaction._owners[self._slot] = None
+                self.total = None
+                out = torch.empty(cnt, device=self.labels.device, dtype=torch.int64)
+                if cnt:
+                    native().compact_write(ptr(self.labels), self.labels.shape[0], self.target, ptr(self.counts),
+                                           ptr(out), self.nb, self.home.cuda_stream)
+                self._out = out
         return self._out
 
 
@@ -398,7 +403,7 @@ def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 
         total = torch.empty(1, device=labels.device, dtype=torch.int64)
         m.compact_count(ptr(labels), n, target, ptr(counts), nb, side.cuda_stream)
         m.exclusive_scan_small(ptr(counts), nb, ptr(total), side.cuda_stream)
-        pend = PendingCompaction(labels, target, nb, counts, total, side=True)
+        pend = PendingCompaction(labels, target, nb, counts, total, side=True, home=compute)
     counts.record_stream(compute)  # result() launches the index write on the compute stream
     return pend
 

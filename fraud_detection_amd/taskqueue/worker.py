@@ -162,29 +162,38 @@ def _spawn_per_gpu(n: int, argv: list[str]) -> int:
     """One worker process per GPU (the service-level data parallelism of the XAI path, BASELINE
     config 4): child i sees only GPU i (HIP_VISIBLE_DEVICES, set before it touches HIP) and leases
     its own disjoint batches from the shared queue.  The parent never initialises the GPU; it
-    forwards SIGTERM/SIGINT and exits with the first non-zero child status."""
+    forwards SIGTERM/SIGINT, and as soon as ANY child exits non-zero it stops the others and exits
+    with that status.  Children get ``--gpus 0`` (and FDX_WORKER_GPUS=0) so none of them spawns
+    again, and ``--metrics-port base+g`` each (base = the parent's --metrics-port, or
+    FDX_WORKER_METRICS_PORT, or 8001) so N workers never contend for one port."""
     import subprocess
     import sys
 
     rest = []
     skip = False
+    base = int(os.environ.get("FDX_WORKER_METRICS_PORT", "8001"))
     for i, a in enumerate(argv):
         if skip:
             skip = False
             continue
-        if a == "--gpus":
+        if a in ("--gpus", "--metrics-port"):
+            if a == "--metrics-port" and i + 1 < len(argv):
+                base = int(argv[i + 1])
             skip = True
             continue
         if a.startswith("--gpus="):
             continue
+        if a.startswith("--metrics-port="):
+            base = int(a.split("=", 1)[1])
+            continue
         rest.append(a)
     procs = []
     for g in range(n):
-        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(g), FDX_DEVICE="cuda:0", FDX_WORKER_RANK=str(g))
-        if "FDX_WORKER_METRICS_PORT" in os.environ or "--metrics-port" not in rest:
-            base = int(os.environ.get("FDX_WORKER_METRICS_PORT", "8001"))
-            env["FDX_WORKER_METRICS_PORT"] = str(base + g)
-        procs.append(subprocess.Popen([sys.executable, "-m", "fraud_detection_amd.taskqueue.worker", *rest], env=env))
+        env = dict(os.environ, HIP_VISIBLE_DEVICES=str(g), FDX_DEVICE="cuda:0", FDX_WORKER_RANK=str(g),
+                   FDX_WORKER_GPUS="0", FDX_WORKER_METRICS_PORT=str(base + g if base else 0))
+        port = ["--metrics-port", str(base + g if base else 0)]
+        procs.append(subprocess.Popen([sys.executable, "-m", "fraud_detection_amd.taskqueue.worker", *rest,
+                                       "--gpus", "0", *port], env=env))
 
     def _fwd(signum, _frame):
         for p in procs:
@@ -194,9 +203,20 @@ def _spawn_per_gpu(n: int, argv: list[str]) -> int:
     signal.signal(signal.SIGTERM, _fwd)
     signal.signal(signal.SIGINT, _fwd)
     rc = 0
-    for p in procs:
-        r = p.wait()
-        rc = rc or r
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r
+                logger.error("worker child pid %d exited with %d: stopping the others", p.pid, r)
+                for q in live:
+                    q.terminate()
+        if live:
+            time.sleep(0.2)
     return rc
 
 

@@ -5,7 +5,9 @@
        train rows -> SMOTE k-NN + generation -> fit) and the fold's validation AUC
     -> final pipeline on the whole train split -> exact test AUC
     -> artifacts in the reference layout (models/logistic_model.joblib, scaler.joblib,
-       columns.joblib, feature_names.json; models/xgb_model.joblib for the GBDT family)
+       columns.joblib, feature_names.json; for the GBDT family models/xgb_model.joblib -- a
+       GBDTClassifier, the reference's joblib contract -- plus models/xgb_model.json, the
+       pickle-free copy serving loads)
     -> MLflow run (params model_type / scale_pos_weight / cv_folds, metrics test_auc /
        cv_auc_mean / cv_auc_std, sklearn model with signature + input example, scaler artifact),
        registration when test_auc >= MLFLOW_AUC_THRESHOLD and the serving alias set to
@@ -130,6 +132,8 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     tm = train_metrics()
     tm.rows_per_second.set(float(res.n_train_rows) * (comm.world_size if comm else 1) / max(t_fit, 1e-9))
     observe_hbm(dev)
+    if model_type == "gbdt":  # the weight the trees were fit with (post-SMOTE balance by default)
+        scale_pos_weight = float(res.scale_pos_weight)
     if model_type == "logistic":
         ev = evaluate(res, Xte, yte, comm)
         auc = ev["auc"]

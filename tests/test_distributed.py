@@ -24,7 +24,7 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world, port, out_dir, smote, scope="global"):
+def _worker(rank, world, port, out_dir, smote, scope="global", zero_min_rank=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank), FDX_COMM_TRACE="1")
     from fraud_detection_amd.data.synthetic import separable
@@ -37,7 +37,10 @@ def _worker(rank, world, port, out_dir, smote, scope="global"):
     sh = slice(rank * len(X) // world, (rank + 1) * len(X) // world)
     sht = slice(rank * len(Xt) // world, (rank + 1) * len(Xt) // world)
     cfg = TrainConfig(smote=smote, tol=1e-8, init_std=0.0, smote_scope=scope)
-    res = DevicePipeline(cfg, comm).fit(X[sh].contiguous(), y[sh].contiguous())
+    Xs, ys = X[sh], y[sh]
+    if rank == zero_min_rank:  # a shard without minority rows
+        Xs, ys = Xs[ys == 0], ys[ys == 0]
+    res = DevicePipeline(cfg, comm).fit(Xs.contiguous(), ys.contiguous())
     ev = evaluate(res, Xt[sht].contiguous(), yt[sht].contiguous(), comm)
     mean, var, scale = res.scaler.numpy()
     np.savez(os.path.join(out_dir, f"r{rank}.npz"), w=res.w, mean=mean, var=var, auc=ev["auc"],
@@ -47,9 +50,10 @@ def _worker(rank, world, port, out_dir, smote, scope="global"):
     comm.close()
 
 
-def _run(world, smote, tmp_path, scope="global"):
+def _run(world, smote, tmp_path, scope="global", zero_min_rank=None):
     port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path), smote, scope), nprocs=world, start_method="spawn")
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), smote, scope, zero_min_rank), nprocs=world,
+                       start_method="spawn")
     return [dict(np.load(os.path.join(tmp_path, f"r{r}.npz"))) for r in range(world)]
 
 
@@ -101,19 +105,50 @@ def test_dp_global_smote_equals_single_process(tmp_path, world):
         assert float(o["auc"]) == pytest.approx(ev["auc"], abs=1e-6)
 
 
-def test_global_smote_slices_cover_the_quota():
+@pytest.mark.parametrize("ranks", [
+    [[37, 5000], [0, 4000], [90, 6100], [12, 333], [5, 9000], [64, 4096], [1, 10], [40, 7777]],
+    [[0, 10000], [10, 100]],          # the zero-minority rank used to overflow rank 1
+    [[10, 100], [0, 10000]],
+    [[500, 1000], [0, 3], [0, 0], [1, 129]],
+])
+def test_global_smote_slices_cover_the_quota(ranks):
     from fraud_detection_amd.models.pipeline import global_smote_slices
 
-    quota = lambda n, m: max(0, (n - m) - m) if m > 0 else 0  # noqa: E731
-    ranks = [[37, 5000], [0, 4000], [90, 6100], [12, 333], [5, 9000], [64, 4096], [1, 10], [40, 7777]]
+    ratio = 1.0
+    quota = lambda n, m: max(0, int(round((n - m) * ratio)) - m) if m > 0 else 0  # noqa: E731
     per, offs = zip(*[global_smote_slices(ranks, quota, r) for r in range(len(ranks))])
     per = per[0]
     total = quota(sum(r[1] for r in ranks), sum(r[0] for r in ranks))
     assert sum(per) == total and all(p >= 0 for p in per)
     assert all(o % 128 == 0 for o in offs) and list(offs) == [sum(per[:r]) for r in range(len(ranks))]
-    # boundaries sit within 64 rows of the cumulative per-rank shares (capped at the global quota)
-    cum = np.cumsum([quota(r[1], r[0]) for r in ranks])[:-1]
-    assert all(abs(o - min(c, total)) <= 64 for o, c in zip(offs[1:], cum))
+    # every slice fits the training buffer the rank sized before the exchange (pipeline.fit: cap)
+    for p, (_, n) in zip(per, ranks):
+        assert p <= int(np.ceil(n * max(ratio, 1.0))) + 128
+    # boundaries sit within 64 rows of the row-proportional cumulative shares
+    n_g = sum(r[1] for r in ranks)
+    cum = [total * int(c) // n_g for c in np.cumsum([r[1] for r in ranks])[:-1]]
+    assert all(abs(o - c) <= 64 for o, c in zip(offs[1:], cum))
+
+
+@pytest.mark.parametrize("scope", ["shard", "global"])
+def test_dp_rank_without_minority_rows(tmp_path, scope):
+    """a shard with no minority rows must neither raise nor hang its peers (shard
+    scope: it skips SMOTE; global scope: it takes a slice of the global draw sequence)."""
+    outs = _run(2, True, tmp_path, scope=scope, zero_min_rank=1)
+    assert np.array_equal(outs[0]["w"], outs[1]["w"])
+    assert float(outs[0]["auc"]) > 0.9
+    if scope == "global":
+        from fraud_detection_amd.data.synthetic import separable
+        from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+        X, y = separable(24_000, fraud_rate=0.02, seed=100)
+        h = len(X) // 2
+        keep = torch.ones(len(X), dtype=torch.bool)
+        keep[h:] = y[h:] == 0
+        ref = DevicePipeline(TrainConfig(smote=True, tol=1e-8, init_std=0.0)).fit(X[keep].contiguous(),
+                                                                                y[keep].contiguous())
+        assert sum(int(o["n_train"]) for o in outs) == ref.n_train_rows
+        np.testing.assert_allclose(outs[0]["w"], ref.w, atol=1e-7)
 
 
 def _knn_worker(rank, world, port, out_dir):

@@ -146,9 +146,11 @@ def test_pipeline_cpu_smote_and_artifacts(tmp_path):
     res = GBDTPipeline(TrainConfig(), gb.GBDTParams(n_estimators=40, max_depth=4)).fit(X, y)
     n_min = int(y.sum())
     assert res.n_train_rows == 2 * (len(y) - n_min)
-    assert res.scale_pos_weight == pytest.approx((len(y) - n_min) / n_min)
+    assert res.scale_pos_weight == pytest.approx(1.0)  # the fitted (post-SMOTE) rows are balanced
     ev = res.evaluate(Xt, yt)
     assert ev["auc"] > 0.9
+    ref = GBDTPipeline(TrainConfig(), gb.GBDTParams(n_estimators=2, max_depth=2), scale_pos_weight="reference").fit(X, y)
+    assert ref.scale_pos_weight == pytest.approx((len(y) - n_min) / n_min)  # train_model.py:52-54
     paths = res.save(str(tmp_path), [f"f{i}" for i in range(30)])
     assert os.path.exists(paths["model"]) and os.path.exists(paths["scaler"])
     o = json.load(open(paths["model"]))
@@ -174,3 +176,18 @@ def test_train_entry_point_gbdt(tmp_path, monkeypatch):
     assert 0.0 <= out["test_auc"] <= 1.0 and len(out["cv_scores"]) == 2  # random labels: AUC ~ 0.5
     assert os.path.exists(tmp_path / "models" / "xgb_model.json")
     assert out["registered_version"] == 1
+    # the reference's artifact contract: joblib.load(models/xgb_model.joblib).predict_proba(scaled X)
+    import joblib
+    import numpy as np
+
+    from fraud_detection_amd.models.gbdt import GBDTClassifier
+
+    clf = joblib.load(tmp_path / "models" / "xgb_model.joblib")
+    assert isinstance(clf, GBDTClassifier)
+    js = GBDTClassifier.load_model(str(tmp_path / "models" / "xgb_model.json"), device="cpu")
+    sc = joblib.load(tmp_path / "models" / "scaler.joblib")
+    Xs = sc.transform(df.drop(columns=["Class"]).to_numpy()[:50])
+    clf.device = "cpu"
+    np.testing.assert_array_equal(clf.predict_proba(Xs), js.predict_proba(Xs))
+    assert clf.params.scale_pos_weight == pytest.approx(out["scale_pos_weight"])
+    assert out["scale_pos_weight"] == pytest.approx(1.0, abs=0.01)  # post-SMOTE balance (App. D #11)

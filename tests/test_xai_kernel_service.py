@@ -147,12 +147,16 @@ def test_worker_spawns_one_process_per_gpu(monkeypatch):
 
     from fraud_detection_amd.taskqueue import worker as W
 
-    seen = []
+    seen, cmds, envs, killed = [], [], [], []
 
     class P:
         def __init__(self, cmd, env):
             seen.append(env["HIP_VISIBLE_DEVICES"])
-            self.rc = 3 if env["HIP_VISIBLE_DEVICES"] == "1" else 0
+            cmds.append(cmd)
+            envs.append(env)
+            self.pid = len(seen)
+            # child 1 fails; the others would run forever until terminated
+            self.rc = 3 if env["HIP_VISIBLE_DEVICES"] == "1" else None
 
         def wait(self):
             return self.rc
@@ -160,9 +164,22 @@ def test_worker_spawns_one_process_per_gpu(monkeypatch):
         def poll(self):
             return self.rc
 
+        def terminate(self):
+            killed.append(self.pid)
+            self.rc = -15
+
+        def send_signal(self, s):
+            self.terminate()
+
     monkeypatch.setattr(subprocess, "Popen", P)
-    assert W.main(["--gpus", "4", "--app", "nope:app"]) == 3
+    monkeypatch.setenv("FDX_WORKER_GPUS", "4")  # inherited env must not make children spawn
+    assert W.main(["--app", "nope:app", "--metrics-port", "9100"]) == 3
     assert seen == ["0", "1", "2", "3"]
+    assert sorted(killed) == [1, 3, 4]  # the failing child is noticed while child 0 still runs
+    for g, (cmd, env) in enumerate(zip(cmds, envs)):
+        assert env["FDX_WORKER_GPUS"] == "0"
+        assert cmd[cmd.index("--gpus") + 1] == "0"
+        assert cmd.count("--metrics-port") == 1 and cmd[cmd.index("--metrics-port") + 1] == str(9100 + g)
 
 
 def test_gbdt_worker_explains_with_treeshap(tmp_path, restore_service, monkeypatch):

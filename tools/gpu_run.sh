@@ -28,6 +28,7 @@
 #   ntscab       bench 50 steps x 3: scaler row stores plain vs nontemporal
 #   smoteab      SMOTE up-front gathers (FDX_SMOTE_G2) A/B: exactness tests, kernel stats, bench
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
+#   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -139,6 +140,9 @@ for st in "$@"; do
     dp2)  # DP rehearsal on one GPU: 2 ranks over host-staged gloo (the RCCL path needs a GPU per rank)
       step dp2 300 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 \
+        --rows-per-gpu 2000000 ;;
+    dp2self)  # bench.py --gpus 2 starts its own 2 ranks (self-launch path), one GPU, gloo
+      step dp2self 300 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 \
         --rows-per-gpu 2000000 ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
