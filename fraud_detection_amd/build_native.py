@@ -117,6 +117,13 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
         if force or _newer(io, [io_obj]):
             _run([HIPCC, "-shared", "-fPIC", io_obj, "-o", io, "-lpthread", *rpath])
         outputs["io"] = io
+    # the serving ring is host-only C++ (front-end processes import it without any HIP runtime)
+    ring_src = os.path.join(CSRC, "serve", "shm_ring.cpp")
+    if os.path.exists(ring_src):
+        ring = os.path.join(PKG_DIR, "_fdx_ring" + EXT_SUFFIX)
+        if force or _newer(ring, [ring_src]):
+            _run([os.environ.get("CXX", "g++"), *COMMON_FLAGS, "-shared", *_py_includes(), ring_src, "-o", ring])
+        outputs["ring"] = ring
     if verbose:
         for k, v in outputs.items():
             print(f"[build_native] {k}: {os.path.relpath(v, os.path.dirname(PKG_DIR))}")

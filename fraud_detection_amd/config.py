@@ -28,6 +28,7 @@ ENV_MAP = {
     "FDX_SOLVER": "solver",
     "FDX_MICROBATCH_US": "microbatch_us",
     "FDX_MICROBATCH_MAX": "microbatch_max",
+    "FDX_GPU_OWNER_RING": "gpu_owner_ring",
     "FDX_QUEUE_URL": "queue_url",
     "FDX_XAI_BATCH": "xai_batch",
     "FDX_KERNELSHAP_NSAMPLES": "kernelshap_nsamples",
@@ -61,13 +62,14 @@ class Settings:
     device: str = "auto"           # auto | cuda | cpu
     dtype: str = "bf16"            # bf16 | fp8 (training row storage)
     solver: str = "newton"         # newton | sgd
-    microbatch_us: int = 300       # GPU serving micro-batch window
-    microbatch_max: int = 4096
+    microbatch_us: int = 0         # GPU owner: extra wait for more rows (0 = continuous batching)
+    microbatch_max: int = 8192
+    gpu_owner_ring: str = ""       # multi-worker serving: the GPU-owner process's ring (serve/launch.py)
     xai_batch: int = 512
     kernelshap_nsamples: int = 0   # 0 -> shap default 2*M + 2048
     kernelshap_background: int = 100   # rows saved with the model (shap_background.npy)
     kernelshap_link: str = "identity"  # identity (probabilities) | logit | logit_model
-    xai_method: str = "auto"           # auto (kernel when a background exists) | linear | kernel | tree (GBDT)
+    xai_method: str = "auto"           # auto (the family default: linear | GBDT kernel) | linear | kernel | tree
     smote_k: int = 5
     seed: int = 42
     split: str = "auto"            # sklearn (reference-exact) | device (K3 kernel) | auto

@@ -8,7 +8,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <string>
+#include <vector>
 
 #include "kernels/launchers.h"
 
@@ -41,6 +43,71 @@ static void stream_sync(u stream) {
   if (e != hipSuccess) throw std::runtime_error(std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
 }
 
+static void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Page-lock a caller's host range for the duration of one call (so DMA reads / writes it in
+// place: no staging memcpy).  Already-pinned memory (hipHostMalloc, or registered elsewhere) is
+// used as it is.
+struct HostPin {
+  void* p = nullptr;
+  explicit HostPin(void* ptr, size_t bytes) {
+    if (!ptr || !bytes) return;
+    hipError_t e = hipHostRegister(ptr, bytes, hipHostRegisterDefault);
+    if (e == hipSuccess) p = ptr;
+    else (void)hipGetLastError();  // hipErrorHostMemoryAlreadyRegistered or unsupported: copy as is
+  }
+  ~HostPin() {
+    if (p) (void)hipHostUnregister(p);
+  }
+};
+
+// Host-to-host batch scoring (BASELINE config 2: 1M x 30 raw fp32 rows in host memory -> fp64
+// P(fraud) and logits in host memory).  The input is page-locked in place and streamed in chunks:
+// H2D of chunk i+1 (DMA engine, stream h2d) overlaps the fused folded-scaler GEMV + sigmoid of
+// chunk i (stream comp), whose fp64 results go back on a third stream (the other DMA direction)
+// while later chunks upload.  Device buffers hold the whole batch (HBM is not the constraint here),
+// so no slot is reused inside a call and only the chunk edges need events.
+static void predict_h2h(u x_host, int64_t n, int ld, int d, u a, float bias, u prob_host, u logit_host,
+                        u x_dev, u prob_dev, u logit_dev, int64_t chunk, u s_h2d, u s_comp, u s_d2h) {
+  if (n <= 0) return;
+  chunk = std::max<int64_t>(chunk, 1024);
+  const size_t row_b = (size_t)ld * 4;
+  HostPin px(P<void>(x_host), (size_t)n * row_b);
+  HostPin pp(P<void>(prob_host), (size_t)n * 8);
+  HostPin pl(P<void>(logit_host), (size_t)n * 8);
+  const int64_t nch = (n + chunk - 1) / chunk;
+  std::vector<hipEvent_t> up(nch), done(nch);
+  for (int64_t i = 0; i < nch; ++i) {
+    hip_check(hipEventCreateWithFlags(&up[i], hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventCreateWithFlags(&done[i], hipEventDisableTiming), "hipEventCreate");
+  }
+  for (int64_t i = 0; i < nch; ++i) {
+    const int64_t r0 = i * chunk, m = std::min(chunk, n - r0);
+    hip_check(hipMemcpyAsync(P<char>(x_dev) + r0 * row_b, P<char>(x_host) + r0 * row_b, (size_t)m * row_b,
+                             hipMemcpyHostToDevice, S(s_h2d)), "H2D");
+    hip_check(hipEventRecord(up[i], S(s_h2d)), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(S(s_comp), up[i], 0), "hipStreamWaitEvent");
+    fdx::launch_predict_raw64(P<const float>(x_dev) + r0 * ld, m, ld, d, P<const float>(a), bias,
+                              P<double>(prob_dev) + r0, P<double>(logit_dev) + r0, S(s_comp));
+    hip_check(hipEventRecord(done[i], S(s_comp)), "hipEventRecord");
+    hip_check(hipStreamWaitEvent(S(s_d2h), done[i], 0), "hipStreamWaitEvent");
+    if (prob_host)
+      hip_check(hipMemcpyAsync(P<double>(prob_host) + r0, P<double>(prob_dev) + r0, (size_t)m * 8,
+                               hipMemcpyDeviceToHost, S(s_d2h)), "D2H");
+    if (logit_host)
+      hip_check(hipMemcpyAsync(P<double>(logit_host) + r0, P<double>(logit_dev) + r0, (size_t)m * 8,
+                               hipMemcpyDeviceToHost, S(s_d2h)), "D2H");
+  }
+  hipError_t e = hipStreamSynchronize(S(s_d2h));
+  for (int64_t i = 0; i < nch; ++i) {
+    (void)hipEventDestroy(up[i]);
+    (void)hipEventDestroy(done[i]);
+  }
+  hip_check(e, "hipStreamSynchronize");
+}
+
 PYBIND11_MODULE(_fdx_native, m) {
   m.doc() = "MI355X (gfx950) HIP kernels for fraud_detection_amd";
   m.attr("ARCH") = "gfx950";
@@ -56,7 +123,8 @@ PYBIND11_MODULE(_fdx_native, m) {
     }
     return reinterpret_cast<u>(d);
   });
-  m.def("stream_sync", &stream_sync);
+  m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
+  m.def("predict_h2h", &predict_h2h, py::call_guard<py::gil_scoped_release>());
 
   // scaler
   m.def("scaler_partial", [](u X, int64_t n, int ld, int d, u pivot, u partial, int nblocks, u s) {
@@ -121,6 +189,14 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_predict_shap(P<const void>(X), in_kind, n, ld, dz, dphi, P<const float>(a), P<const float>(c), bias,
                              P<float>(prob), P<float>(logit), P<float>(phi), ld_phi, S(s));
   });
+  // GPU-owner batch (serve/gpu_owner.py): launch + wait in one call with the GIL released, so the
+  // owner thread never holds the interpreter while the device works
+  m.def("predict_shap_sync", [](u X, int in_kind, int64_t n, int ld, int dz, int dphi, u a, u c, float bias, u prob,
+                                u logit, u phi, int ld_phi, u s) {
+    fdx::launch_predict_shap(P<const void>(X), in_kind, n, ld, dz, dphi, P<const float>(a), P<const float>(c), bias,
+                             P<float>(prob), P<float>(logit), P<float>(phi), ld_phi, S(s));
+    stream_sync(s);
+  }, py::call_guard<py::gil_scoped_release>());
 
   // logistic regression
   m.def("logreg_pass_blocks", &fdx::logreg_pass_blocks);

@@ -92,6 +92,8 @@ void launch_predict_fp8(const uint8_t* X, int64_t n, const float* w, float* prob
                         hipStream_t stream);
 // Fused predict + linear SHAP.  in_kind: 0 = bf16 [n][32], 1 = raw fp32 [n][ld].
 // z = sum_{j<dz} a_j x_j + bias;  phi_j = a_j (x_j - c_j), j < dphi.
+void launch_predict_raw64(const float* X, int64_t n, int ld, int d, const float* a, float bias, double* prob,
+                          double* logit, hipStream_t stream);
 void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, int dphi,
                          const float* a, const float* c, float bias, float* prob, float* logit,
                          float* phi, int ld_phi, hipStream_t stream);

@@ -97,11 +97,13 @@ __global__ __launch_bounds__(kThreads) void predict_kernel(const uint4* __restri
   }
 }
 
-// Fused predict + linear SHAP.  8 lanes per row, 4 columns per lane.
-template <int IN, int VEC>  // IN: 0 = bf16 [n][32], 1 = fp32 [n][ld]
+// Fused predict + linear SHAP.  8 lanes per row, 4 columns per lane.  OT: the prob / logit
+// element type -- float, or double for host-to-host batch scoring (the fp32 result widened on the
+// device, so the host receives final fp64 arrays with no conversion pass).
+template <int IN, int VEC, typename OT = float>  // IN: 0 = bf16 [n][32], 1 = fp32 [n][ld]
 __global__ __launch_bounds__(kThreads) void predict_shap_kernel(
     const void* __restrict__ Xv, int64_t n, int ld, int dz, int dphi, const float* __restrict__ a,
-    const float* __restrict__ c, float bias, float* __restrict__ prob, float* __restrict__ logit,
+    const float* __restrict__ c, float bias, OT* __restrict__ prob, OT* __restrict__ logit,
     float* __restrict__ phi, int ld_phi) {
   const int lane = lane_id();
   const int c0 = (lane & 7) * 4;
@@ -181,8 +183,8 @@ __global__ __launch_bounds__(kThreads) void predict_shap_kernel(
         }
       }
       if ((lane & 7) == 0) {
-        if (logit) logit[rows[u]] = z;
-        if (prob) prob[rows[u]] = fast_sigmoid(z);
+        if (logit) logit[rows[u]] = (OT)z;
+        if (prob) prob[rows[u]] = (OT)fast_sigmoid(z);
       }
     }
   }
@@ -231,6 +233,21 @@ void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, 
                                                                prob, logit, phi, ld_phi);
   }
   check_launch("predict_shap");
+}
+
+void launch_predict_raw64(const float* X, int64_t n, int ld, int d, const float* a, float bias, double* prob,
+                          double* logit, hipStream_t stream) {
+  static const int cap2 = resident_cap(predict_shap_kernel<1, 2, double>, kThreads);
+  static const int cap1 = resident_cap(predict_shap_kernel<1, 1, double>, kThreads);
+  const int64_t units = (n + 7) / 8, per_block = (kThreads / kWave) * 4;
+  // raw fp32 rows of 30 features: 8-byte aligned pairs when ld is even
+  if ((ld % 2) == 0 && (reinterpret_cast<uintptr_t>(X) % 8) == 0)
+    predict_shap_kernel<1, 2, double><<<capped_grid(units, per_block, cap2), kThreads, 0, stream>>>(
+        X, n, ld, d, 0, a, a, bias, prob, logit, nullptr, 0);
+  else
+    predict_shap_kernel<1, 1, double><<<capped_grid(units, per_block, cap1), kThreads, 0, stream>>>(
+        X, n, ld, d, 0, a, a, bias, prob, logit, nullptr, 0);
+  check_launch("predict_raw64");
 }
 
 }  // namespace fdx

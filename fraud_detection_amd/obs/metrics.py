@@ -33,6 +33,8 @@ class ApiMetrics:
     http_req_size: Histogram
     http_resp_size: Histogram
     microbatch_size: Histogram
+    host_rows: Counter          # rows scored on the exact host path (small batches, owner down)
+    owner_rows: Gauge           # rows the GPU owner has scored (ring statistics, multi-worker)
 
     def render(self) -> bytes:
         """This app's metrics plus the process-global ones (worker / training / span / GPU
@@ -66,6 +68,9 @@ def api_metrics(registry: CollectorRegistry | None = None) -> ApiMetrics:
                                  ["handler"], buckets=size_buckets, registry=r),
         microbatch_size=Histogram("fdx_microbatch_size", "Rows per fused GPU predict launch",
                                   buckets=(1, 2, 4, 8, 16, 32, 64, 128, 256, 512, 1024, 4096), registry=r),
+        host_rows=Counter("fdx_host_path_rows", "Rows scored on the exact host fp64 path", registry=r),
+        owner_rows=Gauge("fdx_gpu_owner_rows", "Rows scored by the GPU-owner process (all front-ends)",
+                         registry=r),
     )
 
 

@@ -3,8 +3,10 @@
 Endpoints (same paths, bodies, status codes and header as the reference):
   POST /predict            200 PredictionOut{transaction_id, prediction, score, correlation_id,
                            explanation_status}; 422 on wrong feature count; header X-Correlation-ID.
-                           Scoring runs through the fused device kernel (micro-batched on GPU);
-                           the SHAP explanation is queued as task xai_tasks.compute_shap.
+                           Scoring: batches up to the calibrated host threshold run on the exact
+                           fp64 host path, larger ones go to the GPU owner (serve/gpu_owner.py:
+                           one process owns the GPU and batches every front-end's rows into one
+                           fused launch); the SHAP explanation is queued as xai_tasks.compute_shap.
   GET  /explain/{id}       200 {transaction_id, created_at, shap_values, feature_names} | 404
   GET  /health             200 {status: OK, dependencies{postgres, redis_broker, mlflow, model}} | 503
   GET  /status             {"status": "UP"}
@@ -39,7 +41,7 @@ from ..obs.metrics import CONTENT_TYPE_LATEST, api_metrics
 from ..store import db as store_db
 from ..store.migrations import upgrade
 from ..store.models import ShapExplanation, StatusEnum, TransactionResult
-from .batcher import MicroBatcher
+from . import gpu_owner
 from .engine import InferenceEngine, load_engine_dir
 from .schemas import BatchIn, BatchOut, PredictAccepted, PredictionOut, PredictResponse, TransactionIn
 
@@ -96,15 +98,10 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
                 upgrade(_db())
         except Exception as e:  # noqa: BLE001 - same policy as the reference: log, keep serving
             logger.error("Failed to connect or create tables: %s", e)
-        if state["engine"] is None:
-            eng, src = load_production_engine(settings, settings.device)
-            state["engine"], state["model_source"] = eng, src
-        b = MicroBatcher(state["engine"], settings.microbatch_us, settings.microbatch_max, metrics)
-        await b.start()
-        state["batcher"] = b
+        state["batcher"] = _make_dispatcher()
         tracing.configure(settings.otel_service_name)
         yield
-        await b.stop()
+        state["batcher"].close()
 
     app = FastAPI(title="Fraud Detection API", version="1.0.0", lifespan=lifespan)
     app.state.fdx = state
@@ -117,9 +114,25 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
             state["engine"], state["model_source"] = eng, src
         return state["engine"]
 
-    def batcher_() -> MicroBatcher:
-        if state["batcher"] is None:
-            state["batcher"] = MicroBatcher(engine_(), 0, settings.microbatch_max, metrics)
+    def _make_dispatcher() -> gpu_owner.Dispatcher:
+        """Multi-worker front-end (FDX_GPU_OWNER_RING): a CPU copy of the model for the host path
+        plus the ring to the GPU-owner process.  Single worker: the owner thread in-process."""
+        if settings.gpu_owner_ring:
+            if state["engine"] is None:
+                eng, src = load_production_engine(settings, "cpu")
+                state["engine"], state["model_source"] = eng, src
+            deadline = time.time() + 120
+            while not os.path.exists(settings.gpu_owner_ring):  # the owner is still loading
+                if time.time() > deadline:
+                    raise RuntimeError(f"GPU owner ring {settings.gpu_owner_ring} never appeared")
+                time.sleep(0.05)
+            return gpu_owner.Dispatcher(state["engine"], gpu_owner.RingClient(settings.gpu_owner_ring),
+                                        metrics=metrics)
+        return gpu_owner.in_process(engine_(), settings.microbatch_us, settings.microbatch_max, metrics)
+
+    def batcher_() -> gpu_owner.Dispatcher:
+        if state["batcher"] is None:  # used without lifespan: no owner thread, direct engine calls
+            state["batcher"] = gpu_owner.Dispatcher(engine_(), metrics=metrics)
         return state["batcher"]
 
     @app.middleware("http")
@@ -221,13 +234,14 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
             return "Queue failed"
 
     @app.post("/predict", response_model=PredictionOut, tags=["Prediction"])
-    async def predict(transaction: TransactionIn, request: Request):
-        """Synchronous scoring and asynchronous SHAP calculation."""
+    def predict(transaction: TransactionIn, request: Request):
+        """Synchronous scoring and asynchronous SHAP calculation.  A plain (threadpool) handler:
+        the ring wait and the DB insert block this request's thread, never the event loop."""
         cid = request.state.correlation_id
         metrics.predictions_submitted.inc()
         x = _validate(transaction.features)
         with metrics.inference_time.time():
-            prob, _ = await batcher_().submit(x)
+            prob, _ = batcher_().predict_one(x)
         prediction = int(prob > 0.5)
         features_dict = {f"feature_{i}": float(v) for i, v in enumerate(x.tolist())}
         _persist_pending(transaction.transaction_id, features_dict, prob)
@@ -237,7 +251,7 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
                              correlation_id=cid, explanation_status=explanation_status)
 
     @app.post("/predict/async", response_model=PredictAccepted, status_code=202, tags=["Prediction"])
-    async def predict_async(transaction: TransactionIn, request: Request):
+    def predict_async(transaction: TransactionIn, request: Request):
         cid = request.state.correlation_id
         metrics.predictions_submitted.inc()
         x = _validate(transaction.features)
@@ -248,18 +262,22 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
         return PredictAccepted(transaction_id=transaction.transaction_id, status="PENDING")
 
     @app.post("/predict/batch", response_model=BatchOut, tags=["Prediction"])
-    async def predict_batch(batch: BatchIn):
+    def predict_batch(batch: BatchIn):
         eng = engine_()
         X = np.asarray(batch.rows, dtype=np.float32)
         if X.ndim != 2 or X.shape[1] != eng.d:
             raise HTTPException(status_code=422, detail=f"rows must be [n, {eng.d}]")
         metrics.predictions_submitted.inc(X.shape[0])
+        disp = batcher_()
         with metrics.inference_time.time():
             if batch.explain:
-                ex = eng.explain(X, settings.xai_method)
-                p, phi = ex.prob, ex.phi
+                if disp.client is not None and disp.owner is None and X.shape[0]:
+                    p, _, phi = disp.client.predict_explain(X)  # the GPU owner explains
+                else:
+                    ex = eng.explain(X, settings.xai_method)
+                    p, phi = ex.prob, ex.phi
             else:
-                p, _ = eng.predict_proba(X)
+                p, _ = disp.predict_proba(X)
                 phi = None
         return BatchOut(predictions=(p > 0.5).astype(int).tolist(), scores=p.tolist(),
                         shap_values=phi.tolist() if phi is not None else None)
@@ -299,6 +317,9 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
 
     @app.get("/metrics", include_in_schema=False)
     def prometheus_metrics():
+        disp = state["batcher"]
+        if disp is not None and disp.client is not None:
+            metrics.owner_rows.set(disp.client.stats()["rows"])
         return Response(metrics.render(), media_type=CONTENT_TYPE_LATEST)
 
     @app.exception_handler(SQLAlchemyError)

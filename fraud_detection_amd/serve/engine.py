@@ -20,6 +20,12 @@ Device policy: ``device="auto"`` uses the GPU when one is present; CPU execution
 numpy (what the reference's sklearn path computes).  Host <-> device traffic goes through
 persistent pinned staging buffers (one upload and one download per call, no per-request pinned
 allocation).
+
+Small-batch routing: a GPU launch + synchronise costs tens of microseconds whatever the batch, the
+exact host fp64 path a few microseconds per row, so a GPU engine measures both at start-up
+(``calibrate``) and sends batches of at most ``host_max_rows`` rows to the host path
+(FDX_HOST_MAX_ROWS pins the threshold; 0 = always the device).  Explanations with KernelSHAP /
+TreeSHAP always run on the device (their host paths are orders of magnitude slower).
 """
 from __future__ import annotations
 
@@ -114,6 +120,20 @@ class _KernelTimer:
 
 
 ZERO_COPY_ROWS = int(os.environ.get("FDX_ZERO_COPY_ROWS", "256"))
+H2H_CHUNK_ROWS = 131072  # host-to-host batch scoring: rows per H2D / kernel / D2H pipeline stage
+CALIBRATION_SIZES = (1, 4, 16, 64, 256, 1024, 4096, 16384, 65536)
+
+
+def _median_time(fn, reps: int = 5) -> float:
+    import time
+
+    fn()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
 
 
 class _Staging:
@@ -172,11 +192,85 @@ class _EngineBase:
         self.kernel_link = kernel_link
         self._lock = threading.Lock()
         self._kexpl = None
+        self.host_max_rows = 0
+        self.calibration: dict = {}
+        self._owner_in = None
         if self.device.type == "cuda":
             from ..ops.native import native
 
             native()  # fail loudly rather than serve through an eager fallback
             self._stream = torch.cuda.Stream(self.device)
+
+    def _finish_init(self):
+        """Subclasses call this once their buffers exist: the small-batch threshold."""
+        if self.device.type != "cuda":
+            self.host_max_rows = 1 << 62  # a CPU engine runs everything on the host
+            return
+        env = os.environ.get("FDX_HOST_MAX_ROWS", "").strip()
+        if env and int(env) >= 0:
+            self.host_max_rows = int(env)
+            self.calibration = {"source": "FDX_HOST_MAX_ROWS"}
+        else:
+            self.calibrate()
+
+    def calibrate(self, sizes=CALIBRATION_SIZES) -> int:
+        """Largest batch size (of ``sizes``) at which the exact host path is no slower than the
+        device path (upload + kernel + download + sync), measured on this machine."""
+        rng = np.random.default_rng(0)
+        thr, rows = 0, []
+        for n in sizes:
+            X = self._calibration_rows(rng, n)
+            th = _median_time(lambda: self._predict_host(X))
+            td = _median_time(lambda: self._predict_device(X))
+            rows.append({"rows": n, "host_us": round(th * 1e6, 2), "device_us": round(td * 1e6, 2)})
+            if th > td:
+                break
+            thr = n
+        self.host_max_rows = thr
+        self.calibration = {"source": "measured", "sizes": rows}
+        logger.info("%s engine: batches <= %d rows take the host path (%s)", self.kind, thr, rows)
+        return thr
+
+    def _calibration_rows(self, rng, n: int) -> np.ndarray:
+        X = rng.normal(0.0, 1.0, (n, self.d)).astype(np.float32)
+        return X
+
+    def _use_host(self, n: int) -> bool:
+        return self.device.type != "cuda" or n == 0 or n <= self.host_max_rows
+
+    # ---- GPU-owner API (serve/gpu_owner.py): rows land in a pinned staging buffer -------------
+    def owner_input(self, cap: int) -> int:
+        """Address of a pinned float32 [cap, d] buffer the ring gathers request rows into."""
+        if self._owner_in is None or self._owner_in.shape[0] < cap:
+            self._owner_in = torch.empty((cap, self.d), dtype=torch.float32,
+                                         pin_memory=self.device.type == "cuda")
+            self._owner_out = np.empty(cap * (self.d + 2), np.float32)
+            self._owner_map = 0
+            if self.device.type == "cuda":
+                from ..ops.native import native
+
+                self._owner_map = native().host_device_pointer(self._owner_in.data_ptr())
+        return self._owner_in.data_ptr()
+
+    def run_staged(self, n: int, explain: bool):
+        """Score (and explain) the n rows at owner_input(): -> (prob, logit, phi, dphi) addresses
+        of float32 column blocks (phi 0 when not explaining).  Generic path: through the public
+        API; InferenceEngine overrides it with a copy-free device launch."""
+        X = self._owner_in[:n].numpy()
+        o = self._owner_out
+        if explain:
+            e = self.explain(X, os.environ.get("FDX_XAI_METHOD", "auto"))
+            p, z, phi = e.prob, e.logit, e.phi
+        else:
+            p, z = self.predict_proba(X)
+            phi = None
+        o[:n] = p
+        o[n:2 * n] = z
+        base = o.ctypes.data
+        if phi is None:
+            return base, base + 4 * n, 0, 0
+        o[2 * n:2 * n + n * self.d] = np.asarray(phi, np.float32).reshape(-1)
+        return base, base + 4 * n, base + 8 * n, self.d
 
     # ---- shared API ------------------------------------------------------------------------
     @property
@@ -194,9 +288,12 @@ class _EngineBase:
         return X
 
     def resolve_method(self, method: str = "auto") -> str:
+        """``auto``: the family's default -- LinearSHAP for the linear model (log-odds
+        attributions, what the reference's worker computes: xai_tasks.py:103-115, api/worker.py:53);
+        KernelSHAP (probability space) is opt-in with ``kernel`` / FDX_XAI_METHOD=kernel."""
         method = (method or "auto").lower()
         if method == "auto":
-            return "kernel" if self.has_background else self.default_method
+            method = self.default_method
         if method in ("kernel", "tree") and not self.has_background:
             raise ValueError(f"{method} SHAP needs a background (shap_background.npy next to the model)")
         if method not in self.methods:
@@ -267,6 +364,11 @@ class InferenceEngine(_EngineBase):
             self._c = torch.from_numpy(self.c.astype(np.float32)).to(self.device)
             self._stage = _Staging(self.device, self.d, self.d + 2)
             self._xstage = _Staging(self.device, self.d, self.d + 2)
+            self._ostage = _Staging(self.device, self.d, self.d + 2)
+            self._h2d_stream = torch.cuda.Stream(self.device)
+            self._d2h_stream = torch.cuda.Stream(self.device)
+            self._h2h_cap = 0
+        self._finish_init()
 
     @classmethod
     def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto",
@@ -282,58 +384,131 @@ class InferenceEngine(_EngineBase):
                    background=bg, **kw)
 
     # ---- core ------------------------------------------------------------------------------
+    def _launch(self, xo: int, n: int, want_phi: bool, st: "_Staging", zero_copy: bool):
+        """Fused folded-scaler predict (+ LinearSHAP) on device rows at ``xo``; results into
+        the staging output ([prob n][logit n][phi n*d]); waits for them.  -> host view."""
+        d = self.d
+        dphi = d if want_phi else 0
+        m = P.native()
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        if zero_copy:
+            oo = st.out_map
+            with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
+                m.predict_shap(xo, 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                               oo, oo + 4 * n, oo + 8 * n if want_phi else 0, dphi, s)
+            torch.cuda.current_stream(self.device).synchronize()
+            o = st.hout[: n * (2 + dphi)].numpy()
+        else:
+            out = st.dout
+            prob, logit = out[:n], out[n:2 * n]
+            phi = out[2 * n:2 * n + n * dphi].view(n, dphi) if want_phi else None
+            with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
+                m.predict_shap(xo, 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                               P.ptr(prob), P.ptr(logit), P.ptr(phi) if want_phi else 0, dphi, s)
+            o = st.download(n * (2 + dphi))
+        kt.observe()
+        return o
+
     def _device_run(self, X: np.ndarray, want_phi: bool):
         n, d = X.shape
         dphi = d if want_phi else 0
         with self._lock, torch.cuda.stream(self._stream):
             st = self._stage
-            m = P.native()
-            s = torch.cuda.current_stream(self.device).cuda_stream
             if st.zero_copy(n):
                 # request and result stay in pinned memory: no memcpy, one launch, one sync
                 st.hin[:n].numpy()[...] = X
-                xo, oo = st.in_map, st.out_map
-                with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
-                    m.predict_shap(xo, 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
-                                   oo, oo + 4 * n, oo + 8 * n if want_phi else 0, dphi, s)
-                torch.cuda.current_stream(self.device).synchronize()
-                o = st.hout[: n * (2 + dphi)].numpy()
+                o = self._launch(st.in_map, n, want_phi, st, True)
             else:
                 xd = st.upload(X)
-                out = st.dout
-                prob, logit = out[:n], out[n:2 * n]
-                phi = out[2 * n:2 * n + n * dphi].view(n, dphi) if want_phi else None
-                with _KernelTimer("predict_shap" if want_phi else "predict") as kt:
-                    m.predict_shap(P.ptr(xd), 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
-                                   P.ptr(prob), P.ptr(logit), P.ptr(phi) if want_phi else 0, dphi, s)
-                o = st.download(n * (2 + dphi))
-            kt.observe()
+                o = self._launch(P.ptr(xd), n, want_phi, st, False)
         p = o[:n].astype(np.float64)
         z = o[n:2 * n].astype(np.float64)
         ph = o[2 * n:].reshape(n, dphi).astype(np.float64) if want_phi else None
         return p, z, ph
 
+    def run_staged(self, n: int, explain: bool):
+        """GPU-owner path: the ring gathered the rows straight into the pinned owner buffer; the
+        kernel reads them there through its device mapping and writes the results into mapped
+        pinned memory (small batches: one launch + wait, GIL released, nothing copied), or after
+        one H2D copy (large batches).  Runs on the owner's own stream, owner thread only."""
+        if self.device.type != "cuda" or (explain and os.environ.get("FDX_XAI_METHOD", "auto") not in ("auto", "linear")):
+            return super().run_staged(n, explain)
+        d = self.d
+        dphi = d if explain else 0
+        st = self._ostage
+        st.ensure(self._owner_in.shape[0])
+        if getattr(self, "_ostream", None) is None:
+            self._ostream = torch.cuda.Stream(self.device)
+        if n <= ZERO_COPY_ROWS and self._owner_map and st.out_map:
+            oo = st.out_map
+            P.native().predict_shap_sync(self._owner_map, 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c),
+                                         float(self.bias), oo, oo + 4 * n, oo + 8 * n if explain else 0, dphi,
+                                         self._ostream.cuda_stream)
+            base = st.hout.data_ptr()
+        else:
+            with torch.cuda.stream(self._ostream):
+                st.din[:n].copy_(self._owner_in[:n], non_blocking=True)
+                o = self._launch(P.ptr(st.din), n, explain, st, False)
+            base = o.ctypes.data
+        return base, base + 4 * n, (base + 8 * n) if explain else 0, dphi
+
+    def _predict_host(self, X: np.ndarray):
+        return self._cpu(X, want_phi=False)
+
+    def _predict_device(self, X: np.ndarray):
+        if X.shape[0] > ZERO_COPY_ROWS:
+            return self._device_h2h(X)
+        return self._device_run(X, False)
+
+    def _device_h2h(self, X: np.ndarray, out=None):
+        """Large batches, host in -> host out (config 2): the caller's rows are page-locked in place
+        and pipelined chunk by chunk (H2D | fused kernel | D2H on three streams); the kernel
+        writes the fp64 results the caller gets, so nothing is staged or converted on the host."""
+        n, d = X.shape
+        p, z = (np.empty(n), np.empty(n)) if out is None else out
+        if p.dtype != np.float64 or z.dtype != np.float64 or not (p.flags.c_contiguous and z.flags.c_contiguous) \
+                or p.shape != (n,) or z.shape != (n,):
+            raise ValueError("out must be two contiguous float64 [n] arrays")
+        with self._lock:
+            if n > self._h2h_cap:
+                cap = max(n, 2 * self._h2h_cap)
+                self._h2h_x = torch.empty((cap, d), dtype=torch.float32, device=self.device)
+                self._h2h_o = torch.empty((2, cap), dtype=torch.float64, device=self.device)
+                self._h2h_cap = cap
+            P.native().predict_h2h(X.ctypes.data, n, d, d, P.ptr(self._a), float(self.bias), p.ctypes.data,
+                                   z.ctypes.data, P.ptr(self._h2h_x), P.ptr(self._h2h_o[0]), P.ptr(self._h2h_o[1]),
+                                   H2H_CHUNK_ROWS, self._h2d_stream.cuda_stream, self._stream.cuda_stream,
+                                   self._d2h_stream.cuda_stream)
+        return p, z
+
     def predict_explain(self, X: np.ndarray):
         """X raw features [B, d] -> (prob [B], logit [B], phi [B, d]) as numpy (LinearSHAP)."""
         X = self._check(X)
-        if self.device.type != "cuda" or X.shape[0] == 0:
+        if self._use_host(X.shape[0]):
             return self._cpu(X)
         return self._device_run(X, True)
 
-    def predict_proba(self, X: np.ndarray):
-        """-> (prob [B], logit [B])."""
+    def predict_proba(self, X: np.ndarray, out=None):
+        """-> (prob [B], logit [B]) float64.  ``out``: optional (prob, logit) float64 arrays to
+        fill (a batch-scoring loop reuses them: no per-call allocation)."""
         X = self._check(X)
-        if self.device.type != "cuda" or X.shape[0] == 0:
-            p, z, _ = self._cpu(X)
-            return p, z
-        p, z, _ = self._device_run(X, False)
+        if self._use_host(X.shape[0]):
+            p, z, _ = self._cpu(X, want_phi=False)
+        elif X.shape[0] > ZERO_COPY_ROWS:
+            return self._device_h2h(X, out)
+        else:
+            p, z, _ = self._device_run(X, False)
+        if out is not None:
+            out[0][...] = p
+            out[1][...] = z
+            return out
         return p, z
 
-    def _cpu(self, X: np.ndarray):
+    def _cpu(self, X: np.ndarray, want_phi: bool = True):
         Xd = X.astype(np.float64)
         z = Xd @ self.a[: self.d] + self.bias
         p = 1.0 / (1.0 + np.exp(-z))
-        phi = self.a[None, : self.d] * (Xd - self.c[None, : self.d])
+        phi = self.a[None, : self.d] * (Xd - self.c[None, : self.d]) if want_phi else None
         return p, z, phi
 
     def _make_kernel_explainer(self):
@@ -387,6 +562,7 @@ class TreeInferenceEngine(_EngineBase):
             self._dens = DeviceEnsemble(ensemble, self.device)
             self._stage = _Staging(self.device, self.d, 1)
             self._xstage = _Staging(self.device, self.d, self.d + 2)
+        self._finish_init()
 
     @classmethod
     def from_paths(cls, model_path=None, scaler_path=None, features_path=None, device="auto", source="local",
@@ -420,14 +596,20 @@ class TreeInferenceEngine(_EngineBase):
     def predict_proba(self, X: np.ndarray):
         """-> (prob [B], margin [B])."""
         X = self._check(X)
-        if self.device.type != "cuda" or X.shape[0] == 0:
-            from ..models.explainers import _standardize
-            from ..ops import reference_gbdt as RG
+        if self._use_host(X.shape[0]):
+            return self._predict_host(X)
+        return self._predict_device(X)
 
-            e = self.ens
-            m = RG.predict_margin(_standardize(X, self.mean, self.scale), e.feat, e.thr, e.leaf, e.depth,
-                                  e.base_margin).astype(np.float64)
-            return 1.0 / (1.0 + np.exp(-m)), m
+    def _predict_host(self, X: np.ndarray):
+        from ..models.explainers import _standardize
+        from ..ops import reference_gbdt as RG
+
+        e = self.ens
+        m = RG.predict_margin(_standardize(X, self.mean, self.scale), e.feat, e.thr, e.leaf, e.depth,
+                              e.base_margin).astype(np.float64)
+        return 1.0 / (1.0 + np.exp(-m)), m
+
+    def _predict_device(self, X: np.ndarray):
         from ..ops import gbdt as gb
         from ..ops.scaler import scale_cast
 

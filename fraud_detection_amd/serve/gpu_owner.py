@@ -1,0 +1,226 @@
+"""The serving process model: ONE process owns the GPU, every front-end forwards to it.
+
+The reference serves with ``gunicorn -k uvicorn.workers.UvicornWorker --workers 2``
+(/root/reference/Dockerfile:21, docker-compose.yml:74): each worker process holds its own model
+copy.  On MI355X a model copy per worker means a HIP context and a set of pinned buffers per
+worker, and every single-row request a launch of its own.  Here:
+
+* ``GpuOwner`` -- the only code that launches kernels.  A collector thread drains the
+  shared-memory request ring (csrc/serve/shm_ring.cpp: lock-free slots, futex wake-ups, no
+  pickling) straight into the engine's pinned input buffer and runs ONE fused launch per batch
+  (continuous batching: whatever is queued when the previous launch returns forms the next
+  batch; an optional window waits for more).  It runs inside a front-end (single-worker
+  deployment: anonymous ring) or as its own process (``python -m
+  fraud_detection_amd.serve.gpu_owner --ring /dev/shm/...``; serve/launch.py starts it first).
+* ``RingClient`` -- a front-end's view: ``predict_proba`` / ``predict_explain`` of [n, d] rows
+  through the ring (blocking, GIL released while waiting).
+* ``Dispatcher`` -- what /predict calls: batches at or below the owner's calibrated
+  ``host_max_rows`` run on the front-end's own exact fp64 host path (a GPU round trip costs more
+  than scoring a few rows on the CPU), larger ones go through the ring to the GPU.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import threading
+import time
+
+import numpy as np
+
+logger = logging.getLogger("fdx.gpu_owner")
+
+OP_PREDICT, OP_EXPLAIN = 0, 1
+DEFAULT_SLOTS, DEFAULT_SLOT_ROWS = 1024, 64
+
+
+def _ring_mod():
+    from .. import _fdx_ring  # host-only C++ (no HIP): front-ends import it without a GPU context
+
+    return _fdx_ring
+
+
+class GpuOwner:
+    """Collector thread: ring -> pinned batch -> one launch -> results back to the slots."""
+
+    def __init__(self, engine, ring_path: str = "", max_batch: int = 8192, window_us: float = 0.0,
+                 nslots: int = DEFAULT_SLOTS, slot_rows: int = DEFAULT_SLOT_ROWS, metrics=None):
+        R = _ring_mod()
+        self.engine = engine
+        self.max_batch = int(max_batch)
+        self.window_us = float(window_us)
+        self.metrics = metrics
+        self.ring = R.Ring(ring_path, nslots, engine.d, slot_rows, engine.d + 2)
+        self.ring_path = ring_path
+        env = os.environ.get("FDX_HOST_MAX_ROWS", "").strip()
+        self.ring.host_max_rows = int(env) if env and int(env) >= 0 else int(min(engine.host_max_rows, 1 << 30))
+        self._buf = engine.owner_input(self.max_batch)
+        self._stop = threading.Event()
+        self._th = threading.Thread(target=self._loop, name="fdx-gpu-owner", daemon=True)
+        self.batches = 0
+        self.rows = 0
+
+    def start(self) -> "GpuOwner":
+        self._th.start()
+        self.ring.owner_state = _ring_mod().OWNER_READY
+        return self
+
+    def stop(self):
+        self._stop.set()
+        self._th.join(timeout=5)
+        self.ring.owner_state = _ring_mod().OWNER_STOPPED
+
+    def _loop(self):
+        ring, eng = self.ring, self.engine
+        while not self._stop.is_set():
+            n, op = ring.collect(self._buf, self.max_batch, self.window_us, 50.0)
+            if n == 0:
+                continue
+            try:
+                p, z, phi, dphi = eng.run_staged(n, op == OP_EXPLAIN)
+                ring.complete(p, z, phi, dphi, True)
+            except Exception:  # noqa: BLE001 - fail the batch, keep serving
+                logger.exception("GPU owner batch of %d rows failed", n)
+                ring.complete(0, 0, 0, 0, False)
+                continue
+            self.batches += 1
+            self.rows += n
+            if self.metrics is not None:
+                self.metrics.microbatch_size.observe(n)
+
+
+class RingClient:
+    """Front-end side of the ring (attach by path, or share an in-process GpuOwner's ring)."""
+
+    def __init__(self, ring_or_path, timeout_ms: float = 10_000.0):
+        self.ring = _ring_mod().Ring(ring_or_path) if isinstance(ring_or_path, str) else ring_or_path
+        self.d = self.ring.d
+        self.timeout_ms = timeout_ms
+
+    @property
+    def host_max_rows(self) -> int:
+        return int(self.ring.host_max_rows)
+
+    def owner_alive(self) -> bool:
+        R = _ring_mod()
+        if self.ring.owner_state != R.OWNER_READY:
+            return False
+        try:
+            os.kill(self.ring.owner_pid, 0)
+            return True
+        except OSError:
+            return False
+
+    def predict_proba(self, X: np.ndarray):
+        o = self.ring.request(np.ascontiguousarray(X, np.float32), OP_PREDICT, self.timeout_ms)
+        return o[:, 0].astype(np.float64), o[:, 1].astype(np.float64)
+
+    def predict_explain(self, X: np.ndarray):
+        o = self.ring.request(np.ascontiguousarray(X, np.float32), OP_EXPLAIN, self.timeout_ms)
+        return o[:, 0].astype(np.float64), o[:, 1].astype(np.float64), o[:, 2:2 + self.d].astype(np.float64)
+
+    def stats(self) -> dict:
+        return dict(self.ring.stats())
+
+
+class Dispatcher:
+    """Routes one front-end's scoring: small batches on the host, the rest through the ring.
+
+    ``engine`` is this process's engine (a CPU engine in a multi-worker front-end; the GPU engine
+    itself when the owner runs in-process) -- its exact host path serves the small batches.
+    ``client`` is None when there is no GPU owner (CPU deployment): everything runs on ``engine``.
+    """
+
+    def __init__(self, engine, client: RingClient | None = None, owner: GpuOwner | None = None,
+                 host_max_rows: int | None = None, metrics=None):
+        self.engine, self.client, self.owner, self.metrics = engine, client, owner, metrics
+        self._host_max = host_max_rows
+
+    @property
+    def host_max_rows(self) -> int:
+        if self._host_max is not None:
+            return self._host_max
+        if self.client is not None:
+            v = self.client.host_max_rows
+            return v if v >= 0 else 0
+        return 1 << 62
+
+    @property
+    def enabled(self) -> bool:  # a GPU owner batches this process's device work
+        return self.client is not None
+
+    def _host(self, X):
+        p, z = self.engine._predict_host(X)[:2]
+        if self.metrics is not None:
+            self.metrics.host_rows.inc(X.shape[0])
+        return p, z
+
+    def predict_proba(self, X: np.ndarray):
+        X = np.ascontiguousarray(X, np.float32)
+        if self.client is None:
+            return self.engine.predict_proba(X)
+        if X.shape[0] <= self.host_max_rows:
+            return self._host(X)
+        try:
+            return self.client.predict_proba(X)
+        except RuntimeError as e:  # owner gone or timed out: degrade to the host path, loudly
+            logger.error("GPU owner unavailable (%s): scoring %d rows on the host", e, X.shape[0])
+            return self._host(X)
+
+    def predict_one(self, x: np.ndarray):
+        p, z = self.predict_proba(x.reshape(1, -1))
+        return float(p[0]), float(z[0])
+
+    def close(self):
+        if self.owner is not None:
+            self.owner.stop()
+            self.owner = None
+
+
+def in_process(engine, window_us: float, max_batch: int, metrics=None) -> Dispatcher:
+    """Single-worker deployment: the owner thread lives in this process (anonymous ring)."""
+    if engine.device.type != "cuda":
+        return Dispatcher(engine, metrics=metrics)
+    owner = GpuOwner(engine, "", max_batch=max_batch, window_us=window_us, metrics=metrics).start()
+    return Dispatcher(engine, RingClient(owner.ring), owner, metrics=metrics)
+
+
+def main(argv=None) -> int:
+    """The GPU-owner process: load the production engine on the GPU, create the ring, serve."""
+    ap = argparse.ArgumentParser(description="GPU-owner process for multi-worker serving")
+    ap.add_argument("--ring", required=True, help="ring file (under /dev/shm)")
+    ap.add_argument("--window-us", type=float, default=float(os.getenv("FDX_MICROBATCH_US", "0")))
+    ap.add_argument("--max-batch", type=int, default=int(os.getenv("FDX_MICROBATCH_MAX", "8192")))
+    ap.add_argument("--slots", type=int, default=DEFAULT_SLOTS)
+    ap.add_argument("--slot-rows", type=int, default=DEFAULT_SLOT_ROWS)
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(name)s - %(levelname)s - %(message)s")
+    from ..config import Settings
+    from ..obs.metrics import api_metrics
+    from .app import load_production_engine
+
+    s = Settings.load()
+    eng, src = load_production_engine(s, s.device)
+    tmp = a.ring + ".tmp"
+    owner = GpuOwner(eng, tmp, max_batch=a.max_batch, window_us=a.window_us, nslots=a.slots,
+                     slot_rows=a.slot_rows, metrics=api_metrics())
+    os.replace(tmp, a.ring)  # front-ends never see a half-initialised ring
+    owner.start()
+    logger.info("GPU owner pid %d serving %s model (%s) on %s via %s; host path <= %d rows", os.getpid(), eng.kind,
+                src, eng.device, a.ring, owner.ring.host_max_rows)
+    done = threading.Event()
+    signal.signal(signal.SIGTERM, lambda *_: done.set())
+    signal.signal(signal.SIGINT, lambda *_: done.set())
+    while not done.wait(0.5):
+        pass
+    owner.stop()
+    try:
+        os.unlink(a.ring)
+    except OSError:
+        pass
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

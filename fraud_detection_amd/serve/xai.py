@@ -2,10 +2,13 @@
 dead duplicate api/worker.py:65-102).
 
 One worker lease = one batched device explanation: every leased task's features are stacked into
-one [B, 30] matrix, scored, and explained -- by KernelSHAP (BASELINE config 4: the MFMA coalition
-GEMM for the linear model, the masked-row tree kernel for GBDT; background = the training rows
-saved with the model) or LinearSHAP (fused predict + phi kernel) when ``FDX_XAI_METHOD=linear`` or
-no background exists -- then all rows are upserted in one DB transaction into BOTH
+one [B, 30] matrix, scored, and explained -- by default with the model family's explainer
+(LinearSHAP for the linear model: log-odds attributions, the reference worker's semantics,
+xai_tasks.py:103-115 / api/worker.py:53; KernelSHAP for GBDT), and with KernelSHAP when
+``FDX_XAI_METHOD=kernel`` (BASELINE config 4: the MFMA coalition GEMM, probability space,
+background = the training rows saved with the model; the stored ``explainer`` field says which)
+or interventional TreeSHAP when ``FDX_XAI_METHOD=tree`` -- then all rows are upserted in one DB
+transaction into BOTH
 ``transaction_results`` (status COMPLETED, prediction_score, shap_values) and
 ``shap_explanations`` (what /explain reads, with the explainer and its base value).  The model is
 the one the API serves: the registry alias, else the local artifacts (either family).  Scaling

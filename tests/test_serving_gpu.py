@@ -42,7 +42,8 @@ def restore_service():
     svc.settings, svc._engine, svc._injected, svc.device = None, None, False, os.getenv("FDX_DEVICE", "auto")
 
 
-def test_gpu_predict_goldens_through_microbatcher(dev, tmp_path, restore_service):
+def test_gpu_predict_goldens_through_microbatcher(dev, tmp_path, restore_service, monkeypatch):
+    monkeypatch.setenv("FDX_HOST_MAX_ROWS", "0")  # every request through the GPU owner's batches
     app, _ = _cuda_service(tmp_path, mlflow_tracking_uri=f"file:{tmp_path}/none")
     with TestClient(app) as c:
         eng = app.state.fdx["engine"]
@@ -63,10 +64,11 @@ def test_gpu_predict_goldens_through_microbatcher(dev, tmp_path, restore_service
         assert 'fdx_gpu_kernel_seconds_count{kernel="predict"}' in m
 
 
-def test_gpu_worker_kernelshap_roundtrip(dev, tmp_path, restore_service):
+def test_gpu_worker_kernelshap_roundtrip(dev, tmp_path, restore_service, monkeypatch):
     """POST /predict -> queue -> worker (CUDA, one batched KernelSHAP launch) -> GET /explain."""
     from fraud_detection_amd.models.explainers import kernelshap_reference
 
+    monkeypatch.setenv("FDX_XAI_METHOD", "kernel")
     mdir = linear_dir_with_background(tmp_path)
     app, xt = _cuda_service(tmp_path, model_path=os.path.join(mdir, "logistic_model.joblib"),
                             mlflow_tracking_uri=f"file:{tmp_path}/none")
@@ -122,6 +124,7 @@ def test_engine_staging_reuses_pinned_buffers(dev):
     from fraud_detection_amd.serve.engine import InferenceEngine
 
     eng = InferenceEngine.from_paths(device="cuda")
+    eng.host_max_rows = 0  # this test is about the device staging paths
     p1, _ = eng.predict_proba(np.asarray([GOLDEN_SAMPLE], np.float32))
     assert eng._stage.zero_copy(1), "pinned host buffers must be device-mapped on MI355X"
     buf = eng._stage.hin.data_ptr()
@@ -139,9 +142,51 @@ def test_engine_staging_reuses_pinned_buffers(dev):
     eng.predict_proba(X2[:5])
     assert eng._stage.hin.data_ptr() == buf            # no per-request pinned allocation
     assert p1[0] == pytest.approx(0.011905, abs=5e-7)
+    assert eng.calibration["source"] == "measured" and eng.calibration["sizes"]
     cpu = InferenceEngine.from_paths(device="cpu")
     X = kaggle_like_rows(300, seed=2)
     pg, zg, phig = eng.predict_explain(X)
     pc, zc, phic = cpu.predict_explain(X)
     np.testing.assert_allclose(pg, pc, atol=2e-6)
     np.testing.assert_allclose(phig, phic, rtol=1e-4, atol=1e-4)
+
+
+def test_engine_routes_small_batches_to_the_host(dev):
+    """a GPU engine measures host vs device at start-up; batches at or below the
+    threshold run on the exact fp64 host path (bit-identical to the CPU engine), larger ones on
+    the device kernel (fp32, within 2e-6)."""
+    from fraud_detection_amd.serve.engine import InferenceEngine
+
+    eng = InferenceEngine.from_paths(device="cuda")
+    cpu = InferenceEngine.from_paths(device="cpu")
+    thr = eng.host_max_rows
+    assert thr >= 1, eng.calibration  # one row: a launch + sync always costs more than 30 FMAs
+    X = kaggle_like_rows(thr + 64, seed=8)
+    ph, zh = eng.predict_proba(X[:thr])
+    pc, zc = cpu.predict_proba(X[:thr])
+    assert np.array_equal(ph, pc) and np.array_equal(zh, zc)
+    pd, _ = eng.predict_proba(X)
+    pc2, _ = cpu.predict_proba(X)
+    np.testing.assert_allclose(pd, pc2, atol=2e-6)
+
+
+def test_host_to_host_batch_predict_is_bit_identical(dev):
+    """Config 2 host-to-host path (page-locked caller rows, H2D | kernel | D2H pipelined, fp64
+    written by the kernel) returns exactly what the staged fp32 path + host widening returned."""
+    from fraud_detection_amd.serve import engine as E
+    from fraud_detection_amd.serve.engine import InferenceEngine
+
+    eng = InferenceEngine.from_paths(device="cuda")
+    eng.host_max_rows = 0
+    X = kaggle_like_rows(E.H2H_CHUNK_ROWS * 2 + 777, seed=21)  # several pipeline chunks + a tail
+    p_h, z_h = eng._device_h2h(X)
+    p_s, z_s, _ = eng._device_run(X, False)
+    assert np.array_equal(p_h, p_s) and np.array_equal(z_h, z_s)
+    out = (np.empty(len(X)), np.empty(len(X)))
+    r = eng.predict_proba(X, out=out)
+    assert r is out and np.array_equal(out[0], p_s)
+    # a non-page-aligned view of a bigger array (registration of an interior range)
+    Xv = np.ascontiguousarray(kaggle_like_rows(5000, seed=3))[1:]
+    p1, _ = eng._device_h2h(np.ascontiguousarray(Xv))
+    p2, _, _ = eng._device_run(np.ascontiguousarray(Xv), False)
+    assert np.array_equal(p1, p2)

@@ -44,9 +44,31 @@ def restore_service():
     xai_tasks.service._injected = False
 
 
-def test_linear_model_with_background_is_explained_by_kernelshap(tmp_path, restore_service):
+def test_linear_model_default_is_linearshap(tmp_path, restore_service):
+    """the default explainer of the linear model stays LinearSHAP (log-odds, the
+    reference worker's semantics) even when a KernelSHAP background is saved with the model."""
+    mdir = linear_dir_with_background(tmp_path)
+    app, xt = _service(tmp_path, model_path=os.path.join(mdir, "logistic_model.joblib"),
+                       scaler_path=os.path.join(mdir, "scaler.joblib"),
+                       feature_names_path=os.path.join(mdir, "feature_names.json"),
+                       mlflow_tracking_uri=f"file:{tmp_path}/none")
+    rows = kaggle_like_rows(3, seed=9)
+    with TestClient(app) as c:
+        tx = str(uuid.uuid4())
+        assert c.post("/predict", json={"features": rows[0].tolist(), "transaction_id": tx}).status_code == 200
+        assert Worker(xt.celery_app, batch=64).run_once() == 1
+        e = c.get(f"/explain/{tx}").json()
+        assert e["explainer"] == "linear"
+        eng = app.state.fdx["engine"]
+        p, z, phi = eng.predict_explain(rows[:1])
+        np.testing.assert_allclose([e["shap_values"][n] for n in e["feature_names"]], phi[0], atol=1e-9)
+
+
+def test_linear_model_with_background_is_explained_by_kernelshap(tmp_path, restore_service, monkeypatch):
     from fraud_detection_amd.models.explainers import kernelshap_reference
     from fraud_detection_amd.obs import tracing
+
+    monkeypatch.setenv("FDX_XAI_METHOD", "kernel")
 
     mdir = linear_dir_with_background(tmp_path)
     app, xt = _service(tmp_path, model_path=os.path.join(mdir, "logistic_model.joblib"),

@@ -3,17 +3,18 @@
 transform + predict_proba p50 52 us / p99 65 us per row; config 2: batch /predict 1M x 30).
 
 Measured (host wall clock, synchronised, after warm-up), each with the shipped model artifacts:
-  * engine batch=1: InferenceEngine.predict_proba on one row -- pinned upload, fused scaler+GEMV+
-    sigmoid kernel, download -- GPU and the exact fp64 CPU path side by side;
-  * micro-batched: N concurrent single-row submissions through serve/batcher.MicroBatcher (what
-    /predict uses on a GPU), per-request latency percentiles and rows/s;
+  * engine batch=1: InferenceEngine.predict_proba on one row -- the exact fp64 CPU path, the GPU
+    engine as deployed (calibrated small-batch routing: one row runs on the host) and the GPU
+    engine forced onto the device (pinned zero-copy, fused scaler+GEMV+sigmoid kernel, sync);
+  * ring micro-batched: P producer processes x T threads, each submitting single rows through
+    the shared-memory ring to ONE GPU-owner process (serve/gpu_owner.py: continuous batching,
+    one fused launch per batch) -- rows/s and per-request latency percentiles;
   * HTTP: /predict through the FastAPI app in-process (TestClient), p50/p99 per request;
   * config 2: 1M rows in one call (host in, host out) and the device-only kernel rate.
 
     python tools/serve_latency.py [--json out.json] [--reps 2000]
 """
 import argparse
-import asyncio
 import json
 import os
 import sys
@@ -42,28 +43,67 @@ def engine_batch1(eng, x, reps):
     return pct(t)
 
 
-async def microbatched(eng, rows, concurrency, window_us):
-    from fraud_detection_amd.serve.batcher import MicroBatcher
+def _producer(ring, threads, per_thread, q):
+    import threading
 
-    b = MicroBatcher(eng, window_us, 4096)
-    await b.start()
-    lat = []
+    from fraud_detection_amd.serve.gpu_owner import RingClient
 
-    async def one(r):
-        t0 = time.perf_counter()
-        await b.submit(r)
-        lat.append(time.perf_counter() - t0)
+    cli = RingClient(ring)
+    rows = np.random.default_rng(os.getpid()).normal(0, 1, (256, 30)).astype(np.float32)
+    lat = [[] for _ in range(threads)]
 
-    for i in range(0, 512, concurrency):  # warm-up
-        await asyncio.gather(*[one(r) for r in rows[i:i + concurrency]])
-    lat.clear()
+    def th(k):
+        for i in range(per_thread):
+            t0 = time.perf_counter()
+            cli.predict_proba(rows[i % 256:i % 256 + 1])
+            lat[k].append(time.perf_counter() - t0)
+
+    for i in range(200):  # warm-up
+        cli.predict_proba(rows[i % 256:i % 256 + 1])
+    ts = [threading.Thread(target=th, args=(k,)) for k in range(threads)]
     t0 = time.perf_counter()
-    for i in range(0, len(rows), concurrency):
-        await asyncio.gather(*[one(r) for r in rows[i:i + concurrency]])
-    dt = time.perf_counter() - t0
-    await b.stop()
-    return {"requests": len(rows), "concurrency": concurrency, "window_us": window_us,
-            "rows_per_sec": round(len(rows) / dt, 1), **pct(lat)}
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    q.put((t0, time.perf_counter(), [x for ls in lat for x in ls]))
+
+
+def ring_microbatched(procs, threads, per_thread, window_us=0):
+    """P producer processes x T threads of single-row requests -> one GPU-owner process."""
+    import multiprocessing as mp
+    import subprocess
+
+    ring = f"/dev/shm/fdx_lat_ring_{os.getpid()}"
+    env = dict(os.environ, FDX_MICROBATCH_US=str(window_us))
+    owner = subprocess.Popen([sys.executable, "-m", "fraud_detection_amd.serve.gpu_owner", "--ring", ring], env=env)
+    try:
+        t_end = time.time() + 240
+        while not os.path.exists(ring):
+            if owner.poll() is not None or time.time() > t_end:
+                raise RuntimeError("GPU owner did not start")
+            time.sleep(0.05)
+        ctx = mp.get_context("spawn")
+        q = ctx.Queue()
+        ps = [ctx.Process(target=_producer, args=(ring, threads, per_thread, q)) for _ in range(procs)]
+        for p in ps:
+            p.start()
+        res = [q.get(timeout=600) for _ in ps]
+        for p in ps:
+            p.join()
+        from fraud_detection_amd.serve.gpu_owner import RingClient
+
+        st = RingClient(ring).stats()
+    finally:
+        owner.terminate()
+        owner.wait(timeout=30)
+    t0 = min(r[0] for r in res)
+    t1 = max(r[1] for r in res)
+    lat = [x for r in res for x in r[2]]
+    n = procs * threads * per_thread
+    return {"producers": procs, "threads_per_producer": threads, "requests": n, "window_us": window_us,
+            "rows_per_sec": round(n / (t1 - t0), 1), "mean_rows_per_launch": round(st["rows"] / max(st["batches"], 1), 2),
+            **pct(lat)}
 
 
 def http(eng_device, reps):
@@ -117,9 +157,13 @@ def main():
     out["cpu_fp64_batch1"] = engine_batch1(cpu, x1, a.reps)
     if torch.cuda.is_available():
         gpu = InferenceEngine.from_paths(device="cuda")
-        out["gpu_batch1"] = engine_batch1(gpu, x1, a.reps)
-        rows = [r for r in rng.normal(0, 1, (20_000, 30)).astype(np.float32)]
-        out["gpu_microbatched"] = [asyncio.run(microbatched(gpu, rows, c, w)) for c, w in ((64, 200), (512, 300))]
+        out["gpu_engine_calibration"] = {"host_max_rows": gpu.host_max_rows, **gpu.calibration}
+        out["gpu_engine_batch1_routed"] = engine_batch1(gpu, x1, a.reps)
+        thr = gpu.host_max_rows
+        gpu.host_max_rows = 0
+        out["gpu_engine_batch1_device"] = engine_batch1(gpu, x1, a.reps)
+        gpu.host_max_rows = thr
+        out["ring_microbatched"] = [ring_microbatched(p, t, n) for p, t, n in ((4, 8, 2000), (8, 8, 2000), (12, 8, 1500))]
         X = rng.normal(0, 1, (1_000_000, 30)).astype(np.float32)
         for _ in range(3):
             gpu.predict_proba(X)
