@@ -26,4 +26,6 @@ USER appuser
 
 EXPOSE 8000 8001
 ENTRYPOINT ["/app/run_migrations.sh"]
-CMD ["uvicorn", "api.app:app", "--host", "0.0.0.0", "--port", "8000", "--workers", "1"]
+# one GPU-owner process + 2 HTTP workers forwarding through a shared-memory ring (serve/launch.py);
+# the reference ran gunicorn --workers 2 with a model copy per worker (Dockerfile:21)
+CMD ["python", "-m", "fraud_detection_amd.serve.launch", "--host", "0.0.0.0", "--port", "8000", "--workers", "2"]

@@ -13,28 +13,11 @@ namespace fdx {
 
 // FDX_SYNC_LAUNCH=1: synchronise after every launch so an asynchronous fault is reported with
 // the name of the kernel that caused it (debug mode, like AMD_SERIALIZE_KERNEL=3 but attributed).
-// Streaming (nontemporal) stores for the big write-once outputs (fused scaler rows, SMOTE rows):
-// on by default (bench 1.487 -> 1.469 ms, SMOTE 164 -> 150 us: the output stream no longer
-// evicts the L2-resident parent rows; profiles/r1_s26); FDX_NT_STORES=0 for A/B runs.
-inline bool nt_stores() {
-  static const bool on = [] {
-    const char* e = std::getenv("FDX_NT_STORES");
-    return e == nullptr || e[0] != '0';
-  }();
-  return on;
-}
-
-// The fused scaler pass's row stream: plain stores by default.  Measured on the current kernel
-// (profiles/r2_s6/nt_stores_ab.txt): 269 us plain vs 280 us nontemporal, while the SMOTE output
-// keeps the nontemporal policy (122 vs 127 us).  FDX_NT_SCALER=1 restores nontemporal stores here;
-// FDX_NT_STORES=0 turns them off everywhere.
-inline bool nt_stores_scaler() {
-  static const bool on = [] {
-    const char* e = std::getenv("FDX_NT_SCALER");
-    return nt_stores() && e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
+// Store policy of the big write-once outputs, fixed by measurement (the A/B switches are gone):
+// SMOTE rows use streaming (nontemporal) stores -- the output stream no longer evicts the
+// L2-resident parent rows (SMOTE 164 -> 150 us, profiles/r1_s26; 122 vs 127 us on the current
+// kernel, profiles/r2_s6) -- while the fused scaler pass's rows use plain stores (269 us plain vs
+// 280 us nontemporal, profiles/r2_s6/nt_stores_ab.txt).
 
 inline bool sync_launch_mode() {
   static const int mode = [] {

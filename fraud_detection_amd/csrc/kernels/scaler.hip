@@ -762,8 +762,7 @@ void launch_fp8_prescale(const float* X, int64_t n, int d, int64_t ns, int64_t s
 
 int scaler_stats_cast_blocks() {
   static const int cap = resident_cap(scaler_stats_cast_kernel<false, false>, kThreads);
-  static const int cap_nt = resident_cap(scaler_stats_cast_kernel<true, false>, kThreads);
-  return nt_stores_scaler() ? cap_nt : cap;
+  return cap;
 }
 
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
@@ -776,12 +775,9 @@ void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* piv
 #define FDX_SSC(NT, F8)                                                                                 \
   scaler_stats_cast_kernel<NT, F8><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value, \
                                                                      out, partial, colscale, out_scale)
-  const bool fp8 = colscale != nullptr;
-  if (nt_stores_scaler()) {
-    if (fp8) FDX_SSC(true, true); else FDX_SSC(true, false);
-  } else {
-    if (fp8) FDX_SSC(false, true); else FDX_SSC(false, false);
-  }
+  // plain row stores (launchers.h: nontemporal ones measured slower for this pass)
+  if (colscale != nullptr) FDX_SSC(false, true);
+  else FDX_SSC(false, false);
 #undef FDX_SSC
   check_launch("scaler_stats_cast");
 }

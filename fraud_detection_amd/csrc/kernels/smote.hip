@@ -244,15 +244,10 @@ void launch_smote_generate(const void* C, int parents_bf16, const int* nbr, int 
         C, nbr, mq, k, q_offset, n_new, sample_offset, k0, k1, c0, c1, label, out_scale, aff, out);   \
   } while (0)
   const bool pb = parents_bf16 != 0;
-  // both halves' gathers up front (default; 125.7 -> 122.4 us at 8M samples, profiles/r2_s6/
-  // smote_g2_ab.txt); FDX_SMOTE_G2=0 restores the per-half gathers for A/B
-  static const bool g2 = [] {
-    const char* e = std::getenv("FDX_SMOTE_G2");
-    return e == nullptr || e[0] != '0';
-  }();
-  if (out_kind == 0 && nt_stores() && pb && g2) FDX_SG(0, true, true, true);
-  else if (out_kind == 0 && nt_stores()) { if (pb) FDX_SG(0, true, true); else FDX_SG(0, true, false); }
-  else if (out_kind == 0) { if (pb) FDX_SG(0, false, true); else FDX_SG(0, false, false); }
+  // bf16 parents: both halves' gathers up front (125.7 -> 122.4 us at 8M samples, profiles/r2_s6/
+  // smote_g2_ab.txt); nontemporal output stores (launchers.h nt_stores)
+  if (out_kind == 0 && pb) FDX_SG(0, true, true, true);
+  else if (out_kind == 0) FDX_SG(0, true, false);
   else if (out_kind == 1) { if (pb) FDX_SG(1, false, true); else FDX_SG(1, false, false); }
   else { if (pb) FDX_SG(2, false, true); else FDX_SG(2, false, false); }
 #undef FDX_SG

@@ -214,19 +214,15 @@ class DevicePipeline:
         if fused:
             # ---- K1+K2 fused: statistics (C1 all-reduce inside) + shifted bf16 / fp8 rows ----
             # ---- class counts (C2) on a side stream beside it; the host reads the total during K1+K2
-            # (profiles/r2_s6: pass first + side-stream count 1.345 ms/fit; count kernels in front
-            # on the compute stream 1.366; side-stream count enqueued before the pass 1.397)
-            if os.environ.get("FDX_COUNT_SIDE", "1") == "1":
-                if self._side is None or self._side.device != dev:
-                    self._side = torch.cuda.Stream(dev)
-                    self._ready = torch.cuda.Event()  # re-recorded every fit (a wait binds the latest record)
-                ready = self._ready
-                ready.record()
-                stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
-                pending = scaler_ops.compact_indices_async(y, 1, side=self._side, ready=ready)
-            else:  # A/B: count kernels in front of the pass on the compute stream
-                pending = scaler_ops.compact_indices_async(y, 1)
-                stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
+            # (profiles/r2_s6/count_side_stream_ab.txt: pass first + side-stream count 1.345 ms/fit;
+            # count kernels in front on the compute stream 1.366 -- that variant is deleted)
+            if self._side is None or self._side.device != dev:
+                self._side = torch.cuda.Stream(dev)
+                self._ready = torch.cuda.Event()  # re-recorded every fit (a wait binds the latest record)
+            ready = self._ready
+            ready.record()
+            stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
+            pending = scaler_ops.compact_indices_async(y, 1, side=self._side, ready=ready)
             tm.mark("scaler_fit")
         else:
             # ---- K1: scaler statistics (C1 all-reduce inside) ----------------------------

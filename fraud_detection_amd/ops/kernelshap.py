@@ -10,7 +10,6 @@ part counts differ only in the fp32 summation order of the projection).
 """
 from __future__ import annotations
 
-import os
 
 import numpy as np
 import torch
@@ -78,27 +77,27 @@ def complement_pairs(Z: np.ndarray):
     return np.asarray(base, np.int64), np.asarray(comp, np.int64)
 
 
-def _paired_enabled(link: str) -> bool:
-    """FDX_KS_PAIRED=1/0 forces the complement-paired / unpaired kernel; by default (auto) the
-    paired one runs for the log-odds link only.  Measured on MI355X (profiles/r2_s5): with the
-    sigmoid links both run ~55 us per 1k batch (bound by the sigmoid epilogue's issue rate); the
-    log-odds link has no epilogue and the paired kernel's half MFMA work shows, 25.2 vs 34.4 us."""
-    env = os.environ.get("FDX_KS_PAIRED", "auto")
-    if env in ("0", "1"):
-        return env == "1"
+def _paired_enabled(link: str, paired: bool | None = None) -> bool:
+    """The complement-paired kernel runs for the log-odds link, the unpaired one for the sigmoid
+    links (``paired`` forces one -- tests and tools/ks_check.py).  Measured on MI355X
+    (profiles/r2_s5): with the sigmoid links both run ~55 us per 1k batch (bound by the sigmoid
+    epilogue's issue rate); the log-odds link has no epilogue and the paired kernel's half MFMA
+    work shows, 25.2 vs 34.4 us."""
+    if paired is not None:
+        return bool(paired)
     return link == "logit_model"
 
 
-def _device_design(expl, dev):
+def _device_design(expl, dev, paired: bool | None = None):
     """Upload the linear explainer's design once: Z as bf16 [S_pad, 32] (col 31 = 1 folds the
     background intercepts into the GEMM), A [d-1, S_pad] (zero-padded), A z_M, the weighted
     background rows W and the background logits.
 
-    Paired layout (FDX_KS_PAIRED=1, kernelshap_paired_kernel): Z holds the Ppad base coalitions of the
+    Paired layout (kernelshap_paired_kernel): Z holds the Ppad base coalitions of the
     complement pairs and A [d-1, 2 Ppad] has the base columns first, then each base's complement
     (zero columns for padding and for complements the design does not contain: they carry no
     weight, so the WLS solution is unchanged)."""
-    key = (str(dev), _paired_enabled(expl.link))
+    key = (str(dev), _paired_enabled(expl.link, paired))
     if expl._dev_cache is not None and expl._dev_cache[0] == key:
         return expl._dev_cache[1]
     d = expl.d
@@ -163,21 +162,22 @@ def _outputs(E, d, dev, out):
 
 
 def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | None = None,
-               parts: int | None = None, out=None):
+               parts: int | None = None, out=None, paired: bool | None = None):
     """Linear model.  X [E, d] raw fp32 on device -> (phi [E, d], fx [E], f0) (numpy if sync else
     device tensors).  ``stamps`` (int64 [E, 8], tools/kernelshap_stamps.py): per-explanation phase
     timestamps (forces parts = 1).  ``parts``: coalition parts per explanation (None = auto).
-    ``out``: preallocated (phi, fx, f0) device tensors (e.g. views of one staging buffer)."""
+    ``out``: preallocated (phi, fx, f0) device tensors (e.g. views of one staging buffer).
+    ``paired``: force the complement-paired (True) / unpaired (False) kernel (None: by link)."""
     _check_x(X, expl.d)
     m = native()
     dev = X.device
-    t = _device_design(expl, dev)
+    t = _device_design(expl, dev, False if stamps is not None else paired)
     E = X.shape[0]
     # MFMA tiles of 32 coalitions (paired: 32 base coalitions, i.e. 64 with the complements)
     n_tiles = t["S_pad"] // (64 if t["paired"] else 32)
     if stamps is not None:
         if t["paired"]:
-            raise ValueError("phase stamps exist only in the unpaired kernel (FDX_KS_PAIRED=0)")
+            raise ValueError("phase stamps exist only in the unpaired kernel")
         parts = 1
     elif parts is None:
         # measured (profiles/r2_e): the split's hand-off costs more than the idle CUs it fills

@@ -12,7 +12,6 @@ The device loop never synchronises with the host inside a chunk of iterations: a
 """
 from __future__ import annotations
 
-import os
 import time
 
 from dataclasses import dataclass, field
@@ -330,9 +329,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     # Under DP every queued iteration also queues its gradient all-reduce, which runs in full even
     # when the iteration is a no-op (~15 us per collective at 8 ranks, profiles/r2_s3l): one chunk
     # of slack there (a full-data pass is >= ~60 us, enough to hide the host's wake-up), two alone.
-    if lookahead is None:
-        lookahead = int(os.environ.get("FDX_NEWTON_LOOKAHEAD", "0")) or (
-            1 if (comm is not None and comm.world_size > 1) else 2)
+    if lookahead is None:  # profiles/r2_s5/newton_lookahead_ab.txt
+        lookahead = 1 if (comm is not None and comm.world_size > 1) else 2
     depth = max(1, int(lookahead))
     if getattr(ws, "_flags", None) is None or len(ws._flags) < depth + 1:
         # pinned allocations cost tens of us: once per workspace.  The chunk's last Newton update
@@ -344,8 +342,6 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         ws._events = [torch.cuda.Event() for _ in range(depth + 1)]
         ws._seq = 0
     flags, events, fdev = ws._flags, ws._events, ws._flag_dev
-    if os.environ.get("FDX_NEWTON_FLAG", "map") == "copy":  # A/B: D2H copy + event per check
-        fdev = [0] * len(fdev)
     pending = []
     it, slot = 0, 0
     while it < max_iter:

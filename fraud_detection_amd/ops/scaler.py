@@ -1,7 +1,6 @@
 """K1 scaler statistics / K2 standardize+pad+cast / stable label compaction."""
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 
 import numpy as np
@@ -155,14 +154,11 @@ _GRID_CACHE: dict = {}
 
 
 def _stats_cast_grid(m, dev) -> int:
-    r = int(os.environ.get("FDX_SCALER_RESERVE", "0"))
-    key = (dev.index, r)
+    """Every block of the fused pass resident at once (occupancy-derived).  Leaving block slots
+    free for the side-stream count kernels was measured no faster (profiles/r2_s6, reserveab)."""
+    key = dev.index
     if key not in _GRID_CACHE:
-        cap = int(m.scaler_stats_cast_blocks())
-        if r > 0:
-            cus = torch.cuda.get_device_properties(dev).multi_processor_count
-            cap = max(cus, cap - r * cus)
-        _GRID_CACHE[key] = cap
+        _GRID_CACHE[key] = int(m.scaler_stats_cast_blocks())
     return _GRID_CACHE[key]
 
 
@@ -252,8 +248,7 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
             raise ValueError("scaler_fit_cast: X must be contiguous and 16-byte aligned with d <= 30")
         m = native()
         piv = _pivot_dev(pivot, d, X.device)
-        # all blocks resident at once (occupancy-derived), never more than the tiles;
-        # FDX_SCALER_RESERVE=r leaves r block slots per CU free for kernels running beside the pass
+        # all blocks resident at once (occupancy-derived), never more than the tiles
         nb = max(1, min(_stats_cast_grid(m, X.device), (n + 127) // 128))
         partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
         sums = torch.empty(64, device=X.device, dtype=torch.float64)

@@ -479,7 +479,7 @@ class InferenceEngine(_EngineBase):
                                    z.ctypes.data, P.ptr(self._h2h_x), P.ptr(self._h2h_o[0]), P.ptr(self._h2h_o[1]),
                                    H2H_CHUNK_ROWS, self._h2d_stream.cuda_stream, self._stream.cuda_stream,
                                    self._d2h_stream.cuda_stream)
-        return p, z
+        return (p, z) if out is None else out
 
     def predict_explain(self, X: np.ndarray):
         """X raw features [B, d] -> (prob [B], logit [B], phi [B, d]) as numpy (LinearSHAP)."""

@@ -73,12 +73,21 @@ class GpuOwner:
 
     def _loop(self):
         ring, eng = self.ring, self.engine
+        try:
+            from ..obs.metrics import gpu_kernel_histogram
+
+            hist = gpu_kernel_histogram().labels("owner_batch")
+        except Exception:  # noqa: BLE001 - metrics are best effort
+            hist = None
         while not self._stop.is_set():
             n, op = ring.collect(self._buf, self.max_batch, self.window_us, 50.0)
             if n == 0:
                 continue
             try:
+                t0 = time.perf_counter()
                 p, z, phi, dphi = eng.run_staged(n, op == OP_EXPLAIN)
+                if hist is not None:  # launch + device time + wait of one batch (host clock)
+                    hist.observe(time.perf_counter() - t0)
                 ring.complete(p, z, phi, dphi, True)
             except Exception:  # noqa: BLE001 - fail the batch, keep serving
                 logger.exception("GPU owner batch of %d rows failed", n)

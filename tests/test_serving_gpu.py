@@ -61,7 +61,7 @@ def test_gpu_predict_goldens_through_microbatcher(dev, tmp_path, restore_service
         n_req = [ln for ln in m.splitlines() if ln.startswith("fdx_microbatch_size_count")]
         n_rows = [ln for ln in m.splitlines() if ln.startswith("fdx_microbatch_size_sum")]
         assert float(n_rows[0].split()[-1]) == 64.0 and float(n_req[0].split()[-1]) <= 64.0
-        assert 'fdx_gpu_kernel_seconds_count{kernel="predict"}' in m
+        assert 'fdx_gpu_kernel_seconds_count{kernel="owner_batch"}' in m
 
 
 def test_gpu_worker_kernelshap_roundtrip(dev, tmp_path, restore_service, monkeypatch):

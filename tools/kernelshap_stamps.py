@@ -10,7 +10,6 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-os.environ.setdefault("FDX_KS_PAIRED", "0")  # the stamps live in the unpaired kernel
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

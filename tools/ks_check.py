@@ -57,19 +57,18 @@ def run(setups):
 
     dev = torch.device("cuda", 0)
     for name, (aa, bb, B, Xe) in setups.items():
-        for paired in ("1", "0"):
-            os.environ["FDX_KS_PAIRED"] = paired
+        for paired in (True, False):
             ke = KernelExplainer(aa, bb, B, device="cuda")
             Xd = torch.from_numpy(np.ascontiguousarray(Xe, np.float32)).to(dev)
-            phi, fx, f0 = kernelshap(Xd, ke)
+            phi, fx, f0 = kernelshap(Xd, ke, paired=paired)
             ref = kernelshap_reference(Xe[:200], ke.a, ke.bias, ke.B, ke.Z, ke.A, ke.zM, "identity")
             err = np.abs(phi[:200] - ref[0])
             for _ in range(10):
-                kernelshap(Xd, ke, sync=False)
+                kernelshap(Xd, ke, sync=False, paired=paired)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(50):
-                kernelshap(Xd, ke, sync=False)
+                kernelshap(Xd, ke, sync=False, paired=paired)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / 50
             zx = Xe.astype(np.float64) @ ke.a[:30] + ke.bias
