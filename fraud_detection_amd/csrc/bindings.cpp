@@ -372,9 +372,10 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_auc_count(P<const float>(scores), P<const uint8_t>(labels), n, P<const float>(pos),
                           P<const unsigned long long>(counter), chunk, nchunks, P<unsigned long long>(out), S(s));
   });
-  m.def("auc_segments", [](u s_sorted, u pos_incl, u seg_start, int64_t n, u out, u s) {
-    fdx::launch_auc_segments(P<const float>(s_sorted), P<const int64_t>(pos_incl), P<const int64_t>(seg_start), n,
-                             P<unsigned long long>(out), S(s));
+  m.def("auc_radix_workspace_bytes", &fdx::auc_radix_workspace_bytes);
+  m.def("auc_radix", [](u scores, u labels, int64_t n, u ws, u res, u auc, u s) {
+    fdx::launch_auc_radix(P<const float>(scores), P<const uint8_t>(labels), n, P<void>(ws), P<int64_t>(res),
+                          P<double>(auc), S(s));
   });
   m.def("confusion", [](u scores, u labels, int64_t n, float thr, u out4, u s) {
     fdx::launch_confusion(P<const float>(scores), P<const uint8_t>(labels), n, thr, P<unsigned long long>(out4), S(s));

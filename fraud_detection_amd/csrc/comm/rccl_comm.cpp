@@ -14,6 +14,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <vector>
 
 namespace py = pybind11;
 
@@ -31,6 +32,18 @@ ncclDataType_t dtype_of(int k) {
     case 3: return ncclUint8;
     case 4: return ncclInt32;
     case 5: return ncclBfloat16;
+    default: throw std::runtime_error("rccl: unsupported dtype code");
+  }
+}
+
+size_t size_of(int k) {
+  switch (k) {
+    case 0: return 4;
+    case 1: return 8;
+    case 2: return 8;
+    case 3: return 1;
+    case 4: return 4;
+    case 5: return 2;
     default: throw std::runtime_error("rccl: unsupported dtype code");
   }
 }
@@ -84,6 +97,34 @@ PYBIND11_MODULE(_fdx_comm, m) {
     check(ncclAllGather(reinterpret_cast<const void*>(sendbuf), reinterpret_cast<void*>(recvbuf), count,
                         dtype_of(dtype), C(comm), S(stream)),
           "AllGather");
+  });
+  // Variable-count all-gather (collective C3: SMOTE minority rows, k-NN neighbour lists, test
+  // scores): every rank sends its rows straight to every peer over its own xGMI link (grouped
+  // point-to-point -- on a fully connected 8-GPU node each pair has a direct link, so the payload
+  // is not relayed around a ring) and receives each peer's rows at that peer's displacement of
+  // the compact output; its own rows are a local D2D copy.  No padding to the largest count and no
+  // concatenation afterwards.  counts / displs are in elements.
+  m.def("all_gatherv", [](uintptr_t comm, uintptr_t send, size_t send_count, uintptr_t recv,
+                          std::vector<size_t> counts, std::vector<size_t> displs, int dtype, int rank,
+                          uintptr_t stream) {
+    const size_t es = size_of(dtype);
+    const int nranks = (int)counts.size();
+    if ((int)displs.size() != nranks || rank < 0 || rank >= nranks || counts[rank] != send_count)
+      throw std::runtime_error("rccl all_gatherv: inconsistent counts");
+    ncclDataType_t dt = dtype_of(dtype);
+    char* out = reinterpret_cast<char*>(recv);
+    check(ncclGroupStart(), "GroupStart");
+    for (int p = 0; p < nranks; ++p) {
+      if (p == rank) continue;
+      if (send_count) check(ncclSend(reinterpret_cast<const void*>(send), send_count, dt, p, C(comm), S(stream)), "Send");
+      if (counts[p]) check(ncclRecv(out + displs[p] * es, counts[p], dt, p, C(comm), S(stream)), "Recv");
+    }
+    check(ncclGroupEnd(), "GroupEnd");
+    if (send_count && out + displs[rank] * es != reinterpret_cast<char*>(send)) {
+      hipError_t e = hipMemcpyAsync(out + displs[rank] * es, reinterpret_cast<const void*>(send), send_count * es,
+                                    hipMemcpyDeviceToDevice, S(stream));
+      if (e != hipSuccess) throw std::runtime_error(std::string("all_gatherv local copy: ") + hipGetErrorString(e));
+    }
   });
   m.def("broadcast", [](uintptr_t comm, uintptr_t buf, size_t count, int dtype, int root, uintptr_t stream) {
     check(ncclBroadcast(reinterpret_cast<const void*>(buf), reinterpret_cast<void*>(buf), count, dtype_of(dtype),

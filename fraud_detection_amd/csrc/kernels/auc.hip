@@ -4,8 +4,8 @@
 // (train_model.py:83,109; evaluate_model.py:31,45,49-50).
 //
 // Exact AUC = (#{(p,n): s_p > s_n} + 0.5 #{(p,n): s_p == s_n}) / (P N).
-// Fraud data is heavily imbalanced, so instead of sorting all N scores we sort only the positive
-// class (compacted, then bitonic-sorted in LDS chunks of <= 16384 floats = 64 KiB) and let every
+// Fraud data is heavily imbalanced, so (small positive class) instead of sorting all N scores we
+// sort only the positive class (compacted, then bitonic-sorted in LDS chunks of <= 16384 floats = 64 KiB) and let every
 // negative count its rank inside each sorted chunk by binary search in LDS.  Integer pair counts
 // are reduced with 64-bit integer atomics, so the result is exact (ties averaged exactly like
 // sklearn) and bitwise deterministic.  Cost ~ N log2(chunk) LDS probes per chunk.
@@ -194,42 +194,212 @@ __global__ __launch_bounds__(1024) void auc_hist_reduce_kernel(const unsigned* _
   }
 }
 
-// Exact AUC for any class balance (the chunked path above costs ~N log(chunk) per 16384
-// positives, quadratic in spirit once positives are common).  Input: the scores sorted ascending
-// (rocPRIM radix sort through torch.sort), the inclusive prefix count of positives in that order
-// and, per element, the index where its tie segment starts (inclusive max-scan of the segment-
-// start positions).  The thread at each segment end adds
-//     pos_in_seg * (2 * neg_before_seg + neg_in_seg)
-// -- twice the pairs the segment's positives win plus the ties -- as an exact 64-bit integer:
-// the sum is order independent, so the result is bitwise deterministic and equal to sklearn's
-// tie-averaged AUC.  O(N) after the sort.
-__global__ __launch_bounds__(kThreads) void auc_segments_kernel(const float* __restrict__ s,
-                                                                const int64_t* __restrict__ pos_incl,
-                                                                const int64_t* __restrict__ seg_start,
-                                                                int64_t n, unsigned long long* __restrict__ out) {
-  unsigned long long acc = 0;
+// ---- exact AUC for any class balance: native LSD radix sort + one counting pass -------------
+// The chunked path above costs ~N log(chunk) per 16384 positives (quadratic in spirit once
+// positives are common).  Here the (score, label) pairs are sorted by (score, label) -- a stable
+// LSD radix sort of the 32-bit order-preserving score key, with the label as the least significant
+// "digit" (pass 0) so inside a tie the negatives come first -- and then, with i the sorted index:
+//   sum over positives of #neg with key <= key_i  =  sum_pos (i - #pos before i)
+//                                                  =  S1 - P (P - 1) / 2,   S1 = sum_pos i
+//   twice_pairs = 2 (S1 - P (P - 1) / 2) - T,      T = sum over tie segments of P_seg N_seg
+// (2 #{s_p > s_n} + #{s_p == s_n} = sum_pos (2 #neg< + #neg=) = 2 sum_pos #neg<= - sum_pos #neg=).
+// T needs the segment bounds only where a segment mixes the classes: at its first positive (its
+// predecessor is a negative of the same key) two binary searches find [lo, hi).  All counts are
+// 64-bit integers (order independent): bitwise deterministic and equal to sklearn's tie-averaged
+// roc_auc_score.  Each radix pass = digit histogram per block -> one-block exclusive scan (digit-
+// major, so offsets are stable across blocks) -> stable scatter (per 256-key sub-chunk: wave-level
+// match of equal digits by 8 ballots, ranks = popcount of lower peers, waves ordered through LDS).
+constexpr int kRadixBlocks = 1024;
+
+__device__ __forceinline__ uint32_t radix_digit(uint32_t k, uint8_t l, int shift) {
+  return shift < 0 ? (uint32_t)l : ((k >> shift) & 255u);
+}
+
+__global__ __launch_bounds__(kThreads) void radix_init_kernel(const float* __restrict__ s,
+                                                              const uint8_t* __restrict__ y, int64_t n,
+                                                              uint32_t* __restrict__ key, uint8_t* __restrict__ lab) {
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
-    const bool end = (i == n - 1) || !(s[i] == s[i + 1]);
-    if (!end) continue;
-    const int64_t st = seg_start[i];
-    const int64_t pos_before = st > 0 ? pos_incl[st - 1] : 0;
-    const int64_t pos_in = pos_incl[i] - pos_before;
-    const int64_t neg_in = (i + 1 - st) - pos_in;
-    const int64_t neg_before = st - pos_before;
-    acc += (unsigned long long)pos_in * (unsigned long long)(2 * neg_before + neg_in);
+    key[i] = order_key(s[i]);
+    lab[i] = y[i] != 0 ? 1 : 0;
   }
-  acc = wave_sum(acc);
-  if (lane_id() == 0 && acc != 0ull) atomicAdd(out, acc);
+}
+
+__global__ __launch_bounds__(kThreads) void radix_hist_kernel(const uint32_t* __restrict__ key,
+                                                              const uint8_t* __restrict__ lab, int64_t n,
+                                                              int shift, int64_t per_blk,
+                                                              uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[256];
+  const int t = threadIdx.x;
+  h[t] = 0;
+  __syncthreads();
+  const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(n, b0 + per_blk);
+  for (int64_t i = b0 + t; i < b1; i += kThreads) atomicAdd(&h[radix_digit(key[i], lab[i], shift)], 1u);
+  __syncthreads();
+  hist[(int64_t)t * gridDim.x + blockIdx.x] = h[t];  // digit-major: the scan order = stable order
+}
+
+// In-place exclusive scan of `total` uint32 counts (digit-major [256][nblk]); one 1024-thread
+// block, each thread a contiguous run.
+__global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__ a, int total) {
+  __shared__ uint32_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (total + 1023) / 1024;
+  const int lo = min(total, t * per), hi = min(total, lo + per);
+  uint32_t sum = 0;
+  for (int i = lo; i < hi; ++i) sum += a[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the run sums
+    const uint32_t v = t >= off ? part[t - off] : 0u;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint32_t run = t > 0 ? part[t - 1] : 0u;
+  for (int i = lo; i < hi; ++i) {
+    const uint32_t c = a[i];
+    a[i] = run;
+    run += c;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void radix_scatter_kernel(const uint32_t* __restrict__ key,
+                                                                 const uint8_t* __restrict__ lab, int64_t n,
+                                                                 int shift, int64_t per_blk,
+                                                                 const uint32_t* __restrict__ offs,
+                                                                 uint32_t* __restrict__ key_out,
+                                                                 uint8_t* __restrict__ lab_out) {
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wc[kThreads / kWave][256];
+  const int t = threadIdx.x, w = wave_id(), lane = lane_id();
+  run[t] = offs[(int64_t)t * gridDim.x + blockIdx.x];
+#pragma unroll
+  for (int v = 0; v < kThreads / kWave; ++v) wc[v][t] = 0;
+  const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  const int64_t b0 = (int64_t)blockIdx.x * per_blk, b1 = min(n, b0 + per_blk);
+  for (int64_t base = b0; base < b1; base += kThreads) {
+    const int64_t i = base + t;
+    const bool valid = i < b1;
+    const uint32_t k = valid ? key[i] : 0u;
+    const uint8_t l = valid ? lab[i] : (uint8_t)0;
+    const uint32_t dg = valid ? radix_digit(k, l, shift) : 0u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const uint64_t bal = __ballot(valid && ((dg >> b) & 1u));
+      peers &= ((dg >> b) & 1u) ? bal : ~bal;
+    }
+    const uint32_t rank = __popcll(peers & lt);
+    __syncthreads();  // previous sub-chunk's run update / wc reset is visible
+    if (valid && rank == 0) wc[w][dg] = __popcll(peers);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = run[dg] + rank;
+      for (int v = 0; v < w; ++v) pos += wc[v][dg];
+      key_out[pos] = k;
+      lab_out[pos] = l;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int v = 0; v < kThreads / kWave; ++v) {
+      add += wc[v][t];
+      wc[v][t] = 0;
+    }
+    run[t] += add;
+  }
+}
+
+__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* a, int64_t lo, int64_t hi, uint32_t v) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int64_t upper_bound_u32(const uint32_t* a, int64_t lo, int64_t hi, uint32_t v) {
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// out[0] += S1 = sum of sorted positions of positives, out[1] += T, out[2] += P
+__global__ __launch_bounds__(kThreads) void auc_sorted_count_kernel(const uint32_t* __restrict__ key,
+                                                                    const uint8_t* __restrict__ lab, int64_t n,
+                                                                    unsigned long long* __restrict__ out) {
+  unsigned long long s1 = 0, tt = 0, p = 0;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    if (!lab[i]) continue;
+    s1 += (unsigned long long)i;
+    p += 1;
+    if (i > 0 && lab[i - 1] == 0 && key[i - 1] == key[i]) {  // first positive of a mixed tie segment
+      const uint32_t kv = key[i];
+      const int64_t lo = lower_bound_u32(key, 0, i, kv);
+      const int64_t hi = upper_bound_u32(key, i, n, kv);
+      tt += (unsigned long long)(hi - i) * (unsigned long long)(i - lo);
+    }
+  }
+  s1 = wave_sum(s1);
+  tt = wave_sum(tt);
+  p = wave_sum(p);
+  if (lane_id() == 0) {
+    if (s1) atomicAdd(out, s1);
+    if (tt) atomicAdd(out + 1, tt);
+    if (p) atomicAdd(out + 2, p);
+  }
+}
+
+// res[0] = twice_pairs, res[1] = P, res[2] = N (int64); auc[0] = twice / (2 P N) (NaN if a class is empty)
+__global__ void auc_sorted_finalize_kernel(const unsigned long long* __restrict__ cnt, int64_t n,
+                                           int64_t* __restrict__ res, double* __restrict__ auc) {
+  const long long P = (long long)cnt[2], N = n - P;
+  const long long twice = 2 * ((long long)cnt[0] - P * (P - 1) / 2) - (long long)cnt[1];
+  res[0] = (P > 0 && N > 0) ? twice : 0;
+  res[1] = P;
+  res[2] = N;
+  auc[0] = (P > 0 && N > 0) ? (double)twice / (2.0 * (double)P * (double)N) : __builtin_nan("");
 }
 
 }  // namespace
 
-void launch_auc_segments(const float* sorted_scores, const int64_t* pos_incl, const int64_t* seg_start, int64_t n,
-                         unsigned long long* out_twice_pairs, hipStream_t stream) {
-  if (n <= 0) return;
-  const int grid = stream_grid(n, kThreads * 4, 4096);
-  auc_segments_kernel<<<grid, kThreads, 0, stream>>>(sorted_scores, pos_incl, seg_start, n, out_twice_pairs);
-  check_launch("auc_segments");
+size_t auc_radix_workspace_bytes(int64_t n) {
+  // two key/label buffers (5 B per element each) + the [256][blocks] digit table + 3 counters
+  return (size_t)n * 10 + (size_t)256 * kRadixBlocks * 4 + 64;
+}
+
+void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, void* ws, int64_t* res, double* auc,
+                      hipStream_t stream) {
+  char* p = static_cast<char*>(ws);
+  uint32_t* k0 = reinterpret_cast<uint32_t*>(p);
+  uint32_t* k1 = k0 + n;
+  uint8_t* l0 = reinterpret_cast<uint8_t*>(k1 + n);
+  uint8_t* l1 = l0 + n;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(l1 + ((n + 3) / 4) * 4);
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(hist + 256 * kRadixBlocks);
+  if (hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), stream) != hipSuccess)
+    throw std::runtime_error("auc_radix: memset failed");
+  if (n > 0) {
+    if (n > 0xFFFFFFFFll) throw std::runtime_error("auc_radix: at most 2^32 scores");
+    radix_init_kernel<<<stream_grid(n, kThreads, 4096), kThreads, 0, stream>>>(scores, labels, n, k0, l0);
+    // fewer blocks for small inputs (each owns a contiguous, 256-aligned range)
+    int64_t per_blk = (n + kRadixBlocks - 1) / kRadixBlocks;
+    per_blk = std::max<int64_t>(kThreads, (per_blk + kThreads - 1) / kThreads * kThreads);
+    const int nblk = (int)((n + per_blk - 1) / per_blk);
+    const int shifts[5] = {-1, 0, 8, 16, 24};  // label digit first (least significant), then key bytes
+    for (int ps = 0; ps < 5; ++ps) {
+      radix_hist_kernel<<<nblk, kThreads, 0, stream>>>(k0, l0, n, shifts[ps], per_blk, hist);
+      radix_scan_kernel<<<1, 1024, 0, stream>>>(hist, 256 * nblk);
+      radix_scatter_kernel<<<nblk, kThreads, 0, stream>>>(k0, l0, n, shifts[ps], per_blk, hist, k1, l1);
+      std::swap(k0, k1);
+      std::swap(l0, l1);
+    }
+    auc_sorted_count_kernel<<<stream_grid(n, kThreads * 4, 2048), kThreads, 0, stream>>>(k0, l0, n, cnt);
+  }
+  auc_sorted_finalize_kernel<<<1, 1, 0, stream>>>(cnt, n, res, auc);
+  check_launch("auc_radix");
 }
 
 void launch_auc_compact(const float* scores, const uint8_t* labels, int64_t n, float* pos,

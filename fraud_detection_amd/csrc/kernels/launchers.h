@@ -144,8 +144,9 @@ void launch_auc_compact(const float* scores, const uint8_t* labels, int64_t n, f
 void launch_sort_chunks(float* pos, int64_t npos_cap, const unsigned long long* counter,
                         int chunk, int nchunks, hipStream_t stream);
 // exact AUC from sorted scores: 2 * pairs won + ties, summed over tie segments (u64, exact)
-void launch_auc_segments(const float* sorted_scores, const int64_t* pos_incl, const int64_t* seg_start, int64_t n,
-                         unsigned long long* out_twice_pairs, hipStream_t stream);
+size_t auc_radix_workspace_bytes(int64_t n);
+void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, void* ws, int64_t* res, double* auc,
+                      hipStream_t stream);
 void launch_auc_count(const float* scores, const uint8_t* labels, int64_t n, const float* pos,
                       const unsigned long long* counter, int chunk, int nchunks,
                       unsigned long long* out_pairs, hipStream_t stream);

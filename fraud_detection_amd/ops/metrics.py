@@ -9,8 +9,34 @@ from .native import native, ptr, stream_of
 
 _CHUNK = 16384
 # above this many positives the sorted-positive-chunk count (~N log(chunk) per 16384 positives)
-# loses to one full sort + an O(N) tie-segment pass
+# loses to the native radix sort + one counting pass
 SORT_PATH_POSITIVES = 100_000
+# from this many scores on, the radix path runs straight away (no positive-count read-back)
+RADIX_ROWS = 8_000_000
+_WS: dict = {}
+
+
+def _radix_ws(dev, nbytes: int) -> torch.Tensor:
+    w = _WS.get(dev)
+    if w is None or w.numel() < nbytes:
+        w = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _WS[dev] = w
+    return w
+
+
+def auc_radix(scores: torch.Tensor, labels: torch.Tensor):
+    """Exact AUC on device with no host synchronisation: native stable LSD radix sort of
+    (score key, label) + one counting pass (csrc/kernels/auc.hip).  Returns (auc float64 0-dim
+    device tensor, int64 [3] device tensor = (twice_pairs, P, N))."""
+    _check(scores, labels)
+    n = scores.shape[0]
+    m = native()
+    dev = scores.device
+    ws = _radix_ws(dev, int(m.auc_radix_workspace_bytes(n)))
+    res = torch.empty(3, dtype=torch.int64, device=dev)
+    auc = torch.empty((), dtype=torch.float64, device=dev)
+    m.auc_radix(ptr(scores), ptr(labels), n, ptr(ws), ptr(res), ptr(auc), stream_of(scores))
+    return auc, res
 
 
 def _check(scores: torch.Tensor, labels: torch.Tensor):
@@ -30,6 +56,10 @@ def auc_pair_counts(scores: torch.Tensor, labels: torch.Tensor):
         P, N = int(y.sum()), int(n - y.sum())
         auc = ref.roc_auc(scores.numpy(), y) if P and N else float("nan")
         return (int(round(auc * 2 * P * N)) if P and N else 0), P, N
+    if n >= RADIX_ROWS:
+        _, res = auc_radix(scores, labels)
+        twice, P, N = (int(v) for v in res.cpu())
+        return twice, P, N
     m = native()
     s = stream_of(scores)
     counter = torch.zeros(1, device=scores.device, dtype=torch.int64)
@@ -40,7 +70,8 @@ def auc_pair_counts(scores: torch.Tensor, labels: torch.Tensor):
     if P == 0 or N == 0:
         return 0, P, N
     if min(P, N) > SORT_PATH_POSITIVES:
-        return auc_pair_counts_sorted(scores, labels), P, N
+        _, res = auc_radix(scores, labels)
+        return int(res[0].item()), P, N
     nchunks = (P + _CHUNK - 1) // _CHUNK
     m.sort_chunks(ptr(pos), n, ptr(counter), _CHUNK, nchunks, s)
     out = torch.zeros(1, device=scores.device, dtype=torch.int64)
@@ -48,24 +79,13 @@ def auc_pair_counts(scores: torch.Tensor, labels: torch.Tensor):
     return int(out.item()), P, N
 
 
-def auc_pair_counts_sorted(scores: torch.Tensor, labels: torch.Tensor) -> int:
-    """twice_pairs via a device sort of all scores (rocPRIM radix sort) and one tie-segment pass
-    (auc_segments kernel): exact for any class balance, O(N log N)."""
-    n = scores.shape[0]
-    s_sorted, order = torch.sort(scores)
-    lab = labels.index_select(0, order).to(torch.int64)
-    pos_incl = torch.cumsum(lab, 0)
-    idx = torch.arange(n, device=scores.device, dtype=torch.int64)
-    is_start = torch.ones(n, dtype=torch.bool, device=scores.device)
-    is_start[1:] = s_sorted[1:] != s_sorted[:-1]
-    seg_start = torch.cummax(torch.where(is_start, idx, torch.zeros_like(idx)), 0).values
-    out = torch.zeros(1, device=scores.device, dtype=torch.int64)
-    native().auc_segments(ptr(s_sorted), ptr(pos_incl), ptr(seg_start), n, ptr(out), stream_of(scores))
-    return int(out.item())
-
-
 def roc_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:
-    """Exact ROC-AUC (ties averaged), equal to sklearn.metrics.roc_auc_score."""
+    """Exact ROC-AUC (ties averaged), equal to sklearn.metrics.roc_auc_score.  Large inputs on a
+    GPU take the sync-free radix path and read the result once."""
+    if scores.is_cuda and scores.shape[0] >= RADIX_ROWS:
+        _check(scores, labels)
+        auc, _ = auc_radix(scores, labels)
+        return float(auc.item())
     twice, P, N = auc_pair_counts(scores, labels)
     if P == 0 or N == 0:
         return float("nan")

@@ -14,8 +14,8 @@ All payloads in this framework are tiny (<= 8.5 KB per Newton iteration) except 
 minority all-gather, so the API is shaped for latency: one fused buffer per step, in-place
 all-reduce on the current stream.
 
-Ordering contract between the two communicators on one GPU (torch ProcessGroup for barriers,
-scalars and gathers; the native RCCL communicator for the hot device all-reduces): both are only
+Ordering contract between the two communicators on one GPU (torch ProcessGroup for barriers and
+device scalars; the native RCCL communicator for every device all-reduce and row all-gather): both are only
 ever driven from this class, in program order, from one host thread per rank.  The native
 collectives run on the current compute stream; a ProcessGroup collective waits for the current
 stream before it starts and (synchronous ops) makes the current stream wait for its completion.
@@ -296,12 +296,23 @@ class Communicator:
         counts when the caller already exchanged them (saves a collective and a host sync)."""
         if self.world_size == 1:
             return x, [x.shape[0]]
+        if self._native is not None and x.is_cuda:
+            if counts is None:
+                counts = [int(c[0]) for c in self.all_gather_ints([x.shape[0]])]
+            with self._timed("all_gather_rows", x, "rccl"):
+                return self._native_gather(x, counts)
         if self._host_staged(x):
             with self._timed("all_gather_rows_staged", x, "gloo-staged"):
                 out, c = self._all_gather_rows(x.cpu(), counts)
                 return out.to(x.device), c
         with self._timed("all_gather_rows", x, self.backend):
             return self._all_gather_rows(x, counts)
+
+    def _native_gather(self, x: torch.Tensor, counts: list):
+        """C3 on the native communicator: grouped xGMI send/recv straight into the compact
+        [sum(counts), ...] output on the compute stream (csrc/comm/rccl_comm.cpp all_gatherv)."""
+        counts = [int(c) for c in counts]
+        return self._native.all_gatherv(x.contiguous(), counts), counts
 
     def _all_gather_rows(self, x: torch.Tensor, counts: list | None):
         dev = x.device

@@ -50,17 +50,45 @@ class NativeRCCL:
         self.lib.all_gather(self.handle, t.data_ptr(), out.data_ptr(), t.numel(), _DT[t.dtype], self._stream(t))
         return out
 
+    def all_gatherv(self, x: torch.Tensor, counts: list, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Rows of every rank concatenated along dim 0 (rank order); ``counts`` = every rank's row
+        count (already exchanged by the caller).  One grouped send/recv launch on the stream."""
+        if not x.is_contiguous():
+            raise ValueError("native all_gatherv needs a contiguous tensor")
+        row = 1
+        for s_ in x.shape[1:]:
+            row *= int(s_)
+        total = int(sum(counts))
+        if out is None:
+            out = torch.empty((total,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        elif out.shape[0] != total or not out.is_contiguous() or out.dtype != x.dtype:
+            raise ValueError("out must be a contiguous [sum(counts), ...] tensor of x's dtype")
+        if int(counts[self.rank]) != x.shape[0]:
+            raise ValueError("counts[rank] must equal this rank's rows")
+        ce = [int(c) * row for c in counts]
+        displs = [sum(ce[:r]) for r in range(len(ce))]
+        self.lib.all_gatherv(self.handle, x.data_ptr(), x.numel(), out.data_ptr(), ce, displs, _DT[x.dtype],
+                             self.rank, self._stream(x))
+        return out
+
     def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
         self.lib.broadcast(self.handle, t.data_ptr(), t.numel(), _DT[t.dtype], root, self._stream(t))
         return t
 
     def verify(self) -> bool:
+        """A known all-reduce and a known variable-count all-gather (rank r sends r+1 rows of
+        value r, so every count differs) must both come back exact."""
         dev = torch.device("cuda", torch.cuda.current_device())
         x = torch.full((1088,), float(self.rank + 1), dtype=torch.float64, device=dev)
         self.all_reduce_(x)
+        counts = [r + 1 for r in range(self.world_size)]
+        mine = torch.full((self.rank + 1, 3), self.rank, dtype=torch.int32, device=dev)
+        g = self.all_gatherv(mine, counts)
         torch.cuda.synchronize(dev)
         expect = self.world_size * (self.world_size + 1) / 2.0
-        return bool(torch.all(x == expect).item())
+        want = torch.repeat_interleave(torch.arange(self.world_size, dtype=torch.int32, device=dev),
+                                       torch.tensor(counts, device=dev))[:, None].expand(-1, 3)
+        return bool(torch.all(x == expect).item()) and bool(torch.equal(g, want))
 
     def close(self):
         if self.handle:

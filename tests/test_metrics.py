@@ -58,10 +58,11 @@ def test_confusion_counts_match_sklearn():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,rate,ties", [(20_000_000, 0.5, False), (3_000_001, 0.3, True)])
+@pytest.mark.parametrize("n,rate,ties", [(20_000_000, 0.5, False), (3_000_001, 0.3, True), (9_000_000, 0.01, True)])
 def test_exact_auc_sort_path_large_p(dev, n, rate, ties):
-    """a 20M-row 50%-positive AUC through the sort + tie-segment path is exact
-    (== sklearn), and the auto-selection takes that path above SORT_PATH_POSITIVES."""
+    """a 20M-row 50%-positive AUC through the native radix-sort path is exact
+    (== sklearn) with no host synchronisation inside; the auto-selection takes that path above
+    SORT_PATH_POSITIVES positives or RADIX_ROWS scores."""
     import time
 
     from sklearn.metrics import roc_auc_score
@@ -81,7 +82,35 @@ def test_exact_auc_sort_path_large_p(dev, n, rate, ties):
     dt = time.perf_counter() - t0
     exp = roc_auc_score(y.numpy(), s.numpy())
     assert got == pytest.approx(exp, abs=1e-12)
-    twice = M.auc_pair_counts_sorted(sd, yd)
-    P = int(y.sum())
+    auc_d, res = M.auc_radix(sd, yd)
+    twice, P, N = (int(v) for v in res.cpu())
+    assert P == int(y.sum()) and N == n - P
     assert twice == round(exp * 2 * P * (n - P))
-    assert dt < 1.0, f"{dt:.3f}s"           # measured budget (sort + scans + segment pass)
+    assert float(auc_d) == got
+    assert dt < 0.05, f"{dt:.3f}s"          # 5 radix passes + one counting pass
+    print(f"[auc] n={n} rate={rate} ties={ties}: {dt * 1e3:.2f} ms")
+
+
+@pytest.mark.gpu
+def test_radix_auc_small_and_degenerate(dev):
+    """The radix path on small inputs (one block, partial sub-chunks), all-tied scores, -0 / +0,
+    and single-class inputs (NaN AUC, no fault)."""
+    from sklearn.metrics import roc_auc_score
+
+    from fraud_detection_amd.ops import metrics as M
+
+    rng = np.random.default_rng(5)
+    for n in (1, 2, 7, 255, 256, 257, 1000, 70_001):
+        y = (rng.random(n) < 0.4).astype(np.uint8)
+        s = np.round(rng.normal(size=n) * 4) / 4
+        s[: n // 3] = -0.0 if n > 3 else s[: n // 3]
+        sd, yd = torch.from_numpy(s.astype(np.float32)).to(dev), torch.from_numpy(y).to(dev)
+        auc, res = M.auc_radix(sd, yd)
+        if 0 < y.sum() < n:
+            assert float(auc) == pytest.approx(roc_auc_score(y, s.astype(np.float32)), abs=1e-12), n
+        else:
+            assert np.isnan(float(auc))
+    y = torch.zeros(1000, dtype=torch.uint8, device=dev)
+    y[::3] = 1
+    auc, _ = M.auc_radix(torch.zeros(1000, device=dev), y)
+    assert float(auc) == 0.5  # every pair tied

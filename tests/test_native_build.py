@@ -7,6 +7,6 @@ def test_native_extension_imports_and_targets_gfx950():
     import fraud_detection_amd._fdx_native as m
 
     assert m.ARCH == "gfx950"
-    for name in ("kernelshap", "kernelshap_tree", "auc_segments", "smote_generate", "scaler_stats_cast",
+    for name in ("kernelshap", "kernelshap_tree", "auc_radix", "predict_h2h", "predict_shap_sync", "smote_generate", "scaler_stats_cast",
                  "host_device_pointer", "predict_shap", "logreg_pass_fp8"):
         assert hasattr(m, name), name
