@@ -196,6 +196,8 @@ def main():
         extras.update(_end_to_end(X, y, Xt, yt, cfg, dev, comm))
         extras.update(_worker_kernelshap(res, X, dev, comm))
         extras.update(_batch_predict(res, dev, comm))
+        if comm is None:
+            extras.update(_knn_dp8_projection(res, X, y, dev))
         extras.update(_gbdt(X, y, Xt, yt, dev, comm))
     out = {
         "metric": "train_rows_per_sec (SMOTE k-NN + logistic fit, post-SMOTE rows/s, whole job); AUC; SHAP values/s",
@@ -393,6 +395,45 @@ def _batch_predict(res, dev, comm) -> dict:
                            "host_to_host_rows_per_sec": round(n * world / t_h2h, 1),
                            "vs_cpu_predict_proba_25.7M": round(n / t_h2h / 25.7e6, 2)},
             "predict_1M_host_to_host_ms": round(t_h2h * 1e3, 3)}
+
+
+def _knn_dp8_projection(res, X, y, dev) -> dict:
+    """Global-scope SMOTE under DP=8 (the single-process SMOTE semantics): every rank queries its
+    own minority rows against ALL ranks' minority rows, so per-rank k-NN work grows with N while the
+    other phases stay constant (weak scaling).  Measured here on one GPU with the real kernels:
+    this rank's minority rows against the minority rows of 8 shards (this one + 7 more generated
+    exactly as ranks 1..7 of an 8-GPU run would generate theirs)."""
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.ops import knn as K
+    from fraud_detection_amd.ops import scaler as S
+
+    def minority(Xs, ys):
+        idx = S.compact_indices(ys, 1)
+        return S.scale_cast(Xs, res.scaler, labels=ys, out_dtype="f32", idx=idx)
+
+    q = minority(X, y)
+    shards = [q]
+    for r in range(1, 8):
+        Xr, yr = separable(X.shape[0], seed=1000 + r, device=dev)
+        shards.append(minority(Xr, yr))
+        del Xr, yr
+    C = torch.cat(shards)
+
+    def t(Cand, reps=20):
+        for _ in range(3):
+            K.knn_topk(q, Cand, k=5, self_offset=0)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            K.knn_topk(q, Cand, k=5, self_offset=0)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) / reps
+
+    t1, t8 = t(q), t(C)
+    return {"dp8_global_scope_knn_projection": {
+        "queries_per_rank": int(q.shape[0]), "candidates_dp1": int(q.shape[0]), "candidates_dp8": int(C.shape[0]),
+        "knn_ms_dp1": round(t1 * 1e3, 4), "knn_ms_dp8_per_rank": round(t8 * 1e3, 4),
+        "note": "per-rank k-NN time at DP=8 global scope (queries = this rank's minority rows)"}}
 
 
 def _gbdt(X, y, Xt, yt, dev, comm) -> dict:

@@ -199,7 +199,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   }, py::call_guard<py::gil_scoped_release>());
 
   // logistic regression
-  m.def("logreg_pass_blocks", &fdx::logreg_pass_blocks);
+  m.def("logreg_pass_blocks", &fdx::logreg_pass_blocks, py::arg("fmt") = 0);
   m.def("logreg_pass", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
                           int nblocks, u s) {
     fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),

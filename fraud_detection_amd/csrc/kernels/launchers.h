@@ -83,7 +83,7 @@ void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, 
 
 // ---- logreg.hip ----
 constexpr int kLRPartStride = 1088;  // [0,32) grad, 32 loss, 33 wsum, [64,1088) Hessian 32x32
-int logreg_pass_blocks();
+int logreg_pass_blocks(int fmt = 0);
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream);

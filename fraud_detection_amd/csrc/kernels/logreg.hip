@@ -95,15 +95,24 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     }
   };
   int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
-  vec_t cur[4];
+  // fp8 rows are 8 bytes per lane per row: half the bytes per load instruction of bf16, so the
+  // fp8 stream keeps TWO tiles in flight ahead of the one being computed (the same bytes in
+  // flight per wave as bf16's one-tile register double buffer)
+  constexpr bool kPF2 = FMT == 1;
+  vec_t cur[4], nx1[4];
   if (base < n) load_tile(base, cur);
+  if (kPF2 && base + step < n) load_tile(base + step, nx1);
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
   // is unchanged; H only shapes the step (sub-sampled Newton).
   int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
   for (; base < n; base += step) {
     vec_t nxt[4];
-    if (base + step < n) load_tile(base + step, nxt);
+    if constexpr (kPF2) {
+      if (base + 2 * step < n) load_tile(base + 2 * step, nxt);
+    } else {
+      if (base + step < n) load_tile(base + step, nxt);
+    }
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
@@ -167,7 +176,14 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     wacc += swq;
     if (do_h) whacc += swq;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (kPF2) {
+        cur[u] = nx1[u];
+        nx1[u] = nxt[u];
+      } else {
+        cur[u] = nxt[u];
+      }
+    }
   }
 
   // ---- block reduction (fixed order) ----
@@ -555,22 +571,25 @@ __global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict
 // Grid = resident capacity of the Hessian pass (blocks/CU from the occupancy query x CUs): a
 // grid-stride stream must not launch a partial second round of blocks, which would double the
 // tail (every block owns an equal share of rows).
-int logreg_pass_blocks() {
-  static int cached = 0;
-  if (cached) return cached;
+// fmt: 0 bf16 rows, 1 fp8 rows (each format's own Hessian-kernel occupancy).
+int logreg_pass_blocks(int fmt) {
+  static int cached[2] = {0, 0};
+  fmt = fmt ? 1 : 0;
+  if (cached[fmt]) return cached[fmt];
   int dev = 0, cus = 256, per_cu = 3;
   if (hipGetDevice(&dev) == hipSuccess) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
     int occ = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true, 0>, kThreads, 0) ==
-            hipSuccess && occ > 0)
-      per_cu = occ;
+    hipError_t e = fmt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true, 1>, kThreads, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true, 0>, kThreads, 0);
+    if (e == hipSuccess && occ > 0) per_cu = occ;
   }
-  cached = cus * per_cu;
-  if (cached < 64) cached = 64;
-  if (cached > kPassBlocks * 2) cached = kPassBlocks * 2;
-  return cached;
+  int c = cus * per_cu;
+  if (c < 64) c = 64;
+  if (c > kPassBlocks * 2) c = kPassBlocks * 2;
+  cached[fmt] = c;
+  return c;
 }
 
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,

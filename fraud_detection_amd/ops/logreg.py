@@ -102,8 +102,11 @@ class LRWorkspace:
     def __init__(self, device, nblocks: int | None = None):
         m = native()
         self.device = device
-        self.nblocks = nblocks or m.logreg_pass_blocks()
-        self.partial = torch.empty(self.nblocks * PART_STRIDE, device=device, dtype=torch.float32)
+        # resident grid of each row format's Hessian pass (fp8 kernels hold more blocks per CU)
+        self.nblocks = nblocks or m.logreg_pass_blocks(0)
+        self.nblocks_fp8 = nblocks or m.logreg_pass_blocks(1)
+        self.partial = torch.empty(max(self.nblocks, self.nblocks_fp8) * PART_STRIDE, device=device,
+                                   dtype=torch.float32)
         self.red = torch.zeros(PART_STRIDE, device=device, dtype=torch.float64)
         # state (f64[256]) | w32 (f32[32]) | class_w (f32[2]) | done (i32): one device blob, so a
         # reset is ONE async copy from a pinned mirror of the same layout
@@ -173,13 +176,15 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
     dptr = ptr(ws.done) if done else 0
     h = int(hessian)
     if storage_kind(rows) == "bf16":
+        nb = ws.nblocks
         m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
-                      ws.nblocks, s)
+                      nb, s)
     else:
+        nb = ws.nblocks_fp8
         m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
-                          ptr(ws.partial), ws.nblocks, s)
+                          ptr(ws.partial), nb, s)
     # gradient-only: reduce slots 0..33 and keep red[34] (weight of the rows behind the held H)
-    m.logreg_reduce(ptr(ws.partial), ws.nblocks, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
+    m.logreg_reduce(ptr(ws.partial), nb, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
 
 
 def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian: bool = True,

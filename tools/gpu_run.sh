@@ -10,6 +10,7 @@
 #   bench        bench.py defaults (N=1)
 #   bench50      bench.py --steps 50
 #   configs      tools/baseline_configs.py (every BASELINE config)
+#   ubench       tools/ubench.py per-kernel event timings
 #   latency      tools/serve_latency.py
 #   plots        the reference script chain (generate -> eda -> preprocess -> train -> evaluate -> explain) with its plots
 #   prof         rocprofv3 --kernel-trace --stats of a short bench
@@ -18,6 +19,7 @@
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   pmc          two PMC passes over a short bench
+#   pmcfp8       logreg pass counters + kernel stats with fp8 and with bf16 rows
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
 #   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
@@ -53,6 +55,7 @@ for st in "$@"; do
     benchfp8) step benchfp8 600 python bench.py --storage fp8 ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
+    ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
     configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;
     plots) step plots 900 python scripts/run_reference_pipeline.py --out "$OUT/plots" --kernel ;;
     latency) step latency 600 python tools/serve_latency.py --json "$OUT/latency.json" ;;
@@ -74,6 +77,13 @@ for st in "$@"; do
       cd /tmp && export TMPDIR=/tmp
       step pmc_a 120 rocprofv3 --pmc FETCH_SIZE SQ_WAVES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU --output-format csv -d "$OUT/pmc_a" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-extras
       step pmc_b 120 rocprofv3 --pmc WRITE_SIZE SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY --output-format csv -d "$OUT/pmc_b" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-extras
+      cd "$R" ;;
+    pmcfp8)  # logreg pass counters, fp8 vs bf16 rows (decode-VALU vs HBM question)
+      cd /tmp && export TMPDIR=/tmp
+      for ST in fp8 bf16; do
+        step "pmc_pass_$ST" 120 rocprofv3 --kernel-include-regex "logreg_pass" --pmc FETCH_SIZE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_pass_$ST" -o run -- python3 "$R/bench.py" --storage $ST --steps 2 --warmup 1 --no-extras || exit 1
+        step "pmc_pass_t_$ST" 120 rocprofv3 --kernel-include-regex "logreg_pass" --kernel-trace --stats --output-format csv -d "$OUT/pmc_pass_t_$ST" -o run -- python3 "$R/bench.py" --storage $ST --steps 2 --warmup 1 --no-extras || exit 1
+      done
       cd "$R" ;;
     pmcks)  # KernelSHAP linear kernel counters (3 passes, 1000-explanation batches)
       cd /tmp && export TMPDIR=/tmp

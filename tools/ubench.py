@@ -96,8 +96,18 @@ def main():
     case("logreg_pass_hess_2n", lr_pass(1), N2 * 64)
     case("logreg_pass_hess_s3_2n", lr_pass(3), N2 * 64)
     case("logreg_pass_grad_2n", lr_pass(0), N2 * 64)
-    case("logreg_pass_fp8_hess", lambda: nat.logreg_pass_fp8(ptr(out8), 0, n, ptr(ws.w32), ptr(ws.class_w), 0, 1, 1, 4.0,
-                                                             ptr(ws.partial), ws.nblocks, s), n * 32)
+    out8_2 = torch.empty((N2, 32), device=dev, dtype=torch.uint8)  # same row count as the bf16 cases
+    out8_2[:n].copy_(out8)
+    out8_2[n:].copy_(out8)
+
+    def lr_pass8(h):
+        def f():
+            nat.logreg_pass_fp8(ptr(out8_2), 0, N2, ptr(ws.w32), ptr(ws.class_w), 0, h, 1, 4.0, ptr(ws.partial),
+                                ws.nblocks_fp8, s)
+        return f
+    case("logreg_pass_fp8_hess_2n", lr_pass8(1), N2 * 32)
+    case("logreg_pass_fp8_hess_s8_2n", lr_pass8(8), N2 * 32)
+    case("logreg_pass_fp8_grad_2n", lr_pass8(0), N2 * 32)
     case("logreg_reduce", lambda: nat.logreg_reduce(ptr(ws.partial), ws.nblocks, 1088, ptr(ws.red), 0, s),
          ws.nblocks * 1088 * 4)
     case("newton_update", lambda: nat.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0,
@@ -123,7 +133,7 @@ def main():
     sc = torch.randn(2_000_000, device=dev)
     yl = (torch.rand(2_000_000, device=dev) < 0.002).to(torch.uint8)
     case("roc_auc_2M", lambda: M.roc_auc(sc, yl), 2_000_000 * 5)
-    out = {"device": info, "rows": n, "results": results, "pass_blocks": ws.nblocks}
+    out = {"device": info, "rows": n, "results": results, "pass_blocks": ws.nblocks, "pass_blocks_fp8": ws.nblocks_fp8}
     if a.json:
         with open(a.json, "w") as f:
             json.dump(out, f, indent=1)
