@@ -373,6 +373,11 @@ PYBIND11_MODULE(_fdx_native, m) {
                           P<const unsigned long long>(counter), chunk, nchunks, P<unsigned long long>(out), S(s));
   });
   m.def("auc_radix_workspace_bytes", &fdx::auc_radix_workspace_bytes);
+  m.def("auc_radix_layout", [](int64_t n) {
+    size_t off[7];
+    fdx::auc_radix_layout(n, off);
+    return std::vector<size_t>(off, off + 7);
+  });
   m.def("auc_radix", [](u scores, u labels, int64_t n, u ws, u res, u auc, u s) {
     fdx::launch_auc_radix(P<const float>(scores), P<const uint8_t>(labels), n, P<void>(ws), P<int64_t>(res),
                           P<double>(auc), S(s));

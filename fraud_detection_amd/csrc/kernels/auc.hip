@@ -365,20 +365,39 @@ __global__ void auc_sorted_finalize_kernel(const unsigned long long* __restrict_
 
 }  // namespace
 
+// Workspace layout, every region 256-byte aligned (the u64 counters take 64-bit atomics; an odd n
+// must not shift them off alignment): k0 | k1 (u32 [n]) | l0 | l1 (u8 [n]) | hist (u32 [256][blocks])
+// | cnt (u64 [3]).  Offsets in bytes; [6] = total.
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+void auc_radix_layout(int64_t n, size_t off[7]) {
+  const size_t nn = (size_t)(n > 0 ? n : 0);
+  off[0] = 0;
+  off[1] = align256(off[0] + nn * 4);
+  off[2] = align256(off[1] + nn * 4);
+  off[3] = align256(off[2] + nn);
+  off[4] = align256(off[3] + nn);
+  off[5] = align256(off[4] + (size_t)256 * kRadixBlocks * 4);
+  off[6] = align256(off[5] + 3 * sizeof(unsigned long long));
+}
+
 size_t auc_radix_workspace_bytes(int64_t n) {
-  // two key/label buffers (5 B per element each) + the [256][blocks] digit table + 3 counters
-  return (size_t)n * 10 + (size_t)256 * kRadixBlocks * 4 + 64;
+  size_t off[7];
+  auc_radix_layout(n, off);
+  return off[6];
 }
 
 void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, void* ws, int64_t* res, double* auc,
                       hipStream_t stream) {
+  if (reinterpret_cast<uintptr_t>(ws) % 256 != 0) throw std::runtime_error("auc_radix: workspace must be 256-byte aligned");
+  size_t off[7];
+  auc_radix_layout(n, off);
   char* p = static_cast<char*>(ws);
-  uint32_t* k0 = reinterpret_cast<uint32_t*>(p);
-  uint32_t* k1 = k0 + n;
-  uint8_t* l0 = reinterpret_cast<uint8_t*>(k1 + n);
-  uint8_t* l1 = l0 + n;
-  uint32_t* hist = reinterpret_cast<uint32_t*>(l1 + ((n + 3) / 4) * 4);
-  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(hist + 256 * kRadixBlocks);
+  uint32_t* k0 = reinterpret_cast<uint32_t*>(p + off[0]);
+  uint32_t* k1 = reinterpret_cast<uint32_t*>(p + off[1]);
+  uint8_t* l0 = reinterpret_cast<uint8_t*>(p + off[2]);
+  uint8_t* l1 = reinterpret_cast<uint8_t*>(p + off[3]);
+  uint32_t* hist = reinterpret_cast<uint32_t*>(p + off[4]);
+  unsigned long long* cnt = reinterpret_cast<unsigned long long*>(p + off[5]);
   if (hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), stream) != hipSuccess)
     throw std::runtime_error("auc_radix: memset failed");
   if (n > 0) {
