@@ -9,6 +9,7 @@
 // RCCL instance.
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 #include <rccl/rccl.h>
 
 #include <cstring>
