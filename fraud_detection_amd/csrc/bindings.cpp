@@ -124,6 +124,19 @@ PYBIND11_MODULE(_fdx_native, m) {
     return reinterpret_cast<u>(d);
   });
   m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
+  // raw HIP events for the GPU owner's pipelined batches (wait with the GIL released)
+  m.def("event_create", [] {
+    hipEvent_t e;
+    hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    return reinterpret_cast<u>(e);
+  });
+  m.def("event_record", [](u e, u stream) {
+    hip_check(hipEventRecord(reinterpret_cast<hipEvent_t>(e), S(stream)), "hipEventRecord");
+  });
+  m.def("event_sync", [](u e) {
+    hip_check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(e)), "hipEventSynchronize");
+  }, py::call_guard<py::gil_scoped_release>());
+  m.def("event_destroy", [](u e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); });
   m.def("predict_h2h", &predict_h2h, py::call_guard<py::gil_scoped_release>());
 
   // scaler

@@ -202,14 +202,23 @@ class Ring {
   }
 
   // ---- owner -------------------------------------------------------------------------------
-  // Gather up to max_rows rows of READY slots (same op, ticket order) into dst [max_rows, d].
-  // Waits up to timeout_ms for the first slot, then up to window_us for more.  Returns
-  // (rows, op); rows == 0 on timeout.
-  std::pair<uint32_t, uint32_t> collect(float* dst, uint32_t max_rows, double window_us, double timeout_ms) {
+  // Gather up to max_rows rows of READY slots (same op, ticket order) into dst [max_rows, d], as
+  // batch `set` (0 or 1: the owner keeps one batch on the device while it gathers the next).
+  // Waits up to timeout_ms for the first slot (timeout_ms <= 0: one look, no wait), then up to
+  // window_us for more.  Returns (rows, op); rows == 0 on timeout.
+  std::pair<uint32_t, uint32_t> collect(float* dst, uint32_t max_rows, double window_us, double timeout_ms,
+                                        int set) {
     const uint32_t N = h_->nslots, d = h_->d;
+    std::vector<Taken>& taken_ = taken_sets_[set & 1];
     taken_.clear();
     uint64_t t = h_->tail.load(std::memory_order_relaxed);
-    if (!wait_ready(slots_[t % N], t, now_ns() + (uint64_t)(timeout_ms * 1e6))) return {0, 0};
+    if (timeout_ms <= 0) {
+      Slot& s0 = slots_[t % N];
+      if (!(s0.turn.load(std::memory_order_acquire) == t && s0.state.load(std::memory_order_acquire) == READY))
+        return {0, 0};
+    } else if (!wait_ready(slots_[t % N], t, now_ns() + (uint64_t)(timeout_ms * 1e6))) {
+      return {0, 0};
+    }
     const uint32_t op = slots_[t % N].op;
     uint32_t rows = 0;
     const uint64_t wdl = now_ns() + (uint64_t)(window_us * 1e3);
@@ -237,8 +246,9 @@ class Ring {
 
   // Scatter the batch results: column-major pieces prob[rows], logit[rows], phi[rows][dphi]
   // (any may be null) into each taken slot's [n][out_w] rows, then one completion wake.
-  void complete(const float* prob, const float* logit, const float* phi, uint32_t dphi, bool ok) {
+  void complete(const float* prob, const float* logit, const float* phi, uint32_t dphi, bool ok, int set) {
     const uint32_t N = h_->nslots, W = h_->out_w;
+    std::vector<Taken>& taken_ = taken_sets_[set & 1];
     uint64_t rows = 0;
     for (const Taken& tk : taken_) {
       Slot& s = slots_[tk.ticket % N];
@@ -263,7 +273,7 @@ class Ring {
     if (h_->sleepers.load(std::memory_order_seq_cst)) futex(&h_->completions, FUTEX_WAKE, INT_MAX, nullptr);
   }
 
-  size_t pending_slots() const { return taken_.size(); }
+  size_t pending_slots() const { return taken_sets_[0].size() + taken_sets_[1].size(); }
 
  private:
   void map(bool create) {
@@ -365,7 +375,7 @@ class Ring {
   char* base_ = nullptr;
   Header* h_ = nullptr;
   Slot* slots_ = nullptr;
-  std::vector<Taken> taken_;
+  std::vector<Taken> taken_sets_[2];
 };
 
 template <class T>
@@ -405,20 +415,21 @@ PYBIND11_MODULE(_fdx_ring, m) {
            },
            py::arg("X"), py::arg("op") = 0, py::arg("timeout_ms") = 10000.0)
       .def("collect",
-           [](Ring& r, uintptr_t dst, uint32_t max_rows, double window_us, double timeout_ms) {
+           [](Ring& r, uintptr_t dst, uint32_t max_rows, double window_us, double timeout_ms, int set) {
              py::gil_scoped_release nogil;
-             auto res = r.collect(reinterpret_cast<float*>(dst), max_rows, window_us, timeout_ms);
+             auto res = r.collect(reinterpret_cast<float*>(dst), max_rows, window_us, timeout_ms, set);
              return std::make_tuple(res.first, res.second);
            },
            py::arg("dst"), py::arg("max_rows"), py::arg("window_us") = 0.0, py::arg("timeout_ms") = 50.0,
-           "gather READY rows into the float32 buffer at address dst; -> (rows, op)")
+           py::arg("set") = 0, "gather READY rows into the float32 buffer at address dst as batch `set`; -> (rows, op)")
       .def("complete",
-           [](Ring& r, uintptr_t prob, uintptr_t logit, uintptr_t phi, uint32_t dphi, bool ok) {
+           [](Ring& r, uintptr_t prob, uintptr_t logit, uintptr_t phi, uint32_t dphi, bool ok, int set) {
              py::gil_scoped_release nogil;
              r.complete(reinterpret_cast<const float*>(prob), reinterpret_cast<const float*>(logit),
-                        reinterpret_cast<const float*>(phi), dphi, ok);
+                        reinterpret_cast<const float*>(phi), dphi, ok, set);
            },
-           py::arg("prob"), py::arg("logit"), py::arg("phi") = 0, py::arg("dphi") = 0, py::arg("ok") = true)
+           py::arg("prob"), py::arg("logit"), py::arg("phi") = 0, py::arg("dphi") = 0, py::arg("ok") = true,
+           py::arg("set") = 0)
       .def("pending_slots", &Ring::pending_slots);
   m.attr("OWNER_STARTING") = (int)OWNER_STARTING;
   m.attr("OWNER_READY") = (int)OWNER_READY;

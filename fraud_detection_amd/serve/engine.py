@@ -195,6 +195,7 @@ class _EngineBase:
         self.host_max_rows = 0
         self.calibration: dict = {}
         self._owner_in = None
+        self._ostream = None
         if self.device.type == "cuda":
             from ..ops.native import native
 
@@ -239,25 +240,26 @@ class _EngineBase:
         return self.device.type != "cuda" or n == 0 or n <= self.host_max_rows
 
     # ---- GPU-owner API (serve/gpu_owner.py): rows land in a pinned staging buffer -------------
-    def owner_input(self, cap: int) -> int:
-        """Address of a pinned float32 [cap, d] buffer the ring gathers request rows into."""
-        if self._owner_in is None or self._owner_in.shape[0] < cap:
-            self._owner_in = torch.empty((cap, self.d), dtype=torch.float32,
-                                         pin_memory=self.device.type == "cuda")
-            self._owner_out = np.empty(cap * (self.d + 2), np.float32)
-            self._owner_map = 0
-            if self.device.type == "cuda":
+    # Two buffer sets: the owner gathers batch i+1 into one while batch i runs from the other.
+    def owner_input(self, cap: int, set_: int = 0) -> int:
+        """Address of pinned float32 [cap, d] buffer `set_` (0/1) the ring gathers rows into."""
+        if getattr(self, "_owner_in", None) is None or self._owner_in[0].shape[0] < cap:
+            pin = self.device.type == "cuda"
+            self._owner_in = [torch.empty((cap, self.d), dtype=torch.float32, pin_memory=pin) for _ in range(2)]
+            self._owner_out = [np.empty(cap * (self.d + 2), np.float32) for _ in range(2)]
+            self._owner_map = [0, 0]
+            if pin:
                 from ..ops.native import native
 
-                self._owner_map = native().host_device_pointer(self._owner_in.data_ptr())
-        return self._owner_in.data_ptr()
+                self._owner_map = [native().host_device_pointer(t.data_ptr()) for t in self._owner_in]
+        return self._owner_in[set_].data_ptr()
 
-    def run_staged(self, n: int, explain: bool):
-        """Score (and explain) the n rows at owner_input(): -> (prob, logit, phi, dphi) addresses
-        of float32 column blocks (phi 0 when not explaining).  Generic path: through the public
-        API; InferenceEngine overrides it with a copy-free device launch."""
-        X = self._owner_in[:n].numpy()
-        o = self._owner_out
+    def run_staged_async(self, n: int, explain: bool, set_: int = 0):
+        """Start scoring (and explaining) the n rows of buffer `set_`; -> a handle for
+        wait_staged.  Generic path: computed right here through the public API (the handle is
+        already complete); InferenceEngine launches on the device and returns at once."""
+        X = self._owner_in[set_][:n].numpy()
+        o = self._owner_out[set_]
         if explain:
             e = self.explain(X, os.environ.get("FDX_XAI_METHOD", "auto"))
             p, z, phi = e.prob, e.logit, e.phi
@@ -268,9 +270,16 @@ class _EngineBase:
         o[n:2 * n] = z
         base = o.ctypes.data
         if phi is None:
-            return base, base + 4 * n, 0, 0
+            return (base, base + 4 * n, 0, 0)
         o[2 * n:2 * n + n * self.d] = np.asarray(phi, np.float32).reshape(-1)
-        return base, base + 4 * n, base + 8 * n, self.d
+        return (base, base + 4 * n, base + 8 * n, self.d)
+
+    def wait_staged(self, handle):
+        """-> (prob, logit, phi, dphi) addresses of float32 column blocks of a started batch."""
+        return handle
+
+    def run_staged(self, n: int, explain: bool, set_: int = 0):
+        return self.wait_staged(self.run_staged_async(n, explain, set_))
 
     # ---- shared API ------------------------------------------------------------------------
     @property
@@ -426,31 +435,44 @@ class InferenceEngine(_EngineBase):
         ph = o[2 * n:].reshape(n, dphi).astype(np.float64) if want_phi else None
         return p, z, ph
 
-    def run_staged(self, n: int, explain: bool):
-        """GPU-owner path: the ring gathered the rows straight into the pinned owner buffer; the
-        kernel reads them there through its device mapping and writes the results into mapped
-        pinned memory (small batches: one launch + wait, GIL released, nothing copied), or after
-        one H2D copy (large batches).  Runs on the owner's own stream, owner thread only."""
+    def run_staged_async(self, n: int, explain: bool, set_: int = 0):
+        """GPU-owner path: the ring gathered the rows straight into pinned buffer `set_`; the kernel
+        reads them there through the device mapping and writes the results into mapped pinned
+        memory (small batches: one launch, nothing copied), or after one H2D copy (large
+        batches).  Returns at once; wait_staged waits on the batch's event with the GIL released.
+        Owner thread only, on the owner's own stream."""
         if self.device.type != "cuda" or (explain and os.environ.get("FDX_XAI_METHOD", "auto") not in ("auto", "linear")):
-            return super().run_staged(n, explain)
+            return super().run_staged_async(n, explain, set_)
         d = self.d
         dphi = d if explain else 0
-        st = self._ostage
-        st.ensure(self._owner_in.shape[0])
-        if getattr(self, "_ostream", None) is None:
+        m = P.native()
+        if self._ostream is None:
             self._ostream = torch.cuda.Stream(self.device)
-        if n <= ZERO_COPY_ROWS and self._owner_map and st.out_map:
+            self._ostages = [_Staging(self.device, d, d + 2) for _ in range(2)]
+            self._oevents = [m.event_create() for _ in range(2)]
+        st = self._ostages[set_]
+        st.ensure(self._owner_in[set_].shape[0])
+        sh = self._ostream.cuda_stream
+        if n <= ZERO_COPY_ROWS and self._owner_map[set_] and st.out_map:
             oo = st.out_map
-            P.native().predict_shap_sync(self._owner_map, 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c),
-                                         float(self.bias), oo, oo + 4 * n, oo + 8 * n if explain else 0, dphi,
-                                         self._ostream.cuda_stream)
-            base = st.hout.data_ptr()
+            m.predict_shap(self._owner_map[set_], 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                           oo, oo + 4 * n, oo + 8 * n if explain else 0, dphi, sh)
         else:
             with torch.cuda.stream(self._ostream):
-                st.din[:n].copy_(self._owner_in[:n], non_blocking=True)
-                o = self._launch(P.ptr(st.din), n, explain, st, False)
-            base = o.ctypes.data
-        return base, base + 4 * n, (base + 8 * n) if explain else 0, dphi
+                st.din[:n].copy_(self._owner_in[set_][:n], non_blocking=True)
+                out = st.dout
+                m.predict_shap(P.ptr(st.din), 1, n, d, d, dphi, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                               P.ptr(out), P.ptr(out) + 4 * n, P.ptr(out) + 8 * n if explain else 0, dphi, sh)
+                st.hout[: n * (2 + dphi)].copy_(out[: n * (2 + dphi)], non_blocking=True)
+        m.event_record(self._oevents[set_], sh)
+        base = st.hout.data_ptr()
+        return ("dev", set_, (base, base + 4 * n, (base + 8 * n) if explain else 0, dphi))
+
+    def wait_staged(self, handle):
+        if handle[0] != "dev":
+            return handle
+        P.native().event_sync(self._oevents[handle[1]])
+        return handle[2]
 
     def _predict_host(self, X: np.ndarray):
         return self._cpu(X, want_phi=False)

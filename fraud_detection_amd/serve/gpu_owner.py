@@ -55,7 +55,7 @@ class GpuOwner:
         self.ring_path = ring_path
         env = os.environ.get("FDX_HOST_MAX_ROWS", "").strip()
         self.ring.host_max_rows = int(env) if env and int(env) >= 0 else int(min(engine.host_max_rows, 1 << 30))
-        self._buf = engine.owner_input(self.max_batch)
+        self._bufs = [engine.owner_input(self.max_batch, 0), engine.owner_input(self.max_batch, 1)]
         self._stop = threading.Event()
         self._th = threading.Thread(target=self._loop, name="fdx-gpu-owner", daemon=True)
         self.batches = 0
@@ -72,6 +72,9 @@ class GpuOwner:
         self.ring.owner_state = _ring_mod().OWNER_STOPPED
 
     def _loop(self):
+        """Pipelined: while batch i runs on the device from buffer set i % 2, whatever requests are
+        queued are gathered into the other set and launched behind it; then batch i is waited for
+        and its slots completed (one futex wake for all its producers)."""
         ring, eng = self.ring, self.engine
         try:
             from ..obs.metrics import gpu_kernel_histogram
@@ -79,24 +82,40 @@ class GpuOwner:
             hist = gpu_kernel_histogram().labels("owner_batch")
         except Exception:  # noqa: BLE001 - metrics are best effort
             hist = None
-        while not self._stop.is_set():
-            n, op = ring.collect(self._buf, self.max_batch, self.window_us, 50.0)
-            if n == 0:
-                continue
-            try:
+        inflight = None  # (set, handle, rows, t_start)
+        cur = 0
+        while not self._stop.is_set() or inflight is not None:
+            n = op = 0
+            if not self._stop.is_set():
+                # with a batch in flight only look (never wait): that batch must be completed promptly
+                n, op = ring.collect(self._bufs[cur], self.max_batch, self.window_us,
+                                     0.0 if inflight is not None else 50.0, cur)
+            started = None
+            if n:
                 t0 = time.perf_counter()
-                p, z, phi, dphi = eng.run_staged(n, op == OP_EXPLAIN)
-                if hist is not None:  # launch + device time + wait of one batch (host clock)
-                    hist.observe(time.perf_counter() - t0)
-                ring.complete(p, z, phi, dphi, True)
-            except Exception:  # noqa: BLE001 - fail the batch, keep serving
-                logger.exception("GPU owner batch of %d rows failed", n)
-                ring.complete(0, 0, 0, 0, False)
-                continue
-            self.batches += 1
-            self.rows += n
-            if self.metrics is not None:
-                self.metrics.microbatch_size.observe(n)
+                try:
+                    started = (cur, eng.run_staged_async(n, op == OP_EXPLAIN, cur), n, t0)
+                except Exception:  # noqa: BLE001 - fail the batch, keep serving
+                    logger.exception("GPU owner batch of %d rows failed to launch", n)
+                    ring.complete(0, 0, 0, 0, False, cur)
+            if inflight is not None:
+                s, h, rows, t0 = inflight
+                try:
+                    p, z, phi, dphi = eng.wait_staged(h)
+                    if hist is not None:  # launch + device time + wait of one batch (host clock)
+                        hist.observe(time.perf_counter() - t0)
+                    ring.complete(p, z, phi, dphi, True, s)
+                    self.batches += 1
+                    self.rows += rows
+                    if self.metrics is not None:
+                        self.metrics.microbatch_size.observe(rows)
+                except Exception:  # noqa: BLE001
+                    logger.exception("GPU owner batch of %d rows failed", rows)
+                    ring.complete(0, 0, 0, 0, False, s)
+                inflight = None
+            if started is not None:
+                inflight = started
+                cur ^= 1
 
 
 class RingClient:
