@@ -9,10 +9,14 @@
 #include <pybind11/stl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels/launchers.h"
+#include "serve/shm_ring.h"
 
 namespace py = pybind11;
 using u = uintptr_t;
@@ -60,6 +64,88 @@ struct HostPin {
   }
   ~HostPin() {
     if (p) (void)hipHostUnregister(p);
+  }
+};
+
+// ---- native GPU-owner loop (serve/gpu_owner.py, linear model) ------------------------------
+// One C++ thread per owner drains the shared-memory request ring (serve/shm_ring.h) into one of
+// two pinned, device-mapped input buffers and runs the fused folded-scaler predict (+ LinearSHAP)
+// kernel straight on them, writing the results into mapped pinned output buffers: no copy
+// kernels, no Python, no GIL on the serving path.  Batches are pipelined only under load: while a
+// batch is on the device, the next is gathered and launched behind it when at least `pipe_rows`
+// rows are already queued; otherwise the loop waits for the in-flight batch and then gathers
+// everything that queued meanwhile (bigger batches amortise the ~16 us launch + wait).
+struct NativeOwner {
+  std::unique_ptr<fdx_ring::Ring> ring;
+  std::thread th;
+  std::atomic<bool> stop{false};
+  const float* a = nullptr;
+  const float* c = nullptr;
+  float bias = 0.f;
+  int d = 30;
+  uint32_t cap = 0, pipe_rows = 64;
+  double window_us = 0.0;
+  hipStream_t stream = nullptr;
+  float* in_host[2] = {nullptr, nullptr};
+  const void* in_dev[2] = {nullptr, nullptr};
+  float* out_host[2] = {nullptr, nullptr};
+  float* out_dev[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  std::atomic<uint64_t> errors{0};
+
+  void launch(int set, uint32_t n, bool explain) {
+    const int dphi = explain ? d : 0;
+    float* o = out_dev[set];
+    fdx::launch_predict_shap(in_dev[set], 1, n, d, d, dphi, a, c, bias, o, o + n, explain ? o + 2 * (size_t)n : nullptr,
+                             dphi, stream);
+    hip_check(hipEventRecord(ev[set], stream), "hipEventRecord");
+  }
+  void finish(int set, uint32_t n, bool explain, bool ok) {
+    hipError_t e = hipSuccess;
+    if (ok) e = hipEventSynchronize(ev[set]);
+    const float* o = out_host[set];
+    const bool good = ok && e == hipSuccess;
+    if (!good) errors.fetch_add(1);
+    ring->complete(o, o + n, explain ? o + 2 * (size_t)n : nullptr, explain ? (uint32_t)d : 0u, good, set);
+  }
+  void run() {
+    int cur = 0, inf_set = -1;
+    uint32_t inf_n = 0;
+    bool inf_explain = false;
+    while (!stop.load(std::memory_order_relaxed) || inf_set >= 0) {
+      uint32_t n = 0, op = 0;
+      if (!stop.load(std::memory_order_relaxed)) {
+        if (inf_set < 0) {
+          auto r = ring->collect(in_host[cur], cap, window_us, 50.0, cur);
+          n = r.first;
+          op = r.second;
+        } else if (ring->ready_rows(pipe_rows) >= pipe_rows) {
+          auto r = ring->collect(in_host[cur], cap, 0.0, 0.0, cur);
+          n = r.first;
+          op = r.second;
+        }
+      }
+      bool launched = false;
+      if (n) {
+        try {
+          launch(cur, n, op == 1);
+          launched = true;
+        } catch (...) {
+          errors.fetch_add(1);
+          ring->complete(nullptr, nullptr, nullptr, 0, false, cur);
+        }
+      }
+      if (inf_set >= 0) {
+        finish(inf_set, inf_n, inf_explain, true);
+        inf_set = -1;
+      }
+      if (launched) {
+        inf_set = cur;
+        inf_n = n;
+        inf_explain = op == 1;
+        cur ^= 1;
+      }
+    }
   }
 };
 
@@ -137,7 +223,52 @@ PYBIND11_MODULE(_fdx_native, m) {
     hip_check(hipEventSynchronize(reinterpret_cast<hipEvent_t>(e)), "hipEventSynchronize");
   }, py::call_guard<py::gil_scoped_release>());
   m.def("event_destroy", [](u e) { (void)hipEventDestroy(reinterpret_cast<hipEvent_t>(e)); });
+  // busy-poll an event (no blocking-wait wake-up latency: for a thread that owns a core)
+  m.def("event_spin", [](u e) {
+    hipEvent_t ev = reinterpret_cast<hipEvent_t>(e);
+    hipError_t r;
+    while ((r = hipEventQuery(ev)) == hipErrorNotReady) __builtin_ia32_pause();
+    hip_check(r, "hipEventQuery");
+  }, py::call_guard<py::gil_scoped_release>());
   m.def("predict_h2h", &predict_h2h, py::call_guard<py::gil_scoped_release>());
+  m.def("owner_start", [](u ring_base, size_t ring_bytes, u a, u c, float bias, int d, uint32_t cap, double window_us,
+                          uint32_t pipe_rows, u stream, u in_host0, u in_host1, u in_dev0, u in_dev1, u out_host0,
+                          u out_host1, u out_dev0, u out_dev1) {
+    auto* o = new NativeOwner();
+    o->ring = std::make_unique<fdx_ring::Ring>(reinterpret_cast<char*>(ring_base), ring_bytes);
+    if ((int)o->ring->d_() != d) {
+      delete o;
+      throw std::runtime_error("owner_start: ring width != model width");
+    }
+    o->a = P<const float>(a);
+    o->c = P<const float>(c);
+    o->bias = bias;
+    o->d = d;
+    o->cap = cap;
+    o->window_us = window_us;
+    o->pipe_rows = pipe_rows ? pipe_rows : 1;
+    o->stream = S(stream);
+    o->in_host[0] = P<float>(in_host0);
+    o->in_host[1] = P<float>(in_host1);
+    o->in_dev[0] = P<const void>(in_dev0);
+    o->in_dev[1] = P<const void>(in_dev1);
+    o->out_host[0] = P<float>(out_host0);
+    o->out_host[1] = P<float>(out_host1);
+    o->out_dev[0] = P<float>(out_dev0);
+    o->out_dev[1] = P<float>(out_dev1);
+    for (int i = 0; i < 2; ++i) hip_check(hipEventCreateWithFlags(&o->ev[i], hipEventDisableTiming), "hipEventCreate");
+    o->th = std::thread([o] { o->run(); });
+    return reinterpret_cast<u>(o);
+  });
+  m.def("owner_stop", [](u h) {
+    auto* o = reinterpret_cast<NativeOwner*>(h);
+    o->stop.store(true);
+    if (o->th.joinable()) o->th.join();
+    const uint64_t err = o->errors.load();
+    for (int i = 0; i < 2; ++i) (void)hipEventDestroy(o->ev[i]);
+    delete o;
+    return err;
+  }, py::call_guard<py::gil_scoped_release>());
 
   // scaler
   m.def("scaler_partial", [](u X, int64_t n, int ld, int d, u pivot, u partial, int nblocks, u s) {

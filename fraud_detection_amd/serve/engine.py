@@ -474,6 +474,27 @@ class InferenceEngine(_EngineBase):
         P.native().event_sync(self._oevents[handle[1]])
         return handle[2]
 
+    def start_native_owner(self, ring, cap: int, window_us: float, pipe_rows: int = 64) -> int:
+        """Start the C++ owner loop on this engine's folded weights (GPU only): two device-mapped
+        pinned input buffers (owner_input) and two device-mapped pinned output buffers."""
+        m = P.native()
+        self.owner_input(cap)
+        if not all(self._owner_map):
+            raise RuntimeError("pinned owner buffers are not device-mapped")
+        if self._ostream is None:
+            self._ostream = torch.cuda.Stream(self.device)
+        self._nout = [torch.empty(cap * (self.d + 2), dtype=torch.float32, pin_memory=True) for _ in range(2)]
+        omap = [m.host_device_pointer(t.data_ptr()) for t in self._nout]
+        if not all(omap):
+            raise RuntimeError("pinned owner outputs are not device-mapped")
+        return m.owner_start(ring.base_address, ring.total_bytes, P.ptr(self._a), P.ptr(self._c), float(self.bias),
+                             self.d, int(cap), float(window_us), int(pipe_rows), self._ostream.cuda_stream,
+                             self._owner_in[0].data_ptr(), self._owner_in[1].data_ptr(), self._owner_map[0],
+                             self._owner_map[1], self._nout[0].data_ptr(), self._nout[1].data_ptr(), omap[0], omap[1])
+
+    def stop_native_owner(self, handle) -> int:
+        return int(P.native().owner_stop(handle))
+
     def _predict_host(self, X: np.ndarray):
         return self._cpu(X, want_phi=False)
 

@@ -58,17 +58,36 @@ class GpuOwner:
         self._bufs = [engine.owner_input(self.max_batch, 0), engine.owner_input(self.max_batch, 1)]
         self._stop = threading.Event()
         self._th = threading.Thread(target=self._loop, name="fdx-gpu-owner", daemon=True)
-        self.batches = 0
-        self.rows = 0
+        self._native = None
+        self.native = _native_capable(engine) and os.environ.get("FDX_OWNER_LOOP", "native") == "native"
+
+    @property
+    def batches(self) -> int:
+        return int(self.ring.stats()["batches"])
+
+    @property
+    def rows(self) -> int:
+        return int(self.ring.stats()["rows"])
 
     def start(self) -> "GpuOwner":
-        self._th.start()
+        if self.native:
+            # the whole serving loop in C++ (csrc/bindings.cpp NativeOwner): ring -> mapped pinned
+            # batch -> fused kernel -> mapped pinned results -> ring, no Python and no GIL per batch
+            self._native = self.engine.start_native_owner(self.ring, self.max_batch, self.window_us)
+        else:
+            self._th.start()
         self.ring.owner_state = _ring_mod().OWNER_READY
         return self
 
     def stop(self):
         self._stop.set()
-        self._th.join(timeout=5)
+        if self._native is not None:
+            errors = self.engine.stop_native_owner(self._native)
+            self._native = None
+            if errors:
+                logger.error("native GPU owner loop failed %d batch(es)", errors)
+        elif self._th.is_alive():
+            self._th.join(timeout=5)
         self.ring.owner_state = _ring_mod().OWNER_STOPPED
 
     def _loop(self):
@@ -105,8 +124,6 @@ class GpuOwner:
                     if hist is not None:  # launch + device time + wait of one batch (host clock)
                         hist.observe(time.perf_counter() - t0)
                     ring.complete(p, z, phi, dphi, True, s)
-                    self.batches += 1
-                    self.rows += rows
                     if self.metrics is not None:
                         self.metrics.microbatch_size.observe(rows)
                 except Exception:  # noqa: BLE001
@@ -116,6 +133,13 @@ class GpuOwner:
             if started is not None:
                 inflight = started
                 cur ^= 1
+
+
+def _native_capable(engine) -> bool:
+    """The native loop serves the linear model's fused predict / LinearSHAP kernel on a GPU."""
+    return (getattr(engine, "kind", "") == "linear" and engine.device.type == "cuda"
+            and os.environ.get("FDX_XAI_METHOD", "auto") in ("auto", "linear")
+            and hasattr(engine, "start_native_owner"))
 
 
 class RingClient:

@@ -58,10 +58,11 @@ def test_gpu_predict_goldens_through_microbatcher(dev, tmp_path, restore_service
         for i, s in res:
             assert s == pytest.approx(0.011905 if i % 2 else 0.000544, abs=5e-7)
         m = c.get("/metrics").text
-        n_req = [ln for ln in m.splitlines() if ln.startswith("fdx_microbatch_size_count")]
-        n_rows = [ln for ln in m.splitlines() if ln.startswith("fdx_microbatch_size_sum")]
-        assert float(n_rows[0].split()[-1]) == 64.0 and float(n_req[0].split()[-1]) <= 64.0
-        assert 'fdx_gpu_kernel_seconds_count{kernel="owner_batch"}' in m
+        owner = app.state.fdx["batcher"].owner
+        assert owner.native  # the linear model is served by the C++ owner loop
+        assert owner.rows == 64 and owner.batches <= 64
+        rows = [ln for ln in m.splitlines() if ln.startswith("fdx_gpu_owner_rows")]
+        assert float(rows[0].split()[-1]) == 64.0
 
 
 def test_gpu_worker_kernelshap_roundtrip(dev, tmp_path, restore_service, monkeypatch):

@@ -179,9 +179,11 @@ def test_multiworker_launcher_gpu_owner(dev, tmp_path):
 
 
 @pytest.mark.gpu
-def test_gpu_owner_in_process_batches(dev):
+@pytest.mark.parametrize("loop", ["native", "python"])
+def test_gpu_owner_in_process_batches(dev, loop, monkeypatch):
     from fraud_detection_amd.serve.gpu_owner import Dispatcher, GpuOwner, RingClient
 
+    monkeypatch.setenv("FDX_OWNER_LOOP", loop)
     eng = _engine("cuda")
     assert eng.calibration.get("source") in ("measured", "FDX_HOST_MAX_ROWS")
     owner = GpuOwner(eng, "").start()
@@ -193,8 +195,12 @@ def test_gpu_owner_in_process_batches(dev):
         with cf.ThreadPoolExecutor(32) as ex:
             got = list(ex.map(lambda i: disp.predict_proba(rows[i:i + 1])[0][0], range(600)))
         np.testing.assert_allclose(got, rp, atol=2e-6)
-        big, _ = disp.predict_proba(rows)  # > ZERO_COPY_ROWS: the H2D copy path
+        big, _ = disp.predict_proba(rows)  # > ZERO_COPY_ROWS: the H2D copy path (python loop)
         np.testing.assert_allclose(big, rp, atol=2e-6)
-        assert owner.batches < 600
+        p, z, phi = RingClient(owner.ring).predict_explain(rows[:100])  # LinearSHAP through the owner
+        _, _, rphi = cpu.predict_explain(rows[:100])
+        np.testing.assert_allclose(phi, rphi, rtol=1e-4, atol=1e-4)
+        assert owner.native == (loop == "native")
+        assert owner.batches < 600 and owner.rows >= 1300
     finally:
         owner.stop()
