@@ -122,7 +122,8 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     if os.path.exists(ring_src):
         ring = os.path.join(PKG_DIR, "_fdx_ring" + EXT_SUFFIX)
         if force or _newer(ring, [ring_src, os.path.join(CSRC, "serve", "shm_ring.h")]):
-            _run([os.environ.get("CXX", "g++"), *COMMON_FLAGS, "-shared", *_py_includes(), ring_src, "-o", ring])
+            _run([os.environ.get("CXX", "g++"), *COMMON_FLAGS, "-shared", *_py_includes(), ring_src, "-o", ring,
+                  "-lpthread"])
         outputs["ring"] = ring
     if verbose:
         for k, v in outputs.items():

@@ -3,6 +3,10 @@
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 
+#include <algorithm>
+#include <chrono>
+#include <thread>
+
 #include "shm_ring.h"
 
 namespace py = pybind11;
@@ -76,6 +80,48 @@ PYBIND11_MODULE(_fdx_ring, m) {
            py::arg("prob"), py::arg("logit"), py::arg("phi") = 0, py::arg("dphi") = 0, py::arg("ok") = true,
            py::arg("set") = 0)
       .def("pending_slots", &Ring::pending_slots);
+  // Native load generator (tools/serve_latency.py): `threads` C++ producer threads, each issuing
+  // `per_thread` synchronous requests of `rows` rows -- the owner's capacity without a Python
+  // producer's interpreter in the measurement.  -> (elapsed seconds, per-request latencies in us)
+  m.def("loadgen", [](const std::string& path, int threads, int per_thread, int rows, double timeout_ms) {
+    Ring r(path);
+    const uint32_t d = r.d(), W = r.out_w();
+    std::vector<std::vector<float>> lat(threads);
+    std::vector<int> failures(threads, 0);
+    double elapsed = 0.0;
+    {
+      py::gil_scoped_release nogil;
+      auto t0 = std::chrono::steady_clock::now();
+      std::vector<std::thread> th;
+      for (int k = 0; k < threads; ++k) {
+        th.emplace_back([&, k] {
+          std::vector<float> X((size_t)rows * d), out((size_t)rows * W);
+          for (size_t i = 0; i < X.size(); ++i) X[i] = (float)((i * 2654435761u + k) % 1000) * 1e-3f - 0.5f;
+          lat[k].reserve(per_thread);
+          for (int i = 0; i < per_thread; ++i) {
+            auto a = std::chrono::steady_clock::now();
+            try {
+              r.request(X.data(), out.data(), (uint32_t)rows, 0, timeout_ms);
+            } catch (...) {
+              ++failures[k];
+            }
+            auto b = std::chrono::steady_clock::now();
+            lat[k].push_back((float)std::chrono::duration<double, std::micro>(b - a).count());
+          }
+        });
+      }
+      for (auto& t : th) t.join();
+      elapsed = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    }
+    size_t total = 0;
+    for (auto& v : lat) total += v.size();
+    py::array_t<float> L(total);
+    float* o = L.mutable_data();
+    for (auto& v : lat) o = std::copy(v.begin(), v.end(), o);
+    int fails = 0;
+    for (int f : failures) fails += f;
+    return py::make_tuple(elapsed, L, fails);
+  }, py::arg("path"), py::arg("threads"), py::arg("per_thread"), py::arg("rows") = 1, py::arg("timeout_ms") = 10000.0);
   m.attr("OWNER_STARTING") = (int)OWNER_STARTING;
   m.attr("OWNER_READY") = (int)OWNER_READY;
   m.attr("OWNER_STOPPED") = (int)OWNER_STOPPED;

@@ -69,6 +69,42 @@ def _producer(ring, threads, per_thread, q):
     q.put((t0, time.perf_counter(), [x for ls in lat for x in ls]))
 
 
+def ring_native_loadgen(configs, window_us=0):
+    """Native producer threads (C++, _fdx_ring.loadgen) against ONE GPU-owner process: the
+    owner's micro-batching capacity without Python producers in the measurement."""
+    import subprocess
+
+    from fraud_detection_amd import _fdx_ring as R
+    from fraud_detection_amd.serve.gpu_owner import RingClient
+
+    ring = f"/dev/shm/fdx_lg_ring_{os.getpid()}"
+    env = dict(os.environ, FDX_MICROBATCH_US=str(window_us))
+    owner = subprocess.Popen([sys.executable, "-m", "fraud_detection_amd.serve.gpu_owner", "--ring", ring], env=env)
+    res = []
+    try:
+        t_end = time.time() + 240
+        while not os.path.exists(ring):
+            if owner.poll() is not None or time.time() > t_end:
+                raise RuntimeError("GPU owner did not start")
+            time.sleep(0.05)
+        cli = RingClient(ring)
+        R.loadgen(ring, 4, 500, 1)  # warm-up
+        for threads, per_thread, rows in configs:
+            s0 = cli.stats()
+            el, lat, fails = R.loadgen(ring, threads, per_thread, rows)
+            s1 = cli.stats()
+            n = threads * per_thread
+            lat = np.asarray(lat) * 1e-6
+            res.append({"producer_threads": threads, "rows_per_request": rows, "requests": n, "failures": int(fails),
+                        "rows_per_sec": round(n * rows / el, 1),
+                        "mean_rows_per_launch": round((s1["rows"] - s0["rows"]) / max(s1["batches"] - s0["batches"], 1), 2),
+                        **pct(lat)})
+    finally:
+        owner.terminate()
+        owner.wait(timeout=30)
+    return res
+
+
 def ring_microbatched(procs, threads, per_thread, window_us=0):
     """P producer processes x T threads of single-row requests -> one GPU-owner process."""
     import multiprocessing as mp
@@ -171,7 +207,8 @@ def main():
         gpu.host_max_rows = 0
         out["gpu_engine_batch1_device"] = engine_batch1(gpu, x1, a.reps)
         gpu.host_max_rows = thr
-        out["ring_microbatched"] = [ring_microbatched(p, t, n) for p, t, n in ((4, 8, 2000), (8, 8, 2000), (12, 8, 1500))]
+        out["ring_native_loadgen"] = ring_native_loadgen([(16, 4000, 1), (32, 3000, 1), (64, 2000, 1), (128, 1000, 1)])
+        out["ring_microbatched"] = [ring_microbatched(p, t, n) for p, t, n in ((4, 8, 2000), (8, 8, 2000))]
         X = rng.normal(0, 1, (1_000_000, 30)).astype(np.float32)
         for _ in range(3):
             gpu.predict_proba(X)
