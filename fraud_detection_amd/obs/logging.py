@@ -46,6 +46,9 @@ def configure(level: int = logging.INFO, fmt: str | None = None):
     if _configured:
         return
     fmt = fmt or os.getenv("FDX_LOG_FORMAT", "text")
+    env_level = os.getenv("FDX_LOG_LEVEL")
+    if env_level:  # e.g. WARNING in a latency benchmark (per-request INFO lines cost ~50 us each)
+        level = getattr(logging, env_level.upper(), level)
     h = logging.StreamHandler()
     h.addFilter(_ContextFilter())
     h.setFormatter(JsonFormatter() if fmt == "json" else logging.Formatter(TEXT_FORMAT))

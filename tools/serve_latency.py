@@ -178,6 +178,58 @@ def http(eng_device, reps):
     return pct(t)
 
 
+def http_launcher(owner_device, reps, workers=2):
+    """/predict over real HTTP (keep-alive connection) against the deployed process model
+    (serve/launch.py: GPU-owner process + HTTP workers with no HIP context)."""
+    import http.client
+    import socket
+    import subprocess
+    import tempfile
+
+    tmp = tempfile.mkdtemp()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ring = f"/dev/shm/fdx_lat_launch_{os.getpid()}_{port}"
+    env = dict(os.environ, DATABASE_URL=f"sqlite:///{tmp}/svc.db", MLFLOW_TRACKING_URI=f"file:{tmp}/none",
+               FDX_DEVICE=owner_device, FDX_LOG_LEVEL="WARNING")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.Popen([sys.executable, "-m", "fraud_detection_amd.serve.launch", "--workers", str(workers),
+                          "--host", "127.0.0.1", "--port", str(port), "--ring", ring], cwd=root, env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, start_new_session=True)
+    try:
+        t_end = time.time() + 240
+        while True:
+            try:
+                c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+                c.request("GET", "/status")
+                if c.getresponse().status == 200:
+                    break
+            except OSError:
+                pass
+            if p.poll() is not None or time.time() > t_end:
+                raise RuntimeError("launcher did not come up")
+            time.sleep(0.2)
+        c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
+        body = json.dumps({"features": [0.1] * 30})
+        hdr = {"Content-Type": "application/json"}
+        t = []
+        for i in range(reps + 100):
+            t0 = time.perf_counter()
+            c.request("POST", "/predict", body, hdr)
+            r = c.getresponse()
+            r.read()
+            dt = time.perf_counter() - t0
+            assert r.status == 200
+            if i >= 100:
+                t.append(dt)
+        return {"owner_device": owner_device, "http_workers": workers, **pct(t)}
+    finally:
+        os.killpg(p.pid, 15)
+        p.wait(timeout=30)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json", default=None)
@@ -199,6 +251,7 @@ def main():
     for dv in devs:
         best = min(runs[dv], key=lambda r: r["p50_us"])
         out["http_predict_gpu" if dv == "cuda" else "http_predict_cpu"] = {**best, "runs": runs[dv]}
+    out["http_predict_deployed"] = [http_launcher(dv, min(a.reps, 1000)) for dv in devs]
     if torch.cuda.is_available():
         gpu = InferenceEngine.from_paths(device="cuda")
         out["gpu_engine_calibration"] = {"host_max_rows": gpu.host_max_rows, **gpu.calibration}
