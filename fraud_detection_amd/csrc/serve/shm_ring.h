@@ -335,10 +335,7 @@ class Ring {
   // sleep on `completions` until pred() or the deadline; spins first (a batch completes in ~tens of us)
   template <class Pred>
   bool sleep_until(Pred pred, uint64_t deadline) {
-    // spin briefly (a batch completes in ~tens of us), less when many producers already sleep:
-    // spinning waiters beyond the core count only take cycles from the owner
-    const int spins = h_->sleepers.load(std::memory_order_relaxed) > 8 ? 16 : 128;
-    for (int i = 0; i < spins; ++i) {
+    for (int i = 0; i < 128; ++i) {
       if (pred()) return true;
       cpu_relax();
     }

@@ -474,7 +474,7 @@ class InferenceEngine(_EngineBase):
         P.native().event_sync(self._oevents[handle[1]])
         return handle[2]
 
-    def start_native_owner(self, ring, cap: int, window_us: float, pipe_rows: int = 64) -> int:
+    def start_native_owner(self, ring, cap: int, window_us: float, pipe_rows: int = 8) -> int:
         """Start the C++ owner loop on this engine's folded weights (GPU only): two device-mapped
         pinned input buffers (owner_input) and two device-mapped pinned output buffers."""
         m = P.native()

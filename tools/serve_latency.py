@@ -212,7 +212,9 @@ def http_launcher(owner_device, reps, workers=2):
                 raise RuntimeError("launcher did not come up")
             time.sleep(0.2)
         c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
-        body = json.dumps({"features": [0.1] * 30})
+        c.connect()
+        c.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)  # headers + body: no Nagle stall
+        body = json.dumps({"features": [0.1] * 30}).encode()
         hdr = {"Content-Type": "application/json"}
         t = []
         for i in range(reps + 100):
