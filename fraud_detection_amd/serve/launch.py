@@ -16,6 +16,7 @@ from __future__ import annotations
 import argparse
 import os
 import signal
+import socket
 import subprocess
 import sys
 import time
@@ -45,8 +46,18 @@ def main(argv=None) -> int:
             return 1
         time.sleep(0.05)
     env = dict(os.environ, FDX_GPU_OWNER_RING=ring, FDX_DEVICE="cpu")
-    front = subprocess.Popen([sys.executable, "-m", "uvicorn", a.app, "--host", a.host, "--port", str(a.port),
-                              "--workers", str(a.workers)], env=env)
+    # The listening socket is made here with TCP_NODELAY set, so every accepted connection
+    # inherits it (Linux copies it on accept): uvicorn's multi-worker mode shares a socket whose
+    # accepted connections asyncio does NOT switch to NODELAY, and a response written in two
+    # segments then waits for the client's delayed ACK (~40 ms per request, measured).
+    lsock = socket.socket(socket.AF_INET6 if ":" in a.host else socket.AF_INET, socket.SOCK_STREAM)
+    lsock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+    lsock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+    lsock.bind((a.host, a.port))
+    lsock.listen(2048)
+    lsock.set_inheritable(True)
+    front = subprocess.Popen([sys.executable, "-m", "uvicorn", a.app, "--fd", str(lsock.fileno()),
+                              "--workers", str(a.workers)], env=env, pass_fds=(lsock.fileno(),))
     procs = [owner, front]
 
     def _fwd(signum, _frame):
