@@ -224,14 +224,47 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
         except (ValueError, SQLAlchemyError) as e:  # non-UUID ids skip the row; DB outage is non-fatal
             logger.warning("could not persist pending row for %s: %s", tx_id, e)
 
-    def _enqueue(tx_id: str, features_dict: dict, cid: str) -> str:
+    def _enqueue(tx_id: str, features_dict: dict, cid: str, conn=None) -> str:
         try:
+            kw = {"conn": conn} if conn is not None else {}
             _tasks().send_task(TASK_NAME, args=[tx_id, features_dict, cid],
-                               headers={"correlation_id": cid, "traceparent": tracing.new_traceparent()})
+                               headers={"correlation_id": cid, "traceparent": tracing.new_traceparent()}, **kw)
             return "Calculation queued"
         except Exception as e:  # noqa: BLE001
+            if conn is not None:
+                raise  # the one-transaction path falls back to the two separate writes
             logger.error("[%s] Failed to queue SHAP task: %s", cid, e)
             return "Queue failed"
+
+    def _shared_queue_engine() -> bool:
+        """The durable broker lives in the store's database (the default: FDX_QUEUE_URL unset)."""
+        try:
+            q = _tasks().queue
+        except Exception:  # noqa: BLE001
+            return False
+        return getattr(q, "engine", None) is _db()
+
+    def _persist_and_enqueue(tx_id: str, features_dict: dict, score: float | None, cid: str) -> str:
+        """Pending row + SHAP task.  When the broker shares the store's database both inserts go
+        in ONE transaction (one commit per request instead of two: the commit, not the model, is
+        what a deployed /predict waits on); otherwise, or if that transaction fails, the two
+        separate writes with their own failure semantics."""
+        if _shared_queue_engine():
+            try:
+                with _db().begin() as c:
+                    try:
+                        rid = uuid.UUID(tx_id)
+                    except ValueError:
+                        rid = None  # non-UUID ids skip the row, as in _persist_pending
+                    t = TransactionResult.__table__
+                    if rid is not None and c.execute(select(t.c.id).where(t.c.id == rid)).first() is None:
+                        c.execute(t.insert().values(id=rid, input_data=features_dict, prediction_score=score,
+                                                    status=StatusEnum.PENDING.value))
+                    return _enqueue(tx_id, features_dict, cid, conn=c)
+            except Exception as e:  # noqa: BLE001
+                logger.warning("[%s] single-transaction enqueue failed (%s); separate writes", cid, e)
+        _persist_pending(tx_id, features_dict, score)
+        return _enqueue(tx_id, features_dict, cid)
 
     @app.post("/predict", response_model=PredictionOut, tags=["Prediction"])
     def predict(transaction: TransactionIn, request: Request):
@@ -244,8 +277,7 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
             prob, _ = batcher_().predict_one(x)
         prediction = int(prob > 0.5)
         features_dict = {f"feature_{i}": float(v) for i, v in enumerate(x.tolist())}
-        _persist_pending(transaction.transaction_id, features_dict, prob)
-        explanation_status = _enqueue(transaction.transaction_id, features_dict, cid)
+        explanation_status = _persist_and_enqueue(transaction.transaction_id, features_dict, prob, cid)
         logger.info("[%s] Prediction done: %s, SHAP status: %s", cid, prediction, explanation_status)
         return PredictionOut(transaction_id=transaction.transaction_id, prediction=prediction, score=prob,
                              correlation_id=cid, explanation_status=explanation_status)
@@ -256,8 +288,7 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
         metrics.predictions_submitted.inc()
         x = _validate(transaction.features)
         features_dict = {f"feature_{i}": float(v) for i, v in enumerate(x.tolist())}
-        _persist_pending(transaction.transaction_id, features_dict, None)
-        if _enqueue(transaction.transaction_id, features_dict, cid) != "Calculation queued":
+        if _persist_and_enqueue(transaction.transaction_id, features_dict, None, cid) != "Calculation queued":
             raise HTTPException(status_code=503, detail="Queue unavailable")
         return PredictAccepted(transaction_id=transaction.transaction_id, status="PENDING")
 

@@ -158,11 +158,12 @@ class TaskApp:
             return deco(dargs[0])
         return deco
 
-    def send_task(self, name: str, args=None, kwargs=None, countdown: float = 0.0, headers=None, task_id=None):
+    def send_task(self, name: str, args=None, kwargs=None, countdown: float = 0.0, headers=None, task_id=None,
+                  conn=None):
         t = self.tasks.get(name)
         max_retries = t.max_retries if t else 5
         tid = self.queue.send(name, args=args, kwargs=kwargs, countdown=countdown, max_retries=max_retries,
-                              headers=headers, task_id=task_id)
+                              headers=headers, task_id=task_id, conn=conn)
         return AsyncResult(self, tid)
 
     def AsyncResult(self, task_id: str) -> AsyncResult:  # noqa: N802 (celery API name)

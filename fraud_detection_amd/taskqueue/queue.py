@@ -51,14 +51,20 @@ class DurableQueue:
 
     # ---- producer ------------------------------------------------------------------------
     def send(self, name: str, args=None, kwargs=None, countdown: float = 0.0, max_retries: int = 5,
-             headers: dict | None = None, task_id: str | None = None) -> str:
+             headers: dict | None = None, task_id: str | None = None, conn=None) -> str:
+        """Insert one QUEUED task.  ``conn``: an open transaction on this queue's engine to insert
+        in (the API's /predict commits its pending row and the task together: one commit)."""
         now = time.time()
         tid = task_id or str(uuid.uuid4())
+        ins = TaskRecord.__table__.insert().values(
+            id=tid, name=name, args=list(args or []), kwargs=dict(kwargs or {}), headers=dict(headers or {}),
+            status=QUEUED, attempts=0, max_retries=max_retries, eta=now + float(countdown), lease_until=0.0,
+            worker=None, result=None, error=None, created_at=now, updated_at=now)
+        if conn is not None:
+            conn.execute(ins)
+            return tid
         with self.engine.begin() as c:
-            c.execute(TaskRecord.__table__.insert().values(
-                id=tid, name=name, args=list(args or []), kwargs=dict(kwargs or {}), headers=dict(headers or {}),
-                status=QUEUED, attempts=0, max_retries=max_retries, eta=now + float(countdown), lease_until=0.0,
-                worker=None, result=None, error=None, created_at=now, updated_at=now))
+            c.execute(ins)
         return tid
 
     # ---- consumer ------------------------------------------------------------------------

@@ -214,19 +214,32 @@ def http_launcher(owner_device, reps, workers=2):
         c = http.client.HTTPConnection("127.0.0.1", port, timeout=10)
         c.connect()
         c.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)  # headers + body: no Nagle stall
-        body = json.dumps({"features": [0.1] * 30}).encode()
         hdr = {"Content-Type": "application/json"}
-        t = []
-        for i in range(reps + 100):
-            t0 = time.perf_counter()
-            c.request("POST", "/predict", body, hdr)
-            r = c.getresponse()
-            r.read()
-            dt = time.perf_counter() - t0
-            assert r.status == 200
-            if i >= 100:
-                t.append(dt)
-        return {"owner_device": owner_device, "http_workers": workers, **pct(t)}
+        feats = [0.1] * 30
+        # predict: the full contract (score + pending row + SHAP task, one DB commit);
+        # predict_no_row: a non-UUID id skips the pending row (task insert only);
+        # score_only: /predict/batch with one row (no DB) -- front-end + routing + model;
+        # status: the HTTP floor of this process model.
+        cases = [("predict", "POST", "/predict", lambda i: {"features": feats}),
+                 ("predict_no_row", "POST", "/predict", lambda i: {"features": feats, "transaction_id": f"lat-{i}"}),
+                 ("score_only", "POST", "/predict/batch", lambda i: {"rows": [feats]}),
+                 ("status", "GET", "/status", None)]
+        res = {"owner_device": owner_device, "http_workers": workers}
+        for name, method, path, mk in cases:
+            t = []
+            for i in range(reps + 100):
+                body = json.dumps(mk(i)).encode() if mk else None
+                t0 = time.perf_counter()
+                c.request(method, path, body, hdr if body else {})
+                r = c.getresponse()
+                r.read()
+                dt = time.perf_counter() - t0
+                assert r.status == 200, (path, r.status)
+                if i >= 100:
+                    t.append(dt)
+            res[name] = pct(t)
+        res.update(res["predict"])  # top-level p50/p99 = the full /predict contract
+        return res
     finally:
         os.killpg(p.pid, 15)
         p.wait(timeout=30)
