@@ -368,6 +368,20 @@ PYBIND11_MODULE(_fdx_native, m) {
   }, py::arg("red"), py::arg("state"), py::arg("w32"), py::arg("done"), py::arg("d"), py::arg("C"), py::arg("tol"),
      py::arg("max_iter"), py::arg("fi"), py::arg("phase_start"), py::arg("aff"), py::arg("s"), py::arg("done_host") = 0,
      py::arg("seq") = 0);
+  m.def("logreg_init", [](u state, u w32, u class_w, u done, std::vector<double> w0, double cw0, double cw1, u aff,
+                          u s) {
+    if (w0.size() != 32) throw std::runtime_error("logreg_init: w0 must have 32 entries");
+    fdx::LRInitArgs a;
+    for (int j = 0; j < 32; ++j) a.w0[j] = w0[j];
+    a.cw0 = (float)cw0;
+    a.cw1 = (float)cw1;
+    fdx::launch_logreg_init(a, P<double>(state), P<float>(w32), P<float>(class_w), P<int>(done),
+                            P<const double>(aff), S(s));
+  }, py::arg("state"), py::arg("w32"), py::arg("class_w"), py::arg("done"), py::arg("w0"), py::arg("cw0"),
+     py::arg("cw1"), py::arg("aff"), py::arg("s"));
+  m.def("logreg_export", [](u state, u host_dev, u s) {
+    fdx::launch_logreg_export(P<const double>(state), P<double>(host_dev), S(s));
+  });
   m.def("logreg_fold", [](u state, u aff, u w32, u s) {
     fdx::launch_logreg_fold(P<const double>(state), P<const double>(aff), P<float>(w32), S(s));
   });

@@ -103,6 +103,14 @@ void launch_newton_update(const double* red, double* state, float* w32, int* don
 void launch_newton_update_stamped(const double* red, double* state, float* w32, int* done, double C,
                                   const double* aff, unsigned long long* stamps, hipStream_t stream);
 void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream);
+// Fit-start state from kernel arguments (w0 in padded layout, class weights).
+struct LRInitArgs {
+  double w0[32];
+  float cw0, cw1;
+};
+void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
+                        const double* aff, hipStream_t stream);
+void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream);
 void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
                        double momentum, int fit_intercept, hipStream_t stream, const double* aff = nullptr);
 

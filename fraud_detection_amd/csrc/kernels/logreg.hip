@@ -226,37 +226,49 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   }
 }
 
-// Stage 2: fixed-order fp64 reduction of [nblocks][1088] partials.  Block = 64 columns x 16
-// row-groups (1024 threads).
+// Stage 2: fixed-order fp64 reduction of [nblocks][1088] partials.  Block = 16 columns x 64
+// row-groups (1024 threads), 68 blocks for the full 1088-wide vector: the partials were just
+// written by the pass and sit in L2/MALL, so the kernel is load-LATENCY bound -- each thread's
+// <= 12 loads are all in flight at once (one round trip, not six as with 16 row-groups), and the
+// 64 row-group sums are combined in a fixed tree order (bitwise reproducible run to run).
+constexpr int kRedCols = 16, kRedGroups = 64, kRedLoads = 12;  // kRedGroups * kRedLoads >= nblocks
 __global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __restrict__ partial,
                                                              int nblocks, int ncols,
                                                              double* __restrict__ out,
                                                              const int* __restrict__ done) {
   if (done != nullptr && *done) return;
-  __shared__ double red[16][64];
-  const int c = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int col = blockIdx.x * 64 + c;
-  // 8 independent accumulators keep 8 loads in flight per lane (the partials were just written
-  // by the pass and sit in L2/MALL: this kernel is load-latency bound, not bandwidth bound).
-  double acc[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  __shared__ double red[kRedGroups][kRedCols + 1];
+  const int c = threadIdx.x & (kRedCols - 1), grp = threadIdx.x / kRedCols;
+  const int col = blockIdx.x * kRedCols + c;
+  double acc = 0.0;
   if (col < ncols) {
-    int b = grp;
-    for (; b + 7 * 16 < nblocks; b += 8 * 16) {
+    for (int b0 = grp; b0 < nblocks; b0 += kRedGroups * kRedLoads) {
+      float v[kRedLoads];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc[u] += (double)partial[(int64_t)(b + u * 16) * kLRPartStride + col];
+      for (int u = 0; u < kRedLoads; ++u) {
+        const int b = b0 + u * kRedGroups;
+        v[u] = b < nblocks ? partial[(int64_t)b * kLRPartStride + col] : 0.0f;
+      }
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+      for (int u = 0; u < kRedLoads; u += 4) {
+        a0 += (double)v[u];
+        a1 += (double)v[u + 1];
+        a2 += (double)v[u + 2];
+        a3 += (double)v[u + 3];
+      }
+      acc += (a0 + a1) + (a2 + a3);
     }
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (b + u * 16 < nblocks) acc[u] += (double)partial[(int64_t)(b + u * 16) * kLRPartStride + col];
   }
-  red[grp][c] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  red[grp][c] = acc;
   __syncthreads();
-  if (grp == 0 && col < ncols) {
-    double s = 0.0;
+  // fixed-order tree over the 64 row-groups: 32 -> 16 -> ... -> 1
 #pragma unroll
-    for (int k = 0; k < 16; ++k) s += red[k][c];
-    out[col] = s;
+  for (int h = kRedGroups / 2; h > 0; h >>= 1) {
+    if (grp < h) red[grp][c] += red[grp + h][c];
+    __syncthreads();
   }
+  if (grp == 0 && col < ncols) out[col] = red[0][c];
 }
 
 // ---- Newton / SGD state (fp64, on device) -------------------------------------------------
@@ -522,6 +534,52 @@ __global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restric
   store_folded(ss, cA, iA, w32, t);
 }
 
+// Fit start: the whole workspace blob (state, w32, class weights, done flag) from kernel
+// arguments, with the affine fold of w0 when the rows are pivot-shifted -- one launch instead of
+// a pinned-staging H2D blit plus the fold kernel (a blit to/from host memory is ~9 us in the
+// step timeline, profiles/r3_f/timeline_bf16_step.txt).
+__global__ __launch_bounds__(64) void logreg_init_kernel(LRInitArgs a, double* __restrict__ st,
+                                                         float* __restrict__ w32, float* __restrict__ cw,
+                                                         int* __restrict__ done, const double* __restrict__ aff) {
+  __shared__ double ss[kW + 32], cA[32], iA[32];
+  const int t = threadIdx.x;
+  double w0 = 0.0;
+#pragma unroll
+  for (int j = 0; j < 32; ++j)  // static indices: no dynamic addressing of the argument struct
+    if ((t & 31) == j) w0 = a.w0[j];
+  if (t < 32) ss[kW + t] = w0;
+#pragma unroll
+  for (int i = 0; i < kStateSize / 64; ++i) {
+    const int e = t + 64 * i;
+    double v = 0.0;
+    if (e < 64) v = w0;  // kW and kWPrev
+    else if (e == kObjPrev) v = __builtin_inf();
+    st[e] = v;
+  }
+  if (t == 0) {
+    cw[0] = a.cw0;
+    cw[1] = a.cw1;
+    *done = 0;
+  }
+  if (aff) {
+    const double av = aff[t];
+    if (t < 32) cA[t] = av; else iA[t - 32] = av;
+    __syncthreads();
+    store_folded(ss, cA, iA, w32, t);
+  } else if (t < kCols) {
+    w32[t] = (t == kLabelCol) ? 0.0f : (float)w0;
+  }
+}
+
+// Solver state -> host: plain vector stores into a mapped pinned buffer (device address of the
+// host allocation), replacing a D2H blit at the end of every fit.
+__global__ __launch_bounds__(64) void logreg_export_kernel(const double* __restrict__ st, double* __restrict__ host) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int i = 0; i < kStateSize / 64; ++i)  // system scope: written through to host memory
+    __hip_atomic_store(host + t + 64 * i, st[t + 64 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.  aff (nullable): the rows are
 // pivot-shifted (fused scaler pass); the gradient maps into standardized space exactly as in the
 // Newton update (g_z[j] = inv_j (g_j - c_j g_30)) and w32 gets the folded weights.
@@ -625,7 +683,7 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream) {
   // ncols = 64 for gradient-only passes (SGD), kLRPartStride when the Hessian was accumulated.
-  logreg_reduce_kernel<<<(ncols + 63) / 64, 1024, 0, stream>>>(partial, nblocks, ncols, out, done);
+  logreg_reduce_kernel<<<(ncols + kRedCols - 1) / kRedCols, 1024, 0, stream>>>(partial, nblocks, ncols, out, done);
   check_launch("logreg_reduce");
 }
 
@@ -646,6 +704,17 @@ void launch_newton_update_stamped(const double* red, double* state, float* w32, 
   newton_update_kernel<31, true><<<1, 64, 0, stream>>>(red, state, w32, done, 30, C, 0.0, 1 << 30, 1, 0, aff,
                                                        stamps);
   check_launch("newton_update_stamped");
+}
+
+void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
+                        const double* aff, hipStream_t stream) {
+  logreg_init_kernel<<<1, 64, 0, stream>>>(a, state, w32, class_w, done, aff);
+  check_launch("logreg_init");
+}
+
+void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream) {
+  logreg_export_kernel<<<1, 64, 0, stream>>>(state, host_dev);
+  check_launch("logreg_export");
 }
 
 void launch_logreg_fold(const double* state, const double* aff, float* w32, hipStream_t stream) {

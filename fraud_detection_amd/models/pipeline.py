@@ -52,6 +52,10 @@ class TrainConfig:
     sgd_epochs: int = 5
     sgd_batch_rows: int = 1 << 22
     check_every: int = 1            # Newton: iterations per convergence-flag read (host reads one chunk behind)
+    # Newton, one process, resident rows: enqueue the full-data iteration count the previous fit
+    # of this shape needed and verify convergence when the training buffer is next reused (two
+    # buffers alternate) -- no host wait and no trailing no-op iterations inside the fit
+    deferred_check: bool = True
     init_std: float = 0.01          # random-init weights ~ N(0, init_std^2) (seeded by `seed`)
     hess_stride: int | str = "auto"  # Newton: Hessian from every k-th row tile (gradient always exact)
     # SMOTE under data parallelism: "global" = the single-process result exactly -- every rank
@@ -122,18 +126,49 @@ class DevicePipeline:
         self.cfg = cfg or TrainConfig()
         self.comm = comm
         self._ws = None
-        self._buf = None
+        self._buf = None   # the training buffer of the latest fit
         self._side = None  # side stream for the class-count kernels (fused path)
+        # deferred convergence checks: two training buffers / solver workspaces alternate; the fit
+        # whose rows live in buffer b is verified before b is written again
+        self._bufs, self._wss, self._pending = [None, None], [None, None], [None, None]
+        self._bi = self._cur = 0
+        self._full_pred = None  # (signature, full-data iterations of the last settled fit)
+        self._defer_now = False
 
     def _world(self):
         c = self.comm
         return (c.rank, c.world_size) if c is not None else (0, 1)
 
-    def _train_buffer(self, n_rows: int, device) -> torch.Tensor:
-        dt = TORCH_STORAGE[self.cfg.storage]
-        if self._buf is None or self._buf.shape[0] < n_rows or self._buf.device != device or self._buf.dtype != dt:
-            self._buf = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
-        return self._buf[:n_rows]
+    def _settle(self, b: int):
+        """Verify the fit whose rows live in buffer b (finishing it if its predicted iteration
+        count was short) and learn its full-data iteration count for the next prediction."""
+        f, self._pending[b] = self._pending[b], None
+        if f is not None:
+            sig = f._fdx_sig
+            f.verify()
+            self._full_pred = (sig, f.full_phase_iters)
+
+    def _train_buffer(self, n_rows: int, device, allow_double: bool = False) -> torch.Tensor:
+        cfg = self.cfg
+        dt = TORCH_STORAGE[cfg.storage]
+        double = (allow_double and cfg.deferred_check and cfg.solver == "newton" and device.type == "cuda"
+                  and self._world()[1] == 1)
+        b = self._bi if double else 0
+        for i in range(2):  # a buffer about to be written must not hold an unverified fit
+            if i == b or not double:
+                self._settle(i)
+        buf = self._bufs[b]
+        if buf is None or buf.shape[0] < n_rows or buf.device != device or buf.dtype != dt:
+            self._bufs[b] = None
+            need = n_rows * NCOLS * torch.empty((), dtype=dt).element_size()
+            if double and b == 1 and torch.cuda.mem_get_info(device)[0] < 2 * need:
+                double, b = False, 0  # no room for a second buffer: checked fits, one buffer
+                self._settle(0)
+                buf = self._bufs[0]
+            if buf is None or buf.shape[0] < n_rows or buf.device != device or buf.dtype != dt:
+                buf = self._bufs[b] = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
+        self._buf, self._cur, self._defer_now = buf, b, double
+        return buf[:n_rows]
 
     def fit_host(self, X: torch.Tensor, y: torch.Tensor, device=None, budget: int | None = None,
                  profile: bool = False) -> PipelineResult:
@@ -210,7 +245,7 @@ class DevicePipeline:
         # training buffer sized for the largest possible SMOTE output, so the cast does not wait
         # for the minority count (+128: a global-scope slice boundary moves by < 128 rows)
         cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) + 128 if cfg.smote else 0)
-        rows_cap = self._train_buffer(cap, dev)
+        rows_cap = self._train_buffer(cap, dev, allow_double=True)
         if fused:
             # ---- K1+K2 fused: statistics (C1 all-reduce inside) + shifted bf16 / fp8 rows ----
             # ---- class counts (C2) on a side stream beside it; the host reads the total during K1+K2
@@ -304,16 +339,26 @@ class DevicePipeline:
             pos = float(sum(r[0] + q for r, q in zip(ranks, new_per_rank)))
             class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         # ---- K4: fit ---------------------------------------------------------------------
-        if dev.type == "cuda" and (self._ws is None or self._ws.device != dev):
-            self._ws = lr_ops.LRWorkspace(dev)
+        b = self._cur
+        if dev.type == "cuda" and (self._wss[b] is None or self._wss[b].device != dev):
+            self._wss[b] = lr_ops.LRWorkspace(dev)
+        self._ws = self._wss[b]
         w0 = np.zeros(NCOLS)
         if cfg.init_std > 0:
             w0[:d] = np.random.default_rng(cfg.seed).normal(0.0, cfg.init_std, d)
         if cfg.solver == "newton":
+            defer = self._defer_now and comm is None and dev.type == "cuda"
+            sig = (rows.shape[0], n_sched, cfg.C, cfg.tol, cfg.max_iter, tuple(class_w), str(cfg.hess_stride),
+                   fused, cfg.storage)
+            pred = self._full_pred[1] if (defer and self._full_pred and self._full_pred[0] == sig) else None
             fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
                                     check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride,
-                                    n_sched=n_sched, affine=stats.aff if fused else None)
+                                    n_sched=n_sched, affine=stats.aff if fused else None, full_iters=pred)
+            if defer and isinstance(fit, lr_ops.PendingFit):
+                fit._fdx_sig = sig
+                self._pending[b] = fit
+                self._bi = b ^ 1
         elif cfg.solver == "sgd":
             fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                  batch_rows=min(cfg.sgd_batch_rows, getattr(getattr(self, "last_plan", None),

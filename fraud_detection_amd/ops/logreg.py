@@ -49,19 +49,28 @@ class PendingFit:
     field waits for that copy only, so a caller that does not look at the result right away (a
     training loop, the benchmark) queues the next fit behind this one with no host round trip at
     the fit boundary.  Pinned slots rotate through a small pool; a slot's previous owner is
-    materialised before the slot is reused."""
+    materialised before the slot is reused.
+
+    ``verify`` (newton_fit(full_iters=...)): a deferred convergence check.  The fit was enqueued
+    with a predicted number of full-data iterations and no host wait; ``verify()`` (implicit in
+    any field read) waits for the last one's flag and, if the fit had not converged, runs the
+    remaining iterations then -- so the caller must keep the rows and the workspace untouched
+    until the fit is verified (models/pipeline.py double-buffers both)."""
 
     _pool: list = []
+    _pool_dev: list = []
     _owners: list = []
     _next = 0
     _POOL = 8
 
-    def __init__(self, state_dev: torch.Tensor, sgd: bool = False):
+    def __init__(self, state_dev: torch.Tensor, sgd: bool = False, verify=None, warm_iters: int = 0):
         cls = PendingFit
         if not cls._pool:
             cls._pool = [torch.empty(state_dev.numel(), dtype=torch.float64, pin_memory=True)
                          for _ in range(cls._POOL)]
             cls._owners = [None] * cls._POOL
+            # device addresses of the mapped pinned slots: the export kernel stores into them
+            cls._pool_dev = [int(native().host_device_pointer(t.data_ptr())) for t in cls._pool]
         slot = cls._next % cls._POOL
         cls._next += 1
         prev = cls._owners[slot]
@@ -69,12 +78,32 @@ class PendingFit:
             prev._materialize()
         cls._owners[slot] = self
         self._slot, self._sgd, self._info = slot, sgd, None
-        cls._pool[slot].copy_(state_dev, non_blocking=True)
+        self._verify, self._state_dev, self.warm_iters = verify, state_dev, int(warm_iters)
+        self._export()
+
+    def _export(self):
+        cls, slot, st = PendingFit, self._slot, self._state_dev
+        if cls._pool_dev[slot] and st.numel() == STATE_SIZE:
+            native().logreg_export(ptr(st), cls._pool_dev[slot], stream_of(st))
+        else:
+            cls._pool[slot].copy_(st, non_blocking=True)
         self._event = torch.cuda.Event()
         self._event.record()
 
+    def verify(self) -> "PendingFit":
+        """Resolve a deferred convergence check (no-op for an already checked fit)."""
+        v, self._verify = self._verify, None
+        if v is not None and v():
+            self._export()  # the fit continued: export its final state again
+        return self
+
+    @property
+    def deferred(self) -> bool:
+        return self._verify is not None
+
     def _materialize(self) -> FitInfo:
         if self._info is None:
+            self.verify()
             self._event.synchronize()
             self._info = _info_from_state(PendingFit._pool[self._slot].numpy().copy(), self._sgd)
             if PendingFit._owners[self._slot] is self:
@@ -88,6 +117,11 @@ class PendingFit:
 
     def as_fit_info(self) -> FitInfo:
         return self._materialize()
+
+    @property
+    def full_phase_iters(self) -> int:
+        """Full-data iterations the fit ran (after the progressive warm-up)."""
+        return int(self._materialize().n_iter) - self.warm_iters
 
 
 def fit_asdict(fit) -> dict:
@@ -113,22 +147,13 @@ class LRWorkspace:
         self._blob = torch.zeros(_BLOB_BYTES, device=device, dtype=torch.uint8)
         self.state, self.w32, self.class_w, self.done = _blob_views(self._blob)
 
-    def reset(self, w0: np.ndarray, class_w=(1.0, 1.0)):
-        """Initial state via pinned staging + one async H2D copy (no stream drain).  The staging
-        buffer is only rewritten after the previous fit's final state read-back synchronised."""
-        if not hasattr(self, "_blob_h"):
-            self._blob_h = torch.zeros(_BLOB_BYTES, dtype=torch.uint8, pin_memory=True)
-            self._views_h = [v.numpy() for v in _blob_views(self._blob_h)]
-        st, w32, cw, done = self._views_h
-        st[:] = 0.0
-        st[S_W:S_W + 32] = w0
-        st[S_WPREV:S_WPREV + 32] = w0
-        st[S_OBJPREV] = np.inf
-        w32[:] = np.asarray(w0, dtype=np.float32)
-        w32[LABEL_COL] = 0
-        cw[:] = class_w
-        done[:] = 0
-        self._blob.copy_(self._blob_h, non_blocking=True)
+    def reset(self, w0: np.ndarray, class_w=(1.0, 1.0), aff: int = 0):
+        """Initial state (w0 in the padded layout, class weights, done = 0) written by ONE kernel
+        whose arguments carry the values -- no pinned staging and no H2D blit.  ``aff``: device
+        address of the [64] affine map of pivot-shifted rows (w32 gets the folded weights)."""
+        w = np.asarray(w0, dtype=np.float64).reshape(-1)
+        native().logreg_init(ptr(self.state), ptr(self.w32), ptr(self.class_w), ptr(self.done), w.tolist(),
+                             float(class_w[0]), float(class_w[1]), int(aff), stream_of(self.state))
 
 
 _BLOB_BYTES = 2304
@@ -149,6 +174,18 @@ GRAD_SLOTS = 34  # red[0:32] gradient, red[32] loss, red[33] weight; red[34] = H
 
 def auto_hess_stride(n_rows: int) -> int:
     return int(max(1, min(8, n_rows // HESS_SAMPLE_ROWS)))
+
+
+# Warm-up phases only need a rough curvature model (they never decide convergence): their Hessian
+# from >= 64k rows.  At 16M rows this is stride 16 in both warm-up phases instead of 1 and 2: the
+# same 7 iterations (2 full-data), AUC within 1e-6, fit -45 us (profiles/r3_n/newton_lab.json:
+# a 1/16-sample pass is 22.8 us with every tile's Hessian, 17.6 with every 8th; a 1/4 pass 56 vs 47).
+WARM_HESS_SAMPLE_ROWS = 1 << 16
+WARM_HESS_MAX_STRIDE = 16
+
+
+def auto_warm_hess_stride(n_rows: int) -> int:
+    return int(max(1, min(WARM_HESS_MAX_STRIDE, n_rows // WARM_HESS_SAMPLE_ROWS)))
 
 
 def auto_hess_refresh(n_rows: int) -> int:
@@ -232,7 +269,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
                hess_refresh: int | str = "auto", n_sched: int | None = None,
                local_warmup: bool = True, affine: torch.Tensor | None = None,
-               lookahead: int | None = None) -> FitInfo:
+               lookahead: int | None = None, full_iters: int | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -242,7 +279,12 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     reuse the last reduced Hessian still held in the workspace (lazy-Hessian Newton).  0 = every
     iteration.  The fixed point is unchanged: only the step's curvature model is older.
     ``affine``: [64] float64 (c | 1/sigma) when the rows are pivot-shifted instead of standardized
-    (ops/scaler.scaler_fit_cast): the fit still runs in standardized space (same w, same C)."""
+    (ops/scaler.scaler_fit_cast): the fit still runs in standardized space (same w, same C).
+    ``full_iters`` (single process): enqueue exactly that many full-data iterations -- the count
+    the previous fit of this shape needed -- with no host wait, and return a PendingFit whose
+    ``verify()`` checks convergence later and finishes the fit if the prediction was short.  The
+    same iterations run either way; the host-checked loop's trailing no-op iterations and its
+    wait at the end of the fit disappear.  Rows and workspace must stay untouched until then."""
     check_rows(rows)
     w0 = _default_w0(w0)
     if not rows.is_cuda:
@@ -252,14 +294,13 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         return _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm, fp8_scale)
     m = native()
     ws = workspace or LRWorkspace(rows.device)
-    ws.reset(w0, class_w)
     s = stream_of(rows)
     aff = 0
     if affine is not None:
         if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
-        m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)  # w0 is standardized-space
+    ws.reset(w0, class_w, aff)  # w0 is standardized-space; w32 gets it folded for shifted rows
     n = rows.shape[0]
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
     # The warm-up schedule sets the number of collectives, so every rank must derive the same one:
@@ -285,7 +326,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     sync_warm = dp and not local_warmup
     first = [0]
     for sub, iters in sched:
-        hs_w = auto_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
+        hs_w = auto_warm_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
             _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub)
             if sync_warm:
@@ -347,26 +388,43 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         ws._events = [torch.cuda.Event() for _ in range(depth + 1)]
         ws._seq = 0
     flags, events, fdev = ws._flags, ws._events, ws._flag_dev
-    pending = []
-    it, slot = 0, 0
-    while it < max_iter:
+
+    def checked_loop(it: int):
+        pending = []
+        slot = 0
+        while it < max_iter:
+            ws._seq = (ws._seq + 1) & 0x3FFFFFFF
+            it += enqueue_chunk(min(check_every, max_iter - it), fdev[slot], ws._seq)
+            if not fdev[slot]:  # not a mapped allocation: copy the flag behind an event instead
+                flags[slot].copy_(ws.done, non_blocking=True)
+                events[slot].record()
+            pending.append((slot, ws._seq))
+            slot = (slot + 1) % (depth + 1)
+            if not sync or len(pending) <= depth:
+                continue
+            c, seq = pending.pop(0)
+            if fdev[c]:
+                _await_flag(flags[c], seq, s)
+            else:
+                events[c].synchronize()
+            if int(flags[c][0]) & 1:
+                break
+
+    if full_iters is not None and not dp and sync and fdev[0]:
+        k = int(max(1, min(int(full_iters), max_iter)))
         ws._seq = (ws._seq + 1) & 0x3FFFFFFF
-        it += enqueue_chunk(min(check_every, max_iter - it), fdev[slot], ws._seq)
-        if not fdev[slot]:  # not a mapped allocation: copy the flag behind an event instead
-            flags[slot].copy_(ws.done, non_blocking=True)
-            events[slot].record()
-        pending.append((slot, ws._seq))
-        slot = (slot + 1) % (depth + 1)
-        if not sync or len(pending) <= depth:
-            continue
-        c, seq = pending.pop(0)
-        if fdev[c]:
-            _await_flag(flags[c], seq, s)
-        else:
-            events[c].synchronize()
-        if int(flags[c][0]) & 1:
-            break
-    return PendingFit(ws.state)
+        seq0 = ws._seq
+        enqueue_chunk(k, fdev[0], seq0)
+
+        def verify() -> bool:
+            _await_flag(flags[0], seq0, s)
+            if int(flags[0][0]) & 1:
+                return False  # converged (or max_iter) within the predicted iterations
+            checked_loop(k)  # the prediction was short: finish the fit now
+            return True
+        return PendingFit(ws.state, verify=verify, warm_iters=warm)
+    checked_loop(0)
+    return PendingFit(ws.state, warm_iters=warm)
 
 
 def _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm):

@@ -217,6 +217,42 @@ def test_newton_deterministic(dev):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("pred", [1, 2, 6])
+def test_newton_deferred_check_same_fit(dev, pred):
+    """newton_fit(full_iters=k): k full-data iterations enqueued with no host wait, convergence
+    verified later.  A short prediction (1) is finished by verify(), a long one (6) runs no-op
+    iterations: every case is bit-identical to the host-checked fit, iteration count included."""
+    X, y = _data(300_000, seed=25, rate=0.02)
+    st = S.scaler_fit(X.to(dev))
+    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
+    sched = [(8, 2), (2, 1)]
+    ref_fit = L.newton_fit(rows, tol=1e-6, max_iter=30, progressive=sched).as_fit_info()
+    f = L.newton_fit(rows, tol=1e-6, max_iter=30, progressive=sched, workspace=L.LRWorkspace(dev), full_iters=pred)
+    assert f.deferred
+    got = f.as_fit_info()
+    assert not f.deferred and got.converged and ref_fit.converged
+    assert got.n_iter == ref_fit.n_iter and f.full_phase_iters == ref_fit.n_iter - 3
+    assert np.array_equal(got.w, ref_fit.w)
+
+
+def test_pipeline_deferred_check_matches_checked(dev):
+    """Pipeline fits with deferred checks (two alternating buffers, predicted iteration count)
+    return the same models as host-checked fits, fit after fit."""
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+    X, y = _data(400_000, seed=26, rate=0.01)
+    X, y = X.to(dev), y.to(dev)
+    on = DevicePipeline(TrainConfig(seed=3))
+    off = DevicePipeline(TrainConfig(seed=3, deferred_check=False))
+    res_on = [on.fit(X, y) for _ in range(4)]  # fit 3+ run with a prediction learned from fit 1
+    res_off = [off.fit(X, y) for _ in range(2)]
+    assert on._full_pred is not None
+    for r in res_on:
+        assert r.fit.n_iter == res_off[0].fit.n_iter
+        assert np.array_equal(r.w, res_off[0].w)
+    assert on._bufs[0] is not None and on._bufs[1] is not None and off._bufs[1] is None
+
+
 def test_sgd_reduces_objective(dev):
     X, y = _data(40_000, seed=13, rate=0.1)
     st = S.scaler_fit(X)

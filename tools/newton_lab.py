@@ -48,10 +48,12 @@ def main():
         w0[:30] = np.random.default_rng(cfg.seed).normal(0.0, cfg.init_std, 30)
     warm_iters = lambda sched: sum(it for _, it in sched)  # noqa: E731
 
-    def run(sched, lookahead=None, hess_stride="auto"):
-        f = L.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, w0=w0, workspace=ws,
+    def run(sched, lookahead=None, hess_stride="auto", max_iter=None):
+        # max_iter given: an "oracle" fit that enqueues exactly that many full-phase iterations
+        # with no host convergence checks (the floor for the host-checked loop)
+        f = L.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=max_iter or cfg.max_iter, w0=w0, workspace=ws,
                          progressive=sched, affine=aff, lookahead=lookahead, hess_stride=hess_stride,
-                         check_every=cfg.check_every)
+                         check_every=cfg.check_every, sync=max_iter is None)
         return f
 
     def timed(fn):
@@ -68,8 +70,41 @@ def main():
             ts.append(e0.elapsed_time(e1))
         return float(np.median(ts)), float(np.min(ts)), f
 
+    from fraud_detection_amd.ops.native import native, ptr, stream_of
+
+    m = native()
+    st = stream_of(rows)
+
+    def burst(fn, k=20):
+        """per-launch microseconds of k back-to-back launches (launch gaps included)"""
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(k):
+            fn()
+        e1.record()
+        e1.synchronize()
+        return round(e0.elapsed_time(e1) * 1000.0 / k, 2)
+
+    ws.reset(w0, (1.0, 1.0), ptr(aff))
+    kern = {}
+    for sub in (16, 4, 1):
+        for h in (0, 1, 2, 8):
+            kern[f"pass_sub{sub}_h{h}"] = burst(lambda: m.logreg_pass(ptr(rows), 0, n, ptr(ws.w32), ptr(ws.class_w), 0,
+                                                                      h, sub, ptr(ws.partial), ws.nblocks, st))
+    kern["reduce_full"] = burst(lambda: m.logreg_reduce(ptr(ws.partial), ws.nblocks, L.PART_STRIDE, ptr(ws.red), 0, st))
+    kern["reduce_grad"] = burst(lambda: m.logreg_reduce(ptr(ws.partial), ws.nblocks, L.GRAD_SLOTS, ptr(ws.red), 0, st))
+    kern["newton_update"] = burst(lambda: m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30,
+                                                          1.0, 0.0, 1 << 30, 1, 0, ptr(aff), st))
+    kern["init"] = burst(lambda: ws.reset(w0, (1.0, 1.0), ptr(aff)))
+    for name, v in kern.items():
+        print(f"{name:22s} {v:9.2f} us/launch", flush=True)
+
     default = L.progressive_schedule(n)
     cases = [("default", default, None, "auto"),
+             ("oracle", default, None, "auto"),
              ("lookahead1", default, 1, "auto"),
              ("lookahead3", default, 3, "auto"),
              ("s16x2_4x2", [(16, 2), (4, 2)], None, "auto"),
@@ -78,11 +113,15 @@ def main():
              ("s32x3_8x2", [(32, 3), (8, 2)], None, "auto"),
              ("s64x3_16x2_4x1", [(64, 3), (16, 2), (4, 1)], None, "auto"),
              ("s8x3_2x1", [(8, 3), (2, 1)], None, "auto"),
+             ("hs4", default, None, 4),
+             ("hs16", default, None, 16),
              ("none", [], None, "auto")]
-    out = {"rows": n, "default_schedule": default, "cases": {}}
+    out = {"rows": n, "default_schedule": default, "kernels_us": kern, "cases": {}}
     w_ref = None
+    full_default = None
     for name, sched, la, hs in cases:
-        med, mn, f = timed(lambda: run(sched, la, hs))
+        mi = full_default if name == "oracle" else None
+        med, mn, f = timed(lambda: run(sched, la, hs, mi))
         fi = f.as_fit_info() if hasattr(f, "as_fit_info") else f
         r2 = PipelineResult(scaler=res.scaler, fit=fi, n_rows=res.n_rows, n_train_rows=res.n_train_rows,
                             n_minority=res.n_minority, n_synthetic=res.n_synthetic, timings={})
@@ -90,6 +129,7 @@ def main():
         w = np.asarray(fi.w, dtype=np.float64)
         if w_ref is None:
             w_ref = w
+            full_default = int(fi.n_iter) - warm_iters(sched)
         rec = {"ms_median": round(med, 4), "ms_min": round(mn, 4), "iters": int(fi.n_iter),
                "full_phase_iters": int(fi.n_iter) - warm_iters(sched), "converged": bool(fi.converged),
                "auc": round(auc, 7), "max_abs_dw_vs_default": float(np.max(np.abs(w - w_ref))),
