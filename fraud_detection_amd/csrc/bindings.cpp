@@ -308,9 +308,9 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("compact_count", [](u labels, int64_t n, int target, u counts, int nblocks, u s) {
     fdx::launch_compact_count(P<const uint8_t>(labels), n, target, P<int64_t>(counts), nblocks, S(s));
   });
-  m.def("exclusive_scan_small", [](u a, int n, u total, u s) {
-    fdx::launch_exclusive_scan_small(P<int64_t>(a), n, P<int64_t>(total), S(s));
-  });
+  m.def("exclusive_scan_small", [](u a, int n, u total, u s, u host_total) {
+    fdx::launch_exclusive_scan_small(P<int64_t>(a), n, P<int64_t>(total), S(s), P<int64_t>(host_total));
+  }, py::arg("a"), py::arg("n"), py::arg("total"), py::arg("s"), py::arg("host_total") = 0);
   m.def("compact_write", [](u labels, int64_t n, int target, u offsets, u out_idx, int nblocks, u s) {
     fdx::launch_compact_write(P<const uint8_t>(labels), n, target, P<const int64_t>(offsets), P<int64_t>(out_idx),
                               nblocks, S(s));

@@ -60,7 +60,8 @@ void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* 
                        hipStream_t stream);
 void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t* counts,
                           int nblocks, hipStream_t stream);
-void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream);
+void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream,
+                                 int64_t* host_total = nullptr);
 void launch_compact_write(const uint8_t* labels, int64_t n, int target, const int64_t* offsets,
                           int64_t* out_idx, int nblocks, hipStream_t stream);
 // K3 stratified split/fold codes (split.hip): 255 = test, 0..k-1 = fold; offsets/total from

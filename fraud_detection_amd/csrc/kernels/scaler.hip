@@ -636,8 +636,11 @@ __global__ __launch_bounds__(kCompactThreads) void compact_write16_kernel(
 // In-place exclusive scan of a small int64 array (n <= 4096), one block of 1024 threads; writes
 // the total to tot.  Each thread owns 4 consecutive elements; lane totals are scanned with wave
 // shuffles, wave totals by wave 0 -- integer adds, so the result is exact and order-free.
+// host_tot (nullable): device address of a mapped pinned word that also receives the total
+// (system-scope store): the host polls it instead of waiting for a D2H copy and its event.
 __global__ __launch_bounds__(1024) void exclusive_scan_small_kernel(int64_t* __restrict__ a, int n,
-                                                                    int64_t* __restrict__ tot) {
+                                                                    int64_t* __restrict__ tot,
+                                                                    int64_t* __restrict__ host_tot) {
   __shared__ int64_t wsum[16];
   const int t = threadIdx.x, lane = lane_id(), w = wave_id();
   int64_t v[4];
@@ -668,7 +671,11 @@ __global__ __launch_bounds__(1024) void exclusive_scan_small_kernel(int64_t* __r
     if (4 * t + j < n) a[4 * t + j] = run;
     run += v[j];
   }
-  if (t == 0) *tot = wsum[15];
+  if (t == 0) {
+    *tot = wsum[15];
+    if (host_tot != nullptr)
+      __hip_atomic_store(host_tot, wsum[15], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 __global__ __launch_bounds__(kCompactThreads) void compact_write_kernel(
@@ -832,8 +839,8 @@ void launch_compact_count(const uint8_t* labels, int64_t n, int target, int64_t*
     compact_count_kernel<<<nblocks, kCompactThreads, 0, stream>>>(labels, n, target, counts);
   check_launch("compact_count");
 }
-void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream) {
-  exclusive_scan_small_kernel<<<1, 1024, 0, stream>>>(a, n, total);
+void launch_exclusive_scan_small(int64_t* a, int n, int64_t* total, hipStream_t stream, int64_t* host_total) {
+  exclusive_scan_small_kernel<<<1, 1024, 0, stream>>>(a, n, total, host_total);
   check_launch("exclusive_scan_small");
 }
 void launch_compact_write(const uint8_t* labels, int64_t n, int target, const int64_t* offsets,

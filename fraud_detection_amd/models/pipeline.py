@@ -127,7 +127,6 @@ class DevicePipeline:
         self.comm = comm
         self._ws = None
         self._buf = None   # the training buffer of the latest fit
-        self._side = None  # side stream for the class-count kernels (fused path)
         # deferred convergence checks: two training buffers / solver workspaces alternate; the fit
         # whose rows live in buffer b is verified before b is written again
         self._bufs, self._wss, self._pending = [None, None], [None, None], [None, None]
@@ -248,16 +247,15 @@ class DevicePipeline:
         rows_cap = self._train_buffer(cap, dev, allow_double=True)
         if fused:
             # ---- K1+K2 fused: statistics (C1 all-reduce inside) + shifted bf16 / fp8 rows ----
-            # ---- class counts (C2) on a side stream beside it; the host reads the total during K1+K2
-            # (profiles/r2_s6/count_side_stream_ab.txt: pass first + side-stream count 1.345 ms/fit;
-            # count kernels in front on the compute stream 1.366 -- that variant is deleted)
-            if self._side is None or self._side.device != dev:
-                self._side = torch.cuda.Stream(dev)
-                self._ready = torch.cuda.Event()  # re-recorded every fit (a wait binds the latest record)
-            ready = self._ready
-            ready.record()
+            # ---- class counts (C2) IN FRONT of the pass on the compute stream: the count/scan read
+            # only the labels (~10 us), their total lands in a mapped pinned word, and the host
+            # enqueues the whole minority -> k-NN -> SMOTE chain while the 265 us pass runs, so the
+            # chain starts with no host gap.  With the Newton fit's deferred convergence check the
+            # host is a fit ahead, so the count no longer sits behind a host wait at the fit
+            # boundary (profiles/r3_q/count_front_ab.txt: 1.273 vs 1.309 ms per step with the
+            # count on a side stream beside the pass, the round-2 winner).
+            pending = scaler_ops.compact_indices_async(y, 1)
             stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
-            pending = scaler_ops.compact_indices_async(y, 1, side=self._side, ready=ready)
             tm.mark("scaler_fit")
         else:
             # ---- K1: scaler statistics (C1 all-reduce inside) ----------------------------

@@ -1,6 +1,8 @@
 """K1 scaler statistics / K2 standardize+pad+cast / stable label compaction."""
 from __future__ import annotations
 
+import time
+
 from dataclasses import dataclass
 
 import numpy as np
@@ -301,16 +303,38 @@ def scale_cast(X: torch.Tensor, stats: ScalerStats, labels: torch.Tensor | None 
 
 
 class PendingCompaction:
-    """Count/scan kernels enqueued, the total on its way to pinned host memory.  ``result()``
-    waits only for those kernels (work enqueued after them keeps the GPU busy meanwhile), then
-    enqueues the write of the stable index list."""
+    """Count/scan kernels enqueued; the scan also stores the total into a mapped pinned word.
+    ``result()`` spins on that word (it lands a few microseconds after the scan, with no D2H
+    copy kernel and no event wake-up on the path), then enqueues the write of the stable index
+    list.  Work enqueued after the scan keeps the GPU busy meanwhile."""
 
     _pool: list = []  # rotating pinned slots (pinned allocation costs tens of microseconds)
+    _views: list = []  # numpy views of the slots (host reads/writes without torch dispatch)
+    _dev: list = []  # device addresses of the slots (0: not mapped -> D2H copy + event)
     _owners: list = []  # the pending compaction whose count each slot still holds
     _next = 0
     _POOL = 8
+    SPIN_S = 0.05  # then fall back to the event (a stalled or faulted stream surfaces as its error)
 
-    def __init__(self, labels, target, nb, counts, total, side: bool = False, home=None):
+    @classmethod
+    def take_slot(cls):
+        """A free pinned slot, reset to -1 (the scan writes a count >= 0).  A ninth compaction in
+        flight settles the slot's previous owner first."""
+        if not cls._pool:
+            cls._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(cls._POOL)]
+            cls._views = [t.numpy() for t in cls._pool]
+            cls._dev = [int(native().host_device_pointer(t.data_ptr())) for t in cls._pool]
+            cls._owners = [None] * cls._POOL
+        slot = cls._next % cls._POOL
+        cls._next += 1
+        prev = cls._owners[slot]
+        if prev is not None:
+            prev.result()
+        cls._owners[slot] = None
+        cls._views[slot][0] = -1
+        return slot, cls._dev[slot]
+
+    def __init__(self, labels, target, nb, counts, total, slot: int, side: bool = False, home=None):
         cls = PendingCompaction
         self.labels, self.target, self.nb, self.counts = labels, target, nb, counts
         # the stream the index list belongs to (its consumers run there): result() enqueues the
@@ -321,29 +345,35 @@ class PendingCompaction:
         # result() has waited for that stream, or the caching allocator hands its block to a
         # compute-stream tensor while the scan may still write it
         self.side, self.total = side, total
-        if not cls._pool:
-            cls._pool = [torch.empty(1, dtype=torch.int64, pin_memory=True) for _ in range(cls._POOL)]
-            cls._owners = [None] * cls._POOL
-        slot = cls._next % cls._POOL
-        cls._next += 1
-        prev = cls._owners[slot]
-        if prev is not None:  # a ninth compaction in flight: settle the slot's previous owner first
-            prev.result()
         cls._owners[slot] = self
         self._slot = slot
         self.host = cls._pool[slot]
-        self.host.copy_(total, non_blocking=True)
+        if not cls._dev[slot]:
+            self.host.copy_(total, non_blocking=True)
         self.event = torch.cuda.Event()
         self.event.record()
         self._out = None
 
+    def _count(self) -> int:
+        v = PendingCompaction._views[self._slot]
+        if PendingCompaction._dev[self._slot]:
+            t0 = time.perf_counter()
+            while v[0] < 0:
+                if time.perf_counter() - t0 > self.SPIN_S:
+                    self.event.synchronize()
+                    if v[0] < 0:
+                        raise RuntimeError("compaction: count not written after its stream drained")
+                    break
+        else:
+            self.event.synchronize()
+        return int(v[0])
+
     def result(self) -> torch.Tensor:
         if self._out is None:
-            self.event.synchronize()
+            cnt = self._count()
             with torch.cuda.stream(self.home):
                 if self.side:  # counts were written on the side stream
                     self.home.wait_event(self.event)
-                cnt = int(self.host[0])
                 if PendingCompaction._owners[self._slot] is self:
                     PendingCompaction._owners[self._slot] = None
                 self.total = None
@@ -384,9 +414,10 @@ def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 
         counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
         total = torch.empty(1, device=labels.device, dtype=torch.int64)
         s = stream_of(labels)
+        slot, hdev = PendingCompaction.take_slot()
         m.compact_count(ptr(labels), n, target, ptr(counts), nb, s)
-        m.exclusive_scan_small(ptr(counts), nb, ptr(total), s)
-        return PendingCompaction(labels, target, nb, counts, total)
+        m.exclusive_scan_small(ptr(counts), nb, ptr(total), s, hdev)
+        return PendingCompaction(labels, target, nb, counts, total, slot)
     compute = torch.cuda.current_stream(labels.device)
     if ready is not None:
         side.wait_event(ready)
@@ -396,9 +427,10 @@ def compact_indices_async(labels: torch.Tensor, target: int = 1, nblocks: int = 
         # pass's partial sums), which is safe only for compute-stream reuse
         counts = torch.empty(nb, device=labels.device, dtype=torch.int64)
         total = torch.empty(1, device=labels.device, dtype=torch.int64)
+        slot, hdev = PendingCompaction.take_slot()
         m.compact_count(ptr(labels), n, target, ptr(counts), nb, side.cuda_stream)
-        m.exclusive_scan_small(ptr(counts), nb, ptr(total), side.cuda_stream)
-        pend = PendingCompaction(labels, target, nb, counts, total, side=True, home=compute)
+        m.exclusive_scan_small(ptr(counts), nb, ptr(total), side.cuda_stream, hdev)
+        pend = PendingCompaction(labels, target, nb, counts, total, slot, side=True, home=compute)
     counts.record_stream(compute)  # result() launches the index write on the compute stream
     return pend
 
