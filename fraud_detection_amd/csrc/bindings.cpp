@@ -274,6 +274,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("scaler_partial", [](u X, int64_t n, int ld, int d, u pivot, u partial, int nblocks, u s) {
     fdx::launch_scaler_partial(P<const float>(X), n, ld, d, P<const float>(pivot), P<double>(partial), nblocks, S(s));
   });
+  m.def("scaler_reduce_scratch_rows", &fdx::scaler_reduce_scratch_rows);
   m.def("scaler_reduce", [](u partial, int nblocks, u sums, u s) {
     fdx::launch_scaler_reduce(P<const double>(partial), nblocks, P<double>(sums), S(s));
   });

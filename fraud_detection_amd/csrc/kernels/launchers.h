@@ -39,6 +39,7 @@ inline void check_launch(const char* what) {
 // ---- scaler.hip ----
 void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float* pivot,
                            double* partial, int nblocks, hipStream_t stream);
+int scaler_reduce_scratch_rows(int nblocks);  // extra [64] rows launch_scaler_reduce needs after the partials
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream);
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,

@@ -284,43 +284,32 @@ __global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
   }
 }
 
-// Fixed-order reduction of [nblocks][64] fp64 partials into sums[64].
-// 16 waves, each summing a strided subset of block partials with 32 independent accumulators:
-// the partials come from a whole-device pass (dirty in other XCDs' L2s), so every load round is
-// a long latency -- 32 loads in flight per lane make ~4 rounds for 2048 blocks instead of 16
-// with 8 (15.7 us).  The summation tree is fixed by (nblocks, thread) only, so results are
-// run-to-run deterministic.
+// Fixed-order fp64 reduction of [nblocks][64] block partials.  Block g folds partials
+// [g * kRedSpan, (g + 1) * kRedSpan) into out[g][64]: 64 columns x 16 row-groups, every thread's
+// <= 8 loads in flight at once.  The partials come from a whole-device pass (dirty in other XCDs'
+// L2s), so a load round is a long latency: a single 1024-thread block over 2048 partials needed
+// 4 rounds of 32 loads (15.7-19 us in the step timeline); two launches of one round each
+// (2048 -> 16 -> 1) replace it.  The tree is fixed by nblocks only: run-to-run deterministic.
+constexpr int kRedSpan = 128;
 __global__ __launch_bounds__(1024) void scaler_reduce_kernel(const double* __restrict__ partial,
-                                                             int nblocks, double* __restrict__ sums) {
-  constexpr int U = 32;
+                                                             int nblocks, double* __restrict__ out) {
   __shared__ double red[16][64];
   const int e = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  double acc[U];
+  const int b0 = blockIdx.x * kRedSpan, b1 = min(nblocks, b0 + kRedSpan);
+  double v[kRedSpan / 16];
 #pragma unroll
-  for (int u = 0; u < U; ++u) acc[u] = 0.0;
-  int b = grp;
-  for (; b + (U - 1) * 16 < nblocks; b += U * 16) {
-    double v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) v[u] = partial[(int64_t)(b + u * 16) * 64 + e];
-#pragma unroll
-    for (int u = 0; u < U; ++u) acc[u] += v[u];
+  for (int u = 0; u < kRedSpan / 16; ++u) {
+    const int b = b0 + grp + 16 * u;
+    v[u] = b < b1 ? partial[(int64_t)b * 64 + e] : 0.0;
   }
-#pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (b + u * 16 < nblocks) acc[u] += partial[(int64_t)(b + u * 16) * 64 + e];
-#pragma unroll
-  for (int w = U / 2; w >= 1; w >>= 1) {
-#pragma unroll
-    for (int u = 0; u < w; ++u) acc[u] += acc[u + w];
-  }
-  red[grp][e] = acc[0];
+  double acc = ((v[0] + v[1]) + (v[2] + v[3])) + ((v[4] + v[5]) + (v[6] + v[7]));
+  red[grp][e] = acc;
   __syncthreads();
   if (threadIdx.x < 64) {
     double s = 0.0;
 #pragma unroll
     for (int g = 0; g < 16; ++g) s += red[g][e];
-    sums[e] = s;
+    out[(int64_t)blockIdx.x * 64 + e] = s;
   }
 }
 
@@ -742,8 +731,22 @@ void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float
   check_launch("scaler_partial");
 }
 
+int scaler_reduce_scratch_rows(int nblocks) {
+  return nblocks > kRedSpan ? (nblocks + kRedSpan - 1) / kRedSpan : 0;
+}
+
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream) {
-  scaler_reduce_kernel<<<1, 1024, 0, stream>>>(partial, nblocks, sums);
+  // nblocks > kRedSpan: `partial` holds scaler_reduce_scratch_rows(nblocks) more [64] rows after
+  // the block partials for the first level's outputs
+  if (nblocks > kRedSpan * kRedSpan) throw std::runtime_error("scaler_reduce: too many block partials");
+  if (nblocks > kRedSpan) {
+    const int g = scaler_reduce_scratch_rows(nblocks);
+    double* mid = const_cast<double*>(partial) + (int64_t)nblocks * 64;
+    scaler_reduce_kernel<<<g, 1024, 0, stream>>>(partial, nblocks, mid);
+    scaler_reduce_kernel<<<1, 1024, 0, stream>>>(mid, g, sums);
+  } else {
+    scaler_reduce_kernel<<<1, 1024, 0, stream>>>(partial, nblocks, sums);
+  }
   check_launch("scaler_reduce");
 }
 

@@ -85,7 +85,7 @@ def scaler_partial_sums(X: torch.Tensor, pivot: torch.Tensor) -> torch.Tensor:
     m = native()
     piv = _pivot_dev(pivot, d, X.device)
     nb = min(_SCALER_BLOCKS, max(1, (n + 255) // 256))
-    partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
+    partial = torch.empty((nb + m.scaler_reduce_scratch_rows(nb)) * 64, device=X.device, dtype=torch.float64)
     sums = torch.empty(64, device=X.device, dtype=torch.float64)
     s = stream_of(X)
     m.scaler_partial(ptr(X), n, X.stride(0), d, ptr(piv), ptr(partial), nb, s)
@@ -252,7 +252,7 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         piv = _pivot_dev(pivot, d, X.device)
         # all blocks resident at once (occupancy-derived), never more than the tiles
         nb = max(1, min(_stats_cast_grid(m, X.device), (n + 127) // 128))
-        partial = torch.empty(nb * 64, device=X.device, dtype=torch.float64)
+        partial = torch.empty((nb + m.scaler_reduce_scratch_rows(nb)) * 64, device=X.device, dtype=torch.float64)
         sums = torch.empty(64, device=X.device, dtype=torch.float64)
         s = stream_of(X)
         if n > 0:
