@@ -7,9 +7,11 @@
 // Design (MI355X-first, not a port of xgboost's CPU/CUDA updaters):
 //  * Features are quantised once to u8 bins (<= 256 quantile cuts per feature; row = 32 bytes),
 //    so the per-level data stream is 32 B/row instead of 120 B of fp32.
-//  * Gradients/Hessians are quantised per boosting round to int32 fixed point (power-of-two
-//    scale) and histograms accumulate in int64: LDS atomics (ds_add_u64) then one global
-//    atomic flush per (block, node).  Integer addition is associative, so histograms -- and
+//  * Gradients/Hessians are quantised per boosting round to fixed point (power-of-two scale,
+//    |g|, h <= 2^14) and histograms accumulate exactly: ONE packed 64-bit LDS atomic per
+//    (row, feature) carries h in the high word and g (signed) in the low word -- exact while a
+//    block's partial sums stay below 2^31, i.e. for <= 2^16 rows between flushes -- then one
+//    global int64 atomic flush per (block, node, g|h).  Integer addition is associative, so histograms -- and
 //    therefore every split decision -- are bitwise deterministic regardless of scheduling, the
 //    sibling histogram is an exact parent - child subtraction, and the data-parallel
 //    all-reduce of histograms over RCCL is exact too.
@@ -107,21 +109,22 @@ __global__ __launch_bounds__(256) void gbdt_grad_kernel(const float* __restrict_
 }
 
 // ---- histograms ------------------------------------------------------------------------------
-// Grid: resident blocks (1 per CU: 120 KiB of LDS).  The rows of this level's *built* nodes
+// Grid: resident blocks (2 per CU: 60 KiB of LDS each).  The rows of this level's *built* nodes
 // are concatenated in node order into a virtual range that the grid splits evenly, so the work
 // per block is balanced whatever the segment sizes are.
 //
-// LDS layout: a g plane [feature][bin] then an h plane, not the global [feature][bin][g, h]
-// interleave.  An int64 LDS atomic's bank pair is (u64 index mod 32); interleaved, every g
-// (h) atomic of a wave lands on the 16 even (odd) pairs, so the 64 random bins of a wave
-// collide twice as often.  Split planes give each atomic all 32 pairs.
-constexpr int kHistPlane = kGBMaxFeat * kGBBins;
-__device__ __forceinline__ int lds_hist_slot(int i) { return (i & 1) * kHistPlane + (i >> 1); }
+// LDS: one packed u64 per [feature][bin]: (h << 32) + g with g sign-extended.  Integer addition
+// of packed words is the pair of additions as long as the low word's true sum stays inside
+// int32 (|sum g| < 2^31, sum h < 2^31): at |g|, h <= 2^14 per row that holds for any 2^16 rows,
+// so a block flushes every kFlushRows rows.  Half the LDS atomics and half the LDS of separate
+// g / h planes (the round-2 kernel was LDS-atomic bound: profiles/README.md, r2_s4a).
+constexpr int kHistWords = kGBMaxFeat * kGBBins;  // 7680 u64 = 60 KiB
+constexpr int64_t kFlushRows = 1 << 16;
 __global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
     const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
     unsigned long long* __restrict__ hist) {
-  __shared__ unsigned long long sh[kHistEntries];  // 120 KiB
+  __shared__ unsigned long long sh[kHistWords];
   const int h0 = heap_first(level), nn = 1 << level;
   int64_t total = 0;
   for (int k = 0; k < nn; ++k)
@@ -130,7 +133,7 @@ __global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
   const int64_t vb = (int64_t)blockIdx.x * chunk;
   const int64_t ve = min(vb + chunk, total);
   if (vb >= ve) return;
-  const int nent = d * kGBBins * 2;
+  const int nw = d * kGBBins;
   int64_t off = 0;
   for (int k = 0; k < nn; ++k) {
     const int node = h0 + k;
@@ -138,35 +141,39 @@ __global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
     const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
     const int64_t lo = max(off, vb), hi = min(off + sc, ve);
     off += sc;
-    if (lo >= hi) continue;
-    for (int i = threadIdx.x; i < nent; i += kHistThreads) sh[lds_hist_slot(i)] = 0ull;
-    __syncthreads();
-    for (int64_t v = lo + threadIdx.x; v < hi; v += kHistThreads) {
-      const int64_t p = sb + (v - (off - sc));
-      const int64_t row = ridx[p];
-      const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
-      const uint4 b0 = br[0], b1 = br[1];
-      const int2 q = gh[row];
-      const unsigned long long qg = (unsigned long long)(long long)q.x;
-      const unsigned long long qh = (unsigned long long)(long long)q.y;
-      const uint32_t words[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    for (int64_t c0 = lo; c0 < hi; c0 += kFlushRows) {
+      const int64_t c1 = min(hi, c0 + kFlushRows);
+      for (int i = threadIdx.x; i < nw; i += kHistThreads) sh[i] = 0ull;
+      __syncthreads();
+      for (int64_t v = c0 + threadIdx.x; v < c1; v += kHistThreads) {
+        const int64_t p = sb + (v - (off - sc));
+        const int64_t row = ridx[p];
+        const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
+        const uint4 b0 = br[0], b1 = br[1];
+        const int2 q = gh[row];
+        const unsigned long long pk = ((unsigned long long)(uint32_t)q.y << 32) + (unsigned long long)(long long)q.x;
+        const uint32_t words[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int f = 0; f < kGBMaxFeat; ++f) {
-        if (f < d) {
-          const int b = (words[f >> 2] >> (8 * (f & 3))) & 0xff;
-          unsigned long long* e = sh + f * kGBBins + b;
-          atomicAdd(e, qg);
-          atomicAdd(e + kHistPlane, qh);
+        for (int f = 0; f < kGBMaxFeat; ++f) {
+          if (f < d) {
+            const int b = (words[f >> 2] >> (8 * (f & 3))) & 0xff;
+            atomicAdd(sh + f * kGBBins + b, pk);
+          }
         }
       }
+      __syncthreads();
+      unsigned long long* dst = hist + (int64_t)node * kHistEntries;
+      for (int i = threadIdx.x; i < nw; i += kHistThreads) {
+        const unsigned long long x = sh[i];
+        if (x) {
+          const long long sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
+          const long long shh = (long long)(x - (unsigned long long)sg) >> 32;
+          if (sg) atomicAdd(dst + 2 * i, (unsigned long long)sg);
+          if (shh) atomicAdd(dst + 2 * i + 1, (unsigned long long)shh);
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
-    unsigned long long* dst = hist + (int64_t)node * kHistEntries;
-    for (int i = threadIdx.x; i < nent; i += kHistThreads) {
-      const unsigned long long x = sh[lds_hist_slot(i)];
-      if (x) atomicAdd(dst + i, x);
-    }
-    __syncthreads();
   }
 }
 
@@ -631,7 +638,7 @@ int gbdt_hist_blocks() {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
   }
-  cached = cus;  // 120 KiB of LDS per block: one resident block per CU
+  cached = 2 * cus;  // 60 KiB of LDS per block: two resident blocks per CU
   return cached;
 }
 

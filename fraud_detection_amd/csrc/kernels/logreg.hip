@@ -36,36 +36,24 @@ constexpr int kPassBlocks = 1024;  // 4 per CU x 4 waves: 16 waves/CU of streami
 
 typedef short lds_s4 __attribute__((ext_vector_type(4)));
 
-template <int FMT>
 __device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
   x[0] = bf16lo(v.x); x[1] = bf16hi(v.x); x[2] = bf16lo(v.y); x[3] = bf16hi(v.y);
   x[4] = bf16lo(v.z); x[5] = bf16hi(v.z); x[6] = bf16lo(v.w); x[7] = bf16hi(v.w);
 }
-// fp8 rows hold features * x_scale: decoded values stay in that scale -- 1/x_scale is folded into
-// the weights (z), the gradient (once, at the end) and the Hessian (once, at the end) instead of
-// one multiply per decoded value.
-__device__ __forceinline__ void unpack8_fp8(const uint2& v, float x[8]) {
-  fp8x4_to_f32(v.x, x);  // hardware OCP e4m3 decode, 2 values per instruction
-  fp8x4_to_f32(v.y, x + 4);
-}
 
-template <bool HESS, int FMT>  // FMT: 0 bf16 rows (64 B), 1 fp8 rows (32 B)
+template <bool HESS>  // bf16 rows (64 B); fp8 rows: logreg_pass_fp8w_kernel
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
-    const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, int row_sub, float* __restrict__ partial) {
+    const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
+    float* __restrict__ partial) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][35];
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 3, rr = lane >> 2;
-  const float inv_s = 1.0f / x_scale;
-  float wl[8], cs[8];  // cs: per-column decode scale (fp8 feature columns: 1/x_scale)
+  float wl[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    cs[j] = (FMT == 1 && q * 8 + j < d_feat) ? inv_s : 1.0f;
-    wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j] * cs[j];
-  }
+  for (int j = 0; j < 8; ++j) wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j];
   const float cw0 = class_w[0], cw1 = class_w[1];
   float g[8];
 #pragma unroll
@@ -83,43 +71,30 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
   // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
-  typedef typename std::conditional<FMT == 0, uint4, uint2>::type vec_t;
-  auto load_tile = [&](int64_t b, vec_t (&v)[4]) {
-    const vec_t* X = reinterpret_cast<const vec_t*>(Xv);
+  auto load_tile = [&](int64_t b, uint4 (&v)[4]) {
+    const uint4* X = reinterpret_cast<const uint4*>(Xv);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = b + 16 * u + rr;
-      if (row < n) v[u] = X[(row_begin + row) * 4 + q];
-      else if constexpr (FMT == 0) v[u] = make_uint4(0, 0, 0, 0);
-      else v[u] = make_uint2(0, 0);
+      v[u] = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
     }
   };
   int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
-  // fp8 rows are 8 bytes per lane per row: half the bytes per load instruction of bf16, so the
-  // fp8 stream keeps TWO tiles in flight ahead of the one being computed (the same bytes in
-  // flight per wave as bf16's one-tile register double buffer)
-  constexpr bool kPF2 = FMT == 1;
-  vec_t cur[4], nx1[4];
+  uint4 cur[4];
   if (base < n) load_tile(base, cur);
-  if (kPF2 && base + step < n) load_tile(base + step, nx1);
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
   // is unchanged; H only shapes the step (sub-sampled Newton).
   int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
   for (; base < n; base += step) {
-    vec_t nxt[4];
-    if constexpr (kPF2) {
-      if (base + 2 * step < n) load_tile(base + 2 * step, nxt);
-    } else {
-      if (base + step < n) load_tile(base + step, nxt);
-    }
+    uint4 nxt[4];
+    if (base + step < n) load_tile(base + step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      if constexpr (FMT == 0) unpack8<0>(cur[u], xs[u]);
-      else unpack8_fp8(cur[u], xs[u]);
+      unpack8(cur[u], xs[u]);
     }
     float zq = 0.0f, yq = 0.0f, swq = 0.0f;  // the row (u == q) whose loss this lane accounts for
 #pragma unroll
@@ -176,19 +151,12 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     wacc += swq;
     if (do_h) whacc += swq;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if constexpr (kPF2) {
-        cur[u] = nx1[u];
-        nx1[u] = nxt[u];
-      } else {
-        cur[u] = nxt[u];
-      }
-    }
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
   }
 
   // ---- block reduction (fixed order) ----
 #pragma unroll
-  for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]) * cs[j];
+  for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
   lacc = wave_sum(lacc);
   wacc = wave_sum(wacc);
   whacc = wave_sum(whacc);
@@ -206,17 +174,188 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     // each wave overwrites only its own tile region (same bytes it read from)
     const float hscale = (float)hess_stride;
     const int hcol = lane & 31;
-    const float ccol = (FMT == 1 && hcol < d_feat) ? hscale * inv_s : hscale;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
       const int row = (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
-      const float crow = (FMT == 1 && row < d_feat) ? inv_s : 1.0f;
-      hb[wv * 1024 + row * kCols + hcol] = acc[k] * (ccol * crow);
+      hb[wv * 1024 + row * kCols + hcol] = acc[k] * hscale;
     }
   }
   __syncthreads();
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
   if (threadIdx.x < (HESS ? 35 : 34)) {  // slot 34 (Hessian weight) only from Hessian passes
+    const int t = threadIdx.x;
+    out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+  }
+  if constexpr (HESS) {
+    for (int e = threadIdx.x; e < 1024; e += kThreads)
+      out[64 + e] = ((hb[e] + hb[1024 + e]) + hb[2048 + e]) + hb[3072 + e];
+  }
+}
+
+// fp8 rows, TWO lanes per row: each lane loads 16 columns (one 16 B load), 32 rows per wave
+// load instruction, and the per-row work that every lane of a row repeats (the dot-product
+// butterfly, sigmoid, loss bookkeeping) is shared by 2 lanes instead of 4.  The dot product and
+// the gradient run on packed fp32 (v_pk_fma_f32, 2 columns per instruction).  The Hessian tile
+// and its MFMA are those of the bf16 kernel.  Measured against the previous 4-lane fp8 kernel
+// (profiles/r3_s): gradient pass 125 -> 99 us, sub-sampled Hessian pass 137 -> 112 us over
+// 16M rows (5.2 TB/s), fp8 bench step 1.164 -> 1.099 ms.
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+template <bool HESS>
+__global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
+    const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
+    const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
+    int hess_stride, int row_sub, float* __restrict__ partial) {
+  if (done != nullptr && *done) return;
+  __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
+  __shared__ float red[kWaves][35];
+  const int lane = lane_id(), wv = wave_id();
+  const int q = lane & 1, rr = lane >> 1;
+  const float inv_s = 1.0f / x_scale;
+  f32x2_t wl[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = 16 * q + 2 * p + e;
+      const float cs = col < d_feat ? inv_s : 1.0f;
+      wl[p][e] = (col == kLabelCol) ? 0.0f : w[col] * cs;
+    }
+  }
+  const float cw0 = class_w[0], cw1 = class_w[1];
+  f32x2_t g[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) g[p] = f32x2_t{0.0f, 0.0f};
+  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f;
+  f32x16_t acc = {};
+  const int grp = lane >> 4, gi = lane & 15;
+  const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
+  uint16_t* my_tile = tile[wv];
+  const int64_t n = row_end - row_begin;
+  const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
+  const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
+  const uint4* X = reinterpret_cast<const uint4*>(X8);
+  auto load_tile = [&](int64_t b, uint4 (&v)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int64_t row = b + 32 * u + rr;
+      v[u] = row < n ? X[(row_begin + row) * 2 + q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
+  // two tiles in flight ahead of the one being computed (4 KiB per wave, as the bf16 stream)
+  uint4 cur[2], nx1[2];
+  if (base < n) load_tile(base, cur);
+  if (base + step < n) load_tile(base + step, nx1);
+  int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
+  for (; base < n; base += step) {
+    uint4 nxt[2];
+    if (base + 2 * step < n) load_tile(base + 2 * step, nxt);
+    const bool do_h = HESS && hphase == 0;
+    hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
+    float zq = 0.0f, yq = 0.0f, swq = 0.0f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      float x[16];
+      fp8x4_to_f32(cur[u].x, x);
+      fp8x4_to_f32(cur[u].y, x + 4);
+      fp8x4_to_f32(cur[u].z, x + 8);
+      fp8x4_to_f32(cur[u].w, x + 12);
+      float y = (q == 1) ? x[15] : 0.0f;
+      if (q == 1) x[15] = 0.0f;
+      f32x2_t zz = f32x2_t{0.0f, 0.0f};
+#pragma unroll
+      for (int p = 0; p < 8; ++p) zz = __builtin_elementwise_fma(wl[p], f32x2_t{x[2 * p], x[2 * p + 1]}, zz);
+      float zp = group_sum<2>(zz[0] + zz[1]);
+      y = group_sum<2>(y);
+      const bool ok = base + 32 * u + rr < n;
+      const bool pos = y > 0.5f;
+      const float sw = ok ? (pos ? cw1 : cw0) : 0.0f;
+      const float zc = fminf(fmaxf(zp, -80.0f), 80.0f);
+      const float eh = __expf(-0.5f * zc);
+      const float pr = fast_rcp(fmaf(eh, eh, 1.0f));
+      const float r = sw * (pr - y);
+      const f32x2_t r2 = f32x2_t{r, r};
+#pragma unroll
+      for (int p = 0; p < 8; ++p) g[p] = __builtin_elementwise_fma(r2, f32x2_t{x[2 * p], x[2 * p + 1]}, g[p]);
+      if (q == u) { zq = zp; yq = y; swq = sw; }
+      if (do_h) {
+        const float dd = ok ? (pos ? scw1 : scw0) * pr * eh : 0.0f;
+        uint4 p0, p1;
+        p0.x = pack_bf16x2(x[0] * dd, x[1] * dd);
+        p0.y = pack_bf16x2(x[2] * dd, x[3] * dd);
+        p0.z = pack_bf16x2(x[4] * dd, x[5] * dd);
+        p0.w = pack_bf16x2(x[6] * dd, x[7] * dd);
+        p1.x = pack_bf16x2(x[8] * dd, x[9] * dd);
+        p1.y = pack_bf16x2(x[10] * dd, x[11] * dd);
+        p1.z = pack_bf16x2(x[12] * dd, x[13] * dd);
+        p1.w = pack_bf16x2(x[14] * dd, x[15] * dd);
+        uint4* dst = reinterpret_cast<uint4*>(my_tile + (32 * u + rr) * kCols + 16 * q);
+        dst[0] = p0;
+        dst[1] = p1;
+      }
+    }
+    if (do_h) {
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const lds_s4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off));
+        const lds_s4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off + 4 * kCols));
+        bf16x8_t f;
+        f[0] = a0[0]; f[1] = a0[1]; f[2] = a0[2]; f[3] = a0[3];
+        f[4] = a1[0]; f[5] = a1[1]; f[6] = a1[2]; f[7] = a1[3];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, f, acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
+    wacc += swq;
+    if (do_h) whacc += swq;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      cur[u] = nx1[u];
+      nx1[u] = nxt[u];
+    }
+  }
+
+  // ---- block reduction (fixed order) ----
+  float gs[16];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = 16 * q + 2 * p + e;
+      gs[2 * p + e] = strided_sum<2>(g[p][e]) * (col < d_feat ? inv_s : 1.0f);
+    }
+  }
+  lacc = wave_sum(lacc);
+  wacc = wave_sum(wacc);
+  whacc = wave_sum(whacc);
+  if (lane < 2) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) red[wv][16 * lane + j] = gs[j];
+  }
+  if (lane == 0) {
+    red[wv][32] = lacc;
+    red[wv][33] = wacc;
+    red[wv][34] = HESS ? whacc * (float)hess_stride : 0.0f;
+  }
+  float* hb = reinterpret_cast<float*>(&tile[0][0]);
+  if constexpr (HESS) {
+    const float hscale = (float)hess_stride;
+    const int hcol = lane & 31;
+    const float ccol = hcol < d_feat ? hscale * inv_s : hscale;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const int row = (k & 3) + 8 * (k >> 2) + 4 * (lane >> 5);
+      const float crow = row < d_feat ? inv_s : 1.0f;
+      hb[wv * 1024 + row * kCols + hcol] = acc[k] * (ccol * crow);
+    }
+  }
+  __syncthreads();
+  float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
+  if (threadIdx.x < (HESS ? 35 : 34)) {
     const int t = threadIdx.x;
     out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
   }
@@ -639,8 +778,8 @@ int logreg_pass_blocks(int fmt) {
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
     int occ = 0;
-    hipError_t e = fmt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true, 1>, kThreads, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true, 0>, kThreads, 0);
+    hipError_t e = fmt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_fp8w_kernel<true>, kThreads, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true>, kThreads, 0);
     if (e == hipSuccess && occ > 0) per_cu = occ;
   }
   int c = cus * per_cu;
@@ -657,11 +796,11 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
   // row_sub >= 1: visit a uniform 1/row_sub of the 64-row tiles (progressive Newton).
   if (row_sub < 1) row_sub = 1;
   if (hessian > 0)
-    logreg_pass_kernel<true, 0><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, 1.0f, 32, hessian, row_sub, partial);
+    logreg_pass_kernel<true><<<nblocks, kThreads, 0, stream>>>(
+        X, row_begin, row_end, w, class_w, done, hessian, row_sub, partial);
   else
-    logreg_pass_kernel<false, 0><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, 1.0f, 32, 1, row_sub, partial);
+    logreg_pass_kernel<false><<<nblocks, kThreads, 0, stream>>>(
+        X, row_begin, row_end, w, class_w, done, 1, row_sub, partial);
   check_launch("logreg_pass");
 }
 
@@ -672,10 +811,10 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
   // are stored unscaled.
   if (row_sub < 1) row_sub = 1;
   if (hessian > 0)
-    logreg_pass_kernel<true, 1><<<nblocks, kThreads, 0, stream>>>(
+    logreg_pass_fp8w_kernel<true><<<nblocks, kThreads, 0, stream>>>(
         X, row_begin, row_end, w, class_w, done, x_scale, 30, hessian, row_sub, partial);
   else
-    logreg_pass_kernel<false, 1><<<nblocks, kThreads, 0, stream>>>(
+    logreg_pass_fp8w_kernel<false><<<nblocks, kThreads, 0, stream>>>(
         X, row_begin, row_end, w, class_w, done, x_scale, 30, 1, row_sub, partial);
   check_launch("logreg_pass_fp8");
 }

@@ -64,9 +64,14 @@ def bin_rows(X: np.ndarray, cuts: np.ndarray, nbins: np.ndarray) -> np.ndarray:
     return out
 
 
+GRAD_BITS = 14  # |g_q|, h_q <= 2^14: the device packs (h, g) of a row into one 64-bit LDS atomic
+
+
 def grad_scales(scale_pos_weight: float):
+    """Power-of-two fixed-point scales with |g * gscale| <= 2^14 and h * hscale <= 2^14
+    (h = p (1 - p) w <= w / 4): 2^16 rows of packed (h << 32) + g sum exactly in 64 bits."""
     wmax = max(float(scale_pos_weight), 1.0)
-    gscale = float(2.0 ** np.floor(np.log2((2.0 ** 30) / wmax)))
+    gscale = float(2.0 ** np.floor(np.log2((2.0 ** GRAD_BITS) / wmax)))
     return gscale, 4.0 * gscale
 
 
