@@ -470,9 +470,10 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_gbdt_grad(P<const float>(margin), P<const uint8_t>(label), n, spw, gscale, hscale, P<int2>(gh), S(s));
   });
   m.def("gbdt_hist_blocks", [] { return fdx::gbdt_hist_blocks(); });
-  m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u s) {
+  m.def("gbdt_hist_slot_words", [] { return fdx::gbdt_hist_slot_words(); });
+  m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u slots, u s) {
     fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const int2>(gh), P<const int>(ridx), P<const int64_t>(seg),
-                          P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), S(s));
+                          P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), P<long long>(slots), S(s));
   });
   m.def("gbdt_split", [](u hist, u gcnt, int level, int d, u nbins, u cuts, double ginv, double hinv, double lam,
                          double mcw, double gamma, u feat, u bin, u thr, u gain, u ng, u nh, u s) {

@@ -116,65 +116,156 @@ __global__ __launch_bounds__(256) void gbdt_grad_kernel(const float* __restrict_
 // LDS: one packed u64 per [feature][bin]: (h << 32) + g with g sign-extended.  Integer addition
 // of packed words is the pair of additions as long as the low word's true sum stays inside
 // int32 (|sum g| < 2^31, sum h < 2^31): at |g|, h <= 2^14 per row that holds for any 2^16 rows,
-// so a block flushes every kFlushRows rows.  Half the LDS atomics and half the LDS of separate
-// g / h planes (the round-2 kernel was LDS-atomic bound: profiles/README.md, r2_s4a).
+// so a block flushes every kFlushRows rows.
+//
+// Flush: NO global atomics from the histogram blocks.  Each (node, block) pair owns a slot of
+// int64 [feature][bin][g, h] that the block writes with plain coalesced stores; a reduce kernel
+// then sums each node's slots (16-way split of the slot axis, one int64 atomic per split).  With
+// 512 blocks all adding 15k int64 atomics to the SAME node words, the flush was a fixed ~140 us
+// per level whatever the row count (profiles/r3_v: 157 us at 2M rows, 322 us at 16M).
 constexpr int kHistWords = kGBMaxFeat * kGBBins;  // 7680 u64 = 60 KiB
 constexpr int64_t kFlushRows = 1 << 16;
-__global__ __launch_bounds__(kHistThreads) void gbdt_hist_kernel(
-    const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
-    const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
-    unsigned long long* __restrict__ hist) {
-  __shared__ unsigned long long sh[kHistWords];
+constexpr int kHistBatch = 4;
+constexpr int kSlotSplit = 16;
+
+// Node k's place in the level's virtual row range and its slot range: blocks [b0, b0 + cnt)
+// touch it, their slots are [base, base + cnt).  Same arithmetic in the histogram and the
+// reduce kernels.
+struct NodeSlots {
+  int64_t off, sc;
+  int b0, cnt, base;
+};
+__device__ __forceinline__ int64_t level_chunk(const int64_t* seg, const int64_t* gcnt, int level, int nblocks,
+                                               int64_t* total_out) {
   const int h0 = heap_first(level), nn = 1 << level;
   int64_t total = 0;
   for (int k = 0; k < nn; ++k)
     if (is_built(h0 + k, gcnt)) total += seg[2 * (h0 + k) + 1];
-  const int64_t chunk = (total + gridDim.x - 1) / gridDim.x;
+  *total_out = total;
+  return (total + nblocks - 1) / nblocks;
+}
+
+__global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
+    const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
+    const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
+    long long* __restrict__ slots) {
+  __shared__ unsigned long long sh[kHistWords];
+  const int h0 = heap_first(level), nn = 1 << level;
+  int64_t total;
+  const int64_t chunk = level_chunk(seg, gcnt, level, gridDim.x, &total);
   const int64_t vb = (int64_t)blockIdx.x * chunk;
   const int64_t ve = min(vb + chunk, total);
   if (vb >= ve) return;
   const int nw = d * kGBBins;
   int64_t off = 0;
+  int slot_base = 0;
   for (int k = 0; k < nn; ++k) {
     const int node = h0 + k;
     if (!is_built(node, gcnt)) continue;
     const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
     const int64_t lo = max(off, vb), hi = min(off + sc, ve);
+    const int b0 = sc > 0 ? (int)(off / chunk) : 0;
+    const int cnt = sc > 0 ? (int)((off + sc - 1) / chunk) - b0 + 1 : 0;
     off += sc;
+    const int my_slot = slot_base + ((int)blockIdx.x - b0);
+    slot_base += cnt;
+    if (lo >= hi) continue;
+    long long* dst = slots + (int64_t)my_slot * kHistEntries;
     for (int64_t c0 = lo; c0 < hi; c0 += kFlushRows) {
       const int64_t c1 = min(hi, c0 + kFlushRows);
       for (int i = threadIdx.x; i < nw; i += kHistThreads) sh[i] = 0ull;
       __syncthreads();
-      for (int64_t v = c0 + threadIdx.x; v < c1; v += kHistThreads) {
-        const int64_t p = sb + (v - (off - sc));
-        const int64_t row = ridx[p];
-        const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
-        const uint4 b0 = br[0], b1 = br[1];
-        const int2 q = gh[row];
-        const unsigned long long pk = ((unsigned long long)(uint32_t)q.y << 32) + (unsigned long long)(long long)q.x;
-        const uint32_t words[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      // kHistBatch rows per thread in flight: every row index, then every row's bins and (g, h),
+      // are loaded before the first atomic.  Level 0 reads rows in order (ridx is the identity
+      // after the round init).
+      const int64_t pbase = sb - (off - sc);
+      for (int64_t v0 = c0 + threadIdx.x; v0 < c1; v0 += kHistThreads * kHistBatch) {
+        int64_t rows[kHistBatch];
 #pragma unroll
-        for (int f = 0; f < kGBMaxFeat; ++f) {
-          if (f < d) {
-            const int b = (words[f >> 2] >> (8 * (f & 3))) & 0xff;
-            atomicAdd(sh + f * kGBBins + b, pk);
+        for (int u = 0; u < kHistBatch; ++u) {
+          const int64_t v = v0 + (int64_t)u * kHistThreads;
+          rows[u] = v < c1 ? (level == 0 ? pbase + v : (int64_t)ridx[pbase + v]) : -1;
+        }
+        uint32_t words[kHistBatch][8];
+        unsigned long long pk[kHistBatch];
+#pragma unroll
+        for (int u = 0; u < kHistBatch; ++u) {
+          const int64_t row = rows[u] < 0 ? 0 : rows[u];
+          const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
+          const uint4 b0v = br[0], b1v = br[1];
+          const int2 q = gh[row];
+          words[u][0] = b0v.x; words[u][1] = b0v.y; words[u][2] = b0v.z; words[u][3] = b0v.w;
+          words[u][4] = b1v.x; words[u][5] = b1v.y; words[u][6] = b1v.z; words[u][7] = b1v.w;
+          pk[u] = ((unsigned long long)(uint32_t)q.y << 32) + (unsigned long long)(long long)q.x;
+        }
+#pragma unroll
+        for (int u = 0; u < kHistBatch; ++u) {
+          if (rows[u] < 0) continue;
+#pragma unroll
+          for (int f = 0; f < kGBMaxFeat; ++f) {
+            if (f < d) {
+              const int b = (words[u][f >> 2] >> (8 * (f & 3))) & 0xff;
+              atomicAdd(sh + f * kGBBins + b, pk[u]);
+            }
           }
         }
       }
       __syncthreads();
-      unsigned long long* dst = hist + (int64_t)node * kHistEntries;
+      const bool first = c0 == lo;  // later flushes of the same slot accumulate (block-private)
       for (int i = threadIdx.x; i < nw; i += kHistThreads) {
         const unsigned long long x = sh[i];
-        if (x) {
-          const long long sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
-          const long long shh = (long long)(x - (unsigned long long)sg) >> 32;
-          if (sg) atomicAdd(dst + 2 * i, (unsigned long long)sg);
-          if (shh) atomicAdd(dst + 2 * i + 1, (unsigned long long)shh);
+        const long long sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
+        const long long shh = (long long)(x - (unsigned long long)sg) >> 32;
+        long long* e = dst + 2 * i;
+        if (first) {
+          e[0] = sg;
+          e[1] = shh;
+        } else {
+          e[0] += sg;
+          e[1] += shh;
         }
       }
       __syncthreads();
     }
   }
+}
+
+// Sum each built node's slots into its histogram: grid (entries / 256, kSlotSplit, 2^level).
+__global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const long long* __restrict__ slots,
+                                                               const int64_t* __restrict__ seg,
+                                                               const int64_t* __restrict__ gcnt, int level,
+                                                               int d, int hist_blocks,
+                                                               unsigned long long* __restrict__ hist) {
+  const int h0 = heap_first(level);
+  int64_t total;
+  const int64_t chunk = level_chunk(seg, gcnt, level, hist_blocks, &total);
+  if (total == 0) return;
+  const int kk = blockIdx.z;
+  int64_t off = 0;
+  int base = 0, cnt = 0;
+  bool mine = false;
+  for (int k = 0; k <= kk; ++k) {
+    const int node = h0 + k;
+    if (!is_built(node, gcnt)) continue;
+    const int64_t sc = seg[2 * node + 1];
+    const int c = sc > 0 ? (int)((off + sc - 1) / chunk) - (int)(off / chunk) + 1 : 0;
+    if (k == kk) {
+      mine = true;
+      cnt = c;
+    } else {
+      base += c;
+    }
+    off += sc;
+  }
+  // >= 8 slots per split: deep levels have many small nodes, whose few slots need no split (each
+  // split costs one int64 atomic per entry)
+  const int split = min(kSlotSplit, (cnt + 7) / 8);
+  if (!mine || cnt == 0 || (int)blockIdx.y >= split) return;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= d * kGBBins * 2) return;
+  long long acc = 0;
+  for (int j = blockIdx.y; j < cnt; j += split) acc += slots[(int64_t)(base + j) * kHistEntries + e];
+  if (acc) atomicAdd(hist + (int64_t)(h0 + kk) * kHistEntries + e, (unsigned long long)acc);
 }
 
 // ---- split search ----------------------------------------------------------------------------
@@ -642,12 +733,20 @@ int gbdt_hist_blocks() {
   return cached;
 }
 
+int64_t gbdt_hist_slot_words() { return (int64_t)(gbdt_hist_blocks() + 2 * kGBMaxNodes) * kHistEntries; }
+
 void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
-                      const int64_t* gcnt, int level, int d, unsigned long long* hist,
+                      const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
                       hipStream_t stream) {
-  gbdt_hist_kernel<<<gbdt_hist_blocks(), kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d,
-                                                                     hist);
+  // slots: gbdt_hist_slot_words() int64 (one [feature][bin][g, h] slot per (node, block) pair:
+  // at most blocks + nodes pairs)
+  if (level < 0 || (1 << level) > kGBMaxNodes + 1) throw std::runtime_error("gbdt_hist: level out of range");
+  const int nb = gbdt_hist_blocks();
+  gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots);
   check_launch("gbdt_hist");
+  const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, 1u << level);
+  gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, nb, hist);
+  check_launch("gbdt_hist_reduce");
 }
 
 void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,

@@ -208,8 +208,10 @@ void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts
 void launch_gbdt_grad(const float* margin, const uint8_t* label, int64_t n, float spw, float gscale,
                       float hscale, int2* gh, hipStream_t stream);
 int gbdt_hist_blocks();
+int64_t gbdt_hist_slot_words();  // int64 words of the per-(node, block) histogram slots
 void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
-                      const int64_t* gcnt, int level, int d, unsigned long long* hist, hipStream_t stream);
+                      const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
+                      hipStream_t stream);
 void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
                        const float* cuts, double ginv, double hinv, double lambda,
                        double min_child_weight, double gamma, int* feat, int* bin, float* thr,

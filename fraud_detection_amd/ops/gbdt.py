@@ -166,6 +166,8 @@ class _Workspace:
         self.segR = torch.zeros(nheap, dtype=torch.int64, device=dev)
         self.gcnt = torch.zeros(nheap, dtype=torch.int64, device=dev)
         self.hist = torch.zeros(((1 << depth) - 1) * HIST_ENTRIES, dtype=torch.int64, device=dev)
+        # per-(node, block) histogram slots the histogram kernel writes without atomics
+        self.slots = torch.empty(native().gbdt_hist_slot_words(), dtype=torch.int64, device=dev)
         self.ng = torch.zeros(nheap, dtype=torch.int64, device=dev)
         self.nh = torch.zeros(nheap, dtype=torch.int64, device=dev)
 
@@ -289,7 +291,7 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
             m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
-                        ptr(ws.hist), st)
+                        ptr(ws.hist), ptr(ws.slots), st)
             if dist:
                 comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,

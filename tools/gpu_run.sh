@@ -20,6 +20,7 @@
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   pmc          two PMC passes over a short bench
 #   pmcfp8       logreg pass counters + kernel stats with fp8 and with bf16 rows
+#   gbdt         tools/gbdt_bench.py at the bench shape; gbdtprof: its kernel trace (20 trees)
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
 #   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
@@ -84,6 +85,12 @@ for st in "$@"; do
         step "pmc_pass_$ST" 120 rocprofv3 --kernel-include-regex "logreg_pass" --pmc FETCH_SIZE SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD --output-format csv -d "$OUT/pmc_pass_$ST" -o run -- python3 "$R/bench.py" --storage $ST --steps 2 --warmup 1 --no-extras || exit 1
         step "pmc_pass_t_$ST" 120 rocprofv3 --kernel-include-regex "logreg_pass" --kernel-trace --stats --output-format csv -d "$OUT/pmc_pass_t_$ST" -o run -- python3 "$R/bench.py" --storage $ST --steps 2 --warmup 1 --no-extras || exit 1
       done
+      cd "$R" ;;
+    gbdt)  # GBDT: 100-tree bench at the bench shape (10M raw rows -> 16M post-SMOTE)
+      step gbdt 300 python tools/gbdt_bench.py --rows 10000000 --json "$OUT/gbdt.json" ;;
+    gbdtprof)  # GBDT round kernel trace (20 trees at the bench shape)
+      cd /tmp && export TMPDIR=/tmp
+      step gbdtprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gbdtprof" -o run -- python3 "$R/tools/gbdt_bench.py" --rows 10000000 --trees 20
       cd "$R" ;;
     pmcks)  # KernelSHAP linear kernel counters (3 passes, 1000-explanation batches)
       cd /tmp && export TMPDIR=/tmp
