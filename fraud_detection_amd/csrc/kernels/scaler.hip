@@ -369,10 +369,26 @@ __global__ __launch_bounds__(kThreads) void sample_partial_kernel(const float* _
   double s = 0.0, q = 0.0;
   if (c < d) {
     const double piv = (double)X[c];
-    for (int64_t i = (int64_t)blockIdx.x * 8 + rl; i < ns; i += (int64_t)gridDim.x * 8) {
-      const double v = (double)X[i * stride * d + c] - piv;
-      s += v;
-      q = fma(v, v, q);
+    // 16 strided rows' loads in flight per thread before any use: the sampled rows are far apart
+    // (no locality), so a one-load-at-a-time loop paid a full memory latency per row (~64 in a
+    // row per thread: ~70 us in front of every fp8 fit)
+    constexpr int U = 16;
+    const int64_t rs = (int64_t)gridDim.x * 8;
+    for (int64_t i0 = (int64_t)blockIdx.x * 8 + rl; i0 < ns; i0 += rs * U) {
+      float x[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t i = i0 + u * rs;
+        x[u] = i < ns ? X[i * stride * d + c] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (i0 + u * rs < ns) {
+          const double v = (double)x[u] - piv;
+          s += v;
+          q = fma(v, v, q);
+        }
+      }
     }
   }
   __shared__ double red[8][64];
