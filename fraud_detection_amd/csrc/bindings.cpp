@@ -292,7 +292,7 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_fp8_prescale(P<const float>(X), n, d, ns, stride, P<double>(partial), P<double>(sums), P<float>(mu),
                              P<float>(k), S(s));
   });
-  m.def("scaler_stats_cast_blocks", []() { return fdx::scaler_stats_cast_blocks(); });
+  m.def("scaler_stats_cast_blocks", [](int fp8) { return fdx::scaler_stats_cast_blocks(fp8); }, py::arg("fp8") = 0);
   m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,
                                 int nblocks, u s, u colscale, float out_scale) {
     fdx::launch_scaler_stats_cast(P<const float>(X), n, d, P<const float>(pivot), P<const uint8_t>(labels), bias_value,

@@ -49,7 +49,7 @@ void launch_fp8_hw_check(float* dec, const float* vals, int n, uint8_t* enc, hip
 int fp8_prescale_blocks();  // partial rows ([n][64] fp64) launch_fp8_prescale needs
 void launch_fp8_prescale(const float* X, int64_t n, int d, int64_t ns, int64_t stride, double* partial,
                          double* sums, float* mu, float* k, hipStream_t stream);
-int scaler_stats_cast_blocks();  // resident blocks of the fused kernel on this device
+int scaler_stats_cast_blocks(int fp8 = 0);  // resident blocks of the fused kernel (per row format)
 // fused K1+K2: shifted sums -> partial[nblocks][64], rows s = x - pivot in bf16, or (colscale set)
 // fp8 e4m3 of (x - pivot) * colscale * out_scale
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,

@@ -361,7 +361,9 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
 // (rows 0, stride, 2 stride, ...), shifted by row 0, in the [nblocks][64] partial layout that
 // scaler_reduce_kernel folds.  Thread (column c = tid & 31, row lane tid >> 5): the 32 lanes of a
 // half-wave read one row's d floats contiguously.
-constexpr int kSampleBlocks = 128;
+// 1024 blocks x 8 row lanes: the 65536 sampled rows are 8 per thread, all loads in flight at
+// once (the sampled rows are a page apart: each load is a DRAM + TLB miss)
+constexpr int kSampleBlocks = 1024;
 
 __global__ __launch_bounds__(kThreads) void sample_partial_kernel(const float* __restrict__ X, int d, int64_t ns,
                                                                   int64_t stride, double* __restrict__ partial) {
@@ -369,10 +371,10 @@ __global__ __launch_bounds__(kThreads) void sample_partial_kernel(const float* _
   double s = 0.0, q = 0.0;
   if (c < d) {
     const double piv = (double)X[c];
-    // 16 strided rows' loads in flight per thread before any use: the sampled rows are far apart
-    // (no locality), so a one-load-at-a-time loop paid a full memory latency per row (~64 in a
-    // row per thread: ~70 us in front of every fp8 fit)
-    constexpr int U = 16;
+    // every strided row load of a thread in flight before any use: the sampled rows are far
+    // apart (no locality); a one-load-at-a-time loop over 128 blocks paid ~64 memory latencies
+    // in a row per thread (~70 us in front of every fp8 fit)
+    constexpr int U = 8;
     const int64_t rs = (int64_t)gridDim.x * 8;
     for (int64_t i0 = (int64_t)blockIdx.x * 8 + rl; i0 < ns; i0 += rs * U) {
       float x[U];
@@ -780,15 +782,19 @@ void launch_fp8_prescale(const float* X, int64_t n, int d, int64_t ns, int64_t s
                          double* sums, float* mu, float* k, hipStream_t stream) {
   if (d < 1 || d > kCols - 2) throw std::runtime_error("fp8_prescale: 1 <= d <= 30");
   if (ns < 1 || stride < 1 || (ns - 1) * stride >= n) throw std::runtime_error("fp8_prescale: sample out of range");
+  // partial: (kSampleBlocks + scaler_reduce_scratch_rows(kSampleBlocks)) x 64 doubles
   sample_partial_kernel<<<kSampleBlocks, kThreads, 0, stream>>>(X, d, ns, stride, partial);
-  scaler_reduce_kernel<<<1, 1024, 0, stream>>>(partial, kSampleBlocks, sums);
+  launch_scaler_reduce(partial, kSampleBlocks, sums, stream);
   sample_finalize_kernel<<<1, 64, 0, stream>>>(sums, X, d, (double)ns, mu, k);
   check_launch("fp8_prescale");
 }
 
-int scaler_stats_cast_blocks() {
-  static const int cap = resident_cap(scaler_stats_cast_kernel<false, false>, kThreads);
-  return cap;
+// Each format's own occupancy: the fp8 instantiation holds more VGPRs (74 vs 68: 6 vs 7 blocks
+// per CU), and a grid sized for bf16 ran 256 fp8 blocks in a second round (+25 us per pass).
+int scaler_stats_cast_blocks(int fp8) {
+  static const int cap16 = resident_cap(scaler_stats_cast_kernel<false, false>, kThreads);
+  static const int cap8 = resident_cap(scaler_stats_cast_kernel<false, true>, kThreads);
+  return fp8 ? cap8 : cap16;
 }
 
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,

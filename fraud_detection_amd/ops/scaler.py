@@ -155,12 +155,13 @@ def scaler_fit(X: torch.Tensor, comm=None, pivot: torch.Tensor | None = None) ->
 _GRID_CACHE: dict = {}
 
 
-def _stats_cast_grid(m, dev) -> int:
-    """Every block of the fused pass resident at once (occupancy-derived).  Leaving block slots
-    free for the side-stream count kernels was measured no faster (profiles/r2_s6, reserveab)."""
-    key = dev.index
+def _stats_cast_grid(m, dev, fp8: bool = False) -> int:
+    """Every block of the fused pass resident at once (occupancy-derived, per row format).
+    Leaving block slots free for the side-stream count kernels was measured no faster
+    (profiles/r2_s6, reserveab)."""
+    key = (dev.index, bool(fp8))
     if key not in _GRID_CACHE:
-        _GRID_CACHE[key] = int(m.scaler_stats_cast_blocks())
+        _GRID_CACHE[key] = int(m.scaler_stats_cast_blocks(int(bool(fp8))))
     return _GRID_CACHE[key]
 
 
@@ -194,7 +195,8 @@ def _sample_moments(X: torch.Tensor, sample_rows: int):
         m = native()
         n, d = X.shape
         ns = min(sample_rows, (n - 1) // stride + 1)
-        ws = torch.empty(m.fp8_prescale_blocks() * 64 + 64, device=X.device, dtype=torch.float64)
+        nb = m.fp8_prescale_blocks()
+        ws = torch.empty((nb + m.scaler_reduce_scratch_rows(nb)) * 64 + 64, device=X.device, dtype=torch.float64)
         out = torch.empty(2 * d, device=X.device, dtype=torch.float32)
         m.fp8_prescale(ptr(X), n, d, ns, stride, ptr(ws), ptr(ws[-64:]), ptr(out), ptr(out[d:]), stream_of(X))
         return out[:d], out[d:]
@@ -251,7 +253,7 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         m = native()
         piv = _pivot_dev(pivot, d, X.device)
         # all blocks resident at once (occupancy-derived), never more than the tiles
-        nb = max(1, min(_stats_cast_grid(m, X.device), (n + 127) // 128))
+        nb = max(1, min(_stats_cast_grid(m, X.device, fp8), (n + 127) // 128))
         partial = torch.empty((nb + m.scaler_reduce_scratch_rows(nb)) * 64, device=X.device, dtype=torch.float64)
         sums = torch.empty(64, device=X.device, dtype=torch.float64)
         s = stream_of(X)
