@@ -278,12 +278,17 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("scaler_reduce", [](u partial, int nblocks, u sums, u s) {
     fdx::launch_scaler_reduce(P<const double>(partial), nblocks, P<double>(sums), S(s));
   });
+  m.def("scaler_reduce_level1", [](u partial, int nblocks, u mid, u s) {
+    return fdx::launch_scaler_reduce_level1(P<const double>(partial), nblocks, P<double>(mid), S(s));
+  });
   m.def("scaler_finalize", [](u sums, double n, u pivot, int d, u mean64, u var64, u scale64, u mean32, u inv32,
-                              u aff, u s, u colscale) {
+                              u aff, u s, u colscale, int nparts) {
     fdx::launch_scaler_finalize(P<const double>(sums), n, P<const float>(pivot), d, P<double>(mean64), P<double>(var64),
                                 P<double>(scale64), P<float>(mean32), P<float>(inv32), P<double>(aff), S(s),
-                                P<const float>(colscale));
-  });
+                                P<const float>(colscale), nparts);
+  }, py::arg("sums"), py::arg("n"), py::arg("pivot"), py::arg("d"), py::arg("mean64"), py::arg("var64"),
+     py::arg("scale64"), py::arg("mean32"), py::arg("inv32"), py::arg("aff"), py::arg("s"), py::arg("colscale"),
+     py::arg("nparts") = 1);
   m.def("fp8_hw_check", [](u dec, u vals, int n, u enc, u s) {
     fdx::launch_fp8_hw_check(P<float>(dec), P<const float>(vals), n, P<uint8_t>(enc), S(s));
   });
@@ -471,10 +476,13 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
   m.def("gbdt_hist_blocks", [] { return fdx::gbdt_hist_blocks(); });
   m.def("gbdt_hist_slot_words", [] { return fdx::gbdt_hist_slot_words(); });
-  m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u slots, u s) {
+  m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u slots, u s,
+                        int64_t flush_rows) {
     fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const int2>(gh), P<const int>(ridx), P<const int64_t>(seg),
-                          P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), P<long long>(slots), S(s));
-  });
+                          P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), P<long long>(slots), S(s),
+                          flush_rows);
+  }, py::arg("bins"), py::arg("gh"), py::arg("ridx"), py::arg("seg"), py::arg("gcnt"), py::arg("level"),
+     py::arg("d"), py::arg("hist"), py::arg("slots"), py::arg("s"), py::arg("flush_rows") = 0);
   m.def("gbdt_split", [](u hist, u gcnt, int level, int d, u nbins, u cuts, double ginv, double hinv, double lam,
                          double mcw, double gamma, u feat, u bin, u thr, u gain, u ng, u nh, u s) {
     fdx::launch_gbdt_split(P<unsigned long long>(hist), P<const int64_t>(gcnt), level, d, P<const int>(nbins),

@@ -148,7 +148,7 @@ __device__ __forceinline__ int64_t level_chunk(const int64_t* seg, const int64_t
 __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
     const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
-    long long* __restrict__ slots) {
+    long long* __restrict__ slots, int64_t flush_rows) {
   __shared__ unsigned long long sh[kHistWords];
   const int h0 = heap_first(level), nn = 1 << level;
   int64_t total;
@@ -171,8 +171,8 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
     slot_base += cnt;
     if (lo >= hi) continue;
     long long* dst = slots + (int64_t)my_slot * kHistEntries;
-    for (int64_t c0 = lo; c0 < hi; c0 += kFlushRows) {
-      const int64_t c1 = min(hi, c0 + kFlushRows);
+    for (int64_t c0 = lo; c0 < hi; c0 += flush_rows) {
+      const int64_t c1 = min(hi, c0 + flush_rows);
       for (int i = threadIdx.x; i < nw; i += kHistThreads) sh[i] = 0ull;
       __syncthreads();
       // kHistBatch rows per thread in flight: every row index, then every row's bins and (g, h),
@@ -737,12 +737,15 @@ int64_t gbdt_hist_slot_words() { return (int64_t)(gbdt_hist_blocks() + 2 * kGBMa
 
 void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
-                      hipStream_t stream) {
+                      hipStream_t stream, int64_t flush_rows) {
+  // flush_rows <= kFlushRows (the packed-word exactness bound); smaller values only for tests of
+  // the multi-flush path
+  if (flush_rows <= 0 || flush_rows > kFlushRows) flush_rows = kFlushRows;
   // slots: gbdt_hist_slot_words() int64 (one [feature][bin][g, h] slot per (node, block) pair:
   // at most blocks + nodes pairs)
   if (level < 0 || (1 << level) > kGBMaxNodes + 1) throw std::runtime_error("gbdt_hist: level out of range");
   const int nb = gbdt_hist_blocks();
-  gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots);
+  gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows);
   check_launch("gbdt_hist");
   const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, 1u << level);
   gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, nb, hist);

@@ -41,10 +41,11 @@ void launch_scaler_partial(const float* X, int64_t n, int ld, int d, const float
                            double* partial, int nblocks, hipStream_t stream);
 int scaler_reduce_scratch_rows(int nblocks);  // extra [64] rows launch_scaler_reduce needs after the partials
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream);
+int launch_scaler_reduce_level1(const double* partial, int nblocks, double* mid, hipStream_t stream);
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
                             float* inv32, double* aff, hipStream_t stream,
-                            const float* colscale = nullptr);
+                            const float* colscale = nullptr, int nparts = 1);
 void launch_fp8_hw_check(float* dec, const float* vals, int n, uint8_t* enc, hipStream_t stream);
 int fp8_prescale_blocks();  // partial rows ([n][64] fp64) launch_fp8_prescale needs
 void launch_fp8_prescale(const float* X, int64_t n, int d, int64_t ns, int64_t stride, double* partial,
@@ -211,7 +212,7 @@ int gbdt_hist_blocks();
 int64_t gbdt_hist_slot_words();  // int64 words of the per-(node, block) histogram slots
 void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
-                      hipStream_t stream);
+                      hipStream_t stream, int64_t flush_rows = 0);
 void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
                        const float* cuts, double ginv, double hinv, double lambda,
                        double min_child_weight, double gamma, int* feat, int* bin, float* thr,

@@ -198,7 +198,7 @@ __device__ __forceinline__ int stats_fetch(const float* __restrict__ X, int64_t 
 // statistics from this same pass turn that into the solver's affine map, so the prescale only
 // has to be roughly right.
 template <bool NT, bool FP8>
-__global__ __launch_bounds__(kThreads) void scaler_stats_cast_kernel(
+__global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kernel(
     const float* __restrict__ X, int64_t n, int d, const float* __restrict__ pivot,
     const uint8_t* __restrict__ labels, float bias_value, void* __restrict__ outv,
     double* __restrict__ partial, const float* __restrict__ colscale, float out_scale) {
@@ -321,16 +321,24 @@ __global__ void scaler_finalize_kernel(const double* __restrict__ sums, double n
                                        double* __restrict__ mean64, double* __restrict__ var64,
                                        double* __restrict__ scale64, float* __restrict__ mean32,
                                        float* __restrict__ inv32, double* __restrict__ aff,
-                                       const float* __restrict__ colscale) {
+                                       const float* __restrict__ colscale, int nparts) {
   const int c = threadIdx.x;
   if (c >= kCols) return;
+  // nparts > 1: `sums` holds the first-level reduce's [nparts][64] rows, summed here in order
+  // (the order of the second-level reduce launch this replaces: bit-identical sums)
+  double s1 = 0.0, s2 = 0.0, sn = 0.0;
+  for (int p = 0; p < nparts; ++p) {
+    s1 += sums[64 * p + c];
+    s2 += sums[64 * p + 32 + c];
+    sn += sums[64 * p + kCols - 1];
+  }
   // n < 0: the (all-reduced) row count rides in the unused slot sums[31] (one collective for the
   // sums and the count, and no host round trip for n)
-  if (n < 0.0) n = sums[kCols - 1];
+  if (n < 0.0) n = sn;
   if (c < d) {
-    const double m = sums[c] / n;
+    const double m = s1 / n;
     const double mean = (double)pivot[c] + m;
-    double var = sums[32 + c] / n - m * m;
+    double var = s2 / n - m * m;
     if (var < 0.0) var = 0.0;
     const double eps = 2.220446049250313e-16;
     const double ub = n * eps * var + (n * mean * eps) * (n * mean * eps);
@@ -753,6 +761,16 @@ int scaler_reduce_scratch_rows(int nblocks) {
   return nblocks > kRedSpan ? (nblocks + kRedSpan - 1) / kRedSpan : 0;
 }
 
+int launch_scaler_reduce_level1(const double* partial, int nblocks, double* mid, hipStream_t stream) {
+  // the first level only: [nblocks][64] -> [g][64] rows at `mid` (g returned), which
+  // scaler_finalize(nparts = g) sums in the order the second level would
+  if (nblocks > kRedSpan * kRedSpan) throw std::runtime_error("scaler_reduce: too many block partials");
+  const int g = (nblocks + kRedSpan - 1) / kRedSpan;
+  scaler_reduce_kernel<<<g, 1024, 0, stream>>>(partial, nblocks, mid);
+  check_launch("scaler_reduce");
+  return g;
+}
+
 void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipStream_t stream) {
   // nblocks > kRedSpan: `partial` holds scaler_reduce_scratch_rows(nblocks) more [64] rows after
   // the block partials for the first level's outputs
@@ -770,9 +788,10 @@ void launch_scaler_reduce(const double* partial, int nblocks, double* sums, hipS
 
 void launch_scaler_finalize(const double* sums, double n, const float* pivot, int d,
                             double* mean64, double* var64, double* scale64, float* mean32,
-                            float* inv32, double* aff, hipStream_t stream, const float* colscale) {
+                            float* inv32, double* aff, hipStream_t stream, const float* colscale, int nparts) {
+  if (nparts < 1 || nparts > kRedSpan) throw std::runtime_error("scaler_finalize: 1 <= nparts <= 128");
   scaler_finalize_kernel<<<1, 64, 0, stream>>>(sums, n, pivot, d, mean64, var64, scale64, mean32,
-                                               inv32, aff, colscale);
+                                               inv32, aff, colscale, nparts);
   check_launch("scaler_finalize");
 }
 

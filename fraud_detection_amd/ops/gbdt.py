@@ -154,6 +154,11 @@ def bin_rows(X: torch.Tensor, cuts: np.ndarray, nbins: np.ndarray) -> torch.Tens
 
 
 # ---- training --------------------------------------------------------------------------------
+# Rows a histogram block accumulates in LDS between flushes to its slot (0: the kernel's bound,
+# 2^16 -- packed (h, g) words stay exact); tests lower it to exercise the multi-flush path.
+HIST_FLUSH_ROWS = 0
+
+
 class _Workspace:
     def __init__(self, n: int, depth: int, dev: torch.device):
         nheap = (2 << depth) - 1
@@ -291,7 +296,7 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
             m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
-                        ptr(ws.hist), ptr(ws.slots), st)
+                        ptr(ws.hist), ptr(ws.slots), st, HIST_FLUSH_ROWS)
             if dist:
                 comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,

@@ -102,9 +102,10 @@ def _aff_cpu(sums: np.ndarray, n: float, scale: np.ndarray, d: int) -> torch.Ten
 
 
 def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int, want_aff: bool = False,
-                    colscale: torch.Tensor | None = None) -> ScalerStats:
+                    colscale: torch.Tensor | None = None, nparts: int = 1) -> ScalerStats:
     """``n_total`` None: the count is in sums[31] (device) -- see scaler_fit.  ``colscale`` (fp8
-    rows, [d] float32): the stored values are v = s * colscale, folded into ``aff``."""
+    rows, [d] float32): the stored values are v = s * colscale, folded into ``aff``.  ``nparts``
+    (device): ``sums`` is [nparts][64] first-level reduce rows, summed in order by the kernel."""
     dev = sums.device
     if n_total is None and not sums.is_cuda:
         n_total = float(sums[31])
@@ -127,7 +128,7 @@ def scaler_finalize(sums: torch.Tensor, n_total, pivot: torch.Tensor, d: int, wa
     aff = torch.empty(64, device=dev, dtype=torch.float64) if want_aff else None
     m.scaler_finalize(ptr(sums), -1.0 if n_total is None else float(n_total), ptr(piv), d, ptr(mean64), ptr(var64),
                       ptr(scale64), ptr(mean32), ptr(inv32), ptr(aff), stream_of(sums),
-                      ptr(colscale if (want_aff and colscale is not None) else None))
+                      ptr(colscale if (want_aff and colscale is not None) else None), int(nparts))
     n_src = sums[31:32] if n_total is None else float(n_total)
     return ScalerStats(n_src, d, mean64, var64, scale64, mean32, inv32, aff=aff)
 
@@ -254,13 +255,21 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         piv = _pivot_dev(pivot, d, X.device)
         # all blocks resident at once (occupancy-derived), never more than the tiles
         nb = max(1, min(_stats_cast_grid(m, X.device, fp8), (n + 127) // 128))
-        partial = torch.empty((nb + m.scaler_reduce_scratch_rows(nb)) * 64, device=X.device, dtype=torch.float64)
+        # block partials, then >= 1 row for the first-level reduce output
+        partial = torch.empty((nb + max(1, m.scaler_reduce_scratch_rows(nb))) * 64, device=X.device,
+                              dtype=torch.float64)
         sums = torch.empty(64, device=X.device, dtype=torch.float64)
         s = stream_of(X)
+        nparts = 1
         if n > 0:
             m.scaler_stats_cast(ptr(X), n, d, ptr(piv), ptr(labels), float(bias_value), ptr(out), ptr(partial), nb, s,
                                 ptr(colscale), float(fp8_scale) if fp8 else 1.0)
-            m.scaler_reduce(ptr(partial), nb, ptr(sums), s)
+            if dist:  # the all-reduce needs the one [64] sums vector
+                m.scaler_reduce(ptr(partial), nb, ptr(sums), s)
+            else:  # first level only: the finalize kernel sums its rows (one launch fewer)
+                mid = partial[nb * 64:]
+                nparts = int(m.scaler_reduce_level1(ptr(partial), nb, ptr(mid), s))
+                sums = mid[: nparts * 64]
         else:
             sums.zero_()
     if dist:
@@ -268,7 +277,8 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         sums = comm.all_reduce(sums)
         st = scaler_finalize(sums, None, pivot, d, want_aff=True, colscale=colscale)
     else:
-        st = scaler_finalize(sums, float(n), pivot, d, want_aff=True, colscale=colscale)
+        st = scaler_finalize(sums, float(n), pivot, d, want_aff=True, colscale=colscale,
+                             nparts=nparts if X.is_cuda else 1)
     # fp8: stored v = s * k  ->  z = (s - c) * inv = (v - k c) * (inv / k), folded in the finalize
     return st
 

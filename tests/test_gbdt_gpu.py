@@ -124,6 +124,23 @@ def test_gbdt_device_resume_bit_identical(dev, tmp_path):
         assert np.array_equal(getattr(res, k), getattr(full, k)), k
 
 
+def test_hist_multi_flush_bit_identical(dev, monkeypatch):
+    """A histogram block flushes its packed LDS words to its slot every HIST_FLUSH_ROWS rows (the
+    bound that keeps (h << 32) + g exact); flushing every 1000 rows -- many flushes per block,
+    accumulated into the same slot -- gives the same trees bit for bit, and so does the oracle."""
+    Xd, yd, X, y = _data(120_000, 30, seed=15)
+    p = gb.GBDTParams(n_estimators=3, max_depth=5)
+    cuts = R.quantile_cuts(X, 256)
+    a, ma = gb.fit(Xd, yd, p, cuts=cuts, return_margin=True)
+    monkeypatch.setattr(gb, "HIST_FLUSH_ROWS", 1000)
+    b, mb = gb.fit(Xd, yd, p, cuts=cuts, return_margin=True)
+    for k in ("feat", "bin", "thr", "gain", "leaf"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert torch.equal(ma, mb)
+    ref = gb.fit(torch.from_numpy(X), torch.from_numpy(y), gb.GBDTParams(n_estimators=1, max_depth=5), cuts=cuts)
+    assert np.array_equal(a.feat[0], ref.feat[0]) and np.array_equal(a.bin[0], ref.bin[0])
+
+
 def test_gbdt_deterministic_runs(dev):
     Xd, yd, X, y = _data(50_000, 30, seed=14)
     p = gb.GBDTParams(n_estimators=8, max_depth=5)
