@@ -150,8 +150,8 @@ class DevicePipeline:
     def _train_buffer(self, n_rows: int, device, allow_double: bool = False) -> torch.Tensor:
         cfg = self.cfg
         dt = TORCH_STORAGE[cfg.storage]
-        double = (allow_double and cfg.deferred_check and cfg.solver == "newton" and device.type == "cuda"
-                  and self._world()[1] == 1)
+        world = self._world()[1]
+        double = allow_double and cfg.deferred_check and cfg.solver == "newton" and device.type == "cuda"
         b = self._bi if double else 0
         for i in range(2):  # a buffer about to be written must not hold an unverified fit
             if i == b or not double:
@@ -160,7 +160,13 @@ class DevicePipeline:
         if buf is None or buf.shape[0] < n_rows or buf.device != device or buf.dtype != dt:
             self._bufs[b] = None
             need = n_rows * NCOLS * torch.empty((), dtype=dt).element_size()
-            if double and b == 1 and torch.cuda.mem_get_info(device)[0] < 2 * need:
+            # under DP every rank must take the same branch (the deferred fit's collectives run at
+            # different points than a checked fit's): decide from the device's total memory, which
+            # is the same on every rank, not from its free memory
+            def room():
+                return (torch.cuda.get_device_properties(device).total_memory // 2 if world > 1
+                        else torch.cuda.mem_get_info(device)[0])
+            if double and b == 1 and room() < 2 * need:
                 double, b = False, 0  # no room for a second buffer: checked fits, one buffer
                 self._settle(0)
                 buf = self._bufs[0]
@@ -345,9 +351,12 @@ class DevicePipeline:
         if cfg.init_std > 0:
             w0[:d] = np.random.default_rng(cfg.seed).normal(0.0, cfg.init_std, d)
         if cfg.solver == "newton":
-            defer = self._defer_now and comm is None and dev.type == "cuda"
-            sig = (rows.shape[0], n_sched, cfg.C, cfg.tol, cfg.max_iter, tuple(class_w), str(cfg.hess_stride),
-                   fused, cfg.storage)
+            defer = self._defer_now and dev.type == "cuda"
+            # global quantities only: under DP every rank must make the same prediction (the
+            # predicted iterations carry the same all-reduces on every rank)
+            n_global = int(sum(r[1] + q for r, q in zip(ranks, new_per_rank)))
+            sig = (n_global, n_sched, len(ranks), cfg.C, cfg.tol, cfg.max_iter, tuple(class_w),
+                   str(cfg.hess_stride), fused, cfg.storage)
             pred = self._full_pred[1] if (defer and self._full_pred and self._full_pred[0] == sig) else None
             fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,

@@ -280,11 +280,13 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     iteration.  The fixed point is unchanged: only the step's curvature model is older.
     ``affine``: [64] float64 (c | 1/sigma) when the rows are pivot-shifted instead of standardized
     (ops/scaler.scaler_fit_cast): the fit still runs in standardized space (same w, same C).
-    ``full_iters`` (single process): enqueue exactly that many full-data iterations -- the count
+    ``full_iters``: enqueue exactly that many full-data iterations -- the count
     the previous fit of this shape needed -- with no host wait, and return a PendingFit whose
     ``verify()`` checks convergence later and finishes the fit if the prediction was short.  The
     same iterations run either way; the host-checked loop's trailing no-op iterations and its
-    wait at the end of the fit disappear.  Rows and workspace must stay untouched until then."""
+    wait at the end of the fit disappear.  Rows and workspace must stay untouched until then.
+    Under DP every rank must pass the same ``full_iters`` and verify at the same point of its
+    program (the iterations, and a continuation, carry the gradient all-reduces)."""
     check_rows(rows)
     w0 = _default_w0(w0)
     if not rows.is_cuda:
@@ -410,7 +412,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             if int(flags[c][0]) & 1:
                 break
 
-    if full_iters is not None and not dp and sync and fdev[0]:
+    if full_iters is not None and sync and fdev[0]:
         k = int(max(1, min(int(full_iters), max_iter)))
         ws._seq = (ws._seq + 1) & 0x3FFFFFFF
         seq0 = ws._seq
