@@ -172,6 +172,12 @@ class DevicePipeline:
                 buf = self._bufs[0]
             if buf is None or buf.shape[0] < n_rows or buf.device != device or buf.dtype != dt:
                 buf = self._bufs[b] = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
+        if double:
+            # allocate the other buffer NOW too: its first allocation (a large hipMalloc, ~0.1 s)
+            # must land in the first fit, not in whichever later fit first alternates to it
+            o = self._bufs[b ^ 1]
+            if o is None or o.shape[0] < n_rows or o.device != device or o.dtype != dt:
+                self._bufs[b ^ 1] = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
         self._buf, self._cur, self._defer_now = buf, b, double
         return buf[:n_rows]
 
@@ -344,8 +350,11 @@ class DevicePipeline:
             class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         # ---- K4: fit ---------------------------------------------------------------------
         b = self._cur
-        if dev.type == "cuda" and (self._wss[b] is None or self._wss[b].device != dev):
-            self._wss[b] = lr_ops.LRWorkspace(dev)
+        if dev.type == "cuda":
+            for i in ((0, 1) if self._defer_now else (b,)):  # both at once (see _train_buffer)
+                if self._wss[i] is None or self._wss[i].device != dev:
+                    self._wss[i] = lr_ops.LRWorkspace(dev)
+                    self._wss[i].prepare_flags()
         self._ws = self._wss[b]
         w0 = np.zeros(NCOLS)
         if cfg.init_std > 0:

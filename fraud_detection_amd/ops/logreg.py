@@ -147,6 +147,16 @@ class LRWorkspace:
         self._blob = torch.zeros(_BLOB_BYTES, device=device, dtype=torch.uint8)
         self.state, self.w32, self.class_w, self.done = _blob_views(self._blob)
 
+    def prepare_flags(self, depth: int = 2):
+        """The mapped pinned convergence-flag words newton_fit polls (pinned allocations cost tens
+        of microseconds to milliseconds: made once per workspace, here or on first use)."""
+        if getattr(self, "_flags", None) is None or len(self._flags) < depth + 1:
+            m = native()
+            self._flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(depth + 1)]
+            self._flag_dev = [int(m.host_device_pointer(f.data_ptr())) for f in self._flags]
+            self._events = [torch.cuda.Event() for _ in range(depth + 1)]
+            self._seq = getattr(self, "_seq", 0)
+
     def reset(self, w0: np.ndarray, class_w=(1.0, 1.0), aff: int = 0):
         """Initial state (w0 in the padded layout, class weights, done = 0) written by ONE kernel
         whose arguments carry the values -- no pinned staging and no H2D blit.  ``aff``: device
@@ -380,15 +390,10 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     if lookahead is None:  # profiles/r2_s5/newton_lookahead_ab.txt
         lookahead = 1 if (comm is not None and comm.world_size > 1) else 2
     depth = max(1, int(lookahead))
-    if getattr(ws, "_flags", None) is None or len(ws._flags) < depth + 1:
-        # pinned allocations cost tens of us: once per workspace.  The chunk's last Newton update
-        # writes (seq << 1) | done straight into a mapped pinned word (device address below) and
-        # the host polls it: no D2H copy kernel and no event per check, whose dependency gaps cost
-        # ~10 us each in the timeline (profiles/r2_s5).
-        ws._flags = [torch.zeros(1, dtype=torch.int32, pin_memory=True) for _ in range(depth + 1)]
-        ws._flag_dev = [int(m.host_device_pointer(f.data_ptr())) for f in ws._flags]
-        ws._events = [torch.cuda.Event() for _ in range(depth + 1)]
-        ws._seq = 0
+    # The chunk's last Newton update writes (seq << 1) | done straight into a mapped pinned word
+    # (device address) and the host polls it: no D2H copy kernel and no event per check, whose
+    # dependency gaps cost ~10 us each in the timeline (profiles/r2_s5).
+    ws.prepare_flags(depth)
     flags, events, fdev = ws._flags, ws._events, ws._flag_dev
 
     def checked_loop(it: int):
