@@ -26,7 +26,6 @@ constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 constexpr int kMaxK = 8;
 constexpr float kNegBig = -3.0e38f;
-constexpr int kSeedTiles = 2;  // candidate tiles of the k-NN seed pass (launch_knn_topk)
 constexpr int kQFlush = 4;               // flush a wave's queues once any lane holds this many
 constexpr int kQCap = kQFlush - 1 + 16 + 1;  // + one tile's worth of appends + the dump slot
 
@@ -118,21 +117,13 @@ __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, i
 //     (exact score-then-index order, self/padding excluded) and the threshold becomes the k-th
 //     best of the UNION of the two half-lists of the query (lanes j and j+32), which is a valid
 //     filter for both halves and about twice as tight.
-//
-// seed (nullable, [mq][K] sorted lists of a pass over the first candidate tiles): the K-th best
-// score of ANY K valid candidates is a lower bound of the K-th best over all of them, so every
-// slice starts filtering at it instead of at -inf.  A slice otherwise appends every score of its
-// first tiles to the queues until its own lists fill (the "list-filling" cost that made a tile
-// ~3,200 SIMD cycles at 13.6k rows vs ~1,900 at 170k, profiles/README.md r2_s3i).  Exact either
-// way: a candidate below the bound cannot be in the top K.
 template <int K>
 __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict__ Q, int mq,
                                                          const float* __restrict__ C,
                                                          int mc_pad, int mc,
                                                          int64_t self_offset,
                                                          int* __restrict__ out_idx,
-                                                         float* __restrict__ out_score,
-                                                         const float* __restrict__ seed) {
+                                                         float* __restrict__ out_score) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
   const int q0 = blockIdx.x * 32;
@@ -151,8 +142,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  const float thr0 = (seed != nullptr && qg < mq) ? seed[(int64_t)qg * K + (K - 1)] : kNegBig;
-  float thr = thr0;
+  float thr = kNegBig;
 
   // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks.  Slot
   // kQCap - 1 is the lane's dump slot.
@@ -183,7 +173,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = fmaxf(kth, thr0);
+    thr = kth;
   };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
@@ -794,19 +784,9 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
   const dim3 grid(mq_pad / 32, nsplit);
   int* oi = nsplit > 1 ? ws_idx : out_idx;
   float* os = nsplit > 1 ? ws_score : out_score;
-  // split search: a seed pass over the first kSeedTiles candidate tiles writes [mq][k] lists
-  // into workspace slice `nsplit` (the workspaces hold nsplit + 1 slices); every slice of the
-  // main search starts filtering at their k-th score
-  const int seed_tiles = std::min(mc_pad / 32, kSeedTiles);
-  const bool seeded = nsplit > 1 && seed_tiles * 32 < mc_pad;
-  float* seed_s = seeded ? ws_score + (int64_t)nsplit * mq * k : nullptr;
-  int* seed_i = seeded ? ws_idx + (int64_t)nsplit * mq * k : nullptr;
 #define FDX_KNN(KK)                                                                             \
-  if (seeded)                                                                                   \
-    knn_topk_kernel<KK><<<dim3(mq_pad / 32, 1), kWave, 0, stream>>>(                            \
-        Q, mq, C, seed_tiles * 32, std::min(mc, seed_tiles * 32), self_offset, seed_i, seed_s, nullptr); \
   knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi,           \
-                                                     os, seed_s);                                \
+                                                     os);                                        \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {

@@ -115,9 +115,9 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     else:
         ns = {"fp32": m.knn_splits, "fp32lds": m.knn_lds_splits, "bf16x3": m.knn3_splits}[eng](mq_pad, mc_pad)
     ws_s = ws_i = None
-    if ns > 1:  # ns slice lists + one for the fp32 engine's seed pass (knn.hip launch_knn_topk)
-        ws_s = torch.empty((ns + 1, mq, k), device=Q.device, dtype=torch.float32)
-        ws_i = torch.empty((ns + 1, mq, k), device=Q.device, dtype=torch.int32)
+    if ns > 1:
+        ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
+        ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
     if eng == "fp32":
         m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
                    ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
