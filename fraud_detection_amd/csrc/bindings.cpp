@@ -10,6 +10,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
+#include <cstring>
 #include <memory>
 #include <string>
 #include <thread>
@@ -92,12 +94,67 @@ struct NativeOwner {
   float* out_dev[2] = {nullptr, nullptr};
   hipEvent_t ev[2] = {nullptr, nullptr};
   std::atomic<uint64_t> errors{0};
+  // persistent small-batch path (predict_persistent_kernel): a mailbox in coherent mapped host
+  // memory instead of a launch + event per batch
+  bool persist = false;
+  fdx::PersistCtl* pctl = nullptr;
+  fdx::PersistCtl* pctl_dev = nullptr;
+  float* p_in = nullptr;
+  float* p_in_dev = nullptr;
+  float* p_out = nullptr;
+  float* p_out_dev = nullptr;
+  uint32_t pcap = 0, pseq = 0;
+  hipStream_t pstream = nullptr;
+  uint64_t idle_ticks = 0, life_ticks = 0;
+  std::atomic<uint64_t> p_batches{0}, p_launches{0};
 
-  void launch(int set, uint32_t n, bool explain) {
+  static uint32_t ld(const uint32_t* q) { return __atomic_load_n(q, __ATOMIC_ACQUIRE); }
+  static void st(uint32_t* q, uint32_t v) { __atomic_store_n(q, v, __ATOMIC_RELEASE); }
+  static double secs_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  // A running persistent kernel, (re)launched if it exited (idle timeout / lifetime).
+  bool ensure_persistent() {
+    if (ld(&pctl->state) == fdx::kPersistRunning) return true;
+    if (hipStreamSynchronize(pstream) != hipSuccess) return false;  // the exited launch is gone
+    st(&pctl->stop, 0u);
+    st(&pctl->state, 0u);
+    try {
+      fdx::launch_predict_persistent(pctl_dev, p_in_dev, d, (int)pcap, a, c, bias, p_out_dev, p_out_dev + pcap,
+                                     idle_ticks, life_ticks, pstream);
+    } catch (...) {
+      return false;
+    }
+    p_launches.fetch_add(1);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (ld(&pctl->state) != fdx::kPersistRunning) {
+      if (ld(&pctl->state) == fdx::kPersistExited || secs_since(t0) > 5.0) return false;
+      __builtin_ia32_pause();
+    }
+    return true;
+  }
+  // Post the n rows already in p_in; true once the kernel has written their results to p_out.
+  bool serve_persistent(uint32_t n) {
+    if (!ensure_persistent()) return false;
+    const uint32_t seq = ++pseq;
+    st(&pctl->n, n);
+    st(&pctl->doorbell, seq);  // release: the rows collect() wrote are visible before the bell
+    const auto t0 = std::chrono::steady_clock::now();
+    while (ld(&pctl->done) != seq) {
+      if (ld(&pctl->state) == fdx::kPersistExited && ld(&pctl->done) != seq) {
+        if (!ensure_persistent()) return false;  // exited just before the bell: serve again
+      }
+      if (secs_since(t0) > 2.0) return false;
+      __builtin_ia32_pause();
+    }
+    return true;
+  }
+
+  void launch(int set, uint32_t n, bool explain, const void* in = nullptr) {
     const int dphi = explain ? d : 0;
     float* o = out_dev[set];
-    fdx::launch_predict_shap(in_dev[set], 1, n, d, d, dphi, a, c, bias, o, o + n, explain ? o + 2 * (size_t)n : nullptr,
-                             dphi, stream);
+    fdx::launch_predict_shap(in ? in : in_dev[set], 1, n, d, d, dphi, a, c, bias, o, o + n,
+                             explain ? o + 2 * (size_t)n : nullptr, dphi, stream);
     hip_check(hipEventRecord(ev[set], stream), "hipEventRecord");
   }
   void finish(int set, uint32_t n, bool explain, bool ok) {
@@ -108,11 +165,37 @@ struct NativeOwner {
     if (!good) errors.fetch_add(1);
     ring->complete(o, o + n, explain ? o + 2 * (size_t)n : nullptr, explain ? (uint32_t)d : 0u, good, set);
   }
+  // Small batch, nothing in flight on the launch path: the persistent kernel (predict) or one
+  // synchronous launch from the same staging (explain, or the persistent kernel unavailable).
+  void run_small() {
+    auto r = ring->collect(p_in, pcap, window_us, 50.0, 0);
+    const uint32_t n = r.first;
+    if (!n) return;
+    const bool explain = r.second == 1;
+    if (!explain && serve_persistent(n)) {
+      p_batches.fetch_add(1);
+      ring->complete(p_out, p_out + pcap, nullptr, 0u, true, 0);
+      return;
+    }
+    try {
+      launch(0, n, explain, p_in_dev);
+      finish(0, n, explain, true);
+    } catch (...) {
+      errors.fetch_add(1);
+      ring->complete(nullptr, nullptr, nullptr, 0, false, 0);
+    }
+  }
+
   void run() {
     int cur = 0, inf_set = -1;
     uint32_t inf_n = 0;
     bool inf_explain = false;
     while (!stop.load(std::memory_order_relaxed) || inf_set >= 0) {
+      if (persist && inf_set < 0 && !stop.load(std::memory_order_relaxed) &&
+          ring->ready_rows(pcap + 1) <= pcap) {
+        run_small();
+        continue;
+      }
       uint32_t n = 0, op = 0;
       if (!stop.load(std::memory_order_relaxed)) {
         if (inf_set < 0) {
@@ -233,7 +316,8 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("predict_h2h", &predict_h2h, py::call_guard<py::gil_scoped_release>());
   m.def("owner_start", [](u ring_base, size_t ring_bytes, u a, u c, float bias, int d, uint32_t cap, double window_us,
                           uint32_t pipe_rows, u stream, u in_host0, u in_host1, u in_dev0, u in_dev1, u out_host0,
-                          u out_host1, u out_dev0, u out_dev1) {
+                          u out_host1, u out_dev0, u out_dev1, uint32_t persist_rows, double idle_ms,
+                          double life_ms) {
     auto* o = new NativeOwner();
     o->ring = std::make_unique<fdx_ring::Ring>(reinterpret_cast<char*>(ring_base), ring_bytes);
     if ((int)o->ring->d_() != d) {
@@ -257,13 +341,55 @@ PYBIND11_MODULE(_fdx_native, m) {
     o->out_dev[0] = P<float>(out_dev0);
     o->out_dev[1] = P<float>(out_dev1);
     for (int i = 0; i < 2; ++i) hip_check(hipEventCreateWithFlags(&o->ev[i], hipEventDisableTiming), "hipEventCreate");
+    if (persist_rows > 0) {
+      o->pcap = std::min(persist_rows, cap);
+      const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+      void* hp = nullptr;
+      hip_check(hipHostMalloc(&hp, sizeof(fdx::PersistCtl), fl), "hipHostMalloc");
+      std::memset(hp, 0, sizeof(fdx::PersistCtl));
+      o->pctl = static_cast<fdx::PersistCtl*>(hp);
+      hip_check(hipHostMalloc(&hp, (size_t)o->pcap * d * sizeof(float), fl), "hipHostMalloc");
+      o->p_in = static_cast<float*>(hp);
+      hip_check(hipHostMalloc(&hp, (size_t)o->pcap * 2 * sizeof(float), fl), "hipHostMalloc");
+      o->p_out = static_cast<float*>(hp);
+      void* dp = nullptr;
+      hip_check(hipHostGetDevicePointer(&dp, o->pctl, 0), "hipHostGetDevicePointer");
+      o->pctl_dev = static_cast<fdx::PersistCtl*>(dp);
+      hip_check(hipHostGetDevicePointer(&dp, o->p_in, 0), "hipHostGetDevicePointer");
+      o->p_in_dev = static_cast<float*>(dp);
+      hip_check(hipHostGetDevicePointer(&dp, o->p_out, 0), "hipHostGetDevicePointer");
+      o->p_out_dev = static_cast<float*>(dp);
+      hip_check(hipStreamCreateWithFlags(&o->pstream, hipStreamNonBlocking), "hipStreamCreate");
+      int dev = 0, khz = 0;
+      hip_check(hipGetDevice(&dev), "hipGetDevice");
+      if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+      o->idle_ticks = (uint64_t)(idle_ms * khz);
+      o->life_ticks = (uint64_t)(life_ms * khz);
+      o->persist = true;
+    }
     o->th = std::thread([o] { o->run(); });
     return reinterpret_cast<u>(o);
+  }, py::arg("ring_base"), py::arg("ring_bytes"), py::arg("a"), py::arg("c"), py::arg("bias"), py::arg("d"),
+     py::arg("cap"), py::arg("window_us"), py::arg("pipe_rows"), py::arg("stream"), py::arg("in_host0"),
+     py::arg("in_host1"), py::arg("in_dev0"), py::arg("in_dev1"), py::arg("out_host0"), py::arg("out_host1"),
+     py::arg("out_dev0"), py::arg("out_dev1"), py::arg("persist_rows") = 0, py::arg("idle_ms") = 200.0,
+     py::arg("life_ms") = 10000.0);
+  m.def("owner_persistent_stats", [](u h) {
+    auto* o = reinterpret_cast<NativeOwner*>(h);
+    return py::make_tuple(o->p_batches.load(), o->p_launches.load(), o->persist);
   });
   m.def("owner_stop", [](u h) {
     auto* o = reinterpret_cast<NativeOwner*>(h);
     o->stop.store(true);
     if (o->th.joinable()) o->th.join();
+    if (o->persist) {  // tell the kernel to exit, then wait for its launch to finish
+      NativeOwner::st(&o->pctl->stop, 1u);
+      (void)hipStreamSynchronize(o->pstream);
+      (void)hipStreamDestroy(o->pstream);
+      (void)hipHostFree(o->pctl);
+      (void)hipHostFree(o->p_in);
+      (void)hipHostFree(o->p_out);
+    }
     const uint64_t err = o->errors.load();
     for (int i = 0; i < 2; ++i) (void)hipEventDestroy(o->ev[i]);
     delete o;

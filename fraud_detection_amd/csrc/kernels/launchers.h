@@ -80,6 +80,25 @@ void launch_predict_fp8(const uint8_t* X, int64_t n, const float* w, float* prob
 // z = sum_{j<dz} a_j x_j + bias;  phi_j = a_j (x_j - c_j), j < dphi.
 void launch_predict_raw64(const float* X, int64_t n, int ld, int d, const float* a, float bias, double* prob,
                           double* logit, hipStream_t stream);
+// Persistent serving kernel (serve/gpu_owner.py native owner, small batches): ONE workgroup that
+// polls a mailbox in fine-grained (coherent, mapped) host memory, scores the posted rows and
+// acknowledges -- no kernel launch and no event per batch.  Every field is written with
+// system-scope atomics on both sides.  The kernel exits on `stop`, after `idle_ticks` of wall
+// clock without a request, or after `life_ticks` in total (every wave reaches the exit; the
+// owner relaunches on demand).
+struct PersistCtl {
+  uint32_t doorbell;  // host: sequence number of the posted batch
+  uint32_t n;         // host: rows of the posted batch (<= the kernel's cap)
+  uint32_t done;      // kernel: sequence number of the last finished batch
+  uint32_t state;     // kernel: 1 running, 2 exited
+  uint32_t stop;      // host: 1 = exit now
+  uint32_t served;    // kernel: batches served by this launch
+  uint32_t pad[2];
+};
+constexpr uint32_t kPersistRunning = 1, kPersistExited = 2;
+void launch_predict_persistent(PersistCtl* ctl, const float* X, int d, int cap, const float* a, const float* c,
+                               float bias, float* prob, float* logit, uint64_t idle_ticks, uint64_t life_ticks,
+                               hipStream_t stream);
 void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, int dphi,
                          const float* a, const float* c, float bias, float* prob, float* logit,
                          float* phi, int ld_phi, hipStream_t stream);

@@ -190,6 +190,105 @@ __global__ __launch_bounds__(kThreads) void predict_shap_kernel(
   }
 }
 
+// Persistent serving kernel (launchers.h PersistCtl).  Rows are scored exactly as
+// predict_shap_kernel<1, 2> scores them (8 lanes per row, 4 columns per lane, the same fma order
+// and DPP row sum, fast_sigmoid), so a request gets the same bits on either path.  Host-memory
+// rows are read with system-scope 64-bit atomic loads (never a stale cache line), results are
+// stored plainly and published by a system-scope release before `done`.
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(kThreads) void predict_persistent_kernel(PersistCtl* __restrict__ ctl,
+                                                                      const float* __restrict__ X, int d, int cap,
+                                                                      const float* __restrict__ a,
+                                                                      const float* __restrict__ c, float bias,
+                                                                      float* __restrict__ prob,
+                                                                      float* __restrict__ logit,
+                                                                      uint64_t idle_ticks, uint64_t life_ticks) {
+  __shared__ uint32_t s_cmd, s_n, s_seq;
+  const int tid = threadIdx.x, lane = lane_id();
+  const int c0 = (lane & 7) * 4, rsub = lane >> 3;
+  float al[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) al[j] = (c0 + j < d) ? a[c0 + j] : 0.0f;
+  (void)c;
+  uint32_t last = 0, served = 0;
+  uint64_t t_start = 0, t_work = 0;
+  if (tid == 0) {
+    last = ld_sys(&ctl->done);
+    t_start = t_work = wall_clock64();
+    st_sys(&ctl->served, 0u);
+    st_sys(&ctl->state, kPersistRunning);
+  }
+  for (;;) {
+    if (tid == 0) {
+      uint32_t cmd = 0, db = 0;
+      for (;;) {  // bounded: stop flag, idle timeout, lifetime
+        db = ld_sys(&ctl->doorbell);
+        if (db != last) { cmd = 1; break; }
+        if (ld_sys(&ctl->stop) != 0u) break;
+        const uint64_t now = wall_clock64();
+        if (now - t_work > idle_ticks || now - t_start > life_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      s_cmd = cmd;
+      s_seq = db;
+      s_n = cmd == 1 ? min(ld_sys(&ctl->n), (uint32_t)cap) : 0u;
+    }
+    __syncthreads();
+    if (s_cmd != 1) break;
+    const int n = (int)s_n;
+    // 8 lanes per row, 32 rows per block pass
+    for (int r0 = (tid >> 3); r0 < n; r0 += kThreads / 8) {
+      float x[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      const float* p = X + (int64_t)r0 * d + c0;
+      if (c0 + 4 <= d) {
+        const uint64_t u0 = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t u1 = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p + 2), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        x[0] = __uint_as_float((uint32_t)u0); x[1] = __uint_as_float((uint32_t)(u0 >> 32));
+        x[2] = __uint_as_float((uint32_t)u1); x[3] = __uint_as_float((uint32_t)(u1 >> 32));
+      } else if (c0 + 2 <= d) {
+        const uint64_t u0 = __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_SYSTEM);
+        x[0] = __uint_as_float((uint32_t)u0); x[1] = __uint_as_float((uint32_t)(u0 >> 32));
+        if (c0 + 2 < d)
+          x[2] = __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p + 2), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_SYSTEM));
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c0 + j < d)
+            x[j] = __uint_as_float(__hip_atomic_load(reinterpret_cast<const uint32_t*>(p + j), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_SYSTEM));
+      }
+      float z = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) z = fmaf(al[j], x[j], z);
+      z = group_sum<8>(z) + bias;
+      if ((lane & 7) == 0) {
+        logit[r0] = z;
+        prob[r0] = fast_sigmoid(z);
+      }
+    }
+    (void)rsub;
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) {
+      last = s_seq;
+      ++served;
+      st_sys(&ctl->served, served);
+      st_sys(&ctl->done, last);
+      t_work = wall_clock64();
+    }
+  }
+  if (tid == 0) st_sys(&ctl->state, kPersistExited);
+}
+
 }  // namespace
 
 void launch_predict_bf16(const uint16_t* X, int64_t n, const float* w, float* prob, float* logit,
@@ -248,6 +347,15 @@ void launch_predict_raw64(const float* X, int64_t n, int ld, int d, const float*
     predict_shap_kernel<1, 1, double><<<capped_grid(units, per_block, cap1), kThreads, 0, stream>>>(
         X, n, ld, d, 0, a, a, bias, prob, logit, nullptr, 0);
   check_launch("predict_raw64");
+}
+
+void launch_predict_persistent(PersistCtl* ctl, const float* X, int d, int cap, const float* a, const float* c,
+                               float bias, float* prob, float* logit, uint64_t idle_ticks, uint64_t life_ticks,
+                               hipStream_t stream) {
+  if (d < 1 || d > kCols || cap < 1) throw std::runtime_error("predict_persistent: bad shape");
+  predict_persistent_kernel<<<1, kThreads, 0, stream>>>(ctl, X, d, cap, a, c, bias, prob, logit, idle_ticks,
+                                                        life_ticks);
+  check_launch("predict_persistent");
 }
 
 }  // namespace fdx

@@ -120,6 +120,8 @@ class _KernelTimer:
 
 
 ZERO_COPY_ROWS = int(os.environ.get("FDX_ZERO_COPY_ROWS", "256"))
+# Batches up to this many rows go to the owner's persistent kernel (mailbox, no launch); 0 = off
+PERSIST_ROWS = int(os.environ.get("FDX_OWNER_PERSIST_ROWS", "256"))
 H2H_CHUNK_ROWS = 131072  # host-to-host batch scoring: rows per H2D / kernel / D2H pipeline stage
 CALIBRATION_SIZES = (1, 4, 16, 64, 256, 1024, 4096, 16384, 65536)
 
@@ -474,9 +476,14 @@ class InferenceEngine(_EngineBase):
         P.native().event_sync(self._oevents[handle[1]])
         return handle[2]
 
-    def start_native_owner(self, ring, cap: int, window_us: float, pipe_rows: int = 8) -> int:
+    def start_native_owner(self, ring, cap: int, window_us: float, pipe_rows: int = 8,
+                           persist_rows: int = PERSIST_ROWS, idle_ms: float = 200.0, life_ms: float = 10000.0) -> int:
         """Start the C++ owner loop on this engine's folded weights (GPU only): two device-mapped
-        pinned input buffers (owner_input) and two device-mapped pinned output buffers."""
+        pinned input buffers (owner_input) and two device-mapped pinned output buffers.
+        ``persist_rows`` > 0: batches of up to that many rows (predict) go to a persistent
+        one-workgroup kernel through a mailbox in coherent host memory -- no launch and no event
+        per batch; it exits after ``idle_ms`` without requests or ``life_ms`` in total and is
+        relaunched on demand (csrc/kernels/predict.hip predict_persistent_kernel)."""
         m = P.native()
         self.owner_input(cap)
         if not all(self._owner_map):
@@ -490,7 +497,12 @@ class InferenceEngine(_EngineBase):
         return m.owner_start(ring.base_address, ring.total_bytes, P.ptr(self._a), P.ptr(self._c), float(self.bias),
                              self.d, int(cap), float(window_us), int(pipe_rows), self._ostream.cuda_stream,
                              self._owner_in[0].data_ptr(), self._owner_in[1].data_ptr(), self._owner_map[0],
-                             self._owner_map[1], self._nout[0].data_ptr(), self._nout[1].data_ptr(), omap[0], omap[1])
+                             self._owner_map[1], self._nout[0].data_ptr(), self._nout[1].data_ptr(), omap[0], omap[1],
+                             int(persist_rows), float(idle_ms), float(life_ms))
+
+    def native_owner_stats(self, handle) -> dict:
+        b, launches, on = P.native().owner_persistent_stats(handle)
+        return {"persistent": bool(on), "persistent_batches": int(b), "persistent_launches": int(launches)}
 
     def stop_native_owner(self, handle) -> int:
         return int(P.native().owner_stop(handle))

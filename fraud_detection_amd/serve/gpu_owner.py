@@ -45,7 +45,8 @@ class GpuOwner:
     """Collector thread: ring -> pinned batch -> one launch -> results back to the slots."""
 
     def __init__(self, engine, ring_path: str = "", max_batch: int = 8192, window_us: float = 0.0,
-                 nslots: int = DEFAULT_SLOTS, slot_rows: int = DEFAULT_SLOT_ROWS, metrics=None):
+                 nslots: int = DEFAULT_SLOTS, slot_rows: int = DEFAULT_SLOT_ROWS, metrics=None,
+                 persist_rows: int | None = None, persist_idle_ms: float | None = None):
         R = _ring_mod()
         self.engine = engine
         self.max_batch = int(max_batch)
@@ -60,6 +61,13 @@ class GpuOwner:
         self._th = threading.Thread(target=self._loop, name="fdx-gpu-owner", daemon=True)
         self._native = None
         self.native = _native_capable(engine) and os.environ.get("FDX_OWNER_LOOP", "native") == "native"
+        # native loop: small predict batches through the persistent mailbox kernel (None: engine default)
+        self.persist_rows = persist_rows
+        self.persist_idle_ms = persist_idle_ms
+
+    def native_stats(self) -> dict:
+        """Persistent-kernel counters of the native loop ({} for the Python loop)."""
+        return self.engine.native_owner_stats(self._native) if self._native is not None else {}
 
     @property
     def batches(self) -> int:
@@ -73,7 +81,10 @@ class GpuOwner:
         if self.native:
             # the whole serving loop in C++ (csrc/bindings.cpp NativeOwner): ring -> mapped pinned
             # batch -> fused kernel -> mapped pinned results -> ring, no Python and no GIL per batch
-            self._native = self.engine.start_native_owner(self.ring, self.max_batch, self.window_us)
+            kw = {} if self.persist_rows is None else {"persist_rows": int(self.persist_rows)}
+            if self.persist_idle_ms is not None:
+                kw["idle_ms"] = float(self.persist_idle_ms)
+            self._native = self.engine.start_native_owner(self.ring, self.max_batch, self.window_us, **kw)
         else:
             self._th.start()
         self.ring.owner_state = _ring_mod().OWNER_READY

@@ -204,3 +204,39 @@ def test_gpu_owner_in_process_batches(dev, loop, monkeypatch):
         assert owner.batches < 600 and owner.rows >= 1300
     finally:
         owner.stop()
+
+
+@pytest.mark.gpu
+def test_native_owner_persistent_kernel(dev):
+    """Small predict batches through the owner's persistent mailbox kernel: the same bits as the
+    launch path, explain still served (launch path from the same staging), and the kernel is
+    relaunched after its idle timeout."""
+    from fraud_detection_amd.serve.gpu_owner import Dispatcher, GpuOwner, RingClient
+
+    eng = _engine("cuda")
+    rows = kaggle_like_rows(400, seed=14)
+    got = {}
+    for persist in (0, 256):
+        owner = GpuOwner(eng, "", persist_rows=persist, persist_idle_ms=30.0).start()
+        try:
+            assert owner.native
+            disp = Dispatcher(eng, RingClient(owner.ring), host_max_rows=0)
+            p = np.array([disp.predict_proba(rows[i:i + 1])[0][0] for i in range(200)])
+            with cf.ThreadPoolExecutor(16) as ex:  # concurrent producers: multi-row batches
+                pc = np.array(list(ex.map(lambda i: disp.predict_proba(rows[i:i + 1])[0][0], range(200, 400))))
+            time.sleep(0.1)  # > idle timeout: the persistent kernel exits ...
+            p2, _ = disp.predict_proba(rows[:5])  # ... and is relaunched for this one
+            _, _, phi = RingClient(owner.ring).predict_explain(rows[:40])
+            got[persist] = (p, pc, p2, phi)
+            st = owner.native_stats()
+            if persist:
+                assert st["persistent"] and st["persistent_batches"] >= 200, st
+                assert st["persistent_launches"] >= 2, st
+            else:
+                assert not st["persistent"]
+        finally:
+            owner.stop()
+    for a, b in zip(got[0], got[256]):
+        assert np.array_equal(a, b)
+    rp, _ = _engine().predict_proba(rows)
+    np.testing.assert_allclose(got[256][0], rp[:200], atol=2e-6)
