@@ -186,7 +186,9 @@ def test_gpu_owner_in_process_batches(dev, loop, monkeypatch):
     monkeypatch.setenv("FDX_OWNER_LOOP", loop)
     eng = _engine("cuda")
     assert eng.calibration.get("source") in ("measured", "FDX_HOST_MAX_ROWS")
-    owner = GpuOwner(eng, "").start()
+    # the launch path's batching (the persistent mailbox path answers single rows too fast to
+    # batch them: test_native_owner_persistent_kernel)
+    owner = GpuOwner(eng, "", persist_rows=0).start()
     try:
         disp = Dispatcher(eng, RingClient(owner.ring), host_max_rows=0)
         rows = kaggle_like_rows(600, seed=12)
