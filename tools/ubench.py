@@ -133,6 +133,10 @@ def main():
     sc = torch.randn(2_000_000, device=dev)
     yl = (torch.rand(2_000_000, device=dev) < 0.002).to(torch.uint8)
     case("roc_auc_2M", lambda: M.roc_auc(sc, yl), 2_000_000 * 5)
+    # exact AUC, large-P path (device radix sort): 20M scores at 50 % positives
+    sc20 = torch.randn(20_000_000, device=dev)
+    yl20 = (torch.rand(20_000_000, device=dev) < 0.5).to(torch.uint8)
+    case("roc_auc_20M_50pct", lambda: M.roc_auc(sc20, yl20), 20_000_000 * 5)
     out = {"device": info, "rows": n, "results": results, "pass_blocks": ws.nblocks, "pass_blocks_fp8": ws.nblocks_fp8}
     if a.json:
         with open(a.json, "w") as f:
