@@ -481,6 +481,26 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
                             hess, sub, P<float>(partial), nblocks, S(s));
   });
+  // the same pass over stored rows [0, n_real) + virtual SMOTE rows [n_real, re) (launchers.h SmoteView)
+  m.def("logreg_pass_virtual", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
+                                  int nblocks, u s, u parents, u nbr, int64_t n_real, int64_t q_offset,
+                                  int64_t s_off, int mq, int k, uint64_t seed, uint64_t counter_base, float label) {
+    fdx::SmoteView v;
+    v.parents = P<const uint16_t>(parents);
+    v.nbr = P<const int>(nbr);
+    v.n_real = n_real;
+    v.q_offset = q_offset;
+    v.s_off = s_off;
+    v.mq = mq;
+    v.k = k;
+    v.key0 = (uint32_t)seed;
+    v.key1 = (uint32_t)(seed >> 32);
+    v.cb0 = (uint32_t)counter_base;
+    v.cb1 = (uint32_t)(counter_base >> 32);
+    v.label = label;
+    fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
+                            hess, sub, P<float>(partial), nblocks, S(s), &v);
+  });
   m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
                               u partial, int nblocks, u s) {
     fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),

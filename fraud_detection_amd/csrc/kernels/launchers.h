@@ -106,9 +106,23 @@ void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, 
 // ---- logreg.hip ----
 constexpr int kLRPartStride = 1088;  // [0,32) grad, 32 loss, 33 wsum, [64,1088) Hessian 32x32
 int logreg_pass_blocks(int fmt = 0);
+// Virtual SMOTE rows (bf16 passes): training rows at absolute index >= n_real are never stored.
+// The pass regenerates each one from its Philox draw exactly as smote_generate<bf16, bf16
+// parents> writes it (same draw, same gathers, same fmaf + bf16 rounding), so a fit over virtual
+// rows is bitwise the fit over materialised ones.  parents == nullptr: every row is stored.
+struct SmoteView {
+  const uint16_t* parents = nullptr;  // bf16 [m, 32] output-space parents (smote_parents)
+  const int* nbr = nullptr;           // int32 [mq, k] neighbour rows (indices into parents)
+  int64_t n_real = 0;                 // first virtual row (absolute row index)
+  int64_t q_offset = 0;               // parent row of query 0
+  int64_t s_off = 0;                  // global sample index of virtual row n_real (multiple of 128)
+  int mq = 0, k = 1;
+  uint32_t key0 = 0, key1 = 0, cb0 = 0, cb1 = 0;
+  float label = 1.0f;
+};
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
-                        float* partial, int nblocks, hipStream_t stream);
+                        float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr);
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
                             float x_scale, float* partial, int nblocks, hipStream_t stream);

@@ -41,11 +41,22 @@ __device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
   x[4] = bf16lo(v.z); x[5] = bf16hi(v.z); x[6] = bf16lo(v.w); x[7] = bf16hi(v.w);
 }
 
-template <bool HESS>  // bf16 rows (64 B); fp8 rows: logreg_pass_fp8w_kernel
+// VIRT: rows at absolute index >= sv.n_real are virtual SMOTE rows (launchers.h SmoteView),
+// regenerated in the pass instead of streamed from HBM.  At the bench shape half of the 16M
+// training rows are synthetic (8M real rows after the split, 0.17% fraud -> balanced), and their
+// 13.6k parents (870 KB) plus neighbour lists stay L2-resident: a virtual row costs two 16 B L2
+// gathers per lane and ~60 VALU ops instead of 64 B of HBM, and the 512 MB SMOTE write disappears.
+// Per-row arithmetic is smote_generate_kernel<0, *, true>'s (smote.hip): one Philox4x32-10 call
+// serves a pair of samples (counter 64 m + L -> samples 128 m + L and 128 m + 64 + L), the
+// interpolation is fmaf(lambda, b - a, a) rounded to bf16, col 30 = 1, col 31 = label.
+// Three-stage software pipeline per wave: the draw (Philox + neighbour-index load) of tile t+2
+// and the parent gathers of tile t+1 are in flight while tile t computes, so the dependent
+// draw -> nbr -> parent chain costs no exposed latency beyond the plain double buffer.
+template <bool HESS, bool VIRT = false>  // bf16 rows (64 B); fp8 rows: logreg_pass_fp8w_kernel
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
-    float* __restrict__ partial) {
+    float* __restrict__ partial, SmoteView sv) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][35];
@@ -70,25 +81,93 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   // grid): a uniform 1/row_sub subsample used by the early progressive-Newton iterations.
   const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
-  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
-  auto load_tile = [&](int64_t b, uint4 (&v)[4]) {
-    const uint4* X = reinterpret_cast<const uint4*>(Xv);
+  const uint4* X = reinterpret_cast<const uint4*>(Xv);
+  // virtual-row draw parameters (smote.hip launch_smote_generate)
+  const uint4* Pb = reinterpret_cast<const uint4*>(sv.parents);
+  const uint32_t vrange = (uint32_t)sv.mq * (uint32_t)sv.k;
+  const float vinv_k = 1.0f / (float)sv.k;
+  const bool vsmall = vrange < (1u << 22);
+  // a tile holds a virtual row (wave-uniform)
+  auto is_virt = [&](int64_t b) { return VIRT && row_begin + b + 64 > sv.n_real; };
+  // Stage 1 (tile t+2): this lane's draw for row b + lane -- Philox, then the neighbour-index
+  // load, left in flight (its first use is stage 2 one iteration later).  Every lane draws: a
+  // draw is in range whatever the counter, so real lanes of a boundary tile need no branch.
+  auto draw = [&](int64_t b) __attribute__((always_inline)) -> uint2 {
+    const int64_t gs = sv.s_off + (row_begin + b + lane - sv.n_real);
+    const int64_t c = ((gs >> 7) << 6) + (gs & 63);
+    const Philox4 r = philox4x32_10((uint32_t)c, (uint32_t)(c >> 32), sv.cb0, sv.cb1, sv.key0, sv.key1);
+    const bool hi = ((gs >> 6) & 1) != 0;
+    return smote_pack_draw(hi ? r.z : r.x, hi ? r.w : r.y, vrange, (uint32_t)sv.k, vinv_k, vsmall, sv.nbr);
+  };
+  // Stage 2 (tile t+1): the row loads -- stored rows from HBM into A; for a virtual row the
+  // parent (A) and neighbour (B) 16 B slices from L2 plus lambda.
+  uint4 A[4], B[4];
+  float lam[4];
+  auto gather = [&](int64_t b, uint2 dd) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = b + 16 * u + rr;
-      v[u] = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
+      if (!is_virt(b)) {
+        A[u] = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
+      } else {  // branch-free: a stored row of a boundary tile loads into A and ignores B
+        const int src = 16 * u + rr;
+        const uint32_t dx = __shfl(dd.x, src, kWave), dy = __shfl(dd.y, src, kWave);
+        const bool stored = row_begin + row < sv.n_real;
+        const uint4* pa = stored ? X + (row_begin + row) * 4 + q
+                                 : Pb + (sv.q_offset + (int64_t)(dx & 0xffffffu)) * 4 + q;
+        A[u] = *pa;
+        B[u] = Pb[(int64_t)(dy & 0xffffffu) * 4 + q];
+        lam[u] = smote_lambda(dx, dy);
+      }
+    }
+  };
+  // Stage 3 (tile t): the rows this tile computes on.  Virtual rows: smote_generate's bf16 output.
+  auto finish = [&](int64_t b, uint4 (&v)[4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (!is_virt(b)) {
+        v[u] = A[u];
+      } else {
+        const int64_t row = b + 16 * u + rr;
+        float av[8], bv[8], o[8];
+        unpack8(A[u], av);
+        unpack8(B[u], bv);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaf(lam[u], bv[j] - av[j], av[j]);
+        if (q == 3) {
+          o[6] = 1.0f;      // col 30: intercept column
+          o[7] = sv.label;  // col 31: label
+        }
+        uint4 s;
+        s.x = pack_bf16x2(o[0], o[1]);
+        s.y = pack_bf16x2(o[2], o[3]);
+        s.z = pack_bf16x2(o[4], o[5]);
+        s.w = pack_bf16x2(o[6], o[7]);
+        const bool stored = row_begin + row < sv.n_real;
+        v[u] = stored ? A[u] : (row < n ? s : make_uint4(0, 0, 0, 0));
+      }
     }
   };
   int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
-  uint4 cur[4];
-  if (base < n) load_tile(base, cur);
+  uint2 dnext = make_uint2(0u, 0u);
+  if (base < n) {
+    if (is_virt(base)) dnext = draw(base);
+    gather(base, dnext);
+    if (base + step < n && is_virt(base + step)) dnext = draw(base + step);
+  }
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
   // is unchanged; H only shapes the step (sub-sampled Newton).
   int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
   for (; base < n; base += step) {
-    uint4 nxt[4];
-    if (base + step < n) load_tile(base + step, nxt);
+    // register pipeline: tile t's rows out of the stage registers, then the loads of tile t+1
+    // and the draw of tile t+2 go in flight while tile t computes
+    uint4 cur[4];
+    finish(base, cur);
+    if (base + step < n) {
+      gather(base + step, dnext);
+      if (base + 2 * step < n && is_virt(base + 2 * step)) dnext = draw(base + 2 * step);
+    }
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
@@ -150,8 +229,6 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
     wacc += swq;
     if (do_h) whacc += swq;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
   }
 
   // ---- block reduction (fixed order) ----
@@ -791,16 +868,31 @@ int logreg_pass_blocks(int fmt) {
 
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
-                        float* partial, int nblocks, hipStream_t stream) {
+                        float* partial, int nblocks, hipStream_t stream, const SmoteView* sv) {
   // hessian: 0 = gradient/loss only; h >= 1 = also the Hessian, from every h-th row tile.
   // row_sub >= 1: visit a uniform 1/row_sub of the 64-row tiles (progressive Newton).
+  // sv (nullable): rows >= sv->n_real are virtual SMOTE rows.
   if (row_sub < 1) row_sub = 1;
-  if (hessian > 0)
-    logreg_pass_kernel<true><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, hessian, row_sub, partial);
-  else
-    logreg_pass_kernel<false><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, 1, row_sub, partial);
+  const bool virt = sv != nullptr && sv->parents != nullptr && row_end > sv->n_real;
+  SmoteView v;
+  if (virt) {
+    v = *sv;
+    if (v.nbr == nullptr || v.mq <= 0 || v.k <= 0 || v.n_real < 0 || v.s_off < 0 || (v.s_off & 127) != 0 ||
+        (uint64_t)v.mq * (uint64_t)v.k >= (1ull << 32))
+      throw std::runtime_error("logreg_pass: invalid virtual SMOTE view");
+  }
+  const int hs = hessian > 0 ? hessian : 1;
+#define FDX_LRP(H, V)                                                                            \
+  logreg_pass_kernel<H, V><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, hs, \
+                                                             row_sub, partial, v)
+  if (hessian > 0) {
+    if (virt) FDX_LRP(true, true);
+    else FDX_LRP(true, false);
+  } else {
+    if (virt) FDX_LRP(false, true);
+    else FDX_LRP(false, false);
+  }
+#undef FDX_LRP
   check_launch("logreg_pass");
 }
 

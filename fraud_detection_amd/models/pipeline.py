@@ -6,7 +6,8 @@ Here every numeric step is a HIP kernel on the rank's row shard:
     K1 scaler stats (+ all-reduce C1) -> K2 standardize/pad/cast into the training buffer
     -> stable minority compaction -> K2 gather (fp32 minority rows) -> all-gather C3
     -> K8 MFMA k-NN (local queries vs global minority) -> K9 Philox SMOTE rows written in place
-       from bf16 parents in the training rows' space
+       from bf16 parents in the training rows' space -- or, for the bf16 Newton fit, regenerated
+       inside every K4 pass (TrainConfig.virtual_smote)
     -> K4 Newton (all-reduce C5 per iteration) or momentum SGD (all-reduce C4 per minibatch).
 Evaluation: folded-scaler predict on raw fp32 test rows (K5) -> exact AUC (K10) + confusion.
 """
@@ -64,6 +65,11 @@ class TrainConfig:
     # of the ranks' synthetic rows equals the one-process SMOTE output bit for bit; "shard" = each
     # rank oversamples its own minority rows (per-partition SMOTE: constant work per rank)
     smote_scope: str = "global"
+    # Newton on bf16 device rows: the SMOTE rows are never stored -- every logistic pass
+    # regenerates them from their Philox draws out of the L2-resident minority parents
+    # (ops/logreg.VirtualSmote), bitwise the rows smote_generate would write.  At the bench shape
+    # half the training rows are synthetic: no 512 MB SMOTE write and half the bytes per pass.
+    virtual_smote: bool = True
 
 
 @dataclass
@@ -132,6 +138,7 @@ class DevicePipeline:
         self._bufs, self._wss, self._pending = [None, None], [None, None], [None, None]
         self._bi = self._cur = 0
         self._full_pred = None  # (signature, full-data iterations of the last settled fit)
+        self._virtual = None    # VirtualSmote of the latest fit (None: its SMOTE rows are stored)
         self._defer_now = False
 
     def _world(self):
@@ -180,6 +187,14 @@ class DevicePipeline:
                 self._bufs[b ^ 1] = torch.empty((n_rows, NCOLS), device=device, dtype=dt)
         self._buf, self._cur, self._defer_now = buf, b, double
         return buf[:n_rows]
+
+    def training_rows(self, res: "PipelineResult") -> torch.Tensor:
+        """The latest fit's post-SMOTE training rows as one stored tensor (diagnostic tools): a
+        fit over virtual SMOTE rows has them materialised into the buffer's tail first."""
+        rows = self._buf[: res.n_train_rows]
+        if self._virtual is not None:
+            self._virtual.materialize(rows[res.n_rows:])
+        return rows
 
     def fit_host(self, X: torch.Tensor, y: torch.Tensor, device=None, budget: int | None = None,
                  profile: bool = False) -> PipelineResult:
@@ -305,6 +320,8 @@ class DevicePipeline:
         if n + n_new > rows_cap.shape[0]:  # global_smote_slices guarantees this never fires
             raise RuntimeError(f"SMOTE slice of {n_new} rows exceeds the training buffer ({rows_cap.shape[0]} rows)")
         rows = rows_cap[: n + n_new]
+        virt = None
+        virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage == "bf16" and dev.type == "cuda")
         tm.mark("scale_cast")
         # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a
         # quota; shard scope has no collective in this block, so only a rank with its own quota enters
@@ -338,9 +355,13 @@ class DevicePipeline:
             if n_new > 0:
                 if parents is None:
                     parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
-                knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
-                                       counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,
-                                       sample_offset=s_off)
+                if virt_ok:  # regenerated inside every Newton pass, never written
+                    virt = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, q_offset=q_off, sample_offset=s_off,
+                                               seed=cfg.seed, counter_base=0 if glob else rank)
+                else:
+                    knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
+                                           counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,
+                                           sample_offset=s_off)
             tm.mark("smote_generate")
         # ---- class weights ---------------------------------------------------------------
         class_w = (1.0, 1.0)
@@ -367,10 +388,11 @@ class DevicePipeline:
             sig = (n_global, n_sched, len(ranks), cfg.C, cfg.tol, cfg.max_iter, tuple(class_w),
                    str(cfg.hess_stride), fused, cfg.storage)
             pred = self._full_pred[1] if (defer and self._full_pred and self._full_pred[0] == sig) else None
-            fit = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
+            fit = lr_ops.newton_fit(rows_cap[:n] if virt is not None else rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, class_w=class_w, d=d, w0=w0,
                                     fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
                                     check_every=cfg.check_every, workspace=self._ws, hess_stride=cfg.hess_stride,
-                                    n_sched=n_sched, affine=stats.aff if fused else None, full_iters=pred)
+                                    n_sched=n_sched, affine=stats.aff if fused else None, full_iters=pred,
+                                    virtual=virt)
             if defer and isinstance(fit, lr_ops.PendingFit):
                 fit._fdx_sig = sig
                 self._pending[b] = fit
@@ -385,6 +407,7 @@ class DevicePipeline:
         else:
             raise ValueError(f"unknown solver {cfg.solver!r}")
         tm.mark("fit")
+        self._virtual = virt
         return PipelineResult(scaler=stats, fit=fit, n_rows=n, n_train_rows=n + n_new, n_minority=n_min,
                               n_synthetic=n_new, timings=dict(tm.t))
 

@@ -41,6 +41,48 @@ class FitInfo:
     history: list = field(default_factory=list)
 
 
+@dataclass
+class VirtualSmote:
+    """SMOTE rows a bf16 Newton fit reads without their ever being stored (launchers.h SmoteView).
+
+    The fit's rows are ``rows`` (the stored real rows, [n_real, 32]) followed by ``n_new`` virtual
+    rows: sample s is regenerated inside every logistic pass exactly as ``knn.smote_generate``
+    would have written it into ``rows_cap[n_real + s]`` with the same arguments (bf16 output-space
+    parents, same Philox draws, same fmaf + bf16 rounding), so the fit is bitwise the fit over
+    the materialised rows.  The parents and neighbour lists are small (the minority class) and
+    stay L2-resident; the pass streams only the real rows from HBM."""
+    parents: torch.Tensor     # bf16 [m, 32] (knn.smote_parents / knn_topk(parents=...))
+    nbr: torch.Tensor         # int32 [mq, k] neighbour rows (indices into parents)
+    n_new: int
+    q_offset: int = 0
+    sample_offset: int = 0    # multiple of 128 (DP ranks: one global draw sequence)
+    seed: int = 42
+    counter_base: int = 0
+    label: float = 1.0
+
+    def check(self, rows: torch.Tensor):
+        if storage_kind(rows) != "bf16" or not rows.is_cuda:
+            raise ValueError("virtual SMOTE rows need bf16 device rows")
+        p, nb = self.parents, self.nbr
+        if p.dtype != torch.bfloat16 or p.dim() != 2 or p.shape[1] != NCOLS or p.device != rows.device:
+            raise ValueError("parents must be bf16 [m, 32] on the rows' device")
+        if nb.dtype != torch.int32 or nb.dim() != 2 or nb.device != rows.device or not nb.is_contiguous():
+            raise ValueError("nbr must be a contiguous int32 [mq, k] tensor on the rows' device")
+        mq, k = nb.shape
+        if self.n_new < 0 or self.sample_offset < 0 or self.sample_offset % 128:
+            raise ValueError("n_new >= 0 and sample_offset a non-negative multiple of 128")
+        if self.n_new and (mq < 1 or k < 1 or self.q_offset < 0 or self.q_offset + mq > p.shape[0]):
+            raise ValueError("query rows out of range of the parents")
+        ref.smote_check_ranges(p.shape[0], mq, k)
+
+    def materialize(self, out: torch.Tensor) -> torch.Tensor:
+        """The stored equivalent: the same rows written by smote_generate (tests, CPU paths)."""
+        from . import knn as knn_ops
+        return knn_ops.smote_generate(self.parents, self.nbr, self.q_offset, self.n_new, out, seed=self.seed,
+                                      counter_base=self.counter_base, label=self.label,
+                                      sample_offset=self.sample_offset)
+
+
 _FIT_FIELDS = ("w", "n_iter", "n_newton_steps", "converged", "objective", "grad_max", "history")
 
 
@@ -217,12 +259,21 @@ def progressive_schedule(n_rows: int) -> list:
 
 
 def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True,
-          sub: int = 1):
+          sub: int = 1, virtual: VirtualSmote | None = None):
     """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact).
-    sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up)."""
+    sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up).
+    virtual: rows >= rows.shape[0] are virtual SMOTE rows (end may reach n_real + n_new)."""
     dptr = ptr(ws.done) if done else 0
     h = int(hessian)
-    if storage_kind(rows) == "bf16":
+    if virtual is not None and virtual.n_new > 0:
+        v = virtual
+        mq, k = v.nbr.shape
+        m.logreg_pass_virtual(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
+                              ptr(ws.partial), ws.nblocks, s, ptr(v.parents), ptr(v.nbr), int(rows.shape[0]),
+                              int(v.q_offset), int(v.sample_offset), int(mq), int(k),
+                              int(v.seed) & (2**64 - 1), int(v.counter_base) & (2**64 - 1), float(v.label))
+        nb = ws.nblocks
+    elif storage_kind(rows) == "bf16":
         nb = ws.nblocks
         m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
                       nb, s)
@@ -235,8 +286,9 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
 
 
 def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian: bool = True,
-                fp8_scale: float = DEFAULT_FP8_SCALE):
-    """One reduced pass: (grad[32], loss, wsum, H[32,32]) as float64 numpy (test/diagnostic API)."""
+                fp8_scale: float = DEFAULT_FP8_SCALE, virtual: VirtualSmote | None = None):
+    """One reduced pass: (grad[32], loss, wsum, H[32,32]) as float64 numpy (test/diagnostic API).
+    ``virtual``: the pass also covers virtual.n_new SMOTE rows after ``rows``."""
     check_rows(rows)
     if not rows.is_cuda:
         R = ref.rows_to_f32(rows, fp8_scale).numpy()
@@ -244,7 +296,11 @@ def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian
     m = native()
     ws = LRWorkspace(rows.device)
     ws.reset(w.cpu().double().numpy(), class_w)
-    _pass(m, rows, ws, hessian, 0, rows.shape[0], fp8_scale, stream_of(rows), done=False)
+    n = rows.shape[0]
+    if virtual is not None:
+        virtual.check(rows)
+        n += virtual.n_new
+    _pass(m, rows, ws, hessian, 0, n, fp8_scale, stream_of(rows), done=False, virtual=virtual)
     red = ws.red.cpu().numpy()
     H = red[64:].reshape(32, 32) if hessian else None
     return red[:32].copy(), float(red[32]), float(red[33]), H
@@ -279,7 +335,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                sync: bool = True, hess_stride: int | str = "auto", progressive="auto",
                hess_refresh: int | str = "auto", n_sched: int | None = None,
                local_warmup: bool = True, affine: torch.Tensor | None = None,
-               lookahead: int | None = None, full_iters: int | None = None) -> FitInfo:
+               lookahead: int | None = None, full_iters: int | None = None,
+               virtual: VirtualSmote | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -296,9 +353,21 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     same iterations run either way; the host-checked loop's trailing no-op iterations and its
     wait at the end of the fit disappear.  Rows and workspace must stay untouched until then.
     Under DP every rank must pass the same ``full_iters`` and verify at the same point of its
-    program (the iterations, and a continuation, carry the gradient all-reduces)."""
+    program (the iterations, and a continuation, carry the gradient all-reduces).
+    ``virtual``: the fit's rows are ``rows`` followed by virtual.n_new SMOTE rows that are
+    regenerated in every pass instead of stored (VirtualSmote; bf16 device rows).  Its tensors,
+    like the rows, must stay alive until a deferred fit is verified."""
     check_rows(rows)
     w0 = _default_w0(w0)
+    if virtual is not None and virtual.n_new == 0:
+        virtual = None
+    if virtual is not None and not rows.is_cuda:  # host path: materialise (CPU tests)
+        full = torch.empty((rows.shape[0] + virtual.n_new, NCOLS), dtype=rows.dtype)
+        full[: rows.shape[0]] = rows
+        virtual.materialize(full[rows.shape[0]:])
+        rows, virtual = full, None
+    if virtual is not None:
+        virtual.check(rows)
     if not rows.is_cuda:
         if affine is not None:
             a = affine.cpu().double()
@@ -313,7 +382,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
     ws.reset(w0, class_w, aff)  # w0 is standardized-space; w32 gets it folded for shifted rows
-    n = rows.shape[0]
+    n = rows.shape[0] + (virtual.n_new if virtual is not None else 0)
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
     # The warm-up schedule sets the number of collectives, so every rank must derive the same one:
     # from ``n_sched`` (the smallest rank's row count, known to all ranks without a collective when
@@ -340,7 +409,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     for sub, iters in sched:
         hs_w = auto_warm_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
-            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub)
+            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual)
             if sync_warm:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
@@ -368,7 +437,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             # 8 vs 7 iterations, profiles/r1_s25)
             fresh = refresh <= 0 or full_it[0] % refresh == 0
             full_it[0] += 1
-            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s)
+            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual)
             if comm is not None and comm.world_size > 1:
                 # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
                 comm.all_reduce_(ws.red if fresh else ws.red[:GRAD_SLOTS])

@@ -39,7 +39,7 @@ def main():
     pipe = DevicePipeline(cfg, None)
     res = pipe.fit(X, y)
     torch.cuda.synchronize()
-    rows = pipe._buf[: res.n_train_rows]
+    rows = pipe.training_rows(res)
     aff = res.scaler.aff
     ws = L.LRWorkspace(dev)
     n = rows.shape[0]

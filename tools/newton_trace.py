@@ -34,7 +34,7 @@ def main():
     X, y = separable(n_train, seed=1000, device=dev)
     pipe = DevicePipeline(TrainConfig(seed=42))
     res = pipe.fit(X, y)
-    rows = pipe._buf[: res.n_train_rows]
+    rows = pipe.training_rows(res)
     n = rows.shape[0]
     m = native()
     s = stream_of(rows)
