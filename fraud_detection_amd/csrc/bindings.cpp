@@ -482,24 +482,34 @@ PYBIND11_MODULE(_fdx_native, m) {
                             hess, sub, P<float>(partial), nblocks, S(s));
   });
   // the same pass over stored rows [0, n_real) + virtual SMOTE rows [n_real, re) (launchers.h SmoteView)
+  // the same pass over the stored rows [0, n_real) plus virtual SMOTE samples (launchers.h
+  // SmoteView); x_scale > 0 selects the fp8 row pass
   m.def("logreg_pass_virtual", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
-                                  int nblocks, u s, u parents, u nbr, int64_t n_real, int64_t q_offset,
-                                  int64_t s_off, int mq, int k, uint64_t seed, uint64_t counter_base, float label) {
+                                  int nblocks, u s, u parents, u nbr, u lam, u off, int64_t n_real,
+                                  int64_t q_offset, int mq, int k, float x_scale) {
     fdx::SmoteView v;
     v.parents = P<const uint16_t>(parents);
     v.nbr = P<const int>(nbr);
+    v.lam = P<const uint16_t>(lam);
+    v.off = P<const int>(off);
     v.n_real = n_real;
     v.q_offset = q_offset;
-    v.s_off = s_off;
     v.mq = mq;
     v.k = k;
-    v.key0 = (uint32_t)seed;
-    v.key1 = (uint32_t)(seed >> 32);
-    v.cb0 = (uint32_t)counter_base;
-    v.cb1 = (uint32_t)(counter_base >> 32);
-    v.label = label;
-    fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
-                            hess, sub, P<float>(partial), nblocks, S(s), &v);
+    if (x_scale > 0.0f)
+      fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
+                                  P<const int>(done), hess, sub, x_scale, P<float>(partial), nblocks, S(s), &v);
+    else
+      fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw),
+                              P<const int>(done), hess, sub, P<float>(partial), nblocks, S(s), &v);
+  });
+  m.def("smote_bucket_bins", &fdx::smote_bucket_bins);
+  m.def("smote_bucket_blocks", &fdx::smote_bucket_blocks);
+  m.def("smote_bucket_max_picks", []() { return (uint64_t)fdx::kSmoteBucketMaxPicks; });
+  m.def("smote_bucket", [](int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
+                           uint64_t counter_base, u table, u rec, u off, u lam, u s) {
+    fdx::launch_smote_bucket(stage, mq, k, n_new, sample_offset, seed, counter_base, P<int>(table),
+                             P<uint32_t>(rec), P<int>(off), P<uint16_t>(lam), S(s));
   });
   m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
                               u partial, int nblocks, u s) {

@@ -106,26 +106,38 @@ void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, 
 // ---- logreg.hip ----
 constexpr int kLRPartStride = 1088;  // [0,32) grad, 32 loss, 33 wsum, [64,1088) Hessian 32x32
 int logreg_pass_blocks(int fmt = 0);
-// Virtual SMOTE rows (bf16 passes): training rows at absolute index >= n_real are never stored.
-// The pass regenerates each one from its Philox draw exactly as smote_generate<bf16, bf16
-// parents> writes it (same draw, same gathers, same fmaf + bf16 rounding), so a fit over virtual
-// rows is bitwise the fit over materialised ones.  parents == nullptr: every row is stored.
+// Virtual SMOTE rows: the fit's rows are the stored rows [0, n_real) followed by SMOTE samples
+// that are never written.  Sample s = a_i + lam (b_j - a_i) with i = pick / k, j = nbr[pick]; its
+// logit is (1 - lam) z(a_i) + lam z(b_j), so a pass needs per pick (i, j) only sums over the
+// pick's lambdas: smote_bucket (once per fit) groups the samples' lambdas by pick, and the pass
+// folds each pick's sums into gradient / loss / Hessian terms of its two parent rows.
 struct SmoteView {
   const uint16_t* parents = nullptr;  // bf16 [m, 32] output-space parents (smote_parents)
-  const int* nbr = nullptr;           // int32 [mq, k] neighbour rows (indices into parents)
-  int64_t n_real = 0;                 // first virtual row (absolute row index)
+  const int* nbr = nullptr;           // int32 [mq * k] neighbour rows (indices into parents)
+  const uint16_t* lam = nullptr;      // [n_new] lambda * 2^16 grouped by pick
+  const int* off = nullptr;           // [mq * k + 1] bucket offsets into lam
+  int64_t n_real = 0;                 // stored rows; the pass covers n_real + n_new rows
   int64_t q_offset = 0;               // parent row of query 0
-  int64_t s_off = 0;                  // global sample index of virtual row n_real (multiple of 128)
   int mq = 0, k = 1;
-  uint32_t key0 = 0, key1 = 0, cb0 = 0, cb1 = 0;
-  float label = 1.0f;
 };
+// Lambda buckets of SMOTE samples [sample_offset, sample_offset + n_new) of one global draw
+// sequence (smote.hip, two-level LDS counting sort).  table: int32 [bins * blocks]; stage 0 fills
+// table[bin * blocks + block] with counts, the caller scans it inclusively in place, stage 1
+// writes the coarse records rec (uint32 [n_new]), stage 2 writes off (int32 [mq k + 1]) and lam
+// (uint16 [n_new]).
+constexpr uint64_t kSmoteBucketMaxPicks = 1ull << 21;  // <= 16384 coarse bins of <= 128 picks
+int smote_bucket_bins(int64_t range, int64_t n_new);
+int smote_bucket_blocks();
+void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
+                         uint64_t counter_base, int* table, uint32_t* rec, int* off, uint16_t* lam,
+                         hipStream_t stream);
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr);
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
-                            float x_scale, float* partial, int nblocks, hipStream_t stream);
+                            float x_scale, float* partial, int nblocks, hipStream_t stream,
+                            const SmoteView* sv = nullptr);
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.

@@ -41,17 +41,128 @@ __device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
   x[4] = bf16lo(v.z); x[5] = bf16hi(v.z); x[6] = bf16lo(v.w); x[7] = bf16hi(v.w);
 }
 
-// VIRT: rows at absolute index >= sv.n_real are virtual SMOTE rows (launchers.h SmoteView),
-// regenerated in the pass instead of streamed from HBM.  At the bench shape half of the 16M
-// training rows are synthetic (8M real rows after the split, 0.17% fraud -> balanced), and their
-// 13.6k parents (870 KB) plus neighbour lists stay L2-resident: a virtual row costs two 16 B L2
-// gathers per lane and ~60 VALU ops instead of 64 B of HBM, and the 512 MB SMOTE write disappears.
-// Per-row arithmetic is smote_generate_kernel<0, *, true>'s (smote.hip): one Philox4x32-10 call
-// serves a pair of samples (counter 64 m + L -> samples 128 m + L and 128 m + 64 + L), the
-// interpolation is fmaf(lambda, b - a, a) rounded to bf16, col 30 = 1, col 31 = label.
-// Three-stage software pipeline per wave: the draw (Philox + neighbour-index load) of tile t+2
-// and the parent gathers of tile t+1 are in flight while tile t computes, so the dependent
-// draw -> nbr -> parent chain costs no exposed latency beyond the plain double buffer.
+// ---- virtual SMOTE rows (launchers.h SmoteView) -------------------------------------------------
+// A SMOTE sample is x = a + lam (b - a) with a = parent row q_offset + pick / k, b = parent row
+// nbr[pick] (bf16, the training rows' space) and lam on a 2^-16 grid, so z = w.x = za + lam (zb - za)
+// and, summed over the samples of one pick,
+//   gradient  sum r x       = (S_r - S_rl) a + S_rl b                 r = s (p - 1)
+//   Hessian   sum d x x^T   = [a b] M [a b]^T,  M = sum d [(1-lam)^2, lam(1-lam); lam(1-lam), lam^2]
+// with d = s p (1 - p).  M is PSD 2x2: M = L L^T gives two rank-1 terms u1 = l11 a + l21 b,
+// u2 = l22 b that go through the same LDS tile + MFMA as stored rows.  A pass therefore streams
+// the stored rows from HBM plus 2 bytes of lambda per sample (bucketed by pick once per fit,
+// smote.hip smote_bucket_kernel) and reads each pick's two parent rows (L2-resident) once --
+// instead of 64 B per stored SMOTE row plus their 512 MB write.  The synthetic rows enter at full
+// fp32 precision (no bf16 rounding of the interpolant).  Per-sample terms are summed in fixed
+// point (int64), so the bucket order the fill's atomics produce does not change a bit: fits stay
+// bitwise reproducible.
+constexpr float kSynQ = 16777216.0f;  // 2^24: r, r lam, d, d lam, d lam^2 (|v| <= s < 128)
+constexpr float kSynQL = 65536.0f;    // 2^16: per-sample loss (<= 80 s)
+
+template <int G>
+__device__ __forceinline__ long long group_sum_i64(long long v) {
+#pragma unroll
+  for (int o = 1; o < G; o <<= 1) {
+    const unsigned long long u = (unsigned long long)v;
+    const unsigned lo = (unsigned)__shfl_xor((int)(u & 0xffffffffu), o, kWave);
+    const unsigned hi = (unsigned)__shfl_xor((int)(u >> 32), o, kWave);
+    v += (long long)(((unsigned long long)hi << 32) | lo);
+  }
+  return v;
+}
+
+// One pick's terms for the LPR lanes that share it (lane q owns columns [C q, C q + C)).  wl: this
+// lane's weights in the kernel's row units; xs: the unit scale of feature columns (fp8 rows hold
+// features * x_scale); p < 0: an empty pick (the lanes still join the shuffles).
+template <int LPR, bool HESS>
+__device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q, const float* wl, float xs,
+                                           float sw1, float hrs, float* gc, float* u1, float* u2, float& loss,
+                                           float& wsum) {
+  constexpr int C = 32 / LPR;
+  const bool ok = p >= 0;
+  const int64_t pp = ok ? p : 0;
+  const int64_t ra = sv.q_offset + pp / sv.k, rb = sv.nbr[pp];
+  const uint4* Pb = reinterpret_cast<const uint4*>(sv.parents);
+  float xa[C], xb[C];
+#pragma unroll
+  for (int h = 0; h < C / 8; ++h) {
+    unpack8(Pb[ra * 4 + (C / 8) * q + h], xa + 8 * h);
+    unpack8(Pb[rb * 4 + (C / 8) * q + h], xb + 8 * h);
+  }
+  float za = 0.0f, zb = 0.0f;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int col = C * q + c;
+    const float cs = col == kLabelCol ? 0.0f : (col < kBiasCol ? xs : 1.0f);
+    xa[c] *= cs;
+    xb[c] *= cs;
+    za = fmaf(wl[c], xa[c], za);
+    zb = fmaf(wl[c], xb[c], zb);
+  }
+  za = group_sum<LPR>(za);
+  zb = group_sum<LPR>(zb);
+  const int o0 = ok ? sv.off[pp] : 0;
+  const int cnt = ok ? sv.off[pp + 1] - o0 : 0;
+  const float dz = zb - za;
+  long long sr = 0, srl = 0, sd = 0, sdl = 0, sdll = 0, sl = 0;
+  // kLamBatch lambdas per lane in flight per step (one load latency per step, not per sample)
+  constexpr int kLamBatch = 8;
+  for (int j0 = q; j0 < cnt; j0 += LPR * kLamBatch) {
+    uint16_t lv[kLamBatch];
+#pragma unroll
+    for (int u = 0; u < kLamBatch; ++u) {
+      const int j = j0 + u * LPR;
+      lv[u] = j < cnt ? sv.lam[o0 + j] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kLamBatch; ++u) {
+    if (j0 + u * LPR >= cnt) break;
+    const float lam = (float)lv[u] * (1.0f / 65536.0f);
+    const float z = fmaf(lam, dz, za);
+    const float zc = fminf(fmaxf(z, -80.0f), 80.0f);
+    const float eh = __expf(-0.5f * zc);
+    const float e2 = eh * eh;
+    const float pr = fast_rcp(1.0f + e2);
+    const float r = -sw1 * pr * e2;  // s (p - 1) without the cancellation
+    sr += __float2int_rn(r * kSynQ);
+    srl += __float2int_rn(r * lam * kSynQ);
+    if constexpr (HESS) {
+      const float d = sw1 * pr * pr * e2;  // s p (1 - p)
+      sd += __float2int_rn(d * kSynQ);
+      sdl += __float2int_rn(d * lam * kSynQ);
+      sdll += __float2int_rn(d * lam * lam * kSynQ);
+    }
+    sl += __float2int_rn(sw1 * (fmaxf(-z, 0.0f) + log1p_fast(__expf(-fabsf(z)))) * kSynQL);
+    }
+  }
+  sr = group_sum_i64<LPR>(sr);
+  srl = group_sum_i64<LPR>(srl);
+  sl = group_sum_i64<LPR>(sl);
+  const double inv = 1.0 / (double)kSynQ;
+  const float ca = (float)((double)(sr - srl) * inv), cb = (float)((double)srl * inv);
+#pragma unroll
+  for (int c = 0; c < C; ++c) gc[c] = fmaf(ca, xa[c], cb * xb[c]);
+  if constexpr (HESS) {
+    sd = group_sum_i64<LPR>(sd);
+    sdl = group_sum_i64<LPR>(sdl);
+    sdll = group_sum_i64<LPR>(sdll);
+    const double m11 = (double)(sd - 2 * sdl + sdll) * inv, m21 = (double)(sdl - sdll) * inv;
+    const double m22 = (double)sdll * inv;
+    const double l11 = sqrt(fmax(m11, 0.0));
+    const double l21 = l11 > 0.0 ? m21 / l11 : 0.0;
+    const double l22 = sqrt(fmax(m22 - l21 * l21, 0.0));
+    const float f11 = (float)(l11 * hrs), f21 = (float)(l21 * hrs), f22 = (float)(l22 * hrs);
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      u1[c] = fmaf(f11, xa[c], f21 * xb[c]);
+      u2[c] = f22 * xb[c];
+    }
+  }
+  loss = (float)((double)sl * (1.0 / (double)kSynQL));
+  wsum = (float)cnt * sw1;
+}
+
+// VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
+// rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
 template <bool HESS, bool VIRT = false>  // bf16 rows (64 B); fp8 rows: logreg_pass_fp8w_kernel
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
@@ -76,98 +187,77 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
   uint16_t* my_tile = tile[wv];
 
-  const int64_t n = row_end - row_begin;
+  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin;  // stored rows
   // row_sub > 1: only 64-row tiles t with (t mod G*row_sub) < G are visited (G = waves in the
   // grid): a uniform 1/row_sub subsample used by the early progressive-Newton iterations.
   const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
-  const uint4* X = reinterpret_cast<const uint4*>(Xv);
-  // virtual-row draw parameters (smote.hip launch_smote_generate)
-  const uint4* Pb = reinterpret_cast<const uint4*>(sv.parents);
-  const uint32_t vrange = (uint32_t)sv.mq * (uint32_t)sv.k;
-  const float vinv_k = 1.0f / (float)sv.k;
-  const bool vsmall = vrange < (1u << 22);
-  // a tile holds a virtual row (wave-uniform)
-  auto is_virt = [&](int64_t b) { return VIRT && row_begin + b + 64 > sv.n_real; };
-  // Stage 1 (tile t+2): this lane's draw for row b + lane -- Philox, then the neighbour-index
-  // load, left in flight (its first use is stage 2 one iteration later).  Every lane draws: a
-  // draw is in range whatever the counter, so real lanes of a boundary tile need no branch.
-  auto draw = [&](int64_t b) __attribute__((always_inline)) -> uint2 {
-    const int64_t gs = sv.s_off + (row_begin + b + lane - sv.n_real);
-    const int64_t c = ((gs >> 7) << 6) + (gs & 63);
-    const Philox4 r = philox4x32_10((uint32_t)c, (uint32_t)(c >> 32), sv.cb0, sv.cb1, sv.key0, sv.key1);
-    const bool hi = ((gs >> 6) & 1) != 0;
-    return smote_pack_draw(hi ? r.z : r.x, hi ? r.w : r.y, vrange, (uint32_t)sv.k, vinv_k, vsmall, sv.nbr);
-  };
-  // Stage 2 (tile t+1): the row loads -- stored rows from HBM into A; for a virtual row the
-  // parent (A) and neighbour (B) 16 B slices from L2 plus lambda.
-  uint4 A[4], B[4];
-  float lam[4];
-  auto gather = [&](int64_t b, uint2 dd) __attribute__((always_inline)) {
+  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
+  auto load_tile = [&](int64_t b, uint4 (&v)[4]) {
+    const uint4* X = reinterpret_cast<const uint4*>(Xv);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = b + 16 * u + rr;
-      if (!is_virt(b)) {
-        A[u] = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
-      } else {  // branch-free: a stored row of a boundary tile loads into A and ignores B
-        const int src = 16 * u + rr;
-        const uint32_t dx = __shfl(dd.x, src, kWave), dy = __shfl(dd.y, src, kWave);
-        const bool stored = row_begin + row < sv.n_real;
-        const uint4* pa = stored ? X + (row_begin + row) * 4 + q
-                                 : Pb + (sv.q_offset + (int64_t)(dx & 0xffffffu)) * 4 + q;
-        A[u] = *pa;
-        B[u] = Pb[(int64_t)(dy & 0xffffffu) * 4 + q];
-        lam[u] = smote_lambda(dx, dy);
-      }
+      v[u] = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
     }
   };
-  // Stage 3 (tile t): the rows this tile computes on.  Virtual rows: smote_generate's bf16 output.
-  auto finish = [&](int64_t b, uint4 (&v)[4]) __attribute__((always_inline)) {
+  // virtual SMOTE samples: tiles of 16 picks (row_sub: every row_sub-th tile).  A wave's pick
+  // tile runs in the middle of its stored-row loop (at a wave-dependent iteration), so the
+  // latency-bound pick work of some waves overlaps the streaming of the others instead of
+  // forming a phase of its own at the end of the kernel (+33 us per full pass measured).
+  const float hrs = rsqrtf((float)hess_stride);  // the final x hess_stride restores u u^T
+  const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
+  const int64_t ntile = (npick + 15) >> 4;
+  const int64_t Gw = (int64_t)gridDim.x * kWaves;
+  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub;  // this wave's next pick tile
+  auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
+    const int64_t p = t * 16 + rr;
+    float gc[8], u1[8], u2[8], ls, ws;
+    pick_terms<4, HESS>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, gc, u1, u2, ls, ws);
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (!is_virt(b)) {
-        v[u] = A[u];
-      } else {
-        const int64_t row = b + 16 * u + rr;
-        float av[8], bv[8], o[8];
-        unpack8(A[u], av);
-        unpack8(B[u], bv);
+    for (int j = 0; j < 8; ++j) g[j] += gc[j];
+    if (q == 0) {
+      lacc += ls;
+      wacc += ws;
+      if (HESS) whacc += ws / (float)hess_stride;
+    }
+    if constexpr (HESS) {  // rows rr (u1) and 16 + rr (u2) of the wave's tile: 2 MFMAs
+      uint4 a, b;
+      a.x = pack_bf16x2(u1[0], u1[1]); a.y = pack_bf16x2(u1[2], u1[3]);
+      a.z = pack_bf16x2(u1[4], u1[5]); a.w = pack_bf16x2(u1[6], u1[7]);
+      b.x = pack_bf16x2(u2[0], u2[1]); b.y = pack_bf16x2(u2[2], u2[3]);
+      b.z = pack_bf16x2(u2[4], u2[5]); b.w = pack_bf16x2(u2[6], u2[7]);
+      *reinterpret_cast<uint4*>(my_tile + rr * kCols + 8 * q) = a;
+      *reinterpret_cast<uint4*>(my_tile + (16 + rr) * kCols + 8 * q) = b;
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = fmaf(lam[u], bv[j] - av[j], av[j]);
-        if (q == 3) {
-          o[6] = 1.0f;      // col 30: intercept column
-          o[7] = sv.label;  // col 31: label
-        }
-        uint4 s;
-        s.x = pack_bf16x2(o[0], o[1]);
-        s.y = pack_bf16x2(o[2], o[3]);
-        s.z = pack_bf16x2(o[4], o[5]);
-        s.w = pack_bf16x2(o[6], o[7]);
-        const bool stored = row_begin + row < sv.n_real;
-        v[u] = stored ? A[u] : (row < n ? s : make_uint4(0, 0, 0, 0));
+      for (int s = 0; s < 2; ++s) {
+        const lds_s4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off));
+        const lds_s4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off + 4 * kCols));
+        bf16x8_t f;
+        f[0] = a0[0]; f[1] = a0[1]; f[2] = a0[2]; f[3] = a0[3];
+        f[4] = a1[0]; f[5] = a1[1]; f[6] = a1[2]; f[7] = a1[3];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, f, acc, 0, 0, 0);
       }
+      __builtin_amdgcn_wave_barrier();
     }
   };
   int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
-  uint2 dnext = make_uint2(0u, 0u);
-  if (base < n) {
-    if (is_virt(base)) dnext = draw(base);
-    gather(base, dnext);
-    if (base + step < n && is_virt(base + step)) dnext = draw(base + step);
-  }
+  uint4 cur[4];
+  if (base < n) load_tile(base, cur);
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
   // is unchanged; H only shapes the step (sub-sampled Newton).
   int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
+  // pick tile after the ptrig-th stored tile of this wave (spread over the wave's iterations)
+  const int64_t witers = n > base ? (n - base + step - 1) / step : 0;
+  const int64_t ptrig = witers > 0 ? 1 + ((blockIdx.x * kWaves + wv) % witers) : 0;
+  int64_t pit = 0;
   for (; base < n; base += step) {
-    // register pipeline: tile t's rows out of the stage registers, then the loads of tile t+1
-    // and the draw of tile t+2 go in flight while tile t computes
-    uint4 cur[4];
-    finish(base, cur);
-    if (base + step < n) {
-      gather(base + step, dnext);
-      if (base + 2 * step < n && is_virt(base + 2 * step)) dnext = draw(base + 2 * step);
-    }
+    uint4 nxt[4];
+    if (base + step < n) load_tile(base + step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
@@ -229,6 +319,18 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
     wacc += swq;
     if (do_h) whacc += swq;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+    if constexpr (VIRT) {
+      if (ptile < ntile && ++pit == ptrig) {
+        pick_tile(ptile);
+        ptile += Gw * row_sub;
+      }
+    }
+  }
+
+  if constexpr (VIRT) {  // the wave's remaining pick tiles
+    for (; ptile < ntile; ptile += Gw * row_sub) pick_tile(ptile);
   }
 
   // ---- block reduction (fixed order) ----
@@ -276,12 +378,13 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 // and its MFMA are those of the bf16 kernel.  Measured against the previous 4-lane fp8 kernel
 // (profiles/r3_s): gradient pass 125 -> 99 us, sub-sampled Hessian pass 137 -> 112 us over
 // 16M rows (5.2 TB/s), fp8 bench step 1.164 -> 1.099 ms.
+// VIRT: virtual SMOTE samples as in the bf16 kernel, tiles of 32 picks (2 lanes per pick).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-template <bool HESS>
+template <bool HESS, bool VIRT = false>
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, int row_sub, float* __restrict__ partial) {
+    int hess_stride, int row_sub, float* __restrict__ partial, SmoteView sv) {
   if (done != nullptr && *done) return;
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][35];
@@ -307,7 +410,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   const int grp = lane >> 4, gi = lane & 15;
   const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
   uint16_t* my_tile = tile[wv];
-  const int64_t n = row_end - row_begin;
+  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin;  // stored rows
   const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
   const uint4* X = reinterpret_cast<const uint4*>(X8);
@@ -316,6 +419,58 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     for (int u = 0; u < 2; ++u) {
       const int64_t row = b + 32 * u + rr;
       v[u] = row < n ? X[(row_begin + row) * 2 + q] : make_uint4(0, 0, 0, 0);
+    }
+  };
+  // virtual SMOTE samples: tiles of 32 picks (2 lanes per pick, 16 columns each), after the
+  // stored-row loop
+  const float hrs = rsqrtf((float)hess_stride);
+  const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
+  const int64_t ntile = (npick + 31) >> 5;
+  const int64_t Gw = (int64_t)gridDim.x * kWaves;
+  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub;
+  auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
+    float wf[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      wf[2 * e] = wl[e][0];
+      wf[2 * e + 1] = wl[e][1];
+    }
+    const int64_t p = t * 32 + rr;
+    float gc[16], u1[16], u2[16], ls, ws;
+    pick_terms<2, HESS>(sv, p < npick ? p : -1, q, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] += f32x2_t{gc[2 * j], gc[2 * j + 1]};
+    if (q == 0) {
+      lacc += ls;
+      wacc += ws;
+      if (HESS) whacc += ws / (float)hess_stride;
+    }
+    if constexpr (HESS) {  // rows rr (u1) and 32 + rr (u2): 4 MFMAs
+      uint4* d1 = reinterpret_cast<uint4*>(my_tile + rr * kCols + 16 * q);
+      uint4* d2 = reinterpret_cast<uint4*>(my_tile + (32 + rr) * kCols + 16 * q);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint4 a, b;
+        a.x = pack_bf16x2(u1[8 * h + 0], u1[8 * h + 1]); a.y = pack_bf16x2(u1[8 * h + 2], u1[8 * h + 3]);
+        a.z = pack_bf16x2(u1[8 * h + 4], u1[8 * h + 5]); a.w = pack_bf16x2(u1[8 * h + 6], u1[8 * h + 7]);
+        b.x = pack_bf16x2(u2[8 * h + 0], u2[8 * h + 1]); b.y = pack_bf16x2(u2[8 * h + 2], u2[8 * h + 3]);
+        b.z = pack_bf16x2(u2[8 * h + 4], u2[8 * h + 5]); b.w = pack_bf16x2(u2[8 * h + 6], u2[8 * h + 7]);
+        d1[h] = a;
+        d2[h] = b;
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const lds_s4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off));
+        const lds_s4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off + 4 * kCols));
+        bf16x8_t f;
+        f[0] = a0[0]; f[1] = a0[1]; f[2] = a0[2]; f[3] = a0[3];
+        f[4] = a1[0]; f[5] = a1[1]; f[6] = a1[2]; f[7] = a1[3];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f, f, acc, 0, 0, 0);
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   };
   int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
@@ -394,6 +549,11 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       cur[u] = nx1[u];
       nx1[u] = nxt[u];
     }
+    // (no mid-loop pick tile here: with the two prefetched fp8 tiles live it spilled 92 B/lane)
+  }
+
+  if constexpr (VIRT) {  // the wave's remaining pick tiles
+    for (; ptile < ntile; ptile += Gw * row_sub) pick_tile(ptile);
   }
 
   // ---- block reduction (fixed order) ----
@@ -866,23 +1026,29 @@ int logreg_pass_blocks(int fmt) {
   return c;
 }
 
+// The view a pass launches with: empty without virtual rows; validated otherwise (a virtual
+// pass covers all rows: the picks are not split by row range).
+static SmoteView checked_view(const SmoteView* sv, int64_t row_begin, int64_t row_end) {
+  SmoteView v;
+  if (sv == nullptr || sv->parents == nullptr) return v;
+  v = *sv;
+  if (v.nbr == nullptr || v.lam == nullptr || v.off == nullptr || v.mq <= 0 || v.k <= 0 || v.n_real < 0 ||
+      v.q_offset < 0 || (uint64_t)v.mq * (uint64_t)v.k >= (1ull << 31) || row_begin != 0 || row_end < v.n_real)
+    throw std::runtime_error("logreg_pass: invalid virtual SMOTE view");
+  return v;
+}
+
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream, const SmoteView* sv) {
   // hessian: 0 = gradient/loss only; h >= 1 = also the Hessian, from every h-th row tile.
   // row_sub >= 1: visit a uniform 1/row_sub of the 64-row tiles (progressive Newton).
-  // sv (nullable): rows >= sv->n_real are virtual SMOTE rows.
+  // sv (nullable): virtual SMOTE samples after the stored rows.
   if (row_sub < 1) row_sub = 1;
-  const bool virt = sv != nullptr && sv->parents != nullptr && row_end > sv->n_real;
-  SmoteView v;
-  if (virt) {
-    v = *sv;
-    if (v.nbr == nullptr || v.mq <= 0 || v.k <= 0 || v.n_real < 0 || v.s_off < 0 || (v.s_off & 127) != 0 ||
-        (uint64_t)v.mq * (uint64_t)v.k >= (1ull << 32))
-      throw std::runtime_error("logreg_pass: invalid virtual SMOTE view");
-  }
+  const SmoteView v = checked_view(sv, row_begin, row_end);
+  const bool virt = v.parents != nullptr;
   const int hs = hessian > 0 ? hessian : 1;
-#define FDX_LRP(H, V)                                                                            \
+#define FDX_LRP(H, V)                                                                                    \
   logreg_pass_kernel<H, V><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, hs, \
                                                              row_sub, partial, v)
   if (hessian > 0) {
@@ -898,16 +1064,24 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
 
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
-                            float x_scale, float* partial, int nblocks, hipStream_t stream) {
+                            float x_scale, float* partial, int nblocks, hipStream_t stream, const SmoteView* sv) {
   // fp8 rows store features * x_scale for columns < 30; the bias (col 30) and label (col 31)
-  // are stored unscaled.
+  // are stored unscaled.  sv (nullable): virtual SMOTE samples after the stored rows.
   if (row_sub < 1) row_sub = 1;
-  if (hessian > 0)
-    logreg_pass_fp8w_kernel<true><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, x_scale, 30, hessian, row_sub, partial);
-  else
-    logreg_pass_fp8w_kernel<false><<<nblocks, kThreads, 0, stream>>>(
-        X, row_begin, row_end, w, class_w, done, x_scale, 30, 1, row_sub, partial);
+  const SmoteView v = checked_view(sv, row_begin, row_end);
+  const bool virt = v.parents != nullptr;
+  const int hs = hessian > 0 ? hessian : 1;
+#define FDX_LRP8(H, V)                                                                                   \
+  logreg_pass_fp8w_kernel<H, V><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, \
+                                                                  x_scale, 30, hs, row_sub, partial, v)
+  if (hessian > 0) {
+    if (virt) FDX_LRP8(true, true);
+    else FDX_LRP8(true, false);
+  } else {
+    if (virt) FDX_LRP8(false, true);
+    else FDX_LRP8(false, false);
+  }
+#undef FDX_LRP8
   check_launch("logreg_pass_fp8");
 }
 

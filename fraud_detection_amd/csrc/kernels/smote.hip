@@ -219,7 +219,161 @@ __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __
   P[e] = f32_to_bf16(v);
 }
 
+// Group this launch's samples by pick (virtual SMOTE rows, launchers.h SmoteView) with a
+// two-level counting sort -- LDS histograms and LDS cursors only (one global atomic per sample
+// measured 318 us to count and 714 us to fill 8M samples into 68k buckets: contended L2 atomics).
+// Draws: one Philox call per pair of samples exactly as smote_generate_kernel draws them (pair
+// t = (m, L) of the launch's 128-sample block m serves samples 128 m + L with words (x, y) and
+// 128 m + 64 + L with (z, w)); pick = u32_range(word_pick, mq k), lambda = word_lam >> 16.
+//   level 1: coarse bin = pick >> fb (2^fb picks per bin, chosen by the host for ~4-8k samples
+//            per bin).  Each of kBucketBlocks blocks histograms its contiguous range of pairs in
+//            LDS (table[bin][block]); after an inclusive scan of the table the same blocks redraw
+//            and scatter 4-byte records (pick & (2^fb - 1) | lambda << 16) into their bins
+//            through LDS cursors.
+//   level 2: one block per coarse bin stages the bin's records in LDS, counts its fine picks,
+//            writes their offsets and assembles the bin's lambdas in LDS, then stores them
+//            coalesced (a bin too big for the stage takes the same steps through global memory).
+// Order inside a bucket follows the LDS atomics; the pass sums a bucket in fixed point.
+constexpr int kBucketBlocks = 256;
+constexpr int kBucketThreads = 1024;  // 4 waves per SIMD: the LDS-atomic + scatter chain is latency-bound
+constexpr int kFineMax = 128;
+constexpr int kStageRecs = 10240;  // 40 KiB of records + 20 KiB of lambdas in LDS
+
+__device__ __forceinline__ int excl_at(const int* incl, int64_t i) { return i == 0 ? 0 : incl[i - 1]; }
+
+__device__ __forceinline__ void bucket_range(int64_t npairs, int64_t* lo, int64_t* hi) {
+  const int64_t per = (npairs + kBucketBlocks - 1) / kBucketBlocks;
+  *lo = min((int64_t)blockIdx.x * per, npairs);
+  *hi = min(*lo + per, npairs);
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_t range, int fb, int nbins, int64_t n_new,
+                                                                   int64_t blk0, uint32_t key0, uint32_t key1,
+                                                                   uint32_t cb0, uint32_t cb1,
+                                                                   int* __restrict__ table,
+                                                                   uint32_t* __restrict__ rec) {
+  extern __shared__ int h[];  // [nbins]
+  for (int b = threadIdx.x; b < nbins; b += kBucketThreads)
+    h[b] = SCATTER ? excl_at(table, (int64_t)b * kBucketBlocks + blockIdx.x) : 0;
+  __syncthreads();
+  const int64_t npairs = ((n_new + 127) >> 7) << 6;
+  const uint32_t fmask = (1u << fb) - 1u;
+  int64_t lo, hi;
+  bucket_range(npairs, &lo, &hi);
+  for (int64_t t = lo + threadIdx.x; t < hi; t += kBucketThreads) {
+    const int64_t m = t >> 6, L = t & 63;
+    const int64_t c = ((blk0 + m) << 6) + L;
+    const Philox4 r = philox4x32_10((uint32_t)c, (uint32_t)(c >> 32), cb0, cb1, key0, key1);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      if ((m << 7) + 64 * hh + L >= n_new) continue;
+      const uint32_t pick = u32_range(hh ? r.z : r.x, range);
+      if constexpr (SCATTER) {
+        const int pos = atomicAdd(h + (pick >> fb), 1);
+        rec[pos] = (pick & fmask) | (((hh ? r.w : r.y) >> 16) << 16);
+      } else {
+        atomicAdd(h + (pick >> fb), 1);
+      }
+    }
+  }
+  if constexpr (!SCATTER) {  // every entry written: the table needs no fill
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbins; b += kBucketThreads) table[(int64_t)b * kBucketBlocks + blockIdx.x] = h[b];
+  }
+}
+
+__global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __restrict__ incl, uint32_t range, int fb,
+                                                               int64_t n_new, const uint32_t* __restrict__ rec,
+                                                               int* __restrict__ off, uint16_t* __restrict__ lam) {
+  __shared__ int cnt[kFineMax], cur[kFineMax];
+  __shared__ uint32_t srec[kStageRecs];
+  __shared__ uint16_t slam[kStageRecs];
+  const int bin = blockIdx.x, fine = 1 << fb;
+  const uint32_t fmask = (uint32_t)fine - 1u;
+  const int b0 = excl_at(incl, (int64_t)bin * kBucketBlocks);
+  const int b1 = excl_at(incl, (int64_t)(bin + 1) * kBucketBlocks);  // the last bin ends at the total
+  const int n = b1 - b0;
+  const bool staged = n <= kStageRecs;
+  if (threadIdx.x < kFineMax) cnt[threadIdx.x] = 0;
+  if (staged)
+    for (int i = threadIdx.x; i < n; i += blockDim.x) srec[i] = rec[b0 + i];
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(cnt + ((staged ? srec[i] : rec[b0 + i]) & fmask), 1);
+  __syncthreads();
+  if (threadIdx.x < kWave) {  // exclusive scan of <= 128 fine counts by one wave (2 per lane)
+    const int l = threadIdx.x;
+    const int a = 2 * l < fine ? cnt[2 * l] : 0, b = 2 * l + 1 < fine ? cnt[2 * l + 1] : 0;
+    int inc = a + b;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int v = __shfl_up(inc, o, kWave);
+      if (l >= o) inc += v;
+    }
+    const int ex = inc - (a + b);  // bin-local
+    if (2 * l < fine) cur[2 * l] = ex;
+    if (2 * l + 1 < fine) cur[2 * l + 1] = ex + a;
+  }
+  __syncthreads();
+  if (threadIdx.x < fine) {
+    const uint32_t pick = ((uint32_t)bin << fb) + threadIdx.x;
+    if (pick < range) off[pick] = b0 + cur[threadIdx.x];
+    if (pick == range - 1) off[range] = (int)n_new;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const uint32_t r = staged ? srec[i] : rec[b0 + i];
+    const int pos = atomicAdd(cur + (r & fmask), 1);
+    if (staged) slam[pos] = (uint16_t)(r >> 16);
+    else lam[b0 + pos] = (uint16_t)(r >> 16);
+  }
+  if (staged) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) lam[b0 + i] = slam[i];
+  }
+}
+
 }  // namespace
+
+// 2^fb picks per coarse bin: ~kTarget samples per bin for the LDS stage, <= 16384 bins for the
+// level-1 LDS histogram, <= kFineMax picks per bin.
+int smote_bucket_fine_bits(int64_t range, int64_t n_new) {
+  constexpr double kTarget = 4096.0;
+  int fb = 0;
+  while (fb < 7 && ((range + (1ll << fb) - 1) >> fb) > 16384) ++fb;
+  while (fb < 7 && (double)n_new * (double)(1ll << (fb + 1)) / (double)range <= kTarget) ++fb;
+  return fb;
+}
+int smote_bucket_bins(int64_t range, int64_t n_new) {
+  const int fb = smote_bucket_fine_bits(range, n_new);
+  return (int)((range + (1ll << fb) - 1) >> fb);
+}
+int smote_bucket_blocks() { return kBucketBlocks; }
+
+void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
+                         uint64_t counter_base, int* table, uint32_t* rec, int* off, uint16_t* lam,
+                         hipStream_t stream) {
+  if (n_new <= 0) return;
+  if (sample_offset < 0 || (sample_offset & 127) != 0)
+    throw std::runtime_error("smote_bucket: sample_offset must be a non-negative multiple of 128");
+  const uint64_t R = (uint64_t)mq * (uint64_t)k;
+  if (mq <= 0 || k <= 0 || R > kSmoteBucketMaxPicks || n_new >= (1ll << 31))
+    throw std::runtime_error("smote_bucket: pick range or sample count out of bounds");
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
+  const int fb = smote_bucket_fine_bits((int64_t)R, n_new);
+  const int nbins = smote_bucket_bins((int64_t)R, n_new);
+  const size_t lds = (size_t)nbins * sizeof(int);
+  if (stage == 0)
+    smote_bucket_l1_kernel<false><<<kBucketBlocks, kBucketThreads, lds, stream>>>(
+        (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec);
+  else if (stage == 1)
+    smote_bucket_l1_kernel<true><<<kBucketBlocks, kBucketThreads, lds, stream>>>(
+        (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec);
+  else
+    smote_bucket_l2_kernel<<<nbins, 1024, 0, stream>>>(table, (uint32_t)R, fb, n_new, rec, off, lam);
+  check_launch("smote_bucket");
+}
 
 void launch_smote_parents(const float* C, int64_t m, const double* aff, uint16_t* P, hipStream_t stream) {
   if (m <= 0) return;

@@ -6,7 +6,7 @@ Here every numeric step is a HIP kernel on the rank's row shard:
     K1 scaler stats (+ all-reduce C1) -> K2 standardize/pad/cast into the training buffer
     -> stable minority compaction -> K2 gather (fp32 minority rows) -> all-gather C3
     -> K8 MFMA k-NN (local queries vs global minority) -> K9 Philox SMOTE rows written in place
-       from bf16 parents in the training rows' space -- or, for the bf16 Newton fit, regenerated
+       from bf16 parents in the training rows' space -- or, for the Newton fit, regenerated
        inside every K4 pass (TrainConfig.virtual_smote)
     -> K4 Newton (all-reduce C5 per iteration) or momentum SGD (all-reduce C4 per minibatch).
 Evaluation: folded-scaler predict on raw fp32 test rows (K5) -> exact AUC (K10) + confusion.
@@ -65,7 +65,7 @@ class TrainConfig:
     # of the ranks' synthetic rows equals the one-process SMOTE output bit for bit; "shard" = each
     # rank oversamples its own minority rows (per-partition SMOTE: constant work per rank)
     smote_scope: str = "global"
-    # Newton on bf16 device rows: the SMOTE rows are never stored -- every logistic pass
+    # Newton on device rows (bf16 or fp8): the SMOTE rows are never stored -- every logistic pass
     # regenerates them from their Philox draws out of the L2-resident minority parents
     # (ops/logreg.VirtualSmote), bitwise the rows smote_generate would write.  At the bench shape
     # half the training rows are synthetic: no 512 MB SMOTE write and half the bytes per pass.
@@ -193,7 +193,7 @@ class DevicePipeline:
         fit over virtual SMOTE rows has them materialised into the buffer's tail first."""
         rows = self._buf[: res.n_train_rows]
         if self._virtual is not None:
-            self._virtual.materialize(rows[res.n_rows:])
+            self._virtual.materialize(rows[res.n_rows:], self.cfg.fp8_scale)
         return rows
 
     def fit_host(self, X: torch.Tensor, y: torch.Tensor, device=None, budget: int | None = None,
@@ -321,7 +321,8 @@ class DevicePipeline:
             raise RuntimeError(f"SMOTE slice of {n_new} rows exceeds the training buffer ({rows_cap.shape[0]} rows)")
         rows = rows_cap[: n + n_new]
         virt = None
-        virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage == "bf16" and dev.type == "cuda")
+        virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage in ("bf16", "fp8")
+                   and dev.type == "cuda")
         tm.mark("scale_cast")
         # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a
         # quota; shard scope has no collective in this block, so only a rank with its own quota enters
@@ -355,7 +356,7 @@ class DevicePipeline:
             if n_new > 0:
                 if parents is None:
                     parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
-                if virt_ok:  # regenerated inside every Newton pass, never written
+                if virt_ok and nbr.numel() <= lr_ops.virtual_max_picks():  # folded into every Newton pass
                     virt = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, q_offset=q_off, sample_offset=s_off,
                                                seed=cfg.seed, counter_base=0 if glob else rank)
                 else:

@@ -43,14 +43,16 @@ class FitInfo:
 
 @dataclass
 class VirtualSmote:
-    """SMOTE rows a bf16 Newton fit reads without their ever being stored (launchers.h SmoteView).
+    """SMOTE samples a Newton fit reads without their ever being stored (launchers.h SmoteView).
 
-    The fit's rows are ``rows`` (the stored real rows, [n_real, 32]) followed by ``n_new`` virtual
-    rows: sample s is regenerated inside every logistic pass exactly as ``knn.smote_generate``
-    would have written it into ``rows_cap[n_real + s]`` with the same arguments (bf16 output-space
-    parents, same Philox draws, same fmaf + bf16 rounding), so the fit is bitwise the fit over
-    the materialised rows.  The parents and neighbour lists are small (the minority class) and
-    stay L2-resident; the pass streams only the real rows from HBM."""
+    The fit's rows are ``rows`` (the stored real rows) followed by ``n_new`` samples
+    x = a + lam (b - a) drawn exactly as ``knn.smote_generate`` draws them (same Philox stream,
+    parents, neighbour lists): a = parents[q_offset + pick // k], b = parents[nbr[pick]].  Every
+    logistic pass folds them in through per-pick sums over the pick's lambdas (logreg.hip
+    pick_terms), so a pass streams 2 bytes per sample instead of a 64 B stored row.  The
+    interpolants enter at fp32 precision (the stored path rounds each to bf16 / e4m3): the fit is
+    the stored-row fit up to that rounding, and bitwise reproducible run to run.
+    ``prepare()`` buckets the lambdas by pick on the device (once per fit, smote.hip)."""
     parents: torch.Tensor     # bf16 [m, 32] (knn.smote_parents / knn_topk(parents=...))
     nbr: torch.Tensor         # int32 [mq, k] neighbour rows (indices into parents)
     n_new: int
@@ -59,10 +61,12 @@ class VirtualSmote:
     seed: int = 42
     counter_base: int = 0
     label: float = 1.0
+    lam: torch.Tensor | None = None   # int16 [n_new] lambda * 2^16 grouped by pick
+    off: torch.Tensor | None = None   # int32 [mq * k + 1] bucket offsets
 
     def check(self, rows: torch.Tensor):
-        if storage_kind(rows) != "bf16" or not rows.is_cuda:
-            raise ValueError("virtual SMOTE rows need bf16 device rows")
+        if storage_kind(rows) not in ("bf16", "fp8") or not rows.is_cuda:
+            raise ValueError("virtual SMOTE rows need bf16 or fp8 device rows")
         p, nb = self.parents, self.nbr
         if p.dtype != torch.bfloat16 or p.dim() != 2 or p.shape[1] != NCOLS or p.device != rows.device:
             raise ValueError("parents must be bf16 [m, 32] on the rows' device")
@@ -73,14 +77,51 @@ class VirtualSmote:
             raise ValueError("n_new >= 0 and sample_offset a non-negative multiple of 128")
         if self.n_new and (mq < 1 or k < 1 or self.q_offset < 0 or self.q_offset + mq > p.shape[0]):
             raise ValueError("query rows out of range of the parents")
+        if mq * k > native().smote_bucket_max_picks():
+            raise ValueError("virtual SMOTE: mq * k exceeds the bucket sort's range")
         ref.smote_check_ranges(p.shape[0], mq, k)
 
-    def materialize(self, out: torch.Tensor) -> torch.Tensor:
-        """The stored equivalent: the same rows written by smote_generate (tests, CPU paths)."""
+    def prepare(self) -> "VirtualSmote":
+        """Bucket the samples' lambdas by pick on the parents' device: count, scan, fill."""
+        if self.off is not None or self.n_new == 0:
+            return self
+        m = native()
+        mq, k = self.nbr.shape
+        R = mq * k
+        dev = self.parents.device
+        s = stream_of(self.parents)
+        nt = m.smote_bucket_bins(R, int(self.n_new)) * m.smote_bucket_blocks()
+        table = torch.empty(nt, dtype=torch.int32, device=dev)   # every entry written by stage 0
+        args = (mq, k, int(self.n_new), int(self.sample_offset), int(self.seed) & (2**64 - 1),
+                int(self.counter_base) & (2**64 - 1))
+        m.smote_bucket(0, *args, ptr(table), 0, 0, 0, s)            # coarse counts [bin][block]
+        table = torch.cumsum(table, 0, dtype=torch.int32)            # inclusive scan
+        rec = torch.empty(int(self.n_new), dtype=torch.int32, device=dev)
+        m.smote_bucket(1, *args, ptr(table), ptr(rec), 0, 0, s)      # coarse records
+        off = torch.empty(R + 1, dtype=torch.int32, device=dev)
+        lam = torch.empty(int(self.n_new), dtype=torch.int16, device=dev)
+        m.smote_bucket(2, *args, ptr(table), ptr(rec), ptr(off), ptr(lam), s)
+        self.lam, self.off = lam, off
+        return self
+
+    def rows_f32(self) -> torch.Tensor:
+        """The samples as fp32 rows (host): the interpolants the virtual passes fold in."""
+        P = self.parents.cpu().float().numpy()
+        out = ref.smote_generate(P, self.nbr.cpu().numpy(), self.q_offset, self.n_new, self.seed,
+                                 self.counter_base, self.label, sample_offset=self.sample_offset)
+        return torch.from_numpy(out)
+
+    def materialize(self, out: torch.Tensor, fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:
+        """The stored-path rows (smote_generate: the same samples rounded to ``out``'s format)."""
         from . import knn as knn_ops
         return knn_ops.smote_generate(self.parents, self.nbr, self.q_offset, self.n_new, out, seed=self.seed,
-                                      counter_base=self.counter_base, label=self.label,
+                                      counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale,
                                       sample_offset=self.sample_offset)
+
+
+def virtual_max_picks() -> int:
+    """Largest minority-rows x k that VirtualSmote's bucket sort handles (else SMOTE is stored)."""
+    return int(native().smote_bucket_max_picks())
 
 
 _FIT_FIELDS = ("w", "n_iter", "n_newton_steps", "converged", "objective", "grad_max", "history")
@@ -268,11 +309,12 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
     if virtual is not None and virtual.n_new > 0:
         v = virtual
         mq, k = v.nbr.shape
+        fp8 = storage_kind(rows) != "bf16"
+        nb = ws.nblocks_fp8 if fp8 else ws.nblocks
         m.logreg_pass_virtual(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
-                              ptr(ws.partial), ws.nblocks, s, ptr(v.parents), ptr(v.nbr), int(rows.shape[0]),
-                              int(v.q_offset), int(v.sample_offset), int(mq), int(k),
-                              int(v.seed) & (2**64 - 1), int(v.counter_base) & (2**64 - 1), float(v.label))
-        nb = ws.nblocks
+                              ptr(ws.partial), nb, s, ptr(v.parents), ptr(v.nbr), ptr(v.lam), ptr(v.off),
+                              int(rows.shape[0]), int(v.q_offset), int(mq), int(k),
+                              float(fp8_scale) if fp8 else 0.0)
     elif storage_kind(rows) == "bf16":
         nb = ws.nblocks
         m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
@@ -299,6 +341,7 @@ def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian
     n = rows.shape[0]
     if virtual is not None:
         virtual.check(rows)
+        virtual.prepare()
         n += virtual.n_new
     _pass(m, rows, ws, hessian, 0, n, fp8_scale, stream_of(rows), done=False, virtual=virtual)
     red = ws.red.cpu().numpy()
@@ -361,13 +404,12 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     w0 = _default_w0(w0)
     if virtual is not None and virtual.n_new == 0:
         virtual = None
-    if virtual is not None and not rows.is_cuda:  # host path: materialise (CPU tests)
-        full = torch.empty((rows.shape[0] + virtual.n_new, NCOLS), dtype=rows.dtype)
-        full[: rows.shape[0]] = rows
-        virtual.materialize(full[rows.shape[0]:])
-        rows, virtual = full, None
+    if virtual is not None and not rows.is_cuda:  # host path: the fp32 interpolants after the rows
+        rows = torch.cat([ref.rows_to_f32(rows, fp8_scale, d), virtual.rows_f32()])
+        virtual = None
     if virtual is not None:
         virtual.check(rows)
+        virtual.prepare()
     if not rows.is_cuda:
         if affine is not None:
             a = affine.cpu().double()

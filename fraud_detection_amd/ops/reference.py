@@ -328,6 +328,15 @@ def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int, sample
     nbr = np.asarray(nbr)
     mq, k = nbr.shape
     smote_check_ranges(mq, mq, k)
+    pick, lam = smote_pick_draws(mq, k, n_new, seed, counter_base, sample_offset)
+    i = (pick // k).astype(np.uint32)
+    j = nbr[i, pick % k].astype(np.uint32)
+    return np.stack([i | ((lam >> np.uint32(8)) << np.uint32(24)), j | ((lam & np.uint32(0xFF)) << np.uint32(24))], 1)
+
+
+def smote_pick_draws(mq: int, k: int, n_new: int, seed: int, counter_base: int, sample_offset: int = 0):
+    """(pick = query row * k + neighbour slot, lam * 2^16) of each sample, uint32 (smote_plan's
+    draws before the neighbour lookup; the virtual-SMOTE buckets group samples by pick)."""
     s = np.arange(n_new, dtype=np.uint64) + np.uint64(sample_offset)
     c = (s // np.uint64(128)) * np.uint64(64) + (s % np.uint64(64))
     half = ((s % np.uint64(128)) // np.uint64(64)).astype(bool)
@@ -337,11 +346,7 @@ def smote_plan(nbr: np.ndarray, n_new: int, seed: int, counter_base: int, sample
                       seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
     wp = np.where(half, r[2], r[0])
     wl = np.where(half, r[3], r[1])
-    pick = u32_range(wp, mq * k)
-    i = (pick // k).astype(np.uint32)
-    j = nbr[i, pick % k].astype(np.uint32)
-    lam = wl.astype(np.uint32) >> np.uint32(16)
-    return np.stack([i | ((lam >> np.uint32(8)) << np.uint32(24)), j | ((lam & np.uint32(0xFF)) << np.uint32(24))], 1)
+    return u32_range(wp, mq * k).astype(np.uint32), wl.astype(np.uint32) >> np.uint32(16)
 
 
 def smote_draws_decode(plan: np.ndarray):
