@@ -485,13 +485,14 @@ PYBIND11_MODULE(_fdx_native, m) {
   // the same pass over the stored rows [0, n_real) plus virtual SMOTE samples (launchers.h
   // SmoteView); x_scale > 0 selects the fp8 row pass
   m.def("logreg_pass_virtual", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
-                                  int nblocks, u s, u parents, u nbr, u lam, u off, int64_t n_real,
+                                  int nblocks, u s, u parents, u nbr, u lam, u off, u cnt, int64_t n_real,
                                   int64_t q_offset, int mq, int k, float x_scale) {
     fdx::SmoteView v;
     v.parents = P<const uint16_t>(parents);
     v.nbr = P<const int>(nbr);
     v.lam = P<const uint16_t>(lam);
     v.off = P<const int>(off);
+    v.cnt = P<const int>(cnt);
     v.n_real = n_real;
     v.q_offset = q_offset;
     v.mq = mq;
@@ -507,9 +508,10 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("smote_bucket_blocks", &fdx::smote_bucket_blocks);
   m.def("smote_bucket_max_picks", []() { return (uint64_t)fdx::kSmoteBucketMaxPicks; });
   m.def("smote_bucket", [](int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
-                           uint64_t counter_base, u table, u rec, u off, u lam, u s) {
+                           uint64_t counter_base, u table, u rec, u tmp, u pstart, u pcnt, u lam, u bump, u s) {
     fdx::launch_smote_bucket(stage, mq, k, n_new, sample_offset, seed, counter_base, P<int>(table),
-                             P<uint32_t>(rec), P<int>(off), P<uint16_t>(lam), S(s));
+                             P<uint32_t>(rec), P<uint32_t>(tmp), P<int>(pstart), P<int>(pcnt), P<uint16_t>(lam),
+                             P<unsigned long long>(bump), S(s));
   });
   m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
                               u partial, int nblocks, u s) {

@@ -115,22 +115,24 @@ struct SmoteView {
   const uint16_t* parents = nullptr;  // bf16 [m, 32] output-space parents (smote_parents)
   const int* nbr = nullptr;           // int32 [mq * k] neighbour rows (indices into parents)
   const uint16_t* lam = nullptr;      // [n_new] lambda * 2^16 grouped by pick
-  const int* off = nullptr;           // [mq * k + 1] bucket offsets into lam
+  const int* off = nullptr;           // [mq * k] start of each pick's run in lam
+  const int* cnt = nullptr;           // [mq * k] length of each pick's run
   int64_t n_real = 0;                 // stored rows; the pass covers n_real + n_new rows
   int64_t q_offset = 0;               // parent row of query 0
   int mq = 0, k = 1;
 };
 // Lambda buckets of SMOTE samples [sample_offset, sample_offset + n_new) of one global draw
-// sequence (smote.hip, two-level LDS counting sort).  table: int32 [bins * blocks]; stage 0 fills
-// table[bin * blocks + block] with counts, the caller scans it inclusively in place, stage 1
-// writes the coarse records rec (uint32 [n_new]), stage 2 writes off (int32 [mq k + 1]) and lam
-// (uint16 [n_new]).
+// sequence (smote.hip, two-level LDS counting sort).  table: int32 [blocks(n_new) * bins];
+// stage 0 fills it with per-(block, bin) counts (and zeroes *bump), the caller scans it
+// inclusively in place, stage 1 writes the coarse records rec (uint32 [n_new]), stage 2 writes
+// each pick's lambda run (pstart, pcnt: int32 [mq k]) into lam (uint16 [n_new]); tmp (uint32
+// [n_new]) is scratch for bins too big for the LDS stage.
 constexpr uint64_t kSmoteBucketMaxPicks = 1ull << 21;  // <= 16384 coarse bins of <= 128 picks
 int smote_bucket_bins(int64_t range, int64_t n_new);
-int smote_bucket_blocks();
+int smote_bucket_blocks(int64_t n_new);
 void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
-                         uint64_t counter_base, int* table, uint32_t* rec, int* off, uint16_t* lam,
-                         hipStream_t stream);
+                         uint64_t counter_base, int* table, uint32_t* rec, uint32_t* tmp, int* pstart, int* pcnt,
+                         uint16_t* lam, unsigned long long* bump, hipStream_t stream);
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr);

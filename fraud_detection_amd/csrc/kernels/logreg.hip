@@ -55,8 +55,8 @@ __device__ __forceinline__ void unpack8(const uint4& v, float x[8]) {
 // fp32 precision (no bf16 rounding of the interpolant).  Per-sample terms are summed in fixed
 // point (int64), so the bucket order the fill's atomics produce does not change a bit: fits stay
 // bitwise reproducible.
-constexpr float kSynQ = 16777216.0f;  // 2^24: r, r lam, d, d lam, d lam^2 (|v| <= s < 128)
-constexpr float kSynQL = 65536.0f;    // 2^16: per-sample loss (<= 80 s)
+constexpr float kSynQ = 4194304.0f;   // 2^22: r, r lam, d, d lam, d lam^2 (|v| <= s <= 32)
+constexpr float kSynQL = 16384.0f;    // 2^14: per-sample loss (<= 80 s)
 
 template <int G>
 __device__ __forceinline__ long long group_sum_i64(long long v) {
@@ -101,10 +101,11 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   za = group_sum<LPR>(za);
   zb = group_sum<LPR>(zb);
   const int o0 = ok ? sv.off[pp] : 0;
-  const int cnt = ok ? sv.off[pp + 1] - o0 : 0;
+  const int cnt = ok ? sv.cnt[pp] : 0;
   const float dz = zb - za;
   long long sr = 0, srl = 0, sd = 0, sdl = 0, sdll = 0, sl = 0;
-  // kLamBatch lambdas per lane in flight per step (one load latency per step, not per sample)
+  // kLamBatch lambdas per lane in flight per step (one load latency per step, not per sample);
+  // a step's fixed-point terms are summed in int32 (|term| < 2^30 / kLamBatch), then into int64
   constexpr int kLamBatch = 8;
   for (int j0 = q; j0 < cnt; j0 += LPR * kLamBatch) {
     uint16_t lv[kLamBatch];
@@ -113,26 +114,29 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
       const int j = j0 + u * LPR;
       lv[u] = j < cnt ? sv.lam[o0 + j] : 0;
     }
+    int br = 0, brl = 0, bd = 0, bdl = 0, bdll = 0, bl = 0;
 #pragma unroll
     for (int u = 0; u < kLamBatch; ++u) {
-    if (j0 + u * LPR >= cnt) break;
-    const float lam = (float)lv[u] * (1.0f / 65536.0f);
-    const float z = fmaf(lam, dz, za);
-    const float zc = fminf(fmaxf(z, -80.0f), 80.0f);
-    const float eh = __expf(-0.5f * zc);
-    const float e2 = eh * eh;
-    const float pr = fast_rcp(1.0f + e2);
-    const float r = -sw1 * pr * e2;  // s (p - 1) without the cancellation
-    sr += __float2int_rn(r * kSynQ);
-    srl += __float2int_rn(r * lam * kSynQ);
-    if constexpr (HESS) {
-      const float d = sw1 * pr * pr * e2;  // s p (1 - p)
-      sd += __float2int_rn(d * kSynQ);
-      sdl += __float2int_rn(d * lam * kSynQ);
-      sdll += __float2int_rn(d * lam * lam * kSynQ);
+      if (j0 + u * LPR >= cnt) break;
+      const float lam = (float)lv[u] * (1.0f / 65536.0f);
+      const float z = fmaf(lam, dz, za);
+      const float zc = fminf(fmaxf(z, -80.0f), 80.0f);
+      const float eh = __expf(-0.5f * zc);
+      const float e2 = eh * eh;  // exp(-z)
+      const float pr = fast_rcp(1.0f + e2);
+      const float r = -sw1 * pr * e2;  // s (p - 1) without the cancellation
+      br += __float2int_rn(r * kSynQ);
+      brl += __float2int_rn(r * lam * kSynQ);
+      if constexpr (HESS) {
+        const float d = sw1 * pr * pr * e2;  // s p (1 - p)
+        bd += __float2int_rn(d * kSynQ);
+        bdl += __float2int_rn(d * lam * kSynQ);
+        bdll += __float2int_rn(d * lam * lam * kSynQ);
+      }
+      bl += __float2int_rn(sw1 * log1p_fast(e2) * kSynQL);  // s softplus(-z) = -s log p
     }
-    sl += __float2int_rn(sw1 * (fmaxf(-z, 0.0f) + log1p_fast(__expf(-fabsf(z)))) * kSynQL);
-    }
+    sr += br; srl += brl; sl += bl;
+    if constexpr (HESS) { sd += bd; sdl += bdl; sdll += bdll; }
   }
   sr = group_sum_i64<LPR>(sr);
   srl = group_sum_i64<LPR>(srl);
@@ -1032,7 +1036,7 @@ static SmoteView checked_view(const SmoteView* sv, int64_t row_begin, int64_t ro
   SmoteView v;
   if (sv == nullptr || sv->parents == nullptr) return v;
   v = *sv;
-  if (v.nbr == nullptr || v.lam == nullptr || v.off == nullptr || v.mq <= 0 || v.k <= 0 || v.n_real < 0 ||
+  if (v.nbr == nullptr || v.lam == nullptr || v.off == nullptr || v.cnt == nullptr || v.mq <= 0 || v.k <= 0 || v.n_real < 0 ||
       v.q_offset < 0 || (uint64_t)v.mq * (uint64_t)v.k >= (1ull << 31) || row_begin != 0 || row_end < v.n_real)
     throw std::runtime_error("logreg_pass: invalid virtual SMOTE view");
   return v;

@@ -18,6 +18,8 @@
 // each parent row, L2-resident) per lane, one 16 B store per lane: 16 rows = 1 KiB per
 // wave-instruction, written straight into the training buffer after the real rows (bf16 with
 // col 30 = 1 and col 31 = label, or fp8).
+#include <algorithm>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -220,47 +222,47 @@ __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __
 }
 
 // Group this launch's samples by pick (virtual SMOTE rows, launchers.h SmoteView) with a
-// two-level counting sort -- LDS histograms and LDS cursors only (one global atomic per sample
-// measured 318 us to count and 714 us to fill 8M samples into 68k buckets: contended L2 atomics).
+// two-level counting sort that keeps every global write coalesced.  Measured dead ends
+// (profiles/r3_v*): one global atomic per sample (318 us to count + 714 us to fill 8M samples
+// into 68k buckets: contended L2 atomics), and a bin-major level-1 scatter (83 us: 2128 bins x 256
+// blocks of open partial lines thrash L2 into partial-line HBM writes).
 // Draws: one Philox call per pair of samples exactly as smote_generate_kernel draws them (pair
 // t = (m, L) of the launch's 128-sample block m serves samples 128 m + L with words (x, y) and
 // 128 m + 64 + L with (z, w)); pick = u32_range(word_pick, mq k), lambda = word_lam >> 16.
-//   level 1: coarse bin = pick >> fb (2^fb picks per bin, chosen by the host for ~4-8k samples
-//            per bin).  Each of kBucketBlocks blocks histograms its contiguous range of pairs in
-//            LDS (table[bin][block]); after an inclusive scan of the table the same blocks redraw
-//            and scatter 4-byte records (pick & (2^fb - 1) | lambda << 16) into their bins
-//            through LDS cursors.
-//   level 2: one block per coarse bin stages the bin's records in LDS, counts its fine picks,
-//            writes their offsets and assembles the bin's lambdas in LDS, then stores them
+//   level 1: coarse bin = pick >> fb (2^fb picks per bin, ~4k samples per bin).  Block blk
+//            histograms its contiguous range of pairs into table[blk][bin] (block-major); after
+//            an inclusive scan, the same block redraws, places 4-byte records
+//            (pick & (2^fb - 1) | lambda << 16) sorted by bin in LDS and stores its whole range
+//            coalesced (its records are one contiguous run, bins in order).
+//   level 2: one block per coarse bin gathers its segment of every level-1 block into LDS,
+//            counts its fine picks, takes room for the bin with one global bump-allocator atomic,
+//            writes each pick's (start, count), assembles the lambdas in LDS and stores them
 //            coalesced (a bin too big for the stage takes the same steps through global memory).
-// Order inside a bucket follows the LDS atomics; the pass sums a bucket in fixed point.
-constexpr int kBucketBlocks = 256;
-constexpr int kBucketThreads = 1024;  // 4 waves per SIMD: the LDS-atomic + scatter chain is latency-bound
+// Order inside a bucket follows LDS atomics; the pass sums a bucket in fixed point.
+constexpr int kBucketThreads = 1024;
+constexpr int kBucketPairs = 8192;    // pairs per level-1 block: <= 16384 records staged (64 KiB)
 constexpr int kFineMax = 128;
-constexpr int kStageRecs = 10240;  // 40 KiB of records + 20 KiB of lambdas in LDS
+constexpr int kStageRecs = 10240;     // level 2: 40 KiB of records + 20 KiB of lambdas
 
 __device__ __forceinline__ int excl_at(const int* incl, int64_t i) { return i == 0 ? 0 : incl[i - 1]; }
 
-__device__ __forceinline__ void bucket_range(int64_t npairs, int64_t* lo, int64_t* hi) {
-  const int64_t per = (npairs + kBucketBlocks - 1) / kBucketBlocks;
-  *lo = min((int64_t)blockIdx.x * per, npairs);
-  *hi = min(*lo + per, npairs);
-}
-
 template <bool SCATTER>
 __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_t range, int fb, int nbins, int64_t n_new,
-                                                                   int64_t blk0, uint32_t key0, uint32_t key1,
-                                                                   uint32_t cb0, uint32_t cb1,
-                                                                   int* __restrict__ table,
-                                                                   uint32_t* __restrict__ rec) {
-  extern __shared__ int h[];  // [nbins]
-  for (int b = threadIdx.x; b < nbins; b += kBucketThreads)
-    h[b] = SCATTER ? excl_at(table, (int64_t)b * kBucketBlocks + blockIdx.x) : 0;
+                                                                         int64_t blk0, uint32_t key0, uint32_t key1,
+                                                                         uint32_t cb0, uint32_t cb1,
+                                                                         int* __restrict__ table,
+                                                                         uint32_t* __restrict__ rec,
+                                                                         unsigned long long* __restrict__ bump) {
+  extern __shared__ int h[];  // [nbins] counts / cursors, then (SCATTER) [2 kBucketPairs] records
+  uint32_t* srec = reinterpret_cast<uint32_t*>(h + nbins);
+  const int64_t tb = (int64_t)blockIdx.x * nbins;
+  const int base = SCATTER ? excl_at(table, tb) : 0;
+  for (int b = threadIdx.x; b < nbins; b += kBucketThreads) h[b] = SCATTER ? excl_at(table, tb + b) - base : 0;
+  if (!SCATTER && blockIdx.x == 0 && threadIdx.x == 0) *bump = 0ull;  // level 2's allocator
   __syncthreads();
   const int64_t npairs = ((n_new + 127) >> 7) << 6;
   const uint32_t fmask = (1u << fb) - 1u;
-  int64_t lo, hi;
-  bucket_range(npairs, &lo, &hi);
+  const int64_t lo = min((int64_t)blockIdx.x * kBucketPairs, npairs), hi = min(lo + kBucketPairs, npairs);
   for (int64_t t = lo + threadIdx.x; t < hi; t += kBucketThreads) {
     const int64_t m = t >> 6, L = t & 63;
     const int64_t c = ((blk0 + m) << 6) + L;
@@ -271,35 +273,61 @@ __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_
       const uint32_t pick = u32_range(hh ? r.z : r.x, range);
       if constexpr (SCATTER) {
         const int pos = atomicAdd(h + (pick >> fb), 1);
-        rec[pos] = (pick & fmask) | (((hh ? r.w : r.y) >> 16) << 16);
+        srec[pos] = (pick & fmask) | (((hh ? r.w : r.y) >> 16) << 16);
       } else {
         atomicAdd(h + (pick >> fb), 1);
       }
     }
   }
-  if constexpr (!SCATTER) {  // every entry written: the table needs no fill
-    __syncthreads();
-    for (int b = threadIdx.x; b < nbins; b += kBucketThreads) table[(int64_t)b * kBucketBlocks + blockIdx.x] = h[b];
+  __syncthreads();
+  if constexpr (SCATTER) {
+    const int cnt = excl_at(table, tb + nbins) - base;  // the next block's start (or the total)
+    for (int i = threadIdx.x; i < cnt; i += kBucketThreads) rec[base + i] = srec[i];
+  } else {  // every entry written: the table needs no fill
+    for (int b = threadIdx.x; b < nbins; b += kBucketThreads) table[tb + b] = h[b];
   }
 }
 
-__global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __restrict__ incl, uint32_t range, int fb,
-                                                               int64_t n_new, const uint32_t* __restrict__ rec,
-                                                               int* __restrict__ off, uint16_t* __restrict__ lam) {
+__global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __restrict__ incl, int nblk, int nbins,
+                                                               uint32_t range, int fb, const uint32_t* __restrict__ rec,
+                                                               uint32_t* __restrict__ tmp, int* __restrict__ pstart,
+                                                               int* __restrict__ pcnt, uint16_t* __restrict__ lam,
+                                                               unsigned long long* __restrict__ bump) {
   __shared__ int cnt[kFineMax], cur[kFineMax];
+  __shared__ int nrec, gbase;
   __shared__ uint32_t srec[kStageRecs];
   __shared__ uint16_t slam[kStageRecs];
   const int bin = blockIdx.x, fine = 1 << fb;
   const uint32_t fmask = (uint32_t)fine - 1u;
-  const int b0 = excl_at(incl, (int64_t)bin * kBucketBlocks);
-  const int b1 = excl_at(incl, (int64_t)(bin + 1) * kBucketBlocks);  // the last bin ends at the total
-  const int n = b1 - b0;
-  const bool staged = n <= kStageRecs;
   if (threadIdx.x < kFineMax) cnt[threadIdx.x] = 0;
-  if (staged)
-    for (int i = threadIdx.x; i < n; i += blockDim.x) srec[i] = rec[b0 + i];
+  if (threadIdx.x == 0) nrec = 0;
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(cnt + ((staged ? srec[i] : rec[b0 + i]) & fmask), 1);
+  // the bin's total, then its room in lam (bump allocator: one atomic per bin)
+  int mine = 0;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
+    const int64_t e = (int64_t)b * nbins + bin;
+    mine += excl_at(incl, e + 1) - excl_at(incl, e);
+  }
+  if (mine) atomicAdd(&nrec, mine);
+  __syncthreads();
+  const int n = nrec;
+  if (threadIdx.x == 0) gbase = n ? (int)atomicAdd(bump, (unsigned long long)n) : 0;
+  __syncthreads();
+  const int g0 = gbase;
+  const bool staged = n <= kStageRecs;
+  uint32_t* R = staged ? srec : tmp + g0;  // unstaged: the bin's records gathered in global scratch
+  if (threadIdx.x == 0) nrec = 0;
+  __syncthreads();
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {  // gather every level-1 block's segment
+    const int64_t e = (int64_t)b * nbins + bin;
+    const int s0 = excl_at(incl, e), s1 = excl_at(incl, e + 1);
+    if (s1 > s0) {
+      const int p0 = atomicAdd(&nrec, s1 - s0);
+      for (int i = s0; i < s1; ++i) R[p0 + i - s0] = rec[i];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(cnt + (R[i] & fmask), 1);
   __syncthreads();
   if (threadIdx.x < kWave) {  // exclusive scan of <= 128 fine counts by one wave (2 per lane)
     const int l = threadIdx.x;
@@ -310,33 +338,35 @@ __global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __rest
       const int v = __shfl_up(inc, o, kWave);
       if (l >= o) inc += v;
     }
-    const int ex = inc - (a + b);  // bin-local
+    const int ex = inc - (a + b);
     if (2 * l < fine) cur[2 * l] = ex;
     if (2 * l + 1 < fine) cur[2 * l + 1] = ex + a;
   }
   __syncthreads();
   if (threadIdx.x < fine) {
     const uint32_t pick = ((uint32_t)bin << fb) + threadIdx.x;
-    if (pick < range) off[pick] = b0 + cur[threadIdx.x];
-    if (pick == range - 1) off[range] = (int)n_new;
+    if (pick < range) {
+      pstart[pick] = g0 + cur[threadIdx.x];
+      pcnt[pick] = cnt[threadIdx.x];
+    }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const uint32_t r = staged ? srec[i] : rec[b0 + i];
+    const uint32_t r = R[i];
     const int pos = atomicAdd(cur + (r & fmask), 1);
     if (staged) slam[pos] = (uint16_t)(r >> 16);
-    else lam[b0 + pos] = (uint16_t)(r >> 16);
+    else lam[g0 + pos] = (uint16_t)(r >> 16);
   }
   if (staged) {
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) lam[b0 + i] = slam[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) lam[g0 + i] = slam[i];
   }
 }
 
 }  // namespace
 
-// 2^fb picks per coarse bin: ~kTarget samples per bin for the LDS stage, <= 16384 bins for the
-// level-1 LDS histogram, <= kFineMax picks per bin.
+// 2^fb picks per coarse bin: ~kTarget samples per bin for the level-2 stage, <= 16384 bins for
+// the level-1 LDS histogram, <= kFineMax picks per bin.
 int smote_bucket_fine_bits(int64_t range, int64_t n_new) {
   constexpr double kTarget = 4096.0;
   int fb = 0;
@@ -348,11 +378,14 @@ int smote_bucket_bins(int64_t range, int64_t n_new) {
   const int fb = smote_bucket_fine_bits(range, n_new);
   return (int)((range + (1ll << fb) - 1) >> fb);
 }
-int smote_bucket_blocks() { return kBucketBlocks; }
+int smote_bucket_blocks(int64_t n_new) {
+  const int64_t npairs = ((n_new + 127) >> 7) << 6;
+  return (int)std::max<int64_t>(1, (npairs + kBucketPairs - 1) / kBucketPairs);
+}
 
 void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
-                         uint64_t counter_base, int* table, uint32_t* rec, int* off, uint16_t* lam,
-                         hipStream_t stream) {
+                         uint64_t counter_base, int* table, uint32_t* rec, uint32_t* tmp, int* pstart, int* pcnt,
+                         uint16_t* lam, unsigned long long* bump, hipStream_t stream) {
   if (n_new <= 0) return;
   if (sample_offset < 0 || (sample_offset & 127) != 0)
     throw std::runtime_error("smote_bucket: sample_offset must be a non-negative multiple of 128");
@@ -363,15 +396,24 @@ void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample
   const uint32_t c0 = (uint32_t)counter_base, c1 = (uint32_t)(counter_base >> 32);
   const int fb = smote_bucket_fine_bits((int64_t)R, n_new);
   const int nbins = smote_bucket_bins((int64_t)R, n_new);
-  const size_t lds = (size_t)nbins * sizeof(int);
-  if (stage == 0)
-    smote_bucket_l1_kernel<false><<<kBucketBlocks, kBucketThreads, lds, stream>>>(
-        (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec);
-  else if (stage == 1)
-    smote_bucket_l1_kernel<true><<<kBucketBlocks, kBucketThreads, lds, stream>>>(
-        (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec);
-  else
-    smote_bucket_l2_kernel<<<nbins, 1024, 0, stream>>>(table, (uint32_t)R, fb, n_new, rec, off, lam);
+  const int nblk = smote_bucket_blocks(n_new);
+  if (stage == 0) {
+    smote_bucket_l1_kernel<false><<<nblk, kBucketThreads, (size_t)nbins * sizeof(int), stream>>>(
+        (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec, bump);
+  } else if (stage == 1) {
+    const size_t lds = (size_t)nbins * sizeof(int) + 2 * (size_t)kBucketPairs * sizeof(uint32_t);
+    static bool attr = false;
+    if (!attr) {  // > 64 KiB of dynamic LDS (gfx950: 160 KiB per workgroup)
+      hipFuncSetAttribute((const void*)smote_bucket_l1_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          (int)(16384 * sizeof(int) + 2 * (size_t)kBucketPairs * sizeof(uint32_t)));
+      attr = true;
+    }
+    smote_bucket_l1_kernel<true><<<nblk, kBucketThreads, lds, stream>>>(
+        (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec, bump);
+  } else {
+    smote_bucket_l2_kernel<<<nbins, 1024, 0, stream>>>(table, nblk, nbins, (uint32_t)R, fb, rec, tmp, pstart, pcnt,
+                                                       lam, bump);
+  }
   check_launch("smote_bucket");
 }
 

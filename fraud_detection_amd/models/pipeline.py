@@ -320,9 +320,15 @@ class DevicePipeline:
         if n + n_new > rows_cap.shape[0]:  # global_smote_slices guarantees this never fires
             raise RuntimeError(f"SMOTE slice of {n_new} rows exceeds the training buffer ({rows_cap.shape[0]} rows)")
         rows = rows_cap[: n + n_new]
+        # ---- class weights ---------------------------------------------------------------
+        class_w = (1.0, 1.0)
+        if cfg.class_weight == "balanced":  # global counts from the exchanged (minority, rows) pairs
+            tot = float(sum(r[1] + q for r, q in zip(ranks, new_per_rank)))
+            pos = float(sum(r[0] + q for r, q in zip(ranks, new_per_rank)))
+            class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         virt = None
         virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage in ("bf16", "fp8")
-                   and dev.type == "cuda")
+                   and dev.type == "cuda" and class_w[1] <= lr_ops.VIRTUAL_MAX_WEIGHT)
         tm.mark("scale_cast")
         # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a
         # quota; shard scope has no collective in this block, so only a rank with its own quota enters
@@ -364,12 +370,6 @@ class DevicePipeline:
                                            counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,
                                            sample_offset=s_off)
             tm.mark("smote_generate")
-        # ---- class weights ---------------------------------------------------------------
-        class_w = (1.0, 1.0)
-        if cfg.class_weight == "balanced":  # global counts from the exchanged (minority, rows) pairs
-            tot = float(sum(r[1] + q for r, q in zip(ranks, new_per_rank)))
-            pos = float(sum(r[0] + q for r, q in zip(ranks, new_per_rank)))
-            class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         # ---- K4: fit ---------------------------------------------------------------------
         b = self._cur
         if dev.type == "cuda":

@@ -62,7 +62,8 @@ class VirtualSmote:
     counter_base: int = 0
     label: float = 1.0
     lam: torch.Tensor | None = None   # int16 [n_new] lambda * 2^16 grouped by pick
-    off: torch.Tensor | None = None   # int32 [mq * k + 1] bucket offsets
+    off: torch.Tensor | None = None   # int32 [mq * k] start of each pick's run in lam
+    cnt: torch.Tensor | None = None   # int32 [mq * k] its length
 
     def check(self, rows: torch.Tensor):
         if storage_kind(rows) not in ("bf16", "fp8") or not rows.is_cuda:
@@ -90,17 +91,22 @@ class VirtualSmote:
         R = mq * k
         dev = self.parents.device
         s = stream_of(self.parents)
-        nt = m.smote_bucket_bins(R, int(self.n_new)) * m.smote_bucket_blocks()
+        n = int(self.n_new)
+        nt = m.smote_bucket_bins(R, n) * m.smote_bucket_blocks(n)
         table = torch.empty(nt, dtype=torch.int32, device=dev)   # every entry written by stage 0
-        args = (mq, k, int(self.n_new), int(self.sample_offset), int(self.seed) & (2**64 - 1),
+        bump = torch.empty(1, dtype=torch.int64, device=dev)      # zeroed by stage 0
+        args = (mq, k, n, int(self.sample_offset), int(self.seed) & (2**64 - 1),
                 int(self.counter_base) & (2**64 - 1))
-        m.smote_bucket(0, *args, ptr(table), 0, 0, 0, s)            # coarse counts [bin][block]
-        table = torch.cumsum(table, 0, dtype=torch.int32)            # inclusive scan
-        rec = torch.empty(int(self.n_new), dtype=torch.int32, device=dev)
-        m.smote_bucket(1, *args, ptr(table), ptr(rec), 0, 0, s)      # coarse records
-        off = torch.empty(R + 1, dtype=torch.int32, device=dev)
-        lam = torch.empty(int(self.n_new), dtype=torch.int16, device=dev)
-        m.smote_bucket(2, *args, ptr(table), ptr(rec), ptr(off), ptr(lam), s)
+        m.smote_bucket(0, *args, ptr(table), 0, 0, 0, 0, 0, ptr(bump), s)   # counts [block][bin]
+        table = torch.cumsum(table, 0, dtype=torch.int32)                  # inclusive scan
+        rec = torch.empty(n, dtype=torch.int32, device=dev)
+        m.smote_bucket(1, *args, ptr(table), ptr(rec), 0, 0, 0, 0, ptr(bump), s)  # coarse records
+        tmp = torch.empty(n, dtype=torch.int32, device=dev)
+        off = torch.empty(R, dtype=torch.int32, device=dev)
+        cnt = torch.empty(R, dtype=torch.int32, device=dev)
+        lam = torch.empty(n, dtype=torch.int16, device=dev)
+        m.smote_bucket(2, *args, ptr(table), ptr(rec), ptr(tmp), ptr(off), ptr(cnt), ptr(lam), ptr(bump), s)
+        self.cnt = cnt
         self.lam, self.off = lam, off
         return self
 
@@ -117,6 +123,10 @@ class VirtualSmote:
         return knn_ops.smote_generate(self.parents, self.nbr, self.q_offset, self.n_new, out, seed=self.seed,
                                       counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale,
                                       sample_offset=self.sample_offset)
+
+
+# the per-sample fixed-point terms of the virtual passes hold a positive-class weight <= 32
+VIRTUAL_MAX_WEIGHT = 32.0
 
 
 def virtual_max_picks() -> int:
@@ -313,7 +323,7 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
         nb = ws.nblocks_fp8 if fp8 else ws.nblocks
         m.logreg_pass_virtual(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
                               ptr(ws.partial), nb, s, ptr(v.parents), ptr(v.nbr), ptr(v.lam), ptr(v.off),
-                              int(rows.shape[0]), int(v.q_offset), int(mq), int(k),
+                              ptr(v.cnt), int(rows.shape[0]), int(v.q_offset), int(mq), int(k),
                               float(fp8_scale) if fp8 else 0.0)
     elif storage_kind(rows) == "bf16":
         nb = ws.nblocks
@@ -409,6 +419,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         virtual = None
     if virtual is not None:
         virtual.check(rows)
+        if class_w[1] > VIRTUAL_MAX_WEIGHT:
+            raise ValueError(f"virtual SMOTE: positive class weight {class_w[1]} > {VIRTUAL_MAX_WEIGHT}")
         virtual.prepare()
     if not rows.is_cuda:
         if affine is not None:

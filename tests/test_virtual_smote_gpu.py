@@ -56,13 +56,17 @@ def test_buckets_hold_the_draws(dev):
     _, par, nbr = _case(10, 500, 300, 5, 2, dev)
     v = L.VirtualSmote(par, nbr, 123_457, q_offset=11, sample_offset=384, seed=5, counter_base=7).prepare()
     pick, lam = ref.smote_pick_draws(300, 5, 123_457, 5, 7, 384)
-    off = v.off.cpu().numpy()
-    np.testing.assert_array_equal(np.diff(off), np.bincount(pick, minlength=1500))
+    off, cnt = v.off.cpu().numpy(), v.cnt.cpu().numpy()
+    np.testing.assert_array_equal(cnt, np.bincount(pick, minlength=1500))
     got = v.lam.cpu().numpy().view(np.uint16)
-    order = np.argsort(pick, kind="stable")
-    exp = lam[order].astype(np.uint16)
-    for p in range(0, 1500, 37):  # each bucket holds its picks' lambdas (any order)
-        np.testing.assert_array_equal(np.sort(got[off[p]:off[p + 1]]), np.sort(exp[off[p]:off[p + 1]]))
+    runs = sorted((int(o), int(c)) for o, c in zip(off, cnt) if c)
+    pos = 0
+    for o, c in runs:  # the runs tile lam exactly
+        assert o == pos
+        pos += c
+    assert pos == 123_457
+    for p in range(0, 1500, 37):  # each run holds its pick's lambdas (any order)
+        np.testing.assert_array_equal(np.sort(got[off[p]:off[p] + cnt[p]]), np.sort(lam[pick == p].astype(np.uint16)))
 
 
 @pytest.mark.gpu
