@@ -507,6 +507,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("smote_bucket_bins", &fdx::smote_bucket_bins);
   m.def("smote_bucket_blocks", &fdx::smote_bucket_blocks);
   m.def("smote_bucket_max_picks", []() { return (uint64_t)fdx::kSmoteBucketMaxPicks; });
+  m.def("smote_bucket_max_samples", &fdx::smote_bucket_max_samples);
   m.def("smote_bucket", [](int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
                            uint64_t counter_base, u table, u rec, u tmp, u pstart, u pcnt, u lam, u bump, u s) {
     fdx::launch_smote_bucket(stage, mq, k, n_new, sample_offset, seed, counter_base, P<int>(table),

@@ -130,6 +130,7 @@ struct SmoteView {
 constexpr uint64_t kSmoteBucketMaxPicks = 1ull << 21;  // <= 16384 coarse bins of <= 128 picks
 int smote_bucket_bins(int64_t range, int64_t n_new);
 int smote_bucket_blocks(int64_t n_new);
+int64_t smote_bucket_max_samples();
 void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
                          uint64_t counter_base, int* table, uint32_t* rec, uint32_t* tmp, int* pstart, int* pcnt,
                          uint16_t* lam, unsigned long long* bump, hipStream_t stream);

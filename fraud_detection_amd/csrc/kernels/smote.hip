@@ -242,7 +242,8 @@ __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __
 constexpr int kBucketThreads = 1024;
 constexpr int kBucketPairs = 8192;    // pairs per level-1 block: <= 16384 records staged (64 KiB)
 constexpr int kFineMax = 128;
-constexpr int kStageRecs = 10240;     // level 2: 40 KiB of records + 20 KiB of lambdas
+constexpr int kStageRecs = 8192;      // level 2: 32 KiB of records + 16 KiB of lambdas
+constexpr int kSegMax = 2048;         // level 2: segment table of <= 2048 level-1 blocks in LDS
 
 __device__ __forceinline__ int excl_at(const int* incl, int64_t i) { return i == 0 ? 0 : incl[i - 1]; }
 
@@ -294,37 +295,67 @@ __global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __rest
                                                                int* __restrict__ pcnt, uint16_t* __restrict__ lam,
                                                                unsigned long long* __restrict__ bump) {
   __shared__ int cnt[kFineMax], cur[kFineMax];
-  __shared__ int nrec, gbase;
+  __shared__ int gbase, wsum[16];
+  __shared__ int sstart[kSegMax], spre[kSegMax + 1];
   __shared__ uint32_t srec[kStageRecs];
   __shared__ uint16_t slam[kStageRecs];
   const int bin = blockIdx.x, fine = 1 << fb;
   const uint32_t fmask = (uint32_t)fine - 1u;
+  const int lane = lane_id(), wv = wave_id();
   if (threadIdx.x < kFineMax) cnt[threadIdx.x] = 0;
-  if (threadIdx.x == 0) nrec = 0;
-  __syncthreads();
-  // the bin's total, then its room in lam (bump allocator: one atomic per bin)
-  int mine = 0;
-  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {
-    const int64_t e = (int64_t)b * nbins + bin;
-    mine += excl_at(incl, e + 1) - excl_at(incl, e);
+  // this bin's segment of every level-1 block (start, length), lengths scanned in LDS: then every
+  // thread copies records in parallel (one thread per segment was a chain of dependent loads)
+  constexpr int kPer = kSegMax / 1024;
+  int len[kPer], tot = 0;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int b = threadIdx.x * kPer + u;
+    int l = 0;
+    if (b < nblk) {
+      const int64_t e = (int64_t)b * nbins + bin;
+      const int s0 = excl_at(incl, e);
+      sstart[b] = s0;
+      l = excl_at(incl, e + 1) - s0;
+    }
+    len[u] = l;
+    tot += l;
   }
-  if (mine) atomicAdd(&nrec, mine);
+  int inc = tot;  // block-wide exclusive scan of the per-thread totals
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const int v = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += v;
+  }
+  if (lane == kWave - 1) wsum[wv] = inc;
   __syncthreads();
-  const int n = nrec;
-  if (threadIdx.x == 0) gbase = n ? (int)atomicAdd(bump, (unsigned long long)n) : 0;
+  int before = 0, n = 0;
+  for (int w = 0; w < 16; ++w) {
+    if (w < wv) before += wsum[w];
+    n += wsum[w];
+  }
+  int run = before + inc - tot;
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int b = threadIdx.x * kPer + u;
+    if (b < nblk) spre[b] = run;
+    run += len[u];
+  }
+  if (threadIdx.x == 0) {
+    spre[nblk] = n;
+    gbase = n ? (int)atomicAdd(bump, (unsigned long long)n) : 0;  // the bin's room in lam
+  }
   __syncthreads();
   const int g0 = gbase;
   const bool staged = n <= kStageRecs;
   uint32_t* R = staged ? srec : tmp + g0;  // unstaged: the bin's records gathered in global scratch
-  if (threadIdx.x == 0) nrec = 0;
-  __syncthreads();
-  for (int b = threadIdx.x; b < nblk; b += blockDim.x) {  // gather every level-1 block's segment
-    const int64_t e = (int64_t)b * nbins + bin;
-    const int s0 = excl_at(incl, e), s1 = excl_at(incl, e + 1);
-    if (s1 > s0) {
-      const int p0 = atomicAdd(&nrec, s1 - s0);
-      for (int i = s0; i < s1; ++i) R[p0 + i - s0] = rec[i];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    int lo = 0, hi = nblk;  // the segment holding record i: spre[lo] <= i < spre[lo + 1]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (spre[mid] <= i) lo = mid;
+      else hi = mid;
     }
+    R[i] = rec[sstart[lo] + (i - spre[lo])];
   }
   __syncthreads();
   for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(cnt + (R[i] & fmask), 1);
@@ -378,6 +409,7 @@ int smote_bucket_bins(int64_t range, int64_t n_new) {
   const int fb = smote_bucket_fine_bits(range, n_new);
   return (int)((range + (1ll << fb) - 1) >> fb);
 }
+int64_t smote_bucket_max_samples() { return (int64_t)kSegMax * 2 * kBucketPairs; }
 int smote_bucket_blocks(int64_t n_new) {
   const int64_t npairs = ((n_new + 127) >> 7) << 6;
   return (int)std::max<int64_t>(1, (npairs + kBucketPairs - 1) / kBucketPairs);
@@ -397,6 +429,7 @@ void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample
   const int fb = smote_bucket_fine_bits((int64_t)R, n_new);
   const int nbins = smote_bucket_bins((int64_t)R, n_new);
   const int nblk = smote_bucket_blocks(n_new);
+  if (nblk > kSegMax) throw std::runtime_error("smote_bucket: too many samples for the level-2 segment table");
   if (stage == 0) {
     smote_bucket_l1_kernel<false><<<nblk, kBucketThreads, (size_t)nbins * sizeof(int), stream>>>(
         (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec, bump);

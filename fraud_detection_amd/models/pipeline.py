@@ -362,7 +362,8 @@ class DevicePipeline:
             if n_new > 0:
                 if parents is None:
                     parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
-                if virt_ok and nbr.numel() <= lr_ops.virtual_max_picks():  # folded into every Newton pass
+                if (virt_ok and nbr.numel() <= lr_ops.virtual_max_picks()
+                        and n_new <= lr_ops.virtual_max_samples()):  # folded into every Newton pass
                     virt = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, q_offset=q_off, sample_offset=s_off,
                                                seed=cfg.seed, counter_base=0 if glob else rank)
                 else:

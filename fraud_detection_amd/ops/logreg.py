@@ -78,8 +78,8 @@ class VirtualSmote:
             raise ValueError("n_new >= 0 and sample_offset a non-negative multiple of 128")
         if self.n_new and (mq < 1 or k < 1 or self.q_offset < 0 or self.q_offset + mq > p.shape[0]):
             raise ValueError("query rows out of range of the parents")
-        if mq * k > native().smote_bucket_max_picks():
-            raise ValueError("virtual SMOTE: mq * k exceeds the bucket sort's range")
+        if mq * k > virtual_max_picks() or self.n_new > virtual_max_samples():
+            raise ValueError("virtual SMOTE: picks or samples exceed the bucket sort's range")
         ref.smote_check_ranges(p.shape[0], mq, k)
 
     def prepare(self) -> "VirtualSmote":
@@ -132,6 +132,11 @@ VIRTUAL_MAX_WEIGHT = 32.0
 def virtual_max_picks() -> int:
     """Largest minority-rows x k that VirtualSmote's bucket sort handles (else SMOTE is stored)."""
     return int(native().smote_bucket_max_picks())
+
+
+def virtual_max_samples() -> int:
+    """Largest per-rank SMOTE sample count VirtualSmote's bucket sort handles."""
+    return int(native().smote_bucket_max_samples())
 
 
 _FIT_FIELDS = ("w", "n_iter", "n_newton_steps", "converged", "objective", "grad_max", "history")
