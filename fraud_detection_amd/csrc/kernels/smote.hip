@@ -242,8 +242,10 @@ __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __
 constexpr int kBucketThreads = 1024;
 constexpr int kBucketPairs = 8192;    // pairs per level-1 block: <= 16384 records staged (64 KiB)
 constexpr int kFineMax = 128;
-constexpr int kStageRecs = 8192;      // level 2: 32 KiB of records + 16 KiB of lambdas
-constexpr int kSegMax = 2048;         // level 2: segment table of <= 2048 level-1 blocks in LDS
+constexpr int kStageRecs = 6144;      // level 2: 24 KiB of records + 12 KiB of lambdas
+constexpr int kSegMax = 1024;         // level 2: segment table of <= 1024 level-1 blocks in LDS
+constexpr int kL2Threads = 256;       // ~44 KiB of LDS: 3 level-2 blocks per CU overlap their latencies
+constexpr int kL2Waves = kL2Threads / 64;
 
 __device__ __forceinline__ int excl_at(const int* incl, int64_t i) { return i == 0 ? 0 : incl[i - 1]; }
 
@@ -289,23 +291,25 @@ __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_
   }
 }
 
-__global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __restrict__ incl, int nblk, int nbins,
+__global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* __restrict__ incl, int nblk, int nbins,
                                                                uint32_t range, int fb, const uint32_t* __restrict__ rec,
                                                                uint32_t* __restrict__ tmp, int* __restrict__ pstart,
                                                                int* __restrict__ pcnt, uint16_t* __restrict__ lam,
                                                                unsigned long long* __restrict__ bump) {
   __shared__ int cnt[kFineMax], cur[kFineMax];
-  __shared__ int gbase, wsum[16];
+  __shared__ int whist[kL2Waves][kFineMax];  // per-wave fine counts, then per-wave cursors: ~16x less
+                                       // same-address LDS atomic contention than one shared set
+  __shared__ int gbase, wsum[kL2Waves];
   __shared__ int sstart[kSegMax], spre[kSegMax + 1];
   __shared__ uint32_t srec[kStageRecs];
   __shared__ uint16_t slam[kStageRecs];
   const int bin = blockIdx.x, fine = 1 << fb;
   const uint32_t fmask = (uint32_t)fine - 1u;
   const int lane = lane_id(), wv = wave_id();
-  if (threadIdx.x < kFineMax) cnt[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < kL2Waves * kFineMax; i += blockDim.x) whist[i / kFineMax][i % kFineMax] = 0;
   // this bin's segment of every level-1 block (start, length), lengths scanned in LDS: then every
   // thread copies records in parallel (one thread per segment was a chain of dependent loads)
-  constexpr int kPer = kSegMax / 1024;
+  constexpr int kPer = kSegMax / kL2Threads;
   int len[kPer], tot = 0;
 #pragma unroll
   for (int u = 0; u < kPer; ++u) {
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __rest
   if (lane == kWave - 1) wsum[wv] = inc;
   __syncthreads();
   int before = 0, n = 0;
-  for (int w = 0; w < 16; ++w) {
+  for (int w = 0; w < kL2Waves; ++w) {
     if (w < wv) before += wsum[w];
     n += wsum[w];
   }
@@ -358,7 +362,13 @@ __global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __rest
     R[i] = rec[sstart[lo] + (i - spre[lo])];
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(cnt + (R[i] & fmask), 1);
+  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&whist[wv][R[i] & fmask], 1);
+  __syncthreads();
+  if (threadIdx.x < fine) {
+    int c = 0;
+    for (int w = 0; w < kL2Waves; ++w) c += whist[w][threadIdx.x];
+    cnt[threadIdx.x] = c;
+  }
   __syncthreads();
   if (threadIdx.x < kWave) {  // exclusive scan of <= 128 fine counts by one wave (2 per lane)
     const int l = threadIdx.x;
@@ -382,9 +392,18 @@ __global__ __launch_bounds__(1024) void smote_bucket_l2_kernel(const int* __rest
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+  if (threadIdx.x < fine) {  // wave w's records of pick f go to [cur[f] + sum_{w' < w} whist[w'][f], ...)
+    int run = cur[threadIdx.x];
+    for (int w = 0; w < kL2Waves; ++w) {
+      const int c = whist[w][threadIdx.x];
+      whist[w][threadIdx.x] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {  // same record -> wave mapping as the count
     const uint32_t r = R[i];
-    const int pos = atomicAdd(cur + (r & fmask), 1);
+    const int pos = atomicAdd(&whist[wv][r & fmask], 1);
     if (staged) slam[pos] = (uint16_t)(r >> 16);
     else lam[g0 + pos] = (uint16_t)(r >> 16);
   }
@@ -444,7 +463,7 @@ void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample
     smote_bucket_l1_kernel<true><<<nblk, kBucketThreads, lds, stream>>>(
         (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec, bump);
   } else {
-    smote_bucket_l2_kernel<<<nbins, 1024, 0, stream>>>(table, nblk, nbins, (uint32_t)R, fb, rec, tmp, pstart, pcnt,
+    smote_bucket_l2_kernel<<<nbins, kL2Threads, 0, stream>>>(table, nblk, nbins, (uint32_t)R, fb, rec, tmp, pstart, pcnt,
                                                        lam, bump);
   }
   check_launch("smote_bucket");
