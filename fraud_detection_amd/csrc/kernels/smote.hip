@@ -242,9 +242,11 @@ __global__ __launch_bounds__(kThreads) void smote_parents_kernel(const float* __
 constexpr int kBucketThreads = 1024;
 constexpr int kBucketPairs = 8192;    // pairs per level-1 block: <= 16384 records staged (64 KiB)
 constexpr int kFineMax = 128;
-constexpr int kStageRecs = 6144;      // level 2: 24 KiB of records + 12 KiB of lambdas
-constexpr int kSegMax = 1024;         // level 2: segment table of <= 1024 level-1 blocks in LDS
-constexpr int kL2Threads = 256;       // ~44 KiB of LDS: 3 level-2 blocks per CU overlap their latencies
+constexpr int kStageRecs = 8192;      // level 2: 32 KiB of records + 16 KiB of lambdas
+constexpr int kSegMax = 2048;         // level 2: segment table of <= 2048 level-1 blocks in LDS
+// level 2 block size: 1024 threads (57-60 us at the bench shape) -- 256-thread blocks at 3 per CU
+// measured 84 us (profiles/r3_virt/timeline_r3_v9.txt)
+constexpr int kL2Threads = 1024;
 constexpr int kL2Waves = kL2Threads / 64;
 
 __device__ __forceinline__ int excl_at(const int* incl, int64_t i) { return i == 0 ? 0 : incl[i - 1]; }
@@ -297,8 +299,8 @@ __global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* 
                                                                int* __restrict__ pcnt, uint16_t* __restrict__ lam,
                                                                unsigned long long* __restrict__ bump) {
   __shared__ int cnt[kFineMax], cur[kFineMax];
-  __shared__ int whist[kL2Waves][kFineMax];  // per-wave fine counts, then per-wave cursors: ~16x less
-                                       // same-address LDS atomic contention than one shared set
+  __shared__ int whist[kL2Waves][kFineMax];  // per-wave fine counts, then per-wave cursors (less
+                                             // same-address LDS atomic contention)
   __shared__ int gbase, wsum[kL2Waves];
   __shared__ int sstart[kSegMax], spre[kSegMax + 1];
   __shared__ uint32_t srec[kStageRecs];
