@@ -509,11 +509,10 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("smote_bucket_max_picks", []() { return (uint64_t)fdx::kSmoteBucketMaxPicks; });
   m.def("smote_bucket_max_samples", &fdx::smote_bucket_max_samples);
   m.def("smote_bucket", [](int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
-                           uint64_t counter_base, u table, u rec, u tmp, u pstart, u pcnt, u lam, u bump, u seg,
-                           u s) {
+                           uint64_t counter_base, u table, u rec, u tmp, u pstart, u pcnt, u lam, u bump, u s) {
     fdx::launch_smote_bucket(stage, mq, k, n_new, sample_offset, seed, counter_base, P<int>(table),
                              P<uint32_t>(rec), P<uint32_t>(tmp), P<int>(pstart), P<int>(pcnt), P<uint16_t>(lam),
-                             P<unsigned long long>(bump), P<int>(seg), S(s));
+                             P<unsigned long long>(bump), S(s));
   });
   m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
                               u partial, int nblocks, u s) {

@@ -126,15 +126,14 @@ struct SmoteView {
 // stage 0 fills it with per-(block, bin) counts (and zeroes *bump), the caller scans it
 // inclusively in place, stage 1 writes the coarse records rec (uint32 [n_new]), stage 2 writes
 // each pick's lambda run (pstart, pcnt: int32 [mq k]) into lam (uint16 [n_new]); tmp (uint32
-// [n_new]) is scratch for bins too big for the LDS stage, seg (int32 [2 * blocks * bins]) holds
-// the bin-major segment table.
+// [n_new]) is scratch for bins too big for the LDS stage.
 constexpr uint64_t kSmoteBucketMaxPicks = 1ull << 21;  // <= 16384 coarse bins of <= 128 picks
 int smote_bucket_bins(int64_t range, int64_t n_new);
 int smote_bucket_blocks(int64_t n_new);
 int64_t smote_bucket_max_samples();
 void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
                          uint64_t counter_base, int* table, uint32_t* rec, uint32_t* tmp, int* pstart, int* pcnt,
-                         uint16_t* lam, unsigned long long* bump, int* seg, hipStream_t stream);
+                         uint16_t* lam, unsigned long long* bump, hipStream_t stream);
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr);

@@ -293,33 +293,7 @@ __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_
   }
 }
 
-// Block-major inclusive offsets -> bin-major (start, length) of every (bin, level-1 block)
-// segment, through 32 x 32 LDS tiles: level 2 then reads its bin's row contiguously (strided
-// reads of the block-major table were 2M distinct cache lines at the bench shape).
-__global__ __launch_bounds__(1024) void smote_bucket_transpose_kernel(const int* __restrict__ incl, int nblk, int nbins,
-                                                                      int* __restrict__ sstart, int* __restrict__ slen) {
-  __shared__ int ts[32][33], tl[32][33];
-  const int bx = blockIdx.x * 32, by = blockIdx.y * 32;  // bins, blocks
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  {
-    const int bin = bx + tx, blk = by + ty;
-    if (bin < nbins && blk < nblk) {
-      const int64_t e = (int64_t)blk * nbins + bin;
-      const int s0 = excl_at(incl, e);
-      ts[ty][tx] = s0;
-      tl[ty][tx] = incl[e] - s0;
-    }
-  }
-  __syncthreads();
-  const int blk = by + tx, bin = bx + ty;
-  if (bin < nbins && blk < nblk) {
-    sstart[(int64_t)bin * nblk + blk] = ts[tx][ty];
-    slen[(int64_t)bin * nblk + blk] = tl[tx][ty];
-  }
-}
-
-__global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* __restrict__ gstart,
-                                                                     const int* __restrict__ glen, int nblk, int nbins,
+__global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* __restrict__ incl, int nblk, int nbins,
                                                                uint32_t range, int fb, const uint32_t* __restrict__ rec,
                                                                uint32_t* __restrict__ tmp, int* __restrict__ pstart,
                                                                int* __restrict__ pcnt, uint16_t* __restrict__ lam,
@@ -344,8 +318,10 @@ __global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* 
     const int b = threadIdx.x * kPer + u;
     int l = 0;
     if (b < nblk) {
-      sstart[b] = gstart[(int64_t)bin * nblk + b];
-      l = glen[(int64_t)bin * nblk + b];
+      const int64_t e = (int64_t)b * nbins + bin;
+      const int s0 = excl_at(incl, e);
+      sstart[b] = s0;
+      l = excl_at(incl, e + 1) - s0;
     }
     len[u] = l;
     tot += l;
@@ -462,7 +438,7 @@ int smote_bucket_blocks(int64_t n_new) {
 
 void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
                          uint64_t counter_base, int* table, uint32_t* rec, uint32_t* tmp, int* pstart, int* pcnt,
-                         uint16_t* lam, unsigned long long* bump, int* seg, hipStream_t stream) {
+                         uint16_t* lam, unsigned long long* bump, hipStream_t stream) {
   if (n_new <= 0) return;
   if (sample_offset < 0 || (sample_offset & 127) != 0)
     throw std::runtime_error("smote_bucket: sample_offset must be a non-negative multiple of 128");
@@ -489,13 +465,8 @@ void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample
     smote_bucket_l1_kernel<true><<<nblk, kBucketThreads, lds, stream>>>(
         (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec, bump);
   } else {
-    // seg: int32 [2][nbins * nblk] bin-major segment starts and lengths (the caller's scratch)
-    int* gstart = seg;
-    int* glen = seg + (int64_t)nbins * nblk;
-    const dim3 tg((unsigned)((nbins + 31) / 32), (unsigned)((nblk + 31) / 32));
-    smote_bucket_transpose_kernel<<<tg, 1024, 0, stream>>>(table, nblk, nbins, gstart, glen);
-    smote_bucket_l2_kernel<<<nbins, kL2Threads, 0, stream>>>(gstart, glen, nblk, nbins, (uint32_t)R, fb, rec, tmp,
-                                                             pstart, pcnt, lam, bump);
+    smote_bucket_l2_kernel<<<nbins, kL2Threads, 0, stream>>>(table, nblk, nbins, (uint32_t)R, fb, rec, tmp, pstart, pcnt,
+                                                       lam, bump);
   }
   check_launch("smote_bucket");
 }

@@ -97,16 +97,15 @@ class VirtualSmote:
         bump = torch.empty(1, dtype=torch.int64, device=dev)      # zeroed by stage 0
         args = (mq, k, n, int(self.sample_offset), int(self.seed) & (2**64 - 1),
                 int(self.counter_base) & (2**64 - 1))
-        m.smote_bucket(0, *args, ptr(table), 0, 0, 0, 0, 0, ptr(bump), 0, s)   # counts [block][bin]
-        table = torch.cumsum(table, 0, dtype=torch.int32)                     # inclusive scan
+        m.smote_bucket(0, *args, ptr(table), 0, 0, 0, 0, 0, ptr(bump), s)   # counts [block][bin]
+        table = torch.cumsum(table, 0, dtype=torch.int32)                  # inclusive scan
         rec = torch.empty(n, dtype=torch.int32, device=dev)
-        m.smote_bucket(1, *args, ptr(table), ptr(rec), 0, 0, 0, 0, ptr(bump), 0, s)  # coarse records
+        m.smote_bucket(1, *args, ptr(table), ptr(rec), 0, 0, 0, 0, ptr(bump), s)  # coarse records
         tmp = torch.empty(n, dtype=torch.int32, device=dev)
-        seg = torch.empty(2 * nt, dtype=torch.int32, device=dev)
         off = torch.empty(R, dtype=torch.int32, device=dev)
         cnt = torch.empty(R, dtype=torch.int32, device=dev)
         lam = torch.empty(n, dtype=torch.int16, device=dev)
-        m.smote_bucket(2, *args, ptr(table), ptr(rec), ptr(tmp), ptr(off), ptr(cnt), ptr(lam), ptr(bump), ptr(seg), s)
+        m.smote_bucket(2, *args, ptr(table), ptr(rec), ptr(tmp), ptr(off), ptr(cnt), ptr(lam), ptr(bump), s)
         self.cnt = cnt
         self.lam, self.off = lam, off
         return self
