@@ -364,8 +364,9 @@ class DevicePipeline:
                     parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
                 if (virt_ok and nbr.numel() <= lr_ops.virtual_max_picks()
                         and n_new <= lr_ops.virtual_max_samples()):  # folded into every Newton pass
+                    # the once-per-fit bucket sort of the samples' lambdas, timed as the SMOTE phase
                     virt = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, q_offset=q_off, sample_offset=s_off,
-                                               seed=cfg.seed, counter_base=0 if glob else rank)
+                                               seed=cfg.seed, counter_base=0 if glob else rank).prepare()
                 else:
                     knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
                                            counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,
