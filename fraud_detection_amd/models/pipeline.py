@@ -65,7 +65,7 @@ class TrainConfig:
     # of the ranks' synthetic rows equals the one-process SMOTE output bit for bit; "shard" = each
     # rank oversamples its own minority rows (per-partition SMOTE: constant work per rank)
     smote_scope: str = "global"
-    # Newton on device rows (bf16 or fp8): the SMOTE rows are never stored -- every logistic pass
+    # Newton on bf16 device rows: the SMOTE rows are never stored -- every logistic pass
     # regenerates them from their Philox draws out of the L2-resident minority parents
     # (ops/logreg.VirtualSmote), bitwise the rows smote_generate would write.  At the bench shape
     # half the training rows are synthetic: no 512 MB SMOTE write and half the bytes per pass.
@@ -327,7 +327,10 @@ class DevicePipeline:
             pos = float(sum(r[0] + q for r, q in zip(ranks, new_per_rank)))
             class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         virt = None
-        virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage in ("bf16", "fp8")
+        # bf16 rows only: with 32-byte fp8 rows the stored SMOTE rows are cheap to stream and the
+        # fp8 fit measured faster stored (c5 shard 1.404 vs 1.594 ms, profiles/r3_fin3); the fp8
+        # pass still takes virtual samples (ops/logreg.VirtualSmote, tested against the oracle)
+        virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage == "bf16"
                    and dev.type == "cuda" and class_w[1] <= lr_ops.VIRTUAL_MAX_WEIGHT)
         tm.mark("scale_cast")
         # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a

@@ -108,7 +108,7 @@ def test_virtual_newton_fit_reproducible_and_close(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("storage", ["bf16", "fp8"])
+@pytest.mark.parametrize("storage", ["bf16"])  # fp8 fits keep stored SMOTE rows (pipeline.py virt_ok)
 def test_pipeline_virtual_vs_stored_smote(dev, storage):
     X, y = separable(600_000, fraud_rate=0.01, seed=12)
     Xt, yt = separable(200_000, fraud_rate=0.01, seed=13)
