@@ -139,6 +139,8 @@ class DevicePipeline:
         self._bi = self._cur = 0
         self._full_pred = None  # (signature, full-data iterations of the last settled fit)
         self._virtual = None    # VirtualSmote of the latest fit (None: its SMOTE rows are stored)
+        # its bucket buffers, one set per training buffer (a fit's set is reused once it is settled)
+        self._bws = [lr_ops.BucketWorkspace(), lr_ops.BucketWorkspace()]
         self._defer_now = False
 
     def _world(self):
@@ -369,7 +371,8 @@ class DevicePipeline:
                         and n_new <= lr_ops.virtual_max_samples()):  # folded into every Newton pass
                     # the once-per-fit bucket sort of the samples' lambdas, timed as the SMOTE phase
                     virt = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, q_offset=q_off, sample_offset=s_off,
-                                               seed=cfg.seed, counter_base=0 if glob else rank).prepare()
+                                               seed=cfg.seed, counter_base=0 if glob else rank
+                                               ).prepare(self._bws[self._cur])
                 else:
                     knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
                                            counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,

@@ -82,32 +82,28 @@ class VirtualSmote:
             raise ValueError("virtual SMOTE: picks or samples exceed the bucket sort's range")
         ref.smote_check_ranges(p.shape[0], mq, k)
 
-    def prepare(self) -> "VirtualSmote":
-        """Bucket the samples' lambdas by pick on the parents' device: count, scan, fill."""
+    def prepare(self, ws: "BucketWorkspace | None" = None) -> "VirtualSmote":
+        """Bucket the samples' lambdas by pick on the parents' device: count, scan, fill.
+        ``ws``: reusable buffers (a training loop passes one per in-flight fit), so a fit
+        allocates nothing here."""
         if self.off is not None or self.n_new == 0:
             return self
         m = native()
         mq, k = self.nbr.shape
         R = mq * k
-        dev = self.parents.device
         s = stream_of(self.parents)
         n = int(self.n_new)
         nt = m.smote_bucket_bins(R, n) * m.smote_bucket_blocks(n)
-        table = torch.empty(nt, dtype=torch.int32, device=dev)   # every entry written by stage 0
-        bump = torch.empty(1, dtype=torch.int64, device=dev)      # zeroed by stage 0
+        w = (ws or BucketWorkspace()).get(self.parents.device, nt, n, R)
         args = (mq, k, n, int(self.sample_offset), int(self.seed) & (2**64 - 1),
                 int(self.counter_base) & (2**64 - 1))
-        m.smote_bucket(0, *args, ptr(table), 0, 0, 0, 0, 0, ptr(bump), s)   # counts [block][bin]
-        table = torch.cumsum(table, 0, dtype=torch.int32)                  # inclusive scan
-        rec = torch.empty(n, dtype=torch.int32, device=dev)
-        m.smote_bucket(1, *args, ptr(table), ptr(rec), 0, 0, 0, 0, ptr(bump), s)  # coarse records
-        tmp = torch.empty(n, dtype=torch.int32, device=dev)
-        off = torch.empty(R, dtype=torch.int32, device=dev)
-        cnt = torch.empty(R, dtype=torch.int32, device=dev)
-        lam = torch.empty(n, dtype=torch.int16, device=dev)
-        m.smote_bucket(2, *args, ptr(table), ptr(rec), ptr(tmp), ptr(off), ptr(cnt), ptr(lam), ptr(bump), s)
-        self.cnt = cnt
-        self.lam, self.off = lam, off
+        # stage 0 writes every table entry (no fill) and zeroes the bump allocator
+        m.smote_bucket(0, *args, ptr(w.table), 0, 0, 0, 0, 0, ptr(w.bump), s)        # counts [block][bin]
+        torch.cumsum(w.table[:nt], 0, dtype=torch.int32, out=w.scan[:nt])          # inclusive scan
+        m.smote_bucket(1, *args, ptr(w.scan), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # coarse records
+        m.smote_bucket(2, *args, ptr(w.scan), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
+                       ptr(w.bump), s)
+        self.lam, self.off, self.cnt, self._ws = w.lam, w.off, w.cnt, w
         return self
 
     def rows_f32(self) -> torch.Tensor:
@@ -123,6 +119,27 @@ class VirtualSmote:
         return knn_ops.smote_generate(self.parents, self.nbr, self.q_offset, self.n_new, out, seed=self.seed,
                                       counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale,
                                       sample_offset=self.sample_offset)
+
+
+class BucketWorkspace:
+    """Device buffers of VirtualSmote.prepare, grown on demand and reused fit to fit."""
+
+    def __init__(self):
+        self.cap, self.dev = None, None
+
+    def get(self, dev, nt: int, n: int, R: int) -> "BucketWorkspace":
+        if self.cap is None or self.dev != dev or nt > self.cap[0] or n > self.cap[1] or R > self.cap[2]:
+            i32 = torch.int32
+            self.table = torch.empty(nt, dtype=i32, device=dev)
+            self.scan = torch.empty(nt, dtype=i32, device=dev)
+            self.bump = torch.empty(1, dtype=torch.int64, device=dev)
+            self.rec = torch.empty(n, dtype=i32, device=dev)
+            self.tmp = torch.empty(n, dtype=i32, device=dev)
+            self.lam = torch.empty(n, dtype=torch.int16, device=dev)
+            self.off = torch.empty(R, dtype=i32, device=dev)
+            self.cnt = torch.empty(R, dtype=i32, device=dev)
+            self.cap, self.dev = (nt, n, R), dev
+        return self
 
 
 # the per-sample fixed-point terms of the virtual passes hold a positive-class weight <= 32
