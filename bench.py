@@ -264,8 +264,11 @@ def _variants(args, X, y, Xt, yt, dev, comm, scope) -> dict:
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
 
     out = {}
-    for name, kw in (("sgd_bf16", dict(solver="sgd", storage="bf16")), ("newton_fp8", dict(solver="newton", storage="fp8"))):
-        if kw["solver"] == args.solver and kw["storage"] == args.storage:
+    # newton_bf16_stored_smote: the headline fit with its SMOTE rows written and streamed (the
+    # headline folds them into the passes instead: TrainConfig.virtual_smote)
+    for name, kw in (("sgd_bf16", dict(solver="sgd", storage="bf16")), ("newton_fp8", dict(solver="newton", storage="fp8")),
+                     ("newton_bf16_stored_smote", dict(solver="newton", storage="bf16", virtual_smote=False))):
+        if kw["solver"] == args.solver and kw["storage"] == args.storage and kw.get("virtual_smote", True):
             continue
         pipe = DevicePipeline(TrainConfig(seed=42, smote_scope=scope, **kw), comm)
         # the headline's own --steps / --warmup: variant numbers as stable as the headline's
