@@ -361,10 +361,11 @@ __global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* 
       if (spre[mid] <= i) lo = mid;
       else hi = mid;
     }
-    R[i] = rec[sstart[lo] + (i - spre[lo])];
+    const uint32_t r = rec[sstart[lo] + (i - spre[lo])];
+    R[i] = r;
+    atomicAdd(&whist[wv][r & fmask], 1);  // fine count in the same pass (same record -> wave map
+                                          // as the scatter below)
   }
-  __syncthreads();
-  for (int i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&whist[wv][R[i] & fmask], 1);
   __syncthreads();
   if (threadIdx.x < fine) {
     int c = 0;
