@@ -425,12 +425,13 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
   m.def("scaler_stats_cast_blocks", [](int fp8) { return fdx::scaler_stats_cast_blocks(fp8); }, py::arg("fp8") = 0);
   m.def("scaler_stats_cast", [](u X, int64_t n, int d, u pivot, u labels, float bias_value, u out, u partial,
-                                int nblocks, u s, u colscale, float out_scale) {
+                                int nblocks, u s, u colscale, float out_scale, u idx) {
     fdx::launch_scaler_stats_cast(P<const float>(X), n, d, P<const float>(pivot), P<const uint8_t>(labels), bias_value,
-                                  P<void>(out), P<double>(partial), nblocks, S(s), P<const float>(colscale), out_scale);
+                                  P<void>(out), P<double>(partial), nblocks, S(s), P<const float>(colscale), out_scale,
+                                  P<const int64_t>(idx));
   }, py::arg("X"), py::arg("n"), py::arg("d"), py::arg("pivot"), py::arg("labels"), py::arg("bias_value"),
      py::arg("out"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("colscale") = 0,
-     py::arg("out_scale") = 1.0f);
+     py::arg("out_scale") = 1.0f, py::arg("idx") = 0);
   m.def("scale_cast", [](u X, int64_t n, int ld, int d, u idx, u mean32, u inv32, u labels, float bias_value,
                          float out_scale, int out_kind, u out, u s) {
     fdx::launch_scale_cast(P<const float>(X), n, ld, d, P<const int64_t>(idx), P<const float>(mean32),
@@ -474,19 +475,32 @@ PYBIND11_MODULE(_fdx_native, m) {
     stream_sync(s);
   }, py::call_guard<py::gil_scoped_release>());
 
+  m.def("predict_gather_logit", [](u X, u idx, int64_t n, int d, u w, u mean, u scale, u logit, u s) {
+    fdx::launch_predict_gather_logit(P<const float>(X), P<const int64_t>(idx), n, d, P<const double>(w),
+                                     P<const double>(mean), P<const double>(scale), P<float>(logit), S(s));
+  });
+
   // logistic regression
   m.def("logreg_pass_blocks", &fdx::logreg_pass_blocks, py::arg("fmt") = 0);
-  m.def("logreg_pass", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
-                          int nblocks, u s) {
+  auto hole_of = [](int64_t at, int64_t len) {
+    fdx::RowHole h;
+    h.at = at;
+    h.len = len;
+    return h;
+  };
+  m.def("logreg_pass", [hole_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
+                                 int nblocks, u s, int phase, bool fisher, int64_t hole_at, int64_t hole_len) {
     fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
-                            hess, sub, P<float>(partial), nblocks, S(s));
-  });
-  // the same pass over stored rows [0, n_real) + virtual SMOTE rows [n_real, re) (launchers.h SmoteView)
+                            hess, sub, P<float>(partial), nblocks, S(s), nullptr, phase, fisher, hole_of(hole_at, hole_len));
+  }, py::arg("X"), py::arg("rb"), py::arg("re"), py::arg("w"), py::arg("cw"), py::arg("done"), py::arg("hess"),
+     py::arg("sub"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("phase") = 0,
+     py::arg("fisher") = false, py::arg("hole_at") = 0, py::arg("hole_len") = 0);
   // the same pass over the stored rows [0, n_real) plus virtual SMOTE samples (launchers.h
   // SmoteView); x_scale > 0 selects the fp8 row pass
-  m.def("logreg_pass_virtual", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
-                                  int nblocks, u s, u parents, u nbr, u lam, u off, u cnt, int64_t n_real,
-                                  int64_t q_offset, int mq, int k, float x_scale) {
+  m.def("logreg_pass_virtual", [hole_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub,
+                                         u partial, int nblocks, u s, u parents, u nbr, u lam, u off, u cnt,
+                                         int64_t n_real, int64_t q_offset, int mq, int k, float x_scale, int phase,
+                                         bool fisher, int64_t hole_at, int64_t hole_len) {
     fdx::SmoteView v;
     v.parents = P<const uint16_t>(parents);
     v.nbr = P<const int>(nbr);
@@ -499,11 +513,17 @@ PYBIND11_MODULE(_fdx_native, m) {
     v.k = k;
     if (x_scale > 0.0f)
       fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
-                                  P<const int>(done), hess, sub, x_scale, P<float>(partial), nblocks, S(s), &v);
+                                  P<const int>(done), hess, sub, x_scale, P<float>(partial), nblocks, S(s), &v, phase,
+                                  fisher, hole_of(hole_at, hole_len));
     else
       fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw),
-                              P<const int>(done), hess, sub, P<float>(partial), nblocks, S(s), &v);
-  });
+                              P<const int>(done), hess, sub, P<float>(partial), nblocks, S(s), &v, phase, fisher,
+                              hole_of(hole_at, hole_len));
+  }, py::arg("X"), py::arg("rb"), py::arg("re"), py::arg("w"), py::arg("cw"), py::arg("done"), py::arg("hess"),
+     py::arg("sub"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("parents"), py::arg("nbr"),
+     py::arg("lam"), py::arg("off"), py::arg("cnt"), py::arg("n_real"), py::arg("q_offset"), py::arg("mq"),
+     py::arg("k"), py::arg("x_scale"), py::arg("phase") = 0, py::arg("fisher") = false, py::arg("hole_at") = 0,
+     py::arg("hole_len") = 0);
   m.def("smote_bucket_bins", &fdx::smote_bucket_bins);
   m.def("smote_bucket_blocks", &fdx::smote_bucket_blocks);
   m.def("smote_bucket_max_picks", []() { return (uint64_t)fdx::kSmoteBucketMaxPicks; });
@@ -514,11 +534,15 @@ PYBIND11_MODULE(_fdx_native, m) {
                              P<uint32_t>(rec), P<uint32_t>(tmp), P<int>(pstart), P<int>(pcnt), P<uint16_t>(lam),
                              P<unsigned long long>(bump), S(s));
   });
-  m.def("logreg_pass_fp8", [](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
-                              u partial, int nblocks, u s) {
+  m.def("logreg_pass_fp8", [hole_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
+                                     u partial, int nblocks, u s, int phase, bool fisher, int64_t hole_at,
+                                     int64_t hole_len) {
     fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
-                                P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s));
-  });
+                                P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s), nullptr, phase,
+                                fisher, hole_of(hole_at, hole_len));
+  }, py::arg("X"), py::arg("rb"), py::arg("re"), py::arg("w"), py::arg("cw"), py::arg("done"), py::arg("hess"),
+     py::arg("sub"), py::arg("xs"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("phase") = 0,
+     py::arg("fisher") = false, py::arg("hole_at") = 0, py::arg("hole_len") = 0);
   m.def("newton_update_stamped", [](u red, u state, u w32, u done, double C, u aff, u stamps, u s) {
     fdx::launch_newton_update_stamped(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), C,
                                       P<const double>(aff), P<unsigned long long>(stamps), S(s));
@@ -550,11 +574,22 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("logreg_fold", [](u state, u aff, u w32, u s) {
     fdx::launch_logreg_fold(P<const double>(state), P<const double>(aff), P<float>(w32), S(s));
   });
-  m.def("sgd_update", [](u red, u state, u w32, int d, double C, double lr, double mom, int fi, u s, u aff) {
-    fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), d, C, lr, mom, fi, S(s),
-                           P<const double>(aff));
-  }, py::arg("red"), py::arg("state"), py::arg("w32"), py::arg("d"), py::arg("C"), py::arg("lr"), py::arg("mom"),
-     py::arg("fi"), py::arg("s"), py::arg("aff") = 0);
+  auto sgd_args = [](int d, double C, double c, double mom, int fi, int nb, int avg, int epoch_end, double tol) {
+    fdx::SgdArgs a;
+    a.d = d; a.C = C; a.c = c; a.momentum = mom; a.fit_intercept = fi; a.nb = nb; a.avg = avg;
+    a.epoch_end = epoch_end; a.tol = tol;
+    return a;
+  };
+  m.def("sgd_step", [sgd_args](u partial, int nblocks, u state, u w32, u done, u aff, int d, double C, double c,
+                               double mom, int fi, int nb, int avg, int epoch_end, double tol, u s) {
+    fdx::launch_sgd_step(P<const float>(partial), nblocks, P<double>(state), P<float>(w32), P<int>(done),
+                         P<const double>(aff), sgd_args(d, C, c, mom, fi, nb, avg, epoch_end, tol), S(s));
+  });
+  m.def("sgd_update", [sgd_args](u red, u state, u w32, u done, u aff, int d, double C, double c, double mom, int fi,
+                                 int nb, int avg, int epoch_end, double tol, u s) {
+    fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), P<const double>(aff),
+                           sgd_args(d, C, c, mom, fi, nb, avg, epoch_end, tol), S(s));
+  });
 
   // knn / smote
   m.def("knn_prep", [](u X, int m_, int m_pad, int role, u out, u s, u outq, u aff, u parents) {

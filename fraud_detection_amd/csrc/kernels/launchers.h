@@ -55,7 +55,8 @@ int scaler_stats_cast_blocks(int fp8 = 0);  // resident blocks of the fused kern
 // fp8 e4m3 of (x - pivot) * colscale * out_scale
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
                               float bias_value, void* out, double* partial, int nblocks, hipStream_t stream,
-                              const float* colscale = nullptr, float out_scale = 1.0f);
+                              const float* colscale = nullptr, float out_scale = 1.0f,
+                              const int64_t* idx = nullptr);
 void launch_scale_cast(const float* X, int64_t n, int ld, int d, const int64_t* idx,
                        const float* mean32, const float* inv32, const uint8_t* labels,
                        float bias_value, float out_scale, int out_kind, void* out,
@@ -99,6 +100,10 @@ constexpr uint32_t kPersistRunning = 1, kPersistExited = 2;
 void launch_predict_persistent(PersistCtl* ctl, const float* X, int d, int cap, const float* a, const float* c,
                                float bias, float* prob, float* logit, uint64_t idle_ticks, uint64_t life_ticks,
                                hipStream_t stream);
+// CV fold scoring: logits of raw rows idx[0..n) under a fit's device state (w: fp64 [32]
+// standardized-space weights; mean / scale: fp64 scaler stats)
+void launch_predict_gather_logit(const float* X, const int64_t* idx, int64_t n, int d, const double* w,
+                                 const double* mean, const double* scale, float* logit, hipStream_t stream);
 void launch_predict_shap(const void* X, int in_kind, int64_t n, int ld, int dz, int dphi,
                          const float* a, const float* c, float bias, float* prob, float* logit,
                          float* phi, int ld_phi, hipStream_t stream);
@@ -134,13 +139,20 @@ int64_t smote_bucket_max_samples();
 void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample_offset, uint64_t seed,
                          uint64_t counter_base, int* table, uint32_t* rec, uint32_t* tmp, int* pstart, int* pcnt,
                          uint16_t* lam, unsigned long long* bump, hipStream_t stream);
+// A block of stored rows a pass steps over (the validation fold of a cross-validation fit on the
+// fold-sorted training table): logical row r >= at reads physical row r + len.
+struct RowHole {
+  int64_t at = 0, len = 0;
+};
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
-                        float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr);
+                        float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr,
+                        int row_phase = 0, bool fisher = false, RowHole hole = {});
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
                             float x_scale, float* partial, int nblocks, hipStream_t stream,
-                            const SmoteView* sv = nullptr);
+                            const SmoteView* sv = nullptr, int row_phase = 0, bool fisher = false,
+                            RowHole hole = {});
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.
@@ -162,8 +174,19 @@ struct LRInitArgs {
 void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
                         const double* aff, hipStream_t stream);
 void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream);
-void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
-                       double momentum, int fit_intercept, hipStream_t stream, const double* aff = nullptr);
+// Minibatch SGD step (logreg.hip sgd_apply): c = epoch step scalar (lr = c / mean curvature),
+// nb = minibatches per epoch, avg = add this step's iterate to the Polyak average, epoch_end =
+// settle the epoch's convergence state (and return the average when one was taken).
+struct SgdArgs {
+  double C = 1.0, c = 0.5, momentum = 0.5, tol = 1e-3;
+  int d = 30, fit_intercept = 1, nb = 1, avg = 0, epoch_end = 0;
+};
+// one process: fixed-order reduce of the FISH pass's partials + the update, one launch
+void launch_sgd_step(const float* partial, int nblocks, double* state, float* w32, int* done, const double* aff,
+                     const SgdArgs& a, hipStream_t stream);
+// data parallel: the update from the all-reduced [36] sums
+void launch_sgd_update(const double* red, double* state, float* w32, int* done, const double* aff,
+                       const SgdArgs& a, hipStream_t stream);
 
 // ---- knn.hip ----
 // role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29);

@@ -73,10 +73,10 @@ __device__ __forceinline__ long long group_sum_i64(long long v) {
 // One pick's terms for the LPR lanes that share it (lane q owns columns [C q, C q + C)).  wl: this
 // lane's weights in the kernel's row units; xs: the unit scale of feature columns (fp8 rows hold
 // features * x_scale); p < 0: an empty pick (the lanes still join the shuffles).
-template <int LPR, bool HESS>
+template <int LPR, bool HESS, bool FISH = false>
 __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q, const float* wl, float xs,
                                            float sw1, float hrs, float* gc, float* u1, float* u2, float& loss,
-                                           float& wsum) {
+                                           float& wsum, float& dsum) {
   constexpr int C = 32 / LPR;
   const bool ok = p >= 0;
   const int64_t pp = ok ? p : 0;
@@ -127,16 +127,19 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
       const float r = -sw1 * pr * e2;  // s (p - 1) without the cancellation
       br += __float2int_rn(r * kSynQ);
       brl += __float2int_rn(r * lam * kSynQ);
-      if constexpr (HESS) {
+      if constexpr (HESS || FISH) {
         const float d = sw1 * pr * pr * e2;  // s p (1 - p)
         bd += __float2int_rn(d * kSynQ);
-        bdl += __float2int_rn(d * lam * kSynQ);
-        bdll += __float2int_rn(d * lam * lam * kSynQ);
+        if constexpr (HESS) {
+          bdl += __float2int_rn(d * lam * kSynQ);
+          bdll += __float2int_rn(d * lam * lam * kSynQ);
+        }
       }
       bl += __float2int_rn(sw1 * log1p_fast(e2) * kSynQL);  // s softplus(-z) = -s log p
     }
     sr += br; srl += brl; sl += bl;
-    if constexpr (HESS) { sd += bd; sdl += bdl; sdll += bdll; }
+    if constexpr (HESS || FISH) sd += bd;
+    if constexpr (HESS) { sdl += bdl; sdll += bdll; }
   }
   sr = group_sum_i64<LPR>(sr);
   srl = group_sum_i64<LPR>(srl);
@@ -163,18 +166,26 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   }
   loss = (float)((double)sl * (1.0 / (double)kSynQL));
   wsum = (float)cnt * sw1;
+  if constexpr (FISH && !HESS) sd = group_sum_i64<LPR>(sd);
+  dsum = (HESS || FISH) ? (float)((double)sd * inv) : 0.0f;
 }
 
 // VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
 // rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
-template <bool HESS, bool VIRT = false>  // bf16 rows (64 B); fp8 rows: logreg_pass_fp8w_kernel
+// row_sub / row_phase: the pass visits the row tiles t with (t / G) mod row_sub == row_phase
+// (G = waves in the grid) and the pick tiles with t mod row_sub == row_phase -- phase 0 of a
+// 1/row_sub sub-sample is the progressive-Newton warm-up, phases 0..row_sub-1 are the disjoint
+// minibatches of one SGD epoch (every stored row and every SMOTE sample in exactly one of them).
+// FISH (gradient-only SGD passes): slot 35 also receives sum s p (1 - p), the minibatch's
+// Gauss-Newton curvature scalar that sets the SGD step size (sgd_step_kernel).
+template <bool HESS, bool VIRT = false, bool FISH = false>  // bf16 rows (64 B); fp8: logreg_pass_fp8w_kernel
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
-    float* __restrict__ partial, SmoteView sv) {
+    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
-  __shared__ float red[kWaves][35];
+  __shared__ float red[kWaves][36];
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 3, rr = lane >> 2;
   float wl[8];
@@ -185,13 +196,15 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 #pragma unroll
   for (int j = 0; j < 8; ++j) g[j] = 0.0f;
   float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f;  // whacc: weight of the rows feeding H
+  float dacc = 0.0f;                              // FISH: sum s p (1 - p)
   f32x16_t acc = {};
   // transpose-read lane geometry (constant per lane): 16-lane group grp reads 4 rows x 16 cols
   const int grp = lane >> 4, gi = lane & 15;
   const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
   uint16_t* my_tile = tile[wv];
 
-  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin;  // stored rows
+  // stored rows (a CV fold's validation block [hole.at, hole.at + hole.len) is stepped over)
+  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin - hole.len;
   // row_sub > 1: only 64-row tiles t with (t mod G*row_sub) < G are visited (G = waves in the
   // grid): a uniform 1/row_sub subsample used by the early progressive-Newton iterations.
   const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
@@ -202,7 +215,8 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t row = b + 16 * u + rr;
-      v[u] = row < n ? X[(row_begin + row) * 4 + q] : make_uint4(0, 0, 0, 0);
+      const int64_t ph = row + (row >= hole.at ? hole.len : 0);
+      v[u] = row < n ? X[(row_begin + ph) * 4 + q] : make_uint4(0, 0, 0, 0);
     }
   };
   // virtual SMOTE samples: tiles of 16 picks (row_sub: every row_sub-th tile).  A wave's pick
@@ -213,17 +227,18 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
   const int64_t Gw = (int64_t)gridDim.x * kWaves;
-  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub;  // this wave's next pick tile
+  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub + row_phase;  // this wave's next pick tile
   auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
     const int64_t p = t * 16 + rr;
-    float gc[8], u1[8], u2[8], ls, ws;
-    pick_terms<4, HESS>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, gc, u1, u2, ls, ws);
+    float gc[8], u1[8], u2[8], ls, ws, ds;
+    pick_terms<4, HESS, FISH>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, gc, u1, u2, ls, ws, ds);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] += gc[j];
     if (q == 0) {
       lacc += ls;
       wacc += ws;
       if (HESS) whacc += ws / (float)hess_stride;
+      if (FISH) dacc += ds;
     }
     if constexpr (HESS) {  // rows rr (u1) and 16 + rr (u2) of the wave's tile: 2 MFMAs
       uint4 a, b;
@@ -248,7 +263,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
       __builtin_amdgcn_wave_barrier();
     }
   };
-  int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
+  int64_t base = ((int64_t)row_phase * Gw + (int64_t)blockIdx.x * kWaves + wv) * 64;
   uint4 cur[4];
   if (base < n) load_tile(base, cur);
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
@@ -269,7 +284,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     for (int u = 0; u < 4; ++u) {
       unpack8(cur[u], xs[u]);
     }
-    float zq = 0.0f, yq = 0.0f, swq = 0.0f;  // the row (u == q) whose loss this lane accounts for
+    float zq = 0.0f, yq = 0.0f, swq = 0.0f, dq = 0.0f;  // the row (u == q) this lane accounts for
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float* x = xs[u];
@@ -289,7 +304,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
       const float r = sw * (p - y);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = fmaf(r, x[j], g[j]);
-      if (q == u) { zq = zp; yq = y; swq = sw; }
+      if (q == u) { zq = zp; yq = y; swq = sw; if (FISH) dq = sw * p * p * (eh * eh); }
       if (do_h) {
         // sqrt(s p (1-p)) = sqrt(s) * p * exp(-z/2)   (1-p = p e^{-z}): no sqrt, no cancellation
         const float dd = ok ? (pos ? scw1 : scw0) * p * eh : 0.0f;
@@ -323,6 +338,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
     wacc += swq;
     if (do_h) whacc += swq;
+    if (FISH) dacc += dq;
 #pragma unroll
     for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
     if constexpr (VIRT) {
@@ -343,6 +359,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   lacc = wave_sum(lacc);
   wacc = wave_sum(wacc);
   whacc = wave_sum(whacc);
+  if (FISH) dacc = wave_sum(dacc);
   if (lane < 4) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) red[wv][8 * lane + j] = g[j];
@@ -351,6 +368,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     red[wv][32] = lacc;
     red[wv][33] = wacc;
     red[wv][34] = HESS ? whacc * (float)hess_stride : 0.0f;
+    red[wv][35] = dacc;
   }
   float* hb = reinterpret_cast<float*>(&tile[0][0]);  // 4 x 1024 floats = the 16 KiB tile
   if constexpr (HESS) {
@@ -365,7 +383,8 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   }
   __syncthreads();
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
-  if (threadIdx.x < (HESS ? 35 : 34)) {  // slot 34 (Hessian weight) only from Hessian passes
+  // slot 34 (Hessian weight) only from Hessian passes, slot 35 (curvature sum) from FISH passes
+  if (threadIdx.x < (HESS ? 35 : 34) || (FISH && threadIdx.x == 35)) {
     const int t = threadIdx.x;
     out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
   }
@@ -384,14 +403,14 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 // 16M rows (5.2 TB/s), fp8 bench step 1.164 -> 1.099 ms.
 // VIRT: virtual SMOTE samples as in the bf16 kernel, tiles of 32 picks (2 lanes per pick).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-template <bool HESS, bool VIRT = false>
+template <bool HESS, bool VIRT = false, bool FISH = false>
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, int row_sub, float* __restrict__ partial, SmoteView sv) {
+    int hess_stride, int row_sub, int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole) {
   if (done != nullptr && *done) return;
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
-  __shared__ float red[kWaves][35];
+  __shared__ float red[kWaves][36];
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 1, rr = lane >> 1;
   const float inv_s = 1.0f / x_scale;
@@ -409,12 +428,12 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   f32x2_t g[8];
 #pragma unroll
   for (int p = 0; p < 8; ++p) g[p] = f32x2_t{0.0f, 0.0f};
-  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f;
+  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f, dacc = 0.0f;
   f32x16_t acc = {};
   const int grp = lane >> 4, gi = lane & 15;
   const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
   uint16_t* my_tile = tile[wv];
-  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin;  // stored rows
+  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin - hole.len;  // stored rows
   const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
   const uint4* X = reinterpret_cast<const uint4*>(X8);
@@ -422,7 +441,8 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int64_t row = b + 32 * u + rr;
-      v[u] = row < n ? X[(row_begin + row) * 2 + q] : make_uint4(0, 0, 0, 0);
+      const int64_t ph = row + (row >= hole.at ? hole.len : 0);
+      v[u] = row < n ? X[(row_begin + ph) * 2 + q] : make_uint4(0, 0, 0, 0);
     }
   };
   // virtual SMOTE samples: tiles of 32 picks (2 lanes per pick, 16 columns each), after the
@@ -431,7 +451,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 31) >> 5;
   const int64_t Gw = (int64_t)gridDim.x * kWaves;
-  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub;
+  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub + row_phase;
   auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
     float wf[16];
 #pragma unroll
@@ -440,14 +460,15 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       wf[2 * e + 1] = wl[e][1];
     }
     const int64_t p = t * 32 + rr;
-    float gc[16], u1[16], u2[16], ls, ws;
-    pick_terms<2, HESS>(sv, p < npick ? p : -1, q, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws);
+    float gc[16], u1[16], u2[16], ls, ws, ds;
+    pick_terms<2, HESS, FISH>(sv, p < npick ? p : -1, q, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws, ds);
 #pragma unroll
     for (int j = 0; j < 8; ++j) g[j] += f32x2_t{gc[2 * j], gc[2 * j + 1]};
     if (q == 0) {
       lacc += ls;
       wacc += ws;
       if (HESS) whacc += ws / (float)hess_stride;
+      if (FISH) dacc += ds;
     }
     if constexpr (HESS) {  // rows rr (u1) and 32 + rr (u2): 4 MFMAs
       uint4* d1 = reinterpret_cast<uint4*>(my_tile + rr * kCols + 16 * q);
@@ -477,7 +498,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       __builtin_amdgcn_wave_barrier();
     }
   };
-  int64_t base = ((int64_t)blockIdx.x * kWaves + wv) * 64;
+  int64_t base = ((int64_t)row_phase * Gw + (int64_t)blockIdx.x * kWaves + wv) * 64;
   // two tiles in flight ahead of the one being computed (4 KiB per wave, as the bf16 stream)
   uint4 cur[2], nx1[2];
   if (base < n) load_tile(base, cur);
@@ -488,7 +509,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     if (base + 2 * step < n) load_tile(base + 2 * step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
-    float zq = 0.0f, yq = 0.0f, swq = 0.0f;
+    float zq = 0.0f, yq = 0.0f, swq = 0.0f, dq = 0.0f;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       float x[16];
@@ -513,7 +534,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       const f32x2_t r2 = f32x2_t{r, r};
 #pragma unroll
       for (int p = 0; p < 8; ++p) g[p] = __builtin_elementwise_fma(r2, f32x2_t{x[2 * p], x[2 * p + 1]}, g[p]);
-      if (q == u) { zq = zp; yq = y; swq = sw; }
+      if (q == u) { zq = zp; yq = y; swq = sw; if (FISH) dq = sw * pr * pr * (eh * eh); }
       if (do_h) {
         const float dd = ok ? (pos ? scw1 : scw0) * pr * eh : 0.0f;
         uint4 p0, p1;
@@ -548,6 +569,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     lacc = fmaf(swq, fmaxf(zq, 0.0f) - yq * zq + log1p_fast(__expf(-fabsf(zq))), lacc);
     wacc += swq;
     if (do_h) whacc += swq;
+    if (FISH) dacc += dq;
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       cur[u] = nx1[u];
@@ -573,6 +595,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   lacc = wave_sum(lacc);
   wacc = wave_sum(wacc);
   whacc = wave_sum(whacc);
+  if (FISH) dacc = wave_sum(dacc);
   if (lane < 2) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) red[wv][16 * lane + j] = gs[j];
@@ -581,6 +604,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     red[wv][32] = lacc;
     red[wv][33] = wacc;
     red[wv][34] = HESS ? whacc * (float)hess_stride : 0.0f;
+    red[wv][35] = dacc;
   }
   float* hb = reinterpret_cast<float*>(&tile[0][0]);
   if constexpr (HESS) {
@@ -596,7 +620,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   }
   __syncthreads();
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
-  if (threadIdx.x < (HESS ? 35 : 34)) {
+  if (threadIdx.x < (HESS ? 35 : 34) || (FISH && threadIdx.x == 35)) {
     const int t = threadIdx.x;
     out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
   }
@@ -960,48 +984,159 @@ __global__ __launch_bounds__(64) void logreg_export_kernel(const double* __restr
     __hip_atomic_store(host + t + 64 * i, st[t + 64 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Momentum SGD on a (possibly huge, HBM-sized) minibatch gradient.  aff (nullable): the rows are
-// pivot-shifted (fused scaler pass); the gradient maps into standardized space exactly as in the
-// Newton update (g_z[j] = inv_j (g_j - c_j g_30)) and w32 gets the folded weights.
-__global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict__ red,
-                                                        double* __restrict__ st,
-                                                        float* __restrict__ w32, int d, double C,
-                                                        double lr, double momentum,
-                                                        int fit_intercept, const double* __restrict__ aff) {
-  __shared__ double grad[32], rz[34], ss[kW + 32], cA[32], iA[32];
-  const int t = threadIdx.x;
-  const double S = red[33] > 0.0 ? red[33] : 1.0;
-  const double reg = 1.0 / (C * S);
-  const double* rr = red;
+// ---- minibatch SGD (config 3: "SMOTE k-NN + logistic SGD") --------------------------------------
+// One step = one pass over minibatch b of the epoch (row_phase b: 1/nb of the stored row tiles and
+// of the virtual-SMOTE pick tiles, logreg_pass_kernel) + this update.  Heavy-ball momentum on the
+// minibatch gradient of sklearn's objective, with the step size normalised by the minibatch's mean
+// Gauss-Newton curvature dbar = sum s p (1-p) / sum s (slot 35 of the FISH pass):
+//     lr_t = c_epoch / dbar_t,   v <- mom v - lr_t g_b(w),   w <- w + v.
+// Standardized features make the curvature ~ dbar x (feature covariance), so c is a
+// dimensionless step that stays valid as the model sharpens (dbar falls 0.25 -> ~0.05 on the
+// bench data while the curvature falls with it).  Polyak-Ruppert averaging (sklearn
+// SGDClassifier(average=True)): the steps flagged `avg` add w to a running sum and the epoch end
+// returns their mean.  Every epoch end also settles the convergence state from the epoch's sums:
+// the epoch gradient sum_b g_b(w_b) / sum_b S_b (for a near-quadratic objective, the gradient at
+// the averaged iterate) -> kGmax, the epoch's mean loss + penalty -> kObj, kConverged when
+// kGmax <= tol, and `done` (every later pass and update of the fit is a no-op).
+enum : int { kAvg = 160, kEpG = 192, kEpLoss = 224, kEpW = 225, kNAvg = 226, kDbar = 227, kLr = 228 };
+constexpr double kDbarFloor = 1e-3;  // lr_t <= c / 1e-3: a saturated minibatch cannot blow the step up
+constexpr int kSgdSlots = 36;        // grad[32] | loss | weight | (34: unused) | curvature sum
+
+__device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done,
+                          const double* __restrict__ aff, const SgdArgs& a, int t) {
+  // rd: the reduced [36] sums in LDS (raw row space).  Every thread of the block calls this (it
+  // holds block barriers); only the first wave (t < 64) reads or writes state.
+  __shared__ double rz[32], ss[kW + 32], cA[32], iA[32];
   if (aff) {
-    const double av = aff[t];
-    if (t < 32) cA[t] = av; else iA[t - 32] = av;
+    if (t < 64) {
+      const double av = aff[t];
+      if (t < 32) cA[t] = av; else iA[t - 32] = av;
+    }
     __syncthreads();
-    if (t < 32) rz[t] = iA[t] * (red[t] - cA[t] * red[kBiasCol]);
-    if (t == 32 || t == 33) rz[t] = red[t];
-    __syncthreads();
-    rr = rz;
   }
-  build_grad(rr, st, d, fit_intercept, reg, S, grad, t);
+  const double S = rd[33] > 0.0 ? rd[33] : 1.0;
+  if (t < 32) rz[t] = aff ? iA[t] * (rd[t] - cA[t] * rd[kBiasCol]) : rd[t];
+  const double reg = 1.0 / (a.C * S * (double)a.nb);  // the minibatch estimates sum s over the epoch as nb S
+  const double dbar = fmax(rd[35] / S, kDbarFloor);
+  const double lr = a.c / dbar;
   __syncthreads();
   if (t < kCols) {
-    const double v = momentum * st[kVel + t] - lr * grad[t];
+    double g = 0.0;
+    if (t < a.d) g = rz[t] / S + reg * st[kW + t];
+    else if (t == kBiasCol && a.fit_intercept) g = rz[t] / S;
+    const double v = a.momentum * st[kVel + t] - lr * g;
+    const double wn = st[kW + t] + v;
     st[kVel + t] = v;
-    ss[kW + t] = st[kW + t] + v;
-    st[kW + t] = ss[kW + t];
+    st[kEpG + t] += rz[t];
+    if (a.avg) st[kAvg + t] += wn;
+    ss[kW + t] = wn;
   }
   __syncthreads();
+  if (t == 0) {
+    st[kEpLoss] += rd[32];
+    st[kEpW] += rd[33];
+    if (a.avg) st[kNAvg] += 1.0;
+    st[kIter] += 1.0;
+    st[kDbar] = dbar;
+    st[kLr] = lr;
+  }
+  __syncthreads();
+  if (a.epoch_end) {
+    const double Sw = st[kEpW] > 0.0 ? st[kEpW] : 1.0;
+    const double na = st[kNAvg];
+    if (t < kCols && na > 0.0) ss[kW + t] = st[kAvg + t] / na;  // the averaged iterate is the model
+    __syncthreads();
+    double g = 0.0;
+    if (t < a.d) g = st[kEpG + t] / Sw + ss[kW + t] / (a.C * Sw);
+    else if (t == kBiasCol && a.fit_intercept) g = st[kEpG + t] / Sw;
+    double ga = t < kCols ? fabs(g) : 0.0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ga = fmax(ga, __shfl_xor(ga, o, kWave));
+    double w2 = (t < a.d) ? ss[kW + t] * ss[kW + t] : 0.0;
+    w2 = wave_sum(w2);
+    if (t < kCols) {
+      st[kEpG + t] = 0.0;
+      st[kAvg + t] = 0.0;
+    }
+    __syncthreads();
+    if (t == 0) {
+      st[kGmax] = ga;
+      st[kObj] = st[kEpLoss] / Sw + 0.5 * w2 / (a.C * Sw);
+      st[kEpLoss] = 0.0;
+      st[kEpW] = 0.0;
+      st[kNAvg] = 0.0;
+      if (ga <= a.tol) {
+        st[kConverged] = 1.0;
+        *done = 1;
+      }
+    }
+  }
+  __syncthreads();
+  if (t < kCols) st[kW + t] = ss[kW + t];
   if (aff) {
     store_folded(ss, cA, iA, w32, t);
   } else if (t < kCols) {
     w32[t] = (t == kLabelCol) ? 0.0f : (float)ss[kW + t];
   }
-  if (t == 0) {
-    double wn2 = 0.0;
-    for (int j = 0; j < d; ++j) wn2 += st[kW + j] * st[kW + j];
-    st[kObj] = red[32] / S + 0.5 * reg * wn2;
-    st[kIter] += 1.0;
+}
+
+// One process: the fixed-order fp64 reduction of the pass's [nblocks][36] partials and the update in
+// ONE launch (the reduce kernel + update kernel pair costs a kernel boundary and a second launch per
+// step).  1008 threads = 36 columns x 28 row-groups; every thread's loads are issued before the
+// first wait (the partials sit in L2/MALL: the kernel is load-latency bound); the 28 row-group
+// sums are combined in a fixed order, then wave 0 applies the step.
+constexpr int kSgdGroups = 28, kSgdLoads = 12;
+__global__ __launch_bounds__(1024) void sgd_step_kernel(const float* __restrict__ partial, int nblocks,
+                                                       double* __restrict__ st, float* __restrict__ w32,
+                                                       int* __restrict__ done, const double* __restrict__ aff,
+                                                       SgdArgs a) {
+  if (*done) return;
+  __shared__ double part[kSgdGroups][kSgdSlots];
+  __shared__ double rd[kSgdSlots];
+  const int c = threadIdx.x % kSgdSlots, grp = threadIdx.x / kSgdSlots;
+  if (grp < kSgdGroups) {
+    double acc = 0.0;
+    for (int b0 = grp; b0 < nblocks; b0 += kSgdGroups * kSgdLoads) {
+      float v[kSgdLoads];
+#pragma unroll
+      for (int u = 0; u < kSgdLoads; ++u) {
+        const int b = b0 + u * kSgdGroups;
+        v[u] = (b < nblocks && c != 34) ? partial[(int64_t)b * kLRPartStride + c] : 0.0f;
+      }
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+      for (int u = 0; u < kSgdLoads; u += 4) {
+        a0 += (double)v[u];
+        a1 += (double)v[u + 1];
+        a2 += (double)v[u + 2];
+        a3 += (double)v[u + 3];
+      }
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    part[grp][c] = acc;
   }
+  __syncthreads();
+  if (threadIdx.x < kSgdSlots) {
+    double r = 0.0;
+#pragma unroll 4
+    for (int g = 0; g < kSgdGroups; ++g) r += part[g][threadIdx.x];
+    rd[threadIdx.x] = r;
+  }
+  __syncthreads();
+  sgd_apply(rd, st, w32, done, aff, a, threadIdx.x);
+}
+
+// Data parallel: the reduced sums were all-reduced across ranks in `red` (logreg_reduce with 36
+// columns, then the collective); the same update from global memory.
+__global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict__ red, double* __restrict__ st,
+                                                        float* __restrict__ w32, int* __restrict__ done,
+                                                        const double* __restrict__ aff, SgdArgs a) {
+  if (*done) return;
+  __shared__ double rd[kSgdSlots];
+  const int t = threadIdx.x;
+  if (t < kSgdSlots) rd[t] = red[t];
+  __syncthreads();
+  sgd_apply(rd, st, w32, done, aff, a, t);
 }
 
 }  // namespace
@@ -1042,25 +1177,41 @@ static SmoteView checked_view(const SmoteView* sv, int64_t row_begin, int64_t ro
   return v;
 }
 
+// The skipped block must lie inside the stored rows (the kernel maps logical row r >= hole.at to
+// physical row r + hole.len: a hole past the end would read beyond the buffer).
+static void check_hole(const RowHole& h, int64_t row_begin, int64_t stored_end) {
+  if (h.len < 0 || h.at < 0 || (h.len > 0 && row_begin + h.at + h.len > stored_end))
+    throw std::runtime_error("logreg_pass: row hole outside the stored rows");
+}
+
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
-                        float* partial, int nblocks, hipStream_t stream, const SmoteView* sv) {
+                        float* partial, int nblocks, hipStream_t stream, const SmoteView* sv, int row_phase,
+                        bool fisher, RowHole hole) {
   // hessian: 0 = gradient/loss only; h >= 1 = also the Hessian, from every h-th row tile.
-  // row_sub >= 1: visit a uniform 1/row_sub of the 64-row tiles (progressive Newton).
-  // sv (nullable): virtual SMOTE samples after the stored rows.
+  // row_sub >= 1, 0 <= row_phase < row_sub: visit the 1/row_sub tile subset row_phase (progressive
+  // Newton: phase 0; SGD: minibatch row_phase of an epoch of row_sub minibatches).
+  // sv (nullable): virtual SMOTE samples after the stored rows.  fisher (gradient-only passes):
+  // also the curvature sum s p (1 - p) in slot 35.
   if (row_sub < 1) row_sub = 1;
+  if (row_phase < 0 || row_phase >= row_sub) throw std::runtime_error("logreg_pass: row_phase out of range");
+  if (fisher && hessian > 0) throw std::runtime_error("logreg_pass: the curvature sum is a gradient-pass output");
   const SmoteView v = checked_view(sv, row_begin, row_end);
+  check_hole(hole, row_begin, v.parents != nullptr ? v.n_real : row_end);
   const bool virt = v.parents != nullptr;
   const int hs = hessian > 0 ? hessian : 1;
-#define FDX_LRP(H, V)                                                                                    \
-  logreg_pass_kernel<H, V><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, hs, \
-                                                             row_sub, partial, v)
+#define FDX_LRP(H, V, F)                                                                                    \
+  logreg_pass_kernel<H, V, F><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, hs, \
+                                                                row_sub, row_phase, partial, v, hole)
   if (hessian > 0) {
-    if (virt) FDX_LRP(true, true);
-    else FDX_LRP(true, false);
+    if (virt) FDX_LRP(true, true, false);
+    else FDX_LRP(true, false, false);
+  } else if (fisher) {
+    if (virt) FDX_LRP(false, true, true);
+    else FDX_LRP(false, false, true);
   } else {
-    if (virt) FDX_LRP(false, true);
-    else FDX_LRP(false, false);
+    if (virt) FDX_LRP(false, true, false);
+    else FDX_LRP(false, false, false);
   }
 #undef FDX_LRP
   check_launch("logreg_pass");
@@ -1068,22 +1219,29 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
 
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
-                            float x_scale, float* partial, int nblocks, hipStream_t stream, const SmoteView* sv) {
+                            float x_scale, float* partial, int nblocks, hipStream_t stream, const SmoteView* sv,
+                            int row_phase, bool fisher, RowHole hole) {
   // fp8 rows store features * x_scale for columns < 30; the bias (col 30) and label (col 31)
-  // are stored unscaled.  sv (nullable): virtual SMOTE samples after the stored rows.
+  // are stored unscaled.  sv, row_phase, fisher: as launch_logreg_pass.
   if (row_sub < 1) row_sub = 1;
+  if (row_phase < 0 || row_phase >= row_sub) throw std::runtime_error("logreg_pass_fp8: row_phase out of range");
+  if (fisher && hessian > 0) throw std::runtime_error("logreg_pass_fp8: the curvature sum is a gradient-pass output");
   const SmoteView v = checked_view(sv, row_begin, row_end);
+  check_hole(hole, row_begin, v.parents != nullptr ? v.n_real : row_end);
   const bool virt = v.parents != nullptr;
   const int hs = hessian > 0 ? hessian : 1;
-#define FDX_LRP8(H, V)                                                                                   \
-  logreg_pass_fp8w_kernel<H, V><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, \
-                                                                  x_scale, 30, hs, row_sub, partial, v)
+#define FDX_LRP8(H, V, F)                                                                                       \
+  logreg_pass_fp8w_kernel<H, V, F><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done,   \
+                                                                     x_scale, 30, hs, row_sub, row_phase, partial, v, hole)
   if (hessian > 0) {
-    if (virt) FDX_LRP8(true, true);
-    else FDX_LRP8(true, false);
+    if (virt) FDX_LRP8(true, true, false);
+    else FDX_LRP8(true, false, false);
+  } else if (fisher) {
+    if (virt) FDX_LRP8(false, true, true);
+    else FDX_LRP8(false, false, true);
   } else {
-    if (virt) FDX_LRP8(false, true);
-    else FDX_LRP8(false, false);
+    if (virt) FDX_LRP8(false, true, false);
+    else FDX_LRP8(false, false, false);
   }
 #undef FDX_LRP8
   check_launch("logreg_pass_fp8");
@@ -1131,9 +1289,15 @@ void launch_logreg_fold(const double* state, const double* aff, float* w32, hipS
   check_launch("logreg_fold");
 }
 
-void launch_sgd_update(const double* red, double* state, float* w32, int d, double C, double lr,
-                       double momentum, int fit_intercept, hipStream_t stream, const double* aff) {
-  sgd_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, d, C, lr, momentum, fit_intercept, aff);
+void launch_sgd_step(const float* partial, int nblocks, double* state, float* w32, int* done, const double* aff,
+                     const SgdArgs& a, hipStream_t stream) {
+  sgd_step_kernel<<<1, kSgdGroups * kSgdSlots, 0, stream>>>(partial, nblocks, state, w32, done, aff, a);
+  check_launch("sgd_step");
+}
+
+void launch_sgd_update(const double* red, double* state, float* w32, int* done, const double* aff,
+                       const SgdArgs& a, hipStream_t stream) {
+  sgd_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, done, aff, a);
   check_launch("sgd_update");
 }
 

@@ -190,6 +190,58 @@ __global__ __launch_bounds__(kThreads) void predict_shap_kernel(
   }
 }
 
+// Cross-validation scoring (models/cv.py): logits of the raw fp32 rows idx[0..n) under a fit's
+// device state -- standardized-space weights w (fp64, w[30] = intercept) and the scaler's mean /
+// scale -- folded per block into a = w / scale, bias = w_30 - sum a mean.  The fold's validation
+// rows are read in place from the raw table (no gathered copy) and the weights never visit the
+// host, so a fold's AUC is enqueued behind its fit with no synchronisation.  8 lanes per row,
+// 4 columns per lane (8-byte pieces: raw rows are 120 B, 8-byte aligned).
+__global__ __launch_bounds__(kThreads) void predict_gather_logit_kernel(const float* __restrict__ X,
+                                                                        const int64_t* __restrict__ idx, int64_t n,
+                                                                        int d, const double* __restrict__ w,
+                                                                        const double* __restrict__ mean,
+                                                                        const double* __restrict__ scale,
+                                                                        float* __restrict__ logit) {
+  __shared__ float sa[32];
+  __shared__ float sb;
+  if (threadIdx.x < 64) {
+    const int t = threadIdx.x;
+    double a = (t < d) ? w[t] / scale[t] : 0.0;
+    double am = (t < d) ? a * mean[t] : 0.0;
+    am = wave_sum(am);
+    if (t < 32) sa[t] = (float)a;
+    if (t == 0) sb = (float)(w[kBiasCol] - am);
+  }
+  __syncthreads();
+  const int lane = lane_id(), c0 = (lane & 7) * 4, rsub = lane >> 3;
+  float al[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) al[j] = sa[c0 + j];
+  const float bias = sb;
+  const int64_t ngroups = (n + 7) >> 3;
+  const int64_t nwaves = (int64_t)gridDim.x * (kThreads / kWave);
+  for (int64_t g = (int64_t)blockIdx.x * (kThreads / kWave) + wave_id(); g < ngroups; g += nwaves) {
+    const int64_t r = g * 8 + rsub;
+    float x[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (r < n) {
+      const float* p = X + idx[r] * (int64_t)d + c0;
+      if (c0 + 2 <= d) {
+        const float2 t = *reinterpret_cast<const float2*>(p);
+        x[0] = t.x; x[1] = t.y;
+      }
+      if (c0 + 4 <= d) {
+        const float2 t = *reinterpret_cast<const float2*>(p + 2);
+        x[2] = t.x; x[3] = t.y;
+      }
+    }
+    float z = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) z = fmaf(al[j], x[j], z);
+    z = group_sum<8>(z) + bias;
+    if (r < n && (lane & 7) == 0) logit[r] = z;
+  }
+}
+
 // Persistent serving kernel (launchers.h PersistCtl).  Rows are scored exactly as
 // predict_shap_kernel<1, 2> scores them (8 lanes per row, 4 columns per lane, the same fma order
 // and DPP row sum, fast_sigmoid), so a request gets the same bits on either path.  Host-memory
@@ -358,4 +410,17 @@ void launch_predict_persistent(PersistCtl* ctl, const float* X, int d, int cap, 
   check_launch("predict_persistent");
 }
 
+}  // namespace fdx
+
+namespace fdx {
+void launch_predict_gather_logit(const float* X, const int64_t* idx, int64_t n, int d, const double* w,
+                                 const double* mean, const double* scale, float* logit, hipStream_t stream) {
+  if (d > 32 || (d & 1) || (reinterpret_cast<uintptr_t>(X) % 8) != 0)
+    throw std::invalid_argument("predict_gather_logit: even d <= 32, 8-byte aligned rows");
+  if (n <= 0) return;
+  const int64_t groups = (n + 7) / 8;
+  const int grid = (int)std::min<int64_t>(2048, (groups + 3) / 4);
+  predict_gather_logit_kernel<<<grid, kThreads, 0, stream>>>(X, idx, n, d, w, mean, scale, logit);
+  check_launch("predict_gather_logit");
+}
 }  // namespace fdx

@@ -197,11 +197,31 @@ __device__ __forceinline__ int stats_fetch(const float* __restrict__ X, int64_t 
 // mean as the pivot and of 1/sigma as colscale (ops/scaler.py fp8_fused_prescale); the exact
 // statistics from this same pass turn that into the solver's affine map, so the prescale only
 // has to be roughly right.
-template <bool NT, bool FP8>
+// Gather form (IDX: cross-validation, models/cv.py): output row i and its statistics come from
+// input row idx[i] -- the fold-sorted training table is cast straight from the raw table in the
+// same single read, with no permuted copy of X.  Rows are 8-byte aligned 2-float pieces (d even).
+__device__ __forceinline__ int stats_fetch_idx(const float* __restrict__ X, const int64_t* __restrict__ idx, int64_t t,
+                                               int d, int64_t n, float2 (&b)[8]) {
+  const int64_t r0 = t * kStatTileRows;
+  const int rows = (int)((n - r0) < (int64_t)kStatTileRows ? (n - r0) : (int64_t)kStatTileRows);
+  const int hp = d >> 1, np = rows * hp;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int e = threadIdx.x + k * kThreads;
+    if (e < np) {
+      const int r = e / hp, p = e - r * hp;
+      b[k] = reinterpret_cast<const float2*>(X + idx[r0 + r] * (int64_t)d)[p];
+    }
+  }
+  return rows * d;
+}
+
+template <bool NT, bool FP8, bool IDX = false>
 __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kernel(
     const float* __restrict__ X, int64_t n, int d, const float* __restrict__ pivot,
     const uint8_t* __restrict__ labels, float bias_value, void* __restrict__ outv,
-    double* __restrict__ partial, const float* __restrict__ colscale, float out_scale) {
+    double* __restrict__ partial, const float* __restrict__ colscale, float out_scale,
+    const int64_t* __restrict__ idx) {
   __shared__ __attribute__((aligned(16))) float tile[kStatTileRows * 30];
   __shared__ double red[2][8][32];
   const int c = threadIdx.x & 31, rg = threadIdx.x >> 5;
@@ -220,10 +240,20 @@ __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kerne
   // in flight while tile t is reduced and cast out of LDS.
   float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, b2 = b0, b3 = b0;
   float tail = 0.0f;
+  float2 bg[8];
   int64_t t = blockIdx.x;
-  int nf = t < ntiles ? stats_fetch(X, t, d, total, b0, b1, b2, b3, tail) : 0;
+  int nf = 0;
+  if (t < ntiles) nf = IDX ? stats_fetch_idx(X, idx, t, d, n, bg) : stats_fetch(X, t, d, total, b0, b1, b2, b3, tail);
   for (; t < ntiles; t += gridDim.x) {
-    {
+    if constexpr (IDX) {
+      const int np = nf >> 1;
+      float2* t2 = reinterpret_cast<float2*>(tile);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int e = threadIdx.x + k * kThreads;
+        if (e < np) t2[e] = bg[k];
+      }
+    } else {
       const int nf4 = nf >> 2, i = threadIdx.x;
       float4* t4 = reinterpret_cast<float4*>(tile);
       if (i < nf4) t4[i] = b0;
@@ -235,7 +265,9 @@ __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kerne
     }
     __syncthreads();
     const int rows = nf / d;
-    if (t + gridDim.x < ntiles) nf = stats_fetch(X, t + gridDim.x, d, total, b0, b1, b2, b3, tail);
+    if (t + gridDim.x < ntiles)
+      nf = IDX ? stats_fetch_idx(X, idx, t + gridDim.x, d, n, bg)
+               : stats_fetch(X, t + gridDim.x, d, total, b0, b1, b2, b3, tail);
     if (c < d) {
       for (int r = rg; r < rows; r += 8) {
         const double dd = (double)tile[r * d + c] - piv;
@@ -255,7 +287,7 @@ __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kerne
         const int cc = 8 * q + j;
         if (cc < d) o[j] = FP8 ? (tile[r * d + cc] - pv[j]) * ks[j] : tile[r * d + cc] - pv[j];
         else if (cc == kBiasCol) o[j] = bias_value;
-        else if (cc == kLabelCol) o[j] = labels ? (float)labels[grow] : 0.0f;
+        else if (cc == kLabelCol) o[j] = labels ? (float)labels[IDX ? idx[grow] : grow] : 0.0f;
         else o[j] = 0.0f;
       }
       if constexpr (FP8) {
@@ -818,17 +850,25 @@ int scaler_stats_cast_blocks(int fp8) {
 
 void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* pivot, const uint8_t* labels,
                               float bias_value, void* out, double* partial, int nblocks, hipStream_t stream,
-                              const float* colscale, float out_scale) {
+                              const float* colscale, float out_scale, const int64_t* idx) {
   if (d > 30 || (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(out) % 16) != 0)
     throw std::invalid_argument("scaler_stats_cast: contiguous 16-byte aligned rows, d <= 30");
+  if (idx != nullptr && (d & 1))
+    throw std::invalid_argument("scaler_stats_cast: the gather form reads 2-float pieces (even d)");
   // every block must be resident at once (a second round of blocks would double the span);
   // nblocks is fixed by the caller (partial buffer), the grid-stride loop covers the rest
-#define FDX_SSC(NT, F8)                                                                                 \
-  scaler_stats_cast_kernel<NT, F8><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value, \
-                                                                     out, partial, colscale, out_scale)
+#define FDX_SSC(NT, F8, I)                                                                                 \
+  scaler_stats_cast_kernel<NT, F8, I><<<nblocks, kThreads, 0, stream>>>(X, n, d, pivot, labels, bias_value, \
+                                                                        out, partial, colscale, out_scale, idx)
   // plain row stores (launchers.h: nontemporal ones measured slower for this pass)
-  if (colscale != nullptr) FDX_SSC(false, true);
-  else FDX_SSC(false, false);
+  if (idx != nullptr) {
+    if (colscale != nullptr) FDX_SSC(false, true, true);
+    else FDX_SSC(false, false, true);
+  } else if (colscale != nullptr) {
+    FDX_SSC(false, true, false);
+  } else {
+    FDX_SSC(false, false, false);
+  }
 #undef FDX_SSC
   check_launch("scaler_stats_cast");
 }

@@ -44,8 +44,12 @@ PYBIND11_MODULE(_fdx_ring, m) {
         o["rows"] = s.rows;
         o["slots"] = s.slots;
         o["queued_tickets"] = s.queued;
+        o["cancelled"] = s.cancelled;
+        o["reclaimed"] = s.reclaimed;
         return o;
       })
+      .def_property("reclaim_ms", &Ring::reclaim_ms, &Ring::set_reclaim_ms,
+                    "how long a tail ticket may stay unpublished / unfreed before the owner reclaims it")
       .def("ready_rows", &Ring::ready_rows, py::arg("limit") = 1u << 30)
       .def_property_readonly("base_address", [](const Ring& r) { return reinterpret_cast<uintptr_t>(r.base_address()); })
       .def_property_readonly("total_bytes", &Ring::total_bytes)
@@ -79,7 +83,14 @@ PYBIND11_MODULE(_fdx_ring, m) {
            },
            py::arg("prob"), py::arg("logit"), py::arg("phi") = 0, py::arg("dphi") = 0, py::arg("ok") = true,
            py::arg("set") = 0)
-      .def("pending_slots", &Ring::pending_slots);
+      .def("pending_slots", &Ring::pending_slots)
+      .def("debug_tags", [](const Ring& r) {
+        py::list o;
+        for (uint64_t v : r.debug_tags()) o.append(v);
+        return o;
+      })
+      .def("debug_take_tickets", &Ring::debug_take_tickets, py::arg("n"),
+           "take n tickets without publishing them (simulates a producer that died mid-request)");
   // Native load generator (tools/serve_latency.py): `threads` C++ producer threads, each issuing
   // `per_thread` synchronous requests of `rows` rows -- the owner's capacity without a Python
   // producer's interpreter in the measurement.  -> (elapsed seconds, per-request latencies in us)

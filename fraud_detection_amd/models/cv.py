@@ -1,0 +1,187 @@
+"""K12 device cross-validation: the reference's whole training job on one device-resident table.
+
+Reference (train_model.py:36-110): StandardScaler fitted once on the training split; 5-fold
+StratifiedKFold(shuffle, random_state=42) over it; inside every fold SMOTE(random_state=42) on the
+fold's training rows, a fit, predict_proba on the fold's validation rows and roc_auc_score; then
+SMOTE on the whole training split, the final fit and the test AUC -- 6 SMOTE + fit + AUC rounds.
+
+MI355X layout (no per-fold copy of the training rows):
+  * fold codes: ops/split.assign (keyed Feistel, stratified, sizes within one row per class);
+  * one permutation sorts the training rows by (fold, label) -- ten stable compactions;
+  * ONE fused scaler pass in gather form (ops/scaler.scaler_fit_cast(idx=perm)) reads the raw
+    table once and writes the fold-sorted training table (pivot-shifted bf16 / fp8 rows) plus the
+    statistics of the whole split (the reference's single scaler);
+  * fold k trains on the table minus its own block: the logistic passes step over the block
+    (ops/logreg ``hole``, logreg.hip RowHole);
+  * fold k's SMOTE minority = the positive tails of the other folds' blocks: the standardized fp32
+    positives are gathered once, fold-sorted, and each fold concatenates its four runs (~1.4 MB);
+    exact k-NN among them, virtual samples (never stored);
+  * fold k's validation logits come straight from the raw rows under the fit's device weights
+    (predict.hip predict_gather_logit), and its exact AUC from the native radix path -- the host
+    never waits inside the job: Newton fits after the first run with the first fold's iteration
+    count and are verified at the end (a short prediction finishes the fit and re-scores its fold).
+"""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+import torch
+
+from ..ops import knn as knn_ops
+from ..ops import logreg as lr_ops
+from ..ops import metrics as metric_ops
+from ..ops import scaler as scaler_ops
+from ..ops import split as split_ops
+from ..ops.layout import NCOLS, TORCH_STORAGE
+from ..ops.native import native, ptr, stream_of
+from .pipeline import PipelineResult, TrainConfig, evaluate
+
+
+@dataclass
+class CVResult:
+    fold_aucs: list
+    final: PipelineResult
+    test_auc: float | None
+    fold_ms: list = field(default_factory=list)     # device time of each fold (k-NN .. AUC)
+    final_ms: float = 0.0                           # device time of the final fit
+    prep_ms: float = 0.0                            # fold codes, permutation, scaler pass, positives
+    total_ms: float = 0.0                           # wall clock, whole job incl. the test AUC
+    fold_iters: list = field(default_factory=list)
+    fold_rows: list = field(default_factory=list)   # post-SMOTE training rows of each fold
+
+    @property
+    def cv_auc_mean(self) -> float:
+        return float(np.mean(self.fold_aucs))
+
+    @property
+    def cv_auc_std(self) -> float:
+        return float(np.std(self.fold_aucs))
+
+
+class DeviceCV:
+    """The train_model.py job (CV + final fit + AUCs) for the logistic model family on one GPU."""
+
+    def __init__(self, cfg: TrainConfig | None = None, n_folds: int = 5, seed: int = 42):
+        self.cfg = cfg or TrainConfig()
+        self.n_folds = int(n_folds)
+        self.seed = int(seed)
+        if self.cfg.solver not in ("newton", "sgd"):
+            raise ValueError("DeviceCV fits the logistic solvers (newton | sgd)")
+
+    def run(self, X: torch.Tensor, y: torch.Tensor, X_test: torch.Tensor | None = None,
+            y_test: torch.Tensor | None = None) -> CVResult:
+        cfg, K = self.cfg, self.n_folds
+        if not X.is_cuda:
+            raise ValueError("DeviceCV runs on the device (train.py's CV path covers host tables)")
+        if cfg.smote_scope != "global" or not cfg.smote:
+            raise ValueError("DeviceCV implements the reference's SMOTE-in-fold semantics (smote=True)")
+        dev = X.device
+        n, d = X.shape
+        t_wall = time.perf_counter()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 3)]
+        ev[0].record()
+        # ---- fold codes and the (fold, label) permutation -----------------------------------
+        codes = split_ops.assign(y, test_frac=0.0, n_folds=K, seed=self.seed)
+        key = (codes * 2 + y).to(torch.uint8)
+        pend = [scaler_ops.compact_indices_async(key, t) for t in range(2 * K)]
+        parts = [p.result() for p in pend]
+        sizes = [int(p.shape[0]) for p in parts]
+        perm = torch.cat(parts)
+        neg = sizes[0::2]
+        pos = sizes[1::2]
+        bounds = np.concatenate([[0], np.cumsum([a + b for a, b in zip(neg, pos)])]).astype(np.int64)
+        pbounds = np.concatenate([[0], np.cumsum(pos)]).astype(np.int64)
+        # ---- ONE fused scaler pass: fold-sorted training table + the split's statistics -------
+        rows = torch.empty((n, NCOLS), device=dev, dtype=TORCH_STORAGE[cfg.storage])
+        stats = scaler_ops.scaler_fit_cast(X, y, rows, fp8_scale=cfg.fp8_scale, idx=perm)
+        y_perm = y[perm]
+        pos_idx = torch.cat(parts[1::2])
+        xpos = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=pos_idx)  # fold-sorted
+        ev[1].record()
+        m = native()
+        s = stream_of(rows)
+        w0 = np.zeros(NCOLS)
+        if cfg.init_std > 0:
+            w0[:d] = np.random.default_rng(cfg.seed).normal(0.0, cfg.init_std, d)
+        fits, logits, aucs, virt_keep = [], [], [], []
+        pred = None
+        # diagnostics (tests): the fold-sorted table and what each fit ran on
+        self.rows, self.perm, self.bounds, self.stats, self.virtuals = rows, perm, bounds, stats, []
+
+        def one_fit(k: int | None):
+            """Fold k (None: the final fit on the whole split)."""
+            nonlocal pred
+            if k is None:
+                hole, xmin = (0, 0), xpos
+            else:
+                hole = (int(bounds[k]), int(bounds[k + 1] - bounds[k]))
+                xmin = torch.cat([xpos[: pbounds[k]], xpos[pbounds[k + 1]:]])
+            n_tr = n - hole[1]
+            n_min = int(xmin.shape[0])
+            n_new = max(0, int(round((n_tr - n_min) * cfg.sampling_ratio)) - n_min) if n_min > 0 else 0
+            cw = (1.0, 1.0)
+            if cfg.class_weight == "balanced":
+                tot, pw = float(n_tr + n_new), float(n_min + n_new)
+                cw = (tot / (2.0 * max(tot - pw, 1.0)), tot / (2.0 * max(pw, 1.0)))
+            kk = min(cfg.k_neighbors, n_min - 1)
+            parents = torch.empty((n_min, NCOLS), dtype=torch.bfloat16, device=dev)
+            nbr = knn_ops.knn_topk(xmin, xmin, k=kk, self_offset=0, parents=parents, parents_affine=stats.aff)
+            v = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, seed=cfg.seed).prepare()
+            ws = lr_ops.LRWorkspace(dev)
+            ws.prepare_flags()
+            if cfg.solver == "newton":
+                f = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, d=d, w0=w0, class_w=cw,
+                                      fit_intercept=cfg.fit_intercept, fp8_scale=cfg.fp8_scale,
+                                      check_every=cfg.check_every, workspace=ws, hess_stride=cfg.hess_stride,
+                                      affine=stats.aff, full_iters=pred, virtual=v, hole=hole)
+                if pred is None:  # the first fit ran host-checked: its count predicts the rest
+                    pred = f.full_phase_iters
+            else:
+                f = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
+                                   batches=cfg.sgd_batches, average=cfg.sgd_average, tol=cfg.sgd_tol, d=d, w0=w0,
+                                   class_w=cw,
+                                   fit_intercept=cfg.fit_intercept, fp8_scale=cfg.fp8_scale, workspace=ws,
+                                   affine=stats.aff, virtual=v, hole=hole)
+            virt_keep.append(v)
+            self.virtuals.append(v)
+            return f, ws, n_tr + n_new, n_min
+
+        def score(k: int, ws) -> tuple:
+            b0, b1 = int(bounds[k]), int(bounds[k + 1])
+            z = torch.empty(b1 - b0, device=dev, dtype=torch.float32)
+            m.predict_gather_logit(ptr(X), ptr(perm[b0:b1]), b1 - b0, d, ptr(ws.state), ptr(stats.mean64),
+                                   ptr(stats.scale64), ptr(z), s)
+            auc, _ = metric_ops.auc_radix(z, y_perm[b0:b1])
+            return z, auc
+
+        fold_rows = []
+        for k in range(K):
+            f, ws, n_post, n_min = one_fit(k)
+            z, auc = score(k, ws)
+            fits.append((f, ws))
+            aucs.append(auc)
+            fold_rows.append(n_post)
+            ev[2 + k].record()
+        f_fin, ws_fin, n_post, n_min = one_fit(None)
+        ev[2 + K].record()
+        # ---- settle: every deferred fit verified; a fit that had to continue is re-scored -----
+        for k, (f, ws) in enumerate(fits):
+            if isinstance(f, lr_ops.PendingFit) and f.deferred:
+                f.verify()
+                if f.full_phase_iters > (pred or 0):
+                    aucs[k] = score(k, ws)[1]
+        if isinstance(f_fin, lr_ops.PendingFit):
+            f_fin.verify()
+        torch.cuda.synchronize(dev)
+        fold_aucs = [float(a) for a in aucs]
+        self.fits = [f for f, _ in fits]
+        final = PipelineResult(scaler=stats, fit=f_fin, n_rows=n, n_train_rows=n_post, n_minority=n_min,
+                               n_synthetic=n_post - n)
+        test_auc = float(evaluate(final, X_test, y_test)["auc"]) if X_test is not None else None
+        total = (time.perf_counter() - t_wall) * 1e3
+        fold_ms = [ev[1 + k].elapsed_time(ev[2 + k]) for k in range(K)]
+        return CVResult(fold_aucs=fold_aucs, final=final, test_auc=test_auc, fold_ms=fold_ms,
+                        final_ms=ev[1 + K].elapsed_time(ev[2 + K]), prep_ms=ev[0].elapsed_time(ev[1]),
+                        total_ms=total, fold_iters=[int(f.n_iter) for f, _ in fits], fold_rows=fold_rows)

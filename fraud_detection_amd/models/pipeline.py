@@ -8,7 +8,8 @@ Here every numeric step is a HIP kernel on the rank's row shard:
     -> K8 MFMA k-NN (local queries vs global minority) -> K9 Philox SMOTE rows written in place
        from bf16 parents in the training rows' space -- or, for the Newton fit, regenerated
        inside every K4 pass (TrainConfig.virtual_smote)
-    -> K4 Newton (all-reduce C5 per iteration) or momentum SGD (all-reduce C4 per minibatch).
+    -> K4 Newton (all-reduce C5 per iteration) or minibatch SGD (all-reduce C4 per minibatch), both
+       folding the virtual SMOTE samples into their passes
 Evaluation: folded-scaler predict on raw fp32 test rows (K5) -> exact AUC (K10) + confusion.
 """
 from __future__ import annotations
@@ -48,10 +49,15 @@ class TrainConfig:
     # map of its sums)
     fold_scaler: bool = True
     fp8_scale: float = DEFAULT_FP8_SCALE
-    sgd_lr: float = 0.5
-    sgd_momentum: float = 0.9
-    sgd_epochs: int = 5
-    sgd_batch_rows: int = 1 << 22
+    # minibatch SGD (config 3, ops/logreg.sgd_fit): `sgd_batches` disjoint strided minibatches per
+    # epoch, curvature-normalised momentum steps (per-epoch step scalars), Polyak averaging over the
+    # last epoch, convergence state on the epoch gradient
+    sgd_lr: tuple = lr_ops.SGD_LR
+    sgd_momentum: float = lr_ops.SGD_MOMENTUM
+    sgd_epochs: int = lr_ops.SGD_EPOCHS
+    sgd_batches: int = lr_ops.SGD_BATCHES
+    sgd_average: bool = True
+    sgd_tol: float = lr_ops.SGD_TOL
     check_every: int = 1            # Newton: iterations per convergence-flag read (host reads one chunk behind)
     # Newton, one process, resident rows: enqueue the full-data iteration count the previous fit
     # of this shape needed and verify convergence when the training buffer is next reused (two
@@ -156,6 +162,14 @@ class DevicePipeline:
             f.verify()
             self._full_pred = (sig, f.full_phase_iters)
 
+    def settle(self) -> "DevicePipeline":
+        """Verify every fit still waiting for its deferred convergence check.  Under data
+        parallelism this is a collective point: every rank calls it at the same place (its
+        continuation may run gradient all-reduces); a DP fit's fields can only be read after it."""
+        for b in range(2):
+            self._settle(b)
+        return self
+
     def _train_buffer(self, n_rows: int, device, allow_double: bool = False) -> torch.Tensor:
         cfg = self.cfg
         dt = TORCH_STORAGE[cfg.storage]
@@ -197,6 +211,41 @@ class DevicePipeline:
         if self._virtual is not None:
             self._virtual.materialize(rows[res.n_rows:], self.cfg.fp8_scale)
         return rows
+
+    def training_objective(self, res: "PipelineResult", w: np.ndarray | None = None) -> dict:
+        """The exact objective (sklearn's: mean weighted log-loss + ||w||^2 / (2 C S)) and gradient
+        max-norm of standardized-space weights ``w`` (default: the latest fit's) over the latest
+        fit's training set -- stored rows plus its SMOTE samples, virtual or stored -- from one
+        device pass (the solvers' own sums, not an estimate).  Diagnostic: compares solvers on
+        the same training set; call it before the next fit reuses the buffers."""
+        cfg = self.cfg
+        w = np.asarray(res.w if w is None else w, dtype=np.float64).copy()
+        rows = self._buf[: res.n_rows] if self._virtual is not None else self._buf[: res.n_train_rows]
+        d = res.scaler.d
+        aff = getattr(res.scaler, "aff", None)
+        wf = w.copy()
+        if aff is not None:  # pivot-shifted rows: fold the standardization into the weights
+            a = aff.double().cpu().numpy()
+            c, inv = a[:32], a[32:]
+            wf[:d] = w[:d] * inv[:d]
+            wf[BIAS_COL] = w[BIAS_COL] - float(np.sum(w[:d] * inv[:d] * c[:d]))
+        wf[31] = 0.0
+        cw = (1.0, 1.0)
+        if cfg.class_weight == "balanced":
+            tot, pos = float(res.n_train_rows), float(res.n_minority + res.n_synthetic)
+            cw = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
+        g, loss, wsum, _ = lr_ops.logreg_pass(rows, torch.from_numpy(wf).float(), class_w=cw, hessian=False,
+                                              fp8_scale=cfg.fp8_scale, virtual=self._virtual)
+        if aff is not None:
+            g = g.copy()
+            g[:d] = inv[:d] * (g[:d] - c[:d] * g[BIAS_COL])
+        S = wsum if wsum > 0 else 1.0
+        grad = np.zeros(32)
+        grad[:d] = g[:d] / S + w[:d] / (cfg.C * S)
+        if cfg.fit_intercept:
+            grad[BIAS_COL] = g[BIAS_COL] / S
+        return {"objective": loss / S + 0.5 * float(w[:d] @ w[:d]) / (cfg.C * S),
+                "grad_max": float(np.abs(grad).max()), "weight": wsum}
 
     def fit_host(self, X: torch.Tensor, y: torch.Tensor, device=None, budget: int | None = None,
                  profile: bool = False) -> PipelineResult:
@@ -332,8 +381,10 @@ class DevicePipeline:
         # bf16 rows only: with 32-byte fp8 rows the stored SMOTE rows are cheap to stream and the
         # fp8 fit measured faster stored (c5 shard 1.404 vs 1.594 ms, profiles/r3_fin3); the fp8
         # pass still takes virtual samples (ops/logreg.VirtualSmote, tested against the oracle)
-        virt_ok = (cfg.virtual_smote and cfg.solver == "newton" and cfg.storage == "bf16"
-                   and dev.type == "cuda" and class_w[1] <= lr_ops.VIRTUAL_MAX_WEIGHT)
+        # SGD: the samples are generated inside every minibatch pass in both row formats (the stored
+        # rows of an fp8 SGD fit would be streamed once per epoch, three times per fit)
+        virt_ok = (cfg.virtual_smote and dev.type == "cuda" and class_w[1] <= lr_ops.VIRTUAL_MAX_WEIGHT
+                   and ((cfg.solver == "newton" and cfg.storage == "bf16") or cfg.solver == "sgd"))
         tm.mark("scale_cast")
         # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a
         # quota; shard scope has no collective in this block, so only a rank with its own quota enters
@@ -407,12 +458,11 @@ class DevicePipeline:
                 self._pending[b] = fit
                 self._bi = b ^ 1
         elif cfg.solver == "sgd":
-            fit = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
-                                 batch_rows=min(cfg.sgd_batch_rows, getattr(getattr(self, "last_plan", None),
-                                                                            "sgd_batch_rows", cfg.sgd_batch_rows)),
-                                 class_w=class_w, d=d, w0=w0,
+            fit = lr_ops.sgd_fit(rows_cap[:n] if virt is not None else rows, C=cfg.C, lr=cfg.sgd_lr,
+                                 momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs, batches=cfg.sgd_batches,
+                                 average=cfg.sgd_average, tol=cfg.sgd_tol, class_w=class_w, d=d, w0=w0,
                                  fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
-                                 workspace=self._ws, affine=stats.aff if fused else None)
+                                 workspace=self._ws, affine=stats.aff if fused else None, virtual=virt)
         else:
             raise ValueError(f"unknown solver {cfg.solver!r}")
         tm.mark("fit")
@@ -510,7 +560,11 @@ def global_smote_slices(ranks, quota, rank: int):
 
 
 def evaluate(result: PipelineResult, X_test: torch.Tensor, y_test: torch.Tensor, comm=None) -> dict:
-    """Exact test ROC-AUC + confusion matrix at p > 0.5 (evaluate_model.py:26-53)."""
+    """Exact test ROC-AUC + confusion matrix at p > 0.5 (evaluate_model.py:26-53).  A collective
+    point under data parallelism: a fit still waiting for its deferred check is settled here, on
+    every rank."""
+    if isinstance(result.fit, lr_ops.PendingFit):
+        result.fit.verify()
     a, c, bias = result.folded()
     dev = X_test.device
     at = torch.from_numpy(a).to(dev)

@@ -178,7 +178,8 @@ class PendingFit:
     _next = 0
     _POOL = 8
 
-    def __init__(self, state_dev: torch.Tensor, sgd: bool = False, verify=None, warm_iters: int = 0):
+    def __init__(self, state_dev: torch.Tensor, sgd: bool = False, verify=None, warm_iters: int = 0,
+                 keep: tuple = (), collective: bool = False):
         cls = PendingFit
         if not cls._pool:
             cls._pool = [torch.empty(state_dev.numel(), dtype=torch.float64, pin_memory=True)
@@ -194,6 +195,14 @@ class PendingFit:
         cls._owners[slot] = self
         self._slot, self._sgd, self._info = slot, sgd, None
         self._verify, self._state_dev, self.warm_iters = verify, state_dev, int(warm_iters)
+        # the tensors a deferred continuation reads by device address (rows, affine map, virtual
+        # SMOTE buffers): referenced here until verified, so the caching allocator cannot hand
+        # their blocks to another fit meanwhile
+        self._keep = tuple(keep) if verify is not None else ()
+        # data parallel: the continuation holds gradient all-reduces, so only an explicit verify()
+        # that every rank makes (DevicePipeline.settle, evaluate) may run it -- a field read on
+        # one rank alone would enter the collectives alone and hang the job
+        self._collective = bool(collective)
         self._export()
 
     def _export(self):
@@ -206,10 +215,12 @@ class PendingFit:
         self._event.record()
 
     def verify(self) -> "PendingFit":
-        """Resolve a deferred convergence check (no-op for an already checked fit)."""
+        """Resolve a deferred convergence check (no-op for an already checked fit).  Under data
+        parallelism every rank must call it at the same point of its program."""
         v, self._verify = self._verify, None
         if v is not None and v():
             self._export()  # the fit continued: export its final state again
+        self._keep = ()
         return self
 
     @property
@@ -218,6 +229,9 @@ class PendingFit:
 
     def _materialize(self) -> FitInfo:
         if self._info is None:
+            if self._verify is not None and self._collective:
+                raise RuntimeError("data-parallel fit with a pending convergence check: settle it on every "
+                                   "rank first (DevicePipeline.settle() or evaluate(...)), then read it")
             self.verify()
             self._event.synchronize()
             self._info = _info_from_state(PendingFit._pool[self._slot].numpy().copy(), self._sgd)
@@ -332,12 +346,16 @@ def progressive_schedule(n_rows: int) -> list:
 
 
 def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True,
-          sub: int = 1, virtual: VirtualSmote | None = None):
+          sub: int = 1, virtual: VirtualSmote | None = None, hole: tuple = (0, 0)):
     """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact).
     sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up).
-    virtual: rows >= rows.shape[0] are virtual SMOTE rows (end may reach n_real + n_new)."""
+    virtual: rows >= rows.shape[0] are virtual SMOTE rows (end may reach n_real + n_new).
+    hole: (at, len) stored rows [at, at + len) the pass steps over (a CV fold's validation block);
+    ``end`` counts logical rows (the hole excluded)."""
     dptr = ptr(ws.done) if done else 0
     h = int(hessian)
+    ha, hl = int(hole[0]), int(hole[1])
+    end += hl  # physical end
     if virtual is not None and virtual.n_new > 0:
         v = virtual
         mq, k = v.nbr.shape
@@ -346,15 +364,15 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
         m.logreg_pass_virtual(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
                               ptr(ws.partial), nb, s, ptr(v.parents), ptr(v.nbr), ptr(v.lam), ptr(v.off),
                               ptr(v.cnt), int(rows.shape[0]), int(v.q_offset), int(mq), int(k),
-                              float(fp8_scale) if fp8 else 0.0)
+                              float(fp8_scale) if fp8 else 0.0, 0, False, ha, hl)
     elif storage_kind(rows) == "bf16":
         nb = ws.nblocks
         m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
-                      nb, s)
+                      nb, s, 0, False, ha, hl)
     else:
         nb = ws.nblocks_fp8
         m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
-                          ptr(ws.partial), nb, s)
+                          ptr(ws.partial), nb, s, 0, False, ha, hl)
     # gradient-only: reduce slots 0..33 and keep red[34] (weight of the rows behind the held H)
     m.logreg_reduce(ptr(ws.partial), nb, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
 
@@ -379,6 +397,19 @@ def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian
     red = ws.red.cpu().numpy()
     H = red[64:].reshape(32, 32) if hessian else None
     return red[:32].copy(), float(red[32]), float(red[33]), H
+
+
+def _apply_hole(rows: torch.Tensor, hole):
+    """(rows, (at, len)) for a device fit that steps over the block; a host fit gets the rows
+    without it (one concatenation: the CPU path is the oracle, not the fast path)."""
+    if not hole or int(hole[1]) == 0:
+        return rows, (0, 0)
+    at, ln = int(hole[0]), int(hole[1])
+    if at < 0 or ln < 0 or at + ln > rows.shape[0]:
+        raise ValueError(f"hole {hole} outside the {rows.shape[0]} stored rows")
+    if rows.is_cuda:
+        return rows, (at, ln)
+    return torch.cat([rows[:at], rows[at + ln:]]), (0, 0)
 
 
 def _default_w0(w0):
@@ -411,7 +442,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                hess_refresh: int | str = "auto", n_sched: int | None = None,
                local_warmup: bool = True, affine: torch.Tensor | None = None,
                lookahead: int | None = None, full_iters: int | None = None,
-               virtual: VirtualSmote | None = None) -> FitInfo:
+               virtual: VirtualSmote | None = None, hole: tuple | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -431,9 +462,12 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     program (the iterations, and a continuation, carry the gradient all-reduces).
     ``virtual``: the fit's rows are ``rows`` followed by virtual.n_new SMOTE rows that are
     regenerated in every pass instead of stored (VirtualSmote; bf16 device rows).  Its tensors,
-    like the rows, must stay alive until a deferred fit is verified."""
+    like the rows, must stay alive until a deferred fit is verified.
+    ``hole``: (at, len) -- the fit's rows are ``rows`` without the block [at, at + len) (a
+    cross-validation fold on the fold-sorted training table: no per-fold copy)."""
     check_rows(rows)
     w0 = _default_w0(w0)
+    rows, hole = _apply_hole(rows, hole)
     if virtual is not None and virtual.n_new == 0:
         virtual = None
     if virtual is not None and not rows.is_cuda:  # host path: the fp32 interpolants after the rows
@@ -458,7 +492,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
     ws.reset(w0, class_w, aff)  # w0 is standardized-space; w32 gets it folded for shifted rows
-    n = rows.shape[0] + (virtual.n_new if virtual is not None else 0)
+    n = rows.shape[0] - hole[1] + (virtual.n_new if virtual is not None else 0)
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
     # The warm-up schedule sets the number of collectives, so every rank must derive the same one:
     # from ``n_sched`` (the smallest rank's row count, known to all ranks without a collective when
@@ -485,7 +519,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     for sub, iters in sched:
         hs_w = auto_warm_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
-            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual)
+            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual, hole=hole)
             if sync_warm:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
@@ -513,7 +547,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             # 8 vs 7 iterations, profiles/r1_s25)
             fresh = refresh <= 0 or full_it[0] % refresh == 0
             full_it[0] += 1
-            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual)
+            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual, hole=hole)
             if comm is not None and comm.world_size > 1:
                 # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
                 comm.all_reduce_(ws.red if fresh else ws.red[:GRAD_SLOTS])
@@ -574,90 +608,199 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                 return False  # converged (or max_iter) within the predicted iterations
             checked_loop(k)  # the prediction was short: finish the fit now
             return True
-        return PendingFit(ws.state, verify=verify, warm_iters=warm)
+        return PendingFit(ws.state, verify=verify, warm_iters=warm, keep=(rows, affine, virtual, ws),
+                          collective=comm is not None and comm.world_size > 1)
     checked_loop(0)
     return PendingFit(ws.state, warm_iters=warm)
 
 
-def _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm):
+def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm):
     from ..utils.checkpoint import config_signature
 
     n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
-    return config_signature(kind="sgd", n=n_all, d=d, C=C, lr=lr, momentum=momentum, batch_rows=batch_rows,
-                            class_w=list(class_w), fit_intercept=fit_intercept)
+    return config_signature(kind="sgd2", n=n_all, d=d, C=C, lr=list(lr), momentum=momentum, batches=nb,
+                            epochs=epochs, average=bool(average), tol=tol, class_w=list(class_w),
+                            fit_intercept=fit_intercept)
 
 
-def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr: float = 0.5, momentum: float = 0.9, epochs: int = 5,
-            batch_rows: int = 1 << 20, class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True,
-            comm=None, fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None,
-            checkpoint=None, checkpoint_every: int = 0, affine: torch.Tensor | None = None) -> FitInfo:
-    """Momentum minibatch SGD.  Each minibatch is a contiguous window of ``batch_rows`` rows of
-    this rank's shard (rows are stored pre-shuffled); DP all-reduces the minibatch gradient.
+# Config 3's solver defaults (BASELINE.json: "SMOTE k-NN + logistic SGD").  Chosen on the bench
+# distribution in fp64 simulation (8M raw rows -> 16M post-SMOTE rows, 3 data seeds plus a 4M-row
+# shard): the Polyak-averaged last epoch lands within 2-3e-5 relative of the Newton optimum and the
+# epoch gradient at 3-5e-4; a constant step instead of the curvature-normalised one needed > 48
+# steps for 1e-3 (the curvature falls ~5x between w = 0 and the optimum).
+SGD_BATCHES = 8
+SGD_EPOCHS = 3
+SGD_LR = (0.4, 0.6, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
+SGD_MOMENTUM = 0.55
+SGD_TOL = 1e-3                # on the epoch gradient max-norm (sklearn SGDClassifier's default tol)
+SGD_SLOTS = 36
 
-    ``checkpoint`` (utils.checkpoint.CheckpointManager): every ``checkpoint_every`` minibatches
-    (and at each epoch end) the solver state -- weights, velocity, objective, step counter -- and
-    the data cursor (epoch, minibatch) are saved; a matching checkpoint is resumed from, giving
-    the same result as an uninterrupted fit.
 
-    ``affine``: [64] float64 (c | 1/sigma) for pivot-shifted rows (the fused scaler pass, as in
-    newton_fit): the fit runs in standardized space, the update kernel maps each minibatch
-    gradient and streams folded weights."""
+def _epoch_lr(lr, ep: int) -> float:
+    if np.ndim(lr) == 0:
+        return float(lr)
+    lr = list(lr)
+    return float(lr[min(ep, len(lr) - 1)])
+
+
+def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD_MOMENTUM,
+            epochs: int = SGD_EPOCHS, batches: int = SGD_BATCHES, average: bool = True, tol: float = SGD_TOL,
+            class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
+            fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None, checkpoint=None,
+            checkpoint_every: int = 0, affine: torch.Tensor | None = None, virtual: VirtualSmote | None = None,
+            batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None):
+    """Minibatch SGD (BASELINE config 3) on sklearn's objective.
+
+    Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
+    -- the stored row tiles t with (t // G) mod batches == b (G = waves in the pass grid: every
+    minibatch strides over the whole shard) plus the virtual-SMOTE pick tiles t mod batches == b
+    (1/batches of the SMOTE samples, generated in the pass, never stored).  Each minibatch
+    therefore holds both classes in the post-SMOTE proportion.  ``batch_rows`` (legacy) sets
+    ``batches`` = ceil(rows / batch_rows).
+
+    Step: heavy-ball momentum on the minibatch gradient, lr_t = lr[epoch] / dbar_t with dbar_t the
+    minibatch's mean Gauss-Newton curvature s p (1 - p) (same pass, slot 35), Polyak-Ruppert
+    averaging over the last epoch (``average``), and a device-side convergence state settled at
+    every epoch end: the epoch gradient max-norm (FitInfo.grad_max) against ``tol``, the epoch's
+    mean objective (FitInfo.objective), ``converged``; a converged fit turns its remaining passes
+    into no-ops.  The whole fit is enqueued with no host synchronisation and returns a PendingFit.
+
+    Data parallel: the minibatch sums (36 values) are all-reduced before every update (C4).
+    ``checkpoint``: every ``checkpoint_every`` steps and at each epoch end the device state
+    (weights, velocity, average, epoch sums) and the cursor (epoch, minibatch) are saved; a
+    matching checkpoint is resumed from.  ``affine``: pivot-shifted rows (fused scaler pass), as in
+    newton_fit.  ``virtual``: the SMOTE samples after ``rows`` (VirtualSmote).  ``max_steps``: stop
+    after that many steps of the schedule (a simulated interruption for the resume tests).
+    ``hole``: (at, len) stored rows the fit steps over (newton_fit)."""
     check_rows(rows)
     w0 = _default_w0(w0)
-    n = rows.shape[0]
+    rows, hole = _apply_hole(rows, hole)
+    if virtual is not None and virtual.n_new == 0:
+        virtual = None
+    n_stored = rows.shape[0] - hole[1]
+    n = n_stored + (virtual.n_new if virtual is not None else 0)
+    if batch_rows:
+        batches = max(1, -(-n // int(batch_rows)))
+    nb = max(1, int(batches))
+    if comm is not None and comm.world_size > 1:
+        nb = int(comm.all_reduce_scalar(nb, op="max"))
+    lrs = [_epoch_lr(lr, e) for e in range(max(epochs, 1))]
     if affine is not None and not rows.is_cuda:
         a = affine.cpu().double()
         rows = ((ref.rows_to_f32(rows, fp8_scale, d).double() - a[:32]) * a[32:]).float()
+        if virtual is not None:  # the samples interpolate shifted parents: map them the same way
+            vr = ((virtual.rows_f32().double() - a[:32]) * a[32:]).float()
+            vr[:, LABEL_COL] = virtual.label
+            return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept,
+                                comm, fp8_scale, checkpoint, checkpoint_every, None, None, virtual=(virtual, vr),
+                                max_steps=max_steps)
         affine = None
     aff = 0
     if affine is not None:
         if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
-    sig = _sgd_signature(n, d, C, lr, momentum, batch_rows, class_w, fit_intercept, comm) if checkpoint else None
+    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm)
+           if checkpoint else None)
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
     if not rows.is_cuda:
-        return _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_intercept, comm, fp8_scale,
-                            checkpoint, checkpoint_every, sig, got)
+        vv = (virtual, virtual.rows_f32()) if virtual is not None else None
+        return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm,
+                            fp8_scale, checkpoint, checkpoint_every, sig, got, virtual=vv, max_steps=max_steps)
+    if virtual is not None:
+        virtual.check(rows)
+        if class_w[1] > VIRTUAL_MAX_WEIGHT:
+            raise ValueError(f"virtual SMOTE: positive class weight {class_w[1]} > {VIRTUAL_MAX_WEIGHT}")
+        virtual.prepare()
     m = native()
     ws = workspace or LRWorkspace(rows.device)
-    ws.reset(w0, class_w)
+    ws.reset(w0, class_w, aff)
     s = stream_of(rows)
     if got is not None:
-        st = got[0]["state"].to(torch.float64)
-        ws.state.copy_(st.to(rows.device))
-        w32 = st[S_W:S_W + 32].to(torch.float32)
-        w32[LABEL_COL] = 0.0
-        ws.w32.copy_(w32.to(rows.device))
+        ws.state.copy_(got[0]["state"].to(torch.float64).to(rows.device))
+        if aff:
+            m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)  # the state is standardized-space
+        else:
+            w32 = ws.state[S_W:S_W + 32].to(torch.float32)
+            w32[LABEL_COL] = 0.0
+            ws.w32.copy_(w32)
         start = (int(got[1]["epoch"]), int(got[1]["batch"]))
-    if aff:
-        m.logreg_fold(ptr(ws.state), aff, ptr(ws.w32), s)  # the state is standardized-space
-    nb = max(1, (n + batch_rows - 1) // batch_rows)
-    if comm is not None and comm.world_size > 1:
-        nb = int(comm.all_reduce_scalar(nb, op="max"))
+    fp8 = storage_kind(rows) != "bf16"
+    blocks = ref.sgd_grid_blocks(n_stored, nb, ws.nblocks_fp8 if fp8 else ws.nblocks)
+    dp = comm is not None and comm.world_size > 1
     for ep in range(start[0], epochs):
+        c = lrs[ep]
         for b in range(start[1] if ep == start[0] else 0, nb):
-            lo = min(b * batch_rows, n)
-            hi = min(lo + batch_rows, n)
-            _pass(m, rows, ws, False, lo, hi, fp8_scale, s, done=False)
-            if comm is not None and comm.world_size > 1:
-                comm.all_reduce_(ws.red[:GRAD_SLOTS])
-            m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), d, float(C), float(lr), float(momentum),
-                         int(fit_intercept), s, aff)
-            gstep = ep * nb + b + 1
+            if max_steps is not None and ep * nb + b >= max_steps:
+                break
+            avg = int(average and ep == epochs - 1)
             last = b + 1 == nb
+            _sgd_pass(m, rows, ws, n, fp8_scale, s, b, nb, blocks, virtual, hole)
+            if dp:
+                m.logreg_reduce(ptr(ws.partial), blocks, SGD_SLOTS, ptr(ws.red), ptr(ws.done), s)
+                comm.all_reduce_(ws.red[:SGD_SLOTS])
+                m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
+                             float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
+            else:
+                m.sgd_step(ptr(ws.partial), blocks, ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
+                           float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
+            gstep = ep * nb + b + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 nxt = (ep + 1, 0) if last else (ep, b + 1)
-                checkpoint.save(ep * nb + b + 1, {"state": ws.state},
+                checkpoint.save(gstep, {"state": ws.state},
                                 {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
-    return _info_from_state(ws.state.cpu().numpy(), sgd=True)
+    return PendingFit(ws.state, sgd=True)
+
+
+def _sgd_pass(m, rows, ws: LRWorkspace, n: int, fp8_scale: float, s: int, phase: int, nb: int, blocks: int,
+              virtual: VirtualSmote | None, hole: tuple = (0, 0)):
+    """Minibatch ``phase`` of ``nb``: the gradient + curvature-sum pass into ws.partial[:blocks]
+    (``n`` logical rows: the hole excluded)."""
+    dptr = ptr(ws.done)
+    fp8 = storage_kind(rows) != "bf16"
+    ha, hl = int(hole[0]), int(hole[1])
+    end = n + hl
+    if virtual is not None:
+        v = virtual
+        mq, k = v.nbr.shape
+        m.logreg_pass_virtual(ptr(rows), 0, end, ptr(ws.w32), ptr(ws.class_w), dptr, 0, nb, ptr(ws.partial), blocks,
+                              s, ptr(v.parents), ptr(v.nbr), ptr(v.lam), ptr(v.off), ptr(v.cnt), int(rows.shape[0]),
+                              int(v.q_offset), int(mq), int(k), float(fp8_scale) if fp8 else 0.0, phase, True, ha, hl)
+    elif not fp8:
+        m.logreg_pass(ptr(rows), 0, end, ptr(ws.w32), ptr(ws.class_w), dptr, 0, nb, ptr(ws.partial), blocks, s,
+                      phase, True, ha, hl)
+    else:
+        m.logreg_pass_fp8(ptr(rows), 0, end, ptr(ws.w32), ptr(ws.class_w), dptr, 0, nb, float(fp8_scale),
+                          ptr(ws.partial), blocks, s, phase, True, ha, hl)
+
+
+def sgd_minibatch_sums(rows: torch.Tensor, w: torch.Tensor, nb: int, phase: int, class_w=(1.0, 1.0),
+                       fp8_scale: float = DEFAULT_FP8_SCALE, virtual: VirtualSmote | None = None,
+                       blocks: int | None = None) -> dict:
+    """One SGD minibatch pass, reduced (test / diagnostic API): gradient, loss, weight and
+    curvature sums of minibatch ``phase`` of ``nb`` at weights ``w`` on the device."""
+    m = native()
+    ws = LRWorkspace(rows.device)
+    ws.reset(w.cpu().double().numpy(), class_w)
+    n = rows.shape[0]
+    if virtual is not None:
+        virtual.check(rows)
+        virtual.prepare()
+        n += virtual.n_new
+    fp8 = storage_kind(rows) != "bf16"
+    blocks = blocks or ref.sgd_grid_blocks(rows.shape[0], nb, ws.nblocks_fp8 if fp8 else ws.nblocks)
+    s = stream_of(rows)
+    _sgd_pass(m, rows, ws, n, fp8_scale, s, phase, nb, blocks, virtual)
+    m.logreg_reduce(ptr(ws.partial), blocks, SGD_SLOTS, ptr(ws.red), 0, s)
+    red = ws.red[:SGD_SLOTS].cpu().numpy()
+    return {"grad": red[:32].copy(), "loss": float(red[32]), "wsum": float(red[33]), "dsum": float(red[35]),
+            "blocks": blocks}
 
 
 def _info_from_state(st: np.ndarray, sgd: bool = False) -> FitInfo:
-    return FitInfo(w=st[S_W:S_W + 32].copy(), n_iter=int(st[S_ITER]), n_newton_steps=int(st[S_NACC]),
-                   converged=bool(st[S_CONV] > 0) if not sgd else True, objective=float(st[S_OBJ]),
-                   grad_max=float(st[S_GMAX]))
+    return FitInfo(w=st[S_W:S_W + 32].copy(), n_iter=int(st[S_ITER]), n_newton_steps=0 if sgd else int(st[S_NACC]),
+                   converged=bool(st[S_CONV] > 0), objective=float(st[S_OBJ]), grad_max=float(st[S_GMAX]))
 
 
 # ------------------------------------------------------------------------------------------
@@ -683,43 +826,65 @@ def _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm,
                    objective=st.obj, grad_max=st.gmax, history=hist)
 
 
-def _sgd_fit_cpu(rows, C, lr, momentum, epochs, batch_rows, class_w, w0, d, fit_intercept, comm, fp8_scale,
-                 checkpoint=None, checkpoint_every=0, sig=None, got=None):
+def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm, fp8_scale,
+                 checkpoint=None, checkpoint_every=0, sig=None, got=None, virtual=None, max_steps=None):
+    """The device SGD's algorithm in fp64 (ref.SgdStateRef) over the same minibatch partition:
+    stored row tiles by the pass grid's strided walk (the full 768-block grid of a 256-CU part,
+    shrunk for small shards like the device), virtual samples by their pick tile."""
     R = ref.rows_to_f32(rows, fp8_scale, d).double().numpy()
-    n = R.shape[0]
-    w = w0.copy()
-    v = np.zeros(32)
-    nb = max(1, (n + batch_rows - 1) // batch_rows)
-    if comm is not None and comm.world_size > 1:
-        nb = int(comm.all_reduce_scalar(nb, op="max"))
-    obj = np.inf
-    it = 0
+    n_stored = R.shape[0]
+    fp8 = storage_kind(rows) == "fp8"
+    rb = ref.sgd_row_batches(n_stored, nb, ref.sgd_grid_blocks(n_stored, nb, 768))
+    parts = [R]
+    bs = [rb]
+    if virtual is not None:
+        v, vr = virtual
+        mq, k = v.nbr.shape
+        pick, _ = ref.smote_pick_draws(int(mq), int(k), int(v.n_new), int(v.seed), int(v.counter_base),
+                                       int(v.sample_offset))
+        parts.append(np.asarray(vr, dtype=np.float64))
+        bs.append(ref.sgd_pick_batches(mq * k, nb, 32 if fp8 else ref.PICK_TILE_BF16)[pick.astype(np.int64)])
+    R = np.concatenate(parts)
+    batch_of = np.concatenate(bs)
+    members = [np.nonzero(batch_of == b)[0] for b in range(nb)]
+    st = ref.SgdStateRef(w0)
     start = (0, 0)
     if got is not None:
-        st = got[0]["state"].numpy()
-        w, v, obj, it = st[S_W:S_W + 32].copy(), st[S_VEL:S_VEL + 32].copy(), float(st[S_OBJ]), int(st[S_ITER])
+        sv = got[0]["state"].numpy()
+        st.w, st.v = sv[S_W:S_W + 32].copy(), sv[S_VEL:S_VEL + 32].copy()
+        st.avg, st.ep_g = sv[160:192].copy(), sv[192:224].copy()
+        st.ep_loss, st.ep_w, st.n_avg, st.iter = float(sv[224]), float(sv[225]), int(sv[226]), int(sv[S_ITER])
+        st.gmax, st.obj, st.converged = float(sv[S_GMAX]), float(sv[S_OBJ]), bool(sv[S_CONV] > 0)
+        st.done = st.converged
         start = (int(got[1]["epoch"]), int(got[1]["batch"]))
     for ep in range(start[0], epochs):
         for b in range(start[1] if ep == start[0] else 0, nb):
-            lo = min(b * batch_rows, n)
-            hi = min(lo + batch_rows, n)
-            red = _reduced_cpu(R[lo:hi], w, class_w, False, comm)
-            S = red[33] if red[33] > 0 else 1.0
-            reg = 1.0 / (C * S)
-            grad = np.zeros(32)
-            grad[:d] = red[:d] / S + reg * w[:d]
-            if fit_intercept:
-                grad[30] = red[30] / S
-            v = momentum * v - lr * grad
-            w = w + v
-            obj = red[32] / S + 0.5 * reg * float(w[:d] @ w[:d])
-            it += 1
+            if max_steps is not None and ep * nb + b >= max_steps:
+                break
+            Rb = R[members[b]]
+            g, loss, wsum, _ = ref.logreg_pass(Rb, st.w, class_w, False)
+            X = Rb.copy()
+            X[:, LABEL_COL] = 0.0
+            wv = st.w.copy()
+            wv[LABEL_COL] = 0.0
+            p = ref.sigmoid(X @ wv)
+            sw = np.where(Rb[:, LABEL_COL] > 0.5, class_w[1], class_w[0])
+            red = np.concatenate([g, [loss, wsum, 0.0, float(np.sum(sw * p * (1 - p)))]])
+            if comm is not None and comm.world_size > 1:
+                red = comm.all_reduce(torch.from_numpy(red)).numpy()
             last = b + 1 == nb
-            if checkpoint is not None and (last or (checkpoint_every and it % checkpoint_every == 0)):
-                st = np.zeros(STATE_SIZE)
-                st[S_W:S_W + 32], st[S_VEL:S_VEL + 32], st[S_OBJ], st[S_ITER] = w, v, obj, it
+            st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nb,
+                    bool(average and ep == epochs - 1), last, tol, fit_intercept)
+            gstep = ep * nb + b + 1
+            if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
+                sv = np.zeros(STATE_SIZE)
+                sv[S_W:S_W + 32], sv[S_VEL:S_VEL + 32], sv[160:192], sv[192:224] = st.w, st.v, st.avg, st.ep_g
+                sv[224], sv[225], sv[226], sv[S_ITER] = st.ep_loss, st.ep_w, st.n_avg, st.iter
+                sv[S_GMAX], sv[S_OBJ], sv[S_CONV] = st.gmax, st.obj, float(st.converged)
                 nxt = (ep + 1, 0) if last else (ep, b + 1)
-                checkpoint.save(ep * nb + b + 1, {"state": st},
+                checkpoint.save(gstep, {"state": sv},
                                 {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
+    w = st.w.copy()
     w[LABEL_COL] = 0.0
-    return FitInfo(w=w, n_iter=it, n_newton_steps=0, converged=True, objective=obj, grad_max=float("nan"))
+    return FitInfo(w=w, n_iter=st.iter, n_newton_steps=0, converged=st.converged, objective=st.obj,
+                   grad_max=st.gmax)

@@ -13,15 +13,13 @@ _CHUNK = 16384
 SORT_PATH_POSITIVES = 100_000
 # from this many scores on, the radix path runs straight away (no positive-count read-back)
 RADIX_ROWS = 8_000_000
-_WS: dict = {}
 
 
 def _radix_ws(dev, nbytes: int) -> torch.Tensor:
-    w = _WS.get(dev)
-    if w is None or w.numel() < nbytes:
-        w = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _WS[dev] = w
-    return w
+    """Sort scratch from the caching allocator, per call: its block is stream-ordered, so two AUC
+    calls on different streams or threads never share keys / labels / counters (a module-level
+    buffer reused by every call raced between concurrent evaluations -- ADVICE r3)."""
+    return torch.empty(nbytes, dtype=torch.uint8, device=dev)
 
 
 def auc_radix(scores: torch.Tensor, labels: torch.Tensor):

@@ -289,6 +289,91 @@ class NewtonStateRef:
             self.done = True
 
 
+WAVES_PER_BLOCK = 4     # logreg.hip kThreads / 64
+ROW_TILE = 64           # rows per wave tile
+PICK_TILE_BF16 = 16     # virtual-SMOTE picks per wave tile (bf16 pass); the fp8 pass takes 32
+SGD_MIN_SPAN = 4        # every SGD minibatch spans >= 4 strided blocks of row tiles
+
+
+def sgd_grid_blocks(n_stored: int, nb: int, full_blocks: int) -> int:
+    """Blocks of the SGD pass grid: the full resident grid, shrunk for small shards so that every
+    minibatch spans >= SGD_MIN_SPAN strided blocks of G = 4 * blocks row tiles (its rows then come
+    from the whole shard, not from one contiguous window)."""
+    want = int(n_stored) // (ROW_TILE * WAVES_PER_BLOCK * max(1, int(nb)) * SGD_MIN_SPAN)
+    return int(max(1, min(int(full_blocks), want)))
+
+
+def sgd_row_batches(n_stored: int, nb: int, blocks: int) -> np.ndarray:
+    """Minibatch of every stored row (logreg.hip logreg_pass_kernel row_phase walk): row tile
+    t = row // 64 belongs to minibatch (t // G) mod nb, G = waves in the grid."""
+    G = WAVES_PER_BLOCK * int(blocks)
+    return ((np.arange(int(n_stored), dtype=np.int64) // ROW_TILE) // G) % int(nb)
+
+
+def sgd_pick_batches(n_picks: int, nb: int, pick_tile: int = PICK_TILE_BF16) -> np.ndarray:
+    """Minibatch of every virtual-SMOTE pick: pick tile t = pick // pick_tile belongs to t mod nb
+    (all samples of a pick land in the pick's minibatch)."""
+    return (np.arange(int(n_picks), dtype=np.int64) // int(pick_tile)) % int(nb)
+
+
+SGD_DBAR_FLOOR = 1e-3
+
+
+class SgdStateRef:
+    """Mirror of logreg.hip sgd_apply (fp64): heavy-ball momentum SGD with the step normalised by
+    the minibatch's mean curvature, Polyak averaging, epoch-end convergence state."""
+
+    def __init__(self, w0: np.ndarray):
+        self.w = np.asarray(w0, dtype=np.float64).copy()
+        self.v = np.zeros(32)
+        self.avg = np.zeros(32)
+        self.n_avg = 0
+        self.ep_g = np.zeros(32)
+        self.ep_loss = 0.0
+        self.ep_w = 0.0
+        self.iter = 0
+        self.gmax = np.inf
+        self.obj = np.inf
+        self.converged = False
+        self.done = False
+
+    def step(self, g_raw, loss, wsum, dsum, d, C, c, mom, nb, avg, epoch_end, tol, fit_intercept=True):
+        if self.done:
+            return
+        S = wsum if wsum > 0 else 1.0
+        reg = 1.0 / (C * S * nb)
+        lr = c / max(dsum / S, SGD_DBAR_FLOOR)
+        g = np.zeros(32)
+        g[:d] = g_raw[:d] / S + reg * self.w[:d]
+        if fit_intercept:
+            g[BIAS_COL] = g_raw[BIAS_COL] / S
+        self.v = mom * self.v - lr * g
+        self.w = self.w + self.v
+        self.ep_g += np.asarray(g_raw[:32], dtype=np.float64)
+        self.ep_loss += loss
+        self.ep_w += wsum
+        if avg:
+            self.avg += self.w
+            self.n_avg += 1
+        self.iter += 1
+        if epoch_end:
+            Sw = self.ep_w if self.ep_w > 0 else 1.0
+            if self.n_avg > 0:
+                self.w = self.avg / self.n_avg
+            G = np.zeros(32)
+            G[:d] = self.ep_g[:d] / Sw + self.w[:d] / (C * Sw)
+            if fit_intercept:
+                G[BIAS_COL] = self.ep_g[BIAS_COL] / Sw
+            self.gmax = float(np.abs(G).max())
+            self.obj = self.ep_loss / Sw + 0.5 * float(self.w[:d] @ self.w[:d]) / (C * Sw)
+            self.ep_g[:] = 0.0
+            self.avg[:] = 0.0
+            self.ep_loss = self.ep_w = 0.0
+            self.n_avg = 0
+            if self.gmax <= tol:
+                self.converged = self.done = True
+
+
 # ------------------------------------------------------------------------------------------
 # K8 / K9 SMOTE
 # ------------------------------------------------------------------------------------------

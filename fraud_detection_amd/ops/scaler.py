@@ -210,7 +210,7 @@ def _sample_moments(X: torch.Tensor, sample_rows: int):
 
 def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Tensor, comm=None,
                     pivot: torch.Tensor | None = None, bias_value: float = 1.0,
-                    fp8_scale: float = DEFAULT_FP8_SCALE) -> ScalerStats:
+                    fp8_scale: float = DEFAULT_FP8_SCALE, idx: torch.Tensor | None = None) -> ScalerStats:
     """StandardScaler.fit fused with the row cast: ONE read of X yields the (all-reduced)
     statistics and the training rows in ``out`` [n, 32] (col 30 = bias_value, col 31 = label):
       * bf16: pivot-shifted rows s = x - pivot;
@@ -219,18 +219,30 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
     The returned stats carry ``aff`` mapping the stored feature values (fp8: after dividing by
     fp8_scale) to standardized ones, z = (v - c) * inv, which the Newton solver applies as an exact
     affine map of its sums (ops/logreg.newton_fit(affine=...)): same model, half the raw-matrix
-    traffic of scaler_fit + scale_cast."""
+    traffic of scaler_fit + scale_cast.
+    ``idx`` (int64 [m] row indices, device): gather form -- output row i (and the statistics) come
+    from X[idx[i]], e.g. the fold-sorted training table of a CV job straight from the raw table."""
     _check_X(X)
-    n, d = X.shape
+    if idx is not None:
+        if idx.dtype != torch.int64 or idx.dim() != 1 or idx.device != X.device:
+            raise ValueError("idx must be an int64 [m] tensor on X's device")
+        if not X.is_cuda:  # host oracle: the gathered copy
+            X = X[idx]
+            labels = None if labels is None else labels[idx]
+            idx = None
+        elif X.shape[1] % 2:
+            raise ValueError("the gather form needs an even feature count")
+    n = X.shape[0] if idx is None else idx.shape[0]
+    d = X.shape[1]
     fp8 = out.dtype == torch.uint8
     if out.shape != (n, NCOLS) or out.dtype not in (torch.bfloat16, torch.uint8) or not out.is_contiguous():
         raise ValueError(f"bad output buffer {tuple(out.shape)} {out.dtype}")
-    if labels is not None and (labels.dtype != torch.uint8 or labels.shape[0] != n):
+    if labels is not None and (labels.dtype != torch.uint8 or labels.shape[0] != X.shape[0]):
         raise ValueError("labels must be uint8 [n] aligned with X")
     dist = comm is not None and comm.world_size > 1
     colscale = None
     if fp8:
-        pivot_fp8, colscale = fp8_fused_prescale(X, comm)
+        pivot_fp8, colscale = fp8_fused_prescale(X, comm)  # a sample of X: any order of its rows
         pivot = pivot_fp8 if pivot is None else pivot
     if pivot is None:
         if dist:
@@ -263,7 +275,7 @@ def scaler_fit_cast(X: torch.Tensor, labels: torch.Tensor | None, out: torch.Ten
         nparts = 1
         if n > 0:
             m.scaler_stats_cast(ptr(X), n, d, ptr(piv), ptr(labels), float(bias_value), ptr(out), ptr(partial), nb, s,
-                                ptr(colscale), float(fp8_scale) if fp8 else 1.0)
+                                ptr(colscale), float(fp8_scale) if fp8 else 1.0, ptr(idx))
             if dist:  # the all-reduce needs the one [64] sums vector
                 m.scaler_reduce(ptr(partial), nb, ptr(sums), s)
             else:  # first level only: the finalize kernel sums its rows (one launch fewer)

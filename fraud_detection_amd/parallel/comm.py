@@ -303,8 +303,7 @@ class Communicator:
                 return self._native_gather(x, counts)
         if self._host_staged(x):
             with self._timed("all_gather_rows_staged", x, "gloo-staged"):
-                out, c = self._all_gather_rows(x.cpu(), counts)
-                return out.to(x.device), c
+                return self._staged_gather(x, counts)
         with self._timed("all_gather_rows", x, self.backend):
             return self._all_gather_rows(x, counts)
 
@@ -313,6 +312,28 @@ class Communicator:
         [sum(counts), ...] output on the compute stream (csrc/comm/rccl_comm.cpp all_gatherv)."""
         counts = [int(c) for c in counts]
         return self._native.all_gatherv(x.contiguous(), counts), counts
+
+    def _staged_gather(self, x: torch.Tensor, counts: list | None):
+        """gloo rehearsal of C3 for CUDA rows: one D2H copy into a padded host buffer, the gloo
+        all-gather, and one H2D copy per rank straight into the compact device output -- no CPU
+        tensor compute (a CPU zero-fill / cat here ran on the OpenMP pool and stalled 5-49 ms per
+        call beside the other rank's threads: profiles/r4_a/dpscope.log)."""
+        if counts is None:
+            counts = [int(c[0]) for c in self.all_gather_ints([x.shape[0]])]
+        counts = [int(c) for c in counts]
+        mx = max(counts)
+        pad = torch.empty((mx,) + tuple(x.shape[1:]), dtype=x.dtype)  # rows past x.shape[0] never read
+        if x.shape[0]:
+            pad[: x.shape[0]].copy_(x)
+        outs = [torch.empty_like(pad) for _ in range(self.world_size)]
+        dist.all_gather(outs, pad)
+        out = torch.empty((sum(counts),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        o0 = 0
+        for o, c in zip(outs, counts):
+            if c:
+                out[o0:o0 + c].copy_(o[:c])
+            o0 += c
+        return out, counts
 
     def _all_gather_rows(self, x: torch.Tensor, counts: list | None):
         dev = x.device

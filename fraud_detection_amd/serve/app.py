@@ -301,12 +301,8 @@ def create_app(settings: Settings | None = None, engine: InferenceEngine | None 
         metrics.predictions_submitted.inc(X.shape[0])
         disp = batcher_()
         with metrics.inference_time.time():
-            if batch.explain:
-                if disp.client is not None and disp.owner is None and X.shape[0]:
-                    p, _, phi = disp.client.predict_explain(X)  # the GPU owner explains
-                else:
-                    ex = eng.explain(X, settings.xai_method)
-                    p, phi = ex.prob, ex.phi
+            if batch.explain:  # the GPU owner explains (split to ring-sized requests), else this engine
+                p, phi = disp.explain(X, settings.xai_method)
             else:
                 p, _ = disp.predict_proba(X)
                 phi = None

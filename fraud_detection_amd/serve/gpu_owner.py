@@ -175,12 +175,27 @@ class RingClient:
         except OSError:
             return False
 
+    @property
+    def max_request_rows(self) -> int:
+        """Rows of one ring request: half the ring, so two such requests can be in flight."""
+        return max(self.ring.slot_rows, (self.ring.nslots // 2) * self.ring.slot_rows)
+
+    def _request(self, X: np.ndarray, op: int) -> np.ndarray:
+        """One ring request per max_request_rows piece (a batch larger than the ring is split
+        instead of refused)."""
+        X = np.ascontiguousarray(X, np.float32)
+        cap = self.max_request_rows
+        if X.shape[0] <= cap:
+            return self.ring.request(X, op, self.timeout_ms)
+        return np.concatenate([self.ring.request(X[i:i + cap], op, self.timeout_ms)
+                               for i in range(0, X.shape[0], cap)])
+
     def predict_proba(self, X: np.ndarray):
-        o = self.ring.request(np.ascontiguousarray(X, np.float32), OP_PREDICT, self.timeout_ms)
+        o = self._request(X, OP_PREDICT)
         return o[:, 0].astype(np.float64), o[:, 1].astype(np.float64)
 
     def predict_explain(self, X: np.ndarray):
-        o = self.ring.request(np.ascontiguousarray(X, np.float32), OP_EXPLAIN, self.timeout_ms)
+        o = self._request(X, OP_EXPLAIN)
         return o[:, 0].astype(np.float64), o[:, 1].astype(np.float64), o[:, 2:2 + self.d].astype(np.float64)
 
     def stats(self) -> dict:
@@ -230,6 +245,20 @@ class Dispatcher:
         except RuntimeError as e:  # owner gone or timed out: degrade to the host path, loudly
             logger.error("GPU owner unavailable (%s): scoring %d rows on the host", e, X.shape[0])
             return self._host(X)
+
+    def explain(self, X: np.ndarray, method: str):
+        """(prob, phi) of a batch: through the GPU owner when one serves this front-end (any size:
+        the client splits it), else -- or when the owner is down or times out -- on this process's
+        engine, loudly (this path used to raise HTTP 500 past 65,536 rows)."""
+        X = np.ascontiguousarray(X, np.float32)
+        if self.client is not None and self.owner is None and X.shape[0]:
+            try:
+                p, _, phi = self.client.predict_explain(X)
+                return p, phi
+            except RuntimeError as e:
+                logger.error("GPU owner unavailable (%s): explaining %d rows on the host", e, X.shape[0])
+        ex = self.engine.explain(X, method)
+        return ex.prob, ex.phi
 
     def predict_one(self, x: np.ndarray):
         p, z = self.predict_proba(x.reshape(1, -1))

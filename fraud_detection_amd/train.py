@@ -108,6 +108,7 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         s, model_type, cv_folds, mode, asdict(cfg), X.shape, comm))
     if progress.folds:
         say(f" Resuming: {len(progress.folds)} completed fold(s) from {progress.path}")
+    res_cv = None
     if cv_folds and cv_folds > 1 and pos >= cv_folds:
         say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
         if mode == "device":
@@ -117,17 +118,32 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         cv_mode = s.cv_parallel
         if cv_mode == "auto":  # small folds are latency-bound under DP: give each rank whole folds
             cv_mode = "fold" if comm is not None and len(tr) < FOLD_PARALLEL_ROWS else "dp"
-        cv_scores = _cross_validate(model_type, cfg, folds, take, comm, cv_mode, progress)
+        if _device_cv_ok(model_type, cfg, dev, comm, progress, Xtr):
+            # models/cv.DeviceCV: the reference's semantics (ONE scaler on the training split,
+            # SMOTE inside every fold) on one fold-sorted device table, final fit included
+            from .models.cv import DeviceCV
+
+            t_fit = time.perf_counter()
+            with tracing.span("train.cv_job", model=model_type), tracing.roctx_range("train.cv_job"):
+                cvr = DeviceCV(cfg, cv_folds, seed=42).run(Xtr, ytr)
+            cv_scores, res_cv = cvr.fold_aucs, cvr.final
+            for k, auc in enumerate(cv_scores):
+                progress.record(k, auc)
+        else:
+            cv_scores = _cross_validate(model_type, cfg, folds, take, comm, cv_mode, progress)
         for k, auc in enumerate(cv_scores):
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
     say(f" Training final {model_type} model with SMOTE on the full training set...")
-    t_fit = time.perf_counter()
-    with tracing.span("train.final_fit", model=model_type), tracing.roctx_range("train.final_fit"):
-        res = _fit(model_type, cfg, Xtr, ytr, comm,
-                   checkpoint=None if ck_dir is None else os.path.join(ck_dir, f"final_{model_type}"))
-        if dev.type == "cuda":
-            torch.cuda.synchronize(dev)
+    if res_cv is None:
+        t_fit = time.perf_counter()
+        with tracing.span("train.final_fit", model=model_type), tracing.roctx_range("train.final_fit"):
+            res = _fit(model_type, cfg, Xtr, ytr, comm,
+                       checkpoint=None if ck_dir is None else os.path.join(ck_dir, f"final_{model_type}"))
+            if dev.type == "cuda":
+                torch.cuda.synchronize(dev)
+    else:
+        res = res_cv  # fitted inside the CV job (t_fit: the whole job)
     t_fit = time.perf_counter() - t_fit
     tm = train_metrics()
     tm.rows_per_second.set(float(res.n_train_rows) * (comm.world_size if comm else 1) / max(t_fit, 1e-9))
@@ -238,6 +254,18 @@ def _cross_validate(model_type, cfg, folds, take, comm, mode: str, progress: _Pr
         for k, auc in sorted(part.items()):
             progress.record(k, auc)
     return [progress.folds[k] for k in range(len(folds))]
+
+
+def _device_cv_ok(model_type, cfg, dev, comm, progress, Xtr) -> bool:
+    """The device CV job (models/cv.py) runs the logistic family on one GPU, from scratch (a
+    resumed job keeps the per-fold path), with virtual SMOTE (bf16 Newton or SGD in either row
+    format) and an even feature count (its gathered scaler pass reads 8-byte row pieces)."""
+    if os.environ.get("FDX_CV_ENGINE", "auto") == "per_fold":
+        return False
+    virt = cfg.solver == "sgd" or (cfg.solver == "newton" and cfg.storage == "bf16")
+    return (model_type == "logistic" and dev.type == "cuda" and comm is None and not progress.folds
+            and cfg.smote and cfg.virtual_smote and cfg.fold_scaler and virt and Xtr.shape[1] % 2 == 0
+            and Xtr.is_contiguous())
 
 
 def _fit(model_type, cfg, X, y, comm=None, checkpoint: str | None = None):

@@ -58,14 +58,20 @@ def test_sgd_resume_is_bit_identical(tmp_path):
 
     X, y = separable(6000, fraud_rate=0.1, seed=4)
     rows = S.scale_cast(X, S.scaler_fit(X), labels=y)
-    kw = dict(lr=0.3, epochs=3, batch_rows=1000)
+    kw = dict(epochs=3, batches=6)
     full = L.sgd_fit(rows, **kw)
     mgr = CheckpointManager(str(tmp_path), prefix="sgd", keep=3)
-    L.sgd_fit(rows, **{**kw, "epochs": 2}, checkpoint=mgr, checkpoint_every=4)  # stop after 2 epochs
+    L.sgd_fit(rows, **kw, checkpoint=mgr, checkpoint_every=4, max_steps=12)  # "crash" after 2 epochs
     got = mgr.latest()
     assert got[1]["epoch"] == 2 and got[1]["batch"] == 0
     resumed = L.sgd_fit(rows, **kw, checkpoint=mgr, checkpoint_every=4)
     assert np.array_equal(resumed.w, full.w) and resumed.n_iter == full.n_iter
+    # mid-epoch interruption (step 9 of 18: epoch 1, minibatch 3) resumes to the same model too
+    mgr2 = CheckpointManager(str(tmp_path / "mid"), prefix="sgd", keep=3)
+    L.sgd_fit(rows, **kw, checkpoint=mgr2, checkpoint_every=3, max_steps=9)
+    assert mgr2.latest()[1]["epoch"] == 1 and mgr2.latest()[1]["batch"] == 3
+    again = L.sgd_fit(rows, **kw, checkpoint=mgr2, checkpoint_every=3)
+    assert np.array_equal(again.w, full.w)
 
 
 def test_gbdt_resume_mid_epoch_checkpoint_every(tmp_path):

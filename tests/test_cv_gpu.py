@@ -1,0 +1,55 @@
+"""Device cross-validation (models/cv.py, K12): the reference's train_model.py job -- one scaler
+on the training split, 5 stratified folds with SMOTE inside each, the final fit and 6 exact AUCs --
+on one fold-sorted device table, with no per-fold copy.  A fold's fit that steps over its
+validation block equals the fit on an explicit copy of the other blocks (bitwise: the passes see
+the same logical rows), and each fold AUC equals the host AUC of that fold's model."""
+import numpy as np
+import pytest
+import torch
+
+from fraud_detection_amd.data.synthetic import separable
+from fraud_detection_amd.models.cv import DeviceCV
+from fraud_detection_amd.models.pipeline import TrainConfig
+from fraud_detection_amd.ops import logreg as L
+from fraud_detection_amd.ops import reference as ref
+from fraud_detection_amd.ops import split as SP
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("solver,storage", [("newton", "bf16"), ("sgd", "bf16"), ("sgd", "fp8")])
+def test_device_cv_job(dev, solver, storage):
+    X, y = separable(1_200_000, fraud_rate=0.004, seed=31, device=dev)
+    Xt, yt = separable(200_000, fraud_rate=0.004, seed=32, device=dev)
+    cv = DeviceCV(TrainConfig(solver=solver, storage=storage, seed=42))
+    r = cv.run(X, y, Xt, yt)
+    assert len(r.fold_aucs) == 5 and all(a > 0.9 for a in r.fold_aucs) and r.test_auc > 0.9
+    # the permutation is a permutation, sorted by fold code, negatives first inside each fold
+    perm = cv.perm.cpu().numpy()
+    assert np.array_equal(np.sort(perm), np.arange(X.shape[0]))
+    codes = SP.assign_numpy(y.cpu().numpy(), 0.0, 5, 42)
+    yp = y.cpu().numpy()[perm]
+    cp = codes[perm]
+    assert np.all(np.diff(cp.astype(int) * 2 + yp) >= 0)
+    b = cv.bounds
+    assert b[-1] == X.shape[0] and np.all(np.diff(b) > 0)
+    # fold 2's fit == the same solver on an explicit copy of the other blocks (same samples)
+    k = 2
+    f = cv.fits[k]
+    part = torch.cat([cv.rows[: b[k]], cv.rows[b[k + 1]:]])
+    v = cv.virtuals[k]
+    w0 = np.zeros(32)
+    w0[:30] = np.random.default_rng(42).normal(0.0, 0.01, 30)
+    if solver == "newton":
+        g = L.newton_fit(part, tol=1e-4, max_iter=25, w0=w0, affine=cv.stats.aff, virtual=v,
+                         fp8_scale=4.0).as_fit_info()
+        assert g.n_iter == f.n_iter
+    else:
+        g = L.sgd_fit(part, w0=w0, affine=cv.stats.aff, virtual=v).as_fit_info()
+    assert np.array_equal(g.w, f.w)
+    # the fold AUC is the exact AUC of the fold model on the fold's raw validation rows
+    mean, _, scale = cv.stats.numpy()
+    Xv = X.cpu().numpy()[perm[b[k]:b[k + 1]]].astype(np.float64)
+    z = ((Xv - mean) / scale) @ f.w[:30] + f.w[30]
+    assert abs(r.fold_aucs[k] - ref.roc_auc(z, yp[b[k]:b[k + 1]].astype(bool))) < 2e-6
+    assert len(r.fold_ms) == 5 and r.final_ms > 0 and r.prep_ms > 0

@@ -58,7 +58,7 @@ def test_affine_sgd_equals_standardized_sgd():
     shifted = torch.empty((X.shape[0], 32), dtype=torch.bfloat16)
     st = S.scaler_fit_cast(X, y, shifted)
     z = S.scale_cast(X, st, labels=y, out_dtype="f32")
-    kw = dict(C=1.0, lr=0.5, momentum=0.9, epochs=3, batch_rows=8192)
+    kw = dict(C=1.0, epochs=3, batches=4)
     f_ref = L.sgd_fit(z, **kw)
     f_aff = L.sgd_fit(shifted, affine=st.aff, **kw)
     assert np.allclose(f_aff.w, f_ref.w, rtol=0, atol=3e-3)

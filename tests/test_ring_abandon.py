@@ -1,0 +1,161 @@
+"""Shared-memory request ring (csrc/serve/shm_ring.h): a producer that gives up -- timed out
+waiting for its results, timed out waiting for a free slot, or dead between taking its tickets
+and publishing them -- must never let another request read its results, and must never stall
+the owner.  The owner is driven by hand from this thread; producers run in threads."""
+import threading
+import time
+
+import numpy as np
+import pytest
+
+R = pytest.importorskip("fraud_detection_amd._fdx_ring")
+
+D, W = 3, 2
+
+
+def _ring(nslots=4, slot_rows=2):
+    r = R.Ring("", nslots, D, slot_rows, W)
+    r.owner_state = R.OWNER_READY
+    return r
+
+
+def _serve(r, rows_expected, dst, fn=lambda x: x[:, 0] * 10.0, delay=0.0, timeout_ms=2000.0):
+    """One owner round: collect, check the batch, answer prob = fn(rows), logit = -prob."""
+    n, op = r.collect(dst.ctypes.data, dst.shape[0], 0.0, timeout_ms, 0)
+    assert n == rows_expected, (n, rows_expected)
+    got = dst[:n].copy()
+    if delay:
+        time.sleep(delay)
+    prob = np.ascontiguousarray(fn(got), np.float32)
+    logit = np.ascontiguousarray(-prob, np.float32)
+    r.complete(prob.ctypes.data, logit.ctypes.data)
+    return got
+
+
+def _request(r, X, timeout_ms, box):
+    try:
+        box["out"] = r.request(X, 0, timeout_ms)
+    except RuntimeError as e:
+        box["err"] = str(e)
+
+
+def _start(r, X, timeout_ms):
+    box = {}
+    th = threading.Thread(target=_request, args=(r, X, timeout_ms, box))
+    th.start()
+    return th, box
+
+
+def _x(v, n=2):
+    return np.full((n, D), v, np.float32) + np.arange(n, dtype=np.float32)[:, None]
+
+
+def test_result_after_producer_timeout_is_not_handed_to_the_next_request():
+    r = _ring()
+    dst = np.zeros((16, D), np.float32)
+    th, box = _start(r, _x(1.0), 150.0)
+    got = _serve(r, 2, dst, delay=0.5)  # the owner holds the batch past the producer's timeout
+    th.join()
+    assert np.array_equal(got, _x(1.0)) and "timed out" in box["err"]
+    assert r.stats()["cancelled"] == 1
+    th, box = _start(r, _x(7.0), 3000.0)
+    got = _serve(r, 2, dst)
+    th.join()
+    assert np.array_equal(got, _x(7.0))
+    np.testing.assert_array_equal(box["out"][:, 0], _x(7.0)[:, 0] * 10.0)  # its own results
+
+
+def test_ready_slot_cancelled_before_collect_is_skipped():
+    r = _ring()
+    dst = np.zeros((16, D), np.float32)
+    th, box = _start(r, _x(2.0), 100.0)
+    th.join()  # nobody collected: the producer cancels its READY slot
+    assert "timed out" in box["err"]
+    th, box = _start(r, _x(5.0), 3000.0)
+    time.sleep(0.05)
+    got = _serve(r, 2, dst)
+    th.join()
+    assert np.array_equal(got, _x(5.0))
+    np.testing.assert_array_equal(box["out"][:, 0], _x(5.0)[:, 0] * 10.0)
+
+
+def test_ticket_abandoned_while_waiting_for_a_slot_is_skipped():
+    r = _ring(nslots=2, slot_rows=2)
+    dst = np.zeros((16, D), np.float32)
+    th1, box1 = _start(r, _x(1.0, 4), 5000.0)  # both slots
+    time.sleep(0.05)
+    th2, box2 = _start(r, _x(9.0), 100.0)  # ticket 2: no free slot before its deadline
+    th2.join()
+    assert "free slot" in box2["err"]
+    _serve(r, 4, dst)
+    th1.join()
+    np.testing.assert_array_equal(box1["out"][:, 0], _x(1.0, 4)[:, 0] * 10.0)
+    th3, box3 = _start(r, _x(4.0), 3000.0)  # ticket 3: the owner must skip abandoned ticket 2
+    time.sleep(0.05)
+    got = _serve(r, 2, dst)
+    th3.join()
+    assert np.array_equal(got, _x(4.0))
+    np.testing.assert_array_equal(box3["out"][:, 0], _x(4.0)[:, 0] * 10.0)
+
+
+def test_owner_reclaims_tickets_of_a_dead_producer():
+    r = _ring()
+    r.reclaim_ms = 150.0
+    dst = np.zeros((16, D), np.float32)
+    r.debug_take_tickets(2)  # a producer died right after taking its tickets
+    th, box = _start(r, _x(3.0), 5000.0)
+    got = _serve(r, 2, dst, timeout_ms=3000.0)
+    th.join()
+    assert np.array_equal(got, _x(3.0))
+    np.testing.assert_array_equal(box["out"][:, 0], _x(3.0)[:, 0] * 10.0)
+    assert r.stats()["reclaimed"] == 2
+
+
+def test_many_producers_with_random_timeouts_keep_the_ring_consistent():
+    """Stress: producers with short deadlines and a slow owner; every answered request got its
+    own rows' results and the owner never stalls."""
+    r = _ring(nslots=8, slot_rows=2)
+    stop = threading.Event()
+
+    def owner():
+        dst = np.zeros((64, D), np.float32)
+        rng = np.random.default_rng(0)
+        while not stop.is_set():
+            n, _ = r.collect(dst.ctypes.data, 64, 0.0, 20.0, 0)
+            if n:
+                time.sleep(float(rng.uniform(0, 0.004)))
+                prob = np.ascontiguousarray(dst[:n, 0] * 10.0, np.float32)
+                r.complete(prob.ctypes.data, prob.ctypes.data)
+
+    ow = threading.Thread(target=owner)
+    ow.start()
+    bad = []
+
+    def producer(k):
+        rng = np.random.default_rng(k)
+        for i in range(60):
+            X = _x(float(k * 1000 + i), int(rng.integers(1, 6)))
+            try:
+                out = r.request(X, 0, float(rng.choice([1.0, 3.0, 50.0])))
+            except RuntimeError:
+                continue
+            if not np.array_equal(out[:, 0], X[:, 0] * 10.0):
+                bad.append((k, i))
+
+    ths = [threading.Thread(target=producer, args=(k,)) for k in range(6)]
+    try:
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        # after the storm a normal request still completes promptly
+        try:
+            out = r.request(_x(-1.0), 0, 3000.0)
+        except RuntimeError:
+            tg = r.debug_tags()
+            raise AssertionError(([(t >> 3, t & 7) for t in tg[:-2]], tg[-2:], r.stats()))
+    finally:
+        stop.set()
+        ow.join()
+    assert not bad
+    np.testing.assert_array_equal(out[:, 0], _x(-1.0)[:, 0] * 10.0)

@@ -78,6 +78,29 @@ def test_dispatcher_routes_small_batches_to_host():
         owner.stop()
 
 
+def test_dispatcher_explain_splits_big_batches_and_falls_back():
+    """/predict/batch with explain=true through a GPU owner must explain any batch size
+    (split into ring-sized requests) and degrade to the front-end's own engine when the owner is
+    down -- never an HTTP 500."""
+    from fraud_detection_amd.serve.gpu_owner import Dispatcher, GpuOwner, RingClient
+
+    eng = _engine()
+    owner = GpuOwner(eng, "", max_batch=64, nslots=4, slot_rows=8).start()  # ring: 32 rows
+    try:
+        cli = RingClient(owner.ring, timeout_ms=3000.0)
+        disp = Dispatcher(eng, cli, host_max_rows=0)  # a front-end: the owner lives elsewhere
+        rows = kaggle_like_rows(150, seed=3)
+        ex = eng.explain(rows, "linear")
+        p, phi = disp.explain(rows, "linear")
+        np.testing.assert_allclose(p, ex.prob, rtol=1e-6, atol=1e-12)
+        np.testing.assert_allclose(phi, ex.phi, rtol=1e-5, atol=1e-6)
+        assert owner.rows >= 150
+    finally:
+        owner.stop()
+    p2, phi2 = disp.explain(rows, "linear")  # owner stopped: this process's engine answers
+    np.testing.assert_allclose(phi2, ex.phi, rtol=1e-12, atol=1e-12)
+
+
 def test_ring_fails_requests_when_owner_stops():
     from fraud_detection_amd import _fdx_ring as R
 

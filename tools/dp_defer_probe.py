@@ -35,6 +35,7 @@ def main():
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             ts.append((round((t1 - t0) * 1e3, 2), round((t2 - t0) * 1e3, 2)))
+        pipe.settle()
         it = r.fit.n_iter
         if comm.rank == 0:
             print(f"defer={defer} (host ms, host+sync ms) per fit: {ts} n_iter={it} pred={pipe._full_pred}", flush=True)

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Attribute the cost of global-scope vs shard-scope SMOTE under data parallelism.
+
+Run under torchrun (the one-GPU rehearsal: FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo, two ranks
+on cuda:0).  For each scope rank 0 prints one JSON line with:
+  * per-fit wall times of back-to-back fits (no sync between them) and of synchronised fits;
+  * the per-phase device-synchronised times of one profiled fit (DevicePipeline profile=True);
+  * the collective breakdown of the timed fits (Communicator stats);
+  * the top host functions by own time over the timed fits (cProfile, rank 0).
+
+    torchrun --nproc-per-node 2 tools/dp_scope_probe.py [--rows 2000000] [--fits 5]
+"""
+import argparse
+import cProfile
+import io
+import json
+import os
+import pstats
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rows", type=int, default=2_000_000)
+    ap.add_argument("--fits", type=int, default=5)
+    ap.add_argument("--scopes", default="shard,global")
+    ap.add_argument("--solver", default="newton")
+    a = ap.parse_args()
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    local = 0 if os.environ.get("FDX_BENCH_ONE_GPU") == "1" else int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    comm = Communicator(backend=os.environ.get("FDX_BENCH_BACKEND") or None, device=dev)
+    n_train = a.rows - a.rows // 5
+    X, y = separable(n_train, seed=1000 + comm.rank, device=dev)
+    for scope in a.scopes.split(","):
+        pipe = DevicePipeline(TrainConfig(seed=42, solver=a.solver, smote_scope=scope), comm)
+        for _ in range(2):
+            pipe.fit(X, y)
+        comm.barrier()
+        torch.cuda.synchronize(dev)
+        comm.stats.reset()
+        prof = cProfile.Profile()
+        prof.enable()
+        t0 = time.perf_counter()
+        for _ in range(a.fits):
+            r = pipe.fit(X, y)
+        torch.cuda.synchronize(dev)
+        back_to_back = (time.perf_counter() - t0) / a.fits
+        prof.disable()
+        coll = comm.collective_summary()
+        synced = []
+        for _ in range(a.fits):
+            comm.barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            r = pipe.fit(X, y)
+            pipe.settle()  # every rank verifies its pending fit here (a deferred check waits)
+            torch.cuda.synchronize(dev)
+            synced.append(round((time.perf_counter() - t1) * 1e3, 3))
+        p = pipe.fit(X, y, profile=True)
+        s = io.StringIO()
+        pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
+        out = {"scope": scope, "rank": comm.rank, "ms_back_to_back": round(back_to_back * 1e3, 3),
+               "ms_synced": synced, "phase_ms": {k: round(v * 1e3, 3) for k, v in p.timings.items()},
+               "n_train_rows": int(r.n_train_rows), "n_synthetic": int(r.n_synthetic),
+               "newton_iters": int(r.fit.n_iter), "virtual_smote": pipe._virtual is not None,
+               "collectives": coll}
+        if comm.rank == 0:
+            print(json.dumps(out), flush=True)
+            print(s.getvalue(), file=sys.stderr, flush=True)
+    comm.close()
+
+
+if __name__ == "__main__":
+    main()

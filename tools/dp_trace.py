@@ -39,6 +39,7 @@ def main():
         torch.cuda.synchronize(dev)
         comm.trace.clear()
         res = pipe.fit(X, y)
+        pipe.settle()
         torch.cuda.synchronize(dev)
         out[name] = {"collectives": len(comm.trace), "trace": [list(t) for t in comm.trace],
                      "newton_iters": int(res.fit.n_iter)}

@@ -18,11 +18,13 @@
 #   marker       rocprofv3 --marker-trace --kernel-trace with the pipeline's roctx phase markers
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
+#   quicksgd     the same with the SGD solver
 #   pmc          two PMC passes over a short bench
 #   pmcfp8       logreg pass counters + kernel stats with fp8 and with bf16 rows
 #   gbdt         tools/gbdt_bench.py at the bench shape; gbdtprof: its kernel trace (20 trees)
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
 #   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
+#   dpscope      tools/dp_scope_probe.py: global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo)
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -54,6 +56,8 @@ for st in "$@"; do
     bench) step bench 600 python bench.py ;;
     bench50) step bench50 600 python bench.py --steps 50 --warmup 5 ;;
     benchfp8) step benchfp8 600 python bench.py --storage fp8 ;;
+    quicksgd) step quicksgd_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd &&
+           step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
@@ -106,6 +110,9 @@ for st in "$@"; do
     dp2self)  # bench.py --gpus 2 starts its own 2 ranks (self-launch path), one GPU, gloo
       step dp2self 300 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python bench.py --gpus 2 --steps 3 --warmup 1 \
         --rows-per-gpu 2000000 ;;
+    dpscope)  # global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo): per-fit times, phases, host profile
+      step dpscope 400 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/dp_scope_probe.py --rows 2000000 ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
     *) echo "unknown stage $st"; exit 2 ;;
