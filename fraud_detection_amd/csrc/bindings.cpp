@@ -585,6 +585,52 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_sgd_step(P<const float>(partial), nblocks, P<double>(state), P<float>(w32), P<int>(done),
                          P<const double>(aff), sgd_args(d, C, c, mom, fi, nb, avg, epoch_end, tol), S(s));
   });
+  // The whole single-process SGD schedule in one call: steps [s0, s1) of epochs x nb minibatches,
+  // each one FISH pass (row phase b) + the fused reduce/update -- no Python per step (the host
+  // enqueue of two launches per step from Python was ~as long as the device step).
+  m.def("sgd_run", [sgd_args](u X, int fp8, float x_scale, int64_t end, u w32, u cw, u done, u partial, int blocks,
+                              u s, u parents, u nbr, u lam, u off, u cnt, int64_t n_real, int64_t q_offset, int mq,
+                              int k, int64_t hole_at, int64_t hole_len, u state, u aff, int d, double C, double mom,
+                              int fi, double tol, int nb, int epochs, int average, std::vector<double> lrs, int s0,
+                              int s1, u acc, u ticket) {
+    if (nb < 1 || epochs < 1 || (int)lrs.size() < epochs || s0 < 0 || s1 > nb * epochs)
+      throw std::runtime_error("sgd_run: bad schedule");
+    fdx::SmoteView v;
+    const fdx::SmoteView* vp = nullptr;
+    if (parents) {
+      v.parents = P<const uint16_t>(parents);
+      v.nbr = P<const int>(nbr);
+      v.lam = P<const uint16_t>(lam);
+      v.off = P<const int>(off);
+      v.cnt = P<const int>(cnt);
+      v.n_real = n_real;
+      v.q_offset = q_offset;
+      v.mq = mq;
+      v.k = k;
+      vp = &v;
+    }
+    fdx::RowHole h;
+    h.at = hole_at;
+    h.len = hole_len;
+    for (int st = s0; st < s1; ++st) {
+      const int ep = st / nb, b = st % nb;
+      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, nb, average && ep == epochs - 1, b == nb - 1, tol);
+      if (acc) {  // one launch per step (fixed-point atomics + last-block update)
+        fdx::launch_sgd_pass_fused(P<const void>(X), fp8, x_scale, end, P<float>(w32), P<const float>(cw), P<int>(done),
+                                   nb, b, blocks, vp, h, P<unsigned long long>(acc), P<unsigned int>(ticket),
+                                   P<double>(state), P<const double>(aff), a, S(s));
+        continue;
+      }
+      if (fp8)
+        fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), 0, end, P<const float>(w32), P<const float>(cw),
+                                    P<const int>(done), 0, nb, x_scale, P<float>(partial), blocks, S(s), vp, b, true, h);
+      else
+        fdx::launch_logreg_pass(P<const uint16_t>(X), 0, end, P<const float>(w32), P<const float>(cw),
+                                P<const int>(done), 0, nb, P<float>(partial), blocks, S(s), vp, b, true, h);
+      fdx::launch_sgd_step(P<const float>(partial), blocks, P<double>(state), P<float>(w32), P<int>(done),
+                           P<const double>(aff), a, S(s));
+    }
+  });
   m.def("sgd_update", [sgd_args](u red, u state, u w32, u done, u aff, int d, double C, double c, double mom, int fi,
                                  int nb, int avg, int epoch_end, double tol, u s) {
     fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), P<const double>(aff),

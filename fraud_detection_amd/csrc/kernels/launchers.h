@@ -128,10 +128,11 @@ struct SmoteView {
 };
 // Lambda buckets of SMOTE samples [sample_offset, sample_offset + n_new) of one global draw
 // sequence (smote.hip, two-level LDS counting sort).  table: int32 [blocks(n_new) * bins];
-// stage 0 fills it with per-(block, bin) counts (and zeroes *bump), the caller scans it
-// inclusively in place, stage 1 writes the coarse records rec (uint32 [n_new]), stage 2 writes
-// each pick's lambda run (pstart, pcnt: int32 [mq k]) into lam (uint16 [n_new]); tmp (uint32
-// [n_new]) is scratch for bins too big for the LDS stage.
+// stage 0 fills it with per-(block, bin) counts (and zeroes *bump), stage 1 turns each block's row
+// into its within-block exclusive prefix and writes the coarse records rec (uint32 [n_new]; a
+// block's run starts at a closed-form offset, no global scan), stage 2 writes each pick's lambda
+// run (pstart, pcnt: int32 [mq k]) into lam (uint16 [n_new]); tmp (uint32 [n_new]) is scratch for
+// bins too big for the LDS stage.
 constexpr uint64_t kSmoteBucketMaxPicks = 1ull << 21;  // <= 16384 coarse bins of <= 128 picks
 int smote_bucket_bins(int64_t range, int64_t n_new);
 int smote_bucket_blocks(int64_t n_new);
@@ -184,6 +185,12 @@ struct SgdArgs {
 // one process: fixed-order reduce of the FISH pass's partials + the update, one launch
 void launch_sgd_step(const float* partial, int nblocks, double* state, float* w32, int* done, const double* aff,
                      const SgdArgs& a, hipStream_t stream);
+// one process, one launch per step: the FISH pass with fixed-point atomic sums and the update in
+// its last block (acc: 36 int64, ticket: 1 uint32 -- both zero between steps)
+void launch_sgd_pass_fused(const void* X, int fp8, float x_scale, int64_t row_end, float* w32, const float* class_w,
+                           int* done, int row_sub, int row_phase, int nblocks, const SmoteView* sv, RowHole hole,
+                           unsigned long long* acc, unsigned int* ticket, double* state, const double* aff,
+                           const SgdArgs& a, hipStream_t stream);
 // data parallel: the update from the all-reduced [36] sums
 void launch_sgd_update(const double* red, double* state, float* w32, int* done, const double* aff,
                        const SgdArgs& a, hipStream_t stream);

@@ -170,6 +170,62 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   dsum = (HESS || FISH) ? (float)((double)sd * inv) : 0.0f;
 }
 
+// ---- fused SGD step (FUSE passes: one launch per SGD step) ------------------------------------
+// Instead of writing [nblocks][36] float partials for a separate reduce + update launch, every block
+// maps its sums to standardized space (the affine map of pivot-shifted rows), rounds them to 2^-20
+// fixed point and adds them into 36 int64 device accumulators with agent-scope atomics -- integer
+// addition is associative, so the totals are bitwise the same whatever the arrival order -- then
+// takes a ticket; the block that draws the last ticket swaps the accumulators back to zero, turns
+// them into the step's sums and applies the update (sgd_apply).  Producer and consumer touch the
+// hand-off words with 8-byte agent atomics only (MI355X_MICROARCH.md: valid without fences).
+struct SgdFuse {
+  unsigned long long* acc = nullptr;  // [36] fixed-point sums (zero between steps)
+  unsigned int* ticket = nullptr;     // arrivals (zero between steps)
+  double* st = nullptr;               // solver state
+  float* w32 = nullptr;               // the weights the next pass reads
+  int* done = nullptr;
+  const double* aff = nullptr;        // pivot-shifted rows: (c | 1/sigma)
+  SgdArgs a;
+};
+constexpr double kFixScale = 1048576.0;  // 2^20
+__device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done,
+                          const double* __restrict__ aff, const SgdArgs& a, int t, bool mapped);
+
+// Called by every thread of the block after `red` (the 4 waves' [36] sums) is complete in LDS.
+template <int NW>
+__device__ __forceinline__ void sgd_fused_tail(const float (*red)[36], const SgdFuse& fz) {
+  __shared__ int s_last;
+  __shared__ double rd[36];
+  const int t = threadIdx.x;
+  if (t < 64) {  // wave 0: this block's sums -> standardized space -> fixed point -> atomics
+    double v = 0.0, g30 = 0.0;
+    if (t < 36) {
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += (double)red[w][t];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) g30 += (double)red[w][kBiasCol];
+      if (fz.aff != nullptr && t < 32) v = fz.aff[32 + t] * (v - fz.aff[t] * g30);
+      const long long q = (long long)__builtin_rint(v * kFixScale);
+      if (t != 34 && q != 0)
+        __hip_atomic_fetch_add(fz.acc + t, (unsigned long long)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t == 0) {
+      const unsigned k = __hip_atomic_fetch_add(fz.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = (k == gridDim.x - 1) ? 1 : 0;
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;  // uniform per block
+  if (t < 36) {
+    const unsigned long long q = __hip_atomic_exchange(fz.acc + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    rd[t] = (double)(long long)q * (1.0 / kFixScale);
+  }
+  if (t == 0) __hip_atomic_exchange(fz.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  sgd_apply(rd, fz.st, fz.w32, fz.done, fz.aff, fz.a, t, true);
+}
+
 // VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
 // rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
 // row_sub / row_phase: the pass visits the row tiles t with (t / G) mod row_sub == row_phase
@@ -178,11 +234,11 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
 // minibatches of one SGD epoch (every stored row and every SMOTE sample in exactly one of them).
 // FISH (gradient-only SGD passes): slot 35 also receives sum s p (1 - p), the minibatch's
 // Gauss-Newton curvature scalar that sets the SGD step size (sgd_step_kernel).
-template <bool HESS, bool VIRT = false, bool FISH = false>  // bf16 rows (64 B); fp8: logreg_pass_fp8w_kernel
+template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>  // bf16 rows; fp8: logreg_pass_fp8w_kernel
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
-    const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
+    const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* w,
     const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
-    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole) {
+    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole, SgdFuse fz) {
   if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][36];
@@ -382,6 +438,10 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     }
   }
   __syncthreads();
+  if constexpr (FUSE) {  // one launch per SGD step: fixed-point atomics + last-block update
+    sgd_fused_tail<kWaves>(red, fz);
+    return;
+  }
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
   // slot 34 (Hessian weight) only from Hessian passes, slot 35 (curvature sum) from FISH passes
   if (threadIdx.x < (HESS ? 35 : 34) || (FISH && threadIdx.x == 35)) {
@@ -403,11 +463,12 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 // 16M rows (5.2 TB/s), fp8 bench step 1.164 -> 1.099 ms.
 // VIRT: virtual SMOTE samples as in the bf16 kernel, tiles of 32 picks (2 lanes per pick).
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-template <bool HESS, bool VIRT = false, bool FISH = false>
+template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
-    const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* __restrict__ w,
+    const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, int row_sub, int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole) {
+    int hess_stride, int row_sub, int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole,
+    SgdFuse fz) {
   if (done != nullptr && *done) return;
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][36];
@@ -619,6 +680,10 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     }
   }
   __syncthreads();
+  if constexpr (FUSE) {
+    sgd_fused_tail<kWaves>(red, fz);
+    return;
+  }
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
   if (threadIdx.x < (HESS ? 35 : 34) || (FISH && threadIdx.x == 35)) {
     const int t = threadIdx.x;
@@ -1003,7 +1068,7 @@ constexpr double kDbarFloor = 1e-3;  // lr_t <= c / 1e-3: a saturated minibatch 
 constexpr int kSgdSlots = 36;        // grad[32] | loss | weight | (34: unused) | curvature sum
 
 __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done,
-                          const double* __restrict__ aff, const SgdArgs& a, int t) {
+                          const double* __restrict__ aff, const SgdArgs& a, int t, bool mapped) {
   // rd: the reduced [36] sums in LDS (raw row space).  Every thread of the block calls this (it
   // holds block barriers); only the first wave (t < 64) reads or writes state.
   __shared__ double rz[32], ss[kW + 32], cA[32], iA[32];
@@ -1015,7 +1080,8 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
     __syncthreads();
   }
   const double S = rd[33] > 0.0 ? rd[33] : 1.0;
-  if (t < 32) rz[t] = aff ? iA[t] * (rd[t] - cA[t] * rd[kBiasCol]) : rd[t];
+  // mapped: the sums arrive in standardized space already (fused passes map them per block)
+  if (t < 32) rz[t] = (aff && !mapped) ? iA[t] * (rd[t] - cA[t] * rd[kBiasCol]) : rd[t];
   const double reg = 1.0 / (a.C * S * (double)a.nb);  // the minibatch estimates sum s over the epoch as nb S
   const double dbar = fmax(rd[35] / S, kDbarFloor);
   const double lr = a.c / dbar;
@@ -1123,7 +1189,7 @@ __global__ __launch_bounds__(1024) void sgd_step_kernel(const float* __restrict_
     rd[threadIdx.x] = r;
   }
   __syncthreads();
-  sgd_apply(rd, st, w32, done, aff, a, threadIdx.x);
+  sgd_apply(rd, st, w32, done, aff, a, threadIdx.x, false);
 }
 
 // Data parallel: the reduced sums were all-reduced across ranks in `red` (logreg_reduce with 36
@@ -1136,7 +1202,7 @@ __global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict
   const int t = threadIdx.x;
   if (t < kSgdSlots) rd[t] = red[t];
   __syncthreads();
-  sgd_apply(rd, st, w32, done, aff, a, t);
+  sgd_apply(rd, st, w32, done, aff, a, t, false);
 }
 
 }  // namespace
@@ -1202,7 +1268,7 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
   const int hs = hessian > 0 ? hessian : 1;
 #define FDX_LRP(H, V, F)                                                                                    \
   logreg_pass_kernel<H, V, F><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, hs, \
-                                                                row_sub, row_phase, partial, v, hole)
+                                                                row_sub, row_phase, partial, v, hole, SgdFuse{})
   if (hessian > 0) {
     if (virt) FDX_LRP(true, true, false);
     else FDX_LRP(true, false, false);
@@ -1232,7 +1298,8 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
   const int hs = hessian > 0 ? hessian : 1;
 #define FDX_LRP8(H, V, F)                                                                                       \
   logreg_pass_fp8w_kernel<H, V, F><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done,   \
-                                                                     x_scale, 30, hs, row_sub, row_phase, partial, v, hole)
+                                                                     x_scale, 30, hs, row_sub, row_phase, partial, v, hole, \
+                                                                     SgdFuse{})
   if (hessian > 0) {
     if (virt) FDX_LRP8(true, true, false);
     else FDX_LRP8(true, false, false);
@@ -1245,6 +1312,44 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
   }
 #undef FDX_LRP8
   check_launch("logreg_pass_fp8");
+}
+
+// One SGD step in ONE launch (single process): minibatch `row_phase` of `row_sub` through the
+// FISH pass whose blocks add their fixed-point sums into acc[36] and whose last block applies the
+// update (sgd_fused_tail).  acc and ticket must be zero before the first step (they are left zero).
+void launch_sgd_pass_fused(const void* X, int fp8, float x_scale, int64_t row_end, float* w32, const float* class_w,
+                           int* done, int row_sub, int row_phase, int nblocks, const SmoteView* sv, RowHole hole,
+                           unsigned long long* acc, unsigned int* ticket, double* state, const double* aff,
+                           const SgdArgs& a, hipStream_t stream) {
+  if (row_sub < 1 || row_phase < 0 || row_phase >= row_sub) throw std::runtime_error("sgd_pass_fused: bad phase");
+  const SmoteView v = checked_view(sv, 0, row_end);
+  check_hole(hole, 0, v.parents != nullptr ? v.n_real : row_end);
+  SgdFuse fz;
+  fz.acc = acc;
+  fz.ticket = ticket;
+  fz.st = state;
+  fz.w32 = w32;
+  fz.done = done;
+  fz.aff = aff;
+  fz.a = a;
+  const bool virt = v.parents != nullptr;
+  if (fp8) {
+    const uint8_t* X8 = static_cast<const uint8_t*>(X);
+    if (virt)
+      logreg_pass_fp8w_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X8, 0, row_end, w32, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+    else
+      logreg_pass_fp8w_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X8, 0, row_end, w32, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+  } else {
+    if (virt)
+      logreg_pass_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X, 0, row_end, w32, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+    else
+      logreg_pass_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X, 0, row_end, w32, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+  }
+  check_launch("sgd_pass_fused");
 }
 
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,

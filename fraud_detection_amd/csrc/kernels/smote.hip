@@ -249,7 +249,14 @@ constexpr int kSegMax = 2048;         // level 2: segment table of <= 2048 level
 constexpr int kL2Threads = 1024;
 constexpr int kL2Waves = kL2Threads / 64;
 
-__device__ __forceinline__ int excl_at(const int* incl, int64_t i) { return i == 0 ? 0 : incl[i - 1]; }
+
+// Samples of one global draw sequence before level-1 block b: every block covers kBucketPairs
+// whole Philox pairs (128-sample blocks of the sequence), so the count is closed-form -- the
+// record array needs no global scan to place a block's run.
+__device__ __forceinline__ int64_t l1_block_base(int64_t b, int64_t n_new) {
+  const int64_t s = b * 2 * (int64_t)kBucketPairs;
+  return s < n_new ? s : n_new;
+}
 
 template <bool SCATTER>
 __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_t range, int fb, int nbins, int64_t n_new,
@@ -259,11 +266,38 @@ __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_
                                                                          uint32_t* __restrict__ rec,
                                                                          unsigned long long* __restrict__ bump) {
   extern __shared__ int h[];  // [nbins] counts / cursors, then (SCATTER) [2 kBucketPairs] records
+  __shared__ int wtot[kBucketThreads / kWave];
   uint32_t* srec = reinterpret_cast<uint32_t*>(h + nbins);
   const int64_t tb = (int64_t)blockIdx.x * nbins;
-  const int base = SCATTER ? excl_at(table, tb) : 0;
-  for (int b = threadIdx.x; b < nbins; b += kBucketThreads) h[b] = SCATTER ? excl_at(table, tb + b) - base : 0;
-  if (!SCATTER && blockIdx.x == 0 && threadIdx.x == 0) *bump = 0ull;  // level 2's allocator
+  if constexpr (SCATTER) {
+    // this block's row of counts -> exclusive prefix in LDS (block-wide scan: each thread a run of
+    // consecutive bins), written back over the counts for level 2 (the within-block start of
+    // every bin; level 2 adds the block's closed-form base)
+    const int per = (nbins + kBucketThreads - 1) / kBucketThreads;
+    const int b0 = threadIdx.x * per, b1 = min(nbins, b0 + per);
+    int run = 0;
+    for (int b = b0; b < b1; ++b) run += table[tb + b];
+    int inc = run;
+    const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+      const int v = __shfl_up(inc, o, kWave);
+      if (lane >= o) inc += v;
+    }
+    if (lane == kWave - 1) wtot[wv] = inc;
+    __syncthreads();
+    int off = inc - run;
+    for (int w = 0; w < wv; ++w) off += wtot[w];
+    for (int b = b0; b < b1; ++b) {
+      const int c = table[tb + b];
+      h[b] = off;
+      table[tb + b] = off;
+      off += c;
+    }
+  } else {
+    for (int b = threadIdx.x; b < nbins; b += kBucketThreads) h[b] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *bump = 0ull;  // level 2's allocator
+  }
   __syncthreads();
   const int64_t npairs = ((n_new + 127) >> 7) << 6;
   const uint32_t fmask = (1u << fb) - 1u;
@@ -286,15 +320,17 @@ __global__ __launch_bounds__(kBucketThreads) void smote_bucket_l1_kernel(uint32_
   }
   __syncthreads();
   if constexpr (SCATTER) {
-    const int cnt = excl_at(table, tb + nbins) - base;  // the next block's start (or the total)
+    const int64_t base = l1_block_base(blockIdx.x, n_new);
+    const int cnt = (int)(l1_block_base(blockIdx.x + 1, n_new) - base);
     for (int i = threadIdx.x; i < cnt; i += kBucketThreads) rec[base + i] = srec[i];
   } else {  // every entry written: the table needs no fill
     for (int b = threadIdx.x; b < nbins; b += kBucketThreads) table[tb + b] = h[b];
   }
 }
 
-__global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* __restrict__ incl, int nblk, int nbins,
-                                                               uint32_t range, int fb, const uint32_t* __restrict__ rec,
+__global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* __restrict__ pref, int nblk, int nbins,
+                                                               uint32_t range, int fb, int64_t n_new,
+                                                               const uint32_t* __restrict__ rec,
                                                                uint32_t* __restrict__ tmp, int* __restrict__ pstart,
                                                                int* __restrict__ pcnt, uint16_t* __restrict__ lam,
                                                                unsigned long long* __restrict__ bump) {
@@ -317,11 +353,13 @@ __global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* 
   for (int u = 0; u < kPer; ++u) {
     const int b = threadIdx.x * kPer + u;
     int l = 0;
-    if (b < nblk) {
+    if (b < nblk) {  // pref: level 1's within-block exclusive prefix of the bins
       const int64_t e = (int64_t)b * nbins + bin;
-      const int s0 = excl_at(incl, e);
-      sstart[b] = s0;
-      l = excl_at(incl, e + 1) - s0;
+      const int64_t base = l1_block_base(b, n_new);
+      const int p0 = pref[e];
+      const int p1 = bin + 1 < nbins ? pref[e + 1] : (int)(l1_block_base(b + 1, n_new) - base);
+      sstart[b] = (int)(base + p0);
+      l = p1 - p0;
     }
     len[u] = l;
     tot += l;
@@ -466,8 +504,8 @@ void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample
     smote_bucket_l1_kernel<true><<<nblk, kBucketThreads, lds, stream>>>(
         (uint32_t)R, fb, nbins, n_new, sample_offset >> 7, k0, k1, c0, c1, table, rec, bump);
   } else {
-    smote_bucket_l2_kernel<<<nbins, kL2Threads, 0, stream>>>(table, nblk, nbins, (uint32_t)R, fb, rec, tmp, pstart, pcnt,
-                                                       lam, bump);
+    smote_bucket_l2_kernel<<<nbins, kL2Threads, 0, stream>>>(table, nblk, nbins, (uint32_t)R, fb, n_new, rec, tmp,
+                                                             pstart, pcnt, lam, bump);
   }
   check_launch("smote_bucket");
 }

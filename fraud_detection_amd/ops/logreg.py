@@ -97,11 +97,12 @@ class VirtualSmote:
         w = (ws or BucketWorkspace()).get(self.parents.device, nt, n, R)
         args = (mq, k, n, int(self.sample_offset), int(self.seed) & (2**64 - 1),
                 int(self.counter_base) & (2**64 - 1))
-        # stage 0 writes every table entry (no fill) and zeroes the bump allocator
+        # stage 0 writes every table entry (no fill) and zeroes the bump allocator; stage 1 scans
+        # each block's row in LDS (no global scan: a block's record run starts at a closed-form
+        # offset) and scatters the coarse records; stage 2 assembles each pick's lambda run
         m.smote_bucket(0, *args, ptr(w.table), 0, 0, 0, 0, 0, ptr(w.bump), s)        # counts [block][bin]
-        torch.cumsum(w.table[:nt], 0, dtype=torch.int32, out=w.scan[:nt])          # inclusive scan
-        m.smote_bucket(1, *args, ptr(w.scan), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # coarse records
-        m.smote_bucket(2, *args, ptr(w.scan), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
+        m.smote_bucket(1, *args, ptr(w.table), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # prefix + records
+        m.smote_bucket(2, *args, ptr(w.table), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
                        ptr(w.bump), s)
         self.lam, self.off, self.cnt, self._ws = w.lam, w.off, w.cnt, w
         return self
@@ -131,7 +132,6 @@ class BucketWorkspace:
         if self.cap is None or self.dev != dev or nt > self.cap[0] or n > self.cap[1] or R > self.cap[2]:
             i32 = torch.int32
             self.table = torch.empty(nt, dtype=i32, device=dev)
-            self.scan = torch.empty(nt, dtype=i32, device=dev)
             self.bump = torch.empty(1, dtype=torch.int64, device=dev)
             self.rec = torch.empty(n, dtype=i32, device=dev)
             self.tmp = torch.empty(n, dtype=i32, device=dev)
@@ -191,7 +191,9 @@ class PendingFit:
         cls._next += 1
         prev = cls._owners[slot]
         if prev is not None:
-            prev._materialize()
+            # a program-order point every rank reaches at the same fit (slots rotate identically
+            # on every rank): verifying a DP fit here is collective-safe
+            prev._materialize(collective_ok=True)
         cls._owners[slot] = self
         self._slot, self._sgd, self._info = slot, sgd, None
         self._verify, self._state_dev, self.warm_iters = verify, state_dev, int(warm_iters)
@@ -227,9 +229,9 @@ class PendingFit:
     def deferred(self) -> bool:
         return self._verify is not None
 
-    def _materialize(self) -> FitInfo:
+    def _materialize(self, collective_ok: bool = False) -> FitInfo:
         if self._info is None:
-            if self._verify is not None and self._collective:
+            if self._verify is not None and self._collective and not collective_ok:
                 raise RuntimeError("data-parallel fit with a pending convergence check: settle it on every "
                                    "rank first (DevicePipeline.settle() or evaluate(...)), then read it")
             self.verify()
@@ -275,6 +277,9 @@ class LRWorkspace:
         # reset is ONE async copy from a pinned mirror of the same layout
         self._blob = torch.zeros(_BLOB_BYTES, device=device, dtype=torch.uint8)
         self.state, self.w32, self.class_w, self.done = _blob_views(self._blob)
+        # fused SGD steps: 36 int64 fixed-point accumulators + the arrival ticket; zero between
+        # steps (every step's last block swaps them back to zero)
+        self.sgd_acc = torch.zeros(40, device=device, dtype=torch.int64)
 
     def prepare_flags(self, depth: int = 2):
         """The mapped pinned convergence-flag words newton_fit polls (pinned allocations cost tens
@@ -729,6 +734,25 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     fp8 = storage_kind(rows) != "bf16"
     blocks = ref.sgd_grid_blocks(n_stored, nb, ws.nblocks_fp8 if fp8 else ws.nblocks)
     dp = comm is not None and comm.world_size > 1
+    v = virtual
+    mq, k = (v.nbr.shape if v is not None else (0, 1))
+
+    def run_steps(s0: int, s1: int):
+        """Steps [s0, s1) of the schedule, one fused launch each (FISH pass whose last block
+        applies the update), enqueued by one native call."""
+        m.sgd_run(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w), ptr(ws.done),
+                  ptr(ws.partial), blocks, s,
+                  ptr(v.parents) if v else 0, ptr(v.nbr) if v else 0, ptr(v.lam) if v else 0,
+                  ptr(v.off) if v else 0, ptr(v.cnt) if v else 0, int(rows.shape[0]),
+                  int(v.q_offset) if v else 0, int(mq), int(k), int(hole[0]), int(hole[1]), ptr(ws.state), aff, d,
+                  float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
+                  [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
+                  ptr(ws.sgd_acc[38:]))
+
+    if not dp and checkpoint is None:
+        s0 = start[0] * nb + start[1]
+        run_steps(s0, epochs * nb if max_steps is None else min(epochs * nb, int(max_steps)))
+        return PendingFit(ws.state, sgd=True)
     for ep in range(start[0], epochs):
         c = lrs[ep]
         for b in range(start[1] if ep == start[0] else 0, nb):
@@ -736,15 +760,14 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                 break
             avg = int(average and ep == epochs - 1)
             last = b + 1 == nb
-            _sgd_pass(m, rows, ws, n, fp8_scale, s, b, nb, blocks, virtual, hole)
             if dp:
+                _sgd_pass(m, rows, ws, n, fp8_scale, s, b, nb, blocks, virtual, hole)
                 m.logreg_reduce(ptr(ws.partial), blocks, SGD_SLOTS, ptr(ws.red), ptr(ws.done), s)
                 comm.all_reduce_(ws.red[:SGD_SLOTS])
                 m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
                              float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
-            else:
-                m.sgd_step(ptr(ws.partial), blocks, ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
-                           float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
+            else:  # the same fused launch as the uninterrupted fit: checkpointed fits stay bit-identical
+                run_steps(ep * nb + b, ep * nb + b + 1)
             gstep = ep * nb + b + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 nxt = (ep + 1, 0) if last else (ep, b + 1)

@@ -11,10 +11,12 @@
 #   bench50      bench.py --steps 50
 #   configs      tools/baseline_configs.py (every BASELINE config)
 #   ubench       tools/ubench.py per-kernel event timings
+#   passlab      tools/pass_lab.py: solver pass / reduce / update launches and whole fits at the bench shape
 #   latency      tools/serve_latency.py
 #   plots        the reference script chain (generate -> eda -> preprocess -> train -> evaluate -> explain) with its plots
 #   prof         rocprofv3 --kernel-trace --stats of a short bench
 #   proffp8      the same with fp8 training rows
+#   profsgd      kernel trace + one-step timeline of the SGD fit
 #   marker       rocprofv3 --marker-trace --kernel-trace with the pipeline's roctx phase markers
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
@@ -60,6 +62,7 @@ for st in "$@"; do
            step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
+    passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
     configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;
     plots) step plots 900 python scripts/run_reference_pipeline.py --out "$OUT/plots" --kernel ;;
@@ -68,6 +71,11 @@ for st in "$@"; do
       cd /tmp && export TMPDIR=/tmp
       step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-extras
       cd "$R" ;;
+    profsgd)  # kernel trace of the SGD fit (config 3's solver)
+      cd /tmp && export TMPDIR=/tmp
+      step profsgd 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profsgd" -o run -- python3 "$R/bench.py" --solver sgd --steps 5 --warmup 1 --no-extras
+      cd "$R"
+      python tools/timeline.py "$OUT/profsgd/run_kernel_trace.csv" > "$OUT/timeline_sgd_step.txt" 2>&1 || true ;;
     proffp8)
       cd /tmp && export TMPDIR=/tmp
       step proffp8 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proffp8" -o run -- python3 "$R/bench.py" --storage fp8 --steps 5 --warmup 1 --no-extras
