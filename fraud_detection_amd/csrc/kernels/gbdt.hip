@@ -53,34 +53,57 @@ __device__ __forceinline__ bool is_built(int node, const int64_t* gcnt) {
 
 // ---- quantisation ----------------------------------------------------------------------------
 // 8 lanes per row, 4 features per lane: the 8 lanes write one 32-byte binned row.
+//  * VEC (rows 16-byte aligned, ld % 4 == 0 -- the pipeline's [n, 32] fp32 rows): each lane reads
+//    its 4 features with ONE 16-byte load, so a row is one coalesced 128-byte read (the scalar
+//    form issued 4 loads per lane);
+//  * the upper-bound search is branchless over the 256 cut slots (cuts past nbins are +inf):
+//    8 dependent LDS reads with the lane's 4 features as 4 independent chains, and a NaN lands in
+//    the last bin exactly as the branchy search did (!(cut > x) holds);
+//  * the LDS cut table is bin-major with a 33-float row (sc[b][f]): the 8 features a wave reads at
+//    the same search depth sit in distinct banks instead of all in bank (mid mod 64).
+// (2.78 ms -> see profiles/README.md r4 GBDT at 16M rows x 30 features)
+constexpr int kCutLd = 33;
+template <bool VEC>
 __global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__ X, int64_t n, int ld,
                                                        int d, const float* __restrict__ cuts,
                                                        const int* __restrict__ nbins,
                                                        uint8_t* __restrict__ bins) {
-  __shared__ float sc[kGBMaxFeat][kGBBins];
+  __shared__ float sc[kGBBins * kCutLd];
   __shared__ int snb[32];
-  for (int i = threadIdx.x; i < d * kGBBins; i += blockDim.x) sc[i / kGBBins][i % kGBBins] = cuts[i];
+  for (int i = threadIdx.x; i < kGBBins * 32; i += blockDim.x) {
+    const int b = i >> 5, f = i & 31;
+    sc[b * kCutLd + f] = f < d ? cuts[f * kGBBins + b] : __builtin_inff();
+  }
   if (threadIdx.x < 32) snb[threadIdx.x] = threadIdx.x < d ? nbins[threadIdx.x] : 1;
   __syncthreads();
   const int sub = threadIdx.x & 7;
+  int nbm1[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) nbm1[j] = snb[sub * 4 + j] - 1;
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 8);
   for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 8) + (threadIdx.x >> 3); r < n; r += stride) {
+    float x[4];
+    if constexpr (VEC) {
+      const float4 v = reinterpret_cast<const float4*>(X + r * ld)[sub];
+      x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) x[j] = (sub * 4 + j < d) ? X[r * ld + sub * 4 + j] : 0.0f;
+    }
+    int b[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int half = kGBBins / 2; half >= 1; half >>= 1) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float c = sc[(b[j] + half - 1) * kCutLd + sub * 4 + j];
+        b[j] += !(c > x[j]) ? half : 0;
+      }
+    }
     uint32_t packed = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int f = sub * 4 + j;
-      int b = 0;
-      if (f < d) {
-        const float x = X[r * ld + f];
-        int lo = 0, hi = snb[f] - 1;  // cuts[f][nb-1] = +inf: result in [0, nb-1]
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (sc[f][mid] > x) hi = mid;
-          else lo = mid + 1;
-        }
-        b = lo;
-      }
-      packed |= (uint32_t)b << (8 * j);
+      const int bb = (sub * 4 + j < d) ? min(b[j], nbm1[j]) : 0;
+      packed |= (uint32_t)bb << (8 * j);
     }
     reinterpret_cast<uint32_t*>(bins + r * kGBRowBytes)[sub] = packed;
   }
@@ -708,9 +731,14 @@ __global__ __launch_bounds__(kPredThreads) void gbdt_predict_kernel(
 void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,
                      uint8_t* bins, hipStream_t stream) {
   if (d > kGBMaxFeat) throw std::runtime_error("gbdt: at most 30 features");
-  static const int cap = resident_cap(gbdt_bin_kernel, 256);
-  const int grid = capped_grid(n, 256 / 8, cap);
-  gbdt_bin_kernel<<<grid, 256, 0, stream>>>(X, n, ld, d, cuts, nbins, bins);
+  const bool vec = (ld % 4) == 0 && (reinterpret_cast<uintptr_t>(X) % 16) == 0 && d <= 32;
+  if (vec) {
+    static const int cap = resident_cap(gbdt_bin_kernel<true>, 256);
+    gbdt_bin_kernel<true><<<capped_grid(n, 256 / 8, cap), 256, 0, stream>>>(X, n, ld, d, cuts, nbins, bins);
+  } else {
+    static const int cap = resident_cap(gbdt_bin_kernel<false>, 256);
+    gbdt_bin_kernel<false><<<capped_grid(n, 256 / 8, cap), 256, 0, stream>>>(X, n, ld, d, cuts, nbins, bins);
+  }
   check_launch("gbdt_bin");
 }
 

@@ -186,7 +186,8 @@ struct SgdArgs {
 void launch_sgd_step(const float* partial, int nblocks, double* state, float* w32, int* done, const double* aff,
                      const SgdArgs& a, hipStream_t stream);
 // one process, one launch per step: the FISH pass with fixed-point atomic sums and the update in
-// its last block (acc: 36 int64, ticket: 1 uint32 -- both zero between steps)
+// its last block (acc: kSgdAccWords = 32 x 36 int64 replicas, ticket: 1 uint32 -- both zero between
+// steps)
 void launch_sgd_pass_fused(const void* X, int fp8, float x_scale, int64_t row_end, float* w32, const float* class_w,
                            int* done, int row_sub, int row_phase, int nblocks, const SmoteView* sv, RowHole hole,
                            unsigned long long* acc, unsigned int* ticket, double* state, const double* aff,

@@ -178,8 +178,14 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
 // takes a ticket; the block that draws the last ticket swaps the accumulators back to zero, turns
 // them into the step's sums and applies the update (sgd_apply).  Producer and consumer touch the
 // hand-off words with 8-byte agent atomics only (MI355X_MICROARCH.md: valid without fences).
+// The accumulators are replicated kSgdReplicas times (block b adds into replica b mod R): 768
+// blocks adding into ONE set of 36 words serialise at the memory-side atomic unit (a fused step
+// measured 41 us against ~26 us for the pass alone, profiles/r4_f); R replicas cut the queue per
+// word R-fold, and the last block folds the replicas in a fixed order.
+constexpr int kSgdReplicas = 32;
+constexpr int kSgdAccWords = kSgdReplicas * 36;
 struct SgdFuse {
-  unsigned long long* acc = nullptr;  // [36] fixed-point sums (zero between steps)
+  unsigned long long* acc = nullptr;  // [kSgdReplicas][36] fixed-point sums (zero between steps)
   unsigned int* ticket = nullptr;     // arrivals (zero between steps)
   double* st = nullptr;               // solver state
   float* w32 = nullptr;               // the weights the next pass reads
@@ -207,7 +213,8 @@ __device__ __forceinline__ void sgd_fused_tail(const float (*red)[36], const Sgd
       if (fz.aff != nullptr && t < 32) v = fz.aff[32 + t] * (v - fz.aff[t] * g30);
       const long long q = (long long)__builtin_rint(v * kFixScale);
       if (t != 34 && q != 0)
-        __hip_atomic_fetch_add(fz.acc + t, (unsigned long long)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(fz.acc + (blockIdx.x % kSgdReplicas) * 36 + t, (unsigned long long)q, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (t == 0) {
@@ -217,11 +224,17 @@ __device__ __forceinline__ void sgd_fused_tail(const float (*red)[36], const Sgd
   }
   __syncthreads();
   if (!s_last) return;  // uniform per block
-  if (t < 36) {
-    const unsigned long long q = __hip_atomic_exchange(fz.acc + t, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __shared__ unsigned long long rep[kSgdAccWords];
+  for (int e = t; e < kSgdAccWords; e += blockDim.x)  // every replica word: read and zero it
+    rep[e] = __hip_atomic_exchange(fz.acc + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) __hip_atomic_exchange(fz.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (t < 36) {  // fixed-order fold of the replicas (integer: exact in any order anyway)
+    unsigned long long q = 0;
+#pragma unroll 8
+    for (int r = 0; r < kSgdReplicas; ++r) q += rep[r * 36 + t];
     rd[t] = (double)(long long)q * (1.0 / kFixScale);
   }
-  if (t == 0) __hip_atomic_exchange(fz.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   sgd_apply(rd, fz.st, fz.w32, fz.done, fz.aff, fz.a, t, true);
 }

@@ -277,9 +277,9 @@ class LRWorkspace:
         # reset is ONE async copy from a pinned mirror of the same layout
         self._blob = torch.zeros(_BLOB_BYTES, device=device, dtype=torch.uint8)
         self.state, self.w32, self.class_w, self.done = _blob_views(self._blob)
-        # fused SGD steps: 36 int64 fixed-point accumulators + the arrival ticket; zero between
-        # steps (every step's last block swaps them back to zero)
-        self.sgd_acc = torch.zeros(40, device=device, dtype=torch.int64)
+        # fused SGD steps: 32 replicas x 36 int64 fixed-point accumulators + the arrival ticket;
+        # zero between steps (every step's last block swaps them back to zero)
+        self.sgd_acc = torch.zeros(SGD_ACC_WORDS + 8, device=device, dtype=torch.int64)
 
     def prepare_flags(self, depth: int = 2):
         """The mapped pinned convergence-flag words newton_fit polls (pinned allocations cost tens
@@ -301,6 +301,7 @@ class LRWorkspace:
 
 
 _BLOB_BYTES = 2304
+SGD_ACC_WORDS = 32 * 36  # logreg.hip kSgdAccWords
 
 
 def _blob_views(blob: torch.Tensor):
@@ -747,7 +748,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                   int(v.q_offset) if v else 0, int(mq), int(k), int(hole[0]), int(hole[1]), ptr(ws.state), aff, d,
                   float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
                   [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
-                  ptr(ws.sgd_acc[38:]))
+                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]))
 
     if not dp and checkpoint is None:
         s0 = start[0] * nb + start[1]

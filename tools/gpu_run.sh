@@ -11,6 +11,7 @@
 #   bench50      bench.py --steps 50
 #   configs      tools/baseline_configs.py (every BASELINE config)
 #   ubench       tools/ubench.py per-kernel event timings
+#   schedlab     tools/sched_lab.py: Newton warm-up schedules on the virtual-SMOTE bench fit
 #   passlab      tools/pass_lab.py: solver pass / reduce / update launches and whole fits at the bench shape
 #   latency      tools/serve_latency.py
 #   plots        the reference script chain (generate -> eda -> preprocess -> train -> evaluate -> explain) with its plots
@@ -62,6 +63,7 @@ for st in "$@"; do
            step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
+    schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
     configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;

@@ -94,11 +94,12 @@ def main():
                                                                       ptr(ws.done), ptr(aff), 30, 1.0, 0.0, 0.5, 1,
                                                                       nb, 0, 0, 0.0, s)), 2)
     mq, k = v.nbr.shape
+    ws.done.zero_()
     us["sgd fused step (pass+update, 1 launch)"] = round(timeit(lambda: m.sgd_run(
         ptr(rows), int(fp8), 4.0, n, ptr(ws.w32), ptr(ws.class_w), ptr(ws.done), ptr(ws.partial), blocks, s,
         ptr(v.parents), ptr(v.nbr), ptr(v.lam), ptr(v.off), ptr(v.cnt), int(rows.shape[0]), int(v.q_offset), int(mq),
         int(k), 0, 0, ptr(ws.state), ptr(aff), 30, 1.0, 0.5, 1, 0.0, nb, 3, 1, [0.4, 0.6, 0.8], 0, 1,
-        ptr(ws.sgd_acc), ptr(ws.sgd_acc[38:]))), 2)
+        ptr(ws.sgd_acc), ptr(ws.sgd_acc[L.SGD_ACC_WORDS:]))), 2)
     out["launch_us"] = us
     w0 = np.zeros(32)
     w0[:30] = np.random.default_rng(42).normal(0.0, 0.01, 30)
