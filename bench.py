@@ -290,11 +290,12 @@ def _variants(args, X, y, Xt, yt, dev, comm, scope) -> dict:
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
 
     out = {}
-    # newton_bf16_stored_smote: the headline fit with its SMOTE rows written and streamed (the
-    # headline folds them into the passes instead: TrainConfig.virtual_smote)
+    # *_stored_smote: the fit with its SMOTE rows written and streamed (the default folds them into
+    # the passes instead: TrainConfig.virtual_smote)
     newton_w = {}
     for name, kw in (("sgd_bf16", dict(solver="sgd", storage="bf16")), ("newton_fp8", dict(solver="newton", storage="fp8")),
                      ("newton_bf16_stored_smote", dict(solver="newton", storage="bf16", virtual_smote=False)),
+                     ("newton_fp8_stored_smote", dict(solver="newton", storage="fp8", virtual_smote=False)),
                      ("sgd_fp8", dict(solver="sgd", storage="fp8"))):
         if kw["solver"] == args.solver and kw["storage"] == args.storage and kw.get("virtual_smote", True):
             continue

@@ -160,6 +160,11 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 // aff (nullable, [64] = c | 1/sigma): the rows are pivot-shifted, not standardized -- the kernel
 // maps the reduced sums into standardized space and writes folded weights to w32.
 // done_host (nullable): device address of a mapped pinned int that receives (seq << 1) | done
+// logreg_reduce + newton_update in one launch (ticket: one zeroed u32; ncols 1088 or 34)
+void launch_newton_reduce_update(const float* partial, int nblocks, int ncols, double* red, unsigned int* ticket,
+                                 double* state, float* w32, int* done, int d, double C, double tol, int max_iter,
+                                 int fit_intercept, int phase_start, const double* aff, hipStream_t stream,
+                                 int* done_host = nullptr, int seq = 0);
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
                           const double* aff, hipStream_t stream, int* done_host = nullptr, int seq = 0);
@@ -216,9 +221,12 @@ void launch_knn_topk_lds(const float* Q, int mq_pad, int mq, const float* C, int
 void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
                       float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
+// seed_tiles > 0: a pilot search over the first seed_tiles candidate tiles (into seed_score /
+// seed_idx [mq][k]) seeds every slice's filter threshold (knn.hip knn_topk_kernel)
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream,
+                     int seed_tiles = 0, float* seed_score = nullptr, int* seed_idx = nullptr);
 
 // ---- smote.hip ----
 // P [m, 32] bf16 = output-space parents: bf16(C * sigma + c) on the feature columns (aff nullable)
@@ -288,6 +296,11 @@ void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts
 void launch_gbdt_grad(const float* margin, const uint8_t* label, int64_t n, float spw, float gscale,
                       float hscale, int2* gh, hipStream_t stream);
 int gbdt_hist_blocks();
+// exact per-feature order statistics of the cut sample (quantile.hip): out [max_bin][d] holds the
+// minimum (row 0) and the values at ranks floor(t m / max_bin); rows r * stride of X [., ld]
+int64_t quantile_select_ws_bytes(int64_t m, int d);
+void launch_quantile_select(const float* X, int64_t m, int64_t stride, int ld, int d, int max_bin, void* ws,
+                            float* out, hipStream_t stream);
 int64_t gbdt_hist_slot_words();  // int64 words of the per-(node, block) histogram slots
 void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,

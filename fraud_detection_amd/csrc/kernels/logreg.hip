@@ -72,17 +72,37 @@ __device__ __forceinline__ long long group_sum_i64(long long v) {
 
 // One pick's terms for the LPR lanes that share it (lane q owns columns [C q, C q + C)).  wl: this
 // lane's weights in the kernel's row units; xs: the unit scale of feature columns (fp8 rows hold
-// features * x_scale); p < 0: an empty pick (the lanes still join the shuffles).
-template <int LPR, bool HESS, bool FISH = false>
+// features * x_scale); p < 0: an empty pick (the lanes still join the shuffles).  The pick's
+// gradient is added into gacc; xa / xb are the caller's scratch for the two parent rows and, for
+// HESS, come back holding the two rank-1 Hessian rows u1 / u2 (in place: no extra registers live
+// beside a mid-loop pick, which is what lets the fp8 pass run its picks mid-loop).
+template <int LPR, bool HESS, bool FISH = false, int kLamLoads = 8>
 __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q, const float* wl, float xs,
-                                           float sw1, float hrs, float* gc, float* u1, float* u2, float& loss,
+                                           float sw1, float hrs, float* gacc, float* xa, float* xb, float& loss,
                                            float& wsum, float& dsum) {
   constexpr int C = 32 / LPR;
   const bool ok = p >= 0;
   const int64_t pp = ok ? p : 0;
   const int64_t ra = sv.q_offset + pp / sv.k, rb = sv.nbr[pp];
   const uint4* Pb = reinterpret_cast<const uint4*>(sv.parents);
-  float xa[C], xb[C];
+  const int o0 = ok ? sv.off[pp] : 0;
+  const int cnt = ok ? sv.cnt[pp] : 0;
+  // kLamLoads lambdas per lane in flight per step: the first step's loads are issued before the
+  // parent rows arrive, so a pick of <= LPR * kLamLoads samples (the bench's ~117) costs one round
+  // trip for its lambdas, overlapped with the parents' -- not one per 8 samples after them (the
+  // chain a wave's pick tile adds to a latency-bound sub-sampled pass).  Integer sums: the
+  // grouping changes no bit.  Compute runs in groups of 8, summed in int32 (|term| < 2^30 / 8).
+  // kLamLoads: as many as the caller's register budget allows (Hessian passes: 8).
+  constexpr int kLamGroup = 8;
+  uint16_t lv[kLamLoads];
+  auto load_lams = [&](int j0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < kLamLoads; ++u) {
+      const int j = j0 + u * LPR;
+      lv[u] = j < cnt ? sv.lam[o0 + j] : 0;
+    }
+  };
+  load_lams(q);
 #pragma unroll
   for (int h = 0; h < C / 8; ++h) {
     unpack8(Pb[ra * 4 + (C / 8) * q + h], xa + 8 * h);
@@ -100,46 +120,40 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   }
   za = group_sum<LPR>(za);
   zb = group_sum<LPR>(zb);
-  const int o0 = ok ? sv.off[pp] : 0;
-  const int cnt = ok ? sv.cnt[pp] : 0;
   const float dz = zb - za;
   long long sr = 0, srl = 0, sd = 0, sdl = 0, sdll = 0, sl = 0;
-  // kLamBatch lambdas per lane in flight per step (one load latency per step, not per sample);
-  // a step's fixed-point terms are summed in int32 (|term| < 2^30 / kLamBatch), then into int64
-  constexpr int kLamBatch = 8;
-  for (int j0 = q; j0 < cnt; j0 += LPR * kLamBatch) {
-    uint16_t lv[kLamBatch];
+  for (int j0 = q; j0 < cnt; j0 += LPR * kLamLoads) {
+    if (j0 != q) load_lams(j0);
 #pragma unroll
-    for (int u = 0; u < kLamBatch; ++u) {
-      const int j = j0 + u * LPR;
-      lv[u] = j < cnt ? sv.lam[o0 + j] : 0;
-    }
-    int br = 0, brl = 0, bd = 0, bdl = 0, bdll = 0, bl = 0;
+    for (int g0 = 0; g0 < kLamLoads; g0 += kLamGroup) {
+      if (j0 + g0 * LPR >= cnt) break;
+      int br = 0, brl = 0, bd = 0, bdl = 0, bdll = 0, bl = 0;
 #pragma unroll
-    for (int u = 0; u < kLamBatch; ++u) {
-      if (j0 + u * LPR >= cnt) break;
-      const float lam = (float)lv[u] * (1.0f / 65536.0f);
-      const float z = fmaf(lam, dz, za);
-      const float zc = fminf(fmaxf(z, -80.0f), 80.0f);
-      const float eh = __expf(-0.5f * zc);
-      const float e2 = eh * eh;  // exp(-z)
-      const float pr = fast_rcp(1.0f + e2);
-      const float r = -sw1 * pr * e2;  // s (p - 1) without the cancellation
-      br += __float2int_rn(r * kSynQ);
-      brl += __float2int_rn(r * lam * kSynQ);
-      if constexpr (HESS || FISH) {
-        const float d = sw1 * pr * pr * e2;  // s p (1 - p)
-        bd += __float2int_rn(d * kSynQ);
-        if constexpr (HESS) {
-          bdl += __float2int_rn(d * lam * kSynQ);
-          bdll += __float2int_rn(d * lam * lam * kSynQ);
+      for (int u = g0; u < g0 + kLamGroup; ++u) {
+        if (j0 + u * LPR >= cnt) break;
+        const float lam = (float)lv[u] * (1.0f / 65536.0f);
+        const float z = fmaf(lam, dz, za);
+        const float zc = fminf(fmaxf(z, -80.0f), 80.0f);
+        const float eh = __expf(-0.5f * zc);
+        const float e2 = eh * eh;  // exp(-z)
+        const float pr = fast_rcp(1.0f + e2);
+        const float r = -sw1 * pr * e2;  // s (p - 1) without the cancellation
+        br += __float2int_rn(r * kSynQ);
+        brl += __float2int_rn(r * lam * kSynQ);
+        if constexpr (HESS || FISH) {
+          const float d = sw1 * pr * pr * e2;  // s p (1 - p)
+          bd += __float2int_rn(d * kSynQ);
+          if constexpr (HESS) {
+            bdl += __float2int_rn(d * lam * kSynQ);
+            bdll += __float2int_rn(d * lam * lam * kSynQ);
+          }
         }
+        bl += __float2int_rn(sw1 * log1p_fast(e2) * kSynQL);  // s softplus(-z) = -s log p
       }
-      bl += __float2int_rn(sw1 * log1p_fast(e2) * kSynQL);  // s softplus(-z) = -s log p
+      sr += br; srl += brl; sl += bl;
+      if constexpr (HESS || FISH) sd += bd;
+      if constexpr (HESS) { sdl += bdl; sdll += bdll; }
     }
-    sr += br; srl += brl; sl += bl;
-    if constexpr (HESS || FISH) sd += bd;
-    if constexpr (HESS) { sdl += bdl; sdll += bdll; }
   }
   sr = group_sum_i64<LPR>(sr);
   srl = group_sum_i64<LPR>(srl);
@@ -147,7 +161,10 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   const double inv = 1.0 / (double)kSynQ;
   const float ca = (float)((double)(sr - srl) * inv), cb = (float)((double)srl * inv);
 #pragma unroll
-  for (int c = 0; c < C; ++c) gc[c] = fmaf(ca, xa[c], cb * xb[c]);
+  for (int c = 0; c < C; ++c) {
+    const float gc = fmaf(ca, xa[c], cb * xb[c]);
+    gacc[c] += gc;
+  }
   if constexpr (HESS) {
     sd = group_sum_i64<LPR>(sd);
     sdl = group_sum_i64<LPR>(sdl);
@@ -160,8 +177,9 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
     const float f11 = (float)(l11 * hrs), f21 = (float)(l21 * hrs), f22 = (float)(l22 * hrs);
 #pragma unroll
     for (int c = 0; c < C; ++c) {
-      u1[c] = fmaf(f11, xa[c], f21 * xb[c]);
-      u2[c] = f22 * xb[c];
+      const float a = xa[c], b = xb[c];
+      xa[c] = fmaf(f11, a, f21 * b);  // u1
+      xb[c] = f22 * b;                // u2
     }
   }
   loss = (float)((double)sl * (1.0 / (double)kSynQL));
@@ -299,10 +317,8 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub + row_phase;  // this wave's next pick tile
   auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
     const int64_t p = t * 16 + rr;
-    float gc[8], u1[8], u2[8], ls, ws, ds;
-    pick_terms<4, HESS, FISH>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, gc, u1, u2, ls, ws, ds);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] += gc[j];
+    float u1[8], u2[8], ls, ws, ds;
+    pick_terms<4, HESS, FISH, HESS ? 8 : 32>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, g, u1, u2, ls, ws, ds);
     if (q == 0) {
       lacc += ls;
       wacc += ws;
@@ -488,6 +504,14 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 1, rr = lane >> 1;
   const float inv_s = 1.0f / x_scale;
+  // VIRT: the weights are read from LDS where used (wsh) instead of living in 16 VGPRs across
+  // the loop -- the room a mid-loop pick tile needs to run without spilling
+  __shared__ __attribute__((aligned(16))) float wsh[32];
+  if (VIRT && threadIdx.x < 32) {
+    const int col = threadIdx.x;
+    wsh[col] = col == kLabelCol ? 0.0f : w[col] * (col < d_feat ? inv_s : 1.0f);
+  }
+  if (VIRT) __syncthreads();
   f32x2_t wl[8];
 #pragma unroll
   for (int p = 0; p < 8; ++p) {
@@ -519,47 +543,56 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       v[u] = row < n ? X[(row_begin + ph) * 2 + q] : make_uint4(0, 0, 0, 0);
     }
   };
-  // virtual SMOTE samples: tiles of 32 picks (2 lanes per pick, 16 columns each), after the
-  // stored-row loop
+  // virtual SMOTE samples: tiles of 16 picks in the bf16 pass's 4-lane layout (lane q4 owns columns
+  // [8 q4, 8 q4 + 8)), run in the middle of the stored-row loop as in the bf16 pass.  The 2-lane
+  // layout of the stored rows would give a pick 16 columns per lane -- with the two prefetched fp8
+  // tiles live that spilled 92 B/lane, which is why picks used to run after the loop (+ ~30 us
+  // of pick latency per pass).  A pick's gradient is moved into the 2-lane
+  // accumulator with one lane swap.
   const float hrs = rsqrtf((float)hess_stride);
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
-  const int64_t ntile = (npick + 31) >> 5;
+  const int64_t ntile = (npick + 15) >> 4;
   const int64_t Gw = (int64_t)gridDim.x * kWaves;
   int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub + row_phase;
+  const int q4 = lane & 3, r4 = lane >> 2;
   auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
-    float wf[16];
+    float wf[8];  // this lane's 4-lane-layout weights in fp8 row units, from LDS (not held in VGPRs
+    asm volatile("" ::: "memory");  // across the stored loop: keeps the loads here)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      wf[2 * e] = wl[e][0];
-      wf[2 * e + 1] = wl[e][1];
+    for (int j = 0; j < 8; ++j) wf[j] = wsh[8 * q4 + j];
+    const int64_t p = t * 16 + r4;
+    float gc[8], u1[8], u2[8], ls, ws, ds;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) gc[j] = 0.0f;
+    pick_terms<4, HESS, FISH, HESS ? 8 : 24>(sv, p < npick ? p : -1, q4, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws, ds);
+    {  // 4-lane columns [8 q4, 8 q4 + 8) -> the 2-lane accumulator g (lane parity h: columns
+       // [16 h, 16 h + 16)): lanes q4 = 1, 2 swap, then each adds at offset 8 (q4 >> 1)
+      const int src = (q4 == 1 || q4 == 2) ? (lane ^ 3) : lane;
+      const bool hi = q4 >= 2;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float a = __shfl(gc[2 * k], src, kWave), b = __shfl(gc[2 * k + 1], src, kWave);
+        g[k] += hi ? f32x2_t{0.0f, 0.0f} : f32x2_t{a, b};
+        g[4 + k] += hi ? f32x2_t{a, b} : f32x2_t{0.0f, 0.0f};
+      }
     }
-    const int64_t p = t * 32 + rr;
-    float gc[16], u1[16], u2[16], ls, ws, ds;
-    pick_terms<2, HESS, FISH>(sv, p < npick ? p : -1, q, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws, ds);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] += f32x2_t{gc[2 * j], gc[2 * j + 1]};
-    if (q == 0) {
+    if (q4 == 0) {
       lacc += ls;
       wacc += ws;
       if (HESS) whacc += ws / (float)hess_stride;
       if (FISH) dacc += ds;
     }
-    if constexpr (HESS) {  // rows rr (u1) and 32 + rr (u2): 4 MFMAs
-      uint4* d1 = reinterpret_cast<uint4*>(my_tile + rr * kCols + 16 * q);
-      uint4* d2 = reinterpret_cast<uint4*>(my_tile + (32 + rr) * kCols + 16 * q);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        uint4 a, b;
-        a.x = pack_bf16x2(u1[8 * h + 0], u1[8 * h + 1]); a.y = pack_bf16x2(u1[8 * h + 2], u1[8 * h + 3]);
-        a.z = pack_bf16x2(u1[8 * h + 4], u1[8 * h + 5]); a.w = pack_bf16x2(u1[8 * h + 6], u1[8 * h + 7]);
-        b.x = pack_bf16x2(u2[8 * h + 0], u2[8 * h + 1]); b.y = pack_bf16x2(u2[8 * h + 2], u2[8 * h + 3]);
-        b.z = pack_bf16x2(u2[8 * h + 4], u2[8 * h + 5]); b.w = pack_bf16x2(u2[8 * h + 6], u2[8 * h + 7]);
-        d1[h] = a;
-        d2[h] = b;
-      }
+    if constexpr (HESS) {  // rows r4 (u1) and 16 + r4 (u2) of the wave's tile: 2 MFMAs
+      uint4 a, b;
+      a.x = pack_bf16x2(u1[0], u1[1]); a.y = pack_bf16x2(u1[2], u1[3]);
+      a.z = pack_bf16x2(u1[4], u1[5]); a.w = pack_bf16x2(u1[6], u1[7]);
+      b.x = pack_bf16x2(u2[0], u2[1]); b.y = pack_bf16x2(u2[2], u2[3]);
+      b.z = pack_bf16x2(u2[4], u2[5]); b.w = pack_bf16x2(u2[6], u2[7]);
+      *reinterpret_cast<uint4*>(my_tile + r4 * kCols + 8 * q4) = a;
+      *reinterpret_cast<uint4*>(my_tile + (16 + r4) * kCols + 8 * q4) = b;
       __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
+      for (int s = 0; s < 2; ++s) {
         const lds_s4 a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
             (__attribute__((address_space(3))) lds_s4*)(my_tile + s * 16 * kCols + tr_off));
         const lds_s4 a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
@@ -578,7 +611,11 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   if (base < n) load_tile(base, cur);
   if (base + step < n) load_tile(base + step, nx1);
   int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
+  const int64_t witers = n > base ? (n - base + step - 1) / step : 0;
+  const int64_t ptrig = witers > 0 ? 1 + ((blockIdx.x * kWaves + wv) % witers) : 0;
+  int64_t pit = 0;
   for (; base < n; base += step) {
+    if constexpr (VIRT) asm volatile("" ::: "memory");  // the LDS weight reads stay in the loop
     uint4 nxt[2];
     if (base + 2 * step < n) load_tile(base + 2 * step, nxt);
     const bool do_h = HESS && hphase == 0;
@@ -595,7 +632,10 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       if (q == 1) x[15] = 0.0f;
       f32x2_t zz = f32x2_t{0.0f, 0.0f};
 #pragma unroll
-      for (int p = 0; p < 8; ++p) zz = __builtin_elementwise_fma(wl[p], f32x2_t{x[2 * p], x[2 * p + 1]}, zz);
+      for (int p = 0; p < 8; ++p) {
+        const f32x2_t wp = VIRT ? *reinterpret_cast<const f32x2_t*>(wsh + 16 * q + 2 * p) : wl[p];
+        zz = __builtin_elementwise_fma(wp, f32x2_t{x[2 * p], x[2 * p + 1]}, zz);
+      }
       float zp = group_sum<2>(zz[0] + zz[1]);
       y = group_sum<2>(y);
       const bool ok = base + 32 * u + rr < n;
@@ -649,7 +689,12 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       cur[u] = nx1[u];
       nx1[u] = nxt[u];
     }
-    // (no mid-loop pick tile here: with the two prefetched fp8 tiles live it spilled 92 B/lane)
+    if constexpr (VIRT) {
+      if (ptile < ntile && ++pit == ptrig) {
+        pick_tile(ptile);
+        ptile += Gw * row_sub;
+      }
+    }
   }
 
   if constexpr (VIRT) {  // the wave's remaining pick tiles
@@ -674,6 +719,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
 #pragma unroll
     for (int j = 0; j < 16; ++j) red[wv][16 * lane + j] = gs[j];
   }
+
   if (lane == 0) {
     red[wv][32] = lacc;
     red[wv][33] = wacc;
@@ -714,11 +760,8 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
 // <= 12 loads are all in flight at once (one round trip, not six as with 16 row-groups), and the
 // 64 row-group sums are combined in a fixed tree order (bitwise reproducible run to run).
 constexpr int kRedCols = 16, kRedGroups = 64, kRedLoads = 12;  // kRedGroups * kRedLoads >= nblocks
-__global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __restrict__ partial,
-                                                             int nblocks, int ncols,
-                                                             double* __restrict__ out,
-                                                             const int* __restrict__ done) {
-  if (done != nullptr && *done) return;
+__device__ __forceinline__ void reduce_columns(const float* __restrict__ partial, int nblocks, int ncols,
+                                               double* __restrict__ out) {
   __shared__ double red[kRedGroups][kRedCols + 1];
   const int c = threadIdx.x & (kRedCols - 1), grp = threadIdx.x / kRedCols;
   const int col = blockIdx.x * kRedCols + c;
@@ -751,6 +794,14 @@ __global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __rest
     __syncthreads();
   }
   if (grp == 0 && col < ncols) out[col] = red[0][c];
+}
+
+__global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __restrict__ partial,
+                                                             int nblocks, int ncols,
+                                                             double* __restrict__ out,
+                                                             const int* __restrict__ done) {
+  if (done != nullptr && *done) return;
+  reduce_columns(partial, nblocks, ncols, out);
 }
 
 // ---- Newton / SGD state (fp64, on device) -------------------------------------------------
@@ -798,16 +849,17 @@ __device__ __forceinline__ void store_folded(const double* ss, const double* cA,
     }                                                                                             \
   } while (0)
 
+// The update runs in ONE wave: the standalone kernel's 64-thread block, or wave 0 of the last
+// block of logreg_reduce_update_kernel.  Its LDS hand-offs therefore need no s_barrier -- a wave's
+// LDS instructions execute in order -- only a compiler ordering point (FDX_WBAR).
+#define FDX_WBAR() __builtin_amdgcn_wave_barrier()
 template <int MT, bool STAMP = false>  // MT > 0: compile-time number of active coordinates (identity index map)
-__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
-                                                           double* __restrict__ st,
-                                                           float* __restrict__ w32,
-                                                           int* __restrict__ done, int d, double C,
-                                                           double tol, int max_iter,
-                                                           int fit_intercept, int phase_start,
-                                                           const double* __restrict__ aff,
-                                                           unsigned long long* __restrict__ stamps = nullptr,
-                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
+__device__ __forceinline__ void newton_update_body(const double* __restrict__ red, double* __restrict__ st,
+                                                   float* __restrict__ w32, int* __restrict__ done, int d,
+                                                   double C, double tol, int max_iter, int fit_intercept,
+                                                   int phase_start, const double* __restrict__ aff,
+                                                   unsigned long long* __restrict__ stamps,
+                                                   int* __restrict__ done_host, int seq) {
   unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   FDX_STAMP(0);
   __shared__ double sr[kLRPartStride];
@@ -839,7 +891,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     for (int i = 0; i < NS; ++i) ss[t + 64 * i] = u[i];
     if (t < 32) cA[t] = av; else iA[t - 32] = av;
   }
-  __syncthreads();
+  FDX_WBAR();
   FDX_STAMP(1);
   if (aff) {
     // Rows hold s = x - pivot; standardized z = (s - c) * inv with c = inv = identity on the
@@ -847,7 +899,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     // H_z[j][k] = inv_j inv_k (H_jk - c_j H_30k - c_k H_j30 + c_j c_k H_30,30) (H symmetric).
     const double g30 = sr[kBiasCol];
     if (t < 32) h30[t] = sr[64 + kBiasCol * kCols + t];
-    __syncthreads();
+    FDX_WBAR();
     if (t < 32) sr[t] = iA[t] * (sr[t] - cA[t] * g30);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -855,7 +907,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       const double hv = sr[64 + e] - cA[j] * h30[k] - cA[k] * h30[j] + cA[j] * cA[k] * h30[kBiasCol];
       sr[64 + e] = iA[j] * iA[k] * hv;
     }
-    __syncthreads();
+    FDX_WBAR();
   }
   FDX_STAMP(2);
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
@@ -865,7 +917,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   const int my = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
   if (t < 32) idx[t] = my;
   build_grad(sr, ss, d, fit_intercept, reg, S, grad, t);
-  __syncthreads();
+  FDX_WBAR();
   double w2 = (t < d) ? ss[kW + t] * ss[kW + t] : 0.0;
   double ga = (t < m) ? fabs(grad[my]) : 0.0;
   w2 = wave_sum(w2);
@@ -884,7 +936,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   if (it > 0 && obj > prev + 1e-6 * fabs(prev) && nbt < 40.0) dec = 1;
   else if (gmax <= tol) dec = 2;
   else dec = 0;
-  __syncthreads();
+  FDX_WBAR();
   if (t == 0) {
     ss[kObj] = obj;
     if (dec != 1) ss[kGmax] = gmax;
@@ -968,7 +1020,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       ss[kWPrev + t] = ss[kW + t];
       ss[kStep + t] = 0.0;
     }
-    __syncthreads();
+    FDX_WBAR();
     if (t < m) {
       ss[kStep + my] = bi;
       ss[kW + my] = ss[kWPrev + my] + bi;
@@ -979,7 +1031,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       ss[kNAccepted] += 1.0;
     }
   }
-  __syncthreads();
+  FDX_WBAR();
   if (t == 0) {
     ss[kIter] += 1.0;
     if (dec != 2 && (int)ss[kIter] >= max_iter) *done = 1;
@@ -989,7 +1041,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     if (done_host != nullptr)
       __hip_atomic_store(done_host, (seq << 1) | *done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __syncthreads();
+  FDX_WBAR();
   if (aff) {
     store_folded(ss, cA, iA, w32, t);
   } else if (t < kCols) {
@@ -1001,6 +1053,52 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   if constexpr (STAMP) {
     if (t < 8) stamps[t] = tsv[t];
   }
+}
+#undef FDX_WBAR
+
+template <int MT, bool STAMP = false>
+__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
+                                                           double* __restrict__ st,
+                                                           float* __restrict__ w32,
+                                                           int* __restrict__ done, int d, double C,
+                                                           double tol, int max_iter,
+                                                           int fit_intercept, int phase_start,
+                                                           const double* __restrict__ aff,
+                                                           unsigned long long* __restrict__ stamps = nullptr,
+                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
+  newton_update_body<MT, STAMP>(red, st, w32, done, d, C, tol, max_iter, fit_intercept, phase_start, aff, stamps,
+                                done_host, seq);
+}
+
+// logreg_reduce + newton_update in ONE launch (single-process fits: no all-reduce between them).
+// The reduce blocks publish their columns (agent fence) and take a ticket; the last block runs the
+// Newton update in its first wave on the just-reduced vector.  Same fixed-order fp64 reduction,
+// same update code: bitwise the two-launch result, one kernel boundary (~2-4 us) less per
+// iteration.  The ticket is zero between launches (the last block resets it).
+template <int MT>
+__global__ __launch_bounds__(1024) void logreg_reduce_update_kernel(
+    const float* __restrict__ partial, int nblocks, int ncols, double* __restrict__ out, unsigned int* ticket,
+    double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done, int d, double C, double tol,
+    int max_iter, int fit_intercept, int phase_start, const double* __restrict__ aff, int* __restrict__ done_host,
+    int seq) {
+  if (*done) {  // converged: the update's own early exit still tags the host's flag word
+    if (blockIdx.x == 0 && threadIdx.x == 0 && done_host != nullptr)
+      __hip_atomic_store(done_host, (seq << 1) | 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  reduce_columns(partial, nblocks, ncols, out);
+  __threadfence();
+  __shared__ int s_last;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < 64)
+    newton_update_body<MT, false>(out, st, w32, done, d, C, tol, max_iter, fit_intercept, phase_start, aff, nullptr,
+                                  done_host, seq);
 }
 #undef FDX_STAMP
 
@@ -1382,6 +1480,23 @@ void launch_newton_update(const double* red, double* state, float* w32, int* don
     newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
                                                   phase_start, aff, nullptr, done_host, seq);
   check_launch("newton_update");
+}
+
+void launch_newton_reduce_update(const float* partial, int nblocks, int ncols, double* red, unsigned int* ticket,
+                                 double* state, float* w32, int* done, int d, double C, double tol, int max_iter,
+                                 int fit_intercept, int phase_start, const double* aff, hipStream_t stream,
+                                 int* done_host, int seq) {
+  if (ncols != kLRPartStride && ncols != 34) throw std::runtime_error("newton_reduce_update: ncols 1088 or 34");
+  const int g = (ncols + kRedCols - 1) / kRedCols;
+  if (d + (fit_intercept ? 1 : 0) == 31)
+    logreg_reduce_update_kernel<31><<<g, 1024, 0, stream>>>(partial, nblocks, ncols, red, ticket, state, w32, done, d,
+                                                            C, tol, max_iter, fit_intercept, phase_start, aff,
+                                                            done_host, seq);
+  else
+    logreg_reduce_update_kernel<0><<<g, 1024, 0, stream>>>(partial, nblocks, ncols, red, ticket, state, w32, done, d,
+                                                           C, tol, max_iter, fit_intercept, phase_start, aff,
+                                                           done_host, seq);
+  check_launch("newton_reduce_update");
 }
 
 void launch_newton_update_stamped(const double* red, double* state, float* w32, int* done, double C,

@@ -378,13 +378,11 @@ class DevicePipeline:
             pos = float(sum(r[0] + q for r, q in zip(ranks, new_per_rank)))
             class_w = (tot / (2.0 * max(tot - pos, 1.0)), tot / (2.0 * max(pos, 1.0)))
         virt = None
-        # bf16 rows only: with 32-byte fp8 rows the stored SMOTE rows are cheap to stream and the
-        # fp8 fit measured faster stored (c5 shard 1.404 vs 1.594 ms, profiles/r3_fin3); the fp8
-        # pass still takes virtual samples (ops/logreg.VirtualSmote, tested against the oracle)
-        # SGD: the samples are generated inside every minibatch pass in both row formats (the stored
-        # rows of an fp8 SGD fit would be streamed once per epoch, three times per fit)
+        # Both row formats, both solvers: the SMOTE samples are generated inside every pass instead of
+        # being written once and streamed by every pass.  (fp8 Newton took stored rows until its pass
+        # could run pick tiles mid-loop without spilling -- logreg.hip logreg_pass_fp8w_kernel.)
         virt_ok = (cfg.virtual_smote and dev.type == "cuda" and class_w[1] <= lr_ops.VIRTUAL_MAX_WEIGHT
-                   and ((cfg.solver == "newton" and cfg.storage == "bf16") or cfg.solver == "sgd"))
+                   and cfg.solver in ("newton", "sgd"))
         tm.mark("scale_cast")
         # global scope: every rank joins the row and neighbour all-gathers whenever ANY rank has a
         # quota; shard scope has no collective in this block, so only a rank with its own quota enters

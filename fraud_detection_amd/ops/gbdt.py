@@ -122,18 +122,23 @@ def quantile_cuts(X: torch.Tensor, max_bin: int = MAX_BIN, sample_rows: int = 1 
     world = comm.world_size if comm is not None else 1
     per = max(1, sample_rows // world)
     stride = max(1, n // per)
-    samp = X[::stride][:per].contiguous()
     if comm is not None and world > 1:
-        samp, _ = comm.all_gather_rows(samp)
-    if not samp.is_cuda:
-        return R.quantile_cuts(samp.float().numpy(), max_bin)
-    # Device sort of the sample (rocPRIM radix sort through torch); only the max_bin - 1 quantile
-    # rows and the minimum row come back to the host, where deduplication is trivial.  Sorting is
-    # exact, so the cuts equal the CPU oracle's on the same sample.
-    m = samp.shape[0]
-    srt = torch.sort(samp.float(), dim=0).values
-    idx = torch.as_tensor((np.arange(1, max_bin, dtype=np.int64) * m) // max_bin, device=samp.device)
-    picks = torch.cat([srt[:1], srt.index_select(0, idx)]).cpu().numpy()
+        samp, _ = comm.all_gather_rows(X[::stride][:per].contiguous())
+        src, m, step = samp, samp.shape[0], 1
+    else:
+        src, m, step = X, min(per, (n + stride - 1) // stride), stride
+    if not src.is_cuda:
+        return R.quantile_cuts(src[::step][:m].float().numpy(), max_bin)
+    # Exact order statistics by a native radix select (quantile.hip): the minimum and the max_bin - 1
+    # quantile rows of the sample come back to the host, where deduplication is trivial.  Selection
+    # is exact, so the cuts equal the CPU oracle's (np.sort) on the same sample.
+    if src.dtype != torch.float32 or src.stride(1) != 1:
+        src, step = src[::step][:m].float().contiguous(), 1
+    nat = native()
+    ws = torch.empty(nat.quantile_select_ws_bytes(m, d), dtype=torch.uint8, device=src.device)
+    picks = torch.empty((max_bin, d), dtype=torch.float32, device=src.device)
+    nat.quantile_select(ptr(src), m, step, src.stride(0), d, max_bin, ptr(ws), ptr(picks), stream_of(src))
+    picks = picks.cpu().numpy()
     return R.cuts_from_sorted_picks(picks[1:], picks[0], max_bin)
 
 

@@ -291,7 +291,8 @@ class NewtonStateRef:
 
 WAVES_PER_BLOCK = 4     # logreg.hip kThreads / 64
 ROW_TILE = 64           # rows per wave tile
-PICK_TILE_BF16 = 16     # virtual-SMOTE picks per wave tile (bf16 pass); the fp8 pass takes 32
+PICK_TILE = 16          # virtual-SMOTE picks per wave tile (bf16 and fp8 passes: 4 lanes per pick)
+PICK_TILE_BF16 = PICK_TILE
 SGD_MIN_SPAN = 4        # every SGD minibatch spans >= 4 strided blocks of row tiles
 
 

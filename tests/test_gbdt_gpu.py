@@ -38,6 +38,42 @@ def test_bin_kernel_strided_rows(dev):
     assert np.array_equal(got, R.bin_rows(X, cuts, nb))
 
 
+@pytest.mark.parametrize("n,d,sample,max_bin", [(300_001, 30, 1 << 16, 256), (5_000, 3, 1 << 20, 256),
+                                                 (70_000, 17, 9_999, 37), (1, 2, 1 << 20, 256)])
+def test_quantile_select_matches_sort(dev, n, d, sample, max_bin):
+    """quantile.hip radix select == np.sort of the same strided sample, bit for bit: ties, a constant
+    feature, signed zeros, huge / tiny magnitudes, infinities."""
+    rng = np.random.default_rng(n)
+    X = rng.normal(size=(n, d)).astype(np.float32)
+    X[:, 0] = np.round(X[:, 0] * 3) / 3
+    if d > 2:
+        X[:, 1] = 7.25                               # constant: every target in one bucket
+        X[:, 2] = np.where(rng.random(n) < 0.5, -0.0, 0.0) * rng.integers(0, 2, n)
+    if d > 5:
+        X[:, 3] *= 1e30
+        X[:, 4] *= 1e-30
+        X[::97, 5] = np.inf
+        X[::89, 5] = -np.inf
+    Xd = torch.from_numpy(X).to(dev)
+    got = gb.quantile_cuts(Xd, max_bin, sample_rows=sample)
+    per = max(1, sample)
+    stride = max(1, n // per)
+    ref = R.quantile_cuts(X[::stride][:per], max_bin)
+    assert np.array_equal(got[1], ref[1])
+    assert np.array_equal(got[0], ref[0])
+
+
+def test_quantile_select_padded_rows(dev):
+    """The pipeline's [n, 32] table: the select reads the 30 features through the row stride."""
+    Xd, _, X, _ = _data(123_457, 30)
+    pad = torch.zeros((123_457, 32), device=dev)
+    pad[:, :30] = Xd
+    got = gb.quantile_cuts(pad[:, :30], 256, sample_rows=50_000)
+    stride = 123_457 // 50_000
+    ref = R.quantile_cuts(X[::stride][:50_000], 256)
+    assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1])
+
+
 @pytest.mark.parametrize("spw", [1.0, 37.5])
 def test_grad_kernel_matches_oracle(dev, spw):
     from fraud_detection_amd.ops.native import native, ptr, stream_of

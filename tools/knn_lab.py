@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""k-NN (SMOTE self-search, k=5, fp32 engine) at the bench shapes: candidate slices x pilot seed.
+
+    python tools/knn_lab.py [--reps 20] [--json out.json]
+
+Shapes: DP1 (the 10M-row bench's 13.6k minority rows against themselves) and the DP=8 global-scope
+rank (its 13.6k minority rows against all 8 ranks' 108.8k).  For every (nsplit, seed_tiles) the
+event-timed median of the whole knn_topk call (prep + pilot + search + merge) and whether the lists
+equal the unseeded auto-split lists exactly.
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--json", default=None)
+    a = ap.parse_args()
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.ops import knn as K
+    from fraud_detection_amd.ops.native import native
+
+    dev = torch.device("cuda", 0)
+    m1, world = 13600, 8
+    X, y = separable(2 * m1 * world + 4096, fraud_rate=0.5, seed=5, device=dev)
+    xm = X[y == 1][: m1 * world]
+    xm = (xm - X.mean(0)) / X.std(0)
+    C = torch.zeros((xm.shape[0], 32), device=dev)
+    C[:, :30] = xm
+    C[:, 30] = 1.0
+    shapes = {"dp1_self": (C[:m1].contiguous(), C[:m1].contiguous(), 0),
+              "dp8_global_rank3": (C[3 * m1: 4 * m1].contiguous(), C, 3 * m1)}
+    out = {"reps": a.reps, "shapes": {}}
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(a.reps + 1)]
+        ev[0].record()
+        for i in range(a.reps):
+            fn()
+            ev[i + 1].record()
+        torch.cuda.synchronize()
+        return float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps)]))
+
+    for name, (Q, Cc, off) in shapes.items():
+        mq, mc = Q.shape[0], Cc.shape[0]
+        auto = native().knn_splits((mq + 31) // 32 * 32, (mc + 31) // 32 * 32)
+        ref = K.knn_topk(Q, Cc, 5, off, engine="fp32", seed_tiles=0)
+        rec = {"mq": mq, "mc": mc, "auto_nsplit": int(auto), "cases": []}
+        for ns in sorted({1, 2, 4, 8, 16, 32, int(auto)}):
+            for st in (0, 2, 4, 8, 16):
+                f = lambda: K.knn_topk(Q, Cc, 5, off, engine="fp32", nsplit=ns, seed_tiles=st)  # noqa: E731
+                got = f()
+                ms = timed(f)
+                case = {"nsplit": ns, "seed_tiles": st, "ms": round(ms, 4),
+                        "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
+                        "lists_equal": bool((got == ref).all().item())}
+                rec["cases"].append(case)
+                print(json.dumps({name: case}), flush=True)
+        best = min(rec["cases"], key=lambda c: c["ms"])
+        base = [c for c in rec["cases"] if c["nsplit"] == auto and c["seed_tiles"] == 0][0]
+        rec["best"], rec["baseline_auto_unseeded"] = best, base
+        out["shapes"][name] = rec
+    if a.json:
+        with open(a.json, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
