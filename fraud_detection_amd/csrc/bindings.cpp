@@ -550,15 +550,6 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("logreg_reduce", [](u partial, int nblocks, int ncols, u out, u done, u s) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });
-  m.def("newton_reduce_update", [](u partial, int nblocks, int ncols, u red, u ticket, u state, u w32, u done, int d,
-                                   double C, double tol, int max_iter, int fi, int phase_start, u aff, u s,
-                                   u done_host, int seq) {
-    fdx::launch_newton_reduce_update(P<const float>(partial), nblocks, ncols, P<double>(red), P<unsigned int>(ticket),
-                                     P<double>(state), P<float>(w32), P<int>(done), d, C, tol, max_iter, fi,
-                                     phase_start, P<const double>(aff), S(s), P<int>(done_host), seq);
-  }, py::arg("partial"), py::arg("nblocks"), py::arg("ncols"), py::arg("red"), py::arg("ticket"), py::arg("state"),
-     py::arg("w32"), py::arg("done"), py::arg("d"), py::arg("C"), py::arg("tol"), py::arg("max_iter"), py::arg("fi"),
-     py::arg("phase_start"), py::arg("aff"), py::arg("s"), py::arg("done_host") = 0, py::arg("seq") = 0);
   m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi,
                             int phase_start, u aff, u s, u done_host, int seq) {
     fdx::launch_newton_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), d, C, tol,
@@ -670,13 +661,11 @@ PYBIND11_MODULE(_fdx_native, m) {
                           P<float>(wss), P<int>(wsi), nsplit, S(s));
   });
   m.def("knn_topk", [](u Q, int mq_pad, int mq, u C, int mc_pad, int mc, int64_t self_off, int k, u oidx,
-                       u oscore, u ws_score, u ws_idx, int nsplit, u s, int seed_tiles, u seed_s, u seed_i) {
+                       u oscore, u ws_score, u ws_idx, int nsplit, u s) {
     fdx::launch_knn_topk(P<const float>(Q), mq_pad, mq, P<const float>(C), mc_pad, mc,
                          self_off, k, P<int>(oidx), P<float>(oscore), P<float>(ws_score), P<int>(ws_idx), nsplit,
-                         S(s), seed_tiles, P<float>(seed_s), P<int>(seed_i));
-  }, py::arg("Q"), py::arg("mq_pad"), py::arg("mq"), py::arg("C"), py::arg("mc_pad"), py::arg("mc"),
-     py::arg("self_off"), py::arg("k"), py::arg("oidx"), py::arg("oscore"), py::arg("ws_score"), py::arg("ws_idx"),
-     py::arg("nsplit"), py::arg("s"), py::arg("seed_tiles") = 0, py::arg("seed_s") = 0, py::arg("seed_i") = 0);
+                         S(s));
+  });
   m.def("smote_parents", [](u C, int64_t m_rows, u aff, u out, u s) {
     fdx::launch_smote_parents(P<const float>(C), m_rows, P<const double>(aff), P<uint16_t>(out), S(s));
   });

@@ -117,20 +117,13 @@ __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, i
 //     (exact score-then-index order, self/padding excluded) and the threshold becomes the k-th
 //     best of the UNION of the two half-lists of the query (lanes j and j+32), which is a valid
 //     filter for both halves and about twice as tight.
-//
-// seed (optional, [mq][K] scores of a pilot search over a few candidate tiles, same kernel): the
-// k-th pilot score of a query is a valid initial threshold -- the query's true k-th best score is
-// at least that, and the pilot scores are bitwise the sweep's own (same tile code) -- so every
-// candidate slice starts filtering at once instead of first filling its lists from scratch.
-// t_hi_all: candidate tiles [0, t_hi_all) are split over gridDim.y (the pilot: its first tiles).
 template <int K>
 __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict__ Q, int mq,
                                                          const float* __restrict__ C,
                                                          int mc_pad, int mc,
                                                          int64_t self_offset,
                                                          int* __restrict__ out_idx,
-                                                         float* __restrict__ out_score,
-                                                         const float* __restrict__ seed, int t_hi_all) {
+                                                         float* __restrict__ out_score) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
   const int q0 = blockIdx.x * 32;
@@ -149,7 +142,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = (seed != nullptr && qg < mq) ? seed[(int64_t)qg * K + K - 1] : kNegBig;
+  float thr = kNegBig;
 
   // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks.  Slot
   // kQCap - 1 is the lane's dump slot.
@@ -180,9 +173,9 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = fmaxf(thr, kth);  // (kth only grows; the max keeps a pilot seed until the lists pass it)
+    thr = kth;
   };
-  const int all_tiles = t_hi_all;
+  const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
   const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
   // register double buffer: the next tile's 16 floats per lane (L2-resident) are in flight
@@ -783,26 +776,17 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
 
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream,
-                     int seed_tiles, float* seed_score, int* seed_idx) {
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk: pads must be x32");
   if (nsplit < 1) nsplit = 1;
   if (nsplit > 1 && (ws_score == nullptr || ws_idx == nullptr))
     throw std::runtime_error("knn_topk: split search needs the [nsplit][mq][k] workspaces");
-  const int tiles = mc_pad / 32;
-  if (seed_tiles > 0 && (seed_score == nullptr || seed_idx == nullptr))
-    throw std::runtime_error("knn_topk: a pilot seed needs the [mq][k] seed workspaces");
-  if (seed_tiles > tiles / 2) seed_tiles = 0;  // too few candidates for a pilot to pay
   const dim3 grid(mq_pad / 32, nsplit);
   int* oi = nsplit > 1 ? ws_idx : out_idx;
   float* os = nsplit > 1 ? ws_score : out_score;
-  const float* sd = seed_tiles > 0 ? seed_score : nullptr;
 #define FDX_KNN(KK)                                                                             \
-  if (seed_tiles > 0)                                                                           \
-    knn_topk_kernel<KK><<<dim3(mq_pad / 32, 1), kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, \
-                                                                    seed_idx, seed_score, nullptr, seed_tiles); \
   knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi,           \
-                                                     os, sd, tiles);                             \
+                                                     os);                                        \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {

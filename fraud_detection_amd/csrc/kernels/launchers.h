@@ -160,11 +160,6 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 // aff (nullable, [64] = c | 1/sigma): the rows are pivot-shifted, not standardized -- the kernel
 // maps the reduced sums into standardized space and writes folded weights to w32.
 // done_host (nullable): device address of a mapped pinned int that receives (seq << 1) | done
-// logreg_reduce + newton_update in one launch (ticket: one zeroed u32; ncols 1088 or 34)
-void launch_newton_reduce_update(const float* partial, int nblocks, int ncols, double* red, unsigned int* ticket,
-                                 double* state, float* w32, int* done, int d, double C, double tol, int max_iter,
-                                 int fit_intercept, int phase_start, const double* aff, hipStream_t stream,
-                                 int* done_host = nullptr, int seq = 0);
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
                           const double* aff, hipStream_t stream, int* done_host = nullptr, int seq = 0);
@@ -221,12 +216,9 @@ void launch_knn_topk_lds(const float* Q, int mq_pad, int mq, const float* C, int
 void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
                       float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
-// seed_tiles > 0: a pilot search over the first seed_tiles candidate tiles (into seed_score /
-// seed_idx [mq][k]) seeds every slice's filter threshold (knn.hip knn_topk_kernel)
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
                      int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream,
-                     int seed_tiles = 0, float* seed_score = nullptr, int* seed_idx = nullptr);
+                     float* out_score, float* ws_score, int* ws_idx, int nsplit, hipStream_t stream);
 
 // ---- smote.hip ----
 // P [m, 32] bf16 = output-space parents: bf16(C * sigma + c) on the feature columns (aff nullable)

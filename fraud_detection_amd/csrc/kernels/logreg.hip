@@ -760,8 +760,11 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
 // <= 12 loads are all in flight at once (one round trip, not six as with 16 row-groups), and the
 // 64 row-group sums are combined in a fixed tree order (bitwise reproducible run to run).
 constexpr int kRedCols = 16, kRedGroups = 64, kRedLoads = 12;  // kRedGroups * kRedLoads >= nblocks
-__device__ __forceinline__ void reduce_columns(const float* __restrict__ partial, int nblocks, int ncols,
-                                               double* __restrict__ out) {
+__global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __restrict__ partial,
+                                                             int nblocks, int ncols,
+                                                             double* __restrict__ out,
+                                                             const int* __restrict__ done) {
+  if (done != nullptr && *done) return;
   __shared__ double red[kRedGroups][kRedCols + 1];
   const int c = threadIdx.x & (kRedCols - 1), grp = threadIdx.x / kRedCols;
   const int col = blockIdx.x * kRedCols + c;
@@ -794,14 +797,6 @@ __device__ __forceinline__ void reduce_columns(const float* __restrict__ partial
     __syncthreads();
   }
   if (grp == 0 && col < ncols) out[col] = red[0][c];
-}
-
-__global__ __launch_bounds__(1024) void logreg_reduce_kernel(const float* __restrict__ partial,
-                                                             int nblocks, int ncols,
-                                                             double* __restrict__ out,
-                                                             const int* __restrict__ done) {
-  if (done != nullptr && *done) return;
-  reduce_columns(partial, nblocks, ncols, out);
 }
 
 // ---- Newton / SGD state (fp64, on device) -------------------------------------------------
@@ -849,17 +844,16 @@ __device__ __forceinline__ void store_folded(const double* ss, const double* cA,
     }                                                                                             \
   } while (0)
 
-// The update runs in ONE wave: the standalone kernel's 64-thread block, or wave 0 of the last
-// block of logreg_reduce_update_kernel.  Its LDS hand-offs therefore need no s_barrier -- a wave's
-// LDS instructions execute in order -- only a compiler ordering point (FDX_WBAR).
-#define FDX_WBAR() __builtin_amdgcn_wave_barrier()
 template <int MT, bool STAMP = false>  // MT > 0: compile-time number of active coordinates (identity index map)
-__device__ __forceinline__ void newton_update_body(const double* __restrict__ red, double* __restrict__ st,
-                                                   float* __restrict__ w32, int* __restrict__ done, int d,
-                                                   double C, double tol, int max_iter, int fit_intercept,
-                                                   int phase_start, const double* __restrict__ aff,
-                                                   unsigned long long* __restrict__ stamps,
-                                                   int* __restrict__ done_host, int seq) {
+__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
+                                                           double* __restrict__ st,
+                                                           float* __restrict__ w32,
+                                                           int* __restrict__ done, int d, double C,
+                                                           double tol, int max_iter,
+                                                           int fit_intercept, int phase_start,
+                                                           const double* __restrict__ aff,
+                                                           unsigned long long* __restrict__ stamps = nullptr,
+                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
   unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   FDX_STAMP(0);
   __shared__ double sr[kLRPartStride];
@@ -891,7 +885,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
     for (int i = 0; i < NS; ++i) ss[t + 64 * i] = u[i];
     if (t < 32) cA[t] = av; else iA[t - 32] = av;
   }
-  FDX_WBAR();
+  __syncthreads();
   FDX_STAMP(1);
   if (aff) {
     // Rows hold s = x - pivot; standardized z = (s - c) * inv with c = inv = identity on the
@@ -899,7 +893,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
     // H_z[j][k] = inv_j inv_k (H_jk - c_j H_30k - c_k H_j30 + c_j c_k H_30,30) (H symmetric).
     const double g30 = sr[kBiasCol];
     if (t < 32) h30[t] = sr[64 + kBiasCol * kCols + t];
-    FDX_WBAR();
+    __syncthreads();
     if (t < 32) sr[t] = iA[t] * (sr[t] - cA[t] * g30);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -907,7 +901,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
       const double hv = sr[64 + e] - cA[j] * h30[k] - cA[k] * h30[j] + cA[j] * cA[k] * h30[kBiasCol];
       sr[64 + e] = iA[j] * iA[k] * hv;
     }
-    FDX_WBAR();
+    __syncthreads();
   }
   FDX_STAMP(2);
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
@@ -917,7 +911,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
   const int my = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
   if (t < 32) idx[t] = my;
   build_grad(sr, ss, d, fit_intercept, reg, S, grad, t);
-  FDX_WBAR();
+  __syncthreads();
   double w2 = (t < d) ? ss[kW + t] * ss[kW + t] : 0.0;
   double ga = (t < m) ? fabs(grad[my]) : 0.0;
   w2 = wave_sum(w2);
@@ -936,7 +930,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
   if (it > 0 && obj > prev + 1e-6 * fabs(prev) && nbt < 40.0) dec = 1;
   else if (gmax <= tol) dec = 2;
   else dec = 0;
-  FDX_WBAR();
+  __syncthreads();
   if (t == 0) {
     ss[kObj] = obj;
     if (dec != 1) ss[kGmax] = gmax;
@@ -1020,7 +1014,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
       ss[kWPrev + t] = ss[kW + t];
       ss[kStep + t] = 0.0;
     }
-    FDX_WBAR();
+    __syncthreads();
     if (t < m) {
       ss[kStep + my] = bi;
       ss[kW + my] = ss[kWPrev + my] + bi;
@@ -1031,7 +1025,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
       ss[kNAccepted] += 1.0;
     }
   }
-  FDX_WBAR();
+  __syncthreads();
   if (t == 0) {
     ss[kIter] += 1.0;
     if (dec != 2 && (int)ss[kIter] >= max_iter) *done = 1;
@@ -1041,7 +1035,7 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
     if (done_host != nullptr)
       __hip_atomic_store(done_host, (seq << 1) | *done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  FDX_WBAR();
+  __syncthreads();
   if (aff) {
     store_folded(ss, cA, iA, w32, t);
   } else if (t < kCols) {
@@ -1053,52 +1047,6 @@ __device__ __forceinline__ void newton_update_body(const double* __restrict__ re
   if constexpr (STAMP) {
     if (t < 8) stamps[t] = tsv[t];
   }
-}
-#undef FDX_WBAR
-
-template <int MT, bool STAMP = false>
-__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
-                                                           double* __restrict__ st,
-                                                           float* __restrict__ w32,
-                                                           int* __restrict__ done, int d, double C,
-                                                           double tol, int max_iter,
-                                                           int fit_intercept, int phase_start,
-                                                           const double* __restrict__ aff,
-                                                           unsigned long long* __restrict__ stamps = nullptr,
-                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
-  newton_update_body<MT, STAMP>(red, st, w32, done, d, C, tol, max_iter, fit_intercept, phase_start, aff, stamps,
-                                done_host, seq);
-}
-
-// logreg_reduce + newton_update in ONE launch (single-process fits: no all-reduce between them).
-// The reduce blocks publish their columns (agent fence) and take a ticket; the last block runs the
-// Newton update in its first wave on the just-reduced vector.  Same fixed-order fp64 reduction,
-// same update code: bitwise the two-launch result, one kernel boundary (~2-4 us) less per
-// iteration.  The ticket is zero between launches (the last block resets it).
-template <int MT>
-__global__ __launch_bounds__(1024) void logreg_reduce_update_kernel(
-    const float* __restrict__ partial, int nblocks, int ncols, double* __restrict__ out, unsigned int* ticket,
-    double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done, int d, double C, double tol,
-    int max_iter, int fit_intercept, int phase_start, const double* __restrict__ aff, int* __restrict__ done_host,
-    int seq) {
-  if (*done) {  // converged: the update's own early exit still tags the host's flag word
-    if (blockIdx.x == 0 && threadIdx.x == 0 && done_host != nullptr)
-      __hip_atomic_store(done_host, (seq << 1) | 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
-  reduce_columns(partial, nblocks, ncols, out);
-  __threadfence();
-  __shared__ int s_last;
-  __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (threadIdx.x < 64)
-    newton_update_body<MT, false>(out, st, w32, done, d, C, tol, max_iter, fit_intercept, phase_start, aff, nullptr,
-                                  done_host, seq);
 }
 #undef FDX_STAMP
 
@@ -1480,23 +1428,6 @@ void launch_newton_update(const double* red, double* state, float* w32, int* don
     newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
                                                   phase_start, aff, nullptr, done_host, seq);
   check_launch("newton_update");
-}
-
-void launch_newton_reduce_update(const float* partial, int nblocks, int ncols, double* red, unsigned int* ticket,
-                                 double* state, float* w32, int* done, int d, double C, double tol, int max_iter,
-                                 int fit_intercept, int phase_start, const double* aff, hipStream_t stream,
-                                 int* done_host, int seq) {
-  if (ncols != kLRPartStride && ncols != 34) throw std::runtime_error("newton_reduce_update: ncols 1088 or 34");
-  const int g = (ncols + kRedCols - 1) / kRedCols;
-  if (d + (fit_intercept ? 1 : 0) == 31)
-    logreg_reduce_update_kernel<31><<<g, 1024, 0, stream>>>(partial, nblocks, ncols, red, ticket, state, w32, done, d,
-                                                            C, tol, max_iter, fit_intercept, phase_start, aff,
-                                                            done_host, seq);
-  else
-    logreg_reduce_update_kernel<0><<<g, 1024, 0, stream>>>(partial, nblocks, ncols, red, ticket, state, w32, done, d,
-                                                           C, tol, max_iter, fit_intercept, phase_start, aff,
-                                                           done_host, seq);
-  check_launch("newton_reduce_update");
 }
 
 void launch_newton_update_stamped(const double* red, double* state, float* w32, int* done, double C,

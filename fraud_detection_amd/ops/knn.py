@@ -34,8 +34,6 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 # the search is bound by the per-tile filter/top-k bookkeeping beside the MFMA chain, neither by
 # the streamed bytes nor by the matrix pipe alone.  auto = fp32; FDX_KNN selects another engine.
 KNN_BF16X3_MIN_CANDIDATES = 1 << 62
-# candidate tiles of the pilot search that seeds the fp32 engine's thresholds (0: off)
-KNN_SEED_TILES = int(os.environ.get("FDX_KNN_SEED", "0"))
 
 
 def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:
@@ -62,7 +60,7 @@ def _check_parents(parents: torch.Tensor | None, C: torch.Tensor, affine: torch.
 
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
              nsplit: int | None = None, engine: str | None = None, parents: torch.Tensor | None = None,
-             parents_affine: torch.Tensor | None = None, seed_tiles: int | None = None):
+             parents_affine: torch.Tensor | None = None):
     """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
@@ -73,8 +71,6 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     "bf16x3" = hi.hi + hi.lo + lo.hi bf16 MFMA filter (6 x 32x32x16 bf16 per tile) with a provable
     margin and exact fp32 re-scoring of the survivors; None/"auto" (FDX_KNN env) picks by size.
     Both return the exact fp32 ranking.
-    ``seed_tiles`` (fp32 engine; None = KNN_SEED_TILES): a pilot search over the first candidate tiles
-    seeds every slice's filter threshold -- exact (the lists are unchanged), less per-tile work.
     ``parents`` (bf16 [mc, 32], optional): also filled with ``smote_parents(C, parents_affine)``
     by the operand-prep launch that already reads C (one launch fewer on the SMOTE path).
     """
@@ -123,13 +119,8 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
     if eng == "fp32":
-        st = KNN_SEED_TILES if seed_tiles is None else int(seed_tiles)
-        sd_s = sd_i = None
-        if st > 0:
-            sd_s = torch.empty((mq, k), device=Q.device, dtype=torch.float32)
-            sd_i = torch.empty((mq, k), device=Q.device, dtype=torch.int32)
         m.knn_topk(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
-                   ptr(score), ptr(ws_s), ptr(ws_i), ns, s, st, ptr(sd_s), ptr(sd_i))
+                   ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     elif eng == "fp32lds":
         m.knn_topk_lds(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
                        ptr(score), ptr(ws_s), ptr(ws_i), ns, s)

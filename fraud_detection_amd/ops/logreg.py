@@ -12,7 +12,6 @@ The device loop never synchronises with the host inside a chunk of iterations: a
 """
 from __future__ import annotations
 
-import os
 import time
 
 from dataclasses import dataclass, field
@@ -281,9 +280,6 @@ class LRWorkspace:
         # fused SGD steps: 32 replicas x 36 int64 fixed-point accumulators + the arrival ticket;
         # zero between steps (every step's last block swaps them back to zero)
         self.sgd_acc = torch.zeros(SGD_ACC_WORDS + 8, device=device, dtype=torch.int64)
-        # ticket of the fused reduce + Newton update (logreg.hip logreg_reduce_update_kernel), zero
-        # between launches
-        self.nticket = torch.zeros(2, device=device, dtype=torch.int32)
 
     def prepare_flags(self, depth: int = 2):
         """The mapped pinned convergence-flag words newton_fit polls (pinned allocations cost tens
@@ -319,8 +315,6 @@ HESS_SAMPLE_ROWS = 1 << 21
 
 
 GRAD_SLOTS = 34  # red[0:32] gradient, red[32] loss, red[33] weight; red[34] = Hessian-sample weight
-# single-process Newton: reduce + update in one launch (False: the two-launch pair, for A/B runs)
-FUSED_UPDATE = os.environ.get("FDX_FUSED_UPDATE", "1") != "0"
 
 
 def auto_hess_stride(n_rows: int) -> int:
@@ -358,7 +352,7 @@ def progressive_schedule(n_rows: int) -> list:
 
 
 def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True,
-          sub: int = 1, virtual: VirtualSmote | None = None, hole: tuple = (0, 0), reduce: bool = True) -> int:
+          sub: int = 1, virtual: VirtualSmote | None = None, hole: tuple = (0, 0)):
     """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact).
     sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up).
     virtual: rows >= rows.shape[0] are virtual SMOTE rows (end may reach n_real + n_new).
@@ -386,20 +380,7 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
         m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
                           ptr(ws.partial), nb, s, 0, False, ha, hl)
     # gradient-only: reduce slots 0..33 and keep red[34] (weight of the rows behind the held H)
-    if reduce:
-        m.logreg_reduce(ptr(ws.partial), nb, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
-    return nb
-
-
-def _step(m, rows, ws: LRWorkspace, hessian: int, n: int, fp8_scale: float, s: int, sub: int,
-          virtual, hole, d: int, C: float, tol: float, max_iter: int, fit_intercept: bool, phase_start: int,
-          aff: int, done_host: int = 0, seq: int = 0):
-    """One single-process Newton iteration: the pass, then the reduce and the update in ONE launch
-    (logreg.hip logreg_reduce_update_kernel -- bitwise the reduce + update pair)."""
-    nb = _pass(m, rows, ws, hessian, 0, n, fp8_scale, s, sub=sub, virtual=virtual, hole=hole, reduce=False)
-    m.newton_reduce_update(ptr(ws.partial), nb, PART_STRIDE if hessian else GRAD_SLOTS, ptr(ws.red),
-                           ptr(ws.nticket), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
-                           int(max_iter), int(fit_intercept), int(phase_start), aff, s, done_host, seq)
+    m.logreg_reduce(ptr(ws.partial), nb, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
 
 
 def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian: bool = True,
@@ -544,10 +525,6 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     for sub, iters in sched:
         hs_w = auto_warm_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
-            if not sync_warm and FUSED_UPDATE:
-                _step(m, rows, ws, hs_w, n, fp8_scale, s, sub, virtual, hole, d, C, 0.0, 1 << 30, fit_intercept,
-                      int(j == 0), aff)
-                continue
             _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual, hole=hole)
             if sync_warm:
                 comm.all_reduce_(ws.red)
@@ -576,11 +553,6 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             # 8 vs 7 iterations, profiles/r1_s25)
             fresh = refresh <= 0 or full_it[0] % refresh == 0
             full_it[0] += 1
-            if not dp and FUSED_UPDATE:
-                _step(m, rows, ws, hs if fresh else 0, n, fp8_scale, s, 1, virtual, hole, d, C, tol, max_iter + warm,
-                      fit_intercept, first[0], aff, done_host if i == k - 1 else 0, seq)
-                first[0] = 0
-                continue
             _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual, hole=hole)
             if comm is not None and comm.world_size > 1:
                 # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
@@ -885,7 +857,6 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
     shrunk for small shards like the device), virtual samples by their pick tile."""
     R = ref.rows_to_f32(rows, fp8_scale, d).double().numpy()
     n_stored = R.shape[0]
-    fp8 = storage_kind(rows) == "fp8"
     rb = ref.sgd_row_batches(n_stored, nb, ref.sgd_grid_blocks(n_stored, nb, 768))
     parts = [R]
     bs = [rb]

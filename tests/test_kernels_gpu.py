@@ -217,25 +217,6 @@ def test_newton_deterministic(dev):
     assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("d", [30, 12])
-def test_newton_fused_reduce_update_bit_identical(dev, monkeypatch, d):
-    """The one-launch reduce + update (logreg_reduce_update_kernel) == the logreg_reduce +
-    newton_update pair, bit for bit: warm-up, lazy-Hessian and deferred full-phase iterations."""
-    X, y = _data(200_000, seed=40 + d, rate=0.03)
-    X = X[:, :d].contiguous()
-    st = S.scaler_fit(X.to(dev))
-    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
-    kw = dict(d=d, tol=1e-7, max_iter=30, progressive=[(8, 2), (2, 1)], hess_refresh=2)
-    monkeypatch.setattr(L, "FUSED_UPDATE", False)
-    a = L.newton_fit(rows, **kw).as_fit_info()
-    monkeypatch.setattr(L, "FUSED_UPDATE", True)
-    b = L.newton_fit(rows, **kw).as_fit_info()
-    c = L.newton_fit(rows, **kw, workspace=L.LRWorkspace(dev), full_iters=2).as_fit_info()
-    assert a.converged and b.converged and c.converged
-    assert a.n_iter == b.n_iter == c.n_iter
-    assert np.array_equal(a.w, b.w) and np.array_equal(a.w, c.w)
-
-
 @pytest.mark.parametrize("pred", [1, 2, 6])
 def test_newton_deferred_check_same_fit(dev, pred):
     """newton_fit(full_iters=k): k full-data iterations enqueued with no host wait, convergence
@@ -355,23 +336,6 @@ def test_knn_split_search_identical(dev, nsplit):
     a, sa = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, nsplit=1)
     b, sb = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, nsplit=nsplit)
     assert torch.equal(a, b) and torch.equal(sa, sb)
-
-
-@pytest.mark.parametrize("seed_tiles", [1, 4, 16])
-@pytest.mark.parametrize("nsplit", [1, 5, 31])
-def test_knn_pilot_seed_identical(dev, seed_tiles, nsplit):
-    """A pilot-seeded threshold changes no list and no score (ties, duplicates across slices, the
-    query's self row inside the pilot tiles), and it also holds with queries offset in C."""
-    rng = np.random.default_rng(8)
-    C = np.zeros((3001, 32), np.float32)
-    C[:, :30] = np.round(rng.normal(size=(3001, 30)) * 4) / 4
-    C[1500:1600] = C[100:200]
-    Ct = torch.from_numpy(C).to(dev)
-    for off, mq in ((0, 1000), (700, 900)):
-        Q = Ct[off: off + mq].contiguous()
-        a, sa = K.knn_topk(Q, Ct, k=5, self_offset=off, want_dist=True, nsplit=nsplit, seed_tiles=0)
-        b, sb = K.knn_topk(Q, Ct, k=5, self_offset=off, want_dist=True, nsplit=nsplit, seed_tiles=seed_tiles)
-        assert torch.equal(a, b) and torch.equal(sa, sb)
 
 
 def test_smote_generate_matches_oracle(dev):

@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""k-NN (SMOTE self-search, k=5, fp32 engine) at the bench shapes: candidate slices x pilot seed.
+"""k-NN (SMOTE self-search, k=5, fp32 engine) at the bench shapes: candidate slices.
 
     python tools/knn_lab.py [--reps 20] [--json out.json]
 
 Shapes: DP1 (the 10M-row bench's 13.6k minority rows against themselves) and the DP=8 global-scope
-rank (its 13.6k minority rows against all 8 ranks' 108.8k).  For every (nsplit, seed_tiles) the
-event-timed median of the whole knn_topk call (prep + pilot + search + merge) and whether the lists
-equal the unseeded auto-split lists exactly.
+rank (its 13.6k minority rows against all 8 ranks' 108.8k).  For every nsplit the event-timed
+median of the whole knn_topk call (prep + search + merge) and whether the lists equal the
+auto-split lists exactly.  (r4: a pilot search seeding every slice's threshold was measured here
+too, 1-3% slower at every split count -- profiles/r4_g/knn_lab.json -- and removed.)
 """
 import argparse
 import json
@@ -54,21 +55,20 @@ def main():
     for name, (Q, Cc, off) in shapes.items():
         mq, mc = Q.shape[0], Cc.shape[0]
         auto = native().knn_splits((mq + 31) // 32 * 32, (mc + 31) // 32 * 32)
-        ref = K.knn_topk(Q, Cc, 5, off, engine="fp32", seed_tiles=0)
+        ref = K.knn_topk(Q, Cc, 5, off, engine="fp32")
         rec = {"mq": mq, "mc": mc, "auto_nsplit": int(auto), "cases": []}
         for ns in sorted({1, 2, 4, 8, 16, 32, int(auto)}):
-            for st in (0, 2, 4, 8, 16):
-                f = lambda: K.knn_topk(Q, Cc, 5, off, engine="fp32", nsplit=ns, seed_tiles=st)  # noqa: E731
-                got = f()
-                ms = timed(f)
-                case = {"nsplit": ns, "seed_tiles": st, "ms": round(ms, 4),
-                        "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
-                        "lists_equal": bool((got == ref).all().item())}
-                rec["cases"].append(case)
-                print(json.dumps({name: case}), flush=True)
+            f = lambda: K.knn_topk(Q, Cc, 5, off, engine="fp32", nsplit=ns)  # noqa: E731
+            got = f()
+            ms = timed(f)
+            case = {"nsplit": ns, "ms": round(ms, 4),
+                    "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
+                    "lists_equal": bool((got == ref).all().item())}
+            rec["cases"].append(case)
+            print(json.dumps({name: case}), flush=True)
         best = min(rec["cases"], key=lambda c: c["ms"])
-        base = [c for c in rec["cases"] if c["nsplit"] == auto and c["seed_tiles"] == 0][0]
-        rec["best"], rec["baseline_auto_unseeded"] = best, base
+        base = [c for c in rec["cases"] if c["nsplit"] == auto][0]
+        rec["best"], rec["auto"] = best, base
         out["shapes"][name] = rec
     if a.json:
         with open(a.json, "w") as fh:
