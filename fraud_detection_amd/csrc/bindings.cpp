@@ -786,9 +786,9 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
   m.def("auc_radix_workspace_bytes", &fdx::auc_radix_workspace_bytes);
   m.def("auc_radix_layout", [](int64_t n) {
-    size_t off[7];
+    size_t off[8];
     fdx::auc_radix_layout(n, off);
-    return std::vector<size_t>(off, off + 7);
+    return std::vector<size_t>(off, off + 8);
   });
   m.def("auc_radix", [](u scores, u labels, int64_t n, u ws, u res, u auc, u s) {
     fdx::launch_auc_radix(P<const float>(scores), P<const uint8_t>(labels), n, P<void>(ws), P<int64_t>(res),

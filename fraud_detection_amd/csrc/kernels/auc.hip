@@ -238,41 +238,64 @@ __global__ __launch_bounds__(kThreads) void radix_hist_kernel(const uint32_t* __
   hist[(int64_t)t * gridDim.x + blockIdx.x] = h[t];  // digit-major: the scan order = stable order
 }
 
-// In-place exclusive scan of `total` uint32 counts (digit-major [256][nblk]); one 1024-thread
-// block, each thread a contiguous run.
-__global__ __launch_bounds__(1024) void radix_scan_kernel(uint32_t* __restrict__ a, int total) {
-  __shared__ uint32_t part[1024];
-  const int t = threadIdx.x;
-  const int per = (total + 1023) / 1024;
-  const int lo = min(total, t * per), hi = min(total, lo + per);
-  uint32_t sum = 0;
-  for (int i = lo; i < hi; ++i) sum += a[i];
-  part[t] = sum;
+// Exclusive scan of one wave's values (inclusive shuffle scan minus the own value); *tot = sum.
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* tot) {
+  const int lane = lane_id();
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < kWave; o <<= 1) {
+    const uint32_t y = __shfl_up(inc, o, kWave);
+    if (lane >= o) inc += y;
+  }
+  *tot = __shfl(inc, kWave - 1, kWave);
+  return inc - v;
+}
+
+// Per-digit scan of the digit-major [256][nblk] block counts: block d scans row d in place
+// (within-digit offsets, stable across blocks) and writes the digit's total; the scatter kernel
+// adds the exclusive scan of the 256 totals.  (Was one 1024-thread block walking 1024-element
+// runs per thread -- uncoalesced, 256 dependent loads per thread: ~330 us per radix pass at 2M
+// scores, profiles/r4_i/timeline_cv_job.txt; now two parallel scans of <= 1024 elements.)
+__global__ __launch_bounds__(1024) void radix_rowscan_kernel(uint32_t* __restrict__ hist, int nblk,
+                                                             uint32_t* __restrict__ tot) {
+  __shared__ uint32_t wsum[16];
+  const int t = threadIdx.x, w = wave_id();
+  uint32_t* row = hist + (int64_t)blockIdx.x * nblk;
+  const uint32_t v = t < nblk ? row[t] : 0u;
+  uint32_t wt;
+  const uint32_t ex = wave_excl_scan(v, &wt);
+  if (lane_id() == 0) wsum[w] = wt;
   __syncthreads();
-  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan of the run sums
-    const uint32_t v = t >= off ? part[t - off] : 0u;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
+  uint32_t wb = 0, all = 0;
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t x = wsum[i];
+    wb += i < w ? x : 0u;
+    all += x;
   }
-  uint32_t run = t > 0 ? part[t - 1] : 0u;
-  for (int i = lo; i < hi; ++i) {
-    const uint32_t c = a[i];
-    a[i] = run;
-    run += c;
-  }
+  if (t < nblk) row[t] = wb + ex;
+  if (t == 0) tot[blockIdx.x] = all;
 }
 
 __global__ __launch_bounds__(kThreads) void radix_scatter_kernel(const uint32_t* __restrict__ key,
                                                                  const uint8_t* __restrict__ lab, int64_t n,
                                                                  int shift, int64_t per_blk,
                                                                  const uint32_t* __restrict__ offs,
+                                                                 const uint32_t* __restrict__ tot,
                                                                  uint32_t* __restrict__ key_out,
                                                                  uint8_t* __restrict__ lab_out) {
   __shared__ uint32_t run[256];
   __shared__ uint32_t wc[kThreads / kWave][256];
+  __shared__ uint32_t dsum[kThreads / kWave];
   const int t = threadIdx.x, w = wave_id(), lane = lane_id();
-  run[t] = offs[(int64_t)t * gridDim.x + blockIdx.x];
+  {  // digit base = exclusive scan of the 256 digit totals (kThreads == 256: one digit per thread)
+    uint32_t wt;
+    const uint32_t ex = wave_excl_scan(tot[t], &wt);
+    if (lane == 0) dsum[w] = wt;
+    __syncthreads();
+    uint32_t wb = 0;
+    for (int i = 0; i < w; ++i) wb += dsum[i];
+    run[t] = wb + ex + offs[(int64_t)t * gridDim.x + blockIdx.x];
+  }
 #pragma unroll
   for (int v = 0; v < kThreads / kWave; ++v) wc[v][t] = 0;
   const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -367,9 +390,9 @@ __global__ void auc_sorted_finalize_kernel(const unsigned long long* __restrict_
 
 // Workspace layout, every region 256-byte aligned (the u64 counters take 64-bit atomics; an odd n
 // must not shift them off alignment): k0 | k1 (u32 [n]) | l0 | l1 (u8 [n]) | hist (u32 [256][blocks])
-// | cnt (u64 [3]).  Offsets in bytes; [6] = total.
+// | cnt (u64 [3]) | tot (u32 [256]).  Offsets in bytes; [7] = total.
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-void auc_radix_layout(int64_t n, size_t off[7]) {
+void auc_radix_layout(int64_t n, size_t off[8]) {
   const size_t nn = (size_t)(n > 0 ? n : 0);
   off[0] = 0;
   off[1] = align256(off[0] + nn * 4);
@@ -378,18 +401,19 @@ void auc_radix_layout(int64_t n, size_t off[7]) {
   off[4] = align256(off[3] + nn);
   off[5] = align256(off[4] + (size_t)256 * kRadixBlocks * 4);
   off[6] = align256(off[5] + 3 * sizeof(unsigned long long));
+  off[7] = align256(off[6] + 256 * 4);  // per-digit totals
 }
 
 size_t auc_radix_workspace_bytes(int64_t n) {
-  size_t off[7];
+  size_t off[8];
   auc_radix_layout(n, off);
-  return off[6];
+  return off[7];
 }
 
 void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, void* ws, int64_t* res, double* auc,
                       hipStream_t stream) {
   if (reinterpret_cast<uintptr_t>(ws) % 256 != 0) throw std::runtime_error("auc_radix: workspace must be 256-byte aligned");
-  size_t off[7];
+  size_t off[8];
   auc_radix_layout(n, off);
   char* p = static_cast<char*>(ws);
   uint32_t* k0 = reinterpret_cast<uint32_t*>(p + off[0]);
@@ -398,6 +422,7 @@ void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, voi
   uint8_t* l1 = reinterpret_cast<uint8_t*>(p + off[3]);
   uint32_t* hist = reinterpret_cast<uint32_t*>(p + off[4]);
   unsigned long long* cnt = reinterpret_cast<unsigned long long*>(p + off[5]);
+  uint32_t* tot = reinterpret_cast<uint32_t*>(p + off[6]);
   if (hipMemsetAsync(cnt, 0, 3 * sizeof(unsigned long long), stream) != hipSuccess)
     throw std::runtime_error("auc_radix: memset failed");
   if (n > 0) {
@@ -410,8 +435,8 @@ void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, voi
     const int shifts[5] = {-1, 0, 8, 16, 24};  // label digit first (least significant), then key bytes
     for (int ps = 0; ps < 5; ++ps) {
       radix_hist_kernel<<<nblk, kThreads, 0, stream>>>(k0, l0, n, shifts[ps], per_blk, hist);
-      radix_scan_kernel<<<1, 1024, 0, stream>>>(hist, 256 * nblk);
-      radix_scatter_kernel<<<nblk, kThreads, 0, stream>>>(k0, l0, n, shifts[ps], per_blk, hist, k1, l1);
+      radix_rowscan_kernel<<<256, 1024, 0, stream>>>(hist, nblk, tot);
+      radix_scatter_kernel<<<nblk, kThreads, 0, stream>>>(k0, l0, n, shifts[ps], per_blk, hist, tot, k1, l1);
       std::swap(k0, k1);
       std::swap(l0, l1);
     }

@@ -235,7 +235,7 @@ void launch_sort_chunks(float* pos, int64_t npos_cap, const unsigned long long* 
                         int chunk, int nchunks, hipStream_t stream);
 // exact AUC from sorted scores: 2 * pairs won + ties, summed over tie segments (u64, exact)
 size_t auc_radix_workspace_bytes(int64_t n);
-void auc_radix_layout(int64_t n, size_t off[7]);
+void auc_radix_layout(int64_t n, size_t off[8]);
 void launch_auc_radix(const float* scores, const uint8_t* labels, int64_t n, void* ws, int64_t* res, double* auc,
                       hipStream_t stream);
 void launch_auc_count(const float* scores, const uint8_t* labels, int64_t n, const float* pos,

@@ -197,25 +197,9 @@ __device__ __forceinline__ int stats_fetch(const float* __restrict__ X, int64_t 
 // mean as the pivot and of 1/sigma as colscale (ops/scaler.py fp8_fused_prescale); the exact
 // statistics from this same pass turn that into the solver's affine map, so the prescale only
 // has to be roughly right.
-// Gather form (IDX: cross-validation, models/cv.py): output row i and its statistics come from
-// input row idx[i] -- the fold-sorted training table is cast straight from the raw table in the
-// same single read, with no permuted copy of X.  Rows are 8-byte aligned 2-float pieces (d even).
-__device__ __forceinline__ int stats_fetch_idx(const float* __restrict__ X, const int64_t* __restrict__ idx, int64_t t,
-                                               int d, int64_t n, float2 (&b)[8]) {
-  const int64_t r0 = t * kStatTileRows;
-  const int rows = (int)((n - r0) < (int64_t)kStatTileRows ? (n - r0) : (int64_t)kStatTileRows);
-  const int hp = d >> 1, np = rows * hp;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int e = threadIdx.x + k * kThreads;
-    if (e < np) {
-      const int r = e / hp, p = e - r * hp;
-      b[k] = reinterpret_cast<const float2*>(X + idx[r0 + r] * (int64_t)d)[p];
-    }
-  }
-  return rows * d;
-}
-
+// Scatter form (IDX: cross-validation, models/cv.py): row i is written to output row idx[i] -- the
+// fold-sorted training table is cast from the raw table read in order (64-byte rows land whole at
+// scattered positions; gathering the 120-byte raw rows instead ran at a third of the stream rate).
 template <bool NT, bool FP8, bool IDX = false>
 __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kernel(
     const float* __restrict__ X, int64_t n, int d, const float* __restrict__ pivot,
@@ -240,20 +224,11 @@ __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kerne
   // in flight while tile t is reduced and cast out of LDS.
   float4 b0 = make_float4(0.f, 0.f, 0.f, 0.f), b1 = b0, b2 = b0, b3 = b0;
   float tail = 0.0f;
-  float2 bg[8];
   int64_t t = blockIdx.x;
   int nf = 0;
-  if (t < ntiles) nf = IDX ? stats_fetch_idx(X, idx, t, d, n, bg) : stats_fetch(X, t, d, total, b0, b1, b2, b3, tail);
+  if (t < ntiles) nf = stats_fetch(X, t, d, total, b0, b1, b2, b3, tail);
   for (; t < ntiles; t += gridDim.x) {
-    if constexpr (IDX) {
-      const int np = nf >> 1;
-      float2* t2 = reinterpret_cast<float2*>(tile);
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const int e = threadIdx.x + k * kThreads;
-        if (e < np) t2[e] = bg[k];
-      }
-    } else {
+    {
       const int nf4 = nf >> 2, i = threadIdx.x;
       float4* t4 = reinterpret_cast<float4*>(tile);
       if (i < nf4) t4[i] = b0;
@@ -265,9 +240,7 @@ __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kerne
     }
     __syncthreads();
     const int rows = nf / d;
-    if (t + gridDim.x < ntiles)
-      nf = IDX ? stats_fetch_idx(X, idx, t + gridDim.x, d, n, bg)
-               : stats_fetch(X, t + gridDim.x, d, total, b0, b1, b2, b3, tail);
+    if (t + gridDim.x < ntiles) nf = stats_fetch(X, t + gridDim.x, d, total, b0, b1, b2, b3, tail);
     if (c < d) {
       for (int r = rg; r < rows; r += 8) {
         const double dd = (double)tile[r * d + c] - piv;
@@ -281,25 +254,26 @@ __global__ __launch_bounds__(kThreads, FP8 ? 6 : 8) void scaler_stats_cast_kerne
       const int r = slot >> 2;
       if (r >= rows) continue;
       const int64_t grow = t * kStatTileRows + r;
+      const int64_t orow = IDX ? idx[grow] : grow;  // destination row
       float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int cc = 8 * q + j;
         if (cc < d) o[j] = FP8 ? (tile[r * d + cc] - pv[j]) * ks[j] : tile[r * d + cc] - pv[j];
         else if (cc == kBiasCol) o[j] = bias_value;
-        else if (cc == kLabelCol) o[j] = labels ? (float)labels[IDX ? idx[grow] : grow] : 0.0f;
+        else if (cc == kLabelCol) o[j] = labels ? (float)labels[grow] : 0.0f;
         else o[j] = 0.0f;
       }
       if constexpr (FP8) {
         const uint2 pk = make_uint2(f32x4_to_fp8(o[0], o[1], o[2], o[3]), f32x4_to_fp8(o[4], o[5], o[6], o[7]));
-        if constexpr (NT) __builtin_nontemporal_store(u32x2_t{pk.x, pk.y}, reinterpret_cast<u32x2_t*>(outv) + grow * 4 + q);
-        else reinterpret_cast<uint2*>(outv)[grow * 4 + q] = pk;
+        if constexpr (NT) __builtin_nontemporal_store(u32x2_t{pk.x, pk.y}, reinterpret_cast<u32x2_t*>(outv) + orow * 4 + q);
+        else reinterpret_cast<uint2*>(outv)[orow * 4 + q] = pk;
       } else {
         uint4 pk;
         pk.x = pack_bf16x2(o[0], o[1]); pk.y = pack_bf16x2(o[2], o[3]);
         pk.z = pack_bf16x2(o[4], o[5]); pk.w = pack_bf16x2(o[6], o[7]);
-        if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(outv) + grow * 4 + q);
-        else reinterpret_cast<uint4*>(outv)[grow * 4 + q] = pk;
+        if constexpr (NT) __builtin_nontemporal_store(u32x4_t{pk.x, pk.y, pk.z, pk.w}, reinterpret_cast<u32x4_t*>(outv) + orow * 4 + q);
+        else reinterpret_cast<uint4*>(outv)[orow * 4 + q] = pk;
       }
     }
     __syncthreads();
@@ -853,8 +827,6 @@ void launch_scaler_stats_cast(const float* X, int64_t n, int d, const float* piv
                               const float* colscale, float out_scale, const int64_t* idx) {
   if (d > 30 || (reinterpret_cast<uintptr_t>(X) % 16) != 0 || (reinterpret_cast<uintptr_t>(out) % 16) != 0)
     throw std::invalid_argument("scaler_stats_cast: contiguous 16-byte aligned rows, d <= 30");
-  if (idx != nullptr && (d & 1))
-    throw std::invalid_argument("scaler_stats_cast: the gather form reads 2-float pieces (even d)");
   // every block must be resident at once (a second round of blocks would double the span);
   // nblocks is fixed by the caller (partial buffer), the grid-stride loop covers the rest
 #define FDX_SSC(NT, F8, I)                                                                                 \

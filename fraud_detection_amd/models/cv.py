@@ -7,10 +7,11 @@ SMOTE on the whole training split, the final fit and the test AUC -- 6 SMOTE + f
 
 MI355X layout (no per-fold copy of the training rows):
   * fold codes: ops/split.assign (keyed Feistel, stratified, sizes within one row per class);
-  * one permutation sorts the training rows by (fold, label) -- ten stable compactions;
-  * ONE fused scaler pass in gather form (ops/scaler.scaler_fit_cast(idx=perm)) reads the raw
-    table once and writes the fold-sorted training table (pivot-shifted bf16 / fp8 rows) plus the
-    statistics of the whole split (the reference's single scaler);
+  * one permutation sorts the training rows by fold (five stable compactions; five more list each
+    fold's positives);
+  * ONE fused scaler pass in scatter form (ops/scaler.scaler_fit_cast(out_idx=...)) reads the raw
+    table once, in order, and writes the fold-sorted training table (pivot-shifted bf16 / fp8 rows)
+    plus the statistics of the whole split (the reference's single scaler);
   * fold k trains on the table minus its own block: the logistic passes step over the block
     (ops/logreg ``hole``, logreg.hip RowHole);
   * fold k's SMOTE minority = the positive tails of the other folds' blocks: the standardized fp32
@@ -67,6 +68,7 @@ class DeviceCV:
         self.cfg = cfg or TrainConfig()
         self.n_folds = int(n_folds)
         self.seed = int(seed)
+        self._ws: list = []
         if self.cfg.solver not in ("newton", "sgd"):
             raise ValueError("DeviceCV fits the logistic solvers (newton | sgd)")
 
@@ -84,20 +86,26 @@ class DeviceCV:
         ev[0].record()
         # ---- fold codes and the (fold, label) permutation -----------------------------------
         codes = split_ops.assign(y, test_frac=0.0, n_folds=K, seed=self.seed)
+        # the table is sorted by fold only: inside a block the rows keep their order, so the
+        # sub-sampled warm-up passes (runs of row tiles) see both classes in proportion.  (Sorted by
+        # (fold, label), a fold's positives formed one contiguous run that a 1/16 tile sample took
+        # whole or missed: 4 full-data Newton iterations per fold instead of 2.)
         key = (codes * 2 + y).to(torch.uint8)
-        pend = [scaler_ops.compact_indices_async(key, t) for t in range(2 * K)]
-        parts = [p.result() for p in pend]
-        sizes = [int(p.shape[0]) for p in parts]
-        perm = torch.cat(parts)
-        neg = sizes[0::2]
-        pos = sizes[1::2]
-        bounds = np.concatenate([[0], np.cumsum([a + b for a, b in zip(neg, pos)])]).astype(np.int64)
+        pend_f = [scaler_ops.compact_indices_async(codes, t) for t in range(K)]
+        pend_p = [scaler_ops.compact_indices_async(key, 2 * t + 1) for t in range(K)]
+        folds = [p.result() for p in pend_f]
+        pos_parts = [p.result() for p in pend_p]
+        perm = torch.cat(folds)
+        pos = [int(p.shape[0]) for p in pos_parts]
+        bounds = np.concatenate([[0], np.cumsum([int(f.shape[0]) for f in folds])]).astype(np.int64)
         pbounds = np.concatenate([[0], np.cumsum(pos)]).astype(np.int64)
         # ---- ONE fused scaler pass: fold-sorted training table + the split's statistics -------
         rows = torch.empty((n, NCOLS), device=dev, dtype=TORCH_STORAGE[cfg.storage])
-        stats = scaler_ops.scaler_fit_cast(X, y, rows, fp8_scale=cfg.fp8_scale, idx=perm)
+        dest = torch.empty(n, device=dev, dtype=torch.int64)  # row i of X -> table row dest[i]
+        dest[perm] = torch.arange(n, device=dev, dtype=torch.int64)
+        stats = scaler_ops.scaler_fit_cast(X, y, rows, fp8_scale=cfg.fp8_scale, out_idx=dest)
         y_perm = y[perm]
-        pos_idx = torch.cat(parts[1::2])
+        pos_idx = torch.cat(pos_parts)
         xpos = scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=pos_idx)  # fold-sorted
         ev[1].record()
         m = native()
@@ -129,8 +137,15 @@ class DeviceCV:
             parents = torch.empty((n_min, NCOLS), dtype=torch.bfloat16, device=dev)
             nbr = knn_ops.knn_topk(xmin, xmin, k=kk, self_offset=0, parents=parents, parents_affine=stats.aff)
             v = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, seed=cfg.seed).prepare()
-            ws = lr_ops.LRWorkspace(dev)
-            ws.prepare_flags()
+            # one workspace per fit, kept across runs (every fit of a run is verified before it
+            # returns; the pinned flag words are costly to allocate)
+            slot = K if k is None else k
+            if len(self._ws) <= slot or self._ws[slot].state.device != dev:
+                while len(self._ws) <= slot:
+                    self._ws.append(None)
+                self._ws[slot] = lr_ops.LRWorkspace(dev)
+                self._ws[slot].prepare_flags()
+            ws = self._ws[slot]
             if cfg.solver == "newton":
                 f = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, d=d, w0=w0, class_w=cw,
                                       fit_intercept=cfg.fit_intercept, fp8_scale=cfg.fp8_scale,

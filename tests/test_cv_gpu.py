@@ -24,13 +24,14 @@ def test_device_cv_job(dev, solver, storage):
     cv = DeviceCV(TrainConfig(solver=solver, storage=storage, seed=42))
     r = cv.run(X, y, Xt, yt)
     assert len(r.fold_aucs) == 5 and all(a > 0.9 for a in r.fold_aucs) and r.test_auc > 0.9
-    # the permutation is a permutation, sorted by fold code, negatives first inside each fold
+    # the permutation is a permutation, sorted by fold code, rows in their order inside a fold
     perm = cv.perm.cpu().numpy()
     assert np.array_equal(np.sort(perm), np.arange(X.shape[0]))
     codes = SP.assign_numpy(y.cpu().numpy(), 0.0, 5, 42)
     yp = y.cpu().numpy()[perm]
-    cp = codes[perm]
-    assert np.all(np.diff(cp.astype(int) * 2 + yp) >= 0)
+    cp = codes[perm].astype(int)
+    assert np.all(np.diff(cp) >= 0)
+    assert np.all(np.diff(perm)[np.diff(cp) == 0] > 0)
     b = cv.bounds
     assert b[-1] == X.shape[0] and np.all(np.diff(b) > 0)
     # fold 2's fit == the same solver on an explicit copy of the other blocks (same samples)

@@ -471,6 +471,30 @@ def test_scaler_fit_cast_fused(dev, n, d):
     np.testing.assert_allclose(st.aff.cpu().numpy(), st_cpu.aff.numpy(), rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("storage,d", [("bf16", 30), ("fp8", 30), ("bf16", 7)])
+def test_scaler_fit_cast_scatter_form(dev, storage, d):
+    """out_idx: row i of X lands in out[out_idx[i]] (the CV table), statistics of the in-order pass."""
+    n = 300_007
+    X, y = _data(n, seed=31 + d)
+    X = X[:, :d].contiguous()
+    Xd, yd = X.to(dev), y.to(dev)
+    dest = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(dev)
+    dt = torch.bfloat16 if storage == "bf16" else torch.uint8
+    plain = torch.empty((n, 32), dtype=dt, device=dev)
+    st0 = S.scaler_fit_cast(Xd, yd, plain, fp8_scale=4.0)
+    scat = torch.empty((n, 32), dtype=dt, device=dev)
+    st1 = S.scaler_fit_cast(Xd, yd, scat, fp8_scale=4.0, out_idx=dest)
+    exp = torch.empty_like(plain)
+    exp[dest] = plain
+    assert torch.equal(scat, exp)
+    for a, b in zip(st0.numpy(), st1.numpy()):
+        assert np.array_equal(a, b)
+    if storage == "bf16":  # the host oracle's scatter too
+        cpu = torch.empty((n, 32), dtype=torch.bfloat16)
+        S.scaler_fit_cast(X, y, cpu, out_idx=dest.cpu())
+        assert torch.equal(cpu, scat.cpu())
+
+
 def test_smote_affine_output_matches_oracle(dev):
     X, y = _data(200_000, seed=23, rate=0.02)
     sh = torch.empty((X.shape[0], 32), dtype=torch.bfloat16)

@@ -20,8 +20,8 @@ def test_auc_radix_workspace_layout_is_aligned():
 
     for n in (0, 1, 3, 255, 256, 257, 3_000_001, 20_000_000, (1 << 31) + 7):
         off = m.auc_radix_layout(n)
-        sizes = [4 * n, 4 * n, n, n, 256 * 1024 * 4, 24]
+        sizes = [4 * n, 4 * n, n, n, 256 * 1024 * 4, 24, 256 * 4]
         assert all(o % 256 == 0 for o in off), (n, off)
-        for i in range(6):
+        for i in range(7):
             assert off[i] + sizes[i] <= off[i + 1], (n, i, off)
-        assert m.auc_radix_workspace_bytes(n) == off[6]
+        assert m.auc_radix_workspace_bytes(n) == off[7]

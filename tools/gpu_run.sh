@@ -103,6 +103,13 @@ for st in "$@"; do
       cd "$R" ;;
     gbdt)  # GBDT: 100-tree bench at the bench shape (10M raw rows -> 16M post-SMOTE)
       step gbdt 300 python tools/gbdt_bench.py --rows 10000000 --json "$OUT/gbdt.json" ;;
+    hostprof) step hostprof 300 python tools/host_profile.py --steps 30 ;;
+    cvhost) step cvhost 300 python tools/cv_probe.py --host-profile ;;
+    cvprof)  # kernel trace + timeline of one device CV job (anchor: its gathered scaler pass)
+      cd /tmp && export TMPDIR=/tmp
+      step cvprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/cvprof" -o run -- python3 "$R/tools/cv_probe.py" --runs 3
+      cd "$R"
+      python tools/timeline.py "$OUT/cvprof/run_kernel_trace.csv" --anchor "scaler_stats_cast_kernel<false, false, true>" > "$OUT/timeline_cv_job.txt" 2>&1 || true ;;
     gbdtprof)  # GBDT round kernel trace (20 trees at the bench shape)
       cd /tmp && export TMPDIR=/tmp
       step gbdtprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gbdtprof" -o run -- python3 "$R/tools/gbdt_bench.py" --rows 10000000 --trees 20

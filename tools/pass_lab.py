@@ -79,6 +79,9 @@ def main():
         "pass+reduce 1/16 grad stored-only": lambda: L._pass(m, rows, ws, 0, 0, n_st, 4.0, s, done=False, sub=16),
         "pass+reduce full grad stored-only": lambda: L._pass(m, rows, ws, 0, 0, n_st, 4.0, s, done=False, sub=1),
     })
+    # (r4: the warm-up passes on 512 / 384 / 256-block grids measured equal or slower at every
+    # sub-sample, profiles/r4_i/pass_lab.json)
+    passes["pass+reduce 1/8 H"] = lp(L.auto_warm_hess_stride(n // 8), 8)
     us = {k: round(timeit(f), 2) for k, f in passes.items()}
     nb = pipe.cfg.sgd_batches
     blocks = ref.sgd_grid_blocks(rows.shape[0], nb, out["pass_blocks"])
