@@ -15,6 +15,7 @@
 // K-index layout: MFMA step s, slot h <-> feature 16h + s, so each lane's operand for all 16
 // steps is 16 CONTIGUOUS floats of one row (four 16 B loads).
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 #include "launchers.h"
@@ -117,7 +118,7 @@ __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, i
 //     (exact score-then-index order, self/padding excluded) and the threshold becomes the k-th
 //     best of the UNION of the two half-lists of the query (lanes j and j+32), which is a valid
 //     filter for both halves and about twice as tight.
-template <int K>
+template <int K, int QF = kQFlush>
 __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict__ Q, int mq,
                                                          const float* __restrict__ C,
                                                          int mc_pad, int mc,
@@ -146,7 +147,8 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
 
   // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks.  Slot
   // kQCap - 1 is the lane's dump slot.
-  __shared__ int2 qent[kQCap * kWave];  // (score bits, candidate index) at [slot * 64 + lane]
+  constexpr int kCap = QF - 1 + 16 + 1;
+  __shared__ int2 qent[kCap * kWave];  // (score bits, candidate index) at [slot * 64 + lane]
   int qn = 0;
   auto flush = [&]() {
     for (int e = 0; __any(e < qn); ++e) {
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
     if (!__any(mx >= thr)) continue;
     const int cbase = c0 + 4 * h;
     int qe = qn * kWave + lane;                     // element of this lane's next free slot
-    const int de = (kQCap - 1) * kWave + lane;      // this lane's dump slot
+    const int de = (kCap - 1) * kWave + lane;      // this lane's dump slot
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const bool pass = acc[r] >= thr;
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
       qe += pass ? kWave : 0;
     }
     qn = (qe - lane) / kWave;
-    if (__any(qn >= kQFlush)) flush();
+    if (__any(qn >= QF)) flush();
   }
   flush();
   // merge with the other half (same query, other candidate rows); lanes h == 0 write
@@ -784,9 +786,17 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
   const dim3 grid(mq_pad / 32, nsplit);
   int* oi = nsplit > 1 ? ws_idx : out_idx;
   float* os = nsplit > 1 ? ws_score : out_score;
+  // queue flush threshold (lab knob, tools/knn_lab.py): FDX_KNN_FLUSH in {2, 4, 8, 12}
+  static const int qf = [] {
+    const char* e = std::getenv("FDX_KNN_FLUSH");
+    const int v = e ? std::atoi(e) : kQFlush;
+    return (v == 2 || v == 8 || v == 12) ? v : kQFlush;
+  }();
 #define FDX_KNN(KK)                                                                             \
-  knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi,           \
-                                                     os);                                        \
+  if (qf == 2) knn_topk_kernel<KK, 2><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
+  else if (qf == 8) knn_topk_kernel<KK, 8><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
+  else if (qf == 12) knn_topk_kernel<KK, 12><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
+  else knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {

@@ -18,8 +18,8 @@ MI355X layout (no per-fold copy of the training rows):
     positives are gathered once, fold-sorted, and each fold concatenates its four runs (~1.4 MB);
     exact k-NN among them, virtual samples (never stored);
   * fold k's validation logits come straight from the raw rows under the fit's device weights
-    (predict.hip predict_gather_logit), and its exact AUC from the native radix path -- the host
-    never waits inside the job: Newton fits after the first run with the first fold's iteration
+    (predict.hip predict_gather_logit), and its exact AUC from the sorted-positives count (the
+    fold's positive count is known on the host: no read-back) -- the host never waits inside the job: Newton fits after the first run with the first fold's iteration
     count and are verified at the end (a short prediction finishes the fit and re-scores its fold).
 """
 from __future__ import annotations
@@ -168,7 +168,9 @@ class DeviceCV:
             z = torch.empty(b1 - b0, device=dev, dtype=torch.float32)
             m.predict_gather_logit(ptr(X), ptr(perm[b0:b1]), b1 - b0, d, ptr(ws.state), ptr(stats.mean64),
                                    ptr(stats.scale64), ptr(z), s)
-            auc, _ = metric_ops.auc_radix(z, y_perm[b0:b1])
+            # the fold's positive count is known here: the sync-free sorted-positives count (~40 us)
+            # instead of the 5-pass radix sort (~240 us at 2M validation rows)
+            auc, _ = metric_ops.auc_known_positives(z, y_perm[b0:b1], pos[k])
             return z, auc
 
         fold_rows = []

@@ -37,6 +37,35 @@ def auc_radix(scores: torch.Tensor, labels: torch.Tensor):
     return auc, res
 
 
+def auc_known_positives(scores: torch.Tensor, labels: torch.Tensor, n_pos: int):
+    """Exact AUC on device with no host synchronisation when the caller knows the positive count
+    (e.g. a CV fold, whose class counts the fold assignment already produced): the positives are
+    compacted and chunk-sorted in LDS and every score counts the positives below it by binary search
+    (~N log P) -- a handful of kernels instead of the 5-pass radix sort.  Returns (auc float64 0-dim
+    device tensor, twice_pairs int64 0-dim device tensor)."""
+    _check(scores, labels)
+    n = scores.shape[0]
+    P = int(n_pos)
+    N = n - P
+    dev = scores.device
+    if P <= 0 or N <= 0:
+        return torch.full((), float("nan"), dtype=torch.float64, device=dev), torch.zeros((), dtype=torch.int64, device=dev)
+    if P > SORT_PATH_POSITIVES:
+        auc, res = auc_radix(scores, labels)
+        return auc, res[0]
+    m = native()
+    s = stream_of(scores)
+    counter = torch.zeros(1, device=dev, dtype=torch.int64)
+    pos = torch.empty(max(n, 1), device=dev, dtype=torch.float32)
+    m.auc_compact(ptr(scores), ptr(labels), n, ptr(pos), ptr(counter), s)
+    nchunks = (P + _CHUNK - 1) // _CHUNK
+    m.sort_chunks(ptr(pos), n, ptr(counter), _CHUNK, nchunks, s)
+    out = torch.zeros(1, device=dev, dtype=torch.int64)
+    m.auc_count(ptr(scores), ptr(labels), n, ptr(pos), ptr(counter), _CHUNK, nchunks, ptr(out), s)
+    twice = out[0]
+    return twice.double() / (2.0 * P * N), twice
+
+
 def _check(scores: torch.Tensor, labels: torch.Tensor):
     if scores.dtype != torch.float32 or scores.dim() != 1:
         raise ValueError("scores must be 1-D float32")

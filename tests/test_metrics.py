@@ -114,3 +114,24 @@ def test_radix_auc_small_and_degenerate(dev):
     y[::3] = 1
     auc, _ = M.auc_radix(torch.zeros(1000, device=dev), y)
     assert float(auc) == 0.5  # every pair tied
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,rate", [(2_000_003, 0.0017), (300_000, 0.05), (50_000, 0.5), (1000, 0.0)])
+def test_auc_known_positives_exact(dev, n, rate):
+    """The sync-free sorted-positives AUC (CV folds know their positive count) == sklearn, and the
+    radix path's pair count; above SORT_PATH_POSITIVES it delegates to the radix path."""
+    from sklearn.metrics import roc_auc_score
+
+    from fraud_detection_amd.ops import metrics as M
+
+    g = torch.Generator().manual_seed(n)
+    y = (torch.rand(n, generator=g) < rate).to(torch.uint8)
+    s = torch.round((torch.randn(n, generator=g) + 1.1 * y.float()) * 32) / 32  # ties
+    sd, yd = s.to(dev), y.to(dev)
+    auc, twice = M.auc_known_positives(sd, yd, int(y.sum()))
+    if 0 < int(y.sum()) < n:
+        assert float(auc) == pytest.approx(roc_auc_score(y.numpy(), s.numpy()), abs=1e-12)
+        assert int(twice) == int(M.auc_radix(sd, yd)[1][0])
+    else:
+        assert np.isnan(float(auc))

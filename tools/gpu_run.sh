@@ -64,6 +64,11 @@ for st in "$@"; do
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
+    knnflush)  # k-NN queue flush threshold sweep
+      step knnflush2 200 env FDX_KNN_FLUSH=2 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush2.json" &&
+      step knnflush4 200 env FDX_KNN_FLUSH=4 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush4.json" &&
+      step knnflush8 200 env FDX_KNN_FLUSH=8 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush8.json" &&
+      step knnflush12 200 env FDX_KNN_FLUSH=12 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush12.json" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" ;;
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
@@ -104,6 +109,11 @@ for st in "$@"; do
     gbdt)  # GBDT: 100-tree bench at the bench shape (10M raw rows -> 16M post-SMOTE)
       step gbdt 300 python tools/gbdt_bench.py --rows 10000000 --json "$OUT/gbdt.json" ;;
     hostprof) step hostprof 300 python tools/host_profile.py --steps 30 ;;
+    gapprobe)  # idle gap after kernels that store to mapped pinned memory
+      cd /tmp && export TMPDIR=/tmp
+      step gapprobe 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/gapprobe" -o run -- python3 "$R/tools/gap_probe.py"
+      cd "$R"
+      python tools/gap_probe.py --report "$OUT/gapprobe/run_kernel_trace.csv" > "$OUT/gap_probe.txt" 2>&1 || true ;;
     cvhost) step cvhost 300 python tools/cv_probe.py --host-profile ;;
     cvprof)  # kernel trace + timeline of one device CV job (anchor: its gathered scaler pass)
       cd /tmp && export TMPDIR=/tmp

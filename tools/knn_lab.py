@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
+    ap.add_argument("--splits", default="1,2,4,8,16,32")
     a = ap.parse_args()
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.ops import knn as K
@@ -39,7 +40,7 @@ def main():
     C[:, 30] = 1.0
     shapes = {"dp1_self": (C[:m1].contiguous(), C[:m1].contiguous(), 0),
               "dp8_global_rank3": (C[3 * m1: 4 * m1].contiguous(), C, 3 * m1)}
-    out = {"reps": a.reps, "shapes": {}}
+    out = {"reps": a.reps, "flush": os.environ.get("FDX_KNN_FLUSH", "4"), "shapes": {}}
 
     def timed(fn):
         for _ in range(3):
@@ -57,7 +58,7 @@ def main():
         auto = native().knn_splits((mq + 31) // 32 * 32, (mc + 31) // 32 * 32)
         ref = K.knn_topk(Q, Cc, 5, off, engine="fp32")
         rec = {"mq": mq, "mc": mc, "auto_nsplit": int(auto), "cases": []}
-        for ns in sorted({1, 2, 4, 8, 16, 32, int(auto)}):
+        for ns in sorted({int(v) for v in a.splits.split(",")} | {int(auto)}):
             f = lambda: K.knn_topk(Q, Cc, 5, off, engine="fp32", nsplit=ns)  # noqa: E731
             got = f()
             ms = timed(f)
