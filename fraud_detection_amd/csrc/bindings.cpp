@@ -712,7 +712,7 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_gbdt_bin(P<const float>(X), n, ld, d, P<const float>(cuts), P<const int>(nbins), P<uint8_t>(bins), S(s));
   });
   m.def("gbdt_grad", [](u margin, u label, int64_t n, float spw, float gscale, float hscale, u gh, u s) {
-    fdx::launch_gbdt_grad(P<const float>(margin), P<const uint8_t>(label), n, spw, gscale, hscale, P<int2>(gh), S(s));
+    fdx::launch_gbdt_grad(P<const float>(margin), P<const uint8_t>(label), n, spw, gscale, hscale, P<uint32_t>(gh), S(s));
   });
   m.def("gbdt_hist_blocks", [] { return fdx::gbdt_hist_blocks(); });
   m.def("quantile_select_ws_bytes", [](int64_t m, int d) { return fdx::quantile_select_ws_bytes(m, d); });
@@ -722,7 +722,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("gbdt_hist_slot_words", [] { return fdx::gbdt_hist_slot_words(); });
   m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u slots, u s,
                         int64_t flush_rows) {
-    fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const int2>(gh), P<const int>(ridx), P<const int64_t>(seg),
+    fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const uint32_t>(gh), P<const int>(ridx), P<const int64_t>(seg),
                           P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), P<long long>(slots), S(s),
                           flush_rows);
   }, py::arg("bins"), py::arg("gh"), py::arg("ridx"), py::arg("seg"), py::arg("gcnt"), py::arg("level"),
@@ -758,7 +758,7 @@ PYBIND11_MODULE(_fdx_native, m) {
                           float spw, float gscale, float hscale, u gh, u s) {
     fdx::launch_gbdt_margin(P<const uint8_t>(binsT), ldt, n, P<const int>(feat), P<const int>(bin),
                             P<const float>(leaf), depth, P<float>(margin), P<const uint8_t>(label), spw, gscale,
-                            hscale, P<int2>(gh), S(s));
+                            hscale, P<uint32_t>(gh), S(s));
   });
   m.def("gbdt_predict", [](u X, int64_t n, int ld, int d, u feat, u thr, u leaf, int ntrees, int depth, float base,
                            u out, u s) {

@@ -61,10 +61,12 @@ __device__ __forceinline__ bool is_built(int node, const int64_t* gcnt) {
 //    the last bin exactly as the branchy search did (!(cut > x) holds);
 //  * the LDS cut table is bin-major with a 33-float row (sc[b][f]): the 8 features a wave reads at
 //    the same search depth sit in distinct banks instead of all in bank (mid mod 64).
-// (2.78 ms -> see profiles/README.md r4 GBDT at 16M rows x 30 features)
+//  * the first three search levels compare against registers (7 cuts per feature), the last five
+//    read LDS.
+// (2.78 ms in round 3; 0.94 ms with the vector loads and the LDS-only search, profiles/r4_k)
 constexpr int kCutLd = 33;
 template <bool VEC>
-__global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__ X, int64_t n, int ld,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void gbdt_bin_kernel(const float* __restrict__ X, int64_t n, int ld,
                                                        int d, const float* __restrict__ cuts,
                                                        const int* __restrict__ nbins,
                                                        uint8_t* __restrict__ bins) {
@@ -80,6 +82,19 @@ __global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__
   int nbm1[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) nbm1[j] = snb[sub * 4 + j] - 1;
+  // the top three levels of every search from registers: the 7 cuts of the implicit tree's first
+  // three levels (indices 127 | 63, 191 | 31, 95, 159, 223) per feature, 28 VGPRs -- the dependent
+  // LDS chain is 5 reads instead of 8, and LDS traffic drops by 3/8
+  float t1[4], t2[4][2], t3[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int f = sub * 4 + j;
+    t1[j] = sc[127 * kCutLd + f];
+    t2[j][0] = sc[63 * kCutLd + f];
+    t2[j][1] = sc[191 * kCutLd + f];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) t3[j][u] = sc[(31 + 64 * u) * kCutLd + f];
+  }
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 8);
   for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 8) + (threadIdx.x >> 3); r < n; r += stride) {
     float x[4];
@@ -90,9 +105,16 @@ __global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__
 #pragma unroll
       for (int j = 0; j < 4; ++j) x[j] = (sub * 4 + j < d) ? X[r * ld + sub * 4 + j] : 0.0f;
     }
-    int b[4] = {0, 0, 0, 0};
+    int b[4];
 #pragma unroll
-    for (int half = kGBBins / 2; half >= 1; half >>= 1) {
+    for (int j = 0; j < 4; ++j) {
+      int bb = !(t1[j] > x[j]) ? 128 : 0;
+      bb += !((bb ? t2[j][1] : t2[j][0]) > x[j]) ? 64 : 0;
+      const float c3 = (bb & 128) ? ((bb & 64) ? t3[j][3] : t3[j][2]) : ((bb & 64) ? t3[j][1] : t3[j][0]);
+      b[j] = bb + (!(c3 > x[j]) ? 32 : 0);
+    }
+#pragma unroll
+    for (int half = kGBBins / 16; half >= 1; half >>= 1) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float c = sc[(b[j] + half - 1) * kCutLd + sub * 4 + j];
@@ -112,6 +134,11 @@ __global__ __launch_bounds__(256) void gbdt_bin_kernel(const float* __restrict__
 // ---- per-round gradients ---------------------------------------------------------------------
 // logistic: g = (p - y) w, h = max(p (1 - p), 1e-16) w, w = scale_pos_weight for positives.
 // fp64 so the quantised values match the numpy oracle except at measure-zero ties.
+// (g, h) of a row packed into one 32-bit word, g in the low int16 and h in the high half
+// (|g|, h <= 2^14): the histogram passes read 4 bytes of gradients per row instead of 8.
+__device__ __forceinline__ uint32_t pack_gh(int2 q) {
+  return (uint32_t)(uint16_t)(int16_t)q.x | ((uint32_t)(uint16_t)q.y << 16);
+}
 __device__ __forceinline__ int2 quantised_grad(float margin, bool pos, float spw, float gscale, float hscale) {
   const double m = (double)margin;
   const double p = 1.0 / (1.0 + exp(-m));
@@ -125,10 +152,10 @@ __device__ __forceinline__ int2 quantised_grad(float margin, bool pos, float spw
 __global__ __launch_bounds__(256) void gbdt_grad_kernel(const float* __restrict__ margin,
                                                         const uint8_t* __restrict__ label, int64_t n,
                                                         float spw, float gscale, float hscale,
-                                                        int2* __restrict__ gh) {
+                                                        uint32_t* __restrict__ gh) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
-    gh[i] = quantised_grad(margin[i], label[i] != 0, spw, gscale, hscale);
+    gh[i] = pack_gh(quantised_grad(margin[i], label[i] != 0, spw, gscale, hscale));
 }
 
 // ---- histograms ------------------------------------------------------------------------------
@@ -169,7 +196,7 @@ __device__ __forceinline__ int64_t level_chunk(const int64_t* seg, const int64_t
 }
 
 __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
-    const uint8_t* __restrict__ bins, const int2* __restrict__ gh, const int* __restrict__ ridx,
+    const uint8_t* __restrict__ bins, const uint32_t* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
     long long* __restrict__ slots, int64_t flush_rows) {
   __shared__ unsigned long long sh[kHistWords];
@@ -216,7 +243,8 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
           const int64_t row = rows[u] < 0 ? 0 : rows[u];
           const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
           const uint4 b0v = br[0], b1v = br[1];
-          const int2 q = gh[row];
+          const uint32_t w = gh[row];
+          const int2 q = make_int2((int)(int16_t)(w & 0xffffu), (int)(w >> 16));
           words[u][0] = b0v.x; words[u][1] = b0v.y; words[u][2] = b0v.z; words[u][3] = b0v.w;
           words[u][4] = b1v.x; words[u][5] = b1v.y; words[u][6] = b1v.z; words[u][7] = b1v.w;
           pk[u] = ((unsigned long long)(uint32_t)q.y << 32) + (unsigned long long)(long long)q.x;
@@ -660,7 +688,7 @@ __global__ __launch_bounds__(256) void gbdt_margin_kernel(const uint8_t* __restr
                                                           const float* __restrict__ leaf, int depth,
                                                           float* __restrict__ margin,
                                                           const uint8_t* __restrict__ label, float spw,
-                                                          float gscale, float hscale, int2* __restrict__ gh) {
+                                                          float gscale, float hscale, uint32_t* __restrict__ gh) {
   __shared__ int sf[kGBMaxNodes], sb[kGBMaxNodes];
   __shared__ float sl[kGBMaxNodes + 1];
   const int ni = heap_first(depth);
@@ -676,7 +704,7 @@ __global__ __launch_bounds__(256) void gbdt_margin_kernel(const uint8_t* __restr
     for (int l = 0; l < depth; ++l) node = 2 * node + 1 + (int)goes_right(binsT, ldt, r, node, sf, sb);
     const float m = margin[r] + sl[node - ni];
     margin[r] = m;
-    if constexpr (GRAD) gh[r] = quantised_grad(m, label[r] != 0, spw, gscale, hscale);
+    if constexpr (GRAD) gh[r] = pack_gh(quantised_grad(m, label[r] != 0, spw, gscale, hscale));
   }
 }
 
@@ -743,7 +771,7 @@ void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts
 }
 
 void launch_gbdt_grad(const float* margin, const uint8_t* label, int64_t n, float spw, float gscale,
-                      float hscale, int2* gh, hipStream_t stream) {
+                      float hscale, uint32_t* gh, hipStream_t stream) {
   const int grid = stream_grid(n, 256, 4096);
   gbdt_grad_kernel<<<grid, 256, 0, stream>>>(margin, label, n, spw, gscale, hscale, gh);
   check_launch("gbdt_grad");
@@ -763,7 +791,7 @@ int gbdt_hist_blocks() {
 
 int64_t gbdt_hist_slot_words() { return (int64_t)(gbdt_hist_blocks() + 2 * kGBMaxNodes) * kHistEntries; }
 
-void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
+void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
                       hipStream_t stream, int64_t flush_rows) {
   // flush_rows <= kFlushRows (the packed-word exactness bound); smaller values only for tests of
@@ -827,7 +855,7 @@ void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, doubl
 
 void launch_gbdt_margin(const uint8_t* binsT, int64_t ldt, int64_t n, const int* feat, const int* bin,
                         const float* leaf, int depth, float* margin, const uint8_t* label, float spw, float gscale,
-                        float hscale, int2* gh, hipStream_t stream) {
+                        float hscale, uint32_t* gh, hipStream_t stream) {
   if (depth < 1 || depth > 7) throw std::runtime_error("gbdt_margin: depth must be in [1, 7]");
   const int grid = stream_grid(n, 256, 4096);
   if (gh)

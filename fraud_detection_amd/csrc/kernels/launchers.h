@@ -286,7 +286,7 @@ void launch_kernelshap_tree(const float* Xs, int ldx, int n_expl, int d, const i
 void launch_gbdt_bin(const float* X, int64_t n, int ld, int d, const float* cuts, const int* nbins,
                      uint8_t* bins, hipStream_t stream);
 void launch_gbdt_grad(const float* margin, const uint8_t* label, int64_t n, float spw, float gscale,
-                      float hscale, int2* gh, hipStream_t stream);
+                      float hscale, uint32_t* gh, hipStream_t stream);
 int gbdt_hist_blocks();
 // exact per-feature order statistics of the cut sample (quantile.hip): out [max_bin][d] holds the
 // minimum (row 0) and the values at ranks floor(t m / max_bin); rows r * stride of X [., ld]
@@ -294,7 +294,7 @@ int64_t quantile_select_ws_bytes(int64_t m, int d);
 void launch_quantile_select(const float* X, int64_t m, int64_t stride, int ld, int d, int max_bin, void* ws,
                             float* out, hipStream_t stream);
 int64_t gbdt_hist_slot_words();  // int64 words of the per-(node, block) histogram slots
-void launch_gbdt_hist(const uint8_t* bins, const int2* gh, const int* ridx, const int64_t* seg,
+void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
                       hipStream_t stream, int64_t flush_rows = 0);
 void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
@@ -313,7 +313,7 @@ void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, doubl
                       double lambda, double min_child_weight, double eta, float* leaf, hipStream_t stream);
 void launch_gbdt_margin(const uint8_t* binsT, int64_t ldt, int64_t n, const int* feat, const int* bin,
                         const float* leaf, int depth, float* margin, const uint8_t* label, float spw, float gscale,
-                        float hscale, int2* gh, hipStream_t stream);
+                        float hscale, uint32_t* gh, hipStream_t stream);
 void launch_gbdt_predict(const float* X, int64_t n, int ld, int d, const int* feat, const float* thr,
                          const float* leaf, int ntrees, int depth, float base_margin, float* out,
                          hipStream_t stream);

@@ -167,7 +167,7 @@ HIST_FLUSH_ROWS = 0
 class _Workspace:
     def __init__(self, n: int, depth: int, dev: torch.device):
         nheap = (2 << depth) - 1
-        self.gh = torch.empty((n, 2), dtype=torch.int32, device=dev)
+        self.gh = torch.empty((n, 2), dtype=torch.int16, device=dev)  # (g, h) packed in 4 bytes
         self.ridx = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2)]
         self.nid = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.flag = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)

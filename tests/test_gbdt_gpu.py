@@ -84,7 +84,7 @@ def test_grad_kernel_matches_oracle(dev, spw):
     y = (rng.random(n) < 0.3).astype(np.uint8)
     gs, hs = R.grad_scales(spw)
     md, yd = torch.from_numpy(margin).to(dev), torch.from_numpy(y).to(dev)
-    gh = torch.empty((n, 2), dtype=torch.int32, device=dev)
+    gh = torch.empty((n, 2), dtype=torch.int16, device=dev)  # (g, h) packed per row
     native().gbdt_grad(ptr(md), ptr(yd), n, spw, gs, hs, ptr(gh), stream_of(md))
     ref = R.gradients(margin, y, spw, gs, hs)
     diff = np.abs(gh.cpu().numpy().astype(np.int64) - ref)
