@@ -15,7 +15,6 @@
 // K-index layout: MFMA step s, slot h <-> feature 16h + s, so each lane's operand for all 16
 // steps is 16 CONTIGUOUS floats of one row (four 16 B loads).
 #include <cmath>
-#include <cstdlib>
 
 #include "common.h"
 #include "launchers.h"
@@ -27,7 +26,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 constexpr int kMaxK = 8;
 constexpr float kNegBig = -3.0e38f;
-constexpr int kQFlush = 4;               // flush a wave's queues once any lane holds this many
+constexpr int kQFlush = 4;  // flush a wave's queues once any lane holds this many (2 / 8 / 12 measured
+                             // slower at both bench shapes: profiles/r4_l/knn_flush*.json)
 constexpr int kQCap = kQFlush - 1 + 16 + 1;  // + one tile's worth of appends + the dump slot
 
 __device__ __forceinline__ bool better(float s, int i, float s2, int i2) {
@@ -786,17 +786,8 @@ void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,
   const dim3 grid(mq_pad / 32, nsplit);
   int* oi = nsplit > 1 ? ws_idx : out_idx;
   float* os = nsplit > 1 ? ws_score : out_score;
-  // queue flush threshold (lab knob, tools/knn_lab.py): FDX_KNN_FLUSH in {2, 4, 8, 12}
-  static const int qf = [] {
-    const char* e = std::getenv("FDX_KNN_FLUSH");
-    const int v = e ? std::atoi(e) : kQFlush;
-    return (v == 2 || v == 8 || v == 12) ? v : kQFlush;
-  }();
 #define FDX_KNN(KK)                                                                             \
-  if (qf == 2) knn_topk_kernel<KK, 2><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
-  else if (qf == 8) knn_topk_kernel<KK, 8><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
-  else if (qf == 12) knn_topk_kernel<KK, 12><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
-  else knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
+  knn_topk_kernel<KK><<<grid, kWave, 0, stream>>>(Q, mq, C, mc_pad, mc, self_offset, oi, os); \
   if (nsplit > 1)                                                                               \
     knn_merge_kernel<KK><<<merge_blocks(mq, nsplit), 256, 0, stream>>>(ws_score, ws_idx, nsplit, merge_log2(nsplit), mq, out_idx, out_score)
   switch (k) {

@@ -64,11 +64,6 @@ for st in "$@"; do
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
-    knnflush)  # k-NN queue flush threshold sweep
-      step knnflush2 200 env FDX_KNN_FLUSH=2 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush2.json" &&
-      step knnflush4 200 env FDX_KNN_FLUSH=4 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush4.json" &&
-      step knnflush8 200 env FDX_KNN_FLUSH=8 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush8.json" &&
-      step knnflush12 200 env FDX_KNN_FLUSH=12 python tools/knn_lab.py --splits 8,16 --json "$OUT/knn_flush12.json" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" ;;
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
