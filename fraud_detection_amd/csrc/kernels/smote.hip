@@ -20,6 +20,8 @@
 // col 30 = 1 and col 31 = label, or fp8).
 #include <algorithm>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "launchers.h"
 
@@ -459,7 +461,11 @@ __global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* 
 // 2^fb picks per coarse bin: ~kTarget samples per bin for the level-2 stage, <= 16384 bins for
 // the level-1 LDS histogram, <= kFineMax picks per bin.
 int smote_bucket_fine_bits(int64_t range, int64_t n_new) {
-  constexpr double kTarget = 4096.0;
+  static const double kTarget = [] {  // lab knob (tools/bucket_lab.py): FDX_BUCKET_TARGET
+    const char* e = std::getenv("FDX_BUCKET_TARGET");
+    const double v = e ? std::atof(e) : 4096.0;
+    return v >= 256.0 && v <= 8192.0 ? v : 4096.0;
+  }();
   int fb = 0;
   while (fb < 7 && ((range + (1ll << fb) - 1) >> fb) > 16384) ++fb;
   while (fb < 7 && (double)n_new * (double)(1ll << (fb + 1)) / (double)range <= kTarget) ++fb;
