@@ -558,16 +558,16 @@ PYBIND11_MODULE(_fdx_native, m) {
      py::arg("max_iter"), py::arg("fi"), py::arg("phase_start"), py::arg("aff"), py::arg("s"), py::arg("done_host") = 0,
      py::arg("seq") = 0, py::arg("lowp") = 0);
   m.def("logreg_init", [](u state, u w32, u class_w, u done, std::vector<double> w0, double cw0, double cw1, u aff,
-                          u s) {
+                          u s, u w0_dev) {
     if (w0.size() != 32) throw std::runtime_error("logreg_init: w0 must have 32 entries");
     fdx::LRInitArgs a;
     for (int j = 0; j < 32; ++j) a.w0[j] = w0[j];
     a.cw0 = (float)cw0;
     a.cw1 = (float)cw1;
     fdx::launch_logreg_init(a, P<double>(state), P<float>(w32), P<float>(class_w), P<int>(done),
-                            P<const double>(aff), S(s));
+                            P<const double>(aff), S(s), P<const double>(w0_dev));
   }, py::arg("state"), py::arg("w32"), py::arg("class_w"), py::arg("done"), py::arg("w0"), py::arg("cw0"),
-     py::arg("cw1"), py::arg("aff"), py::arg("s"));
+     py::arg("cw1"), py::arg("aff"), py::arg("s"), py::arg("w0_dev") = 0);
   m.def("logreg_export", [](u state, u host_dev, u s) {
     fdx::launch_logreg_export(P<const double>(state), P<double>(host_dev), S(s));
   });

@@ -174,7 +174,7 @@ struct LRInitArgs {
   float cw0, cw1;
 };
 void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
-                        const double* aff, hipStream_t stream);
+                        const double* aff, hipStream_t stream, const double* w0_dev = nullptr);
 void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream);
 // Minibatch SGD step (logreg.hip sgd_apply): c = epoch step scalar (lr = c / mean curvature),
 // nb = minibatches per epoch, avg = add this step's iterate to the Polyak average, epoch_end =

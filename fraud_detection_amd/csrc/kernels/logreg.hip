@@ -1080,15 +1080,20 @@ __global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restric
 // arguments, with the affine fold of w0 when the rows are pivot-shifted -- one launch instead of
 // a pinned-staging H2D blit plus the fold kernel (a blit to/from host memory is ~9 us in the
 // step timeline, profiles/r3_f/timeline_bf16_step.txt).
+// w0_dev (nullable): the initial weights from device memory instead of the arguments -- another
+// fit's standardized-space state (a CV fold warm-started from the previous fold, stream-ordered
+// after that fit's enqueued iterations, no host round trip).
 __global__ __launch_bounds__(64) void logreg_init_kernel(LRInitArgs a, double* __restrict__ st,
                                                          float* __restrict__ w32, float* __restrict__ cw,
-                                                         int* __restrict__ done, const double* __restrict__ aff) {
+                                                         int* __restrict__ done, const double* __restrict__ aff,
+                                                         const double* __restrict__ w0_dev) {
   __shared__ double ss[kW + 32], cA[32], iA[32];
   const int t = threadIdx.x;
   double w0 = 0.0;
 #pragma unroll
   for (int j = 0; j < 32; ++j)  // static indices: no dynamic addressing of the argument struct
     if ((t & 31) == j) w0 = a.w0[j];
+  if (w0_dev != nullptr) w0 = (t & 31) == kLabelCol ? 0.0 : w0_dev[t & 31];
   if (t < 32) ss[kW + t] = w0;
 #pragma unroll
   for (int i = 0; i < kStateSize / 64; ++i) {
@@ -1456,8 +1461,8 @@ void launch_newton_update_stamped(const double* red, double* state, float* w32, 
 }
 
 void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
-                        const double* aff, hipStream_t stream) {
-  logreg_init_kernel<<<1, 64, 0, stream>>>(a, state, w32, class_w, done, aff);
+                        const double* aff, hipStream_t stream, const double* w0_dev) {
+  logreg_init_kernel<<<1, 64, 0, stream>>>(a, state, w32, class_w, done, aff, w0_dev);
   check_launch("logreg_init");
 }
 

@@ -64,10 +64,14 @@ class CVResult:
 class DeviceCV:
     """The train_model.py job (CV + final fit + AUCs) for the logistic model family on one GPU."""
 
-    def __init__(self, cfg: TrainConfig | None = None, n_folds: int = 5, seed: int = 42):
+    def __init__(self, cfg: TrainConfig | None = None, n_folds: int = 5, seed: int = 42, warm_start: bool = True):
         self.cfg = cfg or TrainConfig()
         self.n_folds = int(n_folds)
         self.seed = int(seed)
+        # Newton: every fit after the first starts from the previous fit's weights (the same convex
+        # objective up to 20% of the rows, so its optimum is near; the fit still runs to the same
+        # tolerance from there, without the progressive warm-up)
+        self.warm_start = bool(warm_start)
         self._ws: list = []
         if self.cfg.solver not in ("newton", "sgd"):
             raise ValueError("DeviceCV fits the logistic solvers (newton | sgd)")
@@ -114,13 +118,14 @@ class DeviceCV:
         if cfg.init_std > 0:
             w0[:d] = np.random.default_rng(cfg.seed).normal(0.0, cfg.init_std, d)
         fits, logits, aucs, virt_keep = [], [], [], []
-        pred = None
+        pred = {}          # full-data iterations predicted per kind of fit ("cold" | "warm")
+        used_pred = []     # the prediction each fold's fit was enqueued with
+        prev_ws = [None]
         # diagnostics (tests): the fold-sorted table and what each fit ran on
         self.rows, self.perm, self.bounds, self.stats, self.virtuals = rows, perm, bounds, stats, []
 
         def one_fit(k: int | None):
             """Fold k (None: the final fit on the whole split)."""
-            nonlocal pred
             if k is None:
                 hole, xmin = (0, 0), xpos
             else:
@@ -147,12 +152,19 @@ class DeviceCV:
                 self._ws[slot].prepare_flags()
             ws = self._ws[slot]
             if cfg.solver == "newton":
+                warm = self.warm_start and prev_ws[0] is not None
+                kind = "warm" if warm else "cold"
+                p = pred.get(kind)
                 f = lr_ops.newton_fit(rows, C=cfg.C, tol=cfg.tol, max_iter=cfg.max_iter, d=d, w0=w0, class_w=cw,
                                       fit_intercept=cfg.fit_intercept, fp8_scale=cfg.fp8_scale,
                                       check_every=cfg.check_every, workspace=ws, hess_stride=cfg.hess_stride,
-                                      affine=stats.aff, full_iters=pred, virtual=v, hole=hole)
-                if pred is None:  # the first fit ran host-checked: its count predicts the rest
-                    pred = f.full_phase_iters
+                                      affine=stats.aff, full_iters=p, virtual=v, hole=hole,
+                                      progressive=[] if warm else "auto",
+                                      w0_from=prev_ws[0].state if warm else None)
+                if p is None:  # the first fit of each kind ran host-checked: its count predicts the rest
+                    pred[kind] = p = f.full_phase_iters
+                used_pred.append(p)
+                prev_ws[0] = ws
             else:
                 f = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                    batches=cfg.sgd_batches, average=cfg.sgd_average, tol=cfg.sgd_tol, d=d, w0=w0,
@@ -187,7 +199,7 @@ class DeviceCV:
         for k, (f, ws) in enumerate(fits):
             if isinstance(f, lr_ops.PendingFit) and f.deferred:
                 f.verify()
-                if f.full_phase_iters > (pred or 0):
+                if f.full_phase_iters > used_pred[k]:
                     aucs[k] = score(k, ws)[1]
         if isinstance(f_fin, lr_ops.PendingFit):
             f_fin.verify()

@@ -291,13 +291,15 @@ class LRWorkspace:
             self._events = [torch.cuda.Event() for _ in range(depth + 1)]
             self._seq = getattr(self, "_seq", 0)
 
-    def reset(self, w0: np.ndarray, class_w=(1.0, 1.0), aff: int = 0):
+    def reset(self, w0: np.ndarray, class_w=(1.0, 1.0), aff: int = 0, w0_dev: int = 0):
         """Initial state (w0 in the padded layout, class weights, done = 0) written by ONE kernel
         whose arguments carry the values -- no pinned staging and no H2D blit.  ``aff``: device
-        address of the [64] affine map of pivot-shifted rows (w32 gets the folded weights)."""
+        address of the [64] affine map of pivot-shifted rows (w32 gets the folded weights).
+        ``w0_dev``: device address of 32 fp64 standardized-space weights that replace ``w0`` (another
+        fit's state: a warm start with no host round trip)."""
         w = np.asarray(w0, dtype=np.float64).reshape(-1)
         native().logreg_init(ptr(self.state), ptr(self.w32), ptr(self.class_w), ptr(self.done), w.tolist(),
-                             float(class_w[0]), float(class_w[1]), int(aff), stream_of(self.state))
+                             float(class_w[0]), float(class_w[1]), int(aff), stream_of(self.state), int(w0_dev))
 
 
 _BLOB_BYTES = 2304
@@ -454,7 +456,8 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
                hess_refresh: int | str = "auto", n_sched: int | None = None,
                local_warmup: bool = True, affine: torch.Tensor | None = None,
                lookahead: int | None = None, full_iters: int | None = None,
-               virtual: VirtualSmote | None = None, hole: tuple | None = None) -> FitInfo:
+               virtual: VirtualSmote | None = None, hole: tuple | None = None,
+               w0_from: torch.Tensor | None = None) -> FitInfo:
     """Full-batch Newton on device rows.  ``comm``: parallel.comm.Communicator for DP (rows are
     this rank's shard; the reduced gradient/Hessian vector is all-reduced each iteration).
     ``hess_stride``: Hessian from every k-th row tile ("auto": keep >= ~2M rows per rank);
@@ -476,7 +479,10 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     regenerated in every pass instead of stored (VirtualSmote; bf16 device rows).  Its tensors,
     like the rows, must stay alive until a deferred fit is verified.
     ``hole``: (at, len) -- the fit's rows are ``rows`` without the block [at, at + len) (a
-    cross-validation fold on the fold-sorted training table: no per-fold copy)."""
+    cross-validation fold on the fold-sorted training table: no per-fold copy).
+    ``w0_from``: another fit's device state (fp64 [>= 32], standardized-space weights first) whose
+    weights start this fit -- read by the init kernel in stream order, so it may be a fit that is
+    still enqueued (a CV fold warm-started from the previous one; device fits only)."""
     check_rows(rows)
     w0 = _default_w0(w0)
     rows, hole = _apply_hole(rows, hole)
@@ -503,7 +509,11 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
         if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
-    ws.reset(w0, class_w, aff)  # w0 is standardized-space; w32 gets it folded for shifted rows
+    if w0_from is not None and (w0_from.dtype != torch.float64 or w0_from.numel() < NCOLS
+                                or w0_from.device != rows.device):
+        raise ValueError("w0_from must be a float64 device state of >= 32 entries on the rows' device")
+    # w0 is standardized-space; w32 gets it folded for shifted rows
+    ws.reset(w0, class_w, aff, ptr(w0_from) if w0_from is not None else 0)
     n = rows.shape[0] - hole[1] + (virtual.n_new if virtual is not None else 0)
     hs = auto_hess_stride(n) if hess_stride == "auto" else max(1, int(hess_stride))
     # The warm-up schedule sets the number of collectives, so every rank must derive the same one:

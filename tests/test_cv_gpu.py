@@ -41,9 +41,9 @@ def test_device_cv_job(dev, solver, storage):
     v = cv.virtuals[k]
     w0 = np.zeros(32)
     w0[:30] = np.random.default_rng(42).normal(0.0, 0.01, 30)
-    if solver == "newton":
+    if solver == "newton":  # fold 2 warm-starts from fold 1's weights, without the warm-up phase
         g = L.newton_fit(part, tol=1e-4, max_iter=25, w0=w0, affine=cv.stats.aff, virtual=v,
-                         fp8_scale=4.0).as_fit_info()
+                         fp8_scale=4.0, progressive=[], w0_from=cv._ws[1].state).as_fit_info()
         assert g.n_iter == f.n_iter
     else:
         g = L.sgd_fit(part, w0=w0, affine=cv.stats.aff, virtual=v).as_fit_info()
@@ -54,3 +54,18 @@ def test_device_cv_job(dev, solver, storage):
     z = ((Xv - mean) / scale) @ f.w[:30] + f.w[30]
     assert abs(r.fold_aucs[k] - ref.roc_auc(z, yp[b[k]:b[k + 1]].astype(bool))) < 2e-6
     assert len(r.fold_ms) == 5 and r.final_ms > 0 and r.prep_ms > 0
+
+
+def test_device_cv_warm_start_same_models(dev):
+    """Warm-started folds (each Newton fit starts from the previous fit's weights) reach the cold
+    folds' optima: weights within the solver tolerance's reach, fold AUCs within 1e-6."""
+    X, y = separable(1_200_000, fraud_rate=0.004, seed=33, device=dev)
+    cold = DeviceCV(TrainConfig(seed=42), warm_start=False)
+    rc = cold.run(X, y)
+    warm = DeviceCV(TrainConfig(seed=42), warm_start=True)
+    rw = warm.run(X, y)
+    for fc, fw in zip(cold.fits, warm.fits):
+        assert fc.converged and fw.converged
+        np.testing.assert_allclose(fw.w[:31], fc.w[:31], atol=2e-4)
+    np.testing.assert_allclose(rw.fold_aucs, rc.fold_aucs, atol=1e-6)
+    assert max(rw.fold_iters[1:]) < min(rc.fold_iters[1:])  # fewer iterations from a warm start
