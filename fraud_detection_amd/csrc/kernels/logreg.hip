@@ -490,7 +490,7 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 // and its MFMA are those of the bf16 kernel.  Measured against the previous 4-lane fp8 kernel
 // (profiles/r3_s): gradient pass 125 -> 99 us, sub-sampled Hessian pass 137 -> 112 us over
 // 16M rows (5.2 TB/s), fp8 bench step 1.164 -> 1.099 ms.
-// VIRT: virtual SMOTE samples as in the bf16 kernel, tiles of 32 picks (2 lanes per pick).
+// VIRT: virtual SMOTE samples as in the bf16 kernel: tiles of 16 picks in its 4-lane layout, mid-loop.
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(

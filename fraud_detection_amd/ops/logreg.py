@@ -476,7 +476,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     Under DP every rank must pass the same ``full_iters`` and verify at the same point of its
     program (the iterations, and a continuation, carry the gradient all-reduces).
     ``virtual``: the fit's rows are ``rows`` followed by virtual.n_new SMOTE rows that are
-    regenerated in every pass instead of stored (VirtualSmote; bf16 device rows).  Its tensors,
+    regenerated in every pass instead of stored (VirtualSmote; bf16 or fp8 device rows).  Its tensors,
     like the rows, must stay alive until a deferred fit is verified.
     ``hole``: (at, len) -- the fit's rows are ``rows`` without the block [at, at + len) (a
     cross-validation fold on the fold-sorted training table: no per-fold copy).
