@@ -381,7 +381,7 @@ def _cv_job(X, y, Xt, yt, args, single_ms) -> dict:
                           "final_fit": round(r.final_ms, 3)},
             "fold_aucs": [round(a, 6) for a in r.fold_aucs], "cv_auc_mean": round(r.cv_auc_mean, 6),
             "test_auc": round(r.test_auc, 6), "fold_iters": r.fold_iters,
-            "includes": "fold codes + (fold,label) permutation + one gathered scaler pass, 5 x (k-NN, SMOTE "
+            "includes": "fold codes + fold permutation + one scatter-form scaler pass, 5 x (k-NN, SMOTE "
                         "buckets, fit, validation logits, exact AUC), final fit, test AUC; best of 3 wall clock"}
     return out
 

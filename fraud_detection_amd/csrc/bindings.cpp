@@ -551,12 +551,12 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_logreg_reduce(P<const float>(partial), nblocks, ncols, P<double>(out), P<const int>(done), S(s));
   });
   m.def("newton_update", [](u red, u state, u w32, u done, int d, double C, double tol, int max_iter, int fi,
-                            int phase_start, u aff, u s, u done_host, int seq, int lowp) {
+                            int phase_start, u aff, u s, u done_host, int seq) {
     fdx::launch_newton_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), d, C, tol,
-                              max_iter, fi, phase_start, P<const double>(aff), S(s), P<int>(done_host), seq, lowp);
+                              max_iter, fi, phase_start, P<const double>(aff), S(s), P<int>(done_host), seq);
   }, py::arg("red"), py::arg("state"), py::arg("w32"), py::arg("done"), py::arg("d"), py::arg("C"), py::arg("tol"),
      py::arg("max_iter"), py::arg("fi"), py::arg("phase_start"), py::arg("aff"), py::arg("s"), py::arg("done_host") = 0,
-     py::arg("seq") = 0, py::arg("lowp") = 0);
+     py::arg("seq") = 0);
   m.def("logreg_init", [](u state, u w32, u class_w, u done, std::vector<double> w0, double cw0, double cw1, u aff,
                           u s, u w0_dev) {
     if (w0.size() != 32) throw std::runtime_error("logreg_init: w0 must have 32 entries");

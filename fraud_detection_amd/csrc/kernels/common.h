@@ -108,10 +108,6 @@ __device__ __forceinline__ double rdlane(double v, int src) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-__device__ __forceinline__ float rdlane(float v, int src) {
-  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), src));
-}
-
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
 #pragma unroll

@@ -162,8 +162,7 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 // done_host (nullable): device address of a mapped pinned int that receives (seq << 1) | done
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
-                          const double* aff, hipStream_t stream, int* done_host = nullptr, int seq = 0,
-                          int lowp = 0);  // lowp: fp32 factorization (warm-up iterations)
+                          const double* aff, hipStream_t stream, int* done_host = nullptr, int seq = 0);
 // tools/newton_stamps.py: the d = 30 update with s_memtime stamps at its 7 phase boundaries
 void launch_newton_update_stamped(const double* red, double* state, float* w32, int* done, double C,
                                   const double* aff, unsigned long long* stamps, hipStream_t stream);

@@ -844,22 +844,7 @@ __device__ __forceinline__ void store_folded(const double* ss, const double* cA,
     }                                                                                             \
   } while (0)
 
-// rsqrt with one Newton refinement, per factorization precision
-__device__ __forceinline__ double rsq_refined(double x) {
-  double r = __builtin_amdgcn_rsq(x);
-  return r * fma(-0.5 * x * r, r, 1.5);
-}
-__device__ __forceinline__ float rsq_refined(float x) {
-  float r = __builtin_amdgcn_rsqf(x);
-  return r * fmaf(-0.5f * x * r, r, 1.5f);
-}
-
-// MT > 0: compile-time number of active coordinates (identity index map).  T: precision of the
-// Cholesky factorization and the triangular solves (double; float for the progressive warm-up's
-// sub-sampled iterations, whose steps only need to be descent directions -- every sum, the
-// gradient, the objective and the state stay fp64, and the full-data iterations that decide
-// convergence always factor in fp64).
-template <int MT, bool STAMP = false, typename T = double>
+template <int MT, bool STAMP = false>  // MT > 0: compile-time number of active coordinates (identity index map)
 __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
                                                            double* __restrict__ st,
                                                            float* __restrict__ w32,
@@ -875,7 +860,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   __shared__ double cA[32], iA[32], h30[32];
   __shared__ double ss[kStateSize];
   __shared__ double grad[32];
-  __shared__ T Lc[64][65];  // [column][row], padded: every lane writes/reads in bounds
+  __shared__ double Lc[64][65];  // [column][row], padded: every lane writes/reads in bounds
   __shared__ int idx[32];
   const int t = threadIdx.x;
   {
@@ -975,7 +960,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     // reusing an older H): red[34] is the weight of the rows behind H, so H * S / S_H is the
     // sample-mean Hessian at the gradient's scale.
     const double hw = sr[34] > 0.0 ? S / sr[34] : 1.0;
-    T a[32];
+    double a[32];
     {
       const int row = (MT > 0) ? (t < 32 ? t : 0) : (my >= 0 ? my : 0);
       const double* hr = sr + 64 + row * kCols;
@@ -985,13 +970,13 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         const double hv = hr[col < 0 ? 0 : col];
         const bool act = (t < m) && (k < m);
         const double dg = (k == t && my < d) ? regS : 0.0;
-        a[k] = (T)(act ? fma(hv, hw, dg) : (k == t ? 1.0 : 0.0));
+        a[k] = act ? fma(hv, hw, dg) : (k == t ? 1.0 : 0.0);
       }
     }
-    T bi = (T)((t < m) ? -grad[my < 0 ? 0 : my] * S : 0.0);
+    double bi = (t < m) ? -grad[my < 0 ? 0 : my] * S : 0.0;
     FDX_STAMP(3);
     constexpr int JE = MT > 0 ? MT : 32;
-    T dv[32];
+    double dv[32];
     // Column k of L is broadcast to the trailing update with v_readlane (L[j][k] lives in lane j:
     // an SGPR operand of the fma) instead of an LDS write + wait + read-back per column, which
     // was ~680 cycles of a 31-step dependent chain (tools/newton_stamps.py).  The forward solve
@@ -999,18 +984,19 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
       if (k < m) {
-        const T akk = fmax(rdlane(a[k], k), sizeof(T) == 8 ? (T)1e-300 : (T)1e-30);
-        const T inv = rsq_refined(akk);
+        const double akk = fmax(rdlane(a[k], k), 1e-300);
+        double inv = __builtin_amdgcn_rsq(akk);
+        inv = inv * fma(-0.5 * akk * inv, inv, 1.5);
         dv[k] = inv;
-        const T ak = (t == k) ? akk * inv : a[k] * inv;  // column k of L (rows t > k)
+        const double ak = (t == k) ? akk * inv : a[k] * inv;  // column k of L (rows t > k)
         a[k] = ak;
         Lc[k][t] = ak;  // only the back substitution reads it (column t of lane t's row)
-        const T yk = rdlane(bi, k) * inv;
+        const double yk = rdlane(bi, k) * inv;
         bi = (t == k) ? yk : (t > k ? fma(-ak, yk, bi) : bi);
 #pragma unroll
         for (int j = k + 1; j < JE; ++j) a[j] = fma(-ak, rdlane(ak, j), a[j]);
       } else {
-        dv[k] = (T)0;
+        dv[k] = 0.0;
       }
     }
     FDX_STAMP(4);
@@ -1018,8 +1004,8 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
 #pragma unroll
     for (int k = 31; k >= 0; --k) {  // L^T x = y (column sweep): lane t < k needs L[k][t] = Lc[t][k]
       if (k < m) {
-        const T xk = rdlane(bi, k) * dv[k];
-        const T lkt = Lc[t][k];
+        const double xk = rdlane(bi, k) * dv[k];
+        const double lkt = Lc[t][k];
         bi = (t == k) ? xk : (t < k ? fma(-lkt, xk, bi) : bi);
       }
     }
@@ -1030,8 +1016,8 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     }
     __syncthreads();
     if (t < m) {
-      ss[kStep + my] = (double)bi;
-      ss[kW + my] = ss[kWPrev + my] + (double)bi;
+      ss[kStep + my] = bi;
+      ss[kW + my] = ss[kWPrev + my] + bi;
     }
     if (t == 0) {
       ss[kObjPrev] = obj;
@@ -1439,17 +1425,13 @@ void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* 
 
 void launch_newton_update(const double* red, double* state, float* w32, int* done, int d,
                           double C, double tol, int max_iter, int fit_intercept, int phase_start,
-                          const double* aff, hipStream_t stream, int* done_host, int seq, int lowp) {
-#define FDX_NU(MTV, TT)                                                                              \
-  newton_update_kernel<MTV, false, TT><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, \
-                                                             fit_intercept, phase_start, aff, nullptr, done_host, seq)
-  const bool m31 = d + (fit_intercept ? 1 : 0) == 31;  // 30 features + intercept: the specialised stream
-  if (m31) {
-    if (lowp) FDX_NU(31, float); else FDX_NU(31, double);
-  } else {
-    if (lowp) FDX_NU(0, float); else FDX_NU(0, double);
-  }
-#undef FDX_NU
+                          const double* aff, hipStream_t stream, int* done_host, int seq) {
+  if (d + (fit_intercept ? 1 : 0) == 31)  // 30 features + intercept: the specialised stream
+    newton_update_kernel<31><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
+                                                   phase_start, aff, nullptr, done_host, seq);
+  else
+    newton_update_kernel<0><<<1, 64, 0, stream>>>(red, state, w32, done, d, C, tol, max_iter, fit_intercept,
+                                                  phase_start, aff, nullptr, done_host, seq);
   check_launch("newton_update");
 }
 

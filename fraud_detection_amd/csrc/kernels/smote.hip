@@ -20,8 +20,6 @@
 // col 30 = 1 and col 31 = label, or fp8).
 #include <algorithm>
 
-#include <cstdlib>
-
 #include "common.h"
 #include "launchers.h"
 
@@ -461,11 +459,9 @@ __global__ __launch_bounds__(kL2Threads) void smote_bucket_l2_kernel(const int* 
 // 2^fb picks per coarse bin: ~kTarget samples per bin for the level-2 stage, <= 16384 bins for
 // the level-1 LDS histogram, <= kFineMax picks per bin.
 int smote_bucket_fine_bits(int64_t range, int64_t n_new) {
-  static const double kTarget = [] {  // lab knob (tools/bucket_lab.py): FDX_BUCKET_TARGET
-    const char* e = std::getenv("FDX_BUCKET_TARGET");
-    const double v = e ? std::atof(e) : 4096.0;
-    return v >= 256.0 && v <= 8192.0 ? v : 4096.0;
-  }();
+  // ~4096 samples per level-2 bin: 2048 measured 117 vs 91 us for the whole sort at the bench
+  // shape (tools/bucket_lab.py, profiles/r4_m/bucket*.log)
+  constexpr double kTarget = 4096.0;
   int fb = 0;
   while (fb < 7 && ((range + (1ll << fb) - 1) >> fb) > 16384) ++fb;
   while (fb < 7 && (double)n_new * (double)(1ll << (fb + 1)) / (double)range <= kTarget) ++fb;

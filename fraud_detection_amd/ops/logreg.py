@@ -317,9 +317,6 @@ HESS_SAMPLE_ROWS = 1 << 21
 
 
 GRAD_SLOTS = 34  # red[0:32] gradient, red[32] loss, red[33] weight; red[34] = Hessian-sample weight
-# the progressive warm-up's Newton steps factor H in fp32 (logreg.hip newton_update_kernel<T>): they
-# run on 1/16 .. 1/4 row samples and only need descent directions; the full-data phase is fp64
-WARM_FP32 = True
 
 
 def auto_hess_stride(n_rows: int) -> int:
@@ -545,7 +542,7 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             if sync_warm:
                 comm.all_reduce_(ws.red)
             m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
-                            int(fit_intercept), int(j == 0), aff, s, lowp=int(WARM_FP32))
+                            int(fit_intercept), int(j == 0), aff, s)
         first[0] = 1
     if dp and local_warmup and sched:
         wv = ws.state[S_W:S_W + 32]

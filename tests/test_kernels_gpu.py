@@ -169,23 +169,6 @@ def test_newton_progressive_same_solution(dev):
     np.testing.assert_allclose(prog.w[:31], base.w[:31], atol=1e-4)
 
 
-@pytest.mark.parametrize("d", [30, 12])
-def test_newton_fp32_warmup_factorization(dev, monkeypatch, d):
-    """The warm-up steps' fp32 factorization (WARM_FP32) reaches the fp64 fit's solution with the
-    same number of iterations (the full-data phase, which decides convergence, is fp64)."""
-    X, y = _data(300_000, seed=50 + d, rate=0.02)
-    X = X[:, :d].contiguous()
-    st = S.scaler_fit(X.to(dev))
-    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev))
-    kw = dict(d=d, tol=1e-6, max_iter=30, progressive=[(8, 3), (2, 1)])
-    monkeypatch.setattr(L, "WARM_FP32", False)
-    a = L.newton_fit(rows, **kw)
-    monkeypatch.setattr(L, "WARM_FP32", True)
-    b = L.newton_fit(rows, **kw)
-    assert a.converged and b.converged and abs(a.n_iter - b.n_iter) <= 1
-    np.testing.assert_allclose(b.w[:31], a.w[:31], atol=2e-5)
-
-
 @pytest.mark.parametrize("d,fi", [(20, True), (30, False), (12, False)])
 def test_newton_generic_shapes(dev, d, fi):
     """The generic (runtime-m) Newton update kernel, beside the m = 31 specialisation."""

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Virtual-SMOTE bucket sort (smote.hip, three launches) at the bench shape: event-timed median of
-VirtualSmote.prepare() for the current FDX_BUCKET_TARGET (samples per level-2 bin).
+VirtualSmote.prepare().  (r4: swept over the level-2 bin size with a since-removed knob -- ~2048
+samples per bin 117 us, ~4096 91 us: profiles/r4_m/bucket*.log.)
 
-    FDX_BUCKET_TARGET=4096 python tools/bucket_lab.py [--reps 30]
+    python tools/bucket_lab.py [--reps 30]
 """
 import argparse
 import json
@@ -45,7 +46,7 @@ def main():
     same = bool(torch.equal(v.cnt, cnt0))  # (off: bins take their room in arrival order)
     R, n = int(v0.nbr.numel()), int(v0.n_new)
     m = native()
-    print(json.dumps({"target": os.environ.get("FDX_BUCKET_TARGET", "4096"), "picks": R, "samples": n,
+    print(json.dumps({"picks": R, "samples": n,
                       "bins": int(m.smote_bucket_bins(R, n)), "us_median": round(float(np.median(ts)), 2),
                       "counts_equal_first": same}), flush=True)
 

@@ -64,10 +64,6 @@ for st in "$@"; do
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
-    bucketlab)  # virtual-SMOTE bucket sort: samples per level-2 bin
-      step bucket2k 200 env FDX_BUCKET_TARGET=2048 python tools/bucket_lab.py &&
-      step bucket4k 200 env FDX_BUCKET_TARGET=4096 python tools/bucket_lab.py &&
-      step bucket7k 200 env FDX_BUCKET_TARGET=7168 python tools/bucket_lab.py ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" ;;
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;

@@ -93,8 +93,6 @@ def main():
     ws.red[64::33] = 1.0  # a PD Hessian diagonal for the timing run
     us["newton_update"] = round(timeit(lambda: m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done),
                                                                 30, 1.0, 0.0, 1 << 30, 1, 0, ptr(aff), s)), 2)
-    us["newton_update fp32 factorization"] = round(timeit(lambda: m.newton_update(
-        ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), 30, 1.0, 0.0, 1 << 30, 1, 0, ptr(aff), s, lowp=1)), 2)
     us["sgd_step (reduce+update)"] = round(timeit(lambda: m.sgd_step(ptr(ws.partial), blocks, ptr(ws.state), ptr(ws.w32),
                                                                       ptr(ws.done), ptr(aff), 30, 1.0, 0.0, 0.5, 1,
                                                                       nb, 0, 0, 0.0, s)), 2)
