@@ -6,15 +6,14 @@
 // merge sort, ~600 dispatches per call) does ~20x the work the cuts need.  Here the
 // order statistics come from a three-level MSD radix select over the floats' order-preserving
 // 32-bit keys (11 + 11 + 10 bits):
-//   0. qsel_keys: the strided sample as order-preserving keys, feature-major (one read of X);
 //   1. qsel_hist: per-(feature, 2048-bin top-11-bit digit) counts, LDS-private per block;
 //   2. qsel_plan (one block per feature): scan, the digit bucket and in-bucket rank of every
 //      target, and a compacted layout of just the target buckets;
 //   3. qsel_scatter: the values of target buckets are copied into their bucket's run (order inside
 //      a run is irrelevant: only values are kept, so LDS-atomic slots are fine);
-//   4. qsel_final (one block per (feature, top-digit bucket)): an LDS histogram of the next 11 bits
-//      over the bucket's run, then of the last 10 bits for all of the bucket's targets at once
-//      (one more pass per 8 distinct level-1 digits) -- the run is L2-resident.
+//   4. qsel_final (one block per (feature, target)): LDS histograms of the next 11 and the last 10
+//      bits over that target's run -- the run is small (a 1/2048-wide slice of the key space, and
+//      of the ranks for a well-spread feature) and L2-resident.
 // Every step counts exactly, so the selected values equal np.sort(sample)[rank] bit for bit (-0.0
 // is taken as +0.0, which compares equal; NaN sorts last as in numpy).
 #include "common.h"
@@ -25,6 +24,7 @@ namespace {
 
 constexpr int kQBins0 = 2048;      // level 0 / 1 digit width: 11 bits
 constexpr int kQBins2 = 1024;      // level 2: the last 10 bits
+constexpr int kQFeatGroup = 4;     // features per histogram / scatter block
 constexpr int kQChunk = 4096;      // sample rows per histogram / scatter block
 constexpr int kQThreads = 256;
 
@@ -70,29 +70,43 @@ __device__ void excl_scan(const uint32_t* h, uint32_t* pre) {
   __syncthreads();
 }
 
-// The sample's order-preserving keys, feature-major: keys[f][r] (one read of each strided sample
-// row; every later pass streams one feature's keys contiguously).
-__global__ __launch_bounds__(kQThreads) void qsel_keys_kernel(const float* __restrict__ X, int64_t m, int64_t stride,
-                                                              int ld, int d, uint32_t* __restrict__ keys) {
-  const int64_t r = (int64_t)blockIdx.x * kQThreads + threadIdx.x;
-  if (r >= m) return;
-  const float* row = X + r * stride * ld;
-  for (int f = 0; f < d; ++f) keys[(int64_t)f * m + r] = ordered_key(row[f]);
+// The bin of an NB-bin LDS histogram holding rank r (0 <= r < total) and r's rank inside it: the
+// largest bin whose exclusive prefix is <= r (it is non-empty).  Uniform: every thread gets it.
+template <int NB>
+__device__ void find_rank(const uint32_t* h, uint32_t* pre, uint32_t r, int& bin, uint32_t& rin) {
+  excl_scan<NB>(h, pre);
+  int lo = 0;
+#pragma unroll
+  for (int half = NB / 2; half >= 1; half >>= 1)
+    if (pre[lo + half] <= r) lo += half;
+  bin = lo;
+  rin = r - pre[lo];
+  __syncthreads();
 }
 
-// grid (chunks, d): the top-11-bit digit counts of one feature, LDS-private per block
-__global__ __launch_bounds__(kQThreads) void qsel_hist_kernel(const uint32_t* __restrict__ keys, int64_t m,
+__device__ __forceinline__ float sample_at(const float* X, int64_t row, int64_t stride, int ld, int f) {
+  return X[row * stride * ld + f];
+}
+
+__global__ __launch_bounds__(kQThreads) void qsel_hist_kernel(const float* __restrict__ X, int64_t m,
+                                                              int64_t stride, int ld, int d,
                                                               uint32_t* __restrict__ hist0) {
-  __shared__ uint32_t h[kQBins0];
-  const int f = blockIdx.y;
-  for (int i = threadIdx.x; i < kQBins0; i += kQThreads) h[i] = 0u;
+  __shared__ uint32_t h[kQFeatGroup][kQBins0];  // 32 KiB
+  const int f0 = blockIdx.y * kQFeatGroup;
+  for (int i = threadIdx.x; i < kQFeatGroup * kQBins0; i += kQThreads) (&h[0][0])[i] = 0u;
   __syncthreads();
-  const uint32_t* kf = keys + (int64_t)f * m;
   const int64_t r0 = (int64_t)blockIdx.x * kQChunk, r1 = min(m, r0 + kQChunk);
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += kQThreads) atomicAdd(&h[kf[r] >> 21], 1u);
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += kQThreads) {
+#pragma unroll
+    for (int j = 0; j < kQFeatGroup; ++j)
+      if (f0 + j < d) atomicAdd(&h[j][ordered_key(sample_at(X, r, stride, ld, f0 + j)) >> 21], 1u);
+  }
   __syncthreads();
-  for (int i = threadIdx.x; i < kQBins0; i += kQThreads)
-    if (h[i] != 0u) atomicAdd(hist0 + (int64_t)f * kQBins0 + i, h[i]);
+  for (int i = threadIdx.x; i < kQFeatGroup * kQBins0; i += kQThreads) {
+    const int j = i / kQBins0, b = i % kQBins0;
+    const uint32_t c = h[j][b];
+    if (c != 0u && f0 + j < d) atomicAdd(hist0 + (int64_t)(f0 + j) * kQBins0 + b, c);
+  }
 }
 
 // One block per feature.  Targets: t = 0 -> rank 0 (the minimum), t >= 1 -> floor(t m / max_bin).
@@ -134,43 +148,53 @@ __global__ __launch_bounds__(kQThreads) void qsel_plan_kernel(const uint32_t* __
   }
 }
 
-// grid (chunks, d): the keys of target buckets into their bucket's run (slots by LDS atomics: the
-// order inside a run is irrelevant, only the values are used)
-__global__ __launch_bounds__(kQThreads) void qsel_scatter_kernel(const uint32_t* __restrict__ keys, int64_t m,
+__global__ __launch_bounds__(kQThreads) void qsel_scatter_kernel(const float* __restrict__ X, int64_t m,
+                                                                 int64_t stride, int ld, int d,
                                                                  int* __restrict__ cursor,
                                                                  uint32_t* __restrict__ runs) {
-  __shared__ uint32_t cnt[kQBins0];
-  __shared__ int lbase[kQBins0];
-  const int f = blockIdx.y;
-  for (int i = threadIdx.x; i < kQBins0; i += kQThreads) {
-    cnt[i] = 0u;
-    lbase[i] = cursor[(int64_t)f * kQBins0 + i];  // -1: not a target bucket
+  __shared__ uint32_t cnt[kQFeatGroup][kQBins0];   // 32 KiB
+  __shared__ int lbase[kQFeatGroup][kQBins0];      // 32 KiB
+  const int f0 = blockIdx.y * kQFeatGroup;
+  for (int i = threadIdx.x; i < kQFeatGroup * kQBins0; i += kQThreads) {
+    const int j = i / kQBins0, b = i % kQBins0;
+    (&cnt[0][0])[i] = 0u;
+    (&lbase[0][0])[i] = f0 + j < d ? cursor[(int64_t)(f0 + j) * kQBins0 + b] : -1;  // -1: not a target
   }
   __syncthreads();
-  const uint32_t* kf = keys + (int64_t)f * m;
   const int64_t r0 = (int64_t)blockIdx.x * kQChunk, r1 = min(m, r0 + kQChunk);
   for (int64_t r = r0 + threadIdx.x; r < r1; r += kQThreads) {
-    const uint32_t b = kf[r] >> 21;
-    if (lbase[b] >= 0) atomicAdd(&cnt[b], 1u);
+#pragma unroll
+    for (int j = 0; j < kQFeatGroup; ++j) {
+      if (f0 + j >= d) continue;
+      const uint32_t b = ordered_key(sample_at(X, r, stride, ld, f0 + j)) >> 21;
+      if (lbase[j][b] >= 0) atomicAdd(&cnt[j][b], 1u);
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kQBins0; i += kQThreads) {  // this block's slice of each run it touches
-    const uint32_t c = cnt[i];
-    if (c != 0u) lbase[i] = atomicAdd(cursor + (int64_t)f * kQBins0 + i, (int)c);
-    cnt[i] = 0u;
+  // reserve this block's slice of every target run it touches
+  for (int i = threadIdx.x; i < kQFeatGroup * kQBins0; i += kQThreads) {
+    const int j = i / kQBins0, b = i % kQBins0;
+    const uint32_t c = cnt[j][b];
+    if (c != 0u) lbase[j][b] = atomicAdd(cursor + (int64_t)(f0 + j) * kQBins0 + b, (int)c);
+    cnt[j][b] = 0u;
   }
   __syncthreads();
   for (int64_t r = r0 + threadIdx.x; r < r1; r += kQThreads) {
-    const uint32_t k = kf[r], b = k >> 21;
-    const int lb = lbase[b];
-    if (lb >= 0) runs[(int64_t)f * m + lb + atomicAdd(&cnt[b], 1u)] = k;
+#pragma unroll
+    for (int j = 0; j < kQFeatGroup; ++j) {
+      if (f0 + j >= d) continue;
+      const uint32_t k = ordered_key(sample_at(X, r, stride, ld, f0 + j));
+      const uint32_t b = k >> 21;
+      const int lb = lbase[j][b];
+      if (lb >= 0) {
+        const uint32_t s = atomicAdd(&cnt[j][b], 1u);
+        runs[(int64_t)(f0 + j) * m + lb + s] = k;
+      }
+    }
   }
 }
 
-// grid (max_bin, d): the block of the FIRST target of each top-digit bucket resolves every target
-// of that bucket (a bucket holds ~10 targets for a well-spread feature) -- one level-1 histogram
-// of the run, then the last 10 bits of up to kQSlots distinct level-1 digits per pass over it.
-constexpr int kQSlots = 8;
+// One block per (target, feature): the next 11 bits, then the last 10, over the target's run.
 __global__ __launch_bounds__(kQThreads) void qsel_final_kernel(const uint32_t* __restrict__ runs, int64_t m,
                                                                int max_bin, const int* __restrict__ tdig,
                                                                const int64_t* __restrict__ trank,
@@ -179,86 +203,38 @@ __global__ __launch_bounds__(kQThreads) void qsel_final_kernel(const uint32_t* _
                                                                float* __restrict__ out) {
   __shared__ uint32_t h[kQBins0];
   __shared__ uint32_t pre[kQBins0];
-  __shared__ uint32_t h2[kQSlots][kQBins2];  // 32 KiB
-  __shared__ short smap[kQBins0];
-  __shared__ int gb1[kQThreads], gslot[kQThreads];
-  __shared__ uint32_t gr1[kQThreads];
-  __shared__ int s_g, s_nslot;
-  const int t0 = blockIdx.x, f = blockIdx.y;
-  const int base = f * kQThreads;
-  if (t0 >= max_bin) return;
-  const uint32_t top = (uint32_t)tdig[base + t0];
-  if (t0 > 0 && (uint32_t)tdig[base + t0 - 1] == top) return;  // not the bucket's first target
-  if (threadIdx.x == 0) {
-    int g = 1;
-    while (t0 + g < max_bin && (uint32_t)tdig[base + t0 + g] == top) ++g;
-    s_g = g;
-  }
+  const int t = blockIdx.x, f = blockIdx.y;
+  if (t >= max_bin) return;
+  const int ti = f * kQThreads + t;
+  const uint32_t* run = runs + (int64_t)f * m + toff[ti];
+  const int64_t n = tcnt[ti];
+  const uint32_t top = (uint32_t)tdig[ti];
+  const uint32_t r = (uint32_t)trank[ti];
   for (int i = threadIdx.x; i < kQBins0; i += kQThreads) h[i] = 0u;
   __syncthreads();
-  const int G = s_g;
-  const uint32_t* run = runs + (int64_t)f * m + toff[base + t0];
-  const int64_t n = tcnt[base + t0];
   for (int64_t i = threadIdx.x; i < n; i += kQThreads) atomicAdd(&h[(run[i] >> 10) & (kQBins0 - 1)], 1u);
   __syncthreads();
-  excl_scan<kQBins0>(h, pre);
-  if (threadIdx.x < G) {  // level-1 digit and remaining rank of each target of the bucket
-    const uint32_t r = (uint32_t)trank[base + t0 + threadIdx.x];
-    int lo = 0;
-#pragma unroll
-    for (int half = kQBins0 / 2; half >= 1; half >>= 1)
-      if (pre[lo + half] <= r) lo += half;
-    gb1[threadIdx.x] = lo;
-    gr1[threadIdx.x] = r - pre[lo];
+  int b1;
+  uint32_t r1;
+  find_rank<kQBins0>(h, pre, r, b1, r1);
+  for (int i = threadIdx.x; i < kQBins2; i += kQThreads) h[i] = 0u;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n; i += kQThreads) {
+    const uint32_t k = run[i];
+    if (((k >> 10) & (kQBins0 - 1)) == (uint32_t)b1) atomicAdd(&h[k & (kQBins2 - 1)], 1u);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {  // distinct level-1 digits (non-decreasing with the rank) -> slots
-    int ns = 0;
-    for (int i = 0; i < G; ++i) {
-      if (i > 0 && gb1[i] != gb1[i - 1]) ++ns;
-      gslot[i] = ns;
-    }
-    s_nslot = ns + 1;
-  }
-  for (int i = threadIdx.x; i < kQBins0; i += kQThreads) smap[i] = -1;
-  __syncthreads();
-  const int nslot = s_nslot;
-  for (int s0 = 0; s0 < nslot; s0 += kQSlots) {  // uniform loop
-    for (int i = threadIdx.x; i < kQSlots * kQBins2; i += kQThreads) (&h2[0][0])[i] = 0u;
-    if (threadIdx.x < G && gslot[threadIdx.x] >= s0 && gslot[threadIdx.x] < s0 + kQSlots)
-      smap[gb1[threadIdx.x]] = (short)(gslot[threadIdx.x] - s0);  // same value from equal digits
-    __syncthreads();
-    for (int64_t i = threadIdx.x; i < n; i += kQThreads) {
-      const uint32_t k = run[i];
-      const int sl = smap[(k >> 10) & (kQBins0 - 1)];
-      if (sl >= 0) atomicAdd(&h2[sl][k & (kQBins2 - 1)], 1u);
-    }
-    __syncthreads();
-    const int sn = min(kQSlots, nslot - s0);
-    for (int sl = 0; sl < sn; ++sl) {  // uniform
-      excl_scan<kQBins2>(h2[sl], pre);
-      if (threadIdx.x < G && gslot[threadIdx.x] == s0 + sl) {
-        const uint32_t r1 = gr1[threadIdx.x];
-        int lo = 0;
-#pragma unroll
-        for (int half = kQBins2 / 2; half >= 1; half >>= 1)
-          if (pre[lo + half] <= r1) lo += half;
-        out[(int64_t)(t0 + threadIdx.x) * gridDim.y + f] =
-            key_value((top << 21) | ((uint32_t)gb1[threadIdx.x] << 10) | (uint32_t)lo);
-      }
-      __syncthreads();
-    }
-    if (threadIdx.x < G && gslot[threadIdx.x] >= s0 && gslot[threadIdx.x] < s0 + kQSlots)
-      smap[gb1[threadIdx.x]] = -1;
-    __syncthreads();
-  }
+  int b2;
+  uint32_t r2;
+  find_rank<kQBins2>(h, pre, r1, b2, r2);
+  if (threadIdx.x == 0) out[(int64_t)t * gridDim.y + f] = key_value((top << 21) | ((uint32_t)b1 << 10) | (uint32_t)b2);
 }
 
 }  // namespace
 
 int64_t quantile_select_ws_bytes(int64_t m, int d) {
-  // hist0 | cursor | trank | toff | tcnt | tdig | keys | runs
-  return (int64_t)d * kQBins0 * 4 * 2 + (int64_t)d * kQThreads * (4 + 8 * 3) + 2 * (int64_t)d * m * 4 + 256;
+  // hist0 | cursor | tdig | trank | toff | tcnt | runs
+  return (int64_t)d * kQBins0 * 4 * 2 + (int64_t)d * kQThreads * (4 + 8 * 3) + (int64_t)d * m * 4 + 256;
 }
 
 void launch_quantile_select(const float* X, int64_t m, int64_t stride, int ld, int d, int max_bin, void* ws,
@@ -273,15 +249,13 @@ void launch_quantile_select(const float* X, int64_t m, int64_t stride, int ld, i
   int64_t* toff = reinterpret_cast<int64_t*>(p); p += (int64_t)d * kQThreads * 8;
   int64_t* tcnt = reinterpret_cast<int64_t*>(p); p += (int64_t)d * kQThreads * 8;
   int* tdig = reinterpret_cast<int*>(p); p += (int64_t)d * kQThreads * 4;
-  uint32_t* keys = reinterpret_cast<uint32_t*>(p); p += (int64_t)d * m * 4;
   uint32_t* runs = reinterpret_cast<uint32_t*>(p);
   if (hipMemsetAsync(hist0, 0, (size_t)d * kQBins0 * 4, stream) != hipSuccess)
     throw std::runtime_error("quantile_select: memset failed");
-  qsel_keys_kernel<<<(unsigned)((m + kQThreads - 1) / kQThreads), kQThreads, 0, stream>>>(X, m, stride, ld, d, keys);
-  const dim3 grid((unsigned)((m + kQChunk - 1) / kQChunk), (unsigned)d);
-  qsel_hist_kernel<<<grid, kQThreads, 0, stream>>>(keys, m, hist0);
+  const dim3 grid((unsigned)((m + kQChunk - 1) / kQChunk), (unsigned)((d + kQFeatGroup - 1) / kQFeatGroup));
+  qsel_hist_kernel<<<grid, kQThreads, 0, stream>>>(X, m, stride, ld, d, hist0);
   qsel_plan_kernel<<<d, kQThreads, 0, stream>>>(hist0, m, max_bin, cursor, tdig, trank, toff, tcnt);
-  qsel_scatter_kernel<<<grid, kQThreads, 0, stream>>>(keys, m, cursor, runs);
+  qsel_scatter_kernel<<<grid, kQThreads, 0, stream>>>(X, m, stride, ld, d, cursor, runs);
   qsel_final_kernel<<<dim3(max_bin, d), kQThreads, 0, stream>>>(runs, m, max_bin, tdig, trank, toff, tcnt, out);
   check_launch("quantile_select");
 }
