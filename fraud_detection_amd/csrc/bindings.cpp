@@ -736,18 +736,18 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("gbdt_transpose", [](u bins, int64_t n, int d, u binsT, int64_t ldt, u s) {
     fdx::launch_gbdt_transpose(P<const uint8_t>(bins), n, d, P<uint8_t>(binsT), ldt, S(s));
   });
-  m.def("gbdt_partition", [](u binsT, int64_t ldt, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u boff,
-                             int nblocks, u seg, u segR, u ridx_out, u nid_out, u s, u gcnt) {
+  m.def("gbdt_partition", [](u binsT, int64_t ldt, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u counts,
+                             int nblocks, u seg, u node_r, u ridx_out, u nid_out, u s, u gcnt) {
     fdx::launch_gbdt_partition(P<const uint8_t>(binsT), ldt, P<const int>(ridx), P<const uint8_t>(nid), n, P<const int>(feat),
-                               P<const int>(bin), level, P<uint8_t>(flag), P<int64_t>(boff), nblocks, P<int64_t>(seg),
-                               P<int64_t>(segR), P<int>(ridx_out), P<uint8_t>(nid_out), S(s), P<int64_t>(gcnt));
+                               P<const int>(bin), level, P<uint8_t>(flag), P<int64_t>(counts), nblocks, P<int64_t>(seg),
+                               P<int64_t>(node_r), P<int>(ridx_out), P<uint8_t>(nid_out), S(s), P<int64_t>(gcnt));
   }, py::arg("binsT"), py::arg("ldt"), py::arg("ridx"), py::arg("nid"), py::arg("n"), py::arg("feat"), py::arg("bin"),
-     py::arg("level"), py::arg("flag"), py::arg("boff"), py::arg("nblocks"), py::arg("seg"), py::arg("segR"),
+     py::arg("level"), py::arg("flag"), py::arg("counts"), py::arg("nblocks"), py::arg("seg"), py::arg("node_r"),
      py::arg("ridx_out"), py::arg("nid_out"), py::arg("s"), py::arg("gcnt") = 0);
   m.def("gbdt_round_init", [](u hist, int64_t hist_words, u seg, u gcnt, int64_t n, int64_t n_global, u ridx, u nid,
-                              u s) {
+                              u s, u node_r, int n_nodes) {
     fdx::launch_gbdt_round_init(P<unsigned long long>(hist), hist_words, P<int64_t>(seg), P<int64_t>(gcnt), n,
-                                n_global, P<int>(ridx), P<uint8_t>(nid), S(s));
+                                n_global, P<int>(ridx), P<uint8_t>(nid), S(s), P<int64_t>(node_r), n_nodes);
   });
   m.def("gbdt_leaf", [](u ng, u nh, int depth, double ginv, double hinv, double lam, double mcw, double eta, u leaf,
                         u s) {

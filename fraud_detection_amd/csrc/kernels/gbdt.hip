@@ -506,21 +506,38 @@ __global__ __launch_bounds__(256) void gbdt_transpose_kernel(const uint8_t* __re
 // 4 consecutive rows per thread per step with every load of the step issued before the first
 // use (the one-row loop was a chain of dependent load latencies: ~45 us per level at 6.4M rows)
 constexpr int kPartRows = 4;
+constexpr int kPartMaxNodes = 64;  // nodes of one partitioned level (levels <= 5 for depth <= 7)
 
+// Level partition = count + scatter, two launches.  The count pass writes the go-right flag of
+// every row, its block's right count (counts[block]) and adds each node's right count into
+// node_r[node] (one agent atomic per (block, node) present; node_r is zeroed by the round init).
+// Rows are grouped by node, so the scatter derives every segment offset from node_r alone: the
+// rights before a segment are the prefix of node_r over the earlier nodes of the level, and the
+// block's base is the prefix of counts -- no scan launch and no per-node seg launch
+// (exclusive_scan_small + gbdt_seg were 4.8 + 7.2 us plus two launch gaps per level,
+// profiles/r4_o/gbdt_kernel_stats.csv).
 __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
     const uint8_t* __restrict__ binsT, int64_t ldt, const int* __restrict__ ridx, const uint8_t* __restrict__ nid,
-    int64_t n, const int* __restrict__ feat, const int* __restrict__ bin,
-    uint8_t* __restrict__ flag, int64_t* __restrict__ counts) {
+    int64_t n, const int* __restrict__ feat, const int* __restrict__ bin, int level,
+    uint8_t* __restrict__ flag, int64_t* __restrict__ counts, int64_t* __restrict__ node_r) {
+  __shared__ int lcnt[kPartMaxNodes];
+  __shared__ int64_t red[kPartThreads / kWave];
+  const int h0 = heap_first(level), nn = 1 << level;
+  if (threadIdx.x < kPartMaxNodes) lcnt[threadIdx.x] = 0;
+  __syncthreads();
   int64_t lo, hi;
   part_range(n, &lo, &hi);
   int64_t c = 0;
+  // per-node right counts: segments are contiguous, so a thread's rows form a few runs of one node;
+  // a run's count goes to LDS when the node changes, and the last runs once per wave at the end
+  int cn = -1, cc = 0;
   for (int64_t p0 = lo + (int64_t)kPartRows * threadIdx.x; p0 < hi; p0 += (int64_t)kPartRows * kPartThreads) {
     int row[kPartRows], nd[kPartRows];
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       const bool ok = p0 + u < hi;
       row[u] = ok ? ridx[p0 + u] : 0;
-      nd[u] = ok ? (int)nid[p0 + u] : 0;
+      nd[u] = ok ? (int)nid[p0 + u] : h0;
     }
     int f[kPartRows], bv[kPartRows];
 #pragma unroll
@@ -534,14 +551,31 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       if (p0 + u < hi) {
-        const bool r = f[u] >= 0 && (int)v[u] > bv[u];
-        flag[p0 + u] = r;
+        const int r = f[u] >= 0 && (int)v[u] > bv[u];
+        flag[p0 + u] = (uint8_t)r;
         c += r;
+        if (nd[u] != cn) {
+          if (cc != 0) atomicAdd(&lcnt[cn - h0], cc);
+          cn = nd[u];
+          cc = 0;
+        }
+        cc += r;
+      }
+    }
+  }
+  {
+    const unsigned long long has = __ballot(cn >= 0);
+    if (has != 0ull) {  // wave-uniform
+      const int lead = __builtin_amdgcn_readlane(cn, __builtin_ctzll(has));
+      if (__ballot(cn >= 0 && cn != lead) == 0ull) {
+        const int s = wave_sum(cc);
+        if (lane_id() == 0 && s != 0) atomicAdd(&lcnt[lead - h0], s);
+      } else if (cc != 0) {
+        atomicAdd(&lcnt[cn - h0], cc);
       }
     }
   }
   c = wave_sum(c);
-  __shared__ int64_t red[kPartThreads / kWave];
   if (lane_id() == 0) red[wave_id()] = c;
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -549,68 +583,63 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
     for (int w = 0; w < kPartThreads / kWave; ++w) t += red[w];
     counts[blockIdx.x] = t;
   }
-}
-
-// Rights before position p (global exclusive prefix of flags), from the scanned block offsets.
-__device__ int64_t rights_before(const uint8_t* flag, const int64_t* boff, int64_t n, int nblocks,
-                                 int64_t p) {
-  const int64_t per = (n + nblocks - 1) / nblocks;
-  if (p >= n) return boff[nblocks];  // boff[nblocks] holds the total
-  const int blk = (int)(p / per);
-  // count the 0/1 flag bytes of [blk * per, p): bytes up to a 16-B boundary, then 16 B per lane
-  // per step (a byte per lane per step was up to ~100 dependent iterations: 27 us per level)
-  const int64_t a = (int64_t)blk * per;
-  const int64_t a16 = min(p, (a + 15) & ~(int64_t)15);
-  int64_t c = 0;
-  if (a + lane_id() < a16) c += flag[a + lane_id()];
-  const int64_t nv = (p - a16) >> 4;
-  const uint4* v = reinterpret_cast<const uint4*>(flag + a16);
-  for (int64_t i = lane_id(); i < nv; i += kWave) {
-    const uint4 w = v[i];
-    // bytes are 0 or 1: the byte sum of a word is (w * 0x01010101) >> 24
-    c += ((w.x * 0x01010101u) >> 24) + ((w.y * 0x01010101u) >> 24) + ((w.z * 0x01010101u) >> 24) +
-         ((w.w * 0x01010101u) >> 24);
-  }
-  for (int64_t q = a16 + (nv << 4) + lane_id(); q < p; q += kWave) c += flag[q];
-  return boff[blk] + wave_sum(c);
-}
-
-// One wave per node of the level: child segments of the next level.
-__global__ __launch_bounds__(kWave) void gbdt_seg_kernel(const uint8_t* __restrict__ flag,
-                                                         const int64_t* __restrict__ boff, int64_t n,
-                                                         int nblocks, int level,
-                                                         int64_t* __restrict__ seg,
-                                                         int64_t* __restrict__ segR,
-                                                         int64_t* __restrict__ gcnt) {
-  const int node = heap_first(level) + blockIdx.x;
-  const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
-  const int64_t r0 = rights_before(flag, boff, n, nblocks, sb);
-  const int64_t r1 = rights_before(flag, boff, n, nblocks, sb + sc);
-  if (lane_id() == 0) {
-    const int64_t nr = r1 - r0;
-    segR[node] = r0;
-    seg[2 * (2 * node + 1)] = sb;
-    seg[2 * (2 * node + 1) + 1] = sc - nr;
-    seg[2 * (2 * node + 2)] = sb + sc - nr;
-    seg[2 * (2 * node + 2) + 1] = nr;
-    if (gcnt != nullptr) {  // the children's (global, once all-reduced) row counts: no copy kernel
-      gcnt[2 * node + 1] = sc - nr;
-      gcnt[2 * node + 2] = nr;
-    }
-  }
+  if ((int)threadIdx.x < nn && lcnt[threadIdx.x] != 0)
+    __hip_atomic_fetch_add(node_r + h0 + threadIdx.x, (int64_t)lcnt[threadIdx.x], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Stable scatter of this block's range into the children's segments, kPartRows consecutive rows
 // per thread per step (one block-wide exclusive prefix of the right-going counts per 1024 rows).
+// Block 0 also writes the children's segments and (local) row counts for the next level.
 __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
-    const uint8_t* __restrict__ flag, const int64_t* __restrict__ boff, const int* __restrict__ ridx,
-    const uint8_t* __restrict__ nid, int64_t n, const int64_t* __restrict__ seg,
-    const int64_t* __restrict__ segR, int* __restrict__ ridx_out, uint8_t* __restrict__ nid_out) {
+    const uint8_t* __restrict__ flag, const int64_t* __restrict__ counts, const int* __restrict__ ridx,
+    const uint8_t* __restrict__ nid, int64_t n, int level, const int64_t* __restrict__ node_r,
+    int64_t* __restrict__ seg, int* __restrict__ ridx_out, uint8_t* __restrict__ nid_out,
+    int64_t* __restrict__ gcnt) {
+  __shared__ int wave_cnt[kPartThreads / kWave];
+  __shared__ int64_t s_red[kPartThreads / kWave];
+  __shared__ int64_t s_sb[kPartMaxNodes], s_left[kPartMaxNodes], s_rb[kPartMaxNodes];
+  const int lane = lane_id(), w = wave_id();
+  const int h0 = heap_first(level), nn = 1 << level;
+  {
+    // this block's base: rights in the rows of the earlier blocks
+    int64_t b = 0;
+    for (int i = threadIdx.x; i < (int)blockIdx.x; i += kPartThreads) b += counts[i];
+    b = wave_sum(b);
+    if (lane == 0) s_red[w] = b;
+    if (w == 0) {  // the level's node table: segment start, left-child size, rights before it
+      const int64_t nr = lane < nn ? node_r[h0 + lane] : 0;
+      int64_t incl = nr;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) {
+        const int64_t t = __shfl_up(incl, o, kWave);
+        if (lane >= o) incl += t;
+      }
+      if (lane < nn) {
+        const int node = h0 + lane;
+        const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
+        s_sb[lane] = sb;
+        s_left[lane] = sc - nr;
+        s_rb[lane] = incl - nr;
+        if (blockIdx.x == 0) {  // children of the next level (distinct heap slots from the parents)
+          seg[2 * (2 * node + 1)] = sb;
+          seg[2 * (2 * node + 1) + 1] = sc - nr;
+          seg[2 * (2 * node + 2)] = sb + sc - nr;
+          seg[2 * (2 * node + 2) + 1] = nr;
+          if (gcnt != nullptr) {  // the children's (global, once all-reduced) row counts
+            gcnt[2 * node + 1] = sc - nr;
+            gcnt[2 * node + 2] = nr;
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  int64_t base = 0;
+#pragma unroll
+  for (int i = 0; i < kPartThreads / kWave; ++i) base += s_red[i];
   int64_t lo, hi;
   part_range(n, &lo, &hi);
-  __shared__ int wave_cnt[kPartThreads / kWave];
-  int64_t base = boff[blockIdx.x];
-  const int lane = lane_id(), w = wave_id();
   for (int64_t s0 = lo; s0 < hi; s0 += (int64_t)kPartRows * kPartThreads) {
     const int64_t p0 = s0 + (int64_t)kPartRows * threadIdx.x;
     int rf[kPartRows], ri[kPartRows], nd[kPartRows];
@@ -619,7 +648,7 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
       const bool ok = p0 + u < hi;
       rf[u] = ok ? (int)flag[p0 + u] : 0;
       ri[u] = ok ? ridx[p0 + u] : 0;
-      nd[u] = ok ? (int)nid[p0 + u] : 0;
+      nd[u] = ok ? (int)nid[p0 + u] : h0;
     }
     const int cnt = rf[0] + rf[1] + rf[2] + rf[3];
     int incl = cnt;  // inclusive wave scan of the per-thread counts (thread order = row order)
@@ -641,14 +670,12 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
     for (int u = 0; u < kPartRows; ++u) {
       const int64_t p = p0 + u;
       if (p < hi) {
-        const int node = nd[u];
-        const int64_t sb = seg[2 * node], sc = seg[2 * node + 1];
-        const int64_t rin = R - segR[node];  // rights before p inside the segment
-        const int64_t nr = seg[2 * (2 * node + 2) + 1];
+        const int k = nd[u] - h0;
+        const int64_t rin = R - s_rb[k];  // rights before p inside the segment
         int64_t dst;
         uint8_t child;
-        if (rf[u]) { dst = sb + (sc - nr) + rin; child = (uint8_t)(2 * node + 2); }
-        else { dst = sb + (p - sb) - rin; child = (uint8_t)(2 * node + 1); }
+        if (rf[u]) { dst = s_sb[k] + s_left[k] + rin; child = (uint8_t)(2 * nd[u] + 2); }
+        else { dst = p - rin; child = (uint8_t)(2 * nd[u] + 1); }
         ridx_out[dst] = ri[u];
         nid_out[dst] = child;
       }
@@ -666,7 +693,8 @@ __global__ __launch_bounds__(256) void gbdt_round_init_kernel(unsigned long long
                                                               int64_t hist_words, int64_t* __restrict__ seg,
                                                               int64_t* __restrict__ gcnt, int64_t n,
                                                               int64_t n_global, int* __restrict__ ridx,
-                                                              uint8_t* __restrict__ nid) {
+                                                              uint8_t* __restrict__ nid,
+                                                              int64_t* __restrict__ node_r, int n_nodes) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t i = i0; i < hist_words; i += stride) hist[i] = 0ull;
@@ -674,6 +702,7 @@ __global__ __launch_bounds__(256) void gbdt_round_init_kernel(unsigned long long
     ridx[i] = (int)i;
     nid[i] = 0;
   }
+  if (i0 < n_nodes) node_r[i0] = 0;
   if (i0 == 0) {
     seg[0] = 0;
     seg[1] = n;
@@ -852,24 +881,25 @@ void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT
 }
 
 void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
-                           const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
-                           int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
+                           const int* feat, const int* bin, int level, uint8_t* flag, int64_t* counts,
+                           int nblocks, int64_t* seg, int64_t* node_r, int* ridx_out, uint8_t* nid_out,
                            hipStream_t stream, int64_t* gcnt) {
-  if (nblocks > 4096) throw std::runtime_error("gbdt: at most 4096 partition blocks");
-  gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(binsT, ldt, ridx, nid, n, feat, bin, flag, boff);
+  if (nblocks > 4096 || nblocks < 1) throw std::runtime_error("gbdt: 1..4096 partition blocks");
+  if (level < 0 || (1 << level) > kPartMaxNodes) throw std::runtime_error("gbdt: partition level out of range");
+  gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(binsT, ldt, ridx, nid, n, feat, bin, level, flag,
+                                                               counts, node_r);
   check_launch("gbdt_part_count");
-  launch_exclusive_scan_small(boff, nblocks, boff + nblocks, stream);
-  gbdt_seg_kernel<<<1 << level, kWave, 0, stream>>>(flag, boff, n, nblocks, level, seg, segR, gcnt);
-  check_launch("gbdt_seg");
-  gbdt_part_scatter_kernel<<<nblocks, kPartThreads, 0, stream>>>(flag, boff, ridx, nid, n, seg, segR,
-                                                                 ridx_out, nid_out);
+  gbdt_part_scatter_kernel<<<nblocks, kPartThreads, 0, stream>>>(flag, counts, ridx, nid, n, level, node_r, seg,
+                                                                 ridx_out, nid_out, gcnt);
   check_launch("gbdt_part_scatter");
 }
 
 void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
-                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream) {
+                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream, int64_t* node_r,
+                            int n_nodes) {
+  if (n_nodes > 256) throw std::runtime_error("gbdt_round_init: at most 256 nodes");
   gbdt_round_init_kernel<<<device_cu_count() * 4, 256, 0, stream>>>(hist, hist_words, seg, gcnt, n, n_global, ridx,
-                                                                    nid);
+                                                                    nid, node_r, n_nodes);
   check_launch("gbdt_round_init");
 }
 

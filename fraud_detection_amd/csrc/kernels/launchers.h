@@ -304,11 +304,13 @@ void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level,
 // row-major [n][32] bins -> feature-major [d][ldt] (the partition's per-row feature reads)
 void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT, int64_t ldt, hipStream_t stream);
 void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
-                           const int* feat, const int* bin, int level, uint8_t* flag, int64_t* boff,
-                           int nblocks, int64_t* seg, int64_t* segR, int* ridx_out, uint8_t* nid_out,
+                           const int* feat, const int* bin, int level, uint8_t* flag, int64_t* counts,
+                           int nblocks, int64_t* seg, int64_t* node_r, int* ridx_out, uint8_t* nid_out,
                            hipStream_t stream, int64_t* gcnt = nullptr);
+// node_r[0, n_nodes) (per-node right counts of the partition) is zeroed too
 void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
-                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream);
+                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream, int64_t* node_r,
+                            int n_nodes);
 void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,
                       double lambda, double min_child_weight, double eta, float* leaf, hipStream_t stream);
 void launch_gbdt_margin(const uint8_t* binsT, int64_t ldt, int64_t n, const int* feat, const int* bin,

@@ -171,9 +171,9 @@ class _Workspace:
         self.ridx = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(2)]
         self.nid = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
         self.flag = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
-        self.boff = torch.empty(PART_BLOCKS + 1, dtype=torch.int64, device=dev)
+        self.counts = torch.empty(PART_BLOCKS, dtype=torch.int64, device=dev)  # right rows per partition block
         self.seg = torch.zeros((nheap, 2), dtype=torch.int64, device=dev)
-        self.segR = torch.zeros(nheap, dtype=torch.int64, device=dev)
+        self.node_r = torch.zeros(nheap, dtype=torch.int64, device=dev)  # right rows per node (zeroed per round)
         self.gcnt = torch.zeros(nheap, dtype=torch.int64, device=dev)
         self.hist = torch.zeros(((1 << depth) - 1) * HIST_ENTRIES, dtype=torch.int64, device=dev)
         # per-(node, block) histogram slots the histogram kernel writes without atomics
@@ -296,7 +296,7 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
         # zero histograms, root segment + global count, ridx = iota, nid = root: one launch
         m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n, n_global,
-                          ptr(ws.ridx[0]), ptr(ws.nid[0]), st)
+                          ptr(ws.ridx[0]), ptr(ws.nid[0]), st, ptr(ws.node_r), ws.node_r.numel())
         cur = 0
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
@@ -309,9 +309,9 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             if level == D - 1:
                 break  # leaves: the margin walk and gbdt_leaf (split-kernel child sums) need no partition
             if n:
-                # the seg kernel also writes the children's counts into gcnt (no copy launch)
+                # count + scatter; the scatter also writes the children's segments and counts (gcnt)
                 m.gbdt_partition(ptr(binsT), ldt, ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
-                                 level, ptr(ws.flag), ptr(ws.boff), PART_BLOCKS, ptr(ws.seg), ptr(ws.segR),
+                                 level, ptr(ws.flag), ptr(ws.counts), PART_BLOCKS, ptr(ws.seg), ptr(ws.node_r),
                                  ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st, ptr(ws.gcnt))
             cur ^= 1
             c0 = 2 * h0 + 1

@@ -91,7 +91,7 @@ def test_grad_kernel_matches_oracle(dev, spw):
     assert diff.max() <= 1 and (diff > 0).mean() < 1e-3
 
 
-@pytest.mark.parametrize("n,d,depth", [(60_000, 30, 5), (5_000, 7, 3), (777, 4, 6)])
+@pytest.mark.parametrize("n,d,depth", [(60_000, 30, 5), (5_000, 7, 3), (777, 4, 6), (3_000, 5, 7)])
 def test_first_tree_exact(dev, n, d, depth):
     """Round 1 (margin 0 -> exactly representable gradients): the device tree equals the oracle."""
     Xd, yd, X, y = _data(n, d, seed=n)
