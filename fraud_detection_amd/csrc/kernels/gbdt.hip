@@ -366,26 +366,34 @@ __global__ __launch_bounds__(kHistThreads) void gbdt_split_kernel(
   const int lane = lane_id(), wv = wave_id();
   constexpr int kW = kHistThreads / kWave;
   long long* H = reinterpret_cast<long long*>(hist) + (int64_t)node * kHistEntries;
-  const int nent = d * kGBBins * 2;
-  if (!is_built(node, gcnt)) {  // exact sibling subtraction: H = parent - built sibling
-    const int parent = (node - 1) >> 1;
-    const int sib = (node & 1) ? node + 1 : node - 1;
-    const long long* P = reinterpret_cast<long long*>(hist) + (int64_t)parent * kHistEntries;
-    const long long* S = reinterpret_cast<long long*>(hist) + (int64_t)sib * kHistEntries;
-    for (int i = threadIdx.x; i < nent; i += kHistThreads) H[i] = P[i] - S[i];
-    __syncthreads();
-  }
+  // A node that was not histogrammed gets the exact sibling subtraction H = parent - built
+  // sibling, computed by the wave that scans the feature (every feature has exactly one wave) and
+  // stored for the children's subtraction -- no block-wide pass + barrier + re-read of H.
+  const bool derived = !is_built(node, gcnt);
+  const int parent = derived ? (node - 1) >> 1 : node, sib = derived ? ((node & 1) ? node + 1 : node - 1) : node;
+  const long long* P = reinterpret_cast<long long*>(hist) + (int64_t)parent * kHistEntries;
+  const long long* S = reinterpret_cast<long long*>(hist) + (int64_t)sib * kHistEntries;
   __shared__ double fgain[32];
   __shared__ int fbin[32];
   __shared__ long long fgl[32], fhl[32];
   __shared__ long long tot[2];
   for (int f = wv; f < d; f += kW) {
-    const long long* hf = H + f * kGBBins * 2;
+    const int e0 = f * kGBBins * 2 + lane * 8;  // this lane's 4 bins x (g, h)
     long long g[4], h[4];
+    if (derived) {
+      long long pv[8], sv[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      g[j] = hf[(lane * 4 + j) * 2];
-      h[j] = hf[(lane * 4 + j) * 2 + 1];
+      for (int j = 0; j < 8; ++j) { pv[j] = P[e0 + j]; sv[j] = S[e0 + j]; }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) H[e0 + j] = pv[j] - sv[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { g[j] = pv[2 * j] - sv[2 * j]; h[j] = pv[2 * j + 1] - sv[2 * j + 1]; }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        g[j] = H[e0 + 2 * j];
+        h[j] = H[e0 + 2 * j + 1];
+      }
     }
 #pragma unroll
     for (int j = 1; j < 4; ++j) { g[j] += g[j - 1]; h[j] += h[j - 1]; }
