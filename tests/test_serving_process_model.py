@@ -210,8 +210,10 @@ def test_gpu_owner_in_process_batches(dev, loop, monkeypatch):
     eng = _engine("cuda")
     assert eng.calibration.get("source") in ("measured", "FDX_HOST_MAX_ROWS")
     # the launch path's batching (the persistent mailbox path answers single rows too fast to
-    # batch them: test_native_owner_persistent_kernel)
-    owner = GpuOwner(eng, "", persist_rows=0).start()
+    # batch them: test_native_owner_persistent_kernel).  A 200 us collection window makes the
+    # coalescing of the 32 concurrent producers deterministic: with no window a fast owner can
+    # drain the ring one request at a time (600 batches for 600 requests on one r4 box).
+    owner = GpuOwner(eng, "", persist_rows=0, window_us=200.0).start()
     try:
         disp = Dispatcher(eng, RingClient(owner.ring), host_max_rows=0)
         rows = kaggle_like_rows(600, seed=12)
