@@ -96,10 +96,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void g
     for (int u = 0; u < 4; ++u) t3[j][u] = sc[(31 + 64 * u) * kCutLd + f];
   }
   const int64_t stride = (int64_t)gridDim.x * (blockDim.x / 8);
-  for (int64_t r = (int64_t)blockIdx.x * (blockDim.x / 8) + (threadIdx.x >> 3); r < n; r += stride) {
+  const int64_t r0 = (int64_t)blockIdx.x * (blockDim.x / 8) + (threadIdx.x >> 3);
+  // VEC: the rows of the next two iterations are in flight while this one is searched -- the
+  // grid is resident-capped (16 waves per CU), and with one 16-byte load per lane outstanding the
+  // whole chip kept ~4 MB in flight, ~2.9 TB/s (0.87 ms at 16M rows, profiles/r4_q; 0.79 ms with
+  // the two-deep prefetch, profiles/r4_v)
+  const float4 zero4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  float4 pf0 = zero4, pf1 = zero4;
+  if constexpr (VEC) {
+    if (r0 < n) pf0 = reinterpret_cast<const float4*>(X + r0 * ld)[sub];
+    if (r0 + stride < n) pf1 = reinterpret_cast<const float4*>(X + (r0 + stride) * ld)[sub];
+  }
+  for (int64_t r = r0; r < n; r += stride) {
     float x[4];
     if constexpr (VEC) {
-      const float4 v = reinterpret_cast<const float4*>(X + r * ld)[sub];
+      const float4 v = pf0;
+      pf0 = pf1;
+      if (r + 2 * stride < n) pf1 = reinterpret_cast<const float4*>(X + (r + 2 * stride) * ld)[sub];
       x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
     } else {
 #pragma unroll
