@@ -552,23 +552,39 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
   // per-node right counts: segments are contiguous, so a thread's rows form a few runs of one node;
   // a run's count goes to LDS when the node changes, and the last runs once per wave at the end
   int cn = -1, cc = 0;
-  for (int64_t p0 = lo + (int64_t)kPartRows * threadIdx.x; p0 < hi; p0 += (int64_t)kPartRows * kPartThreads) {
-    int row[kPartRows], nd[kPartRows];
+  // software pipeline over the thread's steps: the row indices / node ids of step i+1 and then
+  // their split feature / bin are loaded while the bins gather of step i is in flight (the
+  // unpipelined loop paid ridx -> feat -> binsT -> flag as three dependent round trips per step)
+  const int64_t step = (int64_t)kPartRows * kPartThreads;
+  int row[kPartRows], nd[kPartRows], f[kPartRows], bv[kPartRows];
+  auto load_ids = [&](int64_t p, int* rw, int* ndv) {
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
-      const bool ok = p0 + u < hi;
-      row[u] = ok ? ridx[p0 + u] : 0;
-      nd[u] = ok ? (int)nid[p0 + u] : h0;
+      const bool ok = p + u < hi;
+      rw[u] = ok ? ridx[p + u] : 0;
+      ndv[u] = ok ? (int)nid[p + u] : h0;
     }
-    int f[kPartRows], bv[kPartRows];
+  };
+  auto load_split = [&](const int* ndv, int* fv, int* bvv) {
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
-      f[u] = feat[nd[u]];
-      bv[u] = bin[nd[u]];
+      fv[u] = feat[ndv[u]];
+      bvv[u] = bin[ndv[u]];
     }
+  };
+  int64_t p0 = lo + (int64_t)kPartRows * threadIdx.x;
+  if (p0 < hi) {
+    load_ids(p0, row, nd);
+    load_split(nd, f, bv);
+  }
+  for (; p0 < hi; p0 += step) {
+    int rowN[kPartRows], ndN[kPartRows], fN[kPartRows], bvN[kPartRows];
+    const bool more = p0 + step < hi;
+    if (more) load_ids(p0 + step, rowN, ndN);
     uint8_t v[kPartRows];
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) v[u] = f[u] >= 0 ? binsT[(int64_t)f[u] * ldt + row[u]] : 0;
+    if (more) load_split(ndN, fN, bvN);
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       if (p0 + u < hi) {
@@ -581,6 +597,15 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
           cc = 0;
         }
         cc += r;
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < kPartRows; ++u) {
+        row[u] = rowN[u];
+        nd[u] = ndN[u];
+        f[u] = fN[u];
+        bv[u] = bvN[u];
       }
     }
   }
@@ -661,16 +686,25 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
   for (int i = 0; i < kPartThreads / kWave; ++i) base += s_red[i];
   int64_t lo, hi;
   part_range(n, &lo, &hi);
-  for (int64_t s0 = lo; s0 < hi; s0 += (int64_t)kPartRows * kPartThreads) {
-    const int64_t p0 = s0 + (int64_t)kPartRows * threadIdx.x;
-    int rf[kPartRows], ri[kPartRows], nd[kPartRows];
+  // the next step's flags / row indices / node ids are loaded while this step is scanned and
+  // scattered
+  const int64_t step = (int64_t)kPartRows * kPartThreads;
+  int rf[kPartRows], ri[kPartRows], nd[kPartRows];
+  auto load_step = [&](int64_t p0, int* rfv, int* riv, int* ndv) {
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       const bool ok = p0 + u < hi;
-      rf[u] = ok ? (int)flag[p0 + u] : 0;
-      ri[u] = ok ? ridx[p0 + u] : 0;
-      nd[u] = ok ? (int)nid[p0 + u] : h0;
+      rfv[u] = ok ? (int)flag[p0 + u] : 0;
+      riv[u] = ok ? ridx[p0 + u] : 0;
+      ndv[u] = ok ? (int)nid[p0 + u] : h0;
     }
+  };
+  if (lo < hi) load_step(lo + (int64_t)kPartRows * threadIdx.x, rf, ri, nd);
+  for (int64_t s0 = lo; s0 < hi; s0 += step) {  // block-uniform trip count (barriers inside)
+    const int64_t p0 = s0 + (int64_t)kPartRows * threadIdx.x;
+    int rfN[kPartRows], riN[kPartRows], ndN[kPartRows];
+    const bool more = s0 + step < hi;
+    if (more) load_step(p0 + step, rfN, riN, ndN);
     const int cnt = rf[0] + rf[1] + rf[2] + rf[3];
     int incl = cnt;  // inclusive wave scan of the per-thread counts (thread order = row order)
 #pragma unroll
@@ -703,6 +737,14 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
       R += rf[u];
     }
     base += total;
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < kPartRows; ++u) {
+        rf[u] = rfN[u];
+        ri[u] = riN[u];
+        nd[u] = ndN[u];
+      }
+    }
     __syncthreads();
   }
 }

@@ -19,7 +19,7 @@ from .native import native, ptr, stream_of
 MAX_BIN = R.MAX_BIN
 MAX_FEAT = 30
 HIST_ENTRIES = MAX_FEAT * MAX_BIN * 2
-PART_BLOCKS = 1024
+PART_BLOCKS = int(os.environ.get("FDX_GBDT_PART_BLOCKS", "1024"))  # partition grid (<= 4096)
 
 
 @dataclass
