@@ -354,6 +354,8 @@ __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const long long* 
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= d * kGBBins * 2) return;
   long long acc = 0;
+  // 8 slot loads in flight per lane (a load -> wait -> add chain per slot otherwise)
+#pragma unroll 8
   for (int j = blockIdx.y; j < cnt; j += split) acc += slots[(int64_t)(base + j) * kHistEntries + e];
   if (acc) atomicAdd(hist + (int64_t)(h0 + kk) * kHistEntries + e, (unsigned long long)acc);
 }
