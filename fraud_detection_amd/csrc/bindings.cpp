@@ -744,10 +744,10 @@ PYBIND11_MODULE(_fdx_native, m) {
   }, py::arg("binsT"), py::arg("ldt"), py::arg("ridx"), py::arg("nid"), py::arg("n"), py::arg("feat"), py::arg("bin"),
      py::arg("level"), py::arg("flag"), py::arg("counts"), py::arg("nblocks"), py::arg("seg"), py::arg("node_r"),
      py::arg("ridx_out"), py::arg("nid_out"), py::arg("s"), py::arg("gcnt") = 0);
-  m.def("gbdt_round_init", [](u hist, int64_t hist_words, u seg, u gcnt, int64_t n, int64_t n_global, u ridx, u nid,
-                              u s, u node_r, int n_nodes) {
+  m.def("gbdt_round_init", [](u hist, int64_t hist_words, u seg, u gcnt, int64_t n, int64_t n_global, u s,
+                              u node_r, int n_nodes) {
     fdx::launch_gbdt_round_init(P<unsigned long long>(hist), hist_words, P<int64_t>(seg), P<int64_t>(gcnt), n,
-                                n_global, P<int>(ridx), P<uint8_t>(nid), S(s), P<int64_t>(node_r), n_nodes);
+                                n_global, S(s), P<int64_t>(node_r), n_nodes);
   });
   m.def("gbdt_leaf", [](u ng, u nh, int depth, double ginv, double hinv, double lam, double mcw, double eta, u leaf,
                         u s) {

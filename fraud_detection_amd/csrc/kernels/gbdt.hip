@@ -559,12 +559,13 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
   // unpipelined loop paid ridx -> feat -> binsT -> flag as three dependent round trips per step)
   const int64_t step = (int64_t)kPartRows * kPartThreads;
   int row[kPartRows], nd[kPartRows], f[kPartRows], bv[kPartRows];
+  // level 0: every row is in the root in row order -- ridx / nid are not read (nor initialised)
   auto load_ids = [&](int64_t p, int* rw, int* ndv) {
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       const bool ok = p + u < hi;
-      rw[u] = ok ? ridx[p + u] : 0;
-      ndv[u] = ok ? (int)nid[p + u] : h0;
+      rw[u] = !ok ? 0 : (level == 0 ? (int)(p + u) : ridx[p + u]);
+      ndv[u] = (ok && level != 0) ? (int)nid[p + u] : h0;
     }
   };
   auto load_split = [&](const int* ndv, int* fv, int* bvv) {
@@ -697,8 +698,8 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
     for (int u = 0; u < kPartRows; ++u) {
       const bool ok = p0 + u < hi;
       rfv[u] = ok ? (int)flag[p0 + u] : 0;
-      riv[u] = ok ? ridx[p0 + u] : 0;
-      ndv[u] = ok ? (int)nid[p0 + u] : h0;
+      riv[u] = !ok ? 0 : (level == 0 ? (int)(p0 + u) : ridx[p0 + u]);  // level 0: identity
+      ndv[u] = (ok && level != 0) ? (int)nid[p0 + u] : h0;
     }
   };
   if (lo < hi) load_step(lo + (int64_t)kPartRows * threadIdx.x, rf, ri, nd);
@@ -753,20 +754,17 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
 
 // ---- per-round state -------------------------------------------------------------------------
 // One launch instead of five torch fills/copies at the start of every boosting round: zero the
-// level histograms, root segment [0, n) and its global count, ridx = 0..n-1, nid = 0 (root).
+// level histograms and per-node right counts, root segment [0, n) and its global count.  ridx /
+// nid are not filled: level 0 (histogram and partition) takes row p = position p in the root,
+// which saved the 80 MB iota / root fill at 16M rows (profiles/r4_z).
 __global__ __launch_bounds__(256) void gbdt_round_init_kernel(unsigned long long* __restrict__ hist,
                                                               int64_t hist_words, int64_t* __restrict__ seg,
                                                               int64_t* __restrict__ gcnt, int64_t n,
-                                                              int64_t n_global, int* __restrict__ ridx,
-                                                              uint8_t* __restrict__ nid,
+                                                              int64_t n_global,
                                                               int64_t* __restrict__ node_r, int n_nodes) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   for (int64_t i = i0; i < hist_words; i += stride) hist[i] = 0ull;
-  for (int64_t i = i0; i < n; i += stride) {
-    ridx[i] = (int)i;
-    nid[i] = 0;
-  }
   if (i0 < n_nodes) node_r[i0] = 0;
   if (i0 == 0) {
     seg[0] = 0;
@@ -960,11 +958,10 @@ void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, c
 }
 
 void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
-                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream, int64_t* node_r,
-                            int n_nodes) {
+                            int64_t n_global, hipStream_t stream, int64_t* node_r, int n_nodes) {
   if (n_nodes > 256) throw std::runtime_error("gbdt_round_init: at most 256 nodes");
-  gbdt_round_init_kernel<<<device_cu_count() * 4, 256, 0, stream>>>(hist, hist_words, seg, gcnt, n, n_global, ridx,
-                                                                    nid, node_r, n_nodes);
+  gbdt_round_init_kernel<<<device_cu_count() * 4, 256, 0, stream>>>(hist, hist_words, seg, gcnt, n, n_global, node_r,
+                                                                    n_nodes);
   check_launch("gbdt_round_init");
 }
 

@@ -309,8 +309,7 @@ void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, c
                            hipStream_t stream, int64_t* gcnt = nullptr);
 // node_r[0, n_nodes) (per-node right counts of the partition) is zeroed too
 void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
-                            int64_t n_global, int* ridx, uint8_t* nid, hipStream_t stream, int64_t* node_r,
-                            int n_nodes);
+                            int64_t n_global, hipStream_t stream, int64_t* node_r, int n_nodes);
 void launch_gbdt_leaf(const long long* ng, const long long* nh, int depth, double ginv, double hinv,
                       double lambda, double min_child_weight, double eta, float* leaf, hipStream_t stream);
 void launch_gbdt_margin(const uint8_t* binsT, int64_t ldt, int64_t n, const int* feat, const int* bin,

@@ -294,9 +294,10 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         st = stream_of(X)  # the capture stream while a hipGraph is being recorded
         if grad_first:
             m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
-        # zero histograms, root segment + global count, ridx = iota, nid = root: one launch
-        m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n, n_global,
-                          ptr(ws.ridx[0]), ptr(ws.nid[0]), st, ptr(ws.node_r), ws.node_r.numel())
+        # zero histograms and per-node counts, root segment + global count: one launch (level 0
+        # reads rows in order, so ridx / nid need no iota / root fill)
+        m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n, n_global, st,
+                          ptr(ws.node_r), ws.node_r.numel())
         cur = 0
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
