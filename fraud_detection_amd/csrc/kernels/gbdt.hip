@@ -319,7 +319,7 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
   }
 }
 
-// Sum each built node's slots into its histogram: grid (entries / 256, kSlotSplit, 2^level).
+// Sum each built node's slots into its histogram: grid (entries / 256, kSlotSplit, sibling pairs).
 __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const long long* __restrict__ slots,
                                                                const int64_t* __restrict__ seg,
                                                                const int64_t* __restrict__ gcnt, int level,
@@ -331,7 +331,8 @@ __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const long long* 
   int64_t total;
   const int64_t chunk = level_chunk(lv, level, hist_blocks, &total);
   if (total == 0) return;
-  const int kk = blockIdx.z;
+  // blockIdx.z = sibling pair: exactly one node of each pair is histogrammed (level 0: the root)
+  const int kk = level == 0 ? 0 : (built_l(lv, level, 2 * (int)blockIdx.z) ? 2 * (int)blockIdx.z : 2 * (int)blockIdx.z + 1);
   int64_t off = 0;
   int base = 0, cnt = 0;
   bool mine = false;
@@ -351,7 +352,7 @@ __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const long long* 
   // split costs one int64 device atomic per entry).  With >= 8 slots per split the level-4 reduce
   // ran 43.9 us, with >= 32 41.9 (profiles/r4_z, r4_aa) against 13 us at level 0 for the same
   // bytes: the rest is the 60 x 16 x 16 grid, every block staging the node table before it can
-  // tell that it has no slots.
+  // tell that it has no slots -- z now runs over sibling pairs, not nodes: 26.4 us (profiles/r4_ab).
   const int split = min(kSlotSplit, (cnt + 31) / 32);
   if (!mine || cnt == 0 || (int)blockIdx.y >= split) return;
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -924,7 +925,7 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   const int nb = gbdt_hist_blocks();
   gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows);
   check_launch("gbdt_hist");
-  const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, 1u << level);
+  const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, level == 0 ? 1u : 1u << (level - 1));
   gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, nb, hist);
   check_launch("gbdt_hist_reduce");
 }
