@@ -90,7 +90,14 @@ PYBIND11_MODULE(_fdx_ring, m) {
         return o;
       })
       .def("debug_take_tickets", &Ring::debug_take_tickets, py::arg("n"),
-           "take n tickets without publishing them (simulates a producer that died mid-request)");
+           "take n tickets without publishing them (simulates a producer that died mid-request)")
+      .def("debug_publish",
+           [](Ring& r, py::array_t<float, py::array::c_style | py::array::forcecast> X, uint32_t op) {
+             if (X.ndim() != 2 || (uint32_t)X.shape(1) != r.d()) throw std::runtime_error("ring: X must be [n, d]");
+             return r.debug_publish(X.data(), (uint32_t)X.shape(0), op);
+           },
+           py::arg("X"), py::arg("op") = 0,
+           "publish rows and never consume the results (simulates a producer killed while waiting)");
   // Native load generator (tools/serve_latency.py): `threads` C++ producer threads, each issuing
   // `per_thread` synchronous requests of `rows` rows -- the owner's capacity without a Python
   // producer's interpreter in the measurement.  -> (elapsed seconds, per-request latencies in us)

@@ -275,6 +275,25 @@ class Ring {
   // Test hook: take n tickets and never publish them -- a producer that died right after its
   // head.fetch_add (tests/test_ring_abandon.py drills the owner's reclaim with it).
   uint64_t debug_take_tickets(uint32_t n) { return h_->head.fetch_add(n); }
+  // Test hook: take tickets, publish n rows and return without waiting for (or ever consuming) the
+  // results -- a producer killed while it waited for them (its slots end at (t, DONE)).
+  uint64_t debug_publish(const float* X, uint32_t n, uint32_t op) {
+    const uint32_t R = h_->slot_rows, d = h_->d, N = h_->nslots;
+    const uint32_t nchunks = (n + R - 1) / R;
+    uint64_t t0 = 0;
+    if (nchunks == 0 || nchunks > N || !try_take(nchunks, t0)) throw std::runtime_error("ring: no room to publish");
+    for (uint32_t c = 0; c < nchunks; ++c) {
+      const uint64_t t = t0 + c;
+      Slot& s = slots_[t % N];
+      const uint32_t m = std::min(R, n - c * R);
+      std::memcpy(in_ptr(t % N), X + (size_t)c * R * d, (size_t)m * d * 4);
+      s.n_rows = m;
+      s.op = op;
+      s.tag.store(tag_of(t, READY), std::memory_order_release);
+    }
+    ring_doorbell();
+    return t0;
+  }
   // Test hook: (turn, state) of every slot plus (head, tail).
   std::vector<uint64_t> debug_tags() const {
     std::vector<uint64_t> v;
@@ -302,7 +321,7 @@ class Ring {
       h_->tail.store(t, std::memory_order_release);
       return {0, 0};
     }
-    const uint32_t op = slots_[t % N].op;
+    uint32_t op = slots_[t % N].op;
     uint32_t rows = 0;
     const uint64_t wdl = now_ns() + (uint64_t)(window_us * 1e3);
     while (true) {
@@ -310,6 +329,11 @@ class Ring {
       const uint64_t g = s.tag.load(std::memory_order_acquire);
       if (g != tag_of(t, READY)) {
         if (skip_dead(t)) continue;
+        if (rows == 0) {  // the first READY slot was cancelled under us: wait again, within the deadline
+          if (!wait_ready(t, deadline, timeout_ms > 0)) break;
+          op = slots_[t % N].op;
+          continue;
+        }
         if (rows > 0 && now_ns() >= wdl) break;
         if (h_->head.load(std::memory_order_acquire) <= t && now_ns() >= wdl) break;
         if (window_us <= 0 && rows > 0) break;
@@ -500,7 +524,11 @@ class Ring {
       }
       return false;
     }
-    if (h_->head.load(std::memory_order_acquire) <= t || (turn == t && st == READY)) {
+    // The previous lap of slot t % N never freed (its producer died or hung after DONE / FAILED, or
+    // cancelled a slot nobody freed): try_take needs (t, FREE) there, so head can never pass t --
+    // this case must run the stall clock even when no producer holds ticket t yet.
+    const bool lap_unfreed = turn + N == t && (st == DONE || st == FAILED || st == CANCELLED);
+    if ((h_->head.load(std::memory_order_acquire) <= t && !lap_unfreed) || (turn == t && st == READY)) {
       stuck_t_ = ~0ull;
       return false;
     }
@@ -520,7 +548,7 @@ class Ring {
         wake_producers();
         return true;
       }
-    } else if (turn + N == t && (st == DONE || st == FAILED || st == CANCELLED)) {  // previous lap never freed
+    } else if (lap_unfreed) {  // previous lap never freed
       if (s.tag.compare_exchange_strong(g, tag_of(t, FREE), std::memory_order_acq_rel)) {
         h_->reclaimed.fetch_add(1);
         stuck_t_ = ~0ull;

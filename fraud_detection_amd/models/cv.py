@@ -1,4 +1,9 @@
-"""K12 device cross-validation: the reference's whole training job on one device-resident table.
+"""K12 device cross-validation of the LOGISTIC model family on one device-resident table.
+
+The reference runs this job with XGBClassifier (train_model.py:58-106); its GBDT counterpart is
+models/gbdt_cv.py.  Folds come from a keyed Feistel stratified assignment (ops/split.assign), not
+sklearn's StratifiedKFold(shuffle, 42) permutation: statistically equivalent folds, so fold-level
+AUC parity with the reference is unpinned.
 
 Reference (train_model.py:36-110): StandardScaler fitted once on the training split; 5-fold
 StratifiedKFold(shuffle, random_state=42) over it; inside every fold SMOTE(random_state=42) on the
@@ -62,7 +67,8 @@ class CVResult:
 
 
 class DeviceCV:
-    """The train_model.py job (CV + final fit + AUCs) for the logistic model family on one GPU."""
+    """The train_model.py job shape (CV + final fit + AUCs) for the logistic model family on one GPU
+    (the reference's XGB family: models/gbdt_cv.DeviceGBDTCV)."""
 
     def __init__(self, cfg: TrainConfig | None = None, n_folds: int = 5, seed: int = 42, warm_start: bool = True):
         self.cfg = cfg or TrainConfig()

@@ -71,10 +71,12 @@ class TrainConfig:
     # of the ranks' synthetic rows equals the one-process SMOTE output bit for bit; "shard" = each
     # rank oversamples its own minority rows (per-partition SMOTE: constant work per rank)
     smote_scope: str = "global"
-    # Newton on bf16 device rows: the SMOTE rows are never stored -- every logistic pass
-    # regenerates them from their Philox draws out of the L2-resident minority parents
-    # (ops/logreg.VirtualSmote), bitwise the rows smote_generate would write.  At the bench shape
-    # half the training rows are synthetic: no 512 MB SMOTE write and half the bytes per pass.
+    # Both solvers, bf16 or fp8 device rows: the SMOTE rows are never stored.  Each sample's lambda
+    # is bucketed by pick once per fit; every logistic pass folds a pick's samples in through
+    # fixed-point sums over its lambdas against the two L2-resident parent rows
+    # (ops/logreg.VirtualSmote, logreg.hip pick_terms).  The interpolants enter at fp32 (the stored
+    # path rounds each to bf16 / e4m3).  At the bench shape half the training rows are synthetic:
+    # no 512 MB SMOTE write and half the bytes per pass.
     virtual_smote: bool = True
 
 

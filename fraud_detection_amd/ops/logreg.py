@@ -5,7 +5,9 @@ Solvers (all minimise sklearn's objective, ops/reference.py NewtonStateRef docst
                 (gradient + loss on VALU, Hessian on MFMA), deterministic reduce, on-device
                 fp64 Cholesky step with backtracking.  Converges to sklearn-lbfgs parity in
                 ~6-10 passes.  Data parallel: ONE all-reduce of 1088 doubles per iteration.
-  * ``sgd``     momentum minibatch SGD over contiguous row windows (gradient-only passes).
+  * ``sgd``     curvature-normalised momentum minibatch SGD: every minibatch strides over the whole
+                shard (row phase b of the pass grid's tile walk) plus 1/nb of the virtual SMOTE
+                picks; gradient-only passes with fixed-point in-launch reduction.
 
 The device loop never synchronises with the host inside a chunk of iterations: a device-side
 ``done`` flag turns converged iterations into no-op launches.
@@ -745,6 +747,9 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             w32[LABEL_COL] = 0.0
             ws.w32.copy_(w32)
         start = (int(got[1]["epoch"]), int(got[1]["batch"]))
+        # a fit that had converged before the checkpoint stays converged: its remaining passes and
+        # updates are no-ops, as in the uninterrupted fit (reset() cleared the device flag)
+        ws.done.fill_(int(float(got[0]["state"][S_CONV]) > 0))
     fp8 = storage_kind(rows) != "bf16"
     blocks = ref.sgd_grid_blocks(n_stored, nb, ws.nblocks_fp8 if fp8 else ws.nblocks)
     dp = comm is not None and comm.world_size > 1

@@ -111,6 +111,29 @@ def test_owner_reclaims_tickets_of_a_dead_producer():
     assert r.stats()["reclaimed"] == 2
 
 
+def test_owner_frees_a_done_slot_whose_producer_never_consumed_it():
+    """a producer killed while waiting for its results leaves its slot at (t, DONE).
+    No producer can take ticket t + N until that slot reads (t + N, FREE), so head stops at t + N;
+    the owner must reclaim the unfreed lap even though nobody holds ticket t + N yet."""
+    r = _ring(nslots=4, slot_rows=2)
+    r.reclaim_ms = 150.0
+    dst = np.zeros((16, D), np.float32)
+    r.debug_publish(_x(6.0))      # ticket 0, never consumed
+    _serve(r, 2, dst)             # the owner completes it: slot 0 stays at (0, DONE)
+    for v in (1.0, 2.0, 3.0):     # tickets 1..3 go round the ring normally
+        th, box = _start(r, _x(v), 3000.0)
+        got = _serve(r, 2, dst)
+        th.join()
+        np.testing.assert_array_equal(box["out"][:, 0], _x(v)[:, 0] * 10.0)
+    th, box = _start(r, _x(8.0), 5000.0)  # ticket 4 needs slot 0 again
+    got = _serve(r, 2, dst, timeout_ms=3000.0)
+    th.join()
+    assert "err" not in box, box
+    assert np.array_equal(got, _x(8.0))
+    np.testing.assert_array_equal(box["out"][:, 0], _x(8.0)[:, 0] * 10.0)
+    assert r.stats()["reclaimed"] == 1
+
+
 def test_many_producers_with_random_timeouts_keep_the_ring_consistent():
     """Stress: producers with short deadlines and a slow owner; every answered request got its
     own rows' results and the owner never stalls."""
