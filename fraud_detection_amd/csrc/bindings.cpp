@@ -636,6 +636,79 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_sgd_update(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), P<const double>(aff),
                            sgd_args(d, C, c, mom, fi, nb, avg, epoch_end, tol), S(s));
   });
+  auto smote_view = [](u parents, u nbr, u lam, u off, u cnt, int64_t n_real, int64_t q_offset, int mq, int k) {
+    fdx::SmoteView v;
+    if (parents) {
+      v.parents = P<const uint16_t>(parents);
+      v.nbr = P<const int>(nbr);
+      v.lam = P<const uint16_t>(lam);
+      v.off = P<const int>(off);
+      v.cnt = P<const int>(cnt);
+      v.n_real = n_real;
+      v.q_offset = q_offset;
+      v.mq = mq;
+      v.k = k;
+    }
+    return v;
+  };
+  // One process: steps [s0, s1) of the schedule in ONE persistent launch (logreg.hip
+  // sgd_persist_kernel).  Gw: waves of the per-step pass grid (4 x its blocks) -- the minibatch
+  // partition.  ws: int64 [kSgdPersistWords] scratch (zeroed by the launcher).
+  m.def("sgd_persist", [smote_view](u X, int fp8, float x_scale, int64_t end, u cw, u parents, u nbr, u lam, u off,
+                                    u cnt, int64_t n_real, int64_t q_offset, int mq, int k, int64_t hole_at,
+                                    int64_t hole_len, u ws, u state, u w32, u done, u aff, int d, double C, double mom,
+                                    int fi, double tol, int nb, int epochs, int average, int serpentine,
+                                    std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps) {
+    if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
+    const fdx::SmoteView v = smote_view(parents, nbr, lam, off, cnt, n_real, q_offset, mq, k);
+    fdx::RowHole h;
+    h.at = hole_at;
+    h.len = hole_len;
+    fdx::SgdPersistArgs a;
+    a.ws = P<unsigned long long>(ws);
+    a.st = P<double>(state);
+    a.w32 = P<float>(w32);
+    a.done = P<int>(done);
+    a.aff = P<const double>(aff);
+    a.C = C;
+    a.momentum = mom;
+    a.tol = tol;
+    for (int e = 0; e < epochs; ++e) a.lr[e] = lrs[e];
+    a.d = d;
+    a.fit_intercept = fi;
+    a.nb = nb;
+    a.epochs = epochs;
+    a.average = average;
+    a.serpentine = serpentine;
+    a.s0 = s0;
+    a.s1 = s1;
+    a.Gw = Gw;
+    a.stamps = P<unsigned long long>(stamps);
+    fdx::launch_sgd_persist(P<const void>(X), fp8, x_scale, end, P<const float>(cw), parents ? &v : nullptr, h, a, S(s));
+  });
+  m.def("sgd_persist_blocks", [](int grid_blocks) { return fdx::sgd_persist_blocks(grid_blocks); });
+  m.def("sgd_full_blocks", []() { return fdx::sgd_full_blocks(); });
+  m.attr("SGD_PERSIST_WORDS") = fdx::kSgdPersistWords;
+  // Data parallel lean step: FISH pass -> fixed-point sums[36] (int64) for the all-reduce, then the
+  // update from the reduced sums.
+  m.def("sgd_pass_sums", [smote_view](u X, int fp8, float x_scale, int64_t end, u w32, u cw, u done, int nb, int b,
+                                      int blocks, u parents, u nbr, u lam, u off, u cnt, int64_t n_real,
+                                      int64_t q_offset, int mq, int k, int64_t hole_at, int64_t hole_len, u acc,
+                                      u ticket, u sums, u aff, u s) {
+    const fdx::SmoteView v = smote_view(parents, nbr, lam, off, cnt, n_real, q_offset, mq, k);
+    fdx::RowHole h;
+    h.at = hole_at;
+    h.len = hole_len;
+    fdx::launch_sgd_pass_sums(P<const void>(X), fp8, x_scale, end, P<const float>(w32), P<const float>(cw),
+                              P<const int>(done), nb, b, blocks, parents ? &v : nullptr, h,
+                              P<unsigned long long>(acc), P<unsigned int>(ticket), P<long long>(sums),
+                              P<const double>(aff), S(s));
+  });
+  m.def("sgd_update_fixed", [sgd_args](u sums, u state, u w32, u done, u aff, int d, double C, double c, double mom,
+                                       int fi, int nb, int avg, int epoch_end, double tol, u s) {
+    fdx::launch_sgd_update_fixed(P<const long long>(sums), P<double>(state), P<float>(w32), P<int>(done),
+                                 P<const double>(aff), sgd_args(d, C, c, mom, fi, nb, avg, epoch_end, tol), S(s));
+  });
 
   // knn / smote
   m.def("knn_prep", [](u X, int m_, int m_pad, int role, u out, u s, u outq, u aff, u parents) {
@@ -721,12 +794,13 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
   m.def("gbdt_hist_slot_words", [] { return fdx::gbdt_hist_slot_words(); });
   m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u slots, u s,
-                        int64_t flush_rows) {
+                        int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
     fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const uint32_t>(gh), P<const int>(ridx), P<const int64_t>(seg),
                           P<const int64_t>(gcnt), level, d, P<unsigned long long>(hist), P<long long>(slots), S(s),
-                          flush_rows);
+                          flush_rows, hole_at, hole_len);
   }, py::arg("bins"), py::arg("gh"), py::arg("ridx"), py::arg("seg"), py::arg("gcnt"), py::arg("level"),
-     py::arg("d"), py::arg("hist"), py::arg("slots"), py::arg("s"), py::arg("flush_rows") = 0);
+     py::arg("d"), py::arg("hist"), py::arg("slots"), py::arg("s"), py::arg("flush_rows") = 0,
+     py::arg("hole_at") = 0, py::arg("hole_len") = 0);
   m.def("gbdt_split", [](u hist, u gcnt, int level, int d, u nbins, u cuts, double ginv, double hinv, double lam,
                          double mcw, double gamma, u feat, u bin, u thr, u gain, u ng, u nh, u s) {
     fdx::launch_gbdt_split(P<unsigned long long>(hist), P<const int64_t>(gcnt), level, d, P<const int>(nbins),
@@ -737,13 +811,16 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_gbdt_transpose(P<const uint8_t>(bins), n, d, P<uint8_t>(binsT), ldt, S(s));
   });
   m.def("gbdt_partition", [](u binsT, int64_t ldt, u ridx, u nid, int64_t n, u feat, u bin, int level, u flag, u counts,
-                             int nblocks, u seg, u node_r, u ridx_out, u nid_out, u s, u gcnt) {
+                             int nblocks, u seg, u node_r, u ridx_out, u nid_out, u s, u gcnt, int64_t hole_at,
+                             int64_t hole_len) {
     fdx::launch_gbdt_partition(P<const uint8_t>(binsT), ldt, P<const int>(ridx), P<const uint8_t>(nid), n, P<const int>(feat),
                                P<const int>(bin), level, P<uint8_t>(flag), P<int64_t>(counts), nblocks, P<int64_t>(seg),
-                               P<int64_t>(node_r), P<int>(ridx_out), P<uint8_t>(nid_out), S(s), P<int64_t>(gcnt));
+                               P<int64_t>(node_r), P<int>(ridx_out), P<uint8_t>(nid_out), S(s), P<int64_t>(gcnt),
+                               hole_at, hole_len);
   }, py::arg("binsT"), py::arg("ldt"), py::arg("ridx"), py::arg("nid"), py::arg("n"), py::arg("feat"), py::arg("bin"),
      py::arg("level"), py::arg("flag"), py::arg("counts"), py::arg("nblocks"), py::arg("seg"), py::arg("node_r"),
-     py::arg("ridx_out"), py::arg("nid_out"), py::arg("s"), py::arg("gcnt") = 0);
+     py::arg("ridx_out"), py::arg("nid_out"), py::arg("s"), py::arg("gcnt") = 0, py::arg("hole_at") = 0,
+     py::arg("hole_len") = 0);
   m.def("gbdt_round_init", [](u hist, int64_t hist_words, u seg, u gcnt, int64_t n, int64_t n_global, u s,
                               u node_r, int n_nodes) {
     fdx::launch_gbdt_round_init(P<unsigned long long>(hist), hist_words, P<int64_t>(seg), P<int64_t>(gcnt), n,

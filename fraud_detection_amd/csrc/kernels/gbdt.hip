@@ -41,6 +41,14 @@ constexpr int kPartThreads = 256;
 
 __device__ __forceinline__ int heap_first(int level) { return (1 << level) - 1; }
 
+// Level 0 walks the fit's rows in order without reading ridx.  A cross-validation fold fits the
+// table minus one contiguous block [hole_at, hole_at + hole_len) (the fold's validation rows, whose
+// margins the round's margin update scores for free): position p of the root is row
+// p + (p >= hole_at ? hole_len : 0).  Deeper levels read ridx, which holds those row ids.
+__device__ __forceinline__ int64_t hole_row(int64_t p, int64_t hole_at, int64_t hole_len) {
+  return p + (p >= hole_at ? hole_len : 0);
+}
+
 // Build flag of a node at level >= 1: the smaller child of each split (ties: the left one) is
 // histogrammed; its sibling is derived.  `gcnt` holds global (all-rank) row counts.
 __device__ __forceinline__ bool is_built(int node, const int64_t* gcnt) {
@@ -233,7 +241,7 @@ __device__ __forceinline__ int64_t level_chunk(const LevelNodes& L, int level, i
 __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
     const uint8_t* __restrict__ bins, const uint32_t* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
-    long long* __restrict__ slots, int64_t flush_rows) {
+    long long* __restrict__ slots, int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
   __shared__ unsigned long long sh[kHistWords];
   __shared__ LevelNodes lv;
   const int h0 = heap_first(level), nn = 1 << level;
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
 #pragma unroll
         for (int u = 0; u < kHistBatch; ++u) {
           const int64_t v = v0 + (int64_t)u * kHistThreads;
-          rows[u] = v < c1 ? (level == 0 ? pbase + v : (int64_t)ridx[pbase + v]) : -1;
+          rows[u] = v < c1 ? (level == 0 ? hole_row(pbase + v, hole_at, hole_len) : (int64_t)ridx[pbase + v]) : -1;
         }
         uint32_t words[kHistBatch][8];
         unsigned long long pk[kHistBatch];
@@ -546,7 +554,8 @@ constexpr int kPartMaxNodes = 64;  // nodes of one partitioned level (levels <= 
 __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
     const uint8_t* __restrict__ binsT, int64_t ldt, const int* __restrict__ ridx, const uint8_t* __restrict__ nid,
     int64_t n, const int* __restrict__ feat, const int* __restrict__ bin, int level,
-    uint8_t* __restrict__ flag, int64_t* __restrict__ counts, int64_t* __restrict__ node_r) {
+    uint8_t* __restrict__ flag, int64_t* __restrict__ counts, int64_t* __restrict__ node_r, int64_t hole_at,
+    int64_t hole_len) {
   __shared__ int lcnt[kPartMaxNodes];
   __shared__ int64_t red[kPartThreads / kWave];
   const int h0 = heap_first(level), nn = 1 << level;
@@ -568,7 +577,7 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_count_kernel(
 #pragma unroll
     for (int u = 0; u < kPartRows; ++u) {
       const bool ok = p + u < hi;
-      rw[u] = !ok ? 0 : (level == 0 ? (int)(p + u) : ridx[p + u]);
+      rw[u] = !ok ? 0 : (level == 0 ? (int)hole_row(p + u, hole_at, hole_len) : ridx[p + u]);
       ndv[u] = (ok && level != 0) ? (int)nid[p + u] : h0;
     }
   };
@@ -648,7 +657,7 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
     const uint8_t* __restrict__ flag, const int64_t* __restrict__ counts, const int* __restrict__ ridx,
     const uint8_t* __restrict__ nid, int64_t n, int level, const int64_t* __restrict__ node_r,
     int64_t* __restrict__ seg, int* __restrict__ ridx_out, uint8_t* __restrict__ nid_out,
-    int64_t* __restrict__ gcnt) {
+    int64_t* __restrict__ gcnt, int64_t hole_at, int64_t hole_len) {
   __shared__ int wave_cnt[kPartThreads / kWave];
   __shared__ int64_t s_red[kPartThreads / kWave];
   __shared__ int64_t s_sb[kPartMaxNodes], s_left[kPartMaxNodes], s_rb[kPartMaxNodes];
@@ -702,7 +711,7 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
     for (int u = 0; u < kPartRows; ++u) {
       const bool ok = p0 + u < hi;
       rfv[u] = ok ? (int)flag[p0 + u] : 0;
-      riv[u] = !ok ? 0 : (level == 0 ? (int)(p0 + u) : ridx[p0 + u]);  // level 0: identity
+      riv[u] = !ok ? 0 : (level == 0 ? (int)hole_row(p0 + u, hole_at, hole_len) : ridx[p0 + u]);  // level 0: in order
       ndv[u] = (ok && level != 0) ? (int)nid[p0 + u] : h0;
     }
   };
@@ -915,7 +924,8 @@ int64_t gbdt_hist_slot_words() { return (int64_t)(gbdt_hist_blocks() + 2 * kGBMa
 
 void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
-                      hipStream_t stream, int64_t flush_rows) {
+                      hipStream_t stream, int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
+  if (hole_at < 0 || hole_len < 0) throw std::runtime_error("gbdt_hist: bad row hole");
   // flush_rows <= kFlushRows (the packed-word exactness bound); smaller values only for tests of
   // the multi-flush path
   if (flush_rows <= 0 || flush_rows > kFlushRows) flush_rows = kFlushRows;
@@ -923,7 +933,8 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   // at most blocks + nodes pairs)
   if (level < 0 || (1 << level) > kGBMaxNodes + 1) throw std::runtime_error("gbdt_hist: level out of range");
   const int nb = gbdt_hist_blocks();
-  gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows);
+  gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows, hole_at,
+                                                     hole_len);
   check_launch("gbdt_hist");
   const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, level == 0 ? 1u : 1u << (level - 1));
   gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, nb, hist);
@@ -950,14 +961,15 @@ void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT
 void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
                            const int* feat, const int* bin, int level, uint8_t* flag, int64_t* counts,
                            int nblocks, int64_t* seg, int64_t* node_r, int* ridx_out, uint8_t* nid_out,
-                           hipStream_t stream, int64_t* gcnt) {
+                           hipStream_t stream, int64_t* gcnt, int64_t hole_at, int64_t hole_len) {
   if (nblocks > 4096 || nblocks < 1) throw std::runtime_error("gbdt: 1..4096 partition blocks");
+  if (hole_at < 0 || hole_len < 0) throw std::runtime_error("gbdt_partition: bad row hole");
   if (level < 0 || (1 << level) > kPartMaxNodes) throw std::runtime_error("gbdt: partition level out of range");
   gbdt_part_count_kernel<<<nblocks, kPartThreads, 0, stream>>>(binsT, ldt, ridx, nid, n, feat, bin, level, flag,
-                                                               counts, node_r);
+                                                               counts, node_r, hole_at, hole_len);
   check_launch("gbdt_part_count");
   gbdt_part_scatter_kernel<<<nblocks, kPartThreads, 0, stream>>>(flag, counts, ridx, nid, n, level, node_r, seg,
-                                                                 ridx_out, nid_out, gcnt);
+                                                                 ridx_out, nid_out, gcnt, hole_at, hole_len);
   check_launch("gbdt_part_scatter");
 }
 

@@ -195,6 +195,43 @@ void launch_sgd_pass_fused(const void* X, int fp8, float x_scale, int64_t row_en
 // data parallel: the update from the all-reduced [36] sums
 void launch_sgd_update(const double* red, double* state, float* w32, int* done, const double* aff,
                        const SgdArgs& a, hipStream_t stream);
+// Data parallel, lean step: the FISH pass adds its fixed-point sums into the replicated
+// accumulators and its last block folds them into sums[36] (int64, 2^-20 units) and zeroes them --
+// the vector the ranks all-reduce (integer: exact, order-free) before launch_sgd_update_fixed.
+void launch_sgd_pass_sums(const void* X, int fp8, float x_scale, int64_t row_end, const float* w32,
+                          const float* class_w, const int* done, int row_sub, int row_phase, int nblocks,
+                          const SmoteView* sv, RowHole hole, unsigned long long* acc, unsigned int* ticket,
+                          long long* sums, const double* aff, hipStream_t stream);
+void launch_sgd_update_fixed(const long long* sums, double* state, float* w32, int* done, const double* aff,
+                             const SgdArgs& a, hipStream_t stream);
+// One process: the whole SGD schedule (steps [s0, s1) of epochs x nb minibatches) in ONE
+// persistent launch (logreg.hip sgd_persist_kernel): one 512-thread block per CU whose 8 waves are
+// waves of the per-step grid, a grid barrier per step, the update applied redundantly by every
+// block to its LDS copy of the state (bitwise the per-step launches' fit).
+// The SGD pass grid (its waves define the minibatch partition): 2 x 256-thread blocks per CU, so
+// that the persistent launch holds it as one 8-wave block per CU.
+int sgd_full_blocks();
+constexpr int kSgdMaxEpochs = 8;
+constexpr int kSgdPersistWords = 128 + 3 * 32 * 36;  // barrier shards (1 KB) + 3 accumulator sets
+struct SgdPersistArgs {
+  unsigned long long* ws = nullptr;  // [kSgdPersistWords] int64 workspace (zeroed by the launcher)
+  double* st = nullptr;
+  float* w32 = nullptr;
+  int* done = nullptr;
+  const double* aff = nullptr;
+  double C = 1.0, momentum = 0.5, tol = 1e-3;
+  double lr[kSgdMaxEpochs] = {};
+  int d = 30, fit_intercept = 1, nb = 1, epochs = 1, average = 1, serpentine = 0;
+  int s0 = 0, s1 = 0;
+  int64_t Gw = 0;  // waves of the per-step pass grid (4 x its blocks): sets the minibatch partition
+  unsigned long long* stamps = nullptr;  // nullable: [steps][3][blocks] wall_clock64 at pass end,
+                                         // barrier exit and update end (tools/sgd_stamps.py)
+};
+void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
+                        const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream);
+// blocks of the persistent launch for a per-step grid of `grid_blocks` 256-thread blocks, or 0 when
+// that many 512-thread blocks cannot all be resident (the caller then launches per step)
+int sgd_persist_blocks(int grid_blocks);
 
 // ---- knn.hip ----
 // role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29);
@@ -294,9 +331,12 @@ int64_t quantile_select_ws_bytes(int64_t m, int d);
 void launch_quantile_select(const float* X, int64_t m, int64_t stride, int ld, int d, int max_bin, void* ws,
                             float* out, hipStream_t stream);
 int64_t gbdt_hist_slot_words();  // int64 words of the per-(node, block) histogram slots
+// hole_at / hole_len (hist and partition): the fit's rows are the table minus the block
+// [hole_at, hole_at + hole_len) -- a cross-validation fold on the fold-sorted table (n counts the
+// fit's rows, not the table's)
 void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
-                      hipStream_t stream, int64_t flush_rows = 0);
+                      hipStream_t stream, int64_t flush_rows = 0, int64_t hole_at = 0, int64_t hole_len = 0);
 void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
                        const float* cuts, double ginv, double hinv, double lambda,
                        double min_child_weight, double gamma, int* feat, int* bin, float* thr,
@@ -306,7 +346,7 @@ void launch_gbdt_transpose(const uint8_t* bins, int64_t n, int d, uint8_t* binsT
 void launch_gbdt_partition(const uint8_t* binsT, int64_t ldt, const int* ridx, const uint8_t* nid, int64_t n,
                            const int* feat, const int* bin, int level, uint8_t* flag, int64_t* counts,
                            int nblocks, int64_t* seg, int64_t* node_r, int* ridx_out, uint8_t* nid_out,
-                           hipStream_t stream, int64_t* gcnt = nullptr);
+                           hipStream_t stream, int64_t* gcnt = nullptr, int64_t hole_at = 0, int64_t hole_len = 0);
 // node_r[0, n_nodes) (per-node right counts of the partition) is zeroed too
 void launch_gbdt_round_init(unsigned long long* hist, int64_t hist_words, int64_t* seg, int64_t* gcnt, int64_t n,
                             int64_t n_global, hipStream_t stream, int64_t* node_r, int n_nodes);

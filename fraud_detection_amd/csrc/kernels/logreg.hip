@@ -22,6 +22,7 @@
 // with no host synchronisation (hipGraph-capturable); a device-side `done` flag turns the
 // remaining iterations into no-ops once converged.  With data parallelism the reduced 1088-double
 // vector is all-reduced over RCCL between the reduce and the update kernels (parallel/dp.py).
+#include <cstdio>
 #include <type_traits>
 
 #include "common.h"
@@ -70,43 +71,72 @@ __device__ __forceinline__ long long group_sum_i64(long long v) {
   return v;
 }
 
-// One pick's terms for the LPR lanes that share it (lane q owns columns [C q, C q + C)).  wl: this
-// lane's weights in the kernel's row units; xs: the unit scale of feature columns (fp8 rows hold
-// features * x_scale); p < 0: an empty pick (the lanes still join the shuffles).  The pick's
-// gradient is added into gacc; xa / xb are the caller's scratch for the two parent rows and, for
-// HESS, come back holding the two rank-1 Hessian rows u1 / u2 (in place: no extra registers live
-// beside a mid-loop pick, which is what lets the fp8 pass run its picks mid-loop).
-template <int LPR, bool HESS, bool FISH = false, int kLamLoads = 8>
-__device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q, const float* wl, float xs,
-                                           float sw1, float hrs, float* gacc, float* xa, float* xb, float& loss,
-                                           float& wsum, float& dsum) {
+// One pick's inputs (pick_terms' load stage): its lambda run (off, cnt), the first L lambdas of
+// this lane, and this lane's columns of the two parent rows.  Nothing here depends on the weights,
+// so the persistent SGD launch loads the next step's pick before the grid barrier (the two
+// dependent round trips -- off / cnt / nbr, then lambdas / parents -- hide behind the barrier).
+template <int LPR, int L>
+struct PickIn {
+  static_assert(L % 2 == 0, "lambdas are held in pairs");
+  int o0 = 0, cnt = 0;
+  uint4 ra[(32 / LPR) / 8], rb[(32 / LPR) / 8];
+  uint32_t lv[L / 2];  // lambda u in bits [16 (u & 1), 16 (u & 1) + 16) of lv[u / 2]
+  __device__ __forceinline__ uint32_t lam(int u) const { return (lv[u >> 1] >> (16 * (u & 1))) & 0xffffu; }
+};
+
+// lambdas u = 0 .. L-1 of this lane from j0 (j = j0 + u * LPR), packed in pairs
+template <int LPR, int L>
+__device__ __forceinline__ void load_lam_pairs(const SmoteView& sv, int o0, int cnt, int j0, uint32_t (&lv)[L / 2]) {
+#pragma unroll
+  for (int u = 0; u < L; u += 2) {
+    const int j = j0 + u * LPR;
+    const uint32_t lo = j < cnt ? sv.lam[o0 + j] : 0u;
+    const uint32_t hi = j + LPR < cnt ? sv.lam[o0 + j + LPR] : 0u;
+    lv[u >> 1] = lo | (hi << 16);
+  }
+}
+
+template <int LPR, int L>
+__device__ __forceinline__ void pick_load(const SmoteView& sv, int64_t p, int q, PickIn<LPR, L>& in) {
   constexpr int C = 32 / LPR;
   const bool ok = p >= 0;
   const int64_t pp = ok ? p : 0;
   const int64_t ra = sv.q_offset + pp / sv.k, rb = sv.nbr[pp];
   const uint4* Pb = reinterpret_cast<const uint4*>(sv.parents);
-  const int o0 = ok ? sv.off[pp] : 0;
-  const int cnt = ok ? sv.cnt[pp] : 0;
-  // kLamLoads lambdas per lane in flight per step: the first step's loads are issued before the
-  // parent rows arrive, so a pick of <= LPR * kLamLoads samples (the bench's ~117) costs one round
-  // trip for its lambdas, overlapped with the parents' -- not one per 8 samples after them (the
-  // chain a wave's pick tile adds to a latency-bound sub-sampled pass).  Integer sums: the
-  // grouping changes no bit.  Compute runs in groups of 8, summed in int32 (|term| < 2^30 / 8).
-  // kLamLoads: as many as the caller's register budget allows (Hessian passes: 8).
-  constexpr int kLamGroup = 8;
-  uint16_t lv[kLamLoads];
-  auto load_lams = [&](int j0) __attribute__((always_inline)) {
-#pragma unroll
-    for (int u = 0; u < kLamLoads; ++u) {
-      const int j = j0 + u * LPR;
-      lv[u] = j < cnt ? sv.lam[o0 + j] : 0;
-    }
-  };
-  load_lams(q);
+  in.o0 = ok ? sv.off[pp] : 0;
+  in.cnt = ok ? sv.cnt[pp] : 0;
+  // L lambdas per lane in flight: the lambda loads are issued before the parent rows arrive, so a
+  // pick of <= LPR * L samples (the bench's ~117) costs one round trip for its lambdas, overlapped
+  // with the parents' -- not one per 8 samples after them (the chain a wave's pick tile adds to a
+  // latency-bound sub-sampled pass).
+  load_lam_pairs<LPR, L>(sv, in.o0, in.cnt, q, in.lv);
 #pragma unroll
   for (int h = 0; h < C / 8; ++h) {
-    unpack8(Pb[ra * 4 + (C / 8) * q + h], xa + 8 * h);
-    unpack8(Pb[rb * 4 + (C / 8) * q + h], xb + 8 * h);
+    in.ra[h] = Pb[ra * 4 + (C / 8) * q + h];
+    in.rb[h] = Pb[rb * 4 + (C / 8) * q + h];
+  }
+}
+
+// One pick's terms for the LPR lanes that share it (lane q owns columns [C q, C q + C)), from its
+// loaded inputs (pick_load; a pick of more than LPR * L samples loads the rest here, L at a time).
+// wl: this lane's weights in the kernel's row units; xs: the unit scale of feature columns (fp8
+// rows hold features * x_scale); an empty pick (p < 0 at load) still joins the shuffles.  The
+// pick's gradient is added into gacc; xa / xb are the caller's scratch for the two parent rows and,
+// for HESS, come back holding the two rank-1 Hessian rows u1 / u2 (in place: no extra registers
+// live beside a mid-loop pick, which is what lets the fp8 pass run its picks mid-loop).  Per-sample
+// terms are summed as integers (groups of 8 in int32, |term| < 2^30 / 8): the grouping -- and L --
+// changes no bit.
+template <int LPR, bool HESS, bool FISH, int L>
+__device__ __forceinline__ void pick_compute(const SmoteView& sv, const PickIn<LPR, L>& in, int q, const float* wl,
+                                             float xs, float sw1, float hrs, float* gacc, float* xa, float* xb,
+                                             float& loss, float& wsum, float& dsum) {
+  constexpr int C = 32 / LPR;
+  constexpr int kLamGroup = 8;
+  const int o0 = in.o0, cnt = in.cnt;
+#pragma unroll
+  for (int h = 0; h < C / 8; ++h) {
+    unpack8(in.ra[h], xa + 8 * h);
+    unpack8(in.rb[h], xb + 8 * h);
   }
   float za = 0.0f, zb = 0.0f;
 #pragma unroll
@@ -122,16 +152,19 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   zb = group_sum<LPR>(zb);
   const float dz = zb - za;
   long long sr = 0, srl = 0, sd = 0, sdl = 0, sdll = 0, sl = 0;
-  for (int j0 = q; j0 < cnt; j0 += LPR * kLamLoads) {
-    if (j0 != q) load_lams(j0);
+  uint32_t lv[L / 2];
 #pragma unroll
-    for (int g0 = 0; g0 < kLamLoads; g0 += kLamGroup) {
+  for (int u = 0; u < L / 2; ++u) lv[u] = in.lv[u];
+  for (int j0 = q; j0 < cnt; j0 += LPR * L) {
+    if (j0 != q) load_lam_pairs<LPR, L>(sv, o0, cnt, j0, lv);
+#pragma unroll
+    for (int g0 = 0; g0 < L; g0 += kLamGroup) {
       if (j0 + g0 * LPR >= cnt) break;
       int br = 0, brl = 0, bd = 0, bdl = 0, bdll = 0, bl = 0;
 #pragma unroll
       for (int u = g0; u < g0 + kLamGroup; ++u) {
         if (j0 + u * LPR >= cnt) break;
-        const float lam = (float)lv[u] * (1.0f / 65536.0f);
+        const float lam = (float)((lv[u >> 1] >> (16 * (u & 1))) & 0xffffu) * (1.0f / 65536.0f);
         const float z = fmaf(lam, dz, za);
         const float zc = fminf(fmaxf(z, -80.0f), 80.0f);
         const float eh = __expf(-0.5f * zc);
@@ -188,6 +221,17 @@ __device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q
   dsum = (HESS || FISH) ? (float)((double)sd * inv) : 0.0f;
 }
 
+// Load + compute of one pick (kLamLoads: as many lambdas in flight as the caller's register budget
+// allows; Hessian passes 8).
+template <int LPR, bool HESS, bool FISH = false, int kLamLoads = 8>
+__device__ __forceinline__ void pick_terms(const SmoteView& sv, int64_t p, int q, const float* wl, float xs,
+                                           float sw1, float hrs, float* gacc, float* xa, float* xb, float& loss,
+                                           float& wsum, float& dsum) {
+  PickIn<LPR, kLamLoads> in;
+  pick_load<LPR, kLamLoads>(sv, p, q, in);
+  pick_compute<LPR, HESS, FISH, kLamLoads>(sv, in, q, wl, xs, sw1, hrs, gacc, xa, xb, loss, wsum, dsum);
+}
+
 // ---- fused SGD step (FUSE passes: one launch per SGD step) ------------------------------------
 // Instead of writing [nblocks][36] float partials for a separate reduce + update launch, every block
 // maps its sums to standardized space (the affine map of pivot-shifted rows), rounds them to 2^-20
@@ -209,11 +253,29 @@ struct SgdFuse {
   float* w32 = nullptr;               // the weights the next pass reads
   int* done = nullptr;
   const double* aff = nullptr;        // pivot-shifted rows: (c | 1/sigma)
+  long long* sums = nullptr;          // non-null: the last block writes the folded [36] sums here
+                                      // instead of applying the update (data parallel lean step)
   SgdArgs a;
 };
 constexpr double kFixScale = 1048576.0;  // 2^20
 __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done,
                           const double* __restrict__ aff, const SgdArgs& a, int t, bool mapped);
+
+// Slot t of NW waves' [36] sums: each wave's sum mapped to standardized space (pivot-shifted rows)
+// and rounded to 2^-20 fixed point ON ITS OWN, then added as integers -- so the step's sums depend
+// only on each wave's rows, not on how waves are grouped into blocks (the per-step launch and the
+// persistent launch group them differently and get bitwise the same sums).
+template <int NW>
+__device__ __forceinline__ long long wave_sums_fixed(const float (*red)[36], const double* aff, int t) {
+  long long q = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    double v = (double)red[w][t];
+    if (aff != nullptr && t < 32) v = aff[32 + t] * (v - aff[t] * (double)red[w][kBiasCol]);
+    q += (long long)__builtin_rint(v * kFixScale);
+  }
+  return q;
+}
 
 // Called by every thread of the block after `red` (the 4 waves' [36] sums) is complete in LDS.
 template <int NW>
@@ -221,15 +283,9 @@ __device__ __forceinline__ void sgd_fused_tail(const float (*red)[36], const Sgd
   __shared__ int s_last;
   __shared__ double rd[36];
   const int t = threadIdx.x;
-  if (t < 64) {  // wave 0: this block's sums -> standardized space -> fixed point -> atomics
-    double v = 0.0, g30 = 0.0;
+  if (t < 64) {  // wave 0: each wave's sums -> standardized space -> fixed point -> atomics
     if (t < 36) {
-#pragma unroll
-      for (int w = 0; w < NW; ++w) v += (double)red[w][t];
-#pragma unroll
-      for (int w = 0; w < NW; ++w) g30 += (double)red[w][kBiasCol];
-      if (fz.aff != nullptr && t < 32) v = fz.aff[32 + t] * (v - fz.aff[t] * g30);
-      const long long q = (long long)__builtin_rint(v * kFixScale);
+      const long long q = wave_sums_fixed<NW>(red, fz.aff, t);
       if (t != 34 && q != 0)
         __hip_atomic_fetch_add(fz.acc + (blockIdx.x % kSgdReplicas) * 36 + t, (unsigned long long)q, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -251,61 +307,62 @@ __device__ __forceinline__ void sgd_fused_tail(const float (*red)[36], const Sgd
     unsigned long long q = 0;
 #pragma unroll 8
     for (int r = 0; r < kSgdReplicas; ++r) q += rep[r * 36 + t];
+    if (fz.sums != nullptr) fz.sums[t] = (long long)q;
     rd[t] = (double)(long long)q * (1.0 / kFixScale);
   }
+  if (fz.sums != nullptr) return;  // uniform: the ranks all-reduce the sums, then sgd_update_fixed
   __syncthreads();
   sgd_apply(rd, fz.st, fz.w32, fz.done, fz.aff, fz.a, t, true);
 }
 
-// VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
-// rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
-// row_sub / row_phase: the pass visits the row tiles t with (t / G) mod row_sub == row_phase
-// (G = waves in the grid) and the pick tiles with t mod row_sub == row_phase -- phase 0 of a
-// 1/row_sub sub-sample is the progressive-Newton warm-up, phases 0..row_sub-1 are the disjoint
-// minibatches of one SGD epoch (every stored row and every SMOTE sample in exactly one of them).
-// FISH (gradient-only SGD passes): slot 35 also receives sum s p (1 - p), the minibatch's
-// Gauss-Newton curvature scalar that sets the SGD step size (sgd_step_kernel).
-template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>  // bf16 rows; fp8: logreg_pass_fp8w_kernel
-__global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
-    const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* w,
-    const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
-    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole, SgdFuse fz) {
-  if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
-  __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
-  __shared__ float red[kWaves][36];
-  const int lane = lane_id(), wv = wave_id();
+__device__ constexpr uint4 kNoTiles[4] = {};  // the `pre` argument of a pass that loads its own first tile
+
+// Stored rows a pass walks (a CV fold's validation block [hole.at, hole.at + hole.len) excluded).
+template <bool VIRT>
+__device__ __forceinline__ int64_t pass_stored_rows(int64_t row_begin, int64_t row_end, const SmoteView& sv,
+                                                    const RowHole& hole) {
+  return (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin - hole.len;
+}
+
+// One 64-row bf16 tile of a wave (4 lanes per row, 16 rows per load): logical row b + 16 u + rr.
+__device__ __forceinline__ void bf16_load_tile(const void* __restrict__ Xv, int64_t row_begin, int64_t n,
+                                               const RowHole& hole, int64_t b, uint4 (&v)[4]) {
+  const int lane = lane_id();
   const int q = lane & 3, rr = lane >> 2;
-  float wl[8];
+  const uint4* X = reinterpret_cast<const uint4*>(Xv);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j];
-  const float cw0 = class_w[0], cw1 = class_w[1];
-  float g[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) g[j] = 0.0f;
-  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f;  // whacc: weight of the rows feeding H
-  float dacc = 0.0f;                              // FISH: sum s p (1 - p)
-  f32x16_t acc = {};
+  for (int u = 0; u < 4; ++u) {
+    const int64_t row = b + 16 * u + rr;
+    const int64_t ph = row + (row >= hole.at ? hole.len : 0);
+    v[u] = row < n ? X[(row_begin + ph) * 4 + q] : make_uint4(0, 0, 0, 0);
+  }
+}
+
+// The share of one pass that ONE wave owns, bf16 rows (4 lanes per row, 8 columns per lane),
+// accumulated into this lane's sums.  `wave` / `Gw`: the wave's index in the pass grid and the
+// grid's wave count -- the row-tile walk and the pick-tile walk depend on them only, so a
+// persistent launch with another block shape walks exactly the rows of the per-pass launches.
+// pre (nullable): the wave's first tile, already loaded (a persistent launch prefetches it across
+// the grid barrier that precedes the pass).
+template <bool HESS, bool VIRT, bool FISH, int kPickLams = (HESS ? 8 : 32), int kPreLams = 32>
+__device__ __forceinline__ void bf16_wave_pass(
+    const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float (&wl)[8], float cw0, float cw1,
+    int hess_stride, int row_sub, int row_phase, const SmoteView& sv, const RowHole& hole, int64_t wave,
+    int64_t Gw, uint16_t* my_tile, float (&g)[8], float& lacc, float& wacc, float& whacc, float& dacc,
+    f32x16_t& acc, const uint4 (&pre)[4], bool use_pre, const PickIn<4, kPreLams>& ppre, bool use_ppre) {
+  wave = __builtin_amdgcn_readfirstlane((int)wave);  // wave-uniform: the tile walk lives in SGPRs
+  const int lane = lane_id();
+  const int q = lane & 3, rr = lane >> 2;
   // transpose-read lane geometry (constant per lane): 16-lane group grp reads 4 rows x 16 cols
   const int grp = lane >> 4, gi = lane & 15;
   const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
-  uint16_t* my_tile = tile[wv];
 
   // stored rows (a CV fold's validation block [hole.at, hole.at + hole.len) is stepped over)
-  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin - hole.len;
+  const int64_t n = pass_stored_rows<VIRT>(row_begin, row_end, sv, hole);
   // row_sub > 1: only 64-row tiles t with (t mod G*row_sub) < G are visited (G = waves in the
   // grid): a uniform 1/row_sub subsample used by the early progressive-Newton iterations.
-  const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
+  const int64_t step = Gw * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
-  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
-  auto load_tile = [&](int64_t b, uint4 (&v)[4]) {
-    const uint4* X = reinterpret_cast<const uint4*>(Xv);
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int64_t row = b + 16 * u + rr;
-      const int64_t ph = row + (row >= hole.at ? hole.len : 0);
-      v[u] = row < n ? X[(row_begin + ph) * 4 + q] : make_uint4(0, 0, 0, 0);
-    }
-  };
   // virtual SMOTE samples: tiles of 16 picks (row_sub: every row_sub-th tile).  A wave's pick
   // tile runs in the middle of its stored-row loop (at a wave-dependent iteration), so the
   // latency-bound pick work of some waves overlaps the streaming of the others instead of
@@ -313,12 +370,15 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
   const float hrs = rsqrtf((float)hess_stride);  // the final x hess_stride restores u u^T
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
-  const int64_t Gw = (int64_t)gridDim.x * kWaves;
-  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub + row_phase;  // this wave's next pick tile
-  auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
+  int64_t ptile = wave * row_sub + row_phase;  // this wave's next pick tile
+  // pre: the tile's inputs are in ppre already (pick_load, issued before the grid barrier)
+  auto pick_tile = [&](int64_t t, bool pre) __attribute__((always_inline)) {
     const int64_t p = t * 16 + rr;
     float u1[8], u2[8], ls, ws, ds;
-    pick_terms<4, HESS, FISH, HESS ? 8 : 32>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, g, u1, u2, ls, ws, ds);
+    if (pre)
+      pick_compute<4, HESS, FISH, kPreLams>(sv, ppre, q, wl, 1.0f, cw1, hrs, g, u1, u2, ls, ws, ds);
+    else
+      pick_terms<4, HESS, FISH, kPickLams>(sv, p < npick ? p : -1, q, wl, 1.0f, cw1, hrs, g, u1, u2, ls, ws, ds);
     if (q == 0) {
       lacc += ls;
       wacc += ws;
@@ -348,20 +408,32 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
       __builtin_amdgcn_wave_barrier();
     }
   };
-  int64_t base = ((int64_t)row_phase * Gw + (int64_t)blockIdx.x * kWaves + wv) * 64;
+  int64_t base = ((int64_t)row_phase * Gw + wave) * 64;
+  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
   uint4 cur[4];
-  if (base < n) load_tile(base, cur);
+  if (use_pre) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = pre[u];
+  } else if (base < n) {
+    bf16_load_tile(Xv, row_begin, n, hole, base, cur);
+  }
+  if constexpr (VIRT && FISH) {  // SGD passes: the wave's first pick tile ahead of its stored rows
+    if (ptile < ntile) {
+      pick_tile(ptile, use_ppre);
+      ptile += Gw * row_sub;
+    }
+  }
   // Sub-sampled Hessian (hess_stride > 1): only every hess_stride-th tile of this wave feeds H
   // (scaled back at the end).  Gradient and loss always use every row, so the Newton fixed point
   // is unchanged; H only shapes the step (sub-sampled Newton).
-  int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
+  int hphase = (int)(wave % hess_stride);
   // pick tile after the ptrig-th stored tile of this wave (spread over the wave's iterations)
   const int64_t witers = n > base ? (n - base + step - 1) / step : 0;
-  const int64_t ptrig = witers > 0 ? 1 + ((blockIdx.x * kWaves + wv) % witers) : 0;
+  const int64_t ptrig = witers > 0 ? 1 + (wave % witers) : 0;
   int64_t pit = 0;
   for (; base < n; base += step) {
     uint4 nxt[4];
-    if (base + step < n) load_tile(base + step, nxt);
+    if (base + step < n) bf16_load_tile(Xv, row_begin, n, hole, base + step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
@@ -426,17 +498,51 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     if (FISH) dacc += dq;
 #pragma unroll
     for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
-    if constexpr (VIRT) {
+    if constexpr (VIRT && !FISH) {
       if (ptile < ntile && ++pit == ptrig) {
-        pick_tile(ptile);
+        pick_tile(ptile, false);
         ptile += Gw * row_sub;
       }
     }
   }
 
   if constexpr (VIRT) {  // the wave's remaining pick tiles
-    for (; ptile < ntile; ptile += Gw * row_sub) pick_tile(ptile);
+    for (; ptile < ntile; ptile += Gw * row_sub) pick_tile(ptile, false);
   }
+}
+
+// VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
+// rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
+// row_sub / row_phase: the pass visits the row tiles t with (t / G) mod row_sub == row_phase
+// (G = waves in the grid) and the pick tiles with t mod row_sub == row_phase -- phase 0 of a
+// 1/row_sub sub-sample is the progressive-Newton warm-up, phases 0..row_sub-1 are the disjoint
+// minibatches of one SGD epoch (every stored row and every SMOTE sample in exactly one of them).
+// FISH (gradient-only SGD passes): slot 35 also receives sum s p (1 - p), the minibatch's
+// Gauss-Newton curvature scalar that sets the SGD step size (sgd_step_kernel).
+template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>  // bf16 rows; fp8: logreg_pass_fp8w_kernel
+__global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
+    const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* w,
+    const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
+    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole, SgdFuse fz) {
+  if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
+  __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
+  __shared__ float red[kWaves][36];
+  const int lane = lane_id(), wv = wave_id();
+  const int q = lane & 3;
+  float wl[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wl[j] = (q * 8 + j == kLabelCol) ? 0.0f : w[q * 8 + j];
+  const float cw0 = class_w[0], cw1 = class_w[1];
+  float g[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) g[j] = 0.0f;
+  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f;  // whacc: weight of the rows feeding H
+  float dacc = 0.0f;                              // FISH: sum s p (1 - p)
+  f32x16_t acc = {};
+  PickIn<4, 32> nopick;
+  bf16_wave_pass<HESS, VIRT, FISH>(Xv, row_begin, row_end, wl, cw0, cw1, hess_stride, row_sub, row_phase, sv, hole,
+                                   (int64_t)blockIdx.x * kWaves + wv, (int64_t)gridDim.x * kWaves, tile[wv], g, lacc,
+                                   wacc, whacc, dacc, acc, kNoTiles, false, nopick, false);
 
   // ---- block reduction (fixed order) ----
 #pragma unroll
@@ -492,57 +598,38 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
 // 16M rows (5.2 TB/s), fp8 bench step 1.164 -> 1.099 ms.
 // VIRT: virtual SMOTE samples as in the bf16 kernel: tiles of 16 picks in its 4-lane layout, mid-loop.
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
-template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>
-__global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
-    const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* w,
-    const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
-    int hess_stride, int row_sub, int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole,
-    SgdFuse fz) {
-  if (done != nullptr && *done) return;
-  __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
-  __shared__ float red[kWaves][36];
-  const int lane = lane_id(), wv = wave_id();
+// One wave's two 32-row fp8 tiles (2 lanes per row, 16 columns per lane): rows b + 32 u + rr.
+__device__ __forceinline__ void fp8_load_tile(const uint8_t* __restrict__ X8, int64_t row_begin, int64_t n,
+                                              const RowHole& hole, int64_t b, uint4 (&v)[2]) {
+  const int lane = lane_id();
   const int q = lane & 1, rr = lane >> 1;
-  const float inv_s = 1.0f / x_scale;
-  // VIRT: the weights are read from LDS where used (wsh) instead of living in 16 VGPRs across
-  // the loop -- the room a mid-loop pick tile needs to run without spilling
-  __shared__ __attribute__((aligned(16))) float wsh[32];
-  if (VIRT && threadIdx.x < 32) {
-    const int col = threadIdx.x;
-    wsh[col] = col == kLabelCol ? 0.0f : w[col] * (col < d_feat ? inv_s : 1.0f);
+  const uint4* X = reinterpret_cast<const uint4*>(X8);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int64_t row = b + 32 * u + rr;
+    const int64_t ph = row + (row >= hole.at ? hole.len : 0);
+    v[u] = row < n ? X[(row_begin + ph) * 2 + q] : make_uint4(0, 0, 0, 0);
   }
-  if (VIRT) __syncthreads();
-  f32x2_t wl[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) {
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int col = 16 * q + 2 * p + e;
-      const float cs = col < d_feat ? inv_s : 1.0f;
-      wl[p][e] = (col == kLabelCol) ? 0.0f : w[col] * cs;
-    }
-  }
-  const float cw0 = class_w[0], cw1 = class_w[1];
-  f32x2_t g[8];
-#pragma unroll
-  for (int p = 0; p < 8; ++p) g[p] = f32x2_t{0.0f, 0.0f};
-  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f, dacc = 0.0f;
-  f32x16_t acc = {};
+}
+
+// The share of one fp8 pass that ONE wave owns (bf16_wave_pass's contract).  wl: this lane's
+// weights in fp8 row units (registers; read when !VIRT); wsh: the same 32 weights in LDS (VIRT
+// reads them where used, see below).  pre (nullable): the wave's first two tiles, loaded already.
+template <bool HESS, bool VIRT, bool FISH, int kPickLams = (HESS ? 8 : 24), int kPreLams = 32>
+__device__ __forceinline__ void fp8_wave_pass(
+    const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const f32x2_t (&wl)[8], const float* wsh,
+    float x_scale, float cw0, float cw1, int hess_stride, int row_sub, int row_phase, const SmoteView& sv,
+    const RowHole& hole, int64_t wave, int64_t Gw, uint16_t* my_tile, f32x2_t (&g)[8], float& lacc, float& wacc,
+    float& whacc, float& dacc, f32x16_t& acc, const uint4 (&pre)[4], bool use_pre, const PickIn<4, kPreLams>& ppre,
+    bool use_ppre) {
+  wave = __builtin_amdgcn_readfirstlane((int)wave);  // wave-uniform: the tile walk lives in SGPRs
+  const int lane = lane_id();
+  const int q = lane & 1, rr = lane >> 1;
   const int grp = lane >> 4, gi = lane & 15;
   const int tr_off = (8 * (grp >> 1) + (gi >> 2)) * kCols + 16 * (grp & 1) + 4 * (gi & 3);
-  uint16_t* my_tile = tile[wv];
-  const int64_t n = (VIRT ? min(row_end, sv.n_real) : row_end) - row_begin - hole.len;  // stored rows
-  const int64_t step = (int64_t)gridDim.x * kWaves * 64 * row_sub;
+  const int64_t n = pass_stored_rows<VIRT>(row_begin, row_end, sv, hole);  // stored rows
+  const int64_t step = Gw * 64 * row_sub;
   const float scw0 = sqrtf(cw0), scw1 = sqrtf(cw1);
-  const uint4* X = reinterpret_cast<const uint4*>(X8);
-  auto load_tile = [&](int64_t b, uint4 (&v)[2]) {
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int64_t row = b + 32 * u + rr;
-      const int64_t ph = row + (row >= hole.at ? hole.len : 0);
-      v[u] = row < n ? X[(row_begin + ph) * 2 + q] : make_uint4(0, 0, 0, 0);
-    }
-  };
   // virtual SMOTE samples: tiles of 16 picks in the bf16 pass's 4-lane layout (lane q4 owns columns
   // [8 q4, 8 q4 + 8)), run in the middle of the stored-row loop as in the bf16 pass.  The 2-lane
   // layout of the stored rows would give a pick 16 columns per lane -- with the two prefetched fp8
@@ -552,10 +639,9 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
   const float hrs = rsqrtf((float)hess_stride);
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
-  const int64_t Gw = (int64_t)gridDim.x * kWaves;
-  int64_t ptile = ((int64_t)blockIdx.x * kWaves + wv) * row_sub + row_phase;
+  int64_t ptile = wave * row_sub + row_phase;
   const int q4 = lane & 3, r4 = lane >> 2;
-  auto pick_tile = [&](int64_t t) __attribute__((always_inline)) {
+  auto pick_tile = [&](int64_t t, bool pre) __attribute__((always_inline)) {
     float wf[8];  // this lane's 4-lane-layout weights in fp8 row units, from LDS (not held in VGPRs
     asm volatile("" ::: "memory");  // across the stored loop: keeps the loads here)
 #pragma unroll
@@ -564,7 +650,11 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     float gc[8], u1[8], u2[8], ls, ws, ds;
 #pragma unroll
     for (int j = 0; j < 8; ++j) gc[j] = 0.0f;
-    pick_terms<4, HESS, FISH, HESS ? 8 : 24>(sv, p < npick ? p : -1, q4, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws, ds);
+    if (pre)
+      pick_compute<4, HESS, FISH, kPreLams>(sv, ppre, q4, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws, ds);
+    else
+      pick_terms<4, HESS, FISH, kPickLams>(sv, p < npick ? p : -1, q4, wf, x_scale, cw1, hrs, gc, u1, u2, ls, ws,
+                                           ds);
     {  // 4-lane columns [8 q4, 8 q4 + 8) -> the 2-lane accumulator g (lane parity h: columns
        // [16 h, 16 h + 16)): lanes q4 = 1, 2 swap, then each adds at offset 8 (q4 >> 1)
       const int src = (q4 == 1 || q4 == 2) ? (lane ^ 3) : lane;
@@ -605,19 +695,29 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       __builtin_amdgcn_wave_barrier();
     }
   };
-  int64_t base = ((int64_t)row_phase * Gw + (int64_t)blockIdx.x * kWaves + wv) * 64;
+  int64_t base = ((int64_t)row_phase * Gw + wave) * 64;
   // two tiles in flight ahead of the one being computed (4 KiB per wave, as the bf16 stream)
   uint4 cur[2], nx1[2];
-  if (base < n) load_tile(base, cur);
-  if (base + step < n) load_tile(base + step, nx1);
-  int hphase = (int)(blockIdx.x * kWaves + wv) % hess_stride;
+  if (use_pre) {
+    cur[0] = pre[0]; cur[1] = pre[1]; nx1[0] = pre[2]; nx1[1] = pre[3];
+  } else {
+    if (base < n) fp8_load_tile(X8, row_begin, n, hole, base, cur);
+    if (base + step < n) fp8_load_tile(X8, row_begin, n, hole, base + step, nx1);
+  }
+  if constexpr (VIRT && FISH) {  // SGD passes: the wave's first pick tile ahead of its stored rows
+    if (ptile < ntile) {
+      pick_tile(ptile, use_ppre);
+      ptile += Gw * row_sub;
+    }
+  }
+  int hphase = (int)(wave % hess_stride);
   const int64_t witers = n > base ? (n - base + step - 1) / step : 0;
-  const int64_t ptrig = witers > 0 ? 1 + ((blockIdx.x * kWaves + wv) % witers) : 0;
+  const int64_t ptrig = witers > 0 ? 1 + (wave % witers) : 0;
   int64_t pit = 0;
   for (; base < n; base += step) {
     if constexpr (VIRT) asm volatile("" ::: "memory");  // the LDS weight reads stay in the loop
     uint4 nxt[2];
-    if (base + 2 * step < n) load_tile(base + 2 * step, nxt);
+    if (base + 2 * step < n) fp8_load_tile(X8, row_begin, n, hole, base + 2 * step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float zq = 0.0f, yq = 0.0f, swq = 0.0f, dq = 0.0f;
@@ -689,17 +789,60 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
       cur[u] = nx1[u];
       nx1[u] = nxt[u];
     }
-    if constexpr (VIRT) {
+    if constexpr (VIRT && !FISH) {
       if (ptile < ntile && ++pit == ptrig) {
-        pick_tile(ptile);
+        pick_tile(ptile, false);
         ptile += Gw * row_sub;
       }
     }
   }
 
   if constexpr (VIRT) {  // the wave's remaining pick tiles
-    for (; ptile < ntile; ptile += Gw * row_sub) pick_tile(ptile);
+    for (; ptile < ntile; ptile += Gw * row_sub) pick_tile(ptile, false);
   }
+
+}
+
+template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>
+__global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
+    const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* w,
+    const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
+    int hess_stride, int row_sub, int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole,
+    SgdFuse fz) {
+  if (done != nullptr && *done) return;
+  __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
+  __shared__ float red[kWaves][36];
+  const int lane = lane_id(), wv = wave_id();
+  const int q = lane & 1;
+  const float inv_s = 1.0f / x_scale;
+  // VIRT: the weights are read from LDS where used (wsh) instead of living in 16 VGPRs across
+  // the loop -- the room a mid-loop pick tile needs to run without spilling
+  __shared__ __attribute__((aligned(16))) float wsh[32];
+  if (VIRT && threadIdx.x < 32) {
+    const int col = threadIdx.x;
+    wsh[col] = col == kLabelCol ? 0.0f : w[col] * (col < d_feat ? inv_s : 1.0f);
+  }
+  if (VIRT) __syncthreads();
+  f32x2_t wl[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int col = 16 * q + 2 * p + e;
+      const float cs = col < d_feat ? inv_s : 1.0f;
+      wl[p][e] = (col == kLabelCol) ? 0.0f : w[col] * cs;
+    }
+  }
+  const float cw0 = class_w[0], cw1 = class_w[1];
+  f32x2_t g[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) g[p] = f32x2_t{0.0f, 0.0f};
+  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f, dacc = 0.0f;
+  f32x16_t acc = {};
+  PickIn<4, 32> nopick;
+  fp8_wave_pass<HESS, VIRT, FISH>(X8, row_begin, row_end, wl, wsh, x_scale, cw0, cw1, hess_stride, row_sub, row_phase,
+                                  sv, hole, (int64_t)blockIdx.x * kWaves + wv, (int64_t)gridDim.x * kWaves, tile[wv],
+                                  g, lacc, wacc, whacc, dacc, acc, kNoTiles, false, nopick, false);
 
   // ---- block reduction (fixed order) ----
   float gs[16];
@@ -1269,6 +1412,277 @@ __global__ __launch_bounds__(64) void sgd_update_kernel(const double* __restrict
   sgd_apply(rd, st, w32, done, aff, a, t, false);
 }
 
+// Data parallel lean step: the update from the all-reduced fixed-point sums of
+// launch_sgd_pass_sums (int64, 2^-20 units; slot 34 unused).
+__global__ __launch_bounds__(64) void sgd_update_fixed_kernel(const long long* __restrict__ sums,
+                                                              double* __restrict__ st, float* __restrict__ w32,
+                                                              int* __restrict__ done,
+                                                              const double* __restrict__ aff, SgdArgs a) {
+  if (*done) return;
+  __shared__ double rd[kSgdSlots];
+  const int t = threadIdx.x;
+  if (t < kSgdSlots) rd[t] = (double)sums[t] * (1.0 / kFixScale);
+  __syncthreads();
+  sgd_apply(rd, st, w32, done, aff, a, t, true);
+}
+
+// ---- persistent SGD: the whole schedule in ONE launch --------------------------------------------
+// The per-step launches pay, per step, a kernel boundary, the grid's fill and drain, and the serial
+// update in the last-arriving block (~14 us of a ~26 us step at the bench shape, profiles/r4_g).
+// Here one 768-thread block per CU runs every step: its 12 waves are waves 12 b .. 12 b + 11 of the
+// per-step grid (bf16_wave_pass / fp8_wave_pass walk the same row and pick tiles), so a step's sums
+// are the per-step launch's sums.  Step t:
+//   pass over minibatch b -> each group of 4 waves (one block of the per-step grid) turns its sums
+//   into 2^-20 fixed point exactly as sgd_fused_tail does -> agent-scope int64 adds into replica
+//   (block mod 32) of accumulator set t mod 3 -> grid barrier -> every block reads the set with
+//   agent-scope loads and applies the SAME update (sgd_apply) to its own LDS copy of the solver
+//   state.  Integer sums are order-free and every block runs the same fp64 code on the same
+//   inputs, so every block holds bitwise the same state -- and bitwise the per-step launches'
+//   state; the convergence flag is therefore uniform across the grid with no broadcast.
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): the payload is written only by
+// agent-scope atomics and read only by agent-scope atomic loads after the barrier, the arrival is an
+// agent atomic add made after the adding wave's vmcnt(0), the poll a relaxed agent load -- the
+// "8-B agent atomics both sides" form, one workgroup per CU.  Sets rotate over three: set t is read
+// after barrier t; set t + 1 is zeroed by block 0 during step t (after barrier t - 1, when every
+// block has finished reading it as set t - 2; before block 0 arrives at barrier t).  The launcher
+// zeroes the barrier shards and all three sets in front of the launch.  Every wait is bounded: a
+// grid whose blocks are not all resident ends with state[kSgdFault] set instead of hanging.
+constexpr int kPersistWaves = 8;
+constexpr int kPersistThreads = kPersistWaves * kWave;
+constexpr int kBarShards = 8, kBarStride = 32;  // arrival shards, one 128-B line each (u32 words)
+enum : int { kSgdFault = 229 };                 // state slot: a grid barrier timed out
+// Variants (template LAMS, PF; FDX_SGD_PERSIST_CFG="lams,pf" picks one at run time, for the lab):
+// LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the same bits);
+// PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick tile's
+// inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the stored
+// tile; 3 the pick inputs only.
+
+// Wave 0 of a block: arrive at the grid barrier and wait until `target` arrivals in all.
+__device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned target, int lane) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's accumulator adds have landed
+  if (lane == 0)
+    __hip_atomic_fetch_add(bar + (blockIdx.x % kBarShards) * kBarStride, 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+  for (unsigned spins = 0;; ++spins) {
+    int v = lane < kBarShards ? (int)__hip_atomic_load(bar + lane * kBarStride, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT) : 0;
+    v += __shfl_xor(v, 1, kWave);
+    v += __shfl_xor(v, 2, kWave);
+    v += __shfl_xor(v, 4, kWave);
+    v = __shfl(v, 0, kWave);
+    if ((unsigned)v >= target) return true;
+    if (spins > (1u << 21)) return false;  // ~1 s: not every block is resident
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <bool FP8, bool VIRT, int kPersistLams = 16, int kPersistPrefetch = 2>
+__global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const void* __restrict__ X,
+                                                                         int64_t row_end, float x_scale,
+                                                                         const float* __restrict__ class_w,
+                                                                         SmoteView sv, RowHole hole,
+                                                                         SgdPersistArgs P) {
+  __shared__ double sst[kStateSize];                      // this block's copy of the solver state
+  __shared__ __attribute__((aligned(16))) float wsh[32];  // weights of the passes (fp8: row units)
+  __shared__ float wnew[32];                              // sgd_apply's folded weights
+  __shared__ float red[kPersistWaves][36];
+  __shared__ unsigned long long rep[kSgdAccWords];
+  __shared__ double rd[kSgdSlots];
+  __shared__ int s_done, s_ok;
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  constexpr int d_feat = 30;
+  const float inv_s = FP8 ? 1.0f / x_scale : 1.0f;
+  unsigned int* bar = reinterpret_cast<unsigned int*>(P.ws);
+  unsigned long long* accs = P.ws + 128;
+  for (int e = t; e < kStateSize; e += kPersistThreads) sst[e] = P.st[e];
+  if (t < 32) {
+    const float w = P.w32[t];
+    wnew[t] = w;
+    wsh[t] = t == kLabelCol ? 0.0f : w * ((FP8 && t < d_feat) ? inv_s : 1.0f);
+  }
+  if (t == 0) {
+    s_done = *P.done;
+    s_ok = 1;
+  }
+  __syncthreads();
+  const float cw0 = class_w[0], cw1 = class_w[1];
+  // wave wv of block b is wave wv * B + b of the per-step grid: the waves that carry the pick tiles
+  // (the low wave indices) spread over every CU instead of filling the first ones
+  const int64_t wave = (int64_t)wv * gridDim.x + blockIdx.x;
+  const bool active = wave < P.Gw;
+  const int64_t n = pass_stored_rows<VIRT>(0, row_end, sv, hole);
+  const int64_t step_rows = P.Gw * 64 * P.nb;
+  uint4 pre[4];
+  bool have_pre = false;
+  constexpr int kPreLams = 32;
+  PickIn<4, kPreLams> ppre;  // the wave's next pick tile, loaded before the barrier
+  bool have_ppre = false;
+  const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
+  const int64_t ntile = (npick + 15) >> 4;
+  unsigned touch = 0;  // FDX_PERSIST_PREFETCH 2: the dummy destination of the L2 touch loads
+  unsigned arrivals = 0;
+  auto phase_of = [&](int st) {
+    const int ep = st / P.nb, pos = st % P.nb;
+    return (P.serpentine && (ep & 1)) ? P.nb - 1 - pos : pos;
+  };
+  auto prefetch = [&](int st) {  // the wave's first tile(s) of step st: rows do not depend on w
+    have_pre = false;
+    have_ppre = false;
+    if (kPersistPrefetch == 0 || !active || st >= P.s1) return;
+    if constexpr (VIRT) {  // the inputs of the wave's first pick tile of step st
+      const int64_t pt = wave * P.nb + phase_of(st);
+      if (pt < ntile) {
+        const int64_t p = pt * 16 + (lane >> 2);
+        pick_load<4, kPreLams>(sv, p < npick ? p : -1, lane & 3, ppre);
+        have_ppre = true;
+      }
+    }
+    const int64_t base = ((int64_t)phase_of(st) * P.Gw + wave) * 64;
+    if (kPersistPrefetch == 3 || base >= n) return;
+    if constexpr (kPersistPrefetch == 2) {
+      // L2 touch: one dword per row of the first tile, into a register nobody reads (held until
+      // the next step's explicit vmcnt(0) so the compiler never reuses it while in flight)
+      const int64_t row = base + lane;
+      if (row < n) {
+        const int64_t ph = row + (row >= hole.at ? hole.len : 0);
+        const char* a = static_cast<const char*>(X) + ph * (FP8 ? 32 : 64);
+        asm volatile("global_load_dword %0, %1, off" : "=v"(touch) : "v"(a) : "memory");
+      }
+      return;
+    }
+    if constexpr (FP8) {
+      const uint8_t* X8 = static_cast<const uint8_t*>(X);
+      uint4 a[2], b[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+      fp8_load_tile(X8, 0, n, hole, base, a);
+      if (base + step_rows < n) fp8_load_tile(X8, 0, n, hole, base + step_rows, b);
+      pre[0] = a[0]; pre[1] = a[1]; pre[2] = b[0]; pre[3] = b[1];
+    } else {
+      bf16_load_tile(X, 0, n, hole, base, pre);
+    }
+    have_pre = true;
+  };
+
+  for (int st = P.s0; st < P.s1 && !s_done; ++st) {
+    if constexpr (kPersistPrefetch == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(touch) : : "memory");
+    const int ep = st / P.nb, pos = st % P.nb, b = phase_of(st);
+    unsigned long long* acc = accs + (st % 3) * kSgdAccWords;
+    if (blockIdx.x == 0 && wv == 0) {  // set st + 1 (read as set st - 2 before barrier st - 1)
+      unsigned long long* nx = accs + ((st + 1) % 3) * kSgdAccWords;
+      for (int e = lane; e < kSgdAccWords; e += kWave)
+        __hip_atomic_store(nx + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- the pass over minibatch b (this wave's share) ----
+    float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f, dacc = 0.0f;
+    f32x16_t hacc = {};
+    if constexpr (FP8) {
+      const int q = lane & 1;
+      f32x2_t wl[8], g[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        wl[p] = f32x2_t{wsh[16 * q + 2 * p], wsh[16 * q + 2 * p + 1]};
+        g[p] = f32x2_t{0.0f, 0.0f};
+      }
+      if (active)
+        fp8_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(static_cast<const uint8_t*>(X), 0, row_end, wl, wsh, x_scale, cw0, cw1, 1,
+                                         P.nb, b, sv, hole, wave, P.Gw, nullptr, g, lacc, wacc, whacc, dacc, hacc,
+                                         pre, have_pre, ppre, have_ppre);
+      float gs[16];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int col = 16 * q + 2 * p + e;
+          gs[2 * p + e] = strided_sum<2>(g[p][e]) * (col < d_feat ? inv_s : 1.0f);
+        }
+      }
+      if (lane < 2) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) red[wv][16 * lane + j] = gs[j];
+      }
+    } else {
+      const int q = lane & 3;
+      float wl[8], g[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        wl[j] = wsh[q * 8 + j];
+        g[j] = 0.0f;
+      }
+      if (active)
+        bf16_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(X, 0, row_end, wl, cw0, cw1, 1, P.nb, b, sv, hole, wave, P.Gw, nullptr, g,
+                                          lacc, wacc, whacc, dacc, hacc, pre, have_pre, ppre, have_ppre);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
+      if (lane < 4) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) red[wv][8 * lane + j] = g[j];
+      }
+    }
+    lacc = wave_sum(lacc);
+    wacc = wave_sum(wacc);
+    dacc = wave_sum(dacc);
+    if (lane == 0) {
+      red[wv][32] = lacc;
+      red[wv][33] = wacc;
+      red[wv][34] = 0.0f;
+      red[wv][35] = dacc;
+    }
+    __syncthreads();
+    if (wv != 0) {
+      prefetch(st + 1);
+    } else {
+      // sgd_fused_tail's per-wave fixed point (inactive waves hold zeros)
+      const long long qs = lane < kSgdSlots ? wave_sums_fixed<kPersistWaves>(red, P.aff, lane) : 0;
+      prefetch(st + 1);  // in flight beside the adds: the arrival waits for both
+      if (lane < kSgdSlots && lane != 34 && qs != 0)
+        __hip_atomic_fetch_add(acc + (blockIdx.x % kSgdReplicas) * 36 + lane, (unsigned long long)qs,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      arrivals += gridDim.x;
+      if (P.stamps != nullptr && lane == 0)
+        P.stamps[((int64_t)(st - P.s0) * 3 + 0) * gridDim.x + blockIdx.x] = wall_clock64();
+      const bool ok = persist_barrier(bar, arrivals, lane);
+      if (!ok && lane == 0) s_ok = 0;
+      if (P.stamps != nullptr && lane == 0)
+        P.stamps[((int64_t)(st - P.s0) * 3 + 1) * gridDim.x + blockIdx.x] = wall_clock64();
+    }
+    __syncthreads();
+    if (!s_ok) break;  // uniform in the block
+    // ---- the update, redundantly in every block ----
+    for (int e = t; e < kSgdAccWords; e += kPersistThreads)
+      rep[e] = __hip_atomic_load(acc + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (t < kSgdSlots) {  // fixed-order fold of the replicas (integer: exact in any order anyway)
+      unsigned long long q = 0;
+#pragma unroll 8
+      for (int r = 0; r < kSgdReplicas; ++r) q += rep[r * 36 + t];
+      rd[t] = (double)(long long)q * (1.0 / kFixScale);
+    }
+    __syncthreads();
+    SgdArgs a;
+    a.d = P.d;
+    a.C = P.C;
+    a.c = P.lr[ep];
+    a.momentum = P.momentum;
+    a.fit_intercept = P.fit_intercept;
+    a.nb = P.nb;
+    a.avg = P.average && ep == P.epochs - 1;
+    a.epoch_end = pos == P.nb - 1;
+    a.tol = P.tol;
+    sgd_apply(rd, sst, wnew, &s_done, P.aff, a, t, true);
+    __syncthreads();
+    if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);
+    __syncthreads();
+    if (P.stamps != nullptr && t == 0)
+      P.stamps[((int64_t)(st - P.s0) * 3 + 2) * gridDim.x + blockIdx.x] = wall_clock64();
+  }
+  if (blockIdx.x == 0) {  // every block holds the same state: block 0 publishes it
+    if (t == 0 && !s_ok) sst[kSgdFault] = 1.0;
+    __syncthreads();
+    for (int e = t; e < kStateSize; e += kPersistThreads) P.st[e] = sst[e];
+    if (t < 32) P.w32[t] = wnew[t];
+    if (t == 0) *P.done = s_done;
+  }
+}
+
 }  // namespace
 
 // Grid = resident capacity of the Hessian pass (blocks/CU from the occupancy query x CUs): a
@@ -1286,7 +1700,10 @@ int logreg_pass_blocks(int fmt) {
     int occ = 0;
     hipError_t e = fmt ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_fp8w_kernel<true>, kThreads, 0)
                        : hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, logreg_pass_kernel<true>, kThreads, 0);
-    if (e == hipSuccess && occ > 0) per_cu = occ;
+    // at most 3 per CU (12 waves): the SGD minibatch partition is defined on this grid (ops/logreg
+    // sgd_grid_blocks; the CPU mirror assumes 768 blocks on 256 CUs) and the persistent SGD launch
+    // maps its 12-wave blocks onto it -- it must not move with the compiler's register allocation
+    if (e == hipSuccess && occ > 0) per_cu = occ < 3 ? occ : 3;
   }
   int c = cus * per_cu;
   if (c < 64) c = 64;
@@ -1468,6 +1885,128 @@ void launch_sgd_update(const double* red, double* state, float* w32, int* done, 
                        const SgdArgs& a, hipStream_t stream) {
   sgd_update_kernel<<<1, 64, 0, stream>>>(red, state, w32, done, aff, a);
   check_launch("sgd_update");
+}
+
+void launch_sgd_pass_sums(const void* X, int fp8, float x_scale, int64_t row_end, const float* w32,
+                          const float* class_w, const int* done, int row_sub, int row_phase, int nblocks,
+                          const SmoteView* sv, RowHole hole, unsigned long long* acc, unsigned int* ticket,
+                          long long* sums, const double* aff, hipStream_t stream) {
+  if (row_sub < 1 || row_phase < 0 || row_phase >= row_sub) throw std::runtime_error("sgd_pass_sums: bad phase");
+  if (sums == nullptr || acc == nullptr || ticket == nullptr) throw std::runtime_error("sgd_pass_sums: null buffer");
+  const SmoteView v = checked_view(sv, 0, row_end);
+  check_hole(hole, 0, v.parents != nullptr ? v.n_real : row_end);
+  SgdFuse fz;
+  fz.acc = acc;
+  fz.ticket = ticket;
+  fz.aff = aff;
+  fz.sums = sums;
+  const bool virt = v.parents != nullptr;
+  float* w = const_cast<float*>(w32);
+  if (fp8) {
+    const uint8_t* X8 = static_cast<const uint8_t*>(X);
+    if (virt)
+      logreg_pass_fp8w_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X8, 0, row_end, w, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+    else
+      logreg_pass_fp8w_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X8, 0, row_end, w, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+  } else {
+    if (virt)
+      logreg_pass_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X, 0, row_end, w, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+    else
+      logreg_pass_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
+          X, 0, row_end, w, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+  }
+  check_launch("sgd_pass_sums");
+}
+
+void launch_sgd_update_fixed(const long long* sums, double* state, float* w32, int* done, const double* aff,
+                             const SgdArgs& a, hipStream_t stream) {
+  sgd_update_fixed_kernel<<<1, 64, 0, stream>>>(sums, state, w32, done, aff, a);
+  check_launch("sgd_update_fixed");
+}
+
+int sgd_full_blocks() {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int dev = 0, cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+      cus = prop.multiProcessorCount;
+    blocks = 2 * cus;
+  }
+  return blocks;
+}
+
+int sgd_persist_blocks(int grid_blocks) {
+  static int capacity = -1;
+  if (capacity < 0) {
+    int dev = 0, cus = 0, occ = 0;
+    capacity = 0;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      hipDeviceProp_t prop;
+      if (hipGetDeviceProperties(&prop, dev) == hipSuccess) cus = prop.multiProcessorCount;
+      int o1 = 0, o2 = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o1, sgd_persist_kernel<false, true>, kPersistThreads, 0) ==
+              hipSuccess &&
+          hipOccupancyMaxActiveBlocksPerMultiprocessor(&o2, sgd_persist_kernel<true, true>, kPersistThreads, 0) ==
+              hipSuccess)
+        occ = o1 < o2 ? o1 : o2;
+      // one block per CU whatever the query says (8 waves = 2 per SIMD: the 256-VGPR budget the
+      // persistent step needs for its prefetched pick and tile across the barrier)
+      capacity = cus * (occ >= 1 ? 1 : 0);
+    }
+  }
+  if (grid_blocks < 1) return 0;
+  const int blocks = (grid_blocks * kWaves + kPersistWaves - 1) / kPersistWaves;
+  return blocks <= capacity ? blocks : 0;
+}
+
+void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
+                        const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream) {
+  if (a.nb < 1 || a.epochs < 1 || a.epochs > kSgdMaxEpochs || a.s0 < 0 || a.s1 > a.nb * a.epochs || a.s0 >= a.s1)
+    throw std::runtime_error("sgd_persist: bad schedule");
+  if (a.Gw < kWaves || a.Gw % kWaves != 0) throw std::runtime_error("sgd_persist: bad pass grid");
+  if (a.ws == nullptr || a.st == nullptr || a.w32 == nullptr || a.done == nullptr)
+    throw std::runtime_error("sgd_persist: null buffer");
+  const int blocks = sgd_persist_blocks((int)(a.Gw / kWaves));
+  if (blocks == 0) throw std::runtime_error("sgd_persist: the grid cannot be resident (launch per step)");
+  const SmoteView v = checked_view(sv, 0, row_end);
+  check_hole(hole, 0, v.parents != nullptr ? v.n_real : row_end);
+  // barrier shards and every accumulator set: zero per call (stream-ordered before the launch)
+  if (hipMemsetAsync(a.ws, 0, sizeof(unsigned long long) * kSgdPersistWords, stream) != hipSuccess)
+    throw std::runtime_error("sgd_persist: memset failed");
+  const bool virt = v.parents != nullptr;
+  static const int cfg = [] {  // lab switch: "lams,pf"
+    const char* e = std::getenv("FDX_SGD_PERSIST_CFG");
+    int l = 16, p = 2;
+    if (e != nullptr) std::sscanf(e, "%d,%d", &l, &p);
+    return (l >= 32 ? 100 : 0) + p;
+  }();
+#define FDX_SGDP(F, V, L, PF) \
+  sgd_persist_kernel<F, V, L, PF><<<blocks, kPersistThreads, 0, stream>>>(X, row_end, x_scale, class_w, v, hole, a)
+#define FDX_SGDP_CFG(F)                              \
+  switch (cfg) {                                     \
+    case 0: FDX_SGDP(F, true, 16, 0); break;         \
+    case 1: FDX_SGDP(F, true, 16, 1); break;         \
+    case 3: FDX_SGDP(F, true, 16, 3); break;         \
+    case 100: FDX_SGDP(F, true, 32, 0); break;       \
+    case 101: FDX_SGDP(F, true, 32, 1); break;       \
+    case 102: FDX_SGDP(F, true, 32, 2); break;       \
+    case 103: FDX_SGDP(F, true, 32, 3); break;       \
+    default: FDX_SGDP(F, true, 16, 2); break;        \
+  }
+  if (fp8) {
+    if (virt) { FDX_SGDP_CFG(true) }
+    else FDX_SGDP(true, false, 16, 2);
+  } else {
+    if (virt) { FDX_SGDP_CFG(false) }
+    else FDX_SGDP(false, false, 16, 2);
+  }
+#undef FDX_SGDP_CFG
+#undef FDX_SGDP
+  check_launch("sgd_persist");
 }
 
 }  // namespace fdx

@@ -142,15 +142,20 @@ def quantile_cuts(X: torch.Tensor, max_bin: int = MAX_BIN, sample_rows: int = 1 
     return R.cuts_from_sorted_picks(picks[1:], picks[0], max_bin)
 
 
-def bin_rows(X: torch.Tensor, cuts: np.ndarray, nbins: np.ndarray) -> torch.Tensor:
-    """u8 [n, 32] bins (features in bytes 0..d-1)."""
+def bin_rows(X: torch.Tensor, cuts: np.ndarray, nbins: np.ndarray, out: torch.Tensor | None = None) -> torch.Tensor:
+    """u8 [n, 32] bins (features in bytes 0..d-1).  ``out``: a [n, 32] u8 view to write (e.g. the
+    SMOTE tail of a binned table)."""
     n, d = X.shape
+    if out is not None and (tuple(out.shape) != (n, R.ROW_BYTES) or out.dtype != torch.uint8
+                            or not out.is_contiguous() or out.device != X.device):
+        raise ValueError("out must be a contiguous u8 [n, 32] tensor on X's device")
     if not X.is_cuda:
-        return torch.from_numpy(R.bin_rows(X.numpy(), cuts, nbins))
+        b = torch.from_numpy(R.bin_rows(X.numpy(), cuts, nbins))
+        return out.copy_(b) if out is not None else b
     if X.dtype != torch.float32 or X.stride(1) != 1:
         raise ValueError("X must be float32 with unit column stride")
     m = native()
-    out = torch.empty((n, R.ROW_BYTES), dtype=torch.uint8, device=X.device)
+    out = out if out is not None else torch.empty((n, R.ROW_BYTES), dtype=torch.uint8, device=X.device)
     ct = torch.from_numpy(np.ascontiguousarray(cuts[:d])).to(X.device)
     nt = torch.from_numpy(np.ascontiguousarray(nbins[:d])).to(X.device)
     if n:
@@ -201,37 +206,55 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
 
     ``checkpoint``: a utils.checkpoint.CheckpointManager.  Every ``checkpoint_every`` rounds the
     trees so far are saved; a later call with the same data/config resumes after the last saved
-    round.  Training margins are recomputed from the saved trees (bins and float thresholds agree
-    exactly), so a resumed fit is bit-identical to an uninterrupted one."""
+    round.  Training margins are recomputed from the saved trees over the same bins, so a resumed
+    fit is bit-identical to an uninterrupted one."""
     p = (params or GBDTParams()).validate()
     n, d = X.shape
     if d > MAX_FEAT:
         raise ValueError(f"at most {MAX_FEAT} features")
-    if y.dtype != torch.uint8 or y.shape[0] != n:
-        raise ValueError("y must be uint8 [n]")
     if cuts is None:
         cuts = quantile_cuts(X, p.max_bin, p.cut_sample_rows, comm)
+    bins = bin_rows(X, cuts[0], cuts[1])
+    return fit_binned(bins, y, cuts, p, comm=comm, sample_weight_pos=sample_weight_pos, return_margin=return_margin,
+                      checkpoint=checkpoint, checkpoint_every=checkpoint_every, use_graph=use_graph)
+
+
+def fit_binned(bins: torch.Tensor, y: torch.Tensor, cuts, params: GBDTParams | None = None, comm=None,
+               sample_weight_pos: float | None = None, return_margin: bool = False, checkpoint=None,
+               checkpoint_every: int = 10, use_graph: bool | None = None, hole: tuple | None = None):
+    """Boosting on already-binned rows (u8 [n, 32], bin_rows) with their cuts (cuts, nbins).
+
+    ``hole``: (at, len) -- the fit's rows are the table without the block [at, at + len) (a
+    cross-validation fold on the fold-sorted table: no per-fold copy).  The returned margin (with
+    ``return_margin``) covers EVERY table row, so the block's margins are the fold's validation
+    scores under the fitted ensemble."""
+    p = (params or GBDTParams()).validate()
     cuts_np, nbins = cuts
+    d = int(len(nbins))
+    n = int(bins.shape[0])  # table rows (the margin walk covers all of them)
+    if d > MAX_FEAT:
+        raise ValueError(f"at most {MAX_FEAT} features")
+    if y.dtype != torch.uint8 or y.shape[0] != n:
+        raise ValueError("y must be uint8 [n] (one label per table row)")
+    ha, hl = (int(hole[0]), int(hole[1])) if hole else (0, 0)
+    if ha < 0 or hl < 0 or ha + hl > n:
+        raise ValueError(f"hole {hole} outside the {n} table rows")
+    n_fit = n - hl
     spw = float(p.scale_pos_weight if sample_weight_pos is None else sample_weight_pos)
     gscale, hscale = R.grad_scales(spw)
     D = p.max_depth
     ni, nl = (1 << D) - 1, 1 << D
     T = p.n_estimators
     base_margin = float(np.log(p.base_score / (1.0 - p.base_score)))
-    bins = bin_rows(X, cuts_np, nbins)
     ens_kw = dict(depth=D, cuts=cuts_np, nbins=nbins, base_score=p.base_score, params=dict(p.__dict__))
     sig = None
     if checkpoint is not None:
         from ..utils.checkpoint import config_signature
 
-        n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
+        n_all = int(comm.all_reduce_scalar(float(n_fit))) if (comm is not None and comm.world_size > 1) else n_fit
         sig = config_signature(params={k: v for k, v in p.__dict__.items() if k != "n_estimators"}, spw=spw,
-                               cuts=cuts_np, nbins=nbins, n=n_all, d=d)
+                               cuts=cuts_np, nbins=nbins, n=n_all, d=d, **({"hole": [ha, hl]} if hl else {}))
     prev, t0 = _resume(checkpoint, sig, T)
-
-    def _partial(t_done, feat, binv, thr, gain, leaf):
-        return TreeEnsemble(feat=feat[:t_done], bin=binv[:t_done], thr=thr[:t_done], gain=gain[:t_done],
-                            leaf=leaf[:t_done], **ens_kw)
 
     def _save(t_done, feat, binv, thr, gain, leaf):
         if checkpoint is not None and t_done > 0:
@@ -242,15 +265,17 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             if fault.startswith("gbdt_crash_after_trees=") and t_done >= int(fault.split("=", 1)[1]):
                 os._exit(17)  # simulated lost rank right after a checkpoint (resume tests)
 
-    if not X.is_cuda:
+    if not bins.is_cuda:
         feat = np.zeros((T, ni), np.int32); binv = np.zeros((T, ni), np.int32)
         thr = np.zeros((T, ni), np.float32); gain = np.zeros((T, ni)); leaf = np.zeros((T, nl), np.float32)
-        b = bins.numpy()
-        yy = y.numpy()
-        margin = np.full(n, np.float32(base_margin), np.float32)
+        b_all = bins.numpy()
+        y_all = y.numpy()
+        keep = np.r_[0:ha, ha + hl:n]
+        b, yy = b_all[keep], y_all[keep]
+        margin = np.full(n_fit, np.float32(base_margin), np.float32)
         if t0:
             feat[:t0], binv[:t0], thr[:t0], gain[:t0], leaf[:t0] = (prev[k] for k in ("feat", "bin", "thr", "gain", "leaf"))
-            margin = R.predict_margin(X.numpy(), feat[:t0], thr[:t0], leaf[:t0], D, base_margin)
+            margin = R.predict_margin_bins(b, feat[:t0], binv[:t0], leaf[:t0], D, base_margin)
         for t in range(t0, T):
             q = R.gradients(margin, yy, spw, gscale, hscale)
             tr, node = R.build_tree(b, q, cuts_np, nbins, D, p.reg_lambda, p.min_child_weight, p.gamma,
@@ -260,18 +285,25 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
             if (t + 1) % max(1, checkpoint_every) == 0 or t + 1 == T:
                 _save(t + 1, feat, binv, thr, gain, leaf)
         ens = TreeEnsemble(feat=feat, bin=binv, thr=thr, gain=gain, leaf=leaf, **ens_kw)
-        return (ens, torch.from_numpy(margin)) if return_margin else ens
+        if not return_margin:
+            return ens
+        full = np.empty(n, np.float32)
+        full[keep] = margin
+        if hl:
+            full[ha:ha + hl] = R.predict_margin_bins(b_all[ha:ha + hl], feat, binv, leaf, D, base_margin)
+        return ens, torch.from_numpy(full)
 
     m = native()
-    dev = X.device
+    dev = bins.device
+    st0 = stream_of(bins)
     ws = _Workspace(n, D, dev)
     # feature-major copy of the bins for the partition's one-byte-per-row reads (gbdt.hip)
     ldt = max(4, (n + 255) // 256 * 256)
     binsT = torch.empty(d * ldt, dtype=torch.uint8, device=dev)
     if n:
-        m.gbdt_transpose(ptr(bins), n, d, ptr(binsT), ldt, stream_of(X))
+        m.gbdt_transpose(ptr(bins), n, d, ptr(binsT), ldt, st0)
     dist = comm is not None and comm.world_size > 1
-    n_global = int(comm.all_reduce_scalar(float(n))) if dist else n
+    n_global = int(comm.all_reduce_scalar(float(n_fit))) if dist else n_fit
     ct = torch.from_numpy(np.ascontiguousarray(cuts_np[:d])).to(dev)
     nt = torch.from_numpy(np.ascontiguousarray(nbins[:d])).to(dev)
     feat = torch.empty((T, ni), dtype=torch.int32, device=dev)
@@ -283,7 +315,9 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
     if t0:
         for name, dst in (("feat", feat), ("bin", binv), ("thr", thr), ("gain", gain), ("leaf", leaf)):
             dst[:t0].copy_(torch.from_numpy(np.ascontiguousarray(prev[name])))
-        margin = predict_margin(X, _partial(t0, prev["feat"], prev["bin"], prev["thr"], prev["gain"], prev["leaf"]))
+        for t in range(t0):  # the margins of the saved trees, by the round's own margin kernel
+            m.gbdt_margin(ptr(binsT), ldt, n, ptr(feat[t]), ptr(binv[t]), ptr(leaf[t]), D, ptr(margin), ptr(y), spw,
+                          gscale, hscale, 0, st0)
     lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
     ginv, hinv = 1.0 / gscale, 1.0 / hscale
 
@@ -291,32 +325,32 @@ def fit(X: torch.Tensor, y: torch.Tensor, params: GBDTParams | None = None, comm
         """One boosting round: a fixed launch sequence with static pointers (graph-capturable).
         The gradients of a round come from the previous round's margin update (gbdt_margin with
         gh), so only the first round of a fit launches gbdt_grad."""
-        st = stream_of(X)  # the capture stream while a hipGraph is being recorded
+        st = stream_of(bins)  # the capture stream while a hipGraph is being recorded
         if grad_first:
             m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
         # zero histograms and per-node counts, root segment + global count: one launch (level 0
         # reads rows in order, so ridx / nid need no iota / root fill)
-        m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n, n_global, st,
+        m.gbdt_round_init(ptr(ws.hist), ws.hist.numel(), ptr(ws.seg), ptr(ws.gcnt), n_fit, n_global, st,
                           ptr(ws.node_r), ws.node_r.numel())
         cur = 0
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
             m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
-                        ptr(ws.hist), ptr(ws.slots), st, HIST_FLUSH_ROWS)
+                        ptr(ws.hist), ptr(ws.slots), st, HIST_FLUSH_ROWS, ha, hl)
             if dist:
                 comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,
                          ptr(o_feat), ptr(o_bin), ptr(o_thr), ptr(o_gain), ptr(ws.ng), ptr(ws.nh), st)
             if level == D - 1:
                 break  # leaves: the margin walk and gbdt_leaf (split-kernel child sums) need no partition
-            if n:
+            if n_fit:
                 # count + scatter; the scatter also writes the children's segments and counts (gcnt)
-                m.gbdt_partition(ptr(binsT), ldt, ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n, ptr(o_feat), ptr(o_bin),
+                m.gbdt_partition(ptr(binsT), ldt, ptr(ws.ridx[cur]), ptr(ws.nid[cur]), n_fit, ptr(o_feat), ptr(o_bin),
                                  level, ptr(ws.flag), ptr(ws.counts), PART_BLOCKS, ptr(ws.seg), ptr(ws.node_r),
-                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st, ptr(ws.gcnt))
+                                 ptr(ws.ridx[cur ^ 1]), ptr(ws.nid[cur ^ 1]), st, ptr(ws.gcnt), ha, hl)
             cur ^= 1
             c0 = 2 * h0 + 1
-            if not n:
+            if not n_fit:
                 ws.seg[2 * h0 + 1:2 * (h0 + nn) + 1].zero_()
                 ws.gcnt[c0:c0 + 2 * nn].zero_()
             if dist:

@@ -272,6 +272,8 @@ class LRWorkspace:
         # resident grid of each row format's Hessian pass (fp8 kernels hold more blocks per CU)
         self.nblocks = nblocks or m.logreg_pass_blocks(0)
         self.nblocks_fp8 = nblocks or m.logreg_pass_blocks(1)
+        # the SGD pass grid (2 blocks per CU, 512 on MI355X): its waves define the minibatch partition
+        self.sgd_blocks = nblocks or m.sgd_full_blocks()
         self.partial = torch.empty(max(self.nblocks, self.nblocks_fp8) * PART_STRIDE, device=device,
                                    dtype=torch.float32)
         self.red = torch.zeros(PART_STRIDE, device=device, dtype=torch.float64)
@@ -282,6 +284,10 @@ class LRWorkspace:
         # fused SGD steps: 32 replicas x 36 int64 fixed-point accumulators + the arrival ticket;
         # zero between steps (every step's last block swaps them back to zero)
         self.sgd_acc = torch.zeros(SGD_ACC_WORDS + 8, device=device, dtype=torch.int64)
+        # persistent SGD launch: barrier shards + 3 accumulator sets (zeroed by the launcher); the
+        # data-parallel lean step's folded fixed-point sums (the all-reduced vector)
+        self.sgd_persist = torch.zeros(int(m.SGD_PERSIST_WORDS), device=device, dtype=torch.int64)
+        self.sgd_sums = torch.zeros(SGD_SLOTS, device=device, dtype=torch.int64)
 
     def prepare_flags(self, depth: int = 2):
         """The mapped pinned convergence-flag words newton_fit polls (pinned allocations cost tens
@@ -635,13 +641,14 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     return PendingFit(ws.state, warm_iters=warm)
 
 
-def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm):
+def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine=False):
     from ..utils.checkpoint import config_signature
 
     n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
+    extra = {"serpentine": True} if serpentine else {}
     return config_signature(kind="sgd2", n=n_all, d=d, C=C, lr=list(lr), momentum=momentum, batches=nb,
                             epochs=epochs, average=bool(average), tol=tol, class_w=list(class_w),
-                            fit_intercept=fit_intercept)
+                            fit_intercept=fit_intercept, **extra)
 
 
 # Config 3's solver defaults (BASELINE.json: "SMOTE k-NN + logistic SGD").  Chosen on the bench
@@ -657,6 +664,19 @@ SGD_TOL = 1e-3                # on the epoch gradient max-norm (sklearn SGDClass
 SGD_SLOTS = 36
 
 
+SGD_MAX_EPOCHS = 8  # launchers.h kSgdMaxEpochs (per-epoch step scalars of the persistent launch)
+
+
+def _sgd_phase(pos: int, ep: int, nb: int, serpentine: bool) -> int:
+    """Minibatch visited at position ``pos`` of epoch ``ep`` (logreg.hip sgd_persist_kernel phase_of)."""
+    return nb - 1 - pos if (serpentine and ep % 2 == 1) else pos
+
+
+def _persist_default() -> bool:
+    import os
+    return os.environ.get("FDX_SGD_PERSIST", "1") != "0"
+
+
 def _epoch_lr(lr, ep: int) -> float:
     if np.ndim(lr) == 0:
         return float(lr)
@@ -669,7 +689,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             class_w=(1.0, 1.0), w0=None, d: int = 30, fit_intercept: bool = True, comm=None,
             fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None, checkpoint=None,
             checkpoint_every: int = 0, affine: torch.Tensor | None = None, virtual: VirtualSmote | None = None,
-            batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None):
+            batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None,
+            persistent: bool | None = None, serpentine: bool = False, _stamps: torch.Tensor | None = None):
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
@@ -692,7 +713,12 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     matching checkpoint is resumed from.  ``affine``: pivot-shifted rows (fused scaler pass), as in
     newton_fit.  ``virtual``: the SMOTE samples after ``rows`` (VirtualSmote).  ``max_steps``: stop
     after that many steps of the schedule (a simulated interruption for the resume tests).
-    ``hole``: (at, len) stored rows the fit steps over (newton_fit)."""
+    ``hole``: (at, len) stored rows the fit steps over (newton_fit).
+    ``persistent``: one process, the whole schedule in ONE launch (logreg.hip sgd_persist_kernel:
+    a grid barrier per step instead of a launch per step; bitwise the same fit).  Default on
+    unless FDX_SGD_PERSIST=0.  ``serpentine``: odd epochs visit the minibatches in reverse order
+    (persistent launch only), so an epoch's first minibatches are the previous epoch's last ones
+    -- still resident in the 256 MB Infinity Cache."""
     check_rows(rows)
     w0 = _default_w0(w0)
     rows, hole = _apply_hole(rows, hole)
@@ -714,21 +740,22 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             vr[:, LABEL_COL] = virtual.label
             return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept,
                                 comm, fp8_scale, checkpoint, checkpoint_every, None, None, virtual=(virtual, vr),
-                                max_steps=max_steps)
+                                max_steps=max_steps, serpentine=serpentine)
         affine = None
     aff = 0
     if affine is not None:
         if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
-    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm)
+    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine)
            if checkpoint else None)
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
     if not rows.is_cuda:
         vv = (virtual, virtual.rows_f32()) if virtual is not None else None
         return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm,
-                            fp8_scale, checkpoint, checkpoint_every, sig, got, virtual=vv, max_steps=max_steps)
+                            fp8_scale, checkpoint, checkpoint_every, sig, got, virtual=vv, max_steps=max_steps,
+                            serpentine=serpentine)
     if virtual is not None:
         virtual.check(rows)
         if class_w[1] > VIRTUAL_MAX_WEIGHT:
@@ -751,19 +778,34 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         # updates are no-ops, as in the uninterrupted fit (reset() cleared the device flag)
         ws.done.fill_(int(float(got[0]["state"][S_CONV]) > 0))
     fp8 = storage_kind(rows) != "bf16"
-    blocks = ref.sgd_grid_blocks(n_stored, nb, ws.nblocks_fp8 if fp8 else ws.nblocks)
+    blocks = ref.sgd_grid_blocks(n_stored, nb, ws.sgd_blocks)
     dp = comm is not None and comm.world_size > 1
     v = virtual
     mq, k = (v.nbr.shape if v is not None else (0, 1))
 
+    vargs = (ptr(v.parents) if v else 0, ptr(v.nbr) if v else 0, ptr(v.lam) if v else 0,
+             ptr(v.off) if v else 0, ptr(v.cnt) if v else 0, int(rows.shape[0]),
+             int(v.q_offset) if v else 0, int(mq), int(k), int(hole[0]), int(hole[1]))
+    persist = (persistent if persistent is not None else _persist_default()) and not dp
+    persist = persist and epochs <= SGD_MAX_EPOCHS and m.sgd_persist_blocks(blocks) > 0
+
     def run_steps(s0: int, s1: int):
-        """Steps [s0, s1) of the schedule, one fused launch each (FISH pass whose last block
-        applies the update), enqueued by one native call."""
+        """Steps [s0, s1) of the schedule: ONE persistent launch (a grid barrier per step, the
+        update in every block), or one fused launch per step (FISH pass whose last block applies
+        the update) -- bitwise the same fit."""
+        if s1 <= s0:
+            return
+        if persist:
+            m.sgd_persist(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.class_w), *vargs,
+                          ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
+                          float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
+                          int(bool(serpentine)), [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(s1),
+                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0)
+            return
+        if serpentine:
+            raise ValueError("serpentine minibatch order needs the persistent SGD launch")
         m.sgd_run(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w), ptr(ws.done),
-                  ptr(ws.partial), blocks, s,
-                  ptr(v.parents) if v else 0, ptr(v.nbr) if v else 0, ptr(v.lam) if v else 0,
-                  ptr(v.off) if v else 0, ptr(v.cnt) if v else 0, int(rows.shape[0]),
-                  int(v.q_offset) if v else 0, int(mq), int(k), int(hole[0]), int(hole[1]), ptr(ws.state), aff, d,
+                  ptr(ws.partial), blocks, s, *vargs, ptr(ws.state), aff, d,
                   float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
                   [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
                   ptr(ws.sgd_acc[SGD_ACC_WORDS:]))
@@ -774,22 +816,26 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         return PendingFit(ws.state, sgd=True)
     for ep in range(start[0], epochs):
         c = lrs[ep]
-        for b in range(start[1] if ep == start[0] else 0, nb):
-            if max_steps is not None and ep * nb + b >= max_steps:
+        for pos in range(start[1] if ep == start[0] else 0, nb):
+            if max_steps is not None and ep * nb + pos >= max_steps:
                 break
+            b = _sgd_phase(pos, ep, nb, serpentine)
             avg = int(average and ep == epochs - 1)
-            last = b + 1 == nb
+            last = pos + 1 == nb
             if dp:
-                _sgd_pass(m, rows, ws, n, fp8_scale, s, b, nb, blocks, virtual, hole)
-                m.logreg_reduce(ptr(ws.partial), blocks, SGD_SLOTS, ptr(ws.red), ptr(ws.done), s)
-                comm.all_reduce_(ws.red[:SGD_SLOTS])
-                m.sgd_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
-                             float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
-            else:  # the same fused launch as the uninterrupted fit: checkpointed fits stay bit-identical
-                run_steps(ep * nb + b, ep * nb + b + 1)
-            gstep = ep * nb + b + 1
+                # lean step: the pass leaves its fixed-point sums (int64: the all-reduce is exact and
+                # order-free, every rank gets bitwise the same vector), one collective, the update
+                m.sgd_pass_sums(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w),
+                                ptr(ws.done), nb, b, blocks, *vargs, ptr(ws.sgd_acc),
+                                ptr(ws.sgd_acc[SGD_ACC_WORDS:]), ptr(ws.sgd_sums), aff, s)
+                comm.all_reduce_(ws.sgd_sums)
+                m.sgd_update_fixed(ptr(ws.sgd_sums), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
+                                   float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
+            else:  # the same kernels as the uninterrupted fit: checkpointed fits stay bit-identical
+                run_steps(ep * nb + pos, ep * nb + pos + 1)
+            gstep = ep * nb + pos + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
-                nxt = (ep + 1, 0) if last else (ep, b + 1)
+                nxt = (ep + 1, 0) if last else (ep, pos + 1)
                 checkpoint.save(gstep, {"state": ws.state},
                                 {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
     return PendingFit(ws.state, sgd=True)
@@ -831,7 +877,7 @@ def sgd_minibatch_sums(rows: torch.Tensor, w: torch.Tensor, nb: int, phase: int,
         virtual.prepare()
         n += virtual.n_new
     fp8 = storage_kind(rows) != "bf16"
-    blocks = blocks or ref.sgd_grid_blocks(rows.shape[0], nb, ws.nblocks_fp8 if fp8 else ws.nblocks)
+    blocks = blocks or ref.sgd_grid_blocks(rows.shape[0], nb, ws.sgd_blocks)
     s = stream_of(rows)
     _sgd_pass(m, rows, ws, n, fp8_scale, s, phase, nb, blocks, virtual)
     m.logreg_reduce(ptr(ws.partial), blocks, SGD_SLOTS, ptr(ws.red), 0, s)
@@ -840,7 +886,12 @@ def sgd_minibatch_sums(rows: torch.Tensor, w: torch.Tensor, nb: int, phase: int,
             "blocks": blocks}
 
 
+S_SGD_FAULT = 229  # logreg.hip kSgdFault: the persistent SGD launch's grid barrier timed out
+
+
 def _info_from_state(st: np.ndarray, sgd: bool = False) -> FitInfo:
+    if sgd and st[S_SGD_FAULT] != 0:
+        raise RuntimeError("persistent SGD launch: a grid barrier timed out (not every block was resident)")
     return FitInfo(w=st[S_W:S_W + 32].copy(), n_iter=int(st[S_ITER]), n_newton_steps=0 if sgd else int(st[S_NACC]),
                    converged=bool(st[S_CONV] > 0), objective=float(st[S_OBJ]), grad_max=float(st[S_GMAX]))
 
@@ -869,13 +920,14 @@ def _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm,
 
 
 def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm, fp8_scale,
-                 checkpoint=None, checkpoint_every=0, sig=None, got=None, virtual=None, max_steps=None):
+                 checkpoint=None, checkpoint_every=0, sig=None, got=None, virtual=None, max_steps=None,
+                 serpentine=False):
     """The device SGD's algorithm in fp64 (ref.SgdStateRef) over the same minibatch partition:
-    stored row tiles by the pass grid's strided walk (the full 768-block grid of a 256-CU part,
-    shrunk for small shards like the device), virtual samples by their pick tile."""
+    stored row tiles by the pass grid's strided walk (the full SGD grid of a 256-CU part,
+    ref.SGD_FULL_BLOCKS, shrunk for small shards like the device), virtual samples by their pick tile."""
     R = ref.rows_to_f32(rows, fp8_scale, d).double().numpy()
     n_stored = R.shape[0]
-    rb = ref.sgd_row_batches(n_stored, nb, ref.sgd_grid_blocks(n_stored, nb, 768))
+    rb = ref.sgd_row_batches(n_stored, nb, ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS))
     parts = [R]
     bs = [rb]
     if virtual is not None:
@@ -899,9 +951,10 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
         st.done = st.converged
         start = (int(got[1]["epoch"]), int(got[1]["batch"]))
     for ep in range(start[0], epochs):
-        for b in range(start[1] if ep == start[0] else 0, nb):
-            if max_steps is not None and ep * nb + b >= max_steps:
+        for pos in range(start[1] if ep == start[0] else 0, nb):
+            if max_steps is not None and ep * nb + pos >= max_steps:
                 break
+            b = _sgd_phase(pos, ep, nb, serpentine)
             Rb = R[members[b]]
             g, loss, wsum, _ = ref.logreg_pass(Rb, st.w, class_w, False)
             X = Rb.copy()
@@ -913,16 +966,16 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
             red = np.concatenate([g, [loss, wsum, 0.0, float(np.sum(sw * p * (1 - p)))]])
             if comm is not None and comm.world_size > 1:
                 red = comm.all_reduce(torch.from_numpy(red)).numpy()
-            last = b + 1 == nb
+            last = pos + 1 == nb
             st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nb,
                     bool(average and ep == epochs - 1), last, tol, fit_intercept)
-            gstep = ep * nb + b + 1
+            gstep = ep * nb + pos + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 sv = np.zeros(STATE_SIZE)
                 sv[S_W:S_W + 32], sv[S_VEL:S_VEL + 32], sv[160:192], sv[192:224] = st.w, st.v, st.avg, st.ep_g
                 sv[224], sv[225], sv[226], sv[S_ITER] = st.ep_loss, st.ep_w, st.n_avg, st.iter
                 sv[S_GMAX], sv[S_OBJ], sv[S_CONV] = st.gmax, st.obj, float(st.converged)
-                nxt = (ep + 1, 0) if last else (ep, b + 1)
+                nxt = (ep + 1, 0) if last else (ep, pos + 1)
                 checkpoint.save(gstep, {"state": sv},
                                 {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
     w = st.w.copy()

@@ -5,18 +5,17 @@ import numpy as np
 import torch
 
 from . import reference as ref
-from .layout import BIAS_COL, DEFAULT_FP8_SCALE, LABEL_COL, NCOLS, check_rows, storage_kind
+from .layout import BIAS_COL, DEFAULT_FP8_SCALE, NCOLS, check_rows, storage_kind
 from .native import native, ptr, stream_of
 
 
 def _w32(w: torch.Tensor, device) -> torch.Tensor:
-    w = w.to(device=device, dtype=torch.float32).contiguous()
-    if w.shape != (NCOLS,):
+    """[32] fp32 weights on ``device``.  The predict kernels ignore w[LABEL_COL] (predict.hip:
+    the label column's weight is taken as 0), so resident fp32 device weights are used as they
+    are: no copy, no read-back, no host synchronisation per call."""
+    if tuple(w.shape) != (NCOLS,):
         raise ValueError("weights must be [32] (padded layout; w[30] = intercept)")
-    if float(w[LABEL_COL]) != 0.0:
-        w = w.clone()
-        w[LABEL_COL] = 0.0
-    return w
+    return w.to(device=device, dtype=torch.float32).contiguous()
 
 
 def fp8_weights(w: torch.Tensor, d: int = 30, fp8_scale: float = DEFAULT_FP8_SCALE) -> torch.Tensor:

@@ -294,6 +294,7 @@ ROW_TILE = 64           # rows per wave tile
 PICK_TILE = 16          # virtual-SMOTE picks per wave tile (bf16 and fp8 passes: 4 lanes per pick)
 PICK_TILE_BF16 = PICK_TILE
 SGD_MIN_SPAN = 4        # every SGD minibatch spans >= 4 strided blocks of row tiles
+SGD_FULL_BLOCKS = 512   # the SGD pass grid of a 256-CU MI355X (logreg.hip sgd_full_blocks: 2 per CU)
 
 
 def sgd_grid_blocks(n_stored: int, nb: int, full_blocks: int) -> int:

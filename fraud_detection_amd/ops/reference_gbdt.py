@@ -194,3 +194,22 @@ def predict_margin(X: np.ndarray, feat: np.ndarray, thr: np.ndarray, leaf: np.nd
             node = 2 * node + 1 + right
         out = (out + leaf[t][node - ((1 << depth) - 1)]).astype(np.float32)
     return out
+
+
+def predict_margin_bins(bins: np.ndarray, feat: np.ndarray, binv: np.ndarray, leaf: np.ndarray, depth: int,
+                        base_margin: float = 0.0) -> np.ndarray:
+    """The device margin walk (gbdt.hip gbdt_margin_kernel) on binned rows: a row goes right at a
+    node when its bin of the node's feature exceeds the split bin.  float32, summed in tree order."""
+    bins = np.asarray(bins)
+    n = bins.shape[0]
+    out = np.full(n, np.float32(base_margin), dtype=np.float32)
+    rows = np.arange(n)
+    for t in range(feat.shape[0]):
+        node = np.zeros(n, np.int64)
+        for _ in range(depth):
+            f = feat[t][node]
+            bv = bins[rows, np.maximum(f, 0)].astype(np.int64)
+            right = (f >= 0) & (bv > binv[t][node])
+            node = 2 * node + 1 + right
+        out = (out + leaf[t][node - ((1 << depth) - 1)]).astype(np.float32)
+    return out

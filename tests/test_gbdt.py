@@ -191,3 +191,23 @@ def test_train_entry_point_gbdt(tmp_path, monkeypatch):
     np.testing.assert_array_equal(clf.predict_proba(Xs), js.predict_proba(Xs))
     assert clf.params.scale_pos_weight == pytest.approx(out["scale_pos_weight"])
     assert out["scale_pos_weight"] == pytest.approx(1.0, abs=0.01)  # post-SMOTE balance (App. D #11)
+
+
+def test_fit_binned_hole_equals_explicit_copy_cpu():
+    """CPU oracle: a fit over the table minus a block equals the fit on the copy without it, and the
+    block's returned margins are the ensemble walked over its bins."""
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.ops import gbdt as gb
+
+    X, y = separable(6000, fraud_rate=0.1, seed=5)
+    p = gb.GBDTParams(n_estimators=4, max_depth=3)
+    cuts = gb.quantile_cuts(X, p.max_bin)
+    bins = gb.bin_rows(X, *cuts)
+    ens_h, m_h = gb.fit_binned(bins, y, cuts, p, hole=(1000, 1500), return_margin=True)
+    keep = np.r_[0:1000, 2500:6000]
+    ens_c, m_c = gb.fit_binned(bins[keep].contiguous(), y[keep].contiguous(), cuts, p, return_margin=True)
+    for a in ("feat", "bin", "thr", "gain", "leaf"):
+        assert np.array_equal(getattr(ens_h, a), getattr(ens_c, a)), a
+    assert torch.equal(m_h[keep], m_c)
+    ref = gb.R.predict_margin_bins(bins[1000:2500].numpy(), ens_c.feat, ens_c.bin, ens_c.leaf, 3, ens_c.base_margin)
+    np.testing.assert_array_equal(m_h[1000:2500].numpy(), ref)

@@ -85,6 +85,23 @@ def test_predict_bf16_and_fp8(dev):
     np.testing.assert_allclose(z8.cpu().numpy(), z8_ref, rtol=1e-5, atol=1e-4)
 
 
+def test_predict_rows_with_device_weights_never_synchronises(dev):
+    """resident fp32 device weights (label slot nonzero: the kernel ignores it) go
+    straight to the kernel -- no D2H read-back, no host synchronisation per call."""
+    X, y = _data(20_000, seed=6)
+    st = S.scaler_fit(X)
+    rows = S.scale_cast(X, st, labels=y, out_dtype="bf16").to(dev)
+    w = torch.from_numpy(np.r_[np.random.default_rng(1).normal(0, 0.5, 30), -3.0, 5.0]).float().to(dev)
+    p_ref = P.predict_rows(rows.cpu(), w.cpu())
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        p = P.predict_rows(rows, w)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    np.testing.assert_allclose(p.cpu().numpy(), p_ref.numpy(), rtol=1e-5, atol=1e-6)
+
+
 def test_predict_shap_raw(dev):
     X, _ = _data(30_011, seed=6)
     st = S.scaler_fit(X)

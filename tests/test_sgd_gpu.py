@@ -72,7 +72,7 @@ def test_device_sgd_follows_fp64_mirror(dev):
     partition: same iterate to fp32-accumulation accuracy."""
     rows, v = _case(600_000, 400, 400, 5, 500_000, 5, dev, pos=0.02)
     ws = L.LRWorkspace(dev)
-    assert ws.nblocks == 768, "the CPU mirror assumes the 768-block pass grid of a 256-CU MI355X"
+    assert ws.sgd_blocks == ref.SGD_FULL_BLOCKS, "the CPU mirror assumes the 512-block SGD grid of a 256-CU MI355X"
     kw = dict(batches=4, epochs=3)
     g = L.sgd_fit(rows, virtual=v, **kw)
     c = L.sgd_fit(rows.cpu(), virtual=L.VirtualSmote(v.parents.cpu(), v.nbr.cpu(), v.n_new, seed=v.seed,
@@ -116,3 +116,67 @@ def test_sgd_reaches_newton_optimum_at_scale(dev, storage):
         assert f.converged and f.grad_max <= L.SGD_TOL, (f.grad_max, gap)
     assert f.converged == (f.grad_max <= L.SGD_TOL)
     assert abs(f.objective - os_["objective"]) < 0.05 * os_["objective"]
+
+
+@pytest.mark.parametrize("storage", ["bf16", "fp8"])
+@pytest.mark.parametrize("virt", [True, False])
+def test_persistent_launch_is_bitwise_the_per_step_launches(dev, storage, virt):
+    """The whole schedule in one persistent launch (grid barrier per step, the update in every
+    block) gives bitwise the fit of one fused launch per step: same minibatch walk, same per-block
+    fixed-point sums, same fp64 update."""
+    rows, v = _case(1_500_000, 500, 500, 5, 1_200_000, 21, dev, pos=0.03)
+    if storage == "fp8":
+        from fraud_detection_amd.ops.layout import DEFAULT_FP8_SCALE
+        scale = torch.tensor([DEFAULT_FP8_SCALE] * 30 + [1.0, 1.0], device=dev)
+        rows = (rows.float() * scale).to(torch.float8_e4m3fn).view(torch.uint8)
+    v = v if virt else None
+    ws = L.LRWorkspace(dev)
+    assert L.native().sgd_persist_blocks(ws.sgd_blocks) > 0, "the SGD grid must fit one 512-thread block per CU"
+    a = L.sgd_fit(rows, virtual=v, persistent=True).as_fit_info()
+    b = L.sgd_fit(rows, virtual=v, persistent=False).as_fit_info()
+    assert np.array_equal(a.w, b.w), np.abs(a.w - b.w).max()
+    assert a.n_iter == b.n_iter and a.objective == b.objective and a.grad_max == b.grad_max
+    assert a.converged == b.converged
+    # one launch per step of the persistent kernel (the checkpointed path) is the same fit too
+    c = L.sgd_fit(rows, virtual=v, persistent=True, max_steps=5).as_fit_info()
+    assert c.n_iter == 5
+
+
+def test_persistent_launch_with_hole_and_affine(dev):
+    """A CV fold (rows stepped over) on pivot-shifted rows: persistent == per-step, bitwise."""
+    rows, v = _case(1_000_000, 400, 400, 5, 800_000, 23, dev, pos=0.03)
+    aff = torch.zeros(64, dtype=torch.float64, device=dev)
+    aff[:30] = 0.1
+    aff[32:62] = 1.3
+    aff[62:] = 1.0
+    aff[30], aff[31], aff[62], aff[63] = 0.0, 0.0, 1.0, 1.0
+    kw = dict(virtual=v, affine=aff, hole=(200_000, 150_000))
+    a = L.sgd_fit(rows, persistent=True, **kw).as_fit_info()
+    b = L.sgd_fit(rows, persistent=False, **kw).as_fit_info()
+    assert np.array_equal(a.w, b.w)
+
+
+def test_serpentine_order_follows_fp64_mirror(dev):
+    rows, v = _case(600_000, 400, 400, 5, 500_000, 5, dev, pos=0.02)
+    kw = dict(batches=4, epochs=3, serpentine=True)
+    g = L.sgd_fit(rows, virtual=v, **kw)
+    c = L.sgd_fit(rows.cpu(), virtual=L.VirtualSmote(v.parents.cpu(), v.nbr.cpu(), v.n_new, seed=v.seed,
+                                                    counter_base=v.counter_base), **kw)
+    assert g.n_iter == c.n_iter == 12
+    np.testing.assert_allclose(g.w[:31], c.w[:31], atol=2e-3, rtol=1e-3)
+
+
+def test_resume_after_convergence_keeps_the_fit(dev, tmp_path):
+    """a checkpoint taken after the fit converged resumes as converged -- the remaining
+    steps stay no-ops, so the resumed fit equals the uninterrupted one bitwise."""
+    from fraud_detection_amd.utils.checkpoint import CheckpointManager
+
+    rows, v = _case(800_000, 300, 300, 5, 600_000, 9, dev, pos=0.03)
+    kw = dict(virtual=v, batches=4, epochs=4, tol=1.0)  # loose tol: converged at the first epoch end
+    full = L.sgd_fit(rows, **kw).as_fit_info()
+    assert full.converged and full.n_iter == 4
+    mgr = CheckpointManager(str(tmp_path / "c"), keep=3)
+    L.sgd_fit(rows, **kw, checkpoint=mgr, checkpoint_every=2, max_steps=10)  # "crash" mid-epoch 2
+    res = L.sgd_fit(rows, **kw, checkpoint=mgr, checkpoint_every=2).as_fit_info()
+    assert res.converged and res.n_iter == full.n_iter
+    assert np.array_equal(res.w, full.w)

@@ -119,6 +119,13 @@ for st in "$@"; do
       cd /tmp && export TMPDIR=/tmp
       step gbdtprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gbdtprof" -o run -- python3 "$R/tools/gbdt_bench.py" --rows 10000000 --trees 20
       cd "$R" ;;
+    pmcgbdt)  # GBDT histogram kernel counters (LDS atomics: bank / address conflicts), 10 trees at the bench shape
+      cd /tmp && export TMPDIR=/tmp
+      GB="python3 $R/tools/gbdt_bench.py --rows 10000000 --trees 10"
+      step pmcgbdt_a 180 rocprofv3 --kernel-include-regex "gbdt_hist_kernel" --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM --output-format csv -d "$OUT/pmcgbdt_a" -o run -- $GB
+      step pmcgbdt_b 180 rocprofv3 --kernel-include-regex "gbdt_hist_kernel" --pmc SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmcgbdt_b" -o run -- $GB
+      step pmcgbdt_t 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmcgbdt_t" -o run -- $GB
+      cd "$R" ;;
     pmcks)  # KernelSHAP linear kernel counters (3 passes, 1000-explanation batches)
       cd /tmp && export TMPDIR=/tmp
       KS="python3 $R/tools/kernelshap_bench.py --quick --skip-tree --reps 5"
