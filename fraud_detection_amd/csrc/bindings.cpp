@@ -592,8 +592,8 @@ PYBIND11_MODULE(_fdx_native, m) {
                               u s, u parents, u nbr, u lam, u off, u cnt, int64_t n_real, int64_t q_offset, int mq,
                               int k, int64_t hole_at, int64_t hole_len, u state, u aff, int d, double C, double mom,
                               int fi, double tol, int nb, int epochs, int average, std::vector<double> lrs, int s0,
-                              int s1, u acc, u ticket) {
-    if (nb < 1 || epochs < 1 || (int)lrs.size() < epochs || s0 < 0 || s1 > nb * epochs)
+                              int s1, u acc, u ticket, std::vector<int> subs) {
+    if (nb < 1 || epochs < 1 || (int)lrs.size() < epochs || (int)subs.size() < epochs || s0 < 0 || s1 > nb * epochs)
       throw std::runtime_error("sgd_run: bad schedule");
     fdx::SmoteView v;
     const fdx::SmoteView* vp = nullptr;
@@ -613,20 +613,23 @@ PYBIND11_MODULE(_fdx_native, m) {
     h.at = hole_at;
     h.len = hole_len;
     for (int st = s0; st < s1; ++st) {
-      const int ep = st / nb, b = st % nb;
-      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, nb, average && ep == epochs - 1, b == nb - 1, tol);
+      const int ep = st / nb, b = st % nb, sub = subs[ep];
+      // sub-sampled epoch: phase b * sub of a grid of nb * sub minibatches; never decides convergence
+      const int rsub = nb * sub, ph = b * sub;
+      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, rsub, average && ep == epochs - 1, b == nb - 1,
+                                      sub > 1 ? -1.0 : tol);
       if (acc) {  // one launch per step (fixed-point atomics + last-block update)
         fdx::launch_sgd_pass_fused(P<const void>(X), fp8, x_scale, end, P<float>(w32), P<const float>(cw), P<int>(done),
-                                   nb, b, blocks, vp, h, P<unsigned long long>(acc), P<unsigned int>(ticket),
+                                   rsub, ph, blocks, vp, h, P<unsigned long long>(acc), P<unsigned int>(ticket),
                                    P<double>(state), P<const double>(aff), a, S(s));
         continue;
       }
       if (fp8)
         fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), 0, end, P<const float>(w32), P<const float>(cw),
-                                    P<const int>(done), 0, nb, x_scale, P<float>(partial), blocks, S(s), vp, b, true, h);
+                                    P<const int>(done), 0, rsub, x_scale, P<float>(partial), blocks, S(s), vp, ph, true, h);
       else
         fdx::launch_logreg_pass(P<const uint16_t>(X), 0, end, P<const float>(w32), P<const float>(cw),
-                                P<const int>(done), 0, nb, P<float>(partial), blocks, S(s), vp, b, true, h);
+                                P<const int>(done), 0, rsub, P<float>(partial), blocks, S(s), vp, ph, true, h);
       fdx::launch_sgd_step(P<const float>(partial), blocks, P<double>(state), P<float>(w32), P<int>(done),
                            P<const double>(aff), a, S(s));
     }
@@ -658,8 +661,10 @@ PYBIND11_MODULE(_fdx_native, m) {
                                     u cnt, int64_t n_real, int64_t q_offset, int mq, int k, int64_t hole_at,
                                     int64_t hole_len, u ws, u state, u w32, u done, u aff, int d, double C, double mom,
                                     int fi, double tol, int nb, int epochs, int average, int serpentine,
-                                    std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps) {
+                                    std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps,
+                                    std::vector<int> subs) {
     if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
+    if ((int)subs.size() < epochs) throw std::runtime_error("sgd_persist: one sub-sample factor per epoch");
     const fdx::SmoteView v = smote_view(parents, nbr, lam, off, cnt, n_real, q_offset, mq, k);
     fdx::RowHole h;
     h.at = hole_at;
@@ -673,7 +678,11 @@ PYBIND11_MODULE(_fdx_native, m) {
     a.C = C;
     a.momentum = mom;
     a.tol = tol;
-    for (int e = 0; e < epochs; ++e) a.lr[e] = lrs[e];
+    for (int e = 0; e < epochs; ++e) {
+      a.lr[e] = lrs[e];
+      if (subs[e] < 1) throw std::runtime_error("sgd_persist: sub-sample factors must be >= 1");
+      a.sub[e] = subs[e];
+    }
     a.d = d;
     a.fit_intercept = fi;
     a.nb = nb;

@@ -1511,7 +1511,6 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   const int64_t wave = (int64_t)wv * gridDim.x + blockIdx.x;
   const bool active = wave < P.Gw;
   const int64_t n = pass_stored_rows<VIRT>(0, row_end, sv, hole);
-  const int64_t step_rows = P.Gw * 64 * P.nb;
   uint4 pre[4];
   bool have_pre = false;
   constexpr int kPreLams = 32;
@@ -1521,16 +1520,18 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   const int64_t ntile = (npick + 15) >> 4;
   unsigned touch = 0;  // FDX_PERSIST_PREFETCH 2: the dummy destination of the L2 touch loads
   unsigned arrivals = 0;
+  // an epoch with sub-sample s visits every s-th phase of a grid of nb * s minibatches
+  auto rowsub_of = [&](int st) { return P.nb * P.sub[st / P.nb]; };
   auto phase_of = [&](int st) {
     const int ep = st / P.nb, pos = st % P.nb;
-    return (P.serpentine && (ep & 1)) ? P.nb - 1 - pos : pos;
+    return ((P.serpentine && (ep & 1)) ? P.nb - 1 - pos : pos) * P.sub[ep];
   };
   auto prefetch = [&](int st) {  // the wave's first tile(s) of step st: rows do not depend on w
     have_pre = false;
     have_ppre = false;
     if (kPersistPrefetch == 0 || !active || st >= P.s1) return;
     if constexpr (VIRT) {  // the inputs of the wave's first pick tile of step st
-      const int64_t pt = wave * P.nb + phase_of(st);
+      const int64_t pt = wave * rowsub_of(st) + phase_of(st);
       if (pt < ntile) {
         const int64_t p = pt * 16 + (lane >> 2);
         pick_load<4, kPreLams>(sv, p < npick ? p : -1, lane & 3, ppre);
@@ -1554,6 +1555,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       const uint8_t* X8 = static_cast<const uint8_t*>(X);
       uint4 a[2], b[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
       fp8_load_tile(X8, 0, n, hole, base, a);
+      const int64_t step_rows = P.Gw * 64 * rowsub_of(st);
       if (base + step_rows < n) fp8_load_tile(X8, 0, n, hole, base + step_rows, b);
       pre[0] = a[0]; pre[1] = a[1]; pre[2] = b[0]; pre[3] = b[1];
     } else {
@@ -1564,7 +1566,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
 
   for (int st = P.s0; st < P.s1 && !s_done; ++st) {
     if constexpr (kPersistPrefetch == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(touch) : : "memory");
-    const int ep = st / P.nb, pos = st % P.nb, b = phase_of(st);
+    const int ep = st / P.nb, pos = st % P.nb, b = phase_of(st), rsub = rowsub_of(st);
     unsigned long long* acc = accs + (st % 3) * kSgdAccWords;
     if (blockIdx.x == 0 && wv == 0) {  // set st + 1 (read as set st - 2 before barrier st - 1)
       unsigned long long* nx = accs + ((st + 1) % 3) * kSgdAccWords;
@@ -1584,7 +1586,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       }
       if (active)
         fp8_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(static_cast<const uint8_t*>(X), 0, row_end, wl, wsh, x_scale, cw0, cw1, 1,
-                                         P.nb, b, sv, hole, wave, P.Gw, nullptr, g, lacc, wacc, whacc, dacc, hacc,
+                                         rsub, b, sv, hole, wave, P.Gw, nullptr, g, lacc, wacc, whacc, dacc, hacc,
                                          pre, have_pre, ppre, have_ppre);
       float gs[16];
 #pragma unroll
@@ -1608,7 +1610,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
         g[j] = 0.0f;
       }
       if (active)
-        bf16_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(X, 0, row_end, wl, cw0, cw1, 1, P.nb, b, sv, hole, wave, P.Gw, nullptr, g,
+        bf16_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(X, 0, row_end, wl, cw0, cw1, 1, rsub, b, sv, hole, wave, P.Gw, nullptr, g,
                                           lacc, wacc, whacc, dacc, hacc, pre, have_pre, ppre, have_ppre);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
@@ -1663,10 +1665,10 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     a.c = P.lr[ep];
     a.momentum = P.momentum;
     a.fit_intercept = P.fit_intercept;
-    a.nb = P.nb;
+    a.nb = rsub;  // the minibatch estimates the epoch's weight as rsub x its own
     a.avg = P.average && ep == P.epochs - 1;
     a.epoch_end = pos == P.nb - 1;
-    a.tol = P.tol;
+    a.tol = P.sub[ep] > 1 ? -1.0 : P.tol;  // a sub-sampled epoch never decides convergence
     sgd_apply(rd, sst, wnew, &s_done, P.aff, a, t, true);
     __syncthreads();
     if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);

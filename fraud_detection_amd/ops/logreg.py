@@ -641,11 +641,14 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     return PendingFit(ws.state, warm_iters=warm)
 
 
-def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine=False):
+def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine=False,
+                   subs=None):
     from ..utils.checkpoint import config_signature
 
     n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
     extra = {"serpentine": True} if serpentine else {}
+    if subs is not None and any(x != 1 for x in subs):
+        extra["subsample"] = [int(x) for x in subs]
     return config_signature(kind="sgd2", n=n_all, d=d, C=C, lr=list(lr), momentum=momentum, batches=nb,
                             epochs=epochs, average=bool(average), tol=tol, class_w=list(class_w),
                             fit_intercept=fit_intercept, **extra)
@@ -658,13 +661,33 @@ def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit
 # steps for 1e-3 (the curvature falls ~5x between w = 0 and the optimum).
 SGD_BATCHES = 8
 SGD_EPOCHS = 3
-SGD_LR = (0.4, 0.6, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
+SGD_LR = (0.4, 0.7, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
+# Per-epoch row sub-sample: epoch 0 visits 1/4 of the rows (its 8 minibatches are every 4th phase
+# of a 32-minibatch grid) -- a growing-batch schedule: the first epoch only has to bring w near the
+# optimum, so it needs no full pass (Smith et al., "Don't decay the learning rate, increase the
+# batch size").  fp64 simulation on the bench distribution (tools/sgd_schedule_lab.py, 16M
+# post-SMOTE rows): (4, 1, 1) with steps (0.4, 0.7, 0.8) ends at epoch gradient 2.2e-4 and 1.3e-4
+# relative above the Newton objective, streaming 2.25 epochs instead of 3 (3 full epochs with
+# (0.4, 0.6, 0.8): 3.6e-4, 4.2e-5).  A sub-sampled epoch never decides convergence.
+SGD_SUB = (4, 1, 1)
 SGD_MOMENTUM = 0.55
 SGD_TOL = 1e-3                # on the epoch gradient max-norm (sklearn SGDClassifier's default tol)
 SGD_SLOTS = 36
 
 
 SGD_MAX_EPOCHS = 8  # launchers.h kSgdMaxEpochs (per-epoch step scalars of the persistent launch)
+
+
+def _effective_subs(subs, n_stored: int, n_picks: int, nb: int, blocks: int) -> list:
+    """Sub-sample factors that keep every minibatch of an epoch's finer grid (nb x s) populated:
+    >= 1 strided group of row tiles and >= 2 pick tiles each; else that epoch visits every row."""
+    groups = n_stored // (ref.ROW_TILE * ref.WAVES_PER_BLOCK * max(1, blocks))
+    ptiles = -(-n_picks // ref.PICK_TILE)
+    out = []
+    for x in subs:
+        ok = x > 1 and groups >= nb * x and (n_picks == 0 or ptiles >= 2 * nb * x)
+        out.append(int(x) if ok else 1)
+    return out
 
 
 def _sgd_phase(pos: int, ep: int, nb: int, serpentine: bool) -> int:
@@ -690,7 +713,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             fp8_scale: float = DEFAULT_FP8_SCALE, workspace: LRWorkspace | None = None, checkpoint=None,
             checkpoint_every: int = 0, affine: torch.Tensor | None = None, virtual: VirtualSmote | None = None,
             batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None,
-            persistent: bool | None = None, serpentine: bool = False, _stamps: torch.Tensor | None = None):
+            persistent: bool | None = None, serpentine: bool = False, subsample=SGD_SUB,
+            _stamps: torch.Tensor | None = None):
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
@@ -718,7 +742,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     a grid barrier per step instead of a launch per step; bitwise the same fit).  Default on
     unless FDX_SGD_PERSIST=0.  ``serpentine``: odd epochs visit the minibatches in reverse order
     (persistent launch only), so an epoch's first minibatches are the previous epoch's last ones
-    -- still resident in the 256 MB Infinity Cache."""
+    -- still resident in the 256 MB Infinity Cache.  ``subsample``: per-epoch row sub-sample factors
+    (SGD_SUB; an epoch with factor s visits 1/s of the rows in its nb minibatches)."""
     check_rows(rows)
     w0 = _default_w0(w0)
     rows, hole = _apply_hole(rows, hole)
@@ -732,6 +757,15 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     if comm is not None and comm.world_size > 1:
         nb = int(comm.all_reduce_scalar(nb, op="max"))
     lrs = [_epoch_lr(lr, e) for e in range(max(epochs, 1))]
+    subs = [int(_epoch_lr(subsample, e)) if subsample is not None else 1 for e in range(max(epochs, 1))]
+    if any(x < 1 for x in subs):
+        raise ValueError("sub-sample factors must be >= 1")
+    # a sub-sampled epoch only where every minibatch of its finer grid still holds row tiles of the
+    # whole shard and SMOTE picks (small shards: every epoch full); one decision for all DP ranks
+    n_picks = int(virtual.nbr.numel()) if virtual is not None else 0
+    subs = _effective_subs(subs, n_stored, n_picks, nb, ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS))
+    if comm is not None and comm.world_size > 1:
+        subs = [int(comm.all_reduce_scalar(float(x), op="min")) for x in subs]
     if affine is not None and not rows.is_cuda:
         a = affine.cpu().double()
         rows = ((ref.rows_to_f32(rows, fp8_scale, d).double() - a[:32]) * a[32:]).float()
@@ -740,14 +774,15 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             vr[:, LABEL_COL] = virtual.label
             return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept,
                                 comm, fp8_scale, checkpoint, checkpoint_every, None, None, virtual=(virtual, vr),
-                                max_steps=max_steps, serpentine=serpentine)
+                                max_steps=max_steps, serpentine=serpentine, subs=subs)
         affine = None
     aff = 0
     if affine is not None:
         if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
-    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine)
+    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine,
+                          subs)
            if checkpoint else None)
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
@@ -755,7 +790,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         vv = (virtual, virtual.rows_f32()) if virtual is not None else None
         return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm,
                             fp8_scale, checkpoint, checkpoint_every, sig, got, virtual=vv, max_steps=max_steps,
-                            serpentine=serpentine)
+                            serpentine=serpentine, subs=subs)
     if virtual is not None:
         virtual.check(rows)
         if class_w[1] > VIRTUAL_MAX_WEIGHT:
@@ -800,7 +835,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                           ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
                           float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
                           int(bool(serpentine)), [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(s1),
-                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0)
+                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs[:max(epochs, 1)])
             return
         if serpentine:
             raise ValueError("serpentine minibatch order needs the persistent SGD launch")
@@ -808,7 +843,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                   ptr(ws.partial), blocks, s, *vargs, ptr(ws.state), aff, d,
                   float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
                   [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
-                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]))
+                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs[:max(epochs, 1)])
 
     if not dp and checkpoint is None:
         s0 = start[0] * nb + start[1]
@@ -820,17 +855,19 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             if max_steps is not None and ep * nb + pos >= max_steps:
                 break
             b = _sgd_phase(pos, ep, nb, serpentine)
+            rsub, ph = nb * subs[ep], b * subs[ep]
             avg = int(average and ep == epochs - 1)
             last = pos + 1 == nb
             if dp:
                 # lean step: the pass leaves its fixed-point sums (int64: the all-reduce is exact and
                 # order-free, every rank gets bitwise the same vector), one collective, the update
                 m.sgd_pass_sums(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w),
-                                ptr(ws.done), nb, b, blocks, *vargs, ptr(ws.sgd_acc),
+                                ptr(ws.done), rsub, ph, blocks, *vargs, ptr(ws.sgd_acc),
                                 ptr(ws.sgd_acc[SGD_ACC_WORDS:]), ptr(ws.sgd_sums), aff, s)
                 comm.all_reduce_(ws.sgd_sums)
                 m.sgd_update_fixed(ptr(ws.sgd_sums), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
-                                   float(momentum), int(fit_intercept), nb, avg, int(last), float(tol), s)
+                                   float(momentum), int(fit_intercept), rsub, avg, int(last),
+                                   -1.0 if subs[ep] > 1 else float(tol), s)
             else:  # the same kernels as the uninterrupted fit: checkpointed fits stay bit-identical
                 run_steps(ep * nb + pos, ep * nb + pos + 1)
             gstep = ep * nb + pos + 1
@@ -921,25 +958,35 @@ def _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm,
 
 def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm, fp8_scale,
                  checkpoint=None, checkpoint_every=0, sig=None, got=None, virtual=None, max_steps=None,
-                 serpentine=False):
+                 serpentine=False, subs=None):
     """The device SGD's algorithm in fp64 (ref.SgdStateRef) over the same minibatch partition:
     stored row tiles by the pass grid's strided walk (the full SGD grid of a 256-CU part,
     ref.SGD_FULL_BLOCKS, shrunk for small shards like the device), virtual samples by their pick tile."""
     R = ref.rows_to_f32(rows, fp8_scale, d).double().numpy()
     n_stored = R.shape[0]
-    rb = ref.sgd_row_batches(n_stored, nb, ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS))
+    subs = list(subs) if subs is not None else [1] * max(epochs, 1)
+    blocks = ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS)
     parts = [R]
-    bs = [rb]
+    pick = None
     if virtual is not None:
         v, vr = virtual
         mq, k = v.nbr.shape
         pick, _ = ref.smote_pick_draws(int(mq), int(k), int(v.n_new), int(v.seed), int(v.counter_base),
                                        int(v.sample_offset))
         parts.append(np.asarray(vr, dtype=np.float64))
-        bs.append(ref.sgd_pick_batches(mq * k, nb, ref.PICK_TILE)[pick.astype(np.int64)])
     R = np.concatenate(parts)
-    batch_of = np.concatenate(bs)
-    members = [np.nonzero(batch_of == b)[0] for b in range(nb)]
+    members_of = {}
+
+    def members(rsub: int, ph: int):
+        """Rows of phase ph of a grid of rsub minibatches (an epoch with sub-sample s: rsub = nb s)."""
+        if rsub not in members_of:
+            bs = [ref.sgd_row_batches(n_stored, rsub, blocks)]
+            if pick is not None:
+                bs.append(ref.sgd_pick_batches(mq * k, rsub, ref.PICK_TILE)[pick.astype(np.int64)])
+            batch_of = np.concatenate(bs)
+            members_of[rsub] = [np.nonzero(batch_of == b)[0] for b in range(rsub)]
+        return members_of[rsub][ph]
+
     st = ref.SgdStateRef(w0)
     start = (0, 0)
     if got is not None:
@@ -955,7 +1002,7 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
             if max_steps is not None and ep * nb + pos >= max_steps:
                 break
             b = _sgd_phase(pos, ep, nb, serpentine)
-            Rb = R[members[b]]
+            Rb = R[members(nb * subs[ep], b * subs[ep])]
             g, loss, wsum, _ = ref.logreg_pass(Rb, st.w, class_w, False)
             X = Rb.copy()
             X[:, LABEL_COL] = 0.0
@@ -967,8 +1014,8 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
             if comm is not None and comm.world_size > 1:
                 red = comm.all_reduce(torch.from_numpy(red)).numpy()
             last = pos + 1 == nb
-            st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nb,
-                    bool(average and ep == epochs - 1), last, tol, fit_intercept)
+            st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nb * subs[ep],
+                    bool(average and ep == epochs - 1), last, -1.0 if subs[ep] > 1 else tol, fit_intercept)
             gstep = ep * nb + pos + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 sv = np.zeros(STATE_SIZE)
