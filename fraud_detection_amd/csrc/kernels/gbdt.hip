@@ -238,11 +238,25 @@ __device__ __forceinline__ int64_t level_chunk(const LevelNodes& L, int level, i
   return (total + nblocks - 1) / nblocks;
 }
 
-__global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
+// ROT: the 64 lanes of a wave do not add into the same feature at the same time.  Lane l walks the
+// 32 feature slots starting at slot (l mod 32) -- its 32-byte bin row rotated by that many bytes
+// once per row (a 3-stage dword barrel shift + one byte funnel), so every bin byte is still
+// extracted with a static shift -- and feature f's sub-histogram starts at f * kHistStrideRot (an
+// odd number of u64: consecutive features start in different bank pairs).  A wave's concurrent
+// atomics then hit 32 different sub-histograms instead of one: no same-address collisions within
+// a feature and no lockstep on one 2 KiB region.  Integer adds: every histogram bit is unchanged.
+constexpr int kHistStrideRot = kGBBins + 1;
+constexpr int kHistWordsRot = 32 * kHistStrideRot;  // 8224 u64 = 64.25 KiB (two blocks per CU fit)
+constexpr int kHistBatchRot = 4;  // rows in flight per thread
+template <bool ROT>
+__global__ __launch_bounds__(kHistThreads, ROT ? 4 : 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
+                                                                           // (ROT: 1 block/CU, <= 128 VGPRs)
     const uint8_t* __restrict__ bins, const uint32_t* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
     long long* __restrict__ slots, int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
-  __shared__ unsigned long long sh[kHistWords];
+  constexpr int kStride = ROT ? kHistStrideRot : kGBBins;
+  constexpr int kBatch = ROT ? kHistBatchRot : kHistBatch;
+  __shared__ unsigned long long sh[ROT ? kHistWordsRot : kHistWords];
   __shared__ LevelNodes lv;
   const int h0 = heap_first(level), nn = 1 << level;
   load_level(lv, seg, gcnt, level);
@@ -269,23 +283,23 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
     long long* dst = slots + (int64_t)my_slot * kHistEntries;
     for (int64_t c0 = lo; c0 < hi; c0 += flush_rows) {
       const int64_t c1 = min(hi, c0 + flush_rows);
-      for (int i = threadIdx.x; i < nw; i += kHistThreads) sh[i] = 0ull;
+      for (int i = threadIdx.x; i < nw; i += kHistThreads) sh[ROT ? (i >> 8) * kStride + (i & 255) : i] = 0ull;
       __syncthreads();
-      // kHistBatch rows per thread in flight: every row index, then every row's bins and (g, h),
+      // kBatch rows per thread in flight: every row index, then every row's bins and (g, h),
       // are loaded before the first atomic.  Level 0 reads rows in order (ridx is the identity
       // after the round init).
       const int64_t pbase = sb - (off - sc);
-      for (int64_t v0 = c0 + threadIdx.x; v0 < c1; v0 += kHistThreads * kHistBatch) {
-        int64_t rows[kHistBatch];
+      for (int64_t v0 = c0 + threadIdx.x; v0 < c1; v0 += kHistThreads * kBatch) {
+        int64_t rows[kBatch];
 #pragma unroll
-        for (int u = 0; u < kHistBatch; ++u) {
+        for (int u = 0; u < kBatch; ++u) {
           const int64_t v = v0 + (int64_t)u * kHistThreads;
           rows[u] = v < c1 ? (level == 0 ? hole_row(pbase + v, hole_at, hole_len) : (int64_t)ridx[pbase + v]) : -1;
         }
-        uint32_t words[kHistBatch][8];
-        unsigned long long pk[kHistBatch];
+        uint32_t words[kBatch][8];
+        unsigned long long pk[kBatch];
 #pragma unroll
-        for (int u = 0; u < kHistBatch; ++u) {
+        for (int u = 0; u < kBatch; ++u) {
           const int64_t row = rows[u] < 0 ? 0 : rows[u];
           const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
           const uint4 b0v = br[0], b1v = br[1];
@@ -296,13 +310,46 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
           pk[u] = ((unsigned long long)(uint32_t)q.y << 32) + (unsigned long long)(long long)q.x;
         }
 #pragma unroll
-        for (int u = 0; u < kHistBatch; ++u) {
+        for (int u = 0; u < kBatch; ++u) {
           if (rows[u] < 0) continue;
+          if constexpr (ROT) {
+            const int rot = lane_id() & 31;
+            uint32_t w[8];
 #pragma unroll
-          for (int f = 0; f < kGBMaxFeat; ++f) {
-            if (f < d) {
-              const int b = (words[u][f >> 2] >> (8 * (f & 3))) & 0xff;
-              atomicAdd(sh + f * kGBBins + b, pk[u]);
+            for (int i = 0; i < 8; ++i) w[i] = words[u][i];
+#pragma unroll
+            for (int stage = 0; stage < 3; ++stage) {  // dwords rotated left by rot >> 2
+              const int sh_d = 1 << stage;
+              const bool on = ((rot >> 2) >> stage) & 1;
+              uint32_t t[8];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) t[i] = on ? w[(i + sh_d) & 7] : w[i];
+#pragma unroll
+              for (int i = 0; i < 8; ++i) w[i] = t[i];
+            }
+            uint32_t rw[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) rw[i] = __builtin_amdgcn_alignbyte(w[(i + 1) & 7], w[i], rot & 3);
+            // feature of slot jj: jj + rot, minus 32 past the end (the LDS offset of slot jj is an
+            // immediate; one wrapped base register)
+            unsigned long long* s0 = sh + rot * kStride;
+            unsigned long long* s1 = s0 - 32 * kStride;
+#pragma unroll
+            for (int jj = 0; jj < 32; ++jj) {
+              const int f = (jj + rot) & 31;
+              if (f < d) {
+                const int b = (rw[jj >> 2] >> (8 * (jj & 3))) & 0xff;
+                atomicAdd((jj + rot < 32 ? s0 : s1) + jj * kStride + b, pk[u]);
+              }
+              if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // keep the live ranges short
+            }
+          } else {
+#pragma unroll
+            for (int f = 0; f < kGBMaxFeat; ++f) {
+              if (f < d) {
+                const int b = (words[u][f >> 2] >> (8 * (f & 3))) & 0xff;
+                atomicAdd(sh + f * kGBBins + b, pk[u]);
+              }
             }
           }
         }
@@ -310,7 +357,7 @@ __global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_kernel(  // 8 waves
       __syncthreads();
       const bool first = c0 == lo;  // later flushes of the same slot accumulate (block-private)
       for (int i = threadIdx.x; i < nw; i += kHistThreads) {
-        const unsigned long long x = sh[i];
+        const unsigned long long x = sh[ROT ? (i >> 8) * kStride + (i & 255) : i];
         const long long sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
         const long long shh = (long long)(x - (unsigned long long)sg) >> 32;
         long long* e = dst + 2 * i;
@@ -933,11 +980,19 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   // at most blocks + nodes pairs)
   if (level < 0 || (1 << level) > kGBMaxNodes + 1) throw std::runtime_error("gbdt_hist: level out of range");
   const int nb = gbdt_hist_blocks();
-  gbdt_hist_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows, hole_at,
-                                                     hole_len);
+  static const bool rot = [] {  // lab switch (FDX_GBDT_HIST_ROT=1: the rotated-feature form)
+    const char* e = std::getenv("FDX_GBDT_HIST_ROT");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (rot)  // one block per CU (its rotation registers): half the blocks of the lockstep form
+    gbdt_hist_kernel<true><<<nb / 2, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows,
+                                                                 hole_at, hole_len);
+  else
+    gbdt_hist_kernel<false><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows,
+                                                              hole_at, hole_len);
   check_launch("gbdt_hist");
   const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, level == 0 ? 1u : 1u << (level - 1));
-  gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, nb, hist);
+  gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, rot ? nb / 2 : nb, hist);
   check_launch("gbdt_hist_reduce");
 }
 
