@@ -38,6 +38,7 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cerrno>
 #include <chrono>
@@ -218,18 +219,46 @@ class Ring {
     if (nchunks > N) throw std::runtime_error("ring: request larger than the ring");
     const uint64_t deadline = now_ns() + (uint64_t)(timeout_ms * 1e6);
     // Tickets are taken only together with free slots (CAS on head after checking that the
-    // nchunks slots at head are FREE at their turns; only a ticket's holder leaves FREE, so they
-    // stay free): a producer that times out waiting for room holds no ticket, and the owner never
-    // waits on a ticket nobody will publish -- except one whose producer died right after this
-    // CAS, which the owner reclaims after reclaim_ms.
-    uint64_t t0 = 0;
-    bool took = false;  // sleep_until may evaluate the predicate again after it held: take once
-    if (!sleep_until([&] { return took || (took = try_take(nchunks, t0)); }, deadline))
-      throw std::runtime_error(owner_gone() ? "ring: GPU owner stopped" : "ring: timed out waiting for a free slot");
-    uint32_t published = 0;
+    // slots at head are FREE at their turns; only a ticket's holder leaves FREE, so they stay
+    // free): a producer that times out waiting for room holds no ticket it has not published, and
+    // the owner never waits on a ticket nobody will publish -- except one whose producer died
+    // right after this CAS, which the owner reclaims after reclaim_ms.  A large request takes its
+    // tickets in pieces of at most a quarter of the ring (publishing each piece before it takes
+    // the next), so a stream of one-chunk requests cannot starve it of nchunks free slots at once.
+    const uint32_t piece = std::max<uint32_t>(1u, N / 4);
+    std::vector<uint64_t> tix;
+    tix.reserve(nchunks);
+    uint32_t published = 0, consumed = 0;
+    bool failed = false, timed_out = false;
     const char* err = nullptr;
+    // consume this request's finished chunks in order (frees their slots for its later pieces)
+    auto consume_finished = [&] {
+      while (consumed < published) {
+        const uint64_t t = tix[consumed];
+        const uint32_t st = state_of(slots_[t % N].tag.load(std::memory_order_acquire));
+        if (st != DONE && st != FAILED) break;
+        const uint32_t m = std::min(R, n - consumed * R);
+        if (cancel_or_consume(t, out + (size_t)consumed * R * W, m, W) != DONE) failed = true;
+        ++consumed;
+      }
+    };
     for (uint32_t c = 0; c < nchunks; ++c) {
-      const uint64_t t = t0 + c;
+      if (c == tix.size()) {  // the next piece of tickets
+        const uint32_t want = std::min(piece, nchunks - c);
+        uint64_t t0 = 0;
+        bool took = false;  // sleep_until may evaluate the predicate again after it held: take once
+        if (!sleep_until([&] {
+              if (took) return true;
+              consume_finished();
+              return took = try_take(want, t0);
+            }, deadline)) {
+          for (uint32_t e = consumed; e < published; ++e) cancel_or_consume(tix[e], nullptr, 0, 0);
+          ring_doorbell();
+          throw std::runtime_error(owner_gone() ? "ring: GPU owner stopped" : "ring: timed out waiting for a free slot");
+        }
+        for (uint32_t e = 0; e < want; ++e) tix.push_back(t0 + e);
+      }
+      const uint64_t t = tix[c];
       Slot& s = slots_[t % N];
       uint64_t g = tag_of(t, FREE);
       if (!s.tag.compare_exchange_strong(g, tag_of(t, CLAIMED), std::memory_order_acq_rel)) {
@@ -249,13 +278,12 @@ class Ring {
       ring_doorbell();
     }
     if (err != nullptr) {  // the unpublished tickets were (or will be) reclaimed by the owner
-      for (uint32_t c = 0; c < published; ++c) cancel_or_consume(t0 + c, nullptr, 0, 0);
+      for (uint32_t c = consumed; c < published; ++c) cancel_or_consume(tix[c], nullptr, 0, 0);
       ring_doorbell();
       throw std::runtime_error(err);
     }
-    bool failed = false, timed_out = false;
-    for (uint32_t c = 0; c < nchunks; ++c) {
-      const uint64_t t = t0 + c;
+    for (uint32_t c = consumed; c < nchunks; ++c) {
+      const uint64_t t = tix[c];
       const uint32_t m = std::min(R, n - c * R);
       Slot& s = slots_[t % N];
       const bool fin = !timed_out && sleep_until([&] {

@@ -182,3 +182,45 @@ def test_many_producers_with_random_timeouts_keep_the_ring_consistent():
         ow.join()
     assert not bad
     np.testing.assert_array_equal(out[:, 0], _x(-1.0)[:, 0] * 10.0)
+
+
+def test_ring_sized_request_is_not_starved_by_a_stream_of_small_ones():
+    """A request as large as the whole ring takes its tickets in pieces and frees its own
+    finished chunks while it waits for room, so a steady stream of one-chunk requests (which
+    never leave the ring empty) cannot starve it."""
+    r = _ring(nslots=8, slot_rows=2)
+    stop = threading.Event()
+
+    def owner():
+        dst = np.zeros((64, D), np.float32)
+        while not stop.is_set():
+            n, _ = r.collect(dst.ctypes.data, 4, 0.0, 20.0, 0)  # small batches: slots stay busy
+            if n:
+                time.sleep(0.0005)
+                prob = np.ascontiguousarray(dst[:n, 0] * 10.0, np.float32)
+                r.complete(prob.ctypes.data, prob.ctypes.data)
+
+    small_done = [0]
+
+    def small(k):
+        while not stop.is_set():
+            try:
+                r.request(_x(float(k), 1), 0, 2000.0)
+                small_done[0] += 1
+            except RuntimeError:
+                pass
+
+    ths = [threading.Thread(target=owner)] + [threading.Thread(target=small, args=(k,)) for k in range(4)]
+    for t in ths:
+        t.start()
+    try:
+        time.sleep(0.05)
+        X = np.arange(16 * D, dtype=np.float32).reshape(16, D)  # 8 chunks = the whole ring
+        for _ in range(3):
+            out = r.request(X, 0, 5000.0)
+            np.testing.assert_array_equal(out[:, 0], X[:, 0] * 10.0)
+    finally:
+        stop.set()
+        for t in ths:
+            t.join()
+    assert small_done[0] > 0
