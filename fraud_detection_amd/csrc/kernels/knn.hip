@@ -574,6 +574,240 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
   }
 }
 
+// ---- bf16x3 collect + exact re-rank (two phases) ---------------------------------------------
+// The engines above run the top-k on the critical path of every tile: the fp32 chain costs 1024
+// MFMA cycles per 32x32 tile plus the filter's VALU (serial per wave: ~200 us at 13.6k minority
+// rows, profiles/r4_g), and knn_topk3 stalls on a dependent fp32 tile load + LDS re-score whenever
+// a lane passes.  Here phase 1 (knn_collect_kernel) never touches fp32 candidate rows: per tile it
+// runs the 6 bf16 MFMAs of knn_topk3 and a max test, and a passing candidate only APPENDS its index
+// to a per-lane global list.  The running threshold is the k-th best LOWER bound approx - m of the
+// union of the query's two half-lists, where m = 2^-13 (||q|| tmax + 0.5 tmax^2) >= 8x the bf16x3
+// error bound (see knn_topk3); a candidate is appended when its UPPER bound approx + m reaches it.
+// Since k distinct candidates have exact >= lower bound >= thr, the exact k-th best s_k >= thr
+// at every moment, so every candidate with exact >= s_k (upper bound >= s_k >= thr) is on a list.
+// Phase 2 (knn_rerank_kernel, 8 lanes per query) re-scores the listed candidates exactly (the
+// k-ordered fp32 fmaf chain of knn_topk3's re-score) and keeps the top-k (ties -> smaller index):
+// the exact fp32 ranking.  A lane list that overflows kListCap sends its query to a brute-force
+// exact scan in phase 2 (correct, slow, and not seen at SMOTE shapes).
+constexpr int kListCap = 64;
+
+template <int K>
+__global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
+                                                            const uint4* __restrict__ Chl,
+                                                            const float* __restrict__ tmax, int mc_pad, int mc,
+                                                            int64_t self_offset, int* __restrict__ lists,
+                                                            int* __restrict__ counts) {
+  const int lane = threadIdx.x;
+  const int h = lane >> 5, j = lane & 31;
+  const int qg = blockIdx.x * 32 + j;
+  const int64_t self_c = self_offset >= 0 ? self_offset + qg : -1;
+  float qn;
+  {  // ||q|| over the 30 feature columns: half h sums columns 16h .. 16h + 15
+    const float4* p = reinterpret_cast<const float4*>(Q + (int64_t)qg * kCols + 16 * h);
+    float s2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = p[k];
+      s2 = fmaf(v.x, v.x, s2);
+      s2 = fmaf(v.y, v.y, s2);
+      if (h == 0 || k < 3) {  // columns 30, 31 (query 1 / 0) are not features
+        s2 = fmaf(v.z, v.z, s2);
+        s2 = fmaf(v.w, v.w, s2);
+      }
+    }
+    s2 += __shfl_xor(s2, 32, kWave);
+    qn = sqrtf(s2) * 1.0001f;
+  }
+  const uint4* qr = Qhl + (int64_t)qg * 8;
+  const bf16x8_t qh0 = __builtin_bit_cast(bf16x8_t, qr[h]), qh1 = __builtin_bit_cast(bf16x8_t, qr[2 + h]);
+  const bf16x8_t ql0 = __builtin_bit_cast(bf16x8_t, qr[4 + h]), ql1 = __builtin_bit_cast(bf16x8_t, qr[6 + h]);
+  float bs[K];
+  int bi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  float thr = kNegBig;
+  constexpr int kCap = kQFlush - 1 + 16 + 1;
+  __shared__ int2 qent[kCap * kWave];  // (lower-bound bits, candidate index) at [slot * 64 + lane]
+  int qc = 0, cnt = 0;
+  const int64_t lbase = (int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * kListCap * kWave + lane;
+  auto flush = [&]() {
+    for (int e = 0; __any(e < qc); ++e) {
+      if (e < qc) {
+        const int2 v = qent[e * kWave + lane];
+        const int ci = v.y;
+        if (ci != self_c && ci < mc) {
+          if (cnt < kListCap) lists[lbase + (int64_t)cnt * kWave] = ci;
+          ++cnt;
+          topk_insert<K>(bs, bi, __int_as_float(v.x), ci);
+        }
+      }
+    }
+    qc = 0;
+    float ps[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
+    int ia = 0, ib = 0;
+    float kth = kNegBig;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float a = kNegBig, b = kNegBig;
+#pragma unroll
+      for (int u = 0; u < K; ++u) { if (u == ia) a = bs[u]; if (u == ib) b = ps[u]; }
+      const bool ta = a >= b;
+      kth = ta ? a : b;
+      ia += ta ? 1 : 0;
+      ib += ta ? 0 : 1;
+    }
+    thr = kth;
+  };
+  const int all_tiles = mc_pad / 32;
+  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
+  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  uint4 cv[4];
+  float tmn = 0.0f;
+  auto fetch = [&](int t, uint4 (&a)[4]) {
+    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
+    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
+    tmn = tmax[t];
+  };
+  if (t_lo < t_hi) fetch(t_lo, cv);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int c0 = t * 32;
+    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, cv[0]), ch1 = __builtin_bit_cast(bf16x8_t, cv[1]);
+    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, cv[2]), cl1 = __builtin_bit_cast(bf16x8_t, cv[3]);
+    const float tm = tmn;
+    if (t + 1 < t_hi) fetch(t + 1, cv);
+    f32x16_t acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, ql0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
+    const float mg = 0x1p-13f * fmaf(qn, tm, 0.5f * tm * tm);
+    const float cut = thr - mg;  // upper bound approx + mg >= thr
+    float mx = acc[0];
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    if (!__any(mx >= cut)) continue;
+    const int cbase = c0 + 4 * h;
+    int qe = qc * kWave + lane;
+    const int de = (kCap - 1) * kWave + lane;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const bool pass = acc[r] >= cut;
+      qent[pass ? qe : de] = make_int2(__float_as_int(acc[r] - mg), cbase + (r & 3) + 8 * (r >> 2));
+      qe += pass ? kWave : 0;
+    }
+    qc = (qe - lane) / kWave;
+    if (__any(qc >= kQFlush)) flush();
+  }
+  flush();
+  counts[(int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * kWave + lane] = cnt;
+}
+
+// Phase 2: 8 lanes per query (lane l takes every 8th listed candidate), exact re-score, per-lane
+// top-k, then a 3-round butterfly merge of the 8 sorted lists (knn_merge_kernel's merge).
+template <int K>
+__global__ __launch_bounds__(256) void knn_rerank_kernel(const float* __restrict__ Q, const float* __restrict__ C,
+                                                         int mq, int mc, int qblocks, int nsplit, int64_t self_offset,
+                                                         const int* __restrict__ lists,
+                                                         const int* __restrict__ counts, int* __restrict__ out_idx,
+                                                         float* __restrict__ out_score) {
+  const int gl = blockIdx.x * 256 + threadIdx.x;
+  const int q = gl >> 3, l = gl & 7;
+  const bool live = q < mq;
+  const int qq = live ? q : 0;
+  const int blk = qq >> 5, j = qq & 31;
+  const int64_t self_c = self_offset >= 0 ? self_offset + qq : -1;
+  float qv[kCols];
+  {
+    const float4* p = reinterpret_cast<const float4*>(Q + (int64_t)qq * kCols);
+#pragma unroll
+    for (int k = 0; k < kCols / 4; ++k) {
+      const float4 v = p[k];
+      qv[4 * k] = v.x; qv[4 * k + 1] = v.y; qv[4 * k + 2] = v.z; qv[4 * k + 3] = v.w;
+    }
+  }
+  auto exact = [&](int ci) -> float {  // knn_topk3's re-score: columns 0..31 in order
+    const float4* c = reinterpret_cast<const float4*>(C + (int64_t)ci * kCols);
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kCols / 4; ++k) {
+      const float4 v = c[k];
+      acc = fmaf(qv[4 * k], v.x, acc);
+      acc = fmaf(qv[4 * k + 1], v.y, acc);
+      acc = fmaf(qv[4 * k + 2], v.z, acc);
+      acc = fmaf(qv[4 * k + 3], v.w, acc);
+    }
+    return acc;
+  };
+  float bs[K];
+  int bi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  if (live) {
+    bool over = false;
+    for (int s = 0; s < nsplit; ++s)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) over |= counts[((int64_t)s * qblocks + blk) * kWave + j + 32 * h] > kListCap;
+    if (!over) {
+      for (int s = 0; s < nsplit; ++s) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int64_t cb = ((int64_t)s * qblocks + blk) * kWave + j + 32 * h;
+          const int n = counts[cb];
+          const int* li = lists + ((int64_t)s * qblocks + blk) * kListCap * kWave + j + 32 * h;
+          for (int e = l; e < n; e += 8) {
+            const int ci = li[(int64_t)e * kWave];
+            topk_insert<K>(bs, bi, exact(ci), ci);
+          }
+        }
+      }
+    } else {  // a list overflowed: exact scan of every candidate
+      for (int ci = l; ci < mc; ci += 8)
+        if (ci != self_c) topk_insert<K>(bs, bi, exact(ci), ci);
+    }
+  }
+#pragma unroll
+  for (int off = 1; off < 8; off <<= 1) {
+    float os[K];
+    int oi[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      os[k] = __shfl_xor(bs[k], off, kWave);
+      oi[k] = __shfl_xor(bi[k], off, kWave);
+    }
+    float ns[K];
+    int ni[K];
+    int ia = 0, ib = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      float a = kNegBig, b = kNegBig;
+      int ai = 0x7fffffff, bj = 0x7fffffff;
+#pragma unroll
+      for (int u = 0; u < K; ++u) {
+        if (u == ia) { a = bs[u]; ai = bi[u]; }
+        if (u == ib) { b = os[u]; bj = oi[u]; }
+      }
+      const bool ta = !better(b, bj, a, ai);
+      ns[k] = ta ? a : b;
+      ni[k] = ta ? ai : bj;
+      ia += ta ? 1 : 0;
+      ib += ta ? 0 : 1;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) { bs[k] = ns[k]; bi[k] = ni[k]; }
+  }
+  if (live && l == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      out_idx[(int64_t)q * K + k] = bi[k];
+      if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+    }
+  }
+}
+
 // Merge the per-slice top-k lists of every query (same ordering: score desc, index asc).
 // lps (a power of two >= nsplit, <= 64) lanes per query: lane s loads slice s's sorted list, then
 // log2(lps) butterfly rounds merge lists pairwise through shuffles (a static-index merge of two
@@ -774,6 +1008,57 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
   }
 #undef FDX_KNN3
   check_launch("knn_topk3");
+}
+
+int knn3r_list_cap() { return kListCap; }
+
+int knn3r_splits(int mq_pad, int mc_pad) {
+  // fewer slices than the one-wave engines: a slice restarts the lists (16 appends per lane on its
+  // first tile) and each slice holds kListCap ints per query lane
+  static const int cap = resident_cap(knn_collect_kernel<5>, kWave);
+  const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
+  int max_s = tiles / 16;
+  if (max_s > 16) max_s = 16;
+  if (max_s < 1) max_s = 1;
+  int best = 1;
+  double best_eff = -1.0;
+  for (int s = 1; s <= max_s; ++s) {
+    const double blocks = (double)qblocks * s;
+    const double rounds = std::ceil(blocks / cap);
+    double eff = blocks / (rounds * cap);
+    eff -= 0.004 * (s - 1);
+    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
+  }
+  return best;
+}
+
+void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
+                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
+                       float* out_score, int* lists, int* counts, int nsplit, hipStream_t stream) {
+  if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk3r: pads must be x32");
+  if (mq > mq_pad || mc > mc_pad || nsplit < 1 || lists == nullptr || counts == nullptr)
+    throw std::runtime_error("knn_topk3r: bad shapes or missing list workspaces");
+  const dim3 grid(mq_pad / 32, nsplit);
+  const uint4* qh = reinterpret_cast<const uint4*>(Qhl);
+  const uint4* chl = reinterpret_cast<const uint4*>(Chl);
+  const unsigned rblocks = (unsigned)(((int64_t)mq * 8 + 255) / 256);
+#define FDX_KNN3R(KK)                                                                                       \
+  knn_collect_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, lists, counts); \
+  knn_rerank_kernel<KK><<<rblocks, 256, 0, stream>>>(Q, C, mq, mc, mq_pad / 32, nsplit, self_offset, lists, counts, \
+                                                     out_idx, out_score)
+  switch (k) {
+    case 1: FDX_KNN3R(1); break;
+    case 2: FDX_KNN3R(2); break;
+    case 3: FDX_KNN3R(3); break;
+    case 4: FDX_KNN3R(4); break;
+    case 5: FDX_KNN3R(5); break;
+    case 6: FDX_KNN3R(6); break;
+    case 7: FDX_KNN3R(7); break;
+    case 8: FDX_KNN3R(8); break;
+    default: throw std::runtime_error("knn_topk3r: k must be in [1, 8]");
+  }
+#undef FDX_KNN3R
+  check_launch("knn_topk3r");
 }
 
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,

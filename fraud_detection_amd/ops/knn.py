@@ -29,6 +29,9 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 #   fp32lds 4-wave workgroups (128 queries) sharing double-buffered LDS-staged candidate chunks
 #           (4x fewer streamed bytes, half the occupancy);
 #   bf16x3  hi.hi + hi.lo + lo.hi bf16 MFMA filter (5.3x fewer MFMA cycles) + exact re-score.
+#   bf16x3r the same filter with no fp32 work in the tile loop: passing candidates are appended to
+#           per-lane lists under a provable lower-bound threshold, and a second kernel re-scores
+#           the listed candidates exactly (8 lanes per query) -- knn.hip knn_collect_kernel.
 # Measured on MI355X from 13.6k to 170k minority rows (profiles/r2_s3i/knn_engines.jsonl): fp32
 # is fastest at every size (46 -> 104 TFLOP/s-equivalent; fp32lds 0.66-0.99x, bf16x3 0.86-0.96x):
 # the search is bound by the per-tile filter/top-k bookkeeping beside the MFMA chain, neither by
@@ -40,7 +43,7 @@ def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:
     e = engine or os.environ.get("FDX_KNN", "auto")
     if e == "auto":
         return "bf16x3" if mc >= KNN_BF16X3_MIN_CANDIDATES else "fp32"
-    if e not in ("fp32", "fp32lds", "bf16x3"):
+    if e not in ("fp32", "fp32lds", "bf16x3", "bf16x3r"):
         raise ValueError(f"unknown k-NN engine {e!r}")
     return e
 
@@ -113,9 +116,10 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     if nsplit is not None:
         ns = max(1, int(nsplit))
     else:
-        ns = {"fp32": m.knn_splits, "fp32lds": m.knn_lds_splits, "bf16x3": m.knn3_splits}[eng](mq_pad, mc_pad)
+        ns = {"fp32": m.knn_splits, "fp32lds": m.knn_lds_splits, "bf16x3": m.knn3_splits,
+              "bf16x3r": m.knn3r_splits}[eng](mq_pad, mc_pad)
     ws_s = ws_i = None
-    if ns > 1:
+    if ns > 1 and eng != "bf16x3r":
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
     if eng == "fp32":
@@ -131,6 +135,13 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
         m.knn_split(ptr(Cp), mc_pad, 0, ptr(Chl), ptr(tmax), s)
         m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
+    if eng == "bf16x3r":
+        nb = ns * (mq_pad // 32) * 64
+        lists = torch.empty(nb * m.KNN3R_LIST_CAP, device=Q.device, dtype=torch.int32)
+        counts = torch.empty(nb, device=Q.device, dtype=torch.int32)
+        m.knn_topk3r(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
+                     int(k), ptr(idx), ptr(score), ptr(lists), ptr(counts), ns, s)
+    elif eng == "bf16x3":
         m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                     int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
     if want_dist:

@@ -293,7 +293,7 @@ def test_knn_topk_exact(dev, mq, k):
     assert not np.any(idx == (np.arange(mq)[:, None] + off))  # self excluded
 
 
-@pytest.mark.parametrize("engine", ["bf16x3", "fp32lds"])
+@pytest.mark.parametrize("engine", ["bf16x3", "bf16x3r", "fp32lds"])
 @pytest.mark.parametrize("mq,k,scale", [(400, 5, 1.0), (2500, 8, 1.0), (3000, 5, 40.0)])
 def test_knn_engine_exact(dev, mq, k, scale, engine):
     """The bf16x3 filter engine returns the exact fp32 ranking: same lists as the oracle (up to
@@ -328,6 +328,9 @@ def test_knn_engines_agree_with_ties_and_auto_selection(dev):
     b, sb = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="bf16x3")
     assert torch.equal(a, b)
     assert torch.allclose(sa, sb, rtol=0, atol=1e-4)
+    for ns in (1, 2, 5):  # collect + re-rank: bf16x3's exact re-score, so bit-identical to it
+        r, sr = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="bf16x3r", nsplit=ns)
+        assert torch.equal(a, r) and torch.equal(sb, sr)
     for ns in (1, 3, 40):  # the LDS engine runs the same MFMA chain: bit-identical lists + scores
         c, sc = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32lds", nsplit=ns)
         assert torch.equal(a, c) and torch.equal(sa, sc)
@@ -336,9 +339,22 @@ def test_knn_engines_agree_with_ties_and_auto_selection(dev):
     Cb = torch.from_numpy(rng.normal(size=(70_000, 32)).astype(np.float32)).to(dev)
     Qb = Cb[:256].contiguous()
     ia = K.knn_topk(Qb, Cb, k=5, self_offset=0, engine="fp32")
-    for eng in ("fp32lds", "bf16x3"):
+    for eng in ("fp32lds", "bf16x3", "bf16x3r"):
         ib = K.knn_topk(Qb, Cb, k=5, self_offset=0, engine=eng)
         assert (ia == ib).all(1).float().mean().item() > 0.99
+
+
+def test_knn_collect_list_overflow_falls_back_to_exact_scan(dev):
+    """All-equal candidates pass every tile's filter, so the per-lane lists overflow: the re-rank
+    kernel's exact scan must still return the k smallest indices (self excluded)."""
+    C = torch.ones((3000, 32), dtype=torch.float32, device=dev)
+    C[:, 30:] = 0.0
+    Q = C[:100].contiguous()
+    for ns in (None, 1):
+        idx = K.knn_topk(Q, C, k=5, self_offset=0, engine="bf16x3r", nsplit=ns).cpu().numpy()
+        for q in range(100):
+            want = [c for c in range(7) if c != q][:5]
+            assert list(idx[q]) == want, (q, idx[q])
 
 
 @pytest.mark.parametrize("nsplit", [2, 3, 7, 40])

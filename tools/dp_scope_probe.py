@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--fits", type=int, default=5)
     ap.add_argument("--scopes", default="shard,global")
     ap.add_argument("--solver", default="newton")
+    ap.add_argument("--storage", default="bf16")
+    ap.add_argument("--virtual", type=int, default=1, help="0: stored SMOTE rows (smote_generate + streamed)")
+    ap.add_argument("--phases", type=int, default=0, help="1: per-phase synced times of every synced fit")
     a = ap.parse_args()
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
@@ -42,7 +45,8 @@ def main():
     n_train = a.rows - a.rows // 5
     X, y = separable(n_train, seed=1000 + comm.rank, device=dev)
     for scope in a.scopes.split(","):
-        pipe = DevicePipeline(TrainConfig(seed=42, solver=a.solver, smote_scope=scope), comm)
+        pipe = DevicePipeline(TrainConfig(seed=42, solver=a.solver, smote_scope=scope, storage=a.storage,
+                                       virtual_smote=bool(a.virtual)), comm)
         for _ in range(2):
             pipe.fit(X, y)
         comm.barrier()
@@ -57,15 +61,17 @@ def main():
         back_to_back = (time.perf_counter() - t0) / a.fits
         prof.disable()
         coll = comm.collective_summary()
-        synced = []
+        synced, phased = [], []
         for _ in range(a.fits):
             comm.barrier()
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
-            r = pipe.fit(X, y)
+            r = pipe.fit(X, y, profile=bool(a.phases))
             pipe.settle()  # every rank verifies its pending fit here (a deferred check waits)
             torch.cuda.synchronize(dev)
             synced.append(round((time.perf_counter() - t1) * 1e3, 3))
+            if a.phases:
+                phased.append({k: round(v * 1e3, 3) for k, v in r.timings.items()})
         p = pipe.fit(X, y, profile=True)
         s = io.StringIO()
         pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
@@ -73,9 +79,11 @@ def main():
                "ms_synced": synced, "phase_ms": {k: round(v * 1e3, 3) for k, v in p.timings.items()},
                "n_train_rows": int(r.n_train_rows), "n_synthetic": int(r.n_synthetic),
                "newton_iters": int(r.fit.n_iter), "virtual_smote": pipe._virtual is not None,
-               "collectives": coll}
+               "collectives": coll, "storage": a.storage, "solver": a.solver}
+        if phased:
+            out["phases_synced"] = phased
+        print(json.dumps(out), flush=True)  # every rank: the two ranks share one GPU
         if comm.rank == 0:
-            print(json.dumps(out), flush=True)
             print(s.getvalue(), file=sys.stderr, flush=True)
     comm.close()
 

@@ -28,6 +28,7 @@
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
 #   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
 #   dpscope      tools/dp_scope_probe.py: global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo)
+#   dpstored     dp_scope_probe.py on stored SMOTE rows (bf16 and fp8), per-phase times of each synced fit
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -64,7 +65,7 @@ for st in "$@"; do
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
-    knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" ;;
+    knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" $FDX_KNN_ARGS ;;  # shellcheck disable=SC2086
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
     configs) step configs 900 python tools/baseline_configs.py --json "$OUT/configs.json" ;;
@@ -143,6 +144,12 @@ for st in "$@"; do
     dpscope)  # global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo): per-fit times, phases, host profile
       step dpscope 400 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
         --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29519 tools/dp_scope_probe.py --rows 2000000 ;;
+    dpstored)  # stored-SMOTE fits at global scope (2 ranks, one GPU, gloo): per-phase times of every synced fit
+      for ST in bf16 fp8; do
+        step "dpstored_$ST" 300 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
+          --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29521 tools/dp_scope_probe.py --rows 2000000 \
+          --scopes global,shard --storage $ST --virtual 0 --phases 1 --fits 6 || exit 1
+      done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
     *) echo "unknown stage $st"; exit 2 ;;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""k-NN (SMOTE self-search, k=5, fp32 engine) at the bench shapes: candidate slices.
+"""k-NN (SMOTE self-search, k=5) at the bench shapes: engines x candidate slices.
 
-    python tools/knn_lab.py [--reps 20] [--json out.json]
+    python tools/knn_lab.py [--reps 20] [--engines fp32,bf16x3r] [--json out.json]
 
 Shapes: DP1 (the 10M-row bench's 13.6k minority rows against themselves) and the DP=8 global-scope
 rank (its 13.6k minority rows against all 8 ranks' 108.8k).  For every nsplit the event-timed
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--json", default=None)
     ap.add_argument("--splits", default="1,2,4,8,16,32")
+    ap.add_argument("--engines", default="fp32")
     a = ap.parse_args()
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.ops import knn as K
@@ -53,24 +54,28 @@ def main():
         torch.cuda.synchronize()
         return float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps)]))
 
+    splitter = {"fp32": "knn_splits", "fp32lds": "knn_lds_splits", "bf16x3": "knn3_splits",
+                "bf16x3r": "knn3r_splits"}
     for name, (Q, Cc, off) in shapes.items():
         mq, mc = Q.shape[0], Cc.shape[0]
-        auto = native().knn_splits((mq + 31) // 32 * 32, (mc + 31) // 32 * 32)
         ref = K.knn_topk(Q, Cc, 5, off, engine="fp32")
-        rec = {"mq": mq, "mc": mc, "auto_nsplit": int(auto), "cases": []}
-        for ns in sorted({int(v) for v in a.splits.split(",")} | {int(auto)}):
-            f = lambda: K.knn_topk(Q, Cc, 5, off, engine="fp32", nsplit=ns)  # noqa: E731
-            got = f()
-            ms = timed(f)
-            case = {"nsplit": ns, "ms": round(ms, 4),
-                    "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
-                    "lists_equal": bool((got == ref).all().item())}
-            rec["cases"].append(case)
-            print(json.dumps({name: case}), flush=True)
-        best = min(rec["cases"], key=lambda c: c["ms"])
-        base = [c for c in rec["cases"] if c["nsplit"] == auto][0]
-        rec["best"], rec["auto"] = best, base
-        out["shapes"][name] = rec
+        for eng in a.engines.split(","):
+            mqp = (mq + 31) // 32 * 32 if eng != "fp32lds" else (mq + 127) // 128 * 128
+            auto = getattr(native(), splitter[eng])(mqp, (mc + 31) // 32 * 32)
+            rec = {"engine": eng, "mq": mq, "mc": mc, "auto_nsplit": int(auto), "cases": []}
+            for ns in sorted({int(v) for v in a.splits.split(",")} | {int(auto)}):
+                f = lambda: K.knn_topk(Q, Cc, 5, off, engine=eng, nsplit=ns)  # noqa: E731
+                got = f()
+                ms = timed(f)
+                case = {"engine": eng, "nsplit": ns, "ms": round(ms, 4),
+                        "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
+                        "lists_equal": bool((got == ref).all().item())}
+                rec["cases"].append(case)
+                print(json.dumps({name: case}), flush=True)
+            best = min(rec["cases"], key=lambda c: c["ms"])
+            base = [c for c in rec["cases"] if c["nsplit"] == auto][0]
+            rec["best"], rec["auto"] = best, base
+            out["shapes"][f"{name}:{eng}"] = rec
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(out, fh, indent=1)
