@@ -109,6 +109,7 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     if progress.folds:
         say(f" Resuming: {len(progress.folds)} completed fold(s) from {progress.path}")
     res_cv = None
+    cv_engine = None
     if cv_folds and cv_folds > 1 and pos >= cv_folds:
         say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
         if mode == "device":
@@ -126,11 +127,23 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
             t_fit = time.perf_counter()
             with tracing.span("train.cv_job", model=model_type), tracing.roctx_range("train.cv_job"):
                 cvr = DeviceCV(cfg, cv_folds, seed=42).run(Xtr, ytr)
-            cv_scores, res_cv = cvr.fold_aucs, cvr.final
+            cv_scores, res_cv, cv_engine = cvr.fold_aucs, cvr.final, "device"
+            for k, auc in enumerate(cv_scores):
+                progress.record(k, auc)
+        elif _device_gbdt_cv_ok(model_type, cfg, dev, comm, progress):
+            # models/gbdt_cv.DeviceGBDTCV: one binned fold-sorted table, fold k fits around its own
+            # block (row hole, no copy), its margins are the validation scores; final fit included
+            from .models.gbdt_cv import DeviceGBDTCV
+
+            t_fit = time.perf_counter()
+            with tracing.span("train.cv_job", model=model_type), tracing.roctx_range("train.cv_job"):
+                cvr = DeviceGBDTCV(cfg, n_folds=cv_folds, seed=42).run(Xtr, ytr)
+            cv_scores, res_cv, cv_engine = cvr.fold_aucs, cvr.final, "device"
             for k, auc in enumerate(cv_scores):
                 progress.record(k, auc)
         else:
             cv_scores = _cross_validate(model_type, cfg, folds, take, comm, cv_mode, progress)
+            cv_engine = f"per_fold:{cv_mode}"
         for k, auc in enumerate(cv_scores):
             say(f"  Fold {k + 1} AUC: {auc:.4f}")
         say(f" CV AUC Mean: {np.mean(cv_scores):.4f} (+/- {np.std(cv_scores) * 2:.4f})")
@@ -178,6 +191,7 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
     except Exception as e:  # noqa: BLE001 - tracking is best effort (reference train_model.py:165-166)
         say(f" MLflow Tracking Failed (likely connection error): {e}")
     summary["split"] = mode
+    summary["cv_engine"] = cv_engine
     summary["resumed_folds"] = sorted(progress.resumed)
     if comm is not None:
         summary["world_size"] = comm.world_size
@@ -266,6 +280,14 @@ def _device_cv_ok(model_type, cfg, dev, comm, progress, Xtr) -> bool:
     return (model_type == "logistic" and dev.type == "cuda" and comm is None and not progress.folds
             and cfg.smote and cfg.virtual_smote and cfg.fold_scaler and virt and Xtr.shape[1] % 2 == 0
             and Xtr.is_contiguous())
+
+
+def _device_gbdt_cv_ok(model_type, cfg, dev, comm, progress) -> bool:
+    """The device GBDT CV job (models/gbdt_cv.py) runs on one GPU, from scratch (a resumed job
+    keeps the per-fold path), with SMOTE inside the folds (the reference's semantics)."""
+    if os.environ.get("FDX_CV_ENGINE", "auto") == "per_fold":
+        return False
+    return model_type == "gbdt" and dev.type == "cuda" and comm is None and not progress.folds and cfg.smote
 
 
 def _fit(model_type, cfg, X, y, comm=None, checkpoint: str | None = None):
