@@ -591,7 +591,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("sgd_run", [sgd_args](u X, int fp8, float x_scale, int64_t end, u w32, u cw, u done, u partial, int blocks,
                               u s, u parents, u nbr, u lam, u off, u cnt, int64_t n_real, int64_t q_offset, int mq,
                               int k, int64_t hole_at, int64_t hole_len, u state, u aff, int d, double C, double mom,
-                              int fi, double tol, int nb, int epochs, int average, std::vector<double> lrs, int s0,
+                              int fi, double tol, int nb, int epochs, int avg_from, std::vector<double> lrs, int s0,
                               int s1, u acc, u ticket, std::vector<int> subs) {
     if (nb < 1 || epochs < 1 || (int)lrs.size() < epochs || (int)subs.size() < epochs || s0 < 0 || s1 > nb * epochs)
       throw std::runtime_error("sgd_run: bad schedule");
@@ -616,7 +616,7 @@ PYBIND11_MODULE(_fdx_native, m) {
       const int ep = st / nb, b = st % nb, sub = subs[ep];
       // sub-sampled epoch: phase b * sub of a grid of nb * sub minibatches; never decides convergence
       const int rsub = nb * sub, ph = b * sub;
-      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, rsub, average && ep == epochs - 1, b == nb - 1,
+      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, rsub, ep >= avg_from, b == nb - 1,
                                       sub > 1 ? -1.0 : tol);
       if (acc) {  // one launch per step (fixed-point atomics + last-block update)
         fdx::launch_sgd_pass_fused(P<const void>(X), fp8, x_scale, end, P<float>(w32), P<const float>(cw), P<int>(done),
@@ -660,7 +660,7 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("sgd_persist", [smote_view](u X, int fp8, float x_scale, int64_t end, u cw, u parents, u nbr, u lam, u off,
                                     u cnt, int64_t n_real, int64_t q_offset, int mq, int k, int64_t hole_at,
                                     int64_t hole_len, u ws, u state, u w32, u done, u aff, int d, double C, double mom,
-                                    int fi, double tol, int nb, int epochs, int average, int serpentine,
+                                    int fi, double tol, int nb, int epochs, int avg_from, int serpentine,
                                     std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps,
                                     std::vector<int> subs) {
     if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
@@ -687,7 +687,7 @@ PYBIND11_MODULE(_fdx_native, m) {
     a.fit_intercept = fi;
     a.nb = nb;
     a.epochs = epochs;
-    a.average = average;
+    a.avg_from = avg_from;
     a.serpentine = serpentine;
     a.s0 = s0;
     a.s1 = s1;

@@ -222,7 +222,9 @@ struct SgdPersistArgs {
   double C = 1.0, momentum = 0.5, tol = 1e-3;
   double lr[kSgdMaxEpochs] = {};
   int sub[kSgdMaxEpochs] = {1, 1, 1, 1, 1, 1, 1, 1};  // per-epoch row sub-sample (1 = every row)
-  int d = 30, fit_intercept = 1, nb = 1, epochs = 1, average = 1, serpentine = 0;
+  // avg_from: steps of epochs >= avg_from add to the Polyak average (each such epoch returns its
+  // own average); >= epochs: no averaging
+  int d = 30, fit_intercept = 1, nb = 1, epochs = 1, avg_from = 0, serpentine = 0;
   int s0 = 0, s1 = 0;
   int64_t Gw = 0;  // waves of the per-step pass grid (4 x its blocks): sets the minibatch partition
   unsigned long long* stamps = nullptr;  // nullable: [steps][3][blocks] wall_clock64 at pass end,

@@ -1666,7 +1666,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     a.momentum = P.momentum;
     a.fit_intercept = P.fit_intercept;
     a.nb = rsub;  // the minibatch estimates the epoch's weight as rsub x its own
-    a.avg = P.average && ep == P.epochs - 1;
+    a.avg = ep >= P.avg_from;
     a.epoch_end = pos == P.nb - 1;
     a.tol = P.sub[ep] > 1 ? -1.0 : P.tol;  // a sub-sampled epoch never decides convergence
     sgd_apply(rd, sst, wnew, &s_done, P.aff, a, t, true);

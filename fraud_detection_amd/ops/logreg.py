@@ -670,6 +670,12 @@ SGD_LR = (0.4, 0.7, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 
 # relative above the Newton objective, streaming 2.25 epochs instead of 3 (3 full epochs with
 # (0.4, 0.6, 0.8): 3.6e-4, 4.2e-5).  A sub-sampled epoch never decides convergence.
 SGD_SUB = (4, 1, 1)
+# Epochs past SGD_EPOCHS that run only while the fit has not converged (the device `done` flag makes
+# them no-ops otherwise; the persistent launch leaves its loop).  Each is averaged like the last
+# nominal epoch, starting from that epoch's averaged iterate.  fp8 rows carry ~6% quantisation
+# noise per feature, which slows the last digits of the epoch gradient (round 4: 1.4e-3 after 3
+# epochs, profiles/r4_c); bf16 rows converge in the nominal 3 and never run it.
+SGD_EXTRA_EPOCHS = 1
 SGD_MOMENTUM = 0.55
 SGD_TOL = 1e-3                # on the epoch gradient max-norm (sklearn SGDClassifier's default tol)
 SGD_SLOTS = 36
@@ -714,7 +720,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             checkpoint_every: int = 0, affine: torch.Tensor | None = None, virtual: VirtualSmote | None = None,
             batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None,
             persistent: bool | None = None, serpentine: bool = False, subsample=SGD_SUB,
-            _stamps: torch.Tensor | None = None):
+            extra_epochs: int = 0, _stamps: torch.Tensor | None = None):
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
@@ -743,7 +749,10 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     unless FDX_SGD_PERSIST=0.  ``serpentine``: odd epochs visit the minibatches in reverse order
     (persistent launch only), so an epoch's first minibatches are the previous epoch's last ones
     -- still resident in the 256 MB Infinity Cache.  ``subsample``: per-epoch row sub-sample factors
-    (SGD_SUB; an epoch with factor s visits 1/s of the rows in its nb minibatches)."""
+    (SGD_SUB; an epoch with factor s visits 1/s of the rows in its nb minibatches).
+    ``extra_epochs``: epochs after ``epochs`` that run only if the fit has not converged yet
+    (the pipelines pass SGD_EXTRA_EPOCHS); with ``average`` each of them returns its own Polyak average, like the
+    last nominal epoch."""
     check_rows(rows)
     w0 = _default_w0(w0)
     rows, hole = _apply_hole(rows, hole)
@@ -756,8 +765,11 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     nb = max(1, int(batches))
     if comm is not None and comm.world_size > 1:
         nb = int(comm.all_reduce_scalar(nb, op="max"))
-    lrs = [_epoch_lr(lr, e) for e in range(max(epochs, 1))]
-    subs = [int(_epoch_lr(subsample, e)) if subsample is not None else 1 for e in range(max(epochs, 1))]
+    nominal = max(int(epochs), 1)
+    epochs = nominal + max(0, int(extra_epochs))  # the schedule's length from here on
+    avg_from = nominal - 1 if average else epochs  # averaged epochs: the last nominal one and the extras
+    lrs = [_epoch_lr(lr, e) for e in range(epochs)]
+    subs = [int(_epoch_lr(subsample, e)) if subsample is not None else 1 for e in range(epochs)]
     if any(x < 1 for x in subs):
         raise ValueError("sub-sample factors must be >= 1")
     # a sub-sampled epoch only where every minibatch of its finer grid still holds row tiles of the
@@ -772,25 +784,25 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         if virtual is not None:  # the samples interpolate shifted parents: map them the same way
             vr = ((virtual.rows_f32().double() - a[:32]) * a[32:]).float()
             vr[:, LABEL_COL] = virtual.label
-            return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept,
+            return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0, d, fit_intercept,
                                 comm, fp8_scale, checkpoint, checkpoint_every, None, None, virtual=(virtual, vr),
-                                max_steps=max_steps, serpentine=serpentine, subs=subs)
+                                max_steps=max_steps, serpentine=serpentine, subs=subs, nominal=nominal)
         affine = None
     aff = 0
     if affine is not None:
         if affine.dtype != torch.float64 or affine.numel() != 64 or affine.device != rows.device:
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
-    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine,
+    sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, avg_from, tol, class_w, fit_intercept, comm, serpentine,
                           subs)
            if checkpoint else None)
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
     if not rows.is_cuda:
         vv = (virtual, virtual.rows_f32()) if virtual is not None else None
-        return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm,
+        return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0, d, fit_intercept, comm,
                             fp8_scale, checkpoint, checkpoint_every, sig, got, virtual=vv, max_steps=max_steps,
-                            serpentine=serpentine, subs=subs)
+                            serpentine=serpentine, subs=subs, nominal=nominal)
     if virtual is not None:
         virtual.check(rows)
         if class_w[1] > VIRTUAL_MAX_WEIGHT:
@@ -833,30 +845,32 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         if persist:
             m.sgd_persist(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.class_w), *vargs,
                           ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
-                          float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
-                          int(bool(serpentine)), [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(s1),
-                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs[:max(epochs, 1)])
+                          float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
+                          int(bool(serpentine)), [float(x) for x in lrs], int(s0), int(s1),
+                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs)
             return
         if serpentine:
             raise ValueError("serpentine minibatch order needs the persistent SGD launch")
         m.sgd_run(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w), ptr(ws.done),
                   ptr(ws.partial), blocks, s, *vargs, ptr(ws.state), aff, d,
-                  float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(bool(average)),
-                  [float(x) for x in lrs[:max(epochs, 1)]], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
-                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs[:max(epochs, 1)])
+                  float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
+                  [float(x) for x in lrs], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
+                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs)
 
     if not dp and checkpoint is None:
         s0 = start[0] * nb + start[1]
         run_steps(s0, epochs * nb if max_steps is None else min(epochs * nb, int(max_steps)))
         return PendingFit(ws.state, sgd=True)
     for ep in range(start[0], epochs):
+        if ep >= nominal and int(ws.done.item()):  # converged: the extra epochs would be no-ops
+            break
         c = lrs[ep]
         for pos in range(start[1] if ep == start[0] else 0, nb):
             if max_steps is not None and ep * nb + pos >= max_steps:
                 break
             b = _sgd_phase(pos, ep, nb, serpentine)
             rsub, ph = nb * subs[ep], b * subs[ep]
-            avg = int(average and ep == epochs - 1)
+            avg = int(ep >= avg_from)
             last = pos + 1 == nb
             if dp:
                 # lean step: the pass leaves its fixed-point sums (int64: the all-reduce is exact and
@@ -956,9 +970,9 @@ def _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm,
                    objective=st.obj, grad_max=st.gmax, history=hist)
 
 
-def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, d, fit_intercept, comm, fp8_scale,
+def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0, d, fit_intercept, comm, fp8_scale,
                  checkpoint=None, checkpoint_every=0, sig=None, got=None, virtual=None, max_steps=None,
-                 serpentine=False, subs=None):
+                 serpentine=False, subs=None, nominal=None):
     """The device SGD's algorithm in fp64 (ref.SgdStateRef) over the same minibatch partition:
     stored row tiles by the pass grid's strided walk (the full SGD grid of a 256-CU part,
     ref.SGD_FULL_BLOCKS, shrunk for small shards like the device), virtual samples by their pick tile."""
@@ -998,6 +1012,8 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
         st.done = st.converged
         start = (int(got[1]["epoch"]), int(got[1]["batch"]))
     for ep in range(start[0], epochs):
+        if nominal is not None and ep >= nominal and st.done:  # converged: extra epochs are no-ops
+            break
         for pos in range(start[1] if ep == start[0] else 0, nb):
             if max_steps is not None and ep * nb + pos >= max_steps:
                 break
@@ -1015,7 +1031,7 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, average, tol, class_w, w0, 
                 red = comm.all_reduce(torch.from_numpy(red)).numpy()
             last = pos + 1 == nb
             st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nb * subs[ep],
-                    bool(average and ep == epochs - 1), last, -1.0 if subs[ep] > 1 else tol, fit_intercept)
+                    ep >= avg_from, last, -1.0 if subs[ep] > 1 else tol, fit_intercept)
             gstep = ep * nb + pos + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 sv = np.zeros(STATE_SIZE)

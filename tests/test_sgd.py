@@ -70,3 +70,20 @@ def test_sgd_virtual_cpu_matches_stored_samples():
     pb = ref.sgd_pick_batches(400, 3)[pick.astype(np.int64)]
     for b in range(3):
         assert (real[rb == b, 31] == 0).any() and (pb == b).any()
+
+
+def test_extra_epochs_run_only_until_converged_cpu():
+    """extra_epochs: a converged fit never runs them (same model as without), an unconverged one
+    runs them, each averaged like the last nominal epoch."""
+    X, y = separable(60_000, fraud_rate=0.3, seed=9)
+    st = S.scaler_fit(X)
+    z = S.scale_cast(X, st, labels=y, out_dtype="f32")
+    base = L.sgd_fit(z, batches=4, epochs=2, tol=1.0)  # loose tol: converged at the first full epoch end
+    more = L.sgd_fit(z, batches=4, epochs=2, tol=1.0, extra_epochs=2)
+    assert base.converged and more.converged and more.n_iter == base.n_iter <= 8
+    assert np.array_equal(base.w, more.w)
+    a = L.sgd_fit(z, batches=4, epochs=2, tol=0.0)  # never converges: every extra epoch runs
+    b = L.sgd_fit(z, batches=4, epochs=2, tol=0.0, extra_epochs=1)
+    assert a.n_iter == 8 and b.n_iter == 12 and not b.converged
+    R = z.double().numpy()
+    assert _objective(R, b.w) <= _objective(R, a.w) + 1e-12
