@@ -810,6 +810,7 @@ PYBIND11_MODULE(_fdx_native, m) {
     fdx::launch_quantile_select(P<const float>(X), m, stride, ld, d, max_bin, P<void>(ws), P<float>(out), S(s));
   });
   m.def("gbdt_hist_slot_words", [] { return fdx::gbdt_hist_slot_words(); });
+  m.def("set_gbdt_hist_variant", [](int v) { fdx::set_gbdt_hist_variant(v); });
   m.def("gbdt_hist", [](u bins, u gh, u ridx, u seg, u gcnt, int level, int d, u hist, u slots, u s,
                         int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
     fdx::launch_gbdt_hist(P<const uint8_t>(bins), P<const uint32_t>(gh), P<const int>(ridx), P<const int64_t>(seg),

@@ -248,15 +248,22 @@ __device__ __forceinline__ int64_t level_chunk(const LevelNodes& L, int level, i
 constexpr int kHistStrideRot = kGBBins + 1;
 constexpr int kHistWordsRot = 32 * kHistStrideRot;  // 8224 u64 = 64.25 KiB (two blocks per CU fit)
 constexpr int kHistBatchRot = 4;  // rows in flight per thread
-template <bool ROT>
-__global__ __launch_bounds__(kHistThreads, ROT ? 4 : 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
+// SPLIT (lab variant 2): g and h in two int32 sub-histograms, two ds_add_u32 per (row, feature)
+// instead of one 64-bit packed add -- a wave's 64 lanes then spread over 64 single-dword banks
+// rather than 32 bank pairs.  Same sums (int32 exact within a flush), same flush layout.
+enum HistVariant : int { kHistLockstep = 0, kHistRot = 1, kHistSplit = 2 };
+template <int VAR>
+__global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
                                                                            // (ROT: 1 block/CU, <= 128 VGPRs)
     const uint8_t* __restrict__ bins, const uint32_t* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
     long long* __restrict__ slots, int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
+  constexpr bool ROT = VAR == kHistRot, SPLIT = VAR == kHistSplit;
   constexpr int kStride = ROT ? kHistStrideRot : kGBBins;
   constexpr int kBatch = ROT ? kHistBatchRot : kHistBatch;
   __shared__ unsigned long long sh[ROT ? kHistWordsRot : kHistWords];
+  int* const shg = reinterpret_cast<int*>(sh);  // SPLIT: g at [f * 256 + b], h kHistWords ints later
+  int* const shh = shg + kHistWords;
   __shared__ LevelNodes lv;
   const int h0 = heap_first(level), nn = 1 << level;
   load_level(lv, seg, gcnt, level);
@@ -283,7 +290,14 @@ __global__ __launch_bounds__(kHistThreads, ROT ? 4 : 8) void gbdt_hist_kernel(  
     long long* dst = slots + (int64_t)my_slot * kHistEntries;
     for (int64_t c0 = lo; c0 < hi; c0 += flush_rows) {
       const int64_t c1 = min(hi, c0 + flush_rows);
-      for (int i = threadIdx.x; i < nw; i += kHistThreads) sh[ROT ? (i >> 8) * kStride + (i & 255) : i] = 0ull;
+      for (int i = threadIdx.x; i < nw; i += kHistThreads) {
+        if constexpr (SPLIT) {
+          shg[i] = 0;
+          shh[i] = 0;
+        } else {
+          sh[ROT ? (i >> 8) * kStride + (i & 255) : i] = 0ull;
+        }
+      }
       __syncthreads();
       // kBatch rows per thread in flight: every row index, then every row's bins and (g, h),
       // are loaded before the first atomic.  Level 0 reads rows in order (ridx is the identity
@@ -343,6 +357,17 @@ __global__ __launch_bounds__(kHistThreads, ROT ? 4 : 8) void gbdt_hist_kernel(  
               }
               if ((jj & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // keep the live ranges short
             }
+          } else if constexpr (SPLIT) {
+            const int qg = (int)(uint32_t)(pk[u] & 0xffffffffull);  // the packed word's (g, h)
+            const int qh = (int)((pk[u] - (unsigned long long)(long long)qg) >> 32);
+#pragma unroll
+            for (int f = 0; f < kGBMaxFeat; ++f) {
+              if (f < d) {
+                const int b = (words[u][f >> 2] >> (8 * (f & 3))) & 0xff;
+                atomicAdd(shg + f * kGBBins + b, qg);
+                atomicAdd(shh + f * kGBBins + b, qh);
+              }
+            }
           } else {
 #pragma unroll
             for (int f = 0; f < kGBMaxFeat; ++f) {
@@ -357,16 +382,22 @@ __global__ __launch_bounds__(kHistThreads, ROT ? 4 : 8) void gbdt_hist_kernel(  
       __syncthreads();
       const bool first = c0 == lo;  // later flushes of the same slot accumulate (block-private)
       for (int i = threadIdx.x; i < nw; i += kHistThreads) {
-        const unsigned long long x = sh[ROT ? (i >> 8) * kStride + (i & 255) : i];
-        const long long sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
-        const long long shh = (long long)(x - (unsigned long long)sg) >> 32;
+        long long sg, sgh;
+        if constexpr (SPLIT) {
+          sg = shg[i];
+          sgh = shh[i];
+        } else {
+          const unsigned long long x = sh[ROT ? (i >> 8) * kStride + (i & 255) : i];
+          sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
+          sgh = (long long)(x - (unsigned long long)sg) >> 32;
+        }
         long long* e = dst + 2 * i;
         if (first) {
           e[0] = sg;
-          e[1] = shh;
+          e[1] = sgh;
         } else {
           e[0] += sg;
-          e[1] += shh;
+          e[1] += sgh;
         }
       }
       __syncthreads();
@@ -969,6 +1000,12 @@ int gbdt_hist_blocks() {
 
 int64_t gbdt_hist_slot_words() { return (int64_t)(gbdt_hist_blocks() + 2 * kGBMaxNodes) * kHistEntries; }
 
+static int g_hist_variant = -1;  // set_gbdt_hist_variant (tests / labs); -1: the environment's choice
+void set_gbdt_hist_variant(int v) {
+  if (v < -1 || v > 2) throw std::invalid_argument("gbdt hist variant: -1 (env), 0 lockstep, 1 rot, 2 split");
+  g_hist_variant = v;
+}
+
 void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
                       hipStream_t stream, int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
@@ -980,16 +1017,23 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   // at most blocks + nodes pairs)
   if (level < 0 || (1 << level) > kGBMaxNodes + 1) throw std::runtime_error("gbdt_hist: level out of range");
   const int nb = gbdt_hist_blocks();
-  static const bool rot = [] {  // lab switch (FDX_GBDT_HIST_ROT=1: the rotated-feature form)
-    const char* e = std::getenv("FDX_GBDT_HIST_ROT");
-    return e != nullptr && e[0] == '1';
+  static const int env_var = [] {  // lab switch FDX_GBDT_HIST_VAR: 1 rotated features, 2 split g/h adds
+    const char* e = std::getenv("FDX_GBDT_HIST_VAR");
+    const char* r = std::getenv("FDX_GBDT_HIST_ROT");  // older spelling of variant 1
+    if (e != nullptr && (e[0] == '1' || e[0] == '2')) return e[0] - '0';
+    return (r != nullptr && r[0] == '1') ? 1 : 0;
   }();
+  const int var = g_hist_variant >= 0 ? g_hist_variant : env_var;
+  const bool rot = var == kHistRot;
   if (rot)  // one block per CU (its rotation registers): half the blocks of the lockstep form
-    gbdt_hist_kernel<true><<<nb / 2, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows,
-                                                                 hole_at, hole_len);
+    gbdt_hist_kernel<kHistRot><<<nb / 2, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
+                                                                    flush_rows, hole_at, hole_len);
+  else if (var == kHistSplit)
+    gbdt_hist_kernel<kHistSplit><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
+                                                                  flush_rows, hole_at, hole_len);
   else
-    gbdt_hist_kernel<false><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots, flush_rows,
-                                                              hole_at, hole_len);
+    gbdt_hist_kernel<kHistLockstep><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
+                                                                     flush_rows, hole_at, hole_len);
   check_launch("gbdt_hist");
   const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, level == 0 ? 1u : 1u << (level - 1));
   gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, rot ? nb / 2 : nb, hist);

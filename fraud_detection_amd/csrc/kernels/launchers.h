@@ -344,6 +344,8 @@ int64_t gbdt_hist_slot_words();  // int64 words of the per-(node, block) histogr
 // hole_at / hole_len (hist and partition): the fit's rows are the table minus the block
 // [hole_at, hole_at + hole_len) -- a cross-validation fold on the fold-sorted table (n counts the
 // fit's rows, not the table's)
+// histogram kernel variant for labs/tests (-1: FDX_GBDT_HIST_VAR; 0 lockstep, 1 rotated, 2 split g/h)
+void set_gbdt_hist_variant(int v);
 void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
                       hipStream_t stream, int64_t flush_rows = 0, int64_t hole_at = 0, int64_t hole_len = 0);

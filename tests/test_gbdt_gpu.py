@@ -177,6 +177,28 @@ def test_hist_multi_flush_bit_identical(dev, monkeypatch):
     assert np.array_equal(a.feat[0], ref.feat[0]) and np.array_equal(a.bin[0], ref.bin[0])
 
 
+@pytest.mark.parametrize("var", [1, 2])
+def test_hist_variants_bit_identical(dev, var):
+    """The histogram kernel's lab variants (rotated features; split int32 g/h adds) build the same
+    integer histograms, so the trees and margins are bit-identical to the lockstep form."""
+    from fraud_detection_amd.ops.native import native
+
+    Xd, yd, X, y = _data(150_000, 30, seed=16)
+    p = gb.GBDTParams(n_estimators=3, max_depth=5)
+    cuts = R.quantile_cuts(X, 256)
+    m = native()
+    try:
+        m.set_gbdt_hist_variant(0)
+        a, ma = gb.fit(Xd, yd, p, cuts=cuts, return_margin=True, use_graph=False)
+        m.set_gbdt_hist_variant(var)
+        b, mb = gb.fit(Xd, yd, p, cuts=cuts, return_margin=True, use_graph=False)
+    finally:
+        m.set_gbdt_hist_variant(-1)
+    for k in ("feat", "bin", "thr", "gain", "leaf"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert torch.equal(ma, mb)
+
+
 def test_gbdt_deterministic_runs(dev):
     Xd, yd, X, y = _data(50_000, 30, seed=14)
     p = gb.GBDTParams(n_estimators=8, max_depth=5)

@@ -28,6 +28,7 @@
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
 #   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
 #   dpscope      tools/dp_scope_probe.py: global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo)
+#   gbdtvar      GBDT histogram kernel variants under a kernel trace (FDX_GBDT_HIST_VAR=0/2/1)
 #   dpstored     dp_scope_probe.py on stored SMOTE rows (bf16 and fp8), per-phase times of each synced fit
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
@@ -126,6 +127,14 @@ for st in "$@"; do
       step pmcgbdt_a 180 rocprofv3 --kernel-include-regex "gbdt_hist_kernel" --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM --output-format csv -d "$OUT/pmcgbdt_a" -o run -- $GB
       step pmcgbdt_b 180 rocprofv3 --kernel-include-regex "gbdt_hist_kernel" --pmc SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS --output-format csv -d "$OUT/pmcgbdt_b" -o run -- $GB
       step pmcgbdt_t 180 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pmcgbdt_t" -o run -- $GB
+      cd "$R" ;;
+    gbdtvar)  # GBDT histogram variants (0 lockstep, 2 split g/h int32 adds, 1 rotated): kernel stats, 10 trees
+      cd /tmp && export TMPDIR=/tmp
+      for V in 0 2 1; do
+        export FDX_GBDT_HIST_VAR=$V
+        step "gbdtvar_$V" 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gbdtvar_$V" -o run -- python3 "$R/tools/gbdt_bench.py" --rows 10000000 --trees 10 || exit 1
+      done
+      unset FDX_GBDT_HIST_VAR
       cd "$R" ;;
     pmcks)  # KernelSHAP linear kernel counters (3 passes, 1000-explanation batches)
       cd /tmp && export TMPDIR=/tmp
