@@ -326,3 +326,69 @@ def test_host_value_exchanges_use_the_cpu_group(tmp_path):
         assert d["got"].tolist() == [[q, 10 * q + 1] for q in range(world)]
         assert float(d["s"]) == 6.0 and float(d["mx"]) == 2.0 and float(d["mn"]) == 5.0
         assert "all_gather_ints" in json.loads(str(d["stats"]))
+
+
+def _sgd_rows():
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.ops import scaler as S
+
+    X, y = separable(30_000, fraud_rate=0.1, seed=77)
+    st = S.scaler_fit(X)
+    return S.scale_cast(X, st, labels=y, out_dtype="f32")
+
+
+def _sgd_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from fraud_detection_amd.ops import logreg as L
+    from fraud_detection_amd.parallel.comm import Communicator
+
+    comm = Communicator(backend="gloo")
+    R = _sgd_rows()
+    n = R.shape[0]
+    sh = slice(rank * n // world, (rank + 1) * n // world)
+    f = L.sgd_fit(R[sh].contiguous(), batches=4, epochs=2, tol=0.0, comm=comm, subsample=None, extra_epochs=1)
+    np.savez(os.path.join(out_dir, f"s{rank}.npz"), w=f.w, n_iter=f.n_iter, obj=f.objective, gmax=f.grad_max)
+    comm.barrier()
+    comm.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dp_sgd_global_minibatch_is_the_union_of_shard_minibatches(tmp_path, world):
+    """Data-parallel SGD: every step's minibatch is the union of the ranks' local minibatch b (their
+    own strided row tiles), its sums all-reduced -- so all ranks hold one model, equal to the fp64
+    mirror run over those unions (extra epochs included: tol 0 never converges)."""
+    from fraud_detection_amd.ops import logreg as L
+    from fraud_detection_amd.ops import reference as ref
+    from fraud_detection_amd.ops.layout import LABEL_COL
+
+    port = _free_port()
+    mp.start_processes(_sgd_worker, args=(world, port, str(tmp_path)), nprocs=world, start_method="spawn")
+    outs = [dict(np.load(os.path.join(tmp_path, f"s{r}.npz"))) for r in range(world)]
+    for o in outs[1:]:
+        assert np.array_equal(o["w"], outs[0]["w"])
+    R = _sgd_rows().double().numpy()
+    n, nb, epochs = R.shape[0], 4, 3
+    parts = []
+    for r in range(world):
+        lo, hi = r * n // world, (r + 1) * n // world
+        parts.append((lo, ref.sgd_row_batches(hi - lo, nb, ref.sgd_grid_blocks(hi - lo, nb, ref.SGD_FULL_BLOCKS))))
+    st = ref.SgdStateRef(np.zeros(32))
+    for ep in range(epochs):
+        for b in range(nb):
+            red = np.zeros(36)
+            for lo, bt in parts:
+                Rb = R[lo + np.nonzero(bt == b)[0]]
+                g, loss, wsum, _ = ref.logreg_pass(Rb, st.w, (1.0, 1.0), False)
+                X = Rb.copy()
+                X[:, LABEL_COL] = 0.0
+                wv = st.w.copy()
+                wv[LABEL_COL] = 0.0
+                p = ref.sigmoid(X @ wv)
+                red += np.concatenate([g, [loss, wsum, 0.0, float(np.sum(p * (1 - p)))]])
+            st.step(red[:32], red[32], red[33], red[35], 30, 1.0, L._epoch_lr(L.SGD_LR, ep), L.SGD_MOMENTUM, nb,
+                    ep >= 1, b == nb - 1, 0.0)
+    assert int(outs[0]["n_iter"]) == epochs * nb == st.iter
+    w = st.w.copy()
+    w[LABEL_COL] = 0.0
+    np.testing.assert_allclose(outs[0]["w"], w, rtol=1e-9, atol=1e-12)

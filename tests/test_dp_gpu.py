@@ -58,7 +58,7 @@ def test_dp_two_ranks_on_one_gpu(tmp_path):
 N_GLOBAL = 1_500_000  # raw rows per rank of the global-scope test
 
 
-def _worker_global(rank, world, port, out_dir, solver):
+def _worker_global(rank, world, port, out_dir, solver, virtual=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK="0")
     from fraud_detection_amd.data.synthetic import separable
@@ -69,13 +69,14 @@ def _worker_global(rank, world, port, out_dir, solver):
     torch.cuda.set_device(dev)
     comm = Communicator(backend="gloo")
     X, y = separable(N_GLOBAL, seed=700 + rank, device=dev)
-    pipe = DevicePipeline(TrainConfig(smote_scope="global", solver=solver, tol=1e-8, max_iter=40, init_std=0.0),
-                          comm)
+    pipe = DevicePipeline(TrainConfig(smote_scope="global", solver=solver, tol=1e-8, max_iter=40, init_std=0.0,
+                                      virtual_smote=virtual), comm)
     res = pipe.fit(X, y)
     res2 = pipe.fit(X, y)  # a second fit through the same buffers (deferred-check path under DP)
     pipe.settle()  # the collective point where every rank verifies its pending fits
     np.savez(os.path.join(out_dir, f"g{rank}.npz"), w=res.w, w2=res2.w, n_train=res.n_train_rows,
-             n_syn=res.n_synthetic, iters=res.fit.n_iter, virtual=pipe._virtual is not None)
+             n_syn=res.n_synthetic, iters=res.fit.n_iter, virtual=pipe._virtual is not None,
+             conv=res.fit.converged, gmax=res.fit.grad_max)
     comm.barrier()
     comm.close()
 
@@ -102,3 +103,47 @@ def test_dp_global_scope_virtual_smote_equals_single_process(tmp_path):
     assert sum(int(o["n_syn"]) for o in outs) == ref.n_synthetic
     np.testing.assert_allclose(outs[0]["w"], ref.w, atol=2e-6, rtol=0)
     assert abs(int(outs[0]["iters"]) - int(ref.fit.n_iter)) <= 1
+
+
+def test_dp_global_scope_stored_smote_equals_single_process(tmp_path):
+    """The stored-SMOTE fallback (samples written by smote_generate and streamed, the path past
+    the bucket sort's range) under DP at global scope: both ranks' model equals the single-process
+    fit on the concatenated shards."""
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+    port = _port()
+    mp.start_processes(_worker_global, args=(2, port, str(tmp_path), "newton", False), nprocs=2,
+                       start_method="spawn")
+    outs = [dict(np.load(tmp_path / f"g{r}.npz")) for r in range(2)]
+    assert not any(bool(o["virtual"]) for o in outs)
+    assert np.array_equal(outs[0]["w"], outs[1]["w"]) and np.array_equal(outs[0]["w2"], outs[0]["w"])
+    dev = torch.device("cuda", 0)
+    Xs, ys = zip(*[separable(N_GLOBAL, seed=700 + r, device=dev) for r in range(2)])
+    X, y = torch.cat(Xs), torch.cat(ys)
+    pipe = DevicePipeline(TrainConfig(smote_scope="global", tol=1e-8, max_iter=40, init_std=0.0, virtual_smote=False))
+    ref = pipe.fit(X, y)
+    assert pipe._virtual is None
+    assert sum(int(o["n_train"]) for o in outs) == ref.n_train_rows
+    assert sum(int(o["n_syn"]) for o in outs) == ref.n_synthetic
+    np.testing.assert_allclose(outs[0]["w"], ref.w, atol=2e-6, rtol=0)
+
+
+def test_dp_sgd_two_ranks_on_one_gpu(tmp_path):
+    """The lean data-parallel SGD step on the device (pass -> int64 fixed-point sums -> one
+    all-reduce -> update): both ranks end with one bitwise-identical model whose training state
+    converged, close to the single-process SGD fit on the concatenated shards."""
+    from fraud_detection_amd.data.synthetic import separable
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+    port = _port()
+    mp.start_processes(_worker_global, args=(2, port, str(tmp_path), "sgd", True), nprocs=2, start_method="spawn")
+    outs = [dict(np.load(tmp_path / f"g{r}.npz")) for r in range(2)]
+    assert all(bool(o["virtual"]) for o in outs)
+    assert np.array_equal(outs[0]["w"], outs[1]["w"]) and np.array_equal(outs[0]["w2"], outs[0]["w"])
+    dev = torch.device("cuda", 0)
+    Xs, ys = zip(*[separable(N_GLOBAL, seed=700 + r, device=dev) for r in range(2)])
+    X, y = torch.cat(Xs), torch.cat(ys)
+    ref = DevicePipeline(TrainConfig(smote_scope="global", solver="sgd", init_std=0.0)).fit(X, y)
+    # different minibatch partitions (each rank strides over its own shard): same optimum, not bitwise
+    np.testing.assert_allclose(outs[0]["w"], ref.w, atol=2e-2, rtol=0)
