@@ -46,7 +46,8 @@ def test_device_cv_job(dev, solver, storage):
                          fp8_scale=4.0, progressive=[], w0_from=cv._ws[1].state).as_fit_info()
         assert g.n_iter == f.n_iter
     else:
-        g = L.sgd_fit(part, w0=w0, affine=cv.stats.aff, virtual=v).as_fit_info()
+        g = L.sgd_fit(part, w0=w0, affine=cv.stats.aff, virtual=v,
+                          extra_epochs=L.SGD_EXTRA_EPOCHS).as_fit_info()
     assert np.array_equal(g.w, f.w)
     # the fold AUC is the exact AUC of the fold model on the fold's raw validation rows
     mean, _, scale = cv.stats.numpy()
