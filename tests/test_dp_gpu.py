@@ -144,6 +144,11 @@ def test_dp_sgd_two_ranks_on_one_gpu(tmp_path):
     dev = torch.device("cuda", 0)
     Xs, ys = zip(*[separable(N_GLOBAL, seed=700 + r, device=dev) for r in range(2)])
     X, y = torch.cat(Xs), torch.cat(ys)
-    ref = DevicePipeline(TrainConfig(smote_scope="global", solver="sgd", init_std=0.0)).fit(X, y)
-    # different minibatch partitions (each rank strides over its own shard): same optimum, not bitwise
-    np.testing.assert_allclose(outs[0]["w"], ref.w, atol=2e-2, rtol=0)
+    pipe = DevicePipeline(TrainConfig(smote_scope="global", solver="sgd", init_std=0.0))
+    ref = pipe.fit(X, y)
+    # different minibatch partitions (each rank strides over its own shard): not bitwise the same
+    # iterates, but the same training problem -- the DP model's exact objective on the single
+    # process's post-SMOTE set is within 1e-3 relative of the single-process model's
+    o_ref = pipe.training_objective(ref)["objective"]
+    o_dp = pipe.training_objective(ref, w=outs[0]["w"])["objective"]
+    assert abs(o_dp - o_ref) / o_ref < 1e-3, (o_dp, o_ref, float(outs[0]["gmax"]), ref.fit.grad_max)
