@@ -344,7 +344,9 @@ __device__ __forceinline__ void bf16_load_tile(const void* __restrict__ Xv, int6
 // persistent launch with another block shape walks exactly the rows of the per-pass launches.
 // pre (nullable): the wave's first tile, already loaded (a persistent launch prefetches it across
 // the grid barrier that precedes the pass).
-template <bool HESS, bool VIRT, bool FISH, int kPickLams = (HESS ? 8 : 32), int kPreLams = 32>
+// kDepth: stored tiles in flight (1: the next tile loads while this one computes; 2: the two next
+// -- the persistent SGD launch runs 2 waves per SIMD, too few to cover HBM latency one tile ahead).
+template <bool HESS, bool VIRT, bool FISH, int kPickLams = (HESS ? 8 : 32), int kPreLams = 32, int kDepth = 1>
 __device__ __forceinline__ void bf16_wave_pass(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float (&wl)[8], float cw0, float cw1,
     int hess_stride, int row_sub, int row_phase, const SmoteView& sv, const RowHole& hole, int64_t wave,
@@ -409,13 +411,17 @@ __device__ __forceinline__ void bf16_wave_pass(
     }
   };
   int64_t base = ((int64_t)row_phase * Gw + wave) * 64;
-  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes.
-  uint4 cur[4];
+  // Register double buffer: the next tile's 4 row loads are in flight while this tile computes
+  // (kDepth 2: a third buffer, the tile after it too).
+  uint4 cur[4], nx2[4];
   if (use_pre) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) cur[u] = pre[u];
   } else if (base < n) {
     bf16_load_tile(Xv, row_begin, n, hole, base, cur);
+  }
+  if constexpr (kDepth >= 2) {
+    if (base + step < n) bf16_load_tile(Xv, row_begin, n, hole, base + step, nx2);
   }
   if constexpr (VIRT && FISH) {  // SGD passes: the wave's first pick tile ahead of its stored rows
     if (ptile < ntile) {
@@ -433,7 +439,7 @@ __device__ __forceinline__ void bf16_wave_pass(
   int64_t pit = 0;
   for (; base < n; base += step) {
     uint4 nxt[4];
-    if (base + step < n) bf16_load_tile(Xv, row_begin, n, hole, base + step, nxt);
+    if (base + kDepth * step < n) bf16_load_tile(Xv, row_begin, n, hole, base + kDepth * step, nxt);
     const bool do_h = HESS && hphase == 0;
     hphase = hphase + 1 == hess_stride ? 0 : hphase + 1;
     float xs[4][8];
@@ -497,7 +503,14 @@ __device__ __forceinline__ void bf16_wave_pass(
     if (do_h) whacc += swq;
     if (FISH) dacc += dq;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
+    for (int u = 0; u < 4; ++u) {
+      if constexpr (kDepth >= 2) {
+        cur[u] = nx2[u];
+        nx2[u] = nxt[u];
+      } else {
+        cur[u] = nxt[u];
+      }
+    }
     if constexpr (VIRT && !FISH) {
       if (ptile < ntile && ++pit == ptrig) {
         pick_tile(ptile, false);
@@ -1451,11 +1464,12 @@ constexpr int kPersistWaves = 8;
 constexpr int kPersistThreads = kPersistWaves * kWave;
 constexpr int kBarShards = 8, kBarStride = 32;  // arrival shards, one 128-B line each (u32 words)
 enum : int { kSgdFault = 229 };                 // state slot: a grid barrier timed out
-// Variants (template LAMS, PF; FDX_SGD_PERSIST_CFG="lams,pf" picks one at run time, for the lab):
-// LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the same bits);
-// PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick tile's
-// inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the stored
-// tile; 3 the pick inputs only.
+// Template knobs: LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the
+// same bits); PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick
+// tile's inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the
+// stored tile; 3 the pick inputs only; DEPTH = stored bf16 tiles in flight per wave (bf16_wave_pass
+// kDepth).  LAMS 16/32 x PF 0-3 all ran within 735-778 us per fit (profiles/r5_e/sgd_lab.json);
+// FDX_SGD_PERSIST_CFG=1 (lab) selects DEPTH 1, the round-4 stored-tile pipeline.
 
 // Wave 0 of a block: arrive at the grid barrier and wait until `target` arrivals in all.
 __device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned target, int lane) {
@@ -1476,7 +1490,7 @@ __device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned targ
   }
 }
 
-template <bool FP8, bool VIRT, int kPersistLams = 16, int kPersistPrefetch = 2>
+template <bool FP8, bool VIRT, int kPersistLams = 16, int kPersistPrefetch = 2, int kPersistDepth = 2>
 __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const void* __restrict__ X,
                                                                          int64_t row_end, float x_scale,
                                                                          const float* __restrict__ class_w,
@@ -1610,7 +1624,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
         g[j] = 0.0f;
       }
       if (active)
-        bf16_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(X, 0, row_end, wl, cw0, cw1, 1, rsub, b, sv, hole, wave, P.Gw, nullptr, g,
+        bf16_wave_pass<false, VIRT, true, kPersistLams, kPreLams, kPersistDepth>(X, 0, row_end, wl, cw0, cw1, 1, rsub, b, sv, hole, wave, P.Gw, nullptr, g,
                                           lacc, wacc, whacc, dacc, hacc, pre, have_pre, ppre, have_ppre);
 #pragma unroll
       for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
@@ -1980,33 +1994,22 @@ void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, 
   if (hipMemsetAsync(a.ws, 0, sizeof(unsigned long long) * kSgdPersistWords, stream) != hipSuccess)
     throw std::runtime_error("sgd_persist: memset failed");
   const bool virt = v.parents != nullptr;
-  static const int cfg = [] {  // lab switch: "lams,pf"
+  static const int depth = [] {  // lab switch: FDX_SGD_PERSIST_CFG=1 -> one stored tile in flight
     const char* e = std::getenv("FDX_SGD_PERSIST_CFG");
-    int l = 16, p = 2;
-    if (e != nullptr) std::sscanf(e, "%d,%d", &l, &p);
-    return (l >= 32 ? 100 : 0) + p;
+    return (e != nullptr && e[0] == '1') ? 1 : 2;
   }();
-#define FDX_SGDP(F, V, L, PF) \
-  sgd_persist_kernel<F, V, L, PF><<<blocks, kPersistThreads, 0, stream>>>(X, row_end, x_scale, class_w, v, hole, a)
-#define FDX_SGDP_CFG(F)                              \
-  switch (cfg) {                                     \
-    case 0: FDX_SGDP(F, true, 16, 0); break;         \
-    case 1: FDX_SGDP(F, true, 16, 1); break;         \
-    case 3: FDX_SGDP(F, true, 16, 3); break;         \
-    case 100: FDX_SGDP(F, true, 32, 0); break;       \
-    case 101: FDX_SGDP(F, true, 32, 1); break;       \
-    case 102: FDX_SGDP(F, true, 32, 2); break;       \
-    case 103: FDX_SGDP(F, true, 32, 3); break;       \
-    default: FDX_SGDP(F, true, 16, 2); break;        \
-  }
-  if (fp8) {
-    if (virt) { FDX_SGDP_CFG(true) }
-    else FDX_SGDP(true, false, 16, 2);
+#define FDX_SGDP(F, V, D) \
+  sgd_persist_kernel<F, V, 16, 2, D><<<blocks, kPersistThreads, 0, stream>>>(X, row_end, x_scale, class_w, v, hole, a)
+  if (fp8) {  // fp8 tiles are half the bytes: its pass keeps two tiles in flight in the same registers
+    if (virt) FDX_SGDP(true, true, 2);
+    else FDX_SGDP(true, false, 2);
+  } else if (depth == 1) {
+    if (virt) FDX_SGDP(false, true, 1);
+    else FDX_SGDP(false, false, 1);
   } else {
-    if (virt) { FDX_SGDP_CFG(false) }
-    else FDX_SGDP(false, false, 16, 2);
+    if (virt) FDX_SGDP(false, true, 2);
+    else FDX_SGDP(false, false, 2);
   }
-#undef FDX_SGDP_CFG
 #undef FDX_SGDP
   check_launch("sgd_persist");
 }

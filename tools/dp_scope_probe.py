@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--scopes", default="shard,global")
     ap.add_argument("--solver", default="newton")
     ap.add_argument("--storage", default="bf16")
-    ap.add_argument("--virtual", type=int, default=1, help="0: stored SMOTE rows (smote_generate + streamed)")
+    ap.add_argument("--smote-virtual", type=int, default=1, help="0: stored SMOTE rows (smote_generate + streamed)")
     ap.add_argument("--phases", type=int, default=0, help="1: per-phase synced times of every synced fit")
     a = ap.parse_args()
     from fraud_detection_amd.data.synthetic import separable
@@ -46,7 +46,7 @@ def main():
     X, y = separable(n_train, seed=1000 + comm.rank, device=dev)
     for scope in a.scopes.split(","):
         pipe = DevicePipeline(TrainConfig(seed=42, solver=a.solver, smote_scope=scope, storage=a.storage,
-                                       virtual_smote=bool(a.virtual)), comm)
+                                       virtual_smote=bool(a.smote_virtual)), comm)
         for _ in range(2):
             pipe.fit(X, y)
         comm.barrier()

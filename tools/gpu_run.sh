@@ -157,7 +157,7 @@ for st in "$@"; do
       for ST in bf16 fp8; do
         step "dpstored_$ST" 300 env FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 \
           --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29521 tools/dp_scope_probe.py --rows 2000000 \
-          --scopes global,shard --storage $ST --virtual 0 --phases 1 --fits 6 || exit 1
+          --scopes global,shard --storage $ST --smote-virtual 0 --phases 1 --fits 6 || exit 1
       done ;;
     py:*) # shellcheck disable=SC2086
       s=${st#py:}; step "py_$(basename "$s" .py)" 600 python -u "$s" $FDX_PY_ARGS ;;
