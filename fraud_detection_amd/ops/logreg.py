@@ -441,11 +441,22 @@ def _default_w0(w0):
     return w
 
 
+FLAG_WAITS: list = []  # host seconds spent in each _await_flag (diagnostics: tools/dp_scope_probe.py)
+
+
 def _await_flag(flag: torch.Tensor, seq: int, stream: int, spin_s: float = 0.05):
     """Poll a mapped pinned flag word until the Newton update tagged ``seq`` has written it.
     After ``spin_s`` the host stops spinning and synchronises the stream instead (a stalled or
     faulted device then surfaces as the stream's error rather than a hang)."""
     t0 = time.perf_counter()
+    try:
+        _spin_flag(flag, seq, stream, spin_s, t0)
+    finally:
+        if len(FLAG_WAITS) < 4096:
+            FLAG_WAITS.append(time.perf_counter() - t0)
+
+
+def _spin_flag(flag: torch.Tensor, seq: int, stream: int, spin_s: float, t0: float):
     while (int(flag[0]) >> 1) != seq:
         if time.perf_counter() - t0 > spin_s:
             native().stream_sync(stream)
@@ -676,6 +687,12 @@ SGD_SUB = (4, 1, 1)
 # noise per feature, which slows the last digits of the epoch gradient (round 4: 1.4e-3 after 3
 # epochs, profiles/r4_c); bf16 rows converge in the nominal 3 and never run it.
 SGD_EXTRA_EPOCHS = 1
+# First Polyak-averaged epoch (every later epoch is averaged too, each returning its own average
+# started from the previous one): epoch 1, the first full epoch after the sub-sampled one.  fp64
+# simulation (tools/sgd_schedule_lab.py): at 16M post-SMOTE rows the epoch gradient ends at 4.8e-4
+# and the objective 9e-5 above Newton's; at 8M rows 9.0e-4 / 5.3e-4 -- where averaging only the
+# last epoch ends at 1.5e-3 / 1.2e-3, short of tol even after an extra epoch (2.0e-3).
+SGD_AVG_FROM = 1
 SGD_MOMENTUM = 0.55
 SGD_TOL = 1e-3                # on the epoch gradient max-norm (sklearn SGDClassifier's default tol)
 SGD_SLOTS = 36
@@ -720,7 +737,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             checkpoint_every: int = 0, affine: torch.Tensor | None = None, virtual: VirtualSmote | None = None,
             batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None,
             persistent: bool | None = None, serpentine: bool = False, subsample=SGD_SUB,
-            extra_epochs: int = 0, _stamps: torch.Tensor | None = None):
+            extra_epochs: int = 0, avg_from: int | None = None, _stamps: torch.Tensor | None = None):
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
@@ -752,7 +769,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     (SGD_SUB; an epoch with factor s visits 1/s of the rows in its nb minibatches).
     ``extra_epochs``: epochs after ``epochs`` that run only if the fit has not converged yet
     (the pipelines pass SGD_EXTRA_EPOCHS); with ``average`` each of them returns its own Polyak average, like the
-    last nominal epoch."""
+    last nominal epoch.  ``avg_from``: first averaged epoch (None: the last nominal one; the
+    pipelines pass SGD_AVG_FROM)."""
     check_rows(rows)
     w0 = _default_w0(w0)
     rows, hole = _apply_hole(rows, hole)
@@ -767,7 +785,9 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         nb = int(comm.all_reduce_scalar(nb, op="max"))
     nominal = max(int(epochs), 1)
     epochs = nominal + max(0, int(extra_epochs))  # the schedule's length from here on
-    avg_from = nominal - 1 if average else epochs  # averaged epochs: the last nominal one and the extras
+    # averaged epochs: avg_from (default the last nominal one) .. the extras
+    avg_from = min(nominal - 1, max(0, int(avg_from))) if (average and avg_from is not None) else \
+        (nominal - 1 if average else epochs)
     lrs = [_epoch_lr(lr, e) for e in range(epochs)]
     subs = [int(_epoch_lr(subsample, e)) if subsample is not None else 1 for e in range(epochs)]
     if any(x < 1 for x in subs):

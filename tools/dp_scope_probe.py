@@ -62,6 +62,9 @@ def main():
         prof.disable()
         coll = comm.collective_summary()
         synced, phased = [], []
+        comm.stats.reset()
+        from fraud_detection_amd.ops import logreg as L
+        L.FLAG_WAITS.clear()
         for _ in range(a.fits):
             comm.barrier()
             torch.cuda.synchronize(dev)
@@ -72,6 +75,8 @@ def main():
             synced.append(round((time.perf_counter() - t1) * 1e3, 3))
             if a.phases:
                 phased.append({k: round(v * 1e3, 3) for k, v in r.timings.items()})
+        coll_synced = comm.collective_summary()
+        flag_waits = sorted(L.FLAG_WAITS, reverse=True)[:5]
         p = pipe.fit(X, y, profile=True)
         s = io.StringIO()
         pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
@@ -79,7 +84,8 @@ def main():
                "ms_synced": synced, "phase_ms": {k: round(v * 1e3, 3) for k, v in p.timings.items()},
                "n_train_rows": int(r.n_train_rows), "n_synthetic": int(r.n_synthetic),
                "newton_iters": int(r.fit.n_iter), "virtual_smote": pipe._virtual is not None,
-               "collectives": coll, "storage": a.storage, "solver": a.solver}
+               "collectives": coll, "storage": a.storage, "solver": a.solver,
+               "collectives_synced_fits": coll_synced, "longest_flag_waits_ms": [round(x * 1e3, 3) for x in flag_waits]}
         if phased:
             out["phases_synced"] = phased
         print(json.dumps(out), flush=True)  # every rank: the two ranks share one GPU

@@ -117,12 +117,16 @@ def newton(chunks, C=1.0, iters=12):
     return w
 
 
-def run_schedule(chunks, nb, epochs, mom=0.55, C=1.0):
-    """epochs: list of (c, s)."""
+def run_schedule(chunks, nb, epochs, mom=0.55, C=1.0, avg_from=None, tol=1e-3):
+    """epochs: list of (c, s).  avg_from: epochs >= avg_from are Polyak-averaged (each returns its
+    own average) and the fit stops at the first converged epoch end (ops/logreg.sgd_fit with
+    extra_epochs); None: only the last epoch is averaged and every epoch runs."""
     st = ref.SgdStateRef(np.zeros(32))
     streamed = 0.0
     for ei, (c, s) in enumerate(epochs):
-        last_epoch = ei == len(epochs) - 1
+        if avg_from is not None and st.done:
+            break
+        last_epoch = (ei == len(epochs) - 1) if avg_from is None else ei >= avg_from
         for b in range(nb):
             fine = [ch for ch in range(FINE) if ch % (nb * s) == b * s] if s > 1 else \
                    [ch for ch in range(FINE) if ch % nb == b]
@@ -137,7 +141,7 @@ def run_schedule(chunks, nb, epochs, mom=0.55, C=1.0):
             streamed += len(fine) / FINE
             red = np.concatenate([g, [loss, S, 0.0, dsum]])
             st.step(red[:32], red[32], red[33], red[35], 30, C, c, mom, nb * s, last_epoch, b == nb - 1,
-                    1e-3, True)
+                    -1.0 if s > 1 else (tol if avg_from is not None else 1e-3), True)
     w = st.w.copy()
     w[31] = 0.0
     return w, st.gmax, streamed
@@ -154,7 +158,26 @@ def main():
     wn = newton(chunks)
     on, gn = full_objective(chunks, wn)
     print(f"newton objective {on:.9f} grad {gn:.2e}", flush=True)
+    # (nb, epochs[, avg_from]): with avg_from the fit stops at its first converged epoch end
     scheds = {
+        "sub4_c_x1": (8, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 2),
+        "sub4_c_x1lo": (8, [(0.4, 4), (0.7, 1), (0.8, 1), (0.4, 1)], 2),
+        "sub4_lo3": (8, [(0.4, 4), (0.7, 1), (0.4, 1), (0.4, 1)], 2),
+        "sub4_lo3b": (8, [(0.4, 4), (0.8, 1), (0.5, 1), (0.3, 1)], 2),
+        "sub4_avg2": (8, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "full_lo3": (8, [(0.4, 1), (0.7, 1), (0.4, 1), (0.4, 1)], 2),
+        "sub4_avg1_b": (8, [(0.4, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub4_avg1_c": (8, [(0.5, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub4_avg1_d": (8, [(0.4, 4), (0.6, 1), (0.6, 1), (0.6, 1)], 1),
+        "sub4_avg1_e": (8, [(0.4, 4), (0.7, 1), (0.6, 1), (0.5, 1)], 1),
+        "sub4_avg1_f": (8, [(0.4, 4), (0.9, 1), (0.8, 1), (0.7, 1)], 1),
+        "sub4_avg1_m45": (8, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1, 0.45),
+        "sub4_avg1_m65": (8, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1, 0.65),
+        "sub4_avg1_m75": (8, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1, 0.75),
+        "sub4_avg1_g": (8, [(0.4, 4), (0.7, 1), (0.9, 1), (0.9, 1)], 1),
+        "sub4_avg1_h": (8, [(0.3, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub2_avg1": (8, [(0.4, 2), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "nb6_avg1": (6, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_8x3": (8, [(0.4, 8), (0.6, 1), (0.8, 1)]),
         "sub4_8x3_b": (8, [(0.5, 4), (0.6, 1), (0.8, 1)]),
         "sub4_8x3_c": (8, [(0.4, 4), (0.7, 1), (0.8, 1)]),
@@ -170,13 +193,16 @@ def main():
     }
     out = {"newton_objective": on}
     only = os.environ.get("LAB_ONLY", "")
-    for name, (nb, ep) in scheds.items():
+    for name, spec in scheds.items():
+        nb, ep = spec[0], spec[1]
+        avg_from = spec[2] if len(spec) > 2 else None
+        mom = spec[3] if len(spec) > 3 else 0.55
         if only and name not in only.split(","):
             continue
         if FINE % (nb * max(s for _, s in ep)) and nb * max(s for _, s in ep) > FINE:
             continue
         t1 = time.time()
-        w, gmax, streamed = run_schedule(chunks, nb, ep)
+        w, gmax, streamed = run_schedule(chunks, nb, ep, mom=mom, avg_from=avg_from)
         o, gfull = full_objective(chunks, w)
         gap = (o - on) / on
         out[name] = {"nb": nb, "epochs": ep, "steps": nb * len(ep), "epoch_gmax": gmax, "full_grad": gfull,
