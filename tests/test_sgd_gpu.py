@@ -111,9 +111,9 @@ def test_sgd_reaches_newton_optimum_at_scale(dev, storage):
     assert -1e-5 < gap < 1e-3, (os_, on)
     assert abs(auc_s - auc_n) <= 1e-4, (auc_s, auc_n)
     f = rs.fit
-    assert f.n_iter == L.SGD_EPOCHS * L.SGD_BATCHES
-    if storage == "bf16":  # fp8 rows: the epoch gradient ends at 1.4e-3 (profiles/r4_c), gap 5.7e-4
-        assert f.converged and f.grad_max <= L.SGD_TOL, (f.grad_max, gap)
+    # the nominal epochs, plus the extra epoch(s) only if the nominal ones did not converge
+    assert f.n_iter in [L.SGD_BATCHES * (L.SGD_EPOCHS + e) for e in range(L.SGD_EXTRA_EPOCHS + 1)], f.n_iter
+    assert f.converged and f.grad_max <= L.SGD_TOL, (f.grad_max, gap, f.n_iter)
     assert f.converged == (f.grad_max <= L.SGD_TOL)
     assert abs(f.objective - os_["objective"]) < 0.05 * os_["objective"]
 
