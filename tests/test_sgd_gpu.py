@@ -92,10 +92,13 @@ def test_sgd_bitwise_deterministic(dev):
 
 @pytest.mark.parametrize("storage", ["bf16", "fp8"])
 def test_sgd_reaches_newton_optimum_at_scale(dev, storage):
-    """5M raw rows (4M train -> 8M post-SMOTE rows, virtual samples): the SGD model's exact
-    training objective is within 1e-3 relative of the Newton optimum's on the same training set,
-    its test AUC within 1e-4, and its device convergence state is set."""
-    X, y = separable(4_000_000, seed=1000, device=dev)
+    """The bench shape (8M training rows -> 16M post-SMOTE rows, virtual samples): the SGD model's
+    exact training objective is within 1e-3 relative of the Newton optimum's on the same training
+    set, its test AUC within 1e-4, and its device convergence state is set (epoch gradient <= tol).
+    At half this size (8M post-SMOTE rows, 1M-row minibatches) the epoch gradient sits at its
+    noise floor, 1.5-1.8e-3 after 4 epochs with the objective gap still < 1e-3 (profiles/README.md
+    round 5, tools/sgd_schedule_lab.py)."""
+    X, y = separable(8_000_000, seed=1000, device=dev)
     Xt, yt = separable(1_000_000, seed=5000, device=dev)
     pn = DevicePipeline(TrainConfig(solver="newton", storage=storage, seed=42, deferred_check=False))
     rn = pn.fit(X, y)
