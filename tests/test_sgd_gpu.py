@@ -175,7 +175,7 @@ def test_resume_after_convergence_keeps_the_fit(dev, tmp_path):
     from fraud_detection_amd.utils.checkpoint import CheckpointManager
 
     rows, v = _case(800_000, 300, 300, 5, 600_000, 9, dev, pos=0.03)
-    kw = dict(virtual=v, batches=4, epochs=4, tol=1.0)  # loose tol: converged at the first epoch end
+    kw = dict(virtual=v, batches=4, epochs=4, tol=1.0, subsample=None)  # converged at the first epoch end
     full = L.sgd_fit(rows, **kw).as_fit_info()
     assert full.converged and full.n_iter == 4
     mgr = CheckpointManager(str(tmp_path / "c"), keep=3)
