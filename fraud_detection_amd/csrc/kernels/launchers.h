@@ -227,8 +227,9 @@ struct SgdPersistArgs {
   int d = 30, fit_intercept = 1, nb = 1, epochs = 1, avg_from = 0, serpentine = 0;
   int s0 = 0, s1 = 0;
   int64_t Gw = 0;  // waves of the per-step pass grid (4 x its blocks): sets the minibatch partition
-  unsigned long long* stamps = nullptr;  // nullable: [steps][3][blocks] wall_clock64 at pass end,
-                                         // barrier exit and update end (tools/sgd_stamps.py)
+  unsigned long long* stamps = nullptr;  // nullable: [steps][3 + 8][blocks] wall_clock64 at pass end,
+                                         // barrier exit, update end, then each wave's pass end
+                                         // (tools/sgd_stamps.py)
 };
 void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
                         const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream);

@@ -1464,6 +1464,9 @@ constexpr int kPersistWaves = 8;
 constexpr int kPersistThreads = kPersistWaves * kWave;
 constexpr int kBarShards = 8, kBarStride = 32;  // arrival shards, one 128-B line each (u32 words)
 enum : int { kSgdFault = 229 };                 // state slot: a grid barrier timed out
+// stamps (tools/sgd_stamps.py): [step][kStampRows][block] wall_clock64 -- pass end, barrier exit,
+// update end, then every wave's own pass end
+constexpr int kStampRows = 3 + kPersistWaves;
 // Template knobs: LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the
 // same bits); PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick
 // tile's inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the
@@ -1636,6 +1639,8 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     lacc = wave_sum(lacc);
     wacc = wave_sum(wacc);
     dacc = wave_sum(dacc);
+    if (P.stamps != nullptr && lane == 0)
+      P.stamps[((int64_t)(st - P.s0) * kStampRows + 3 + wv) * gridDim.x + blockIdx.x] = wall_clock64();
     if (lane == 0) {
       red[wv][32] = lacc;
       red[wv][33] = wacc;
@@ -1654,11 +1659,11 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       arrivals += gridDim.x;
       if (P.stamps != nullptr && lane == 0)
-        P.stamps[((int64_t)(st - P.s0) * 3 + 0) * gridDim.x + blockIdx.x] = wall_clock64();
+        P.stamps[((int64_t)(st - P.s0) * kStampRows + 0) * gridDim.x + blockIdx.x] = wall_clock64();
       const bool ok = persist_barrier(bar, arrivals, lane);
       if (!ok && lane == 0) s_ok = 0;
       if (P.stamps != nullptr && lane == 0)
-        P.stamps[((int64_t)(st - P.s0) * 3 + 1) * gridDim.x + blockIdx.x] = wall_clock64();
+        P.stamps[((int64_t)(st - P.s0) * kStampRows + 1) * gridDim.x + blockIdx.x] = wall_clock64();
     }
     __syncthreads();
     if (!s_ok) break;  // uniform in the block
@@ -1688,7 +1693,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);
     __syncthreads();
     if (P.stamps != nullptr && t == 0)
-      P.stamps[((int64_t)(st - P.s0) * 3 + 2) * gridDim.x + blockIdx.x] = wall_clock64();
+      P.stamps[((int64_t)(st - P.s0) * kStampRows + 2) * gridDim.x + blockIdx.x] = wall_clock64();
   }
   if (blockIdx.x == 0) {  // every block holds the same state: block 0 publishes it
     if (t == 0 && !s_ok) sst[kSgdFault] = 1.0;

@@ -81,30 +81,41 @@ def main():
 
     steps = L.SGD_EPOCHS * L.SGD_BATCHES
     blocks = L.native().sgd_persist_blocks(ws.sgd_blocks)
-    stamps = torch.zeros(steps * 3 * blocks, dtype=torch.int64, device=dev)
+    nrow = 3 + 8  # logreg.hip kStampRows: pass end, barrier exit, update end, 8 waves' pass ends
+    stamps = torch.zeros(steps * nrow * blocks, dtype=torch.int64, device=dev)
     L.sgd_fit(rows, persistent=True, _stamps=stamps, **kw).as_fit_info()
     torch.cuda.synchronize()
-    t = stamps.cpu().numpy().astype(np.int64).reshape(steps, 3, blocks) * 10  # ns
+    t = stamps.cpu().numpy().astype(np.int64).reshape(steps, nrow, blocks) * 10  # ns
     t0 = t[0, 0].min()
     rows_out = []
     for k in range(steps):
         pe, be, ue = t[k, 0], t[k, 1], t[k, 2]
+        we = t[k, 3:]  # [8][blocks] each wave's pass end
         start = t[k - 1, 2] if k else None
         pas = (pe - start) if start is not None else None
+        wp = (we - start[None, :]) if start is not None else None
         rows_out.append({
             "step": k,
             "pass_us_med": float(np.median(pas)) / 1e3 if pas is not None else None,
             "pass_us_max": float(np.max(pas)) / 1e3 if pas is not None else None,
+            "wave_pass_us_p10": float(np.percentile(wp, 10)) / 1e3 if wp is not None else None,
+            "wave_pass_us_med": float(np.median(wp)) / 1e3 if wp is not None else None,
+            "wave_pass_us_p90": float(np.percentile(wp, 90)) / 1e3 if wp is not None else None,
+            "block_epilogue_us": float(np.median(pe - we.max(0))) / 1e3,
             "arrival_skew_us": float(pe.max() - np.median(pe)) / 1e3,
             "barrier_wake_us": float(np.median(be) - pe.max()) / 1e3,
             "update_us": float(np.median(ue - be)) / 1e3,
             "step_end_us": float(ue.max() - t0) / 1e3,
         })
-    print(f"{'step':>4} {'pass med':>9} {'pass max':>9} {'skew':>7} {'wake':>7} {'update':>7} {'end':>8}")
+    print(f"{'step':>4} {'wave p10':>9} {'wave med':>9} {'wave p90':>9} {'epilog':>7} {'pass med':>9} "
+          f"{'pass max':>9} {'skew':>7} {'wake':>7} {'update':>7} {'end':>8}")
+    nan = float("nan")
     for r in rows_out:
+        v = [r[k] if r[k] is not None else nan for k in ("wave_pass_us_p10", "wave_pass_us_med", "wave_pass_us_p90")]
         pm = r["pass_us_med"]
         px = r["pass_us_max"]
-        print(f"{r['step']:4d} {pm if pm is not None else float('nan'):9.1f} {px if px is not None else float('nan'):9.1f} "
+        print(f"{r['step']:4d} {v[0]:9.1f} {v[1]:9.1f} {v[2]:9.1f} {r['block_epilogue_us']:7.1f} "
+              f"{pm if pm is not None else nan:9.1f} {px if px is not None else nan:9.1f} "
               f"{r['arrival_skew_us']:7.1f} {r['barrier_wake_us']:7.1f} {r['update_us']:7.1f} {r['step_end_us']:8.1f}")
     out["steps"] = rows_out
     if a.json:
