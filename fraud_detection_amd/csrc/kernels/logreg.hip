@@ -1467,6 +1467,12 @@ enum : int { kSgdFault = 229 };                 // state slot: a grid barrier ti
 // stamps (tools/sgd_stamps.py): [step][kStampRows][block] wall_clock64 -- pass end, barrier exit,
 // update end, then every wave's own pass end
 constexpr int kStampRows = 3 + kPersistWaves;
+// The wave that reduces the block's sums, zeroes the next accumulator set (block 0) and arrives at
+// the barrier: the LAST wave of the block.  The pick tiles of a step sit on the low wave indices
+// (wave wv of block b is wave wv * B + b of the pass grid), i.e. on wave 0 of every block, whose
+// next-pick input chain (dependent loads) would otherwise delay the arrival (r5_h stamps: an
+// 8.4 us block epilogue after the last wave's pass).
+constexpr int kArriveWave = kPersistWaves - 1;
 // Template knobs: LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the
 // same bits); PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick
 // tile's inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the
@@ -1585,7 +1591,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     if constexpr (kPersistPrefetch == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(touch) : : "memory");
     const int ep = st / P.nb, pos = st % P.nb, b = phase_of(st), rsub = rowsub_of(st);
     unsigned long long* acc = accs + (st % 3) * kSgdAccWords;
-    if (blockIdx.x == 0 && wv == 0) {  // set st + 1 (read as set st - 2 before barrier st - 1)
+    if (blockIdx.x == 0 && wv == kArriveWave) {  // set st + 1 (read as set st - 2 before barrier st - 1)
       unsigned long long* nx = accs + ((st + 1) % 3) * kSgdAccWords;
       for (int e = lane; e < kSgdAccWords; e += kWave)
         __hip_atomic_store(nx + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1648,12 +1654,12 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       red[wv][35] = dacc;
     }
     __syncthreads();
-    if (wv != 0) {
-      prefetch(st + 1);
+    if (wv != kArriveWave) {
+      prefetch(st + 1);  // wave 0 (the pick tiles' wave) runs its pick-input chain during the barrier
     } else {
       // sgd_fused_tail's per-wave fixed point (inactive waves hold zeros)
       const long long qs = lane < kSgdSlots ? wave_sums_fixed<kPersistWaves>(red, P.aff, lane) : 0;
-      prefetch(st + 1);  // in flight beside the adds: the arrival waits for both
+      prefetch(st + 1);  // no pick tile on this wave: an L2 touch, in flight beside the adds
       if (lane < kSgdSlots && lane != 34 && qs != 0)
         __hip_atomic_fetch_add(acc + (blockIdx.x % kSgdReplicas) * 36 + lane, (unsigned long long)qs,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
