@@ -1512,8 +1512,11 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   __shared__ unsigned long long rep[kSgdAccWords];
   __shared__ double rd[kSgdSlots];
   __shared__ int s_done, s_ok;
+  __shared__ double saff[64];  // the affine map, read from LDS by every step's reduce and update
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   constexpr int d_feat = 30;
+  if (P.aff != nullptr && t < 64) saff[t] = P.aff[t];
+  const double* affl = P.aff != nullptr ? saff : nullptr;
   const float inv_s = FP8 ? 1.0f / x_scale : 1.0f;
   unsigned int* bar = reinterpret_cast<unsigned int*>(P.ws);
   unsigned long long* accs = P.ws + 128;
@@ -1658,7 +1661,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       prefetch(st + 1);  // wave 0 (the pick tiles' wave) runs its pick-input chain during the barrier
     } else {
       // sgd_fused_tail's per-wave fixed point (inactive waves hold zeros)
-      const long long qs = lane < kSgdSlots ? wave_sums_fixed<kPersistWaves>(red, P.aff, lane) : 0;
+      const long long qs = lane < kSgdSlots ? wave_sums_fixed<kPersistWaves>(red, affl, lane) : 0;
       prefetch(st + 1);  // no pick tile on this wave: an L2 touch, in flight beside the adds
       if (lane < kSgdSlots && lane != 34 && qs != 0)
         __hip_atomic_fetch_add(acc + (blockIdx.x % kSgdReplicas) * 36 + lane, (unsigned long long)qs,
@@ -1694,7 +1697,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     a.avg = ep >= P.avg_from;
     a.epoch_end = pos == P.nb - 1;
     a.tol = P.sub[ep] > 1 ? -1.0 : P.tol;  // a sub-sampled epoch never decides convergence
-    sgd_apply(rd, sst, wnew, &s_done, P.aff, a, t, true);
+    sgd_apply(rd, sst, wnew, &s_done, affl, a, t, true);
     __syncthreads();
     if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);
     __syncthreads();
