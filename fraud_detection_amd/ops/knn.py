@@ -63,7 +63,7 @@ def _check_parents(parents: torch.Tensor | None, C: torch.Tensor, affine: torch.
 
 def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1, want_dist: bool = False,
              nsplit: int | None = None, engine: str | None = None, parents: torch.Tensor | None = None,
-             parents_affine: torch.Tensor | None = None):
+             parents_affine: torch.Tensor | None = None, _diag: dict | None = None):
     """k nearest candidates (squared L2 over the 30 feature columns) of each query row.
 
     Q [mq, 32] / C [mc, 32] fp32 padded rows (columns 30/31, intercept and label, are ignored).  If ``self_offset >= 0``, query row q is candidate
@@ -141,6 +141,11 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         counts = torch.empty(nb, device=Q.device, dtype=torch.int32)
         m.knn_topk3r(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                      int(k), ptr(idx), ptr(score), ptr(lists), ptr(counts), ns, s)
+        if _diag is not None:  # list lengths (diagnostics; synchronises)
+            c = counts.float()
+            _diag.update(nsplit=ns, list_cap=int(m.KNN3R_LIST_CAP), mean=float(c.mean()), max=int(c.max()),
+                         p99=float(torch.quantile(c[: min(c.numel(), 1 << 24)], 0.99)),
+                         over_cap=int((c > m.KNN3R_LIST_CAP).sum()))
     elif eng == "bf16x3":
         m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                     int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, s)

@@ -66,6 +66,11 @@ for st in "$@"; do
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
+    knnprof)  # kernel trace of the k-NN lab (engines/splits from FDX_KNN_ARGS)
+      cd /tmp && export TMPDIR=/tmp
+      # shellcheck disable=SC2086
+      step knnprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/knnprof" -o run -- python3 "$R/tools/knn_lab.py" --reps 5 $FDX_KNN_ARGS
+      cd "$R" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" $FDX_KNN_ARGS ;;  # shellcheck disable=SC2086
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;

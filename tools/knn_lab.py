@@ -67,6 +67,10 @@ def main():
                 f = lambda: K.knn_topk(Q, Cc, 5, off, engine=eng, nsplit=ns)  # noqa: E731
                 got = f()
                 ms = timed(f)
+                if eng == "bf16x3r":
+                    dg = {}
+                    K.knn_topk(Q, Cc, 5, off, engine=eng, nsplit=ns, _diag=dg)
+                    print(json.dumps({name: {"engine": eng, "nsplit": ns, "lists": dg}}), flush=True)
                 case = {"engine": eng, "nsplit": ns, "ms": round(ms, 4),
                         "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
                         "lists_equal": bool((got == ref).all().item())}

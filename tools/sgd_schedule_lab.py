@@ -178,6 +178,10 @@ def main():
         "sub4_avg1_h": (8, [(0.3, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub2_avg1": (8, [(0.4, 2), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "nb6_avg1": (6, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "nb4_avg1": (4, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "nb4_avg1_b": (4, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "nb6_avg1_b": (6, [(0.5, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "nb4_avg1_c": (4, [(0.5, 4), (0.8, 1), (0.9, 1), (0.9, 1)], 1),
         "sub8_8x3": (8, [(0.4, 8), (0.6, 1), (0.8, 1)]),
         "sub4_8x3_b": (8, [(0.5, 4), (0.6, 1), (0.8, 1)]),
         "sub4_8x3_c": (8, [(0.4, 4), (0.7, 1), (0.8, 1)]),
