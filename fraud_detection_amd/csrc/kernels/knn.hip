@@ -581,8 +581,10 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
 // a lane passes.  Here phase 1 (knn_collect_kernel) never touches fp32 candidate rows: per tile it
 // runs the 6 bf16 MFMAs of knn_topk3 and a max test, and a passing candidate only APPENDS its index
 // to a per-lane global list.  The running threshold is the k-th best LOWER bound approx - m of the
-// union of the query's two half-lists, where m = 2^-13 (||q|| tmax + 0.5 tmax^2) >= 8x the bf16x3
-// error bound (see knn_topk3); a candidate is appended when its UPPER bound approx + m reaches it.
+// union of the query's two half-lists, where m = 2^-14 (||q|| tmax + 0.5 tmax^2) >= 4x the bf16x3
+// error bound 2^-16 sum|q_f c_f| (see knn_topk3; fp32 accumulation of the 96 products and the
+// exact fmaf chain add < 0.6 x 2^-16 more); a candidate is appended when its UPPER bound approx + m
+// reaches it.
 // Since k distinct candidates have exact >= lower bound >= thr, the exact k-th best s_k >= thr
 // at every moment, so every candidate with exact >= s_k (upper bound >= s_k >= thr) is on a list.
 // Phase 2 (knn_rerank_kernel, 8 lanes per query) re-scores the listed candidates exactly (the
@@ -590,6 +592,8 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
 // the exact fp32 ranking.  A lane list that overflows kListCap sends its query to a brute-force
 // exact scan in phase 2 (correct, slow, and not seen at SMOTE shapes).
 constexpr int kListCap = 64;
+constexpr int kSeedTiles = 2;             // seed candidates per slice > 0: 64
+constexpr float kMarginScale = 0x1p-14f;  // m = 2^-14 (||q|| tmax + 0.5 tmax^2): >= 4x the error bound
 
 template <int K>
 __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
@@ -630,19 +634,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
   __shared__ int2 qent[kCap * kWave];  // (lower-bound bits, candidate index) at [slot * 64 + lane]
   int qc = 0, cnt = 0;
   const int64_t lbase = (int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * kListCap * kWave + lane;
-  auto flush = [&]() {
-    for (int e = 0; __any(e < qc); ++e) {
-      if (e < qc) {
-        const int2 v = qent[e * kWave + lane];
-        const int ci = v.y;
-        if (ci != self_c && ci < mc) {
-          if (cnt < kListCap) lists[lbase + (int64_t)cnt * kWave] = ci;
-          ++cnt;
-          topk_insert<K>(bs, bi, __int_as_float(v.x), ci);
-        }
-      }
-    }
-    qc = 0;
+  auto union_thr = [&]() {  // k-th best lower bound of the union of this lane's and its partner's lists
     float ps[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
@@ -660,23 +652,32 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     }
     thr = kth;
   };
+  auto flush = [&]() {
+    for (int e = 0; __any(e < qc); ++e) {
+      if (e < qc) {
+        const int2 v = qent[e * kWave + lane];
+        const int ci = v.y;
+        if (ci != self_c && ci < mc) {
+          if (cnt < kListCap) lists[lbase + (int64_t)cnt * kWave] = ci;
+          ++cnt;
+          topk_insert<K>(bs, bi, __int_as_float(v.x), ci);
+        }
+      }
+    }
+    qc = 0;
+    union_thr();
+  };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
   const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
-  uint4 cv[4];
-  float tmn = 0.0f;
-  auto fetch = [&](int t, uint4 (&a)[4]) {
+  auto fetch = [&](int t, uint4 (&a)[4], float& tmv) {
     const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
     a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
-    tmn = tmax[t];
+    tmv = tmax[t];
   };
-  if (t_lo < t_hi) fetch(t_lo, cv);
-  for (int t = t_lo; t < t_hi; ++t) {
-    const int c0 = t * 32;
-    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, cv[0]), ch1 = __builtin_bit_cast(bf16x8_t, cv[1]);
-    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, cv[2]), cl1 = __builtin_bit_cast(bf16x8_t, cv[3]);
-    const float tm = tmn;
-    if (t + 1 < t_hi) fetch(t + 1, cv);
+  auto approx = [&](const uint4 (&c)[4]) -> f32x16_t {
+    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, c[0]), ch1 = __builtin_bit_cast(bf16x8_t, c[1]);
+    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, c[2]), cl1 = __builtin_bit_cast(bf16x8_t, c[3]);
     f32x16_t acc = {};
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh0, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh1, acc, 0, 0, 0);
@@ -684,7 +685,45 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql1, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh0, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
-    const float mg = 0x1p-13f * fmaf(qn, tm, 0.5f * tm * tm);
+    return acc;
+  };
+  // Seed (slices > 0): the lower bounds of the first kSeedTiles tiles of the candidate set -- slice
+  // 0's, so distinct from this slice's candidates -- fill the top-k before the slice starts.  They
+  // are never appended (slice 0 lists them), but the threshold they give is valid (k distinct
+  // candidates with exact >= lower bound >= thr) and spares every slice its fill phase: with
+  // thr = -inf the first tile appends all 16 candidates of every lane (r5_j: 62 list entries per
+  // query and slice at 13.6k x 13.6k, 4 slices, a 124 us re-rank).
+  if (blockIdx.y > 0) {
+    const int ns0 = (int)((int64_t)all_tiles / gridDim.y);  // slice 0's tile count
+    const int nseed = ns0 < kSeedTiles ? ns0 : kSeedTiles;
+    for (int t = 0; t < nseed; ++t) {
+      uint4 c[4];
+      float tm;
+      fetch(t, c, tm);
+      const f32x16_t acc = approx(c);
+      const float mg = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = t * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+        if (ci != self_c && ci < mc) topk_insert<K>(bs, bi, acc[r] - mg, ci);
+      }
+    }
+    union_thr();
+  }
+  // two tiles in flight (a slice's wave is latency-bound on its loads at ~2 waves per SIMD)
+  uint4 cv[4], cv2[4];
+  float tmn = 0.0f, tmn2 = 0.0f;
+  if (t_lo < t_hi) fetch(t_lo, cv, tmn);
+  if (t_lo + 1 < t_hi) fetch(t_lo + 1, cv2, tmn2);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int c0 = t * 32;
+    const f32x16_t acc = approx(cv);
+    const float tm = tmn;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cv[u] = cv2[u];
+    tmn = tmn2;
+    if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
+    const float mg = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
     const float cut = thr - mg;  // upper bound approx + mg >= thr
     float mx = acc[0];
 #pragma unroll
