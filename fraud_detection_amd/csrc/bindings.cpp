@@ -745,10 +745,10 @@ PYBIND11_MODULE(_fdx_native, m) {
   m.def("knn3r_splits", [](int mq_pad, int mc_pad) { return fdx::knn3r_splits(mq_pad, mc_pad); });
   m.attr("KNN3R_LIST_CAP") = fdx::knn3r_list_cap();
   m.def("knn_topk3r", [](u Q, u Qhl, int mq_pad, int mq, u C, u Chl, u tmax, int mc_pad, int mc, int64_t self_off,
-                         int k, u oidx, u oscore, u lists, u counts, u thr_seed, int nsplit, u s) {
+                         int k, u oidx, u oscore, u lists, u counts, int nsplit, u s) {
     fdx::launch_knn_topk3r(P<const float>(Q), P<const void>(Qhl), mq_pad, mq, P<const float>(C), P<const void>(Chl),
                            P<const float>(tmax), mc_pad, mc, self_off, k, P<int>(oidx), P<float>(oscore),
-                           P<int>(lists), P<int>(counts), P<float>(thr_seed), nsplit, S(s));
+                           P<int>(lists), P<int>(counts), nsplit, S(s));
   });
   m.def("knn_topk", [](u Q, int mq_pad, int mq, u C, int mc_pad, int mc, int64_t self_off, int k, u oidx,
                        u oscore, u ws_score, u ws_idx, int nsplit, u s) {

@@ -592,15 +592,15 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
 // the exact fp32 ranking.  A lane list that overflows kListCap sends its query to a brute-force
 // exact scan in phase 2 (correct, slow, and not seen at SMOTE shapes).
 constexpr int kListCap = 64;
-constexpr int kSeedTiles = 32;            // seed pass: 1024 candidates per query
+constexpr int kSeedTiles = 2;             // seed candidates per slice > 0: 64
 constexpr float kMarginScale = 0x1p-14f;  // m = 2^-14 (||q|| tmax + 0.5 tmax^2): >= 4x the error bound
 
-template <int K, bool SEED>
+template <int K>
 __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
                                                             const uint4* __restrict__ Chl,
                                                             const float* __restrict__ tmax, int mc_pad, int mc,
                                                             int64_t self_offset, int* __restrict__ lists,
-                                                            int* __restrict__ counts, float* __restrict__ thr_seed) {
+                                                            int* __restrict__ counts) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
   const int qg = blockIdx.x * 32 + j;
@@ -629,10 +629,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  // the seed pass's threshold (a valid lower bound of the k-th best on its own, so the running
-  // threshold is the max of it and the slice's own k-th lower bound -- no list merging needed)
-  const float seed = (!SEED && thr_seed != nullptr) ? thr_seed[qg] : kNegBig;
-  float thr = seed;
+  float thr = kNegBig;
   constexpr int kCap = kQFlush - 1 + 16 + 1;
   __shared__ int2 qent[kCap * kWave];  // (lower-bound bits, candidate index) at [slot * 64 + lane]
   int qc = 0, cnt = 0;
@@ -653,7 +650,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = fmaxf(kth, seed);
+    thr = kth;
   };
   auto flush = [&]() {
     for (int e = 0; __any(e < qc); ++e) {
@@ -690,13 +687,15 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
     return acc;
   };
-  if constexpr (SEED) {
-    // Seed pass (grid: query blocks x 1): the lower bounds of the first kSeedTiles tiles give every
-    // query a threshold -- the k-th best lower bound of kSeedTiles x 32 candidates -- that each
-    // slice of the collect pass starts from.  A slice starting at -inf appended all 16 candidates
-    // of every lane on its first tile and then every record-breaker of its own candidates
-    // (r5_j: 62 list entries per query and slice at 13.6k x 13.6k, a 124 us re-rank).
-    const int nseed = all_tiles < kSeedTiles ? all_tiles : kSeedTiles;
+  // Seed (slices > 0): the lower bounds of the first kSeedTiles tiles of the candidate set -- slice
+  // 0's, so distinct from this slice's candidates -- fill the top-k before the slice starts.  They
+  // are never appended (slice 0 lists them), but the threshold they give is valid (k distinct
+  // candidates with exact >= lower bound >= thr) and spares every slice its fill phase: with
+  // thr = -inf the first tile appends all 16 candidates of every lane (r5_j: 62 list entries per
+  // query and slice at 13.6k x 13.6k, 4 slices, a 124 us re-rank).
+  if (blockIdx.y > 0) {
+    const int ns0 = (int)((int64_t)all_tiles / gridDim.y);  // slice 0's tile count
+    const int nseed = ns0 < kSeedTiles ? ns0 : kSeedTiles;
     for (int t = 0; t < nseed; ++t) {
       uint4 c[4];
       float tm;
@@ -710,17 +709,20 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
       }
     }
     union_thr();
-    if (h == 0) thr_seed[qg] = thr;
-    return;
   }
-  uint4 cv[4];
-  float tmn = 0.0f;
+  // two tiles in flight (a slice's wave is latency-bound on its loads at ~2 waves per SIMD)
+  uint4 cv[4], cv2[4];
+  float tmn = 0.0f, tmn2 = 0.0f;
   if (t_lo < t_hi) fetch(t_lo, cv, tmn);
+  if (t_lo + 1 < t_hi) fetch(t_lo + 1, cv2, tmn2);
   for (int t = t_lo; t < t_hi; ++t) {
     const int c0 = t * 32;
     const f32x16_t acc = approx(cv);
     const float tm = tmn;
-    if (t + 1 < t_hi) fetch(t + 1, cv, tmn);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cv[u] = cv2[u];
+    tmn = tmn2;
+    if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
     const float mg = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
     const float cut = thr - mg;  // upper bound approx + mg >= thr
     float mx = acc[0];
@@ -1052,7 +1054,7 @@ int knn3r_list_cap() { return kListCap; }
 int knn3r_splits(int mq_pad, int mc_pad) {
   // fewer slices than the one-wave engines: a slice restarts the lists (16 appends per lane on its
   // first tile) and each slice holds kListCap ints per query lane
-  static const int cap = resident_cap(knn_collect_kernel<5, false>, kWave);
+  static const int cap = resident_cap(knn_collect_kernel<5>, kWave);
   const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
   int max_s = tiles / 16;
   if (max_s > 16) max_s = 16;
@@ -1071,20 +1073,16 @@ int knn3r_splits(int mq_pad, int mc_pad) {
 
 void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                        const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                       float* out_score, int* lists, int* counts, float* thr_seed, int nsplit,
-                       hipStream_t stream) {
+                       float* out_score, int* lists, int* counts, int nsplit, hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk3r: pads must be x32");
-  if (mq > mq_pad || mc > mc_pad || nsplit < 1 || lists == nullptr || counts == nullptr || thr_seed == nullptr)
+  if (mq > mq_pad || mc > mc_pad || nsplit < 1 || lists == nullptr || counts == nullptr)
     throw std::runtime_error("knn_topk3r: bad shapes or missing list workspaces");
   const dim3 grid(mq_pad / 32, nsplit);
   const uint4* qh = reinterpret_cast<const uint4*>(Qhl);
   const uint4* chl = reinterpret_cast<const uint4*>(Chl);
   const unsigned rblocks = (unsigned)(((int64_t)mq * 8 + 255) / 256);
 #define FDX_KNN3R(KK)                                                                                       \
-  knn_collect_kernel<KK, true><<<dim3(mq_pad / 32, 1), kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, \
-                                                                          lists, counts, thr_seed);              \
-  knn_collect_kernel<KK, false><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, lists,    \
-                                                            counts, thr_seed);                                  \
+  knn_collect_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, lists, counts); \
   knn_rerank_kernel<KK><<<rblocks, 256, 0, stream>>>(Q, C, mq, mc, mq_pad / 32, nsplit, self_offset, lists, counts, \
                                                      out_idx, out_score)
   switch (k) {

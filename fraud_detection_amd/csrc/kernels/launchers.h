@@ -251,15 +251,13 @@ int knn3_splits(int mq_pad, int mc_pad);
 // LDS-tiled fp32 engine: workgroups of 4 waves x 32 queries share staged candidate chunks
 // (mq_pad multiple of 128)
 int knn_lds_splits(int mq_pad, int mc_pad);
-// bf16x3 seed + collect (per-lane candidate lists [nsplit][mq_pad / 32][cap][64] int32 + counts
-// [nsplit][mq_pad / 32][64], per-query seed thresholds thr_seed [mq_pad] fp32) then exact fp32
-// re-rank of the listed candidates (knn.hip)
+// bf16x3 collect (per-lane candidate lists [nsplit][mq_pad / 32][cap][64] int32 + counts
+// [nsplit][mq_pad / 32][64]) then exact fp32 re-rank of the listed candidates (knn.hip)
 int knn3r_list_cap();
 int knn3r_splits(int mq_pad, int mc_pad);
 void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                        const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                       float* out_score, int* lists, int* counts, float* thr_seed, int nsplit,
-                       hipStream_t stream);
+                       float* out_score, int* lists, int* counts, int nsplit, hipStream_t stream);
 void launch_knn_topk_lds(const float* Q, int mq_pad, int mq, const float* C, int mc_pad, int mc,
                          int64_t self_offset, int k, int* out_idx, float* out_score, float* ws_score, int* ws_idx,
                          int nsplit, hipStream_t stream);

@@ -139,9 +139,8 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         nb = ns * (mq_pad // 32) * 64
         lists = torch.empty(nb * m.KNN3R_LIST_CAP, device=Q.device, dtype=torch.int32)
         counts = torch.empty(nb, device=Q.device, dtype=torch.int32)
-        seeds = torch.empty(mq_pad, device=Q.device, dtype=torch.float32)
         m.knn_topk3r(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
-                     int(k), ptr(idx), ptr(score), ptr(lists), ptr(counts), ptr(seeds), ns, s)
+                     int(k), ptr(idx), ptr(score), ptr(lists), ptr(counts), ns, s)
         if _diag is not None:  # list lengths (diagnostics; synchronises)
             c = counts.float()
             _diag.update(nsplit=ns, list_cap=int(m.KNN3R_LIST_CAP), mean=float(c.mean()), max=int(c.max()),
