@@ -33,16 +33,18 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 #           per-lane lists under a provable lower-bound threshold, and a second kernel re-scores
 #           the listed candidates exactly (8 lanes per query) -- knn.hip knn_collect_kernel.
 # Measured on MI355X from 13.6k to 170k minority rows (profiles/r2_s3i/knn_engines.jsonl): fp32
-# is fastest at every size (46 -> 104 TFLOP/s-equivalent; fp32lds 0.66-0.99x, bf16x3 0.86-0.96x):
-# the search is bound by the per-tile filter/top-k bookkeeping beside the MFMA chain, neither by
-# the streamed bytes nor by the matrix pipe alone.  auto = fp32; FDX_KNN selects another engine.
-KNN_BF16X3_MIN_CANDIDATES = 1 << 62
+# beat fp32lds (0.66-0.99x) and bf16x3 (0.86-0.96x) at every size.  bf16x3r (round 5,
+# profiles/r5_k): at the bench's DP=1 self-search (13.6k x 13.6k) 0.195 ms against fp32's 0.20
+# (its collect pass stays ~100 us: latency-bound at ~2 waves per SIMD), at the DP=8 global-scope
+# rank (13.6k queries x 108.8k candidates) 0.80 ms against 1.04 ms.  auto = bf16x3r from 64k
+# candidates, fp32 below; FDX_KNN selects an engine.
+KNN_BF16X3_MIN_CANDIDATES = 1 << 16
 
 
 def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:
     e = engine or os.environ.get("FDX_KNN", "auto")
     if e == "auto":
-        return "bf16x3" if mc >= KNN_BF16X3_MIN_CANDIDATES else "fp32"
+        return "bf16x3r" if mc >= KNN_BF16X3_MIN_CANDIDATES else "fp32"
     if e not in ("fp32", "fp32lds", "bf16x3", "bf16x3r"):
         raise ValueError(f"unknown k-NN engine {e!r}")
     return e
