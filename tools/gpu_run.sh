@@ -71,6 +71,13 @@ for st in "$@"; do
       # shellcheck disable=SC2086
       step knnprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/knnprof" -o run -- python3 "$R/tools/knn_lab.py" --reps 5 $FDX_KNN_ARGS
       cd "$R" ;;
+    pmcknn)  # bf16x3r collect / rerank counters (FDX_KNN_ARGS picks engines and splits)
+      cd /tmp && export TMPDIR=/tmp
+      # shellcheck disable=SC2086
+      step pmcknn_a 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel)" --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_SALU --output-format csv -d "$OUT/pmcknn_a" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS || exit 1
+      # shellcheck disable=SC2086
+      step pmcknn_b 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel)" --pmc SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcknn_b" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS
+      cd "$R" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" $FDX_KNN_ARGS ;;  # shellcheck disable=SC2086
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
