@@ -112,8 +112,8 @@ __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, i
 // candidate tiles (the per-slice lists are merged by knn_merge_kernel).  Per 32-candidate tile:
 //   * 16 v_mfma_f32_32x32x2_f32 give lane (j, h) the scores of query j against the 16 candidate
 //     rows of half h (exact fp32: score = q.c - 0.5||c||^2, the norm term is column 30);
-//   * a branch-free filter appends every score >= the lane's threshold to a per-lane LDS queue
-//     (non-passing lanes store into a private dump slot instead: no exec-mask juggling);
+//   * every score >= the lane's threshold is appended to a per-lane LDS queue (a wave-uniform
+//     branch per accumulator row skips the rows no lane passes);
 //   * once any lane holds kQFlush entries the queues are inserted into the per-lane top-k
 //     (exact score-then-index order, self/padding excluded) and the threshold becomes the k-th
 //     best of the UNION of the two half-lists of the query (lanes j and j+32), which is a valid
@@ -145,8 +145,8 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
   float thr = kNegBig;
 
-  // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks.  Slot
-  // kQCap - 1 is the lane's dump slot.
+  // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks (the last
+  // slot is spare: kept from the select-and-store form's dump slot).
   constexpr int kCap = QF - 1 + 16 + 1;
   __shared__ int2 qent[kCap * kWave];  // (score bits, candidate index) at [slot * 64 + lane]
   int qn = 0;
@@ -205,13 +205,20 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
     for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
     if (!__any(mx >= thr)) continue;
     const int cbase = c0 + 4 * h;
+    // Append: a wave-uniform branch per accumulator row skips the rows no lane passes (usually all
+    // but one or two once the lists are full); the passing lanes store under their exec mask.  The
+    // per-row select-and-store of every row (dump slot for non-passing lanes) was ~110 of the
+    // ~135 VALU instructions per tile whenever ANY lane passed (r5_n PMC).
     int qe = qn * kWave + lane;                     // element of this lane's next free slot
-    const int de = (kCap - 1) * kWave + lane;      // this lane's dump slot
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const bool pass = acc[r] >= thr;
-      qent[pass ? qe : de] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
-      qe += pass ? kWave : 0;
+      if (__any(pass)) {
+        if (pass) {
+          qent[qe] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
+          qe += kWave;
+        }
+      }
     }
     qn = (qe - lane) / kWave;
     if (__any(qn >= QF)) flush();
@@ -354,12 +361,15 @@ __global__ __launch_bounds__(kLW * kWave) void knn_topk_lds_kernel(const float* 
       if (!__any(mx >= thr)) continue;
       const int cbase = c0 + 4 * h;
       int qe = qn * kWave + lane;
-      const int de = (kQCap - 1) * kWave + lane;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
+      for (int r = 0; r < 16; ++r) {  // knn_topk_kernel's uniform-skip append
         const bool pass = acc[r] >= thr;
-        qent[pass ? qe : de] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
-        qe += pass ? kWave : 0;
+        if (__any(pass)) {
+          if (pass) {
+            qent[qe] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
+            qe += kWave;
+          }
+        }
       }
       qn = (qe - lane) / kWave;
       if (__any(qn >= kQFlush)) flush();
@@ -731,12 +741,15 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     if (!__any(mx >= cut)) continue;
     const int cbase = c0 + 4 * h;
     int qe = qc * kWave + lane;
-    const int de = (kCap - 1) * kWave + lane;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < 16; ++r) {  // knn_topk_kernel's uniform-skip append
       const bool pass = acc[r] >= cut;
-      qent[pass ? qe : de] = make_int2(__float_as_int(acc[r] - mg), cbase + (r & 3) + 8 * (r >> 2));
-      qe += pass ? kWave : 0;
+      if (__any(pass)) {
+        if (pass) {
+          qent[qe] = make_int2(__float_as_int(acc[r] - mg), cbase + (r & 3) + 8 * (r >> 2));
+          qe += kWave;
+        }
+      }
     }
     qc = (qe - lane) / kWave;
     if (__any(qc >= kQFlush)) flush();
