@@ -7,7 +7,10 @@ Solvers (all minimise sklearn's objective, ops/reference.py NewtonStateRef docst
                 ~6-10 passes.  Data parallel: ONE all-reduce of 1088 doubles per iteration.
   * ``sgd``     curvature-normalised momentum minibatch SGD: every minibatch strides over the whole
                 shard (row phase b of the pass grid's tile walk) plus 1/nb of the virtual SMOTE
-                picks; gradient-only passes with fixed-point in-launch reduction.
+                picks; epoch 0 on a quarter of the rows, Polyak averaging from the first full epoch;
+                gradient-only passes with fixed-point sums.  One process: the whole schedule is ONE
+                persistent launch (grid barrier per step); data parallel: pass -> one all-reduce of
+                36 int64 -> update per step.
 
 The device loop never synchronises with the host inside a chunk of iterations: a device-side
 ``done`` flag turns converged iterations into no-op launches.
