@@ -1065,23 +1065,16 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
 int knn3r_list_cap() { return kListCap; }
 
 int knn3r_splits(int mq_pad, int mc_pad) {
-  // fewer slices than the one-wave engines: a slice restarts the lists (16 appends per lane on its
-  // first tile) and each slice holds kListCap ints per query lane
-  static const int cap = resident_cap(knn_collect_kernel<5>, kWave);
-  const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
-  int max_s = tiles / 16;
-  if (max_s > 16) max_s = 16;
-  if (max_s < 1) max_s = 1;
-  int best = 1;
-  double best_eff = -1.0;
-  for (int s = 1; s <= max_s; ++s) {
-    const double blocks = (double)qblocks * s;
-    const double rounds = std::ceil(blocks / cap);
-    double eff = blocks / (rounds * cap);
-    eff -= 0.004 * (s - 1);
-    if (eff > best_eff + 1e-9) { best_eff = eff; best = s; }
-  }
-  return best;
+  // Four slices (fewer on small candidate sets: >= 16 tiles each).  Measured at the bench's DP=1
+  // self-search and the DP=8 global-scope rank, 4 beat 8, 9 and 16 (r5_o: 0.194 vs 0.208-0.247 ms,
+  // 0.783 vs 0.803-0.883 ms): every slice adds its own list entries and re-rank work, so filling
+  // the machine with slices does not pay.
+  (void)mq_pad;
+  const int tiles = mc_pad / 32;
+  int s = tiles / 16;
+  if (s > 4) s = 4;
+  if (s < 1) s = 1;
+  return s;
 }
 
 void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
