@@ -111,9 +111,15 @@ def c5(dev):
                             label="c5 reference point: the same shard with bf16 rows")
     shard["fp8_vs_bf16_rows_per_s"] = round(shard["post_smote_rows_per_s"] / shard_bf16["post_smote_rows_per_s"], 3)
     shard["fp8_vs_bf16_fit_phase"] = round(shard_bf16["phase_ms"]["fit"] / shard["phase_ms"]["fit"], 3)
+    # config 5 names a gradient all-reduce: the minibatch SGD solver on the same shard
+    sgd = _train_cfg(dev, 12_500_000, "fp8", "sgd", reps=5,
+                     label="c5 fp8 rows, minibatch SGD: the 12.5M-row per-GPU shard")
+    sgd_bf16 = _train_cfg(dev, 12_500_000, "bf16", "sgd", reps=5,
+                          label="c5 reference point: SGD on the same shard with bf16 rows")
+    sgd["fp8_vs_bf16_rows_per_s"] = round(sgd["post_smote_rows_per_s"] / sgd_bf16["post_smote_rows_per_s"], 3)
     whole = _train_cfg(dev, 100_000_000, "fp8", "newton", reps=2,
                        label="c5 fp8 rows: all 100M rows on one GPU (HBM sizing)")
-    return [shard, shard_bf16, whole]
+    return [shard, shard_bf16, sgd, sgd_bf16, whole]
 
 
 def main():
