@@ -599,8 +599,11 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
 // at every moment, so every candidate with exact >= s_k (upper bound >= s_k >= thr) is on a list.
 // Phase 2 (knn_rerank_kernel, 8 lanes per query) re-scores the listed candidates exactly (the
 // k-ordered fp32 fmaf chain of knn_topk3's re-score) and keeps the top-k (ties -> smaller index):
-// the exact fp32 ranking.  A lane list that overflows kListCap sends its query to a brute-force
-// exact scan in phase 2 (correct, slow, and not seen at SMOTE shapes).
+// the exact fp32 ranking.  A full lane list is compacted in place first: an entry (lower bound
+// lb) whose upper bound -- at most lb + 2 m_max, m_max the largest margin the lane has used -- is
+// below the current threshold cannot reach s_k and is dropped.  A list still full after that
+// sends its query to a brute-force exact scan in phase 2 (correct, slow: r5_q measured the config-5
+// shard, 17k x 17k, at 0.67 ms before the compaction).
 constexpr int kListCap = 64;
 constexpr int kSeedTiles = 2;             // seed candidates per slice > 0: 64
 constexpr float kMarginScale = 0x1p-14f;  // m = 2^-14 (||q|| tmax + 0.5 tmax^2): >= 4x the error bound
@@ -609,7 +612,7 @@ template <int K>
 __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
                                                             const uint4* __restrict__ Chl,
                                                             const float* __restrict__ tmax, int mc_pad, int mc,
-                                                            int64_t self_offset, int* __restrict__ lists,
+                                                            int64_t self_offset, int2* __restrict__ lists,
                                                             int* __restrict__ counts) {
   const int lane = threadIdx.x;
   const int h = lane >> 5, j = lane & 31;
@@ -640,6 +643,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
   float thr = kNegBig;
+  float mgmax = 0.0f;  // the largest margin this lane has used (list compaction bound)
   constexpr int kCap = kQFlush - 1 + 16 + 1;
   __shared__ int2 qent[kCap * kWave];  // (lower-bound bits, candidate index) at [slot * 64 + lane]
   int qc = 0, cnt = 0;
@@ -668,7 +672,16 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
         const int2 v = qent[e * kWave + lane];
         const int ci = v.y;
         if (ci != self_c && ci < mc) {
-          if (cnt < kListCap) lists[lbase + (int64_t)cnt * kWave] = ci;
+          if (cnt == kListCap) {  // full: drop the entries that can no longer reach s_k (rare path)
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this lane's list stores have landed
+            int w = 0;
+            for (int e2 = 0; e2 < kListCap; ++e2) {
+              const int2 o = lists[lbase + (int64_t)e2 * kWave];
+              if (__int_as_float(o.x) + 2.0f * mgmax >= thr) lists[lbase + (int64_t)(w++) * kWave] = o;
+            }
+            cnt = w;
+          }
+          if (cnt < kListCap) lists[lbase + (int64_t)cnt * kWave] = v;
           ++cnt;
           topk_insert<K>(bs, bi, __int_as_float(v.x), ci);
         }
@@ -734,6 +747,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     tmn = tmn2;
     if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
     const float mg = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
+    mgmax = fmaxf(mgmax, mg);
     const float cut = thr - mg;  // upper bound approx + mg >= thr
     float mx = acc[0];
 #pragma unroll
@@ -763,7 +777,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
 template <int K>
 __global__ __launch_bounds__(256) void knn_rerank_kernel(const float* __restrict__ Q, const float* __restrict__ C,
                                                          int mq, int mc, int qblocks, int nsplit, int64_t self_offset,
-                                                         const int* __restrict__ lists,
+                                                         const int2* __restrict__ lists,
                                                          const int* __restrict__ counts, int* __restrict__ out_idx,
                                                          float* __restrict__ out_score) {
   const int gl = blockIdx.x * 256 + threadIdx.x;
@@ -809,9 +823,9 @@ __global__ __launch_bounds__(256) void knn_rerank_kernel(const float* __restrict
         for (int h = 0; h < 2; ++h) {
           const int64_t cb = ((int64_t)s * qblocks + blk) * kWave + j + 32 * h;
           const int n = counts[cb];
-          const int* li = lists + ((int64_t)s * qblocks + blk) * kListCap * kWave + j + 32 * h;
+          const int2* li = lists + ((int64_t)s * qblocks + blk) * kListCap * kWave + j + 32 * h;
           for (int e = l; e < n; e += 8) {
-            const int ci = li[(int64_t)e * kWave];
+            const int ci = li[(int64_t)e * kWave].y;
             topk_insert<K>(bs, bi, exact(ci), ci);
           }
         }
@@ -1080,6 +1094,7 @@ int knn3r_splits(int mq_pad, int mc_pad) {
 void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                        const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
                        float* out_score, int* lists, int* counts, int nsplit, hipStream_t stream) {
+  int2* lists2 = reinterpret_cast<int2*>(lists);  // [.. ][cap][64] (lower bound, index) pairs
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_topk3r: pads must be x32");
   if (mq > mq_pad || mc > mc_pad || nsplit < 1 || lists == nullptr || counts == nullptr)
     throw std::runtime_error("knn_topk3r: bad shapes or missing list workspaces");
@@ -1088,8 +1103,8 @@ void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, cons
   const uint4* chl = reinterpret_cast<const uint4*>(Chl);
   const unsigned rblocks = (unsigned)(((int64_t)mq * 8 + 255) / 256);
 #define FDX_KNN3R(KK)                                                                                       \
-  knn_collect_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, lists, counts); \
-  knn_rerank_kernel<KK><<<rblocks, 256, 0, stream>>>(Q, C, mq, mc, mq_pad / 32, nsplit, self_offset, lists, counts, \
+  knn_collect_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, lists2, counts); \
+  knn_rerank_kernel<KK><<<rblocks, 256, 0, stream>>>(Q, C, mq, mc, mq_pad / 32, nsplit, self_offset, lists2, counts, \
                                                      out_idx, out_score)
   switch (k) {
     case 1: FDX_KNN3R(1); break;

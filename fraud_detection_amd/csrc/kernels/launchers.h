@@ -251,7 +251,7 @@ int knn3_splits(int mq_pad, int mc_pad);
 // LDS-tiled fp32 engine: workgroups of 4 waves x 32 queries share staged candidate chunks
 // (mq_pad multiple of 128)
 int knn_lds_splits(int mq_pad, int mc_pad);
-// bf16x3 collect (per-lane candidate lists [nsplit][mq_pad / 32][cap][64] int32 + counts
+// bf16x3 collect (per-lane candidate lists [nsplit][mq_pad / 32][cap][64] int32 pairs + counts
 // [nsplit][mq_pad / 32][64]) then exact fp32 re-rank of the listed candidates (knn.hip)
 int knn3r_list_cap();
 int knn3r_splits(int mq_pad, int mc_pad);

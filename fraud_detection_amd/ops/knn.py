@@ -138,7 +138,7 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
     if eng == "bf16x3r":
         nb = ns * (mq_pad // 32) * 64
-        lists = torch.empty(nb * m.KNN3R_LIST_CAP, device=Q.device, dtype=torch.int32)
+        lists = torch.empty(nb * m.KNN3R_LIST_CAP * 2, device=Q.device, dtype=torch.int32)  # (lb, index)
         counts = torch.empty(nb, device=Q.device, dtype=torch.int32)
         m.knn_topk3r(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                      int(k), ptr(idx), ptr(score), ptr(lists), ptr(counts), ns, s)

@@ -344,6 +344,26 @@ def test_knn_engines_agree_with_ties_and_auto_selection(dev):
         assert (ia == ib).all(1).float().mean().item() > 0.99
 
 
+def test_knn_bf16x3r_lists_stay_bounded_on_heavy_tailed_rows(dev):
+    """The config-5 shard's minority set (17k standardized rows with the heavy-tailed Amount
+    column): the collect pass compacts full lists instead of overflowing (no brute-force scan),
+    and the lists equal the fp32 engine's."""
+    from fraud_detection_amd.data.synthetic import separable
+
+    X, y = separable(200_000, fraud_rate=0.085, seed=31, device=dev)
+    xm = X[y == 1][:17_000]
+    xm = (xm - X.mean(0)) / X.std(0)
+    C = torch.zeros((xm.shape[0], 32), device=dev)
+    C[:, :30] = xm
+    C[:, 30] = 1.0
+    C = C.contiguous()
+    a = K.knn_topk(C, C, k=5, self_offset=0, engine="fp32")
+    dg = {}
+    b = K.knn_topk(C, C, k=5, self_offset=0, engine="bf16x3r", _diag=dg)
+    assert dg["over_cap"] == 0, dg
+    assert (a == b).all(1).float().mean().item() > 0.999
+
+
 def test_knn_collect_list_overflow_falls_back_to_exact_scan(dev):
     """All-equal candidates pass every tile's filter, so the per-lane lists overflow: the re-rank
     kernel's exact scan must still return the k smallest indices (self excluded)."""
