@@ -143,7 +143,9 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = kNegBig;
+  // padding queries (qg >= mq: zero rows, every score equal) never pass the filter: a lane that
+  // appended every candidate made its wave the slowest of the grid (r5_r: 17k minority rows)
+  float thr = qg < mq ? kNegBig : __builtin_inff();
 
   // Per-lane queue, [slot][lane]: same-slot stores of a wave hit 64 distinct banks (the last
   // slot is spare: kept from the select-and-store form's dump slot).
@@ -175,7 +177,7 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = kth;
+    thr = qg < mq ? kth : __builtin_inff();
   };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
@@ -281,7 +283,9 @@ __global__ __launch_bounds__(kLW * kWave) void knn_topk_lds_kernel(const float* 
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = kNegBig;
+  // padding queries (qg >= mq: zero rows, every score equal) never pass the filter: a lane that
+  // appended every candidate made its wave the slowest of the grid (r5_r: 17k minority rows)
+  float thr = qg < mq ? kNegBig : __builtin_inff();
   int qn = 0;
   auto flush = [&]() {
     for (int e = 0; __any(e < qn); ++e) {
@@ -307,7 +311,7 @@ __global__ __launch_bounds__(kLW * kWave) void knn_topk_lds_kernel(const float* 
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = kth;
+    thr = qg < mq ? kth : __builtin_inff();
   };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
@@ -483,7 +487,9 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = kNegBig;
+  // padding queries (qg >= mq: zero rows, every score equal) never pass the filter: a lane that
+  // appended every candidate made its wave the slowest of the grid (r5_r: 17k minority rows)
+  float thr = qg < mq ? kNegBig : __builtin_inff();
   // exact fp32 score of tile row rl against this lane's query (a k-ordered fmaf chain)
   auto rescore = [&](int rl) -> float {
     float acc = 0.0f;
@@ -566,7 +572,7 @@ __global__ __launch_bounds__(kWave) void knn_topk3_kernel(const float* __restric
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = kth;
+    thr = qg < mq ? kth : __builtin_inff();
   }
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -611,7 +617,7 @@ constexpr float kMarginScale = 0x1p-14f;  // m = 2^-14 (||q|| tmax + 0.5 tmax^2)
 template <int K>
 __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
                                                             const uint4* __restrict__ Chl,
-                                                            const float* __restrict__ tmax, int mc_pad, int mc,
+                                                            const float* __restrict__ tmax, int mq, int mc_pad, int mc,
                                                             int64_t self_offset, int2* __restrict__ lists,
                                                             int* __restrict__ counts) {
   const int lane = threadIdx.x;
@@ -642,7 +648,9 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
   int bi[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-  float thr = kNegBig;
+  // padding queries (qg >= mq: zero rows, every score equal) never pass the filter: a lane that
+  // appended every candidate made its wave the slowest of the grid (r5_r: 17k minority rows)
+  float thr = qg < mq ? kNegBig : __builtin_inff();
   float mgmax = 0.0f;  // the largest margin this lane has used (list compaction bound)
   constexpr int kCap = kQFlush - 1 + 16 + 1;
   __shared__ int2 qent[kCap * kWave];  // (lower-bound bits, candidate index) at [slot * 64 + lane]
@@ -664,7 +672,7 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
       ia += ta ? 1 : 0;
       ib += ta ? 0 : 1;
     }
-    thr = kth;
+    thr = qg < mq ? kth : __builtin_inff();
   };
   auto flush = [&]() {
     for (int e = 0; __any(e < qc); ++e) {
@@ -1103,7 +1111,7 @@ void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, cons
   const uint4* chl = reinterpret_cast<const uint4*>(Chl);
   const unsigned rblocks = (unsigned)(((int64_t)mq * 8 + 255) / 256);
 #define FDX_KNN3R(KK)                                                                                       \
-  knn_collect_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mc_pad, mc, self_offset, lists2, counts); \
+  knn_collect_kernel<KK><<<grid, kWave, 0, stream>>>(Q, qh, chl, tmax, mq, mc_pad, mc, self_offset, lists2, counts); \
   knn_rerank_kernel<KK><<<rblocks, 256, 0, stream>>>(Q, C, mq, mc, mq_pad / 32, nsplit, self_offset, lists2, counts, \
                                                      out_idx, out_score)
   switch (k) {

@@ -146,7 +146,7 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
             c = counts.float()
             _diag.update(nsplit=ns, list_cap=int(m.KNN3R_LIST_CAP), mean=float(c.mean()), max=int(c.max()),
                          p99=float(torch.quantile(c[: min(c.numel(), 1 << 24)], 0.99)),
-                         over_cap=int((c > m.KNN3R_LIST_CAP).sum()))
+                         over_cap=int((c > m.KNN3R_LIST_CAP).sum()), counts=counts.view(ns, mq_pad // 32, 64))
     elif eng == "bf16x3":
         m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                     int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
