@@ -70,6 +70,7 @@ def main():
                 if eng == "bf16x3r":
                     dg = {}
                     K.knn_topk(Q, Cc, 5, off, engine=eng, nsplit=ns, _diag=dg)
+                    dg.pop("counts", None)
                     print(json.dumps({name: {"engine": eng, "nsplit": ns, "lists": dg}}), flush=True)
                 case = {"engine": eng, "nsplit": ns, "ms": round(ms, 4),
                         "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
