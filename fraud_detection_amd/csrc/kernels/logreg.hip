@@ -372,7 +372,10 @@ __device__ __forceinline__ void bf16_wave_pass(
   const float hrs = rsqrtf((float)hess_stride);  // the final x hess_stride restores u u^T
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
-  int64_t ptile = wave * row_sub + row_phase;  // this wave's next pick tile
+  // this wave's next pick tile: the pick tiles go to the HIGH wave indices, whose share of the
+  // stored tiles is one smaller where the tiles do not divide evenly (the low waves get the extra
+  // tile), so the pick waves are not also the longest stored-row waves (persistent SGD: r5_t)
+  int64_t ptile = (Gw - 1 - wave) * row_sub + row_phase;
   // pre: the tile's inputs are in ppre already (pick_load, issued before the grid barrier)
   auto pick_tile = [&](int64_t t, bool pre) __attribute__((always_inline)) {
     const int64_t p = t * 16 + rr;
@@ -652,7 +655,7 @@ __device__ __forceinline__ void fp8_wave_pass(
   const float hrs = rsqrtf((float)hess_stride);
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
-  int64_t ptile = wave * row_sub + row_phase;
+  int64_t ptile = (Gw - 1 - wave) * row_sub + row_phase;  // high waves (bf16_wave_pass)
   const int q4 = lane & 3, r4 = lane >> 2;
   auto pick_tile = [&](int64_t t, bool pre) __attribute__((always_inline)) {
     float wf[8];  // this lane's 4-lane-layout weights in fp8 row units, from LDS (not held in VGPRs
@@ -1468,11 +1471,16 @@ enum : int { kSgdFault = 229 };                 // state slot: a grid barrier ti
 // update end, then every wave's own pass end
 constexpr int kStampRows = 3 + kPersistWaves;
 // The wave that reduces the block's sums, zeroes the next accumulator set (block 0) and arrives at
-// the barrier: the LAST wave of the block.  The pick tiles of a step sit on the low wave indices
-// (wave wv of block b is wave wv * B + b of the pass grid), i.e. on wave 0 of every block, whose
-// next-pick input chain (dependent loads) would otherwise delay the arrival (r5_h stamps: an
-// 8.4 us block epilogue after the last wave's pass).
-constexpr int kArriveWave = kPersistWaves - 1;
+// the barrier: the FIRST wave of the block.  The pick tiles of a step sit on the high wave indices
+// of the pass grid (wave wv of block b is wave wv * B + b), i.e. on the last waves of every block,
+// whose next-pick input chain (dependent loads) would otherwise delay the arrival (r5_h stamps:
+// an 8.4 us block epilogue when the arriving wave also carried the picks).
+constexpr int kArriveWave = 0;
+// Accumulator replicas of the persistent launch: 256 blocks over 16 replicas (16 adds per word;
+// 16 and 8 both took the fit 608 -> 585 us, r5_t / r5_u).
+// Every block folds all of them after the barrier, so fewer replicas is fewer loads per update.
+constexpr int kPersistReplicas = 16;
+constexpr int kPersistAccWords = kPersistReplicas * 36;
 // Template knobs: LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the
 // same bits); PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick
 // tile's inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the
@@ -1494,8 +1502,7 @@ __device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned targ
     v += __shfl_xor(v, 4, kWave);
     v = __shfl(v, 0, kWave);
     if ((unsigned)v >= target) return true;
-    if (spins > (1u << 21)) return false;  // ~1 s: not every block is resident
-    __builtin_amdgcn_s_sleep(1);
+    if (spins > (1u << 21)) return false;  // ~2 s of polls: not every block is resident
   }
 }
 
@@ -1509,7 +1516,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   __shared__ __attribute__((aligned(16))) float wsh[32];  // weights of the passes (fp8: row units)
   __shared__ float wnew[32];                              // sgd_apply's folded weights
   __shared__ float red[kPersistWaves][36];
-  __shared__ unsigned long long rep[kSgdAccWords];
+  __shared__ unsigned long long rep[kPersistAccWords];
   __shared__ double rd[kSgdSlots];
   __shared__ int s_done, s_ok;
   __shared__ double saff[64];  // the affine map, read from LDS by every step's reduce and update
@@ -1533,7 +1540,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   __syncthreads();
   const float cw0 = class_w[0], cw1 = class_w[1];
   // wave wv of block b is wave wv * B + b of the per-step grid: the waves that carry the pick tiles
-  // (the low wave indices) spread over every CU instead of filling the first ones
+  // (the high wave indices) spread over every CU instead of filling the last ones
   const int64_t wave = (int64_t)wv * gridDim.x + blockIdx.x;
   const bool active = wave < P.Gw;
   const int64_t n = pass_stored_rows<VIRT>(0, row_end, sv, hole);
@@ -1557,7 +1564,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     have_ppre = false;
     if (kPersistPrefetch == 0 || !active || st >= P.s1) return;
     if constexpr (VIRT) {  // the inputs of the wave's first pick tile of step st
-      const int64_t pt = wave * rowsub_of(st) + phase_of(st);
+      const int64_t pt = (P.Gw - 1 - wave) * rowsub_of(st) + phase_of(st);
       if (pt < ntile) {
         const int64_t p = pt * 16 + (lane >> 2);
         pick_load<4, kPreLams>(sv, p < npick ? p : -1, lane & 3, ppre);
@@ -1593,10 +1600,10 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   for (int st = P.s0; st < P.s1 && !s_done; ++st) {
     if constexpr (kPersistPrefetch == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(touch) : : "memory");
     const int ep = st / P.nb, pos = st % P.nb, b = phase_of(st), rsub = rowsub_of(st);
-    unsigned long long* acc = accs + (st % 3) * kSgdAccWords;
+    unsigned long long* acc = accs + (st % 3) * kPersistAccWords;
     if (blockIdx.x == 0 && wv == kArriveWave) {  // set st + 1 (read as set st - 2 before barrier st - 1)
-      unsigned long long* nx = accs + ((st + 1) % 3) * kSgdAccWords;
-      for (int e = lane; e < kSgdAccWords; e += kWave)
+      unsigned long long* nx = accs + ((st + 1) % 3) * kPersistAccWords;
+      for (int e = lane; e < kPersistAccWords; e += kWave)
         __hip_atomic_store(nx + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- the pass over minibatch b (this wave's share) ----
@@ -1658,13 +1665,13 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     }
     __syncthreads();
     if (wv != kArriveWave) {
-      prefetch(st + 1);  // wave 0 (the pick tiles' wave) runs its pick-input chain during the barrier
+      prefetch(st + 1);  // the pick tiles' waves run their pick-input chains during the barrier
     } else {
       // sgd_fused_tail's per-wave fixed point (inactive waves hold zeros)
       const long long qs = lane < kSgdSlots ? wave_sums_fixed<kPersistWaves>(red, affl, lane) : 0;
       prefetch(st + 1);  // no pick tile on this wave: an L2 touch, in flight beside the adds
       if (lane < kSgdSlots && lane != 34 && qs != 0)
-        __hip_atomic_fetch_add(acc + (blockIdx.x % kSgdReplicas) * 36 + lane, (unsigned long long)qs,
+        __hip_atomic_fetch_add(acc + (blockIdx.x % kPersistReplicas) * 36 + lane, (unsigned long long)qs,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       arrivals += gridDim.x;
       if (P.stamps != nullptr && lane == 0)
@@ -1677,13 +1684,13 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     __syncthreads();
     if (!s_ok) break;  // uniform in the block
     // ---- the update, redundantly in every block ----
-    for (int e = t; e < kSgdAccWords; e += kPersistThreads)
+    for (int e = t; e < kPersistAccWords; e += kPersistThreads)
       rep[e] = __hip_atomic_load(acc + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (t < kSgdSlots) {  // fixed-order fold of the replicas (integer: exact in any order anyway)
       unsigned long long q = 0;
 #pragma unroll 8
-      for (int r = 0; r < kSgdReplicas; ++r) q += rep[r * 36 + t];
+      for (int r = 0; r < kPersistReplicas; ++r) q += rep[r * 36 + t];
       rd[t] = (double)(long long)q * (1.0 / kFixScale);
     }
     __syncthreads();

@@ -22,7 +22,7 @@ import numpy as np  # noqa: E402
 
 from fraud_detection_amd.ops import reference as ref  # noqa: E402
 
-FINE = 32  # finest partition: (tile // G) mod 32, (pick // 16) mod 32
+FINE = 64  # finest partition: (tile // G) mod 64, (pick // 16) mod 64
 
 
 def build(rows: int, seed: int = 1000):
@@ -179,6 +179,9 @@ def main():
         "sub2_avg1": (8, [(0.4, 2), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "nb6_avg1": (6, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "nb4_avg1": (4, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub8_avg1": (8, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub8_avg1_b": (8, [(0.5, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub4x2_avg2": (8, [(0.4, 4), (0.5, 2), (0.8, 1), (0.8, 1)], 2),
         "nb4_avg1_b": (4, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "nb6_avg1_b": (6, [(0.5, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
         "nb4_avg1_c": (4, [(0.5, 4), (0.8, 1), (0.9, 1), (0.9, 1)], 1),
