@@ -102,7 +102,9 @@ def test_dp_global_scope_virtual_smote_equals_single_process(tmp_path):
     assert sum(int(o["n_train"]) for o in outs) == ref.n_train_rows
     assert sum(int(o["n_syn"]) for o in outs) == ref.n_synthetic
     np.testing.assert_allclose(outs[0]["w"], ref.w, atol=2e-6, rtol=0)
-    assert abs(int(outs[0]["iters"]) - int(ref.fit.n_iter)) <= 1
+    # tol 1e-8 sits at the fp32 pass noise floor: the iteration that first meets it can move by a
+    # couple of steps with the summation grouping (the ranks' shards vs one process)
+    assert abs(int(outs[0]["iters"]) - int(ref.fit.n_iter)) <= 2
 
 
 def test_dp_global_scope_stored_smote_equals_single_process(tmp_path):
