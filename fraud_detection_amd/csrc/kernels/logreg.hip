@@ -372,10 +372,10 @@ __device__ __forceinline__ void bf16_wave_pass(
   const float hrs = rsqrtf((float)hess_stride);  // the final x hess_stride restores u u^T
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
-  // this wave's next pick tile: the pick tiles go to the HIGH wave indices, whose share of the
-  // stored tiles is one smaller where the tiles do not divide evenly (the low waves get the extra
-  // tile), so the pick waves are not also the longest stored-row waves (persistent SGD: r5_t)
-  int64_t ptile = (Gw - 1 - wave) * row_sub + row_phase;
+  // this wave's next pick tile (the low wave indices: in the per-pass grids they are the first
+  // blocks dispatched; carrying the picks on the high ones -- the waves with one stored tile
+  // fewer -- made the Newton step 1.094 -> 1.123 ms and the persistent SGD fit 585 -> 655 us, r5_v)
+  int64_t ptile = wave * row_sub + row_phase;
   // pre: the tile's inputs are in ppre already (pick_load, issued before the grid barrier)
   auto pick_tile = [&](int64_t t, bool pre) __attribute__((always_inline)) {
     const int64_t p = t * 16 + rr;
@@ -655,7 +655,7 @@ __device__ __forceinline__ void fp8_wave_pass(
   const float hrs = rsqrtf((float)hess_stride);
   const int64_t npick = VIRT ? (int64_t)sv.mq * sv.k : 0;
   const int64_t ntile = (npick + 15) >> 4;
-  int64_t ptile = (Gw - 1 - wave) * row_sub + row_phase;  // high waves (bf16_wave_pass)
+  int64_t ptile = wave * row_sub + row_phase;
   const int q4 = lane & 3, r4 = lane >> 2;
   auto pick_tile = [&](int64_t t, bool pre) __attribute__((always_inline)) {
     float wf[8];  // this lane's 4-lane-layout weights in fp8 row units, from LDS (not held in VGPRs
@@ -1471,11 +1471,11 @@ enum : int { kSgdFault = 229 };                 // state slot: a grid barrier ti
 // update end, then every wave's own pass end
 constexpr int kStampRows = 3 + kPersistWaves;
 // The wave that reduces the block's sums, zeroes the next accumulator set (block 0) and arrives at
-// the barrier: the FIRST wave of the block.  The pick tiles of a step sit on the high wave indices
-// of the pass grid (wave wv of block b is wave wv * B + b), i.e. on the last waves of every block,
-// whose next-pick input chain (dependent loads) would otherwise delay the arrival (r5_h stamps:
-// an 8.4 us block epilogue when the arriving wave also carried the picks).
-constexpr int kArriveWave = 0;
+// the barrier: the LAST wave of the block.  The pick tiles of a step sit on the low wave indices
+// (wave wv of block b is wave wv * B + b of the pass grid), i.e. on wave 0 of every block, whose
+// next-pick input chain (dependent loads) would otherwise delay the arrival (r5_h stamps: an
+// 8.4 us block epilogue after the last wave's pass).
+constexpr int kArriveWave = kPersistWaves - 1;
 // Accumulator replicas of the persistent launch: 256 blocks over 16 replicas (16 adds per word;
 // 16 and 8 both took the fit 608 -> 585 us, r5_t / r5_u).
 // Every block folds all of them after the barrier, so fewer replicas is fewer loads per update.
@@ -1540,7 +1540,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   __syncthreads();
   const float cw0 = class_w[0], cw1 = class_w[1];
   // wave wv of block b is wave wv * B + b of the per-step grid: the waves that carry the pick tiles
-  // (the high wave indices) spread over every CU instead of filling the last ones
+  // (the low wave indices) spread over every CU instead of filling the first ones
   const int64_t wave = (int64_t)wv * gridDim.x + blockIdx.x;
   const bool active = wave < P.Gw;
   const int64_t n = pass_stored_rows<VIRT>(0, row_end, sv, hole);
@@ -1564,7 +1564,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     have_ppre = false;
     if (kPersistPrefetch == 0 || !active || st >= P.s1) return;
     if constexpr (VIRT) {  // the inputs of the wave's first pick tile of step st
-      const int64_t pt = (P.Gw - 1 - wave) * rowsub_of(st) + phase_of(st);
+      const int64_t pt = wave * rowsub_of(st) + phase_of(st);
       if (pt < ntile) {
         const int64_t p = pt * 16 + (lane >> 2);
         pick_load<4, kPreLams>(sv, p < npick ? p : -1, lane & 3, ppre);
