@@ -34,10 +34,12 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 #           the listed candidates exactly (8 lanes per query) -- knn.hip knn_collect_kernel.
 # Measured on MI355X from 13.6k to 170k minority rows (profiles/r2_s3i/knn_engines.jsonl): fp32
 # beat fp32lds (0.66-0.99x) and bf16x3 (0.86-0.96x) at every size.  bf16x3r (round 5,
-# profiles/r5_k, r5_o): at the bench's DP=1 self-search (13.6k x 13.6k) 0.194 ms against fp32's
-# 0.209, at the DP=8 global-scope rank (13.6k queries x 108.8k candidates) 0.78 ms against 1.07.
-# auto = bf16x3r from 8k candidates, fp32 below; FDX_KNN selects an engine.
-KNN_BF16X3_MIN_CANDIDATES = 1 << 13
+# profiles/r5_k, r5_o): at the DP=8 global-scope rank (13.6k queries x 108.8k candidates) 0.78 ms
+# against 1.07.  At the bench's DP=1 self-search the lab had it at 0.194 vs 0.209 ms, but inside
+# the pipeline's step its collect + re-rank took 199 us against the fp32 engine's ~200 us
+# (profiles/r5_x timeline): no gain.  auto = bf16x3r from 64k candidates, fp32 below; FDX_KNN
+# selects an engine.
+KNN_BF16X3_MIN_CANDIDATES = 1 << 16
 
 
 def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:

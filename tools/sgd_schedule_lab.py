@@ -123,13 +123,15 @@ def run_schedule(chunks, nb, epochs, mom=0.55, C=1.0, avg_from=None, tol=1e-3):
     extra_epochs); None: only the last epoch is averaged and every epoch runs."""
     st = ref.SgdStateRef(np.zeros(32))
     streamed = 0.0
-    for ei, (c, s) in enumerate(epochs):
+    for ei, spec in enumerate(epochs):
+        c, s = spec[0], spec[1]
+        nbe = spec[2] if len(spec) > 2 else nb  # per-epoch minibatch count (optional)
         if avg_from is not None and st.done:
             break
         last_epoch = (ei == len(epochs) - 1) if avg_from is None else ei >= avg_from
-        for b in range(nb):
-            fine = [ch for ch in range(FINE) if ch % (nb * s) == b * s] if s > 1 else \
-                   [ch for ch in range(FINE) if ch % nb == b]
+        for b in range(nbe):
+            fine = [ch for ch in range(FINE) if ch % (nbe * s) == b * s] if s > 1 else \
+                   [ch for ch in range(FINE) if ch % nbe == b]
             g = np.zeros(32)
             loss = S = dsum = 0.0
             for ch in fine:
@@ -140,7 +142,7 @@ def run_schedule(chunks, nb, epochs, mom=0.55, C=1.0, avg_from=None, tol=1e-3):
                 dsum += dd
             streamed += len(fine) / FINE
             red = np.concatenate([g, [loss, S, 0.0, dsum]])
-            st.step(red[:32], red[32], red[33], red[35], 30, C, c, mom, nb * s, last_epoch, b == nb - 1,
+            st.step(red[:32], red[32], red[33], red[35], 30, C, c, mom, nbe * s, last_epoch, b == nbe - 1,
                     -1.0 if s > 1 else (tol if avg_from is not None else 1e-3), True)
     w = st.w.copy()
     w[31] = 0.0
@@ -179,6 +181,10 @@ def main():
         "sub2_avg1": (8, [(0.4, 2), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "nb6_avg1": (6, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "nb4_avg1": (4, [(0.4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub4nb4_avg1": (8, [(0.4, 4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub4nb4_avg1_b": (8, [(0.5, 4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub4nb4_avg1_c": (8, [(0.6, 4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub8nb4_avg1": (8, [(0.5, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1": (8, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1_b": (8, [(0.5, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub4x2_avg2": (8, [(0.4, 4), (0.5, 2), (0.8, 1), (0.8, 1)], 2),
@@ -206,13 +212,13 @@ def main():
         mom = spec[3] if len(spec) > 3 else 0.55
         if only and name not in only.split(","):
             continue
-        if FINE % (nb * max(s for _, s in ep)) and nb * max(s for _, s in ep) > FINE:
+        if nb * max(e[1] for e in ep) > FINE:
             continue
         t1 = time.time()
         w, gmax, streamed = run_schedule(chunks, nb, ep, mom=mom, avg_from=avg_from)
         o, gfull = full_objective(chunks, w)
         gap = (o - on) / on
-        out[name] = {"nb": nb, "epochs": ep, "steps": nb * len(ep), "epoch_gmax": gmax, "full_grad": gfull,
+        out[name] = {"nb": nb, "epochs": ep, "steps": sum(e[2] if len(e) > 2 else nb for e in ep), "epoch_gmax": gmax, "full_grad": gfull,
                      "gap": gap, "epochs_streamed": streamed}
         print(f"{name:16s} steps {nb * len(ep):3d} streamed {streamed:.2f} ep_gmax {gmax:.2e} "
               f"full_grad {gfull:.2e} gap {gap:.2e} ({time.time() - t1:.0f}s)", flush=True)
