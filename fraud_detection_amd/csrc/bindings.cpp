@@ -592,9 +592,15 @@ PYBIND11_MODULE(_fdx_native, m) {
                               u s, u parents, u nbr, u lam, u off, u cnt, int64_t n_real, int64_t q_offset, int mq,
                               int k, int64_t hole_at, int64_t hole_len, u state, u aff, int d, double C, double mom,
                               int fi, double tol, int nb, int epochs, int avg_from, std::vector<double> lrs, int s0,
-                              int s1, u acc, u ticket, std::vector<int> subs) {
-    if (nb < 1 || epochs < 1 || (int)lrs.size() < epochs || (int)subs.size() < epochs || s0 < 0 || s1 > nb * epochs)
+                              int s1, u acc, u ticket, std::vector<int> subs, std::vector<int> nbs) {
+    if (nb < 1 || epochs < 1 || (int)lrs.size() < epochs || (int)subs.size() < epochs || (int)nbs.size() < epochs)
       throw std::runtime_error("sgd_run: bad schedule");
+    std::vector<int> estart(epochs + 1, 0);  // first step of every epoch (per-epoch minibatch counts)
+    for (int e = 0; e < epochs; ++e) {
+      if (nbs[e] < 1) throw std::runtime_error("sgd_run: minibatch counts must be >= 1");
+      estart[e + 1] = estart[e] + nbs[e];
+    }
+    if (s0 < 0 || s1 > estart[epochs]) throw std::runtime_error("sgd_run: bad step range");
     fdx::SmoteView v;
     const fdx::SmoteView* vp = nullptr;
     if (parents) {
@@ -613,10 +619,12 @@ PYBIND11_MODULE(_fdx_native, m) {
     h.at = hole_at;
     h.len = hole_len;
     for (int st = s0; st < s1; ++st) {
-      const int ep = st / nb, b = st % nb, sub = subs[ep];
-      // sub-sampled epoch: phase b * sub of a grid of nb * sub minibatches; never decides convergence
-      const int rsub = nb * sub, ph = b * sub;
-      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, rsub, ep >= avg_from, b == nb - 1,
+      int ep = 0;
+      while (ep + 1 < epochs && st >= estart[ep + 1]) ++ep;
+      const int nbe = nbs[ep], b = st - estart[ep], sub = subs[ep];
+      // sub-sampled epoch: phase b * sub of a grid of nbe * sub minibatches; never decides convergence
+      const int rsub = nbe * sub, ph = b * sub;
+      const fdx::SgdArgs a = sgd_args(d, C, lrs[ep], mom, fi, rsub, ep >= avg_from, b == nbe - 1,
                                       sub > 1 ? -1.0 : tol);
       if (acc) {  // one launch per step (fixed-point atomics + last-block update)
         fdx::launch_sgd_pass_fused(P<const void>(X), fp8, x_scale, end, P<float>(w32), P<const float>(cw), P<int>(done),
@@ -662,9 +670,10 @@ PYBIND11_MODULE(_fdx_native, m) {
                                     int64_t hole_len, u ws, u state, u w32, u done, u aff, int d, double C, double mom,
                                     int fi, double tol, int nb, int epochs, int avg_from, int serpentine,
                                     std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps,
-                                    std::vector<int> subs) {
+                                    std::vector<int> subs, std::vector<int> nbs) {
     if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
     if ((int)subs.size() < epochs) throw std::runtime_error("sgd_persist: one sub-sample factor per epoch");
+    if ((int)nbs.size() < epochs) throw std::runtime_error("sgd_persist: one minibatch count per epoch");
     const fdx::SmoteView v = smote_view(parents, nbr, lam, off, cnt, n_real, q_offset, mq, k);
     fdx::RowHole h;
     h.at = hole_at;
@@ -678,10 +687,14 @@ PYBIND11_MODULE(_fdx_native, m) {
     a.C = C;
     a.momentum = mom;
     a.tol = tol;
+    a.estart[0] = 0;
     for (int e = 0; e < epochs; ++e) {
       a.lr[e] = lrs[e];
       if (subs[e] < 1) throw std::runtime_error("sgd_persist: sub-sample factors must be >= 1");
+      if (nbs[e] < 1) throw std::runtime_error("sgd_persist: minibatch counts must be >= 1");
       a.sub[e] = subs[e];
+      a.nbe[e] = nbs[e];
+      a.estart[e + 1] = a.estart[e] + nbs[e];
     }
     a.d = d;
     a.fit_intercept = fi;

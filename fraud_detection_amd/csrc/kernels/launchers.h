@@ -222,6 +222,8 @@ struct SgdPersistArgs {
   double C = 1.0, momentum = 0.5, tol = 1e-3;
   double lr[kSgdMaxEpochs] = {};
   int sub[kSgdMaxEpochs] = {1, 1, 1, 1, 1, 1, 1, 1};  // per-epoch row sub-sample (1 = every row)
+  int nbe[kSgdMaxEpochs] = {1, 1, 1, 1, 1, 1, 1, 1};  // per-epoch minibatch count (steps)
+  int estart[kSgdMaxEpochs + 1] = {};                  // first step of every epoch (prefix of nbe)
   // avg_from: steps of epochs >= avg_from add to the Polyak average (each such epoch returns its
   // own average); >= epochs: no averaging
   int d = 30, fit_intercept = 1, nb = 1, epochs = 1, avg_from = 0, serpentine = 0;

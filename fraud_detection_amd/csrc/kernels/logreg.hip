@@ -1554,10 +1554,19 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   unsigned touch = 0;  // FDX_PERSIST_PREFETCH 2: the dummy destination of the L2 touch loads
   unsigned arrivals = 0;
   // an epoch with sub-sample s visits every s-th phase of a grid of nb * s minibatches
-  auto rowsub_of = [&](int st) { return P.nb * P.sub[st / P.nb]; };
+  // per-epoch minibatch counts: step st is minibatch st - estart[ep] of epoch ep
+  auto ep_of = [&](int st) {
+    int e = 0;
+    while (e + 1 < P.epochs && st >= P.estart[e + 1]) ++e;
+    return e;
+  };
+  auto rowsub_of = [&](int st) {
+    const int e = ep_of(st);
+    return P.nbe[e] * P.sub[e];
+  };
   auto phase_of = [&](int st) {
-    const int ep = st / P.nb, pos = st % P.nb;
-    return ((P.serpentine && (ep & 1)) ? P.nb - 1 - pos : pos) * P.sub[ep];
+    const int ep = ep_of(st), pos = st - P.estart[ep];
+    return ((P.serpentine && (ep & 1)) ? P.nbe[ep] - 1 - pos : pos) * P.sub[ep];
   };
   auto prefetch = [&](int st) {  // the wave's first tile(s) of step st: rows do not depend on w
     have_pre = false;
@@ -1599,7 +1608,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
 
   for (int st = P.s0; st < P.s1 && !s_done; ++st) {
     if constexpr (kPersistPrefetch == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(touch) : : "memory");
-    const int ep = st / P.nb, pos = st % P.nb, b = phase_of(st), rsub = rowsub_of(st);
+    const int ep = ep_of(st), pos = st - P.estart[ep], b = phase_of(st), rsub = rowsub_of(st);
     unsigned long long* acc = accs + (st % 3) * kPersistAccWords;
     if (blockIdx.x == 0 && wv == kArriveWave) {  // set st + 1 (read as set st - 2 before barrier st - 1)
       unsigned long long* nx = accs + ((st + 1) % 3) * kPersistAccWords;
@@ -1702,7 +1711,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
     a.fit_intercept = P.fit_intercept;
     a.nb = rsub;  // the minibatch estimates the epoch's weight as rsub x its own
     a.avg = ep >= P.avg_from;
-    a.epoch_end = pos == P.nb - 1;
+    a.epoch_end = pos == P.nbe[ep] - 1;
     a.tol = P.sub[ep] > 1 ? -1.0 : P.tol;  // a sub-sampled epoch never decides convergence
     sgd_apply(rd, sst, wnew, &s_done, affl, a, t, true);
     __syncthreads();
@@ -2002,7 +2011,7 @@ int sgd_persist_blocks(int grid_blocks) {
 
 void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
                         const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream) {
-  if (a.nb < 1 || a.epochs < 1 || a.epochs > kSgdMaxEpochs || a.s0 < 0 || a.s1 > a.nb * a.epochs || a.s0 >= a.s1)
+  if (a.nb < 1 || a.epochs < 1 || a.epochs > kSgdMaxEpochs || a.s0 < 0 || a.s1 > a.estart[a.epochs] || a.s0 >= a.s1)
     throw std::runtime_error("sgd_persist: bad schedule");
   if (a.Gw < kWaves || a.Gw % kWaves != 0) throw std::runtime_error("sgd_persist: bad pass grid");
   if (a.ws == nullptr || a.st == nullptr || a.w32 == nullptr || a.done == nullptr)

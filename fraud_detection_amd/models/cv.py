@@ -175,7 +175,7 @@ class DeviceCV:
                 f = lr_ops.sgd_fit(rows, C=cfg.C, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
                                    batches=cfg.sgd_batches, average=cfg.sgd_average, tol=cfg.sgd_tol,
                                    subsample=cfg.sgd_subsample, extra_epochs=cfg.sgd_extra_epochs,
-                                   avg_from=cfg.sgd_avg_from, d=d, w0=w0,
+                                   avg_from=cfg.sgd_avg_from, epoch_batches=cfg.sgd_epoch_batches, d=d, w0=w0,
                                    class_w=cw,
                                    fit_intercept=cfg.fit_intercept, fp8_scale=cfg.fp8_scale, workspace=ws,
                                    affine=stats.aff, virtual=v, hole=hole)

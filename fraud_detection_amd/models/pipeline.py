@@ -59,6 +59,7 @@ class TrainConfig:
     sgd_subsample: tuple = lr_ops.SGD_SUB  # per-epoch row sub-sample (growing-batch schedule)
     sgd_extra_epochs: int = lr_ops.SGD_EXTRA_EPOCHS  # run only while not converged
     sgd_avg_from: int = lr_ops.SGD_AVG_FROM  # first Polyak-averaged epoch
+    sgd_epoch_batches: tuple = lr_ops.SGD_EPOCH_BATCHES  # per-epoch minibatch counts
     sgd_average: bool = True
     sgd_tol: float = lr_ops.SGD_TOL
     check_every: int = 1            # Newton: iterations per convergence-flag read (host reads one chunk behind)
@@ -465,6 +466,7 @@ class DevicePipeline:
                                  momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs, batches=cfg.sgd_batches,
                                  average=cfg.sgd_average, tol=cfg.sgd_tol, subsample=cfg.sgd_subsample,
                                  extra_epochs=cfg.sgd_extra_epochs, avg_from=cfg.sgd_avg_from,
+                                 epoch_batches=cfg.sgd_epoch_batches,
                                  class_w=class_w, d=d, w0=w0,
                                  fit_intercept=cfg.fit_intercept, comm=comm, fp8_scale=cfg.fp8_scale,
                                  workspace=self._ws, affine=stats.aff if fused else None, virtual=virt)

@@ -656,13 +656,15 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
 
 
 def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit_intercept, comm, serpentine=False,
-                   subs=None):
+                   subs=None, nbs=None):
     from ..utils.checkpoint import config_signature
 
     n_all = int(comm.all_reduce_scalar(float(n))) if (comm is not None and comm.world_size > 1) else n
     extra = {"serpentine": True} if serpentine else {}
     if subs is not None and any(x != 1 for x in subs):
         extra["subsample"] = [int(x) for x in subs]
+    if nbs is not None and any(x != nb for x in nbs):
+        extra["epoch_batches"] = [int(x) for x in nbs]
     return config_signature(kind="sgd2", n=n_all, d=d, C=C, lr=list(lr), momentum=momentum, batches=nb,
                             epochs=epochs, average=bool(average), tol=tol, class_w=list(class_w),
                             fit_intercept=fit_intercept, **extra)
@@ -675,7 +677,7 @@ def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit
 # steps for 1e-3 (the curvature falls ~5x between w = 0 and the optimum).
 SGD_BATCHES = 8
 SGD_EPOCHS = 3
-SGD_LR = (0.4, 0.7, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
+SGD_LR = (0.5, 0.7, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
 # Per-epoch row sub-sample: epoch 0 visits 1/4 of the rows (its 8 minibatches are every 4th phase
 # of a 32-minibatch grid) -- a growing-batch schedule: the first epoch only has to bring w near the
 # optimum, so it needs no full pass (Smith et al., "Don't decay the learning rate, increase the
@@ -683,7 +685,13 @@ SGD_LR = (0.4, 0.7, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 
 # post-SMOTE rows): (4, 1, 1) with steps (0.4, 0.7, 0.8) ends at epoch gradient 2.2e-4 and 1.3e-4
 # relative above the Newton objective, streaming 2.25 epochs instead of 3 (3 full epochs with
 # (0.4, 0.6, 0.8): 3.6e-4, 4.2e-5).  A sub-sampled epoch never decides convergence.
-SGD_SUB = (4, 1, 1)
+SGD_SUB = (8, 1, 1)
+# Per-epoch minibatch counts: epoch 0 takes 4 steps over an eighth of the rows (4 minibatches of
+# 1/32) instead of 8 over a quarter -- half the epoch-0 steps and bytes.  fp64 simulation
+# (tools/sgd_schedule_lab.py "sub8nb4_avg1"): 16M post-SMOTE rows epoch gradient 7.4e-4, objective
+# 5.8e-5 above Newton's; 8M rows 5.6e-4 / 4.4e-4, both within the nominal 3 epochs (the 8 x 1/32
+# schedule: 4.8e-4 / 9.4e-5 and 9.0e-4 / 5.3e-4).
+SGD_EPOCH_BATCHES = (4, 8, 8)
 # Epochs past SGD_EPOCHS that run only while the fit has not converged (the device `done` flag makes
 # them no-ops otherwise; the persistent launch leaves its loop).  Each is averaged like the last
 # nominal epoch, starting from that epoch's averaged iterate.  fp8 rows carry ~6% quantisation
@@ -704,13 +712,13 @@ SGD_SLOTS = 36
 SGD_MAX_EPOCHS = 8  # launchers.h kSgdMaxEpochs (per-epoch step scalars of the persistent launch)
 
 
-def _effective_subs(subs, n_stored: int, n_picks: int, nb: int, blocks: int) -> list:
-    """Sub-sample factors that keep every minibatch of an epoch's finer grid (nb x s) populated:
+def _effective_subs(subs, n_stored: int, n_picks: int, nbs, blocks: int) -> list:
+    """Sub-sample factors that keep every minibatch of an epoch's finer grid (nb_e x s) populated:
     >= 1 strided group of row tiles and >= 2 pick tiles each; else that epoch visits every row."""
     groups = n_stored // (ref.ROW_TILE * ref.WAVES_PER_BLOCK * max(1, blocks))
     ptiles = -(-n_picks // ref.PICK_TILE)
     out = []
-    for x in subs:
+    for x, nb in zip(subs, nbs):
         ok = x > 1 and groups >= nb * x and (n_picks == 0 or ptiles >= 2 * nb * x)
         out.append(int(x) if ok else 1)
     return out
@@ -740,7 +748,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             checkpoint_every: int = 0, affine: torch.Tensor | None = None, virtual: VirtualSmote | None = None,
             batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None,
             persistent: bool | None = None, serpentine: bool = False, subsample=SGD_SUB,
-            extra_epochs: int = 0, avg_from: int | None = None, _stamps: torch.Tensor | None = None):
+            extra_epochs: int = 0, avg_from: int | None = None, epoch_batches=None,
+            _stamps: torch.Tensor | None = None):
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
@@ -773,7 +782,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     ``extra_epochs``: epochs after ``epochs`` that run only if the fit has not converged yet
     (the pipelines pass SGD_EXTRA_EPOCHS); with ``average`` each of them returns its own Polyak average, like the
     last nominal epoch.  ``avg_from``: first averaged epoch (None: the last nominal one; the
-    pipelines pass SGD_AVG_FROM)."""
+    pipelines pass SGD_AVG_FROM).  ``epoch_batches``: per-epoch minibatch counts (default
+    ``batches`` for every epoch; the pass grid and its partition are sized for ``batches``)."""
     check_rows(rows)
     w0 = _default_w0(w0)
     rows, hole = _apply_hole(rows, hole)
@@ -795,10 +805,12 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     subs = [int(_epoch_lr(subsample, e)) if subsample is not None else 1 for e in range(epochs)]
     if any(x < 1 for x in subs):
         raise ValueError("sub-sample factors must be >= 1")
+    nbs = [nb if epoch_batches is None else max(1, int(_epoch_lr(epoch_batches, e))) for e in range(epochs)]
+    estart = np.concatenate([[0], np.cumsum(nbs)]).astype(int).tolist()  # first step of every epoch
     # a sub-sampled epoch only where every minibatch of its finer grid still holds row tiles of the
     # whole shard and SMOTE picks (small shards: every epoch full); one decision for all DP ranks
     n_picks = int(virtual.nbr.numel()) if virtual is not None else 0
-    subs = _effective_subs(subs, n_stored, n_picks, nb, ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS))
+    subs = _effective_subs(subs, n_stored, n_picks, nbs, ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS))
     if comm is not None and comm.world_size > 1:
         subs = [int(comm.all_reduce_scalar(float(x), op="min")) for x in subs]
     if affine is not None and not rows.is_cuda:
@@ -809,7 +821,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             vr[:, LABEL_COL] = virtual.label
             return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0, d, fit_intercept,
                                 comm, fp8_scale, checkpoint, checkpoint_every, None, None, virtual=(virtual, vr),
-                                max_steps=max_steps, serpentine=serpentine, subs=subs, nominal=nominal)
+                                max_steps=max_steps, serpentine=serpentine, subs=subs, nominal=nominal, nbs=nbs)
         affine = None
     aff = 0
     if affine is not None:
@@ -817,7 +829,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             raise ValueError("affine must be a [64] float64 tensor on the rows' device")
         aff = ptr(affine)
     sig = (_sgd_signature(n, d, C, lrs, momentum, nb, epochs, avg_from, tol, class_w, fit_intercept, comm, serpentine,
-                          subs)
+                          subs, nbs)
            if checkpoint else None)
     got = checkpoint.latest(sig) if checkpoint is not None else None
     start = (0, 0)
@@ -825,7 +837,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         vv = (virtual, virtual.rows_f32()) if virtual is not None else None
         return _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0, d, fit_intercept, comm,
                             fp8_scale, checkpoint, checkpoint_every, sig, got, virtual=vv, max_steps=max_steps,
-                            serpentine=serpentine, subs=subs, nominal=nominal)
+                            serpentine=serpentine, subs=subs, nominal=nominal, nbs=nbs)
     if virtual is not None:
         virtual.check(rows)
         if class_w[1] > VIRTUAL_MAX_WEIGHT:
@@ -870,7 +882,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                           ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
                           float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
                           int(bool(serpentine)), [float(x) for x in lrs], int(s0), int(s1),
-                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs)
+                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs, nbs)
             return
         if serpentine:
             raise ValueError("serpentine minibatch order needs the persistent SGD launch")
@@ -878,23 +890,24 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                   ptr(ws.partial), blocks, s, *vargs, ptr(ws.state), aff, d,
                   float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
                   [float(x) for x in lrs], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
-                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs)
+                  ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs, nbs)
 
     if not dp and checkpoint is None:
-        s0 = start[0] * nb + start[1]
-        run_steps(s0, epochs * nb if max_steps is None else min(epochs * nb, int(max_steps)))
+        s0 = estart[start[0]] + start[1]
+        run_steps(s0, estart[epochs] if max_steps is None else min(estart[epochs], int(max_steps)))
         return PendingFit(ws.state, sgd=True)
     for ep in range(start[0], epochs):
         if ep >= nominal and int(ws.done.item()):  # converged: the extra epochs would be no-ops
             break
         c = lrs[ep]
-        for pos in range(start[1] if ep == start[0] else 0, nb):
-            if max_steps is not None and ep * nb + pos >= max_steps:
+        nbe = nbs[ep]
+        for pos in range(start[1] if ep == start[0] else 0, nbe):
+            if max_steps is not None and estart[ep] + pos >= max_steps:
                 break
-            b = _sgd_phase(pos, ep, nb, serpentine)
-            rsub, ph = nb * subs[ep], b * subs[ep]
+            b = _sgd_phase(pos, ep, nbe, serpentine)
+            rsub, ph = nbe * subs[ep], b * subs[ep]
             avg = int(ep >= avg_from)
-            last = pos + 1 == nb
+            last = pos + 1 == nbe
             if dp:
                 # lean step: the pass leaves its fixed-point sums (int64: the all-reduce is exact and
                 # order-free, every rank gets bitwise the same vector), one collective, the update
@@ -906,8 +919,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                                    float(momentum), int(fit_intercept), rsub, avg, int(last),
                                    -1.0 if subs[ep] > 1 else float(tol), s)
             else:  # the same kernels as the uninterrupted fit: checkpointed fits stay bit-identical
-                run_steps(ep * nb + pos, ep * nb + pos + 1)
-            gstep = ep * nb + pos + 1
+                run_steps(estart[ep] + pos, estart[ep] + pos + 1)
+            gstep = estart[ep] + pos + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 nxt = (ep + 1, 0) if last else (ep, pos + 1)
                 checkpoint.save(gstep, {"state": ws.state},
@@ -995,13 +1008,15 @@ def _newton_fit_cpu(rows, C, tol, max_iter, class_w, w0, d, fit_intercept, comm,
 
 def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0, d, fit_intercept, comm, fp8_scale,
                  checkpoint=None, checkpoint_every=0, sig=None, got=None, virtual=None, max_steps=None,
-                 serpentine=False, subs=None, nominal=None):
+                 serpentine=False, subs=None, nominal=None, nbs=None):
     """The device SGD's algorithm in fp64 (ref.SgdStateRef) over the same minibatch partition:
     stored row tiles by the pass grid's strided walk (the full SGD grid of a 256-CU part,
     ref.SGD_FULL_BLOCKS, shrunk for small shards like the device), virtual samples by their pick tile."""
     R = ref.rows_to_f32(rows, fp8_scale, d).double().numpy()
     n_stored = R.shape[0]
     subs = list(subs) if subs is not None else [1] * max(epochs, 1)
+    nbs = list(nbs) if nbs is not None else [nb] * max(epochs, 1)
+    estart = np.concatenate([[0], np.cumsum(nbs)]).astype(int).tolist()
     blocks = ref.sgd_grid_blocks(n_stored, nb, ref.SGD_FULL_BLOCKS)
     parts = [R]
     pick = None
@@ -1037,11 +1052,12 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0,
     for ep in range(start[0], epochs):
         if nominal is not None and ep >= nominal and st.done:  # converged: extra epochs are no-ops
             break
-        for pos in range(start[1] if ep == start[0] else 0, nb):
-            if max_steps is not None and ep * nb + pos >= max_steps:
+        nbe = nbs[ep]
+        for pos in range(start[1] if ep == start[0] else 0, nbe):
+            if max_steps is not None and estart[ep] + pos >= max_steps:
                 break
-            b = _sgd_phase(pos, ep, nb, serpentine)
-            Rb = R[members(nb * subs[ep], b * subs[ep])]
+            b = _sgd_phase(pos, ep, nbe, serpentine)
+            Rb = R[members(nbe * subs[ep], b * subs[ep])]
             g, loss, wsum, _ = ref.logreg_pass(Rb, st.w, class_w, False)
             X = Rb.copy()
             X[:, LABEL_COL] = 0.0
@@ -1052,10 +1068,10 @@ def _sgd_fit_cpu(rows, C, lrs, momentum, epochs, nb, avg_from, tol, class_w, w0,
             red = np.concatenate([g, [loss, wsum, 0.0, float(np.sum(sw * p * (1 - p)))]])
             if comm is not None and comm.world_size > 1:
                 red = comm.all_reduce(torch.from_numpy(red)).numpy()
-            last = pos + 1 == nb
-            st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nb * subs[ep],
+            last = pos + 1 == nbe
+            st.step(red[:32], red[32], red[33], red[35], d, C, lrs[ep], momentum, nbe * subs[ep],
                     ep >= avg_from, last, -1.0 if subs[ep] > 1 else tol, fit_intercept)
-            gstep = ep * nb + pos + 1
+            gstep = estart[ep] + pos + 1
             if checkpoint is not None and (last or (checkpoint_every and gstep % checkpoint_every == 0)):
                 sv = np.zeros(STATE_SIZE)
                 sv[S_W:S_W + 32], sv[S_VEL:S_VEL + 32], sv[160:192], sv[192:224] = st.w, st.v, st.avg, st.ep_g

@@ -47,7 +47,8 @@ def test_device_cv_job(dev, solver, storage):
         assert g.n_iter == f.n_iter
     else:
         g = L.sgd_fit(part, w0=w0, affine=cv.stats.aff, virtual=v,
-                          extra_epochs=L.SGD_EXTRA_EPOCHS, avg_from=L.SGD_AVG_FROM).as_fit_info()
+                          extra_epochs=L.SGD_EXTRA_EPOCHS, avg_from=L.SGD_AVG_FROM,
+                          epoch_batches=L.SGD_EPOCH_BATCHES).as_fit_info()
     assert np.array_equal(g.w, f.w)
     # the fold AUC is the exact AUC of the fold model on the fold's raw validation rows
     mean, _, scale = cv.stats.numpy()

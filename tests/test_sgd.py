@@ -87,3 +87,16 @@ def test_extra_epochs_run_only_until_converged_cpu():
     assert a.n_iter == 8 and b.n_iter == 12 and not b.converged
     R = z.double().numpy()
     assert _objective(R, b.w) <= _objective(R, a.w) + 1e-12
+
+
+def test_per_epoch_minibatch_counts_cpu():
+    """epoch_batches: an epoch of 2 minibatches then one of 4 -- 6 steps; with 4 and 4 it is the
+    uniform schedule exactly."""
+    X, y = separable(40_000, fraud_rate=0.3, seed=12)
+    st = S.scaler_fit(X)
+    z = S.scale_cast(X, st, labels=y, out_dtype="f32")
+    a = L.sgd_fit(z, batches=4, epochs=2, tol=0.0, subsample=None, epoch_batches=(2, 4))
+    assert a.n_iter == 6 and np.all(np.isfinite(a.w))
+    b = L.sgd_fit(z, batches=4, epochs=2, tol=0.0, subsample=None, epoch_batches=(4, 4))
+    c = L.sgd_fit(z, batches=4, epochs=2, tol=0.0, subsample=None)
+    assert np.array_equal(b.w, c.w) and b.n_iter == c.n_iter == 8

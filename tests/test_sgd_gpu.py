@@ -115,7 +115,8 @@ def test_sgd_reaches_newton_optimum_at_scale(dev, storage):
     assert abs(auc_s - auc_n) <= 1e-4, (auc_s, auc_n)
     f = rs.fit
     # the nominal epochs, plus the extra epoch(s) only if the nominal ones did not converge
-    assert f.n_iter in [L.SGD_BATCHES * (L.SGD_EPOCHS + e) for e in range(L.SGD_EXTRA_EPOCHS + 1)], f.n_iter
+    nominal = sum(L.SGD_EPOCH_BATCHES)
+    assert f.n_iter in [nominal + L.SGD_BATCHES * e for e in range(L.SGD_EXTRA_EPOCHS + 1)], f.n_iter
     assert f.converged and f.grad_max <= L.SGD_TOL, (f.grad_max, gap, f.n_iter)
     assert f.converged == (f.grad_max <= L.SGD_TOL)
     assert abs(f.objective - os_["objective"]) < 0.05 * os_["objective"]
@@ -140,6 +141,11 @@ def test_persistent_launch_is_bitwise_the_per_step_launches(dev, storage, virt):
     assert np.array_equal(a.w, b.w), np.abs(a.w - b.w).max()
     assert a.n_iter == b.n_iter and a.objective == b.objective and a.grad_max == b.grad_max
     assert a.converged == b.converged
+    # per-epoch minibatch counts with a sub-sampled first epoch: persistent == per step
+    kw = dict(virtual=v, epoch_batches=(4, 8, 8), subsample=(8, 1, 1), lr=(0.5, 0.7, 0.8))
+    e = L.sgd_fit(rows, persistent=True, **kw).as_fit_info()
+    f = L.sgd_fit(rows, persistent=False, **kw).as_fit_info()
+    assert np.array_equal(e.w, f.w) and e.n_iter == f.n_iter
     # one launch per step of the persistent kernel (the checkpointed path) is the same fit too
     c = L.sgd_fit(rows, virtual=v, persistent=True, max_steps=5).as_fit_info()
     assert c.n_iter == 5

@@ -185,6 +185,8 @@ def main():
         "sub4nb4_avg1_b": (8, [(0.5, 4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub4nb4_avg1_c": (8, [(0.6, 4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8nb4_avg1": (8, [(0.5, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub8nb4_avg1_b": (8, [(0.4, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "sub8nb4_avg1_c": (8, [(0.6, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1": (8, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1_b": (8, [(0.5, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub4x2_avg2": (8, [(0.4, 4), (0.5, 2), (0.8, 1), (0.8, 1)], 2),
