@@ -55,7 +55,10 @@ def main():
     v = pipe._virtual
     aff = res.scaler.aff
     ws = L.LRWorkspace(dev)
-    kw = dict(virtual=v, affine=aff, workspace=ws)
+    cfg = pipe.cfg  # the pipeline's schedule (sub-sampled first epoch, per-epoch minibatch counts, ...)
+    kw = dict(virtual=v, affine=aff, workspace=ws, lr=cfg.sgd_lr, momentum=cfg.sgd_momentum, epochs=cfg.sgd_epochs,
+              batches=cfg.sgd_batches, subsample=cfg.sgd_subsample, extra_epochs=cfg.sgd_extra_epochs,
+              avg_from=cfg.sgd_avg_from, epoch_batches=cfg.sgd_epoch_batches)
     out = {"rows": a.rows, "storage": a.storage, "post_smote_rows": res.n_train_rows,
            "cfg": os.environ.get("FDX_SGD_PERSIST_CFG", "default")}
     print("cfg", out["cfg"], flush=True)
@@ -79,16 +82,16 @@ def main():
         out[name] = {"fit_ms": ms, "converged": info.converged, "grad_max": info.grad_max, "obj": info.objective}
         print(f"{name:24s} {ms * 1e3:8.1f} us  converged={info.converged} gmax={info.grad_max:.2e}", flush=True)
 
-    steps = L.SGD_EPOCHS * L.SGD_BATCHES
+    steps = int(sum(cfg.sgd_epoch_batches)) + cfg.sgd_batches * cfg.sgd_extra_epochs  # room for every step
     blocks = L.native().sgd_persist_blocks(ws.sgd_blocks)
     nrow = 3 + 8  # logreg.hip kStampRows: pass end, barrier exit, update end, 8 waves' pass ends
     stamps = torch.zeros(steps * nrow * blocks, dtype=torch.int64, device=dev)
-    L.sgd_fit(rows, persistent=True, _stamps=stamps, **kw).as_fit_info()
+    ran = L.sgd_fit(rows, persistent=True, _stamps=stamps, **kw).as_fit_info().n_iter
     torch.cuda.synchronize()
     t = stamps.cpu().numpy().astype(np.int64).reshape(steps, nrow, blocks) * 10  # ns
     t0 = t[0, 0].min()
     rows_out = []
-    for k in range(steps):
+    for k in range(min(steps, ran)):
         pe, be, ue = t[k, 0], t[k, 1], t[k, 2]
         we = t[k, 3:]  # [8][blocks] each wave's pass end
         start = t[k - 1, 2] if k else None
