@@ -153,9 +153,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=8_000_000)
     ap.add_argument("--json", default="")
+    ap.add_argument("--seed", type=int, default=1000)
     a = ap.parse_args()
     t0 = time.time()
-    chunks = build(a.rows)
+    chunks = build(a.rows, a.seed)
     print(f"built {sum(len(c) for c in chunks)} rows in {time.time() - t0:.0f}s", flush=True)
     wn = newton(chunks)
     on, gn = full_objective(chunks, wn)
@@ -222,7 +223,7 @@ def main():
         gap = (o - on) / on
         out[name] = {"nb": nb, "epochs": ep, "steps": sum(e[2] if len(e) > 2 else nb for e in ep), "epoch_gmax": gmax, "full_grad": gfull,
                      "gap": gap, "epochs_streamed": streamed}
-        print(f"{name:16s} steps {nb * len(ep):3d} streamed {streamed:.2f} ep_gmax {gmax:.2e} "
+        print(f"{name:16s} steps {out[name]['steps']:3d} streamed {streamed:.2f} ep_gmax {gmax:.2e} "
               f"full_grad {gfull:.2e} gap {gap:.2e} ({time.time() - t1:.0f}s)", flush=True)
     if a.json:
         with open(a.json, "w") as f:
