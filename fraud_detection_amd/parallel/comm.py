@@ -237,12 +237,28 @@ class Communicator:
                 self._native.all_reduce_(t)
                 return t
             if self._host_staged(t):
-                h = t.cpu()
+                h = self._stage_d2h(t)
                 dist.all_reduce(h, op=_op(op))
                 t.copy_(h)
                 return t
             dist.all_reduce(t, op=_op(op))
             return t
+
+    def _stage_d2h(self, t: torch.Tensor) -> torch.Tensor:
+        """Device -> host copy of a gloo-staged collective's operand into a reused pinned buffer
+        (a pageable copy goes through the runtime's staging path on every call).  Timed on its own
+        ("stage_d2h"): the wait for the device work that produces ``t`` shows up here, apart from
+        the collective's wait for the other ranks."""
+        key = (tuple(t.shape), t.dtype)
+        pool = self.__dict__.setdefault("_pinned", {})
+        h = pool.get(key)
+        if h is None:
+            h = pool[key] = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+        t0 = time.perf_counter()
+        h.copy_(t)  # synchronous: waits for the stream's work that writes t
+        if self._timing:  # stats only (not a collective: the trace does not list it)
+            self.stats._add("stage_d2h", t.numel() * t.element_size(), time.perf_counter() - t0)
+        return h
 
     def all_reduce(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
         return self.all_reduce_(t.clone(), op)
@@ -266,7 +282,7 @@ class Communicator:
             t = t.contiguous()
             with self._timed("broadcast", t, "gloo-staged" if self._host_staged(t) else self.backend):
                 if self._host_staged(t):
-                    h = t.cpu()
+                    h = self._stage_d2h(t)
                     dist.broadcast(h, src=src)
                     t.copy_(h)
                 else:

@@ -12,6 +12,7 @@ on cuda:0).  For each scope rank 0 prints one JSON line with:
 """
 import argparse
 import cProfile
+import gc
 import io
 import json
 import os
@@ -33,7 +34,17 @@ def main():
     ap.add_argument("--storage", default="bf16")
     ap.add_argument("--smote-virtual", type=int, default=1, help="0: stored SMOTE rows (smote_generate + streamed)")
     ap.add_argument("--phases", type=int, default=0, help="1: per-phase synced times of every synced fit")
+    ap.add_argument("--gc-freeze", type=int, default=0, help="1: gc.freeze() after the warm-up fits")
     a = ap.parse_args()
+    gc_pauses = []  # (generation, ms) of every collection: a host pause that stalls one rank
+    gc_t0 = [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t0[0] = time.perf_counter()
+        else:
+            gc_pauses.append((info["generation"], (time.perf_counter() - gc_t0[0]) * 1e3))
+    gc.callbacks.append(_gc_cb)
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
     from fraud_detection_amd.parallel.comm import Communicator
@@ -49,9 +60,13 @@ def main():
                                        virtual_smote=bool(a.smote_virtual)), comm)
         for _ in range(2):
             pipe.fit(X, y)
+        if a.gc_freeze:
+            gc.collect()
+            gc.freeze()
         comm.barrier()
         torch.cuda.synchronize(dev)
         comm.stats.reset()
+        gc_pauses.clear()
         prof = cProfile.Profile()
         prof.enable()
         t0 = time.perf_counter()
@@ -77,6 +92,7 @@ def main():
                 phased.append({k: round(v * 1e3, 3) for k, v in r.timings.items()})
         coll_synced = comm.collective_summary()
         flag_waits = sorted(L.FLAG_WAITS, reverse=True)[:5]
+        gcs = sorted(gc_pauses, key=lambda g: -g[1])[:5]
         p = pipe.fit(X, y, profile=True)
         s = io.StringIO()
         pstats.Stats(prof, stream=s).sort_stats("tottime").print_stats(18)
@@ -85,7 +101,9 @@ def main():
                "n_train_rows": int(r.n_train_rows), "n_synthetic": int(r.n_synthetic),
                "newton_iters": int(r.fit.n_iter), "virtual_smote": pipe._virtual is not None,
                "collectives": coll, "storage": a.storage, "solver": a.solver,
-               "collectives_synced_fits": coll_synced, "longest_flag_waits_ms": [round(x * 1e3, 3) for x in flag_waits]}
+               "collectives_synced_fits": coll_synced, "longest_flag_waits_ms": [round(x * 1e3, 3) for x in flag_waits],
+               "gc_collections": len(gc_pauses), "longest_gc_pauses_ms": [[g, round(t, 3)] for g, t in gcs],
+               "gc_freeze": bool(a.gc_freeze)}
         if phased:
             out["phases_synced"] = phased
         print(json.dumps(out), flush=True)  # every rank: the two ranks share one GPU

@@ -188,6 +188,13 @@ def main():
         "sub8nb4_avg1": (8, [(0.5, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8nb4_avg1_b": (8, [(0.4, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8nb4_avg1_c": (8, [(0.6, 8, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "full6_avg1": (8, [(0.4, 4), (0.7, 1, 6), (0.8, 1, 6), (0.8, 1, 6)], 1),
+        "full6_avg1_b": (8, [(0.4, 4), (0.8, 1, 6), (0.9, 1, 6), (0.9, 1, 6)], 1),
+        "full6_avg1_c": (8, [(0.4, 4), (0.6, 1, 6), (0.7, 1, 6), (0.7, 1, 6)], 1),
+        "full4_avg1": (8, [(0.4, 4), (0.7, 1, 4), (0.8, 1, 4), (0.8, 1, 4)], 1),
+        "full4_avg1_b": (8, [(0.4, 4), (0.9, 1, 4), (1.0, 1, 4), (1.0, 1, 4)], 1),
+        "sub6_full6": (8, [(0.4, 4, 6), (0.7, 1, 6), (0.8, 1, 6), (0.8, 1, 6)], 1),
+        "full8_6": (8, [(0.4, 4), (0.7, 1), (0.8, 1, 6), (0.8, 1, 6)], 1),
         "sub8_avg1": (8, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1_b": (8, [(0.5, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub4x2_avg2": (8, [(0.4, 4), (0.5, 2), (0.8, 1), (0.8, 1)], 2),
