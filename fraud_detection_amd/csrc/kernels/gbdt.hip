@@ -799,7 +799,9 @@ __global__ __launch_bounds__(kPartThreads) void gbdt_part_scatter_kernel(
     int rfN[kPartRows], riN[kPartRows], ndN[kPartRows];
     const bool more = s0 + step < hi;
     if (more) load_step(p0 + step, rfN, riN, ndN);
-    const int cnt = rf[0] + rf[1] + rf[2] + rf[3];
+    int cnt = 0;
+#pragma unroll
+    for (int u = 0; u < kPartRows; ++u) cnt += rf[u];
     int incl = cnt;  // inclusive wave scan of the per-thread counts (thread order = row order)
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {

@@ -19,7 +19,10 @@ from .native import native, ptr, stream_of
 MAX_BIN = R.MAX_BIN
 MAX_FEAT = 30
 HIST_ENTRIES = MAX_FEAT * MAX_BIN * 2
-PART_BLOCKS = int(os.environ.get("FDX_GBDT_PART_BLOCKS", "1024"))  # partition grid (<= 4096)
+# partition grid (<= 4096): 2048 blocks of 256 -- count kernel 57.5 us vs 62.0 at 1024 per level at
+# 16M rows, scatter unchanged; 4096 and 512 slower, and 8 rows per thread instead of 4 slowed both
+# kernels (67-79 us) (profiles/r5_zp, r5_zq)
+PART_BLOCKS = int(os.environ.get("FDX_GBDT_PART_BLOCKS", "2048"))
 
 
 @dataclass
