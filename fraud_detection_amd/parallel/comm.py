@@ -123,6 +123,7 @@ class Communicator:
         self._timing = os.environ.get("FDX_COMM_TIMING", "1") == "1"
         self.trace = [] if os.environ.get("FDX_COMM_TRACE", "0") == "1" else None
         self._native = None
+        self._shm = None  # host-staged sums over shared memory (lazy, collective; False: off)
         mode = os.environ.get("FDX_COMM", "auto")  # auto | rccl | torch
         if self.world_size > 1 and self.backend == "nccl" and mode in ("auto", "rccl") and torch.cuda.is_available():
             self._native = self._try_native(strict=(mode == "rccl"))
@@ -238,11 +239,35 @@ class Communicator:
                 return t
             if self._host_staged(t):
                 h = self._stage_d2h(t)
-                dist.all_reduce(h, op=_op(op))
+                shm = self._shm_group() if op == "sum" else None
+                if shm is not None and shm.fits(h.numpy()):  # same size on every rank: same branch
+                    shm.all_reduce_(h.numpy())
+                else:
+                    dist.all_reduce(h, op=_op(op))
                 t.copy_(h)
                 return t
             dist.all_reduce(t, op=_op(op))
             return t
+
+    def _shm_group(self):
+        """The shared-memory sum all-reduce of the host-staged path (parallel/shm_reduce.py), set up
+        at the first staged sum -- a point every rank reaches together -- when all ranks share one
+        host (torchrun's LOCAL_WORLD_SIZE == WORLD_SIZE).  FDX_COMM_SHM=0 keeps gloo."""
+        if self._shm is None:
+            self._shm = False
+            if (os.environ.get("FDX_COMM_SHM", "1") == "1"
+                    and int(os.environ.get("LOCAL_WORLD_SIZE", "0")) == self.world_size):
+                from .shm_reduce import ShmAllReduce
+
+                cap = int(os.environ.get("FDX_COMM_SHM_BYTES", str(4 << 20)))
+                tmo = float(os.environ.get("FDX_DIST_TIMEOUT", "600"))
+                obj = ShmAllReduce(0, self.world_size, cap, timeout_s=tmo) if self.rank == 0 else None
+                name = [obj.name if obj is not None else None]
+                dist.broadcast_object_list(name, src=0)
+                if obj is None:
+                    obj = ShmAllReduce(self.rank, self.world_size, cap, name=name[0], timeout_s=tmo)
+                self._shm = obj
+        return self._shm or None
 
     def _stage_d2h(self, t: torch.Tensor) -> torch.Tensor:
         """Device -> host copy of a gloo-staged collective's operand into a reused pinned buffer
@@ -380,6 +405,10 @@ class Communicator:
         if self._native is not None:
             self._native.close()
             self._native = None
+        if self._shm:
+            self.barrier()  # no rank may still be reading the segment when the creator unlinks it
+            self._shm.close()
+            self._shm = None
         self._host_pg = None
         if self.initialized_here and dist.is_initialized():
             dist.destroy_process_group()

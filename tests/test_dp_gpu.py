@@ -59,8 +59,10 @@ N_GLOBAL = 1_500_000  # raw rows per rank of the global-scope test
 
 
 def _worker_global(rank, world, port, out_dir, solver, virtual=True):
+    # LOCAL_WORLD_SIZE == WORLD_SIZE: the host-staged sums go through shared memory
+    # (parallel/shm_reduce.py) -- the other DP test keeps the gloo all-reduce
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      LOCAL_RANK="0")
+                      LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world))
     from fraud_detection_amd.data.synthetic import separable
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
     from fraud_detection_amd.parallel.comm import Communicator
