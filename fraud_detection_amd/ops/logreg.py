@@ -7,8 +7,8 @@ Solvers (all minimise sklearn's objective, ops/reference.py NewtonStateRef docst
                 ~6-10 passes.  Data parallel: ONE all-reduce of 1088 doubles per iteration.
   * ``sgd``     curvature-normalised momentum minibatch SGD: every minibatch strides over the whole
                 shard (row phase b of the pass grid's tile walk) plus 1/nb of the virtual SMOTE
-                picks; epoch 0 on a quarter of the rows, Polyak averaging from the first full epoch;
-                gradient-only passes with fixed-point sums.  One process: the whole schedule is ONE
+                picks; epoch 0 = 4 steps over a quarter of the rows, Polyak averaging from the
+                first full epoch; gradient-only passes with fixed-point sums.  One process: the whole schedule is ONE
                 persistent launch (grid barrier per step); data parallel: pass -> one all-reduce of
                 36 int64 -> update per step.
 
@@ -677,21 +677,19 @@ def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit
 # steps for 1e-3 (the curvature falls ~5x between w = 0 and the optimum).
 SGD_BATCHES = 8
 SGD_EPOCHS = 3
-SGD_LR = (0.4, 0.7, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
-# Per-epoch row sub-sample: epoch 0 visits 1/4 of the rows (its 8 minibatches are every 4th phase
-# of a 32-minibatch grid) -- a growing-batch schedule: the first epoch only has to bring w near the
-# optimum, so it needs no full pass (Smith et al., "Don't decay the learning rate, increase the
-# batch size").  fp64 simulation on the bench distribution (tools/sgd_schedule_lab.py, 16M
-# post-SMOTE rows): (4, 1, 1) with steps (0.4, 0.7, 0.8) ends at epoch gradient 2.2e-4 and 1.3e-4
-# relative above the Newton objective, streaming 2.25 epochs instead of 3 (3 full epochs with
-# (0.4, 0.6, 0.8): 3.6e-4, 4.2e-5).  A sub-sampled epoch never decides convergence.
+SGD_LR = (0.6, 0.8, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
+# Per-epoch row sub-sample: epoch 0 visits 1/4 of the rows -- a growing-batch schedule: the first
+# epoch only has to bring w near the optimum, so it needs no full pass (Smith et al., "Don't decay
+# the learning rate, increase the batch size").  A sub-sampled epoch never decides convergence.
 SGD_SUB = (4, 1, 1)
-# Per-epoch minibatch counts (the kernel supports fewer steps in an epoch; tests cover it).  The
-# default keeps 8 everywhere: 4 epoch-0 steps over an eighth of the rows ("sub8nb4_avg1" in
-# tools/sgd_schedule_lab.py) saves ~35 us of passes, but over five data seeds at 16M post-SMOTE rows
-# it ends the nominal epochs at 4.7-8.9e-4 (one seed needed the extra epoch, +170 us), where the
-# 8-step schedule ends at 4.5-7.2e-4 on all five without it.
-SGD_EPOCH_BATCHES = (8, 8, 8)
+# Per-epoch minibatch counts: epoch 0 takes 4 steps of 1/16 of the rows (every 4th phase of a
+# 16-minibatch grid), the full epochs 8.  fp64 simulation on the bench distribution
+# (tools/sgd_schedule_lab.py "s4n4_d", 16M post-SMOTE rows, seven data seeds): every seed converges
+# in the nominal 3 epochs with the epoch gradient at 2.6-5.5e-4 and the objective <= 2.0e-4 above
+# Newton's.  The previous 8-step epoch 0 at c = 0.4 ("sub4_avg2") ended at 4.5-9.8e-4 (one seed
+# 2% under tol) with 4 more grid barriers; 4 steps over an eighth of the rows, or 4- and 6-step full
+# epochs, ran the extra epoch on some seeds.
+SGD_EPOCH_BATCHES = (4, 8, 8)
 # Epochs past SGD_EPOCHS that run only while the fit has not converged (the device `done` flag makes
 # them no-ops otherwise; the persistent launch leaves its loop).  Each is averaged like the last
 # nominal epoch, starting from that epoch's averaged iterate.  fp8 rows carry ~6% quantisation

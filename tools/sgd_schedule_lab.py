@@ -195,6 +195,14 @@ def main():
         "full4_avg1_b": (8, [(0.4, 4), (0.9, 1, 4), (1.0, 1, 4), (1.0, 1, 4)], 1),
         "sub6_full6": (8, [(0.4, 4, 6), (0.7, 1, 6), (0.8, 1, 6), (0.8, 1, 6)], 1),
         "full8_6": (8, [(0.4, 4), (0.7, 1), (0.8, 1, 6), (0.8, 1, 6)], 1),
+        "s4n4_a": (8, [(0.5, 4, 4), (0.6, 1), (0.8, 1), (0.8, 1)], 1),
+        "s4n4_b": (8, [(0.6, 4, 4), (0.6, 1), (0.8, 1), (0.8, 1)], 1),
+        "s4n4_c": (8, [(0.7, 4, 4), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "s4n4_d": (8, [(0.6, 4, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "s4n4_e": (8, [(0.6, 4, 4), (0.7, 1), (0.7, 1), (0.7, 1)], 1),
+        "s4n4_f": (8, [(0.6, 4, 4), (0.7, 1), (0.9, 1), (0.9, 1)], 1),
+        "s4n6_a": (8, [(0.5, 4, 6), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "s4n6_b": (8, [(0.4, 4, 6), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1": (8, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1_b": (8, [(0.5, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub4x2_avg2": (8, [(0.4, 4), (0.5, 2), (0.8, 1), (0.8, 1)], 2),
