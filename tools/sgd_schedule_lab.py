@@ -203,6 +203,12 @@ def main():
         "s4n4_f": (8, [(0.6, 4, 4), (0.7, 1), (0.9, 1), (0.9, 1)], 1),
         "s4n6_a": (8, [(0.5, 4, 6), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "s4n6_b": (8, [(0.4, 4, 6), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
+        "d86": (8, [(0.6, 4, 4), (0.8, 1, 8), (0.8, 1, 6), (0.8, 1, 6)], 1),
+        "d66": (8, [(0.6, 4, 4), (0.8, 1, 6), (0.8, 1, 6), (0.8, 1, 6)], 1),
+        "d3": (8, [(0.6, 4, 3), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "d2": (8, [(0.7, 4, 2), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "d48": (8, [(0.6, 8, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
+        "d816": (8, [(0.6, 16, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1": (8, [(0.4, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub8_avg1_b": (8, [(0.5, 8), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "sub4x2_avg2": (8, [(0.4, 4), (0.5, 2), (0.8, 1), (0.8, 1)], 2),
