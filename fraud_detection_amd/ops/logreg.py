@@ -683,13 +683,14 @@ SGD_LR = (0.6, 0.8, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 
 # the learning rate, increase the batch size").  A sub-sampled epoch never decides convergence.
 SGD_SUB = (4, 1, 1)
 # Per-epoch minibatch counts: epoch 0 takes 4 steps of 1/16 of the rows (every 4th phase of a
-# 16-minibatch grid), the full epochs 8.  fp64 simulation on the bench distribution
-# (tools/sgd_schedule_lab.py "s4n4_d", 16M post-SMOTE rows, seven data seeds): every seed converges
-# in the nominal 3 epochs with the epoch gradient at 2.6-5.5e-4 and the objective <= 2.0e-4 above
-# Newton's.  The previous 8-step epoch 0 at c = 0.4 ("sub4_avg2") ended at 4.5-9.8e-4 (one seed
-# 2% under tol) with 4 more grid barriers; 4 steps over an eighth of the rows, or 4- and 6-step full
-# epochs, ran the extra epoch on some seeds.
-SGD_EPOCH_BATCHES = (4, 8, 8)
+# 16-minibatch grid), the full epochs 6 steps of 1/6.  fp64 simulation on the bench distribution
+# (tools/sgd_schedule_lab.py "d66", 16M post-SMOTE rows, seven data seeds): every seed converges in
+# the nominal 3 epochs (epoch gradient 3.8-8.4e-4, objective <= 4e-4 above Newton's); on the GPU at
+# the bench shape bf16 and fp8 both end at 5.6e-4, the same as with 8-step full epochs, in 16 steps
+# instead of 20: 1.050 vs 1.111 ms per bf16 fit, 0.997 vs 1.066 fp8 (profiles/r5_zz,
+# tools/sgd_schedule_ab.py).  8 steps at c = 0.4 in epoch 0 ("sub4_avg2") ended at 4.5-9.8e-4 with 8
+# more grid barriers; 4 steps over an eighth of the rows ran the extra epoch on some seeds.
+SGD_EPOCH_BATCHES = (4, 6, 6)
 # Epochs past SGD_EPOCHS that run only while the fit has not converged (the device `done` flag makes
 # them no-ops otherwise; the persistent launch leaves its loop).  Each is averaged like the last
 # nominal epoch, starting from that epoch's averaged iterate.  fp8 rows carry ~6% quantisation
