@@ -325,7 +325,8 @@ def _variants(args, X, y, Xt, yt, dev, comm, scope) -> dict:
             f = r.fit
             mine = pipe.training_objective(r)
             opt = pipe.training_objective(r, w=newton_w[kw["storage"]])
-            o.update(steps=int(f.n_iter), epochs=pipe.cfg.sgd_epochs, minibatches_per_epoch=pipe.cfg.sgd_batches,
+            o.update(steps=int(f.n_iter), epochs=pipe.cfg.sgd_epochs,
+                     minibatches_per_epoch=[int(v) for v in pipe.cfg.sgd_epoch_batches],
                      converged=bool(f.converged), epoch_grad_max=float(f.grad_max), tol=pipe.cfg.sgd_tol,
                      objective=round(mine["objective"], 9), newton_objective=round(opt["objective"], 9),
                      objective_rel_gap_vs_newton=float((mine["objective"] - opt["objective"]) / opt["objective"]),
