@@ -1,19 +1,26 @@
 #!/usr/bin/env python3
-"""Flagship benchmark (BASELINE.json config 3, scaled by data parallelism for configs 4/5).
+"""Flagship benchmark: BASELINE.json config 3 ("SMOTE k-NN + logistic SGD HIP train on one MI355X,
+10M x 30 bf16, AUC >= 0.95"), scaled by data parallelism for configs 4/5.
 
 One step = one complete training fit on every rank's shard, exactly the hot path of the
 reference's train_model.py re-done on MI355X kernels:
-    StandardScaler fit (K1, all-reduce) -> standardize/pad/cast to bf16 (K2)
-    -> SMOTE: minority all-gather, MFMA k-NN (K8), Philox interpolation (K9)
-    -> LogisticRegression Newton fit to convergence (K4: fused grad/loss/MFMA-Hessian pass,
-       one 1088-double all-reduce per iteration, on-device Cholesky step), random-init weights.
+    StandardScaler fit (K1, all-reduce) -> standardize/pad/cast to bf16 (K2, the same pass)
+    -> SMOTE: minority all-gather, MFMA k-NN (K8), Philox interpolation folded into the passes (K9)
+    -> LogisticRegression (C=1) by minibatch SGD to convergence (K4, the default --solver sgd:
+       3 epochs of 4 / 6 / 6 minibatches, curvature-normalised heavy-ball steps, Polyak averaging,
+       device-side convergence test on the epoch gradient, tol 1e-3; one persistent launch with a
+       grid barrier per step on one GPU, one int64 all-reduce per step under DP), random-init weights.
+    --solver newton: the same pipeline with the Newton fit (fused grad/loss/MFMA-Hessian pass, one
+       1088-double all-reduce per iteration, on-device Cholesky) -- reported as an extra otherwise.
 Weak scaling: every GPU owns ``--rows-per-gpu`` raw rows (80% train / 20% test, stratified by
 construction), credit_card-shaped synthetic data (30 features, 0.17% fraud, Bayes AUC 0.970).
 
 value = post-SMOTE training rows fitted per second, whole job (sum over ranks / slowest rank's
 time).  Baseline = 3.50 M rows/s: sklearn lbfgs fit alone on the 10M-row post-SMOTE set
 (our step additionally includes the scaler and SMOTE work).  After timing, the
-test AUC (exact, K10) and the LinearSHAP / KernelSHAP throughputs are reported as extra fields.
+test AUC (exact, K10), the SGD fit's convergence state and objective against the Newton optimum on
+the same training set, the other solver / row formats, and the LinearSHAP / KernelSHAP
+throughputs are reported as extra fields.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -43,7 +50,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rows-per-gpu", type=int, default=10_000_000)
-    ap.add_argument("--solver", default="newton", choices=["newton", "sgd"])
+    ap.add_argument("--solver", default="sgd", choices=["newton", "sgd"],
+                    help="sgd: config 3's solver (the headline); newton: the Newton fit")
     ap.add_argument("--storage", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--smote-scope", default="auto", choices=["auto", "global", "shard"],
                     help="SMOTE under DP: global = exactly the single-process SMOTE, the reference's "
@@ -194,6 +202,8 @@ def main():
         extras["confusion"] = {k: ev[k] for k in ("tn", "fp", "fn", "tp")}
         extras["newton_iters" if args.solver == "newton" else "sgd_steps"] = res.fit.n_iter
         extras["fit_converged"] = res.fit.converged
+        if args.solver == "sgd" and comm is None:
+            extras["sgd"] = _sgd_details(pipe, res, X, y, scope, args.storage)
         prof = pipe.fit(X, y, profile=True)
         extras["phase_ms"] = {k: round(v * 1000, 3) for k, v in prof.timings.items()}
         extras.update(_shap_throughput(res, dev, comm))
@@ -294,15 +304,15 @@ def _timed_fits(pipe, X, y, dev, comm, reps=3, warmup=1):
 
 
 def _variants(args, X, y, Xt, yt, dev, comm, scope) -> dict:
-    """Config 3 names the SGD solver and config 5 fp8 rows: ms/fit + AUC of those variants in the
-    same run (the headline step above is the bf16 Newton fit)."""
+    """The other solver and row formats (config 5 names fp8 rows): ms/fit + AUC of each variant in
+    the same run (the headline step above is config 3's bf16 SGD fit by default)."""
     from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig, evaluate
 
     out = {}
     # *_stored_smote: the fit with its SMOTE rows written and streamed (the default folds them into
     # the passes instead: TrainConfig.virtual_smote)
-    newton_w = {}
-    for name, kw in (("sgd_bf16", dict(solver="sgd", storage="bf16")), ("newton_fp8", dict(solver="newton", storage="fp8")),
+    for name, kw in (("newton_bf16", dict(solver="newton", storage="bf16")),
+                     ("sgd_bf16", dict(solver="sgd", storage="bf16")), ("newton_fp8", dict(solver="newton", storage="fp8")),
                      ("newton_bf16_stored_smote", dict(solver="newton", storage="bf16", virtual_smote=False)),
                      ("newton_fp8_stored_smote", dict(solver="newton", storage="fp8", virtual_smote=False)),
                      ("sgd_fp8", dict(solver="sgd", storage="fp8"))):
@@ -316,23 +326,33 @@ def _variants(args, X, y, Xt, yt, dev, comm, scope) -> dict:
              "rows_per_sec": round(rows / dt, 1),
              "auc": round(evaluate(r, Xt, yt, comm)["auc"], 6)}
         if kw["solver"] == "sgd" and comm is None:
-            # config 3's solver: its device convergence state and its exact training objective
-            # against the Newton optimum on the SAME training set (same rows and SMOTE samples)
-            if kw["storage"] not in newton_w:
-                npipe = DevicePipeline(TrainConfig(seed=42, smote_scope=scope, storage=kw["storage"],
-                                                   deferred_check=False), comm)
-                newton_w[kw["storage"]] = npipe.fit(X, y).w
-            f = r.fit
-            mine = pipe.training_objective(r)
-            opt = pipe.training_objective(r, w=newton_w[kw["storage"]])
-            o.update(steps=int(f.n_iter), epochs=pipe.cfg.sgd_epochs,
-                     minibatches_per_epoch=[int(v) for v in pipe.cfg.sgd_epoch_batches],
-                     converged=bool(f.converged), epoch_grad_max=float(f.grad_max), tol=pipe.cfg.sgd_tol,
-                     objective=round(mine["objective"], 9), newton_objective=round(opt["objective"], 9),
-                     objective_rel_gap_vs_newton=float((mine["objective"] - opt["objective"]) / opt["objective"]),
-                     virtual_smote=pipe._virtual is not None)
+            o.update(_sgd_details(pipe, r, X, y, scope, kw["storage"]))
         out[name] = o
     return out
+
+
+_NEWTON_W = {}
+
+
+def _sgd_details(pipe, r, X, y, scope, storage) -> dict:
+    """Config 3's solver: its device convergence state and its exact training objective against the
+    Newton optimum on the SAME training set (same rows and SMOTE samples).  Call right after the
+    fit (the objective is evaluated over the pipeline's current training buffer)."""
+    from fraud_detection_amd.models.pipeline import DevicePipeline, TrainConfig
+
+    if storage not in _NEWTON_W:
+        npipe = DevicePipeline(TrainConfig(seed=42, smote_scope=scope, storage=storage, deferred_check=False))
+        _NEWTON_W[storage] = npipe.fit(X, y).w
+    f = r.fit
+    mine = pipe.training_objective(r)
+    opt = pipe.training_objective(r, w=_NEWTON_W[storage])
+    return dict(steps=int(f.n_iter), epochs=pipe.cfg.sgd_epochs,
+                minibatches_per_epoch=[int(v) for v in pipe.cfg.sgd_epoch_batches],
+                converged=bool(f.converged), epoch_grad_max=float(f.grad_max), tol=pipe.cfg.sgd_tol,
+                recovered_launch=bool(getattr(f, "recovered", False)),
+                objective=round(mine["objective"], 9), newton_objective=round(opt["objective"], 9),
+                objective_rel_gap_vs_newton=float((mine["objective"] - opt["objective"]) / opt["objective"]),
+                virtual_smote=pipe._virtual is not None)
 
 
 def _end_to_end(X, y, Xt, yt, cfg, dev, comm) -> dict:

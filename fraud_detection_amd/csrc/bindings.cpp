@@ -670,7 +670,8 @@ PYBIND11_MODULE(_fdx_native, m) {
                                     int64_t hole_len, u ws, u state, u w32, u done, u aff, int d, double C, double mom,
                                     int fi, double tol, int nb, int epochs, int avg_from, int serpentine,
                                     std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps,
-                                    std::vector<int> subs, std::vector<int> nbs) {
+                                    std::vector<int> subs, std::vector<int> nbs, int fault_test,
+                                    unsigned spin_limit) -> int {
     if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
     if ((int)subs.size() < epochs) throw std::runtime_error("sgd_persist: one sub-sample factor per epoch");
     if ((int)nbs.size() < epochs) throw std::runtime_error("sgd_persist: one minibatch count per epoch");
@@ -706,8 +707,18 @@ PYBIND11_MODULE(_fdx_native, m) {
     a.s1 = s1;
     a.Gw = Gw;
     a.stamps = P<unsigned long long>(stamps);
-    fdx::launch_sgd_persist(P<const void>(X), fp8, x_scale, end, P<const float>(cw), parents ? &v : nullptr, h, a, S(s));
-  });
+    a.fault_test = fault_test;
+    if (spin_limit > 0) a.spin_limit = spin_limit;
+    // 0: enqueued; 1: the cooperative launch refused the grid (the caller launches per step)
+    return fdx::launch_sgd_persist(P<const void>(X), fp8, x_scale, end, P<const float>(cw), parents ? &v : nullptr, h,
+                                   a, S(s));
+  }, py::arg("X"), py::arg("fp8"), py::arg("x_scale"), py::arg("end"), py::arg("cw"), py::arg("parents"),
+     py::arg("nbr"), py::arg("lam"), py::arg("off"), py::arg("cnt"), py::arg("n_real"), py::arg("q_offset"),
+     py::arg("mq"), py::arg("k"), py::arg("hole_at"), py::arg("hole_len"), py::arg("ws"), py::arg("state"),
+     py::arg("w32"), py::arg("done"), py::arg("aff"), py::arg("d"), py::arg("C"), py::arg("mom"), py::arg("fi"),
+     py::arg("tol"), py::arg("nb"), py::arg("epochs"), py::arg("avg_from"), py::arg("serpentine"), py::arg("lrs"),
+     py::arg("s0"), py::arg("s1"), py::arg("Gw"), py::arg("s"), py::arg("stamps"), py::arg("subs"), py::arg("nbs"),
+     py::arg("fault_test") = 0, py::arg("spin_limit") = 0u);
   m.def("sgd_persist_blocks", [](int grid_blocks) { return fdx::sgd_persist_blocks(grid_blocks); });
   m.def("sgd_full_blocks", []() { return fdx::sgd_full_blocks(); });
   m.attr("SGD_PERSIST_WORDS") = fdx::kSgdPersistWords;

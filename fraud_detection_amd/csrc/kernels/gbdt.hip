@@ -251,17 +251,30 @@ constexpr int kHistBatchRot = 4;  // rows in flight per thread
 // SPLIT (lab variant 2): g and h in two int32 sub-histograms, two ds_add_u32 per (row, feature)
 // instead of one 64-bit packed add -- a wave's 64 lanes then spread over 64 single-dword banks
 // rather than 32 bank pairs.  Same sums (int32 exact within a flush), same flush layout.
-enum HistVariant : int { kHistLockstep = 0, kHistRot = 1, kHistSplit = 2 };
+// LANE (variant 3, the default): EIGHT lanes per row instead of one -- lane j of a row owns its
+// bins dword j (features 4j .. 4j + 3), so a wave instruction adds 8 rows x 8 features, and every
+// lane of a 16-lane group (and of a 32-lane group) adds into a DIFFERENT bank pair by construction.
+// Words are bin-major, [bin][slot] with 32 slots, slot(f) = 8 (f & 3) + (f >> 2), i.e. feature
+// 4j + kk at slot 8 kk + j (bank pair = slot mod 16 with 32 banks, mod 32 with 64).  At step k the
+// row r-th of a 32-lane group (r = 0..3) adds its byte kk = k ^ r: rows 0..3 take the four kk, so
+// the 32 lanes hit slots 8 kk + j = all 32 residues -- no bank conflict in any lane grouping, and
+// no same-address collision (r5 PMC of the lockstep form: 8.4 bank-conflict + 2.6 address-conflict
+// cycles per LDS instruction, 64 lanes adding random bins of ONE feature).  One row's (g, h) word is
+// read by its 8 lanes (one broadcast fetch), its 32 bin bytes as 8 coalesced dwords.  Integer adds
+// into the same packed words: every histogram -- and tree -- bit is unchanged.
+constexpr int kHistWordsLane = kGBBins * 32;  // 8192 u64 = 64 KiB (two 1024-thread blocks per CU fit)
+constexpr int kHistBatchLane = 4;             // row groups in flight per lane
+enum HistVariant : int { kHistLockstep = 0, kHistRot = 1, kHistSplit = 2, kHistLane = 3 };
 template <int VAR>
 __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
                                                                            // (ROT: 1 block/CU, <= 128 VGPRs)
     const uint8_t* __restrict__ bins, const uint32_t* __restrict__ gh, const int* __restrict__ ridx,
     const int64_t* __restrict__ seg, const int64_t* __restrict__ gcnt, int level, int d,
     long long* __restrict__ slots, int64_t flush_rows, int64_t hole_at, int64_t hole_len) {
-  constexpr bool ROT = VAR == kHistRot, SPLIT = VAR == kHistSplit;
+  constexpr bool ROT = VAR == kHistRot, SPLIT = VAR == kHistSplit, LANE = VAR == kHistLane;
   constexpr int kStride = ROT ? kHistStrideRot : kGBBins;
-  constexpr int kBatch = ROT ? kHistBatchRot : kHistBatch;
-  __shared__ unsigned long long sh[ROT ? kHistWordsRot : kHistWords];
+  constexpr int kBatch = ROT ? kHistBatchRot : (LANE ? kHistBatchLane : kHistBatch);
+  __shared__ unsigned long long sh[ROT ? kHistWordsRot : (LANE ? kHistWordsLane : kHistWords)];
   int* const shg = reinterpret_cast<int*>(sh);  // SPLIT: g at [f * 256 + b], h kHistWords ints later
   int* const shh = shg + kHistWords;
   __shared__ LevelNodes lv;
@@ -290,12 +303,16 @@ __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hi
     long long* dst = slots + (int64_t)my_slot * kHistEntries;
     for (int64_t c0 = lo; c0 < hi; c0 += flush_rows) {
       const int64_t c1 = min(hi, c0 + flush_rows);
-      for (int i = threadIdx.x; i < nw; i += kHistThreads) {
-        if constexpr (SPLIT) {
-          shg[i] = 0;
-          shh[i] = 0;
-        } else {
-          sh[ROT ? (i >> 8) * kStride + (i & 255) : i] = 0ull;
+      if constexpr (LANE) {
+        for (int i = threadIdx.x; i < kHistWordsLane; i += kHistThreads) sh[i] = 0ull;
+      } else {
+        for (int i = threadIdx.x; i < nw; i += kHistThreads) {
+          if constexpr (SPLIT) {
+            shg[i] = 0;
+            shh[i] = 0;
+          } else {
+            sh[ROT ? (i >> 8) * kStride + (i & 255) : i] = 0ull;
+          }
         }
       }
       __syncthreads();
@@ -303,6 +320,38 @@ __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hi
       // are loaded before the first atomic.  Level 0 reads rows in order (ridx is the identity
       // after the round init).
       const int64_t pbase = sb - (off - sc);
+      if constexpr (LANE) {
+        const int lane = lane_id();
+        const int j = lane & 7, r4 = (lane >> 3) & 3;
+        constexpr int kRowsPerIter = kHistThreads / 8;  // 128 rows per block per batch slot
+        unsigned long long* const hs = sh + j;          // slot 8 kk + j of bin b: hs[b * 32 + 8 kk]
+        for (int64_t v0 = c0 + (threadIdx.x >> 3); v0 < c1; v0 += (int64_t)kRowsPerIter * kBatch) {
+          int64_t rows[kBatch];
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u) {
+            const int64_t v = v0 + (int64_t)u * kRowsPerIter;
+            rows[u] = v < c1 ? (level == 0 ? hole_row(pbase + v, hole_at, hole_len) : (int64_t)ridx[pbase + v]) : -1;
+          }
+          uint32_t bw[kBatch], gw[kBatch];
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u) {
+            const int64_t row = rows[u] < 0 ? 0 : rows[u];
+            bw[u] = reinterpret_cast<const uint32_t*>(bins + row * kGBRowBytes)[j];
+            gw[u] = gh[row];
+          }
+#pragma unroll
+          for (int u = 0; u < kBatch; ++u) {
+            if (rows[u] < 0) continue;
+            const unsigned long long pk =
+                ((unsigned long long)(gw[u] >> 16) << 32) + (unsigned long long)(long long)(int16_t)(gw[u] & 0xffffu);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const int kk = k ^ r4;
+              if (4 * j + kk < d) atomicAdd(hs + ((bw[u] >> (8 * kk)) & 0xffu) * 32 + 8 * kk, pk);
+            }
+          }
+        }
+      } else
       for (int64_t v0 = c0 + threadIdx.x; v0 < c1; v0 += kHistThreads * kBatch) {
         int64_t rows[kBatch];
 #pragma unroll
@@ -386,6 +435,11 @@ __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hi
         if constexpr (SPLIT) {
           sg = shg[i];
           sgh = shh[i];
+        } else if constexpr (LANE) {
+          const int f = i >> 8, b = i & 255;
+          const unsigned long long x = sh[b * 32 + 8 * (f & 3) + (f >> 2)];
+          sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
+          sgh = (long long)(x - (unsigned long long)sg) >> 32;
         } else {
           const unsigned long long x = sh[ROT ? (i >> 8) * kStride + (i & 255) : i];
           sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
@@ -1004,7 +1058,7 @@ int64_t gbdt_hist_slot_words() { return (int64_t)(gbdt_hist_blocks() + 2 * kGBMa
 
 static int g_hist_variant = -1;  // set_gbdt_hist_variant (tests / labs); -1: the environment's choice
 void set_gbdt_hist_variant(int v) {
-  if (v < -1 || v > 2) throw std::invalid_argument("gbdt hist variant: -1 (env), 0 lockstep, 1 rot, 2 split");
+  if (v < -1 || v > 3) throw std::invalid_argument("gbdt hist variant: -1 (env), 0 lockstep, 1 rot, 2 split, 3 lane");
   g_hist_variant = v;
 }
 
@@ -1019,17 +1073,20 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   // at most blocks + nodes pairs)
   if (level < 0 || (1 << level) > kGBMaxNodes + 1) throw std::runtime_error("gbdt_hist: level out of range");
   const int nb = gbdt_hist_blocks();
-  static const int env_var = [] {  // lab switch FDX_GBDT_HIST_VAR: 1 rotated features, 2 split g/h adds
+  static const int env_var = [] {  // lab switch FDX_GBDT_HIST_VAR: 0 lockstep, 1 rotated, 2 split, 3 lane (default)
     const char* e = std::getenv("FDX_GBDT_HIST_VAR");
     const char* r = std::getenv("FDX_GBDT_HIST_ROT");  // older spelling of variant 1
-    if (e != nullptr && (e[0] == '1' || e[0] == '2')) return e[0] - '0';
-    return (r != nullptr && r[0] == '1') ? 1 : 0;
+    if (e != nullptr && e[0] >= '0' && e[0] <= '3') return e[0] - '0';
+    return (r != nullptr && r[0] == '1') ? 1 : (int)kHistLane;
   }();
   const int var = g_hist_variant >= 0 ? g_hist_variant : env_var;
   const bool rot = var == kHistRot;
   if (rot)  // one block per CU (its rotation registers): half the blocks of the lockstep form
     gbdt_hist_kernel<kHistRot><<<nb / 2, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
                                                                     flush_rows, hole_at, hole_len);
+  else if (var == kHistLane)
+    gbdt_hist_kernel<kHistLane><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
+                                                                 flush_rows, hole_at, hole_len);
   else if (var == kHistSplit)
     gbdt_hist_kernel<kHistSplit><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
                                                                   flush_rows, hole_at, hole_len);

@@ -212,7 +212,9 @@ void launch_sgd_update_fixed(const long long* sums, double* state, float* w32, i
 // that the persistent launch holds it as one 8-wave block per CU.
 int sgd_full_blocks();
 constexpr int kSgdMaxEpochs = 8;
-constexpr int kSgdPersistWords = 128 + 3 * 32 * 36;  // barrier shards (1 KB) + 3 accumulator sets
+// barrier shards (1 KB) | 3 accumulator sets | fault word | backup of the initial state + weights + done
+// (logreg.hip kWs*: static_assert that it fits)
+constexpr int kSgdPersistWords = 128 + 3 * 32 * 36;
 struct SgdPersistArgs {
   unsigned long long* ws = nullptr;  // [kSgdPersistWords] int64 workspace (zeroed by the launcher)
   double* st = nullptr;
@@ -232,9 +234,13 @@ struct SgdPersistArgs {
   unsigned long long* stamps = nullptr;  // nullable: [steps][3 + 8][blocks] wall_clock64 at pass end,
                                          // barrier exit, update end, then each wave's pass end
                                          // (tools/sgd_stamps.py)
+  unsigned spin_limit = 1u << 20;        // barrier polls before a block declares the grid not resident
+  int fault_test = 0;                    // test knob: barrier s0 unreachable -> the recovery launch runs
 };
-void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
-                        const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream);
+// Returns 0 when enqueued (prep kernel, the persistent launch, its recovery launch); 1 when the
+// cooperative launch refused the grid (nothing enqueued: the caller runs the per-step launches).
+int launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
+                       const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream);
 // blocks of the persistent launch for a per-step grid of `grid_blocks` 256-thread blocks, or 0 when
 // that many 512-thread blocks cannot all be resident (the caller then launches per step)
 int sgd_persist_blocks(int grid_blocks);

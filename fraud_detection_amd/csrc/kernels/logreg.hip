@@ -23,6 +23,9 @@
 // remaining iterations into no-ops once converged.  With data parallelism the reduced 1088-double
 // vector is all-reduced over RCCL between the reduce and the update kernels (parallel/dp.py).
 #include <cstdio>
+#include <cstdlib>
+#include <stdexcept>
+#include <string>
 #include <type_traits>
 
 #include "common.h"
@@ -1445,12 +1448,13 @@ __global__ __launch_bounds__(64) void sgd_update_fixed_kernel(const long long* _
 // ---- persistent SGD: the whole schedule in ONE launch --------------------------------------------
 // The per-step launches pay, per step, a kernel boundary, the grid's fill and drain, and the serial
 // update in the last-arriving block (~14 us of a ~26 us step at the bench shape, profiles/r4_g).
-// Here one 768-thread block per CU runs every step: its 12 waves are waves 12 b .. 12 b + 11 of the
-// per-step grid (bf16_wave_pass / fp8_wave_pass walk the same row and pick tiles), so a step's sums
-// are the per-step launch's sums.  Step t:
-//   pass over minibatch b -> each group of 4 waves (one block of the per-step grid) turns its sums
-//   into 2^-20 fixed point exactly as sgd_fused_tail does -> agent-scope int64 adds into replica
-//   (block mod 32) of accumulator set t mod 3 -> grid barrier -> every block reads the set with
+// Here one 512-thread block (kPersistWaves = 8 waves) per CU runs every step: wave wv of block b is
+// wave wv * B + b of the per-step grid (B = blocks; bf16_wave_pass / fp8_wave_pass walk the same row
+// and pick tiles), so a step's sums are the per-step launch's sums.  Step t:
+//   pass over minibatch b -> every wave's [36] sums in LDS -> the block's LAST wave (kArriveWave)
+//   turns each wave's sums into 2^-20 fixed point exactly as sgd_fused_tail does, adds the block's
+//   total into replica (block mod kPersistReplicas = 16) of accumulator set t mod 3 with
+//   agent-scope int64 atomics, and arrives at the grid barrier -> every block reads the set with
 //   agent-scope loads and applies the SAME update (sgd_apply) to its own LDS copy of the solver
 //   state.  Integer sums are order-free and every block runs the same fp64 code on the same
 //   inputs, so every block holds bitwise the same state -- and bitwise the per-step launches'
@@ -1460,13 +1464,20 @@ __global__ __launch_bounds__(64) void sgd_update_fixed_kernel(const long long* _
 // agent atomic add made after the adding wave's vmcnt(0), the poll a relaxed agent load -- the
 // "8-B agent atomics both sides" form, one workgroup per CU.  Sets rotate over three: set t is read
 // after barrier t; set t + 1 is zeroed by block 0 during step t (after barrier t - 1, when every
-// block has finished reading it as set t - 2; before block 0 arrives at barrier t).  The launcher
-// zeroes the barrier shards and all three sets in front of the launch.  Every wait is bounded: a
-// grid whose blocks are not all resident ends with state[kSgdFault] set instead of hanging.
+// block has finished reading it as set t - 2; before block 0 arrives at barrier t).
+// Residency: the launch goes through hipLaunchCooperativeKernel (it refuses a grid the occupancy
+// query says cannot be co-resident; the caller then launches per step), but co-residency can still
+// fail at run time when another stream or process holds CUs.  So every wait is bounded: a block
+// whose barrier poll times out (or that sees another block's timeout) raises the workspace's fault
+// word and leaves; blocks dispatched after that exit at once; nothing is published from a faulted
+// grid.  The one-block recovery launch queued behind every persistent launch (sgd_recover_kernel)
+// is a no-op unless the fault word is set; then it re-runs the steps from the backup of the
+// initial state (sgd_persist_prep_kernel) with the same per-wave fixed-point sums -- bitwise the fit
+// the persistent launch would have produced, at one CU's speed.
 constexpr int kPersistWaves = 8;
 constexpr int kPersistThreads = kPersistWaves * kWave;
 constexpr int kBarShards = 8, kBarStride = 32;  // arrival shards, one 128-B line each (u32 words)
-enum : int { kSgdFault = 229 };                 // state slot: a grid barrier timed out
+enum : int { kSgdFault = 229 };                 // state slot: 2 = the fit ran on the recovery launch
 // stamps (tools/sgd_stamps.py): [step][kStampRows][block] wall_clock64 -- pass end, barrier exit,
 // update end, then every wave's own pass end
 constexpr int kStampRows = 3 + kPersistWaves;
@@ -1481,6 +1492,18 @@ constexpr int kArriveWave = kPersistWaves - 1;
 // Every block folds all of them after the barrier, so fewer replicas is fewer loads per update.
 constexpr int kPersistReplicas = 16;
 constexpr int kPersistAccWords = kPersistReplicas * 36;
+// Workspace layout (int64 words, launchers.h kSgdPersistWords): barrier shards | 3 accumulator sets
+// | fault word | backup of the initial state [kStateSize], weights [16 words = 32 floats], done.
+enum : int {
+  kWsAcc = 128,
+  kWsFault = kWsAcc + 3 * kPersistAccWords,
+  kWsBackup = kWsFault + 8,  // zeroed per launch: [0, kWsBackup)
+  kWsBackupW = kWsBackup + kStateSize,
+  kWsBackupDone = kWsBackupW + 16,
+  kWsEnd = kWsBackupDone + 1
+};
+static_assert(kWsEnd <= kSgdPersistWords, "launchers.h kSgdPersistWords too small for the persistent workspace");
+static_assert(kBarShards * kBarStride <= 2 * kWsAcc, "barrier shards overlap the accumulator sets");
 // Template knobs: LAMS = lambdas in flight per lane in a pick (integer sums: any grouping gives the
 // same bits); PF = what is loaded for the next step before the barrier: 0 nothing; 1 the first pick
 // tile's inputs and the first stored tile into registers; 2 the pick inputs + an L2 touch of the
@@ -1488,8 +1511,11 @@ constexpr int kPersistAccWords = kPersistReplicas * 36;
 // kDepth).  LAMS 16/32 x PF 0-3 all ran within 735-778 us per fit (profiles/r5_e/sgd_lab.json);
 // FDX_SGD_PERSIST_CFG=1 (lab) selects DEPTH 1, the round-4 stored-tile pipeline.
 
-// Wave 0 of a block: arrive at the grid barrier and wait until `target` arrivals in all.
-__device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned target, int lane) {
+// The arriving wave of a block: arrive at the grid barrier and wait until `target` arrivals in all.
+// false: the wait timed out (spin_limit polls) or another block had already given up (fault word);
+// the fault word is raised either way.
+__device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned target, int lane, unsigned int* fault,
+                                                unsigned spin_limit) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's accumulator adds have landed
   if (lane == 0)
     __hip_atomic_fetch_add(bar + (blockIdx.x % kBarShards) * kBarStride, 1u, __ATOMIC_RELAXED,
@@ -1497,14 +1523,114 @@ __device__ __forceinline__ bool persist_barrier(unsigned int* bar, unsigned targ
   for (unsigned spins = 0;; ++spins) {
     int v = lane < kBarShards ? (int)__hip_atomic_load(bar + lane * kBarStride, __ATOMIC_RELAXED,
                                                        __HIP_MEMORY_SCOPE_AGENT) : 0;
+    const int f = lane == kBarShards ? (int)__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
     v += __shfl_xor(v, 1, kWave);
     v += __shfl_xor(v, 2, kWave);
     v += __shfl_xor(v, 4, kWave);
     v = __shfl(v, 0, kWave);
     if ((unsigned)v >= target) return true;
-    if (spins > (1u << 21)) return false;  // ~2 s of polls: not every block is resident
+    if (__shfl(f, kBarShards, kWave) != 0 || spins > spin_limit) {  // not every block is resident
+      if (lane == 0) __hip_atomic_store(fault, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
   }
 }
+
+// One wave's share of a step's pass -- wave `wave` of the per-step grid of Gw waves, minibatch b of
+// a grid of rsub -- into red[wv][0..35] (gradient in row units | loss | weight | 0 | curvature).  The
+// persistent launch (with the next tiles prefetched across its barrier) and the one-block recovery
+// launch (a loop over the grid's waves) run the same code, so their per-wave sums are equal.
+template <bool FP8, bool VIRT, int kLams, int kPreLams, int kDepth>
+__device__ __forceinline__ void persist_wave_sums(const void* __restrict__ X, int64_t row_end, float x_scale,
+                                                  float inv_s, float cw0, float cw1, const float* wsh,
+                                                  const SmoteView& sv, const RowHole& hole, int64_t wave, int64_t Gw,
+                                                  bool active, int rsub, int b, float (*red)[36], int wv, int lane,
+                                                  const uint4 (&pre)[4], bool have_pre,
+                                                  const PickIn<4, kPreLams>& ppre, bool have_ppre) {
+  constexpr int d_feat = 30;
+  float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f, dacc = 0.0f;
+  f32x16_t hacc = {};
+  if constexpr (FP8) {
+    const int q = lane & 1;
+    f32x2_t wl[8], g[8];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      wl[p] = f32x2_t{wsh[16 * q + 2 * p], wsh[16 * q + 2 * p + 1]};
+      g[p] = f32x2_t{0.0f, 0.0f};
+    }
+    if (active)
+      fp8_wave_pass<false, VIRT, true, kLams, kPreLams>(static_cast<const uint8_t*>(X), 0, row_end, wl, wsh, x_scale,
+                                                        cw0, cw1, 1, rsub, b, sv, hole, wave, Gw, nullptr, g, lacc,
+                                                        wacc, whacc, dacc, hacc, pre, have_pre, ppre, have_ppre);
+    float gs[16];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int col = 16 * q + 2 * p + e;
+        gs[2 * p + e] = strided_sum<2>(g[p][e]) * (col < d_feat ? inv_s : 1.0f);
+      }
+    }
+    if (lane < 2) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) red[wv][16 * lane + j] = gs[j];
+    }
+  } else {
+    const int q = lane & 3;
+    float wl[8], g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      wl[j] = wsh[q * 8 + j];
+      g[j] = 0.0f;
+    }
+    if (active)
+      bf16_wave_pass<false, VIRT, true, kLams, kPreLams, kDepth>(X, 0, row_end, wl, cw0, cw1, 1, rsub, b, sv, hole,
+                                                                 wave, Gw, nullptr, g, lacc, wacc, whacc, dacc, hacc,
+                                                                 pre, have_pre, ppre, have_ppre);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
+    if (lane < 4) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) red[wv][8 * lane + j] = g[j];
+    }
+  }
+  lacc = wave_sum(lacc);
+  wacc = wave_sum(wacc);
+  dacc = wave_sum(dacc);
+  if (lane == 0) {
+    red[wv][32] = lacc;
+    red[wv][33] = wacc;
+    red[wv][34] = 0.0f;
+    red[wv][35] = dacc;
+  }
+}
+
+// Step st of the schedule -> (epoch, position in it, minibatch phase, grid of the epoch's minibatches):
+// an epoch with sub-sample s visits every s-th phase of a grid of nbe * s minibatches.
+struct PersistStep {
+  int ep, pos, phase, rsub;
+  __device__ __forceinline__ PersistStep(const SgdPersistArgs& P, int st) {
+    int e = 0;
+    while (e + 1 < P.epochs && st >= P.estart[e + 1]) ++e;
+    ep = e;
+    pos = st - P.estart[e];
+    phase = ((P.serpentine && (e & 1)) ? P.nbe[e] - 1 - pos : pos) * P.sub[e];
+    rsub = P.nbe[e] * P.sub[e];
+  }
+  __device__ __forceinline__ SgdArgs args(const SgdPersistArgs& P) const {
+    SgdArgs a;
+    a.d = P.d;
+    a.C = P.C;
+    a.c = P.lr[ep];
+    a.momentum = P.momentum;
+    a.fit_intercept = P.fit_intercept;
+    a.nb = rsub;  // the minibatch estimates the epoch's weight as rsub x its own
+    a.avg = ep >= P.avg_from;
+    a.epoch_end = pos == P.nbe[ep] - 1;
+    a.tol = P.sub[ep] > 1 ? -1.0 : P.tol;  // a sub-sampled epoch never decides convergence
+    return a;
+  }
+};
 
 template <bool FP8, bool VIRT, int kPersistLams = 16, int kPersistPrefetch = 2, int kPersistDepth = 2>
 __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const void* __restrict__ X,
@@ -1522,22 +1648,25 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   __shared__ double saff[64];  // the affine map, read from LDS by every step's reduce and update
   const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
   constexpr int d_feat = 30;
+  unsigned int* bar = reinterpret_cast<unsigned int*>(P.ws);
+  unsigned long long* accs = P.ws + kWsAcc;
+  unsigned int* fault = reinterpret_cast<unsigned int*>(P.ws + kWsFault);
+  if (t == 0) {  // dispatched after another block gave up: leave at once (nothing to wait for)
+    s_done = *P.done;
+    s_ok = __hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u;
+  }
   if (P.aff != nullptr && t < 64) saff[t] = P.aff[t];
   const double* affl = P.aff != nullptr ? saff : nullptr;
   const float inv_s = FP8 ? 1.0f / x_scale : 1.0f;
-  unsigned int* bar = reinterpret_cast<unsigned int*>(P.ws);
-  unsigned long long* accs = P.ws + 128;
   for (int e = t; e < kStateSize; e += kPersistThreads) sst[e] = P.st[e];
   if (t < 32) {
     const float w = P.w32[t];
     wnew[t] = w;
     wsh[t] = t == kLabelCol ? 0.0f : w * ((FP8 && t < d_feat) ? inv_s : 1.0f);
   }
-  if (t == 0) {
-    s_done = *P.done;
-    s_ok = 1;
-  }
   __syncthreads();
+  if (!s_ok) return;  // uniform in the block
+  if (t == 0) sst[kSgdFault] = 0.0;
   const float cw0 = class_w[0], cw1 = class_w[1];
   // wave wv of block b is wave wv * B + b of the per-step grid: the waves that carry the pick tiles
   // (the low wave indices) spread over every CU instead of filling the first ones
@@ -1553,34 +1682,20 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   const int64_t ntile = (npick + 15) >> 4;
   unsigned touch = 0;  // FDX_PERSIST_PREFETCH 2: the dummy destination of the L2 touch loads
   unsigned arrivals = 0;
-  // an epoch with sub-sample s visits every s-th phase of a grid of nb * s minibatches
-  // per-epoch minibatch counts: step st is minibatch st - estart[ep] of epoch ep
-  auto ep_of = [&](int st) {
-    int e = 0;
-    while (e + 1 < P.epochs && st >= P.estart[e + 1]) ++e;
-    return e;
-  };
-  auto rowsub_of = [&](int st) {
-    const int e = ep_of(st);
-    return P.nbe[e] * P.sub[e];
-  };
-  auto phase_of = [&](int st) {
-    const int ep = ep_of(st), pos = st - P.estart[ep];
-    return ((P.serpentine && (ep & 1)) ? P.nbe[ep] - 1 - pos : pos) * P.sub[ep];
-  };
   auto prefetch = [&](int st) {  // the wave's first tile(s) of step st: rows do not depend on w
     have_pre = false;
     have_ppre = false;
     if (kPersistPrefetch == 0 || !active || st >= P.s1) return;
+    const PersistStep S(P, st);
     if constexpr (VIRT) {  // the inputs of the wave's first pick tile of step st
-      const int64_t pt = wave * rowsub_of(st) + phase_of(st);
+      const int64_t pt = wave * S.rsub + S.phase;
       if (pt < ntile) {
         const int64_t p = pt * 16 + (lane >> 2);
         pick_load<4, kPreLams>(sv, p < npick ? p : -1, lane & 3, ppre);
         have_ppre = true;
       }
     }
-    const int64_t base = ((int64_t)phase_of(st) * P.Gw + wave) * 64;
+    const int64_t base = ((int64_t)S.phase * P.Gw + wave) * 64;
     if (kPersistPrefetch == 3 || base >= n) return;
     if constexpr (kPersistPrefetch == 2) {
       // L2 touch: one dword per row of the first tile, into a register nobody reads (held until
@@ -1597,7 +1712,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       const uint8_t* X8 = static_cast<const uint8_t*>(X);
       uint4 a[2], b[2] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
       fp8_load_tile(X8, 0, n, hole, base, a);
-      const int64_t step_rows = P.Gw * 64 * rowsub_of(st);
+      const int64_t step_rows = P.Gw * 64 * S.rsub;
       if (base + step_rows < n) fp8_load_tile(X8, 0, n, hole, base + step_rows, b);
       pre[0] = a[0]; pre[1] = a[1]; pre[2] = b[0]; pre[3] = b[1];
     } else {
@@ -1608,70 +1723,19 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
 
   for (int st = P.s0; st < P.s1 && !s_done; ++st) {
     if constexpr (kPersistPrefetch == 2) asm volatile("s_waitcnt vmcnt(0)" : "+v"(touch) : : "memory");
-    const int ep = ep_of(st), pos = st - P.estart[ep], b = phase_of(st), rsub = rowsub_of(st);
+    const PersistStep S(P, st);
     unsigned long long* acc = accs + (st % 3) * kPersistAccWords;
     if (blockIdx.x == 0 && wv == kArriveWave) {  // set st + 1 (read as set st - 2 before barrier st - 1)
       unsigned long long* nx = accs + ((st + 1) % 3) * kPersistAccWords;
       for (int e = lane; e < kPersistAccWords; e += kWave)
         __hip_atomic_store(nx + e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // ---- the pass over minibatch b (this wave's share) ----
-    float lacc = 0.0f, wacc = 0.0f, whacc = 0.0f, dacc = 0.0f;
-    f32x16_t hacc = {};
-    if constexpr (FP8) {
-      const int q = lane & 1;
-      f32x2_t wl[8], g[8];
-#pragma unroll
-      for (int p = 0; p < 8; ++p) {
-        wl[p] = f32x2_t{wsh[16 * q + 2 * p], wsh[16 * q + 2 * p + 1]};
-        g[p] = f32x2_t{0.0f, 0.0f};
-      }
-      if (active)
-        fp8_wave_pass<false, VIRT, true, kPersistLams, kPreLams>(static_cast<const uint8_t*>(X), 0, row_end, wl, wsh, x_scale, cw0, cw1, 1,
-                                         rsub, b, sv, hole, wave, P.Gw, nullptr, g, lacc, wacc, whacc, dacc, hacc,
-                                         pre, have_pre, ppre, have_ppre);
-      float gs[16];
-#pragma unroll
-      for (int p = 0; p < 8; ++p) {
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int col = 16 * q + 2 * p + e;
-          gs[2 * p + e] = strided_sum<2>(g[p][e]) * (col < d_feat ? inv_s : 1.0f);
-        }
-      }
-      if (lane < 2) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) red[wv][16 * lane + j] = gs[j];
-      }
-    } else {
-      const int q = lane & 3;
-      float wl[8], g[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        wl[j] = wsh[q * 8 + j];
-        g[j] = 0.0f;
-      }
-      if (active)
-        bf16_wave_pass<false, VIRT, true, kPersistLams, kPreLams, kPersistDepth>(X, 0, row_end, wl, cw0, cw1, 1, rsub, b, sv, hole, wave, P.Gw, nullptr, g,
-                                          lacc, wacc, whacc, dacc, hacc, pre, have_pre, ppre, have_ppre);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) g[j] = strided_sum<4>(g[j]);
-      if (lane < 4) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) red[wv][8 * lane + j] = g[j];
-      }
-    }
-    lacc = wave_sum(lacc);
-    wacc = wave_sum(wacc);
-    dacc = wave_sum(dacc);
+    // ---- the pass over minibatch S.phase (this wave's share) ----
+    persist_wave_sums<FP8, VIRT, kPersistLams, kPreLams, kPersistDepth>(
+        X, row_end, x_scale, inv_s, cw0, cw1, wsh, sv, hole, wave, P.Gw, active, S.rsub, S.phase, red, wv, lane, pre,
+        have_pre, ppre, have_ppre);
     if (P.stamps != nullptr && lane == 0)
       P.stamps[((int64_t)(st - P.s0) * kStampRows + 3 + wv) * gridDim.x + blockIdx.x] = wall_clock64();
-    if (lane == 0) {
-      red[wv][32] = lacc;
-      red[wv][33] = wacc;
-      red[wv][34] = 0.0f;
-      red[wv][35] = dacc;
-    }
     __syncthreads();
     if (wv != kArriveWave) {
       prefetch(st + 1);  // the pick tiles' waves run their pick-input chains during the barrier
@@ -1682,16 +1746,17 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       if (lane < kSgdSlots && lane != 34 && qs != 0)
         __hip_atomic_fetch_add(acc + (blockIdx.x % kPersistReplicas) * 36 + lane, (unsigned long long)qs,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      arrivals += gridDim.x;
+      // the fault-test knob: barrier s0 waits for one arrival more than the grid has
+      arrivals += gridDim.x + ((P.fault_test && st == P.s0) ? 1u : 0u);
       if (P.stamps != nullptr && lane == 0)
         P.stamps[((int64_t)(st - P.s0) * kStampRows + 0) * gridDim.x + blockIdx.x] = wall_clock64();
-      const bool ok = persist_barrier(bar, arrivals, lane);
+      const bool ok = persist_barrier(bar, arrivals, lane, fault, P.spin_limit);
       if (!ok && lane == 0) s_ok = 0;
       if (P.stamps != nullptr && lane == 0)
         P.stamps[((int64_t)(st - P.s0) * kStampRows + 1) * gridDim.x + blockIdx.x] = wall_clock64();
     }
     __syncthreads();
-    if (!s_ok) break;  // uniform in the block
+    if (!s_ok) return;  // uniform in the block: a faulted grid publishes nothing
     // ---- the update, redundantly in every block ----
     for (int e = t; e < kPersistAccWords; e += kPersistThreads)
       rep[e] = __hip_atomic_load(acc + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1703,17 +1768,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       rd[t] = (double)(long long)q * (1.0 / kFixScale);
     }
     __syncthreads();
-    SgdArgs a;
-    a.d = P.d;
-    a.C = P.C;
-    a.c = P.lr[ep];
-    a.momentum = P.momentum;
-    a.fit_intercept = P.fit_intercept;
-    a.nb = rsub;  // the minibatch estimates the epoch's weight as rsub x its own
-    a.avg = ep >= P.avg_from;
-    a.epoch_end = pos == P.nbe[ep] - 1;
-    a.tol = P.sub[ep] > 1 ? -1.0 : P.tol;  // a sub-sampled epoch never decides convergence
-    sgd_apply(rd, sst, wnew, &s_done, affl, a, t, true);
+    sgd_apply(rd, sst, wnew, &s_done, affl, S.args(P), t, true);
     __syncthreads();
     if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);
     __syncthreads();
@@ -1721,12 +1776,97 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       P.stamps[((int64_t)(st - P.s0) * kStampRows + 2) * gridDim.x + blockIdx.x] = wall_clock64();
   }
   if (blockIdx.x == 0) {  // every block holds the same state: block 0 publishes it
-    if (t == 0 && !s_ok) sst[kSgdFault] = 1.0;
-    __syncthreads();
     for (int e = t; e < kStateSize; e += kPersistThreads) P.st[e] = sst[e];
     if (t < 32) P.w32[t] = wnew[t];
     if (t == 0) *P.done = s_done;
   }
+}
+
+// In front of every persistent launch (replaces a memset): zero the barrier shards, the accumulator
+// sets and the fault word, and back up the initial solver state, weights and done flag for the
+// recovery launch (a faulted grid may have advanced some blocks' copies; the recovery restarts from
+// exactly what the persistent launch started from).
+__global__ __launch_bounds__(256) void sgd_persist_prep_kernel(unsigned long long* __restrict__ ws,
+                                                               const double* __restrict__ st,
+                                                               const float* __restrict__ w32,
+                                                               const int* __restrict__ done) {
+  const int t = threadIdx.x;
+  for (int e = t; e < kWsBackup; e += 256) ws[e] = 0ull;
+  double* bst = reinterpret_cast<double*>(ws + kWsBackup);
+  for (int e = t; e < kStateSize; e += 256) bst[e] = st[e];
+  float* bw = reinterpret_cast<float*>(ws + kWsBackupW);
+  if (t < 32) bw[t] = w32[t];
+  if (t == 0) ws[kWsBackupDone] = (unsigned long long)(unsigned)*done;
+}
+
+// Behind every persistent launch: a no-op unless its fault word is set.  Then one block re-runs
+// steps [s0, s1) from the backup: its 8 waves walk the per-step grid's Gw waves in turn, each
+// wave's sums go to fixed point on their own (the persistent launch converts per wave too), so the
+// integer step sums -- and the fit -- are bitwise those of a persistent launch that had run; state
+// slot kSgdFault = 2 records the recovery.  Its barrier is __syncthreads: one block is always
+// resident eventually.
+template <bool FP8, bool VIRT>
+__global__ __launch_bounds__(kPersistThreads, 1) void sgd_recover_kernel(const void* __restrict__ X, int64_t row_end,
+                                                                         float x_scale,
+                                                                         const float* __restrict__ class_w,
+                                                                         SmoteView sv, RowHole hole,
+                                                                         SgdPersistArgs P) {
+  if (__hip_atomic_load(reinterpret_cast<unsigned int*>(P.ws + kWsFault), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_AGENT) == 0u)
+    return;  // uniform: every thread reads the same word written by the previous launch
+  __shared__ double sst[kStateSize];
+  __shared__ __attribute__((aligned(16))) float wsh[32];
+  __shared__ float wnew[32];
+  __shared__ float red[kPersistWaves][36];
+  __shared__ long long qw[kPersistWaves][36];
+  __shared__ double rd[kSgdSlots];
+  __shared__ int s_done;
+  __shared__ double saff[64];
+  const int t = threadIdx.x, lane = lane_id(), wv = wave_id();
+  constexpr int d_feat = 30;
+  const double* bst = reinterpret_cast<const double*>(P.ws + kWsBackup);
+  const float* bw = reinterpret_cast<const float*>(P.ws + kWsBackupW);
+  if (P.aff != nullptr && t < 64) saff[t] = P.aff[t];
+  const double* affl = P.aff != nullptr ? saff : nullptr;
+  const float inv_s = FP8 ? 1.0f / x_scale : 1.0f;
+  for (int e = t; e < kStateSize; e += kPersistThreads) sst[e] = bst[e];
+  if (t < 32) {
+    const float w = bw[t];
+    wnew[t] = w;
+    wsh[t] = t == kLabelCol ? 0.0f : w * ((FP8 && t < d_feat) ? inv_s : 1.0f);
+  }
+  if (t == 0) s_done = (int)P.ws[kWsBackupDone];
+  __syncthreads();
+  const float cw0 = class_w[0], cw1 = class_w[1];
+  PickIn<4, 32> nopick;
+  for (int st = P.s0; st < P.s1 && !s_done; ++st) {
+    const PersistStep S(P, st);
+    long long q = 0;
+    for (int64_t w = wv; w < P.Gw; w += kPersistWaves) {
+      persist_wave_sums<FP8, VIRT, 16, 32, 1>(X, row_end, x_scale, inv_s, cw0, cw1, wsh, sv, hole, w, P.Gw, true,
+                                              S.rsub, S.phase, red, wv, lane, kNoTiles, false, nopick, false);
+      __builtin_amdgcn_wave_barrier();  // this wave's row of red (LDS ops of one wave retire in order)
+      if (lane < kSgdSlots) q += wave_sums_fixed<1>(&red[wv], affl, lane);
+      __builtin_amdgcn_wave_barrier();
+    }
+    if (lane < kSgdSlots) qw[wv][lane] = q;
+    __syncthreads();
+    if (t < kSgdSlots) {
+      unsigned long long s = 0;
+      for (int w = 0; w < kPersistWaves; ++w) s += (unsigned long long)qw[w][t];
+      rd[t] = t == 34 ? 0.0 : (double)(long long)s * (1.0 / kFixScale);
+    }
+    __syncthreads();
+    sgd_apply(rd, sst, wnew, &s_done, affl, S.args(P), t, true);
+    __syncthreads();
+    if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);
+    __syncthreads();
+  }
+  if (t == 0) sst[kSgdFault] = 2.0;
+  __syncthreads();
+  for (int e = t; e < kStateSize; e += kPersistThreads) P.st[e] = sst[e];
+  if (t < 32) P.w32[t] = wnew[t];
+  if (t == 0) *P.done = s_done;
 }
 
 }  // namespace
@@ -2009,8 +2149,8 @@ int sgd_persist_blocks(int grid_blocks) {
   return blocks <= capacity ? blocks : 0;
 }
 
-void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
-                        const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream) {
+int launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, const float* class_w,
+                       const SmoteView* sv, RowHole hole, const SgdPersistArgs& a, hipStream_t stream) {
   if (a.nb < 1 || a.epochs < 1 || a.epochs > kSgdMaxEpochs || a.s0 < 0 || a.s1 > a.estart[a.epochs] || a.s0 >= a.s1)
     throw std::runtime_error("sgd_persist: bad schedule");
   if (a.Gw < kWaves || a.Gw % kWaves != 0) throw std::runtime_error("sgd_persist: bad pass grid");
@@ -2020,28 +2160,48 @@ void launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, 
   if (blocks == 0) throw std::runtime_error("sgd_persist: the grid cannot be resident (launch per step)");
   const SmoteView v = checked_view(sv, 0, row_end);
   check_hole(hole, 0, v.parents != nullptr ? v.n_real : row_end);
-  // barrier shards and every accumulator set: zero per call (stream-ordered before the launch)
-  if (hipMemsetAsync(a.ws, 0, sizeof(unsigned long long) * kSgdPersistWords, stream) != hipSuccess)
-    throw std::runtime_error("sgd_persist: memset failed");
   const bool virt = v.parents != nullptr;
   static const int depth = [] {  // lab switch: FDX_SGD_PERSIST_CFG=1 -> one stored tile in flight
     const char* e = std::getenv("FDX_SGD_PERSIST_CFG");
     return (e != nullptr && e[0] == '1') ? 1 : 2;
   }();
-#define FDX_SGDP(F, V, D) \
-  sgd_persist_kernel<F, V, 16, 2, D><<<blocks, kPersistThreads, 0, stream>>>(X, row_end, x_scale, class_w, v, hole, a)
+  // FDX_SGD_COOP=0 (lab): a plain launch of the same grid (same residency, no launch-time check)
+  static const bool coop = [] {
+    const char* e = std::getenv("FDX_SGD_COOP");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  const void* kern = nullptr;
   if (fp8) {  // fp8 tiles are half the bytes: its pass keeps two tiles in flight in the same registers
-    if (virt) FDX_SGDP(true, true, 2);
-    else FDX_SGDP(true, false, 2);
+    kern = virt ? (const void*)sgd_persist_kernel<true, true, 16, 2, 2> : (const void*)sgd_persist_kernel<true, false, 16, 2, 2>;
   } else if (depth == 1) {
-    if (virt) FDX_SGDP(false, true, 1);
-    else FDX_SGDP(false, false, 1);
+    kern = virt ? (const void*)sgd_persist_kernel<false, true, 16, 2, 1> : (const void*)sgd_persist_kernel<false, false, 16, 2, 1>;
   } else {
-    if (virt) FDX_SGDP(false, true, 2);
-    else FDX_SGDP(false, false, 2);
+    kern = virt ? (const void*)sgd_persist_kernel<false, true, 16, 2, 2> : (const void*)sgd_persist_kernel<false, false, 16, 2, 2>;
   }
-#undef FDX_SGDP
-  check_launch("sgd_persist");
+  // barrier shards, accumulator sets, fault word: zero; the initial state: backed up (stream-ordered)
+  sgd_persist_prep_kernel<<<1, 256, 0, stream>>>(a.ws, a.st, a.w32, a.done);
+  check_launch("sgd_persist_prep");
+  SgdPersistArgs pa = a;
+  void* args[] = {(void*)&X, (void*)&row_end, (void*)&x_scale, (void*)&class_w, (void*)&v, (void*)&hole,
+                  (void*)&pa};
+  hipError_t e = coop ? hipLaunchCooperativeKernel(kern, dim3(blocks), dim3(kPersistThreads), args, 0, stream)
+                      : hipLaunchKernel(kern, dim3(blocks), dim3(kPersistThreads), args, 0, stream);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // clear the sticky launch error
+    if (e == hipErrorCooperativeLaunchTooLarge) return 1;  // the prep kernel alone is harmless
+    throw std::runtime_error(std::string("sgd_persist: launch failed: ") + hipGetErrorString(e));
+  }
+#define FDX_SGDR(F, V) sgd_recover_kernel<F, V><<<1, kPersistThreads, 0, stream>>>(X, row_end, x_scale, class_w, v, hole, a)
+  if (fp8) {
+    if (virt) FDX_SGDR(true, true);
+    else FDX_SGDR(true, false);
+  } else {
+    if (virt) FDX_SGDR(false, true);
+    else FDX_SGDR(false, false);
+  }
+#undef FDX_SGDR
+  check_launch("sgd_recover");
+  return 0;
 }
 
 }  // namespace fdx

@@ -3,7 +3,10 @@
 The reference runs this job with XGBClassifier (train_model.py:58-106); its GBDT counterpart is
 models/gbdt_cv.py.  Folds come from a keyed Feistel stratified assignment (ops/split.assign), not
 sklearn's StratifiedKFold(shuffle, 42) permutation: statistically equivalent folds, so fold-level
-AUC parity with the reference is unpinned.
+AUC parity with the reference is unpinned -- unless the caller passes ``fold_codes``: train.py hands
+in sklearn's StratifiedKFold(5, shuffle=True, random_state=42) membership in ``split=sklearn`` mode
+(and the K3 codes of the device split in ``split=device`` mode), so the job's folds are exactly the
+per-fold path's (tests/test_cv_gpu.py::test_device_cv_sklearn_folds).
 
 Reference (train_model.py:36-110): StandardScaler fitted once on the training split; 5-fold
 StratifiedKFold(shuffle, random_state=42) over it; inside every fold SMOTE(random_state=42) on the
@@ -66,6 +69,33 @@ class CVResult:
         return float(np.std(self.fold_aucs))
 
 
+def fold_codes_from_splits(splits, n: int) -> np.ndarray:
+    """[(train_idx, val_idx)] * K (sklearn StratifiedKFold.split over n rows) -> uint8 fold code of
+    every row (the fold it validates in).  Every row must validate in exactly one fold."""
+    codes = np.full(int(n), 255, np.uint8)
+    for k, (_, va) in enumerate(splits):
+        va = np.asarray(va, dtype=np.int64)
+        if (codes[va] != 255).any():
+            raise ValueError("a row validates in more than one fold")
+        codes[va] = k
+    if (codes == 255).any():
+        raise ValueError("the folds do not cover every row")
+    return codes
+
+
+def resolve_fold_codes(y: torch.Tensor, K: int, seed: int, fold_codes=None) -> torch.Tensor:
+    """The job's per-row fold codes on y's device: the caller's (checked) or the K3 Feistel ones."""
+    if fold_codes is None:
+        return split_ops.assign(y, test_frac=0.0, n_folds=K, seed=seed)
+    c = torch.as_tensor(np.asarray(fold_codes) if not isinstance(fold_codes, torch.Tensor) else fold_codes)
+    if c.dim() != 1 or c.shape[0] != y.shape[0]:
+        raise ValueError(f"fold_codes must be 1-D with one code per training row ({y.shape[0]})")
+    c = c.to(device=y.device, dtype=torch.uint8).contiguous()
+    if int(c.max()) >= K:  # one host read per job (the caller's codes are host data anyway)
+        raise ValueError(f"fold codes must lie in 0..{K - 1}")
+    return c
+
+
 class DeviceCV:
     """The train_model.py job shape (CV + final fit + AUCs) for the logistic model family on one GPU
     (the reference's XGB family: models/gbdt_cv.DeviceGBDTCV)."""
@@ -83,7 +113,9 @@ class DeviceCV:
             raise ValueError("DeviceCV fits the logistic solvers (newton | sgd)")
 
     def run(self, X: torch.Tensor, y: torch.Tensor, X_test: torch.Tensor | None = None,
-            y_test: torch.Tensor | None = None) -> CVResult:
+            y_test: torch.Tensor | None = None, fold_codes=None) -> CVResult:
+        """``fold_codes``: per-row fold index (0..K-1) of the training rows, e.g. sklearn's
+        StratifiedKFold membership (fold_codes_from_splits); None: the keyed Feistel assignment."""
         cfg, K = self.cfg, self.n_folds
         if not X.is_cuda:
             raise ValueError("DeviceCV runs on the device (train.py's CV path covers host tables)")
@@ -95,7 +127,7 @@ class DeviceCV:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 3)]
         ev[0].record()
         # ---- fold codes and the (fold, label) permutation -----------------------------------
-        codes = split_ops.assign(y, test_frac=0.0, n_folds=K, seed=self.seed)
+        codes = resolve_fold_codes(y, K, self.seed, fold_codes)
         # the table is sorted by fold only: inside a block the rows keep their order, so the
         # sub-sampled warm-up passes (runs of row tiles) see both classes in proportion.  (Sorted by
         # (fold, label), a fold's positives formed one contiguous run that a 1/16 tile sample took

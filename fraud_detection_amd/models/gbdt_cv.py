@@ -22,8 +22,9 @@ MI355X layout (no per-fold copy of the training rows):
     predict kernel.
 Cuts come from one quantile pass for all six fits (xgboost sketches each fit's own rows); a fold's
 fit on an explicit copy of its rows with the same cuts grows bit-identical trees
-(tests/test_gbdt_cv_gpu.py).  Folds come from the keyed Feistel assignment, not sklearn's
-permutation: statistically equivalent folds, fold-level AUC parity with the reference unpinned.
+(tests/test_gbdt_cv_gpu.py).  Folds come from the keyed Feistel assignment unless the caller passes
+``fold_codes`` (train.py: sklearn's StratifiedKFold(5, shuffle, 42) membership in split=sklearn
+mode, so the folds are the reference's; tests/test_gbdt_cv_gpu.py::test_gbdt_cv_sklearn_folds).
 """
 from __future__ import annotations
 
@@ -37,7 +38,7 @@ from ..ops import gbdt as gb
 from ..ops import knn as knn_ops
 from ..ops import metrics as metric_ops
 from ..ops import scaler as scaler_ops
-from ..ops import split as split_ops
+from .cv import resolve_fold_codes
 from .gbdt import GBDTResult
 from .pipeline import TrainConfig
 
@@ -82,7 +83,8 @@ class DeviceGBDTCV:
         return float(self.spw)
 
     def run(self, X: torch.Tensor, y: torch.Tensor, X_test: torch.Tensor | None = None,
-            y_test: torch.Tensor | None = None) -> GBDTCVResult:
+            y_test: torch.Tensor | None = None, fold_codes=None) -> GBDTCVResult:
+        """``fold_codes``: per-row fold index of the training rows (models/cv.resolve_fold_codes)."""
         cfg, K = self.cfg, self.n_folds
         if not X.is_cuda:
             raise ValueError("DeviceGBDTCV runs on the device (train.py's per-fold path covers host tables)")
@@ -94,7 +96,7 @@ class DeviceGBDTCV:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(K + 3)]
         ev[0].record()
         # ---- fold codes, fold-sorted permutation, the fold's positives ------------------------
-        codes = split_ops.assign(y, test_frac=0.0, n_folds=K, seed=self.seed)
+        codes = resolve_fold_codes(y, K, self.seed, fold_codes)
         key = (codes * 2 + y).to(torch.uint8)
         pend_f = [scaler_ops.compact_indices_async(codes, t) for t in range(K)]
         pend_p = [scaler_ops.compact_indices_async(key, 2 * t + 1) for t in range(K)]
@@ -110,7 +112,13 @@ class DeviceGBDTCV:
         p = self.params.validate()
         cuts = gb.quantile_cuts(xs[:, :d], p.max_bin, p.cut_sample_rows)
         n_pos = int(sum(pos))
-        cap = max(0, int(round((n - n_pos) * cfg.sampling_ratio)) - n_pos)  # the final fit's quota (the largest)
+
+        def quota(n_tr: int, n_min: int) -> int:
+            return max(0, int(round((n_tr - n_min) * cfg.sampling_ratio)) - n_min) if n_min > 0 else 0
+
+        # the SMOTE tail holds the largest quota of the six fits (with sampling_ratio < 1 a fold's
+        # quota can exceed the final fit's by rounding near the class balance)
+        cap = max([quota(n, n_pos)] + [quota(n - int(bounds[k + 1] - bounds[k]), n_pos - pos[k]) for k in range(K)])
         bins = torch.empty((n + cap, 32), dtype=torch.uint8, device=dev)
         gb.bin_rows(xs[:, :d], cuts[0], cuts[1], out=bins[:n])
         del xs
@@ -133,7 +141,7 @@ class DeviceGBDTCV:
                 xmin = torch.cat([xpos[: pbounds[k]], xpos[pbounds[k + 1]:]])
             n_tr = n - hole[1]
             n_min = int(xmin.shape[0])
-            n_new = max(0, int(round((n_tr - n_min) * cfg.sampling_ratio)) - n_min) if n_min > 0 else 0
+            n_new = quota(n_tr, n_min)
             if n_new > 0:
                 kk = min(cfg.k_neighbors, n_min - 1)
                 if kk < 1:

@@ -44,6 +44,9 @@ class FitInfo:
     objective: float
     grad_max: float
     history: list = field(default_factory=list)
+    # persistent SGD: the fit ran on the one-block recovery launch (its grid barrier faulted because
+    # not every block was resident -- another stream or process held CUs); bitwise the same fit
+    recovered: bool = False
 
 
 @dataclass
@@ -748,7 +751,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
             batch_rows: int | None = None, max_steps: int | None = None, hole: tuple | None = None,
             persistent: bool | None = None, serpentine: bool = False, subsample=SGD_SUB,
             extra_epochs: int = 0, avg_from: int | None = None, epoch_batches=None,
-            _stamps: torch.Tensor | None = None):
+            _stamps: torch.Tensor | None = None, _fault_test: bool = False, _spin_limit: int = 0):
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
@@ -774,7 +777,11 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     ``hole``: (at, len) stored rows the fit steps over (newton_fit).
     ``persistent``: one process, the whole schedule in ONE launch (logreg.hip sgd_persist_kernel:
     a grid barrier per step instead of a launch per step; bitwise the same fit).  Default on
-    unless FDX_SGD_PERSIST=0.  ``serpentine``: odd epochs visit the minibatches in reverse order
+    unless FDX_SGD_PERSIST=0.  It is a cooperative launch: a grid the occupancy query refuses runs
+    on the per-step launches instead; a grid barrier that times out at run time (CUs held by another
+    stream or process) hands the fit to the one-block recovery launch queued behind it, which
+    re-runs it from the initial state -- bitwise the same fit, FitInfo.recovered set.
+    ``_fault_test`` forces that path (test knob).  ``serpentine``: odd epochs visit the minibatches in reverse order
     (persistent launch only), so an epoch's first minibatches are the previous epoch's last ones
     -- still resident in the 256 MB Infinity Cache.  ``subsample``: per-epoch row sub-sample factors
     (SGD_SUB; an epoch with factor s visits 1/s of the rows in its nb minibatches).
@@ -877,12 +884,15 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         if s1 <= s0:
             return
         if persist:
-            m.sgd_persist(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.class_w), *vargs,
-                          ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
-                          float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
-                          int(bool(serpentine)), [float(x) for x in lrs], int(s0), int(s1),
-                          4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs, nbs)
-            return
+            refused = m.sgd_persist(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.class_w), *vargs,
+                                    ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
+                                    float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
+                                    int(bool(serpentine)), [float(x) for x in lrs], int(s0), int(s1),
+                                    4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs, nbs,
+                                    int(bool(_fault_test)), int(_spin_limit))
+            if not refused:
+                return
+            # the cooperative launch refused the grid: the per-step launches (bitwise the same fit)
         if serpentine:
             raise ValueError("serpentine minibatch order needs the persistent SGD launch")
         m.sgd_run(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w), ptr(ws.done),
@@ -972,14 +982,15 @@ def sgd_minibatch_sums(rows: torch.Tensor, w: torch.Tensor, nb: int, phase: int,
             "blocks": blocks}
 
 
-S_SGD_FAULT = 229  # logreg.hip kSgdFault: the persistent SGD launch's grid barrier timed out
+S_SGD_FAULT = 229  # logreg.hip kSgdFault: 2 = the persistent SGD fit ran on its recovery launch
 
 
 def _info_from_state(st: np.ndarray, sgd: bool = False) -> FitInfo:
-    if sgd and st[S_SGD_FAULT] != 0:
-        raise RuntimeError("persistent SGD launch: a grid barrier timed out (not every block was resident)")
+    if sgd and st[S_SGD_FAULT] not in (0.0, 2.0):
+        raise RuntimeError(f"persistent SGD launch: unexpected fault state {st[S_SGD_FAULT]}")
     return FitInfo(w=st[S_W:S_W + 32].copy(), n_iter=int(st[S_ITER]), n_newton_steps=0 if sgd else int(st[S_NACC]),
-                   converged=bool(st[S_CONV] > 0), objective=float(st[S_OBJ]), grad_max=float(st[S_GMAX]))
+                   converged=bool(st[S_CONV] > 0), objective=float(st[S_OBJ]), grad_max=float(st[S_GMAX]),
+                   recovered=bool(sgd and st[S_SGD_FAULT] == 2.0))
 
 
 # ------------------------------------------------------------------------------------------

@@ -114,8 +114,18 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
         say(f" Performing Stratified K-Fold Cross-Validation ({cv_folds} folds) with SMOTE inside each fold...")
         if mode == "device":
             folds = dev_folds
+            # the device jobs run on the K3 codes of this split (the per-fold path's folds)
+            job_codes = codes.index_select(0, tr) if comm is None else None
         else:
-            folds = [(tr[a], tr[b]) for a, b in stratified_folds(y[tr], cv_folds, 42)]
+            sk = stratified_folds(y[tr], cv_folds, 42)
+            folds = [(tr[a], tr[b]) for a, b in sk]
+            # sklearn's StratifiedKFold(5, shuffle, 42) membership (train_model.py:49,58) for the
+            # device jobs too: their fold AUCs are on the reference's folds
+            job_codes = None
+            if comm is None:
+                from .models.cv import fold_codes_from_splits
+
+                job_codes = fold_codes_from_splits(sk, len(tr))
         cv_mode = s.cv_parallel
         if cv_mode == "auto":  # small folds are latency-bound under DP: give each rank whole folds
             cv_mode = "fold" if comm is not None and len(tr) < FOLD_PARALLEL_ROWS else "dp"
@@ -126,7 +136,7 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
 
             t_fit = time.perf_counter()
             with tracing.span("train.cv_job", model=model_type), tracing.roctx_range("train.cv_job"):
-                cvr = DeviceCV(cfg, cv_folds, seed=42).run(Xtr, ytr)
+                cvr = DeviceCV(cfg, cv_folds, seed=42).run(Xtr, ytr, fold_codes=job_codes)
             cv_scores, res_cv, cv_engine = cvr.fold_aucs, cvr.final, "device"
             for k, auc in enumerate(cv_scores):
                 progress.record(k, auc)
@@ -137,7 +147,7 @@ def run(settings: Settings | None = None, model_type: str = "logistic", cv_folds
 
             t_fit = time.perf_counter()
             with tracing.span("train.cv_job", model=model_type), tracing.roctx_range("train.cv_job"):
-                cvr = DeviceGBDTCV(cfg, n_folds=cv_folds, seed=42).run(Xtr, ytr)
+                cvr = DeviceGBDTCV(cfg, n_folds=cv_folds, seed=42).run(Xtr, ytr, fold_codes=job_codes)
             cv_scores, res_cv, cv_engine = cvr.fold_aucs, cvr.final, "device"
             for k, auc in enumerate(cv_scores):
                 progress.record(k, auc)

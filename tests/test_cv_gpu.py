@@ -73,3 +73,30 @@ def test_device_cv_warm_start_same_models(dev):
         assert fc.converged and fw.converged and fw.grad_max <= 1e-4
     np.testing.assert_allclose(rw.fold_aucs, rc.fold_aucs, atol=1e-4)
     assert sum(rw.fold_iters[1:]) < sum(rc.fold_iters[1:])  # fewer iterations from a warm start
+
+
+@pytest.mark.parametrize("solver", ["newton", "sgd"])
+def test_device_cv_sklearn_folds(dev, solver):
+    """With sklearn's StratifiedKFold(5, shuffle=True, random_state=42) codes (train.py split=sklearn,
+    train_model.py:49,58) the job's fold blocks are exactly sklearn's validation folds, and every fold
+    AUC agrees within 1e-3 with the per-fold path (scaler + SMOTE + fit on a copy of the fold's
+    training rows, AUC of its validation rows) on the same folds."""
+    from sklearn.model_selection import StratifiedKFold
+
+    from fraud_detection_amd.models.cv import fold_codes_from_splits
+    from fraud_detection_amd.models.pipeline import DevicePipeline, evaluate
+
+    X, y = separable(1_200_000, fraud_rate=0.004, seed=35, device=dev)
+    yh = y.cpu().numpy()
+    sk = list(StratifiedKFold(n_splits=5, shuffle=True, random_state=42).split(np.zeros(len(yh)), yh))
+    cfg = TrainConfig(solver=solver, seed=42)
+    cv = DeviceCV(cfg)
+    r = cv.run(X, y, fold_codes=fold_codes_from_splits(sk, len(yh)))
+    perm, b = cv.perm.cpu().numpy(), cv.bounds
+    for k, (tr, va) in enumerate(sk):
+        assert np.array_equal(perm[b[k]:b[k + 1]], np.sort(va)), k  # exactly sklearn's fold k, in row order
+        t = torch.from_numpy(tr).to(dev)
+        v = torch.from_numpy(va).to(dev)
+        res = DevicePipeline(cfg).fit(X.index_select(0, t), y.index_select(0, t))
+        auc = evaluate(res, X.index_select(0, v), y.index_select(0, v))["auc"]
+        assert abs(r.fold_aucs[k] - auc) < 1e-3, (k, r.fold_aucs[k], auc)

@@ -74,3 +74,28 @@ def test_train_entry_point_runs_the_device_gbdt_cv_job(tmp_path, monkeypatch):
     assert out["cv_engine"] == "device", out["cv_engine"]
     assert len(out["cv_scores"]) == 3 and all(0.0 <= a <= 1.0 for a in out["cv_scores"])
     assert os.path.exists(tmp_path / "models" / "xgb_model.json")
+
+
+def test_gbdt_cv_sklearn_folds(dev):
+    """sklearn StratifiedKFold(5, shuffle, 42) codes: the GBDT job's fold blocks are sklearn's
+    validation folds; fold AUCs agree with the per-fold GBDT pipeline on the same folds (its own
+    scaler, cuts and SMOTE draws on the fold copy, so a looser bound than the logistic job's)."""
+    from sklearn.model_selection import StratifiedKFold
+
+    from fraud_detection_amd.models.cv import fold_codes_from_splits
+    from fraud_detection_amd.models.gbdt import GBDTPipeline
+
+    X, y = separable(400_000, fraud_rate=0.004, seed=63, device=dev)
+    yh = y.cpu().numpy()
+    sk = list(StratifiedKFold(n_splits=5, shuffle=True, random_state=42).split(np.zeros(len(yh)), yh))
+    params = gb.GBDTParams(n_estimators=20, max_depth=5)
+    cv = DeviceGBDTCV(TrainConfig(), params)
+    r = cv.run(X, y, fold_codes=fold_codes_from_splits(sk, len(yh)))
+    perm, b = cv.perm.cpu().numpy(), cv.bounds
+    for k, (tr, va) in enumerate(sk):
+        assert np.array_equal(perm[b[k]:b[k + 1]], np.sort(va)), k
+    for k in (0, 3):
+        t, v = torch.from_numpy(sk[k][0]).to(dev), torch.from_numpy(sk[k][1]).to(dev)
+        res = GBDTPipeline(TrainConfig(), params).fit(X.index_select(0, t), y.index_select(0, t))
+        auc = res.evaluate(X.index_select(0, v), y.index_select(0, v))["auc"]
+        assert abs(r.fold_aucs[k] - auc) < 5e-3, (k, r.fold_aucs[k], auc)

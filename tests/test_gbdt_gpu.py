@@ -177,10 +177,11 @@ def test_hist_multi_flush_bit_identical(dev, monkeypatch):
     assert np.array_equal(a.feat[0], ref.feat[0]) and np.array_equal(a.bin[0], ref.bin[0])
 
 
-@pytest.mark.parametrize("var", [1, 2])
+@pytest.mark.parametrize("var", [1, 2, 3])
 def test_hist_variants_bit_identical(dev, var):
-    """The histogram kernel's lab variants (rotated features; split int32 g/h adds) build the same
-    integer histograms, so the trees and margins are bit-identical to the lockstep form."""
+    """The histogram kernel's variants (rotated features; split int32 g/h adds; eight lanes per row,
+    conflict-free bin-major slots -- the default) build the same integer histograms, so the trees and
+    margins are bit-identical to the lockstep form."""
     from fraud_detection_amd.ops.native import native
 
     Xd, yd, X, y = _data(150_000, 30, seed=16)

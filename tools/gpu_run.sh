@@ -22,13 +22,14 @@
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   quicksgd     the same with the SGD solver
+#   quicksgdnc   quicksgd bf16 with a plain (not cooperative) persistent launch (FDX_SGD_COOP=0)
 #   pmc          two PMC passes over a short bench
 #   pmcfp8       logreg pass counters + kernel stats with fp8 and with bf16 rows
 #   gbdt         tools/gbdt_bench.py at the bench shape; gbdtprof: its kernel trace (20 trees)
 #   dp2          2-rank DP rehearsal of bench.py on one GPU over gloo (both SMOTE scopes)
 #   dp2self      the same rehearsal through bench.py's own launcher (python bench.py --gpus 2, no torchrun)
 #   dpscope      tools/dp_scope_probe.py: global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo)
-#   gbdtvar      GBDT histogram kernel variants under a kernel trace (FDX_GBDT_HIST_VAR=0/2/1)
+#   gbdtvar      GBDT histogram kernel variants under a kernel trace (FDX_GBDT_VARS, default "0 3")
 #   dpstored     dp_scope_probe.py on stored SMOTE rows (bf16 and fp8), per-phase times of each synced fit
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
@@ -63,6 +64,7 @@ for st in "$@"; do
     benchfp8) step benchfp8 600 python bench.py --storage fp8 ;;
     quicksgd) step quicksgd_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd &&
            step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
+    quicksgdnc) step quicksgd_nocoop 300 env FDX_SGD_COOP=0 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
@@ -142,7 +144,7 @@ for st in "$@"; do
       cd "$R" ;;
     gbdtvar)  # GBDT histogram variants (0 lockstep, 2 split g/h int32 adds, 1 rotated): kernel stats, 10 trees
       cd /tmp && export TMPDIR=/tmp
-      for V in 0 2 1; do
+      for V in ${FDX_GBDT_VARS:-0 3}; do
         export FDX_GBDT_HIST_VAR=$V
         step "gbdtvar_$V" 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/gbdtvar_$V" -o run -- python3 "$R/tools/gbdt_bench.py" --rows 10000000 --trees 10 || exit 1
       done
