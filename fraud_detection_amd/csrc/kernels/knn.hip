@@ -15,6 +15,7 @@
 // K-index layout: MFMA step s, slot h <-> feature 16h + s, so each lane's operand for all 16
 // steps is 16 CONTIGUOUS floats of one row (four 16 B loads).
 #include <cmath>
+#include <cstdlib>
 
 #include "common.h"
 #include "launchers.h"
@@ -941,6 +942,332 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict_
   }
 }
 
+
+// ---- bf16x3 scores + register top-K' + exact verification ("b3top") -------------------------
+// The fp32 engine's structure (one wave = 32 queries x 32-candidate tiles, per-lane LDS queue and
+// top list, the union threshold of the two half-lists) on the bf16x3 approximate score of
+// knn_collect_kernel (6 x v_mfma_f32_32x32x16_bf16 per tile = 192 SIMD cycles instead of the fp32
+// chain's 1024), with NO per-candidate fp32 work and no global lists in the tile loop: the per-lane
+// lists hold APPROXIMATE scores, kTopP = 8 of them (more than k).  Exactness comes at the end
+// (knn_b3top_final_kernel): the per-slice lists are merged to the query's top kTopP approximate
+// candidates, those are re-scored exactly (knn_rerank_kernel's fmaf chain) and their exact top k is
+// returned when it is PROVABLY the exact top k of every candidate:
+//   a candidate outside the merged list was filtered against, or evicted by, kTopP entries at least
+//   as good (seeds included: slice 0 lists them or kTopP better ones), so its approx <= a_P (the
+//   merged list's last approximate score) and its exact score <= a_P + m, m the largest margin the
+//   query met (m = 2^-14 (||q|| tmax + 0.5 tmax^2) >= 4x the bf16x3 error bound, knn_collect_kernel).
+//   If the exact k-th best s_k > a_P + m, nothing outside can reach it -- ties included.
+// Otherwise (k-th and kTopP-th within the margin: near-duplicates) the query takes an exact scan of
+// every candidate.  Slices > 0 seed their threshold with slice 0's first kSeedTiles tiles (flagged
+// entries, never output), sparing each slice its fill phase, so the grid can hold enough slices to
+// put ~6 waves on every SIMD.
+constexpr int kTopP = 8;
+constexpr int kSeedFlag = 0x40000000;
+
+__device__ __forceinline__ float union_kth(const float (&bs)[kTopP]) {
+  // kTopP-th best of the union of this lane's and its partner's (other half) sorted lists
+  float ps[kTopP];
+#pragma unroll
+  for (int k = 0; k < kTopP; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
+  int ia = 0, ib = 0;
+  float kth = kNegBig;
+#pragma unroll
+  for (int k = 0; k < kTopP; ++k) {
+    float a = kNegBig, b = kNegBig;
+#pragma unroll
+    for (int u = 0; u < kTopP; ++u) { if (u == ia) a = bs[u]; if (u == ib) b = ps[u]; }
+    const bool ta = a >= b;
+    kth = ta ? a : b;
+    ia += ta ? 1 : 0;
+    ib += ta ? 0 : 1;
+  }
+  return kth;
+}
+
+// Merge two sorted (score desc, index asc) lists of N into the best N (static indices).
+template <int N>
+__device__ __forceinline__ void merge_sorted(float (&bs)[N], int (&bi)[N], const float (&os)[N], const int (&oi)[N]) {
+  float ns[N];
+  int ni[N];
+  int ia = 0, ib = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
+    float a = kNegBig, b = kNegBig;
+    int ai = 0x7fffffff, bj = 0x7fffffff;
+#pragma unroll
+    for (int u = 0; u < N; ++u) {
+      if (u == ia) { a = bs[u]; ai = bi[u]; }
+      if (u == ib) { b = os[u]; bj = oi[u]; }
+    }
+    const bool ta = !better(b, bj, a, ai);
+    ns[k] = ta ? a : b;
+    ni[k] = ta ? ai : bj;
+    ia += ta ? 1 : 0;
+    ib += ta ? 0 : 1;
+  }
+#pragma unroll
+  for (int k = 0; k < N; ++k) { bs[k] = ns[k]; bi[k] = ni[k]; }
+}
+
+template <int QF = kQFlush>
+__global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restrict__ Q, const uint4* __restrict__ Qhl,
+                                                          const uint4* __restrict__ Chl,
+                                                          const float* __restrict__ tmax, int mq, int mc_pad, int mc,
+                                                          int64_t self_offset, float* __restrict__ ws_s,
+                                                          int* __restrict__ ws_i, float* __restrict__ ws_m) {
+  const int lane = threadIdx.x;
+  const int h = lane >> 5, j = lane & 31;
+  const int qg = blockIdx.x * 32 + j;
+  const int64_t self_c = self_offset >= 0 ? self_offset + qg : -1;
+  float qn;
+  {  // ||q|| over the 30 feature columns: half h sums columns 16h .. 16h + 15
+    const float4* p = reinterpret_cast<const float4*>(Q + (int64_t)qg * kCols + 16 * h);
+    float s2 = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 v = p[k];
+      s2 = fmaf(v.x, v.x, s2);
+      s2 = fmaf(v.y, v.y, s2);
+      if (h == 0 || k < 3) {  // columns 30, 31 (query 1 / 0) are not features
+        s2 = fmaf(v.z, v.z, s2);
+        s2 = fmaf(v.w, v.w, s2);
+      }
+    }
+    s2 += __shfl_xor(s2, 32, kWave);
+    qn = sqrtf(s2) * 1.0001f;
+  }
+  const uint4* qr = Qhl + (int64_t)qg * 8;
+  const bf16x8_t qh0 = __builtin_bit_cast(bf16x8_t, qr[h]), qh1 = __builtin_bit_cast(bf16x8_t, qr[2 + h]);
+  const bf16x8_t ql0 = __builtin_bit_cast(bf16x8_t, qr[4 + h]), ql1 = __builtin_bit_cast(bf16x8_t, qr[6 + h]);
+  float bs[kTopP];
+  int bi[kTopP];
+#pragma unroll
+  for (int k = 0; k < kTopP; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+  float thr = qg < mq ? kNegBig : __builtin_inff();
+  float mgmax = 0.0f;  // the largest candidate-tile norm this lane met (its margin bounds every tile's)
+  constexpr int kCap = QF - 1 + 16 + 1;
+  __shared__ int2 qent[kCap * kWave];  // (approx bits, candidate index) at [slot * 64 + lane]
+  int qn_ = 0;
+  auto flush = [&]() {
+    for (int e = 0; __any(e < qn_); ++e) {
+      if (e < qn_) {
+        const int2 v = qent[e * kWave + lane];
+        topk_insert<kTopP>(bs, bi, __int_as_float(v.x), v.y);
+      }
+    }
+    qn_ = 0;
+    const float kth = union_kth(bs);
+    thr = qg < mq ? kth : __builtin_inff();
+  };
+  const int all_tiles = mc_pad / 32;
+  const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
+  const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  auto fetch = [&](int t, uint4 (&a)[4], float& tmv) {
+    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
+    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
+    tmv = tmax[t];
+  };
+  auto approx = [&](const uint4 (&c)[4]) -> f32x16_t {
+    const bf16x8_t ch0 = __builtin_bit_cast(bf16x8_t, c[0]), ch1 = __builtin_bit_cast(bf16x8_t, c[1]);
+    const bf16x8_t cl0 = __builtin_bit_cast(bf16x8_t, c[2]), cl1 = __builtin_bit_cast(bf16x8_t, c[3]);
+    f32x16_t acc = {};
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(cl1, qh1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, ql0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, ql1, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch0, qh0, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ch1, qh1, acc, 0, 0, 0);
+    return acc;
+  };
+  // seed: slice 0's first tiles (flagged: they set the threshold, slice 0 outputs them)
+  if (blockIdx.y > 0) {
+    const int ns0 = (int)((int64_t)all_tiles / gridDim.y);
+    const int nseed = ns0 < kSeedTiles ? ns0 : kSeedTiles;
+    for (int t = 0; t < nseed; ++t) {
+      uint4 c[4];
+      float tm;
+      fetch(t, c, tm);
+      const f32x16_t acc = approx(c);
+      mgmax = fmaxf(mgmax, tm);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int ci = t * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+        if (ci != self_c && ci < mc) topk_insert<kTopP>(bs, bi, acc[r], ci | kSeedFlag);
+      }
+    }
+    const float kth = union_kth(bs);
+    thr = qg < mq ? kth : __builtin_inff();
+  }
+  uint4 cv[4], cv2[4];
+  float tmn = 0.0f, tmn2 = 0.0f;
+  if (t_lo < t_hi) fetch(t_lo, cv, tmn);
+  if (t_lo + 1 < t_hi) fetch(t_lo + 1, cv2, tmn2);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int c0 = t * 32;
+    const f32x16_t acc = approx(cv);
+    const float tm = tmn;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cv[u] = cv2[u];
+    tmn = tmn2;
+    if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
+    mgmax = fmaxf(mgmax, tm);
+    float mx = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
+#pragma unroll
+    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, acc[r]), acc[r + 1]);
+    mx = fmaxf(mx, acc[15]);
+    if (!__any(mx >= thr)) continue;
+    const int cbase = c0 + 4 * h;
+    int qe = qn_ * kWave + lane;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ci = cbase + (r & 3) + 8 * (r >> 2);
+      const bool pass = acc[r] >= thr && ci != self_c && ci < mc;
+      if (__any(pass)) {
+        if (pass) {
+          qent[qe] = make_int2(__float_as_int(acc[r]), ci);
+          qe += kWave;
+        }
+      }
+    }
+    qn_ = (qe - lane) / kWave;
+    if (__any(qn_ >= QF)) flush();
+  }
+  flush();
+  // the margin is monotone in the tile norm: the largest norm's margin bounds every tile's
+  float mg = kMarginScale * fmaf(qn, mgmax, 0.5f * mgmax * mgmax);
+  mg = fmaxf(mg, __shfl_xor(mg, 32, kWave));
+  // merge the two halves; drop the seeds (lanes h == 0 write)
+  float os[kTopP];
+  int oi[kTopP];
+#pragma unroll
+  for (int k = 0; k < kTopP; ++k) {
+    os[k] = __shfl_xor(bs[k], 32, kWave);
+    oi[k] = __shfl_xor(bi[k], 32, kWave);
+  }
+  merge_sorted<kTopP>(bs, bi, os, oi);
+  if (h == 0 && qg < mq) {  // the non-seed entries, still sorted, then empty slots
+    const int64_t o = ((int64_t)blockIdx.y * mq + qg) * kTopP;
+    int w = 0;
+#pragma unroll
+    for (int k = 0; k < kTopP; ++k) {
+      if (bi[k] != 0x7fffffff && !(bi[k] & kSeedFlag)) {
+        ws_s[o + w] = bs[k];
+        ws_i[o + w] = bi[k];
+        ++w;
+      }
+    }
+    for (; w < kTopP; ++w) {
+      ws_s[o + w] = kNegBig;
+      ws_i[o + w] = 0x7fffffff;
+    }
+    ws_m[(int64_t)blockIdx.y * mq + qg] = mg;
+  }
+}
+
+// Per query: lps lanes (a power of two >= max(nsplit, kTopP)) merge the slices' approximate lists,
+// re-score the best kTopP exactly and verify (see above); a query that fails the check is answered
+// by an exact scan of every candidate by its lps lanes.
+template <int K>
+__global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __restrict__ Q, const float* __restrict__ C,
+                                                              int mq, int mc, int nsplit, int lps_log2,
+                                                              int64_t self_offset, const float* __restrict__ ws_s,
+                                                              const int* __restrict__ ws_i,
+                                                              const float* __restrict__ ws_m,
+                                                              int* __restrict__ out_idx, float* __restrict__ out_score,
+                                                              int* __restrict__ n_scan) {
+  const int lps = 1 << lps_log2;
+  const int gl = blockIdx.x * 256 + threadIdx.x;
+  const int q = gl >> lps_log2, sl = gl & (lps - 1);
+  const bool live = q < mq;
+  const int qq = live ? q : 0;
+  const int64_t self_c = self_offset >= 0 ? self_offset + qq : -1;
+  float as[kTopP];
+  int ai[kTopP];
+  float mg = 0.0f;
+#pragma unroll
+  for (int k = 0; k < kTopP; ++k) { as[k] = kNegBig; ai[k] = 0x7fffffff; }
+  if (live && sl < nsplit) {
+    const int64_t o = ((int64_t)sl * mq + qq) * kTopP;
+#pragma unroll
+    for (int k = 0; k < kTopP; ++k) { as[k] = ws_s[o + k]; ai[k] = ws_i[o + k]; }
+    mg = ws_m[(int64_t)sl * mq + qq];
+  }
+  for (int off = 1; off < lps; off <<= 1) {
+    float os[kTopP];
+    int oi[kTopP];
+#pragma unroll
+    for (int k = 0; k < kTopP; ++k) {
+      os[k] = __shfl_xor(as[k], off, kWave);
+      oi[k] = __shfl_xor(ai[k], off, kWave);
+    }
+    merge_sorted<kTopP>(as, ai, os, oi);
+    mg = fmaxf(mg, __shfl_xor(mg, off, kWave));
+  }
+  float qv[kCols];
+  {
+    const float4* p = reinterpret_cast<const float4*>(Q + (int64_t)qq * kCols);
+#pragma unroll
+    for (int k = 0; k < kCols / 4; ++k) {
+      const float4 v = p[k];
+      qv[4 * k] = v.x; qv[4 * k + 1] = v.y; qv[4 * k + 2] = v.z; qv[4 * k + 3] = v.w;
+    }
+  }
+  auto exact = [&](int ci) -> float {  // knn_rerank_kernel's re-score: columns 0..31 in order
+    const float4* c = reinterpret_cast<const float4*>(C + (int64_t)ci * kCols);
+    float acc = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kCols / 4; ++k) {
+      const float4 v = c[k];
+      acc = fmaf(qv[4 * k], v.x, acc);
+      acc = fmaf(qv[4 * k + 1], v.y, acc);
+      acc = fmaf(qv[4 * k + 2], v.z, acc);
+      acc = fmaf(qv[4 * k + 3], v.w, acc);
+    }
+    return acc;
+  };
+  // lane sl < kTopP re-scores merged entry sl; every lane of the query then ranks all kTopP
+  int my = 0x7fffffff;
+#pragma unroll
+  for (int u = 0; u < kTopP; ++u) if (u == sl) my = ai[u];
+  const float ex = (my != 0x7fffffff && sl < kTopP) ? exact(my) : kNegBig;
+  const int base = threadIdx.x & ~(lps - 1) & (kWave - 1);
+  float bs[K];
+  int bi[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+#pragma unroll
+  for (int u = 0; u < kTopP; ++u) {
+    const float e = __shfl(ex, base + u, kWave);
+    if (ai[u] != 0x7fffffff) topk_insert<K>(bs, bi, e, ai[u]);
+  }
+  // proof of exactness: the exact k-th best beats every unlisted candidate's upper bound
+  const bool ok = !(as[kTopP - 1] > kNegBig) || bs[K - 1] > as[kTopP - 1] + mg;
+  if (live && !ok) {  // uniform over the query's lps lanes
+    if (sl == 0 && n_scan != nullptr) atomicAdd(n_scan, 1);
+#pragma unroll
+    for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
+    for (int ci = sl; ci < mc; ci += lps)
+      if (ci != self_c) topk_insert<K>(bs, bi, exact(ci), ci);
+    for (int off = 1; off < lps; off <<= 1) {
+      float os[K];
+      int oi[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        os[k] = __shfl_xor(bs[k], off, kWave);
+        oi[k] = __shfl_xor(bi[k], off, kWave);
+      }
+      merge_sorted<K>(bs, bi, os, oi);
+    }
+  }
+  if (live && sl == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      out_idx[(int64_t)q * K + k] = bi[k];
+      if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+    }
+  }
+}
+
 }  // namespace
 
 int merge_log2(int nsplit) {
@@ -1127,6 +1454,55 @@ void launch_knn_topk3r(const float* Q, const void* Qhl, int mq_pad, int mq, cons
   }
 #undef FDX_KNN3R
   check_launch("knn_topk3r");
+}
+
+int knn_b3top_splits(int mq_pad, int mc_pad) {
+  // As many slices as fill the resident one-wave workgroups in ONE round (the seeds spare each slice
+  // its fill phase; 108 VGPRs: 4 waves per SIMD), >= 8 tiles each, <= 32 (the final merge's lanes per
+  // query).  FDX_KNN_B3_SPLITS: lab override.
+  static const int cap = resident_cap(knn_b3top_kernel<>, kWave);
+  static const int forced = [] {
+    const char* e = std::getenv("FDX_KNN_B3_SPLITS");
+    return e != nullptr ? std::atoi(e) : 0;
+  }();
+  const int qblocks = mq_pad / 32, tiles = mc_pad / 32;
+  int s = forced > 0 ? forced : cap / (qblocks > 0 ? qblocks : 1);
+  if (s > 32) s = 32;
+  if (s > tiles / 8) s = tiles / 8;
+  if (s < 1) s = 1;
+  return s;
+}
+
+void launch_knn_b3top(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
+                      const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
+                      float* out_score, float* ws_s, int* ws_i, float* ws_m, int* n_scan, int nsplit,
+                      hipStream_t stream) {
+  if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_b3top: pads must be x32");
+  if (mq > mq_pad || mc > mc_pad || nsplit < 1 || nsplit > 32 || ws_s == nullptr || ws_i == nullptr || ws_m == nullptr)
+    throw std::runtime_error("knn_b3top: bad shapes or missing [nsplit][mq][8] workspaces");
+  if (k < 1 || k > kTopP) throw std::runtime_error("knn_b3top: k must be in [1, 8]");
+  const dim3 grid(mq_pad / 32, nsplit);
+  knn_b3top_kernel<><<<grid, kWave, 0, stream>>>(Q, reinterpret_cast<const uint4*>(Qhl),
+                                                  reinterpret_cast<const uint4*>(Chl), tmax, mq, mc_pad, mc,
+                                                  self_offset, ws_s, ws_i, ws_m);
+  int lg = merge_log2(nsplit);
+  if (lg < 3) lg = 3;  // >= kTopP lanes per query: lane u re-scores merged entry u
+  const unsigned fb = (unsigned)((((int64_t)mq << lg) + 255) / 256);
+#define FDX_KNNB3(KK)                                                                                         \
+  knn_b3top_final_kernel<KK><<<fb, 256, 0, stream>>>(Q, C, mq, mc, nsplit, lg, self_offset, ws_s, ws_i, ws_m, \
+                                                     out_idx, out_score, n_scan)
+  switch (k) {
+    case 1: FDX_KNNB3(1); break;
+    case 2: FDX_KNNB3(2); break;
+    case 3: FDX_KNNB3(3); break;
+    case 4: FDX_KNNB3(4); break;
+    case 5: FDX_KNNB3(5); break;
+    case 6: FDX_KNNB3(6); break;
+    case 7: FDX_KNNB3(7); break;
+    default: FDX_KNNB3(8); break;
+  }
+#undef FDX_KNNB3
+  check_launch("knn_b3top");
 }
 
 void launch_knn_topk(const float* Q, int mq_pad, int mq, const float* C,

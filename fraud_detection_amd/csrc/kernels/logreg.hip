@@ -1465,9 +1465,10 @@ __global__ __launch_bounds__(64) void sgd_update_fixed_kernel(const long long* _
 // "8-B agent atomics both sides" form, one workgroup per CU.  Sets rotate over three: set t is read
 // after barrier t; set t + 1 is zeroed by block 0 during step t (after barrier t - 1, when every
 // block has finished reading it as set t - 2; before block 0 arrives at barrier t).
-// Residency: the launch goes through hipLaunchCooperativeKernel (it refuses a grid the occupancy
-// query says cannot be co-resident; the caller then launches per step), but co-residency can still
-// fail at run time when another stream or process holds CUs.  So every wait is bounded: a block
+// Residency: the grid is sized from the occupancy query (FDX_SGD_COOP=1 launches it through
+// hipLaunchCooperativeKernel, which re-checks that at launch and refuses an oversize grid; the caller
+// then launches per step), but co-residency can still fail at run time when another stream or
+// process holds CUs.  So every wait is bounded: a block
 // whose barrier poll times out (or that sees another block's timeout) raises the workspace's fault
 // word and leaves; blocks dispatched after that exit at once; nothing is published from a faulted
 // grid.  The one-block recovery launch queued behind every persistent launch (sgd_recover_kernel)
@@ -2165,10 +2166,14 @@ int launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, c
     const char* e = std::getenv("FDX_SGD_PERSIST_CFG");
     return (e != nullptr && e[0] == '1') ? 1 : 2;
   }();
-  // FDX_SGD_COOP=0 (lab): a plain launch of the same grid (same residency, no launch-time check)
+  // FDX_SGD_COOP=1: hipLaunchCooperativeKernel, which checks the grid against the occupancy query
+  // at launch (hipErrorCooperativeLaunchTooLarge -> the caller runs per step).  Off by default: the
+  // grid is already sized from that query (sgd_persist_blocks), so the check never refuses it, and
+  // it cost ~30 us per fit at the bench shape (medians 1.097 vs 1.067 ms, profiles/r6_a); run-time
+  // co-residency is covered by the bounded barrier + recovery launch either way.
   static const bool coop = [] {
     const char* e = std::getenv("FDX_SGD_COOP");
-    return !(e != nullptr && e[0] == '0');
+    return e != nullptr && e[0] == '1';
   }();
   const void* kern = nullptr;
   if (fp8) {  // fp8 tiles are half the bytes: its pass keeps two tiles in flight in the same registers

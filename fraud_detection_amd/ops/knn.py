@@ -32,6 +32,10 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 #   bf16x3r the same filter with no fp32 work in the tile loop: passing candidates are appended to
 #           per-lane lists under a provable lower-bound threshold, and a second kernel re-scores
 #           the listed candidates exactly (8 lanes per query) -- knn.hip knn_collect_kernel.
+#   b3top   the bf16x3 score with register top-8 APPROXIMATE lists (no lists in memory, no fp32 work
+#           in the tile loop, seeded slices so ~6 waves fill every SIMD); one merge kernel re-scores
+#           each query's 8 best exactly and proves the exact top-k from the error margin (else an
+#           exact scan of that query) -- knn.hip knn_b3top_kernel.
 # Measured on MI355X from 13.6k to 170k minority rows (profiles/r2_s3i/knn_engines.jsonl): fp32
 # beat fp32lds (0.66-0.99x) and bf16x3 (0.86-0.96x) at every size.  bf16x3r (round 5,
 # profiles/r5_k, r5_o): at the DP=8 global-scope rank (13.6k queries x 108.8k candidates) 0.78 ms
@@ -46,7 +50,7 @@ def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:
     e = engine or os.environ.get("FDX_KNN", "auto")
     if e == "auto":
         return "bf16x3r" if mc >= KNN_BF16X3_MIN_CANDIDATES else "fp32"
-    if e not in ("fp32", "fp32lds", "bf16x3", "bf16x3r"):
+    if e not in ("fp32", "fp32lds", "bf16x3", "bf16x3r", "b3top"):
         raise ValueError(f"unknown k-NN engine {e!r}")
     return e
 
@@ -120,9 +124,9 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         ns = max(1, int(nsplit))
     else:
         ns = {"fp32": m.knn_splits, "fp32lds": m.knn_lds_splits, "bf16x3": m.knn3_splits,
-              "bf16x3r": m.knn3r_splits}[eng](mq_pad, mc_pad)
+              "bf16x3r": m.knn3r_splits, "b3top": m.knn_b3top_splits}[eng](mq_pad, mc_pad)
     ws_s = ws_i = None
-    if ns > 1 and eng != "bf16x3r":
+    if ns > 1 and eng not in ("bf16x3r", "b3top"):
         ws_s = torch.empty((ns, mq, k), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, k), device=Q.device, dtype=torch.int32)
     if eng == "fp32":
@@ -138,7 +142,17 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
         m.knn_split(ptr(Cp), mc_pad, 0, ptr(Chl), ptr(tmax), s)
         m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
-    if eng == "bf16x3r":
+    if eng == "b3top":
+        ns = min(ns, 32)
+        ws_s = torch.empty((ns, mq, 8), device=Q.device, dtype=torch.float32)
+        ws_i = torch.empty((ns, mq, 8), device=Q.device, dtype=torch.int32)
+        ws_m = torch.empty((ns, mq), device=Q.device, dtype=torch.float32)
+        nscan = torch.zeros(1, device=Q.device, dtype=torch.int32) if _diag is not None else None
+        m.knn_b3top(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
+                    int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ptr(ws_m), ptr(nscan), ns, s)
+        if _diag is not None:  # queries answered by the exact scan (diagnostics; synchronises)
+            _diag.update(nsplit=ns, exact_scans=int(nscan.item()))
+    elif eng == "bf16x3r":
         nb = ns * (mq_pad // 32) * 64
         lists = torch.empty(nb * m.KNN3R_LIST_CAP * 2, device=Q.device, dtype=torch.int32)  # (lb, index)
         counts = torch.empty(nb, device=Q.device, dtype=torch.int32)

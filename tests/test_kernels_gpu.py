@@ -293,7 +293,7 @@ def test_knn_topk_exact(dev, mq, k):
     assert not np.any(idx == (np.arange(mq)[:, None] + off))  # self excluded
 
 
-@pytest.mark.parametrize("engine", ["bf16x3", "bf16x3r", "fp32lds"])
+@pytest.mark.parametrize("engine", ["bf16x3", "bf16x3r", "fp32lds", "b3top"])
 @pytest.mark.parametrize("mq,k,scale", [(400, 5, 1.0), (2500, 8, 1.0), (3000, 5, 40.0)])
 def test_knn_engine_exact(dev, mq, k, scale, engine):
     """The bf16x3 filter engine returns the exact fp32 ranking: same lists as the oracle (up to
@@ -331,6 +331,9 @@ def test_knn_engines_agree_with_ties_and_auto_selection(dev):
     for ns in (1, 2, 5):  # collect + re-rank: bf16x3's exact re-score, so bit-identical to it
         r, sr = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="bf16x3r", nsplit=ns)
         assert torch.equal(a, r) and torch.equal(sb, sr)
+    for ns in (1, 2, 5, 32):  # register top-8 + exact verification: bf16x3's exact re-score too
+        r, sr = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="b3top", nsplit=ns)
+        assert torch.equal(a, r) and torch.equal(sb, sr)
     for ns in (1, 3, 40):  # the LDS engine runs the same MFMA chain: bit-identical lists + scores
         c, sc = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32lds", nsplit=ns)
         assert torch.equal(a, c) and torch.equal(sa, sc)
@@ -339,7 +342,7 @@ def test_knn_engines_agree_with_ties_and_auto_selection(dev):
     Cb = torch.from_numpy(rng.normal(size=(70_000, 32)).astype(np.float32)).to(dev)
     Qb = Cb[:256].contiguous()
     ia = K.knn_topk(Qb, Cb, k=5, self_offset=0, engine="fp32")
-    for eng in ("fp32lds", "bf16x3", "bf16x3r"):
+    for eng in ("fp32lds", "bf16x3", "bf16x3r", "b3top"):
         ib = K.knn_topk(Qb, Cb, k=5, self_offset=0, engine=eng)
         assert (ia == ib).all(1).float().mean().item() > 0.99
 
@@ -375,6 +378,34 @@ def test_knn_collect_list_overflow_falls_back_to_exact_scan(dev):
         for q in range(100):
             want = [c for c in range(7) if c != q][:5]
             assert list(idx[q]) == want, (q, idx[q])
+
+
+def test_knn_b3top_proof_fails_over_to_exact_scan(dev):
+    """All-equal candidates: the approximate top-8 cannot prove the exact top-5 (every score ties the
+    8th), so every query takes the exact scan and still returns the 5 smallest indices; on the bench's
+    minority rows the proof holds for (nearly) every query."""
+    C = torch.ones((3000, 32), dtype=torch.float32, device=dev)
+    C[:, 30:] = 0.0
+    Q = C[:100].contiguous()
+    for ns in (None, 1, 4):
+        dg = {}
+        idx = K.knn_topk(Q, C, k=5, self_offset=0, engine="b3top", nsplit=ns, _diag=dg).cpu().numpy()
+        assert dg["exact_scans"] == 100, dg
+        for q in range(100):
+            assert list(idx[q]) == [c for c in range(7) if c != q][:5], (q, idx[q])
+    from fraud_detection_amd.data.synthetic import separable
+
+    X, y = separable(2_000_000, seed=1000, device=dev)
+    xm = X[y == 1]
+    xm = (xm - X.mean(0)) / X.std(0)
+    Cm = torch.zeros((xm.shape[0], 32), device=dev)
+    Cm[:, :30] = xm
+    Cm[:, 30] = 1.0
+    dg = {}
+    a = K.knn_topk(Cm, Cm, k=5, self_offset=0, engine="fp32")
+    b = K.knn_topk(Cm, Cm, k=5, self_offset=0, engine="b3top", _diag=dg)
+    assert dg["exact_scans"] <= max(2, xm.shape[0] // 1000), dg
+    assert (a == b).all(1).float().mean().item() > 0.999
 
 
 @pytest.mark.parametrize("nsplit", [2, 3, 7, 40])

@@ -22,7 +22,7 @@
 #   benchfp8     bench.py --storage fp8
 #   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
 #   quicksgd     the same with the SGD solver
-#   quicksgdnc   quicksgd bf16 with a plain (not cooperative) persistent launch (FDX_SGD_COOP=0)
+#   quicksgdnc   quicksgd bf16 with the cooperative persistent launch (FDX_SGD_COOP=1)
 #   pmc          two PMC passes over a short bench
 #   pmcfp8       logreg pass counters + kernel stats with fp8 and with bf16 rows
 #   gbdt         tools/gbdt_bench.py at the bench shape; gbdtprof: its kernel trace (20 trees)
@@ -64,7 +64,7 @@ for st in "$@"; do
     benchfp8) step benchfp8 600 python bench.py --storage fp8 ;;
     quicksgd) step quicksgd_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd &&
            step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
-    quicksgdnc) step quicksgd_nocoop 300 env FDX_SGD_COOP=0 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
+    quicksgdnc) step quicksgd_coop 300 env FDX_SGD_COOP=1 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;

@@ -55,7 +55,7 @@ def main():
         return float(np.median([ev[i].elapsed_time(ev[i + 1]) for i in range(a.reps)]))
 
     splitter = {"fp32": "knn_splits", "fp32lds": "knn_lds_splits", "bf16x3": "knn3_splits",
-                "bf16x3r": "knn3r_splits"}
+                "bf16x3r": "knn3r_splits", "b3top": "knn_b3top_splits"}
     for name, (Q, Cc, off) in shapes.items():
         mq, mc = Q.shape[0], Cc.shape[0]
         ref = K.knn_topk(Q, Cc, 5, off, engine="fp32")
@@ -67,12 +67,13 @@ def main():
                 f = lambda: K.knn_topk(Q, Cc, 5, off, engine=eng, nsplit=ns)  # noqa: E731
                 got = f()
                 ms = timed(f)
-                if eng == "bf16x3r":
+                if eng in ("bf16x3r", "b3top"):
                     dg = {}
                     K.knn_topk(Q, Cc, 5, off, engine=eng, nsplit=ns, _diag=dg)
                     dg.pop("counts", None)
                     print(json.dumps({name: {"engine": eng, "nsplit": ns, "lists": dg}}), flush=True)
                 case = {"engine": eng, "nsplit": ns, "ms": round(ms, 4),
+                        "lists_match_frac": float((got == ref).all(1).float().mean().item()),
                         "tflops_equiv": round(2.0 * mq * mc * 32 / (ms * 1e-3) / 1e12, 1),
                         "lists_equal": bool((got == ref).all().item())}
                 rec["cases"].append(case)

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--seeds", default="1000,1001")
     ap.add_argument("--storage", default="bf16")
     ap.add_argument("--cv", action="store_true")
+    ap.add_argument("--order", action="store_true",
+                    help="row-order probe: the pipeline fit on the CV job's fold-sorted rows, and both on a "
+                         "shuffled Time column")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
@@ -50,6 +53,27 @@ def main():
                      "fold_rows": r.fold_rows, "final_steps": int(r.final.fit.n_iter),
                      "final_grad_max": float(r.final.fit.grad_max)}
         print(json.dumps(out["cv"]), flush=True)
+    if a.order:
+        from fraud_detection_amd.models.cv import DeviceCV
+
+        X, y = separable(8_000_000, seed=1000, device=dev)
+        cv = DeviceCV(TrainConfig(solver="sgd", storage=a.storage, seed=42))
+        cv.run(X, y)
+        perm = cv.perm
+        res = {}
+        for name, (Xo, yo) in {"orig": (X, y), "fold_sorted": (X[perm], y[perm]),
+                               "row_shuffled": (lambda p: (X[p], y[p]))(torch.randperm(X.shape[0], device=dev))}.items():
+            f = DevicePipeline(TrainConfig(solver="sgd", storage=a.storage, seed=42)).fit(Xo.contiguous(), yo.contiguous()).fit
+            res[name] = {"steps": int(f.n_iter), "grad_max": float(f.grad_max)}
+            print(name, json.dumps(res[name]), flush=True)
+        Xs = X.clone()
+        Xs[:, 0] = Xs[torch.randperm(X.shape[0], device=dev), 0]
+        cv2 = DeviceCV(TrainConfig(solver="sgd", storage=a.storage, seed=42))
+        r2 = cv2.run(Xs, y)
+        res["cv_time_shuffled"] = {"fold_iters": r2.fold_iters, "final_steps": int(r2.final.fit.n_iter),
+                                   "final_grad_max": float(r2.final.fit.grad_max)}
+        print("cv_time_shuffled", json.dumps(res["cv_time_shuffled"]), flush=True)
+        out["order"] = res
     if a.json:
         with open(a.json, "w") as fh:
             json.dump(out, fh, indent=1)
