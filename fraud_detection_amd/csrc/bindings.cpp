@@ -768,10 +768,10 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
   m.def("knn_b3top_splits", [](int mq_pad, int mc_pad) { return fdx::knn_b3top_splits(mq_pad, mc_pad); });
   m.def("knn_b3top", [](u Q, u Qhl, int mq_pad, int mq, u C, u Chl, u tmax, int mc_pad, int mc, int64_t self_off,
-                        int k, u oidx, u oscore, u wss, u wsi, u wsm, u nscan, int nsplit, u s) {
+                        int k, u oidx, u oscore, u wss, u wsi, u wsm, u fail, int nsplit, u s) {
     fdx::launch_knn_b3top(P<const float>(Q), P<const void>(Qhl), mq_pad, mq, P<const float>(C), P<const void>(Chl),
                           P<const float>(tmax), mc_pad, mc, self_off, k, P<int>(oidx), P<float>(oscore),
-                          P<float>(wss), P<int>(wsi), P<float>(wsm), P<int>(nscan), nsplit, S(s));
+                          P<float>(wss), P<int>(wsi), P<float>(wsm), P<int>(fail), nsplit, S(s));
   });
   m.def("knn3r_splits", [](int mq_pad, int mc_pad) { return fdx::knn3r_splits(mq_pad, mc_pad); });
   m.attr("KNN3R_LIST_CAP") = fdx::knn3r_list_cap();

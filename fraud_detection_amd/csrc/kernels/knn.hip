@@ -954,11 +954,15 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict_
 // returned when it is PROVABLY the exact top k of every candidate:
 //   a candidate outside the merged list was filtered against, or evicted by, kTopP entries at least
 //   as good (seeds included: slice 0 lists them or kTopP better ones), so its approx <= a_P (the
-//   merged list's last approximate score) and its exact score <= a_P + m, m the largest margin the
-//   query met (m = 2^-14 (||q|| tmax + 0.5 tmax^2) >= 4x the bf16x3 error bound, knn_collect_kernel).
-//   If the exact k-th best s_k > a_P + m, nothing outside can reach it -- ties included.
-// Otherwise (k-th and kTopP-th within the margin: near-duplicates) the query takes an exact scan of
-// every candidate.  Slices > 0 seed their threshold with slice 0's first kSeedTiles tiles (flagged
+//   merged list's last approximate score); its exact score is within its tile's margin m_t =
+//   2^-14 (||q|| tmax_t + 0.5 tmax_t^2) (>= 4x the bf16x3 error bound, knn_collect_kernel) of that.
+//   Per lane and tile: a tile none of whose 16 entries reached the threshold bounds its candidates
+//   by U = max (tile max approx + m_t); a tile with an entry at or above it by a_P + M, M = max m_t
+//   over such tiles (the tiles near the query -- a far outlier tile, whose norm sets a large margin,
+//   lands in U with its low scores).  If the exact k-th best s_k > max(U, a_P + M), nothing outside
+//   the list can reach it -- ties included.
+// Otherwise (near-ties within the margin) the query is queued for knn_b3top_scan_kernel: one
+// workgroup re-scans every candidate exactly.  Slices > 0 seed their threshold with slice 0's first kSeedTiles tiles (flagged
 // entries, never output), sparing each slice its fill phase, so the grid can hold enough slices to
 // put ~6 waves on every SIMD.
 constexpr int kTopP = 8;
@@ -1044,7 +1048,8 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
 #pragma unroll
   for (int k = 0; k < kTopP; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
   float thr = qg < mq ? kNegBig : __builtin_inff();
-  float mgmax = 0.0f;  // the largest candidate-tile norm this lane met (its margin bounds every tile's)
+  float ub_f = kNegBig;  // U: max over this lane's fully filtered tiles of (tile max approx + m_t)
+  float mg_p = 0.0f;     // M: max m_t over this lane's tiles with an entry at or above the threshold
   constexpr int kCap = QF - 1 + 16 + 1;
   __shared__ int2 qent[kCap * kWave];  // (approx bits, candidate index) at [slot * 64 + lane]
   int qn_ = 0;
@@ -1088,7 +1093,7 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
       float tm;
       fetch(t, c, tm);
       const f32x16_t acc = approx(c);
-      mgmax = fmaxf(mgmax, tm);
+      (void)tm;  // seeds are slice 0's candidates: slice 0's bookkeeping bounds them
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int ci = t * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
@@ -1110,11 +1115,15 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
     for (int u = 0; u < 4; ++u) cv[u] = cv2[u];
     tmn = tmn2;
     if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
-    mgmax = fmaxf(mgmax, tm);
     float mx = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
 #pragma unroll
     for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, acc[r]), acc[r + 1]);
     mx = fmaxf(mx, acc[15]);
+    {
+      const float mt = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
+      if (mx >= thr) mg_p = fmaxf(mg_p, mt);
+      else ub_f = fmaxf(ub_f, mx + mt);  // the self row stays in mx: a valid (if loose) bound
+    }
     if (!__any(mx >= thr)) continue;
     const int cbase = c0 + 4 * h;
     int qe = qn_ * kWave + lane;
@@ -1133,9 +1142,8 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
     if (__any(qn_ >= QF)) flush();
   }
   flush();
-  // the margin is monotone in the tile norm: the largest norm's margin bounds every tile's
-  float mg = kMarginScale * fmaf(qn, mgmax, 0.5f * mgmax * mgmax);
-  mg = fmaxf(mg, __shfl_xor(mg, 32, kWave));
+  ub_f = fmaxf(ub_f, __shfl_xor(ub_f, 32, kWave));
+  mg_p = fmaxf(mg_p, __shfl_xor(mg_p, 32, kWave));
   // merge the two halves; drop the seeds (lanes h == 0 write)
   float os[kTopP];
   int oi[kTopP];
@@ -1160,13 +1168,14 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
       ws_s[o + w] = kNegBig;
       ws_i[o + w] = 0x7fffffff;
     }
-    ws_m[(int64_t)blockIdx.y * mq + qg] = mg;
+    ws_m[2 * ((int64_t)blockIdx.y * mq + qg)] = ub_f;
+    ws_m[2 * ((int64_t)blockIdx.y * mq + qg) + 1] = mg_p;
   }
 }
 
 // Per query: lps lanes (a power of two >= max(nsplit, kTopP)) merge the slices' approximate lists,
-// re-score the best kTopP exactly and verify (see above); a query that fails the check is answered
-// by an exact scan of every candidate by its lps lanes.
+// re-score the best kTopP exactly and verify (see above); a query that fails the check is appended
+// to `fail` (count in fail[0]) for knn_b3top_scan_kernel.
 template <int K>
 __global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __restrict__ Q, const float* __restrict__ C,
                                                               int mq, int mc, int nsplit, int lps_log2,
@@ -1174,7 +1183,7 @@ __global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __res
                                                               const int* __restrict__ ws_i,
                                                               const float* __restrict__ ws_m,
                                                               int* __restrict__ out_idx, float* __restrict__ out_score,
-                                                              int* __restrict__ n_scan) {
+                                                              int* __restrict__ fail) {
   const int lps = 1 << lps_log2;
   const int gl = blockIdx.x * 256 + threadIdx.x;
   const int q = gl >> lps_log2, sl = gl & (lps - 1);
@@ -1183,14 +1192,15 @@ __global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __res
   const int64_t self_c = self_offset >= 0 ? self_offset + qq : -1;
   float as[kTopP];
   int ai[kTopP];
-  float mg = 0.0f;
+  float ub = kNegBig, mg = 0.0f;
 #pragma unroll
   for (int k = 0; k < kTopP; ++k) { as[k] = kNegBig; ai[k] = 0x7fffffff; }
   if (live && sl < nsplit) {
     const int64_t o = ((int64_t)sl * mq + qq) * kTopP;
 #pragma unroll
     for (int k = 0; k < kTopP; ++k) { as[k] = ws_s[o + k]; ai[k] = ws_i[o + k]; }
-    mg = ws_m[(int64_t)sl * mq + qq];
+    ub = ws_m[2 * ((int64_t)sl * mq + qq)];
+    mg = ws_m[2 * ((int64_t)sl * mq + qq) + 1];
   }
   for (int off = 1; off < lps; off <<= 1) {
     float os[kTopP];
@@ -1202,6 +1212,7 @@ __global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __res
     }
     merge_sorted<kTopP>(as, ai, os, oi);
     mg = fmaxf(mg, __shfl_xor(mg, off, kWave));
+    ub = fmaxf(ub, __shfl_xor(ub, off, kWave));
   }
   float qv[kCols];
   {
@@ -1241,14 +1252,60 @@ __global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __res
     if (ai[u] != 0x7fffffff) topk_insert<K>(bs, bi, e, ai[u]);
   }
   // proof of exactness: the exact k-th best beats every unlisted candidate's upper bound
-  const bool ok = !(as[kTopP - 1] > kNegBig) || bs[K - 1] > as[kTopP - 1] + mg;
-  if (live && !ok) {  // uniform over the query's lps lanes
-    if (sl == 0 && n_scan != nullptr) atomicAdd(n_scan, 1);
+  const float bound = fmaxf(ub, as[kTopP - 1] > kNegBig ? as[kTopP - 1] + mg : kNegBig);
+  const bool ok = bs[K - 1] > bound;
+  if (live && !ok && sl == 0) fail[1 + atomicAdd(fail, 1)] = q;  // answered by the scan kernel
+  if (live && sl == 0) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      out_idx[(int64_t)q * K + k] = bi[k];
+      if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+    }
+  }
+}
+
+// The queries whose approximate lists could not prove their exact top k (fail[1 .. fail[0]]): one
+// workgroup per query (grid-stride over the list; an empty list exits at once) scans every candidate
+// with the exact fmaf chain -- 256 lanes, then a butterfly merge per wave and a 4-way merge in LDS.
+template <int K>
+__global__ __launch_bounds__(256) void knn_b3top_scan_kernel(const float* __restrict__ Q, const float* __restrict__ C,
+                                                             int mc, int64_t self_offset, const int* __restrict__ fail,
+                                                             int* __restrict__ out_idx, float* __restrict__ out_score) {
+  const int nf = fail[0];
+  __shared__ float ls[4][K];
+  __shared__ int li[4][K];
+  const int lane = lane_id(), wv = threadIdx.x >> 6;
+  for (int f = blockIdx.x; f < nf; f += gridDim.x) {
+    const int q = fail[1 + f];
+    const int64_t self_c = self_offset >= 0 ? self_offset + q : -1;
+    float qv[kCols];
+    {
+      const float4* p = reinterpret_cast<const float4*>(Q + (int64_t)q * kCols);
+#pragma unroll
+      for (int k = 0; k < kCols / 4; ++k) {
+        const float4 v = p[k];
+        qv[4 * k] = v.x; qv[4 * k + 1] = v.y; qv[4 * k + 2] = v.z; qv[4 * k + 3] = v.w;
+      }
+    }
+    float bs[K];
+    int bi[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-    for (int ci = sl; ci < mc; ci += lps)
-      if (ci != self_c) topk_insert<K>(bs, bi, exact(ci), ci);
-    for (int off = 1; off < lps; off <<= 1) {
+    for (int ci = threadIdx.x; ci < mc; ci += 256) {
+      if (ci == self_c) continue;
+      const float4* c = reinterpret_cast<const float4*>(C + (int64_t)ci * kCols);
+      float acc = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kCols / 4; ++k) {
+        const float4 v = c[k];
+        acc = fmaf(qv[4 * k], v.x, acc);
+        acc = fmaf(qv[4 * k + 1], v.y, acc);
+        acc = fmaf(qv[4 * k + 2], v.z, acc);
+        acc = fmaf(qv[4 * k + 3], v.w, acc);
+      }
+      topk_insert<K>(bs, bi, acc, ci);
+    }
+    for (int off = 1; off < kWave; off <<= 1) {
       float os[K];
       int oi[K];
 #pragma unroll
@@ -1258,13 +1315,26 @@ __global__ __launch_bounds__(256) void knn_b3top_final_kernel(const float* __res
       }
       merge_sorted<K>(bs, bi, os, oi);
     }
-  }
-  if (live && sl == 0) {
+    if (lane == 0) {
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      out_idx[(int64_t)q * K + k] = bi[k];
-      if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+      for (int k = 0; k < K; ++k) { ls[wv][k] = bs[k]; li[wv][k] = bi[k]; }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      for (int w = 1; w < 4; ++w) {
+        float os[K];
+        int oi[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) { os[k] = ls[w][k]; oi[k] = li[w][k]; }
+        merge_sorted<K>(bs, bi, os, oi);
+      }
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        out_idx[(int64_t)q * K + k] = bi[k];
+        if (out_score) out_score[(int64_t)q * K + k] = bs[k];
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -1475,11 +1545,13 @@ int knn_b3top_splits(int mq_pad, int mc_pad) {
 
 void launch_knn_b3top(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                      float* out_score, float* ws_s, int* ws_i, float* ws_m, int* n_scan, int nsplit,
+                      float* out_score, float* ws_s, int* ws_i, float* ws_m, int* fail, int nsplit,
                       hipStream_t stream) {
   if (mq_pad % 32 != 0 || mc_pad % 32 != 0) throw std::runtime_error("knn_b3top: pads must be x32");
   if (mq > mq_pad || mc > mc_pad || nsplit < 1 || nsplit > 32 || ws_s == nullptr || ws_i == nullptr || ws_m == nullptr)
     throw std::runtime_error("knn_b3top: bad shapes or missing [nsplit][mq][8] workspaces");
+  if (fail == nullptr) throw std::runtime_error("knn_b3top: missing the [1 + mq] failed-query list");
+  if (hipMemsetAsync(fail, 0, sizeof(int), stream) != hipSuccess) throw std::runtime_error("knn_b3top: memset");
   if (k < 1 || k > kTopP) throw std::runtime_error("knn_b3top: k must be in [1, 8]");
   const dim3 grid(mq_pad / 32, nsplit);
   knn_b3top_kernel<><<<grid, kWave, 0, stream>>>(Q, reinterpret_cast<const uint4*>(Qhl),
@@ -1490,7 +1562,8 @@ void launch_knn_b3top(const float* Q, const void* Qhl, int mq_pad, int mq, const
   const unsigned fb = (unsigned)((((int64_t)mq << lg) + 255) / 256);
 #define FDX_KNNB3(KK)                                                                                         \
   knn_b3top_final_kernel<KK><<<fb, 256, 0, stream>>>(Q, C, mq, mc, nsplit, lg, self_offset, ws_s, ws_i, ws_m, \
-                                                     out_idx, out_score, n_scan)
+                                                     out_idx, out_score, fail);                                   \
+  knn_b3top_scan_kernel<KK><<<256, 256, 0, stream>>>(Q, C, mc, self_offset, fail, out_idx, out_score)
   switch (k) {
     case 1: FDX_KNNB3(1); break;
     case 2: FDX_KNNB3(2); break;

@@ -262,11 +262,12 @@ int knn_lds_splits(int mq_pad, int mc_pad);
 // bf16x3 collect (per-lane candidate lists [nsplit][mq_pad / 32][cap][64] int32 pairs + counts
 // [nsplit][mq_pad / 32][64]) then exact fp32 re-rank of the listed candidates (knn.hip)
 // bf16x3 scores with register top-8 approximate lists per (slice, query), then ONE merge kernel that
-// re-scores the 8 best exactly and proves the exact top-k (else an exact scan of that query)
+// re-scores the 8 best exactly and proves the exact top-k; the queries it cannot prove go to an exact
+// scan (one workgroup each).  ws_m [nsplit][mq][2]; fail int [1 + mq] (count, query ids).
 int knn_b3top_splits(int mq_pad, int mc_pad);
 void launch_knn_b3top(const float* Q, const void* Qhl, int mq_pad, int mq, const float* C, const void* Chl,
                       const float* tmax, int mc_pad, int mc, int64_t self_offset, int k, int* out_idx,
-                      float* out_score, float* ws_s, int* ws_i, float* ws_m, int* n_scan, int nsplit,
+                      float* out_score, float* ws_s, int* ws_i, float* ws_m, int* fail, int nsplit,
                       hipStream_t stream);
 int knn3r_list_cap();
 int knn3r_splits(int mq_pad, int mc_pad);

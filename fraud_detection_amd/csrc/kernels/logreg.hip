@@ -416,7 +416,12 @@ __device__ __forceinline__ void bf16_wave_pass(
       __builtin_amdgcn_wave_barrier();
     }
   };
-  int64_t base = ((int64_t)row_phase * Gw + wave) * 64;
+  // tile-interleaved phases: wave w's i-th tile is (i Gw + w) row_sub + row_phase, so phase b of
+  // row_sub is every row_sub-th 64-row tile of the shard (t mod row_sub == b) -- a minibatch samples
+  // the whole shard at 64-row granularity whatever order the rows are stored in (the CV job's
+  // fold-sorted table of time-sorted rows made group-strided minibatches differ in mean Time:
+  // SGD stalled at an epoch gradient of 3.7e-3, profiles/r6_b)
+  int64_t base = ((int64_t)wave * row_sub + row_phase) * 64;
   // Register double buffer: the next tile's 4 row loads are in flight while this tile computes
   // (kDepth 2: a third buffer, the tile after it too).
   uint4 cur[4], nx2[4];
@@ -532,8 +537,8 @@ __device__ __forceinline__ void bf16_wave_pass(
 
 // VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
 // rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
-// row_sub / row_phase: the pass visits the row tiles t with (t / G) mod row_sub == row_phase
-// (G = waves in the grid) and the pick tiles with t mod row_sub == row_phase -- phase 0 of a
+// row_sub / row_phase: the pass visits the row tiles t with t mod row_sub == row_phase and the pick
+// tiles with t mod row_sub == row_phase -- phase 0 of a
 // 1/row_sub sub-sample is the progressive-Newton warm-up, phases 0..row_sub-1 are the disjoint
 // minibatches of one SGD epoch (every stored row and every SMOTE sample in exactly one of them).
 // FISH (gradient-only SGD passes): slot 35 also receives sum s p (1 - p), the minibatch's
@@ -714,7 +719,12 @@ __device__ __forceinline__ void fp8_wave_pass(
       __builtin_amdgcn_wave_barrier();
     }
   };
-  int64_t base = ((int64_t)row_phase * Gw + wave) * 64;
+  // tile-interleaved phases: wave w's i-th tile is (i Gw + w) row_sub + row_phase, so phase b of
+  // row_sub is every row_sub-th 64-row tile of the shard (t mod row_sub == b) -- a minibatch samples
+  // the whole shard at 64-row granularity whatever order the rows are stored in (the CV job's
+  // fold-sorted table of time-sorted rows made group-strided minibatches differ in mean Time:
+  // SGD stalled at an epoch gradient of 3.7e-3, profiles/r6_b)
+  int64_t base = ((int64_t)wave * row_sub + row_phase) * 64;
   // two tiles in flight ahead of the one being computed (4 KiB per wave, as the bf16 stream)
   uint4 cur[2], nx1[2];
   if (use_pre) {
@@ -1696,7 +1706,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
         have_ppre = true;
       }
     }
-    const int64_t base = ((int64_t)S.phase * P.Gw + wave) * 64;
+    const int64_t base = ((int64_t)wave * S.rsub + S.phase) * 64;  // bf16_wave_pass tile walk
     if (kPersistPrefetch == 3 || base >= n) return;
     if constexpr (kPersistPrefetch == 2) {
       // L2 touch: one dword per row of the first tile, into a register nobody reads (held until

@@ -146,12 +146,12 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         ns = min(ns, 32)
         ws_s = torch.empty((ns, mq, 8), device=Q.device, dtype=torch.float32)
         ws_i = torch.empty((ns, mq, 8), device=Q.device, dtype=torch.int32)
-        ws_m = torch.empty((ns, mq), device=Q.device, dtype=torch.float32)
-        nscan = torch.zeros(1, device=Q.device, dtype=torch.int32) if _diag is not None else None
+        ws_m = torch.empty((ns, mq, 2), device=Q.device, dtype=torch.float32)
+        fail = torch.empty(1 + mq, device=Q.device, dtype=torch.int32)  # count, then failed query ids
         m.knn_b3top(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
-                    int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ptr(ws_m), ptr(nscan), ns, s)
+                    int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ptr(ws_m), ptr(fail), ns, s)
         if _diag is not None:  # queries answered by the exact scan (diagnostics; synchronises)
-            _diag.update(nsplit=ns, exact_scans=int(nscan.item()))
+            _diag.update(nsplit=ns, exact_scans=int(fail[0].item()))
     elif eng == "bf16x3r":
         nb = ns * (mq_pad // 32) * 64
         lists = torch.empty(nb * m.KNN3R_LIST_CAP * 2, device=Q.device, dtype=torch.int32)  # (lb, index)

@@ -715,8 +715,8 @@ SGD_MAX_EPOCHS = 8  # launchers.h kSgdMaxEpochs (per-epoch step scalars of the p
 
 
 def _effective_subs(subs, n_stored: int, n_picks: int, nbs, blocks: int) -> list:
-    """Sub-sample factors that keep every minibatch of an epoch's finer grid (nb_e x s) populated:
-    >= 1 strided group of row tiles and >= 2 pick tiles each; else that epoch visits every row."""
+    """Sub-sample factors that keep every minibatch of an epoch's finer grid (nb_e x s) well populated
+    (>= one grid's worth of row tiles and >= 2 pick tiles each); else that epoch visits every row."""
     groups = n_stored // (ref.ROW_TILE * ref.WAVES_PER_BLOCK * max(1, blocks))
     ptiles = -(-n_picks // ref.PICK_TILE)
     out = []
@@ -755,8 +755,8 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
     """Minibatch SGD (BASELINE config 3) on sklearn's objective.
 
     Minibatches: an epoch is ``batches`` disjoint minibatches; minibatch b is the pass's row phase b
-    -- the stored row tiles t with (t // G) mod batches == b (G = waves in the pass grid: every
-    minibatch strides over the whole shard) plus the virtual-SMOTE pick tiles t mod batches == b
+    -- the stored 64-row tiles t with t mod batches == b (every minibatch samples the whole shard,
+    whatever the row order: a time-sorted or fold-sorted table included) plus the virtual-SMOTE pick tiles t mod batches == b
     (1/batches of the SMOTE samples, generated in the pass, never stored).  Each minibatch
     therefore holds both classes in the post-SMOTE proportion.  ``batch_rows`` (legacy) sets
     ``batches`` = ceil(rows / batch_rows).

@@ -305,11 +305,11 @@ def sgd_grid_blocks(n_stored: int, nb: int, full_blocks: int) -> int:
     return int(max(1, min(int(full_blocks), want)))
 
 
-def sgd_row_batches(n_stored: int, nb: int, blocks: int) -> np.ndarray:
-    """Minibatch of every stored row (logreg.hip logreg_pass_kernel row_phase walk): row tile
-    t = row // 64 belongs to minibatch (t // G) mod nb, G = waves in the grid."""
-    G = WAVES_PER_BLOCK * int(blocks)
-    return ((np.arange(int(n_stored), dtype=np.int64) // ROW_TILE) // G) % int(nb)
+def sgd_row_batches(n_stored: int, nb: int, blocks: int | None = None) -> np.ndarray:
+    """Minibatch of every stored row (logreg.hip bf16_wave_pass row_phase walk): row tile
+    t = row // 64 belongs to minibatch t mod nb (tile-interleaved: every minibatch samples the whole
+    shard at 64-row granularity; the grid size ``blocks`` no longer enters)."""
+    return (np.arange(int(n_stored), dtype=np.int64) // ROW_TILE) % int(nb)
 
 
 def sgd_pick_batches(n_picks: int, nb: int, pick_tile: int = PICK_TILE_BF16) -> np.ndarray:

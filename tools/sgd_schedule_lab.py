@@ -22,7 +22,7 @@ import numpy as np  # noqa: E402
 
 from fraud_detection_amd.ops import reference as ref  # noqa: E402
 
-FINE = 64  # finest partition: (tile // G) mod 64, (pick // 16) mod 64
+FINE = 64  # finest partition: tile mod 64, (pick // 16) mod 64
 
 
 def build(rows: int, seed: int = 1000):
@@ -59,8 +59,7 @@ def build(rows: int, seed: int = 1000):
     b = P[idx.reshape(-1)[picks]]
     S = a + lam[:, None] * (b - a)
     S[:, 31] = 1.0
-    G = 4 * ref.sgd_grid_blocks(n, 8, ref.SGD_FULL_BLOCKS)
-    cr = ((np.arange(n) // 64) // G) % FINE
+    cr = (np.arange(n) // 64) % FINE
     cs = (picks // 16) % FINE
     chunks = []
     for c in range(FINE):
