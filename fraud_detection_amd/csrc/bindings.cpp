@@ -293,6 +293,28 @@ PYBIND11_MODULE(_fdx_native, m) {
     return reinterpret_cast<u>(d);
   });
   m.def("stream_sync", &stream_sync, py::call_guard<py::gil_scoped_release>());
+  // Native hipGraph capture / launch (runtime/graphs.NativeGraph): stream capture in thread-local
+  // mode around launches the caller makes on `stream` (native launchers, RCCL collectives), then
+  // one hipGraphLaunch per replay.  torch.cuda.CUDAGraph.replay() waited for the device on this
+  // build (a replay call cost the fit's device time, profiles/r6_j): this path does not.
+  m.def("graph_begin", [](u stream) {
+    hip_check(hipStreamBeginCapture(S(stream), hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+  });
+  m.def("graph_end", [](u stream) -> u {
+    hipGraph_t g = nullptr;
+    hip_check(hipStreamEndCapture(S(stream), &g), "hipStreamEndCapture");
+    hipGraphExec_t ex = nullptr;
+    const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(g);
+    hip_check(e, "hipGraphInstantiate");
+    return reinterpret_cast<u>(ex);
+  });
+  m.def("graph_launch", [](u exec, u stream) {
+    hip_check(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(exec), S(stream)), "hipGraphLaunch");
+  });
+  m.def("graph_destroy", [](u exec) {
+    if (exec) (void)hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(exec));
+  });
   // raw HIP events for the GPU owner's pipelined batches (wait with the GIL released)
   m.def("event_create", [] {
     hipEvent_t e;

@@ -412,7 +412,8 @@ __global__ __launch_bounds__(kLW * kWave) void knn_topk_lds_kernel(const float* 
 // fp32 (ties -> smaller index).
 
 // hi/lo bf16 split of prepped rows: hl[r] = 8 x uint4 (hi cols 0..31, then lo cols 0..31);
-// role 0 (candidates) also writes tmax[r / 32] = max feature norm over the 32-row tile.
+// role 0 (candidates) also writes tmax[r / 32] = max feature norm over the 32-row tile; role 2 = role 0
+// with hl in the b3top fragment order (below).
 __global__ __launch_bounds__(256) void knn_split_kernel(const float* __restrict__ Xp, int m_pad, int role,
                                                         uint4* __restrict__ hl, float* __restrict__ tmax) {
   const int r = blockIdx.x * 256 + threadIdx.x;
@@ -432,14 +433,26 @@ __global__ __launch_bounds__(256) void knn_split_kernel(const float* __restrict_
     h[k] = ph;
     l[k] = pack_bf16x2(a - bf16lo(ph), b - bf16hi(ph));
   }
-  if (ok) {
+  if (ok && role == 2) {
+    // fragment order (b3top): tile r / 32 as [u 0..3][lane 64] uint4, lane (half hh, row j) of load u
+    // holding chunk 2u + hh of row j (chunks 0..3 hi, 4..7 lo) -- each of the tile loop's four
+    // loads is one contiguous 1 KiB per wave instead of 16 B pieces of 32 rows
+    const int64_t tb = (int64_t)(r >> 5) * 256 + (r & 31);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const int k = v & 3;
+      const uint4 c = v < 4 ? make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3])
+                            : make_uint4(l[4 * k], l[4 * k + 1], l[4 * k + 2], l[4 * k + 3]);
+      hl[tb + (v >> 1) * 64 + (v & 1) * 32] = c;
+    }
+  } else if (ok) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       hl[(int64_t)r * 8 + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
       hl[(int64_t)r * 8 + 4 + k] = make_uint4(l[4 * k], l[4 * k + 1], l[4 * k + 2], l[4 * k + 3]);
     }
   }
-  if (role == 0) {
+  if (role == 0 || role == 2) {
     // candidate rows carry -0.5 ||c||^2 in column 30 (padding rows: -3e38 -> norm 0)
     float n2 = (ok && x[30] > -1.0e37f) ? -2.0f * x[30] : 0.0f;
 #pragma unroll
@@ -968,26 +981,6 @@ __global__ __launch_bounds__(256) void knn_merge_kernel(const float* __restrict_
 constexpr int kTopP = 8;
 constexpr int kSeedFlag = 0x40000000;
 
-__device__ __forceinline__ float union_kth(const float (&bs)[kTopP]) {
-  // kTopP-th best of the union of this lane's and its partner's (other half) sorted lists
-  float ps[kTopP];
-#pragma unroll
-  for (int k = 0; k < kTopP; ++k) ps[k] = __shfl_xor(bs[k], 32, kWave);
-  int ia = 0, ib = 0;
-  float kth = kNegBig;
-#pragma unroll
-  for (int k = 0; k < kTopP; ++k) {
-    float a = kNegBig, b = kNegBig;
-#pragma unroll
-    for (int u = 0; u < kTopP; ++u) { if (u == ia) a = bs[u]; if (u == ib) b = ps[u]; }
-    const bool ta = a >= b;
-    kth = ta ? a : b;
-    ia += ta ? 1 : 0;
-    ib += ta ? 0 : 1;
-  }
-  return kth;
-}
-
 // Merge two sorted (score desc, index asc) lists of N into the best N (static indices).
 template <int N>
 __device__ __forceinline__ void merge_sorted(float (&bs)[N], int (&bi)[N], const float (&os)[N], const int (&oi)[N]) {
@@ -1061,15 +1054,18 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
       }
     }
     qn_ = 0;
-    const float kth = union_kth(bs);
+    // max of the two half-lists' kTopP-th best: one of them holds kTopP entries at or above it, so
+    // it is a valid threshold -- one shuffle instead of a kTopP x kTopP union merge (the flush
+    // ran ~500 VALU per call, the kernel's dominant cost, r6_e)
+    const float kth = fmaxf(bs[kTopP - 1], __shfl_xor(bs[kTopP - 1], 32, kWave));
     thr = qg < mq ? kth : __builtin_inff();
   };
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
   const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
-  auto fetch = [&](int t, uint4 (&a)[4], float& tmv) {
-    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
-    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
+  auto fetch = [&](int t, uint4 (&a)[4], float& tmv) {  // Chl in fragment order (knn_split role 2)
+    const uint4* p = Chl + (int64_t)t * 256 + lane;
+    a[0] = p[0]; a[1] = p[64]; a[2] = p[128]; a[3] = p[192];
     tmv = tmax[t];
   };
   auto approx = [&](const uint4 (&c)[4]) -> f32x16_t {
@@ -1100,46 +1096,69 @@ __global__ __launch_bounds__(kWave) void knn_b3top_kernel(const float* __restric
         if (ci != self_c && ci < mc) topk_insert<kTopP>(bs, bi, acc[r], ci | kSeedFlag);
       }
     }
-    const float kth = union_kth(bs);
+    const float kth = fmaxf(bs[kTopP - 1], __shfl_xor(bs[kTopP - 1], 32, kWave));
     thr = qg < mq ? kth : __builtin_inff();
   }
-  uint4 cv[4], cv2[4];
-  float tmn = 0.0f, tmn2 = 0.0f;
-  if (t_lo < t_hi) fetch(t_lo, cv, tmn);
-  if (t_lo + 1 < t_hi) fetch(t_lo + 1, cv2, tmn2);
-  for (int t = t_lo; t < t_hi; ++t) {
-    const int c0 = t * 32;
-    const f32x16_t acc = approx(cv);
-    const float tm = tmn;
+  // kBufs tiles in flight in separate registers, the loop unrolled by kBufs: a buffer is refilled
+  // right after its 6 MFMAs consumed it, kBufs tiles (~kBufs x 200 cycles) ahead of its next use.
+  // (A rotating copy cv = cv2 made the compiler wait for the newest loads every tile: one tile of
+  // prefetch distance against an L2 round trip of several, r6_d.)
+  constexpr int kBufs = 3;
+  uint4 cb[kBufs][4];
+  float tb[kBufs];
+  const int tlast = t_hi > 0 ? t_hi - 1 : 0;  // a valid tile even for an empty slice
 #pragma unroll
-    for (int u = 0; u < 4; ++u) cv[u] = cv2[u];
-    tmn = tmn2;
-    if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
-    float mx = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
+  for (int u = 0; u < kBufs; ++u) {  // in buffer order (the loop head's vmcnt assumes it)
+    fetch(t_lo + u < t_hi ? t_lo + u : tlast, cb[u], tb[u]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // Every step issues its refill (clamped to the slice's last tile), so every path has the same
+  // loads in the same order and the compiler's vmcnt waits stay exact (a conditional refill made it
+  // wait for all outstanding loads at the loop head).
+  for (int t0 = t_lo; t0 < t_hi; t0 += kBufs) {
 #pragma unroll
-    for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, acc[r]), acc[r + 1]);
-    mx = fmaxf(mx, acc[15]);
-    {
-      const float mt = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
-      if (mx >= thr) mg_p = fmaxf(mg_p, mt);
-      else ub_f = fmaxf(ub_f, mx + mt);  // the self row stays in mx: a valid (if loose) bound
-    }
-    if (!__any(mx >= thr)) continue;
-    const int cbase = c0 + 4 * h;
-    int qe = qn_ * kWave + lane;
+    for (int u = 0; u < kBufs; ++u) {
+      const int t = t0 + u;
+      const f32x16_t acc = approx(cb[u]);
+      const float tm = tb[u];
+      fetch(t + kBufs < t_hi ? t + kBufs : tlast, cb[u], tb[u]);
+      if (t >= t_hi) continue;  // wave-uniform: the last group's spare steps
+      const int c0 = t * 32;
+      float mx = fmaxf(fmaxf(acc[0], acc[1]), acc[2]);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int ci = cbase + (r & 3) + 8 * (r >> 2);
-      const bool pass = acc[r] >= thr && ci != self_c && ci < mc;
-      if (__any(pass)) {
-        if (pass) {
+      for (int r = 3; r < 15; r += 2) mx = fmaxf(fmaxf(mx, acc[r]), acc[r + 1]);
+      mx = fmaxf(mx, acc[15]);
+      {
+        const float mt = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
+        if (mx >= thr) mg_p = fmaxf(mg_p, mt);
+        else ub_f = fmaxf(ub_f, mx + mt);  // the self row stays in mx: a valid (if loose) bound
+      }
+      if (!__any(mx >= thr)) continue;
+      // With 64 queries per wave SOME lane passes on most tiles, so the append must cost little
+      // when few rows pass: a 16-bit pass mask per lane, OR-reduced over the wave, and a loop over
+      // just the rows some lane passed (uniform row index: one indexed register read each).  The
+      // per-row uniform branch over all 16 rows ran ~245 VALU + ~140 SALU per tile (r6_f PMC).
+      uint32_t pm = 0;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) pm |= (acc[r] >= thr ? 1u : 0u) << r;
+      uint32_t wm = pm;
+#pragma unroll
+      for (int o = 1; o < kWave; o <<= 1) wm |= (uint32_t)__shfl_xor((int)wm, o, kWave);
+      wm = __builtin_amdgcn_readfirstlane(wm);
+      const int cbase = c0 + 4 * h;
+      int qe = qn_ * kWave + lane;
+      while (wm) {
+        const int r = __builtin_ctz(wm);  // wave-uniform
+        wm &= wm - 1;
+        const int ci = cbase + (r & 3) + 8 * (r >> 2);
+        if (((pm >> r) & 1u) && ci != self_c && ci < mc) {
           qent[qe] = make_int2(__float_as_int(acc[r]), ci);
           qe += kWave;
         }
       }
+      qn_ = (qe - lane) / kWave;
+      if (__any(qn_ >= QF)) flush();
     }
-    qn_ = (qe - lane) / kWave;
-    if (__any(qn_ >= QF)) flush();
   }
   flush();
   ub_f = fmaxf(ub_f, __shfl_xor(ub_f, 32, kWave));
@@ -1291,19 +1310,29 @@ __global__ __launch_bounds__(256) void knn_b3top_scan_kernel(const float* __rest
     int bi[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
-    for (int ci = threadIdx.x; ci < mc; ci += 256) {
-      if (ci == self_c) continue;
-      const float4* c = reinterpret_cast<const float4*>(C + (int64_t)ci * kCols);
-      float acc = 0.0f;
+    // 4 candidates per lane in flight (every row load issued before the first fma)
+    for (int c0 = threadIdx.x; c0 < mc; c0 += 4 * 256) {
+      float4 rv[4][kCols / 4];
 #pragma unroll
-      for (int k = 0; k < kCols / 4; ++k) {
-        const float4 v = c[k];
-        acc = fmaf(qv[4 * k], v.x, acc);
-        acc = fmaf(qv[4 * k + 1], v.y, acc);
-        acc = fmaf(qv[4 * k + 2], v.z, acc);
-        acc = fmaf(qv[4 * k + 3], v.w, acc);
+      for (int u = 0; u < 4; ++u) {
+        const int ci = c0 + u * 256;
+        const float4* c = reinterpret_cast<const float4*>(C + (int64_t)(ci < mc ? ci : 0) * kCols);
+#pragma unroll
+        for (int k = 0; k < kCols / 4; ++k) rv[u][k] = c[k];
       }
-      topk_insert<K>(bs, bi, acc, ci);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int ci = c0 + u * 256;
+        float acc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < kCols / 4; ++k) {
+          acc = fmaf(qv[4 * k], rv[u][k].x, acc);
+          acc = fmaf(qv[4 * k + 1], rv[u][k].y, acc);
+          acc = fmaf(qv[4 * k + 2], rv[u][k].z, acc);
+          acc = fmaf(qv[4 * k + 3], rv[u][k].w, acc);
+        }
+        if (ci < mc && ci != self_c) topk_insert<K>(bs, bi, acc, ci);
+      }
     }
     for (int off = 1; off < kWave; off <<= 1) {
       float os[K];

@@ -140,7 +140,7 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
         Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
         Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
         tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
-        m.knn_split(ptr(Cp), mc_pad, 0, ptr(Chl), ptr(tmax), s)
+        m.knn_split(ptr(Cp), mc_pad, 2 if eng == "b3top" else 0, ptr(Chl), ptr(tmax), s)  # 2: fragment order
         m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
     if eng == "b3top":
         ns = min(ns, 32)

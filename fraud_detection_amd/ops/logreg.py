@@ -905,6 +905,60 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         s0 = estart[start[0]] + start[1]
         run_steps(s0, estart[epochs] if max_steps is None else min(estart[epochs], int(max_steps)))
         return PendingFit(ws.state, sgd=True)
+
+    def dp_epochs(e0: int, e1: int, all_reduce):
+        """Epochs [e0, e1) of the lean data-parallel schedule, enqueued with no host sync: per step
+        the pass leaves its fixed-point sums (int64: the all-reduce is exact and order-free, every
+        rank gets bitwise the same vector), one collective, the update.  A converged fit's passes
+        and updates are no-ops (device `done`); its collectives still run on every rank.  The stream
+        is queried here: under capture it is the capture stream."""
+        s = stream_of(rows)
+        for ep in range(e0, e1):
+            c, nbe = lrs[ep], nbs[ep]
+            for pos in range(nbe):
+                b = _sgd_phase(pos, ep, nbe, serpentine)
+                rsub, ph = nbe * subs[ep], b * subs[ep]
+                m.sgd_pass_sums(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.w32), ptr(ws.class_w),
+                                ptr(ws.done), rsub, ph, blocks, *vargs, ptr(ws.sgd_acc),
+                                ptr(ws.sgd_acc[SGD_ACC_WORDS:]), ptr(ws.sgd_sums), aff, s)
+                all_reduce(ws.sgd_sums)
+                m.sgd_update_fixed(ptr(ws.sgd_sums), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C), c,
+                                   float(momentum), int(fit_intercept), rsub, int(ep >= avg_from), int(pos + 1 == nbe),
+                                   -1.0 if subs[ep] > 1 else float(tol), s)
+
+    if dp and checkpoint is None and max_steps is None and start == (0, 0) and _dp_graph_ok(comm):
+        # The whole DP schedule as hipGraph replays (SURVEY.md §5.8): the nominal epochs in one
+        # graph, the extra epochs in another replayed only when the fit has not converged (the
+        # same host check the eager loop makes).  Capture happens once per (buffers, schedule) key;
+        # the graph holds the native RCCL all-reduces on the capture stream.
+        key = (ptr(rows), int(rows.shape[0]), int(fp8), float(fp8_scale), n, tuple(hole), vargs, aff, d, float(C),
+               float(momentum), int(fit_intercept), float(tol), tuple(lrs), tuple(subs), tuple(nbs), avg_from,
+               bool(serpentine), blocks, nominal, epochs)
+        # Captured natively (runtime/graphs.capture_native, one hipGraphLaunch per replay).  Opt-in:
+        # on this ROCm build a launch of these graphs (kernels + RCCL nodes) returns only when the
+        # device has run it -- with torch's CUDAGraph, natively, and alternating two instances alike
+        # -- so the host enqueue per fit equals its device time (0.63 of 0.64 ms), where the eager
+        # schedule enqueues in 0.25 ms and stays a fit ahead (profiles/r6_dpgraph).
+        cache = ws.__dict__.setdefault("_dp_graphs", {})
+        gs = cache.get(key)
+        if gs is None:
+            from ..runtime import graphs as rt_graphs
+
+            nat = comm._native.all_reduce_
+            gs = [rt_graphs.capture_native(lambda: dp_epochs(0, nominal, nat))]
+            if epochs > nominal:
+                gs.append(rt_graphs.capture_native(lambda: dp_epochs(nominal, epochs, nat)))
+            if all(g is not None for g in gs):
+                if len(cache) >= 4:  # a handful of shapes per workspace: drop the oldest
+                    cache.pop(next(iter(cache)))
+                cache[key] = gs
+            else:
+                gs = None
+        if gs is not None:
+            gs[0].replay()
+            if len(gs) > 1 and not int(ws.done.item()):
+                gs[1].replay()
+            return PendingFit(ws.state, sgd=True)
     for ep in range(start[0], epochs):
         if ep >= nominal and int(ws.done.item()):  # converged: the extra epochs would be no-ops
             break
@@ -935,6 +989,14 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                 checkpoint.save(gstep, {"state": ws.state},
                                 {"signature": sig, "epoch": nxt[0], "batch": nxt[1], "kind": "sgd"})
     return PendingFit(ws.state, sgd=True)
+
+
+def _dp_graph_ok(comm) -> bool:
+    """FDX_DP_GRAPH=1: the DP SGD schedule runs as hipGraph replays when its collectives are the
+    native RCCL ones on the compute stream (default eager: see sgd_fit's measurement note)."""
+    import os
+
+    return getattr(comm, "_native", None) is not None and os.environ.get("FDX_DP_GRAPH", "0") == "1"
 
 
 def _sgd_pass(m, rows, ws: LRWorkspace, n: int, fp8_scale: float, s: int, phase: int, nb: int, blocks: int,

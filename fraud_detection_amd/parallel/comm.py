@@ -44,6 +44,9 @@ import torch
 import torch.distributed as dist
 
 
+_SHM_DTYPES = (torch.float32, torch.float64, torch.int32, torch.int64)
+
+
 class CollectiveStats:
     """Per-op count / bytes / total and max seconds.  Device-timed entries are resolved lazily
     (their events complete asynchronously); ``summary()`` synchronises and resolves them."""
@@ -64,6 +67,12 @@ class CollectiveStats:
             train_metrics().allreduce_seconds.labels(op).observe(sec)
         except Exception:  # noqa: BLE001 - metrics are best effort
             pass
+
+    def count(self, op: str, nbytes: int):
+        """An untimed collective: count and bytes only."""
+        a = self.acc.setdefault(op, [0, 0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += nbytes
 
     def resolve(self, block: bool = False):
         keep = []
@@ -120,7 +129,10 @@ class Communicator:
             self.backend = "single"
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.stats = CollectiveStats()
-        self._timing = os.environ.get("FDX_COMM_TIMING", "1") == "1"
+        # per-collective hipEvent timing is opt-in (FDX_COMM_TIMING=1): two events and list
+        # bookkeeping around every collective of a timed fit otherwise; counts and
+        # bytes are always kept
+        self._timing = os.environ.get("FDX_COMM_TIMING", "0") == "1"
         self.trace = [] if os.environ.get("FDX_COMM_TRACE", "0") == "1" else None
         self._native = None
         self._shm = None  # host-staged sums over shared memory (lazy, collective; False: off)
@@ -193,6 +205,8 @@ class Communicator:
             self.trace.append((op, path, nbytes))
         if not self._timing or self.world_size == 1:
             yield
+            if self.world_size > 1:
+                self.stats.count(op, nbytes)
             return
         if t is not None and t.is_cuda and path in ("rccl", "nccl"):
             e0 = torch.cuda.Event(enable_timing=True)
@@ -239,7 +253,8 @@ class Communicator:
                 return t
             if self._host_staged(t):
                 h = self._stage_d2h(t)
-                shm = self._shm_group() if op == "sum" else None
+                # the shared-memory sums take numpy dtypes only (bf16 / fp16 stay on gloo: ADVICE r5)
+                shm = self._shm_group() if (op == "sum" and h.dtype in _SHM_DTYPES) else None
                 if shm is not None and shm.fits(h.numpy()):  # same size on every rank: same branch
                     shm.all_reduce_(h.numpy())
                 else:

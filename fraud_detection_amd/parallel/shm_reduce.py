@@ -1,7 +1,8 @@
 """Sum all-reduce of small host vectors among the ranks of ONE host through shared memory.
 
-The gloo path of a single-host job (CPU ranks, or the one-GPU multi-process rehearsal whose CUDA
-tensors are staged through host memory) pays a TCP-loopback round trip per collective: ~200 us
+The host-staged gloo path of a single-host job (the one-GPU multi-process rehearsal, whose CUDA
+tensors are staged through host memory; CPU-tensor collectives go straight to gloo and do not come
+here, nor do dtypes numpy lacks, e.g. bf16) pays a TCP-loopback round trip per collective: ~200 us
 for a 1.1 KB SGD step vector in `profiles/r5_ze` -- 24 of them per SGD fit.  Here every rank
 writes its vector into its own slot of a shared segment and publishes a sequence number; each rank
 then sums the W slots itself in rank order (the same fixed order on every rank, so every rank gets

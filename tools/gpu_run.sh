@@ -76,9 +76,9 @@ for st in "$@"; do
     pmcknn)  # bf16x3r collect / rerank counters (FDX_KNN_ARGS picks engines and splits)
       cd /tmp && export TMPDIR=/tmp
       # shellcheck disable=SC2086
-      step pmcknn_a 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel)" --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_SALU --output-format csv -d "$OUT/pmcknn_a" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS || exit 1
+      step pmcknn_a 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel|b3top)" --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_VMEM SQ_INSTS_SALU --output-format csv -d "$OUT/pmcknn_a" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS || exit 1
       # shellcheck disable=SC2086
-      step pmcknn_b 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel)" --pmc SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcknn_b" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS
+      step pmcknn_b 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel|b3top)" --pmc SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcknn_b" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS
       cd "$R" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" $FDX_KNN_ARGS ;;  # shellcheck disable=SC2086
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
@@ -120,6 +120,7 @@ for st in "$@"; do
     gbdt)  # GBDT: 100-tree bench at the bench shape (10M raw rows -> 16M post-SMOTE)
       step gbdt 300 python tools/gbdt_bench.py --rows 10000000 --json "$OUT/gbdt.json" ;;
     hostprof) step hostprof 300 python tools/host_profile.py --steps 30 ;;
+    hostprofn) step hostprof_newton 300 python tools/host_profile.py --steps 30 --solver newton ;;
     gapprobe)  # idle gap after kernels that store to mapped pinned memory
       cd /tmp && export TMPDIR=/tmp
       step gapprobe 200 rocprofv3 --kernel-trace --output-format csv -d "$OUT/gapprobe" -o run -- python3 "$R/tools/gap_probe.py"

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rows", type=int, default=10_000_000)
     ap.add_argument("--storage", default="bf16")
     ap.add_argument("--top", type=int, default=35)
+    ap.add_argument("--solver", default="sgd")
     a = ap.parse_args()
     import torch
 
@@ -33,7 +34,7 @@ def main():
     dev = torch.device("cuda", 0)
     n_train = a.rows - a.rows // 5
     X, y = separable(n_train, seed=1000, device=dev)
-    pipe = DevicePipeline(TrainConfig(storage=a.storage, seed=42, smote_scope="global"))
+    pipe = DevicePipeline(TrainConfig(solver=a.solver, storage=a.storage, seed=42, smote_scope="global"))
     for _ in range(3):
         pipe.fit(X, y)
     torch.cuda.synchronize()
@@ -42,6 +43,24 @@ def main():
         pipe.fit(X, y)
     torch.cuda.synchronize()
     plain = (time.perf_counter() - t0) / a.steps
+    # host time spent inside fit() per call, back to back (the device queue never drains if this
+    # stays below the device time per fit), and the same with the device idle at every call
+    host = []
+    for _ in range(a.steps):
+        t1 = time.perf_counter()
+        pipe.fit(X, y)
+        host.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    idle = []
+    for _ in range(a.steps):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        pipe.fit(X, y)
+        idle.append(time.perf_counter() - t1)
+    torch.cuda.synchronize()
+    import numpy as np
+    print(f"[host_profile] host time in fit(), back to back: median {np.median(host) * 1e3:.4f} ms; "
+          f"from an idle device: median {np.median(idle) * 1e3:.4f} ms (blocks on the minority count)")
     pr = cProfile.Profile()
     pr.enable()
     for _ in range(a.steps):

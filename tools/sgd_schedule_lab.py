@@ -204,6 +204,12 @@ def main():
         "s4n6_b": (8, [(0.4, 4, 6), (0.7, 1), (0.8, 1), (0.8, 1)], 1),
         "d86": (8, [(0.6, 4, 4), (0.8, 1, 8), (0.8, 1, 6), (0.8, 1, 6)], 1),
         "d66": (8, [(0.6, 4, 4), (0.8, 1, 6), (0.8, 1, 6), (0.8, 1, 6)], 1),
+        # round 6: the same 16 steps with a smaller last-epoch step (iterate noise at <= 0.8x rows)
+        "d66lo": (8, [(0.6, 4, 4), (0.8, 1, 6), (0.5, 1, 6), (0.5, 1, 6)], 1),
+        "d66lo6": (8, [(0.6, 4, 4), (0.8, 1, 6), (0.6, 1, 6), (0.6, 1, 6)], 1),
+        "d66lo4": (8, [(0.6, 4, 4), (0.8, 1, 6), (0.4, 1, 6), (0.4, 1, 6)], 1),
+        "d76lo": (8, [(0.6, 4, 4), (0.7, 1, 6), (0.5, 1, 6), (0.5, 1, 6)], 1),
+        "d96lo": (8, [(0.6, 4, 4), (0.9, 1, 6), (0.5, 1, 6), (0.5, 1, 6)], 1),
         "d3": (8, [(0.6, 4, 3), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
         "d2": (8, [(0.7, 4, 2), (0.8, 1), (0.8, 1), (0.8, 1)], 1),
         "d48": (8, [(0.6, 8, 4), (0.8, 1), (0.8, 1), (0.8, 1)], 1),

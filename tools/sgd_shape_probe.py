@@ -66,6 +66,19 @@ def main():
             f = DevicePipeline(TrainConfig(solver="sgd", storage=a.storage, seed=42)).fit(Xo.contiguous(), yo.contiguous()).fit
             res[name] = {"steps": int(f.n_iter), "grad_max": float(f.grad_max)}
             print(name, json.dumps(res[name]), flush=True)
+        # the CV job's fold-k training rows as a fresh pipeline fit (own scaler, own SMOTE) and the
+        # CV's own fold fits on the same rows
+        b = cv.bounds
+        Xp, yp = X[perm], y[perm]
+        res["fold_rows_pipeline"] = []
+        for k in range(5):
+            keep = torch.cat([torch.arange(0, int(b[k]), device=dev), torch.arange(int(b[k + 1]), X.shape[0], device=dev)])
+            f = DevicePipeline(TrainConfig(solver="sgd", storage=a.storage, seed=42)).fit(
+                Xp.index_select(0, keep).contiguous(), yp.index_select(0, keep).contiguous()).fit
+            res["fold_rows_pipeline"].append({"steps": int(f.n_iter), "grad_max": float(f.grad_max)})
+        res["cv_fold_fits"] = [{"steps": int(f.n_iter), "grad_max": float(f.grad_max)} for f in cv.fits]
+        print("fold_rows_pipeline", json.dumps(res["fold_rows_pipeline"]), flush=True)
+        print("cv_fold_fits", json.dumps(res["cv_fold_fits"]), flush=True)
         Xs = X.clone()
         Xs[:, 0] = Xs[torch.randperm(X.shape[0], device=dev), 0]
         cv2 = DeviceCV(TrainConfig(solver="sgd", storage=a.storage, seed=42))
