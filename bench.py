@@ -169,7 +169,9 @@ def main():
     # device-side step boundaries (hipEvent times): an event behind every fit's
     # last kernel on the compute stream; the host runs ahead, so event i -> i+1 spans exactly
     # fit i+1's kernels and any device idle in front of them
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if dev.type == "cuda" else None
+    # FDX_BENCH_EVENTS=0 (lab): no per-fit events, wall clock only (isolates the events' own cost)
+    use_ev = dev.type == "cuda" and os.environ.get("FDX_BENCH_EVENTS", "1") != "0"
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)] if use_ev else None
     t0 = time.perf_counter()
     if ev:
         ev[0].record()

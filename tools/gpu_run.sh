@@ -65,6 +65,12 @@ for st in "$@"; do
     quicksgd) step quicksgd_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd &&
            step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
     quicksgdnc) step quicksgd_coop 300 env FDX_SGD_COOP=1 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
+    evab)  # per-fit timing events and the side-stream export, on / off (quick SGD bench each)
+      step evab_default 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step evab_noev 300 env FDX_BENCH_EVENTS=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step evab_noside 300 env FDX_EXPORT_SIDE=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step evab_noev_noside 300 env FDX_BENCH_EVENTS=0 FDX_EXPORT_SIDE=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step evab_default2 300 python bench.py --steps 30 --warmup 3 --no-extras ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
