@@ -31,6 +31,7 @@
 #   dpscope      tools/dp_scope_probe.py: global vs shard SMOTE scope attribution (2 ranks, one GPU, gloo)
 #   gbdtvar      GBDT histogram kernel variants under a kernel trace (FDX_GBDT_VARS, default "0 3")
 #   dpstored     dp_scope_probe.py on stored SMOTE rows (bf16 and fp8), per-phase times of each synced fit
+#   stall        tools/stall_probe.py: 2 ranks on one GPU under rocprofv3 markers + kernel trace, stall attribution
 #   py:<script>  python <script> (extra args via FDX_PY_ARGS)
 # Output lands in gpurun_out/<tag>/.
 set -o pipefail
@@ -71,6 +72,12 @@ for st in "$@"; do
       step evab_noside 300 env FDX_EXPORT_SIDE=0 python bench.py --steps 30 --warmup 3 --no-extras &&
       step evab_noev_noside 300 env FDX_BENCH_EVENTS=0 FDX_EXPORT_SIDE=0 python bench.py --steps 30 --warmup 3 --no-extras &&
       step evab_default2 300 python bench.py --steps 30 --warmup 3 --no-extras ;;
+    stall)  # 2-rank one-GPU rehearsal under a marker + kernel trace: attribute the intermittent fit stall
+      cd /tmp && export TMPDIR=/tmp FDX_BENCH_ONE_GPU=1 FDX_BENCH_BACKEND=gloo
+      step stall 400 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$OUT/stall" -o run -- python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29523 "$R/tools/stall_probe.py" --fits 12
+      unset FDX_BENCH_ONE_GPU FDX_BENCH_BACKEND
+      cd "$R"
+      python tools/stall_probe.py --analyze "$OUT/stall" --json "$OUT/stall_attribution.json" > "$OUT/stall_analyze.log" 2>&1 || true ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
