@@ -510,19 +510,48 @@ PYBIND11_MODULE(_fdx_native, m) {
     h.len = len;
     return h;
   };
-  m.def("logreg_pass", [hole_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
-                                 int nblocks, u s, int phase, bool fisher, int64_t hole_at, int64_t hole_len) {
+  // nf (optional): (red, ws, state, w32, done, aff, done_host, C, tol, d, max_iter, fit_intercept,
+  // phase_start, seq) -- the pass also reduces and applies the Newton update (launchers.h NewtonFuse)
+  auto nf_of = [](const py::object& o, fdx::NewtonFuse& f) -> const fdx::NewtonFuse* {
+    if (o.is_none()) return nullptr;
+    const py::tuple t = o.cast<py::tuple>();
+    if (t.size() != 14) throw std::runtime_error("logreg_pass: nf must have 14 entries");
+    f.red = P<double>(t[0].cast<u>());
+    f.ws = P<unsigned long long>(t[1].cast<u>());
+    f.st = P<double>(t[2].cast<u>());
+    f.w32 = P<float>(t[3].cast<u>());
+    f.done = P<int>(t[4].cast<u>());
+    f.aff = P<const double>(t[5].cast<u>());
+    f.done_host = P<int>(t[6].cast<u>());
+    f.C = t[7].cast<double>();
+    f.tol = t[8].cast<double>();
+    f.d = t[9].cast<int>();
+    f.max_iter = t[10].cast<int>();
+    f.fit_intercept = t[11].cast<int>();
+    f.phase_start = t[12].cast<int>();
+    f.seq = t[13].cast<int>();
+    return &f;
+  };
+  m.attr("NEWTON_FUSE_WORDS") = fdx::kNewtonFuseWords;
+  m.def("logreg_pass", [hole_of, nf_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, u partial,
+                                        int nblocks, u s, int phase, bool fisher, int64_t hole_at, int64_t hole_len,
+                                        py::object nf) {
+    fdx::NewtonFuse f;
     fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw), P<const int>(done),
-                            hess, sub, P<float>(partial), nblocks, S(s), nullptr, phase, fisher, hole_of(hole_at, hole_len));
+                            hess, sub, P<float>(partial), nblocks, S(s), nullptr, phase, fisher, hole_of(hole_at, hole_len),
+                            nf_of(nf, f));
   }, py::arg("X"), py::arg("rb"), py::arg("re"), py::arg("w"), py::arg("cw"), py::arg("done"), py::arg("hess"),
      py::arg("sub"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("phase") = 0,
-     py::arg("fisher") = false, py::arg("hole_at") = 0, py::arg("hole_len") = 0);
+     py::arg("fisher") = false, py::arg("hole_at") = 0, py::arg("hole_len") = 0, py::arg("nf") = py::none());
   // the same pass over the stored rows [0, n_real) plus virtual SMOTE samples (launchers.h
   // SmoteView); x_scale > 0 selects the fp8 row pass
-  m.def("logreg_pass_virtual", [hole_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub,
-                                         u partial, int nblocks, u s, u parents, u nbr, u lam, u off, u cnt,
-                                         int64_t n_real, int64_t q_offset, int mq, int k, float x_scale, int phase,
-                                         bool fisher, int64_t hole_at, int64_t hole_len) {
+  m.def("logreg_pass_virtual", [hole_of, nf_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub,
+                                                u partial, int nblocks, u s, u parents, u nbr, u lam, u off, u cnt,
+                                                int64_t n_real, int64_t q_offset, int mq, int k, float x_scale,
+                                                int phase, bool fisher, int64_t hole_at, int64_t hole_len,
+                                                py::object nf) {
+    fdx::NewtonFuse f;
+    const fdx::NewtonFuse* nfp = nf_of(nf, f);
     fdx::SmoteView v;
     v.parents = P<const uint16_t>(parents);
     v.nbr = P<const int>(nbr);
@@ -536,16 +565,16 @@ PYBIND11_MODULE(_fdx_native, m) {
     if (x_scale > 0.0f)
       fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
                                   P<const int>(done), hess, sub, x_scale, P<float>(partial), nblocks, S(s), &v, phase,
-                                  fisher, hole_of(hole_at, hole_len));
+                                  fisher, hole_of(hole_at, hole_len), nfp);
     else
       fdx::launch_logreg_pass(P<const uint16_t>(X), rb, re, P<const float>(w), P<const float>(cw),
                               P<const int>(done), hess, sub, P<float>(partial), nblocks, S(s), &v, phase, fisher,
-                              hole_of(hole_at, hole_len));
+                              hole_of(hole_at, hole_len), nfp);
   }, py::arg("X"), py::arg("rb"), py::arg("re"), py::arg("w"), py::arg("cw"), py::arg("done"), py::arg("hess"),
      py::arg("sub"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("parents"), py::arg("nbr"),
      py::arg("lam"), py::arg("off"), py::arg("cnt"), py::arg("n_real"), py::arg("q_offset"), py::arg("mq"),
      py::arg("k"), py::arg("x_scale"), py::arg("phase") = 0, py::arg("fisher") = false, py::arg("hole_at") = 0,
-     py::arg("hole_len") = 0);
+     py::arg("hole_len") = 0, py::arg("nf") = py::none());
   m.def("smote_bucket_bins", &fdx::smote_bucket_bins);
   m.def("smote_bucket_blocks", &fdx::smote_bucket_blocks);
   m.def("smote_bucket_max_picks", []() { return (uint64_t)fdx::kSmoteBucketMaxPicks; });
@@ -556,15 +585,16 @@ PYBIND11_MODULE(_fdx_native, m) {
                              P<uint32_t>(rec), P<uint32_t>(tmp), P<int>(pstart), P<int>(pcnt), P<uint16_t>(lam),
                              P<unsigned long long>(bump), S(s));
   });
-  m.def("logreg_pass_fp8", [hole_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub, float xs,
-                                     u partial, int nblocks, u s, int phase, bool fisher, int64_t hole_at,
-                                     int64_t hole_len) {
+  m.def("logreg_pass_fp8", [hole_of, nf_of](u X, int64_t rb, int64_t re, u w, u cw, u done, int hess, int sub,
+                                            float xs, u partial, int nblocks, u s, int phase, bool fisher,
+                                            int64_t hole_at, int64_t hole_len, py::object nf) {
+    fdx::NewtonFuse f;
     fdx::launch_logreg_pass_fp8(P<const uint8_t>(X), rb, re, P<const float>(w), P<const float>(cw),
                                 P<const int>(done), hess, sub, xs, P<float>(partial), nblocks, S(s), nullptr, phase,
-                                fisher, hole_of(hole_at, hole_len));
+                                fisher, hole_of(hole_at, hole_len), nf_of(nf, f));
   }, py::arg("X"), py::arg("rb"), py::arg("re"), py::arg("w"), py::arg("cw"), py::arg("done"), py::arg("hess"),
      py::arg("sub"), py::arg("xs"), py::arg("partial"), py::arg("nblocks"), py::arg("s"), py::arg("phase") = 0,
-     py::arg("fisher") = false, py::arg("hole_at") = 0, py::arg("hole_len") = 0);
+     py::arg("fisher") = false, py::arg("hole_at") = 0, py::arg("hole_len") = 0, py::arg("nf") = py::none());
   m.def("newton_update_stamped", [](u red, u state, u w32, u done, double C, u aff, u stamps, u s) {
     fdx::launch_newton_update_stamped(P<const double>(red), P<double>(state), P<float>(w32), P<int>(done), C,
                                       P<const double>(aff), P<unsigned long long>(stamps), S(s));
@@ -580,16 +610,17 @@ PYBIND11_MODULE(_fdx_native, m) {
      py::arg("max_iter"), py::arg("fi"), py::arg("phase_start"), py::arg("aff"), py::arg("s"), py::arg("done_host") = 0,
      py::arg("seq") = 0);
   m.def("logreg_init", [](u state, u w32, u class_w, u done, std::vector<double> w0, double cw0, double cw1, u aff,
-                          u s, u w0_dev) {
+                          u s, u w0_dev, u persist_ws) {
     if (w0.size() != 32) throw std::runtime_error("logreg_init: w0 must have 32 entries");
     fdx::LRInitArgs a;
     for (int j = 0; j < 32; ++j) a.w0[j] = w0[j];
     a.cw0 = (float)cw0;
     a.cw1 = (float)cw1;
     fdx::launch_logreg_init(a, P<double>(state), P<float>(w32), P<float>(class_w), P<int>(done),
-                            P<const double>(aff), S(s), P<const double>(w0_dev));
+                            P<const double>(aff), S(s), P<const double>(w0_dev),
+                            P<unsigned long long>(persist_ws));
   }, py::arg("state"), py::arg("w32"), py::arg("class_w"), py::arg("done"), py::arg("w0"), py::arg("cw0"),
-     py::arg("cw1"), py::arg("aff"), py::arg("s"), py::arg("w0_dev") = 0);
+     py::arg("cw1"), py::arg("aff"), py::arg("s"), py::arg("w0_dev") = 0, py::arg("persist_ws") = 0);
   m.def("logreg_export", [](u state, u host_dev, u s) {
     fdx::launch_logreg_export(P<const double>(state), P<double>(host_dev), S(s));
   });
@@ -693,7 +724,7 @@ PYBIND11_MODULE(_fdx_native, m) {
                                     int fi, double tol, int nb, int epochs, int avg_from, int serpentine,
                                     std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps,
                                     std::vector<int> subs, std::vector<int> nbs, int fault_test,
-                                    unsigned spin_limit) -> int {
+                                    unsigned spin_limit, u export_host, int prepped) -> int {
     if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
     if ((int)subs.size() < epochs) throw std::runtime_error("sgd_persist: one sub-sample factor per epoch");
     if ((int)nbs.size() < epochs) throw std::runtime_error("sgd_persist: one minibatch count per epoch");
@@ -731,6 +762,8 @@ PYBIND11_MODULE(_fdx_native, m) {
     a.stamps = P<unsigned long long>(stamps);
     a.fault_test = fault_test;
     if (spin_limit > 0) a.spin_limit = spin_limit;
+    a.export_host = P<double>(export_host);
+    a.prepped = prepped;
     // 0: enqueued; 1: the cooperative launch refused the grid (the caller launches per step)
     return fdx::launch_sgd_persist(P<const void>(X), fp8, x_scale, end, P<const float>(cw), parents ? &v : nullptr, h,
                                    a, S(s));
@@ -740,7 +773,7 @@ PYBIND11_MODULE(_fdx_native, m) {
      py::arg("w32"), py::arg("done"), py::arg("aff"), py::arg("d"), py::arg("C"), py::arg("mom"), py::arg("fi"),
      py::arg("tol"), py::arg("nb"), py::arg("epochs"), py::arg("avg_from"), py::arg("serpentine"), py::arg("lrs"),
      py::arg("s0"), py::arg("s1"), py::arg("Gw"), py::arg("s"), py::arg("stamps"), py::arg("subs"), py::arg("nbs"),
-     py::arg("fault_test") = 0, py::arg("spin_limit") = 0u);
+     py::arg("fault_test") = 0, py::arg("spin_limit") = 0u, py::arg("export_host") = 0, py::arg("prepped") = 0);
   m.def("sgd_persist_blocks", [](int grid_blocks) { return fdx::sgd_persist_blocks(grid_blocks); });
   m.def("sgd_full_blocks", []() { return fdx::sgd_full_blocks(); });
   m.attr("SGD_PERSIST_WORDS") = fdx::kSgdPersistWords;

@@ -145,15 +145,39 @@ void launch_smote_bucket(int stage, int mq, int k, int64_t n_new, int64_t sample
 struct RowHole {
   int64_t at = 0, len = 0;
 };
+// A Newton iteration in ONE launch (single process): the pass's blocks write their partials as
+// usual; the last block of each group of kNewtonGroup blocks reduces its group's partials to fp64
+// (fixed block order; the Hessian's upper triangle only), the last of those reduces the groups
+// (fixed order) into `red` -- logreg_reduce's output with H mirrored exactly symmetric -- and runs
+// the Newton update on its first wave.  Replaces the logreg_reduce + newton_update launches.
+constexpr int kNewtonGroup = 16;
+constexpr int kNewtonMaxGroups = 128;
+constexpr int kNewtonCols = 35 + 528;  // grad, loss, weight, H weight + the upper triangle of H
+constexpr int kNewtonColStride = 576;
+// workspace (8-byte words): tickets (kNewtonMaxGroups + 1 uint32, zero, left zero), then the fp64
+// group sums [kNewtonMaxGroups][kNewtonColStride]
+constexpr int kNewtonFuseWords = (kNewtonMaxGroups + 2) / 2 + kNewtonMaxGroups * kNewtonColStride;
+struct NewtonFuse {
+  double* red = nullptr;  // null: no fused update (the plain pass)
+  unsigned long long* ws = nullptr;  // [kNewtonFuseWords]
+  double* st = nullptr;
+  float* w32 = nullptr;
+  int* done = nullptr;
+  const double* aff = nullptr;
+  int* done_host = nullptr;
+  double C = 1.0, tol = 0.0;
+  int d = 30, max_iter = 1, fit_intercept = 1, phase_start = 0, seq = 0;
+};
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream, const SmoteView* sv = nullptr,
-                        int row_phase = 0, bool fisher = false, RowHole hole = {});
+                        int row_phase = 0, bool fisher = false, RowHole hole = {},
+                        const NewtonFuse* nf = nullptr);
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
                             float x_scale, float* partial, int nblocks, hipStream_t stream,
                             const SmoteView* sv = nullptr, int row_phase = 0, bool fisher = false,
-                            RowHole hole = {});
+                            RowHole hole = {}, const NewtonFuse* nf = nullptr);
 void launch_logreg_reduce(const float* partial, int nblocks, int ncols, double* out,
                           const int* done, hipStream_t stream);
 // state layout: see logreg.hip NewtonState.
@@ -172,8 +196,11 @@ struct LRInitArgs {
   double w0[32];
   float cw0, cw1;
 };
+// persist_ws (nullable): also do the persistent SGD launch's prep (zero the barrier/accumulator
+// words, back up the initial state) in the same kernel -- SgdPersistArgs::prepped
 void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
-                        const double* aff, hipStream_t stream, const double* w0_dev = nullptr);
+                        const double* aff, hipStream_t stream, const double* w0_dev = nullptr,
+                        unsigned long long* persist_ws = nullptr);
 void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream);
 // Minibatch SGD step (logreg.hip sgd_apply): c = epoch step scalar (lr = c / mean curvature),
 // nb = minibatches per epoch, avg = add this step's iterate to the Polyak average, epoch_end =
@@ -236,6 +263,10 @@ struct SgdPersistArgs {
                                          // (tools/sgd_stamps.py)
   unsigned spin_limit = 1u << 20;        // barrier polls before a block declares the grid not resident
   int fault_test = 0;                    // test knob: barrier s0 unreachable -> the recovery launch runs
+  // nullable: device address of a mapped pinned [kStateSize] fp64 slot -- the recovery launch
+  // exports the final state there (instead of a separate logreg_export launch behind it)
+  double* export_host = nullptr;
+  int prepped = 0;  // logreg_init already zeroed ws and backed up the initial state (no prep launch)
 };
 // Returns 0 when enqueued (prep kernel, the persistent launch, its recovery launch); 1 when the
 // cooperative launch refused the grid (nothing enqueued: the caller runs the per-step launches).

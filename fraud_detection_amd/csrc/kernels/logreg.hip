@@ -535,6 +535,43 @@ __device__ __forceinline__ void bf16_wave_pass(
   }
 }
 
+// Agent-scope relaxed loads/stores: coherent across the XCDs' L2s within one launch.
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The Newton update's LDS (one wave).  Lc, the Cholesky factor's columns ([column][row], rows
+// padded to 33), reuses sr's Hessian words [64, 64 + 32*33): H is in registers by then.  Fits in
+// the pass kernels' 16 KiB row tile, so a pass that runs the update in its last block
+// (newton_fused_tail) needs no extra LDS.
+struct NewtonLds {
+  double sr[64 + 32 * 33];  // >= kLRPartStride
+  double cA[32], iA[32], h30[32];
+  double ss[256];  // kStateSize
+  double grad[32];
+  double dv[32];
+  int idx[32];
+};
+static_assert(64 + 32 * 33 >= kLRPartStride, "NewtonLds::sr holds the reduced vector");
+
+// One-wave LDS ordering: LDS ops of one wave retire in order; this keeps the compiler from moving
+// them across (the update runs on one wave, alone or as the last wave standing in a pass block).
+__device__ __forceinline__ void nsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// A Newton iteration's fused tail (launchers.h NewtonFuse), behind the partials of a pass block;
+// defined with the update (newton_update_body).  lds: the block's row tile, free by then.
+template <bool HESS>
+__device__ __forceinline__ void newton_fused_tail(const float* __restrict__ partial, const NewtonFuse nf, void* lds);
+
 // VIRT: the rows past the stored ones are virtual SMOTE samples (pick_terms above); the stored
 // rows stream as usual, then the grid walks tiles of 16 picks (4 lanes per pick, 8 columns each).
 // row_sub / row_phase: the pass visits the row tiles t with t mod row_sub == row_phase and the pick
@@ -547,9 +584,14 @@ template <bool HESS, bool VIRT = false, bool FISH = false, bool FUSE = false>  /
 __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     const void* __restrict__ Xv, int64_t row_begin, int64_t row_end, const float* w,
     const float* __restrict__ class_w, const int* __restrict__ done, int hess_stride, int row_sub,
-    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole, SgdFuse fz) {
-  if (done != nullptr && *done) return;  // converged: uniform early exit for the whole grid
+    int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole, SgdFuse fz, NewtonFuse nf) {
+  if (done != nullptr && *done) {  // converged: uniform early exit for the whole grid
+    if (nf.done_host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)  // the update's flag word
+      __hip_atomic_store(nf.done_host, (nf.seq << 1) | 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
+  static_assert(sizeof(NewtonLds) <= sizeof(tile), "the fused Newton update reuses the row tile");
   __shared__ float red[kWaves][36];
   const int lane = lane_id(), wv = wave_id();
   const int q = lane & 3;
@@ -602,14 +644,26 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_kernel(
     return;
   }
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
+  const bool coherent = !FISH && nf.red != nullptr;  // a fused Newton tail reads them in this launch
   // slot 34 (Hessian weight) only from Hessian passes, slot 35 (curvature sum) from FISH passes
   if (threadIdx.x < (HESS ? 35 : 34) || (FISH && threadIdx.x == 35)) {
     const int t = threadIdx.x;
-    out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    const float v = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if (coherent) st_agent(out + t, v);
+    else out[t] = v;
   }
   if constexpr (HESS) {
-    for (int e = threadIdx.x; e < 1024; e += kThreads)
-      out[64 + e] = ((hb[e] + hb[1024 + e]) + hb[2048 + e]) + hb[3072 + e];
+    for (int e = threadIdx.x; e < 1024; e += kThreads) {
+      const float v = ((hb[e] + hb[1024 + e]) + hb[2048 + e]) + hb[3072 + e];
+      if (coherent) st_agent(out + 64 + e, v);
+      else out[64 + e] = v;
+    }
+  }
+  if constexpr (!FISH) {
+    if (nf.red != nullptr) {  // uniform: this launch also reduces and applies the Newton update
+      __syncthreads();        // hb (the row tile) read out before the tail reuses it
+      newton_fused_tail<HESS>(partial, nf, &tile[0][0]);
+    }
   }
 }
 
@@ -837,8 +891,12 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     const uint8_t* __restrict__ X8, int64_t row_begin, int64_t row_end, const float* w,
     const float* __restrict__ class_w, const int* __restrict__ done, float x_scale, int d_feat,
     int hess_stride, int row_sub, int row_phase, float* __restrict__ partial, SmoteView sv, RowHole hole,
-    SgdFuse fz) {
-  if (done != nullptr && *done) return;
+    SgdFuse fz, NewtonFuse nf) {
+  if (done != nullptr && *done) {
+    if (nf.done_host != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+      __hip_atomic_store(nf.done_host, (nf.seq << 1) | 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   __shared__ __attribute__((aligned(16))) uint16_t tile[kWaves][64 * kCols];  // 16 KiB
   __shared__ float red[kWaves][36];
   const int lane = lane_id(), wv = wave_id();
@@ -916,13 +974,25 @@ __global__ __launch_bounds__(kThreads, 3) void logreg_pass_fp8w_kernel(
     return;
   }
   float* out = partial + (int64_t)blockIdx.x * kLRPartStride;
+  const bool coherent = !FISH && nf.red != nullptr;
   if (threadIdx.x < (HESS ? 35 : 34) || (FISH && threadIdx.x == 35)) {
     const int t = threadIdx.x;
-    out[t] = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    const float v = ((red[0][t] + red[1][t]) + red[2][t]) + red[3][t];
+    if (coherent) st_agent(out + t, v);
+    else out[t] = v;
   }
   if constexpr (HESS) {
-    for (int e = threadIdx.x; e < 1024; e += kThreads)
-      out[64 + e] = ((hb[e] + hb[1024 + e]) + hb[2048 + e]) + hb[3072 + e];
+    for (int e = threadIdx.x; e < 1024; e += kThreads) {
+      const float v = ((hb[e] + hb[1024 + e]) + hb[2048 + e]) + hb[3072 + e];
+      if (coherent) st_agent(out + 64 + e, v);
+      else out[64 + e] = v;
+    }
+  }
+  if constexpr (!FISH) {
+    if (nf.red != nullptr) {  // uniform: this launch also reduces and applies the Newton update
+      __syncthreads();        // hb (the row tile) read out before the tail reuses it
+      newton_fused_tail<HESS>(partial, nf, &tile[0][0]);
+    }
   }
 }
 
@@ -977,6 +1047,7 @@ enum : int {
   kObjPrev = 128, kIter = 129, kBacktracks = 130, kGmax = 131, kObj = 132, kNAccepted = 133,
   kConverged = 134, kStateSize = 256
 };
+static_assert(kStateSize == 256, "NewtonLds::ss is sized for the state");
 
 __device__ void build_grad(const double* red, const double* st, int d, int fit_intercept,
                            double reg, double S, double* grad, int t) {
@@ -1016,25 +1087,24 @@ __device__ __forceinline__ void store_folded(const double* ss, const double* cA,
     }                                                                                             \
   } while (0)
 
-template <int MT, bool STAMP = false>  // MT > 0: compile-time number of active coordinates (identity index map)
-__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
-                                                           double* __restrict__ st,
-                                                           float* __restrict__ w32,
-                                                           int* __restrict__ done, int d, double C,
-                                                           double tol, int max_iter,
-                                                           int fit_intercept, int phase_start,
-                                                           const double* __restrict__ aff,
-                                                           unsigned long long* __restrict__ stamps = nullptr,
-                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
+// MT > 0: compile-time number of active coordinates (identity index map).  Lane t of one wave.
+// SR_READY: L.sr already holds the reduced vector (the fused tail wrote it): no reload of red.
+template <int MT, bool STAMP = false, bool SR_READY = false>
+__device__ __forceinline__ void newton_update_body(const double* __restrict__ red, double* __restrict__ st, float* __restrict__ w32,
+                                   int* __restrict__ done, int d, double C, double tol, int max_iter,
+                                   int fit_intercept, int phase_start, const double* __restrict__ aff,
+                                   unsigned long long* __restrict__ stamps, int* __restrict__ done_host, int seq,
+                                   NewtonLds& L, int t) {
   unsigned long long tsv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   FDX_STAMP(0);
-  __shared__ double sr[kLRPartStride];
-  __shared__ double cA[32], iA[32], h30[32];
-  __shared__ double ss[kStateSize];
-  __shared__ double grad[32];
-  __shared__ double Lc[64][65];  // [column][row], padded: every lane writes/reads in bounds
-  __shared__ int idx[32];
-  const int t = threadIdx.x;
+  double* sr = L.sr;
+  double* cA = L.cA;
+  double* iA = L.iA;
+  double* h30 = L.h30;
+  double* ss = L.ss;
+  double* grad = L.grad;
+  int* idx = L.idx;
+  auto Lc = [&L](int k, int r) -> double& { return L.sr[64 + k * 33 + r]; };
   {
     // Issue every global load before the first wait: 17 + 4 independent loads per lane plus
     // the done flag, instead of a load -> wait -> ds_write chain per element.
@@ -1042,8 +1112,10 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     const int dn = *done;
     const double av = aff ? aff[t] : 0.0;
     double v[NR], u[NS];
+    if constexpr (!SR_READY) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) v[i] = red[t + 64 * i];
+      for (int i = 0; i < NR; ++i) v[i] = red[t + 64 * i];
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) u[i] = st[t + 64 * i];
     if (dn) {
@@ -1051,13 +1123,15 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         __hip_atomic_store(done_host, (seq << 1) | 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       return;
     }
+    if constexpr (!SR_READY) {
 #pragma unroll
-    for (int i = 0; i < NR; ++i) sr[t + 64 * i] = v[i];
+      for (int i = 0; i < NR; ++i) sr[t + 64 * i] = v[i];
+    }
 #pragma unroll
     for (int i = 0; i < NS; ++i) ss[t + 64 * i] = u[i];
     if (t < 32) cA[t] = av; else iA[t - 32] = av;
   }
-  __syncthreads();
+  nsync();
   FDX_STAMP(1);
   if (aff) {
     // Rows hold s = x - pivot; standardized z = (s - c) * inv with c = inv = identity on the
@@ -1065,7 +1139,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     // H_z[j][k] = inv_j inv_k (H_jk - c_j H_30k - c_k H_j30 + c_j c_k H_30,30) (H symmetric).
     const double g30 = sr[kBiasCol];
     if (t < 32) h30[t] = sr[64 + kBiasCol * kCols + t];
-    __syncthreads();
+    nsync();
     if (t < 32) sr[t] = iA[t] * (sr[t] - cA[t] * g30);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -1073,7 +1147,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       const double hv = sr[64 + e] - cA[j] * h30[k] - cA[k] * h30[j] + cA[j] * cA[k] * h30[kBiasCol];
       sr[64 + e] = iA[j] * iA[k] * hv;
     }
-    __syncthreads();
+    nsync();
   }
   FDX_STAMP(2);
   const double S = sr[33] > 0.0 ? sr[33] : 1.0;
@@ -1083,7 +1157,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   const int my = (t < d) ? t : (t == d && fit_intercept ? kBiasCol : -1);
   if (t < 32) idx[t] = my;
   build_grad(sr, ss, d, fit_intercept, reg, S, grad, t);
-  __syncthreads();
+  nsync();
   double w2 = (t < d) ? ss[kW + t] * ss[kW + t] : 0.0;
   double ga = (t < m) ? fabs(grad[my]) : 0.0;
   w2 = wave_sum(w2);
@@ -1102,7 +1176,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
   if (it > 0 && obj > prev + 1e-6 * fabs(prev) && nbt < 40.0) dec = 1;
   else if (gmax <= tol) dec = 2;
   else dec = 0;
-  __syncthreads();
+  nsync();
   if (t == 0) {
     ss[kObj] = obj;
     if (dec != 1) ss[kGmax] = gmax;
@@ -1146,9 +1220,9 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       }
     }
     double bi = (t < m) ? -grad[my < 0 ? 0 : my] * S : 0.0;
+    nsync();  // every read of H (sr[64..]) before the first write of Lc, which reuses it
     FDX_STAMP(3);
     constexpr int JE = MT > 0 ? MT : 32;
-    double dv[32];
     // Column k of L is broadcast to the trailing update with v_readlane (L[j][k] lives in lane j:
     // an SGPR operand of the fma) instead of an LDS write + wait + read-back per column, which
     // was ~680 cycles of a 31-step dependent chain (tools/newton_stamps.py).  The forward solve
@@ -1159,25 +1233,25 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
         const double akk = fmax(rdlane(a[k], k), 1e-300);
         double inv = __builtin_amdgcn_rsq(akk);
         inv = inv * fma(-0.5 * akk * inv, inv, 1.5);
-        dv[k] = inv;
+        if (t == k) L.dv[k] = inv;  // uniform: read back by the back substitution
         const double ak = (t == k) ? akk * inv : a[k] * inv;  // column k of L (rows t > k)
         a[k] = ak;
-        Lc[k][t] = ak;  // only the back substitution reads it (column t of lane t's row)
+        if (t < 32) Lc(k, t) = ak;  // only the back substitution reads it (column t of lane t's row)
         const double yk = rdlane(bi, k) * inv;
         bi = (t == k) ? yk : (t > k ? fma(-ak, yk, bi) : bi);
 #pragma unroll
         for (int j = k + 1; j < JE; ++j) a[j] = fma(-ak, rdlane(ak, j), a[j]);
       } else {
-        dv[k] = 0.0;
+        if (t == 0) L.dv[k] = 0.0;
       }
     }
     FDX_STAMP(4);
-    __builtin_amdgcn_wave_barrier();  // Lc complete (one wave: LDS ops retire in order)
+    nsync();  // Lc and dv complete
 #pragma unroll
     for (int k = 31; k >= 0; --k) {  // L^T x = y (column sweep): lane t < k needs L[k][t] = Lc[t][k]
       if (k < m) {
-        const double xk = rdlane(bi, k) * dv[k];
-        const double lkt = Lc[t][k];
+        const double xk = rdlane(bi, k) * L.dv[k];
+        const double lkt = Lc(t & 31, k);
         bi = (t == k) ? xk : (t < k ? fma(-lkt, xk, bi) : bi);
       }
     }
@@ -1186,7 +1260,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       ss[kWPrev + t] = ss[kW + t];
       ss[kStep + t] = 0.0;
     }
-    __syncthreads();
+    nsync();
     if (t < m) {
       ss[kStep + my] = bi;
       ss[kW + my] = ss[kWPrev + my] + bi;
@@ -1197,7 +1271,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
       ss[kNAccepted] += 1.0;
     }
   }
-  __syncthreads();
+  nsync();
   if (t == 0) {
     ss[kIter] += 1.0;
     if (dec != 2 && (int)ss[kIter] >= max_iter) *done = 1;
@@ -1207,7 +1281,7 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     if (done_host != nullptr)
       __hip_atomic_store(done_host, (seq << 1) | *done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
-  __syncthreads();
+  nsync();
   if (aff) {
     store_folded(ss, cA, iA, w32, t);
   } else if (t < kCols) {
@@ -1220,7 +1294,149 @@ __global__ __launch_bounds__(64) void newton_update_kernel(const double* __restr
     if (t < 8) stamps[t] = tsv[t];
   }
 }
+
+template <int MT, bool STAMP = false>
+__global__ __launch_bounds__(64) void newton_update_kernel(const double* __restrict__ red,
+                                                           double* __restrict__ st,
+                                                           float* __restrict__ w32,
+                                                           int* __restrict__ done, int d, double C,
+                                                           double tol, int max_iter,
+                                                           int fit_intercept, int phase_start,
+                                                           const double* __restrict__ aff,
+                                                           unsigned long long* __restrict__ stamps = nullptr,
+                                                           int* __restrict__ done_host = nullptr, int seq = 0) {
+  __shared__ NewtonLds L;
+  newton_update_body<MT, STAMP>(red, st, w32, done, d, C, tol, max_iter, fit_intercept, phase_start, aff, stamps,
+                                done_host, seq, L, threadIdx.x);
+}
 #undef FDX_STAMP
+
+// Behind a pass block's partials (NewtonFuse): group tickets, then the global one.  The last block
+// of each group of kNewtonGroup blocks sums the group's partials in block order (fp64), the last
+// group reducer sums the groups in order into nf.red and its first wave runs newton_update_body.
+// Columns: [0, 35) and the Hessian [64, 1088) after a Hessian pass; [0, 34) after a gradient pass,
+// whose update keeps red[34..] (the held Hessian and its weight), as logreg_reduce does.
+// Cross-block data moves through agent-scope relaxed atomic stores and loads (coherent across the
+// XCDs' L2s) ordered by vmcnt(0) before each arrival: no release/acquire fence, whose L2 write-back
+// cost ~115 us per launch here (profiles/r6_t).
+// Compact column i of the fused reduction -> its slot in the [1088] vector: [0, 35) as is, then the
+// Hessian's upper triangle (j <= k) row by row.
+__device__ __forceinline__ void newton_col(int i, int kLo, int& j, int& k) {
+  if (i < kLo) {
+    j = -1;
+    k = i;
+    return;
+  }
+  int e = i - kLo, r = 0;
+  while (e >= 32 - r) {  // <= 32 steps, once per column
+    e -= 32 - r;
+    ++r;
+  }
+  j = r;
+  k = r + e;
+}
+
+template <bool HESS>
+__device__ __forceinline__ void newton_fused_tail(const float* __restrict__ partial, const NewtonFuse nf, void* lds) {
+  __shared__ int s_last;
+  const int t = threadIdx.x;
+  const int nblk = gridDim.x, grp = blockIdx.x / kNewtonGroup;
+  const int g0 = grp * kNewtonGroup, g1 = min(g0 + kNewtonGroup, nblk);
+  const int ngroups = (nblk + kNewtonGroup - 1) / kNewtonGroup;
+  unsigned int* tickets = reinterpret_cast<unsigned int*>(nf.ws);
+  double* gsum = reinterpret_cast<double*>(nf.ws + (kNewtonMaxGroups + 2) / 2);
+  constexpr int kLo = HESS ? 35 : 34;
+  constexpr int kCnt = HESS ? kLo + 528 : kLo;
+  constexpr int kPer = (kCnt + kThreads - 1) / kThreads;  // compact columns per thread (<= 3)
+  int cj[kPer], ck[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) newton_col(t + r * kThreads, kLo, cj[r], ck[r]);
+  auto slot = [](int j, int k) { return j < 0 ? k : 64 + j * kCols + k; };
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores have landed
+  __syncthreads();
+  if (t == 0) {
+    const unsigned q = __hip_atomic_fetch_add(tickets + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = q == (unsigned)(g1 - g0 - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_last) return;  // uniform per block
+  if (t == 0) st_agent(tickets + grp, 0u);
+  {  // the group's partials: every load of this thread in flight at once, summed in block order
+    float v[kPer][kNewtonGroup];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const bool on = t + r * kThreads < kCnt;
+      const float* p = partial + slot(cj[r], ck[r]);
+#pragma unroll
+      for (int u = 0; u < kNewtonGroup; ++u)
+        v[r][u] = (on && g0 + u < g1) ? ld_agent(p + (int64_t)(g0 + u) * kLRPartStride) : 0.0f;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      double acc = 0.0;
+#pragma unroll
+      for (int u = 0; u < kNewtonGroup; ++u) acc += (double)v[r][u];
+      if (t + r * kThreads < kCnt) st_agent(gsum + (int64_t)grp * kNewtonColStride + t + r * kThreads, acc);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) {
+    const unsigned q =
+        __hip_atomic_fetch_add(tickets + kNewtonMaxGroups, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = q == (unsigned)(ngroups - 1) ? 1 : 0;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (t == 0) st_agent(tickets + kNewtonMaxGroups, 0u);
+  NewtonLds& L = *reinterpret_cast<NewtonLds*>(lds);
+  // the groups, in order, kB loads per column in flight -> L.sr (H mirrored) and nf.red
+  double acc[kPer];
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) acc[r] = 0.0;
+  constexpr int kB = 8;  // group sums per column in flight (registers: the pass's budget)
+  for (int g = 0; g < ngroups; g += kB) {
+    double v[kPer][kB];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const bool on = t + r * kThreads < kCnt;
+      const double* p = gsum + t + r * kThreads;
+#pragma unroll
+      for (int u = 0; u < kB; ++u) v[r][u] = (on && g + u < ngroups) ? ld_agent(p + (int64_t)(g + u) * kNewtonColStride) : 0.0;
+    }
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+#pragma unroll
+      for (int u = 0; u < kB; ++u) acc[r] += v[r][u];
+    }
+  }
+  if constexpr (!HESS) {  // a gradient pass keeps the held Hessian and its weight: red[34..]
+    for (int e = 34 + t; e < kLRPartStride; e += kThreads) L.sr[e] = nf.red[e];
+  } else {
+    if (t < 64 - kLo) L.sr[kLo + t] = 0.0;  // slots [35, 64): unused
+  }
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) {
+    if (t + r * kThreads < kCnt) {
+      const int j = cj[r], k = ck[r];
+      L.sr[slot(j, k)] = acc[r];
+      nf.red[slot(j, k)] = acc[r];
+      if (j >= 0 && j != k) {
+        L.sr[slot(k, j)] = acc[r];
+        nf.red[slot(k, j)] = acc[r];
+      }
+    }
+  }
+  __syncthreads();
+  if (t >= kWave) return;  // whole waves: the update is one wave's work
+  if (nf.d == 30 && nf.fit_intercept)
+    newton_update_body<31, false, true>(nf.red, nf.st, nf.w32, nf.done, nf.d, nf.C, nf.tol, nf.max_iter,
+                                        nf.fit_intercept, nf.phase_start, nf.aff, nullptr, nf.done_host, nf.seq, L, t);
+  else
+    newton_update_body<0, false, true>(nf.red, nf.st, nf.w32, nf.done, nf.d, nf.C, nf.tol, nf.max_iter,
+                                       nf.fit_intercept, nf.phase_start, nf.aff, nullptr, nf.done_host, nf.seq, L, t);
+}
+
 
 // Standardized-space weights (state) -> weights for pivot-shifted rows.  One wave.
 __global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restrict__ st,
@@ -1241,10 +1457,16 @@ __global__ __launch_bounds__(64) void logreg_fold_kernel(const double* __restric
 // w0_dev (nullable): the initial weights from device memory instead of the arguments -- another
 // fit's standardized-space state (a CV fold warm-started from the previous fold, stream-ordered
 // after that fit's enqueued iterations, no host round trip).
+__device__ void persist_prep_block(unsigned long long* ws, const double* st, const float* w32, int done, int t,
+                                   int nt);  // defined with the persistent workspace layout below
+
+// pws (nullable): the persistent SGD workspace -- its prep (persist_prep_block) runs here too, one
+// launch less per fit (SgdPersistArgs::prepped).
 __global__ __launch_bounds__(64) void logreg_init_kernel(LRInitArgs a, double* __restrict__ st,
                                                          float* __restrict__ w32, float* __restrict__ cw,
                                                          int* __restrict__ done, const double* __restrict__ aff,
-                                                         const double* __restrict__ w0_dev) {
+                                                         const double* __restrict__ w0_dev,
+                                                         unsigned long long* __restrict__ pws) {
   __shared__ double ss[kW + 32], cA[32], iA[32];
   const int t = threadIdx.x;
   double w0 = 0.0;
@@ -1273,6 +1495,12 @@ __global__ __launch_bounds__(64) void logreg_init_kernel(LRInitArgs a, double* _
     store_folded(ss, cA, iA, w32, t);
   } else if (t < kCols) {
     w32[t] = (t == kLabelCol) ? 0.0f : (float)w0;
+  }
+  if (pws != nullptr) {
+    // the state and weights this block just stored: one work-group on one CU, so a barrier is the
+    // only ordering its own global reads need
+    __syncthreads();
+    persist_prep_block(pws, st, w32, 0, t, 64);
   }
 }
 
@@ -1797,17 +2025,21 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
 // sets and the fault word, and back up the initial solver state, weights and done flag for the
 // recovery launch (a faulted grid may have advanced some blocks' copies; the recovery restarts from
 // exactly what the persistent launch started from).
+__device__ void persist_prep_block(unsigned long long* ws, const double* st, const float* w32, int done, int t,
+                                   int nt) {
+  for (int e = t; e < kWsBackup; e += nt) ws[e] = 0ull;
+  double* bst = reinterpret_cast<double*>(ws + kWsBackup);
+  for (int e = t; e < kStateSize; e += nt) bst[e] = st[e];
+  float* bw = reinterpret_cast<float*>(ws + kWsBackupW);
+  if (t < 32) bw[t] = w32[t];
+  if (t == 0) ws[kWsBackupDone] = (unsigned long long)(unsigned)done;
+}
+
 __global__ __launch_bounds__(256) void sgd_persist_prep_kernel(unsigned long long* __restrict__ ws,
                                                                const double* __restrict__ st,
                                                                const float* __restrict__ w32,
                                                                const int* __restrict__ done) {
-  const int t = threadIdx.x;
-  for (int e = t; e < kWsBackup; e += 256) ws[e] = 0ull;
-  double* bst = reinterpret_cast<double*>(ws + kWsBackup);
-  for (int e = t; e < kStateSize; e += 256) bst[e] = st[e];
-  float* bw = reinterpret_cast<float*>(ws + kWsBackupW);
-  if (t < 32) bw[t] = w32[t];
-  if (t == 0) ws[kWsBackupDone] = (unsigned long long)(unsigned)*done;
+  persist_prep_block(ws, st, w32, *done, threadIdx.x, 256);
 }
 
 // Behind every persistent launch: a no-op unless its fault word is set.  Then one block re-runs
@@ -1823,8 +2055,12 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_recover_kernel(const v
                                                                          SmoteView sv, RowHole hole,
                                                                          SgdPersistArgs P) {
   if (__hip_atomic_load(reinterpret_cast<unsigned int*>(P.ws + kWsFault), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_AGENT) == 0u)
-    return;  // uniform: every thread reads the same word written by the previous launch
+                        __HIP_MEMORY_SCOPE_AGENT) == 0u) {  // uniform: the word the previous launch left
+    if (P.export_host != nullptr)  // the fit's final state -> the mapped pinned slot (logreg_export)
+      for (int e = threadIdx.x; e < kStateSize; e += kPersistThreads)
+        __hip_atomic_store(P.export_host + e, P.st[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   __shared__ double sst[kStateSize];
   __shared__ __attribute__((aligned(16))) float wsh[32];
   __shared__ float wnew[32];
@@ -1875,7 +2111,11 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_recover_kernel(const v
   }
   if (t == 0) sst[kSgdFault] = 2.0;
   __syncthreads();
-  for (int e = t; e < kStateSize; e += kPersistThreads) P.st[e] = sst[e];
+  for (int e = t; e < kStateSize; e += kPersistThreads) {
+    P.st[e] = sst[e];
+    if (P.export_host != nullptr)
+      __hip_atomic_store(P.export_host + e, sst[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
   if (t < 32) P.w32[t] = wnew[t];
   if (t == 0) *P.done = s_done;
 }
@@ -1928,10 +2168,22 @@ static void check_hole(const RowHole& h, int64_t row_begin, int64_t stored_end) 
     throw std::runtime_error("logreg_pass: row hole outside the stored rows");
 }
 
+// A fused Newton iteration (NewtonFuse) needs its buffers, a gradient or Hessian pass (not the
+// SGD curvature pass), the grid within the group workspace, and the pass's own done flag.
+static NewtonFuse checked_fuse(const NewtonFuse* nf, int nblocks, bool fisher, const int* done) {
+  if (nf == nullptr || nf->red == nullptr) return NewtonFuse{};
+  if (fisher) throw std::runtime_error("logreg_pass: a fused Newton update follows a gradient or Hessian pass");
+  if (nf->ws == nullptr || nf->st == nullptr || nf->w32 == nullptr || nf->done == nullptr || done != nf->done)
+    throw std::runtime_error("logreg_pass: fused Newton update needs ws/state/w32 and the pass's done flag");
+  if (nblocks < 1 || nblocks > kNewtonGroup * kNewtonMaxGroups)
+    throw std::runtime_error("logreg_pass: grid too large for the fused Newton workspace");
+  return *nf;
+}
+
 void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, const float* w,
                         const float* class_w, const int* done, int hessian, int row_sub,
                         float* partial, int nblocks, hipStream_t stream, const SmoteView* sv, int row_phase,
-                        bool fisher, RowHole hole) {
+                        bool fisher, RowHole hole, const NewtonFuse* nf) {
   // hessian: 0 = gradient/loss only; h >= 1 = also the Hessian, from every h-th row tile.
   // row_sub >= 1, 0 <= row_phase < row_sub: visit the 1/row_sub tile subset row_phase (progressive
   // Newton: phase 0; SGD: minibatch row_phase of an epoch of row_sub minibatches).
@@ -1944,9 +2196,10 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
   check_hole(hole, row_begin, v.parents != nullptr ? v.n_real : row_end);
   const bool virt = v.parents != nullptr;
   const int hs = hessian > 0 ? hessian : 1;
+  const NewtonFuse nfa = checked_fuse(nf, nblocks, fisher, done);
 #define FDX_LRP(H, V, F)                                                                                    \
   logreg_pass_kernel<H, V, F><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done, hs, \
-                                                                row_sub, row_phase, partial, v, hole, SgdFuse{})
+                                                                row_sub, row_phase, partial, v, hole, SgdFuse{}, nfa)
   if (hessian > 0) {
     if (virt) FDX_LRP(true, true, false);
     else FDX_LRP(true, false, false);
@@ -1964,7 +2217,7 @@ void launch_logreg_pass(const uint16_t* X, int64_t row_begin, int64_t row_end, c
 void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end, const float* w,
                             const float* class_w, const int* done, int hessian, int row_sub,
                             float x_scale, float* partial, int nblocks, hipStream_t stream, const SmoteView* sv,
-                            int row_phase, bool fisher, RowHole hole) {
+                            int row_phase, bool fisher, RowHole hole, const NewtonFuse* nf) {
   // fp8 rows store features * x_scale for columns < 30; the bias (col 30) and label (col 31)
   // are stored unscaled.  sv, row_phase, fisher: as launch_logreg_pass.
   if (row_sub < 1) row_sub = 1;
@@ -1974,10 +2227,11 @@ void launch_logreg_pass_fp8(const uint8_t* X, int64_t row_begin, int64_t row_end
   check_hole(hole, row_begin, v.parents != nullptr ? v.n_real : row_end);
   const bool virt = v.parents != nullptr;
   const int hs = hessian > 0 ? hessian : 1;
+  const NewtonFuse nfa = checked_fuse(nf, nblocks, fisher, done);
 #define FDX_LRP8(H, V, F)                                                                                       \
   logreg_pass_fp8w_kernel<H, V, F><<<nblocks, kThreads, 0, stream>>>(X, row_begin, row_end, w, class_w, done,   \
                                                                      x_scale, 30, hs, row_sub, row_phase, partial, v, hole, \
-                                                                     SgdFuse{})
+                                                                     SgdFuse{}, nfa)
   if (hessian > 0) {
     if (virt) FDX_LRP8(true, true, false);
     else FDX_LRP8(true, false, false);
@@ -2015,17 +2269,17 @@ void launch_sgd_pass_fused(const void* X, int fp8, float x_scale, int64_t row_en
     const uint8_t* X8 = static_cast<const uint8_t*>(X);
     if (virt)
       logreg_pass_fp8w_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X8, 0, row_end, w32, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X8, 0, row_end, w32, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
     else
       logreg_pass_fp8w_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X8, 0, row_end, w32, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X8, 0, row_end, w32, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
   } else {
     if (virt)
       logreg_pass_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X, 0, row_end, w32, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X, 0, row_end, w32, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
     else
       logreg_pass_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X, 0, row_end, w32, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X, 0, row_end, w32, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
   }
   check_launch("sgd_pass_fused");
 }
@@ -2057,8 +2311,9 @@ void launch_newton_update_stamped(const double* red, double* state, float* w32, 
 }
 
 void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
-                        const double* aff, hipStream_t stream, const double* w0_dev) {
-  logreg_init_kernel<<<1, 64, 0, stream>>>(a, state, w32, class_w, done, aff, w0_dev);
+                        const double* aff, hipStream_t stream, const double* w0_dev,
+                        unsigned long long* persist_ws) {
+  logreg_init_kernel<<<1, 64, 0, stream>>>(a, state, w32, class_w, done, aff, w0_dev, persist_ws);
   check_launch("logreg_init");
 }
 
@@ -2103,17 +2358,17 @@ void launch_sgd_pass_sums(const void* X, int fp8, float x_scale, int64_t row_end
     const uint8_t* X8 = static_cast<const uint8_t*>(X);
     if (virt)
       logreg_pass_fp8w_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X8, 0, row_end, w, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X8, 0, row_end, w, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
     else
       logreg_pass_fp8w_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X8, 0, row_end, w, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X8, 0, row_end, w, class_w, done, x_scale, 30, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
   } else {
     if (virt)
       logreg_pass_kernel<false, true, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X, 0, row_end, w, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X, 0, row_end, w, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
     else
       logreg_pass_kernel<false, false, true, true><<<nblocks, kThreads, 0, stream>>>(
-          X, 0, row_end, w, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz);
+          X, 0, row_end, w, class_w, done, 1, row_sub, row_phase, nullptr, v, hole, fz, NewtonFuse{});
   }
   check_launch("sgd_pass_sums");
 }
@@ -2194,8 +2449,10 @@ int launch_sgd_persist(const void* X, int fp8, float x_scale, int64_t row_end, c
     kern = virt ? (const void*)sgd_persist_kernel<false, true, 16, 2, 2> : (const void*)sgd_persist_kernel<false, false, 16, 2, 2>;
   }
   // barrier shards, accumulator sets, fault word: zero; the initial state: backed up (stream-ordered)
-  sgd_persist_prep_kernel<<<1, 256, 0, stream>>>(a.ws, a.st, a.w32, a.done);
-  check_launch("sgd_persist_prep");
+  if (!a.prepped) {  // else logreg_init did it (stream-ordered in front of this launch)
+    sgd_persist_prep_kernel<<<1, 256, 0, stream>>>(a.ws, a.st, a.w32, a.done);
+    check_launch("sgd_persist_prep");
+  }
   SgdPersistArgs pa = a;
   void* args[] = {(void*)&X, (void*)&row_end, (void*)&x_scale, (void*)&class_w, (void*)&v, (void*)&hole,
                   (void*)&pa};

@@ -17,6 +17,7 @@ The device loop never synchronises with the host inside a chunk of iterations: a
 """
 from __future__ import annotations
 
+import os
 import time
 
 from dataclasses import dataclass, field
@@ -187,21 +188,10 @@ class PendingFit:
     _POOL = 8
 
     def __init__(self, state_dev: torch.Tensor, sgd: bool = False, verify=None, warm_iters: int = 0,
-                 keep: tuple = (), collective: bool = False):
+                 keep: tuple = (), collective: bool = False, slot: int | None = None, exported: bool = False):
         cls = PendingFit
-        if not cls._pool:
-            cls._pool = [torch.empty(state_dev.numel(), dtype=torch.float64, pin_memory=True)
-                         for _ in range(cls._POOL)]
-            cls._owners = [None] * cls._POOL
-            # device addresses of the mapped pinned slots: the export kernel stores into them
-            cls._pool_dev = [int(native().host_device_pointer(t.data_ptr())) for t in cls._pool]
-        slot = cls._next % cls._POOL
-        cls._next += 1
-        prev = cls._owners[slot]
-        if prev is not None:
-            # a program-order point every rank reaches at the same fit (slots rotate identically
-            # on every rank): verifying a DP fit here is collective-safe
-            prev._materialize(collective_ok=True)
+        if slot is None:
+            slot = cls.reserve()
         cls._owners[slot] = self
         self._slot, self._sgd, self._info = slot, sgd, None
         self._verify, self._state_dev, self.warm_iters = verify, state_dev, int(warm_iters)
@@ -213,11 +203,37 @@ class PendingFit:
         # that every rank makes (DevicePipeline.settle, evaluate) may run it -- a field read on
         # one rank alone would enter the collectives alone and hang the job
         self._collective = bool(collective)
-        self._export()
+        self._export(exported)
 
-    def _export(self):
+    @classmethod
+    def reserve(cls) -> int:
+        """The next pinned slot, its previous owner materialised.  A fit that exports its own final
+        state (the persistent SGD launch's recovery kernel stores it into ``slot_address``) reserves
+        the slot before enqueueing, then wraps it with ``PendingFit(..., slot=, exported=True)``."""
+        if not cls._pool:
+            cls._pool = [torch.empty(STATE_SIZE, dtype=torch.float64, pin_memory=True) for _ in range(cls._POOL)]
+            cls._owners = [None] * cls._POOL
+            # device addresses of the mapped pinned slots: the export kernel stores into them
+            cls._pool_dev = [int(native().host_device_pointer(t.data_ptr())) for t in cls._pool]
+        slot = cls._next % cls._POOL
+        cls._next += 1
+        prev = cls._owners[slot]
+        if prev is not None:
+            # a program-order point every rank reaches at the same fit (slots rotate identically
+            # on every rank): verifying a DP fit here is collective-safe
+            prev._materialize(collective_ok=True)
+        cls._owners[slot] = None
+        return slot
+
+    @classmethod
+    def slot_address(cls, slot: int) -> int:
+        return cls._pool_dev[slot]
+
+    def _export(self, done: bool = False):
         cls, slot, st = PendingFit, self._slot, self._state_dev
-        if cls._pool_dev[slot] and st.numel() == STATE_SIZE:
+        if done:
+            pass  # already enqueued by the fit's last kernel
+        elif cls._pool_dev[slot] and st.numel() == STATE_SIZE:
             native().logreg_export(ptr(st), cls._pool_dev[slot], stream_of(st))
         else:
             cls._pool[slot].copy_(st, non_blocking=True)
@@ -294,6 +310,8 @@ class LRWorkspace:
         # data-parallel lean step's folded fixed-point sums (the all-reduced vector)
         self.sgd_persist = torch.zeros(int(m.SGD_PERSIST_WORDS), device=device, dtype=torch.int64)
         self.sgd_sums = torch.zeros(SGD_SLOTS, device=device, dtype=torch.int64)
+        # fused Newton iterations: group tickets (zero, left zero) + fp64 group sums
+        self.newton_fuse = torch.zeros(int(m.NEWTON_FUSE_WORDS), device=device, dtype=torch.int64)
 
     def prepare_flags(self, depth: int = 2):
         """The mapped pinned convergence-flag words newton_fit polls (pinned allocations cost tens
@@ -305,15 +323,18 @@ class LRWorkspace:
             self._events = [torch.cuda.Event() for _ in range(depth + 1)]
             self._seq = getattr(self, "_seq", 0)
 
-    def reset(self, w0: np.ndarray, class_w=(1.0, 1.0), aff: int = 0, w0_dev: int = 0):
+    def reset(self, w0: np.ndarray, class_w=(1.0, 1.0), aff: int = 0, w0_dev: int = 0, persist: bool = False):
         """Initial state (w0 in the padded layout, class weights, done = 0) written by ONE kernel
         whose arguments carry the values -- no pinned staging and no H2D blit.  ``aff``: device
         address of the [64] affine map of pivot-shifted rows (w32 gets the folded weights).
         ``w0_dev``: device address of 32 fp64 standardized-space weights that replace ``w0`` (another
-        fit's state: a warm start with no host round trip)."""
+        fit's state: a warm start with no host round trip).  ``persist``: the same kernel also preps
+        the persistent SGD workspace (zeroed barrier/accumulators, initial-state backup), so the
+        persistent launch that follows needs no prep launch (sgd_persist(prepped=1))."""
         w = np.asarray(w0, dtype=np.float64).reshape(-1)
         native().logreg_init(ptr(self.state), ptr(self.w32), ptr(self.class_w), ptr(self.done), w.tolist(),
-                             float(class_w[0]), float(class_w[1]), int(aff), stream_of(self.state), int(w0_dev))
+                             float(class_w[0]), float(class_w[1]), int(aff), stream_of(self.state), int(w0_dev),
+                             ptr(self.sgd_persist) if persist else 0)
 
 
 _BLOB_BYTES = 2304
@@ -371,13 +392,22 @@ def progressive_schedule(n_rows: int) -> list:
 
 
 def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scale: float, s: int, done=True,
-          sub: int = 1, virtual: VirtualSmote | None = None, hole: tuple = (0, 0)):
+          sub: int = 1, virtual: VirtualSmote | None = None, hole: tuple = (0, 0), update: tuple | None = None):
     """hessian: 0 = gradient/loss only; h >= 1 = Hessian from every h-th row tile (h = 1 exact).
     sub: visit a uniform 1/sub of the row tiles (progressive Newton warm-up).
     virtual: rows >= rows.shape[0] are virtual SMOTE rows (end may reach n_real + n_new).
     hole: (at, len) stored rows [at, at + len) the pass steps over (a CV fold's validation block);
-    ``end`` counts logical rows (the hole excluded)."""
+    ``end`` counts logical rows (the hole excluded).
+    update: (aff, C, tol, d, max_iter, fit_intercept, phase_start, done_host, seq) -- the Newton
+    update after the pass.  Fused (FDX_NEWTON_FUSE=1): the pass's last blocks reduce the
+    partials and apply it in the same launch (logreg.hip newton_fused_tail); else logreg_reduce +
+    newton_update launches."""
     dptr = ptr(ws.done) if done else 0
+    nf = None
+    if update is not None and _newton_fuse() and done:
+        aff, C, tol, d, max_iter, fi, phase_start, done_host, seq = update
+        nf = (ptr(ws.red), ptr(ws.newton_fuse), ptr(ws.state), ptr(ws.w32), ptr(ws.done), int(aff), int(done_host),
+              float(C), float(tol), int(d), int(max_iter), int(fi), int(phase_start), int(seq))
     h = int(hessian)
     ha, hl = int(hole[0]), int(hole[1])
     end += hl  # physical end
@@ -389,17 +419,28 @@ def _pass(m, rows, ws: LRWorkspace, hessian: int, begin: int, end: int, fp8_scal
         m.logreg_pass_virtual(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub),
                               ptr(ws.partial), nb, s, ptr(v.parents), ptr(v.nbr), ptr(v.lam), ptr(v.off),
                               ptr(v.cnt), int(rows.shape[0]), int(v.q_offset), int(mq), int(k),
-                              float(fp8_scale) if fp8 else 0.0, 0, False, ha, hl)
+                              float(fp8_scale) if fp8 else 0.0, 0, False, ha, hl, nf)
     elif storage_kind(rows) == "bf16":
         nb = ws.nblocks
         m.logreg_pass(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), ptr(ws.partial),
-                      nb, s, 0, False, ha, hl)
+                      nb, s, 0, False, ha, hl, nf)
     else:
         nb = ws.nblocks_fp8
         m.logreg_pass_fp8(ptr(rows), begin, end, ptr(ws.w32), ptr(ws.class_w), dptr, h, int(sub), float(fp8_scale),
-                          ptr(ws.partial), nb, s, 0, False, ha, hl)
+                          ptr(ws.partial), nb, s, 0, False, ha, hl, nf)
+    if nf is not None:
+        return
     # gradient-only: reduce slots 0..33 and keep red[34] (weight of the rows behind the held H)
     m.logreg_reduce(ptr(ws.partial), nb, PART_STRIDE if h else GRAD_SLOTS, ptr(ws.red), dptr, s)
+    if update is not None:
+        aff, C, tol, d, max_iter, fi, phase_start, done_host, seq = update
+        m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), int(d), float(C), float(tol),
+                        int(max_iter), int(fi), int(phase_start), int(aff), s, int(done_host), int(seq))
+
+
+def _newton_fuse() -> bool:
+    """FDX_NEWTON_FUSE=1: the Newton update in the pass launch (newton_fused_tail); else the pass, logreg_reduce and newton_update launches."""
+    return os.environ.get("FDX_NEWTON_FUSE", "0") == "1"
 
 
 def logreg_pass(rows: torch.Tensor, w: torch.Tensor, class_w=(1.0, 1.0), hessian: bool = True,
@@ -563,11 +604,14 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
     for sub, iters in sched:
         hs_w = auto_warm_hess_stride(n_sched // sub) if hess_stride == "auto" else hs
         for j in range(iters):
-            _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual, hole=hole)
+            upd = (aff, C, 0.0, d, 1 << 30, int(fit_intercept), int(j == 0), 0, 0)
             if sync_warm:
+                _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual, hole=hole)
                 comm.all_reduce_(ws.red)
-            m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
-                            int(fit_intercept), int(j == 0), aff, s)
+                m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), 0.0, 1 << 30,
+                                int(fit_intercept), int(j == 0), aff, s)
+            else:  # the update in the pass's launch (fused) or right behind it
+                _pass(m, rows, ws, hs_w, 0, n, fp8_scale, s, sub=sub, virtual=virtual, hole=hole, update=upd)
         first[0] = 1
     if dp and local_warmup and sched:
         wv = ws.state[S_W:S_W + 32]
@@ -591,13 +635,16 @@ def newton_fit(rows: torch.Tensor, C: float = 1.0, tol: float = 1e-8, max_iter: 
             # 8 vs 7 iterations, profiles/r1_s25)
             fresh = refresh <= 0 or full_it[0] % refresh == 0
             full_it[0] += 1
-            _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual, hole=hole)
+            dh = done_host if i == k - 1 else 0
             if comm is not None and comm.world_size > 1:
+                _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual, hole=hole)
                 # a gradient-only pass leaves the (already all-reduced) Hessian and its weight
                 comm.all_reduce_(ws.red if fresh else ws.red[:GRAD_SLOTS])
-            m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
-                            int(max_iter + warm), int(fit_intercept), first[0], aff, s,
-                            done_host if i == k - 1 else 0, seq)
+                m.newton_update(ptr(ws.red), ptr(ws.state), ptr(ws.w32), ptr(ws.done), d, float(C), float(tol),
+                                int(max_iter + warm), int(fit_intercept), first[0], aff, s, dh, seq)
+            else:
+                _pass(m, rows, ws, hs if fresh else 0, 0, n, fp8_scale, s, virtual=virtual, hole=hole,
+                      update=(aff, C, tol, d, max_iter + warm, int(fit_intercept), first[0], dh, seq))
             first[0] = 0
         return k
 
@@ -851,7 +898,15 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         virtual.prepare()
     m = native()
     ws = workspace or LRWorkspace(rows.device)
-    ws.reset(w0, class_w, aff)
+    fp8 = storage_kind(rows) != "bf16"
+    blocks = ref.sgd_grid_blocks(n_stored, nb, ws.sgd_blocks)
+    dp = comm is not None and comm.world_size > 1
+    persist = (persistent if persistent is not None else _persist_default()) and not dp
+    persist = persist and epochs <= SGD_MAX_EPOCHS and m.sgd_persist_blocks(blocks) > 0
+    # the one-launch path (no checkpoint, no DP): the init kernel preps the persistent workspace and
+    # the recovery kernel exports the final state into a reserved pinned slot -- 2 launches fewer
+    fused = persist and checkpoint is None and got is None
+    ws.reset(w0, class_w, aff, persist=fused)
     s = stream_of(rows)
     if got is not None:
         ws.state.copy_(got[0]["state"].to(torch.float64).to(rows.device))
@@ -865,33 +920,31 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
         # a fit that had converged before the checkpoint stays converged: its remaining passes and
         # updates are no-ops, as in the uninterrupted fit (reset() cleared the device flag)
         ws.done.fill_(int(float(got[0]["state"][S_CONV]) > 0))
-    fp8 = storage_kind(rows) != "bf16"
-    blocks = ref.sgd_grid_blocks(n_stored, nb, ws.sgd_blocks)
-    dp = comm is not None and comm.world_size > 1
     v = virtual
     mq, k = (v.nbr.shape if v is not None else (0, 1))
 
     vargs = (ptr(v.parents) if v else 0, ptr(v.nbr) if v else 0, ptr(v.lam) if v else 0,
              ptr(v.off) if v else 0, ptr(v.cnt) if v else 0, int(rows.shape[0]),
              int(v.q_offset) if v else 0, int(mq), int(k), int(hole[0]), int(hole[1]))
-    persist = (persistent if persistent is not None else _persist_default()) and not dp
-    persist = persist and epochs <= SGD_MAX_EPOCHS and m.sgd_persist_blocks(blocks) > 0
 
-    def run_steps(s0: int, s1: int):
+    def run_steps(s0: int, s1: int, prepped: bool = False, export_slot: int | None = None) -> bool:
         """Steps [s0, s1) of the schedule: ONE persistent launch (a grid barrier per step, the
         update in every block), or one fused launch per step (FISH pass whose last block applies
-        the update) -- bitwise the same fit."""
+        the update) -- bitwise the same fit.  Returns True when the final state was exported into
+        ``export_slot`` by the persistent launch's recovery kernel."""
         if s1 <= s0:
-            return
+            return False
         if persist:
             refused = m.sgd_persist(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.class_w), *vargs,
                                     ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
                                     float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
                                     int(bool(serpentine)), [float(x) for x in lrs], int(s0), int(s1),
                                     4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs, nbs,
-                                    int(bool(_fault_test)), int(_spin_limit))
+                                    int(bool(_fault_test)), int(_spin_limit),
+                                    PendingFit.slot_address(export_slot) if export_slot is not None else 0,
+                                    int(bool(prepped)))
             if not refused:
-                return
+                return export_slot is not None
             # the cooperative launch refused the grid: the per-step launches (bitwise the same fit)
         if serpentine:
             raise ValueError("serpentine minibatch order needs the persistent SGD launch")
@@ -900,11 +953,14 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                   float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
                   [float(x) for x in lrs], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
                   ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs, nbs)
+        return False
 
     if not dp and checkpoint is None:
         s0 = estart[start[0]] + start[1]
-        run_steps(s0, estart[epochs] if max_steps is None else min(estart[epochs], int(max_steps)))
-        return PendingFit(ws.state, sgd=True)
+        slot = PendingFit.reserve() if fused else None
+        exported = run_steps(s0, estart[epochs] if max_steps is None else min(estart[epochs], int(max_steps)),
+                             prepped=fused, export_slot=slot)
+        return PendingFit(ws.state, sgd=True, slot=slot, exported=exported)
 
     def dp_epochs(e0: int, e1: int, all_reduce):
         """Epochs [e0, e1) of the lean data-parallel schedule, enqueued with no host sync: per step

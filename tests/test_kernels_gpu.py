@@ -234,6 +234,31 @@ def test_newton_deterministic(dev):
     assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("kind", ["bf16", "fp8", "virtual"])
+def test_newton_fused_iteration_matches_unfused(dev, kind, monkeypatch):
+    """FDX_NEWTON_FUSE: the pass's last blocks reduce the partials and run the Newton update in the
+    same launch (logreg.hip newton_fused_tail).  Same fit as pass + logreg_reduce + newton_update
+    up to the fp64 summation order (group sums instead of 64 row-groups): same iteration count and
+    convergence, weights within 1e-6.  The fused fit is bitwise reproducible run to run."""
+    X, y = _data(300_000, seed=27, rate=0.03)
+    st = S.scaler_fit(X.to(dev))
+    rows = S.scale_cast(X.to(dev), st, labels=y.to(dev), out_dtype="fp8" if kind == "fp8" else "bf16")
+    kw = dict(tol=1e-6, max_iter=30, progressive=[(8, 2), (2, 1)], hess_refresh=2)
+    if kind == "virtual":  # SMOTE samples of the positives, generated inside every pass
+        pos = rows[rows[:, 31].float() > 0].contiguous()
+        g = torch.Generator().manual_seed(5)
+        nbr = torch.randint(0, pos.shape[0], (pos.shape[0], 5), generator=g, dtype=torch.int32).to(dev)
+        kw["virtual"] = L.VirtualSmote(pos, nbr, 100_000, seed=3, counter_base=1)
+    fits = {}
+    for fuse in ("0", "1", "1"):  # FDX_NEWTON_FUSE: 0 unfused, 1 fused
+        monkeypatch.setenv("FDX_NEWTON_FUSE", fuse)
+        fits.setdefault(fuse, []).append(L.newton_fit(rows, workspace=L.LRWorkspace(dev), **kw).as_fit_info())
+    a, b, b2 = fits["0"][0], fits["1"][0], fits["1"][1]
+    assert a.converged and b.converged and a.n_iter == b.n_iter
+    np.testing.assert_allclose(b.w, a.w, atol=1e-6)
+    assert np.array_equal(b.w, b2.w)
+
+
 @pytest.mark.parametrize("pred", [1, 2, 6])
 def test_newton_deferred_check_same_fit(dev, pred):
     """newton_fit(full_iters=k): k full-data iterations enqueued with no host wait, convergence

@@ -15,12 +15,12 @@
 #   passlab      tools/pass_lab.py: solver pass / reduce / update launches and whole fits at the bench shape
 #   latency      tools/serve_latency.py
 #   plots        the reference script chain (generate -> eda -> preprocess -> train -> evaluate -> explain) with its plots
-#   prof         rocprofv3 --kernel-trace --stats of a short bench
+#   prof         rocprofv3 --kernel-trace --stats of a short Newton bench + its one-step timeline
 #   proffp8      the same with fp8 training rows
 #   profsgd      kernel trace + one-step timeline of the SGD fit
 #   marker       rocprofv3 --marker-trace --kernel-trace with the pipeline's roctx phase markers
 #   benchfp8     bench.py --storage fp8
-#   quick        bench.py --no-extras, bf16 then fp8 (20 steps)
+#   quick        bench.py --solver newton --no-extras, bf16 then fp8 (20 steps); quicknf: unfused Newton iterations
 #   quicksgd     the same with the SGD solver
 #   quicksgdnc   quicksgd bf16 with the cooperative persistent launch (FDX_SGD_COOP=1)
 #   pmc          two PMC passes over a short bench
@@ -78,8 +78,11 @@ for st in "$@"; do
       unset FDX_BENCH_ONE_GPU FDX_BENCH_BACKEND
       cd "$R"
       python tools/stall_probe.py --analyze "$OUT/stall" --json "$OUT/stall_attribution.json" > "$OUT/stall_analyze.log" 2>&1 || true ;;
-    quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras &&
-           step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --storage fp8 ;;
+    quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver newton &&
+           step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver newton --storage fp8 ;;
+    quicknf)  # the Newton iteration unfused (pass + logreg_reduce + newton_update launches)
+      step quicknf_bf16 300 env FDX_NEWTON_FUSE=0 python bench.py --steps 20 --warmup 3 --no-extras --solver newton &&
+      step quicknf_fp8 300 env FDX_NEWTON_FUSE=0 python bench.py --steps 20 --warmup 3 --no-extras --solver newton --storage fp8 ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
     knnprof)  # kernel trace of the k-NN lab (engines/splits from FDX_KNN_ARGS)
       cd /tmp && export TMPDIR=/tmp
@@ -101,8 +104,9 @@ for st in "$@"; do
     latency) step latency 600 python tools/serve_latency.py --json "$OUT/latency.json" ;;
     prof)
       cd /tmp && export TMPDIR=/tmp
-      step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$R/bench.py" --steps 5 --warmup 1 --no-extras
-      cd "$R" ;;
+      step prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$R/bench.py" --solver newton --steps 5 --warmup 1 --no-extras
+      cd "$R"
+      python tools/timeline.py "$OUT/prof/run_kernel_trace.csv" > "$OUT/timeline_newton_step.txt" 2>&1 || true ;;
     profsgd)  # kernel trace of the SGD fit (config 3's solver)
       cd /tmp && export TMPDIR=/tmp
       step profsgd 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profsgd" -o run -- python3 "$R/bench.py" --solver sgd --steps 5 --warmup 1 --no-extras
