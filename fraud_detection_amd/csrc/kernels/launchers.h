@@ -150,6 +150,10 @@ struct RowHole {
 // (fixed block order; the Hessian's upper triangle only), the last of those reduces the groups
 // (fixed order) into `red` -- logreg_reduce's output with H mirrored exactly symmetric -- and runs
 // the Newton update on its first wave.  Replaces the logreg_reduce + newton_update launches.
+// Opt-in (FDX_NEWTON_FUSE=1): measured SLOWER than the two launches it replaces -- a warm-up
+// iteration 64 us against 21 + 6 + 12 (profiles/r6_newton_fuse): inside one launch the cross-XCD
+// hand-off needs agent-coherent loads and ticket round trips (~3 us each, ~9 on the chain), where a
+// kernel boundary publishes the partials to the next launch's ordinary cached loads for free.
 constexpr int kNewtonGroup = 16;
 constexpr int kNewtonMaxGroups = 128;
 constexpr int kNewtonCols = 35 + 528;  // grad, loss, weight, H weight + the upper triangle of H

@@ -1327,8 +1327,8 @@ __device__ __forceinline__ void newton_col(int i, int kLo, int& j, int& k) {
     k = i;
     return;
   }
-  int e = i - kLo, r = 0;
-  while (e >= 32 - r) {  // <= 32 steps, once per column
+  int e = i - kLo, r = 0;  // i < kLo + 528
+  while (r < 31 && e >= 32 - r) {  // <= 31 steps, once per column
     e -= 32 - r;
     ++r;
   }
@@ -1348,9 +1348,6 @@ __device__ __forceinline__ void newton_fused_tail(const float* __restrict__ part
   constexpr int kLo = HESS ? 35 : 34;
   constexpr int kCnt = HESS ? kLo + 528 : kLo;
   constexpr int kPer = (kCnt + kThreads - 1) / kThreads;  // compact columns per thread (<= 3)
-  int cj[kPer], ck[kPer];
-#pragma unroll
-  for (int r = 0; r < kPer; ++r) newton_col(t + r * kThreads, kLo, cj[r], ck[r]);
   auto slot = [](int j, int k) { return j < 0 ? k : 64 + j * kCols + k; };
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's partial stores have landed
   __syncthreads();
@@ -1360,6 +1357,9 @@ __device__ __forceinline__ void newton_fused_tail(const float* __restrict__ part
   }
   __syncthreads();
   if (!s_last) return;  // uniform per block
+  int cj[kPer], ck[kPer];  // this thread's compact columns (out-of-range ones: unused)
+#pragma unroll
+  for (int r = 0; r < kPer; ++r) newton_col(min(t + r * kThreads, kCnt - 1), kLo, cj[r], ck[r]);
   if (t == 0) st_agent(tickets + grp, 0u);
   {  // the group's partials: every load of this thread in flight at once, summed in block order
     float v[kPer][kNewtonGroup];

@@ -20,7 +20,7 @@
 #   profsgd      kernel trace + one-step timeline of the SGD fit
 #   marker       rocprofv3 --marker-trace --kernel-trace with the pipeline's roctx phase markers
 #   benchfp8     bench.py --storage fp8
-#   quick        bench.py --solver newton --no-extras, bf16 then fp8 (20 steps); quicknf: unfused Newton iterations
+#   quick        bench.py --solver newton --no-extras, bf16 then fp8 (20 steps); quickfuse: fused Newton iterations (FDX_NEWTON_FUSE=1); proffuse: their trace
 #   quicksgd     the same with the SGD solver
 #   quicksgdnc   quicksgd bf16 with the cooperative persistent launch (FDX_SGD_COOP=1)
 #   pmc          two PMC passes over a short bench
@@ -80,9 +80,15 @@ for st in "$@"; do
       python tools/stall_probe.py --analyze "$OUT/stall" --json "$OUT/stall_attribution.json" > "$OUT/stall_analyze.log" 2>&1 || true ;;
     quick) step quick_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver newton &&
            step quick_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver newton --storage fp8 ;;
-    quicknf)  # the Newton iteration unfused (pass + logreg_reduce + newton_update launches)
-      step quicknf_bf16 300 env FDX_NEWTON_FUSE=0 python bench.py --steps 20 --warmup 3 --no-extras --solver newton &&
-      step quicknf_fp8 300 env FDX_NEWTON_FUSE=0 python bench.py --steps 20 --warmup 3 --no-extras --solver newton --storage fp8 ;;
+    quickfuse)  # the Newton iteration fused into the pass launch (FDX_NEWTON_FUSE=1)
+      step quickfuse_bf16 300 env FDX_NEWTON_FUSE=1 python bench.py --steps 20 --warmup 3 --no-extras --solver newton &&
+      step quickfuse_fp8 300 env FDX_NEWTON_FUSE=1 python bench.py --steps 20 --warmup 3 --no-extras --solver newton --storage fp8 ;;
+    proffuse)  # kernel trace + timeline of the fused Newton iteration
+      cd /tmp && export TMPDIR=/tmp FDX_NEWTON_FUSE=1
+      step proffuse 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/proffuse" -o run -- python3 "$R/bench.py" --solver newton --steps 5 --warmup 1 --no-extras
+      unset FDX_NEWTON_FUSE
+      cd "$R"
+      python tools/timeline.py "$OUT/proffuse/run_kernel_trace.csv" > "$OUT/timeline_newton_fused_step.txt" 2>&1 || true ;;
     schedlab) step schedlab 400 python tools/sched_lab.py --json "$OUT/sched_lab.json" ;;
     knnprof)  # kernel trace of the k-NN lab (engines/splits from FDX_KNN_ARGS)
       cd /tmp && export TMPDIR=/tmp
