@@ -148,17 +148,20 @@ __device__ __forceinline__ void finish(int e, int p, int P, int d, float* ph, co
                                        float* __restrict__ ws, unsigned* __restrict__ cnt, int* flag) {
   __syncthreads();
   if (P > 1) {
-    if (threadIdx.x < d - 1) {
-      ws[((int64_t)e * kMaxParts + p) * 32 + threadIdx.x] = ph[threadIdx.x];
-      __threadfence();  // each writer publishes its partial device-wide before the arrival counts
-    }
+    // Partials move through agent-coherent stores / loads, ordered by vmcnt(0) before the arrival:
+    // no __threadfence, whose L2 write-back (buffer_wbl2) per workgroup made every P > 1 launch
+    // 2-4x slower than P = 1 (profiles/r6_ks).
+    if (threadIdx.x < d - 1)
+      __hip_atomic_store(ws + ((int64_t)e * kMaxParts + p) * 32 + threadIdx.x, ph[threadIdx.x], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      const unsigned old = atomicAdd(cnt + e, 1u);
+      const unsigned old = __hip_atomic_fetch_add(cnt + e, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool last = old == (unsigned)(P - 1);
-      if (last) cnt[e] = 0u;  // self-cleaning for the next launch (no other part touches it now)
+      // self-cleaning for the next launch (no other part touches it now)
+      if (last) __hip_atomic_store(cnt + e, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *flag = last ? 1 : 0;
-      __threadfence();
     }
     __syncthreads();
     if (*flag == 0) return;

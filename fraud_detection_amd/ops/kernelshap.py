@@ -22,10 +22,11 @@ MAX_PARTS = 8
 
 def choose_parts(n_expl: int, n_tiles: int, target_wgs: int) -> int:
     """Coalition parts per explanation: split only while E x P is below ``target_wgs`` (enough
-    workgroups to keep every SIMD issuing).  Measured on MI355X (profiles/r2_b): a split costs
-    each extra part its own U build / f0 and a device-scope release fence at the hand-off (the
-    L2s of the 8 XCDs are not coherent, so the fence writes back L2), so above the target P = 1
-    wins -- 1000 explanations run 78 us at P = 1 vs 114 us at P = 2."""
+    workgroups to keep every SIMD issuing).  A split costs each extra part its own U build / f0
+    and an agent-coherent hand-off of its partial projection.  Round 6 replaced the hand-off's
+    release fence (an L2 write-back per workgroup: P = 2 ran 2-4x slower than P = 1) with
+    agent-scope stores/loads (profiles/r6_ks): P = 4 now wins for small batches (64 explanations
+    13.6 vs 23.0 us, identity link) and P = 1 from ~512 explanations (33.6 vs 33.7 / 38.0 us)."""
     if n_expl <= 0:
         return 1
     return int(max(1, min(MAX_PARTS, max(1, n_tiles // 4), -(-target_wgs // n_expl))))
@@ -180,9 +181,8 @@ def kernelshap(X: torch.Tensor, expl, sync: bool = True, stamps: torch.Tensor | 
             raise ValueError("phase stamps exist only in the unpaired kernel")
         parts = 1
     elif parts is None:
-        # measured (profiles/r2_e): the split's hand-off costs more than the idle CUs it fills
-        # until the batch is tiny (64 explanations: 25.8 us at P = 1 vs 31.9 at P = 8)
-        parts = choose_parts(E, n_tiles, 16)
+        # E x P ~ 256 workgroups (profiles/r6_ks: 64 explanations run at P = 4, >= 512 at P = 1)
+        parts = choose_parts(E, n_tiles, 256)
     parts = max(1, min(int(parts), MAX_PARTS, n_tiles))
     phi, fx, f0 = _outputs(E, expl.d, dev, out)
     ws, cnt = t["ws"].get(E, dev) if parts > 1 else (None, None)
