@@ -153,7 +153,13 @@ class DevicePipeline:
         self._virtual = None    # VirtualSmote of the latest fit (None: its SMOTE rows are stored)
         # its bucket buffers, one set per training buffer (a fit's set is reused once it is settled)
         self._bws = [lr_ops.BucketWorkspace(), lr_ops.BucketWorkspace()]
+        self._side = None  # side stream of the SMOTE bucket sort (overlaps the k-NN)
         self._defer_now = False
+
+    def _side_stream(self, dev) -> torch.cuda.Stream:
+        if self._side is None or self._side.device != dev:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
 
     def _world(self):
         c = self.comm
@@ -404,6 +410,23 @@ class DevicePipeline:
             k = min(cfg.k_neighbors, xall.shape[0] - 1)
             if k < 1:
                 raise ValueError("SMOTE needs at least 2 minority samples")
+            # Virtual SMOTE's bucket sort needs only the draw (picks = minority rows x k, samples,
+            # seed), not the neighbour table: it runs on a side stream while the k-NN -- VALU-bound
+            # where the sort is memory-bound -- runs on the compute stream (FDX_SMOTE_OVERLAP=0: in line).
+            mq_all = int(xall.shape[0])  # the neighbour table's rows (all ranks' under global scope)
+            use_virt = (n_new > 0 and virt_ok and mq_all * k <= lr_ops.virtual_max_picks()
+                        and n_new <= lr_ops.virtual_max_samples())
+            pre_w = None
+            if use_virt and os.environ.get("FDX_SMOTE_OVERLAP", "1") != "0":
+                main = torch.cuda.current_stream(dev)
+                side = self._side_stream(dev)
+                ev = torch.cuda.Event()
+                ev.record(main)  # every earlier use of the bucket buffers is ordered before the sort
+                side.wait_event(ev)
+                pre_w = lr_ops.bucket_lambdas(mq_all, k, n_new, s_off, cfg.seed, 0 if glob else rank, dev,
+                                              self._bws[self._cur], side.cuda_stream)
+                bucket_done = torch.cuda.Event()
+                bucket_done.record(side)
             # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the
             # neighbours found in standardized space are interpolated in shifted coordinates.
             # Parents live in the training rows' space (bf16, pivot-shifted when the scaler is
@@ -422,12 +445,14 @@ class DevicePipeline:
             if n_new > 0:
                 if parents is None:
                     parents = knn_ops.smote_parents(xall, stats.aff if fused else None)
-                if (virt_ok and nbr.numel() <= lr_ops.virtual_max_picks()
-                        and n_new <= lr_ops.virtual_max_samples()):  # folded into every Newton pass
-                    # the once-per-fit bucket sort of the samples' lambdas, timed as the SMOTE phase
+                if use_virt:  # folded into every logistic pass
                     virt = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, q_offset=q_off, sample_offset=s_off,
-                                               seed=cfg.seed, counter_base=0 if glob else rank
-                                               ).prepare(self._bws[self._cur])
+                                               seed=cfg.seed, counter_base=0 if glob else rank)
+                    if pre_w is not None:  # the side stream's buckets: the fit's passes wait for them
+                        torch.cuda.current_stream(dev).wait_event(bucket_done)
+                        virt.adopt(pre_w)
+                    else:  # the once-per-fit bucket sort of the samples' lambdas, timed as the SMOTE phase
+                        virt.prepare(self._bws[self._cur])
                 else:
                     knn_ops.smote_generate(parents, nbr, q_off, n_new, rows[n:], seed=cfg.seed,
                                            counter_base=0 if glob else rank, fp8_scale=cfg.fp8_scale,

@@ -97,22 +97,18 @@ class VirtualSmote:
         allocates nothing here."""
         if self.off is not None or self.n_new == 0:
             return self
-        m = native()
         mq, k = self.nbr.shape
-        R = mq * k
-        s = stream_of(self.parents)
-        n = int(self.n_new)
-        nt = m.smote_bucket_bins(R, n) * m.smote_bucket_blocks(n)
-        w = (ws or BucketWorkspace()).get(self.parents.device, nt, n, R)
-        args = (mq, k, n, int(self.sample_offset), int(self.seed) & (2**64 - 1),
-                int(self.counter_base) & (2**64 - 1))
-        # stage 0 writes every table entry (no fill) and zeroes the bump allocator; stage 1 scans
-        # each block's row in LDS (no global scan: a block's record run starts at a closed-form
-        # offset) and scatters the coarse records; stage 2 assembles each pick's lambda run
-        m.smote_bucket(0, *args, ptr(w.table), 0, 0, 0, 0, 0, ptr(w.bump), s)        # counts [block][bin]
-        m.smote_bucket(1, *args, ptr(w.table), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # prefix + records
-        m.smote_bucket(2, *args, ptr(w.table), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
-                       ptr(w.bump), s)
+        w = bucket_lambdas(mq, k, self.n_new, self.sample_offset, self.seed, self.counter_base, self.parents.device,
+                           ws, stream_of(self.parents))
+        return self.adopt(w)
+
+    def adopt(self, w: "BucketWorkspace") -> "VirtualSmote":
+        """Take the buckets of a bucket_lambdas call made for this draw (same picks, samples, seed)
+        -- e.g. one enqueued on a side stream while the neighbour search ran."""
+        mq, k = self.nbr.shape
+        if getattr(w, "key", None) != (mq * k, int(self.n_new), int(self.sample_offset), int(self.seed),
+                                       int(self.counter_base)):
+            raise ValueError("bucket workspace was filled for another SMOTE draw")
         self.lam, self.off, self.cnt, self._ws = w.lam, w.off, w.cnt, w
         return self
 
@@ -129,6 +125,28 @@ class VirtualSmote:
         return knn_ops.smote_generate(self.parents, self.nbr, self.q_offset, self.n_new, out, seed=self.seed,
                                       counter_base=self.counter_base, label=self.label, fp8_scale=fp8_scale,
                                       sample_offset=self.sample_offset)
+
+
+def bucket_lambdas(mq: int, k: int, n_new: int, sample_offset: int, seed: int, counter_base: int, dev,
+                   ws: "BucketWorkspace | None" = None, stream: int | None = None) -> "BucketWorkspace":
+    """The samples' lambdas bucketed by pick (VirtualSmote.prepare).  Needs only the draw -- pick
+    count mq x k, sample count, seed, counters -- not the neighbour table, so a pipeline enqueues
+    it on a side stream while the k-NN runs (models/pipeline.py) and adopts the result."""
+    m = native()
+    R, n = int(mq) * int(k), int(n_new)
+    s = int(stream) if stream is not None else int(torch.cuda.current_stream(dev).cuda_stream)
+    nt = m.smote_bucket_bins(R, n) * m.smote_bucket_blocks(n)
+    w = (ws or BucketWorkspace()).get(dev, nt, n, R)
+    args = (int(mq), int(k), n, int(sample_offset), int(seed) & (2**64 - 1), int(counter_base) & (2**64 - 1))
+    # stage 0 writes every table entry (no fill) and zeroes the bump allocator; stage 1 scans
+    # each block's row in LDS (no global scan: a block's record run starts at a closed-form
+    # offset) and scatters the coarse records; stage 2 assembles each pick's lambda run
+    m.smote_bucket(0, *args, ptr(w.table), 0, 0, 0, 0, 0, ptr(w.bump), s)        # counts [block][bin]
+    m.smote_bucket(1, *args, ptr(w.table), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # prefix + records
+    m.smote_bucket(2, *args, ptr(w.table), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
+                   ptr(w.bump), s)
+    w.key = (R, n, int(sample_offset), int(seed), int(counter_base))
+    return w
 
 
 class BucketWorkspace:
