@@ -158,7 +158,8 @@ class DevicePipeline:
 
     def _side_stream(self, dev) -> torch.cuda.Stream:
         if self._side is None or self._side.device != dev:
-            self._side = torch.cuda.Stream(dev)
+            # FDX_SMOTE_SIDE_PRIO=-1: a high-priority side stream (lab knob; torch's range is [-1, 0])
+            self._side = torch.cuda.Stream(dev, priority=int(os.environ.get("FDX_SMOTE_SIDE_PRIO", "0")))
         return self._side
 
     def _world(self):
@@ -344,6 +345,10 @@ class DevicePipeline:
             # host is a fit ahead, so the count no longer sits behind a host wait at the fit
             # boundary (profiles/r3_q/count_front_ab.txt: 1.273 vs 1.309 ms per step with the
             # count on a side stream beside the pass, the round-2 winner).
+            # the compute stream's position before this fit: the SMOTE bucket sort's side stream
+            # starts from here, beside the scaler pass (_finish)
+            self._fit_start = torch.cuda.Event()
+            self._fit_start.record()
             pending = scaler_ops.compact_indices_async(y, 1)
             stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
             tm.mark("scaler_fit")
@@ -411,18 +416,23 @@ class DevicePipeline:
             if k < 1:
                 raise ValueError("SMOTE needs at least 2 minority samples")
             # Virtual SMOTE's bucket sort needs only the draw (picks = minority rows x k, samples,
-            # seed), not the neighbour table: it runs on a side stream while the k-NN -- VALU-bound
-            # where the sort is memory-bound -- runs on the compute stream (FDX_SMOTE_OVERLAP=0: in line).
+            # seed), not the neighbour table: it can run on a side stream.  FDX_SMOTE_OVERLAP:
+            # "scaler" (default) starts it from the compute stream's position before this fit, i.e.
+            # beside the fused scaler pass; "knn" beside the k-NN; "0" in line.
             mq_all = int(xall.shape[0])  # the neighbour table's rows (all ranks' under global scope)
             use_virt = (n_new > 0 and virt_ok and mq_all * k <= lr_ops.virtual_max_picks()
                         and n_new <= lr_ops.virtual_max_samples())
             pre_w = None
-            if use_virt and os.environ.get("FDX_SMOTE_OVERLAP", "1") != "0":
+            mode = os.environ.get("FDX_SMOTE_OVERLAP", "scaler")
+            if use_virt and mode != "0":
                 main = torch.cuda.current_stream(dev)
                 side = self._side_stream(dev)
-                ev = torch.cuda.Event()
-                ev.record(main)  # every earlier use of the bucket buffers is ordered before the sort
-                side.wait_event(ev)
+                ev = getattr(self, "_fit_start", None) if mode == "scaler" else None
+                if ev is None:
+                    ev = torch.cuda.Event()
+                    ev.record(main)
+                self._fit_start = None
+                side.wait_event(ev)  # every earlier use of the bucket buffers is ordered before the sort
                 pre_w = lr_ops.bucket_lambdas(mq_all, k, n_new, s_off, cfg.seed, 0 if glob else rank, dev,
                                               self._bws[self._cur], side.cuda_stream)
                 bucket_done = torch.cuda.Event()

@@ -65,6 +65,12 @@ for st in "$@"; do
     benchfp8) step benchfp8 600 python bench.py --storage fp8 ;;
     quicksgd) step quicksgd_bf16 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd &&
            step quicksgd_fp8 300 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd --storage fp8 ;;
+    smoteov)  # the virtual-SMOTE bucket sort beside the scaler pass / beside the k-NN / in line (quick SGD benches)
+      step smoteov_scaler 300 env FDX_SMOTE_OVERLAP=scaler python bench.py --steps 30 --warmup 3 --no-extras &&
+      step smoteov_knn 300 env FDX_SMOTE_OVERLAP=knn python bench.py --steps 30 --warmup 3 --no-extras &&
+      step smoteov_off 300 env FDX_SMOTE_OVERLAP=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step smoteov_scaler2 300 env FDX_SMOTE_OVERLAP=scaler python bench.py --steps 30 --warmup 3 --no-extras &&
+      step smoteov_scaler_hi 300 env FDX_SMOTE_OVERLAP=scaler FDX_SMOTE_SIDE_PRIO=-1 python bench.py --steps 30 --warmup 3 --no-extras ;;
     quicksgdnc) step quicksgd_coop 300 env FDX_SGD_COOP=1 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
     evab)  # per-fit timing events and the side-stream export, on / off (quick SGD bench each)
       step evab_default 300 python bench.py --steps 30 --warmup 3 --no-extras &&
