@@ -336,6 +336,7 @@ class DevicePipeline:
         # for the minority count (+128: a global-scope slice boundary moves by < 128 rows)
         cap = n + (int(np.ceil(n * max(cfg.sampling_ratio, 1.0))) + 128 if cfg.smote else 0)
         rows_cap = self._train_buffer(cap, dev, allow_double=True)
+        self._fit_start = None  # set below on the fused path only (never an earlier fit's event)
         if fused:
             # ---- K1+K2 fused: statistics (C1 all-reduce inside) + shifted bf16 / fp8 rows ----
             # ---- class counts (C2) IN FRONT of the pass on the compute stream: the count/scan read
@@ -427,7 +428,10 @@ class DevicePipeline:
             if use_virt and mode != "0":
                 main = torch.cuda.current_stream(dev)
                 side = self._side_stream(dev)
-                ev = getattr(self, "_fit_start", None) if mode == "scaler" else None
+                # buffers (re)allocated now come from the compute stream's pool, possibly from
+                # blocks its queued kernels still use: then the sort waits for the present position
+                grew = self._bws[self._cur].reserve(dev, mq_all, k, n_new)
+                ev = getattr(self, "_fit_start", None) if (mode == "scaler" and not grew) else None
                 if ev is None:
                     ev = torch.cuda.Event()
                     ev.record(main)

@@ -135,8 +135,12 @@ def bucket_lambdas(mq: int, k: int, n_new: int, sample_offset: int, seed: int, c
     m = native()
     R, n = int(mq) * int(k), int(n_new)
     s = int(stream) if stream is not None else int(torch.cuda.current_stream(dev).cuda_stream)
-    nt = m.smote_bucket_bins(R, n) * m.smote_bucket_blocks(n)
-    w = (ws or BucketWorkspace()).get(dev, nt, n, R)
+    w = ws or BucketWorkspace()
+    if w.reserve(dev, mq, k, n_new):
+        # fresh buffers come from the CURRENT stream's pool: another stream may only write them
+        # after everything this stream has enqueued so far (the caller orders that: pipeline.py)
+        if stream is not None and int(stream) != int(torch.cuda.current_stream(dev).cuda_stream):
+            raise RuntimeError("bucket_lambdas: reserve the workspace before enqueueing on another stream")
     args = (int(mq), int(k), n, int(sample_offset), int(seed) & (2**64 - 1), int(counter_base) & (2**64 - 1))
     # stage 0 writes every table entry (no fill) and zeroes the bump allocator; stage 1 scans
     # each block's row in LDS (no global scan: a block's record run starts at a closed-form
@@ -154,6 +158,17 @@ class BucketWorkspace:
 
     def __init__(self):
         self.cap, self.dev = None, None
+
+    def reserve(self, dev, mq: int, k: int, n_new: int) -> bool:
+        """Size the buffers for a draw of mq x k picks and n_new samples (on the current stream);
+        True when they were (re)allocated -- a side stream must then wait for the current stream's
+        present position, not an earlier one, before writing them."""
+        m = native()
+        R, n = int(mq) * int(k), int(n_new)
+        nt = m.smote_bucket_bins(R, n) * m.smote_bucket_blocks(n)
+        before = self.cap, self.dev
+        self.get(dev, nt, n, R)
+        return (self.cap, self.dev) != before
 
     def get(self, dev, nt: int, n: int, R: int) -> "BucketWorkspace":
         if self.cap is None or self.dev != dev or nt > self.cap[0] or n > self.cap[1] or R > self.cap[2]:
