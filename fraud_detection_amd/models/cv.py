@@ -32,6 +32,7 @@ MI355X layout (no per-fold copy of the training rows):
 """
 from __future__ import annotations
 
+import os
 import time
 from dataclasses import dataclass, field
 
@@ -109,6 +110,8 @@ class DeviceCV:
         # tolerance from there, without the progressive warm-up)
         self.warm_start = bool(warm_start)
         self._ws: list = []
+        self._bws: list = []  # per-fit SMOTE bucket workspaces (side-stream sorts), kept across runs
+        self._side = None
         if self.cfg.solver not in ("newton", "sgd"):
             raise ValueError("DeviceCV fits the logistic solvers (newton | sgd)")
 
@@ -141,6 +144,41 @@ class DeviceCV:
         pos = [int(p.shape[0]) for p in pos_parts]
         bounds = np.concatenate([[0], np.cumsum([int(f.shape[0]) for f in folds])]).astype(np.int64)
         pbounds = np.concatenate([[0], np.cumsum(pos)]).astype(np.int64)
+
+        def draw(k: int | None):
+            """(minority rows, k, SMOTE samples) of fold k's fit (None: the final fit)."""
+            hl = 0 if k is None else int(bounds[k + 1] - bounds[k])
+            nm = int(pbounds[-1]) - (0 if k is None else int(pbounds[k + 1] - pbounds[k]))
+            nn = max(0, int(round((n - hl - nm) * cfg.sampling_ratio)) - nm) if nm > 0 else 0
+            return nm, min(cfg.k_neighbors, nm - 1), nn
+
+        # Every fit's bucket sort needs only its draw, not its neighbours: all of them run on a side
+        # stream from here, beside the scaler pass and the first folds (FDX_SMOTE_OVERLAP=0: each
+        # in line before its fit).  The workspaces are sized on this stream first, then the side
+        # stream starts from its present position (a fresh buffer may reuse a block a queued
+        # kernel of this stream still reads).
+        pre = {}
+        if os.environ.get("FDX_SMOTE_OVERLAP", "scaler") != "0":
+            specs = {}
+            for k in list(range(K)) + [None]:
+                nm, kk, nn = draw(k)
+                slot = K if k is None else k
+                if nn > 0 and kk >= 1 and nm * kk <= lr_ops.virtual_max_picks() and nn <= lr_ops.virtual_max_samples():
+                    while len(self._bws) <= slot:
+                        self._bws.append(lr_ops.BucketWorkspace())
+                    self._bws[slot].reserve(dev, nm, kk, nn)
+                    specs[k] = (slot, nm, kk, nn)
+            if specs:
+                if self._side is None or self._side.device != dev:
+                    self._side = torch.cuda.Stream(dev)
+                start = torch.cuda.Event()
+                start.record()
+                self._side.wait_event(start)
+                for k, (slot, nm, kk, nn) in specs.items():
+                    w = lr_ops.bucket_lambdas(nm, kk, nn, 0, cfg.seed, 0, dev, self._bws[slot], self._side.cuda_stream)
+                    done = torch.cuda.Event()
+                    done.record(self._side)
+                    pre[k] = (w, done)
         # ---- ONE fused scaler pass: fold-sorted training table + the split's statistics -------
         rows = torch.empty((n, NCOLS), device=dev, dtype=TORCH_STORAGE[cfg.storage])
         dest = torch.empty(n, device=dev, dtype=torch.int64)  # row i of X -> table row dest[i]
@@ -179,7 +217,12 @@ class DeviceCV:
             kk = min(cfg.k_neighbors, n_min - 1)
             parents = torch.empty((n_min, NCOLS), dtype=torch.bfloat16, device=dev)
             nbr = knn_ops.knn_topk(xmin, xmin, k=kk, self_offset=0, parents=parents, parents_affine=stats.aff)
-            v = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, seed=cfg.seed).prepare()
+            v = lr_ops.VirtualSmote(parents, nbr.contiguous(), n_new, seed=cfg.seed)
+            if k in pre:  # sorted on the side stream: this fit's passes wait for it
+                torch.cuda.current_stream(dev).wait_event(pre[k][1])
+                v.adopt(pre[k][0])
+            else:
+                v.prepare()
             # one workspace per fit, kept across runs (every fit of a run is verified before it
             # returns; the pinned flag words are costly to allocate)
             slot = K if k is None else k
