@@ -265,7 +265,9 @@ constexpr int kHistBatchRot = 4;  // rows in flight per thread
 constexpr int kHistWordsLane = kGBBins * 32;  // 8192 u64 = 64 KiB (two 1024-thread blocks per CU fit)
 constexpr int kHistBatchLane = 4;             // row groups in flight per lane
 enum HistVariant : int { kHistLockstep = 0, kHistRot = 1, kHistSplit = 2, kHistLane = 3 };
-template <int VAR>
+// L0 (LANE only): level 0, whose rows are the fit's rows in order (hole skipped): no ridx reads and
+// no per-row level test.
+template <int VAR, bool L0 = false>
 __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hist_kernel(  // 8 waves/SIMD = 2 blocks/CU: <= 64 VGPRs
                                                                            // (ROT: 1 block/CU, <= 128 VGPRs)
     const uint8_t* __restrict__ bins, const uint32_t* __restrict__ gh, const int* __restrict__ ridx,
@@ -324,31 +326,38 @@ __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hi
         const int lane = lane_id();
         const int j = lane & 7, r4 = (lane >> 3) & 3;
         constexpr int kRowsPerIter = kHistThreads / 8;  // 128 rows per block per batch slot
-        unsigned long long* const hs = sh + j;          // slot 8 kk + j of bin b: hs[b * 32 + 8 kk]
+        // Step k adds byte kk = k ^ r4 of the row's dword j.  One v_perm per row puts byte kk at
+        // position k, so every step extracts a STATIC byte (the k = 1 step is a single and-or), and
+        // its slot offset 8 kk is a per-lane base pointer.  Rows past the range add 0 (no branch).
+        const uint32_t sel = (uint32_t)(0 ^ r4) | ((uint32_t)(1 ^ r4) << 8) | ((uint32_t)(2 ^ r4) << 16) |
+                             ((uint32_t)(3 ^ r4) << 24);
+        unsigned long long* hk[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) hk[k] = sh + j + 8 * (k ^ r4);  // slot 8 kk + j of bin b: hk[k][b * 32]
         for (int64_t v0 = c0 + (threadIdx.x >> 3); v0 < c1; v0 += (int64_t)kRowsPerIter * kBatch) {
-          int64_t rows[kBatch];
+          int rows[kBatch];
+          bool ok[kBatch];
 #pragma unroll
           for (int u = 0; u < kBatch; ++u) {
             const int64_t v = v0 + (int64_t)u * kRowsPerIter;
-            rows[u] = v < c1 ? (level == 0 ? hole_row(pbase + v, hole_at, hole_len) : (int64_t)ridx[pbase + v]) : -1;
+            ok[u] = v < c1;
+            const int64_t p = ok[u] ? pbase + v : pbase + c0;  // in range either way
+            rows[u] = L0 ? (int)hole_row(p, hole_at, hole_len) : ridx[p];
           }
           uint32_t bw[kBatch], gw[kBatch];
 #pragma unroll
           for (int u = 0; u < kBatch; ++u) {
-            const int64_t row = rows[u] < 0 ? 0 : rows[u];
-            bw[u] = reinterpret_cast<const uint32_t*>(bins + row * kGBRowBytes)[j];
-            gw[u] = gh[row];
+            bw[u] = reinterpret_cast<const uint32_t*>(bins + (int64_t)rows[u] * kGBRowBytes)[j];
+            gw[u] = gh[rows[u]];
           }
 #pragma unroll
           for (int u = 0; u < kBatch; ++u) {
-            if (rows[u] < 0) continue;
+            const uint32_t g = ok[u] ? gw[u] : 0u;
             const unsigned long long pk =
-                ((unsigned long long)(gw[u] >> 16) << 32) + (unsigned long long)(long long)(int16_t)(gw[u] & 0xffffu);
+                ((unsigned long long)(g >> 16) << 32) + (unsigned long long)(long long)(int16_t)(g & 0xffffu);
+            const uint32_t b = __builtin_amdgcn_perm(bw[u], bw[u], sel);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const int kk = k ^ r4;
-              if (4 * j + kk < d) atomicAdd(hs + ((bw[u] >> (8 * kk)) & 0xffu) * 32 + 8 * kk, pk);
-            }
+            for (int k = 0; k < 4; ++k) atomicAdd(hk[k] + ((b >> (8 * k)) & 0xffu) * 32, pk);
           }
         }
       } else
@@ -1084,6 +1093,9 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   if (rot)  // one block per CU (its rotation registers): half the blocks of the lockstep form
     gbdt_hist_kernel<kHistRot><<<nb / 2, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
                                                                     flush_rows, hole_at, hole_len);
+  else if (var == kHistLane && level == 0)
+    gbdt_hist_kernel<kHistLane, true><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
+                                                                       flush_rows, hole_at, hole_len);
   else if (var == kHistLane)
     gbdt_hist_kernel<kHistLane><<<nb, kHistThreads, 0, stream>>>(bins, gh, ridx, seg, gcnt, level, d, slots,
                                                                  flush_rows, hole_at, hole_len);
