@@ -905,6 +905,15 @@ PYBIND11_MODULE(_fdx_native, m) {
   }, py::arg("bins"), py::arg("gh"), py::arg("ridx"), py::arg("seg"), py::arg("gcnt"), py::arg("level"),
      py::arg("d"), py::arg("hist"), py::arg("slots"), py::arg("s"), py::arg("flush_rows") = 0,
      py::arg("hole_at") = 0, py::arg("hole_len") = 0);
+  m.def("gbdt_hist_l0_fused", [](u bins, u gh, u seg, u gcnt, int d, u hist, u slots, u s, int64_t flush_rows,
+                                 int64_t hole_at, int64_t hole_len, u feat, u bin, u leaf, int depth, u margin,
+                                 u label, float spw, float gscale, float hscale) {
+    fdx::launch_gbdt_hist_l0_fused(P<const uint8_t>(bins), P<uint32_t>(gh), P<const int64_t>(seg),
+                                   P<const int64_t>(gcnt), d, P<unsigned long long>(hist), P<long long>(slots), S(s),
+                                   flush_rows, hole_at, hole_len, P<const int>(feat), P<const int>(bin),
+                                   P<const float>(leaf), depth, P<float>(margin), P<const uint8_t>(label), spw, gscale,
+                                   hscale);
+  });
   m.def("gbdt_split", [](u hist, u gcnt, int level, int d, u nbins, u cuts, double ginv, double hinv, double lam,
                          double mcw, double gamma, u feat, u bin, u thr, u gain, u ng, u nh, u s) {
     fdx::launch_gbdt_split(P<unsigned long long>(hist), P<const int64_t>(gcnt), level, d, P<const int>(nbins),

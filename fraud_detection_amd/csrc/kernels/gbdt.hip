@@ -468,6 +468,135 @@ __global__ __launch_bounds__(kHistThreads, VAR == kHistRot ? 4 : 8) void gbdt_hi
   }
 }
 
+// Level 0 of a boosting round with the previous round's margin walk and gradients fused in (every
+// round of a fit after its first).  Per step of 1024 root positions: phase A, one thread per row,
+// walks the previous tree on the row's 32 bin bytes (two 16-byte loads; the walk selects bytes in
+// registers), updates the row's margin and writes its quantised (g, h) to gh (the deeper levels)
+// and to LDS; phase B adds the same rows into the LANE histogram (8 lanes per row, the bins
+// re-read from L2).  The separate margin kernel's pass over the table (140 us per tree at the bench
+// shape) disappears; the decisions, margins and (g, h) are bitwise those of gbdt_margin_kernel<true>.
+// Hole rows (a CV fold's validation block) get phase A only, after the histogram.
+constexpr int kFuseStep = kHistThreads;
+// byte f of a 32-byte bin row held as two 16-byte words (a 3-level select: no array, no stack)
+__device__ __forceinline__ int row_byte(const uint4& a, const uint4& b, int f) {
+  const int q = f >> 2;
+  const uint32_t lo = (q & 2) ? ((q & 1) ? a.w : a.z) : ((q & 1) ? a.y : a.x);
+  const uint32_t hi = (q & 2) ? ((q & 1) ? b.w : b.z) : ((q & 1) ? b.y : b.x);
+  return (int)((((q & 4) ? hi : lo) >> (8 * (f & 3))) & 0xffu);
+}
+// Phase A of one row: the previous tree's leaf by a walk on the row's bins, the margin update, the
+// row's packed quantised (g, h) -- gbdt_margin_kernel<true>'s arithmetic on the same bytes.
+__device__ __forceinline__ uint32_t fused_margin_row(const uint8_t* __restrict__ bins, int64_t row, int depth,
+                                                     const int* sf, const int* sbn, const float* sl, int ni,
+                                                     float* __restrict__ margin, const uint8_t* __restrict__ label,
+                                                     float spw, float gscale, float hscale) {
+  const uint4* br = reinterpret_cast<const uint4*>(bins + row * kGBRowBytes);
+  const uint4 a = br[0], b = br[1];
+  int node = 0;
+  for (int l = 0; l < depth; ++l) {
+    const int f = sf[node];
+    node = 2 * node + 1 + (int)(f >= 0 && row_byte(a, b, f) > sbn[node]);
+  }
+  const float m = margin[row] + sl[node - ni];
+  margin[row] = m;
+  return pack_gh(quantised_grad(m, label[row] != 0, spw, gscale, hscale));
+}
+__global__ __launch_bounds__(kHistThreads, 8) void gbdt_hist_l0_fused_kernel(
+    const uint8_t* __restrict__ bins, uint32_t* __restrict__ gh, const int64_t* __restrict__ seg,
+    const int64_t* __restrict__ gcnt, int d, long long* __restrict__ slots, int64_t flush_rows, int64_t hole_at,
+    int64_t hole_len, const int* __restrict__ feat, const int* __restrict__ bin, const float* __restrict__ leaf,
+    int depth, float* __restrict__ margin, const uint8_t* __restrict__ label, float spw, float gscale,
+    float hscale) {
+  __shared__ unsigned long long sh[kHistWordsLane];
+  __shared__ LevelNodes lv;
+  __shared__ int sf[kGBMaxNodes], sbn[kGBMaxNodes];
+  __shared__ float sl[kGBMaxNodes + 1];
+  __shared__ uint32_t ghs[kFuseStep];
+  __shared__ int rws[kFuseStep];
+  const int ni = heap_first(depth);
+  for (int i = threadIdx.x; i < ni; i += blockDim.x) {
+    sf[i] = feat[i];
+    sbn[i] = bin[i];
+  }
+  for (int i = threadIdx.x; i <= ni; i += blockDim.x) sl[i] = leaf[i];
+  load_level(lv, seg, gcnt, 0);  // its barrier also covers the tree tables
+  int64_t total;
+  const int64_t chunk = level_chunk(lv, 0, gridDim.x, &total);
+  const int64_t lo = (int64_t)blockIdx.x * chunk, hi = min(lo + chunk, total);
+  const int64_t sb = seg[0];  // the root's first position
+  long long* dst = slots + (int64_t)blockIdx.x * kHistEntries;  // level 0: block b owns slot b
+  const int lane = lane_id();
+  const int j = lane & 7, r4 = (lane >> 3) & 3;
+  const uint32_t sel = (uint32_t)(0 ^ r4) | ((uint32_t)(1 ^ r4) << 8) | ((uint32_t)(2 ^ r4) << 16) |
+                       ((uint32_t)(3 ^ r4) << 24);
+  unsigned long long* const hk0 = sh + j + 8 * (0 ^ r4);
+  unsigned long long* const hk1 = sh + j + 8 * (1 ^ r4);
+  unsigned long long* const hk2 = sh + j + 8 * (2 ^ r4);
+  unsigned long long* const hk3 = sh + j + 8 * (3 ^ r4);
+  for (int64_t c0 = lo; c0 < hi; c0 += flush_rows) {
+    const int64_t c1 = min(hi, c0 + flush_rows);
+    for (int i = threadIdx.x; i < kHistWordsLane; i += kHistThreads) sh[i] = 0ull;
+    for (int64_t s0 = c0; s0 < c1; s0 += kFuseStep) {  // block-uniform
+      {  // phase A
+        const int64_t v = s0 + threadIdx.x;
+        uint32_t g = 0u;
+        int row = 0;
+        if (v < c1) {
+          row = (int)hole_row(sb + v, hole_at, hole_len);
+          g = fused_margin_row(bins, row, depth, sf, sbn, sl, ni, margin, label, spw, gscale, hscale);
+          gh[row] = g;
+        }
+        ghs[threadIdx.x] = g;  // rows past the range add 0 in phase B
+        rws[threadIdx.x] = row;
+      }
+      __syncthreads();  // also orders the zeroing above before the first atomic
+      // phase B: 8 passes of 128 rows, kHistBatchLane passes' loads in flight at once
+#pragma unroll
+      for (int p0 = 0; p0 < kHistThreads / kHistBatchLane / 128 * kHistBatchLane; p0 += kHistBatchLane) {
+        uint32_t bw[kHistBatchLane], gw[kHistBatchLane];
+#pragma unroll
+        for (int u = 0; u < kHistBatchLane; ++u) {
+          const int i = (p0 + u) * 128 + (threadIdx.x >> 3);
+          gw[u] = ghs[i];
+          bw[u] = reinterpret_cast<const uint32_t*>(bins + (int64_t)rws[i] * kGBRowBytes)[j];
+        }
+#pragma unroll
+        for (int u = 0; u < kHistBatchLane; ++u) {
+          const uint32_t g = gw[u];
+          const unsigned long long pk =
+              ((unsigned long long)(g >> 16) << 32) + (unsigned long long)(long long)(int16_t)(g & 0xffffu);
+          const uint32_t b = __builtin_amdgcn_perm(bw[u], bw[u], sel);
+          atomicAdd(hk0 + (b & 0xffu) * 32, pk);
+          atomicAdd(hk1 + ((b >> 8) & 0xffu) * 32, pk);
+          atomicAdd(hk2 + ((b >> 16) & 0xffu) * 32, pk);
+          atomicAdd(hk3 + (b >> 24) * 32, pk);
+        }
+      }
+      __syncthreads();  // ghs / rws reused by the next step
+    }
+    const bool first = c0 == lo;
+    for (int i = threadIdx.x; i < d * kGBBins; i += kHistThreads) {
+      const int f = i >> 8, b = i & 255;
+      const unsigned long long x = sh[b * 32 + 8 * (f & 3) + (f >> 2)];
+      const long long sg = (long long)(int32_t)(uint32_t)(x & 0xffffffffull);
+      const long long sgh = (long long)(x - (unsigned long long)sg) >> 32;
+      long long* e = dst + 2 * i;
+      if (first) {
+        e[0] = sg;
+        e[1] = sgh;
+      } else {
+        e[0] += sg;
+        e[1] += sgh;
+      }
+    }
+    __syncthreads();
+  }
+  // the hole rows: margins (and (g, h), unused) only
+  for (int64_t r = hole_at + (int64_t)blockIdx.x * kHistThreads + threadIdx.x; r < hole_at + hole_len;
+       r += (int64_t)gridDim.x * kHistThreads)
+    gh[r] = fused_margin_row(bins, r, depth, sf, sbn, sl, ni, margin, label, spw, gscale, hscale);
+}
+
 // Sum each built node's slots into its histogram: grid (entries / 256, kSlotSplit, sibling pairs).
 __global__ __launch_bounds__(256) void gbdt_hist_reduce_kernel(const long long* __restrict__ slots,
                                                                const int64_t* __restrict__ seg,
@@ -1108,6 +1237,24 @@ void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, 
   check_launch("gbdt_hist");
   const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, level == 0 ? 1u : 1u << (level - 1));
   gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, level, d, rot ? nb / 2 : nb, hist);
+  check_launch("gbdt_hist_reduce");
+}
+
+void launch_gbdt_hist_l0_fused(const uint8_t* bins, uint32_t* gh, const int64_t* seg, const int64_t* gcnt, int d,
+                               unsigned long long* hist, long long* slots, hipStream_t stream, int64_t flush_rows,
+                               int64_t hole_at, int64_t hole_len, const int* feat, const int* bin, const float* leaf,
+                               int depth, float* margin, const uint8_t* label, float spw, float gscale, float hscale) {
+  if (hole_at < 0 || hole_len < 0) throw std::runtime_error("gbdt_hist_l0_fused: bad row hole");
+  if (depth < 1 || depth > 7) throw std::runtime_error("gbdt_hist_l0_fused: depth must be in [1, 7]");
+  if (d < 1 || d > kGBMaxFeat) throw std::runtime_error("gbdt_hist_l0_fused: bad feature count");
+  if (flush_rows <= 0 || flush_rows > kFlushRows) flush_rows = kFlushRows;
+  const int nb = gbdt_hist_blocks();
+  gbdt_hist_l0_fused_kernel<<<nb, kHistThreads, 0, stream>>>(bins, gh, seg, gcnt, d, slots, flush_rows, hole_at,
+                                                             hole_len, feat, bin, leaf, depth, margin, label, spw,
+                                                             gscale, hscale);
+  check_launch("gbdt_hist_l0_fused");
+  const dim3 rg((unsigned)((d * kGBBins * 2 + 255) / 256), kSlotSplit, 1u);
+  gbdt_hist_reduce_kernel<<<rg, 256, 0, stream>>>(slots, seg, gcnt, 0, d, nb, hist);
   check_launch("gbdt_hist_reduce");
 }
 

@@ -401,6 +401,12 @@ void set_gbdt_hist_variant(int v);
 void launch_gbdt_hist(const uint8_t* bins, const uint32_t* gh, const int* ridx, const int64_t* seg,
                       const int64_t* gcnt, int level, int d, unsigned long long* hist, long long* slots,
                       hipStream_t stream, int64_t flush_rows = 0, int64_t hole_at = 0, int64_t hole_len = 0);
+// Level 0 of a round after a fit's first: the previous tree's margin walk + (g, h) fused in front of
+// the histogram (gbdt.hip gbdt_hist_l0_fused_kernel); replaces gbdt_margin<GRAD> + gbdt_hist(level 0).
+void launch_gbdt_hist_l0_fused(const uint8_t* bins, uint32_t* gh, const int64_t* seg, const int64_t* gcnt, int d,
+                               unsigned long long* hist, long long* slots, hipStream_t stream, int64_t flush_rows,
+                               int64_t hole_at, int64_t hole_len, const int* feat, const int* bin, const float* leaf,
+                               int depth, float* margin, const uint8_t* label, float spw, float gscale, float hscale);
 void launch_gbdt_split(unsigned long long* hist, const int64_t* gcnt, int level, int d, const int* nbins,
                        const float* cuts, double ginv, double hinv, double lambda,
                        double min_child_weight, double gamma, int* feat, int* bin, float* thr,

@@ -324,10 +324,13 @@ def fit_binned(bins: torch.Tensor, y: torch.Tensor, cuts, params: GBDTParams | N
     lam, mcw, gam = float(p.reg_lambda), float(p.min_child_weight), float(p.gamma)
     ginv, hinv = 1.0 / gscale, 1.0 / hscale
 
-    def round_body(o_feat, o_bin, o_thr, o_gain, o_leaf, grad_first=False, grad_next=True):
+    def round_body(o_feat, o_bin, o_thr, o_gain, o_leaf, grad_first=False, grad_next=True, prev=None,
+                   defer_margin=False):
         """One boosting round: a fixed launch sequence with static pointers (graph-capturable).
         The gradients of a round come from the previous round's margin update (gbdt_margin with
-        gh), so only the first round of a fit launches gbdt_grad."""
+        gh), so only the first round of a fit launches gbdt_grad.  ``prev`` (feat, bin, leaf of the
+        previous tree, its margin walk deferred): level 0 runs that walk fused in front of its
+        histogram (gbdt_hist_l0_fused).  ``defer_margin``: leave this tree's walk to the next round."""
         st = stream_of(bins)  # the capture stream while a hipGraph is being recorded
         if grad_first:
             m.gbdt_grad(ptr(margin), ptr(y), n, spw, gscale, hscale, ptr(ws.gh), st)
@@ -338,8 +341,13 @@ def fit_binned(bins: torch.Tensor, y: torch.Tensor, cuts, params: GBDTParams | N
         cur = 0
         for level in range(D):
             h0, nn = (1 << level) - 1, 1 << level
-            m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
-                        ptr(ws.hist), ptr(ws.slots), st, HIST_FLUSH_ROWS, ha, hl)
+            if level == 0 and prev is not None:
+                m.gbdt_hist_l0_fused(ptr(bins), ptr(ws.gh), ptr(ws.seg), ptr(ws.gcnt), d, ptr(ws.hist), ptr(ws.slots),
+                                     st, HIST_FLUSH_ROWS, ha, hl, ptr(prev[0]), ptr(prev[1]), ptr(prev[2]), D,
+                                     ptr(margin), ptr(y), spw, gscale, hscale)
+            else:
+                m.gbdt_hist(ptr(bins), ptr(ws.gh), ptr(ws.ridx[cur]), ptr(ws.seg), ptr(ws.gcnt), level, d,
+                            ptr(ws.hist), ptr(ws.slots), st, HIST_FLUSH_ROWS, ha, hl)
             if dist:
                 comm.all_reduce_(ws.hist[h0 * HIST_ENTRIES:(h0 + nn) * HIST_ENTRIES])
             m.gbdt_split(ptr(ws.hist), ptr(ws.gcnt), level, d, ptr(nt), ptr(ct), ginv, hinv, lam, mcw, gam,
@@ -359,7 +367,7 @@ def fit_binned(bins: torch.Tensor, y: torch.Tensor, cuts, params: GBDTParams | N
             if dist:
                 comm.all_reduce_(ws.gcnt[c0:c0 + 2 * nn])
         m.gbdt_leaf(ptr(ws.ng), ptr(ws.nh), D, ginv, hinv, lam, mcw, float(p.learning_rate), ptr(o_leaf), st)
-        if n:
+        if n and not defer_margin:
             m.gbdt_margin(ptr(binsT), ldt, n, ptr(o_feat), ptr(o_bin), ptr(o_leaf), D, ptr(margin), ptr(y), spw,
                           gscale, hscale, ptr(ws.gh) if grad_next else 0, st)
 
@@ -376,6 +384,7 @@ def fit_binned(bins: torch.Tensor, y: torch.Tensor, cuts, params: GBDTParams | N
     if use_graph is None:  # opt-in: measured slower than eager launches (profiles/r1_s22)
         use_graph = os.environ.get("FDX_GBDT_GRAPH", "0") == "1"
     graphable = use_graph and not dist and n > 0 and T - t0 >= 3
+    fuse_margin = os.environ.get("FDX_GBDT_FUSE_MARGIN", "0") == "1" and not graphable
     graph = None
     for t in range(t0, T):
         if graphable and t == t0 + 1:  # round t0 ran eagerly: its kernels had to execute
@@ -390,7 +399,14 @@ def fit_binned(bins: torch.Tensor, y: torch.Tensor, cuts, params: GBDTParams | N
             for dst, src in zip((feat[t], binv[t], thr[t], gain[t], leaf[t]), rec):
                 dst.copy_(src)
         else:
-            round_body(feat[t], binv[t], thr[t], gain[t], leaf[t], grad_first=(t == t0), grad_next=(t + 1 < T))
+            # FDX_GBDT_FUSE_MARGIN=1: a round's margin walk runs fused into the next round's level-0
+            # histogram pass (one pass over the table fewer) -- measured slower: 410 us for the fused
+            # pass against 151 + 140 us (its per-row fp64 phase and the LANE phase alternate behind
+            # block barriers, 64-VGPR budget, profiles/r6_gbdt), so opt-in
+            fuse = fuse_margin and n_fit > 0
+            round_body(feat[t], binv[t], thr[t], gain[t], leaf[t], grad_first=(t == t0), grad_next=(t + 1 < T),
+                       prev=(feat[t - 1], binv[t - 1], leaf[t - 1]) if (fuse and t > t0) else None,
+                       defer_margin=fuse and t + 1 < T)
         after_round(t)
     ens = TreeEnsemble(feat=feat.cpu().numpy(), bin=binv.cpu().numpy(), thr=thr.cpu().numpy(),
                        gain=gain.cpu().numpy(), leaf=leaf.cpu().numpy(), **ens_kw)
