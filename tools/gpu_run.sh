@@ -108,6 +108,9 @@ for st in "$@"; do
       # shellcheck disable=SC2086
       step pmcknn_b 180 rocprofv3 --kernel-include-regex "knn_(collect|rerank|topk_kernel|b3top)" --pmc SQ_INSTS_LDS SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_ANY --output-format csv -d "$OUT/pmcknn_b" -o run -- python3 "$R/tools/knn_lab.py" --reps 3 $FDX_KNN_ARGS
       cd "$R" ;;
+    knndepth)  # bf16x3r collect: 2 vs 4 candidate tiles in flight (FDX_KNN3R_DEPTH), lab at DP1 / DP8 shapes
+      step knndepth_4 300 env FDX_KNN3R_DEPTH=4 python tools/knn_lab.py --engines bf16x3r --splits 2,4,8 --json "$OUT/knndepth_4.json" &&
+      step knndepth_2 300 env FDX_KNN3R_DEPTH=2 python tools/knn_lab.py --engines bf16x3r --splits 2,4,8 --json "$OUT/knndepth_2.json" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" $FDX_KNN_ARGS ;;  # shellcheck disable=SC2086
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
