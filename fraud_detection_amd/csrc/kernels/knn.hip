@@ -203,23 +203,30 @@ __global__ __launch_bounds__(kWave) void knn_topk_kernel(const float* __restrict
     if (t + 1 < t_hi) fetch(t + 1, cv);
 #pragma unroll
     for (int s = 0; s < 16; ++s) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(ac[s], bq[s], acc, 0, 0, 0);
-    float mx = acc[0];
+    // quad maxima first (rows 4q .. 4q+3 = 4 consecutive candidates), then the tile's
+    float m4[4];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    for (int q = 0; q < 4; ++q) m4[q] = fmaxf(fmaxf(acc[4 * q], acc[4 * q + 1]), fmaxf(acc[4 * q + 2], acc[4 * q + 3]));
+    const float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     if (!__any(mx >= thr)) continue;
     const int cbase = c0 + 4 * h;
-    // Append: a wave-uniform branch per accumulator row skips the rows no lane passes (usually all
-    // but one or two once the lists are full); the passing lanes store under their exec mask.  The
-    // per-row select-and-store of every row (dump slot for non-passing lanes) was ~110 of the
-    // ~135 VALU instructions per tile whenever ANY lane passed (r5_n PMC).
+    // Append: a wave-uniform branch per passing quad, then per accumulator row of it, skips the rows
+    // no lane passes (usually all but one or two once the lists are full); the passing lanes store
+    // under their exec mask.  The per-row select-and-store of every row (dump slot for non-passing
+    // lanes) was ~110 of the ~135 VALU instructions per tile whenever ANY lane passed (r5_n PMC).
     int qe = qn * kWave + lane;                     // element of this lane's next free slot
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const bool pass = acc[r] >= thr;
-      if (__any(pass)) {
-        if (pass) {
-          qent[qe] = make_int2(__float_as_int(acc[r]), cbase + (r & 3) + 8 * (r >> 2));
-          qe += kWave;
+    for (int q = 0; q < 4; ++q) {
+      if (!__any(m4[q] >= thr)) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = 4 * q + rr;
+        const bool pass = acc[r] >= thr;
+        if (__any(pass)) {
+          if (pass) {
+            qent[qe] = make_int2(__float_as_int(acc[r]), cbase + rr + 8 * q);
+            qe += kWave;
+          }
         }
       }
     }
@@ -771,19 +778,25 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     const float mg = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
     mgmax = fmaxf(mgmax, mg);
     const float cut = thr - mg;  // upper bound approx + mg >= thr
-    float mx = acc[0];
+    float m4[4];
 #pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[r]);
+    for (int q = 0; q < 4; ++q) m4[q] = fmaxf(fmaxf(acc[4 * q], acc[4 * q + 1]), fmaxf(acc[4 * q + 2], acc[4 * q + 3]));
+    const float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
     if (!__any(mx >= cut)) continue;
     const int cbase = c0 + 4 * h;
     int qe = qc * kWave + lane;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {  // knn_topk_kernel's uniform-skip append
-      const bool pass = acc[r] >= cut;
-      if (__any(pass)) {
-        if (pass) {
-          qent[qe] = make_int2(__float_as_int(acc[r] - mg), cbase + (r & 3) + 8 * (r >> 2));
-          qe += kWave;
+    for (int q = 0; q < 4; ++q) {  // knn_topk_kernel's quad-then-row uniform-skip append
+      if (!__any(m4[q] >= cut)) continue;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int r = 4 * q + rr;
+        const bool pass = acc[r] >= cut;
+        if (__any(pass)) {
+          if (pass) {
+            qent[qe] = make_int2(__float_as_int(acc[r] - mg), cbase + rr + 8 * q);
+            qe += kWave;
+          }
         }
       }
     }

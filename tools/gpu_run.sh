@@ -111,6 +111,13 @@ for st in "$@"; do
     knndepth)  # bf16x3r collect: 2 vs 4 candidate tiles in flight (FDX_KNN3R_DEPTH), lab at DP1 / DP8 shapes
       step knndepth_4 300 env FDX_KNN3R_DEPTH=4 python tools/knn_lab.py --engines bf16x3r --splits 2,4,8 --json "$OUT/knndepth_4.json" &&
       step knndepth_2 300 env FDX_KNN3R_DEPTH=2 python tools/knn_lab.py --engines bf16x3r --splits 2,4,8 --json "$OUT/knndepth_2.json" ;;
+    knnab)  # the pipeline's k-NN engine at DP1: bf16x3r vs the fp32 default (quick SGD benches, twice each)
+      step knnab_3r 300 env FDX_KNN=bf16x3r python bench.py --steps 30 --warmup 3 --no-extras &&
+      step knnab_fp32 300 env FDX_KNN=fp32 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step knnab_3r_b 300 env FDX_KNN=bf16x3r python bench.py --steps 30 --warmup 3 --no-extras &&
+      step knnab_fp32_b 300 env FDX_KNN=fp32 python bench.py --steps 30 --warmup 3 --no-extras ;;
+    knnquad)  # fp32 and bf16x3r engines around their default splits (append-path A/Bs)
+      step knnquad 300 python tools/knn_lab.py --engines fp32,bf16x3r --splits 4,16,19 --json "$OUT/knnquad.json" ;;
     knnlab) step knnlab 400 python tools/knn_lab.py --json "$OUT/knn_lab.json" $FDX_KNN_ARGS ;;  # shellcheck disable=SC2086
     passlab) step passlab 300 python tools/pass_lab.py --json "$OUT/pass_lab.json" ;;
     ubench) step ubench 300 python tools/ubench.py --json "$OUT/ubench.json" ;;
