@@ -762,19 +762,8 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     }
     union_thr();
   }
-  // two tiles in flight (a slice's wave is latency-bound on its loads at ~2 waves per SIMD)
-  uint4 cv[4], cv2[4];
-  float tmn = 0.0f, tmn2 = 0.0f;
-  if (t_lo < t_hi) fetch(t_lo, cv, tmn);
-  if (t_lo + 1 < t_hi) fetch(t_lo + 1, cv2, tmn2);
-  for (int t = t_lo; t < t_hi; ++t) {
-    const int c0 = t * 32;
-    const f32x16_t acc = approx(cv);
-    const float tm = tmn;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) cv[u] = cv2[u];
-    tmn = tmn2;
-    if (t + 2 < t_hi) fetch(t + 2, cv2, tmn2);
+  // The filter of one scored tile (knn_topk_kernel's quad-then-row uniform-skip append).
+  auto filter = [&](int t, const f32x16_t& acc, float tm) {
     const float mg = kMarginScale * fmaf(qn, tm, 0.5f * tm * tm);
     mgmax = fmaxf(mgmax, mg);
     const float cut = thr - mg;  // upper bound approx + mg >= thr
@@ -782,11 +771,11 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
 #pragma unroll
     for (int q = 0; q < 4; ++q) m4[q] = fmaxf(fmaxf(acc[4 * q], acc[4 * q + 1]), fmaxf(acc[4 * q + 2], acc[4 * q + 3]));
     const float mx = fmaxf(fmaxf(m4[0], m4[1]), fmaxf(m4[2], m4[3]));
-    if (!__any(mx >= cut)) continue;
-    const int cbase = c0 + 4 * h;
+    if (!__any(mx >= cut)) return;
+    const int cbase = t * 32 + 4 * h;
     int qe = qc * kWave + lane;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {  // knn_topk_kernel's quad-then-row uniform-skip append
+    for (int q = 0; q < 4; ++q) {
       if (!__any(m4[q] >= cut)) continue;
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
@@ -802,6 +791,41 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     }
     qc = (qe - lane) / kWave;
     if (__any(qc >= kQFlush)) flush();
+  };
+  // Tiles in PAIRS: the two tiles' 6-MFMA chains are interleaved (independent accumulators), so one
+  // chain's result latency is covered by the other's issue -- at ~1.7 waves per SIMD a lone chain's
+  // latency was exposed on every tile.  The next pair's loads are in flight meanwhile.
+  uint4 ca[4], cb[4];
+  float tma = 0.0f, tmb = 0.0f;
+  if (t_lo < t_hi) fetch(t_lo, ca, tma);
+  if (t_lo + 1 < t_hi) fetch(t_lo + 1, cb, tmb);
+  for (int t = t_lo; t < t_hi; t += 2) {
+    const bool two = t + 1 < t_hi;  // wave-uniform
+    f32x16_t acc0 = {}, acc1 = {};
+    {
+      const bf16x8_t ah0 = __builtin_bit_cast(bf16x8_t, ca[0]), ah1 = __builtin_bit_cast(bf16x8_t, ca[1]);
+      const bf16x8_t al0 = __builtin_bit_cast(bf16x8_t, ca[2]), al1 = __builtin_bit_cast(bf16x8_t, ca[3]);
+      const bf16x8_t bh0 = __builtin_bit_cast(bf16x8_t, cb[0]), bh1 = __builtin_bit_cast(bf16x8_t, cb[1]);
+      const bf16x8_t bl0 = __builtin_bit_cast(bf16x8_t, cb[2]), bl1 = __builtin_bit_cast(bf16x8_t, cb[3]);
+      // approx()'s order per tile (bitwise the same sums), the two chains alternating
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al0, qh0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl0, qh0, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al1, qh1, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bl1, qh1, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, ql0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh0, ql0, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, ql1, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh1, ql1, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah0, qh0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh0, qh0, acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah1, qh1, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bh1, qh1, acc1, 0, 0, 0);
+    }
+    const float ta = tma, tb = tmb;
+    if (t + 2 < t_hi) fetch(t + 2, ca, tma);  // the next pair
+    if (t + 3 < t_hi) fetch(t + 3, cb, tmb);
+    filter(t, acc0, ta);
+    if (two) filter(t + 1, acc1, tb);
   }
   flush();
   counts[(int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * kWave + lane] = cnt;

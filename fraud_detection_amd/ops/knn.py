@@ -41,9 +41,11 @@ def _padded(X: torch.Tensor, n_pad: int) -> torch.Tensor:
 # profiles/r5_k, r5_o): at the DP=8 global-scope rank (13.6k queries x 108.8k candidates) 0.78 ms
 # against 1.07.  At the bench's DP=1 self-search the lab had it at 0.194 vs 0.209 ms, but inside
 # the pipeline's step its collect + re-rank took 199 us against the fp32 engine's ~200 us
-# (profiles/r5_x timeline): no gain.  auto = bf16x3r from 64k candidates, fp32 below; FDX_KNN
-# selects an engine.
-KNN_BF16X3_MIN_CANDIDATES = 1 << 16
+# (profiles/r5_x timeline): no gain.  Round 6 (profiles/r6_knn): with a quad-max pre-test in the
+# append path and the pair-interleaved MFMA chains the lab has bf16x3r at 0.184 ms vs fp32's 0.217
+# at DP=1, and in the pipeline's step (quick SGD benches, two runs each) 1.006 / 1.015 ms medians
+# against 1.037 / 1.035.  auto = bf16x3r from 8k candidates, fp32 below; FDX_KNN selects an engine.
+KNN_BF16X3_MIN_CANDIDATES = 1 << 13
 
 
 def knn_engine(mq: int, mc: int, engine: str | None = None) -> str:

@@ -362,7 +362,7 @@ def test_knn_engines_agree_with_ties_and_auto_selection(dev):
     for ns in (1, 3, 40):  # the LDS engine runs the same MFMA chain: bit-identical lists + scores
         c, sc = K.knn_topk(Q, Ct, k=5, self_offset=0, want_dist=True, engine="fp32lds", nsplit=ns)
         assert torch.equal(a, c) and torch.equal(sa, sc)
-    assert K.knn_engine(10, 13_600) == "fp32" and K.knn_engine(10, 170_000) == "bf16x3r"  # ops/knn.py
+    assert K.knn_engine(10, 4_000) == "fp32" and K.knn_engine(10, 13_600) == "bf16x3r"  # ops/knn.py
     # a larger candidate set: 256 queries, all three engines
     Cb = torch.from_numpy(rng.normal(size=(70_000, 32)).astype(np.float32)).to(dev)
     Qb = Cb[:256].contiguous()
