@@ -828,7 +828,14 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
     if (two) filter(t + 1, acc1, tb);
   }
   flush();
-  counts[(int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * kWave + lane] = cnt;
+  // counts holds three planes of gridDim.x * gridDim.y * 64 ints: the list length, then this lane's
+  // final threshold (the union's k-th best lower bound) and largest margin -- the re-rank skips
+  // every entry whose upper bound cannot reach the best of the slices' final thresholds
+  const int64_t ci0 = (int64_t)(blockIdx.y * gridDim.x + blockIdx.x) * kWave + lane;
+  const int64_t plane = (int64_t)gridDim.x * gridDim.y * kWave;
+  counts[ci0] = cnt;
+  counts[plane + ci0] = __float_as_int(thr);
+  counts[2 * plane + ci0] = __float_as_int(mgmax);
 }
 
 // Phase 2: 8 lanes per query (lane l takes every 8th listed candidate), exact re-score, per-lane
@@ -873,19 +880,27 @@ __global__ __launch_bounds__(256) void knn_rerank_kernel(const float* __restrict
   for (int k = 0; k < K; ++k) { bs[k] = kNegBig; bi[k] = 0x7fffffff; }
   if (live) {
     bool over = false;
-    for (int s = 0; s < nsplit; ++s)
+    const int64_t plane = (int64_t)nsplit * qblocks * kWave;
+    float T = kNegBig;  // the best slice threshold: a lower bound of the exact k-th best s_k
+    for (int s = 0; s < nsplit; ++s) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) over |= counts[((int64_t)s * qblocks + blk) * kWave + j + 32 * h] > kListCap;
+      T = fmaxf(T, __int_as_float(counts[plane + ((int64_t)s * qblocks + blk) * kWave + j]));
+    }
     if (!over) {
       for (int s = 0; s < nsplit; ++s) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int64_t cb = ((int64_t)s * qblocks + blk) * kWave + j + 32 * h;
           const int n = counts[cb];
+          // an entry's upper bound is at most lb + 2 m_max; below T <= s_k it cannot be in the top-k
+          // (not even on a tie), so its fp32 row is never gathered
+          const float skip = T - 2.0f * __int_as_float(counts[2 * plane + cb]);
           const int2* li = lists + ((int64_t)s * qblocks + blk) * kListCap * kWave + j + 32 * h;
           for (int e = l; e < n; e += 8) {
-            const int ci = li[(int64_t)e * kWave].y;
-            topk_insert<K>(bs, bi, exact(ci), ci);
+            const int2 v = li[(int64_t)e * kWave];
+            if (__int_as_float(v.x) < skip) continue;
+            topk_insert<K>(bs, bi, exact(v.y), v.y);
           }
         }
       }

@@ -157,14 +157,15 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     elif eng == "bf16x3r":
         nb = ns * (mq_pad // 32) * 64
         lists = torch.empty(nb * m.KNN3R_LIST_CAP * 2, device=Q.device, dtype=torch.int32)  # (lb, index)
-        counts = torch.empty(nb, device=Q.device, dtype=torch.int32)
+        # list lengths, then each lane's final threshold and largest margin (knn_collect_kernel)
+        counts = torch.empty(3 * nb, device=Q.device, dtype=torch.int32)
         m.knn_topk3r(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                      int(k), ptr(idx), ptr(score), ptr(lists), ptr(counts), ns, s)
         if _diag is not None:  # list lengths (diagnostics; synchronises)
-            c = counts.float()
+            c = counts[:nb].float()
             _diag.update(nsplit=ns, list_cap=int(m.KNN3R_LIST_CAP), mean=float(c.mean()), max=int(c.max()),
                          p99=float(torch.quantile(c[: min(c.numel(), 1 << 24)], 0.99)),
-                         over_cap=int((c > m.KNN3R_LIST_CAP).sum()), counts=counts.view(ns, mq_pad // 32, 64))
+                         over_cap=int((c > m.KNN3R_LIST_CAP).sum()), counts=counts[:nb].view(ns, mq_pad // 32, 64))
     elif eng == "bf16x3":
         m.knn_topk3(ptr(Qp), ptr(Qhl), mq_pad, mq, ptr(Cp), ptr(Chl), ptr(tmax), mc_pad, mc, int(self_offset),
                     int(k), ptr(idx), ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
