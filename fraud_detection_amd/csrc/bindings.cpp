@@ -799,11 +799,13 @@ PYBIND11_MODULE(_fdx_native, m) {
   });
 
   // knn / smote
-  m.def("knn_prep", [](u X, int m_, int m_pad, int role, u out, u s, u outq, u aff, u parents) {
+  m.def("knn_prep", [](u X, int m_, int m_pad, int role, u out, u s, u outq, u aff, u parents, u chl, u qhl,
+                       u tmax) {
     fdx::launch_knn_prep(P<const float>(X), m_, m_pad, role, P<float>(out), P<float>(outq),
-                         P<const double>(aff), P<uint16_t>(parents), S(s));
+                         P<const double>(aff), P<uint16_t>(parents), S(s), P<void>(chl), P<void>(qhl), P<float>(tmax));
   }, py::arg("X"), py::arg("m"), py::arg("m_pad"), py::arg("role"), py::arg("out"), py::arg("s"),
-     py::arg("outq") = 0, py::arg("aff") = 0, py::arg("parents") = 0);
+     py::arg("outq") = 0, py::arg("aff") = 0, py::arg("parents") = 0, py::arg("chl") = 0, py::arg("qhl") = 0,
+     py::arg("tmax") = 0);
   m.def("knn_splits", [](int mq_pad, int mc_pad) { return fdx::knn_splits(mq_pad, mc_pad); });
   m.def("knn_lds_splits", [](int mq_pad, int mc_pad) { return fdx::knn_lds_splits(mq_pad, mc_pad); });
   m.def("knn_topk_lds", [](u Q, int mq_pad, int mq, u C, int mc_pad, int mc, int64_t self_off, int k, u oidx,

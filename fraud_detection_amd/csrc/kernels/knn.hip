@@ -57,11 +57,67 @@ __device__ __forceinline__ void topk_insert(float (&bs)[K], int (&bi)[K], float 
 // role 2 (queries == candidates, the SMOTE self-search): one read of X writes both operands,
 // candidates to `out` and queries to `outq`.  P != nullptr (candidate roles): the same launch also
 // writes the bf16 SMOTE parents of smote_parents_kernel (smote.hip), bit for bit.
+// chl / qhl / tmax (role 2 only, nullable): the hi/lo bf16 split of both operands in the same
+// launch -- knn_split_kernel's role 2 (candidates, fragment order, per-tile norm bound) and role 1
+// (queries, row order) on the values this thread just wrote, bitwise the same -- so the self-search
+// of the bf16x3 engines needs no split launches.
+__device__ __forceinline__ void split_row(const float (&x)[32], uint32_t (&h)[16], uint32_t (&l)[16]);
 __global__ void knn_prep_kernel(const float* __restrict__ X, int m, int m_pad, int role,
                                 float* __restrict__ out, float* __restrict__ outq,
-                                const double* __restrict__ aff, uint16_t* __restrict__ P) {
+                                const double* __restrict__ aff, uint16_t* __restrict__ P,
+                                uint4* __restrict__ chl = nullptr, uint4* __restrict__ qhl = nullptr,
+                                float* __restrict__ tmax = nullptr) {
 #pragma clang fp contract(off)  // the parents' mul-then-add must match smote_parents_kernel
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (chl != nullptr) {  // the fused split (blockDim 256, m_pad % 32 == 0: whole tiles per wave half)
+    const bool ok = r < m_pad;
+    float x[32];
+    if (ok && r < m) {
+      const float4* p = reinterpret_cast<const float4*>(X + (int64_t)r * kCols);
+      float s = 0.0f;
+#pragma unroll
+      for (int k = 0; k < kCols / 4; ++k) {
+        float4 v = p[k];
+        if (k == kCols / 4 - 1) {
+          s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s);
+          v.z = 0.0f; v.w = 0.0f;
+        } else {
+          s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s); s = fmaf(v.z, v.z, s); s = fmaf(v.w, v.w, s);
+        }
+        x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+      }
+      x[30] = -0.5f * s;  // the candidate row; the query row has 1 there
+    } else {
+#pragma unroll
+      for (int k = 0; k < 32; ++k) x[k] = 0.0f;
+      x[30] = -3.0e38f;  // padding candidate
+    }
+    uint32_t h[16], l[16];
+    split_row(x, h, l);
+    if (ok) {
+      const int64_t tb = (int64_t)(r >> 5) * 256 + (r & 31);
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        const int k = v & 3;
+        const uint4 c = v < 4 ? make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3])
+                              : make_uint4(l[4 * k], l[4 * k + 1], l[4 * k + 2], l[4 * k + 3]);
+        chl[tb + (v >> 1) * 64 + (v & 1) * 32] = c;
+      }
+    }
+    float n2 = (ok && x[30] > -1.0e37f) ? -2.0f * x[30] : 0.0f;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) n2 = fmaxf(n2, __shfl_xor(n2, o, kWave));
+    if (ok && (r & 31) == 0) tmax[r >> 5] = sqrtf(n2) * 1.0001f;
+    x[30] = (ok && r < m) ? 1.0f : 0.0f;  // the query row (padding queries: zeros)
+    split_row(x, h, l);
+    if (ok) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        qhl[(int64_t)r * 8 + k] = make_uint4(h[4 * k], h[4 * k + 1], h[4 * k + 2], h[4 * k + 3]);
+        qhl[(int64_t)r * 8 + 4 + k] = make_uint4(l[4 * k], l[4 * k + 1], l[4 * k + 2], l[4 * k + 3]);
+      }
+    }
+  }
   if (r >= m_pad) return;
   float4* o = reinterpret_cast<float4*>(out + (int64_t)r * kCols);
   float4* oq = role == 2 ? reinterpret_cast<float4*>(outq + (int64_t)r * kCols) : nullptr;
@@ -418,6 +474,16 @@ __global__ __launch_bounds__(kLW * kWave) void knn_topk_lds_kernel(const float* 
 // -- no true neighbour can be filtered out, and lists, threshold and returned scores are exact
 // fp32 (ties -> smaller index).
 
+__device__ __forceinline__ void split_row(const float (&x)[32], uint32_t (&h)[16], uint32_t (&l)[16]) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const float a = x[2 * k], b = x[2 * k + 1];
+    const uint32_t ph = pack_bf16x2(a, b);
+    h[k] = ph;
+    l[k] = pack_bf16x2(a - bf16lo(ph), b - bf16hi(ph));
+  }
+}
+
 // hi/lo bf16 split of prepped rows: hl[r] = 8 x uint4 (hi cols 0..31, then lo cols 0..31);
 // role 0 (candidates) also writes tmax[r / 32] = max feature norm over the 32-row tile; role 2 = role 0
 // with hl in the b3top fragment order (below).
@@ -433,13 +499,7 @@ __global__ __launch_bounds__(256) void knn_split_kernel(const float* __restrict_
     x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
   }
   uint32_t h[16], l[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const float a = x[2 * k], b = x[2 * k + 1];
-    const uint32_t ph = pack_bf16x2(a, b);
-    h[k] = ph;
-    l[k] = pack_bf16x2(a - bf16lo(ph), b - bf16hi(ph));
-  }
+  split_row(x, h, l);
   if (ok && role == 2) {
     // fragment order (b3top): tile r / 32 as [u 0..3][lane 64] uint4, lane (half hh, row j) of load u
     // holding chunk 2u + hh of row j (chunks 0..3 hi, 4..7 lo) -- each of the tile loop's four
@@ -722,9 +782,12 @@ __global__ __launch_bounds__(kWave) void knn_collect_kernel(const float* __restr
   const int all_tiles = mc_pad / 32;
   const int t_lo = (int)(((int64_t)all_tiles * blockIdx.y) / gridDim.y);
   const int t_hi = (int)(((int64_t)all_tiles * (blockIdx.y + 1)) / gridDim.y);
+  // Chl in the fragment order of knn_split role 2: each of a tile's four loads is one contiguous
+  // 1 KiB per wave (lane (h, j) of load u holds chunk 2u + h of row j -- the same registers as the
+  // row layout's p[h], p[2 + h], p[4 + h], p[6 + h]) instead of 32 rows' 16-byte pieces
   auto fetch = [&](int t, uint4 (&a)[4], float& tmv) {
-    const uint4* p = Chl + (int64_t)(t * 32 + j) * 8;
-    a[0] = p[h]; a[1] = p[2 + h]; a[2] = p[4 + h]; a[3] = p[6 + h];
+    const uint4* p = Chl + (int64_t)t * 256 + lane;
+    a[0] = p[0]; a[1] = p[64]; a[2] = p[128]; a[3] = p[192];
     tmv = tmax[t];
   };
   auto approx = [&](const uint4 (&c)[4]) -> f32x16_t {
@@ -1433,10 +1496,14 @@ unsigned merge_blocks(int mq, int nsplit) {
 }
 
 void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, float* outq,
-                     const double* aff, uint16_t* P, hipStream_t stream) {
+                     const double* aff, uint16_t* P, hipStream_t stream, void* chl, void* qhl, float* tmax) {
   if (role < 0 || role > 2 || (role == 2) != (outq != nullptr) || (role == 1 && P != nullptr))
     throw std::invalid_argument("knn_prep: role 2 needs outq (and only it); parents need a candidate role");
-  knn_prep_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, m_pad, role, out, outq, aff, P);
+  if ((chl != nullptr || qhl != nullptr || tmax != nullptr) &&
+      (role != 2 || chl == nullptr || qhl == nullptr || tmax == nullptr || m_pad % 32 != 0))
+    throw std::invalid_argument("knn_prep: the fused split needs role 2, all three outputs and m_pad % 32 == 0");
+  knn_prep_kernel<<<(m_pad + 255) / 256, 256, 0, stream>>>(X, m, m_pad, role, out, outq, aff, P,
+                                                            static_cast<uint4*>(chl), static_cast<uint4*>(qhl), tmax);
   check_launch("knn_prep");
 }
 

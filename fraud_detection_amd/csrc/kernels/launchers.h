@@ -284,8 +284,11 @@ int sgd_persist_blocks(int grid_blocks);
 // role 0: candidate rows [x, -0.5||x||^2, 0]; role 1: query rows [x, 1, 0] (features = cols 0..29);
 // role 2: both from one read (candidates -> out, queries -> outq).  P (roles 0/2, optional): the
 // bf16 SMOTE parents of launch_smote_parents (with aff) written by the same launch.
+// chl / qhl / tmax (role 2, all or none): the bf16x3 engines' hi/lo split fused in (knn_split role 2
+// for the candidates, role 1 for the queries)
 void launch_knn_prep(const float* X, int m, int m_pad, int role, float* out, float* outq,
-                     const double* aff, uint16_t* P, hipStream_t stream);
+                     const double* aff, uint16_t* P, hipStream_t stream, void* chl = nullptr, void* qhl = nullptr,
+                     float* tmax = nullptr);
 int knn_splits(int mq_pad, int mc_pad);
 // bf16x3 MFMA filter + exact fp32 re-score (knn.hip): hl [m_pad][8] uint4 = hi | lo bf16 rows of
 // the prepped rows; tmax [mc_pad / 32] max candidate norm per tile (role 0 only)

@@ -114,9 +114,19 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     Qp = torch.empty((mq_pad, NCOLS), device=Q.device, dtype=torch.float32)
     Cp = torch.empty((mc_pad, NCOLS), device=C.device, dtype=torch.float32)
     pp = _check_parents(parents, Cc, parents_affine)
-    if Qc.data_ptr() == Cc.data_ptr() and mq == mc and mq_pad == mc_pad:
-        # SMOTE self-search: one launch reads the rows once and writes both operands (+ parents)
-        m.knn_prep(ptr(Cc), mc, mc_pad, 2, ptr(Cp), s, ptr(Qp), ptr(parents_affine), pp)
+    self_search = Qc.data_ptr() == Cc.data_ptr() and mq == mc and mq_pad == mc_pad
+    split_done = False
+    if eng in ("bf16x3r", "b3top"):  # their hi/lo bf16 operands (+ per-tile candidate norm bound)
+        Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
+        Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
+        tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
+    if self_search:
+        # SMOTE self-search: one launch reads the rows once and writes both operands (+ parents, and
+        # for the bf16x3 engines that stream candidate tiles, their hi/lo split)
+        fuse = eng in ("bf16x3r", "b3top")
+        m.knn_prep(ptr(Cc), mc, mc_pad, 2, ptr(Cp), s, ptr(Qp), ptr(parents_affine), pp,
+                   ptr(Chl) if fuse else 0, ptr(Qhl) if fuse else 0, ptr(tmax) if fuse else 0)
+        split_done = fuse
     else:
         m.knn_prep(ptr(Cc), mc, mc_pad, 0, ptr(Cp), s, 0, ptr(parents_affine), pp)
         m.knn_prep(ptr(Qc), mq, mq_pad, 1, ptr(Qp), s)
@@ -137,12 +147,14 @@ def knn_topk(Q: torch.Tensor, C: torch.Tensor, k: int = 5, self_offset: int = -1
     elif eng == "fp32lds":
         m.knn_topk_lds(ptr(Qp), mq_pad, mq, ptr(Cp), mc_pad, mc, int(self_offset), int(k), ptr(idx),
                        ptr(score), ptr(ws_s), ptr(ws_i), ns, s)
-    else:
+    elif not split_done:
         # hi/lo bf16 split of both operands (+ per-tile candidate norm bound) for the filter
-        Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
-        Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
-        tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
-        m.knn_split(ptr(Cp), mc_pad, 2 if eng == "b3top" else 0, ptr(Chl), ptr(tmax), s)  # 2: fragment order
+        if eng == "bf16x3":
+            Qhl = torch.empty((mq_pad, 64), device=Q.device, dtype=torch.bfloat16)
+            Chl = torch.empty((mc_pad, 64), device=C.device, dtype=torch.bfloat16)
+            tmax = torch.empty(mc_pad // 32, device=C.device, dtype=torch.float32)
+        # 2: fragment order (b3top and the bf16x3r collect stream candidate tiles; bf16x3 reads rows)
+        m.knn_split(ptr(Cp), mc_pad, 2 if eng in ("b3top", "bf16x3r") else 0, ptr(Chl), ptr(tmax), s)
         m.knn_split(ptr(Qp), mq_pad, 1, ptr(Qhl), 0, s)
     if eng == "b3top":
         ns = min(ns, 32)
