@@ -417,14 +417,16 @@ class DevicePipeline:
             if k < 1:
                 raise ValueError("SMOTE needs at least 2 minority samples")
             # Virtual SMOTE's bucket sort needs only the draw (picks = minority rows x k, samples,
-            # seed), not the neighbour table: it can run on a side stream.  FDX_SMOTE_OVERLAP:
-            # "scaler" (default) starts it from the compute stream's position before this fit, i.e.
-            # beside the fused scaler pass; "knn" beside the k-NN; "0" in line.
+            # seed), not the neighbour table: it can run on a side stream.  FDX_SMOTE_OVERLAP: "knn"
+            # (default) beside the k-NN, whose latency-bound bf16x3r collect (~1.7 waves per SIMD)
+            # leaves CUs idle; "scaler" counts + records beside the fused scaler pass and the lambda
+            # assembly beside the k-NN; "0" in line (quick benches, profiles/r6_smote_overlap:
+            # 0.990 / 0.995-1.003 / 1.029 ms medians).
             mq_all = int(xall.shape[0])  # the neighbour table's rows (all ranks' under global scope)
             use_virt = (n_new > 0 and virt_ok and mq_all * k <= lr_ops.virtual_max_picks()
                         and n_new <= lr_ops.virtual_max_samples())
             pre_w = None
-            mode = os.environ.get("FDX_SMOTE_OVERLAP", "scaler")
+            mode = os.environ.get("FDX_SMOTE_OVERLAP", "knn")
             if use_virt and mode != "0":
                 main = torch.cuda.current_stream(dev)
                 side = self._side_stream(dev)
@@ -437,8 +439,19 @@ class DevicePipeline:
                     ev.record(main)
                 self._fit_start = None
                 side.wait_event(ev)  # every earlier use of the bucket buffers is ordered before the sort
-                pre_w = lr_ops.bucket_lambdas(mq_all, k, n_new, s_off, cfg.seed, 0 if glob else rank, dev,
-                                              self._bws[self._cur], side.cuda_stream)
+                bargs = (mq_all, k, n_new, s_off, cfg.seed, 0 if glob else rank, dev, self._bws[self._cur],
+                         side.cuda_stream)
+                if mode == "scaler":
+                    # counts + records beside the scaler pass; the lambda assembly (stage 2) waits for
+                    # the k-NN, whose latency-bound collect leaves CUs idle -- beside the small
+                    # memory-bound kernels in between it slowed each of them ~3x (profiles/r6_p5)
+                    lr_ops.bucket_lambdas(*bargs, stages=(0, 1))
+                    at_knn = torch.cuda.Event()
+                    at_knn.record(main)
+                    side.wait_event(at_knn)
+                    pre_w = lr_ops.bucket_lambdas(*bargs, stages=(2,))
+                else:
+                    pre_w = lr_ops.bucket_lambdas(*bargs)
                 bucket_done = torch.cuda.Event()
                 bucket_done.record(side)
             # SMOTE interpolation is affine-equivariant: with pivot-shifted training rows the

@@ -128,7 +128,8 @@ class VirtualSmote:
 
 
 def bucket_lambdas(mq: int, k: int, n_new: int, sample_offset: int, seed: int, counter_base: int, dev,
-                   ws: "BucketWorkspace | None" = None, stream: int | None = None) -> "BucketWorkspace":
+                   ws: "BucketWorkspace | None" = None, stream: int | None = None,
+                   stages: tuple = (0, 1, 2)) -> "BucketWorkspace":
     """The samples' lambdas bucketed by pick (VirtualSmote.prepare).  Needs only the draw -- pick
     count mq x k, sample count, seed, counters -- not the neighbour table, so a pipeline enqueues
     it on a side stream while the k-NN runs (models/pipeline.py) and adopts the result."""
@@ -145,11 +146,15 @@ def bucket_lambdas(mq: int, k: int, n_new: int, sample_offset: int, seed: int, c
     # stage 0 writes every table entry (no fill) and zeroes the bump allocator; stage 1 scans
     # each block's row in LDS (no global scan: a block's record run starts at a closed-form
     # offset) and scatters the coarse records; stage 2 assembles each pick's lambda run
-    m.smote_bucket(0, *args, ptr(w.table), 0, 0, 0, 0, 0, ptr(w.bump), s)        # counts [block][bin]
-    m.smote_bucket(1, *args, ptr(w.table), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # prefix + records
-    m.smote_bucket(2, *args, ptr(w.table), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
-                   ptr(w.bump), s)
-    w.key = (R, n, int(sample_offset), int(seed), int(counter_base))
+    # ``stages``: a caller may enqueue the stages at different points of another stream's timeline
+    if 0 in stages:
+        m.smote_bucket(0, *args, ptr(w.table), 0, 0, 0, 0, 0, ptr(w.bump), s)        # counts [block][bin]
+    if 1 in stages:
+        m.smote_bucket(1, *args, ptr(w.table), ptr(w.rec), 0, 0, 0, 0, ptr(w.bump), s)  # prefix + records
+    if 2 in stages:
+        m.smote_bucket(2, *args, ptr(w.table), ptr(w.rec), ptr(w.tmp), ptr(w.off), ptr(w.cnt), ptr(w.lam),
+                       ptr(w.bump), s)
+        w.key = (R, n, int(sample_offset), int(seed), int(counter_base))
     return w
 
 
