@@ -1632,14 +1632,14 @@ void launch_knn_topk3(const float* Q, const void* Qhl, int mq_pad, int mq, const
 int knn3r_list_cap() { return kListCap; }
 
 int knn3r_splits(int mq_pad, int mc_pad) {
-  // Four slices (fewer on small candidate sets: >= 16 tiles each).  Measured at the bench's DP=1
-  // self-search and the DP=8 global-scope rank, 4 beat 8, 9 and 16 (r5_o: 0.194 vs 0.208-0.247 ms,
-  // 0.783 vs 0.803-0.883 ms): every slice adds its own list entries and re-rank work, so filling
-  // the machine with slices does not pay.
+  // Six slices (fewer on small candidate sets: >= 16 tiles each).  Round 5 measured 4 best (r5_o:
+  // every slice adds its own list entries and re-rank work); with the fragment-order fetch, the
+  // re-rank's final-threshold skip and the seeded slices, 6 edges it (profiles/r6_knn
+  // slice_sweep.json: 0.162 vs 0.170 ms at DP=1, 0.485 vs 0.491 at the DP=8 rank; 2, 3, 5, 8 slower).
   (void)mq_pad;
   const int tiles = mc_pad / 32;
   int s = tiles / 16;
-  if (s > 4) s = 4;
+  if (s > 6) s = 6;
   if (s < 1) s = 1;
   return s;
 }
