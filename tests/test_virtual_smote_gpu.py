@@ -122,3 +122,31 @@ def test_pipeline_virtual_vs_stored_smote(dev, storage):
     av = evaluate(rv, Xt.to(dev), yt.to(dev))["auc"]
     as_ = evaluate(rs, Xt.to(dev), yt.to(dev))["auc"]
     assert abs(av - as_) < 1e-3, (av, as_)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("solver", ["sgd", "newton"])
+def test_bucket_sort_placement_does_not_change_the_fit(dev, solver, monkeypatch):
+    """FDX_SMOTE_OVERLAP: the virtual-SMOTE bucket sort in line, on a side stream beside the k-NN
+    (default) or beside the scaler pass (staged) -- the same draw, so bitwise the same model, fit
+    after fit with nothing synchronising the host in between (a cross-stream race on the bucket
+    buffers would show as a changed model).  The CV job's up-front side-stream sorts likewise."""
+    from fraud_detection_amd.models.cv import DeviceCV
+
+    X, y = separable(1_500_000, seed=31, device=dev)
+    got = {}
+    for mode in ("0", "knn", "scaler"):
+        monkeypatch.setenv("FDX_SMOTE_OVERLAP", mode)
+        pipe = DevicePipeline(TrainConfig(seed=42, solver=solver))
+        runs = [pipe.fit(X, y) for _ in range(3)]
+        torch.cuda.synchronize()
+        got[mode] = [np.asarray(r.w).copy() for r in runs]
+    for mode in ("knn", "scaler"):
+        for a, b in zip(got["0"], got[mode]):
+            assert np.array_equal(a, b), mode
+    cv = {}
+    for mode in ("0", "scaler"):
+        monkeypatch.setenv("FDX_SMOTE_OVERLAP", mode)
+        r = DeviceCV(TrainConfig(seed=42, solver=solver)).run(X, y)
+        cv[mode] = (list(r.fold_aucs), np.asarray(r.final.w).copy())
+    assert cv["0"][0] == cv["scaler"][0] and np.array_equal(cv["0"][1], cv["scaler"][1])
