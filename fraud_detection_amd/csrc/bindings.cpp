@@ -621,9 +621,9 @@ PYBIND11_MODULE(_fdx_native, m) {
                             P<unsigned long long>(persist_ws));
   }, py::arg("state"), py::arg("w32"), py::arg("class_w"), py::arg("done"), py::arg("w0"), py::arg("cw0"),
      py::arg("cw1"), py::arg("aff"), py::arg("s"), py::arg("w0_dev") = 0, py::arg("persist_ws") = 0);
-  m.def("logreg_export", [](u state, u host_dev, u s) {
-    fdx::launch_logreg_export(P<const double>(state), P<double>(host_dev), S(s));
-  });
+  m.def("logreg_export", [](u state, u host_dev, u s, long long seq) {
+    fdx::launch_logreg_export(P<const double>(state), P<double>(host_dev), S(s), seq);
+  }, py::arg("state"), py::arg("host_dev"), py::arg("s"), py::arg("seq") = 0);
   m.def("logreg_fold", [](u state, u aff, u w32, u s) {
     fdx::launch_logreg_fold(P<const double>(state), P<const double>(aff), P<float>(w32), S(s));
   });
@@ -724,7 +724,7 @@ PYBIND11_MODULE(_fdx_native, m) {
                                     int fi, double tol, int nb, int epochs, int avg_from, int serpentine,
                                     std::vector<double> lrs, int s0, int s1, int64_t Gw, u s, u stamps,
                                     std::vector<int> subs, std::vector<int> nbs, int fault_test,
-                                    unsigned spin_limit, u export_host, int prepped) -> int {
+                                    unsigned spin_limit, u export_host, int prepped, long long export_seq) -> int {
     if ((int)lrs.size() < epochs || epochs > fdx::kSgdMaxEpochs) throw std::runtime_error("sgd_persist: bad lrs");
     if ((int)subs.size() < epochs) throw std::runtime_error("sgd_persist: one sub-sample factor per epoch");
     if ((int)nbs.size() < epochs) throw std::runtime_error("sgd_persist: one minibatch count per epoch");
@@ -764,6 +764,7 @@ PYBIND11_MODULE(_fdx_native, m) {
     if (spin_limit > 0) a.spin_limit = spin_limit;
     a.export_host = P<double>(export_host);
     a.prepped = prepped;
+    a.export_seq = export_seq;
     // 0: enqueued; 1: the cooperative launch refused the grid (the caller launches per step)
     return fdx::launch_sgd_persist(P<const void>(X), fp8, x_scale, end, P<const float>(cw), parents ? &v : nullptr, h,
                                    a, S(s));
@@ -773,7 +774,8 @@ PYBIND11_MODULE(_fdx_native, m) {
      py::arg("w32"), py::arg("done"), py::arg("aff"), py::arg("d"), py::arg("C"), py::arg("mom"), py::arg("fi"),
      py::arg("tol"), py::arg("nb"), py::arg("epochs"), py::arg("avg_from"), py::arg("serpentine"), py::arg("lrs"),
      py::arg("s0"), py::arg("s1"), py::arg("Gw"), py::arg("s"), py::arg("stamps"), py::arg("subs"), py::arg("nbs"),
-     py::arg("fault_test") = 0, py::arg("spin_limit") = 0u, py::arg("export_host") = 0, py::arg("prepped") = 0);
+     py::arg("fault_test") = 0, py::arg("spin_limit") = 0u, py::arg("export_host") = 0, py::arg("prepped") = 0,
+     py::arg("export_seq") = 0);
   m.def("sgd_persist_blocks", [](int grid_blocks) { return fdx::sgd_persist_blocks(grid_blocks); });
   m.def("sgd_full_blocks", []() { return fdx::sgd_full_blocks(); });
   m.attr("SGD_PERSIST_WORDS") = fdx::kSgdPersistWords;

@@ -205,7 +205,7 @@ struct LRInitArgs {
 void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* class_w, int* done,
                         const double* aff, hipStream_t stream, const double* w0_dev = nullptr,
                         unsigned long long* persist_ws = nullptr);
-void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream);
+void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream, long long seq = 0);
 // Minibatch SGD step (logreg.hip sgd_apply): c = epoch step scalar (lr = c / mean curvature),
 // nb = minibatches per epoch, avg = add this step's iterate to the Polyak average, epoch_end =
 // settle the epoch's convergence state (and return the average when one was taken).
@@ -267,9 +267,12 @@ struct SgdPersistArgs {
                                          // (tools/sgd_stamps.py)
   unsigned spin_limit = 1u << 20;        // barrier polls before a block declares the grid not resident
   int fault_test = 0;                    // test knob: barrier s0 unreachable -> the recovery launch runs
-  // nullable: device address of a mapped pinned [kStateSize] fp64 slot -- the recovery launch
-  // exports the final state there (instead of a separate logreg_export launch behind it)
+  // nullable: device address of a mapped pinned [kStateSize + 1] fp64 slot -- the recovery launch
+  // exports the final state there (instead of a separate logreg_export launch behind it), then
+  // export_seq into word kStateSize (int64): the host polls that stamp, so no event is recorded
+  // behind the launch (a marker the command processor spends ~7 us on at the fit boundary)
   double* export_host = nullptr;
+  long long export_seq = 0;
   int prepped = 0;  // logreg_init already zeroed ws and backed up the initial state (no prep launch)
 };
 // Returns 0 when enqueued (prep kernel, the persistent launch, its recovery launch); 1 when the

@@ -1505,12 +1505,20 @@ __global__ __launch_bounds__(64) void logreg_init_kernel(LRInitArgs a, double* _
 }
 
 // Solver state -> host: plain vector stores into a mapped pinned buffer (device address of the
-// host allocation), replacing a D2H blit at the end of every fit.
-__global__ __launch_bounds__(64) void logreg_export_kernel(const double* __restrict__ st, double* __restrict__ host) {
+// host allocation), replacing a D2H blit at the end of every fit.  seq != 0: then the stamp into
+// word kStateSize once the wave's stores have landed -- the host polls it instead of an event.
+__global__ __launch_bounds__(64) void logreg_export_kernel(const double* __restrict__ st, double* __restrict__ host,
+                                                           long long seq) {
   const int t = threadIdx.x;
 #pragma unroll
   for (int i = 0; i < kStateSize / 64; ++i)  // system scope: written through to host memory
     __hip_atomic_store(host + t + 64 * i, st[t + 64 * i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (seq != 0) {  // one wave: its vmcnt covers every lane's stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t == 0)
+      __hip_atomic_store(reinterpret_cast<long long*>(host + kStateSize), seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // ---- minibatch SGD (config 3: "SMOTE k-NN + logistic SGD") --------------------------------------
@@ -2042,6 +2050,19 @@ __global__ __launch_bounds__(256) void sgd_persist_prep_kernel(unsigned long lon
   persist_prep_block(ws, st, w32, *done, threadIdx.x, 256);
 }
 
+// The fit's final state -> the mapped pinned slot (system-scope stores, written through to host
+// memory), then the slot's stamp once every thread's stores have landed: the host polls the stamp
+// (PendingFit) instead of an event recorded behind the launch.  Whole block, uniform.
+__device__ __forceinline__ void export_state_stamped(double* host, const double* src, long long seq, int t) {
+  for (int e = t; e < kStateSize; e += kPersistThreads)
+    __hip_atomic_store(host + e, src[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0)
+    __hip_atomic_store(reinterpret_cast<long long*>(host + kStateSize), seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Behind every persistent launch: a no-op unless its fault word is set.  Then one block re-runs
 // steps [s0, s1) from the backup: its 8 waves walk the per-step grid's Gw waves in turn, each
 // wave's sums go to fixed point on their own (the persistent launch converts per wave too), so the
@@ -2057,8 +2078,7 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_recover_kernel(const v
   if (__hip_atomic_load(reinterpret_cast<unsigned int*>(P.ws + kWsFault), __ATOMIC_RELAXED,
                         __HIP_MEMORY_SCOPE_AGENT) == 0u) {  // uniform: the word the previous launch left
     if (P.export_host != nullptr)  // the fit's final state -> the mapped pinned slot (logreg_export)
-      for (int e = threadIdx.x; e < kStateSize; e += kPersistThreads)
-        __hip_atomic_store(P.export_host + e, P.st[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      export_state_stamped(P.export_host, P.st, P.export_seq, threadIdx.x);
     return;
   }
   __shared__ double sst[kStateSize];
@@ -2111,13 +2131,10 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_recover_kernel(const v
   }
   if (t == 0) sst[kSgdFault] = 2.0;
   __syncthreads();
-  for (int e = t; e < kStateSize; e += kPersistThreads) {
-    P.st[e] = sst[e];
-    if (P.export_host != nullptr)
-      __hip_atomic_store(P.export_host + e, sst[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  for (int e = t; e < kStateSize; e += kPersistThreads) P.st[e] = sst[e];
   if (t < 32) P.w32[t] = wnew[t];
   if (t == 0) *P.done = s_done;
+  if (P.export_host != nullptr) export_state_stamped(P.export_host, sst, P.export_seq, t);
 }
 
 }  // namespace
@@ -2317,8 +2334,8 @@ void launch_logreg_init(const LRInitArgs& a, double* state, float* w32, float* c
   check_launch("logreg_init");
 }
 
-void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream) {
-  logreg_export_kernel<<<1, 64, 0, stream>>>(state, host_dev);
+void launch_logreg_export(const double* state, double* host_dev, hipStream_t stream, long long seq) {
+  logreg_export_kernel<<<1, 64, 0, stream>>>(state, host_dev, seq);
   check_launch("logreg_export");
 }
 

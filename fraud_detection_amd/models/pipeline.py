@@ -319,7 +319,9 @@ class DevicePipeline:
                 xmins.append(scaler_ops.scale_cast(xd, stats, labels=yd, out_dtype="f32", idx=idx))
         xmin = torch.cat(xmins) if xmins else torch.empty((0, NCOLS), dtype=torch.float32, device=dev)
         _maybe_fault(rank)
-        return self._finish(stats, rows_cap, n, d, int(xmin.shape[0]), False, tm, comm, rank, dev, lambda: xmin)
+        # host_ordered: the last chunk's compact_indices waited for its count, behind every earlier kernel
+        return self._finish(stats, rows_cap, n, d, int(xmin.shape[0]), False, tm, comm, rank, dev, lambda: xmin,
+                            host_ordered=n > 0)
 
     def fit(self, X: torch.Tensor, y: torch.Tensor, profile: bool = False) -> PipelineResult:
         cfg = self.cfg
@@ -346,10 +348,12 @@ class DevicePipeline:
             # host is a fit ahead, so the count no longer sits behind a host wait at the fit
             # boundary (profiles/r3_q/count_front_ab.txt: 1.273 vs 1.309 ms per step with the
             # count on a side stream beside the pass, the round-2 winner).
-            # the compute stream's position before this fit: the SMOTE bucket sort's side stream
-            # starts from here, beside the scaler pass (_finish)
-            self._fit_start = torch.cuda.Event()
-            self._fit_start.record()
+            # the compute stream's position before this fit: under FDX_SMOTE_OVERLAP=scaler the SMOTE
+            # bucket sort's side stream starts from here, beside the scaler pass (_finish).  Only
+            # then: the marker costs the command processor ~7 us at the fit boundary (r6_marker)
+            if os.environ.get("FDX_SMOTE_OVERLAP", "knn") == "scaler":
+                self._fit_start = torch.cuda.Event()
+                self._fit_start.record()
             pending = scaler_ops.compact_indices_async(y, 1)
             stats = scaler_ops.scaler_fit_cast(X, y, rows_cap[:n], comm=comm, fp8_scale=cfg.fp8_scale)
             tm.mark("scaler_fit")
@@ -365,11 +369,15 @@ class DevicePipeline:
         n_min = int(idx_min.shape[0])
         _maybe_fault(rank)
         return self._finish(stats, rows_cap, n, d, n_min, fused, tm, comm, rank, dev,
-                            lambda: scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min))
+                            lambda: scaler_ops.scale_cast(X, stats, labels=y, out_dtype="f32", idx=idx_min),
+                            host_ordered=True)
 
-    def _finish(self, stats, rows_cap, n, d, n_min, fused, tm, comm, rank, dev, get_xmin) -> PipelineResult:
+    def _finish(self, stats, rows_cap, n, d, n_min, fused, tm, comm, rank, dev, get_xmin,
+                host_ordered: bool = False) -> PipelineResult:
         """SMOTE (+ DP exchange) and the solver on the device-resident training rows
-        rows_cap[:n] (shared by the resident and the host-streaming preparation)."""
+        rows_cap[:n] (shared by the resident and the host-streaming preparation).  host_ordered:
+        the host has waited for a compute-stream result enqueued behind every earlier kernel (the
+        minority count), so everything enqueued before this fit has finished."""
         cfg = self.cfg
 
         def quota(n_r, nmin_r):
@@ -418,10 +426,12 @@ class DevicePipeline:
                 raise ValueError("SMOTE needs at least 2 minority samples")
             # Virtual SMOTE's bucket sort needs only the draw (picks = minority rows x k, samples,
             # seed), not the neighbour table: it can run on a side stream.  FDX_SMOTE_OVERLAP: "knn"
-            # (default) beside the k-NN, whose latency-bound bf16x3r collect (~1.7 waves per SIMD)
-            # leaves CUs idle; "scaler" counts + records beside the fused scaler pass and the lambda
-            # assembly beside the k-NN; "0" in line (quick benches, profiles/r6_smote_overlap:
-            # 0.990 / 0.995-1.003 / 1.029 ms medians).
+            # (default) the whole sort from here on, with no event in front of it unless its buffers
+            # grew -- it runs beside the scaler pass that is still going; "scaler" counts + records
+            # from the fit's start and the lambda assembly beside the k-NN; "0" in line (quick
+            # benches, profiles/r6_marker: 0.983 / 0.980 / 1.018 ms means, 0.978 / 0.971 / 1.010
+            # medians; before the events came off the fit boundary, r6_smote_overlap: 0.990 /
+            # 0.995-1.003 / 1.029 medians).
             mq_all = int(xall.shape[0])  # the neighbour table's rows (all ranks' under global scope)
             use_virt = (n_new > 0 and virt_ok and mq_all * k <= lr_ops.virtual_max_picks()
                         and n_new <= lr_ops.virtual_max_samples())
@@ -433,12 +443,19 @@ class DevicePipeline:
                 # buffers (re)allocated now come from the compute stream's pool, possibly from
                 # blocks its queued kernels still use: then the sort waits for the present position
                 grew = self._bws[self._cur].reserve(dev, mq_all, k, n_new)
+                # Otherwise every earlier use of the buffers (an earlier fit's passes) is already
+                # done: the host has seen this fit's minority count (idx_min above), written by a
+                # kernel behind all of them on the compute stream -- no event needed, and the sort
+                # starts at once, beside the scaler pass.  An event recorded behind the scaler pass
+                # costs a marker there and holds the sort back into the k-NN's critical path
+                # (profiles/r6_marker).
                 ev = getattr(self, "_fit_start", None) if (mode == "scaler" and not grew) else None
-                if ev is None:
+                if ev is None and (grew or not host_ordered):
                     ev = torch.cuda.Event()
                     ev.record(main)
                 self._fit_start = None
-                side.wait_event(ev)  # every earlier use of the bucket buffers is ordered before the sort
+                if ev is not None:
+                    side.wait_event(ev)
                 bargs = (mq_all, k, n_new, s_off, cfg.seed, 0 if glob else rank, dev, self._bws[self._cur],
                          side.cuda_stream)
                 if mode == "scaler":

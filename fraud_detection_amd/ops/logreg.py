@@ -226,12 +226,13 @@ class PendingFit:
     _POOL = 8
 
     def __init__(self, state_dev: torch.Tensor, sgd: bool = False, verify=None, warm_iters: int = 0,
-                 keep: tuple = (), collective: bool = False, slot: int | None = None, exported: bool = False):
+                 keep: tuple = (), collective: bool = False, slot: int | None = None, exported: int = 0):
         cls = PendingFit
         if slot is None:
             slot = cls.reserve()
         cls._owners[slot] = self
         self._slot, self._sgd, self._info = slot, sgd, None
+        self._stream = torch.cuda.current_stream(state_dev.device) if state_dev.is_cuda else None
         self._verify, self._state_dev, self.warm_iters = verify, state_dev, int(warm_iters)
         # the tensors a deferred continuation reads by device address (rows, affine map, virtual
         # SMOTE buffers): referenced here until verified, so the caching allocator cannot hand
@@ -247,9 +248,11 @@ class PendingFit:
     def reserve(cls) -> int:
         """The next pinned slot, its previous owner materialised.  A fit that exports its own final
         state (the persistent SGD launch's recovery kernel stores it into ``slot_address``) reserves
-        the slot before enqueueing, then wraps it with ``PendingFit(..., slot=, exported=True)``."""
+        the slot before enqueueing, then wraps it with ``PendingFit(..., slot=, exported=stamp)``."""
         if not cls._pool:
-            cls._pool = [torch.empty(STATE_SIZE, dtype=torch.float64, pin_memory=True) for _ in range(cls._POOL)]
+            # word STATE_SIZE: the stamp (int64) an exporting launch stores after the state
+            cls._pool = [torch.zeros(STATE_SIZE + 1, dtype=torch.float64, pin_memory=True) for _ in range(cls._POOL)]
+            cls._stamps = [t.view(torch.int64).numpy()[STATE_SIZE:] for t in cls._pool]
             cls._owners = [None] * cls._POOL
             # device addresses of the mapped pinned slots: the export kernel stores into them
             cls._pool_dev = [int(native().host_device_pointer(t.data_ptr())) for t in cls._pool]
@@ -267,16 +270,38 @@ class PendingFit:
     def slot_address(cls, slot: int) -> int:
         return cls._pool_dev[slot]
 
-    def _export(self, done: bool = False):
+    @classmethod
+    def next_stamp(cls) -> int:
+        """A fresh stamp (> every earlier one) for a launch that exports into a slot."""
+        cls._seq = getattr(cls, "_seq", 0) + 1
+        return cls._seq
+
+    def _export(self, stamp: int = 0):
+        """``stamp`` > 0: the fit's last kernel exports the state and then this stamp into the slot
+        (sgd_persist(export_seq=)); the host polls the stamp, so no event is recorded behind it --
+        each marker cost the command processor ~7 us at the fit boundary (profiles/r6_marker)."""
         cls, slot, st = PendingFit, self._slot, self._state_dev
-        if done:
-            pass  # already enqueued by the fit's last kernel
-        elif cls._pool_dev[slot] and st.numel() == STATE_SIZE:
-            native().logreg_export(ptr(st), cls._pool_dev[slot], stream_of(st))
+        self._stamp, self._event = int(stamp), None
+        if stamp:
+            return
+        if cls._pool_dev[slot] and st.numel() == STATE_SIZE:  # the export kernel stamps the slot too
+            self._stamp = cls.next_stamp()
+            native().logreg_export(ptr(st), cls._pool_dev[slot], stream_of(st), self._stamp)
         else:
-            cls._pool[slot].copy_(st, non_blocking=True)
+            cls._pool[slot][:STATE_SIZE].copy_(st, non_blocking=True)
         self._event = torch.cuda.Event()
         self._event.record()
+
+    SPIN_S = 0.05  # stamp polling, then a wait on the fit's stream (a faulted stream raises there)
+
+    def _wait_stamp(self):
+        view, t0 = PendingFit._stamps[self._slot], time.perf_counter()
+        while int(view[0]) != self._stamp:
+            if time.perf_counter() - t0 > self.SPIN_S:
+                self._stream.synchronize()
+                if int(view[0]) != self._stamp:
+                    raise RuntimeError("PendingFit: state not exported after its stream drained")
+                return
 
     def verify(self) -> "PendingFit":
         """Resolve a deferred convergence check (no-op for an already checked fit).  Under data
@@ -297,8 +322,11 @@ class PendingFit:
                 raise RuntimeError("data-parallel fit with a pending convergence check: settle it on every "
                                    "rank first (DevicePipeline.settle() or evaluate(...)), then read it")
             self.verify()
-            self._event.synchronize()
-            self._info = _info_from_state(PendingFit._pool[self._slot].numpy().copy(), self._sgd)
+            if self._event is not None:
+                self._event.synchronize()
+            else:
+                self._wait_stamp()
+            self._info = _info_from_state(PendingFit._pool[self._slot][:STATE_SIZE].numpy().copy(), self._sgd)
             if PendingFit._owners[self._slot] is self:
                 PendingFit._owners[self._slot] = None
         return self._info
@@ -965,13 +993,14 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
              ptr(v.off) if v else 0, ptr(v.cnt) if v else 0, int(rows.shape[0]),
              int(v.q_offset) if v else 0, int(mq), int(k), int(hole[0]), int(hole[1]))
 
-    def run_steps(s0: int, s1: int, prepped: bool = False, export_slot: int | None = None) -> bool:
+    def run_steps(s0: int, s1: int, prepped: bool = False, export_slot: int | None = None) -> int:
         """Steps [s0, s1) of the schedule: ONE persistent launch (a grid barrier per step, the
         update in every block), or one fused launch per step (FISH pass whose last block applies
-        the update) -- bitwise the same fit.  Returns True when the final state was exported into
-        ``export_slot`` by the persistent launch's recovery kernel."""
+        the update) -- bitwise the same fit.  Returns the stamp (> 0) when the persistent launch's
+        recovery kernel exported the final state into ``export_slot``, else 0."""
         if s1 <= s0:
-            return False
+            return 0
+        stamp = PendingFit.next_stamp() if (persist and export_slot is not None) else 0
         if persist:
             refused = m.sgd_persist(ptr(rows), int(fp8), float(fp8_scale), n + hole[1], ptr(ws.class_w), *vargs,
                                     ptr(ws.sgd_persist), ptr(ws.state), ptr(ws.w32), ptr(ws.done), aff, d, float(C),
@@ -980,9 +1009,9 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                                     4 * blocks, s, ptr(_stamps) if _stamps is not None else 0, subs, nbs,
                                     int(bool(_fault_test)), int(_spin_limit),
                                     PendingFit.slot_address(export_slot) if export_slot is not None else 0,
-                                    int(bool(prepped)))
+                                    int(bool(prepped)), stamp)
             if not refused:
-                return export_slot is not None
+                return stamp
             # the cooperative launch refused the grid: the per-step launches (bitwise the same fit)
         if serpentine:
             raise ValueError("serpentine minibatch order needs the persistent SGD launch")
@@ -991,7 +1020,7 @@ def sgd_fit(rows: torch.Tensor, C: float = 1.0, lr=SGD_LR, momentum: float = SGD
                   float(C), float(momentum), int(fit_intercept), float(tol), nb, int(epochs), int(avg_from),
                   [float(x) for x in lrs], int(s0), int(max(s0, s1)), ptr(ws.sgd_acc),
                   ptr(ws.sgd_acc[SGD_ACC_WORDS:]), subs, nbs)
-        return False
+        return 0
 
     if not dp and checkpoint is None:
         s0 = estart[start[0]] + start[1]
