@@ -261,6 +261,7 @@ struct SgdFuse {
   SgdArgs a;
 };
 constexpr double kFixScale = 1048576.0;  // 2^20
+template <bool kWaveOnly = false>
 __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done,
                           const double* __restrict__ aff, const SgdArgs& a, int t, bool mapped);
 
@@ -1539,6 +1540,16 @@ enum : int { kAvg = 160, kEpG = 192, kEpLoss = 224, kEpW = 225, kNAvg = 226, kDb
 constexpr double kDbarFloor = 1e-3;  // lr_t <= c / 1e-3: a saturated minibatch cannot blow the step up
 constexpr int kSgdSlots = 36;        // grad[32] | loss | weight | (34: unused) | curvature sum
 
+template <bool kWaveOnly>
+__device__ __forceinline__ void sgd_sync() {
+  if constexpr (kWaveOnly) nsync();
+  else sgd_sync<kWaveOnly>();
+}
+
+// kWaveOnly: ONE wave calls it (t = its lane) and its phases are ordered by wave barriers only --
+// the persistent launch's arriving wave applies the step while the block's other waves wait at
+// one block barrier (the same operations in the same order: bitwise the block version's state).
+template <bool kWaveOnly>
 __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __restrict__ w32, int* __restrict__ done,
                           const double* __restrict__ aff, const SgdArgs& a, int t, bool mapped) {
   // rd: the reduced [36] sums in LDS (raw row space).  Every thread of the block calls this (it
@@ -1549,7 +1560,7 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
       const double av = aff[t];
       if (t < 32) cA[t] = av; else iA[t - 32] = av;
     }
-    __syncthreads();
+    sgd_sync<kWaveOnly>();
   }
   const double S = rd[33] > 0.0 ? rd[33] : 1.0;
   // mapped: the sums arrive in standardized space already (fused passes map them per block)
@@ -1557,7 +1568,7 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
   const double reg = 1.0 / (a.C * S * (double)a.nb);  // the minibatch estimates sum s over the epoch as nb S
   const double dbar = fmax(rd[35] / S, kDbarFloor);
   const double lr = a.c / dbar;
-  __syncthreads();
+  sgd_sync<kWaveOnly>();
   if (t < kCols) {
     double g = 0.0;
     if (t < a.d) g = rz[t] / S + reg * st[kW + t];
@@ -1569,7 +1580,7 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
     if (a.avg) st[kAvg + t] += wn;
     ss[kW + t] = wn;
   }
-  __syncthreads();
+  sgd_sync<kWaveOnly>();
   if (t == 0) {
     st[kEpLoss] += rd[32];
     st[kEpW] += rd[33];
@@ -1578,12 +1589,12 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
     st[kDbar] = dbar;
     st[kLr] = lr;
   }
-  __syncthreads();
+  sgd_sync<kWaveOnly>();
   if (a.epoch_end) {
     const double Sw = st[kEpW] > 0.0 ? st[kEpW] : 1.0;
     const double na = st[kNAvg];
     if (t < kCols && na > 0.0) ss[kW + t] = st[kAvg + t] / na;  // the averaged iterate is the model
-    __syncthreads();
+    sgd_sync<kWaveOnly>();
     double g = 0.0;
     if (t < a.d) g = st[kEpG + t] / Sw + ss[kW + t] / (a.C * Sw);
     else if (t == kBiasCol && a.fit_intercept) g = st[kEpG + t] / Sw;
@@ -1596,7 +1607,7 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
       st[kEpG + t] = 0.0;
       st[kAvg + t] = 0.0;
     }
-    __syncthreads();
+    sgd_sync<kWaveOnly>();
     if (t == 0) {
       st[kGmax] = ga;
       st[kObj] = st[kEpLoss] / Sw + 0.5 * w2 / (a.C * Sw);
@@ -1609,7 +1620,7 @@ __device__ void sgd_apply(const double* rd, double* __restrict__ st, float* __re
       }
     }
   }
-  __syncthreads();
+  sgd_sync<kWaveOnly>();
   if (t < kCols) st[kW + t] = ss[kW + t];
   if (aff) {
     store_folded(ss, cA, iA, w32, t);
@@ -1889,7 +1900,6 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
   __shared__ __attribute__((aligned(16))) float wsh[32];  // weights of the passes (fp8: row units)
   __shared__ float wnew[32];                              // sgd_apply's folded weights
   __shared__ float red[kPersistWaves][36];
-  __shared__ unsigned long long rep[kPersistAccWords];
   __shared__ double rd[kSgdSlots];
   __shared__ int s_done, s_ok;
   __shared__ double saff[64];  // the affine map, read from LDS by every step's reduce and update
@@ -1998,27 +2008,31 @@ __global__ __launch_bounds__(kPersistThreads, 1) void sgd_persist_kernel(const v
       if (P.stamps != nullptr && lane == 0)
         P.stamps[((int64_t)(st - P.s0) * kStampRows + 0) * gridDim.x + blockIdx.x] = wall_clock64();
       const bool ok = persist_barrier(bar, arrivals, lane, fault, P.spin_limit);
-      if (!ok && lane == 0) s_ok = 0;
       if (P.stamps != nullptr && lane == 0)
         P.stamps[((int64_t)(st - P.s0) * kStampRows + 1) * gridDim.x + blockIdx.x] = wall_clock64();
+      if (!ok) {
+        if (lane == 0) s_ok = 0;
+      } else {
+        // ---- the update, redundantly in every block, by this wave alone (wave barriers only;
+        // the block's other waves wait at the one block barrier below) ----
+        if (lane < kSgdSlots) {  // the replicas' sums (integer: exact in any order)
+          unsigned long long v[kPersistReplicas];
+#pragma unroll
+          for (int r = 0; r < kPersistReplicas; ++r)
+            v[r] = __hip_atomic_load(acc + r * 36 + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          unsigned long long q = 0;
+#pragma unroll
+          for (int r = 0; r < kPersistReplicas; ++r) q += v[r];
+          rd[lane] = (double)(long long)q * (1.0 / kFixScale);
+        }
+        nsync();
+        sgd_apply<true>(rd, sst, wnew, &s_done, affl, S.args(P), lane, true);
+        nsync();
+        if (lane < 32) wsh[lane] = lane == kLabelCol ? 0.0f : wnew[lane] * ((FP8 && lane < d_feat) ? inv_s : 1.0f);
+      }
     }
     __syncthreads();
     if (!s_ok) return;  // uniform in the block: a faulted grid publishes nothing
-    // ---- the update, redundantly in every block ----
-    for (int e = t; e < kPersistAccWords; e += kPersistThreads)
-      rep[e] = __hip_atomic_load(acc + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    if (t < kSgdSlots) {  // fixed-order fold of the replicas (integer: exact in any order anyway)
-      unsigned long long q = 0;
-#pragma unroll 8
-      for (int r = 0; r < kPersistReplicas; ++r) q += rep[r * 36 + t];
-      rd[t] = (double)(long long)q * (1.0 / kFixScale);
-    }
-    __syncthreads();
-    sgd_apply(rd, sst, wnew, &s_done, affl, S.args(P), t, true);
-    __syncthreads();
-    if (t < 32) wsh[t] = t == kLabelCol ? 0.0f : wnew[t] * ((FP8 && t < d_feat) ? inv_s : 1.0f);
-    __syncthreads();
     if (P.stamps != nullptr && t == 0)
       P.stamps[((int64_t)(st - P.s0) * kStampRows + 2) * gridDim.x + blockIdx.x] = wall_clock64();
   }
