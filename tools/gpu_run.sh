@@ -71,6 +71,13 @@ for st in "$@"; do
       step smoteov_off 300 env FDX_SMOTE_OVERLAP=0 python bench.py --steps 30 --warmup 3 --no-extras &&
       step smoteov_scaler2 300 env FDX_SMOTE_OVERLAP=scaler python bench.py --steps 30 --warmup 3 --no-extras &&
       step smoteov_scaler_hi 300 env FDX_SMOTE_OVERLAP=scaler FDX_SMOTE_SIDE_PRIO=-1 python bench.py --steps 30 --warmup 3 --no-extras ;;
+    sortpoll)  # host-polled bucket-sort completion (default) vs the cross-stream wait, alternating
+      step sortpoll_on1 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step sortpoll_off1 300 env FDX_SORT_POLL_US=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step sortpoll_on2 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step sortpoll_off2 300 env FDX_SORT_POLL_US=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step sortpoll_on3 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step sortpoll_off3 300 env FDX_SORT_POLL_US=0 python bench.py --steps 30 --warmup 3 --no-extras ;;
     quicksgdnc) step quicksgd_coop 300 env FDX_SGD_COOP=1 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
     evab)  # per-fit timing events and the side-stream export, on / off (quick SGD bench each)
       step evab_default 300 python bench.py --steps 30 --warmup 3 --no-extras &&
