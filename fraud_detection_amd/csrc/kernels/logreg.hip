@@ -1711,9 +1711,10 @@ __global__ __launch_bounds__(64) void sgd_update_fixed_kernel(const long long* _
 //   pass over minibatch b -> every wave's [36] sums in LDS -> the block's LAST wave (kArriveWave)
 //   turns each wave's sums into 2^-20 fixed point exactly as sgd_fused_tail does, adds the block's
 //   total into replica (block mod kPersistReplicas = 16) of accumulator set t mod 3 with
-//   agent-scope int64 atomics, and arrives at the grid barrier -> every block reads the set with
-//   agent-scope loads and applies the SAME update (sgd_apply) to its own LDS copy of the solver
-//   state.  Integer sums are order-free and every block runs the same fp64 code on the same
+//   agent-scope int64 atomics, and arrives at the grid barrier -> in every block that same wave
+//   reads the set with agent-scope loads and applies the SAME update (sgd_apply<true>: wave
+//   barriers only, while the block's other waves wait at one block barrier; 3.5 -> 2.0 us per step,
+//   profiles/r6_wave_update) to the block's LDS copy of the solver state.  Integer sums are order-free and every block runs the same fp64 code on the same
 //   inputs, so every block holds bitwise the same state -- and bitwise the per-step launches'
 //   state; the convergence flag is therefore uniform across the grid with no broadcast.
 // Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): the payload is written only by
