@@ -349,7 +349,8 @@ def _sgd_details(pipe, r, X, y, scope, storage) -> dict:
     mine = pipe.training_objective(r)
     opt = pipe.training_objective(r, w=_NEWTON_W[storage])
     return dict(steps=int(f.n_iter), epochs=pipe.cfg.sgd_epochs,
-                minibatches_per_epoch=[int(v) for v in pipe.cfg.sgd_epoch_batches],
+                minibatches_per_epoch=[int(v) for v in pipe.cfg.sgd_epoch_batches[:pipe.cfg.sgd_epochs]],
+                extra_epoch_minibatches=[int(v) for v in pipe.cfg.sgd_epoch_batches[pipe.cfg.sgd_epochs:]],
                 converged=bool(f.converged), epoch_grad_max=float(f.grad_max), tol=pipe.cfg.sgd_tol,
                 recovered_launch=bool(getattr(f, "recovered", False)),
                 objective=round(mine["objective"], 9), newton_objective=round(opt["objective"], 9),

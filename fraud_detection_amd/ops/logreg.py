@@ -793,7 +793,9 @@ def _sgd_signature(n, d, C, lr, momentum, nb, epochs, average, tol, class_w, fit
 # steps for 1e-3 (the curvature falls ~5x between w = 0 and the optimum).
 SGD_BATCHES = 8
 SGD_EPOCHS = 3
-SGD_LR = (0.6, 0.8, 0.8)      # per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch)
+# per-epoch step scalar c (lr_t = c / mean s p (1 - p) of the minibatch); the 4th entry is the
+# extra epoch's (SGD_EXTRA_EPOCHS)
+SGD_LR = (0.6, 0.8, 0.8, 0.6)
 # Per-epoch row sub-sample: epoch 0 visits 1/4 of the rows -- a growing-batch schedule: the first
 # epoch only has to bring w near the optimum, so it needs no full pass (Smith et al., "Don't decay
 # the learning rate, increase the batch size").  A sub-sampled epoch never decides convergence.
@@ -806,7 +808,12 @@ SGD_SUB = (4, 1, 1)
 # instead of 20: 1.050 vs 1.111 ms per bf16 fit, 0.997 vs 1.066 fp8 (profiles/r5_zz,
 # tools/sgd_schedule_ab.py).  8 steps at c = 0.4 in epoch 0 ("sub4_avg2") ended at 4.5-9.8e-4 with 8
 # more grid barriers; 4 steps over an eighth of the rows ran the extra epoch on some seeds.
-SGD_EPOCH_BATCHES = (4, 6, 6)
+# The extra epoch (4th entry) takes 3 minibatches at c = 0.6: the CV job's folds that miss tol after
+# the nominal 16 steps end at the same epoch gradient (1.4-1.7e-3 vs 1.1-1.8e-3 after a 6-step extra
+# epoch at c = 0.8 -- the statistic's noise level, tol is not reached either way) and the same AUCs
+# in 19 steps instead of 22 (profiles/r6_sgd/extra_epoch_candidates_gpu.log: 2, 3 or 4 minibatches
+# at c = 0.8, 0.4 or 0.3 ended at 1.8-8.6e-3).  Nominal fits never run it.
+SGD_EPOCH_BATCHES = (4, 6, 6, 3)
 # Epochs past SGD_EPOCHS that run only while the fit has not converged (the device `done` flag makes
 # them no-ops otherwise; the persistent launch leaves its loop).  Each is averaged like the last
 # nominal epoch, starting from that epoch's averaged iterate.  fp8 rows carry ~6% quantisation

@@ -116,7 +116,7 @@ def test_sgd_reaches_newton_optimum_at_scale(dev, storage):
     f = rs.fit
     # the nominal epochs, plus the extra epoch(s) only if the nominal ones did not converge
     # (an extra epoch takes the count of the schedule's last epoch: ops/logreg._epoch_lr clamps)
-    nominal = sum(L.SGD_EPOCH_BATCHES)
+    nominal = sum(L.SGD_EPOCH_BATCHES[:L.SGD_EPOCHS])
     extra = [int(L._epoch_lr(L.SGD_EPOCH_BATCHES, L.SGD_EPOCHS + e)) for e in range(L.SGD_EXTRA_EPOCHS)]
     assert f.n_iter in [nominal + sum(extra[:e]) for e in range(L.SGD_EXTRA_EPOCHS + 1)], f.n_iter
     assert f.converged and f.grad_max <= L.SGD_TOL, (f.grad_max, gap, f.n_iter)

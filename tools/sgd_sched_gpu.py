@@ -28,6 +28,16 @@ CANDS = {
     "lr23_09_06": {"sgd_lr": (0.6, 0.9, 0.6)},
     "mom05": {"sgd_momentum": 0.5},
     "mom06_lr3_06": {"sgd_momentum": 0.6, "sgd_lr": (0.6, 0.8, 0.6)},
+    # the extra epoch (run only while not converged) with its own, smaller minibatch count
+    "x2": {"sgd_epoch_batches": (4, 6, 6, 2)},
+    "x3": {"sgd_epoch_batches": (4, 6, 6, 3)},
+    "x4": {"sgd_epoch_batches": (4, 6, 6, 4)},
+    "x3_lr06": {"sgd_epoch_batches": (4, 6, 6, 3), "sgd_lr": (0.6, 0.8, 0.8, 0.6)},
+    "x3_lr04": {"sgd_epoch_batches": (4, 6, 6, 3), "sgd_lr": (0.6, 0.8, 0.8, 0.4)},
+    "x3_lr03": {"sgd_epoch_batches": (4, 6, 6, 3), "sgd_lr": (0.6, 0.8, 0.8, 0.3)},
+    "x4_lr04": {"sgd_epoch_batches": (4, 6, 6, 4), "sgd_lr": (0.6, 0.8, 0.8, 0.4)},
+    "x6_lr04": {"sgd_lr": (0.6, 0.8, 0.8, 0.4)},
+    "x6_lr05": {"sgd_lr": (0.6, 0.8, 0.8, 0.5)},
 }
 
 
