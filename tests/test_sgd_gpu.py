@@ -220,3 +220,19 @@ def test_persistent_fault_recovers_bitwise(dev, storage):
     assert np.array_equal(a.w, b.w), np.abs(a.w - b.w).max()
     assert a.n_iter == b.n_iter and a.objective == b.objective and a.grad_max == b.grad_max
     assert np.array_equal(c.w, b.w) and c.n_iter == b.n_iter
+
+
+def test_stamped_exports_survive_slot_rotation(dev):
+    """The persistent launch exports each fit's final state into a rotating mapped pinned slot
+    followed by a per-fit stamp (no event): more fits in flight than slots, read afterwards in
+    order, each equals the same fit read at once (the ninth fit settles the first slot's owner)."""
+    X, y = separable(400_000, seed=21, device=dev)
+    pipe = DevicePipeline(TrainConfig(solver="sgd", seed=42))
+    ref_fit = pipe.fit(X, y).fit.as_fit_info()  # read at once
+    fits = [pipe.fit(X, y).fit for _ in range(L.PendingFit._POOL + 3)]  # nothing read yet
+    for f in fits:
+        info = f.as_fit_info()
+        assert info.n_iter == ref_fit.n_iter
+        np.testing.assert_array_equal(info.w, ref_fit.w)
+        assert info.grad_max == ref_fit.grad_max
+    assert len({f._stamp for f in fits}) == len(fits) and all(f._stamp > 0 for f in fits)
