@@ -78,6 +78,13 @@ for st in "$@"; do
       step sortpoll_off2 300 env FDX_SORT_POLL_US=0 python bench.py --steps 30 --warmup 3 --no-extras &&
       step sortpoll_on3 300 python bench.py --steps 30 --warmup 3 --no-extras &&
       step sortpoll_off3 300 env FDX_SORT_POLL_US=0 python bench.py --steps 30 --warmup 3 --no-extras ;;
+    benchclk)  # per-fit boundaries from the device clock in the exports (default) vs events behind every fit
+      step benchclk_c1 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step benchclk_e1 300 env FDX_BENCH_EVENTS=1 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step benchclk_c2 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step benchclk_e2 300 env FDX_BENCH_EVENTS=1 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step benchclk_c3 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step benchclk_e3 300 env FDX_BENCH_EVENTS=1 python bench.py --steps 30 --warmup 3 --no-extras ;;
     quicksgdnc) step quicksgd_coop 300 env FDX_SGD_COOP=1 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
     evab)  # per-fit timing events and the side-stream export, on / off (quick SGD bench each)
       step evab_default 300 python bench.py --steps 30 --warmup 3 --no-extras &&
