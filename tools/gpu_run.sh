@@ -85,6 +85,13 @@ for st in "$@"; do
       step benchclk_e2 300 env FDX_BENCH_EVENTS=1 python bench.py --steps 30 --warmup 3 --no-extras &&
       step benchclk_c3 300 python bench.py --steps 30 --warmup 3 --no-extras &&
       step benchclk_e3 300 env FDX_BENCH_EVENTS=1 python bench.py --steps 30 --warmup 3 --no-extras ;;
+    cgather)  # minority rows gathered by the index-list launch (default) vs a scale_cast launch behind it
+      step cgather_on1 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step cgather_off1 300 env FDX_COMPACT_GATHER=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step cgather_on2 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step cgather_off2 300 env FDX_COMPACT_GATHER=0 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step cgather_on3 300 python bench.py --steps 30 --warmup 3 --no-extras &&
+      step cgather_off3 300 env FDX_COMPACT_GATHER=0 python bench.py --steps 30 --warmup 3 --no-extras ;;
     quicksgdnc) step quicksgd_coop 300 env FDX_SGD_COOP=1 python bench.py --steps 20 --warmup 3 --no-extras --solver sgd ;;
     evab)  # per-fit timing events and the side-stream export, on / off (quick SGD bench each)
       step evab_default 300 python bench.py --steps 30 --warmup 3 --no-extras &&
